@@ -1,0 +1,630 @@
+"""CPU restatement (numpy, float64) of the reference's multimodal-DINO training step,
+with an explicit backward pass.
+
+TEST INFRASTRUCTURE ONLY -- the checker, never the thing measured or shipped.
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use it.
+Pinned against golden vectors produced by running the reference itself
+(tests/golden/gen_golden.py -> tests/golden/*.npz; tests/test_oracle_golden.py).
+
+Each function cites the reference code (paths relative to
+/root/reference/AVMNIST_Experiments) whose math it restates.
+
+Conventions: activations of a conv stack are [N, C, H, W] with N = G*B, rows
+ordered group-major (group g owns rows g*B .. g*B+B-1).  Train-mode BatchNorm
+statistics are taken per (group, channel) because the reference calls the
+encoder once per view (models/dino.py:680-704), giving each view its own batch
+statistics.
+"""
+import math
+
+import numpy as np
+from numpy.lib.stride_tricks import sliding_window_view
+from scipy.special import erf
+
+F64 = np.float64
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+NORM_EPS = 1e-12
+
+
+# --------------------------------------------------------------------------- conv
+def conv2d_fwd(x, w, b, pad):
+    """nn.Conv2d(stride 1) forward -- models/unimodal.py:113-176, models/dino.py:20-61."""
+    k = w.shape[-1]
+    xp = np.pad(x, ((0, 0), (0, 0), (pad, pad), (pad, pad)))
+    win = sliding_window_view(xp, (k, k), axis=(2, 3))  # N,C,Ho,Wo,k,k
+    y = np.einsum("nchwij,ocij->nohw", win, w, optimize=True) + b[None, :, None, None]
+    return y, win
+
+
+def conv2d_bwd(dy, win, w, x_shape, pad):
+    k = w.shape[-1]
+    dw = np.einsum("nohw,nchwij->ocij", dy, win, optimize=True)
+    db = dy.sum(axis=(0, 2, 3))
+    N, C, H, W = x_shape
+    dwin = np.einsum("nohw,ocij->nchwij", dy, w, optimize=True)
+    Ho, Wo = dy.shape[2], dy.shape[3]
+    dxp = np.zeros((N, C, H + 2 * pad, W + 2 * pad), F64)
+    for i in range(k):
+        for j in range(k):
+            dxp[:, :, i:i + Ho, j:j + Wo] += dwin[..., i, j]
+    dx = dxp[:, :, pad:pad + H, pad:pad + W]
+    return dx, dw, db
+
+
+# --------------------------------------------------------------------------- batchnorm
+def bn_train_fwd(x, gamma, beta, G, axes):
+    """Train-mode BatchNorm (biased var for normalisation) per group.
+
+    x: [G*B, C, ...]; statistics over the rows of each group and the spatial axes.
+    Restates nn.BatchNorm2d/1d train mode (unimodal.py:114,130; dino.py:1245).
+    """
+    N = x.shape[0]
+    B = N // G
+    xs = x.reshape((G, B) + x.shape[1:])
+    red = (1,) + tuple(a + 1 for a in axes)
+    mean = xs.mean(axis=red, keepdims=True)
+    var = ((xs - mean) ** 2).mean(axis=red, keepdims=True)
+    invstd = 1.0 / np.sqrt(var + BN_EPS)
+    xhat = (xs - mean) * invstd
+    shape = (1, 1, -1) + (1,) * (x.ndim - 2)
+    y = xhat * gamma.reshape(shape) + beta.reshape(shape)
+    n = xs.size // (G * x.shape[1])
+    cache = (xhat, invstd, gamma, G, red, shape, x.shape)
+    stats = (mean.reshape(G, -1), var.reshape(G, -1), n)
+    return y.reshape(x.shape), cache, stats
+
+
+def bn_train_bwd(dy, cache):
+    xhat, invstd, gamma, G, red, shape, xshape = cache
+    dys = dy.reshape(xhat.shape)
+    n = xhat.size // (G * xhat.shape[2])
+    dbeta = dys.sum(axis=red).sum(axis=0)
+    dgamma = (dys * xhat).sum(axis=red).sum(axis=0)
+    dxhat = dys * gamma.reshape(shape)
+    s1 = dxhat.sum(axis=red, keepdims=True)
+    s2 = (dxhat * xhat).sum(axis=red, keepdims=True)
+    dx = invstd / n * (n * dxhat - s1 - xhat * s2)
+    return dx.reshape(xshape), dgamma, dbeta
+
+
+def bn_running_update(rm, rv, stats):
+    """Sequential per-group running-stat update: group order = call order in the
+    reference (views 0..V-1, then originals).  Unbiased variance, momentum 0.1."""
+    mean, var, n = stats
+    rm = rm.astype(F64).copy()
+    rv = rv.astype(F64).copy()
+    for g in range(mean.shape[0]):
+        rm = (1 - BN_MOMENTUM) * rm + BN_MOMENTUM * mean[g]
+        rv = (1 - BN_MOMENTUM) * rv + BN_MOMENTUM * var[g] * n / (n - 1)
+    return rm, rv
+
+
+# --------------------------------------------------------------------------- relu / maxpool
+def maxpool2_fwd(x):
+    """F.max_pool2d(x, 2) (floor mode); ties resolved to the first element in
+    row-major window order, as ATen's CPU kernel does (scan with '>')."""
+    N, C, H, W = x.shape
+    Ho, Wo = H // 2, W // 2
+    xc = x[:, :, :2 * Ho, :2 * Wo].reshape(N, C, Ho, 2, Wo, 2).transpose(0, 1, 2, 4, 3, 5)
+    xc = xc.reshape(N, C, Ho, Wo, 4)
+    arg = xc.argmax(axis=-1)
+    y = np.take_along_axis(xc, arg[..., None], axis=-1)[..., 0]
+    return y, (arg, x.shape)
+
+
+def maxpool2_bwd(dy, cache):
+    arg, xshape = cache
+    N, C, H, W = xshape
+    Ho, Wo = dy.shape[2], dy.shape[3]
+    d = np.zeros((N, C, Ho, Wo, 4), F64)
+    np.put_along_axis(d, arg[..., None], dy[..., None], axis=-1)
+    d = d.reshape(N, C, Ho, Wo, 2, 2).transpose(0, 1, 2, 4, 3, 5).reshape(N, C, 2 * Ho, 2 * Wo)
+    dx = np.zeros(xshape, F64)
+    dx[:, :, :2 * Ho, :2 * Wo] = d
+    return dx
+
+
+# --------------------------------------------------------------------------- dense ops
+def linear_fwd(x, w, b):
+    return x @ w.T + b
+
+
+def linear_bwd(dy, x, w):
+    return dy @ w, dy.T @ x, dy.sum(axis=0)
+
+
+def gelu_fwd(x):
+    """nn.GELU() (erf form) -- ProjectionHead dino.py:1246."""
+    return 0.5 * x * (1.0 + erf(x / math.sqrt(2.0)))
+
+
+def gelu_bwd(dy, x):
+    cdf = 0.5 * (1.0 + erf(x / math.sqrt(2.0)))
+    pdf = np.exp(-0.5 * x * x) / math.sqrt(2.0 * math.pi)
+    return dy * (cdf + x * pdf)
+
+
+def l2norm_fwd(x):
+    """F.normalize(x, p=2, dim=-1): x / max(||x||, 1e-12)."""
+    n = np.sqrt((x * x).sum(axis=-1, keepdims=True))
+    d = np.maximum(n, NORM_EPS)
+    return x / d, (x, n, d)
+
+
+def l2norm_bwd(dy, cache):
+    x, n, d = cache
+    y = x / d
+    proj = (dy * y).sum(axis=-1, keepdims=True)
+    dx = (dy - y * proj * (n > NORM_EPS)) / d
+    return dx
+
+
+def log_softmax(z):
+    m = z.max(axis=-1, keepdims=True)
+    return z - m - np.log(np.exp(z - m).sum(axis=-1, keepdims=True))
+
+
+def softmax(z):
+    return np.exp(log_softmax(z))
+
+
+# --------------------------------------------------------------------------- encoders
+class ConvStack:
+    """[conv -> BN(train) -> ReLU -> maxpool2] x L, optional global average pool.
+
+    CentralUnimodalImage/Audio (unimodal.py:127-153, 185-211) and the 3x3 CNNs
+    (dino.py:18-73: the AdaptiveAvgPool2d(1) tail)."""
+
+    def __init__(self, arch, prefix_fmt):
+        self.arch = arch
+        self.prefix_fmt = prefix_fmt  # callable(i) -> (conv_key, bn_key)
+
+    def forward(self, P, x, G):
+        caches, stats = [], []
+        h = x
+        for i, (ci, co, k, pad) in enumerate(self.arch["convs"]):
+            ck, bk = self.prefix_fmt(i)
+            y, win = conv2d_fwd(h, P[ck + ".weight"], P[ck + ".bias"], pad)
+            z, bnc, st = bn_train_fwd(y, P[bk + ".weight"], P[bk + ".bias"], G, axes=(2, 3))
+            r = np.maximum(z, 0.0)
+            p, pc = maxpool2_fwd(r)
+            caches.append((win, h.shape, pad, ck, bk, bnc, z, pc))
+            stats.append((bk, st))
+            h = p
+        if self.arch["gap"]:
+            feat = h.mean(axis=(2, 3))
+            caches.append(("gap", h.shape))
+        else:
+            feat = h.reshape(h.shape[0], -1)
+            caches.append(("flat", h.shape))
+        return feat, (caches, stats)
+
+    def backward(self, P, dfeat, cache, grads):
+        caches, _ = cache
+        kind, hshape = caches[-1]
+        if kind == "gap":
+            dh = np.broadcast_to(dfeat[:, :, None, None] / (hshape[2] * hshape[3]), hshape).copy()
+        else:
+            dh = dfeat.reshape(hshape)
+        for i in reversed(range(len(self.arch["convs"]))):
+            win, xshape, pad, ck, bk, bnc, z, pc = caches[i]
+            dr = maxpool2_bwd(dh, pc)
+            dz = dr * (z > 0)
+            dy, dg, dbt = bn_train_bwd(dz, bnc)
+            dx, dw, db = conv2d_bwd(dy, win, P[ck + ".weight"], xshape, pad)
+            _acc(grads, ck + ".weight", dw)
+            _acc(grads, ck + ".bias", db)
+            _acc(grads, bk + ".weight", dg)
+            _acc(grads, bk + ".bias", dbt)
+            dh = dx
+        return dh
+
+
+def _acc(grads, k, v):
+    if k in grads:
+        grads[k] = grads[k] + v
+    else:
+        grads[k] = v
+
+
+def lenet_stack(arch, prefix):
+    return ConvStack(arch, lambda i: (f"{prefix}.conv{i + 1}", f"{prefix}.bn{i + 1}"))
+
+
+def cnn3_stack(arch, prefix):
+    return ConvStack(arch, lambda i: (f"{prefix}.{4 * i}", f"{prefix}.{4 * i + 1}"))
+
+
+class Branch:
+    """Conv stack followed by the Linear that maps its flattened output to E
+    (CentralMultiModalEncoder image_encoder/audio_encoder, dino.py:459-468)."""
+
+    def __init__(self, stack, lin_key):
+        self.stack = stack
+        self.lin = lin_key
+
+    def forward(self, P, x, G):
+        feat, sc = self.stack.forward(P, x, G)
+        out = linear_fwd(feat, P[self.lin + ".weight"], P[self.lin + ".bias"])
+        return out, (feat, sc)
+
+    def backward(self, P, dout, cache, grads):
+        feat, sc = cache
+        dfeat, dw, db = linear_bwd(dout, feat, P[self.lin + ".weight"])
+        _acc(grads, self.lin + ".weight", dw)
+        _acc(grads, self.lin + ".bias", db)
+        return self.stack.backward(P, dfeat, sc, grads)
+
+
+class CentralMultiModal:
+    """CentralMultiModalEncoder forward (SimpleMultiModalEncoder.forward, dino.py:229-234):
+    cat(image_branch, audio_branch) -> Linear -> ReLU -> Dropout -> Linear."""
+
+    def __init__(self, prefix):
+        from .spec import CENTRAL_IMAGE, CENTRAL_AUDIO
+        self.p = prefix
+        self.img = Branch(lenet_stack(CENTRAL_IMAGE, f"{prefix}.image_encoder.0"), f"{prefix}.image_encoder.1")
+        self.aud = Branch(lenet_stack(CENTRAL_AUDIO, f"{prefix}.audio_encoder.0"), f"{prefix}.audio_encoder.1")
+
+    def forward(self, P, img, aud, G, drop_mask=None):
+        fi, ci = self.img.forward(P, img, G)
+        fa, ca = self.aud.forward(P, aud, G)
+        cat = np.concatenate([fi, fa], axis=1)
+        h = linear_fwd(cat, P[self.p + ".fusion.0.weight"], P[self.p + ".fusion.0.bias"])
+        r = np.maximum(h, 0.0)
+        if drop_mask is not None:
+            r = r * drop_mask
+        out = linear_fwd(r, P[self.p + ".fusion.3.weight"], P[self.p + ".fusion.3.bias"])
+        return out, (ci, ca, cat, h, r, drop_mask)
+
+    def backward(self, P, dout, cache, grads):
+        ci, ca, cat, h, r, drop_mask = cache
+        dr, dw, db = linear_bwd(dout, r, P[self.p + ".fusion.3.weight"])
+        _acc(grads, self.p + ".fusion.3.weight", dw)
+        _acc(grads, self.p + ".fusion.3.bias", db)
+        if drop_mask is not None:
+            dr = dr * drop_mask
+        dh = dr * (h > 0)
+        dcat, dw, db = linear_bwd(dh, cat, P[self.p + ".fusion.0.weight"])
+        _acc(grads, self.p + ".fusion.0.weight", dw)
+        _acc(grads, self.p + ".fusion.0.bias", db)
+        E = dcat.shape[1] // 2
+        self.img.backward(P, dcat[:, :E], ci, grads)
+        self.aud.backward(P, dcat[:, E:], ca, grads)
+
+
+class ProjHead:
+    """ProjectionHead (dino.py:1240-1254): Linear -> BN1d(train) -> GELU -> Dropout -> Linear."""
+
+    def __init__(self, prefix):
+        self.p = prefix
+
+    def forward(self, P, x, G=1, drop_mask=None):
+        p = self.p
+        h = linear_fwd(x, P[p + ".mlp.0.weight"], P[p + ".mlp.0.bias"])
+        z, bnc, st = bn_train_fwd(h, P[p + ".mlp.1.weight"], P[p + ".mlp.1.bias"], G, axes=())
+        a = gelu_fwd(z)
+        if drop_mask is not None:
+            a = a * drop_mask
+        out = linear_fwd(a, P[p + ".mlp.4.weight"], P[p + ".mlp.4.bias"])
+        return out, (x, h, bnc, z, a, drop_mask, st)
+
+    def backward(self, P, dout, cache, grads):
+        p = self.p
+        x, h, bnc, z, a, drop_mask, _ = cache
+        da, dw, db = linear_bwd(dout, a, P[p + ".mlp.4.weight"])
+        _acc(grads, p + ".mlp.4.weight", dw)
+        _acc(grads, p + ".mlp.4.bias", db)
+        if drop_mask is not None:
+            da = da * drop_mask
+        dz = gelu_bwd(da, z)
+        dh, dg, dbt = bn_train_bwd(dz, bnc)
+        _acc(grads, p + ".mlp.1.weight", dg)
+        _acc(grads, p + ".mlp.1.bias", dbt)
+        dx, dw, db = linear_bwd(dh, x, P[p + ".mlp.0.weight"])
+        _acc(grads, p + ".mlp.0.weight", dw)
+        _acc(grads, p + ".mlp.0.bias", db)
+        return dx
+
+
+# --------------------------------------------------------------------------- losses
+def dino_loss(s, t, tau_s, tau_t, center_teacher=False):
+    """MultiModalDINOLightning.dino_loss (dino.py:822-854); with center_teacher=True
+    the UniModalDINOLightning variant that subtracts the per-view batch mean of the
+    normalised teacher (dino.py:1606-1617).  Returns (loss, d_loss/d_s)."""
+    V, B, _ = s.shape
+    T = t.shape[0]
+    sn, sc = l2norm_fwd(s)
+    tn, _ = l2norm_fwd(t)
+    if center_teacher:
+        tn = tn - tn.mean(axis=1, keepdims=True)
+    pt = softmax(tn / tau_t)          # [T,B,K]
+    ls = log_softmax(sn / tau_s)      # [V,B,K]
+    # sum over all (student view, teacher view) pairs, each a batch mean, / (V*T)
+    ptsum = pt.sum(axis=0)            # [B,K]
+    loss = -(ptsum[None] * ls).sum() / (B * V * T)
+    # d/d(ls) = -ptsum/(B V T); log-softmax backward: g - softmax * sum(g)
+    g = np.broadcast_to(-ptsum[None] / (B * V * T), ls.shape)
+    dz = g - np.exp(ls) * g.sum(axis=-1, keepdims=True)
+    dsn = dz / tau_s
+    ds = l2norm_bwd(dsn, sc)
+    return loss, ds
+
+
+def mse_loss(i, a):
+    """MultiModalDINOWithMSELightning.mse_loss (dino.py:1193-1211)."""
+    inn, ic = l2norm_fwd(i)
+    an, ac = l2norm_fwd(a)
+    d = inn - an
+    loss = (d * d).mean()
+    g = 2.0 * d / d.size
+    return loss, l2norm_bwd(g, ic), l2norm_bwd(-g, ac)
+
+
+def cross_entropy(logits, labels):
+    """F.cross_entropy mean reduction; returns (loss, dlogits)."""
+    n = logits.shape[0]
+    ls = log_softmax(logits)
+    loss = -ls[np.arange(n), labels].mean()
+    d = np.exp(ls)
+    d[np.arange(n), labels] -= 1.0
+    return loss, d / n
+
+
+def infonce_loss(i, a, temperature=0.07):
+    """infoNCE_loss (dino.py:1091-1128; other_ssl/info_nce/info_nce.py:75-112)."""
+    B = i.shape[0]
+    inn, ic = l2norm_fwd(i)
+    an, ac = l2norm_fwd(a)
+    S = inn @ an.T / temperature
+    lab = np.arange(B)
+    l1, d1 = cross_entropy(S, lab)
+    l2, d2 = cross_entropy(S.T, lab)
+    dS = (d1 + d2.T) / 2.0
+    loss = (l1 + l2) / 2.0
+    dinn = dS @ an / temperature
+    dan = dS.T @ inn / temperature
+    return loss, l2norm_bwd(dinn, ic), l2norm_bwd(dan, ac)
+
+
+def nt_xent_loss(reps, temperature=0.07):
+    """MultiModalSimCLRLightning.nt_xent_loss (multimodal_simclr.py:74-89)."""
+    N = reps.shape[0]
+    B = N // 2
+    rn, rc = l2norm_fwd(reps)
+    S = rn @ rn.T / temperature
+    np.fill_diagonal(S, -np.inf)
+    lab = np.concatenate([np.arange(B) + B, np.arange(B)])
+    loss, dS = cross_entropy(S, lab)
+    np.fill_diagonal(dS, 0.0)
+    drn = (dS + dS.T) @ rn / temperature
+    return loss, l2norm_bwd(drn, rc)
+
+
+# --------------------------------------------------------------------------- optimiser / EMA
+def adam_step(p, g, m, v, step, lr, wd, b1=0.9, b2=0.999, eps=1e-8):
+    """torch.optim.Adam (L2 weight decay added to the gradient), configure_optimizers
+    dino.py:953-962."""
+    g = g + wd * p
+    m = b1 * m + (1 - b1) * g
+    v = b2 * v + (1 - b2) * g * g
+    bc1 = 1 - b1 ** step
+    bc2 = 1 - b2 ** step
+    denom = np.sqrt(v) / math.sqrt(bc2) + eps
+    p = p - (lr / bc1) * m / denom
+    return p, m, v
+
+
+def ema(teacher, student, m):
+    """MultiModalDINO.update_teacher (dino.py:635-646)."""
+    return m * teacher + (1 - m) * student
+
+
+# --------------------------------------------------------------------------- full step
+def _views_to_rows(v):
+    """[B, V, 1, H, W] -> [V*B, 1, H, W] (view-major, matching torch.cat of the
+    per-view features, dino.py:695)."""
+    B, V = v.shape[:2]
+    return np.ascontiguousarray(v.transpose(1, 0, 2, 3, 4).reshape(V * B, *v.shape[2:]))
+
+
+def multimodal_step(P, batch, mode, hp, masks=None):
+    """One MultiModalDINO* training step in the reference's order:
+    forward -> losses -> EMA (pre-step student) -> backward -> Adam.
+
+    P: dict key -> float64 ndarray (full state dict, incl. teacher / BN buffers / center).
+    Returns dict with losses, outputs, grads (live student params), new state.
+    masks: optional dropout masks (already scaled by 1/(1-p)) for the fusion of the
+    student ('fusion_s' [V*B,E]), teacher ('fusion_t' [G*B,E]), heads ('fusion_o' [B,E])
+    and the student projection ('proj_s' [V*B,512]); None = p 0.
+    """
+    masks = masks or {}
+    P = {k: np.asarray(v, F64) if np.asarray(v).dtype != np.int64 else np.asarray(v) for k, v in P.items()}
+    g_img, g_aud, l_img, l_aud = batch["g_img"], batch["g_aud"], batch["l_img"], batch["l_aud"]
+    B, G = g_img.shape[:2]
+    L = l_img.shape[1]
+    V = G + L
+    img_v = np.concatenate([_views_to_rows(g_img), _views_to_rows(l_img)]).astype(F64)
+    aud_v = np.concatenate([_views_to_rows(g_aud), _views_to_rows(l_aud)]).astype(F64)
+
+    stu = CentralMultiModal("student")
+    tea = CentralMultiModal("teacher")
+    sproj, tproj = ProjHead("student_projection"), ProjHead("teacher_projection")
+
+    # student: all views (each view its own BN group)
+    s_feat, s_cache = stu.forward(P, img_v, aud_v, V, masks.get("fusion_s"))
+    # teacher: global views, no grad, train mode (batch-stat BN)
+    t_feat, t_cache = tea.forward(P, img_v[:G * B], aud_v[:G * B], G, masks.get("fusion_t"))
+    s_proj, sp_cache = sproj.forward(P, s_feat, 1, masks.get("proj_s"))
+    t_proj, tp_cache = tproj.forward(P, t_feat, 1)
+    center = P["center"]
+    t_c = t_proj - center
+    new_center = center * hp["center_momentum"] + t_proj.mean(axis=0, keepdims=True) * (1 - hp["center_momentum"])
+    s_out = s_proj.reshape(V, B, -1)
+    t_out = t_c.reshape(G, B, -1)
+
+    dino, ds = dino_loss(s_out, t_out, hp["tau_s"], hp["tau_t"])
+    out = {"dino_loss": dino, "s_out": s_out, "t_out": t_out, "center_after": new_center}
+    grads = {}
+    bn_stats = []  # (bn key, stats) in call order
+    bn_stats += [(k, st) for k, st in _stack_stats(s_cache)]
+    bn_stats += [("student_projection.mlp.1", sp_cache[-1])]
+    bn_stats += [(k, st) for k, st in _stack_stats(t_cache)]
+    bn_stats += [("teacher_projection.mlp.1", tp_cache[-1])]
+
+    aux = 0.0
+    if mode in ("mse", "infonce", "semi_supervised"):
+        img_o = batch["image"].astype(F64)
+        aud_o = batch["audio"].astype(F64)
+        fi, ci = stu.img.forward(P, img_o, 1)
+        fa, ca = stu.aud.forward(P, aud_o, 1)
+        hi = {"mse": "image_projection_head", "infonce": "image_projection_head",
+              "semi_supervised": "image_classifier"}[mode]
+        ha = hi.replace("image", "audio")
+        hI, hA = ProjHead(hi), ProjHead(ha)
+        zi, zic = hI.forward(P, fi)
+        za, zac = hA.forward(P, fa)
+        if mode == "mse":
+            aux, dzi, dza = mse_loss(zi, za)
+        elif mode == "infonce":
+            aux, dzi, dza = infonce_loss(zi, za)
+        else:
+            li, dzi = cross_entropy(zi, batch["label"])
+            la, dza = cross_entropy(za, batch["label"])
+            aux = li + la
+        out["f_img"], out["f_aud"] = zi, za
+        bn_stats += [(k, st) for k, st in _branch_stats(ci)]
+        bn_stats += [(k, st) for k, st in _branch_stats(ca)]
+        bn_stats += [(hi + ".mlp.1", zic[-1]), (ha + ".mlp.1", zac[-1])]
+        dfi = hI.backward(P, dzi, zic, grads)
+        dfa = hA.backward(P, dza, zac, grads)
+        stu.img.backward(P, dfi, ci, grads)
+        stu.aud.backward(P, dfa, ca, grads)
+    out["aux_loss"] = aux
+    out["loss"] = dino + aux
+
+    # backward of the DINO branch
+    dsf = sproj.backward(P, ds.reshape(V * B, -1), sp_cache, grads)
+    stu.backward(P, dsf, s_cache, grads)
+
+    # new state: EMA uses the pre-step student (update_teacher precedes backward/step)
+    new = dict(P)
+    m = hp["momentum"]
+    for k in P:
+        if k.startswith("teacher") and not (k.endswith("running_mean") or k.endswith("running_var")
+                                            or k.endswith("num_batches_tracked")):
+            new[k] = ema(P[k], P["student" + k[len("teacher"):]], m)
+    new["center"] = new_center
+    # BN running stats, group order per call order
+    for bk, st in bn_stats:
+        rm, rv = bn_running_update(new[bk + ".running_mean"], new[bk + ".running_var"], st)
+        new[bk + ".running_mean"], new[bk + ".running_var"] = rm, rv
+        new[bk + ".num_batches_tracked"] = np.asarray(new[bk + ".num_batches_tracked"]) + st[0].shape[0]
+    out["grads"] = grads
+    out["state"] = new
+    return out
+
+
+def _stack_stats(enc_cache):
+    ci, ca = enc_cache[0], enc_cache[1]
+    return list(_branch_stats(ci)) + list(_branch_stats(ca))
+
+
+def _branch_stats(branch_cache):
+    _feat, (_caches, stats) = branch_cache
+    return stats
+
+
+def adam_update_state(state, grads, opt, step, hp):
+    """Apply Adam to every parameter with a gradient; opt holds (m, v) per key."""
+    new = dict(state)
+    for k, g in grads.items():
+        m, v = opt.get(k, (np.zeros_like(g), np.zeros_like(g)))
+        p, m, v = adam_step(state[k], g, m, v, step, hp["lr"], hp["wd"])
+        new[k] = p
+        opt[k] = (m, v)
+    return new
+
+
+def unimodal_image_step(P, batch, hp):
+    """UniModalDINO(ImageEncoder) + UniModalDINOLightning.dino_loss (dino.py:1319-1398,
+    1596-1635), 2 global / 0 local views (BASELINE config 1)."""
+    from .spec import CNN3_IMAGE
+    P = {k: np.asarray(v, F64) if np.asarray(v).dtype != np.int64 else np.asarray(v) for k, v in P.items()}
+    g_img = batch["g_img"]
+    B, G = g_img.shape[:2]
+    x = _views_to_rows(g_img).astype(F64)
+
+    def enc(prefix):
+        return Branch(cnn3_stack(CNN3_IMAGE, f"{prefix}.encoder"), f"{prefix}.encoder.14")
+
+    def run(prefix, x):
+        e = enc(prefix)
+        f, c = e.forward(P, x, G)
+        o = linear_fwd(f, P[f"{prefix}.projection.0.weight"], P[f"{prefix}.projection.0.bias"])
+        return o, (e, f, c)
+
+    s_feat, (se, sf, sc) = run("student", x)
+    t_feat, _ = run("teacher", x)
+    sp, tp = ProjHead("student_projection"), ProjHead("teacher_projection")
+    s_proj, spc = sp.forward(P, s_feat)
+    t_proj, _ = tp.forward(P, t_feat)
+    t_c = t_proj - P["center"]
+    s_out = s_proj.reshape(G, B, -1)
+    t_out = t_c.reshape(G, B, -1)
+    loss, ds = dino_loss(s_out, t_out, hp["tau_s"], hp["tau_t"], center_teacher=True)
+    grads = {}
+    dsf = sp.backward(P, ds.reshape(G * B, -1), spc, grads)
+    df, dw, db = linear_bwd(dsf, sf, P["student.projection.0.weight"])
+    _acc(grads, "student.projection.0.weight", dw)
+    _acc(grads, "student.projection.0.bias", db)
+    se.backward(P, df, sc, grads)
+    new_center = P["center"] * hp["center_momentum"] + t_proj.mean(axis=0, keepdims=True) * (1 - hp["center_momentum"])
+    return {"loss": loss, "s_out": s_out, "t_out": t_out, "grads": grads, "center_after": new_center}
+
+
+def simclr_step(P, batch, mode, temperature=0.07):
+    """MultiModalSimCLRModel.forward + nt_xent_loss (multimodal_simclr.py:22-47, 74-89)
+    for a pinned modality mode (0 img/img, 1 aud/aud, 2 img/aud, 3 aud/img)."""
+    from .spec import CNN3_IMAGE, CNN3_AUDIO
+    P = {k: np.asarray(v, F64) if np.asarray(v).dtype != np.int64 else np.asarray(v) for k, v in P.items()}
+    grads = {}
+
+    def image_enc(x):
+        e = Branch(cnn3_stack(CNN3_IMAGE, "image_encoder.encoder"), "image_encoder.encoder.14")
+        f, c = e.forward(P, x, 1)
+        o = linear_fwd(f, P["image_encoder.projection.0.weight"], P["image_encoder.projection.0.bias"])
+        h = ProjHead("image_projection_head")
+        z, hc = h.forward(P, o)
+
+        def bwd(dz):
+            do = h.backward(P, dz, hc, grads)
+            df, dw, db = linear_bwd(do, f, P["image_encoder.projection.0.weight"])
+            _acc(grads, "image_encoder.projection.0.weight", dw)
+            _acc(grads, "image_encoder.projection.0.bias", db)
+            e.backward(P, df, c, grads)
+        return z, bwd
+
+    def audio_enc(x):
+        e = Branch(cnn3_stack(CNN3_AUDIO, "audio_encoder.encoder"), "audio_encoder.encoder.18")
+        f, c = e.forward(P, x, 1)
+        h = ProjHead("audio_projection_head")
+        z, hc = h.forward(P, f)
+
+        def bwd(dz):
+            do = h.backward(P, dz, hc, grads)
+            e.backward(P, do, c, grads)
+        return z, bwd
+
+    i1, s1 = batch["img1"].astype(F64), batch["spec1"].astype(F64)
+    i2, s2 = batch["img2"].astype(F64), batch["spec2"].astype(F64)
+    f1 = image_enc if mode in (0, 2) else audio_enc
+    f2 = image_enc if mode in (0, 3) else audio_enc
+    z1, b1 = f1(i1 if f1 is image_enc else s1)
+    z2, b2 = f2(i2 if f2 is image_enc else s2)
+    B = z1.shape[0]
+    loss, dr = nt_xent_loss(np.concatenate([z1, z2]), temperature)
+    b1(dr[:B])
+    b2(dr[B:])
+    return {"loss": loss, "z1": z1, "z2": z2, "grads": grads}

@@ -1,0 +1,314 @@
+"""Generate golden vectors by running the REFERENCE hot path in this container.
+
+Usage (only where /root/reference exists; the GPU box never runs this):
+    python tests/golden/gen_golden.py [--out tests/golden]
+
+How the reference is run: the reference is pure Python; its
+hot-path modules import only fine after placeholder modules for the absent
+third-party packages (lightning, torchvision, torchaudio, torchmetrics) are put
+first on sys.path.  Those placeholders are written to /tmp at run time and are
+never part of this repo.  The *Lightning wrappers are not instantiated (their
+__init__ loads AVMNIST data from disk, models/dino.py:795-802); the loss methods
+are called unbound with a SimpleNamespace as ``self`` and Lightning's automatic
+optimisation order is replayed by hand: forward -> loss -> update_teacher
+(dino.py:1233) -> zero_grad -> backward -> Adam.step (dino.py:953-962).
+
+All dropout modules are set to p=0 so the vectors are deterministic.
+Parameters and inputs come from oracle/params.py (a pure function of seed and
+state-dict key), so fixtures only hold outputs.
+
+Each fixture stores, per tensor: the full array when it has <= FULL_MAX
+elements, otherwise its float64 sum, L2 norm and SAMPLE entries at seeded
+indices (the check is then on those size-independent properties).
+"""
+import argparse
+import os
+import sys
+import textwrap
+import types
+import zlib
+
+import numpy as np
+
+REF = "/root/reference/AVMNIST_Experiments"
+STUB_DIR = "/tmp/avdino_ref_stubs"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from oracle import spec as ospec  # noqa: E402
+from oracle.params import make_state, make_multimodal_batch, make_simclr_batch  # noqa: E402
+
+FULL_MAX = 8192
+SAMPLE = 256
+
+STUBS = {
+    "lightning/__init__.py": "from . import pytorch\n",
+    "lightning/pytorch/__init__.py": textwrap.dedent("""
+        import torch.nn as nn
+        class LightningModule(nn.Module):
+            def save_hyperparameters(self, *a, **k): pass
+            def log(self, *a, **k): pass
+        class LightningDataModule: pass
+        class Callback: pass
+        def seed_everything(*a, **k): pass
+        """),
+    "lightning/pytorch/callbacks.py": "class ModelCheckpoint: pass\n",
+    "lightning/pytorch/loggers.py": "class CSVLogger: pass\n",
+    "torchvision/__init__.py": "from . import transforms, models\n",
+    "torchvision/transforms.py": "".join(
+        f"class {n}:\n    def __init__(self, *a, **k): pass\n"
+        for n in ["Compose", "RandomResizedCrop", "RandomRotation", "RandomAffine",
+                  "RandomErasing", "RandomApply", "ElasticTransform", "GaussianBlur",
+                  "Resize", "ToTensor", "Normalize", "RandomCrop", "Lambda"]),
+    "torchvision/models/__init__.py": "",
+    "torchvision/models/mobilenetv3.py": "def mobilenet_v3_small(*a, **k): raise RuntimeError('stub')\n",
+    "torchvision/models/resnet.py": "def resnet18(*a, **k): raise RuntimeError('stub')\n",
+    "torchaudio/__init__.py": "from . import transforms\n",
+    "torchaudio/transforms.py": "".join(
+        f"class {n}:\n    def __init__(self, *a, **k): pass\n"
+        for n in ["TimeStretch", "FrequencyMasking", "TimeMasking", "Spectrogram"]),
+    "torchmetrics/__init__.py": "",
+    "torchmetrics/classification.py": "class Accuracy:\n    def __init__(self, *a, **k): pass\n",
+}
+
+
+def write_stubs():
+    for rel, src in STUBS.items():
+        path = os.path.join(STUB_DIR, rel)
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            f.write(src)
+    sys.path.insert(0, REF)
+    sys.path.insert(0, STUB_DIR)
+
+
+STORE = {"dtype": np.float32}
+
+
+def summarize(prefix, arr, out):
+    """Store a tensor fully or as (sum, norm, sampled entries)."""
+    a = np.asarray(arr, dtype=np.float64)
+    if a.size <= FULL_MAX:
+        out[prefix] = a.astype(STORE["dtype"])
+        return
+    flat = a.reshape(-1)
+    g = np.random.Generator(np.random.PCG64([zlib.crc32(prefix.encode()), 3]))
+    idx = np.sort(g.choice(flat.size, size=SAMPLE, replace=False))
+    out[prefix + "@sum"] = np.float64(flat.sum())
+    out[prefix + "@norm"] = np.float64(np.sqrt((flat * flat).sum()))
+    out[prefix + "@idx"] = idx.astype(np.int64)
+    out[prefix + "@val"] = flat[idx].astype(STORE["dtype"])
+
+
+def load_into(model, spec, state):
+    import torch
+    sd = model.state_dict()
+    keys = list(sd.keys())
+    assert keys == list(spec.keys()), (
+        "state-dict key mismatch:\n" +
+        "\n".join(f"{a} | {b}" for a, b in zip(keys, spec.keys()) if a != b)[:2000])
+    for k, (shp, _kind) in spec.items():
+        assert tuple(sd[k].shape) == tuple(shp), (k, sd[k].shape, shp)
+    model.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state.items()})
+
+
+def zero_dropout(model):
+    import torch.nn as nn
+    for m in model.modules():
+        if isinstance(m, nn.Dropout):
+            m.p = 0.0
+
+
+HP = dict(lr=1e-4, wd=1e-6, momentum=0.996, center_momentum=0.9, tau_s=0.1, tau_t=0.04)
+
+
+def multimodal_case(name, mode, E, D, P, B, G, L, pseed, bseed, steps, out_dir, dt="float32"):
+    import torch
+    dt = getattr(torch, dt)
+    import torch.nn as nn
+    import models.dino as rd
+
+    cls = {"default": rd.MultiModalDINO, "mse": rd.MultiModalDINOWithMSE,
+           "infonce": rd.MultiModalDINOWithINFONCE,
+           "semi_supervised": rd.MultiModalDINOSemiSupervised}[mode]
+    lcls = {"default": rd.MultiModalDINOLightning, "mse": rd.MultiModalDINOWithMSELightning,
+            "infonce": rd.MultiModalDINOWithINFONCELightning,
+            "semi_supervised": rd.MultiModalDINOSemiSupervisedLightning}[mode]
+    torch.manual_seed(0)
+    model = cls(encoder_class=rd.CentralMultiModalEncoder, output_dim=D, encoder_output_dim=E,
+                projection_dim=P, momentum=HP["momentum"], center_momentum=HP["center_momentum"],
+                dropout=0.0)
+    spec = ospec.multimodal_dino_spec(mode, E, D, P)
+    state = make_state(spec, pseed)
+    load_into(model, spec, state)
+    zero_dropout(model)
+    model = model.to(dt)
+    model.train()
+    selfns = types.SimpleNamespace(student_temperature=HP["tau_s"], teacher_temperature=HP["tau_t"],
+                                   alpha=1, ce_loss=nn.CrossEntropyLoss())
+    opt = torch.optim.Adam(model.parameters(), lr=HP["lr"], weight_decay=HP["wd"])
+    out = {"meta_mode": np.array(mode), "meta_dims": np.array([E, D, P, B, G, L, pseed, bseed])}
+    curve = []
+    for step in range(steps):
+        b = make_multimodal_batch(B, G, L, bseed + step)
+        t = {k: torch.from_numpy(v) for k, v in b.items()}
+        t = {k: (v.to(dt) if v.is_floating_point() else v) for k, v in t.items()}
+        views = (t["g_img"], t["g_aud"], t["l_img"], t["l_aud"])
+        if mode == "default":
+            s_out, t_out, _ = model(views)
+            dino = lcls.dino_loss(selfns, s_out, t_out)
+            aux = torch.zeros(())
+            loss = dino
+        else:
+            f_i, f_a, s_out, t_out = model((t["image"], t["audio"], views))
+            dino = lcls.dino_loss(selfns, s_out, t_out)
+            if mode == "mse":
+                aux = lcls.mse_loss(selfns, f_i, f_a)
+            elif mode == "infonce":
+                aux = lcls.infoNCE_loss(selfns, f_i, f_a)
+            else:
+                aux = lcls.supervised_loss(selfns, f_i, f_a, t["label"])
+            loss = dino + 1 * aux
+        model.update_teacher()
+        opt.zero_grad()
+        loss.backward()
+        if step == 0:
+            out["loss"] = np.float64(loss.item())
+            out["dino_loss"] = np.float64(dino.item())
+            out["aux_loss"] = np.float64(aux.item())
+            summarize("s_out", s_out.detach().numpy(), out)
+            summarize("t_out", t_out.detach().numpy(), out)
+            if mode != "default":
+                summarize("f_img", f_i.detach().numpy(), out)
+                summarize("f_aud", f_a.detach().numpy(), out)
+            for k, p in model.named_parameters():
+                if p.grad is not None:
+                    summarize("grad/" + k, p.grad.numpy(), out)
+            out["live_keys"] = np.array([k for k, p in model.named_parameters() if p.grad is not None])
+        opt.step()
+        if step == 0:
+            sd = model.state_dict()
+            for k, v in sd.items():
+                if k.endswith("running_mean") or k.endswith("running_var"):
+                    summarize("rs/" + k, v.numpy(), out)
+                elif k.startswith("teacher") and not k.endswith("num_batches_tracked"):
+                    summarize("ema/" + k, v.numpy(), out)
+                elif k == "center":
+                    out["center_after"] = v.numpy().astype(STORE["dtype"])
+                elif not k.endswith("num_batches_tracked"):
+                    summarize("post/" + k, v.numpy(), out)
+        curve.append(loss.item())
+    out["curve"] = np.array(curve, np.float64)
+    np.savez_compressed(os.path.join(out_dir, name + ".npz"), **out)
+    print(f"{name}: loss={out['loss']:.8f} curve={np.array(curve)}")
+
+
+def unimodal_case(name, D, P, B, pseed, bseed, steps, out_dir, dt="float32"):
+    import torch
+    dt = getattr(torch, dt)
+    import models.dino as rd
+    torch.manual_seed(0)
+    model = rd.UniModalDINO(encoder_class=rd.ImageEncoder, output_dim=D, projection_dim=P,
+                            momentum=HP["momentum"], center_momentum=HP["center_momentum"],
+                            dropout=0.0)
+    spec = ospec.unimodal_image_dino_spec(D, P)
+    state = make_state(spec, pseed)
+    load_into(model, spec, state)
+    zero_dropout(model)
+    model = model.to(dt)
+    model.train()
+    selfns = types.SimpleNamespace(student_temperature=HP["tau_s"], teacher_temperature=HP["tau_t"])
+    opt = torch.optim.Adam(model.parameters(), lr=HP["lr"], weight_decay=HP["wd"])
+    out = {"meta_dims": np.array([D, P, B, 2, 0, pseed, bseed])}
+    curve = []
+    for step in range(steps):
+        b = make_multimodal_batch(B, 2, 0, bseed + step, with_originals=False)
+        t = {k: torch.from_numpy(v).to(dt) for k, v in b.items()}
+        s_out, t_out, emb = model((t["g_img"], t["g_aud"], t["l_img"], t["l_aud"]))
+        loss = rd.UniModalDINOLightning.dino_loss(selfns, s_out, t_out)
+        model.update_teacher()
+        opt.zero_grad()
+        loss.backward()
+        if step == 0:
+            out["loss"] = np.float64(loss.item())
+            summarize("s_out", s_out.detach().numpy(), out)
+            summarize("t_out", t_out.detach().numpy(), out)
+            for k, p in model.named_parameters():
+                if p.grad is not None:
+                    summarize("grad/" + k, p.grad.numpy(), out)
+            out["live_keys"] = np.array([k for k, p in model.named_parameters() if p.grad is not None])
+        opt.step()
+        if step == 0:
+            for k, v in model.state_dict().items():
+                if k.endswith("running_mean") or k.endswith("running_var"):
+                    summarize("rs/" + k, v.numpy(), out)
+                elif k == "center":
+                    out["center_after"] = v.numpy().astype(STORE["dtype"])
+        curve.append(loss.item())
+    out["curve"] = np.array(curve, np.float64)
+    np.savez_compressed(os.path.join(out_dir, name + ".npz"), **out)
+    print(f"{name}: loss={out['loss']:.8f} curve={np.array(curve)}")
+
+
+def simclr_case(name, D, P, B, pseed, bseed, out_dir, dt="float32"):
+    import torch
+    dt = getattr(torch, dt)
+    sys.path.insert(0, os.path.join(REF, "other_ssl", "multimodal_simclr"))
+    import multimodal_simclr as rs
+    out = {"meta_dims": np.array([D, P, B, pseed, bseed])}
+    for mode in range(4):
+        torch.manual_seed(0)
+        model = rs.MultiModalSimCLRModel(output_dim=D, projection_dim=P)
+        spec = ospec.simclr_spec(D, P)
+        state = make_state(spec, pseed)
+        load_into(model, spec, state)
+        zero_dropout(model)
+        model = model.to(dt)
+        model.train()
+        b = make_simclr_batch(B, bseed)
+        t = [torch.from_numpy(b[k]).to(dt) for k in ("img1", "spec1", "img2", "spec2")]
+        real_randint = torch.randint
+        torch.randint = lambda *a, **k: torch.tensor([mode])
+        real_float = torch.Tensor.float
+        torch.Tensor.float = lambda self: self  # forward() calls .float(); keep dt
+        try:
+            z1, z2 = model(tuple(t))
+        finally:
+            torch.randint = real_randint
+            torch.Tensor.float = real_float
+        loss = rs.MultiModalSimCLRLightning.nt_xent_loss(None, torch.cat([z1, z2], 0))
+        loss.backward()
+        out[f"m{mode}/loss"] = np.float64(loss.item())
+        summarize(f"m{mode}/z1", z1.detach().numpy(), out)
+        summarize(f"m{mode}/z2", z2.detach().numpy(), out)
+        for k, p in model.named_parameters():
+            if p.grad is not None:
+                summarize(f"m{mode}/grad/" + k, p.grad.numpy(), out)
+        print(f"{name} mode {mode}: loss={loss.item():.8f}")
+    np.savez_compressed(os.path.join(out_dir, name + ".npz"), **out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=HERE)
+    args = ap.parse_args()
+    write_stubs()
+    import torch
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    o = args.out
+    # Each case twice: the reference executed in fp32 (its CPU numerics) and in float64
+    # (the same algorithm without rounding noise: the tight pin for the oracle).
+    for dt, sfx, store in (("float32", "", np.float32), ("float64", "_f64", np.float64)):
+        STORE["dtype"] = store
+        multimodal_case("mm_mse_small" + sfx, "mse", 32, 32, 16, 4, 2, 4, 101, 1001, 5, o, dt)
+        multimodal_case("mm_default_small" + sfx, "default", 32, 32, 16, 4, 2, 4, 102, 1002, 3, o, dt)
+        multimodal_case("mm_infonce_small" + sfx, "infonce", 32, 32, 16, 4, 2, 4, 103, 1003, 3, o, dt)
+        multimodal_case("mm_semi_small" + sfx, "semi_supervised", 32, 32, 16, 4, 2, 4, 104, 1004, 3, o, dt)
+        multimodal_case("mm_mse_full" + sfx, "mse", 256, 256, 128, 2, 2, 4, 105, 1005, 2, o, dt)
+        unimodal_case("uni_image_g2l0" + sfx, 256, 128, 8, 106, 1006, 3, o, dt)
+        simclr_case("simclr_small" + sfx, 256, 256, 4, 107, 1007, o, dt)
+
+
+if __name__ == "__main__":
+    main()

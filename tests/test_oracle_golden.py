@@ -1,0 +1,142 @@
+"""Pin the numpy oracle to the reference: every golden vector produced by running
+the reference (tests/golden/gen_golden.py) must be reproduced by oracle/.
+
+Two fixture variants per case (tests/golden/gen_golden.py):
+  *_f64  -- the reference executed in float64: the tight pin.  The oracle must agree
+            to rounding (rel-L2 1e-8 on every output / gradient / state tensor).
+  (none) -- the reference executed in fp32 on CPU, as shipped.  Its own rounding
+            error vs its float64 execution reaches ~2e-3 rel-L2 on the first audio
+            conv layers' gradients (measured: tests/golden/*), so that is the bound.
+Pre-BN biases (gradient mathematically zero) are checked against an absolute floor.
+"""
+import numpy as np
+import pytest
+
+from oracle import numpy_oracle as O
+from oracle import spec as S
+from oracle.params import make_state, make_multimodal_batch, make_simclr_batch
+from tests import golden_util as gu
+
+HP = dict(lr=1e-4, wd=1e-6, momentum=0.996, center_momentum=0.9, tau_s=0.1, tau_t=0.04)
+
+MM_CASES = ["mm_mse_small", "mm_default_small", "mm_infonce_small", "mm_semi_small", "mm_mse_full"]
+# variant suffix -> (loss abs tol, output rel, grad rel, state rel, zero-grad floor, curve abs tol)
+TOL = {"_f64": (1e-9, 1e-8, 1e-8, 1e-9, 1e-10, 1e-8),
+       "": (2e-5, 1e-4, 1e-2, 1e-4, 1e-10, 1e-3)}
+VARIANTS = ["_f64", ""]
+
+
+def _zero(name):
+    return gu.zero_grad_keys(gu.load(name + "_f64"))
+
+
+def _check_all(fx, items, rel, floor_fn=None):
+    bad = []
+    for key, val in items:
+        floor = floor_fn(key) if floor_fn else 0.0
+        ok, msg = gu.compare(fx, key, val, rel=rel, abs_floor=floor)
+        if not ok:
+            bad.append(msg)
+    assert not bad, "\n".join(bad[:20])
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("case", MM_CASES)
+def test_multimodal_step_matches_reference(case, variant):
+    fx = gu.load(case + variant)
+    lt, orel, grel, srel, floor, _ = TOL[variant]
+    mode = str(fx["meta_mode"])
+    E, D, P, B, G, L, pseed, bseed = [int(x) for x in fx["meta_dims"]]
+    spec = S.multimodal_dino_spec(mode, E, D, P)
+    state = make_state(spec, pseed)
+    batch = make_multimodal_batch(B, G, L, bseed)
+    r = O.multimodal_step(state, batch, mode, HP)
+
+    assert abs(r["loss"] - fx["loss"]) < lt, (r["loss"], fx["loss"])
+    assert abs(r["dino_loss"] - fx["dino_loss"]) < lt
+    assert abs(r["aux_loss"] - fx["aux_loss"]) < lt
+    _check_all(fx, [("s_out", r["s_out"]), ("t_out", r["t_out"])], orel)
+    if mode != "default":
+        _check_all(fx, [("f_img", r["f_img"]), ("f_aud", r["f_aud"])], orel)
+    _check_all(fx, [("center_after", r["center_after"])], orel)
+
+    live = [str(k) for k in fx["live_keys"]]
+    assert sorted(live) == sorted(r["grads"].keys())
+    zero = _zero(case)
+    _check_all(fx, [("grad/" + k, r["grads"][k]) for k in live], grel,
+               floor_fn=lambda k: floor if k in zero else 0.0)
+
+    st = r["state"]
+    _check_all(fx, [("rs/" + k, st[k]) for k in spec if k.endswith("running_mean") or k.endswith("running_var")], srel)
+    _check_all(fx, [("ema/" + k, st[k]) for k in spec if k.startswith("teacher")
+                    and not (k.endswith("running_mean") or k.endswith("running_var") or k.endswith("num_batches_tracked"))],
+               srel)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("case", ["mm_mse_small", "mm_default_small"])
+def test_multimodal_loss_curve_matches_reference(case, variant):
+    """Free-running curve (new batch per step, Adam + EMA + center carried over).
+    fp32 reference vs its own float64 run drifts 3e-4 by step 5 (pre-BN-bias noise that
+    Adam turns into +-lr steps), hence the fp32 bound."""
+    fx = gu.load(case + variant)
+    ctol = TOL[variant][5]
+    mode = str(fx["meta_mode"])
+    E, D, P, B, G, L, pseed, bseed = [int(x) for x in fx["meta_dims"]]
+    spec = S.multimodal_dino_spec(mode, E, D, P)
+    state = {k: np.asarray(v, np.float64) if v.dtype != np.int64 else v for k, v in make_state(spec, pseed).items()}
+    opt = {}
+    curve = []
+    for step in range(len(fx["curve"])):
+        r = O.multimodal_step(state, make_multimodal_batch(B, G, L, bseed + step), mode, HP)
+        curve.append(r["loss"])
+        state = O.adam_update_state(r["state"], r["grads"], opt, step + 1, HP)
+    np.testing.assert_allclose(curve, fx["curve"], atol=ctol, rtol=0)
+    # post-step parameters after step 1 are pinned separately (one step, identical state)
+
+
+def test_post_adam_params_match_reference():
+    fx = gu.load("mm_mse_small_f64")
+    E, D, P, B, G, L, pseed, bseed = [int(x) for x in fx["meta_dims"]]
+    spec = S.multimodal_dino_spec("mse", E, D, P)
+    state = make_state(spec, pseed)
+    r = O.multimodal_step(state, make_multimodal_batch(B, G, L, bseed), "mse", HP)
+    new = O.adam_update_state(r["state"], r["grads"], {}, 1, HP)
+    zero = _zero("mm_mse_small")
+    items = [("post/" + k, new[k]) for k in r["grads"] if ("grad/" + k) not in zero]
+    _check_all(fx, items, 1e-8)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_unimodal_image_config1_matches_reference(variant):
+    case = "uni_image_g2l0"
+    fx = gu.load(case + variant)
+    lt, orel, grel, srel, floor, _ = TOL[variant]
+    D, P, B, G, L, pseed, bseed = [int(x) for x in fx["meta_dims"]]
+    spec = S.unimodal_image_dino_spec(D, P)
+    state = make_state(spec, pseed)
+    batch = make_multimodal_batch(B, G, L, bseed, with_originals=False)
+    r = O.unimodal_image_step(state, batch, HP)
+    assert abs(r["loss"] - fx["loss"]) < lt
+    _check_all(fx, [("s_out", r["s_out"]), ("t_out", r["t_out"])], orel)
+    live = [str(k) for k in fx["live_keys"]]
+    assert sorted(live) == sorted(r["grads"].keys())
+    zero = _zero(case)
+    _check_all(fx, [("grad/" + k, r["grads"][k]) for k in live], grel,
+               floor_fn=lambda k: floor if k in zero else 0.0)
+    _check_all(fx, [("center_after", r["center_after"])], orel)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_simclr_config4_matches_reference(mode, variant):
+    fx = gu.load("simclr_small" + variant)
+    lt, orel, grel, srel, floor, _ = TOL[variant]
+    D, P, B, pseed, bseed = [int(x) for x in fx["meta_dims"]]
+    state = make_state(S.simclr_spec(D, P), pseed)
+    r = O.simclr_step(state, make_simclr_batch(B, bseed), mode)
+    assert abs(r["loss"] - fx[f"m{mode}/loss"]) < lt
+    _check_all(fx, [(f"m{mode}/z1", r["z1"]), (f"m{mode}/z2", r["z2"])], orel)
+    zero = _zero("simclr_small")
+    _check_all(fx, [(f"m{mode}/grad/" + k, g) for k, g in r["grads"].items()], grel,
+               floor_fn=lambda k: floor if k in zero else 0.0)
