@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Benchmark: AVMNIST audio-image pairs/sec of the multimodal-DINO training step
+(BASELINE.json metric), BASELINE config 2: multi_central, training_mode mse, B=1024 per GPU,
+2 global + 4 local views, E=D=256, P=128, bf16 activations (fp32 params/accumulation).
+
+A step = everything the reference's training step does: staging of the views,
+student (6 views + originals) and teacher (2 views) encoders, projections, DINO + MSE losses,
+centre update, teacher EMA, full backward, gradient all-reduce (N>1), Adam.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank/GPU)
+
+Rank 0 prints ONE JSON line.  Inputs are synthetic AVMNIST-shaped tensors (pixel values
+randint(0,256)/255) generated on the device before the timed region; weights random-init.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "multimodal-ssl-avmnist_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+METRIC = "AVMNIST audio-image pairs/sec (multimodal DINO step) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MFMA_PEAK_TFS = {"bf16": 2500.0, "f32": 157.3}   # dense, no sparsity
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1024, help="pairs per GPU per step")
+    ap.add_argument("--mode", default="mse", choices=["default", "mse", "infonce", "semi_supervised"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=32)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+def synthetic_pool(n, B, G, L, device, seed):
+    """Device-resident AVMNIST-shaped batches (get_data.py:456-467 value range)."""
+    gen = torch.Generator(device=device).manual_seed(seed)
+    pool = []
+
+    def px(*shape):
+        return torch.randint(0, 256, shape, generator=gen, device=device, dtype=torch.int32).float() / 255.0
+
+    for _ in range(n):
+        pool.append({"g_img": px(B, G, 1, 28, 28), "g_aud": px(B, G, 1, 112, 112),
+                     "l_img": px(B, L, 1, 28, 28), "l_aud": px(B, L, 1, 112, 112),
+                     "image": px(B, 1, 28, 28), "audio": px(B, 1, 112, 112),
+                     "label": torch.randint(0, 10, (B,), generator=gen, device=device)})
+    return pool
+
+
+def cpu_baseline(batch, seconds):
+    """The reference algorithm on the host cores (oracle/torch_port.py, fp32, per-view loops,
+    Python EMA, torch.optim.Adam) on a bounded sample: B pairs/step, >= 2 timed steps."""
+    from oracle import torch_port as TP
+    torch.manual_seed(0)
+    model = TP.DinoMSE()
+    model.train()
+    opt = TP.make_optimizer(model)
+    g = torch.Generator().manual_seed(1)
+
+    def px(*shape):
+        return torch.randint(0, 256, shape, generator=g).float() / 255.0
+
+    b = {"g_img": px(batch, 2, 1, 28, 28), "g_aud": px(batch, 2, 1, 112, 112),
+         "l_img": px(batch, 4, 1, 28, 28), "l_aud": px(batch, 4, 1, 112, 112),
+         "image": px(batch, 1, 28, 28), "audio": px(batch, 1, 112, 112)}
+    TP.train_step(model, opt, b)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        TP.train_step(model, opt, b)
+        n += 1
+        el = time.perf_counter() - t0
+        if (n >= 2 and el >= seconds) or n >= 50:
+            break
+    return {"value": round(batch * n / el, 2), "unit": "pairs/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle/torch_port.py multi_central mse step, fp32, B={batch}, 2 global + 4 local "
+                      f"views, {n} timed steps ({el:.1f} s) after 1 warm-up, torch CPU "
+                      f"{torch.get_num_threads()} threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+
+    from avdino import ops
+    from avdino.engine import Hyper, MultiCentralEngine
+    from avdino.params import ParamStore
+    from avdino.spec import multimodal_dino_sd
+
+    E, D, P, G, L, B = 256, 256, 128, 2, 4, args.batch
+    act = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    store = ParamStore(multimodal_dino_sd(args.mode, E, D, P), device, seed=0)
+
+    def allreduce_avg(grad):
+        dist.all_reduce(grad)
+        grad.mul_(1.0 / world)
+
+    eng = MultiCentralEngine(store, args.mode, E, D, P, Hyper(), act_dtype=act,
+                             grad_hook=allreduce_avg if world > 1 else None, seed=rank)
+    pool = synthetic_pool(2, B, G, L, device, 1234 + rank)
+
+    # warm-up, timing every instrumented kernel once to find the dominant one
+    ops.TIMER = ops.KernelTimer()
+    for i in range(args.warmup):
+        eng.step(pool[i % len(pool)])
+    summ = ops.TIMER.summary() if args.warmup else {}
+    dominant = max(summ, key=lambda k: summ[k]["ms"]) if summ else None
+    ops.TIMER = ops.KernelTimer(only=dominant)
+
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = eng.step(pool[i % len(pool)])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    lv = loss.item()
+    if not math.isfinite(lv):
+        raise SystemExit(f"non-finite loss {lv}")
+
+    timed = ops.TIMER.summary()
+    if dominant is None and timed:
+        dominant = max(timed, key=lambda k: timed[k]["ms"])
+    roof = None
+    if dominant in timed:
+        d = timed[dominant]
+        avg_s = d["ms"] / d["calls"] / 1e3
+        nb = d["bytes"] / d["calls"]
+        fl = d["flops"] / d["calls"]
+        peak_tf = MFMA_PEAK_TFS[args.dtype]
+        hbm_bound = nb / (HBM_PEAK_GBS * 1e9) >= fl / (peak_tf * 1e12)
+        if hbm_bound:
+            ach, peak, unit = nb / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
+        else:
+            ach, peak, unit = fl / avg_s / 1e12, peak_tf, "TFLOP/s"
+        roof = {"bound": "hbm" if hbm_bound else "mfma", "kernel": dominant,
+                "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
+                "traffic": None, "avg_launch_us": round(avg_s * 1e6, 2),
+                "algorithmic_bytes": int(nb), "algorithmic_flops": int(fl),
+                "kernel_share_of_step": round(d["ms"] / (elapsed * 1e3), 4)}
+
+    total_pairs = world * B * args.steps
+    value = total_pairs / elapsed
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "pairs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic: randint(0,256)/255 AVMNIST-shaped views resident in HBM; random-init weights",
+        "config": {"workload": f"multi_central {args.mode} training step, B={B}/GPU, {G} global + {L} local "
+                               f"views, E=D={E}, P={P} (BASELINE config 2)",
+                   "model": "multi_central", "global_batch": world * B, "seq_len": None,
+                   "parallelism": f"dp{world}"},
+        "roofline": roof,
+        "final_loss": round(lv, 6),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_batch, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,240 @@
+/*
+ * avdino.h -- C ABI of libavdino.so, the MI355X (gfx950) kernels of the multimodal-DINO
+ * training step of wardvdnb/Multimodal-SSL-AVMNIST.
+ *
+ * The reference has no FFI: its hot path is Python over ATen.  Each
+ * entry point below replaces the ATen op sequence named in its comment (paths relative to
+ * the reference's AVMNIST_Experiments/).  The Python host package
+ * (multimodal-ssl-avmnist_amd/avdino) binds this header through ctypes; INTEGRATION.md
+ * shows the binding.
+ *
+ * Contract (all functions):
+ *   - plain pointers + sizes; the caller owns every buffer (including partial-sum
+ *     workspaces, sized with the *_parts / *_chunks helpers); the library allocates nothing
+ *     and keeps no mutable global state;
+ *   - `stream` is a hipStream_t (NULL = default stream); launches are asynchronous;
+ *   - return AVD_OK (0) or a negative avd_status; shapes are validated before any launch;
+ *   - tensors are dense row-major (NCHW for feature maps, N = G*B samples stored
+ *     group-major: group g = view g owns samples g*B .. g*B+B-1);
+ *   - reductions are deterministic (fixed-order partial sums, no float atomics): the same
+ *     inputs give bitwise-identical outputs run to run.
+ */
+#ifndef AVDINO_H
+#define AVDINO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum { AVD_F32 = 0, AVD_BF16 = 1 } avd_dtype;
+
+typedef enum {
+  AVD_OK = 0,
+  AVD_ERR_SHAPE = -1,       /* unsupported / inconsistent shape */
+  AVD_ERR_DTYPE = -2,       /* unsupported dtype combination */
+  AVD_ERR_HIP = -3,         /* a HIP launch failed (hipGetLastError) */
+  AVD_ERR_ARG = -4          /* null pointer / bad enum */
+} avd_status;
+
+/* Library version, (major << 16) | minor. */
+int avd_version(void);
+/* Human-readable name of the last HIP error seen by this thread (or "ok"). */
+const char* avd_last_error(void);
+
+/* ------------------------------------------------------------------ conv blocks
+ * One CentralNet / CNN block is conv(KxK, stride 1) -> BatchNorm2d(train) -> ReLU -> maxpool2
+ * (models/unimodal.py:127-153 and 185-211; models/dino.py:18-73).
+ */
+
+/* Number of partial-statistic rows per sample written by avd_conv2d_fwd. */
+int avd_conv2d_stat_tiles(int Ho, int Wo);
+
+/* Re-lay a conv weight w [Cout,Cin,K,K] (f32) for the kernels:
+ * mode 0 (f32 forward):    wt[ci][tap][co] = w[co][ci][tap]        (f32)
+ * mode 1 (f32 input-grad): wt[co][tap][ci] = w[co][ci][K*K-1-tap] (f32)
+ *   (VALU kernels: per tap the weights a workgroup needs are contiguous and uniform, so
+ *    they arrive through scalar loads)
+ * mode 2 (bf16 forward, MFMA):    wk[co][tap*Cin + ci] = w[co][ci][tap]          (bf16)
+ * mode 3 (bf16 input-grad, MFMA): wk[ci][tap*Cout + co] = w[co][ci][K*K-1-tap]   (bf16)
+ *   (rows padded with zeros to a multiple of 32 k and of 16/64 output channels: the MFMA
+ *    B-operand fragment of a lane is one 16-byte load)
+ * avd_conv_weight_layout_elems gives the element count of wt for a mode. */
+int avd_conv_weight_layout_elems(int Cout, int Cin, int K, int mode);
+int avd_conv_weight_layout(const float* w, void* wt, int Cout, int Cin, int K, int mode,
+                           void* stream);
+
+/* y = conv2d(x, w) + bias   (nn.Conv2d forward, unimodal.py:113-176)
+ * x [N,Cin,H,W] (xdt), bias [Cout] f32 (NULL = 0),
+ * wt = avd_conv_weight_layout(w, mode 2) when x and y are bf16 and Cin % 8 == 0 (MFMA
+ *      implicit GEMM, v_mfma_f32_16x16x32_bf16), else mode 0 (VALU direct conv),
+ * y [N,Cout,Ho,Wo] (ydt),
+ * Ho = H + 2*pad - K + 1.  If stats != NULL, writes per-(channel, sample, tile) partial
+ * (sum, sum of squares) of the stored y: stats [Cout, N, T, 2] f32, T = avd_conv2d_stat_tiles.
+ * K in {3, 5}. */
+int avd_conv2d_fwd(const void* x, int xdt, const void* wt, const float* bias, void* y, int ydt,
+                   float* stats, int N, int Cin, int H, int W, int Cout, int K, int pad,
+                   void* stream);
+
+/* dx = conv2d_input_grad(dy, w)   (autograd of nn.Conv2d w.r.t. its input)
+ * dy [N,Cout,Ho,Wo] (dt), dx [N,Cin,H,W] (dt),
+ * wt_dgrad = avd_conv_weight_layout(w, mode 3) for bf16 (MFMA), mode 1 for f32. */
+int avd_conv2d_dgrad(const void* dy, const void* wt_dgrad, void* dx, int dt,
+                     int N, int Cin, int H, int W, int Cout, int K, int pad, void* stream);
+
+/* Number of sample chunks (partial slabs) avd_conv2d_wgrad writes for N samples. */
+int avd_conv2d_wgrad_chunks(int N, int Cout, int Cin, int K);
+
+/* dw_parts[c] = sum over the samples of chunk c of conv2d_weight_grad(x, dy)
+ * x [N,Cin,H,W] (xdt), dy [N,Cout,Ho,Wo] (dydt), dw_parts [chunks, Cout, Cin*K*K] f32.
+ * bf16 x/dy run on MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulate); f32 on the VALU.
+ * Reduce with avd_sum_rows. */
+int avd_conv2d_wgrad(const void* x, int xdt, const void* dy, int dydt, float* dw_parts,
+                     int N, int Cin, int H, int W, int Cout, int K, int pad, void* stream);
+
+/* BatchNorm2d / BatchNorm1d train-mode statistics, per (group, channel):
+ * parts [C, G, R, 2] f32 partial (sum, sumsq) rows, channel-major (R rows per group: for
+ * conv stats R = B*T), count = elements per (group, channel).  Outputs mean/invstd/scale/shift [G,C] (scale = gamma*invstd,
+ * shift = beta - mean*scale).  If running_mean != NULL, applies the reference's sequential
+ * per-call update for g = 0..G-1: rm = 0.9 rm + 0.1 mean_g, rv = 0.9 rv + 0.1 var_g*n/(n-1)
+ * (nn.BatchNorm momentum 0.1; group order = the reference's call order, dino.py:680-704). */
+int avd_bn_finalize(const float* parts, int G, int R, int C, long long count,
+                    const float* gamma, const float* beta, float eps, float momentum,
+                    float* mean, float* invstd, float* scale, float* shift,
+                    float* running_mean, float* running_var, void* stream);
+
+/* out = maxpool2(relu(scale*y + shift))  [N,C,H/2,W/2]  (floor mode)      pool_mode 0
+ * out = mean_hw(maxpool2(relu(...)))        [N,C]   f32 (AdaptiveAvgPool2d(1)) pool_mode 1
+ * y [N,C,H,W] (ydt); scale/shift [G,C]; B samples per group. */
+int avd_bn_relu_pool(const void* y, int ydt, const float* scale, const float* shift,
+                     void* out, int odt, int pool_mode, int N, int B, int C, int H, int W,
+                     void* stream);
+
+/* Backward of maxpool2(relu(BN(y))) up to the BN-output gradient dz, reduced:
+ * parts [C, N, 2] f32 = per-sample (sum dz, sum dz*xhat)  (= [C, G, B, 2]).
+ * gout: grad of the block output: pool_mode 0 [N,C,H/2,W/2] (gdt); pool_mode 1 [N,C] f32. */
+int avd_bn_bwd_reduce(const void* y, int ydt, const void* gout, int gdt, int pool_mode,
+                      const float* scale, const float* shift, const float* mean,
+                      const float* invstd, float* parts, int N, int B, int C, int H, int W,
+                      void* stream);
+
+/* From the partials [C, G, R, 2] build the input-gradient coefficients
+ * coef [G, C, 3] (dy = k1*dz + kx*y + k0) and write dgamma/dbeta/dbias [C] (sums over
+ * groups; dbias = sum of dy = the grad of a bias feeding this BN, NULL to skip).
+ * accumulate != 0 adds into dgamma/dbeta/dbias instead of overwriting. */
+int avd_bn_bwd_finalize(const float* parts, int G, int R, int C, long long count,
+                        const float* gamma, const float* mean, const float* invstd,
+                        float* coef, float* dgamma, float* dbeta, float* dbias, int accumulate,
+                        void* stream);
+
+/* dy [N,C,H,W] (dt) = gradient w.r.t. the conv output y of the whole block
+ * (maxpool2 + ReLU + BN backward), using coef from avd_bn_bwd_finalize. */
+int avd_bn_bwd_apply(const void* y, int ydt, const void* gout, int gdt, int pool_mode,
+                     const float* scale, const float* shift, const float* coef,
+                     void* dy, int dt, int N, int B, int C, int H, int W, void* stream);
+
+/* ------------------------------------------------------------------ dense layers */
+
+/* C[m,n] = alpha * sum_k A[m,k] B[k,n] + bias[n] + beta * C[m,n]   (f32, arbitrary strides)
+ * nn.Linear forward (x W^T + b), input grad (dy W) and weight grad (dy^T x).
+ * a_rowsum (nullable) [M] = sum_k A[m,k] from the same launch (the Linear bias gradient when
+ * A = dy^T).  Deterministic (no split-K). */
+int avd_gemm(int M, int N, int K, const float* A, long long sam, long long sak,
+             const float* B, long long sbk, long long sbn, float* C, long long ldc,
+             const float* bias, float alpha, float beta, float* a_rowsum, void* stream);
+
+/* out[r] (+)= sum_{i<rows} in[i, r]   (fixed order; in [rows, cols] f32) -- reduces partial
+ * slabs (conv weight grads) and column sums (Linear bias grads). */
+int avd_sum_rows(const float* in, int rows, int cols, float* out, int accumulate, void* stream);
+
+/* Column partial statistics of x [rows, C] f32 for BatchNorm1d: parts [C, G, R, 2] with
+ * R = avd_colstats_parts(rows/G) row-chunks per group. */
+int avd_colstats_parts(int rows_per_group);
+int avd_colstats(const float* x, int rows, int G, int C, float* parts, void* stream);
+
+/* Elementwise activation with optional dropout (keep mask from a counter hash of
+ * (seed, index), scaled by 1/(1-p)); act 0 = ReLU (fusion, dino.py:222-227),
+ * act 1 = GELU(erf) after BN1d (ProjectionHead, dino.py:1243-1249; scale/shift [G,C]
+ * per-column affine applied first, rows grouped into G groups of rows/G).
+ * x [rows, C] f32 -> out [rows, C] f32. */
+int avd_act_fwd(const float* x, float* out, int act, const float* scale, const float* shift,
+                int rows, int G, int C, float p, unsigned long long seed, void* stream);
+
+/* Backward of avd_act_fwd w.r.t. its input x (pre-affine value for act 1: returns dz, the
+ * grad w.r.t. the BN output).  dout [rows,C] -> dx [rows,C]. */
+int avd_act_bwd(const float* x, const float* dout, float* dx, int act, const float* scale,
+                const float* shift, int rows, int G, int C, float p, unsigned long long seed,
+                void* stream);
+
+/* BatchNorm1d backward partials: parts [C, G, R, 2] = (sum dz, sum dz*xhat) per row chunk. */
+int avd_bn1d_bwd_reduce(const float* x, const float* dz, const float* mean, const float* invstd,
+                        int rows, int G, int C, float* parts, void* stream);
+
+/* dx = k1*dz + kx*x + k0 per (group, column), coef [G,C,3] from avd_bn_bwd_finalize. */
+int avd_bn1d_bwd_apply(const float* x, const float* dz, const float* coef, float* dx,
+                       int rows, int G, int C, void* stream);
+
+/* ------------------------------------------------------------------ losses */
+
+/* DINO loss forward+backward (MultiModalDINOLightning.dino_loss, dino.py:822-854, plus the
+ * centring of MultiModalDINO.forward, dino.py:709-720):
+ *   t_raw [T*B, P] teacher projections (uncentred), center [P];
+ *   s [V*B, P] student projections (view-major rows);
+ *   loss_parts [V*B] per-row loss terms (sum = loss), ds [V*B, P] = d loss / d s;
+ *   center_new [P] = m*center + (1-m)*mean_rows(t_raw)  (update_center, dino.py:648-653);
+ *   center_teacher != 0: also subtract the per-view batch mean of the normalised teacher
+ *   (UniModalDINOLightning.dino_loss, dino.py:1613-1614).
+ *   work: >= (B + T*B) * P floats. */
+int avd_dino_loss(const float* s, const float* t_raw, const float* center, int V, int T, int B,
+                  int P, float tau_s, float tau_t, float center_m, int center_teacher,
+                  float* loss_parts, float* ds, float* center_new, float* work, void* stream);
+
+/* MSE between L2-normalised rows (MultiModalDINOWithMSELightning.mse_loss, dino.py:1193-1211):
+ * a, b [B,P] -> loss_parts [B], da, db [B,P]. */
+int avd_mse_loss(const float* a, const float* b, int B, int P, float* loss_parts,
+                 float* da, float* db, void* stream);
+
+/* Row-wise L2 normalisation (F.normalize, eps 1e-12): y = x / max(|x|, eps), norms [rows]. */
+int avd_l2norm_fwd(const float* x, float* y, float* norms, int rows, int P, void* stream);
+/* dx = (dy - y (y.dy)) / max(|x|, eps)  (dy overwritten-safe: dx may alias dy). */
+int avd_l2norm_bwd(const float* y, const float* norms, const float* dy, float* dx, int rows,
+                   int P, void* stream);
+
+/* Softmax cross-entropy over rows of logits [R, C] with integer targets (F.cross_entropy):
+ * loss_parts [R] (unnormalised per-row -log p_target), dlogits [R,C] = (softmax - onehot)*gscale.
+ * mask_diag != 0 excludes column r == (row index + diag_offset) (NT-Xent self-similarity,
+ * multimodal_simclr.py:79-81).  col_major != 0 reads logits transposed (logits^T rows). */
+int avd_softmax_xent(const float* logits, long long ld, int R, int C, const int64_t* targets,
+                     int target_mode, int col_major, int mask_diag, float gscale,
+                     float* loss_parts, float* dlogits, long long ldd, int accumulate,
+                     void* stream);
+
+/* ------------------------------------------------------------------ input staging */
+
+/* Re-lay a collated batch view-major for the encoder (MultiModalDINO.forward's per-view loop,
+ * dino.py:680-704): out[(v*B + b)] = g[b, v] (v < G), then l[b, v-G] (v < G+L), then orig[b]
+ * (if orig != NULL).  g [B,G,HW], l [B,L,HW], orig [B,HW] f32; out [(G+L+1?)*B, HW] (odt).
+ * HW % 4 == 0. */
+int avd_stage_views(const float* g, int G, const float* l, int L, const float* orig, int B,
+                    int HW, void* out, int odt, void* stream);
+
+/* ------------------------------------------------------------------ optimiser / EMA */
+
+/* teacher = m*teacher + (1-m)*student over n floats (MultiModalDINO.update_teacher,
+ * dino.py:635-646, on a flat parameter arena). */
+int avd_ema(float* teacher, const float* student, long long n, float m, void* stream);
+
+/* torch.optim.Adam step with L2 weight decay added to the gradient (configure_optimizers,
+ * dino.py:953-962) over flat arenas p/g/m/v of n floats; bc1 = 1-b1^t, bc2 = 1-b2^t. */
+int avd_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float b1,
+             float b2, float eps, float wd, float bc1, float bc2, void* stream);
+
+/* out = sum(in[0..n)) in fixed order (loss reduction); out is one float. */
+int avd_sum(const float* in, int n, float scale, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AVDINO_H */

@@ -1,0 +1,90 @@
+"""ctypes binding of libavdino.so (include/avdino.h).
+
+There is no fallback: if the shared library is missing or was built for another
+architecture, importing this module raises, so nothing can silently run a CPU path.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("AVDINO_LIB", os.path.join(_HERE, "libavdino.so"))
+
+F32, BF16 = 0, 1
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_longlong
+F = ctypes.c_float
+U64 = ctypes.c_ulonglong
+
+# name -> argtypes (restype is always c_int except where noted)
+PROTOS = {
+    "avd_version": [],
+    "avd_conv2d_stat_tiles": [I, I],
+    "avd_conv_weight_layout": [P, P, I, I, I, I, P],
+    "avd_conv_weight_layout_elems": [I, I, I, I],
+    "avd_conv2d_fwd": [P, I, P, P, P, I, P, I, I, I, I, I, I, I, P],
+    "avd_conv2d_dgrad": [P, P, P, I, I, I, I, I, I, I, I, P],
+    "avd_conv2d_wgrad_chunks": [I, I, I, I],
+    "avd_conv2d_wgrad": [P, I, P, I, P, I, I, I, I, I, I, I, P],
+    "avd_bn_finalize": [P, I, I, I, L, P, P, F, F, P, P, P, P, P, P, P],
+    "avd_bn_relu_pool": [P, I, P, P, P, I, I, I, I, I, I, I, P],
+    "avd_bn_bwd_reduce": [P, I, P, I, I, P, P, P, P, P, I, I, I, I, I, P],
+    "avd_bn_bwd_finalize": [P, I, I, I, L, P, P, P, P, P, P, P, I, P],
+    "avd_bn_bwd_apply": [P, I, P, I, I, P, P, P, P, I, I, I, I, I, I, P],
+    "avd_gemm": [I, I, I, P, L, L, P, L, L, P, L, P, F, F, P, P],
+    "avd_sum_rows": [P, I, I, P, I, P],
+    "avd_colstats_parts": [I],
+    "avd_colstats": [P, I, I, I, P, P],
+    "avd_act_fwd": [P, P, I, P, P, I, I, I, F, U64, P],
+    "avd_act_bwd": [P, P, P, I, P, P, I, I, I, F, U64, P],
+    "avd_bn1d_bwd_reduce": [P, P, P, P, I, I, I, P, P],
+    "avd_bn1d_bwd_apply": [P, P, P, P, I, I, I, P],
+    "avd_dino_loss": [P, P, P, I, I, I, I, F, F, F, I, P, P, P, P, P],
+    "avd_mse_loss": [P, P, I, I, P, P, P, P],
+    "avd_l2norm_fwd": [P, P, P, I, I, P],
+    "avd_l2norm_bwd": [P, P, P, P, I, I, P],
+    "avd_softmax_xent": [P, L, I, I, P, I, I, I, F, P, P, L, I, P],
+    "avd_ema": [P, P, L, F, P],
+    "avd_adam": [P, P, P, P, L, F, F, F, F, F, F, F, P],
+    "avd_sum": [P, I, F, P, P],
+    "avd_stage_views": [P, I, P, I, P, I, I, P, I, P],
+}
+
+
+class AvdError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libavdino.so not found at {LIB_PATH}: build it with "
+            f"`make -C multimodal-ssl-avmnist_amd/csrc` (or __graft_entry__.build()). "
+            f"There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, args in PROTOS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    lib.avd_last_error.argtypes = []
+    lib.avd_last_error.restype = ctypes.c_char_p
+    return lib
+
+
+lib = _load()
+
+STATUS = {-1: "AVD_ERR_SHAPE", -2: "AVD_ERR_DTYPE", -3: "AVD_ERR_HIP", -4: "AVD_ERR_ARG"}
+
+
+def check(rc, name="avd"):
+    if rc != 0:
+        msg = STATUS.get(rc, str(rc))
+        if rc == -3:
+            msg += f" ({lib.avd_last_error().decode()})"
+        raise AvdError(f"{name} failed: {msg}")
+    return rc
+
+
+def call(name, *args):
+    return check(getattr(lib, name)(*args), name)

@@ -1,0 +1,445 @@
+"""The training-step engine: explicit forward and backward of the reference's multimodal-DINO
+step over libavdino kernels (no autograd, no per-view Python loop, no per-parameter loops).
+
+Reference step, multi_central with training_mode mse:
+  MultiModalDINOWithMSELightning.training_step (dino.py:1214-1238)
+    MultiModalDINO.forward (dino.py:655-727): student over 2 global + 4 local views, teacher
+      over the global views (no grad, train mode), projections, centring, update_center
+    + image/audio projection heads on the original image/audio (dino.py:1163-1171)
+    dino_loss (822-854) + alpha * mse_loss (1193-1211)
+    update_teacher (635-646)  <- before backward / Adam, so the EMA sees the pre-step student
+  Lightning: zero_grad -> backward -> Adam.step (configure_optimizers 953-962)
+
+MI355X-native restructuring (results identical up to fp32 rounding):
+  * all views of a step go through each conv layer in ONE launch (N = views*B samples) with
+    BatchNorm statistics kept per (view, channel): same math as the reference's per-view
+    calls, one launch instead of V;
+  * the student's original-image/audio pass of the MSE / InfoNCE / supervised heads shares
+    those launches (one more BN group), and its gradient accumulates in the same wgrad;
+  * cat() of image/audio features is a strided GEMM write; slices are pointer offsets;
+  * EMA / Adam / grad all-reduce run on flat arenas (params.py).
+"""
+import torch
+
+from . import ops
+from .spec import (CENTRAL_AUDIO_CONVS, CENTRAL_IMAGE_CONVS, CNN3_AUDIO_CONVS, CNN3_IMAGE_CONVS,
+                   HEAD_NAMES, PROJ_HIDDEN, central_stack, cnn3_stack)
+
+F32 = torch.float32
+
+
+class Workspace:
+    """Named device scratch buffers, grown on demand and reused across steps."""
+
+    def __init__(self, device):
+        self.device = device
+        self.bufs = {}
+
+    def get(self, name, numel, dtype=F32):
+        b = self.bufs.get(name)
+        if b is None or b.numel() < numel or b.dtype != dtype:
+            b = torch.empty(max(numel, 1), dtype=dtype, device=self.device)
+            self.bufs[name] = b
+        return b[:numel]
+
+    def nbytes(self):
+        return sum(b.numel() * b.element_size() for b in self.bufs.values())
+
+
+# ============================================================================ conv stacks
+class ConvBranch:
+    """conv -> BN(train, per group) -> ReLU -> maxpool2 stack (+ flatten or GAP), fwd/bwd."""
+
+    def __init__(self, stack, act_dtype):
+        self.stack = stack
+        self.act = act_dtype
+        self.dims = stack.layer_dims()
+
+    def prepare(self, ws, store, tag, need_dgrad):
+        """Kernel weight layouts for this step (weights change every step)."""
+        wts = []
+        for i, (ci, co, k, _p) in enumerate(self.stack.convs):
+            w = store[self.stack.conv_keys[i] + ".weight"]
+            mf = 2 if ops.mfma_conv(self.act, ci) else 0
+            wt = ws.get(f"{tag}.wt{i}", ops.conv_weight_layout_elems(co, ci, k, mf),
+                        torch.bfloat16 if mf else F32)
+            ops.conv_weight_layout(w, wt, mf)
+            wd = None
+            if need_dgrad and i > 0:
+                md = 3 if ops.mfma_conv(self.act, co) else 1
+                wd = ws.get(f"{tag}.wd{i}", ops.conv_weight_layout_elems(co, ci, k, md),
+                            torch.bfloat16 if md == 3 else F32)
+                ops.conv_weight_layout(w, wd, md)
+            wts.append((wt, wd))
+        return wts
+
+    def forward(self, ws, store, tag, x, N, G, update_running=True, need_dgrad=False):
+        """x: staged input [N,1,H,W] (act dtype).  Returns (features f32 [N, F], ctx)."""
+        B = N // G
+        wts = self.prepare(ws, store, tag, need_dgrad)
+        ctx = {"x": [x], "y": [], "stats": [], "wts": wts, "N": N, "G": G}
+        h = x
+        for i, (ci, co, k, pad) in enumerate(self.stack.convs):
+            H, Ho, Hp = self.dims[i]
+            T = ops.conv_stat_tiles(Ho, Ho)
+            y = ws.get(f"{tag}.y{i}", N * co * Ho * Ho, self.act)
+            parts = ws.get("stat_parts", co * N * T * 2)
+            ops.conv2d_fwd(h, wts[i][0], store[self.stack.conv_keys[i] + ".bias"], y, parts,
+                           N, ci, H, H, co, k, pad)
+            st = ws.get(f"{tag}.bn{i}", 4 * G * co).view(4, G * co)
+            bk = self.stack.bn_keys[i]
+            ops.bn_finalize(parts, G, B * T, co, B * Ho * Ho, store[bk + ".weight"], store[bk + ".bias"],
+                            st[0], st[1], st[2], st[3],
+                            store[bk + ".running_mean"] if update_running else None,
+                            store[bk + ".running_var"] if update_running else None)
+            if update_running:
+                store.buffers[bk + ".num_batches_tracked"] += G
+            ctx["y"].append(y)
+            ctx["stats"].append(st)
+            last = i == len(self.stack.convs) - 1
+            if last and self.stack.gap:
+                out = ws.get(f"{tag}.feat", N * co, F32)
+                ops.bn_relu_pool(y, st[2], st[3], out, 1, N, B, co, Ho, Ho)
+            elif last:
+                out = ws.get(f"{tag}.feat", N * co * Hp * Hp, F32)
+                ops.bn_relu_pool(y, st[2], st[3], out, 0, N, B, co, Ho, Ho)
+            else:
+                out = ws.get(f"{tag}.x{i + 1}", N * co * Hp * Hp, self.act)
+                ops.bn_relu_pool(y, st[2], st[3], out, 0, N, B, co, Ho, Ho)
+                ctx["x"].append(out)
+            h = out
+        return h.view(N, -1), ctx
+
+    def backward(self, ws, store, ctx, dfeat):
+        """dfeat: f32 [N, F] gradient of the features; writes conv/BN parameter grads."""
+        N, G = ctx["N"], ctx["G"]
+        B = N // G
+        gout = dfeat
+        nl = len(self.stack.convs)
+        for i in reversed(range(nl)):
+            ci, co, k, pad = self.stack.convs[i]
+            H, Ho, Hp = self.dims[i]
+            y, st = ctx["y"][i], ctx["stats"][i]
+            pool_mode = 1 if (i == nl - 1 and self.stack.gap) else 0
+            bk, ck = self.stack.bn_keys[i], self.stack.conv_keys[i]
+            parts = ws.get("bwd_parts", co * N * 2)
+            ops.bn_bwd_reduce(y, gout, pool_mode, st[2], st[3], st[0], st[1], parts, N, B, co, Ho, Ho)
+            coef = ws.get("bwd_coef", G * co * 3)
+            ops.bn_bwd_finalize(parts, G, B, co, B * Ho * Ho, store[bk + ".weight"], st[0], st[1],
+                                coef, store.grad_of(bk + ".weight"), store.grad_of(bk + ".bias"),
+                                store.grad_of(ck + ".bias"))
+            dy = ws.get("bwd_dy", N * co * Ho * Ho, self.act)
+            ops.bn_bwd_apply(y, gout, pool_mode, st[2], st[3], coef, dy, N, B, co, Ho, Ho)
+            x = ctx["x"][i]
+            nch = ops.wgrad_chunks(N, co, ci, k)
+            wparts = ws.get("wgrad_parts", nch * co * ci * k * k)
+            ops.conv2d_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
+            ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
+            if i > 0:
+                dx = ws.get("bwd_dx", N * ci * H * H, self.act)
+                ops.conv2d_dgrad(dy, ctx["wts"][i][1], dx, N, ci, H, H, co, k, pad)
+                gout = dx
+
+
+# ============================================================================ dense heads
+class ProjHead:
+    """ProjectionHead (dino.py:1240-1254): Linear -> BN1d(train) -> GELU -> Dropout -> Linear."""
+
+    def __init__(self, prefix, in_dim, out_dim, hidden=PROJ_HIDDEN):
+        self.p = prefix
+        self.i, self.o, self.h = in_dim, out_dim, hidden
+
+    def forward(self, ws, store, tag, x, rows, out, drop_p=0.0, seed=0, x_ld=None, x_off=0,
+                update_running=True):
+        p, Hd = self.p, self.h
+        h = ws.get(f"{tag}.h", rows * Hd)
+        ops.linear_fwd(x, store[p + ".mlp.0.weight"], store[p + ".mlp.0.bias"], h, rows,
+                       x_ld=x_ld, x_off=x_off)
+        R = ops.colstats_parts(rows)
+        parts = ws.get("stat_parts", Hd * R * 2)
+        ops.colstats(h, rows, 1, Hd, parts)
+        st = ws.get(f"{tag}.bn", 4 * Hd).view(4, Hd)
+        ops.bn_finalize(parts, 1, R, Hd, rows, store[p + ".mlp.1.weight"], store[p + ".mlp.1.bias"],
+                        st[0], st[1], st[2], st[3],
+                        store[p + ".mlp.1.running_mean"] if update_running else None,
+                        store[p + ".mlp.1.running_var"] if update_running else None)
+        if update_running:
+            store.buffers[p + ".mlp.1.num_batches_tracked"] += 1
+        a = ws.get(f"{tag}.a", rows * Hd)
+        ops.act_fwd(h, a, 1, st[2], st[3], rows, 1, Hd, drop_p, seed)
+        ops.linear_fwd(a, store[p + ".mlp.4.weight"], store[p + ".mlp.4.bias"], out, rows)
+        return {"x": x, "x_ld": x_ld if x_ld is not None else self.i, "x_off": x_off, "h": h,
+                "a": a, "st": st, "rows": rows, "drop_p": drop_p, "seed": seed}
+
+    def backward(self, ws, store, ctx, dout, dx, dx_ld=None, dx_off=0):
+        p, Hd, rows = self.p, self.h, ctx["rows"]
+        da = ws.get("head_da", rows * Hd)
+        ops.linear_bwd(dout, ctx["a"], store[p + ".mlp.4.weight"], store.grad_of(p + ".mlp.4.weight"),
+                       store.grad_of(p + ".mlp.4.bias"), da, rows)
+        st = ctx["st"]
+        dz = ws.get("head_dz", rows * Hd)
+        ops.act_bwd(ctx["h"], da, dz, 1, st[2], st[3], rows, 1, Hd, ctx["drop_p"], ctx["seed"])
+        R = ops.colstats_parts(rows)
+        parts = ws.get("bwd_parts", Hd * R * 2)
+        ops.bn1d_bwd_reduce(ctx["h"], dz, st[0], st[1], rows, 1, Hd, parts)
+        coef = ws.get("bwd_coef", Hd * 3)
+        ops.bn_bwd_finalize(parts, 1, R, Hd, rows, store[p + ".mlp.1.weight"], st[0], st[1], coef,
+                            store.grad_of(p + ".mlp.1.weight"), store.grad_of(p + ".mlp.1.bias"), None)
+        dh = ws.get("head_dh", rows * Hd)
+        ops.bn1d_bwd_apply(ctx["h"], dz, coef, dh, rows, 1, Hd)
+        ops.linear_bwd(dh, ctx["x"], store[p + ".mlp.0.weight"], store.grad_of(p + ".mlp.0.weight"),
+                       store.grad_of(p + ".mlp.0.bias"), dx, rows, x_ld=ctx["x_ld"],
+                       x_off=ctx["x_off"], dx_ld=dx_ld, dx_off=dx_off)
+
+
+class Hyper:
+    def __init__(self, lr=1e-4, weight_decay=1e-6, momentum=0.996, center_momentum=0.9,
+                 student_temperature=0.1, teacher_temperature=0.04, dropout=0.3,
+                 fusion_dropout=0.3, alpha=1.0, betas=(0.9, 0.999), eps=1e-8):
+        self.lr, self.wd = lr, weight_decay
+        self.momentum, self.center_momentum = momentum, center_momentum
+        self.tau_s, self.tau_t = student_temperature, teacher_temperature
+        self.dropout, self.fusion_dropout = dropout, fusion_dropout
+        self.alpha = alpha
+        self.betas, self.eps = betas, eps
+
+
+def adam_step(store, hp):
+    """torch.optim.Adam over the live arena (params with grad=None are outside it)."""
+    store.adam_step += 1
+    t = store.adam_step
+    b1, b2 = hp.betas
+    ops.adam(store.student, store.grad, store.adam_m, store.adam_v, store.n_live, hp.lr, b1, b2,
+             hp.eps, hp.wd, 1 - b1 ** t, 1 - b2 ** t)
+
+
+def ema_step(store, m):
+    ops.ema(store.teacher, store.student[store.n_heads:], store.n_ema, m)
+
+
+# ============================================================================ multimodal DINO
+class MultiCentralEngine:
+    """Training step of MultiModalDINO{,WithMSE,WithINFONCE,SemiSupervised} over
+    CentralMultiModalEncoder (``--model multi_central --training_mode {default,mse,infonce,
+    semi_supervised}``)."""
+
+    def __init__(self, store, mode, E, D, P, hp, act_dtype=F32, grad_hook=None, seed=0):
+        self.store, self.mode, self.E, self.D, self.P, self.hp = store, mode, E, D, P, hp
+        self.act = act_dtype
+        self.ws = Workspace(store.device)
+        self.img = ConvBranch(central_stack("student.image_encoder.0", CENTRAL_IMAGE_CONVS, 28), act_dtype)
+        self.aud = ConvBranch(central_stack("student.audio_encoder.0", CENTRAL_AUDIO_CONVS, 112), act_dtype)
+        self.t_img = ConvBranch(central_stack("teacher.image_encoder.0", CENTRAL_IMAGE_CONVS, 28), act_dtype)
+        self.t_aud = ConvBranch(central_stack("teacher.audio_encoder.0", CENTRAL_AUDIO_CONVS, 112), act_dtype)
+        self.sproj = ProjHead("student_projection", D, P)
+        self.tproj = ProjHead("teacher_projection", D, P)
+        self.heads = None
+        if mode in HEAD_NAMES:
+            hi, ha = HEAD_NAMES[mode]
+            out = 10 if mode == "semi_supervised" else P
+            self.heads = (ProjHead(hi, E, out), ProjHead(ha, E, out))
+        self.grad_hook = grad_hook  # e.g. DDP all-reduce of store.grad
+        self.seed = seed
+        self.step_idx = 0
+        self.last = {}
+
+    # -------------------------------------------------------------- pieces
+    def _encoder_fwd(self, prefix, ib, ab, x_img, x_aud, N, G, tag, need_dgrad, update_running=True):
+        """Image + audio conv stacks and their Linear(., E) into one [N, 2E] buffer (= the cat)."""
+        ws, st, E = self.ws, self.store, self.E
+        fi, ci = ib.forward(ws, st, tag + ".img", x_img, N, G, update_running, need_dgrad)
+        fa, ca = ab.forward(ws, st, tag + ".aud", x_aud, N, G, update_running, need_dgrad)
+        cat = ws.get(tag + ".cat", N * 2 * E)
+        ops.linear_fwd(fi, st[prefix + ".image_encoder.1.weight"], st[prefix + ".image_encoder.1.bias"],
+                       cat, N, out_ld=2 * E, out_off=0)
+        ops.linear_fwd(fa, st[prefix + ".audio_encoder.1.weight"], st[prefix + ".audio_encoder.1.bias"],
+                       cat, N, out_ld=2 * E, out_off=E)
+        return cat, (fi, ci, fa, ca)
+
+    def _fusion_fwd(self, prefix, cat, rows, tag, seed):
+        """fusion: Linear(2E,E) -> ReLU -> Dropout(0.3, hard-coded dino.py:204/215) -> Linear(E,D)."""
+        ws, st, E, D = self.ws, self.store, self.E, self.D
+        h = ws.get(tag + ".fh", rows * E)
+        ops.linear_fwd(cat, st[prefix + ".fusion.0.weight"], st[prefix + ".fusion.0.bias"], h, rows,
+                       x_ld=2 * E)
+        r = ws.get(tag + ".fr", rows * E)
+        ops.act_fwd(h, r, 0, None, None, rows, 1, E, self.hp.fusion_dropout, seed)
+        out = ws.get(tag + ".fout", rows * D)
+        ops.linear_fwd(r, st[prefix + ".fusion.3.weight"], st[prefix + ".fusion.3.bias"], out, rows)
+        return out, (h, r)
+
+    def stage(self, batch, with_orig):
+        """Device batch dict -> view-major staged image/audio inputs (act dtype)."""
+        ws = self.ws
+        g_img, l_img = batch["g_img"], batch["l_img"]
+        B, G = g_img.shape[:2]
+        L = l_img.shape[1]
+        nv = G + L + (1 if with_orig else 0)
+        x_img = ws.get("in.img", nv * B * 784, self.act)
+        x_aud = ws.get("in.aud", nv * B * 12544, self.act)
+        ops.stage_views(g_img.contiguous(), G, l_img.contiguous() if L else None, L,
+                        batch["image"].contiguous() if with_orig else None, B, 784, x_img)
+        ops.stage_views(batch["g_aud"].contiguous(), G, batch["l_aud"].contiguous() if L else None, L,
+                        batch["audio"].contiguous() if with_orig else None, B, 12544, x_aud)
+        return x_img, x_aud, B, G, L
+
+    # -------------------------------------------------------------- the step
+    def forward(self, batch, training=True):
+        # training=False skips the input-grad weight layouts (forward-only use of the API)
+        """Forward of the whole step; fills self.last with everything backward needs.
+        Returns device tensors (s_out [V,B,P], t_out [G,B,P] centred, head outputs or None)."""
+        hp, ws, st = self.hp, self.ws, self.store
+        E, D, P = self.E, self.D, self.P
+        with_orig = self.heads is not None
+        x_img, x_aud, B, G, L = self.stage(batch, with_orig)
+        V = G + L
+        NG = V + (1 if with_orig else 0)   # BN groups of the student pass
+        N = NG * B
+        base = (self.seed * 1000003 + self.step_idx * 16) & 0xFFFFFFFFFFFF
+
+        # student: all views (+ originals) in one pass per conv layer
+        cat, senc = self._encoder_fwd("student", self.img, self.aud, x_img, x_aud, N, NG, "s",
+                                      need_dgrad=training)
+        fout, sfus = self._fusion_fwd("student", cat, V * B, "s", base + 1)
+        # teacher: global views (prefix of the staged buffers), train-mode BN, no grad
+        tcat, _ = self._encoder_fwd("teacher", self.t_img, self.t_aud, x_img[:G * B * 784],
+                                    x_aud[:G * B * 12544], G * B, G, "t", need_dgrad=False)
+        tout, _ = self._fusion_fwd("teacher", tcat, G * B, "t", base + 2)
+        s_proj = ws.get("s_proj", V * B * P)
+        spc = self.sproj.forward(ws, st, "sp", fout, V * B, s_proj, hp.dropout, base + 3)
+        t_proj = ws.get("t_proj", G * B * P)
+        self.tproj.forward(ws, st, "tp", tout, G * B, t_proj, 0.0, 0)
+
+        # DINO loss (+ centring and centre EMA) -- forward and d/ds in one pass
+        loss_parts = ws.get("loss_parts", V * B + B)
+        ds = ws.get("ds", V * B * P)
+        center_new = ws.get("center_new", P)
+        work = ws.get("dino_work", (B + G * B) * P)
+        center = st["center"]
+        ops.dino_loss(s_proj, t_proj, center, V, G, B, P, hp.tau_s, hp.tau_t, hp.center_momentum,
+                      False, loss_parts[:V * B], ds, center_new, work)
+        t_out = ws.get("t_out", G * B * P)  # centred teacher output (API only; the loss used t_raw)
+        head_out = None
+        hctx = None
+        n_parts = V * B
+        if with_orig:
+            hi, ha = self.heads
+            no = hi.o
+            zi = ws.get("zi", B * no)
+            za = ws.get("za", B * no)
+            off = V * B * 2 * E
+            ci = hi.forward(ws, st, "hi", cat, B, zi, 0.0, 0, x_ld=2 * E, x_off=off)
+            ca = ha.forward(ws, st, "ha", cat, B, za, 0.0, 0, x_ld=2 * E, x_off=off + E)
+            dzi = ws.get("dzi", B * no)
+            dza = ws.get("dza", B * no)
+            aux = loss_parts[V * B:V * B + B]
+            if self.mode == "mse":
+                ops.mse_loss(zi, za, B, no, aux, dzi, dza)
+                # mse parts are already divided by B*P; loss = sum
+            elif self.mode == "infonce":
+                self._infonce(zi, za, B, no, aux, dzi, dza)
+            else:
+                self._supervised(zi, za, batch["label"], B, no, aux, dzi, dza)
+            if hp.alpha != 1.0:
+                aux.mul_(hp.alpha)
+                dzi.mul_(hp.alpha)
+                dza.mul_(hp.alpha)
+            n_parts = V * B + B
+            head_out = (zi, za)
+            hctx = (ci, ca, dzi, dza)
+        loss = ws.get("loss", 1)
+        ops.sum_to(loss_parts, n_parts, 1.0, loss)
+        self.last = dict(B=B, G=G, L=L, V=V, NG=NG, N=N, cat=cat, senc=senc, sfus=sfus, spc=spc,
+                         ds=ds, hctx=hctx, center_new=center_new, loss=loss, s_proj=s_proj,
+                         t_proj=t_proj, training=training)
+        return loss
+
+    def _infonce(self, zi, za, B, P, aux, dzi, dza, temperature=0.07):
+        """infoNCE_loss (dino.py:1091-1128): symmetric CE over S = n(i) n(a)^T / tau."""
+        ws = self.ws
+        ni, na = ws.get("nce.ni", B * P), ws.get("nce.na", B * P)
+        nri, nra = ws.get("nce.nri", B), ws.get("nce.nra", B)
+        ops.l2norm_fwd(zi, ni, nri, B, P)
+        ops.l2norm_fwd(za, na, nra, B, P)
+        S = ws.get("nce.S", B * B)
+        ops.gemm(B, B, P, ni, P, 1, na, 1, P, S, B, alpha=1.0 / temperature)
+        dS = ws.get("nce.dS", B * B)
+        parts = ws.get("nce.parts", 2 * B)
+        ops.softmax_xent(S, B, B, B, None, 1, False, False, 0.5 / B, parts[:B], dS, B, False)
+        ops.softmax_xent(S, B, B, B, None, 1, True, False, 0.5 / B, parts[B:], dS, B, True)
+        ops.sum_to(parts, 2 * B, 0.5 / B, aux[:1])
+        aux[1:].zero_()
+        dni, dna = ws.get("nce.dni", B * P), ws.get("nce.dna", B * P)
+        ops.gemm(B, P, B, dS, B, 1, na, P, 1, dni, P, alpha=1.0 / temperature)
+        ops.gemm(B, P, B, dS, 1, B, ni, P, 1, dna, P, alpha=1.0 / temperature)
+        ops.l2norm_bwd(ni, nri, dni, dzi, B, P)
+        ops.l2norm_bwd(na, nra, dna, dza, B, P)
+
+    def _supervised(self, zi, za, labels, B, C, aux, dzi, dza):
+        """supervised_loss (dino.py:1001-1025): CE(image) + CE(audio), mean over the batch."""
+        ws = self.ws
+        parts = ws.get("sup.parts", 2 * B)
+        ops.softmax_xent(zi, C, B, C, labels, 0, False, False, 1.0 / B, parts[:B], dzi, C, False)
+        ops.softmax_xent(za, C, B, C, labels, 0, False, False, 1.0 / B, parts[B:], dza, C, False)
+        ops.sum_to(parts, 2 * B, 1.0 / B, aux[:1])
+        aux[1:].zero_()
+
+    def update_center(self):
+        self.store["center"].copy_(self.last["center_new"].view(1, -1))
+
+    def backward(self):
+        ws, st, E, D, P = self.ws, self.store, self.E, self.D, self.P
+        c = self.last
+        B, V, N = c["B"], c["V"], c["N"]
+        # d cat buffer [N, 2E]: rows [0, V*B) from the fusion, rows [V*B, N) from the heads
+        dcat = ws.get("dcat", N * 2 * E)
+        dfout = ws.get("dfout", V * B * D)
+        self.sproj.backward(ws, st, c["spc"], c["ds"], dfout)
+        h, r = c["sfus"]
+        dr = ws.get("fus_dr", V * B * E)
+        ops.linear_bwd(dfout, r, st["student.fusion.3.weight"], st.grad_of("student.fusion.3.weight"),
+                       st.grad_of("student.fusion.3.bias"), dr, V * B)
+        dh = ws.get("fus_dh", V * B * E)
+        ops.act_bwd(h, dr, dh, 0, None, None, V * B, 1, E, self.hp.fusion_dropout,
+                    (self.seed * 1000003 + self.step_idx * 16 + 1) & 0xFFFFFFFFFFFF)
+        ops.linear_bwd(dh, c["cat"], st["student.fusion.0.weight"], st.grad_of("student.fusion.0.weight"),
+                       st.grad_of("student.fusion.0.bias"), dcat, V * B, x_ld=2 * E)
+        if c["hctx"] is not None:
+            ci, ca, dzi, dza = c["hctx"]
+            hi, ha = self.heads
+            off = V * B * 2 * E
+            hi.backward(ws, st, ci, dzi, dcat, dx_ld=2 * E, dx_off=off)
+            ha.backward(ws, st, ca, dza, dcat, dx_ld=2 * E, dx_off=off + E)
+        fi, cimg, fa, caud = c["senc"]
+        dfi = ws.get("dfeat_img", N * fi.shape[1])
+        ops.linear_bwd(dcat, fi, st["student.image_encoder.1.weight"],
+                       st.grad_of("student.image_encoder.1.weight"),
+                       st.grad_of("student.image_encoder.1.bias"), dfi, N, dout_ld=2 * E)
+        self.img.backward(ws, st, cimg, dfi)
+        dfa = ws.get("dfeat_aud", N * fa.shape[1])
+        ops.linear_bwd(dcat, fa, st["student.audio_encoder.1.weight"],
+                       st.grad_of("student.audio_encoder.1.weight"),
+                       st.grad_of("student.audio_encoder.1.bias"), dfa, N, dout_ld=2 * E, dout_off=E)
+        self.aud.backward(ws, st, caud, dfa)
+
+    def step(self, batch):
+        """One full training step; returns the loss as a device tensor (no host sync)."""
+        loss = self.forward(batch, training=True)
+        self.update_center()
+        ema_step(self.store, self.hp.momentum)     # update_teacher: pre-step student
+        self.backward()
+        if self.grad_hook is not None:
+            self.grad_hook(self.store.grad)
+        adam_step(self.store, self.hp)
+        self.step_idx += 1
+        return loss
+
+    def outputs(self):
+        """(s_out [V,B,P], t_out [G,B,P] centred with the pre-update centre) of the last
+        forward, as MultiModalDINO.forward returns them (dino.py:719-727).  Call before
+        update_center()."""
+        c = self.last
+        B, V, G, P = c["B"], c["V"], c["G"], self.P
+        s = c["s_proj"].view(V, B, P)
+        t = c["t_proj"].view(G, B, P) - self.store["center"].view(1, 1, P)
+        return s, t

@@ -1,0 +1,293 @@
+"""Tensor-level wrappers over the C ABI (include/avdino.h).
+
+Every function takes torch tensors that live on the HIP device, checks shapes/dtypes on the
+host, and launches on torch's current stream.  PyTorch is used here only for device memory
+and streams; all arithmetic happens in libavdino.so.
+"""
+import torch
+
+from ._lib import BF16, F32, call, lib
+
+_DT = {torch.float32: F32, torch.bfloat16: BF16}
+
+
+def dtcode(t):
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {t.dtype}") from None
+
+
+def p(t):
+    """Device pointer of a (contiguous) tensor, or None."""
+    if t is None:
+        return None
+    if not t.is_contiguous():
+        raise ValueError("tensor must be contiguous")
+    return t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+class KernelTimer:
+    """Optional HIP-event timing of selected launches (bench.py's live roofline).
+
+    Each instrumented op reports a key (op name + shape), its algorithmic HBM bytes and
+    FLOPs; events are recorded on the launching stream around the launch.  ``only`` limits
+    timing to one key (the dominant kernel) so the timed region stays undisturbed."""
+
+    def __init__(self, only=None):
+        self.only = only
+        self.rec = []  # (key, bytes, flops, start_event, end_event)
+
+    def wrap(self, key, nbytes, flops, fn):
+        if self.only is not None and key != self.only:
+            return fn()
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        out = fn()
+        e.record()
+        self.rec.append((key, nbytes, flops, s, e))
+        return out
+
+    def summary(self):
+        torch.cuda.synchronize()
+        agg = {}
+        for key, nb, fl, s, e in self.rec:
+            a = agg.setdefault(key, [0, 0.0, 0, 0])
+            a[0] += 1
+            a[1] += s.elapsed_time(e)
+            a[2] += nb
+            a[3] += fl
+        return {k: dict(calls=v[0], ms=v[1], bytes=v[2], flops=v[3]) for k, v in agg.items()}
+
+
+TIMER = None
+
+
+def _timed(key, nbytes, flops, fn):
+    if TIMER is None:
+        return fn()
+    return TIMER.wrap(key, nbytes, flops, fn)
+
+
+def _need(cond, msg):
+    if not cond:
+        raise ValueError(msg)
+
+
+# ---------------------------------------------------------------- conv blocks
+def conv_stat_tiles(Ho, Wo):
+    return lib.avd_conv2d_stat_tiles(Ho, Wo)
+
+
+def conv_weight_layout_elems(Cout, Cin, K, mode):
+    return lib.avd_conv_weight_layout_elems(Cout, Cin, K, mode)
+
+
+def conv_weight_layout(w, wt, mode):
+    """mode 0/1: f32 VALU layouts (fwd / input-grad); 2/3: bf16 MFMA layouts."""
+    Cout, Cin, K, _ = w.shape
+    _need(wt.numel() >= conv_weight_layout_elems(Cout, Cin, K, mode), "wt size")
+    _need(wt.dtype == (torch.bfloat16 if mode >= 2 else torch.float32), "wt dtype")
+    call("avd_conv_weight_layout", p(w), p(wt), Cout, Cin, K, mode, stream())
+
+
+def mfma_conv(x_dtype, cin):
+    """True when avd_conv2d_fwd / _dgrad take the MFMA path (and want layouts 2 / 3)."""
+    return x_dtype == torch.bfloat16 and cin % 8 == 0 and cin <= 128
+
+
+def conv2d_fwd(x, wt, bias, y, stats, N, Cin, H, W, Cout, K, pad):
+    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
+    _need(x.numel() == N * Cin * H * W, "conv x size")
+    _need(y.numel() == N * Cout * Ho * Wo, "conv y size")
+    if stats is not None:
+        _need(stats.numel() >= Cout * N * conv_stat_tiles(Ho, Wo) * 2, "conv stats size")
+    nb = x.numel() * x.element_size() + y.numel() * y.element_size()
+    fl = 2 * N * Cout * Ho * Wo * Cin * K * K
+    _timed(f"conv2d_fwd[{N}x{Cin}x{H}x{W}->{Cout} k{K}p{pad} {x.dtype}]", nb, fl,
+           lambda: call("avd_conv2d_fwd", p(x), dtcode(x), p(wt), p(bias), p(y), dtcode(y),
+                        p(stats), N, Cin, H, W, Cout, K, pad, stream()))
+
+
+def conv2d_dgrad(dy, wt_d, dx, N, Cin, H, W, Cout, K, pad):
+    _need(dx.numel() == N * Cin * H * W and dx.dtype == dy.dtype, "dgrad dx")
+    nb = (dy.numel() + dx.numel()) * dy.element_size()
+    fl = 2 * N * Cin * H * W * Cout * K * K
+    _timed(f"conv2d_dgrad[{N}x{Cout}->{Cin}x{H}x{W} k{K}p{pad} {dy.dtype}]", nb, fl,
+           lambda: call("avd_conv2d_dgrad", p(dy), p(wt_d), p(dx), dtcode(dy), N, Cin, H, W, Cout,
+                        K, pad, stream()))
+
+
+def wgrad_chunks(N, Cout, Cin, K):
+    return lib.avd_conv2d_wgrad_chunks(N, Cout, Cin, K)
+
+
+def conv2d_wgrad(x, dy, parts, N, Cin, H, W, Cout, K, pad):
+    _need(parts.numel() >= wgrad_chunks(N, Cout, Cin, K) * Cout * Cin * K * K, "wgrad parts")
+    nb = x.numel() * x.element_size() + dy.numel() * dy.element_size()
+    fl = 2 * dy.numel() * Cin * K * K
+    _timed(f"conv2d_wgrad[{N}x{Cin}x{H}x{W}->{Cout} k{K}p{pad} {x.dtype}]", nb, fl,
+           lambda: call("avd_conv2d_wgrad", p(x), dtcode(x), p(dy), dtcode(dy), p(parts), N, Cin,
+                        H, W, Cout, K, pad, stream()))
+
+
+def bn_finalize(parts, G, R, C, count, gamma, beta, mean, invstd, scale, shift, rm=None, rv=None,
+                eps=1e-5, momentum=0.1):
+    call("avd_bn_finalize", p(parts), G, R, C, count, p(gamma), p(beta), eps, momentum, p(mean),
+         p(invstd), p(scale), p(shift), p(rm), p(rv), stream())
+
+
+def bn_relu_pool(y, scale, shift, out, pool_mode, N, B, C, H, W):
+    _need(y.numel() == N * C * H * W and scale.numel() >= (N // B) * C, "bn_relu_pool y")
+    _need(out.numel() == (N * C if pool_mode else N * C * (H // 2) * (W // 2)), "bn_relu_pool out")
+    nb = y.numel() * y.element_size() + out.numel() * out.element_size()
+    _timed(f"bn_relu_pool[{N}x{C}x{H}x{W} {y.dtype}]", nb, 0,
+           lambda: call("avd_bn_relu_pool", p(y), dtcode(y), p(scale), p(shift), p(out),
+                        dtcode(out), pool_mode, N, B, C, H, W, stream()))
+
+
+def bn_bwd_reduce(y, gout, pool_mode, scale, shift, mean, invstd, parts, N, B, C, H, W):
+    _need(y.numel() == N * C * H * W and parts.numel() >= C * N * 2, "bn_bwd_reduce sizes")
+    _need(gout.numel() == (N * C if pool_mode else N * C * (H // 2) * (W // 2)), "bn_bwd gout")
+    nb = y.numel() * y.element_size() + gout.numel() * gout.element_size()
+    _timed(f"bn_bwd_reduce[{N}x{C}x{H}x{W} {y.dtype}]", nb, 0,
+           lambda: call("avd_bn_bwd_reduce", p(y), dtcode(y), p(gout), dtcode(gout), pool_mode,
+                        p(scale), p(shift), p(mean), p(invstd), p(parts), N, B, C, H, W, stream()))
+
+
+def bn_bwd_finalize(parts, G, R, C, count, gamma, mean, invstd, coef, dgamma, dbeta, dbias,
+                    accumulate=0):
+    call("avd_bn_bwd_finalize", p(parts), G, R, C, count, p(gamma), p(mean), p(invstd), p(coef),
+         p(dgamma), p(dbeta), p(dbias), accumulate, stream())
+
+
+def bn_bwd_apply(y, gout, pool_mode, scale, shift, coef, dy, N, B, C, H, W):
+    _need(y.numel() == N * C * H * W and dy.numel() == y.numel(), "bn_bwd_apply sizes")
+    _need(gout.numel() == (N * C if pool_mode else N * C * (H // 2) * (W // 2)), "bn_bwd gout")
+    _need(coef.numel() >= (N // B) * C * 3, "bn_bwd coef")
+    nb = (y.numel() * y.element_size() + gout.numel() * gout.element_size()
+          + dy.numel() * dy.element_size())
+    _timed(f"bn_bwd_apply[{N}x{C}x{H}x{W} {y.dtype}]", nb, 0,
+           lambda: call("avd_bn_bwd_apply", p(y), dtcode(y), p(gout), dtcode(gout), pool_mode,
+                        p(scale), p(shift), p(coef), p(dy), dtcode(dy), N, B, C, H, W, stream()))
+
+
+# ---------------------------------------------------------------- dense
+def gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, bias=None, alpha=1.0, beta=0.0,
+         a_rowsum=None, a_off=0, b_off=0, c_off=0):
+    """C[m,n] = alpha*sum_k A[m,k]B[k,n] (+bias[n]) (+beta*C).  *_off are element offsets into
+    the (flat, f32) storage of A/B/C so row/column slices need no copies."""
+    for t in (A, B, C):
+        _need(t.dtype == torch.float32 and t.is_contiguous(), "gemm operands are contiguous f32")
+    # every element the kernel may touch must lie inside the tensors (no device OOB)
+    _need(a_off >= 0 and a_off + (M - 1) * sam + (K - 1) * sak < A.numel(), "gemm A bounds")
+    _need(b_off >= 0 and b_off + (K - 1) * sbk + (N - 1) * sbn < B.numel(), "gemm B bounds")
+    _need(c_off >= 0 and c_off + (M - 1) * ldc + (N - 1) < C.numel(), "gemm C bounds")
+    _need(bias is None or bias.numel() >= N, "gemm bias")
+    _need(a_rowsum is None or a_rowsum.numel() >= M, "gemm rowsum")
+    _timed(f"gemm[{M}x{N}x{K}]", 4 * (M * K + K * N + M * N), 2 * M * N * K,
+           lambda: call("avd_gemm", M, N, K, A.data_ptr() + 4 * a_off, sam, sak,
+                        B.data_ptr() + 4 * b_off, sbk, sbn, C.data_ptr() + 4 * c_off, ldc, p(bias),
+                        alpha, beta, p(a_rowsum), stream()))
+
+
+def linear_fwd(x, w, b, out, rows, x_ld=None, x_off=0, out_ld=None, out_off=0):
+    """out[rows, O] = x[rows, I] W^T + b   (W [O, I])."""
+    O, In = w.shape
+    x_ld = In if x_ld is None else x_ld
+    out_ld = O if out_ld is None else out_ld
+    gemm(rows, O, In, x, x_ld, 1, w, 1, In, out, out_ld, bias=b, a_off=x_off, c_off=out_off)
+
+
+def linear_bwd(dout, x, w, dw, db, dx, rows, dout_ld=None, dout_off=0, x_ld=None, x_off=0,
+               dx_ld=None, dx_off=0):
+    """dW = dout^T x ; db = sum_rows dout ; dx = dout W  (dx optional)."""
+    O, In = w.shape
+    dout_ld = O if dout_ld is None else dout_ld
+    x_ld = In if x_ld is None else x_ld
+    dx_ld = In if dx_ld is None else dx_ld
+    # dW[o, i] = sum_r dout[r, o] x[r, i]: A = dout^T (M=O, K=rows), B = x (K=rows, N=In)
+    gemm(O, In, rows, dout, 1, dout_ld, x, x_ld, 1, dw, In, a_rowsum=db, a_off=dout_off,
+         b_off=x_off)
+    if dx is not None:
+        gemm(rows, In, O, dout, dout_ld, 1, w, In, 1, dx, dx_ld, a_off=dout_off, c_off=dx_off)
+
+
+def sum_rows(x, rows, cols, out, accumulate=0):
+    call("avd_sum_rows", p(x), rows, cols, p(out), accumulate, stream())
+
+
+def colstats_parts(rows_per_group):
+    return lib.avd_colstats_parts(rows_per_group)
+
+
+def colstats(x, rows, G, C, parts):
+    call("avd_colstats", p(x), rows, G, C, p(parts), stream())
+
+
+def act_fwd(x, out, act, scale, shift, rows, G, C, drop_p, seed):
+    call("avd_act_fwd", p(x), p(out), act, p(scale), p(shift), rows, G, C, drop_p, seed, stream())
+
+
+def act_bwd(x, dout, dx, act, scale, shift, rows, G, C, drop_p, seed):
+    call("avd_act_bwd", p(x), p(dout), p(dx), act, p(scale), p(shift), rows, G, C, drop_p, seed,
+         stream())
+
+
+def bn1d_bwd_reduce(x, dz, mean, invstd, rows, G, C, parts):
+    call("avd_bn1d_bwd_reduce", p(x), p(dz), p(mean), p(invstd), rows, G, C, p(parts), stream())
+
+
+def bn1d_bwd_apply(x, dz, coef, dx, rows, G, C):
+    call("avd_bn1d_bwd_apply", p(x), p(dz), p(coef), p(dx), rows, G, C, stream())
+
+
+# ---------------------------------------------------------------- losses
+def dino_loss(s, t_raw, center, V, T, B, P, tau_s, tau_t, center_m, center_teacher, loss_parts,
+              ds, center_new, work):
+    _need(work.numel() >= (B + T * B) * P, "dino work")
+    call("avd_dino_loss", p(s), p(t_raw), p(center), V, T, B, P, tau_s, tau_t, center_m,
+         int(center_teacher), p(loss_parts), p(ds), p(center_new), p(work), stream())
+
+
+def mse_loss(a, b, B, P, loss_parts, da, db):
+    call("avd_mse_loss", p(a), p(b), B, P, p(loss_parts), p(da), p(db), stream())
+
+
+def l2norm_fwd(x, y, norms, rows, P):
+    call("avd_l2norm_fwd", p(x), p(y), p(norms), rows, P, stream())
+
+
+def l2norm_bwd(y, norms, dy, dx, rows, P):
+    call("avd_l2norm_bwd", p(y), p(norms), p(dy), p(dx), rows, P, stream())
+
+
+def softmax_xent(logits, ld, R, C, targets, target_mode, col_major, mask_diag, gscale, loss_parts,
+                 dlogits, ldd, accumulate):
+    call("avd_softmax_xent", p(logits), ld, R, C, p(targets), target_mode, int(col_major),
+         int(mask_diag), gscale, p(loss_parts), p(dlogits), ldd, int(accumulate), stream())
+
+
+# ---------------------------------------------------------------- optimiser / misc
+def ema(teacher, student, n, m):
+    call("avd_ema", p(teacher), p(student), n, m, stream())
+
+
+def adam(p_, g, m, v, n, lr, b1, b2, eps, wd, bc1, bc2):
+    call("avd_adam", p(p_), p(g), p(m), p(v), n, lr, b1, b2, eps, wd, bc1, bc2, stream())
+
+
+def sum_to(x, n, scale, out):
+    call("avd_sum", p(x), n, scale, p(out), stream())
+
+
+def stage_views(g, G, l, L, orig, B, HW, out):
+    _need(g.numel() == B * G * HW and (l is None or l.numel() == B * L * HW), "stage views")
+    _need(orig is None or orig.numel() == B * HW, "stage orig")
+    _need(out.numel() == (G + L + (orig is not None)) * B * HW, "stage out")
+    call("avd_stage_views", p(g), G, p(l), L, p(orig), B, HW, p(out), dtcode(out), stream())

@@ -1,0 +1,577 @@
+// BatchNorm (train mode, per-(group, channel) statistics), ReLU, maxpool2 / global-average
+// pool, GELU and dropout kernels, forward and backward, plus deterministic reductions.
+//
+// Reference semantics:
+//  * BatchNorm2d/1d train mode, eps 1e-5, momentum 0.1, biased variance for normalisation,
+//    unbiased for running_var (nn.BatchNorm, unimodal.py:114,130; dino.py:1245);
+//  * one BN "group" per encoder call: the reference runs each view separately
+//    (dino.py:680-704), so statistics are per (view, channel);
+//  * F.max_pool2d(2) floor mode with first-max tie-break (ATen CPU scan order);
+//  * nn.GELU() erf form; nn.Dropout inverted scaling.
+//
+// Partial-statistic layout everywhere: channel-major parts [C][G][R][2] so the finaliser
+// reads contiguous rows.  All reductions are fixed-order (f64 in the finalisers).
+#include "common.h"
+
+using namespace avd;
+
+namespace {
+
+// ----------------------------------------------------------------------------- helpers
+template <int NT>
+__device__ __forceinline__ double block_sum_d(double v, double* sh) {
+  v = wave_sum_d(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  double r = 0.0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r += sh[i];
+  return r;
+}
+
+// Sum of rows [r0, r0+R) of a channel-major (sum, sumsq)-pair array, block of 256, f64.
+__device__ __forceinline__ void reduce_pairs(const float* __restrict__ p, long long R, double* sh,
+                                             double& a, double& b) {
+  double s = 0.0, q = 0.0;
+  for (long long r = threadIdx.x; r < R; r += 256) {
+    const float2 v = reinterpret_cast<const float2*>(p)[r];
+    s += v.x;
+    q += v.y;
+  }
+  a = block_sum_d<256>(s, sh);
+  b = block_sum_d<256>(q, sh);
+}
+
+// ----------------------------------------------------------------------------- forward stats
+__global__ __launch_bounds__(256) void bn_finalize_kernel(
+    const float* __restrict__ parts, int G, int R, int C, long long count,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
+    float* mean_o, float* invstd_o, float* scale_o, float* shift_o, float* rm, float* rv) {
+  __shared__ double sh[4];
+  const int c = blockIdx.x;
+  double rmean = rm ? (double)rm[c] : 0.0, rvar = rv ? (double)rv[c] : 0.0;
+  for (int g = 0; g < G; ++g) {
+    double s, q;
+    reduce_pairs(parts + ((size_t)c * G + g) * R * 2, R, sh, s, q);
+    const double n = (double)count;
+    const double mean = s / n;
+    double var = q / n - mean * mean;
+    if (var < 0) var = 0;
+    const double invstd = 1.0 / sqrt(var + (double)eps);
+    if (threadIdx.x == 0) {
+      const double sc = (double)gamma[c] * invstd;
+      mean_o[g * C + c] = (float)mean;
+      invstd_o[g * C + c] = (float)invstd;
+      scale_o[g * C + c] = (float)sc;
+      shift_o[g * C + c] = (float)((double)beta[c] - mean * sc);
+      rmean = (1.0 - momentum) * rmean + momentum * mean;
+      rvar = (1.0 - momentum) * rvar + momentum * var * n / (n - 1.0);
+    }
+  }
+  if (threadIdx.x == 0 && rm) {
+    rm[c] = (float)rmean;
+    rv[c] = (float)rvar;
+  }
+}
+
+// ----------------------------------------------------------------------------- relu + pool
+template <typename TY, typename TO>
+__global__ __launch_bounds__(256) void bn_relu_pool_kernel(
+    const TY* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
+    TO* __restrict__ out, long long total, int B, int C, int H, int W) {
+  const int Hp = H / 2, Wp = W / 2;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int wp = (int)(i % Wp);
+    const int hp = (int)((i / Wp) % Hp);
+    const long long nc = i / ((long long)Hp * Wp);
+    const int c = (int)(nc % C);
+    const int n = (int)(nc / C);
+    const int g = n / B;
+    const float sc = scale[g * C + c], sf = shift[g * C + c];
+    const size_t base = ((size_t)nc * H + 2 * hp) * W + 2 * wp;
+    float m = 0.f;  // relu output >= 0
+    m = fmaxf(m, fmaf(io<TY>::ld(y, base), sc, sf));
+    m = fmaxf(m, fmaf(io<TY>::ld(y, base + 1), sc, sf));
+    m = fmaxf(m, fmaf(io<TY>::ld(y, base + W), sc, sf));
+    m = fmaxf(m, fmaf(io<TY>::ld(y, base + W + 1), sc, sf));
+    io<TO>::st(out, i, m);
+  }
+}
+
+template <typename TY>
+__global__ __launch_bounds__(256) void bn_relu_pool_gap_kernel(
+    const TY* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
+    float* __restrict__ out, long long total, int B, int C, int H, int W) {
+  const int Hp = H / 2, Wp = W / 2;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const int n = (int)(i / C);
+    const int g = n / B;
+    const float sc = scale[g * C + c], sf = shift[g * C + c];
+    float acc = 0.f;
+    for (int hp = 0; hp < Hp; ++hp)
+      for (int wp = 0; wp < Wp; ++wp) {
+        const size_t base = ((size_t)i * H + 2 * hp) * W + 2 * wp;
+        float m = 0.f;
+        m = fmaxf(m, fmaf(io<TY>::ld(y, base), sc, sf));
+        m = fmaxf(m, fmaf(io<TY>::ld(y, base + 1), sc, sf));
+        m = fmaxf(m, fmaf(io<TY>::ld(y, base + W), sc, sf));
+        m = fmaxf(m, fmaf(io<TY>::ld(y, base + W + 1), sc, sf));
+        acc += m;
+      }
+    out[i] = acc / (float)(Hp * Wp);
+  }
+}
+
+// Window helper: z values of the 2x2 window, first-max argmax and the max of relu(z).
+struct Win {
+  float y[4];
+  int arg;
+  float zmax;
+};
+template <typename TY>
+__device__ __forceinline__ Win load_win(const TY* y, size_t base, int W, float sc, float sf) {
+  Win w;
+  w.y[0] = io<TY>::ld(y, base);
+  w.y[1] = io<TY>::ld(y, base + 1);
+  w.y[2] = io<TY>::ld(y, base + W);
+  w.y[3] = io<TY>::ld(y, base + W + 1);
+  // max over relu(z) with first-max tie-break in row-major window order (scan with '>')
+  float best = fmaxf(fmaf(w.y[0], sc, sf), 0.f);
+  int arg = 0;
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    const float r = fmaxf(fmaf(w.y[k], sc, sf), 0.f);
+    if (r > best) { best = r; arg = k; }
+  }
+  w.arg = arg;
+  w.zmax = best;
+  return w;
+}
+
+template <typename TG>
+__device__ __forceinline__ float gout_at(const TG* gout, int pool_mode, long long nc, int q, int HpWp) {
+  if (pool_mode == 0) return io<TG>::ld(gout, (size_t)nc * HpWp + q);
+  return reinterpret_cast<const float*>(gout)[nc] / (float)HpWp;
+}
+
+// ----------------------------------------------------------------------------- backward reduce
+template <typename TY, typename TG>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
+    const TY* __restrict__ y, const TG* __restrict__ gout, int pool_mode,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ parts,
+    int N, int B, int C, int H, int W) {
+  const int Hp = H / 2, Wp = W / 2, HpWp = Hp * Wp;
+  const long long nc = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (nc >= (long long)N * C) return;
+  const int c = (int)(nc % C), n = (int)(nc / C), g = n / B;
+  const float sc = scale[g * C + c], sf = shift[g * C + c];
+  const float mu = mean[g * C + c], is = invstd[g * C + c];
+  float s1 = 0.f, s2 = 0.f;
+  for (int q = lane; q < HpWp; q += 64) {
+    const int hp = q / Wp, wp = q % Wp;
+    const Win w = load_win<TY>(y, ((size_t)nc * H + 2 * hp) * W + 2 * wp, W, sc, sf);
+    if (w.zmax > 0.f) {
+      const float d = gout_at<TG>(gout, pool_mode, nc, q, HpWp);
+      s1 += d;
+      s2 += d * (w.y[w.arg] - mu) * is;
+    }
+  }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (lane == 0) {
+    parts[((size_t)c * N + n) * 2] = s1;
+    parts[((size_t)c * N + n) * 2 + 1] = s2;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
+    const float* __restrict__ parts, int G, int R, int C, long long count,
+    const float* __restrict__ gamma, const float* __restrict__ mean,
+    const float* __restrict__ invstd, float* coef, float* dgamma, float* dbeta, float* dbias,
+    int accumulate) {
+  __shared__ double sh[4];
+  const int c = blockIdx.x;
+  double dg = 0.0, db = 0.0, dbi = 0.0;
+  const double n = (double)count;
+  for (int g = 0; g < G; ++g) {
+    double s1, s2;
+    reduce_pairs(parts + ((size_t)c * G + g) * R * 2, R, sh, s1, s2);
+    if (threadIdx.x == 0) {
+      const double is = invstd[g * C + c], mu = mean[g * C + c], ga = gamma[c];
+      const double k1 = ga * is;
+      const double kx = -ga * is * is * s2 / n;
+      const double k0 = -ga * is * s1 / n + ga * is * is * mu * s2 / n;
+      coef[(g * C + c) * 3 + 0] = (float)k1;
+      coef[(g * C + c) * 3 + 1] = (float)kx;
+      coef[(g * C + c) * 3 + 2] = (float)k0;
+      dg += s2;
+      db += s1;
+      dbi += k1 * s1 + kx * mu * n + k0 * n;  // = sum of dy over the group (analytically 0)
+    }
+  }
+  if (threadIdx.x == 0) {
+    if (dgamma) dgamma[c] = (float)(accumulate ? dgamma[c] + dg : dg);
+    if (dbeta) dbeta[c] = (float)(accumulate ? dbeta[c] + db : db);
+    if (dbias) dbias[c] = (float)(accumulate ? dbias[c] + dbi : dbi);
+  }
+}
+
+template <typename TY, typename TG, typename TD>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const TY* __restrict__ y, const TG* __restrict__ gout, int pool_mode,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ coef, TD* __restrict__ dy, long long total, int B, int C, int H,
+    int W) {
+  const int Hp = H / 2, Wp = W / 2, HpWp = Hp * Wp;
+  const int Hc = (H + 1) / 2, Wc = (W + 1) / 2;  // windows incl. floor-mode leftovers
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int wc = (int)(i % Wc);
+    const int hc = (int)((i / Wc) % Hc);
+    const long long nc = i / ((long long)Hc * Wc);
+    const int c = (int)(nc % C), n = (int)(nc / C), g = n / B;
+    const float sc = scale[g * C + c], sf = shift[g * C + c];
+    const float k1 = coef[(g * C + c) * 3], kx = coef[(g * C + c) * 3 + 1],
+                k0 = coef[(g * C + c) * 3 + 2];
+    const int h0 = 2 * hc, w0 = 2 * wc;
+    const size_t base = ((size_t)nc * H + h0) * W + w0;
+    if (hc < Hp && wc < Wp) {
+      const Win w = load_win<TY>(y, base, W, sc, sf);
+      const float d = w.zmax > 0.f ? gout_at<TG>(gout, pool_mode, nc, hc * Wp + wc, HpWp) : 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float dz = (k == w.arg) ? d : 0.f;
+        const size_t o = base + (k >> 1) * W + (k & 1);
+        io<TD>::st(dy, o, fmaf(k1, dz, fmaf(kx, w.y[k], k0)));
+      }
+    } else {  // incomplete window (odd H/W): no gradient flows through pooling
+      for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b)
+          if (h0 + a < H && w0 + b < W) {
+            const size_t o = base + a * W + b;
+            io<TD>::st(dy, o, fmaf(kx, io<TY>::ld(y, o), k0));
+          }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- BN1d / dense
+constexpr int CS_ROWS = 64;
+
+__global__ __launch_bounds__(256) void colstats_kernel(const float* __restrict__ x, int rpg, int G,
+                                                       int C, int R, float* __restrict__ parts) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int r = blockIdx.y, g = blockIdx.z;
+  if (c >= C) return;
+  const int r0 = r * CS_ROWS, r1 = min(rpg, r0 + CS_ROWS);
+  float s = 0.f, q = 0.f;
+  for (int row = r0; row < r1; ++row) {
+    const float v = x[((size_t)g * rpg + row) * C + c];
+    s += v;
+    q += v * v;
+  }
+  float* p = parts + (((size_t)c * G + g) * R + r) * 2;
+  p[0] = s;
+  p[1] = q;
+}
+
+__global__ __launch_bounds__(256) void bn1d_bwd_reduce_kernel(
+    const float* __restrict__ x, const float* __restrict__ dz, const float* __restrict__ mean,
+    const float* __restrict__ invstd, int rpg, int G, int C, int R, float* __restrict__ parts) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int r = blockIdx.y, g = blockIdx.z;
+  if (c >= C) return;
+  const float mu = mean[g * C + c], is = invstd[g * C + c];
+  const int r0 = r * CS_ROWS, r1 = min(rpg, r0 + CS_ROWS);
+  float s1 = 0.f, s2 = 0.f;
+  for (int row = r0; row < r1; ++row) {
+    const size_t o = ((size_t)g * rpg + row) * C + c;
+    const float d = dz[o];
+    s1 += d;
+    s2 += d * (x[o] - mu) * is;
+  }
+  float* p = parts + (((size_t)c * G + g) * R + r) * 2;
+  p[0] = s1;
+  p[1] = s2;
+}
+
+__global__ __launch_bounds__(256) void bn1d_bwd_apply_kernel(
+    const float* __restrict__ x, const float* __restrict__ dz, const float* __restrict__ coef,
+    float* __restrict__ dx, long long total, int rpg, int C) {
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const int g = (int)(i / C / rpg);
+    const float* k = coef + (g * C + c) * 3;
+    dx[i] = fmaf(k[0], dz[i], fmaf(k[1], x[i], k[2]));
+  }
+}
+
+__device__ __forceinline__ float gelu_f(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_d(float z) {
+  return 0.5f * (1.f + erff(z * 0.70710678118654752f)) + z * 0.39894228040143268f * expf(-0.5f * z * z);
+}
+
+__global__ __launch_bounds__(256) void act_fwd_kernel(
+    const float* __restrict__ x, float* __restrict__ out, int act, const float* __restrict__ scale,
+    const float* __restrict__ shift, long long total, int rpg, int C, float p,
+    unsigned long long seed) {
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    float v = x[i];
+    if (act == 0) {
+      v = fmaxf(v, 0.f);
+    } else {
+      const int c = (int)(i % C);
+      const int g = (int)(i / C / rpg);
+      v = gelu_f(fmaf(v, scale[g * C + c], shift[g * C + c]));
+    }
+    out[i] = v * dropout_scale(seed, (unsigned long long)i, p);
+  }
+}
+
+__global__ __launch_bounds__(256) void act_bwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ dout, float* __restrict__ dx, int act,
+    const float* __restrict__ scale, const float* __restrict__ shift, long long total, int rpg,
+    int C, float p, unsigned long long seed) {
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const float d = dout[i] * dropout_scale(seed, (unsigned long long)i, p);
+    const float v = x[i];
+    if (act == 0) {
+      dx[i] = v > 0.f ? d : 0.f;
+    } else {
+      const int c = (int)(i % C);
+      const int g = (int)(i / C / rpg);
+      dx[i] = d * gelu_d(fmaf(v, scale[g * C + c], shift[g * C + c]));
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- reductions
+// out[col] (+)= sum_rows in[row, col]; 64 columns x 16 row phases per block, fixed order.
+__global__ __launch_bounds__(1024) void sum_rows_kernel(const float* __restrict__ in, int rows,
+                                                        int cols, float* __restrict__ out,
+                                                        int accumulate) {
+  __shared__ double sh[16][64];
+  const int lc = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lc;
+  double s = 0.0;
+  if (col < cols)
+    for (int r = ph; r < rows; r += 16) s += in[(size_t)r * cols + col];
+  sh[ph][lc] = s;
+  __syncthreads();
+  if (ph == 0 && col < cols) {
+    double t = 0.0;
+    for (int k = 0; k < 16; ++k) t += sh[k][lc];
+    out[col] = (float)(accumulate ? out[col] + t : t);
+  }
+}
+
+__global__ __launch_bounds__(1024) void sum_kernel(const float* __restrict__ in, int n, float scale,
+                                                   float* out) {
+  __shared__ double sh[16];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 1024) s += in[i];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int k = 0; k < 16; ++k) t += sh[k];
+    *out = (float)(t * scale);
+  }
+}
+
+inline int grid_for(long long total) {
+  long long b = (total + 255) / 256;
+  if (b > 65536) b = 65536;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int avd_bn_finalize(const float* parts, int G, int R, int C, long long count, const float* gamma,
+                    const float* beta, float eps, float momentum, float* mean, float* invstd,
+                    float* scale, float* shift, float* running_mean, float* running_var,
+                    void* stream) {
+  if (!parts || !gamma || !beta || !mean || !invstd || !scale || !shift) return AVD_ERR_ARG;
+  if (G <= 0 || R <= 0 || C <= 0 || count <= 1) return AVD_ERR_SHAPE;
+  if ((running_mean == nullptr) != (running_var == nullptr)) return AVD_ERR_ARG;
+  bn_finalize_kernel<<<C, 256, 0, avd_stream(stream)>>>(parts, G, R, C, count, gamma, beta, eps,
+                                                         momentum, mean, invstd, scale, shift,
+                                                         running_mean, running_var);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_bn_relu_pool(const void* y, int ydt, const float* scale, const float* shift, void* out,
+                     int odt, int pool_mode, int N, int B, int C, int H, int W, void* stream) {
+  if (!y || !scale || !shift || !out) return AVD_ERR_ARG;
+  if (N <= 0 || B <= 0 || N % B || H < 2 || W < 2) return AVD_ERR_SHAPE;
+  hipStream_t st = avd_stream(stream);
+  if (pool_mode == 0) {
+    const long long total = (long long)N * C * (H / 2) * (W / 2);
+#define AVD_P(TY, TO)                                                                     \
+  bn_relu_pool_kernel<TY, TO><<<grid_for(total), 256, 0, st>>>((const TY*)y, scale, shift, \
+                                                              (TO*)out, total, B, C, H, W);
+    if (ydt == AVD_F32 && odt == AVD_F32) { AVD_P(float, float) }
+    else if (ydt == AVD_F32 && odt == AVD_BF16) { AVD_P(float, bf16) }
+    else if (ydt == AVD_BF16 && odt == AVD_BF16) { AVD_P(bf16, bf16) }
+    else if (ydt == AVD_BF16 && odt == AVD_F32) { AVD_P(bf16, float) }
+    else return AVD_ERR_DTYPE;
+#undef AVD_P
+  } else if (pool_mode == 1) {
+    if (odt != AVD_F32) return AVD_ERR_DTYPE;
+    const long long total = (long long)N * C;
+    if (ydt == AVD_F32)
+      bn_relu_pool_gap_kernel<float><<<grid_for(total), 256, 0, st>>>((const float*)y, scale, shift,
+                                                                      (float*)out, total, B, C, H, W);
+    else if (ydt == AVD_BF16)
+      bn_relu_pool_gap_kernel<bf16><<<grid_for(total), 256, 0, st>>>((const bf16*)y, scale, shift,
+                                                                     (float*)out, total, B, C, H, W);
+    else return AVD_ERR_DTYPE;
+  } else {
+    return AVD_ERR_ARG;
+  }
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_bn_bwd_reduce(const void* y, int ydt, const void* gout, int gdt, int pool_mode,
+                      const float* scale, const float* shift, const float* mean,
+                      const float* invstd, float* parts, int N, int B, int C, int H, int W,
+                      void* stream) {
+  if (!y || !gout || !scale || !shift || !mean || !invstd || !parts) return AVD_ERR_ARG;
+  if (N <= 0 || B <= 0 || N % B || (pool_mode != 0 && pool_mode != 1)) return AVD_ERR_SHAPE;
+  if (pool_mode == 1 && gdt != AVD_F32) return AVD_ERR_DTYPE;
+  hipStream_t st = avd_stream(stream);
+  const int grid = avd_cdiv((long long)N * C, 4);
+#define AVD_R(TY, TG)                                                                         \
+  bn_bwd_reduce_kernel<TY, TG><<<grid, 256, 0, st>>>((const TY*)y, (const TG*)gout, pool_mode, \
+                                                     scale, shift, mean, invstd, parts, N, B,  \
+                                                     C, H, W);
+  if (ydt == AVD_F32 && gdt == AVD_F32) { AVD_R(float, float) }
+  else if (ydt == AVD_BF16 && gdt == AVD_BF16) { AVD_R(bf16, bf16) }
+  else if (ydt == AVD_BF16 && gdt == AVD_F32) { AVD_R(bf16, float) }
+  else if (ydt == AVD_F32 && gdt == AVD_BF16) { AVD_R(float, bf16) }
+  else return AVD_ERR_DTYPE;
+#undef AVD_R
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_bn_bwd_finalize(const float* parts, int G, int R, int C, long long count,
+                        const float* gamma, const float* mean, const float* invstd, float* coef,
+                        float* dgamma, float* dbeta, float* dbias, int accumulate, void* stream) {
+  if (!parts || !gamma || !mean || !invstd || !coef) return AVD_ERR_ARG;
+  if (G <= 0 || R <= 0 || C <= 0 || count <= 0) return AVD_ERR_SHAPE;
+  bn_bwd_finalize_kernel<<<C, 256, 0, avd_stream(stream)>>>(parts, G, R, C, count, gamma, mean,
+                                                             invstd, coef, dgamma, dbeta, dbias,
+                                                             accumulate);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_bn_bwd_apply(const void* y, int ydt, const void* gout, int gdt, int pool_mode,
+                     const float* scale, const float* shift, const float* coef, void* dy, int dt,
+                     int N, int B, int C, int H, int W, void* stream) {
+  if (!y || !gout || !scale || !shift || !coef || !dy) return AVD_ERR_ARG;
+  if (N <= 0 || B <= 0 || N % B || (pool_mode != 0 && pool_mode != 1)) return AVD_ERR_SHAPE;
+  if (pool_mode == 1 && gdt != AVD_F32) return AVD_ERR_DTYPE;
+  hipStream_t st = avd_stream(stream);
+  const long long total = (long long)N * C * ((H + 1) / 2) * ((W + 1) / 2);
+#define AVD_A(TY, TG, TD)                                                                       \
+  bn_bwd_apply_kernel<TY, TG, TD><<<grid_for(total), 256, 0, st>>>(                            \
+      (const TY*)y, (const TG*)gout, pool_mode, scale, shift, coef, (TD*)dy, total, B, C, H, W);
+  if (ydt == AVD_F32 && gdt == AVD_F32 && dt == AVD_F32) { AVD_A(float, float, float) }
+  else if (ydt == AVD_BF16 && gdt == AVD_BF16 && dt == AVD_BF16) { AVD_A(bf16, bf16, bf16) }
+  else if (ydt == AVD_BF16 && gdt == AVD_F32 && dt == AVD_BF16) { AVD_A(bf16, float, bf16) }
+  else if (ydt == AVD_F32 && gdt == AVD_BF16 && dt == AVD_F32) { AVD_A(float, bf16, float) }
+  else return AVD_ERR_DTYPE;
+#undef AVD_A
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_colstats_parts(int rows_per_group) { return avd_cdiv(rows_per_group, CS_ROWS); }
+
+int avd_colstats(const float* x, int rows, int G, int C, float* parts, void* stream) {
+  if (!x || !parts) return AVD_ERR_ARG;
+  if (rows <= 0 || G <= 0 || rows % G || C <= 0) return AVD_ERR_SHAPE;
+  const int rpg = rows / G, R = avd_colstats_parts(rpg);
+  dim3 grid(avd_cdiv(C, 256), R, G);
+  colstats_kernel<<<grid, 256, 0, avd_stream(stream)>>>(x, rpg, G, C, R, parts);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_act_fwd(const float* x, float* out, int act, const float* scale, const float* shift,
+                int rows, int G, int C, float p, unsigned long long seed, void* stream) {
+  if (!x || !out || (act == 1 && (!scale || !shift)) || (act != 0 && act != 1)) return AVD_ERR_ARG;
+  if (rows <= 0 || G <= 0 || rows % G || p < 0.f || p >= 1.f) return AVD_ERR_SHAPE;
+  const long long total = (long long)rows * C;
+  act_fwd_kernel<<<grid_for(total), 256, 0, avd_stream(stream)>>>(x, out, act, scale, shift, total,
+                                                                  rows / G, C, p, seed);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_act_bwd(const float* x, const float* dout, float* dx, int act, const float* scale,
+                const float* shift, int rows, int G, int C, float p, unsigned long long seed,
+                void* stream) {
+  if (!x || !dout || !dx || (act == 1 && (!scale || !shift)) || (act != 0 && act != 1))
+    return AVD_ERR_ARG;
+  if (rows <= 0 || G <= 0 || rows % G || p < 0.f || p >= 1.f) return AVD_ERR_SHAPE;
+  const long long total = (long long)rows * C;
+  act_bwd_kernel<<<grid_for(total), 256, 0, avd_stream(stream)>>>(x, dout, dx, act, scale, shift,
+                                                                  total, rows / G, C, p, seed);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_bn1d_bwd_reduce(const float* x, const float* dz, const float* mean, const float* invstd,
+                        int rows, int G, int C, float* parts, void* stream) {
+  if (!x || !dz || !mean || !invstd || !parts) return AVD_ERR_ARG;
+  if (rows <= 0 || G <= 0 || rows % G) return AVD_ERR_SHAPE;
+  const int rpg = rows / G, R = avd_colstats_parts(rpg);
+  dim3 grid(avd_cdiv(C, 256), R, G);
+  bn1d_bwd_reduce_kernel<<<grid, 256, 0, avd_stream(stream)>>>(x, dz, mean, invstd, rpg, G, C, R,
+                                                               parts);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_bn1d_bwd_apply(const float* x, const float* dz, const float* coef, float* dx, int rows,
+                       int G, int C, void* stream) {
+  if (!x || !dz || !coef || !dx) return AVD_ERR_ARG;
+  if (rows <= 0 || G <= 0 || rows % G) return AVD_ERR_SHAPE;
+  const long long total = (long long)rows * C;
+  bn1d_bwd_apply_kernel<<<grid_for(total), 256, 0, avd_stream(stream)>>>(x, dz, coef, dx, total,
+                                                                         rows / G, C);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_sum_rows(const float* in, int rows, int cols, float* out, int accumulate, void* stream) {
+  if (!in || !out) return AVD_ERR_ARG;
+  if (rows <= 0 || cols <= 0) return AVD_ERR_SHAPE;
+  sum_rows_kernel<<<avd_cdiv(cols, 64), 1024, 0, avd_stream(stream)>>>(in, rows, cols, out,
+                                                                       accumulate);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_sum(const float* in, int n, float scale, float* out, void* stream) {
+  if (!in || !out) return AVD_ERR_ARG;
+  if (n <= 0) return AVD_ERR_SHAPE;
+  sum_kernel<<<1, 1024, 0, avd_stream(stream)>>>(in, n, scale, out);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,94 @@
+// Shared device helpers for libavdino (gfx950 / CDNA4: wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/avdino.h"
+
+namespace avd {
+
+typedef uint16_t bf16;
+
+__device__ __forceinline__ float bf2f(bf16 v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// Round-to-nearest-even f32 -> bf16 (NaN kept NaN).
+__device__ __forceinline__ bf16 f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (bf16)((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16)(u >> 16);
+}
+
+template <typename T> struct io;
+template <> struct io<float> {
+  static __device__ __forceinline__ float ld(const float* p, size_t i) { return p[i]; }
+  static __device__ __forceinline__ void st(float* p, size_t i, float v) { p[i] = v; }
+  static __device__ __forceinline__ float rnd(float v) { return v; }
+};
+template <> struct io<bf16> {
+  static __device__ __forceinline__ float ld(const bf16* p, size_t i) { return bf2f(p[i]); }
+  static __device__ __forceinline__ void st(bf16* p, size_t i, float v) { p[i] = f2bf(v); }
+  static __device__ __forceinline__ float rnd(float v) { return bf2f(f2bf(v)); }
+};
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64).  `sh` needs NT/64 floats.
+// Result valid in every thread.  Deterministic (fixed tree).
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r += sh[i];
+  return r;
+}
+
+// Counter-based hash (murmur3 finaliser on a mixed 64-bit counter): dropout masks that
+// forward and backward regenerate identically from (seed, element index).
+__device__ __forceinline__ uint32_t hash_u32(unsigned long long seed, unsigned long long idx) {
+  unsigned long long x = seed * 0x9E3779B97F4A7C15ull ^ (idx + 0xD1B54A32D192ED03ull);
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+// Keep-scale for inverted dropout: 0 or 1/(1-p).
+__device__ __forceinline__ float dropout_scale(unsigned long long seed, unsigned long long idx, float p) {
+  if (p <= 0.f) return 1.f;
+  float u = (hash_u32(seed, idx) >> 8) * (1.0f / 16777216.0f);
+  return u >= p ? 1.f / (1.f - p) : 0.f;
+}
+
+}  // namespace avd
+
+#define AVD_CHECK_LAUNCH()                                  \
+  do {                                                      \
+    hipError_t e_ = hipGetLastError();                      \
+    if (e_ != hipSuccess) { avd_set_error(e_); return AVD_ERR_HIP; } \
+  } while (0)
+
+void avd_set_error(hipError_t e);
+
+static inline hipStream_t avd_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+static inline int avd_cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }

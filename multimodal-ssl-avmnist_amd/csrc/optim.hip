@@ -1,0 +1,107 @@
+// Flat-arena parameter updates: teacher EMA (MultiModalDINO.update_teacher, dino.py:635-646)
+// and Adam with L2 weight decay (configure_optimizers, dino.py:953-962).  Both stream the
+// arenas once with 16-byte vector accesses (HBM-bound: EMA 12 B/param, Adam 28 B/param).
+#include <string.h>
+
+#include "common.h"
+
+using namespace avd;
+
+static thread_local char g_err[128] = "ok";
+void avd_set_error(hipError_t e) {
+  strncpy(g_err, hipGetErrorString(e), sizeof(g_err) - 1);
+  g_err[sizeof(g_err) - 1] = 0;
+}
+
+namespace {
+
+__global__ __launch_bounds__(256) void ema_kernel(float* __restrict__ t, const float* __restrict__ s,
+                                                  long long n, float m) {
+  const float om = 1.f - m;
+  const long long n4 = n / 4;
+  float4* t4 = reinterpret_cast<float4*>(t);
+  const float4* s4 = reinterpret_cast<const float4*>(s);
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    float4 a = t4[i];
+    const float4 b = s4[i];
+    a.x = m * a.x + om * b.x;
+    a.y = m * a.y + om * b.y;
+    a.z = m * a.z + om * b.z;
+    a.w = m * a.w + om * b.w;
+    t4[i] = a;
+  }
+  for (long long i = n4 * 4 + blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    t[i] = m * t[i] + om * s[i];
+}
+
+__device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, float lr, float b1,
+                                      float b2, float eps, float wd, float inv_bc1,
+                                      float inv_sqrt_bc2) {
+  g = fmaf(wd, p, g);
+  m = b1 * m + (1.f - b1) * g;
+  v = b2 * v + (1.f - b2) * g * g;
+  const float denom = sqrtf(v) * inv_sqrt_bc2 + eps;
+  p -= lr * inv_bc1 * m / denom;
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   long long n, float lr, float b1, float b2,
+                                                   float eps, float wd, float inv_bc1,
+                                                   float inv_sqrt_bc2) {
+  const long long n4 = n / 4;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    const float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    adam1(pp.x, gg.x, mm.x, vv.x, lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2);
+    adam1(pp.y, gg.y, mm.y, vv.y, lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2);
+    adam1(pp.z, gg.z, mm.z, vv.z, lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2);
+    adam1(pp.w, gg.w, mm.w, vv.w, lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2);
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+  }
+  for (long long i = n4 * 4 + blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    adam1(p[i], g[i], m[i], v[i], lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2);
+}
+
+inline int stream_grid(long long n) {
+  long long b = (n / 4 + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int avd_version(void) { return (0 << 16) | 1; }
+
+const char* avd_last_error(void) { return g_err; }
+
+int avd_ema(float* teacher, const float* student, long long n, float m, void* stream) {
+  if (!teacher || !student) return AVD_ERR_ARG;
+  if (n < 0 || !aligned16(teacher) || !aligned16(student)) return AVD_ERR_SHAPE;
+  if (n == 0) return AVD_OK;
+  ema_kernel<<<stream_grid(n), 256, 0, avd_stream(stream)>>>(teacher, student, n, m);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float b1,
+             float b2, float eps, float wd, float bc1, float bc2, void* stream) {
+  if (!p || !g || !m || !v) return AVD_ERR_ARG;
+  if (n < 0 || !aligned16(p) || !aligned16(g) || !aligned16(m) || !aligned16(v)) return AVD_ERR_SHAPE;
+  if (n == 0) return AVD_OK;
+  adam_kernel<<<stream_grid(n), 256, 0, avd_stream(stream)>>>(p, g, m, v, n, lr, b1, b2, eps, wd,
+                                                              1.f / bc1, 1.f / sqrtf(bc2));
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+}  // extern "C"

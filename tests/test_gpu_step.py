@@ -1,0 +1,166 @@
+"""Full training-step parity: the HIP engine (fp32) vs the float64 oracle (which is itself
+pinned to the reference by tests/test_oracle_golden.py), from identical parameters and inputs.
+
+Tolerances (fp32 kernels vs float64 truth; the reference's own fp32 CPU path is ~2e-3 off
+the truth on the first audio conv gradients, tests/test_oracle_golden.py):
+  loss 3e-5 abs; outputs / centre rel-L2 1e-5; gradients rel-L2 1e-3 (mathematically-zero
+  gradients -- biases feeding a BatchNorm -- |g| <= 1e-4); EMA'd teacher 1e-6; running stats
+  1e-5; post-Adam parameters 1e-5 (zero-gradient biases excluded: their Adam step is the sign
+  of rounding noise, in the reference too); free-running loss curve: 3e-5 on step 1, 5e-4
+  over 4 steps (Adam turns rounding noise on near-zero gradients into +-lr steps; the
+  reference's own fp32 run drifts 1.8e-4 from its float64 run by step 4, 3e-4 by step 5).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+from oracle import numpy_oracle as O  # noqa: E402
+from oracle import spec as OS  # noqa: E402
+from oracle.params import make_multimodal_batch, make_state  # noqa: E402
+
+HP = dict(lr=1e-4, wd=1e-6, momentum=0.996, center_momentum=0.9, tau_s=0.1, tau_t=0.04)
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64).ravel()
+    b = np.asarray(b, np.float64).ravel()
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+def host(t):
+    return t.detach().float().cpu().numpy().astype(np.float64)
+
+
+def build(mode, E, D, P, pseed, act=torch.float32):
+    from avdino.engine import Hyper, MultiCentralEngine
+    from avdino.params import ParamStore
+    from avdino.spec import multimodal_dino_sd
+    sd = multimodal_dino_sd(mode, E, D, P)
+    assert list(sd.keys()) == list(OS.multimodal_dino_spec(mode, E, D, P).keys())
+    store = ParamStore(sd, "cuda")
+    state = make_state(OS.multimodal_dino_spec(mode, E, D, P), pseed)
+    store.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state.items()})
+    hp = Hyper(lr=HP["lr"], weight_decay=HP["wd"], momentum=HP["momentum"],
+               center_momentum=HP["center_momentum"], student_temperature=HP["tau_s"],
+               teacher_temperature=HP["tau_t"], dropout=0.0, fusion_dropout=0.0)
+    return store, MultiCentralEngine(store, mode, E, D, P, hp, act_dtype=act), state
+
+
+def dev_batch(b):
+    return {k: torch.from_numpy(v).cuda() for k, v in b.items()}
+
+
+def zero_grad_keys(grads):
+    return {k for k, g in grads.items() if np.linalg.norm(g) < 1e-9}
+
+
+@pytest.mark.parametrize("mode", ["mse", "default", "infonce", "semi_supervised"])
+def test_step_matches_oracle(mode):
+    from avdino.engine import adam_step, ema_step
+    E, D, P, B, G, L = 32, 32, 16, 4, 2, 4
+    store, eng, state = build(mode, E, D, P, 201)
+    batch = make_multimodal_batch(B, G, L, 2001)
+    ref = O.multimodal_step(state, batch, mode, HP)
+
+    loss = eng.forward(dev_batch(batch))
+    s_out, t_out = eng.outputs()
+    assert abs(loss.item() - ref["loss"]) < 3e-5, (loss.item(), ref["loss"])
+    assert rel(host(s_out), ref["s_out"]) < 1e-5
+    assert rel(host(t_out), ref["t_out"]) < 1e-5
+    eng.update_center()
+    assert rel(host(store["center"]), ref["center_after"]) < 1e-5
+    ema_step(store, HP["momentum"])
+    eng.backward()
+    zero = zero_grad_keys(ref["grads"])
+    assert sorted(store.live_keys) == sorted(ref["grads"].keys())
+    errs = {}
+    for k in store.live_keys:
+        g = host(store.grad_of(k))
+        if k in zero:
+            assert np.linalg.norm(g) <= 1e-4, (k, np.linalg.norm(g))
+        else:
+            errs[k] = rel(g, ref["grads"][k])
+    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:5]
+    print("worst grad rel errors:", worst)
+    assert worst[0][1] < 1e-3, worst
+    new = ref["state"]
+    for k in store.t_offs:
+        assert rel(host(store[k]), new[k]) < 1e-6, k
+    for k in store.buffers:
+        if k.endswith("running_mean") or k.endswith("running_var"):
+            assert rel(host(store.buffers[k]), new[k]) < 1e-5, k
+        elif k.endswith("num_batches_tracked"):
+            assert int(store.buffers[k].item()) == int(new[k]), k
+    # Adam on the arena == torch.optim.Adam semantics applied to the same gradients (the
+    # first Adam step is ~lr*sign(g), so comparing against the oracle's own gradients would
+    # only measure sign flips of near-zero gradient entries)
+    ours = {k: host(store.grad_of(k)) for k in store.live_keys}
+    pre = {k: host(store[k]) for k in store.live_keys}
+    adam_step(store, eng.hp)
+    post = O.adam_update_state(pre, ours, {}, 1, HP)
+    for k in store.live_keys:
+        assert rel(host(store[k]), post[k]) < 1e-6, k
+
+
+def test_loss_curve_matches_oracle():
+    E, D, P, B, G, L = 32, 32, 16, 4, 2, 4
+    store, eng, state = build("mse", E, D, P, 202)
+    st = {k: np.asarray(v, np.float64) if v.dtype != np.int64 else v for k, v in state.items()}
+    opt, ref_curve, curve = {}, [], []
+    for step in range(4):
+        b = make_multimodal_batch(B, G, L, 3000 + step)
+        r = O.multimodal_step(st, b, "mse", HP)
+        ref_curve.append(r["loss"])
+        st = O.adam_update_state(r["state"], r["grads"], opt, step + 1, HP)
+        curve.append(eng.step(dev_batch(b)).item())
+    print("curve", curve, "ref", ref_curve)
+    np.testing.assert_allclose(curve[:1], ref_curve[:1], atol=3e-5, rtol=0)
+    np.testing.assert_allclose(curve, ref_curve, atol=5e-4, rtol=0)
+
+
+def test_step_is_deterministic():
+    """Fixed-order reductions everywhere: two runs from the same state are bitwise equal."""
+    outs = []
+    for _ in range(2):
+        store, eng, _ = build("mse", 32, 32, 16, 203)
+        b = dev_batch(make_multimodal_batch(4, 2, 4, 4000))
+        eng.step(b)
+        eng.step(b)
+        outs.append((store.student.clone(), store.teacher.clone(), store.grad.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+def test_full_dims_step_matches_oracle():
+    """Reference dims (E=D=256, P=128) at a small batch."""
+    E, D, P, B, G, L = 256, 256, 128, 2, 2, 4
+    store, eng, state = build("mse", E, D, P, 204)
+    batch = make_multimodal_batch(B, G, L, 5000)
+    ref = O.multimodal_step(state, batch, "mse", HP)
+    loss = eng.forward(dev_batch(batch))
+    assert abs(loss.item() - ref["loss"]) < 3e-5
+    eng.update_center()
+    eng.backward()
+    zero = zero_grad_keys(ref["grads"])
+    errs = sorted(((rel(host(store.grad_of(k)), ref["grads"][k]), k) for k in store.live_keys
+                   if k not in zero), reverse=True)
+    assert errs[0][0] < 1e-3, errs[:5]
+
+
+def test_bf16_step_close_to_oracle():
+    """bf16 activation storage (fp32 accumulate / statistics): statistical tolerance."""
+    E, D, P, B, G, L = 32, 32, 16, 8, 2, 4
+    store, eng, state = build("mse", E, D, P, 205, act=torch.bfloat16)
+    batch = make_multimodal_batch(B, G, L, 6000)
+    ref = O.multimodal_step(state, batch, "mse", HP)
+    loss = eng.forward(dev_batch(batch))
+    assert abs(loss.item() - ref["loss"]) < 2e-2 * abs(ref["loss"])
+    eng.update_center()
+    eng.backward()
+    zero = zero_grad_keys(ref["grads"])
+    errs = sorted(((rel(host(store.grad_of(k)), ref["grads"][k]), k) for k in store.live_keys
+                   if k not in zero), reverse=True)
+    med = np.median([e for e, _ in errs])
+    assert med < 5e-2 and errs[0][0] < 0.5, (med, errs[:6])
