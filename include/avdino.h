@@ -68,7 +68,7 @@ int avd_conv_weight_layout(const float* w, void* wt, int Cout, int Cin, int K, i
 
 /* y = conv2d(x, w) + bias   (nn.Conv2d forward, unimodal.py:113-176)
  * x [N,Cin,H,W] (xdt), bias [Cout] f32 (NULL = 0),
- * wt = avd_conv_weight_layout(w, mode 2) when x and y are bf16 and Cin % 8 == 0 (MFMA
+ * wt = avd_conv_weight_layout(w, mode 2) when x and y are bf16, Cin % 8 == 0, Cin <= 256 (MFMA
  *      implicit GEMM, v_mfma_f32_16x16x32_bf16), else mode 0 (VALU direct conv),
  * y [N,Cout,Ho,Wo] (ydt),
  * Ho = H + 2*pad - K + 1.  If stats != NULL, writes per-(channel, sample, tile) partial
@@ -80,7 +80,8 @@ int avd_conv2d_fwd(const void* x, int xdt, const void* wt, const float* bias, vo
 
 /* dx = conv2d_input_grad(dy, w)   (autograd of nn.Conv2d w.r.t. its input)
  * dy [N,Cout,Ho,Wo] (dt), dx [N,Cin,H,W] (dt),
- * wt_dgrad = avd_conv_weight_layout(w, mode 3) for bf16 (MFMA), mode 1 for f32. */
+ * wt_dgrad = avd_conv_weight_layout(w, mode 3) for bf16 with Cout % 8 == 0, Cout <= 256 (MFMA),
+ * mode 1 otherwise (f32 VALU). */
 int avd_conv2d_dgrad(const void* dy, const void* wt_dgrad, void* dx, int dt,
                      int N, int Cin, int H, int W, int Cout, int K, int pad, void* stream);
 
@@ -137,17 +138,19 @@ int avd_bn_bwd_apply(const void* y, int ydt, const void* gout, int gdt, int pool
 
 /* ------------------------------------------------------------------ dense layers */
 
-/* C[m,n] = alpha * sum_k A[m,k] B[k,n] + bias[n] + beta * C[m,n]   (f32, arbitrary strides)
+/* C[m,n] = alpha * sum_k A[m,k] B[k,n] + bias[n] + beta * C[m,n]   (f32 in HBM, any strides)
  * nn.Linear forward (x W^T + b), input grad (dy W) and weight grad (dy^T x).
- * a_rowsum (nullable) [M] = sum_k A[m,k] from the same launch (the Linear bias gradient when
- * A = dy^T).  Deterministic (no split-K). */
+ * mode 0: f32 VALU FMA; mode 1: f32 MFMA (v_mfma_f32_16x16x4_f32, exact f32 products);
+ * mode 2: bf16 MFMA (operands rounded to bf16, f32 accumulate; the bf16 training mode).
+ * Deterministic (no split-K, no atomics). */
 int avd_gemm(int M, int N, int K, const float* A, long long sam, long long sak,
              const float* B, long long sbk, long long sbn, float* C, long long ldc,
-             const float* bias, float alpha, float beta, float* a_rowsum, void* stream);
+             const float* bias, float alpha, float beta, int mode, void* stream);
 
-/* out[r] (+)= sum_{i<rows} in[i, r]   (fixed order; in [rows, cols] f32) -- reduces partial
- * slabs (conv weight grads) and column sums (Linear bias grads). */
-int avd_sum_rows(const float* in, int rows, int cols, float* out, int accumulate, void* stream);
+/* out[c] (+)= sum_{r<rows} in[r*ld + c]   (fixed order, f64 accumulation) -- reduces the conv
+ * weight-grad partial slabs and gives Linear bias gradients (column sums of dy). */
+int avd_sum_rows(const float* in, int rows, int cols, long long ld, float* out, int accumulate,
+                 void* stream);
 
 /* Column partial statistics of x [rows, C] f32 for BatchNorm1d: parts [C, G, R, 2] with
  * R = avd_colstats_parts(rows/G) row-chunks per group. */

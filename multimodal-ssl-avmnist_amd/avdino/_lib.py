@@ -32,8 +32,8 @@ PROTOS = {
     "avd_bn_bwd_reduce": [P, I, P, I, I, P, P, P, P, P, I, I, I, I, I, P],
     "avd_bn_bwd_finalize": [P, I, I, I, L, P, P, P, P, P, P, P, I, P],
     "avd_bn_bwd_apply": [P, I, P, I, I, P, P, P, P, I, I, I, I, I, I, P],
-    "avd_gemm": [I, I, I, P, L, L, P, L, L, P, L, P, F, F, P, P],
-    "avd_sum_rows": [P, I, I, P, I, P],
+    "avd_gemm": [I, I, I, P, L, L, P, L, L, P, L, P, F, F, I, P],
+    "avd_sum_rows": [P, I, I, L, P, I, P],
     "avd_colstats_parts": [I],
     "avd_colstats": [P, I, I, I, P, P],
     "avd_act_fwd": [P, P, I, P, P, I, I, I, F, U64, P],

@@ -145,16 +145,17 @@ class ConvBranch:
 class ProjHead:
     """ProjectionHead (dino.py:1240-1254): Linear -> BN1d(train) -> GELU -> Dropout -> Linear."""
 
-    def __init__(self, prefix, in_dim, out_dim, hidden=PROJ_HIDDEN):
+    def __init__(self, prefix, in_dim, out_dim, hidden=PROJ_HIDDEN, gemm_mode=ops.GEMM_F32_MFMA):
         self.p = prefix
         self.i, self.o, self.h = in_dim, out_dim, hidden
+        self.gm = gemm_mode
 
     def forward(self, ws, store, tag, x, rows, out, drop_p=0.0, seed=0, x_ld=None, x_off=0,
                 update_running=True):
         p, Hd = self.p, self.h
         h = ws.get(f"{tag}.h", rows * Hd)
         ops.linear_fwd(x, store[p + ".mlp.0.weight"], store[p + ".mlp.0.bias"], h, rows,
-                       x_ld=x_ld, x_off=x_off)
+                       x_ld=x_ld, x_off=x_off, mode=self.gm)
         R = ops.colstats_parts(rows)
         parts = ws.get("stat_parts", Hd * R * 2)
         ops.colstats(h, rows, 1, Hd, parts)
@@ -167,7 +168,7 @@ class ProjHead:
             store.buffers[p + ".mlp.1.num_batches_tracked"] += 1
         a = ws.get(f"{tag}.a", rows * Hd)
         ops.act_fwd(h, a, 1, st[2], st[3], rows, 1, Hd, drop_p, seed)
-        ops.linear_fwd(a, store[p + ".mlp.4.weight"], store[p + ".mlp.4.bias"], out, rows)
+        ops.linear_fwd(a, store[p + ".mlp.4.weight"], store[p + ".mlp.4.bias"], out, rows, mode=self.gm)
         return {"x": x, "x_ld": x_ld if x_ld is not None else self.i, "x_off": x_off, "h": h,
                 "a": a, "st": st, "rows": rows, "drop_p": drop_p, "seed": seed}
 
@@ -175,7 +176,7 @@ class ProjHead:
         p, Hd, rows = self.p, self.h, ctx["rows"]
         da = ws.get("head_da", rows * Hd)
         ops.linear_bwd(dout, ctx["a"], store[p + ".mlp.4.weight"], store.grad_of(p + ".mlp.4.weight"),
-                       store.grad_of(p + ".mlp.4.bias"), da, rows)
+                       store.grad_of(p + ".mlp.4.bias"), da, rows, mode=self.gm)
         st = ctx["st"]
         dz = ws.get("head_dz", rows * Hd)
         ops.act_bwd(ctx["h"], da, dz, 1, st[2], st[3], rows, 1, Hd, ctx["drop_p"], ctx["seed"])
@@ -189,7 +190,7 @@ class ProjHead:
         ops.bn1d_bwd_apply(ctx["h"], dz, coef, dh, rows, 1, Hd)
         ops.linear_bwd(dh, ctx["x"], store[p + ".mlp.0.weight"], store.grad_of(p + ".mlp.0.weight"),
                        store.grad_of(p + ".mlp.0.bias"), dx, rows, x_ld=ctx["x_ld"],
-                       x_off=ctx["x_off"], dx_ld=dx_ld, dx_off=dx_off)
+                       x_off=ctx["x_off"], dx_ld=dx_ld, dx_off=dx_off, mode=self.gm)
 
 
 class Hyper:
@@ -226,18 +227,21 @@ class MultiCentralEngine:
     def __init__(self, store, mode, E, D, P, hp, act_dtype=F32, grad_hook=None, seed=0):
         self.store, self.mode, self.E, self.D, self.P, self.hp = store, mode, E, D, P, hp
         self.act = act_dtype
+        # Linear layers: bf16 MFMA in the bf16 mode (like the reference's fp16 autocast),
+        # exact-f32 MFMA in the fp32 (parity) mode
+        self.gm = ops.GEMM_BF16_MFMA if act_dtype == torch.bfloat16 else ops.GEMM_F32_MFMA
         self.ws = Workspace(store.device)
         self.img = ConvBranch(central_stack("student.image_encoder.0", CENTRAL_IMAGE_CONVS, 28), act_dtype)
         self.aud = ConvBranch(central_stack("student.audio_encoder.0", CENTRAL_AUDIO_CONVS, 112), act_dtype)
         self.t_img = ConvBranch(central_stack("teacher.image_encoder.0", CENTRAL_IMAGE_CONVS, 28), act_dtype)
         self.t_aud = ConvBranch(central_stack("teacher.audio_encoder.0", CENTRAL_AUDIO_CONVS, 112), act_dtype)
-        self.sproj = ProjHead("student_projection", D, P)
-        self.tproj = ProjHead("teacher_projection", D, P)
+        self.sproj = ProjHead("student_projection", D, P, gemm_mode=self.gm)
+        self.tproj = ProjHead("teacher_projection", D, P, gemm_mode=self.gm)
         self.heads = None
         if mode in HEAD_NAMES:
             hi, ha = HEAD_NAMES[mode]
             out = 10 if mode == "semi_supervised" else P
-            self.heads = (ProjHead(hi, E, out), ProjHead(ha, E, out))
+            self.heads = (ProjHead(hi, E, out, gemm_mode=self.gm), ProjHead(ha, E, out, gemm_mode=self.gm))
         self.grad_hook = grad_hook  # e.g. DDP all-reduce of store.grad
         self.seed = seed
         self.step_idx = 0
@@ -251,9 +255,9 @@ class MultiCentralEngine:
         fa, ca = ab.forward(ws, st, tag + ".aud", x_aud, N, G, update_running, need_dgrad)
         cat = ws.get(tag + ".cat", N * 2 * E)
         ops.linear_fwd(fi, st[prefix + ".image_encoder.1.weight"], st[prefix + ".image_encoder.1.bias"],
-                       cat, N, out_ld=2 * E, out_off=0)
+                       cat, N, out_ld=2 * E, out_off=0, mode=self.gm)
         ops.linear_fwd(fa, st[prefix + ".audio_encoder.1.weight"], st[prefix + ".audio_encoder.1.bias"],
-                       cat, N, out_ld=2 * E, out_off=E)
+                       cat, N, out_ld=2 * E, out_off=E, mode=self.gm)
         return cat, (fi, ci, fa, ca)
 
     def _fusion_fwd(self, prefix, cat, rows, tag, seed):
@@ -261,11 +265,12 @@ class MultiCentralEngine:
         ws, st, E, D = self.ws, self.store, self.E, self.D
         h = ws.get(tag + ".fh", rows * E)
         ops.linear_fwd(cat, st[prefix + ".fusion.0.weight"], st[prefix + ".fusion.0.bias"], h, rows,
-                       x_ld=2 * E)
+                       x_ld=2 * E, mode=self.gm)
         r = ws.get(tag + ".fr", rows * E)
         ops.act_fwd(h, r, 0, None, None, rows, 1, E, self.hp.fusion_dropout, seed)
         out = ws.get(tag + ".fout", rows * D)
-        ops.linear_fwd(r, st[prefix + ".fusion.3.weight"], st[prefix + ".fusion.3.bias"], out, rows)
+        ops.linear_fwd(r, st[prefix + ".fusion.3.weight"], st[prefix + ".fusion.3.bias"], out, rows,
+                       mode=self.gm)
         return out, (h, r)
 
     def stage(self, batch, with_orig):
@@ -351,7 +356,7 @@ class MultiCentralEngine:
         ops.sum_to(loss_parts, n_parts, 1.0, loss)
         self.last = dict(B=B, G=G, L=L, V=V, NG=NG, N=N, cat=cat, senc=senc, sfus=sfus, spc=spc,
                          ds=ds, hctx=hctx, center_new=center_new, loss=loss, s_proj=s_proj,
-                         t_proj=t_proj, training=training)
+                         t_proj=t_proj, training=training, head_out=head_out)
         return loss
 
     def _infonce(self, zi, za, B, P, aux, dzi, dza, temperature=0.07):
@@ -362,7 +367,7 @@ class MultiCentralEngine:
         ops.l2norm_fwd(zi, ni, nri, B, P)
         ops.l2norm_fwd(za, na, nra, B, P)
         S = ws.get("nce.S", B * B)
-        ops.gemm(B, B, P, ni, P, 1, na, 1, P, S, B, alpha=1.0 / temperature)
+        ops.gemm(B, B, P, ni, P, 1, na, 1, P, S, B, alpha=1.0 / temperature, mode=self.gm)
         dS = ws.get("nce.dS", B * B)
         parts = ws.get("nce.parts", 2 * B)
         ops.softmax_xent(S, B, B, B, None, 1, False, False, 0.5 / B, parts[:B], dS, B, False)
@@ -370,8 +375,8 @@ class MultiCentralEngine:
         ops.sum_to(parts, 2 * B, 0.5 / B, aux[:1])
         aux[1:].zero_()
         dni, dna = ws.get("nce.dni", B * P), ws.get("nce.dna", B * P)
-        ops.gemm(B, P, B, dS, B, 1, na, P, 1, dni, P, alpha=1.0 / temperature)
-        ops.gemm(B, P, B, dS, 1, B, ni, P, 1, dna, P, alpha=1.0 / temperature)
+        ops.gemm(B, P, B, dS, B, 1, na, P, 1, dni, P, alpha=1.0 / temperature, mode=self.gm)
+        ops.gemm(B, P, B, dS, 1, B, ni, P, 1, dna, P, alpha=1.0 / temperature, mode=self.gm)
         ops.l2norm_bwd(ni, nri, dni, dzi, B, P)
         ops.l2norm_bwd(na, nra, dna, dza, B, P)
 
@@ -398,12 +403,13 @@ class MultiCentralEngine:
         h, r = c["sfus"]
         dr = ws.get("fus_dr", V * B * E)
         ops.linear_bwd(dfout, r, st["student.fusion.3.weight"], st.grad_of("student.fusion.3.weight"),
-                       st.grad_of("student.fusion.3.bias"), dr, V * B)
+                       st.grad_of("student.fusion.3.bias"), dr, V * B, mode=self.gm)
         dh = ws.get("fus_dh", V * B * E)
         ops.act_bwd(h, dr, dh, 0, None, None, V * B, 1, E, self.hp.fusion_dropout,
                     (self.seed * 1000003 + self.step_idx * 16 + 1) & 0xFFFFFFFFFFFF)
         ops.linear_bwd(dh, c["cat"], st["student.fusion.0.weight"], st.grad_of("student.fusion.0.weight"),
-                       st.grad_of("student.fusion.0.bias"), dcat, V * B, x_ld=2 * E)
+                       st.grad_of("student.fusion.0.bias"), dcat, V * B, x_ld=2 * E, dx_ld=2 * E,
+                       mode=self.gm)
         if c["hctx"] is not None:
             ci, ca, dzi, dza = c["hctx"]
             hi, ha = self.heads
@@ -414,12 +420,13 @@ class MultiCentralEngine:
         dfi = ws.get("dfeat_img", N * fi.shape[1])
         ops.linear_bwd(dcat, fi, st["student.image_encoder.1.weight"],
                        st.grad_of("student.image_encoder.1.weight"),
-                       st.grad_of("student.image_encoder.1.bias"), dfi, N, dout_ld=2 * E)
+                       st.grad_of("student.image_encoder.1.bias"), dfi, N, dout_ld=2 * E, mode=self.gm)
         self.img.backward(ws, st, cimg, dfi)
         dfa = ws.get("dfeat_aud", N * fa.shape[1])
         ops.linear_bwd(dcat, fa, st["student.audio_encoder.1.weight"],
                        st.grad_of("student.audio_encoder.1.weight"),
-                       st.grad_of("student.audio_encoder.1.bias"), dfa, N, dout_ld=2 * E, dout_off=E)
+                       st.grad_of("student.audio_encoder.1.bias"), dfa, N, dout_ld=2 * E, dout_off=E,
+                       mode=self.gm)
         self.aud.backward(ws, st, caud, dfa)
 
     def step(self, batch):
@@ -433,6 +440,12 @@ class MultiCentralEngine:
         adam_step(self.store, self.hp)
         self.step_idx += 1
         return loss
+
+    def last_head_outputs(self):
+        """(image head output, audio head output) [B, P or classes] of the last forward."""
+        c = self.last
+        zi, za = c["head_out"]
+        return zi.view(c["B"], -1), za.view(c["B"], -1)
 
     def outputs(self):
         """(s_out [V,B,P], t_out [G,B,P] centred with the pre-update centre) of the last

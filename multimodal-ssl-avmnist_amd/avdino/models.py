@@ -1,0 +1,415 @@
+"""Reference-shaped model API over the HIP training engine.
+
+Class names, constructor arguments, forward() signatures/returns and state-dict keys follow
+the reference (paths relative to its AVMNIST_Experiments/):
+
+  CentralMultiModalEncoder          models/dino.py:454-468   (``--model multi_central``)
+  ProjectionHead                    models/dino.py:1240-1254
+  MultiModalDINO                    models/dino.py:588-727
+  MultiModalDINOWithMSE             models/dino.py:1156-1171
+  MultiModalDINOWithINFONCE         models/dino.py:1053-1068
+  MultiModalDINOSemiSupervised      models/dino.py:964-980
+  MultiModalDINO*Lightning          models/dino.py:730-962, 982-1051, 1070-1154, 1173-1238
+
+Encoder classes are architecture descriptors (the compute is the engine's fused kernels);
+the models own a flat parameter arena (params.ParamStore) whose tensors are exposed under the
+reference's state-dict keys.  The *Lightning wrappers keep the reference's training_step /
+dino_loss / mse_loss / infoNCE_loss / supervised_loss / configure_optimizers surface; the step
+itself runs on the device with no host synchronisation (see engine.py).
+"""
+import math
+
+import torch
+
+from . import ops
+from .engine import Hyper, MultiCentralEngine, adam_step, ema_step
+from .params import ParamStore
+from .spec import HEAD_NAMES, multimodal_dino_sd
+
+_DT = {"bf16": torch.bfloat16, "16-mixed": torch.bfloat16, "bf16-mixed": torch.bfloat16,
+       "32": torch.float32, "fp32": torch.float32, "f32": torch.float32}
+
+
+# ============================================================================ encoders
+class BaseMultiModalEncoder:
+    """models/dino.py:203-211 -- descriptor base."""
+
+    arch = None
+
+    def __init__(self, output_dim=256, encoder_output_dim=512, fusion_dropout=0.3):
+        self.output_dim = output_dim
+        self.encoder_output_dim = encoder_output_dim
+        self.fusion_dropout = fusion_dropout
+
+
+class CentralMultiModalEncoder(BaseMultiModalEncoder):
+    """CentralNet LeNet image (conv5x5 1->32->64) and audio (conv5x5 1->8->16->32->64)
+    branches + Linear(., E) each, concat fusion Linear(2E,E)-ReLU-Dropout(0.3)-Linear(E,D)
+    (models/dino.py:454-468, unimodal.py:105-221, fusion 214-234)."""
+
+    arch = "multi_central"
+
+    def __init__(self, output_dim=256, encoder_output_dim=512):
+        super().__init__(output_dim, encoder_output_dim, fusion_dropout=0.3)
+
+
+class ProjectionHead:
+    """Linear(in, 512) -> BatchNorm1d -> GELU -> Dropout -> Linear(512, out) (dino.py:1240-1254)."""
+
+    def __init__(self, input_dim, projection_dim=256, dropout_rate=0, hidden_dim=512):
+        self.input_dim, self.projection_dim = input_dim, projection_dim
+        self.dropout_rate, self.hidden_dim = dropout_rate, hidden_dim
+
+
+# ============================================================================ DINO models
+def _device(device):
+    if device is not None:
+        return torch.device(device)
+    return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+
+class MultiModalDINO:
+    """Student/teacher multimodal DINO (models/dino.py:588-727) on the HIP engine."""
+
+    mode = "default"
+
+    def __init__(self, encoder_class=CentralMultiModalEncoder, encoder_kwargs=None, output_dim=256,
+                 encoder_output_dim=512, projection_dim=128, momentum=0.996, center_momentum=0.9,
+                 dropout=0.3, device=None, precision="bf16", seed=0):
+        encoder_kwargs = dict(encoder_kwargs or {})
+        encoder_kwargs["output_dim"] = output_dim
+        encoder_kwargs["encoder_output_dim"] = encoder_output_dim
+        enc = encoder_class(**encoder_kwargs)
+        if getattr(enc, "arch", None) != "multi_central":
+            raise NotImplementedError(
+                f"{encoder_class.__name__}: only CentralMultiModalEncoder (multi_central) runs on the "
+                f"MI355X engine in this release (BASELINE hot path)")
+        self.student_spec = enc
+        self.projection_dim, self.output_dim = projection_dim, output_dim
+        self.encoder_output_dim = encoder_output_dim
+        self.momentum, self.center_momentum, self.dropout = momentum, center_momentum, dropout
+        self.device = _device(device)
+        self.store = ParamStore(multimodal_dino_sd(self.mode, encoder_output_dim, output_dim,
+                                                   projection_dim), self.device, seed=seed)
+        self.hp = Hyper(momentum=momentum, center_momentum=center_momentum, dropout=dropout,
+                        fusion_dropout=enc.fusion_dropout)
+        self.engine = None
+        if self.device.type == "cuda":
+            self.engine = MultiCentralEngine(self.store, self.mode, encoder_output_dim, output_dim,
+                                             projection_dim, self.hp, act_dtype=_DT[precision], seed=seed)
+        self.training = True
+
+    # ---------------------------------------------------------------- nn.Module-like surface
+    def train(self, mode=True):
+        self.training = mode
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    def state_dict(self):
+        return self.store.state_dict()
+
+    def load_state_dict(self, sd, strict=True):
+        self.store.load_state_dict(sd, strict)
+
+    def named_parameters(self):
+        for k in self.store.spec:
+            if k in self.store.s_offs or k in self.store.t_offs:
+                yield k, self.store[k]
+
+    def parameters(self):
+        return [v for _, v in self.named_parameters()]
+
+    @property
+    def center(self):
+        return self.store["center"]
+
+    def _need_engine(self):
+        if self.engine is None:
+            raise RuntimeError("the HIP engine needs a ROCm device (no CPU fallback)")
+        return self.engine
+
+    # ---------------------------------------------------------------- reference methods
+    @torch.no_grad()
+    def update_teacher(self):
+        """teacher <- m * teacher + (1-m) * student over ALL student params (dino.py:635-646)."""
+        ema_step(self.store, self.momentum)
+
+    @torch.no_grad()
+    def update_center(self, teacher_output):
+        """center <- 0.9 center + 0.1 mean_rows(teacher_output) (dino.py:648-653)."""
+        c = self.store["center"]
+        c.mul_(self.center_momentum).add_(teacher_output.reshape(-1, c.shape[1]).mean(0, keepdim=True)
+                                          * (1 - self.center_momentum))
+
+    @staticmethod
+    def _views_dict(views):
+        g_img, g_aud, l_img, l_aud = views
+        return {"g_img": g_img, "g_aud": g_aud, "l_img": l_img, "l_aud": l_aud}
+
+    def forward(self, batch):
+        """batch = (global_images, global_audios, local_images, local_audios), each
+        [B, V, 1, H, W] -> (student_outputs [G+L,B,P], teacher_outputs [G,B,P] centred, None).
+        Updates the centre, like the reference."""
+        eng = self._need_engine()
+        eng.forward({k: v.to(self.device) for k, v in self._views_dict(batch).items()}, training=False)
+        s, t = eng.outputs()
+        eng.update_center()
+        return s.clone(), t.clone(), None
+
+    __call__ = forward
+
+
+class _WithHeads(MultiModalDINO):
+    def forward(self, batch):
+        """batch = (image, audio, views) -> (image_out, audio_out, student_out, teacher_out)."""
+        image, audio, views = batch
+        eng = self._need_engine()
+        b = self._views_dict(views)
+        b.update(image=image, audio=audio)
+        if self.mode == "semi_supervised":
+            b["label"] = torch.zeros(image.shape[0], dtype=torch.long)
+        eng.forward({k: v.to(self.device) for k, v in b.items()}, training=False)
+        s, t = eng.outputs()
+        eng.update_center()
+        zi, za = eng.last_head_outputs()
+        return zi.clone(), za.clone(), s.clone(), t.clone()
+
+    __call__ = forward
+
+
+class MultiModalDINOWithMSE(_WithHeads):
+    mode = "mse"
+
+
+class MultiModalDINOWithINFONCE(_WithHeads):
+    mode = "infonce"
+
+
+class MultiModalDINOSemiSupervised(_WithHeads):
+    mode = "semi_supervised"
+
+    def __init__(self, *args, num_classes=10, **kwargs):
+        if num_classes != 10:
+            raise NotImplementedError("AVMNIST has 10 classes")
+        self.num_classes = num_classes
+        super().__init__(*args, **kwargs)
+
+
+# ============================================================================ loss functions
+class _DinoLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, s, t, tau_s, tau_t, center_teacher):
+        V, B, P = s.shape
+        T = t.shape[0]
+        s_ = s.detach().float().contiguous().view(V * B, P)
+        t_ = t.detach().float().contiguous().view(T * B, P)
+        zero = torch.zeros(P, device=s.device)
+        parts = torch.empty(V * B, device=s.device)
+        ds = torch.empty(V * B, P, device=s.device)
+        cn = torch.empty(P, device=s.device)
+        work = torch.empty((B + T * B) * P, device=s.device)
+        ops.dino_loss(s_, t_, zero, V, T, B, P, tau_s, tau_t, 0.9, center_teacher, parts, ds, cn, work)
+        loss = torch.empty(1, device=s.device)
+        ops.sum_to(parts, V * B, 1.0, loss)
+        ctx.save_for_backward(ds.view(V, B, P))
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        (ds,) = ctx.saved_tensors
+        return ds * g, None, None, None, None
+
+
+class _MseLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        B, P = a.shape
+        parts = torch.empty(B, device=a.device)
+        da, db = torch.empty_like(a, dtype=torch.float32), torch.empty_like(b, dtype=torch.float32)
+        ops.mse_loss(a.detach().float().contiguous(), b.detach().float().contiguous(), B, P, parts, da, db)
+        loss = torch.empty(1, device=a.device)
+        ops.sum_to(parts, B, 1.0, loss)
+        ctx.save_for_backward(da, db)
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        da, db = ctx.saved_tensors
+        return da * g, db * g
+
+
+# ============================================================================ Lightning-shaped
+class FlatAdam:
+    """torch.optim.Adam(lr, weight_decay) semantics (L2 added to the gradient) over the flat
+    gradient arena -- one kernel for all live parameters (configure_optimizers, dino.py:953-962)."""
+
+    def __init__(self, store, hp):
+        self.store, self.hp = store, hp
+        self.param_groups = [{"lr": hp.lr, "initial_lr": hp.lr, "weight_decay": hp.wd}]
+
+    def zero_grad(self, set_to_none=False):
+        self.store.grad.zero_()
+
+    def step(self):
+        self.hp.lr = self.param_groups[0]["lr"]
+        adam_step(self.store, self.hp)
+
+
+class CosineAnnealingLR:
+    """torch.optim.lr_scheduler.CosineAnnealingLR(T_max), stepped once per epoch."""
+
+    def __init__(self, optimizer, T_max, eta_min=0.0):
+        self.opt, self.T_max, self.eta_min = optimizer, T_max, eta_min
+        self.base = optimizer.param_groups[0]["initial_lr"]
+        self.last_epoch = 0
+
+    def step(self):
+        self.last_epoch += 1
+        t = self.last_epoch
+        self.opt.param_groups[0]["lr"] = self.eta_min + (self.base - self.eta_min) * (
+            1 + math.cos(math.pi * t / self.T_max)) / 2
+
+    def get_last_lr(self):
+        return [self.opt.param_groups[0]["lr"]]
+
+
+class MultiModalDINOLightning:
+    """Training wrapper (models/dino.py:730-962).  training_step runs forward + losses + EMA on
+    the device; backward_and_step() finishes the step (gradients + all-reduce + Adam), which is
+    what Lightning's automatic optimisation does after training_step."""
+
+    model_class = MultiModalDINO
+
+    def __init__(self, data_dir="data/avmnist", data_augmentation="burst_noise", dino_model=None,
+                 encoder_class=CentralMultiModalEncoder, encoder_kwargs=None, projection_dim=256,
+                 output_dim=256, encoder_output_dim=512, momentum=0.996, center_momentum=0.9,
+                 student_temperature=0.1, teacher_temperature=0.04, learning_rate=0.0001,
+                 use_mixed_precision=True, num_epochs=100, weight_decay=1e-6, dropout=0.3,
+                 alpha=1, device=None, precision=None, seed=0):
+        self.hparams = dict(data_dir=data_dir, data_augmentation=data_augmentation,
+                            encoder_class=encoder_class.__name__, encoder_kwargs=encoder_kwargs,
+                            projection_dim=projection_dim, output_dim=output_dim,
+                            encoder_output_dim=encoder_output_dim, momentum=momentum,
+                            center_momentum=center_momentum, student_temperature=student_temperature,
+                            teacher_temperature=teacher_temperature, learning_rate=learning_rate,
+                            use_mixed_precision=use_mixed_precision, num_epochs=num_epochs,
+                            weight_decay=weight_decay, dropout=dropout, alpha=alpha)
+        self.encoder_class, self.encoder_kwargs = encoder_class, encoder_kwargs
+        self.learning_rate, self.num_epochs = learning_rate, num_epochs
+        self.student_temperature, self.teacher_temperature = student_temperature, teacher_temperature
+        self.weight_decay, self.alpha = weight_decay, alpha
+        self.precision = precision or ("bf16" if use_mixed_precision else "32")
+        if dino_model is None:
+            dino_model = self.model_class(encoder_class=encoder_class, encoder_kwargs=encoder_kwargs,
+                                          output_dim=output_dim, encoder_output_dim=encoder_output_dim,
+                                          projection_dim=projection_dim, momentum=momentum,
+                                          center_momentum=center_momentum, dropout=dropout,
+                                          device=device, precision=self.precision, seed=seed)
+        self.model = dino_model
+        hp = self.model.hp
+        hp.tau_s, hp.tau_t = student_temperature, teacher_temperature
+        hp.lr, hp.wd, hp.alpha = learning_rate, weight_decay, float(alpha)
+        self.logged = {}
+        self._optim = None
+
+    # ---------------------------------------------------------------- losses (reference API)
+    def dino_loss(self, student_outputs, teacher_outputs, alignment_loss=None):
+        """dino.py:822-854 -- fused HIP kernel; differentiable w.r.t. student_outputs."""
+        return _DinoLossFn.apply(student_outputs, teacher_outputs, self.student_temperature,
+                                 self.teacher_temperature, False)
+
+    def mse_loss(self, image_outputs, audio_outputs):
+        """dino.py:1193-1211."""
+        return _MseLossFn.apply(image_outputs, audio_outputs)
+
+    # ---------------------------------------------------------------- step
+    def _batch_dict(self, batch):
+        if self.model.mode == "default":
+            return self.model._views_dict(batch)
+        image, audio, labels, views = batch
+        d = self.model._views_dict(views)
+        d.update(image=image, audio=audio, label=labels)
+        return d
+
+    def log(self, name, value, **kw):
+        self.logged[name] = value
+
+    def training_step(self, batch, batch_idx):
+        """Forward + losses (+ centre update) + teacher EMA (before backward, as dino.py:871).
+        Returns the loss as a device tensor."""
+        eng = self.model._need_engine()
+        b = {k: v.to(self.model.device, non_blocking=True) for k, v in self._batch_dict(batch).items()}
+        loss = eng.forward(b, training=True)
+        eng.update_center()
+        self.model.update_teacher()
+        self.log("train_loss", loss)
+        return loss
+
+    def backward_and_step(self, optimizer=None):
+        eng = self.model._need_engine()
+        eng.backward()
+        if eng.grad_hook is not None:
+            eng.grad_hook(self.model.store.grad)
+        (optimizer or self.configure_optimizers()["optimizer"]).step()
+        eng.step_idx += 1
+
+    def configure_optimizers(self):
+        """Adam(lr, weight_decay) + CosineAnnealingLR(T_max=num_epochs) (dino.py:953-962)."""
+        if self._optim is None:
+            opt = FlatAdam(self.model.store, self.model.hp)
+            self._optim = {"optimizer": opt,
+                           "lr_scheduler": {"scheduler": CosineAnnealingLR(opt, T_max=self.num_epochs)}}
+        return self._optim
+
+    def forward(self, batch):
+        return self.model(batch)
+
+    def state_dict(self):
+        return {"model." + k: v for k, v in self.model.state_dict().items()}
+
+    def load_state_dict(self, sd, strict=True):
+        self.model.load_state_dict({k[len("model."):]: v for k, v in sd.items() if k.startswith("model.")},
+                                   strict)
+
+    def parameters(self):
+        return self.model.parameters()
+
+
+class MultiModalDINOWithMSELightning(MultiModalDINOLightning):
+    """dino.py:1173-1238 (reference ctor defaults encoder_output_dim=128)."""
+
+    model_class = MultiModalDINOWithMSE
+
+    def __init__(self, *args, output_dim=256, encoder_output_dim=128,
+                 encoder_class=CentralMultiModalEncoder, alpha=1, **kwargs):
+        super().__init__(*args, output_dim=output_dim, encoder_output_dim=encoder_output_dim,
+                         encoder_class=encoder_class, alpha=alpha, **kwargs)
+
+
+class MultiModalDINOWithINFONCELightning(MultiModalDINOLightning):
+    """dino.py:1070-1154."""
+
+    model_class = MultiModalDINOWithINFONCE
+
+    def __init__(self, *args, output_dim=256, encoder_output_dim=128,
+                 encoder_class=CentralMultiModalEncoder, alpha=1, **kwargs):
+        super().__init__(*args, output_dim=output_dim, encoder_output_dim=encoder_output_dim,
+                         encoder_class=encoder_class, alpha=alpha, **kwargs)
+
+
+class MultiModalDINOSemiSupervisedLightning(MultiModalDINOLightning):
+    """dino.py:982-1051."""
+
+    model_class = MultiModalDINOSemiSupervised
+
+
+MULTIMODAL_WRAPPERS = {
+    "default": MultiModalDINOLightning,
+    "semi_supervised": MultiModalDINOSemiSupervisedLightning,
+    "mse": MultiModalDINOWithMSELightning,
+    "infonce": MultiModalDINOWithINFONCELightning,
+}
+
+MODEL_MAP = {"multi_central": CentralMultiModalEncoder}

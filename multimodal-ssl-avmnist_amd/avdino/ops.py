@@ -98,7 +98,7 @@ def conv_weight_layout(w, wt, mode):
 
 def mfma_conv(x_dtype, cin):
     """True when avd_conv2d_fwd / _dgrad take the MFMA path (and want layouts 2 / 3)."""
-    return x_dtype == torch.bfloat16 and cin % 8 == 0 and cin <= 128
+    return x_dtype == torch.bfloat16 and cin % 8 == 0 and cin <= 256
 
 
 def conv2d_fwd(x, wt, bias, y, stats, N, Cin, H, W, Cout, K, pad):
@@ -178,8 +178,11 @@ def bn_bwd_apply(y, gout, pool_mode, scale, shift, coef, dy, N, B, C, H, W):
 
 
 # ---------------------------------------------------------------- dense
+GEMM_F32_VALU, GEMM_F32_MFMA, GEMM_BF16_MFMA = 0, 1, 2
+
+
 def gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, bias=None, alpha=1.0, beta=0.0,
-         a_rowsum=None, a_off=0, b_off=0, c_off=0):
+         a_off=0, b_off=0, c_off=0, mode=GEMM_F32_MFMA):
     """C[m,n] = alpha*sum_k A[m,k]B[k,n] (+bias[n]) (+beta*C).  *_off are element offsets into
     the (flat, f32) storage of A/B/C so row/column slices need no copies."""
     for t in (A, B, C):
@@ -189,37 +192,41 @@ def gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, bias=None, alpha=1.0, beta=0
     _need(b_off >= 0 and b_off + (K - 1) * sbk + (N - 1) * sbn < B.numel(), "gemm B bounds")
     _need(c_off >= 0 and c_off + (M - 1) * ldc + (N - 1) < C.numel(), "gemm C bounds")
     _need(bias is None or bias.numel() >= N, "gemm bias")
-    _need(a_rowsum is None or a_rowsum.numel() >= M, "gemm rowsum")
-    _timed(f"gemm[{M}x{N}x{K}]", 4 * (M * K + K * N + M * N), 2 * M * N * K,
+    _timed(f"gemm[{M}x{N}x{K} m{mode}]", 4 * (M * K + K * N + M * N), 2 * M * N * K,
            lambda: call("avd_gemm", M, N, K, A.data_ptr() + 4 * a_off, sam, sak,
                         B.data_ptr() + 4 * b_off, sbk, sbn, C.data_ptr() + 4 * c_off, ldc, p(bias),
-                        alpha, beta, p(a_rowsum), stream()))
+                        alpha, beta, mode, stream()))
 
 
-def linear_fwd(x, w, b, out, rows, x_ld=None, x_off=0, out_ld=None, out_off=0):
+def linear_fwd(x, w, b, out, rows, x_ld=None, x_off=0, out_ld=None, out_off=0, mode=GEMM_F32_MFMA):
     """out[rows, O] = x[rows, I] W^T + b   (W [O, I])."""
     O, In = w.shape
     x_ld = In if x_ld is None else x_ld
     out_ld = O if out_ld is None else out_ld
-    gemm(rows, O, In, x, x_ld, 1, w, 1, In, out, out_ld, bias=b, a_off=x_off, c_off=out_off)
+    gemm(rows, O, In, x, x_ld, 1, w, 1, In, out, out_ld, bias=b, a_off=x_off, c_off=out_off,
+         mode=mode)
 
 
 def linear_bwd(dout, x, w, dw, db, dx, rows, dout_ld=None, dout_off=0, x_ld=None, x_off=0,
-               dx_ld=None, dx_off=0):
+               dx_ld=None, dx_off=0, mode=GEMM_F32_MFMA):
     """dW = dout^T x ; db = sum_rows dout ; dx = dout W  (dx optional)."""
     O, In = w.shape
     dout_ld = O if dout_ld is None else dout_ld
     x_ld = In if x_ld is None else x_ld
     dx_ld = In if dx_ld is None else dx_ld
     # dW[o, i] = sum_r dout[r, o] x[r, i]: A = dout^T (M=O, K=rows), B = x (K=rows, N=In)
-    gemm(O, In, rows, dout, 1, dout_ld, x, x_ld, 1, dw, In, a_rowsum=db, a_off=dout_off,
-         b_off=x_off)
+    gemm(O, In, rows, dout, 1, dout_ld, x, x_ld, 1, dw, In, a_off=dout_off, b_off=x_off, mode=mode)
+    if db is not None:
+        sum_rows(dout, rows, O, db, ld=dout_ld, off=dout_off)
     if dx is not None:
-        gemm(rows, In, O, dout, dout_ld, 1, w, In, 1, dx, dx_ld, a_off=dout_off, c_off=dx_off)
+        gemm(rows, In, O, dout, dout_ld, 1, w, In, 1, dx, dx_ld, a_off=dout_off, c_off=dx_off,
+             mode=mode)
 
 
-def sum_rows(x, rows, cols, out, accumulate=0):
-    call("avd_sum_rows", p(x), rows, cols, p(out), accumulate, stream())
+def sum_rows(x, rows, cols, out, accumulate=0, ld=None, off=0):
+    ld = cols if ld is None else ld
+    _need(off + (rows - 1) * ld + cols <= x.numel() and out.numel() >= cols, "sum_rows bounds")
+    call("avd_sum_rows", x.data_ptr() + 4 * off, rows, cols, ld, p(out), accumulate, stream())
 
 
 def colstats_parts(rows_per_group):

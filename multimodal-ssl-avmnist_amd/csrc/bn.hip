@@ -352,14 +352,14 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(
 // ----------------------------------------------------------------------------- reductions
 // out[col] (+)= sum_rows in[row, col]; 64 columns x 16 row phases per block, fixed order.
 __global__ __launch_bounds__(1024) void sum_rows_kernel(const float* __restrict__ in, int rows,
-                                                        int cols, float* __restrict__ out,
-                                                        int accumulate) {
+                                                        int cols, long long ld,
+                                                        float* __restrict__ out, int accumulate) {
   __shared__ double sh[16][64];
   const int lc = threadIdx.x & 63, ph = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + lc;
   double s = 0.0;
   if (col < cols)
-    for (int r = ph; r < rows; r += 16) s += in[(size_t)r * cols + col];
+    for (int r = ph; r < rows; r += 16) s += in[(size_t)r * ld + col];
   sh[ph][lc] = s;
   __syncthreads();
   if (ph == 0 && col < cols) {
@@ -557,10 +557,11 @@ int avd_bn1d_bwd_apply(const float* x, const float* dz, const float* coef, float
   return AVD_OK;
 }
 
-int avd_sum_rows(const float* in, int rows, int cols, float* out, int accumulate, void* stream) {
+int avd_sum_rows(const float* in, int rows, int cols, long long ld, float* out, int accumulate,
+                 void* stream) {
   if (!in || !out) return AVD_ERR_ARG;
-  if (rows <= 0 || cols <= 0) return AVD_ERR_SHAPE;
-  sum_rows_kernel<<<avd_cdiv(cols, 64), 1024, 0, avd_stream(stream)>>>(in, rows, cols, out,
+  if (rows <= 0 || cols <= 0 || ld < cols) return AVD_ERR_SHAPE;
+  sum_rows_kernel<<<avd_cdiv(cols, 64), 1024, 0, avd_stream(stream)>>>(in, rows, cols, ld, out,
                                                                        accumulate);
   AVD_CHECK_LAUNCH();
   return AVD_OK;

@@ -280,7 +280,7 @@ int avd_mfma_layout_size(int Cout, int Cin, int K, int mode);
 
 // MFMA path for bf16 activations when the conv's input channels are a multiple of 8
 static bool use_mfma(int dt_in, int dt_out, int cin) {
-  return dt_in == AVD_BF16 && dt_out == AVD_BF16 && cin % 8 == 0 && cin <= 128;
+  return dt_in == AVD_BF16 && dt_out == AVD_BF16 && cin % 8 == 0 && cin <= 256;
 }
 
 extern "C" {

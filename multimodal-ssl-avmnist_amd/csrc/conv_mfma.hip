@@ -487,7 +487,7 @@ int avd_weight_layout_mfma(const float* w, void* wk, int Cout, int Cin, int K, i
   return AVD_OK;
 }
 
-// Forward (STATS as requested) / input-grad convolution on MFMA; Cin % 8 == 0, Cin <= 128.
+// Forward (STATS as requested) / input-grad convolution on MFMA; Cin % 8 == 0, Cin <= 256.
 int avd_conv_mfma_bf16(const void* x, const void* wk, const float* bias, void* y, float* stats,
                        int N, int Cin, int H, int W, int Cout, int K, int pad, hipStream_t st) {
   const int NT = Cout <= 16 ? 1 : Cout <= 32 ? 2 : 4;
@@ -502,7 +502,7 @@ int avd_conv_mfma_bf16(const void* x, const void* wk, const float* bias, void* y
                                                          pad, st);
 #define AVD_FN(KK, CI) AVD_F(KK, CI, 1) AVD_F(KK, CI, 2) AVD_F(KK, CI, 4)
   AVD_FN(5, 8) AVD_FN(5, 16) AVD_FN(5, 32) AVD_FN(5, 64)
-  AVD_FN(3, 8) AVD_FN(3, 16) AVD_FN(3, 32) AVD_FN(3, 64) AVD_FN(3, 128)
+  AVD_FN(3, 8) AVD_FN(3, 16) AVD_FN(3, 32) AVD_FN(3, 64) AVD_FN(3, 128) AVD_FN(3, 256)
 #undef AVD_FN
 #undef AVD_F
   return AVD_ERR_SHAPE;

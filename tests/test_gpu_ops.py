@@ -188,23 +188,31 @@ def test_bn_relu_pool_block_fwd_bwd(ops, H, gap):
     assert np.abs(host(dbias)).max() < 1e-4  # sum of dy through BN is analytically zero
 
 
-def test_gemm_strides_and_rowsum(ops):
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("shape", [(70, 130, 45), (256, 3136, 300), (130, 64, 1000)])
+def test_gemm_modes_and_strides(ops, mode, shape):
+    """f32 VALU (0), f32 MFMA (1), bf16 MFMA (2; operands rounded to bf16 on both sides)."""
     g = np.random.default_rng(1)
-    M, N, K = 70, 130, 45
+    M, N, K = shape
     A = g.normal(size=(M, K)).astype(np.float32)
     Bm = g.normal(size=(K, N)).astype(np.float32)
+    if mode == 2:
+        A, Bm = _bf16_round(A), _bf16_round(Bm)
     bias = g.normal(size=N).astype(np.float32)
+    tol = 1e-6 if mode < 2 else 1e-5
     ref = A.astype(np.float64) @ Bm + bias
     C = torch.empty(M, N, device="cuda")
-    ops.gemm(M, N, K, dev(A), K, 1, dev(Bm), N, 1, C, N, bias=dev(bias))
-    assert rel(host(C), ref) < 1e-6
-    # A^T and B^T storage, alpha/beta, row sums of A
+    ops.gemm(M, N, K, dev(A), K, 1, dev(Bm), N, 1, C, N, bias=dev(bias), mode=mode)
+    assert rel(host(C), ref) < tol
+    # A^T and B^T storage (scalar / transposed staging paths), alpha / beta
     At, Bt = dev(A.T.copy()), dev(Bm.T.copy())
     C2 = dev(np.ones((M, N), np.float32))
-    rs = torch.empty(M, device="cuda")
-    ops.gemm(M, N, K, At, 1, M, Bt, 1, K, C2, N, alpha=0.5, beta=2.0, a_rowsum=rs)
-    assert rel(host(C2), 0.5 * (A.astype(np.float64) @ Bm) + 2.0) < 1e-6
-    assert rel(host(rs), A.sum(1)) < 1e-6
+    ops.gemm(M, N, K, At, 1, M, Bt, 1, K, C2, N, alpha=0.5, beta=2.0, mode=mode)
+    assert rel(host(C2), 0.5 * (A.astype(np.float64) @ Bm) + 2.0) < tol
+    # column sums with a leading dimension and offset (Linear bias gradient)
+    cs = torch.empty(N - 3, device="cuda")
+    ops.sum_rows(dev(Bm), K, N - 3, cs, ld=N, off=3)
+    assert rel(host(cs), Bm[:, 3:].sum(0)) < 1e-6
 
 
 def test_linear_fwd_bwd_with_offsets(ops):
