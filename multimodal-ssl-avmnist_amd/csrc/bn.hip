@@ -259,6 +259,144 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   }
 }
 
+// ----------------------------------------------------------------------------- bf16 x4 paths
+// bf16 maps whose row width is a multiple of 8: one thread handles 4 consecutive pooling
+// windows of an output row -> two 16-byte loads of y (the two input rows), 8-byte gradient
+// loads/stores.  (f32 maps and other widths take the scalar kernels above.)
+typedef __attribute__((ext_vector_type(4))) unsigned u4v;
+typedef __attribute__((ext_vector_type(2))) unsigned u2v;
+
+__device__ __forceinline__ void unpack8(u4v v, float (&f)[8]) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+__device__ __forceinline__ unsigned pack2(float a, float b) {
+  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+}
+
+// per window k = 0..3 of the quad: first-max argmax over relu(z) and the max
+__device__ __forceinline__ void quad_windows(const float (&r0)[8], const float (&r1)[8], float sc,
+                                             float sf, int (&arg)[4], float (&mx)[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float v[4] = {r0[2 * k], r0[2 * k + 1], r1[2 * k], r1[2 * k + 1]};
+    float best = fmaxf(fmaf(v[0], sc, sf), 0.f);
+    int a = 0;
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      const float r = fmaxf(fmaf(v[j], sc, sf), 0.f);
+      if (r > best) { best = r; a = j; }
+    }
+    arg[k] = a;
+    mx[k] = best;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_relu_pool_q4_kernel(
+    const bf16* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
+    bf16* __restrict__ out, long long total4, int B, int C, int H, int W) {
+  const int Hp = H / 2, Wp = W / 2, Q = Wp / 4;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total4; i += (long long)gridDim.x * 256) {
+    const int q = (int)(i % Q);
+    const int hp = (int)((i / Q) % Hp);
+    const long long nc = i / ((long long)Q * Hp);
+    const int c = (int)(nc % C), g = (int)(nc / C) / B;
+    const float sc = scale[g * C + c], sf = shift[g * C + c];
+    const size_t base = ((size_t)nc * H + 2 * hp) * W + 8 * q;
+    float r0[8], r1[8];
+    unpack8(*reinterpret_cast<const u4v*>(y + base), r0);
+    unpack8(*reinterpret_cast<const u4v*>(y + base + W), r1);
+    int arg[4];
+    float mx[4];
+    quad_windows(r0, r1, sc, sf, arg, mx);
+    *reinterpret_cast<u2v*>(out + ((size_t)nc * Hp + hp) * Wp + 4 * q) =
+        u2v{pack2(mx[0], mx[1]), pack2(mx[2], mx[3])};
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_reduce_q4_kernel(
+    const bf16* __restrict__ y, const bf16* __restrict__ gout, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ mean,
+    const float* __restrict__ invstd, float* __restrict__ parts, int N, int B, int C, int H, int W) {
+  const int Hp = H / 2, Wp = W / 2, Q = Wp / 4, HQ = Hp * Q;
+  const long long nc = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (nc >= (long long)N * C) return;
+  const int c = (int)(nc % C), n = (int)(nc / C), g = n / B;
+  const float sc = scale[g * C + c], sf = shift[g * C + c];
+  const float mu = mean[g * C + c], is = invstd[g * C + c];
+  float s1 = 0.f, s2 = 0.f;
+  for (int t = lane; t < HQ; t += 64) {
+    const int hp = t / Q, q = t - (t / Q) * Q;
+    const size_t base = ((size_t)nc * H + 2 * hp) * W + 8 * q;
+    float r0[8], r1[8];
+    unpack8(*reinterpret_cast<const u4v*>(y + base), r0);
+    unpack8(*reinterpret_cast<const u4v*>(y + base + W), r1);
+    const u2v gv = *reinterpret_cast<const u2v*>(gout + ((size_t)nc * Hp + hp) * Wp + 4 * q);
+    const float gg[4] = {__uint_as_float(gv.x << 16), __uint_as_float(gv.x & 0xffff0000u),
+                         __uint_as_float(gv.y << 16), __uint_as_float(gv.y & 0xffff0000u)};
+    int arg[4];
+    float mx[4];
+    quad_windows(r0, r1, sc, sf, arg, mx);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (mx[k] > 0.f) {
+        const int a = arg[k];
+        const float ya = (a < 2) ? r0[2 * k + a] : r1[2 * k + a - 2];
+        s1 += gg[k];
+        s2 += gg[k] * (ya - mu) * is;
+      }
+    }
+  }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (lane == 0) {
+    parts[((size_t)c * N + n) * 2] = s1;
+    parts[((size_t)c * N + n) * 2 + 1] = s2;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_q4_kernel(
+    const bf16* __restrict__ y, const bf16* __restrict__ gout, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ coef, bf16* __restrict__ dy,
+    long long total4, int B, int C, int H, int W) {
+  const int Hp = H / 2, Wp = W / 2, Q = Wp / 4;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total4; i += (long long)gridDim.x * 256) {
+    const int q = (int)(i % Q);
+    const int hp = (int)((i / Q) % Hp);
+    const long long nc = i / ((long long)Q * Hp);
+    const int c = (int)(nc % C), g = (int)(nc / C) / B;
+    const float sc = scale[g * C + c], sf = shift[g * C + c];
+    const float k1 = coef[(g * C + c) * 3], kx = coef[(g * C + c) * 3 + 1],
+                k0 = coef[(g * C + c) * 3 + 2];
+    const size_t base = ((size_t)nc * H + 2 * hp) * W + 8 * q;
+    float r0[8], r1[8];
+    unpack8(*reinterpret_cast<const u4v*>(y + base), r0);
+    unpack8(*reinterpret_cast<const u4v*>(y + base + W), r1);
+    const u2v gv = *reinterpret_cast<const u2v*>(gout + ((size_t)nc * Hp + hp) * Wp + 4 * q);
+    const float gg[4] = {__uint_as_float(gv.x << 16), __uint_as_float(gv.x & 0xffff0000u),
+                         __uint_as_float(gv.y << 16), __uint_as_float(gv.y & 0xffff0000u)};
+    int arg[4];
+    float mx[4];
+    quad_windows(r0, r1, sc, sf, arg, mx);
+    float d0[8], d1[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float d = mx[k] > 0.f ? gg[k] : 0.f;
+      d0[2 * k] = fmaf(k1, arg[k] == 0 ? d : 0.f, fmaf(kx, r0[2 * k], k0));
+      d0[2 * k + 1] = fmaf(k1, arg[k] == 1 ? d : 0.f, fmaf(kx, r0[2 * k + 1], k0));
+      d1[2 * k] = fmaf(k1, arg[k] == 2 ? d : 0.f, fmaf(kx, r1[2 * k], k0));
+      d1[2 * k + 1] = fmaf(k1, arg[k] == 3 ? d : 0.f, fmaf(kx, r1[2 * k + 1], k0));
+    }
+    *reinterpret_cast<u4v*>(dy + base) =
+        u4v{pack2(d0[0], d0[1]), pack2(d0[2], d0[3]), pack2(d0[4], d0[5]), pack2(d0[6], d0[7])};
+    *reinterpret_cast<u4v*>(dy + base + W) =
+        u4v{pack2(d1[0], d1[1]), pack2(d1[2], d1[3]), pack2(d1[4], d1[5]), pack2(d1[6], d1[7])};
+  }
+}
+
 // ----------------------------------------------------------------------------- BN1d / dense
 constexpr int CS_ROWS = 64;
 
@@ -350,21 +488,32 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(
 }
 
 // ----------------------------------------------------------------------------- reductions
-// out[col] (+)= sum_rows in[row, col]; 64 columns x 16 row phases per block, fixed order.
+// out[col] (+)= sum_rows in[row, col]; CW columns x (1024/CW) row phases per block, fixed order.
+// Narrow matrices (Linear bias gradients: 256 columns x thousands of rows) use CW = 16 so 64
+// phases share the rows; wide ones (conv weight-grad slabs) CW = 64.
+template <int CW>
 __global__ __launch_bounds__(1024) void sum_rows_kernel(const float* __restrict__ in, int rows,
                                                         int cols, long long ld,
                                                         float* __restrict__ out, int accumulate) {
-  __shared__ double sh[16][64];
-  const int lc = threadIdx.x & 63, ph = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + lc;
+  constexpr int PH = 1024 / CW;
+  __shared__ double sh[PH][CW];
+  const int lc = threadIdx.x % CW, ph = threadIdx.x / CW;
+  const int col = blockIdx.x * CW + lc;
   double s = 0.0;
-  if (col < cols)
-    for (int r = ph; r < rows; r += 16) s += in[(size_t)r * ld + col];
+  if (col < cols) {
+    int r = ph;
+    for (; r + 3 * PH < rows; r += 4 * PH) {
+      const float a = in[(size_t)r * ld + col], b = in[(size_t)(r + PH) * ld + col];
+      const float c = in[(size_t)(r + 2 * PH) * ld + col], d = in[(size_t)(r + 3 * PH) * ld + col];
+      s += (double)a + (double)b + (double)c + (double)d;
+    }
+    for (; r < rows; r += PH) s += in[(size_t)r * ld + col];
+  }
   sh[ph][lc] = s;
   __syncthreads();
   if (ph == 0 && col < cols) {
     double t = 0.0;
-    for (int k = 0; k < 16; ++k) t += sh[k][lc];
+    for (int k = 0; k < PH; ++k) t += sh[k][lc];
     out[col] = (float)(accumulate ? out[col] + t : t);
   }
 }
@@ -414,7 +563,11 @@ int avd_bn_relu_pool(const void* y, int ydt, const float* scale, const float* sh
   if (!y || !scale || !shift || !out) return AVD_ERR_ARG;
   if (N <= 0 || B <= 0 || N % B || H < 2 || W < 2) return AVD_ERR_SHAPE;
   hipStream_t st = avd_stream(stream);
-  if (pool_mode == 0) {
+  if (pool_mode == 0 && ydt == AVD_BF16 && odt == AVD_BF16 && W % 8 == 0 && H % 2 == 0) {
+    const long long total4 = (long long)N * C * (H / 2) * (W / 8);
+    bn_relu_pool_q4_kernel<<<grid_for(total4), 256, 0, st>>>((const bf16*)y, scale, shift,
+                                                             (bf16*)out, total4, B, C, H, W);
+  } else if (pool_mode == 0) {
     const long long total = (long long)N * C * (H / 2) * (W / 2);
 #define AVD_P(TY, TO)                                                                     \
   bn_relu_pool_kernel<TY, TO><<<grid_for(total), 256, 0, st>>>((const TY*)y, scale, shift, \
@@ -451,6 +604,12 @@ int avd_bn_bwd_reduce(const void* y, int ydt, const void* gout, int gdt, int poo
   if (pool_mode == 1 && gdt != AVD_F32) return AVD_ERR_DTYPE;
   hipStream_t st = avd_stream(stream);
   const int grid = avd_cdiv((long long)N * C, 4);
+  if (pool_mode == 0 && ydt == AVD_BF16 && gdt == AVD_BF16 && W % 8 == 0 && H % 2 == 0) {
+    bn_bwd_reduce_q4_kernel<<<grid, 256, 0, st>>>((const bf16*)y, (const bf16*)gout, scale, shift,
+                                                  mean, invstd, parts, N, B, C, H, W);
+    AVD_CHECK_LAUNCH();
+    return AVD_OK;
+  }
 #define AVD_R(TY, TG)                                                                         \
   bn_bwd_reduce_kernel<TY, TG><<<grid, 256, 0, st>>>((const TY*)y, (const TG*)gout, pool_mode, \
                                                      scale, shift, mean, invstd, parts, N, B,  \
@@ -484,6 +643,15 @@ int avd_bn_bwd_apply(const void* y, int ydt, const void* gout, int gdt, int pool
   if (N <= 0 || B <= 0 || N % B || (pool_mode != 0 && pool_mode != 1)) return AVD_ERR_SHAPE;
   if (pool_mode == 1 && gdt != AVD_F32) return AVD_ERR_DTYPE;
   hipStream_t st = avd_stream(stream);
+  if (pool_mode == 0 && ydt == AVD_BF16 && gdt == AVD_BF16 && dt == AVD_BF16 && W % 8 == 0 &&
+      H % 2 == 0) {
+    const long long total4 = (long long)N * C * (H / 2) * (W / 8);
+    bn_bwd_apply_q4_kernel<<<grid_for(total4), 256, 0, st>>>((const bf16*)y, (const bf16*)gout, scale,
+                                                             shift, coef, (bf16*)dy, total4, B, C, H,
+                                                             W);
+    AVD_CHECK_LAUNCH();
+    return AVD_OK;
+  }
   const long long total = (long long)N * C * ((H + 1) / 2) * ((W + 1) / 2);
 #define AVD_A(TY, TG, TD)                                                                       \
   bn_bwd_apply_kernel<TY, TG, TD><<<grid_for(total), 256, 0, st>>>(                            \
@@ -561,8 +729,12 @@ int avd_sum_rows(const float* in, int rows, int cols, long long ld, float* out, 
                  void* stream) {
   if (!in || !out) return AVD_ERR_ARG;
   if (rows <= 0 || cols <= 0 || ld < cols) return AVD_ERR_SHAPE;
-  sum_rows_kernel<<<avd_cdiv(cols, 64), 1024, 0, avd_stream(stream)>>>(in, rows, cols, ld, out,
-                                                                       accumulate);
+  if (cols <= 2048)
+    sum_rows_kernel<16><<<avd_cdiv(cols, 16), 1024, 0, avd_stream(stream)>>>(in, rows, cols, ld, out,
+                                                                            accumulate);
+  else
+    sum_rows_kernel<64><<<avd_cdiv(cols, 64), 1024, 0, avd_stream(stream)>>>(in, rows, cols, ld, out,
+                                                                            accumulate);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

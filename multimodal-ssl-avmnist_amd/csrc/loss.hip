@@ -153,16 +153,25 @@ __global__ __launch_bounds__(256) void student_kernel(const float* __restrict__ 
   }
 }
 
-// center_new = m*center + (1-m) * mean over rows of t_raw  (fixed-order f64 column sums)
-__global__ __launch_bounds__(256) void center_kernel(const float* __restrict__ t_raw,
-                                                     const float* __restrict__ center,
-                                                     float* __restrict__ center_new, int rows, int P,
-                                                     float cm) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= P) return;
+// center_new = m*center + (1-m) * mean over rows of t_raw  (fixed-order f64 column sums:
+// 16 columns x 64 row phases per block)
+__global__ __launch_bounds__(1024) void center_kernel(const float* __restrict__ t_raw,
+                                                      const float* __restrict__ center,
+                                                      float* __restrict__ center_new, int rows, int P,
+                                                      float cm) {
+  __shared__ double sh[64][16];
+  const int lc = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const int k = blockIdx.x * 16 + lc;
   double s = 0.0;
-  for (int r = 0; r < rows; ++r) s += t_raw[(size_t)r * P + k];
-  center_new[k] = (float)((double)center[k] * cm + (s / rows) * (1.0 - (double)cm));
+  if (k < P)
+    for (int r = ph; r < rows; r += 64) s += t_raw[(size_t)r * P + k];
+  sh[ph][lc] = s;
+  __syncthreads();
+  if (ph == 0 && k < P) {
+    double t = 0.0;
+    for (int i = 0; i < 64; ++i) t += sh[i][lc];
+    center_new[k] = (float)((double)center[k] * cm + (t / rows) * (1.0 - (double)cm));
+  }
 }
 
 __global__ __launch_bounds__(256) void mse_kernel(const float* __restrict__ a,
@@ -309,7 +318,7 @@ int avd_dino_loss(const float* s, const float* t_raw, const float* center, int V
   teacher_probs_kernel<<<avd_cdiv(B, 4), 256, 0, st>>>(tn, ptsum, T, B, P, 1.f / tau_t);
   student_kernel<<<avd_cdiv((long long)V * B, 4), 256, 0, st>>>(s, ptsum, loss_parts, ds, V, T, B,
                                                                  P, 1.f / tau_s);
-  center_kernel<<<avd_cdiv(P, 256), 256, 0, st>>>(t_raw, center, center_new, T * B, P, center_m);
+  center_kernel<<<avd_cdiv(P, 16), 1024, 0, st>>>(t_raw, center, center_new, T * B, P, center_m);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

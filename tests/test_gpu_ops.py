@@ -188,6 +188,37 @@ def test_bn_relu_pool_block_fwd_bwd(ops, H, gap):
     assert np.abs(host(dbias)).max() < 1e-4  # sum of dy through BN is analytically zero
 
 
+@pytest.mark.parametrize("H", [112, 56, 16, 28])
+def test_bn_relu_pool_bf16_matches_f32(ops, H):
+    """bf16 maps (the 4-window vector kernels when W % 8 == 0) against the f32 kernels fed the
+    same bf16-rounded values: reductions agree to f32 rounding, stored maps to one bf16 ulp."""
+    G, B, C = 2, 3, 8
+    N = G * B
+    g = np.random.default_rng(H)
+    y = _bf16_round(g.normal(0.3, 1.5, (N, C, H, H)))
+    gout = _bf16_round(g.uniform(-1, 1, (N, C, H // 2, H // 2)))
+    scale = dev(g.uniform(0.5, 1.5, G * C).astype(np.float32))
+    shift = dev(g.uniform(-0.5, 0.5, G * C).astype(np.float32))
+    mean = dev(g.uniform(-0.2, 0.2, G * C).astype(np.float32))
+    invstd = dev(g.uniform(0.5, 1.5, G * C).astype(np.float32))
+    coef = dev(g.uniform(-1, 1, G * C * 3).astype(np.float32))
+    res = {}
+    for dt in (torch.float32, torch.bfloat16):
+        ty, tg = dev(y, dt), dev(gout, dt)
+        out = torch.empty(N, C, H // 2, H // 2, device="cuda", dtype=dt)
+        ops.bn_relu_pool(ty, scale, shift, out, 0, N, B, C, H, H)
+        parts = torch.empty(C * N * 2, device="cuda")
+        ops.bn_bwd_reduce(ty, tg, 0, scale, shift, mean, invstd, parts, N, B, C, H, H)
+        dy = torch.empty_like(ty)
+        ops.bn_bwd_apply(ty, tg, 0, scale, shift, coef, dy, N, B, C, H, H)
+        res[dt] = (host(out), host(parts), host(dy))
+    (o32, p32, d32), (o16, p16, d16) = res[torch.float32], res[torch.bfloat16]
+    np.testing.assert_allclose(o16, o32, rtol=8e-3, atol=1e-6)
+    np.testing.assert_allclose(p16, p32, rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(d16, d32, rtol=8e-3, atol=1e-2)
+    assert rel(d16, d32) < 4e-3
+
+
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("shape", [(70, 130, 45), (256, 3136, 300), (130, 64, 1000)])
 def test_gemm_modes_and_strides(ops, mode, shape):
