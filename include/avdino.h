@@ -100,8 +100,9 @@ int avd_conv2d_wgrad(const void* x, int xdt, const void* dy, int dydt, float* dw
  * conv stats R = B*T), count = elements per (group, channel).  Outputs mean/invstd/scale/shift [G,C] (scale = gamma*invstd,
  * shift = beta - mean*scale).  If running_mean != NULL, applies the reference's sequential
  * per-call update for g = 0..G-1: rm = 0.9 rm + 0.1 mean_g, rv = 0.9 rv + 0.1 var_g*n/(n-1)
- * (nn.BatchNorm momentum 0.1; group order = the reference's call order, dino.py:680-704). */
-int avd_bn_finalize(const float* parts, int G, int R, int C, long long count,
+ * (nn.BatchNorm momentum 0.1; group order = the reference's call order, dino.py:680-704).
+ * parts is consumed: the chunked first pass writes f64 chunk sums over it. */
+int avd_bn_finalize(float* parts, int G, int R, int C, long long count,
                     const float* gamma, const float* beta, float eps, float momentum,
                     float* mean, float* invstd, float* scale, float* shift,
                     float* running_mean, float* running_var, void* stream);
@@ -142,10 +143,15 @@ int avd_bn_bwd_apply(const void* y, int ydt, const void* gout, int gdt, int pool
  * nn.Linear forward (x W^T + b), input grad (dy W) and weight grad (dy^T x).
  * mode 0: f32 VALU FMA; mode 1: f32 MFMA (v_mfma_f32_16x16x4_f32, exact f32 products);
  * mode 2: bf16 MFMA (operands rounded to bf16, f32 accumulate; the bf16 training mode).
- * Deterministic (no split-K, no atomics). */
+ * Modes 1/2 split deep-K products (weight gradients, K = batch rows) across blocks when the
+ * caller passes a workspace of avd_gemm_ws_elems(M,N,K,mode) floats: partial tiles are summed
+ * in fixed split order by a second kernel (deterministic, no atomics; ws may be NULL, then
+ * one pass over K).  Results do not depend on the workspace beyond that choice. */
+long long avd_gemm_ws_elems(int M, int N, int K, int mode);
 int avd_gemm(int M, int N, int K, const float* A, long long sam, long long sak,
              const float* B, long long sbk, long long sbn, float* C, long long ldc,
-             const float* bias, float alpha, float beta, int mode, void* stream);
+             const float* bias, float alpha, float beta, int mode, float* ws,
+             long long ws_elems, void* stream);
 
 /* out[c] (+)= sum_{r<rows} in[r*ld + c]   (fixed order, f64 accumulation) -- reduces the conv
  * weight-grad partial slabs and gives Linear bias gradients (column sums of dy). */

@@ -32,7 +32,8 @@ PROTOS = {
     "avd_bn_bwd_reduce": [P, I, P, I, I, P, P, P, P, P, I, I, I, I, I, P],
     "avd_bn_bwd_finalize": [P, I, I, I, L, P, P, P, P, P, P, P, I, P],
     "avd_bn_bwd_apply": [P, I, P, I, I, P, P, P, P, I, I, I, I, I, I, P],
-    "avd_gemm": [I, I, I, P, L, L, P, L, L, P, L, P, F, F, I, P],
+    "avd_gemm": [I, I, I, P, L, L, P, L, L, P, L, P, F, F, I, P, L, P],
+    "avd_gemm_ws_elems": [I, I, I, I],
     "avd_sum_rows": [P, I, I, L, P, I, P],
     "avd_colstats_parts": [I],
     "avd_colstats": [P, I, I, I, P, P],
@@ -67,6 +68,7 @@ def _load():
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = ctypes.c_int
+    lib.avd_gemm_ws_elems.restype = ctypes.c_longlong
     lib.avd_last_error.argtypes = []
     lib.avd_last_error.restype = ctypes.c_char_p
     return lib

@@ -192,10 +192,25 @@ def gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, bias=None, alpha=1.0, beta=0
     _need(b_off >= 0 and b_off + (K - 1) * sbk + (N - 1) * sbn < B.numel(), "gemm B bounds")
     _need(c_off >= 0 and c_off + (M - 1) * ldc + (N - 1) < C.numel(), "gemm C bounds")
     _need(bias is None or bias.numel() >= N, "gemm bias")
+    nws = lib.avd_gemm_ws_elems(M, N, K, mode)
+    ws = _gemm_workspace(C.device, nws) if nws > 0 else None
     _timed(f"gemm[{M}x{N}x{K} m{mode}]", 4 * (M * K + K * N + M * N), 2 * M * N * K,
            lambda: call("avd_gemm", M, N, K, A.data_ptr() + 4 * a_off, sam, sak,
                         B.data_ptr() + 4 * b_off, sbk, sbn, C.data_ptr() + 4 * c_off, ldc, p(bias),
-                        alpha, beta, mode, stream()))
+                        alpha, beta, mode, p(ws), nws, stream()))
+
+
+_GEMM_WS = {}
+
+
+def _gemm_workspace(device, n):
+    """Split-K partial-tile scratch, one per device, grown on demand (stream-ordered reuse:
+    every GEMM on the stream finishes its reduce before the next one writes)."""
+    t = _GEMM_WS.get(device)
+    if t is None or t.numel() < n:
+        t = torch.empty(max(n, 1 << 20), device=device, dtype=torch.float32)
+        _GEMM_WS[device] = t
+    return t
 
 
 def linear_fwd(x, w, b, out, rows, x_ld=None, x_off=0, out_ld=None, out_off=0, mode=GEMM_F32_MFMA):

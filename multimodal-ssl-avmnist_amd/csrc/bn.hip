@@ -11,6 +11,8 @@
 //
 // Partial-statistic layout everywhere: channel-major parts [C][G][R][2] so the finaliser
 // reads contiguous rows.  All reductions are fixed-order (f64 in the finalisers).
+#include <algorithm>
+
 #include "common.h"
 
 using namespace avd;
@@ -45,32 +47,60 @@ __device__ __forceinline__ void reduce_pairs(const float* __restrict__ p, long l
 }
 
 // ----------------------------------------------------------------------------- forward stats
-__global__ __launch_bounds__(256) void bn_finalize_kernel(
-    const float* __restrict__ parts, int G, int R, int C, long long count,
+// Two passes.  (1) grid (S, G, C): block (s, g, c) sums rows [s*chunk, ...) of the (g, c)
+// partial-pair list in f64 and, once every thread has read its rows, stores the two doubles
+// over the first rows of its own chunk (disjoint per block, so the in-place write is safe:
+// parts is consumed).  (2) one thread per channel folds the S chunk sums of every group in
+// fixed order and applies the running-stat updates sequentially over g.
+__global__ __launch_bounds__(256) void bn_stats_partial_kernel(float* __restrict__ parts, int G,
+                                                               int R, int S, int chunk) {
+  __shared__ double sh[4];
+  const int s = blockIdx.x, g = blockIdx.y, c = blockIdx.z;
+  float* p = parts + (((size_t)c * G + g) * R + (size_t)s * chunk) * 2;
+  // the last chunk takes the remainder, so every chunk has >= 2 rows = room for 2 doubles
+  const int rows = s == S - 1 ? R - s * chunk : chunk;
+  double a, q;
+  reduce_pairs(p, rows, sh, a, q);   // ends with a barrier after all reads
+  if (threadIdx.x == 0) {
+    double* d = reinterpret_cast<double*>(p);   // 8-byte aligned: even float offset
+    d[0] = a;
+    d[1] = q;
+  }
+}
+
+__global__ __launch_bounds__(64) void bn_finalize_kernel(
+    const float* __restrict__ parts, int G, int R, int C, int S, int chunk, long long count,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
     float* mean_o, float* invstd_o, float* scale_o, float* shift_o, float* rm, float* rv) {
-  __shared__ double sh[4];
-  const int c = blockIdx.x;
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= C) return;
   double rmean = rm ? (double)rm[c] : 0.0, rvar = rv ? (double)rv[c] : 0.0;
+  const double n = (double)count;
   for (int g = 0; g < G; ++g) {
-    double s, q;
-    reduce_pairs(parts + ((size_t)c * G + g) * R * 2, R, sh, s, q);
-    const double n = (double)count;
-    const double mean = s / n;
-    double var = q / n - mean * mean;
+    double sum = 0.0, sq = 0.0;
+    if (S == 0) {   // R == 1: the single partial row as is
+      sum = parts[((size_t)c * G + g) * 2];
+      sq = parts[((size_t)c * G + g) * 2 + 1];
+    }
+    for (int s = 0; s < S; ++s) {
+      const double* d =
+          reinterpret_cast<const double*>(parts + (((size_t)c * G + g) * R + (size_t)s * chunk) * 2);
+      sum += d[0];
+      sq += d[1];
+    }
+    const double mean = sum / n;
+    double var = sq / n - mean * mean;
     if (var < 0) var = 0;
     const double invstd = 1.0 / sqrt(var + (double)eps);
-    if (threadIdx.x == 0) {
-      const double sc = (double)gamma[c] * invstd;
-      mean_o[g * C + c] = (float)mean;
-      invstd_o[g * C + c] = (float)invstd;
-      scale_o[g * C + c] = (float)sc;
-      shift_o[g * C + c] = (float)((double)beta[c] - mean * sc);
-      rmean = (1.0 - momentum) * rmean + momentum * mean;
-      rvar = (1.0 - momentum) * rvar + momentum * var * n / (n - 1.0);
-    }
+    const double sc = (double)gamma[c] * invstd;
+    mean_o[g * C + c] = (float)mean;
+    invstd_o[g * C + c] = (float)invstd;
+    scale_o[g * C + c] = (float)sc;
+    shift_o[g * C + c] = (float)((double)beta[c] - mean * sc);
+    rmean = (1.0 - momentum) * rmean + momentum * mean;
+    rvar = (1.0 - momentum) * rvar + momentum * var * n / (n - 1.0);
   }
-  if (threadIdx.x == 0 && rm) {
+  if (rm) {
     rm[c] = (float)rmean;
     rv[c] = (float)rvar;
   }
@@ -328,25 +358,45 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_q4_kernel(
   const float sc = scale[g * C + c], sf = shift[g * C + c];
   const float mu = mean[g * C + c], is = invstd[g * C + c];
   float s1 = 0.f, s2 = 0.f;
-  for (int t = lane; t < HQ; t += 64) {
-    const int hp = t / Q, q = t - (t / Q) * Q;
-    const size_t base = ((size_t)nc * H + 2 * hp) * W + 8 * q;
-    float r0[8], r1[8];
-    unpack8(*reinterpret_cast<const u4v*>(y + base), r0);
-    unpack8(*reinterpret_cast<const u4v*>(y + base + W), r1);
-    const u2v gv = *reinterpret_cast<const u2v*>(gout + ((size_t)nc * Hp + hp) * Wp + 4 * q);
-    const float gg[4] = {__uint_as_float(gv.x << 16), __uint_as_float(gv.x & 0xffff0000u),
-                         __uint_as_float(gv.y << 16), __uint_as_float(gv.y & 0xffff0000u)};
-    int arg[4];
-    float mx[4];
-    quad_windows(r0, r1, sc, sf, arg, mx);
+  const bf16* yp = y + (size_t)nc * H * W;
+  const bf16* gp = gout + (size_t)nc * Hp * Wp;
+  // 4 quads per lane per pass with every load issued before any math: a wave-per-plane
+  // reduction is bound by load latency, not bandwidth
+  for (int t0 = lane; t0 < HQ; t0 += 256) {
+    u4v a0[4], a1[4];
+    u2v gv[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (mx[k] > 0.f) {
-        const int a = arg[k];
-        const float ya = (a < 2) ? r0[2 * k + a] : r1[2 * k + a - 2];
-        s1 += gg[k];
-        s2 += gg[k] * (ya - mu) * is;
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + 64 * u;
+      if (t < HQ) {
+        const int hp = t / Q, q = t - hp * Q;
+        const size_t base = (size_t)(2 * hp) * W + 8 * q;
+        a0[u] = *reinterpret_cast<const u4v*>(yp + base);
+        a1[u] = *reinterpret_cast<const u4v*>(yp + base + W);
+        gv[u] = *reinterpret_cast<const u2v*>(gp + (size_t)hp * Wp + 4 * q);
+      } else {   // zero gradient: contributes nothing
+        a0[u] = u4v{0u, 0u, 0u, 0u};
+        a1[u] = u4v{0u, 0u, 0u, 0u};
+        gv[u] = u2v{0u, 0u};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float r0[8], r1[8];
+      unpack8(a0[u], r0);
+      unpack8(a1[u], r1);
+      const float gg[4] = {__uint_as_float(gv[u].x << 16), __uint_as_float(gv[u].x & 0xffff0000u),
+                           __uint_as_float(gv[u].y << 16), __uint_as_float(gv[u].y & 0xffff0000u)};
+      int arg[4];
+      float mx[4];
+      quad_windows(r0, r1, sc, sf, arg, mx);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int a = arg[k];   // selects, not a runtime register index
+        const float ya = a == 0 ? r0[2 * k] : a == 1 ? r0[2 * k + 1] : a == 2 ? r1[2 * k] : r1[2 * k + 1];
+        const float gk = mx[k] > 0.f ? gg[k] : 0.f;
+        s1 += gk;
+        s2 += gk * (ya - mu) * is;
       }
     }
   }
@@ -544,16 +594,24 @@ inline int grid_for(long long total) {
 
 extern "C" {
 
-int avd_bn_finalize(const float* parts, int G, int R, int C, long long count, const float* gamma,
+int avd_bn_finalize(float* parts, int G, int R, int C, long long count, const float* gamma,
                     const float* beta, float eps, float momentum, float* mean, float* invstd,
                     float* scale, float* shift, float* running_mean, float* running_var,
                     void* stream) {
   if (!parts || !gamma || !beta || !mean || !invstd || !scale || !shift) return AVD_ERR_ARG;
   if (G <= 0 || R <= 0 || C <= 0 || count <= 1) return AVD_ERR_SHAPE;
   if ((running_mean == nullptr) != (running_var == nullptr)) return AVD_ERR_ARG;
-  bn_finalize_kernel<<<C, 256, 0, avd_stream(stream)>>>(parts, G, R, C, count, gamma, beta, eps,
-                                                         momentum, mean, invstd, scale, shift,
-                                                         running_mean, running_var);
+  hipStream_t st = avd_stream(stream);
+  // ~2048 partial rows per block, >= 2 rows per chunk (room for the in-place doubles)
+  int S = 0, chunk = 1;
+  if (R >= 2) {
+    chunk = std::max(2, avd_cdiv(R, std::min(avd_cdiv(R, 2048), 1024)));
+    S = R / chunk;
+    bn_stats_partial_kernel<<<dim3(S, G, C), 256, 0, st>>>(parts, G, R, S, chunk);
+  }
+  bn_finalize_kernel<<<avd_cdiv(C, 64), 64, 0, st>>>(parts, G, R, C, S, chunk, count, gamma, beta,
+                                                    eps, momentum, mean, invstd, scale, shift,
+                                                    running_mean, running_var);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

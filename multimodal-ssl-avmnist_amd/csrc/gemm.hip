@@ -5,6 +5,8 @@
 //
 // v1: LDS-tiled 64x64x16 tiles, 256 threads, 4x4 outputs per thread, fp32 FMA (bitwise
 // deterministic: no split-K).
+#include <algorithm>
+
 #include "common.h"
 
 using namespace avd;
@@ -89,9 +91,14 @@ __global__ __launch_bounds__(256) void sgemm_kernel(int M, int N, int K, const f
 // MFMA GEMM.  MODE 1: v_mfma_f32_16x16x4_f32 (f32 operands: exact f32 FMA chains, the fp32
 // parity mode); MODE 2: v_mfma_f32_16x16x32_bf16 (operands rounded to bf16 while staging,
 // fp32 accumulate: the bf16 training mode, like the reference's fp16 autocast Linear).
-// Block tile 64x64, BK 32, 4 waves x (32x32 = 2x2 MFMA tiles).  Operands are staged in LDS
-// with k contiguous ([m][k] for A, [n][k] for B) so every fragment is one LDS read; global
-// loads are float4 whenever the contiguous stride is 1 and rows are 16-byte aligned.
+//
+// Block tile BM x BN (128x128, 128x64 or 64x64), BK 32, 4 waves in a 2x2 grid, each wave
+// (BM/2)x(BN/2) = TI x TJ MFMA 16x16 tiles.  Operands live in LDS k-contiguous ([m][k] for A,
+// [n][k] for B) so every fragment is one LDS read.  Software pipeline: the next k-tile is
+// loaded into registers (float4 whenever a stride is 1) while the current one feeds the
+// MFMAs, then written to the other half of a double-buffered LDS ring -> one barrier per
+// k-tile.  Split-K (blockIdx.z) writes raw partial tiles to a workspace that a second kernel
+// sums in fixed split order: deterministic, no atomics.
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f4;
 
@@ -100,46 +107,44 @@ struct GemmT { typedef float T; static constexpr int LDK = 33; };
 template <>
 struct GemmT<2> { typedef bf16 T; static constexpr int LDK = 40; };
 
-template <int MODE>
-__device__ __forceinline__ void lds_put(typename GemmT<MODE>::T* p, float v) {
-  if constexpr (MODE == 2) *p = f2bf(v); else *p = v;
-}
+// Operand layouts of a (rows x 32) tile of X with element (r, k) at X[r*sr + k*sk]:
+// LAY_K: k contiguous & 16B aligned rows (float4 along k); LAY_R: rows contiguous (float4 along
+// r); LAY_S: anything else (scalar).
+enum { LAY_K = 0, LAY_R = 1, LAY_S = 2 };
 
-// Stage a 64 (rows r) x 32 (k) tile of a matrix X with element (r, k) at X[r*sr + k*sk] into
-// S[r*LDK + k].  rows/ks = valid extent.
-template <int MODE>
-__device__ __forceinline__ void stage_tile(const float* __restrict__ X, long long sr, long long sk,
-                                           int r0, int k0, int rows, int ks, bool vec,
-                                           typename GemmT<MODE>::T* S) {
-  constexpr int LDK = GemmT<MODE>::LDK;
+template <int ROWS>
+struct TileRegs { float v[ROWS / 8]; };   // ROWS*32 elements over 256 threads
+
+template <int ROWS, int LAY>
+__device__ __forceinline__ void load_tile(const float* __restrict__ X, long long sr, long long sk,
+                                          int r0, int k0, int rows, int kend, TileRegs<ROWS>& t) {
   const int tid = threadIdx.x;
-  if (vec && sk == 1) {  // k contiguous: float4 along k
+  if constexpr (LAY == LAY_K) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < ROWS / 32; ++i) {
       const int e4 = tid + 256 * i;
       const int r = e4 >> 3, k = (e4 & 7) * 4;
       const int gr = r0 + r, gk = k0 + k;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (gr < rows) {
         const float* p = X + (size_t)gr * sr + gk;
-        if (gk + 3 < ks) v = *reinterpret_cast<const float4*>(p);
+        if (gk + 3 < kend) v = *reinterpret_cast<const float4*>(p);
         else {
-          if (gk < ks) v.x = p[0];
-          if (gk + 1 < ks) v.y = p[1];
-          if (gk + 2 < ks) v.z = p[2];
+          if (gk < kend) v.x = p[0];
+          if (gk + 1 < kend) v.y = p[1];
+          if (gk + 2 < kend) v.z = p[2];
         }
       }
-      typename GemmT<MODE>::T* d = S + r * LDK + k;
-      lds_put<MODE>(d, v.x); lds_put<MODE>(d + 1, v.y); lds_put<MODE>(d + 2, v.z); lds_put<MODE>(d + 3, v.w);
+      t.v[4 * i] = v.x; t.v[4 * i + 1] = v.y; t.v[4 * i + 2] = v.z; t.v[4 * i + 3] = v.w;
     }
-  } else if (vec && sr == 1) {  // rows contiguous: float4 along r
+  } else if constexpr (LAY == LAY_R) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < ROWS / 32; ++i) {
       const int e4 = tid + 256 * i;
-      const int k = e4 >> 4, r = (e4 & 15) * 4;
+      const int k = e4 / (ROWS / 4), r = (e4 % (ROWS / 4)) * 4;
       const int gr = r0 + r, gk = k0 + k;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (gk < ks) {
+      if (gk < kend) {
         const float* p = X + (size_t)gk * sk + gr;
         if (gr + 3 < rows) v = *reinterpret_cast<const float4*>(p);
         else {
@@ -148,127 +153,280 @@ __device__ __forceinline__ void stage_tile(const float* __restrict__ X, long lon
           if (gr + 2 < rows) v.z = p[2];
         }
       }
-      lds_put<MODE>(S + r * LDK + k, v.x);
-      lds_put<MODE>(S + (r + 1) * LDK + k, v.y);
-      lds_put<MODE>(S + (r + 2) * LDK + k, v.z);
-      lds_put<MODE>(S + (r + 3) * LDK + k, v.w);
+      t.v[4 * i] = v.x; t.v[4 * i + 1] = v.y; t.v[4 * i + 2] = v.z; t.v[4 * i + 3] = v.w;
     }
   } else {
     const bool kfast = sk <= sr;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < ROWS / 8; ++i) {
       const int e = tid + 256 * i;
       int r, k;
-      if (kfast) { r = e >> 5; k = e & 31; } else { k = e >> 6; r = e & 63; }
+      if (kfast) { r = e >> 5; k = e & 31; } else { k = e / ROWS; r = e % ROWS; }
       const int gr = r0 + r, gk = k0 + k;
-      const float v = (gr < rows && gk < ks) ? X[(size_t)gr * sr + (size_t)gk * sk] : 0.f;
-      lds_put<MODE>(S + r * LDK + k, v);
+      t.v[i] = (gr < rows && gk < kend) ? X[(size_t)gr * sr + (size_t)gk * sk] : 0.f;
     }
   }
 }
 
 template <int MODE>
-__global__ __launch_bounds__(256) void gemm_mfma_kernel(int M, int N, int K, const float* __restrict__ A,
-                                                        long long sam, long long sak,
-                                                        const float* __restrict__ B, long long sbk,
-                                                        long long sbn, float* __restrict__ C,
-                                                        long long ldc, const float* __restrict__ bias,
-                                                        float alpha, float beta, int vecA, int vecB) {
+__device__ __forceinline__ void lds_put(typename GemmT<MODE>::T* p, float v) {
+  if constexpr (MODE == 2) *p = f2bf(v); else *p = v;
+}
+
+template <int MODE, int ROWS, int LAY>
+__device__ __forceinline__ void store_tile(const TileRegs<ROWS>& t, long long sr, long long sk,
+                                           typename GemmT<MODE>::T* S) {
+  constexpr int LDK = GemmT<MODE>::LDK;
+  const int tid = threadIdx.x;
+  if constexpr (LAY == LAY_K) {
+#pragma unroll
+    for (int i = 0; i < ROWS / 32; ++i) {
+      const int e4 = tid + 256 * i;
+      const int r = e4 >> 3, k = (e4 & 7) * 4;
+      typename GemmT<MODE>::T* d = S + r * LDK + k;
+      if constexpr (MODE == 2) {
+        // 4 bf16 = one 8-byte LDS store
+        const unsigned lo = (unsigned)f2bf(t.v[4 * i]) | ((unsigned)f2bf(t.v[4 * i + 1]) << 16);
+        const unsigned hi = (unsigned)f2bf(t.v[4 * i + 2]) | ((unsigned)f2bf(t.v[4 * i + 3]) << 16);
+        *reinterpret_cast<uint2*>(d) = make_uint2(lo, hi);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = t.v[4 * i + j];
+      }
+    }
+  } else if constexpr (LAY == LAY_R) {
+#pragma unroll
+    for (int i = 0; i < ROWS / 32; ++i) {
+      const int e4 = tid + 256 * i;
+      const int k = e4 / (ROWS / 4), r = (e4 % (ROWS / 4)) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) lds_put<MODE>(S + (r + j) * LDK + k, t.v[4 * i + j]);
+    }
+  } else {
+    const bool kfast = sk <= sr;
+#pragma unroll
+    for (int i = 0; i < ROWS / 8; ++i) {
+      const int e = tid + 256 * i;
+      int r, k;
+      if (kfast) { r = e >> 5; k = e & 31; } else { k = e / ROWS; r = e % ROWS; }
+      lds_put<MODE>(S + r * LDK + k, t.v[i]);
+    }
+  }
+}
+
+template <int MODE, int BM, int BN, int LA, int LB>
+__global__ __launch_bounds__(256) void gemm_mfma_kernel(
+    int M, int N, int K, int kchunk, const float* __restrict__ A, long long sam, long long sak,
+    const float* __restrict__ B, long long sbk, long long sbn, float* __restrict__ C, long long ldc,
+    const float* __restrict__ bias, float alpha, float beta, float* __restrict__ ws) {
   typedef typename GemmT<MODE>::T T;
   constexpr int LDK = GemmT<MODE>::LDK;
-  __shared__ __attribute__((aligned(16))) T As[64 * LDK];
-  __shared__ __attribute__((aligned(16))) T Bs[64 * LDK];
+  constexpr int TI = BM / 32, TJ = BN / 32;   // MFMA tiles per wave
+  __shared__ __attribute__((aligned(16))) T As[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) T Bs[2][BN * LDK];
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
   const int g = lane >> 4, r16 = lane & 15;
-  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
-  f4 acc[2][2];
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int kbeg = blockIdx.z * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+  f4 acc[TI][TJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  for (int k0 = 0; k0 < K; k0 += 32) {
-    stage_tile<MODE>(A, sam, sak, m0, k0, M, K, vecA, As);
-    stage_tile<MODE>(B, sbn, sbk, n0, k0, N, K, vecB, Bs);   // B^T tile: rows = n
-    __syncthreads();
+  TileRegs<BM> ta;
+  TileRegs<BN> tb;
+  const int nk = (kend - kbeg + 31) / 32;
+  load_tile<BM, LA>(A, sam, sak, m0, kbeg, M, kend, ta);
+  load_tile<BN, LB>(B, sbn, sbk, n0, kbeg, N, kend, tb);   // B^T tile: rows = n
+  store_tile<MODE, BM, LA>(ta, sam, sak, As[0]);
+  store_tile<MODE, BN, LB>(tb, sbn, sbk, Bs[0]);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      load_tile<BM, LA>(A, sam, sak, m0, kbeg + 32 * (kt + 1), M, kend, ta);
+      load_tile<BN, LB>(B, sbn, sbk, n0, kbeg + 32 * (kt + 1), N, kend, tb);
+    }
+    const T* as = As[cur] + (BM / 2 * wm + r16) * LDK;
+    const T* bs = Bs[cur] + (BN / 2 * wn + r16) * LDK;
     if constexpr (MODE == 2) {
-      bf16x8 a[2], b[2];
+      bf16x8 a[TI], b[TJ];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        a[i] = *reinterpret_cast<const bf16x8*>(As + (32 * wm + 16 * i + r16) * LDK + 8 * g);
+      for (int i = 0; i < TI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(as + 16 * i * LDK + 8 * g);
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        b[j] = *reinterpret_cast<const bf16x8*>(Bs + (32 * wn + 16 * j + r16) * LDK + 8 * g);
+      for (int j = 0; j < TJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(bs + 16 * j * LDK + 8 * g);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < TJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     } else {
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
-        float a[2], b[2];
+        float a[TI], b[TJ];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) a[i] = As[(32 * wm + 16 * i + r16) * LDK + 4 * ks + g];
+        for (int i = 0; i < TI; ++i) a[i] = as[16 * i * LDK + 4 * ks + g];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) b[j] = Bs[(32 * wn + 16 * j + r16) * LDK + 4 * ks + g];
+        for (int j = 0; j < TJ; ++j) b[j] = bs[16 * j * LDK + 4 * ks + g];
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < TJ; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
       }
     }
+    if (more) {
+      store_tile<MODE, BM, LA>(ta, sam, sak, As[cur ^ 1]);
+      store_tile<MODE, BN, LB>(tb, sbn, sbk, Bs[cur ^ 1]);
+    }
     __syncthreads();
   }
+  float* part = ws ? ws + (size_t)blockIdx.z * M * N : nullptr;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + 32 * wn + 16 * j + r16;
+    for (int j = 0; j < TJ; ++j) {
+      const int n = n0 + BN / 2 * wn + 16 * j + r16;
       if (n >= N) continue;
-      const float bv = bias ? bias[n] : 0.f;
+      const float bv = (!part && bias) ? bias[n] : 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int m = m0 + 32 * wm + 16 * i + 4 * g + e;
+        const int m = m0 + BM / 2 * wm + 16 * i + 4 * g + e;
         if (m >= M) continue;
-        float* c = C + (size_t)m * ldc + n;
-        float v = alpha * acc[i][j][e] + bv;
-        if (beta != 0.f) v += beta * *c;
-        *c = v;
+        if (part) {
+          part[(size_t)m * N + n] = acc[i][j][e];
+        } else {
+          float* c = C + (size_t)m * ldc + n;
+          float v = alpha * acc[i][j][e] + bv;
+          if (beta != 0.f) v += beta * *c;
+          *c = v;
+        }
       }
     }
 }
 
-bool vec_ok(const float* p, long long s_contig, long long s_other) {
-  return s_contig == 1 && (s_other % 4) == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+// C = alpha * sum_{z < S} ws[z] (+bias) (+beta C), fixed split order
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S,
+                                                            int M, int N, float* __restrict__ C,
+                                                            long long ldc,
+                                                            const float* __restrict__ bias,
+                                                            float alpha, float beta) {
+  const long long MN = (long long)M * N;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < MN; i += (long long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int z = 0; z < S; ++z) s += ws[(size_t)z * MN + i];
+    const int m = (int)(i / N), n = (int)(i % N);
+    float* c = C + (size_t)m * ldc + n;
+    float v = alpha * s + (bias ? bias[n] : 0.f);
+    if (beta != 0.f) v += beta * *c;
+    *c = v;
+  }
+}
+
+int lay_of(const float* p, long long s_rows, long long s_k) {
+  const bool al = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+  if (s_k == 1 && s_rows % 4 == 0 && al) return LAY_K;
+  if (s_rows == 1 && s_k % 4 == 0 && al) return LAY_R;
+  return LAY_S;
+}
+
+// Launch plan: the largest tile whose grid still covers the chip; deep-K products with few
+// tiles (weight gradients: K = batch rows) split K so >= ~2 blocks per CU run.
+struct Plan { int bm, bn, splits, kchunk; };
+
+Plan plan_for(int M, int N, int K) {
+  auto tiles = [&](int bm, int bn) { return (long long)avd_cdiv(M, bm) * avd_cdiv(N, bn); };
+  Plan p{64, 64, 1, K};
+  if (tiles(128, 128) >= 224) p = {128, 128, 1, K};
+  else if (tiles(128, 64) >= 224) p = {128, 64, 1, K};
+  else if (K >= 1024)   // deep K: the split below restores the block count
+    p = (M >= 128 && N >= 128) ? Plan{128, 128, 1, K} : (M >= 128 ? Plan{128, 64, 1, K} : p);
+  const long long t = tiles(p.bm, p.bn);
+  if (t < 224 && K >= 512) {
+    int s = (int)std::min<long long>(avd_cdiv(512, t), K / 256);
+    s = std::max(1, std::min(s, 64));
+    if (s > 1) {
+      p.kchunk = avd_cdiv(avd_cdiv(K, s), 32) * 32;
+      p.splits = avd_cdiv(K, p.kchunk);
+    }
+  }
+  return p;
+}
+
+template <int MODE, int LA, int LB>
+void launch_gemm(const Plan& pl, int M, int N, int K, const float* A, long long sam, long long sak,
+                 const float* B, long long sbk, long long sbn, float* C, long long ldc,
+                 const float* bias, float alpha, float beta, float* ws, hipStream_t st) {
+  dim3 grid(avd_cdiv(N, pl.bn), avd_cdiv(M, pl.bm), pl.splits);
+  float* w = pl.splits > 1 ? ws : nullptr;
+#define AVD_G(BM_, BN_)                                                                        \
+  if (pl.bm == BM_ && pl.bn == BN_)                                                            \
+    gemm_mfma_kernel<MODE, BM_, BN_, LA, LB><<<grid, 256, 0, st>>>(                            \
+        M, N, K, pl.kchunk, A, sam, sak, B, sbk, sbn, C, ldc, bias, alpha, beta, w);
+  AVD_G(128, 128) else AVD_G(128, 64) else AVD_G(64, 64)
+#undef AVD_G
+  if (pl.splits > 1) {
+    const long long MN = (long long)M * N;
+    const int blocks = (int)std::min<long long>(avd_cdiv(MN, 256), 4096);
+    splitk_reduce_kernel<<<blocks, 256, 0, st>>>(ws, pl.splits, M, N, C, ldc, bias, alpha, beta);
+  }
+}
+
+// operand layouts are template parameters (the index math of the others would otherwise sit in
+// registers): K/R combinations get vector loads, anything with a scalar operand the generic path
+template <int MODE>
+void dispatch_gemm(const Plan& pl, int lA, int lB, int M, int N, int K, const float* A,
+                   long long sam, long long sak, const float* B, long long sbk, long long sbn,
+                   float* C, long long ldc, const float* bias, float alpha, float beta, float* ws,
+                   hipStream_t st) {
+#define AVD_L(LA_, LB_) launch_gemm<MODE, LA_, LB_>(pl, M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, \
+                                                   bias, alpha, beta, ws, st)
+  if (lA == LAY_K && lB == LAY_K) AVD_L(LAY_K, LAY_K);
+  else if (lA == LAY_K && lB == LAY_R) AVD_L(LAY_K, LAY_R);
+  else if (lA == LAY_R && lB == LAY_R) AVD_L(LAY_R, LAY_R);
+  else if (lA == LAY_R && lB == LAY_K) AVD_L(LAY_R, LAY_K);
+  else AVD_L(LAY_S, LAY_S);
+#undef AVD_L
 }
 
 }  // namespace
 
 extern "C" {
 
+long long avd_gemm_ws_elems(int M, int N, int K, int mode) {
+  if (mode != 1 && mode != 2) return 0;
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const Plan p = plan_for(M, N, K);
+  return p.splits > 1 ? (long long)p.splits * M * N : 0;
+}
+
 int avd_gemm(int M, int N, int K, const float* A, long long sam, long long sak, const float* B,
              long long sbk, long long sbn, float* C, long long ldc, const float* bias, float alpha,
-             float beta, int mode, void* stream) {
+             float beta, int mode, float* ws, long long ws_elems, void* stream) {
   if (!A || !B || !C) return AVD_ERR_ARG;
   if (M <= 0 || N <= 0 || K <= 0) return AVD_ERR_SHAPE;
   hipStream_t st = avd_stream(stream);
-  dim3 grid(avd_cdiv(N, 64), avd_cdiv(M, 64));
   if (mode == 0) {
+    dim3 grid(avd_cdiv(N, 64), avd_cdiv(M, 64));
     sgemm_kernel<<<grid, 256, 0, st>>>(M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, bias, alpha,
                                         beta, nullptr);
   } else if (mode == 1 || mode == 2) {
-    const int vA = vec_ok(A, sak == 1 ? sak : sam, sak == 1 ? sam : sak);
-    const int vB = vec_ok(B, sbk == 1 ? sbk : sbn, sbk == 1 ? sbn : sbk);
+    Plan pl = plan_for(M, N, K);
+    if (pl.splits > 1 && (!ws || ws_elems < (long long)pl.splits * M * N)) {
+      pl.splits = 1;   // no (or too small a) workspace: single pass over K
+      pl.kchunk = K;
+    }
+    const int lA = lay_of(A, sam, sak);
+    const int lB = lay_of(B, sbn, sbk);
     if (mode == 1)
-      gemm_mfma_kernel<1><<<grid, 256, 0, st>>>(M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, bias,
-                                                 alpha, beta, vA, vB);
+      dispatch_gemm<1>(pl, lA, lB, M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, bias, alpha, beta, ws, st);
     else
-      gemm_mfma_kernel<2><<<grid, 256, 0, st>>>(M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, bias,
-                                                 alpha, beta, vA, vB);
+      dispatch_gemm<2>(pl, lA, lB, M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, bias, alpha, beta, ws, st);
   } else {
     return AVD_ERR_ARG;
   }
