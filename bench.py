@@ -41,9 +41,30 @@ def parse():
     ap.add_argument("--mode", default="mse", choices=["default", "mse", "infonce", "semi_supervised"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL) for real runs; gloo only to rehearse N>1 with several "
+                         "ranks sharing one GPU")
     ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--probe-dominant", type=int, default=0, metavar="K",
+                    help="after warm-up, replay only the dominant launch K times and exit "
+                         "(run under rocprofv3 --pmc; tools/pmc_traffic.py turns the last K "
+                         "dispatches into the roofline's per-launch HBM traffic)")
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"),
+                    help="PMC traffic table written by tools/pmc_traffic.py")
     return ap.parse_args()
+
+
+def load_traffic(path, key):
+    """Per-launch HBM bytes of ``key`` measured by a separate rocprofv3 --pmc pass (FETCH_SIZE
+    doubled per the gfx950 correction + WRITE_SIZE), or None if that launch was not probed."""
+    try:
+        with open(path) as f:
+            tab = json.load(f)
+    except (OSError, ValueError):
+        return None
+    e = tab.get(key)
+    return None if e is None else e.get("traffic_bytes")
 
 
 def synthetic_pool(n, B, G, L, device, seed):
@@ -100,12 +121,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    local = local % max(torch.cuda.device_count(), 1)   # (rehearsal: ranks may share a GPU)
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
 
     from avdino import ops
     from avdino.engine import Hyper, MultiCentralEngine
@@ -116,12 +141,14 @@ def main():
     act = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     store = ParamStore(multimodal_dino_sd(args.mode, E, D, P), device, seed=0)
 
-    def allreduce_avg(grad):
-        dist.all_reduce(grad)
-        grad.mul_(1.0 / world)
-
+    from avdino import dist as avdist
+    if world > 1:
+        avdist.broadcast_parameters(store)
+    # DDP semantics of the reference's multi-GPU run: rank-0 buffers broadcast before each
+    # forward, one averaged all-reduce of the flat live-gradient arena after backward
     eng = MultiCentralEngine(store, args.mode, E, D, P, Hyper(), act_dtype=act,
-                             grad_hook=allreduce_avg if world > 1 else None, seed=rank)
+                             grad_hook=avdist.grad_allreduce_hook() if world > 1 else None,
+                             buffer_hook=avdist.broadcast_buffers if world > 1 else None, seed=rank)
     pool = synthetic_pool(2, B, G, L, device, 1234 + rank)
 
     # warm-up, timing every instrumented kernel once to find the dominant one
@@ -131,6 +158,19 @@ def main():
     summ = ops.TIMER.summary() if args.warmup else {}
     dominant = max(summ, key=lambda k: summ[k]["ms"]) if summ else None
     ops.TIMER = ops.KernelTimer(only=dominant)
+
+    if args.probe_dominant:
+        eng.step(pool[0])                 # captures the dominant launch (inputs stay live)
+        torch.cuda.synchronize()
+        fn = ops.TIMER.replay
+        for _ in range(args.probe_dominant):
+            fn()
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(json.dumps({"probe": dominant, "replays": args.probe_dominant,
+                              "algorithmic_bytes": int(summ[dominant]["bytes"] / summ[dominant]["calls"])}),
+                  flush=True)
+        return
 
     if dist is not None:
         dist.barrier()
@@ -167,7 +207,8 @@ def main():
             ach, peak, unit = fl / avg_s / 1e12, peak_tf, "TFLOP/s"
         roof = {"bound": "hbm" if hbm_bound else "mfma", "kernel": dominant,
                 "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
-                "traffic": None, "avg_launch_us": round(avg_s * 1e6, 2),
+                "traffic": load_traffic(args.traffic, dominant),
+                "avg_launch_us": round(avg_s * 1e6, 2),
                 "algorithmic_bytes": int(nb), "algorithmic_flops": int(fl),
                 "kernel_share_of_step": round(d["ms"] / (elapsed * 1e3), 4)}
 

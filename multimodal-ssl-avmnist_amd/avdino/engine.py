@@ -224,7 +224,8 @@ class MultiCentralEngine:
     CentralMultiModalEncoder (``--model multi_central --training_mode {default,mse,infonce,
     semi_supervised}``)."""
 
-    def __init__(self, store, mode, E, D, P, hp, act_dtype=F32, grad_hook=None, seed=0):
+    def __init__(self, store, mode, E, D, P, hp, act_dtype=F32, grad_hook=None, seed=0,
+                 buffer_hook=None):
         self.store, self.mode, self.E, self.D, self.P, self.hp = store, mode, E, D, P, hp
         self.act = act_dtype
         # Linear layers: bf16 MFMA in the bf16 mode (like the reference's fp16 autocast),
@@ -242,7 +243,8 @@ class MultiCentralEngine:
             hi, ha = HEAD_NAMES[mode]
             out = 10 if mode == "semi_supervised" else P
             self.heads = (ProjHead(hi, E, out, gemm_mode=self.gm), ProjHead(ha, E, out, gemm_mode=self.gm))
-        self.grad_hook = grad_hook  # e.g. DDP all-reduce of store.grad
+        self.grad_hook = grad_hook      # e.g. DDP all-reduce of store.grad (avdino.dist)
+        self.buffer_hook = buffer_hook  # e.g. rank-0 buffer broadcast before each forward
         self.seed = seed
         self.step_idx = 0
         self.last = {}
@@ -431,6 +433,8 @@ class MultiCentralEngine:
 
     def step(self, batch):
         """One full training step; returns the loss as a device tensor (no host sync)."""
+        if self.buffer_hook is not None:
+            self.buffer_hook(self.store)
         loss = self.forward(batch, training=True)
         self.update_center()
         ema_step(self.store, self.hp.momentum)     # update_teacher: pre-step student

@@ -41,10 +41,13 @@ class KernelTimer:
     def __init__(self, only=None):
         self.only = only
         self.rec = []  # (key, bytes, flops, start_event, end_event)
+        self.replay = None  # last launch closure of the ``only`` key (bench --probe-dominant)
 
     def wrap(self, key, nbytes, flops, fn):
         if self.only is not None and key != self.only:
             return fn()
+        if self.only is not None:
+            self.replay = fn
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
