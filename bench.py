@@ -105,7 +105,7 @@ def cpu_baseline(batch, seconds):
         TP.train_step(model, opt, b)
         n += 1
         el = time.perf_counter() - t0
-        if (n >= 2 and el >= seconds) or n >= 50:
+        if (n >= 2 and el >= seconds) or n >= 400:
             break
     return {"value": round(batch * n / el, 2), "unit": "pairs/s", "cores": torch.get_num_threads(),
             "kind": "port",
