@@ -153,6 +153,57 @@ int avd_gemm(int M, int N, int K, const float* A, long long sam, long long sak,
              const float* bias, float alpha, float beta, int mode, float* ws,
              long long ws_elems, void* stream);
 
+/* ------------------------------------------------------------------ channels-last conv blocks
+ * The training path's conv blocks on NHWC maps ([N][H][W][C]; Cin = 1 maps are the plain
+ * images), on MFMA for both storage types: dt = AVD_BF16 (v_mfma_f32_16x16x32_bf16) or AVD_F32
+ * (v_mfma_f32_16x16x4f32, exact f32 products -- the parity mode).  They replace one
+ * conv -> BatchNorm2d(train) -> ReLU -> max_pool2d(2) block of CentralUnimodalImage /
+ * CentralUnimodalAudio.forward (unimodal.py:127-221) and the 3x3 CNN blocks (dino.py:18-73),
+ * forward and backward.  K in {3, 5}; Cin = 1 or a multiple of 8; Cout a multiple of 8.
+ *
+ * Weights: wk = avd_cl_weight_layout(w [Cout,Cin,K,K] f32) in dt, dgrad=0 for the forward,
+ * dgrad=1 (flipped taps, swapped channels) for the input gradient; avd_cl_weight_elems gives
+ * its element count. */
+int avd_cl_weight_elems(int Cout, int Cin, int K, int dgrad);
+int avd_cl_weight_layout(const float* w, void* wk, int dt, int Cout, int Cin, int K, int dgrad,
+                         void* stream);
+
+/* y = conv2d(x, w) + bias (stride 1, zero padding pad), x [N,H,W,Cin] -> y [N,Ho,Wo,Cout].
+ * stats != NULL: BatchNorm partial (sum, sumsq) of the stored y values, [Cout][G][R][2] with
+ * G = N/B groups (B = samples per BN group = per view) and R = avd_cl_stat_rows(...) rows per
+ * group, for avd_bn_finalize. */
+int avd_cl_stat_rows(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt);
+int avd_cl_conv_fwd(const void* x, const void* wk, const float* bias, void* y, float* stats,
+                    int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
+                    void* stream);
+
+/* dx [N,H,W,Cin] = input gradient of the conv for dy [N,Ho,Wo,Cout]; wk_d = dgrad layout. */
+int avd_cl_conv_dgrad(const void* dy, const void* wk_d, void* dx, int dt, int N, int Cin, int H,
+                      int W, int Cout, int K, int pad, void* stream);
+
+/* dw_parts[c] [Cout][Cin][K][K] f32 = weight gradient over sample chunk c of
+ * avd_cl_wgrad_chunks(...) chunks; reduce with avd_sum_rows (fixed order). */
+int avd_cl_wgrad_chunks(int N, int Cout, int Cin, int K);
+int avd_cl_conv_wgrad(const void* x, const void* dy, int dt, float* dw_parts, int N, int Cin,
+                      int H, int W, int Cout, int K, int pad, void* stream);
+
+/* out = maxpool2(relu(y*scale[g,c] + shift[g,c])) over NHWC y (floor mode, first-max ties):
+ *   mode 0: out NHWC [N,H/2,W/2,C] in dt;  mode 1: global average of that, f32 [N,C];
+ *   mode 2: f32 [N, C*(H/2)*(W/2)] flattened in (c, h, w) order (the encoder Linear input). */
+int avd_cl_bn_relu_pool(const void* y, int dt, const float* scale, const float* shift, void* out,
+                        int mode, int N, int B, int C, int H, int W, void* stream);
+
+/* Backward of the block above, given gout (mode 0: NHWC dt; mode 1: [N,C] f32; mode 2: f32 in
+ * the mode-2 layout).  reduce: parts [C][G][R][2], R = avd_cl_bn_bwd_rows(...), then
+ * avd_bn_bwd_finalize -> coef; apply: dy [N,H,W,C] (dt) = k1*dz + kx*y + k0. */
+int avd_cl_bn_bwd_rows(int B, int C, int H, int W, int dt);
+int avd_cl_bn_bwd_reduce(const void* y, int dt, const void* gout, int mode, const float* scale,
+                         const float* shift, const float* mean, const float* invstd, float* parts,
+                         int N, int B, int C, int H, int W, void* stream);
+int avd_cl_bn_bwd_apply(const void* y, int dt, const void* gout, int mode, const float* scale,
+                        const float* shift, const float* coef, void* dy, int N, int B, int C,
+                        int H, int W, void* stream);
+
 /* out[c] (+)= sum_{r<rows} in[r*ld + c]   (fixed order, f64 accumulation) -- reduces the conv
  * weight-grad partial slabs and gives Linear bias gradients (column sums of dy). */
 int avd_sum_rows(const float* in, int rows, int cols, long long ld, float* out, int accumulate,

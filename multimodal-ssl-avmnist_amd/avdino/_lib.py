@@ -34,6 +34,17 @@ PROTOS = {
     "avd_bn_bwd_apply": [P, I, P, I, I, P, P, P, P, I, I, I, I, I, I, P],
     "avd_gemm": [I, I, I, P, L, L, P, L, L, P, L, P, F, F, I, P, L, P],
     "avd_gemm_ws_elems": [I, I, I, I],
+    "avd_cl_weight_elems": [I, I, I, I],
+    "avd_cl_weight_layout": [P, P, I, I, I, I, I, P],
+    "avd_cl_stat_rows": [I, I, I, I, I, I, I],
+    "avd_cl_conv_fwd": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "avd_cl_conv_dgrad": [P, P, P, I, I, I, I, I, I, I, I, P],
+    "avd_cl_wgrad_chunks": [I, I, I, I],
+    "avd_cl_conv_wgrad": [P, P, I, P, I, I, I, I, I, I, I, P],
+    "avd_cl_bn_relu_pool": [P, I, P, P, P, I, I, I, I, I, I, P],
+    "avd_cl_bn_bwd_rows": [I, I, I, I, I],
+    "avd_cl_bn_bwd_reduce": [P, I, P, I, P, P, P, P, P, I, I, I, I, I, P],
+    "avd_cl_bn_bwd_apply": [P, I, P, I, P, P, P, P, I, I, I, I, I, P],
     "avd_sum_rows": [P, I, I, L, P, I, P],
     "avd_colstats_parts": [I],
     "avd_colstats": [P, I, I, I, P, P],

@@ -48,7 +48,11 @@ class Workspace:
 
 # ============================================================================ conv stacks
 class ConvBranch:
-    """conv -> BN(train, per group) -> ReLU -> maxpool2 stack (+ flatten or GAP), fwd/bwd."""
+    """[conv -> BN(train, per group) -> ReLU -> maxpool2] x L (+ (c,h,w) flatten or GAP) over
+    channels-last maps, forward and backward (CentralUnimodalImage/Audio.forward,
+    unimodal.py:127-221; the 3x3 CNNs, dino.py:18-73).  Same kernels for f32 (parity, f32
+    MFMA) and bf16 (bench) storage; only the final features are f32 [N, F] in the reference's
+    flatten order."""
 
     def __init__(self, stack, act_dtype):
         self.stack = stack
@@ -56,39 +60,39 @@ class ConvBranch:
         self.dims = stack.layer_dims()
 
     def prepare(self, ws, store, tag, need_dgrad):
-        """Kernel weight layouts for this step (weights change every step)."""
+        """MFMA weight layouts for this step (the weights change every step)."""
         wts = []
         for i, (ci, co, k, _p) in enumerate(self.stack.convs):
             w = store[self.stack.conv_keys[i] + ".weight"]
-            mf = 2 if ops.mfma_conv(self.act, ci) else 0
-            wt = ws.get(f"{tag}.wt{i}", ops.conv_weight_layout_elems(co, ci, k, mf),
-                        torch.bfloat16 if mf else F32)
-            ops.conv_weight_layout(w, wt, mf)
+            wk = ws.get(f"{tag}.wk{i}", ops.cl_weight_elems(co, ci, k, 0), self.act)
+            ops.cl_weight_layout(w, wk, 0)
             wd = None
             if need_dgrad and i > 0:
-                md = 3 if ops.mfma_conv(self.act, co) else 1
-                wd = ws.get(f"{tag}.wd{i}", ops.conv_weight_layout_elems(co, ci, k, md),
-                            torch.bfloat16 if md == 3 else F32)
-                ops.conv_weight_layout(w, wd, md)
-            wts.append((wt, wd))
+                wd = ws.get(f"{tag}.wd{i}", ops.cl_weight_elems(co, ci, k, 1), self.act)
+                ops.cl_weight_layout(w, wd, 1)
+            wts.append((wk, wd))
         return wts
 
+    def _tail_mode(self):
+        return 1 if self.stack.gap else 2
+
     def forward(self, ws, store, tag, x, N, G, update_running=True, need_dgrad=False):
-        """x: staged input [N,1,H,W] (act dtype).  Returns (features f32 [N, F], ctx)."""
+        """x: staged input [N,H,W,1] (act dtype).  Returns (features f32 [N, F], ctx)."""
         B = N // G
         wts = self.prepare(ws, store, tag, need_dgrad)
         ctx = {"x": [x], "y": [], "stats": [], "wts": wts, "N": N, "G": G}
         h = x
+        nl = len(self.stack.convs)
         for i, (ci, co, k, pad) in enumerate(self.stack.convs):
             H, Ho, Hp = self.dims[i]
-            T = ops.conv_stat_tiles(Ho, Ho)
-            y = ws.get(f"{tag}.y{i}", N * co * Ho * Ho, self.act)
-            parts = ws.get("stat_parts", co * N * T * 2)
-            ops.conv2d_fwd(h, wts[i][0], store[self.stack.conv_keys[i] + ".bias"], y, parts,
-                           N, ci, H, H, co, k, pad)
+            R = ops.cl_stat_rows(Ho, Ho, B, k, ci, co, self.act)
+            y = ws.get(f"{tag}.y{i}", N * Ho * Ho * co, self.act)
+            parts = ws.get("stat_parts", co * G * R * 2)
+            ops.cl_conv_fwd(h, wts[i][0], store[self.stack.conv_keys[i] + ".bias"], y, parts,
+                            N, B, ci, H, H, co, k, pad)
             st = ws.get(f"{tag}.bn{i}", 4 * G * co).view(4, G * co)
             bk = self.stack.bn_keys[i]
-            ops.bn_finalize(parts, G, B * T, co, B * Ho * Ho, store[bk + ".weight"], store[bk + ".bias"],
+            ops.bn_finalize(parts, G, R, co, B * Ho * Ho, store[bk + ".weight"], store[bk + ".bias"],
                             st[0], st[1], st[2], st[3],
                             store[bk + ".running_mean"] if update_running else None,
                             store[bk + ".running_var"] if update_running else None)
@@ -96,16 +100,14 @@ class ConvBranch:
                 store.buffers[bk + ".num_batches_tracked"] += G
             ctx["y"].append(y)
             ctx["stats"].append(st)
-            last = i == len(self.stack.convs) - 1
-            if last and self.stack.gap:
-                out = ws.get(f"{tag}.feat", N * co, F32)
-                ops.bn_relu_pool(y, st[2], st[3], out, 1, N, B, co, Ho, Ho)
-            elif last:
-                out = ws.get(f"{tag}.feat", N * co * Hp * Hp, F32)
-                ops.bn_relu_pool(y, st[2], st[3], out, 0, N, B, co, Ho, Ho)
+            if i == nl - 1:
+                mode = self._tail_mode()
+                out = ws.get(f"{tag}.feat", N * co * (1 if mode == 1 else Hp * Hp), F32)
             else:
-                out = ws.get(f"{tag}.x{i + 1}", N * co * Hp * Hp, self.act)
-                ops.bn_relu_pool(y, st[2], st[3], out, 0, N, B, co, Ho, Ho)
+                mode = 0
+                out = ws.get(f"{tag}.x{i + 1}", N * Hp * Hp * co, self.act)
+            ops.cl_bn_relu_pool(y, st[2], st[3], out, mode, N, B, co, Ho, Ho)
+            if i < nl - 1:
                 ctx["x"].append(out)
             h = out
         return h.view(N, -1), ctx
@@ -120,24 +122,25 @@ class ConvBranch:
             ci, co, k, pad = self.stack.convs[i]
             H, Ho, Hp = self.dims[i]
             y, st = ctx["y"][i], ctx["stats"][i]
-            pool_mode = 1 if (i == nl - 1 and self.stack.gap) else 0
+            mode = self._tail_mode() if i == nl - 1 else 0
             bk, ck = self.stack.bn_keys[i], self.stack.conv_keys[i]
-            parts = ws.get("bwd_parts", co * N * 2)
-            ops.bn_bwd_reduce(y, gout, pool_mode, st[2], st[3], st[0], st[1], parts, N, B, co, Ho, Ho)
+            R = ops.cl_bn_bwd_rows(B, co, Ho, Ho, self.act)
+            parts = ws.get("bwd_parts", co * G * R * 2)
+            ops.cl_bn_bwd_reduce(y, gout, mode, st[2], st[3], st[0], st[1], parts, N, B, co, Ho, Ho)
             coef = ws.get("bwd_coef", G * co * 3)
-            ops.bn_bwd_finalize(parts, G, B, co, B * Ho * Ho, store[bk + ".weight"], st[0], st[1],
+            ops.bn_bwd_finalize(parts, G, R, co, B * Ho * Ho, store[bk + ".weight"], st[0], st[1],
                                 coef, store.grad_of(bk + ".weight"), store.grad_of(bk + ".bias"),
                                 store.grad_of(ck + ".bias"))
-            dy = ws.get("bwd_dy", N * co * Ho * Ho, self.act)
-            ops.bn_bwd_apply(y, gout, pool_mode, st[2], st[3], coef, dy, N, B, co, Ho, Ho)
+            dy = ws.get("bwd_dy", N * Ho * Ho * co, self.act)
+            ops.cl_bn_bwd_apply(y, gout, mode, st[2], st[3], coef, dy, N, B, co, Ho, Ho)
             x = ctx["x"][i]
-            nch = ops.wgrad_chunks(N, co, ci, k)
+            nch = ops.cl_wgrad_chunks(N, co, ci, k)
             wparts = ws.get("wgrad_parts", nch * co * ci * k * k)
-            ops.conv2d_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
+            ops.cl_conv_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
             ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
             if i > 0:
-                dx = ws.get("bwd_dx", N * ci * H * H, self.act)
-                ops.conv2d_dgrad(dy, ctx["wts"][i][1], dx, N, ci, H, H, co, k, pad)
+                dx = ws.get("bwd_dx", N * H * H * ci, self.act)
+                ops.cl_conv_dgrad(dy, ctx["wts"][i][1], dx, N, ci, H, H, co, k, pad)
                 gout = dx
 
 

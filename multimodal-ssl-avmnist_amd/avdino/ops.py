@@ -42,12 +42,14 @@ class KernelTimer:
         self.only = only
         self.rec = []  # (key, bytes, flops, start_event, end_event)
         self.replay = None  # last launch closure of the ``only`` key (bench --probe-dominant)
+        self.fns = {}       # key -> last launch closure (tools/opbench.py replays them)
 
     def wrap(self, key, nbytes, flops, fn):
         if self.only is not None and key != self.only:
             return fn()
         if self.only is not None:
             self.replay = fn
+        self.fns[key] = (fn, nbytes, flops)
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
@@ -239,6 +241,100 @@ def linear_bwd(dout, x, w, dw, db, dx, rows, dout_ld=None, dout_off=0, x_ld=None
     if dx is not None:
         gemm(rows, In, O, dout, dout_ld, 1, w, In, 1, dx, dx_ld, a_off=dout_off, c_off=dx_off,
              mode=mode)
+
+
+# ---------------------------------------------------------------- channels-last conv blocks
+def cl_weight_elems(Cout, Cin, K, dgrad):
+    return lib.avd_cl_weight_elems(Cout, Cin, K, int(dgrad))
+
+
+def cl_weight_layout(w, wk, dgrad):
+    """w [Cout,Cin,K,K] f32 -> MFMA layout in wk's dtype (forward, or input-grad if dgrad)."""
+    Cout, Cin, K, _ = w.shape
+    _need(w.dtype == torch.float32 and wk.numel() >= cl_weight_elems(Cout, Cin, K, dgrad), "cl wk")
+    call("avd_cl_weight_layout", p(w), p(wk), dtcode(wk), Cout, Cin, K, int(dgrad), stream())
+
+
+def cl_stat_rows(Ho, Wo, B, K, Cin, Cout, dtype):
+    return lib.avd_cl_stat_rows(Ho, Wo, B, K, Cin, Cout, _DT[dtype])
+
+
+def cl_conv_fwd(x, wk, bias, y, stats, N, B, Cin, H, W, Cout, K, pad):
+    """NHWC conv (+bias) with fused BN partial sums: stats [Cout][N/B][R][2]."""
+    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
+    _need(x.numel() == N * H * W * Cin and y.numel() == N * Ho * Wo * Cout, "cl conv sizes")
+    _need(x.dtype == y.dtype == wk.dtype, "cl conv dtypes")
+    _need(wk.numel() >= cl_weight_elems(Cout, Cin, K, 0), "cl conv wk")
+    if stats is not None:
+        R = cl_stat_rows(Ho, Wo, B, K, Cin, Cout, x.dtype)
+        _need(R > 0 and stats.numel() >= Cout * (N // B) * R * 2, "cl conv stats size")
+    nb = x.numel() * x.element_size() + y.numel() * y.element_size()
+    fl = 2 * N * Cout * Ho * Wo * Cin * K * K
+    _timed(f"cl_conv_fwd[{N}x{H}x{W}x{Cin}->{Cout} k{K}p{pad} {x.dtype}]", nb, fl,
+           lambda: call("avd_cl_conv_fwd", p(x), p(wk), p(bias), p(y), p(stats), dtcode(x), N, B,
+                        Cin, H, W, Cout, K, pad, stream()))
+
+
+def cl_conv_dgrad(dy, wk_d, dx, N, Cin, H, W, Cout, K, pad):
+    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
+    _need(dy.numel() == N * Ho * Wo * Cout and dx.numel() == N * H * W * Cin, "cl dgrad sizes")
+    _need(dy.dtype == dx.dtype == wk_d.dtype, "cl dgrad dtypes")
+    _need(wk_d.numel() >= cl_weight_elems(Cout, Cin, K, 1), "cl dgrad wk")
+    nb = (dy.numel() + dx.numel()) * dy.element_size()
+    fl = 2 * N * Cin * H * W * Cout * K * K
+    _timed(f"cl_conv_dgrad[{N}x{Ho}x{Wo}x{Cout}->{Cin} k{K}p{pad} {dy.dtype}]", nb, fl,
+           lambda: call("avd_cl_conv_dgrad", p(dy), p(wk_d), p(dx), dtcode(dy), N, Cin, H, W, Cout,
+                        K, pad, stream()))
+
+
+def cl_wgrad_chunks(N, Cout, Cin, K):
+    return lib.avd_cl_wgrad_chunks(N, Cout, Cin, K)
+
+
+def cl_conv_wgrad(x, dy, parts, N, Cin, H, W, Cout, K, pad):
+    """Per-sample-chunk weight-gradient slabs [chunks][Cout][Cin][K][K] (reduce: sum_rows)."""
+    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
+    _need(x.numel() == N * H * W * Cin and dy.numel() == N * Ho * Wo * Cout, "cl wgrad sizes")
+    _need(x.dtype == dy.dtype, "cl wgrad dtypes")
+    _need(parts.numel() >= cl_wgrad_chunks(N, Cout, Cin, K) * Cout * Cin * K * K, "cl wgrad parts")
+    nb = x.numel() * x.element_size() + dy.numel() * dy.element_size()
+    fl = 2 * dy.numel() * Cin * K * K
+    _timed(f"cl_conv_wgrad[{N}x{H}x{W}x{Cin}->{Cout} k{K}p{pad} {x.dtype}]", nb, fl,
+           lambda: call("avd_cl_conv_wgrad", p(x), p(dy), dtcode(x), p(parts), N, Cin, H, W, Cout,
+                        K, pad, stream()))
+
+
+def cl_bn_relu_pool(y, scale, shift, out, mode, N, B, C, H, W):
+    """mode 0: NHWC pooled (y dtype); 1: GAP f32 [N,C]; 2: f32 (c,h,w)-flattened pooled map."""
+    _need(y.numel() == N * H * W * C, "cl pool y")
+    want = {0: N * (H // 2) * (W // 2) * C, 1: N * C, 2: N * C * (H // 2) * (W // 2)}[mode]
+    _need(out.numel() == want and (out.dtype == y.dtype if mode == 0 else out.dtype == torch.float32),
+          "cl pool out")
+    nb = y.numel() * y.element_size() + out.numel() * out.element_size()
+    _timed(f"cl_bn_relu_pool[{N}x{H}x{W}x{C} m{mode} {y.dtype}]", nb, 0,
+           lambda: call("avd_cl_bn_relu_pool", p(y), dtcode(y), p(scale), p(shift), p(out), mode, N,
+                        B, C, H, W, stream()))
+
+
+def cl_bn_bwd_rows(B, C, H, W, dtype):
+    return lib.avd_cl_bn_bwd_rows(B, C, H, W, _DT[dtype])
+
+
+def cl_bn_bwd_reduce(y, gout, mode, scale, shift, mean, invstd, parts, N, B, C, H, W):
+    R = cl_bn_bwd_rows(B, C, H, W, y.dtype)
+    _need(parts.numel() >= C * (N // B) * R * 2, "cl bwd parts")
+    nb = y.numel() * y.element_size() + gout.numel() * gout.element_size()
+    _timed(f"cl_bn_bwd_reduce[{N}x{H}x{W}x{C} m{mode} {y.dtype}]", nb, 0,
+           lambda: call("avd_cl_bn_bwd_reduce", p(y), dtcode(y), p(gout), mode, p(scale), p(shift),
+                        p(mean), p(invstd), p(parts), N, B, C, H, W, stream()))
+
+
+def cl_bn_bwd_apply(y, gout, mode, scale, shift, coef, dy, N, B, C, H, W):
+    _need(dy.numel() == y.numel() and dy.dtype == y.dtype, "cl bwd dy")
+    nb = 2 * y.numel() * y.element_size() + gout.numel() * gout.element_size()
+    _timed(f"cl_bn_bwd_apply[{N}x{H}x{W}x{C} m{mode} {y.dtype}]", nb, 0,
+           lambda: call("avd_cl_bn_bwd_apply", p(y), dtcode(y), p(gout), mode, p(scale), p(shift),
+                        p(coef), p(dy), N, B, C, H, W, stream()))
 
 
 def sum_rows(x, rows, cols, out, accumulate=0, ld=None, off=0):

@@ -1,0 +1,109 @@
+// C ABI of the channels-last (NHWC) conv-block path (include/avdino.h, "avd_cl_*").
+#include "common.h"
+
+int avd_cl_layout_rows_impl(int O);
+int avd_cl_stat_rows_impl(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt);
+int avd_cl_weight_layout_impl(const float* w, void* wk, int dt, int Cout, int Cin, int K,
+                              int dgrad, hipStream_t st);
+int avd_cl_conv_fwd_impl(const void* x, const void* wk, const float* bias, void* y, float* stats,
+                         int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
+                         hipStream_t st);
+int avd_cl_conv_dgrad_impl(const void* dy, const void* wk_d, void* dx, int dt, int N, int Cin,
+                           int H, int W, int Cout, int K, int pad, hipStream_t st);
+int avd_cl_wgrad_chunks_impl(int N, int Cout, int Cin, int K);
+int avd_cl_conv_wgrad_impl(const void* x, const void* dy, int dt, float* parts, int N, int Cin,
+                           int H, int W, int Cout, int K, int pad, hipStream_t st);
+int avd_cl_bn_relu_pool_impl(const void* y, int dt, const float* scale, const float* shift,
+                             void* out, int mode, int N, int B, int C, int H, int W,
+                             hipStream_t st);
+int avd_cl_bn_bwd_rows_impl(int B, int C, int H, int W, int dt);
+int avd_cl_bn_bwd_reduce_impl(const void* y, int dt, const void* gout, int mode,
+                              const float* scale, const float* shift, const float* mean,
+                              const float* invstd, float* parts, int N, int B, int C, int H,
+                              int W, hipStream_t st);
+int avd_cl_bn_bwd_apply_impl(const void* y, int dt, const void* gout, int mode,
+                             const float* scale, const float* shift, const float* coef, void* dy,
+                             int N, int B, int C, int H, int W, hipStream_t st);
+
+namespace {
+bool dt_ok(int dt) { return dt == AVD_F32 || dt == AVD_BF16; }
+}  // namespace
+
+extern "C" {
+
+int avd_cl_weight_elems(int Cout, int Cin, int K, int dgrad) {
+  const int O = dgrad ? Cin : Cout, C = dgrad ? Cout : Cin;
+  return avd_cl_layout_rows_impl(O) * avd_cdiv(K * K * C, 32) * 32;
+}
+
+int avd_cl_weight_layout(const float* w, void* wk, int dt, int Cout, int Cin, int K, int dgrad,
+                         void* stream) {
+  if (!w || !wk || !dt_ok(dt)) return AVD_ERR_ARG;
+  if (Cout <= 0 || Cin <= 0 || K <= 0) return AVD_ERR_SHAPE;
+  return avd_cl_weight_layout_impl(w, wk, dt, Cout, Cin, K, dgrad, avd_stream(stream));
+}
+
+int avd_cl_stat_rows(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt) {
+  return avd_cl_stat_rows_impl(Ho, Wo, B, K, Cin, Cout, dt);
+}
+
+int avd_cl_conv_fwd(const void* x, const void* wk, const float* bias, void* y, float* stats,
+                    int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
+                    void* stream) {
+  if (!x || !wk || !y || !dt_ok(dt)) return AVD_ERR_ARG;
+  if (N <= 0 || B <= 0 || (K != 3 && K != 5)) return AVD_ERR_SHAPE;
+  return avd_cl_conv_fwd_impl(x, wk, bias, y, stats, dt, N, B, Cin, H, W, Cout, K, pad,
+                              avd_stream(stream));
+}
+
+int avd_cl_conv_dgrad(const void* dy, const void* wk_d, void* dx, int dt, int N, int Cin, int H,
+                      int W, int Cout, int K, int pad, void* stream) {
+  if (!dy || !wk_d || !dx || !dt_ok(dt)) return AVD_ERR_ARG;
+  if (N <= 0 || (K != 3 && K != 5)) return AVD_ERR_SHAPE;
+  return avd_cl_conv_dgrad_impl(dy, wk_d, dx, dt, N, Cin, H, W, Cout, K, pad, avd_stream(stream));
+}
+
+int avd_cl_wgrad_chunks(int N, int Cout, int Cin, int K) {
+  return avd_cl_wgrad_chunks_impl(N, Cout, Cin, K);
+}
+
+int avd_cl_conv_wgrad(const void* x, const void* dy, int dt, float* dw_parts, int N, int Cin,
+                      int H, int W, int Cout, int K, int pad, void* stream) {
+  if (!x || !dy || !dw_parts || !dt_ok(dt)) return AVD_ERR_ARG;
+  if (N <= 0 || (K != 3 && K != 5)) return AVD_ERR_SHAPE;
+  return avd_cl_conv_wgrad_impl(x, dy, dt, dw_parts, N, Cin, H, W, Cout, K, pad,
+                                avd_stream(stream));
+}
+
+int avd_cl_bn_relu_pool(const void* y, int dt, const float* scale, const float* shift, void* out,
+                        int mode, int N, int B, int C, int H, int W, void* stream) {
+  if (!y || !scale || !shift || !out || !dt_ok(dt)) return AVD_ERR_ARG;
+  if (N <= 0 || B <= 0) return AVD_ERR_SHAPE;
+  return avd_cl_bn_relu_pool_impl(y, dt, scale, shift, out, mode, N, B, C, H, W,
+                                  avd_stream(stream));
+}
+
+int avd_cl_bn_bwd_rows(int B, int C, int H, int W, int dt) {
+  return avd_cl_bn_bwd_rows_impl(B, C, H, W, dt);
+}
+
+int avd_cl_bn_bwd_reduce(const void* y, int dt, const void* gout, int mode, const float* scale,
+                         const float* shift, const float* mean, const float* invstd, float* parts,
+                         int N, int B, int C, int H, int W, void* stream) {
+  if (!y || !gout || !scale || !shift || !mean || !invstd || !parts || !dt_ok(dt))
+    return AVD_ERR_ARG;
+  if (N <= 0 || B <= 0) return AVD_ERR_SHAPE;
+  return avd_cl_bn_bwd_reduce_impl(y, dt, gout, mode, scale, shift, mean, invstd, parts, N, B, C,
+                                   H, W, avd_stream(stream));
+}
+
+int avd_cl_bn_bwd_apply(const void* y, int dt, const void* gout, int mode, const float* scale,
+                        const float* shift, const float* coef, void* dy, int N, int B, int C,
+                        int H, int W, void* stream) {
+  if (!y || !gout || !scale || !shift || !coef || !dy || !dt_ok(dt)) return AVD_ERR_ARG;
+  if (N <= 0 || B <= 0) return AVD_ERR_SHAPE;
+  return avd_cl_bn_bwd_apply_impl(y, dt, gout, mode, scale, shift, coef, dy, N, B, C, H, W,
+                                  avd_stream(stream));
+}
+
+}  // extern "C"

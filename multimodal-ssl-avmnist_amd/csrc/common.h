@@ -33,6 +33,17 @@ template <> struct io<bf16> {
 
 constexpr int WAVE = 64;
 
+// Division by a block-uniform divisor through an f32 reciprocal: exact for 0 <= p < 2^22
+// ((p + 0.5)/d sits >= 0.5/d from an integer; the two roundings err by <= (p+0.5)/d * 2^-23).
+// Replaces ~30-instruction integer divisions in index decoding of the conv kernels.
+struct FastDiv {
+  float r;
+  int d;
+  __device__ __forceinline__ explicit FastDiv(int dd) : r(1.0f / (float)dd), d(dd) {}
+  __device__ __forceinline__ int div(int p) const { return (int)(((float)p + 0.5f) * r); }
+  __device__ __forceinline__ int mod(int p) const { return p - div(p) * d; }
+};
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -1,0 +1,449 @@
+// Channels-last (NHWC) conv weight gradient on MFMA (bf16 16x16x32 / f32 16x16x4), the
+// autograd of nn.Conv2d w.r.t. its weight for the CentralNet / CNN encoder convs
+// (unimodal.py:105-221, dino.py:18-73):
+//     dW[co][ci][kh][kw] = sum_{n, oy, ox} dY[n][oy][ox][co] * X[n][oy+kh-p][ox+kw-p][ci]
+// as a GEMM  M = co,  N = (tap, 16-channel ci tile),  K = output pixels.
+//
+// A strip of TR output rows of one sample is staged channels-last in LDS: dY as
+// [pixel][co] and X (+halo) as [pixel][ci].  An MFMA k-group is 8 consecutive output pixels of
+// one row; for bf16 both fragments are read pixel-contiguous straight out of those
+// [pixel][channel] images with ds_read_b64_tr_b16 (4 pixels x 16 channels per read, two reads
+// per fragment), and the tap (kh, kw) is only a row/column offset of the X read -- no shifted
+// copies, no transposing writes.  f32 fragments are single LDS reads.
+// Cin = 1 (first layers): N = taps; bf16 B fragments come from K shifted copies of the input
+// rows (8 consecutive pixels at column offset kw = one aligned 16-byte read).
+// Deterministic: each block owns disjoint weight entries of its sample chunk's partial slab
+// dw_parts[chunk][co][ci][tap] (reduced by avd_sum_rows in fixed order); no atomics.
+#include <algorithm>
+
+#include "common.h"
+
+using namespace avd;
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f4;
+typedef __attribute__((ext_vector_type(4))) unsigned u4;
+typedef __attribute__((ext_vector_type(4))) short s4;
+typedef __attribute__((ext_vector_type(2))) unsigned u2;
+
+// bf16: ~4 blocks per CU in flight (strips are short loops); f32 (parity mode) needs room for
+// one 112-wide strip of 16 f32 channels
+inline size_t lds_cap(int esz) { return esz == 2 ? 40 * 1024 : 64 * 1024; }
+
+// 4 pixels (rows) x 16 channels (columns) transposed: lane i of each 16-lane group gets
+// channel i of the 4 pixels.  Lane 4q+p passes &image[pixel q][channel 4p].
+__device__ __forceinline__ u2 tr4(const bf16* p) {
+  const s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s4*)(reinterpret_cast<uintptr_t>(p)));
+  return __builtin_bit_cast(u2, v);
+}
+__device__ __forceinline__ bf16x8 frag8(u2 lo, u2 hi) {
+  return __builtin_bit_cast(bf16x8, u4{lo.x, lo.y, hi.x, hi.y});
+}
+__device__ __forceinline__ f4 mma(bf16x8 a, bf16x8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f4 mma(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <typename T> struct VecW { static constexpr int V = 16 / sizeof(T); };
+
+// 8 consecutive bf16 starting at element offset o of a dword window w[]
+__device__ __forceinline__ u4 window8(const unsigned (&w)[8], int o) {
+  const int d = o >> 1;
+  if ((o & 1) == 0) return u4{w[d], w[d + 1], w[d + 2], w[d + 3]};
+  return u4{__builtin_amdgcn_alignbyte(w[d + 1], w[d], 2), __builtin_amdgcn_alignbyte(w[d + 2], w[d + 1], 2),
+            __builtin_amdgcn_alignbyte(w[d + 3], w[d + 2], 2), __builtin_amdgcn_alignbyte(w[d + 4], w[d + 3], 2)};
+}
+
+// Stage channel vectors of an NHWC row segment: dst[pixel][CP] <- src, zero outside.
+// npix pixels (c = 0..npix-1 of row iy, column c - off), channels [c0, c0+CP) of C.
+template <typename T>
+__device__ __forceinline__ void stage_rows(const T* __restrict__ src, int n, int H, int W, int C,
+                                           int c0, int row0, int rows, int col_off, int cols,
+                                           int CP, T* dst, int tid) {
+  constexpr int V = VecW<T>::V;
+  const int QV = CP / V;
+  const int tasks = rows * cols * QV;
+  const FastDiv fQV(QV), fC(cols);
+  for (int task = tid; task < tasks; task += 256) {
+    const int pix = fQV.div(task), q = task - pix * QV;
+    const int r = fC.div(pix), c = pix - r * cols;
+    const int iy = row0 + r, ix = c - col_off, ch = c0 + q * V;
+    const bool ok = iy >= 0 && iy < H && ix >= 0 && ix < W && ch < C;
+    const u4 v = *reinterpret_cast<const u4*>(src + (ok ? (((size_t)n * H + iy) * W + ix) * C + ch : 0));
+    *reinterpret_cast<u4*>(dst + (size_t)pix * CP + q * V) = ok ? v : u4{0u, 0u, 0u, 0u};
+  }
+}
+
+// --------------------------------------------------------------------------- Cin >= 8
+template <typename T, int K, int MT, int NW>
+__global__ __launch_bounds__(256) void wgrad_cl_kernel(
+    const T* __restrict__ x, const T* __restrict__ dy, float* __restrict__ parts, int N, int Cin,
+    int H, int W, int Cout, int Ho, int Wo, int pad, int spc, int TR, int Wo8, int CinP, int NTT) {
+  constexpr int KK = K * K;
+  constexpr int CoP = MT * 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int XW = Wo8 + K - 1;
+  T* dys = reinterpret_cast<T*>(smem);                    // [TR*Wo8 + 8][CoP] (+8 zero pixels)
+  T* xs = dys + (size_t)(TR * Wo8 + 8) * CoP;             // [TR+K-1][XW][CinP]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int q4 = r16 >> 2, p4 = r16 & 3;                  // transposed-read lane roles
+  const int co0 = blockIdx.z * CoP;
+  const int chunk = blockIdx.y;
+  const int n0 = chunk * spc, n1 = min(N, n0 + spc);
+  const int CT = CinP / 16;
+  const int QW = Wo8 >> 3;
+  const int ZERO = TR * Wo8;                              // first zero pixel
+
+  int boff[NW], tapv[NW], ctv[NW];
+  bool nv[NW];
+#pragma unroll
+  for (int u = 0; u < NW; ++u) {
+    const int nt = (blockIdx.x * 4 + wave) * NW + u;
+    nv[u] = nt < NTT;
+    const int t = nv[u] ? nt / CT : 0, ct = nv[u] ? nt % CT : 0;
+    tapv[u] = t;
+    ctv[u] = ct;
+    boff[u] = ((t / K) * XW + t % K) * CinP + 16 * ct;
+  }
+  f4 acc[MT][NW];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int u = 0; u < NW; ++u) acc[m][u] = f4{0.f, 0.f, 0.f, 0.f};
+
+  for (int i = tid; i < 8 * CoP; i += 256) dys[(size_t)ZERO * CoP + i] = T(0);
+  for (int n = n0; n < n1; ++n) {
+    for (int y0 = 0; y0 < Ho; y0 += TR) {
+      const int tr = min(TR, Ho - y0);
+      __syncthreads();
+      stage_rows<T>(dy, n, Ho, Wo, Cout, co0, y0, tr, 0, Wo8, CoP, dys, tid);
+      stage_rows<T>(x, n, H, W, Cin, 0, y0 - pad, tr + K - 1, pad, XW, CinP, xs, tid);
+      __syncthreads();
+      if constexpr (sizeof(T) == 2) {
+        const int ng = tr * QW;                          // 8-pixel groups in the strip
+        const FastDiv fQW(QW);
+        for (int s = 0; s < (ng + 3) >> 2; ++s) {
+          const int G = 4 * s + g;
+          const bool gv = G < ng;
+          const int rq = fQW.div(G);
+          const int r = gv ? rq : 0, x0 = gv ? 8 * (G - rq * QW) : 0;
+          const int P0 = gv ? r * Wo8 + x0 : ZERO;
+          bf16x8 a[MT];
+#pragma unroll
+          for (int m = 0; m < MT; ++m) {
+            const bf16* pa = dys + (size_t)(P0 + q4) * CoP + 16 * m + 4 * p4;
+            a[m] = frag8(tr4(pa), tr4(pa + 4 * CoP));
+          }
+          const int xb = (r * XW + x0 + q4) * CinP + 4 * p4;
+#pragma unroll
+          for (int u = 0; u < NW; ++u) {
+            const bf16* pb = xs + xb + boff[u];
+            const bf16x8 b = frag8(tr4(pb), tr4(pb + 4 * CinP));
+#pragma unroll
+            for (int m = 0; m < MT; ++m) acc[m][u] = mma(a[m], b, acc[m][u]);
+          }
+        }
+      } else {
+        const int np = tr * Wo8;
+        const FastDiv fW8(Wo8);
+        for (int s = 0; s < (np + 3) >> 2; ++s) {
+          const int P = 4 * s + g;
+          const bool pv = P < np;
+          const int pr = fW8.div(P);
+          const int r = pv ? pr : 0, xx = pv ? P - pr * Wo8 : 0;
+          const int PA = pv ? P : ZERO;
+          float a[MT];
+#pragma unroll
+          for (int m = 0; m < MT; ++m) a[m] = dys[(size_t)PA * CoP + 16 * m + r16];
+          const int xb = (r * XW + xx) * CinP + r16;
+#pragma unroll
+          for (int u = 0; u < NW; ++u) {
+            const float b = xs[xb + boff[u]];
+#pragma unroll
+            for (int m = 0; m < MT; ++m) acc[m][u] = mma(a[m], b, acc[m][u]);
+          }
+        }
+      }
+    }
+  }
+  // C[m = co][n = ci]: lane holds co = co0 + 16m + 4g + i, ci = 16 ct + r16
+  float* out = parts + (size_t)chunk * Cout * Cin * KK;
+#pragma unroll
+  for (int u = 0; u < NW; ++u) {
+    if (!nv[u]) continue;
+    const int ci = 16 * ctv[u] + r16;
+    if (ci >= Cin) continue;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = co0 + 16 * m + 4 * g + i;
+        if (co < Cout) out[((size_t)co * Cin + ci) * KK + tapv[u]] = acc[m][u][i];
+      }
+  }
+}
+
+// --------------------------------------------------------------------------- Cin == 1
+template <typename T, int K, int MT>
+__global__ __launch_bounds__(256) void wgrad_c1_kernel(
+    const T* __restrict__ x, const T* __restrict__ dy, float* __restrict__ parts, int N, int H,
+    int W, int Cout, int Ho, int Wo, int pad, int spc, int TR, int Wo8) {
+  constexpr int KK = K * K;
+  constexpr int NTN = (KK + 15) / 16;     // tap tiles
+  constexpr int CoP = MT * 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int XR = TR + K - 1;
+  const int XW = sizeof(T) == 2 ? Wo8 : Wo8 + K - 1;      // bf16: K shifted copies of width Wo8
+  T* dys = reinterpret_cast<T*>(smem);                    // [TR*Wo8 + 8][CoP]
+  T* xs = dys + (size_t)(TR * Wo8 + 8) * CoP;             // bf16 [K][XR][Wo8]; f32 [XR][XW]
+  float* red = reinterpret_cast<float*>(smem);            // reused after the loop
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int q4 = r16 >> 2, p4 = r16 & 3;
+  const int chunk = blockIdx.y;
+  const int n0 = chunk * spc, n1 = min(N, n0 + spc);
+  const int QW = Wo8 >> 3;
+  const int ZERO = TR * Wo8;
+
+  int tkh[NTN], tkw[NTN];
+  bool tv[NTN];
+#pragma unroll
+  for (int u = 0; u < NTN; ++u) {
+    const int t = 16 * u + r16;
+    tv[u] = t < KK;
+    tkh[u] = tv[u] ? t / K : 0;
+    tkw[u] = tv[u] ? t % K : 0;
+  }
+  f4 acc[MT][NTN];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int u = 0; u < NTN; ++u) acc[m][u] = f4{0.f, 0.f, 0.f, 0.f};
+
+  for (int i = tid; i < 8 * CoP; i += 256) dys[(size_t)ZERO * CoP + i] = T(0);
+  for (int n = n0; n < n1; ++n) {
+    for (int y0 = 0; y0 < Ho; y0 += TR) {
+      const int tr = min(TR, Ho - y0);
+      const int xr = tr + K - 1;
+      __syncthreads();
+      stage_rows<T>(dy, n, Ho, Wo, Cout, 0, y0, tr, 0, Wo8, CoP, dys, tid);
+      if constexpr (sizeof(T) == 2) {
+        // xs[kw][r][c] = X[y0 - pad + r][c + kw - pad]: one dword window of the input row per
+        // 8-column group, the K shifted copies cut out of it with v_alignbyte
+        const int sh = pad & 1;                       // keeps the window start even
+        const FastDiv fQW(QW);
+        for (int task = tid; task < xr * QW; task += 256) {
+          const int r = fQW.div(task), q = task - r * QW;
+          const int iy = y0 - pad + r, cs = 8 * q - pad - sh;
+          const bool row_ok = iy >= 0 && iy < H;
+          const T* src = x + ((size_t)n * H + (row_ok ? iy : 0)) * W;
+          unsigned w[8];
+          if (!(W & 1)) {
+            const unsigned* s32 = reinterpret_cast<const unsigned*>(src);
+#pragma unroll
+            for (int d = 0; d < 8; ++d) {
+              const int c = cs + 2 * d;                 // W even: both halves in or out together
+              const bool ok = row_ok && c >= 0 && c < W;
+              const unsigned v = s32[ok ? c >> 1 : 0];  // unconditional load, then select
+              w[d] = ok ? v : 0u;
+            }
+          } else {
+#pragma unroll
+            for (int d = 0; d < 8; ++d) {
+              const int c = cs + 2 * d;
+              const unsigned lo = (row_ok && c >= 0 && c < W) ? (unsigned)src[c] : 0u;
+              const unsigned hi = (row_ok && c + 1 >= 0 && c + 1 < W) ? (unsigned)src[c + 1] : 0u;
+              w[d] = lo | (hi << 16);
+            }
+          }
+#pragma unroll
+          for (int kw = 0; kw < K; ++kw)
+            *reinterpret_cast<u4*>(xs + ((size_t)kw * XR + r) * Wo8 + 8 * q) = window8(w, sh + kw);
+        }
+      } else {
+        const FastDiv fXW(XW);
+        for (int task = tid; task < xr * XW; task += 256) {
+          const int r = fXW.div(task), c = task - r * XW;
+          const int iy = y0 - pad + r, ix = c - pad;
+          T v = T(0);
+          if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = x[((size_t)n * H + iy) * W + ix];
+          xs[(size_t)r * XW + c] = v;
+        }
+      }
+      __syncthreads();
+      if constexpr (sizeof(T) == 2) {
+        const int ng = tr * QW;
+        const FastDiv fQW(QW);
+        for (int s = wave; s < (ng + 3) >> 2; s += 4) {   // waves split the k-steps
+          const int G = 4 * s + g;
+          const bool gv = G < ng;
+          const int rq = fQW.div(G);
+          const int r = gv ? rq : 0, x0 = gv ? 8 * (G - rq * QW) : 0;
+          const int P0 = gv ? r * Wo8 + x0 : ZERO;
+          bf16x8 a[MT];
+#pragma unroll
+          for (int m = 0; m < MT; ++m) {
+            const bf16* pa = dys + (size_t)(P0 + q4) * CoP + 16 * m + 4 * p4;
+            a[m] = frag8(tr4(pa), tr4(pa + 4 * CoP));
+          }
+#pragma unroll
+          for (int u = 0; u < NTN; ++u) {
+            u4 v = *reinterpret_cast<const u4*>(xs + ((size_t)tkw[u] * XR + r + tkh[u]) * Wo8 + x0);
+            if (!tv[u]) v = u4{0u, 0u, 0u, 0u};
+            const bf16x8 b = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+            for (int m = 0; m < MT; ++m) acc[m][u] = mma(a[m], b, acc[m][u]);
+          }
+        }
+      } else {
+        const int np = tr * Wo8;
+        const FastDiv fW8(Wo8);
+        for (int s = wave; s < (np + 3) >> 2; s += 4) {
+          const int P = 4 * s + g;
+          const bool pv = P < np;
+          const int pr = fW8.div(P);
+          const int r = pv ? pr : 0, xx = pv ? P - pr * Wo8 : 0;
+          const int PA = pv ? P : ZERO;
+          float a[MT];
+#pragma unroll
+          for (int m = 0; m < MT; ++m) a[m] = dys[(size_t)PA * CoP + 16 * m + r16];
+#pragma unroll
+          for (int u = 0; u < NTN; ++u) {
+            const float b = tv[u] ? xs[(size_t)(r + tkh[u]) * XW + xx + tkw[u]] : 0.f;
+#pragma unroll
+            for (int m = 0; m < MT; ++m) acc[m][u] = mma(a[m], b, acc[m][u]);
+          }
+        }
+      }
+    }
+  }
+  // fixed-order reduction of the 4 waves' k-splits, then the slab write
+  __syncthreads();
+  if (wave > 0) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int u = 0; u < NTN; ++u)
+        *reinterpret_cast<f4*>(red + ((((wave - 1) * MT + m) * NTN + u) * 64 + lane) * 4) = acc[m][u];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float* out = parts + (size_t)chunk * Cout * KK;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int u = 0; u < NTN; ++u) {
+        f4 v = acc[m][u];
+        for (int w = 1; w < 4; ++w)
+          v += *reinterpret_cast<const f4*>(red + ((((w - 1) * MT + m) * NTN + u) * 64 + lane) * 4);
+        const int tap = 16 * u + r16;
+        if (!tv[u]) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int co = 16 * m + 4 * g + i;
+          if (co < Cout) out[(size_t)co * KK + tap] = v[i];
+        }
+      }
+  }
+}
+
+// Rows per strip so the LDS images fit.
+int strip_rows(int Ho, int Wo8, int K, int CoP, int CinP, int esz, bool c1) {
+  int TR = Ho;
+  auto need = [&](int tr) {
+    const size_t dyb = (size_t)(tr * Wo8 + 8) * CoP * esz;
+    size_t xb;
+    if (c1) xb = esz == 2 ? (size_t)K * (tr + K - 1) * Wo8 * esz : (size_t)(tr + K - 1) * (Wo8 + K - 1) * esz;
+    else xb = (size_t)(tr + K - 1) * (Wo8 + K - 1) * CinP * esz;
+    return dyb + xb;
+  };
+  while (TR > 1 && need(TR) > lds_cap(esz)) --TR;
+  return need(TR) <= lds_cap(esz) ? TR : 0;
+}
+
+template <typename T, int K, int MT, int NW>
+int launch_wgrad(const void* x, const void* dy, float* parts, int N, int Cin, int H, int W,
+                 int Cout, int pad, int chunks, hipStream_t st) {
+  const int Ho = H + 2 * pad - K + 1, Wo = W + 2 * pad - K + 1;
+  const int Wo8 = (Wo + 7) & ~7;
+  const int CinP = std::max(16, (Cin + 15) / 16 * 16);
+  const int TR = strip_rows(Ho, Wo8, K, MT * 16, CinP, sizeof(T), false);
+  if (!TR) return AVD_ERR_SHAPE;
+  const size_t lds = (size_t)(TR * Wo8 + 8) * MT * 16 * sizeof(T) +
+                     (size_t)(TR + K - 1) * (Wo8 + K - 1) * CinP * sizeof(T);
+  const int NTT = K * K * (CinP / 16);
+  const int spc = avd_cdiv(N, chunks);
+  dim3 grid(avd_cdiv(NTT, 4 * NW), chunks, avd_cdiv(Cout, MT * 16));
+  wgrad_cl_kernel<T, K, MT, NW><<<grid, 256, lds, st>>>((const T*)x, (const T*)dy, parts, N, Cin, H,
+                                                        W, Cout, Ho, Wo, pad, spc, TR, Wo8, CinP,
+                                                        NTT);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+template <typename T, int K, int MT>
+int launch_wgrad_c1(const void* x, const void* dy, float* parts, int N, int H, int W, int Cout,
+                    int pad, int chunks, hipStream_t st) {
+  const int Ho = H + 2 * pad - K + 1, Wo = W + 2 * pad - K + 1;
+  const int Wo8 = (Wo + 7) & ~7;
+  const int TR = strip_rows(Ho, Wo8, K, MT * 16, 1, sizeof(T), true);
+  if (!TR) return AVD_ERR_SHAPE;
+  size_t lds = (size_t)(TR * Wo8 + 8) * MT * 16 * sizeof(T) +
+               (sizeof(T) == 2 ? (size_t)K * (TR + K - 1) * Wo8 * 2
+                               : (size_t)(TR + K - 1) * (Wo8 + K - 1) * 4);
+  constexpr int NTN = (K * K + 15) / 16;
+  lds = std::max(lds, (size_t)3 * MT * NTN * 64 * 16);   // wave-reduction scratch
+  const int spc = avd_cdiv(N, chunks);
+  dim3 grid(1, chunks, 1);
+  wgrad_c1_kernel<T, K, MT><<<grid, 256, lds, st>>>((const T*)x, (const T*)dy, parts, N, H, W,
+                                                    Cout, Ho, Wo, pad, spc, TR, Wo8);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+template <typename T>
+int dispatch_wgrad(const void* x, const void* dy, float* parts, int N, int Cin, int H, int W,
+                   int Cout, int K, int pad, int chunks, hipStream_t st) {
+  if (Cin == 1) {
+    if (Cout > 64) return AVD_ERR_SHAPE;
+    const int MT = Cout <= 16 ? 1 : Cout <= 32 ? 2 : 4;
+#define AVD_W1(KK, M) \
+    if (K == KK && MT == M) return launch_wgrad_c1<T, KK, M>(x, dy, parts, N, H, W, Cout, pad, chunks, st);
+    AVD_W1(5, 1) AVD_W1(5, 2) AVD_W1(5, 4) AVD_W1(3, 1) AVD_W1(3, 2) AVD_W1(3, 4)
+#undef AVD_W1
+    return AVD_ERR_SHAPE;
+  }
+  const int MT = Cout <= 16 ? 1 : Cout <= 32 ? 2 : 4;
+#define AVD_W(KK, M, NW_) \
+  if (K == KK && MT == M) return launch_wgrad<T, KK, M, NW_>(x, dy, parts, N, Cin, H, W, Cout, pad, chunks, st);
+  AVD_W(5, 1, 8) AVD_W(5, 2, 8) AVD_W(5, 4, 4) AVD_W(3, 1, 8) AVD_W(3, 2, 8) AVD_W(3, 4, 4)
+#undef AVD_W
+  return AVD_ERR_SHAPE;
+}
+
+}  // namespace
+
+// Sample chunks (= partial slabs) of avd_cl_conv_wgrad: >= ~4 blocks per CU in flight while
+// keeping the slabs (chunks * Cout*Cin*K*K f32) small next to the activations.
+int avd_cl_wgrad_chunks_impl(int N, int Cout, int Cin, int K) {
+  const long long per = (long long)Cout * Cin * K * K;
+  long long c = (1ll << 24) / std::max(per, 1ll);
+  c = std::max(128ll, std::min(c, Cin == 1 ? 4096ll : 1024ll));
+  return (int)std::min<long long>(N, c);
+}
+
+int avd_cl_conv_wgrad_impl(const void* x, const void* dy, int dt, float* parts, int N, int Cin,
+                           int H, int W, int Cout, int K, int pad, hipStream_t st) {
+  if (Cin != 1 && Cin % 8) return AVD_ERR_SHAPE;
+  if (Cout % 8) return AVD_ERR_SHAPE;
+  const int chunks = avd_cl_wgrad_chunks_impl(N, Cout, Cin, K);
+  if (dt == AVD_BF16)
+    return dispatch_wgrad<bf16>(x, dy, parts, N, Cin, H, W, Cout, K, pad, chunks, st);
+  return dispatch_wgrad<float>(x, dy, parts, N, Cin, H, W, Cout, K, pad, chunks, st);
+}

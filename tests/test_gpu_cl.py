@@ -1,0 +1,201 @@
+"""Per-kernel parity of the channels-last (NHWC) conv-block path (include/avdino.h avd_cl_*)
+against the float64 numpy oracle, in both storage types:
+  f32  (v_mfma_f32_16x16x4f32, exact f32 products): rel-L2 <= 2e-6 on maps, 1e-5 on reductions
+  bf16 (v_mfma_f32_16x16x32_bf16 on bf16-rounded operands, fp32 accumulate, bf16 stores):
+       rel-L2 <= 5e-3 on stored maps (one bf16 rounding), 1e-5 on f32 reductions of them.
+Shapes cover every conv of the CentralNet image/audio encoders and the 3x3 CNNs, ragged
+tilings, whole-map packing of small maps (NS > 1), and two BN groups."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+from oracle import numpy_oracle as O  # noqa: E402
+
+
+def dev(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    return t.to(dtype) if dtype is not None else t
+
+
+def host(t):
+    return t.detach().float().cpu().numpy().astype(np.float64)
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64).ravel()
+    b = np.asarray(b, np.float64).ravel()
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+def bf(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(torch.bfloat16).float().numpy()
+
+
+def nhwc(a):
+    return np.ascontiguousarray(np.asarray(a).transpose(0, 2, 3, 1))
+
+
+def nchw(a):
+    return np.ascontiguousarray(np.asarray(a).transpose(0, 3, 1, 2))
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from avdino import ops as _ops
+    return _ops
+
+
+DT = {"f32": torch.float32, "bf16": torch.bfloat16}
+TOL = {"f32": 2e-6, "bf16": 5e-3}
+
+CASES = [  # N, Cin, H, Cout, K, pad
+    (3, 1, 28, 32, 5, 2), (2, 1, 112, 8, 5, 2), (2, 8, 56, 16, 5, 2), (2, 16, 28, 32, 5, 2),
+    (4, 32, 14, 64, 5, 2), (8, 32, 14, 64, 5, 0), (2, 1, 28, 32, 3, 1), (4, 32, 14, 64, 3, 1),
+    (8, 64, 7, 128, 3, 1), (2, 128, 14, 256, 3, 1), (2, 8, 20, 8, 5, 2),
+]
+
+
+def _inputs(case, dt, seed):
+    N, Cin, H, Cout, K, pad = case
+    g = np.random.default_rng(seed)
+    x = g.uniform(-1, 1, (N, Cin, H, H))
+    w = g.uniform(-1, 1, (Cout, Cin, K, K)) / np.sqrt(Cin * K * K)
+    b = g.uniform(-0.1, 0.1, Cout).astype(np.float32)
+    if dt == "bf16":
+        x, w = bf(x), bf(w)
+    return x.astype(np.float32), w.astype(np.float32), b
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("case", CASES)
+def test_cl_conv_fwd_stats(ops, case, dt):
+    N, Cin, H, Cout, K, pad = case
+    B = N // 2 if N % 2 == 0 else N
+    G = N // B
+    x, w, b = _inputs(case, dt, hash(case) % 2**32)
+    y_ref, _ = O.conv2d_fwd(x.astype(np.float64), w.astype(np.float64), b.astype(np.float64), pad)
+    Ho = y_ref.shape[2]
+    T = DT[dt]
+    wk = torch.empty(ops.cl_weight_elems(Cout, Cin, K, 0), device="cuda", dtype=T)
+    ops.cl_weight_layout(dev(w), wk, 0)
+    y = torch.empty(N, Ho, Ho, Cout, device="cuda", dtype=T)
+    R = ops.cl_stat_rows(Ho, Ho, B, K, Cin, Cout, T)
+    stats = torch.full((Cout * G * R * 2,), float("nan"), device="cuda")
+    ops.cl_conv_fwd(dev(nhwc(x), T), wk, dev(b), y, stats, N, B, Cin, H, H, Cout, K, pad)
+    yh = nchw(host(y))
+    assert rel(yh, y_ref) < TOL[dt], rel(yh, y_ref)
+    st = host(stats).reshape(Cout, G, R, 2).sum(2)               # per (channel, group)
+    ys = yh.reshape(G, B, Cout, Ho, Ho)                          # statistics of the stored values
+    assert rel(st[..., 0], ys.sum((1, 3, 4)).T) < 1e-5
+    assert rel(st[..., 1], (ys ** 2).sum((1, 3, 4)).T) < 1e-5
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("case", [c for c in CASES if c[1] > 1])
+def test_cl_conv_dgrad(ops, case, dt):
+    N, Cin, H, Cout, K, pad = case
+    x, w, _ = _inputs(case, dt, hash(case) % 2**32 + 1)
+    y_ref, win = O.conv2d_fwd(x.astype(np.float64), w.astype(np.float64), np.zeros(Cout), pad)
+    g = np.random.default_rng(5)
+    dy = g.uniform(-1, 1, y_ref.shape).astype(np.float32)
+    if dt == "bf16":
+        dy = bf(dy)
+    dx_ref, _, _ = O.conv2d_bwd(dy.astype(np.float64), win, w.astype(np.float64), x.shape, pad)
+    T = DT[dt]
+    wd = torch.empty(ops.cl_weight_elems(Cout, Cin, K, 1), device="cuda", dtype=T)
+    ops.cl_weight_layout(dev(w), wd, 1)
+    dx = torch.empty(N, H, H, Cin, device="cuda", dtype=T)
+    ops.cl_conv_dgrad(dev(nhwc(dy), T), wd, dx, N, Cin, H, H, Cout, K, pad)
+    assert rel(nchw(host(dx)), dx_ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("case", CASES + [(5, 8, 112, 16, 5, 2), (3, 32, 10, 64, 5, 0)])
+def test_cl_conv_wgrad(ops, case, dt):
+    N, Cin, H, Cout, K, pad = case
+    x, _, _ = _inputs(case, dt, hash(case) % 2**32 + 2)
+    Ho = H + 2 * pad - K + 1
+    g = np.random.default_rng(6)
+    dy = g.uniform(-1, 1, (N, Cout, Ho, Ho)).astype(np.float32)
+    if dt == "bf16":
+        dy = bf(dy)
+    wz = np.zeros((Cout, Cin, K, K))
+    _, win = O.conv2d_fwd(x.astype(np.float64), wz, np.zeros(Cout), pad)
+    _, dw_ref, _ = O.conv2d_bwd(dy.astype(np.float64), win, wz, x.shape, pad)
+    T = DT[dt]
+    nch = ops.cl_wgrad_chunks(N, Cout, Cin, K)
+    parts = torch.full((nch * Cout * Cin * K * K,), float("nan"), device="cuda")
+    ops.cl_conv_wgrad(dev(nhwc(x), T), dev(nhwc(dy), T), parts, N, Cin, H, H, Cout, K, pad)
+    dw = torch.empty(Cout, Cin, K, K, device="cuda")
+    ops.sum_rows(parts, nch, Cout * Cin * K * K, dw)
+    # operands are exact in both types; only the fp32 accumulation order differs
+    assert rel(host(dw), dw_ref) < 1e-5
+
+
+POOL_CASES = [(112, 8), (56, 16), (28, 32), (14, 64), (10, 64), (7, 128), (28, 8)]
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("HC", POOL_CASES)
+def test_cl_bn_block_fwd_bwd(ops, HC, mode, dt):
+    """BN(train, per group) -> ReLU -> maxpool2 [-> GAP | -> (c,h,w) flatten] forward and the
+    full backward (reduce -> avd_bn_bwd_finalize -> apply), NHWC, incl. odd maps (7x7)."""
+    H, C = HC
+    G, B = 2, 3
+    N = G * B
+    T = DT[dt]
+    g = np.random.default_rng(H * 1000 + C + 7 * mode)
+    y = g.normal(0.3, 1.5, (N, C, H, H))
+    if dt == "bf16":
+        y = bf(y)
+    y = y.astype(np.float32)
+    gamma = (1 + g.uniform(-0.2, 0.2, C)).astype(np.float32)
+    beta = g.uniform(-0.2, 0.2, C).astype(np.float32)
+    z, bnc, stats = O.bn_train_fwd(y.astype(np.float64), gamma.astype(np.float64),
+                                   beta.astype(np.float64), G, (2, 3))
+    r = np.maximum(z, 0)
+    pmap, pc = O.maxpool2_fwd(r)
+    Hp = H // 2
+    out_ref = {0: pmap, 1: pmap.mean((2, 3)), 2: pmap.reshape(N, -1)}[mode]
+    gout = g.uniform(-1, 1, out_ref.shape).astype(np.float32)
+    if mode == 0 and dt == "bf16":
+        gout = bf(gout)
+    if mode == 0:
+        dp = gout.astype(np.float64)
+    elif mode == 1:
+        dp = np.broadcast_to(gout[:, :, None, None] / (Hp * Hp), pmap.shape)
+    else:
+        dp = gout.reshape(pmap.shape).astype(np.float64)
+    dz = O.maxpool2_bwd(dp, pc) * (z > 0)
+    dy_ref, dg_ref, db_ref = O.bn_train_bwd(dz, bnc)
+
+    # stats from the oracle's partials (conv epilogue tested above), finalize on device
+    parts = np.stack([y.astype(np.float64).reshape(G, B, C, -1).transpose(2, 0, 1, 3).sum(-1),
+                      (y.astype(np.float64) ** 2).reshape(G, B, C, -1).transpose(2, 0, 1, 3).sum(-1)], -1)
+    st = torch.empty(4, G * C, device="cuda")
+    ops.bn_finalize(dev(parts.astype(np.float32)), G, B, C, B * H * H, dev(gamma), dev(beta),
+                    st[0], st[1], st[2], st[3])
+    ty = dev(nhwc(y), T)
+    if mode == 0:
+        out = torch.empty(N, Hp, Hp, C, device="cuda", dtype=T)
+    else:
+        out = torch.empty(out_ref.shape, device="cuda")
+    ops.cl_bn_relu_pool(ty, st[2], st[3], out, mode, N, B, C, H, H)
+    oh = nchw(host(out)) if mode == 0 else host(out)
+    assert rel(oh, out_ref) < (4e-3 if (dt == "bf16" and mode == 0) else 1e-5)
+
+    tg = dev(nhwc(gout), T) if mode == 0 else dev(gout)
+    R = ops.cl_bn_bwd_rows(B, C, H, H, T)
+    bparts = torch.full((C * G * R * 2,), float("nan"), device="cuda")
+    ops.cl_bn_bwd_reduce(ty, tg, mode, st[2], st[3], st[0], st[1], bparts, N, B, C, H, H)
+    coef = torch.empty(G * C * 3, device="cuda")
+    dgam, dbet = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    ops.bn_bwd_finalize(bparts, G, R, C, B * H * H, dev(gamma), st[0], st[1], coef, dgam, dbet, None)
+    assert rel(host(dgam), dg_ref) < 1e-5
+    assert rel(host(dbet), db_ref) < 1e-5
+    dy = torch.empty_like(ty)
+    ops.cl_bn_bwd_apply(ty, tg, mode, st[2], st[3], coef, dy, N, B, C, H, H)
+    assert rel(nchw(host(dy)), dy_ref) < (5e-3 if dt == "bf16" else 1e-5)
