@@ -1,10 +1,13 @@
 """Full training-step parity: the HIP engine (fp32) vs the float64 oracle (which is itself
 pinned to the reference by tests/test_oracle_golden.py), from identical parameters and inputs.
 
-Tolerances (fp32 kernels vs float64 truth; the reference's own fp32 CPU path is ~2e-3 off
-the truth on the first audio conv gradients, tests/test_oracle_golden.py):
-  loss 3e-5 abs; outputs / centre rel-L2 1e-5; gradients rel-L2 1e-3 (mathematically-zero
-  gradients -- biases feeding a BatchNorm -- |g| <= 1e-4); EMA'd teacher 1e-6; running stats
+Tolerances (fp32 kernels vs float64 truth):
+  loss 3e-5 abs; outputs / centre rel-L2 1e-5; gradients rel-L2 1e-3, except the audio-encoder
+  conv/BN tensors, whose bound is 1.5x the REFERENCE's own fp32-vs-float64 error on the same
+  tensors (read from the committed golden fixtures at test time: the reference's fp32 run misses
+  its float64 run by up to 5.7e-3 there -- max-pool argmax near-ties in the deeper audio layers
+  relocate gradient, tests/golden/mm_mse_small*.npz); median gradient error 1e-4
+  (mathematically-zero gradients -- biases feeding a BatchNorm -- |g| <= 1e-4); EMA'd teacher 1e-6; running stats
   1e-5; post-Adam parameters 1e-5 (zero-gradient biases excluded: their Adam step is the sign
   of rounding noise, in the reference too); free-running loss curve: 3e-5 on step 1, 5e-4
   over 4 steps (Adam turns rounding noise on near-zero gradients into +-lr steps; the
@@ -56,6 +59,35 @@ def zero_grad_keys(grads):
     return {k for k, g in grads.items() if np.linalg.norm(g) < 1e-9}
 
 
+def _ref_fp32_audio_err():
+    """Worst rel-L2 error of the reference's own fp32 run vs its float64 run over the
+    audio-encoder gradients of the committed golden step (the fp32 chaos floor)."""
+    import os
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    f32, f64 = np.load(os.path.join(d, "mm_mse_small.npz")), np.load(os.path.join(d, "mm_mse_small_f64.npz"))
+    worst = 0.0
+    for k in f64.files:
+        if k.startswith("grad/student.audio_encoder") and "@" not in k:
+            b = f64[k].ravel()
+            if np.linalg.norm(b) > 1e-9:
+                worst = max(worst, rel(f32[k], b))
+    return worst
+
+
+AUDIO_TOL = max(1e-3, 1.5 * _ref_fp32_audio_err())
+
+
+def check_grads(errs):
+    """errs: {key: rel-L2}.  Audio-encoder tensors within the reference's fp32 floor, the rest
+    within 1e-3, and the median tight."""
+    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:5]
+    print("worst grad rel errors:", worst, "audio bound", AUDIO_TOL)
+    for k, e in errs.items():
+        bound = AUDIO_TOL if k.startswith("student.audio_encoder") else 1e-3
+        assert e < bound, (k, e, bound)
+    assert np.median(list(errs.values())) < 1e-4, np.median(list(errs.values()))
+
+
 @pytest.mark.parametrize("mode", ["mse", "default", "infonce", "semi_supervised"])
 def test_step_matches_oracle(mode):
     from avdino.engine import adam_step, ema_step
@@ -82,9 +114,7 @@ def test_step_matches_oracle(mode):
             assert np.linalg.norm(g) <= 1e-4, (k, np.linalg.norm(g))
         else:
             errs[k] = rel(g, ref["grads"][k])
-    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:5]
-    print("worst grad rel errors:", worst)
-    assert worst[0][1] < 1e-3, worst
+    check_grads(errs)
     new = ref["state"]
     for k in store.t_offs:
         assert rel(host(store[k]), new[k]) < 1e-6, k
@@ -153,9 +183,8 @@ def test_full_dims_step_matches_oracle():
     eng.update_center()
     eng.backward()
     zero = zero_grad_keys(ref["grads"])
-    errs = sorted(((rel(host(store.grad_of(k)), ref["grads"][k]), k) for k in store.live_keys
-                   if k not in zero), reverse=True)
-    assert errs[0][0] < 1e-3, errs[:5]
+    check_grads({k: rel(host(store.grad_of(k)), ref["grads"][k]) for k in store.live_keys
+                 if k not in zero})
 
 
 def test_bf16_step_close_to_oracle():
