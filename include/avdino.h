@@ -262,14 +262,26 @@ int avd_l2norm_fwd(const float* x, float* y, float* norms, int rows, int P, void
 int avd_l2norm_bwd(const float* y, const float* norms, const float* dy, float* dx, int rows,
                    int P, void* stream);
 
-/* Softmax cross-entropy over rows of logits [R, C] with integer targets (F.cross_entropy):
- * loss_parts [R] (unnormalised per-row -log p_target), dlogits [R,C] = (softmax - onehot)*gscale.
- * mask_diag != 0 excludes column r == (row index + diag_offset) (NT-Xent self-similarity,
- * multimodal_simclr.py:79-81).  col_major != 0 reads logits transposed (logits^T rows). */
+/* Softmax cross-entropy over rows of logits [R, C] (F.cross_entropy, dino.py:1001-1025 /
+ * 1091-1128, multimodal_simclr.py:74-89): loss_parts [R] (unnormalised per-row -log p_target),
+ * dlogits [R,C] = (softmax - onehot)*gscale (added to dlogits when accumulate != 0).
+ * Targets: target_mode 0 = targets[r] (int64); 1 = r + tgt_off (InfoNCE diagonal, tgt_off =
+ * this shard's first global row when the columns are all-gathered negatives); 2 = (r + R/2) % R
+ * (NT-Xent positives over a local [2B] batch).  mask_off >= 0 excludes column r + mask_off
+ * (NT-Xent self-similarity, multimodal_simclr.py:79-81); < 0 masks nothing.  col_major != 0
+ * reads logits transposed (logits^T rows). */
 int avd_softmax_xent(const float* logits, long long ld, int R, int C, const int64_t* targets,
-                     int target_mode, int col_major, int mask_diag, float gscale,
+                     int target_mode, int tgt_off, int col_major, int mask_off, float gscale,
                      float* loss_parts, float* dlogits, long long ldd, int accumulate,
                      void* stream);
+
+/* Cosine-consistency term of the unimodal DINO loss (UniModalDINOLightning.
+ * _cosine_consistency_loss, dino.py:1575-1594) over view-major embeddings emb [V*B, D]:
+ * loss_parts [B] = alpha * per-sample share of mean_{i<j} mean_b (1 - n_i.n_j)^2 with
+ * n = F.normalize(emb); demb [V*B, D] += alpha * d loss / d emb.  Either output may be NULL
+ * (not both).  2 <= V <= 32. */
+int avd_cosine_consistency(const float* emb, int V, int B, int D, float alpha, float* loss_parts,
+                           float* demb, void* stream);
 
 /* ------------------------------------------------------------------ input staging */
 
@@ -290,6 +302,11 @@ int avd_ema(float* teacher, const float* student, long long n, float m, void* st
  * dino.py:953-962) over flat arenas p/g/m/v of n floats; bc1 = 1-b1^t, bc2 = 1-b2^t. */
 int avd_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float b1,
              float b2, float eps, float wd, float bc1, float bc2, void* stream);
+
+/* torch.optim.AdamW step (decoupled weight decay: p *= 1 - lr*wd, then Adam without wd) --
+ * the optimiser of the epoch-end linear probe (on_train_epoch_end, dino.py:898, 1678). */
+int avd_adamw(float* p, const float* g, float* m, float* v, long long n, float lr, float b1,
+              float b2, float eps, float wd, float bc1, float bc2, void* stream);
 
 /* out = sum(in[0..n)) in fixed order (loss reduction); out is one float. */
 int avd_sum(const float* in, int n, float scale, float* out, void* stream);

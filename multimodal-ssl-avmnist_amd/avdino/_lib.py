@@ -56,9 +56,11 @@ PROTOS = {
     "avd_mse_loss": [P, P, I, I, P, P, P, P],
     "avd_l2norm_fwd": [P, P, P, I, I, P],
     "avd_l2norm_bwd": [P, P, P, P, I, I, P],
-    "avd_softmax_xent": [P, L, I, I, P, I, I, I, F, P, P, L, I, P],
+    "avd_softmax_xent": [P, L, I, I, P, I, I, I, I, F, P, P, L, I, P],
+    "avd_cosine_consistency": [P, I, I, I, F, P, P, P],
     "avd_ema": [P, P, L, F, P],
     "avd_adam": [P, P, P, P, L, F, F, F, F, F, F, F, P],
+    "avd_adamw": [P, P, P, P, L, F, F, F, F, F, F, F, P],
     "avd_sum": [P, I, F, P, P],
     "avd_stage_views": [P, I, P, I, P, I, I, P, I, P],
 }

@@ -23,7 +23,7 @@ import torch
 
 from . import ops
 from .spec import (CENTRAL_AUDIO_CONVS, CENTRAL_IMAGE_CONVS, CNN3_AUDIO_CONVS, CNN3_IMAGE_CONVS,
-                   HEAD_NAMES, PROJ_HIDDEN, central_stack, cnn3_stack)
+                   HEAD_NAMES, PROJ_HIDDEN, UNI_ALIASES, UNI_ENCODERS, central_stack, cnn3_stack)
 
 F32 = torch.float32
 
@@ -463,3 +463,141 @@ class MultiCentralEngine:
         s = c["s_proj"].view(V, B, P)
         t = c["t_proj"].view(G, B, P) - self.store["center"].view(1, 1, P)
         return s, t
+
+
+# ============================================================================ unimodal DINO
+class UniEncoder:
+    """An UNIMODAL_MODEL_MAP encoder (run_dino.py:542-550) on channels-last maps: conv stack
+    (ConvBranch) then its Linear chain -- ImageEncoder: GAP -> Linear(128,512) -> Linear(512,D)
+    (dino.py:483-499); SpectrogramEncoder: GAP -> Linear(256,D) (502-513);
+    SpectrogramEncoderCentral: CentralUnimodalAudio flatten -> Linear(3136,D) (515-523)."""
+
+    def __init__(self, kind, prefix, act_dtype, gemm_mode):
+        modality, stack, lins, _sd = UNI_ENCODERS[UNI_ALIASES.get(kind, kind)]
+        self.modality = modality
+        self.hw = 28 if modality == "image" else 112
+        self.branch = ConvBranch(stack(prefix), act_dtype)
+        self.lins = [f"{prefix}.{k}" for k in lins]
+        self.gm = gemm_mode
+
+    def forward(self, ws, store, tag, x, N, G, need_dgrad):
+        feat, ctx = self.branch.forward(ws, store, tag, x, N, G, True, need_dgrad)
+        acts = [feat]
+        h = feat
+        for i, k in enumerate(self.lins):
+            w = store[k + ".weight"]
+            out = ws.get(f"{tag}.lin{i}", N * w.shape[0])
+            ops.linear_fwd(h, w, store[k + ".bias"], out, N, mode=self.gm)
+            acts.append(out)
+            h = out
+        return h.view(N, -1), (ctx, acts)
+
+    def backward(self, ws, store, ctx, dout):
+        bctx, acts = ctx
+        N = bctx["N"]
+        g = dout
+        for i in reversed(range(len(self.lins))):
+            k = self.lins[i]
+            w = store[k + ".weight"]
+            dx = ws.get(f"uni.dlin{i}", N * w.shape[1])
+            ops.linear_bwd(g, acts[i], w, store.grad_of(k + ".weight"), store.grad_of(k + ".bias"),
+                           dx, N, mode=self.gm)
+            g = dx
+        self.branch.backward(ws, store, bctx, g)
+
+
+class UniModalEngine:
+    """Training step of UniModalDINO + UniModalDINOLightning (dino.py:1257-1398, 1575-1668):
+    student over G global + L local views of one modality (one launch per layer, BN per view),
+    teacher over the global views (train-mode BN, no grad), projection heads, the unimodal DINO
+    loss (teacher centred by ``center`` AND by its per-view batch mean, dino.py:1613-1614), the
+    cosine-consistency term over the student embeddings when cosine_loss_alpha > 0, centre EMA,
+    teacher EMA (before backward, dino.py:1661), backward, Adam with L2 weight decay."""
+
+    def __init__(self, store, kind, D, P, hp, act_dtype=F32, cos_alpha=0.0, grad_hook=None,
+                 buffer_hook=None, seed=0):
+        self.store, self.D, self.P, self.hp = store, D, P, hp
+        self.kind = UNI_ALIASES.get(kind, kind)
+        self.act = act_dtype
+        self.gm = ops.GEMM_BF16_MFMA if act_dtype == torch.bfloat16 else ops.GEMM_F32_MFMA
+        self.cos_alpha = float(cos_alpha)
+        self.ws = Workspace(store.device)
+        self.enc = UniEncoder(self.kind, "student", act_dtype, self.gm)
+        self.t_enc = UniEncoder(self.kind, "teacher", act_dtype, self.gm)
+        self.modality = self.enc.modality
+        self.sproj = ProjHead("student_projection", D, P, gemm_mode=self.gm)
+        self.tproj = ProjHead("teacher_projection", D, P, gemm_mode=self.gm)
+        self.grad_hook, self.buffer_hook = grad_hook, buffer_hook
+        self.seed, self.step_idx = seed, 0
+        self.last = {}
+
+    def stage(self, batch):
+        key = "img" if self.modality == "image" else "aud"
+        g = batch["g_" + key]
+        l = batch.get("l_" + key)
+        B, G = g.shape[:2]
+        L = 0 if l is None else l.shape[1]
+        HW = self.enc.hw * self.enc.hw
+        x = self.ws.get("in.x", (G + L) * B * HW, self.act)
+        ops.stage_views(g.contiguous(), G, l.contiguous() if L else None, L, None, B, HW, x)
+        return x, B, G, L
+
+    def forward(self, batch, training=True):
+        hp, ws, st, D, P = self.hp, self.ws, self.store, self.D, self.P
+        x, B, G, L = self.stage(batch)
+        V = G + L
+        HW = self.enc.hw * self.enc.hw
+        base = (self.seed * 1000003 + self.step_idx * 16) & 0xFFFFFFFFFFFF
+        emb, sctx = self.enc.forward(ws, st, "s", x, V * B, V, need_dgrad=training)
+        temb, _ = self.t_enc.forward(ws, st, "t", x[:G * B * HW], G * B, G, need_dgrad=False)
+        s_proj = ws.get("s_proj", V * B * P)
+        spc = self.sproj.forward(ws, st, "sp", emb, V * B, s_proj, hp.dropout, base + 3)
+        t_proj = ws.get("t_proj", G * B * P)
+        self.tproj.forward(ws, st, "tp", temb, G * B, t_proj, 0.0, 0)
+        cos = self.cos_alpha > 0 and V >= 2
+        loss_parts = ws.get("loss_parts", V * B + (B if cos else 0))
+        ds = ws.get("ds", V * B * P)
+        center_new = ws.get("center_new", P)
+        work = ws.get("dino_work", (B + G * B) * P)
+        ops.dino_loss(s_proj, t_proj, st["center"], V, G, B, P, hp.tau_s, hp.tau_t,
+                      hp.center_momentum, True, loss_parts[:V * B], ds, center_new, work)
+        if cos:
+            ops.cosine_consistency(emb, V, B, D, self.cos_alpha, loss_parts[V * B:], None)
+        loss = ws.get("loss", 1)
+        ops.sum_to(loss_parts, loss_parts.numel(), 1.0, loss)
+        self.last = dict(B=B, G=G, L=L, V=V, emb=emb, sctx=sctx, spc=spc, ds=ds, cos=cos,
+                         center_new=center_new, s_proj=s_proj, t_proj=t_proj, loss=loss)
+        return loss
+
+    def update_center(self):
+        self.store["center"].copy_(self.last["center_new"].view(1, -1))
+
+    def backward(self):
+        ws, st, c = self.ws, self.store, self.last
+        B, V, D = c["B"], c["V"], self.D
+        demb = ws.get("demb", V * B * D)
+        self.sproj.backward(ws, st, c["spc"], c["ds"], demb)
+        if c["cos"]:
+            ops.cosine_consistency(c["emb"], V, B, D, self.cos_alpha, None, demb)
+        self.enc.backward(ws, st, c["sctx"], demb)
+
+    def step(self, batch):
+        if self.buffer_hook is not None:
+            self.buffer_hook(self.store)
+        loss = self.forward(batch, training=True)
+        self.update_center()
+        ema_step(self.store, self.hp.momentum)
+        self.backward()
+        if self.grad_hook is not None:
+            self.grad_hook(self.store.grad)
+        adam_step(self.store, self.hp)
+        self.step_idx += 1
+        return loss
+
+    def outputs(self):
+        """(s_out [V,B,P], t_out [G,B,P] centred with the pre-update centre, embeddings [V,B,D])
+        as UniModalDINO.forward returns them (dino.py:1392-1398).  Call before update_center()."""
+        c = self.last
+        B, V, G, P = c["B"], c["V"], c["G"], self.P
+        return (c["s_proj"].view(V, B, P), c["t_proj"].view(G, B, P) - self.store["center"].view(1, 1, P),
+                c["emb"].view(V, B, -1))

@@ -22,9 +22,9 @@ import math
 import torch
 
 from . import ops
-from .engine import Hyper, MultiCentralEngine, adam_step, ema_step
+from .engine import Hyper, MultiCentralEngine, UniModalEngine, adam_step, ema_step
 from .params import ParamStore
-from .spec import HEAD_NAMES, multimodal_dino_sd
+from .spec import HEAD_NAMES, multimodal_dino_sd, unimodal_dino_sd
 
 _DT = {"bf16": torch.bfloat16, "16-mixed": torch.bfloat16, "bf16-mixed": torch.bfloat16,
        "32": torch.float32, "fp32": torch.float32, "f32": torch.float32}
@@ -413,3 +413,164 @@ MULTIMODAL_WRAPPERS = {
 }
 
 MODEL_MAP = {"multi_central": CentralMultiModalEncoder}
+
+
+# ============================================================================ unimodal DINO
+class BaseUniModalEncoder:
+    """models/dino.py:471-480 -- descriptor base (output_dim, modality)."""
+
+    kind = None
+    modality = None
+
+    def __init__(self, output_dim=256):
+        self.output_dim = output_dim
+
+
+class ImageEncoder(BaseUniModalEncoder):
+    """image_encoder(512) 3x3 CNN 1->32->64->128, GAP, Linear(128,512), projection
+    Linear(512, output_dim) (models/dino.py:18-42, 483-499)."""
+    kind, modality = "image_simple", "image"
+
+
+class SpectrogramEncoder(BaseUniModalEncoder):
+    """audio_encoder(output_dim) 3x3 CNN 1->32->64->128->256, GAP, Linear(256, output_dim)
+    (models/dino.py:44-73, 502-513)."""
+    kind, modality = "spectrogram_simple", "audio"
+
+
+class SpectrogramEncoderCentral(SpectrogramEncoder):
+    """CentralUnimodalAudio + Linear(3136, output_dim) (models/dino.py:515-523)."""
+    kind = "spectrogram_central"
+
+
+class UniModalDINO:
+    """Student/teacher unimodal DINO (models/dino.py:1257-1398) on the HIP engine."""
+
+    def __init__(self, encoder_class=ImageEncoder, encoder_kwargs=None, output_dim=256,
+                 projection_dim=128, momentum=0.996, center_momentum=0.9, dropout=0.3,
+                 device=None, precision="bf16", seed=0, cosine_loss_alpha=0.0):
+        encoder_kwargs = dict(encoder_kwargs or {})
+        encoder_kwargs["output_dim"] = output_dim
+        enc = encoder_class(**encoder_kwargs)
+        if getattr(enc, "kind", None) is None:
+            raise NotImplementedError(
+                f"{encoder_class.__name__}: the MI355X engine runs ImageEncoder, SpectrogramEncoder "
+                f"and SpectrogramEncoderCentral")
+        self.student_spec = enc
+        self.projection_dim, self.output_dim = projection_dim, output_dim
+        self.momentum, self.center_momentum, self.dropout = momentum, center_momentum, dropout
+        self.device = _device(device)
+        self.store = ParamStore(unimodal_dino_sd(enc.kind, output_dim, projection_dim), self.device,
+                                seed=seed)
+        self.hp = Hyper(momentum=momentum, center_momentum=center_momentum, dropout=dropout)
+        self.engine = None
+        if self.device.type == "cuda":
+            self.engine = UniModalEngine(self.store, enc.kind, output_dim, projection_dim, self.hp,
+                                         act_dtype=_DT[precision], cos_alpha=cosine_loss_alpha,
+                                         seed=seed)
+        self.training = True
+
+    train, eval = MultiModalDINO.train, MultiModalDINO.eval
+    state_dict, load_state_dict = MultiModalDINO.state_dict, MultiModalDINO.load_state_dict
+    named_parameters, parameters = MultiModalDINO.named_parameters, MultiModalDINO.parameters
+    center = MultiModalDINO.center
+    _need_engine = MultiModalDINO._need_engine
+    update_teacher = MultiModalDINO.update_teacher
+    update_center = MultiModalDINO.update_center
+
+    def forward(self, batch):
+        """batch = (global_images, global_audios, local_images, local_audios) -> (student_outputs
+        [G+L,B,P], teacher_outputs [G,B,P] centred, embeddings [G+L,B,D]); updates the centre."""
+        eng = self._need_engine()
+        eng.forward({k: v.to(self.device) for k, v in MultiModalDINO._views_dict(batch).items()},
+                    training=False)
+        s, t, e = eng.outputs()
+        eng.update_center()
+        return s.clone(), t.clone(), e.clone()
+
+    __call__ = forward
+
+
+class _UniCosineLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, emb):
+        V, B, D = emb.shape
+        e = emb.detach().float().contiguous()
+        parts = torch.empty(B, device=emb.device)
+        ops.cosine_consistency(e, V, B, D, 1.0, parts, None)
+        d = torch.zeros(V * B * D, device=emb.device)
+        ops.cosine_consistency(e, V, B, D, 1.0, None, d)
+        loss = torch.empty(1, device=emb.device)
+        ops.sum_to(parts, B, 1.0, loss)
+        ctx.save_for_backward(d.view(V, B, D))
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        (d,) = ctx.saved_tensors
+        return d * g
+
+
+class UniModalDINOLightning(MultiModalDINOLightning):
+    """models/dino.py:1490-1693: unimodal DINO loss (teacher centred per view) + optional
+    cosine-consistency term (cosine_loss_alpha, default 0.3), EMA before backward, Adam(L2)."""
+
+    model_class = UniModalDINO
+
+    def __init__(self, data_dir="data/avmnist", dino_model=None, encoder_class=ImageEncoder,
+                 encoder_kwargs=None, projection_dim=128, output_dim=256, momentum=0.996,
+                 center_momentum=0.9, student_temperature=0.1, teacher_temperature=0.04,
+                 learning_rate=0.0001, use_mixed_precision=True, weight_decay=1e-6,
+                 cosine_loss_alpha=0.3, dropout=0.3, num_epochs=10, data_augmentation="burst_noise",
+                 use_original_model=True, device=None, precision=None, seed=0):
+        self.hparams = dict(data_dir=data_dir, encoder_class=encoder_class.__name__,
+                            encoder_kwargs=encoder_kwargs, projection_dim=projection_dim,
+                            output_dim=output_dim, momentum=momentum, center_momentum=center_momentum,
+                            student_temperature=student_temperature,
+                            teacher_temperature=teacher_temperature, learning_rate=learning_rate,
+                            use_mixed_precision=use_mixed_precision, weight_decay=weight_decay,
+                            cosine_loss_alpha=cosine_loss_alpha, dropout=dropout,
+                            num_epochs=num_epochs, data_augmentation=data_augmentation)
+        if not use_original_model:
+            raise NotImplementedError("UniModalDINOV2 is not on the MI355X hot path")
+        self.learning_rate, self.num_epochs = learning_rate, num_epochs
+        self.student_temperature, self.teacher_temperature = student_temperature, teacher_temperature
+        self.weight_decay, self.cosine_loss_alpha = weight_decay, cosine_loss_alpha
+        self.precision = precision or ("bf16" if use_mixed_precision else "32")
+        if dino_model is None:
+            dino_model = UniModalDINO(encoder_class=encoder_class, encoder_kwargs=encoder_kwargs,
+                                      output_dim=output_dim, projection_dim=projection_dim,
+                                      momentum=momentum, center_momentum=center_momentum,
+                                      dropout=dropout, device=device, precision=self.precision,
+                                      seed=seed, cosine_loss_alpha=cosine_loss_alpha)
+        self.model = dino_model
+        hp = self.model.hp
+        hp.tau_s, hp.tau_t = student_temperature, teacher_temperature
+        hp.lr, hp.wd = learning_rate, weight_decay
+        self.logged = {}
+        self._optim = None
+
+    def dino_loss(self, student_outputs, teacher_outputs):
+        """dino.py:1596-1635 (teacher additionally centred by its per-view batch mean)."""
+        return _DinoLossFn.apply(student_outputs, teacher_outputs, self.student_temperature,
+                                 self.teacher_temperature, True)
+
+    def _cosine_consistency_loss(self, embeddings):
+        """dino.py:1575-1594."""
+        return _UniCosineLossFn.apply(embeddings)
+
+    def _batch_dict(self, batch):
+        return MultiModalDINO._views_dict(batch)
+
+    def training_step(self, batch, batch_idx):
+        eng = self.model._need_engine()
+        b = {k: v.to(self.model.device, non_blocking=True) for k, v in self._batch_dict(batch).items()}
+        loss = eng.forward(b, training=True)
+        eng.update_center()
+        self.model.update_teacher()
+        self.log("train_loss", loss)
+        return loss
+
+
+UNIMODAL_MODEL_MAP = {"image_simple": ImageEncoder, "spectrogram_simple": SpectrogramEncoder,
+                      "spectrogram_central": SpectrogramEncoderCentral}

@@ -389,9 +389,19 @@ def l2norm_bwd(y, norms, dy, dx, rows, P):
 
 
 def softmax_xent(logits, ld, R, C, targets, target_mode, col_major, mask_diag, gscale, loss_parts,
-                 dlogits, ldd, accumulate):
-    call("avd_softmax_xent", p(logits), ld, R, C, p(targets), target_mode, int(col_major),
-         int(mask_diag), gscale, p(loss_parts), p(dlogits), ldd, int(accumulate), stream())
+                 dlogits, ldd, accumulate, tgt_off=0, mask_off=None):
+    """mask_diag masks column r (+ mask_off when given); tgt_off shifts target_mode 1."""
+    if mask_off is None:
+        mask_off = 0 if mask_diag else -1
+    call("avd_softmax_xent", p(logits), ld, R, C, p(targets), target_mode, int(tgt_off),
+         int(col_major), int(mask_off), gscale, p(loss_parts), p(dlogits), ldd, int(accumulate),
+         stream())
+
+
+def cosine_consistency(emb, V, B, D, alpha, loss_parts, demb):
+    _need(emb.numel() >= V * B * D and (demb is None or demb.numel() >= V * B * D)
+          and (loss_parts is None or loss_parts.numel() >= B), "cosine consistency shapes")
+    call("avd_cosine_consistency", p(emb), V, B, D, alpha, p(loss_parts), p(demb), stream())
 
 
 # ---------------------------------------------------------------- optimiser / misc
@@ -401,6 +411,10 @@ def ema(teacher, student, n, m):
 
 def adam(p_, g, m, v, n, lr, b1, b2, eps, wd, bc1, bc2):
     call("avd_adam", p(p_), p(g), p(m), p(v), n, lr, b1, b2, eps, wd, bc1, bc2, stream())
+
+
+def adamw(p_, g, m, v, n, lr, b1, b2, eps, wd, bc1, bc2):
+    call("avd_adamw", p(p_), p(g), p(m), p(v), n, lr, b1, b2, eps, wd, bc1, bc2, stream())
 
 
 def sum_to(x, n, scale, out):

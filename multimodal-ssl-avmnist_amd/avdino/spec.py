@@ -145,6 +145,38 @@ def unimodal_image_dino_sd(D, P):
     return sd
 
 
+def spectrogram_central_sd(sd, prefix, out_dim):
+    _central_lenet(sd, f"{prefix}.encoder.0", CENTRAL_AUDIO_CONVS, 64 * 7 * 7)
+    _dense(sd, f"{prefix}.encoder.1", out_dim, 64 * 7 * 7)
+
+
+# UNIMODAL_MODEL_MAP encoders that run on the engine (run_dino.py:542-550):
+#   kind -> (modality, stack builder(prefix), [Linear keys after the stack, relative to prefix],
+#            state-dict builder)
+UNI_ENCODERS = {
+    "image_simple": ("image", lambda p: cnn3_stack(f"{p}.encoder", CNN3_IMAGE_CONVS, 28),
+                     ["encoder.14", "projection.0"], image_encoder_sd),
+    "spectrogram_simple": ("audio", lambda p: cnn3_stack(f"{p}.encoder", CNN3_AUDIO_CONVS, 112),
+                           ["encoder.18"], spectrogram_encoder_sd),
+    "spectrogram_central": ("audio", lambda p: central_stack(f"{p}.encoder.0", CENTRAL_AUDIO_CONVS, 112),
+                            ["encoder.1"], spectrogram_central_sd),
+}
+UNI_ALIASES = {"image": "image_simple", "audio": "spectrogram_simple"}
+
+
+def unimodal_dino_sd(kind, D, P):
+    """UniModalDINO (models/dino.py:1257-1297) state dict over an UNI_ENCODERS kind."""
+    kind = UNI_ALIASES.get(kind, kind)
+    build = UNI_ENCODERS[kind][3]
+    sd = OrderedDict()
+    sd["center"] = ((1, P), "center")
+    build(sd, "student", D)
+    build(sd, "teacher", D)
+    projection_head_sd(sd, "student_projection", D, P)
+    projection_head_sd(sd, "teacher_projection", D, P)
+    return sd
+
+
 def simclr_sd(D, P):
     sd = OrderedDict()
     image_encoder_sd(sd, "image_encoder", D)

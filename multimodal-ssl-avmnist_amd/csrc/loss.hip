@@ -270,30 +270,95 @@ __global__ __launch_bounds__(256) void l2norm_bwd_kernel(const float* __restrict
 
 __global__ __launch_bounds__(256) void softmax_xent_kernel(
     const float* __restrict__ logits, long long ld, int R, int C, const int64_t* __restrict__ targets,
-    int target_mode, int col_major, int mask_diag, float gscale, float* __restrict__ loss_parts,
-    float* dlogits, long long ldd, int accumulate) {
+    int target_mode, int tgt_off, int col_major, int mask_off, float gscale,
+    float* __restrict__ loss_parts, float* dlogits, long long ldd, int accumulate) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int l = lane_id();
   if (r >= R) return;
   auto at = [&](int j) -> size_t { return col_major ? (size_t)j * ld + r : (size_t)r * ld + j; };
   auto atd = [&](int j) -> size_t { return col_major ? (size_t)j * ldd + r : (size_t)r * ldd + j; };
-  const int tgt = target_mode == 0 ? (int)targets[r] : target_mode == 1 ? r : (r + R / 2) % R;
+  const int tgt = target_mode == 0 ? (int)targets[r] : target_mode == 1 ? r + tgt_off : (r + R / 2) % R;
+  const int mcol = mask_off >= 0 ? r + mask_off : -1;   // excluded column (-inf logit)
   float m = -INFINITY;
   for (int j = l; j < C; j += 64)
-    if (!(mask_diag && j == r)) m = fmaxf(m, logits[at(j)]);
+    if (j != mcol) m = fmaxf(m, logits[at(j)]);
   m = wave_max(m);
   float se = 0.f;
   for (int j = l; j < C; j += 64)
-    if (!(mask_diag && j == r)) se += expf(logits[at(j)] - m);
+    if (j != mcol) se += expf(logits[at(j)] - m);
   se = wave_sum(se);
   const float lse = m + logf(se);
   if (l == 0) loss_parts[r] = lse - logits[at(tgt)];
   if (dlogits) {
     for (int j = l; j < C; j += 64) {
       float g = 0.f;
-      if (!(mask_diag && j == r)) g = (expf(logits[at(j)] - lse) - (j == tgt ? 1.f : 0.f)) * gscale;
+      if (j != mcol) g = (expf(logits[at(j)] - lse) - (j == tgt ? 1.f : 0.f)) * gscale;
       const size_t o = atd(j);
       dlogits[o] = accumulate ? dlogits[o] + g : g;
+    }
+  }
+}
+
+// Cosine-consistency term of UniModalDINOLightning (_cosine_consistency_loss, dino.py:1575-1594):
+// one block per sample b over its V view rows e_v = emb[v*B + b] (view-major [V*B, D]):
+//   n_v = e_v / max(|e_v|, eps),  loss_b = sum_{i<j} (1 - n_i.n_j)^2 / (count * B)
+//   demb_i = alpha * (dn_i - n_i (n_i.dn_i)) / max(|e_i|, eps),
+//   dn_i = sum_{j != i} -2 (1 - n_i.n_j) n_j / (count * B)
+// demb is ACCUMULATED (added to the projection head's input gradient); either output may be
+// NULL (forward: loss only; backward: gradient only).
+constexpr int COS_MAXV = 32;
+__global__ __launch_bounds__(256) void cosine_consistency_kernel(
+    const float* __restrict__ emb, int V, int B, int D, float alpha, float* __restrict__ loss_parts,
+    float* __restrict__ demb) {
+  __shared__ float inv[COS_MAXV];
+  __shared__ float sim[COS_MAXV][COS_MAXV];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  auto row = [&](int v) { return emb + ((size_t)v * B + b) * D; };
+  // norms: wave w handles views w, w+4, ...
+  for (int v = w; v < V; v += 4) {
+    float ss = 0.f;
+    for (int k = l; k < D; k += 64) { const float x = row(v)[k]; ss += x * x; }
+    ss = wave_sum(ss);
+    if (l == 0) inv[v] = 1.f / fmaxf(sqrtf(ss), NORM_EPS);
+  }
+  __syncthreads();
+  // pairwise cosine similarities (i < j), one wave per pair
+  const int npair = V * (V - 1) / 2;
+  for (int q = w; q < npair; q += 4) {
+    int i = 0, rem = q;
+    while (rem >= V - 1 - i) { rem -= V - 1 - i; ++i; }
+    const int j = i + 1 + rem;
+    float d = 0.f;
+    for (int k = l; k < D; k += 64) d += row(i)[k] * row(j)[k];
+    d = wave_sum(d) * inv[i] * inv[j];
+    if (l == 0) { sim[i][j] = d; sim[j][i] = d; }
+  }
+  __syncthreads();
+  const float scale = 1.f / ((float)npair * (float)B);
+  if (tid == 0 && loss_parts) {
+    float s = 0.f;
+    for (int i = 0; i < V; ++i)
+      for (int j = i + 1; j < V; ++j) s += (1.f - sim[i][j]) * (1.f - sim[i][j]);
+    loss_parts[b] = s * scale * alpha;
+  }
+  if (!demb) return;
+  // gradient: wave w handles views w, w+4, ...
+  for (int i = w; i < V; i += 4) {
+    float dot = 0.f;   // n_i . dn_i
+    for (int k = l; k < D; k += 64) {
+      float dn = 0.f;
+      for (int j = 0; j < V; ++j)
+        if (j != i) dn += -2.f * (1.f - sim[i][j]) * scale * row(j)[k] * inv[j];
+      dot += dn * row(i)[k] * inv[i];
+    }
+    dot = wave_sum(dot);
+    for (int k = l; k < D; k += 64) {
+      float dn = 0.f;
+      for (int j = 0; j < V; ++j)
+        if (j != i) dn += -2.f * (1.f - sim[i][j]) * scale * row(j)[k] * inv[j];
+      const float g = alpha * (dn - row(i)[k] * inv[i] * dot) * inv[i];
+      demb[((size_t)i * B + b) * D + k] += g;
     }
   }
 }
@@ -350,15 +415,26 @@ int avd_l2norm_bwd(const float* y, const float* norms, const float* dy, float* d
 }
 
 int avd_softmax_xent(const float* logits, long long ld, int R, int C, const int64_t* targets,
-                     int target_mode, int col_major, int mask_diag, float gscale,
+                     int target_mode, int tgt_off, int col_major, int mask_off, float gscale,
                      float* loss_parts, float* dlogits, long long ldd, int accumulate,
                      void* stream) {
   if (!logits || !loss_parts || (target_mode == 0 && !targets)) return AVD_ERR_ARG;
   if (target_mode < 0 || target_mode > 2) return AVD_ERR_ARG;
   if (R <= 0 || C <= 0) return AVD_ERR_SHAPE;
+  if (target_mode == 1 && (tgt_off < 0 || R - 1 + tgt_off >= C)) return AVD_ERR_SHAPE;
   softmax_xent_kernel<<<avd_cdiv(R, 4), 256, 0, avd_stream(stream)>>>(
-      logits, ld, R, C, targets, target_mode, col_major, mask_diag, gscale, loss_parts, dlogits,
-      ldd, accumulate);
+      logits, ld, R, C, targets, target_mode, tgt_off, col_major, mask_off, gscale, loss_parts,
+      dlogits, ldd, accumulate);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_cosine_consistency(const float* emb, int V, int B, int D, float alpha, float* loss_parts,
+                           float* demb, void* stream) {
+  if (!emb || (!loss_parts && !demb)) return AVD_ERR_ARG;
+  if (V < 2 || V > COS_MAXV || B <= 0 || D <= 0) return AVD_ERR_SHAPE;
+  cosine_consistency_kernel<<<B, 256, 0, avd_stream(stream)>>>(emb, V, B, D, alpha, loss_parts,
+                                                               demb);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

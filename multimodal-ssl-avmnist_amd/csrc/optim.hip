@@ -34,16 +34,22 @@ __global__ __launch_bounds__(256) void ema_kernel(float* __restrict__ t, const f
     t[i] = m * t[i] + om * s[i];
 }
 
+// DECOUPLED = false: torch.optim.Adam (wd added to the gradient);
+// DECOUPLED = true:  torch.optim.AdamW (p *= 1 - lr*wd before the moment update; the linear
+//                    probe's optimiser, dino.py:898)
+template <bool DECOUPLED>
 __device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, float lr, float b1,
                                       float b2, float eps, float wd, float inv_bc1,
                                       float inv_sqrt_bc2) {
-  g = fmaf(wd, p, g);
+  if (DECOUPLED) p *= 1.f - lr * wd;
+  else g = fmaf(wd, p, g);
   m = b1 * m + (1.f - b1) * g;
   v = b2 * v + (1.f - b2) * g * g;
   const float denom = sqrtf(v) * inv_sqrt_bc2 + eps;
   p -= lr * inv_bc1 * m / denom;
 }
 
+template <bool DECOUPLED>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    long long n, float lr, float b1, float b2,
@@ -55,16 +61,16 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     const float4 gg = reinterpret_cast<const float4*>(g)[i];
     float4 mm = reinterpret_cast<float4*>(m)[i];
     float4 vv = reinterpret_cast<float4*>(v)[i];
-    adam1(pp.x, gg.x, mm.x, vv.x, lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2);
-    adam1(pp.y, gg.y, mm.y, vv.y, lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2);
-    adam1(pp.z, gg.z, mm.z, vv.z, lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2);
-    adam1(pp.w, gg.w, mm.w, vv.w, lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2);
+    adam1<DECOUPLED>(pp.x, gg.x, mm.x, vv.x, lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2);
+    adam1<DECOUPLED>(pp.y, gg.y, mm.y, vv.y, lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2);
+    adam1<DECOUPLED>(pp.z, gg.z, mm.z, vv.z, lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2);
+    adam1<DECOUPLED>(pp.w, gg.w, mm.w, vv.w, lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2);
     reinterpret_cast<float4*>(p)[i] = pp;
     reinterpret_cast<float4*>(m)[i] = mm;
     reinterpret_cast<float4*>(v)[i] = vv;
   }
   for (long long i = n4 * 4 + blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
-    adam1(p[i], g[i], m[i], v[i], lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2);
+    adam1<DECOUPLED>(p[i], g[i], m[i], v[i], lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2);
 }
 
 inline int stream_grid(long long n) {
@@ -98,8 +104,19 @@ int avd_adam(float* p, const float* g, float* m, float* v, long long n, float lr
   if (!p || !g || !m || !v) return AVD_ERR_ARG;
   if (n < 0 || !aligned16(p) || !aligned16(g) || !aligned16(m) || !aligned16(v)) return AVD_ERR_SHAPE;
   if (n == 0) return AVD_OK;
-  adam_kernel<<<stream_grid(n), 256, 0, avd_stream(stream)>>>(p, g, m, v, n, lr, b1, b2, eps, wd,
-                                                              1.f / bc1, 1.f / sqrtf(bc2));
+  adam_kernel<false><<<stream_grid(n), 256, 0, avd_stream(stream)>>>(p, g, m, v, n, lr, b1, b2, eps,
+                                                                     wd, 1.f / bc1, 1.f / sqrtf(bc2));
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_adamw(float* p, const float* g, float* m, float* v, long long n, float lr, float b1,
+              float b2, float eps, float wd, float bc1, float bc2, void* stream) {
+  if (!p || !g || !m || !v) return AVD_ERR_ARG;
+  if (n < 0 || !aligned16(p) || !aligned16(g) || !aligned16(m) || !aligned16(v)) return AVD_ERR_SHAPE;
+  if (n == 0) return AVD_OK;
+  adam_kernel<true><<<stream_grid(n), 256, 0, avd_stream(stream)>>>(p, g, m, v, n, lr, b1, b2, eps,
+                                                                    wd, 1.f / bc1, 1.f / sqrtf(bc2));
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

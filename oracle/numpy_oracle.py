@@ -416,6 +416,16 @@ def adam_step(p, g, m, v, step, lr, wd, b1=0.9, b2=0.999, eps=1e-8):
     return p, m, v
 
 
+def adamw_step(p, g, m, v, step, lr, wd=0.01, b1=0.9, b2=0.999, eps=1e-8):
+    """torch.optim.AdamW (decoupled weight decay, default wd 0.01): the epoch-end linear
+    probe's optimiser (dino.py:898, 1678)."""
+    p = p * (1 - lr * wd)
+    m = b1 * m + (1 - b1) * g
+    v = b2 * v + (1 - b2) * g * g
+    denom = np.sqrt(v) / math.sqrt(1 - b2 ** step) + eps
+    return p - (lr / (1 - b1 ** step)) * m / denom, m, v
+
+
 def ema(teacher, student, m):
     """MultiModalDINO.update_teacher (dino.py:635-646)."""
     return m * teacher + (1 - m) * student
@@ -547,41 +557,124 @@ def adam_update_state(state, grads, opt, step, hp):
     return new
 
 
-def unimodal_image_step(P, batch, hp):
-    """UniModalDINO(ImageEncoder) + UniModalDINOLightning.dino_loss (dino.py:1319-1398,
-    1596-1635), 2 global / 0 local views (BASELINE config 1)."""
-    from .spec import CNN3_IMAGE
+def cosine_consistency_loss(emb):
+    """UniModalDINOLightning._cosine_consistency_loss (dino.py:1575-1594): mean over view
+    pairs i<j of batch-mean (1 - n_i . n_j)^2 with n = F.normalize(emb).  emb [V,B,D].
+    Returns (loss, d loss / d emb)."""
+    V, B, _ = emb.shape
+    n, c = l2norm_fwd(emb)
+    count = V * (V - 1) // 2
+    if count == 0:
+        return 0.0, np.zeros_like(emb)
+    loss = 0.0
+    dn = np.zeros_like(n)
+    for i in range(V):
+        for j in range(i + 1, V):
+            sim = (n[i] * n[j]).sum(-1)
+            loss += ((1 - sim) ** 2).mean()
+            g = (-2.0 * (1 - sim) / (B * count))[:, None]
+            dn[i] += g * n[j]
+            dn[j] += g * n[i]
+    return loss / count, l2norm_bwd(dn, c)
+
+
+UNI_KINDS = {"image": "image_simple", "audio": "spectrogram_simple"}
+
+
+def uni_encoder(kind, prefix):
+    """Unimodal student/teacher encoders of UNIMODAL_MODEL_MAP (run_dino.py:542-550):
+    image_simple = ImageEncoder (dino.py:483-499: image_encoder(512) + projection Linear(512,D)),
+    spectrogram_simple = SpectrogramEncoder (502-513: audio_encoder(D)),
+    spectrogram_central = SpectrogramEncoderCentral (515-523: CentralUnimodalAudio + Linear(3136,D)).
+    Returns (forward, backward)."""
+    from .spec import CNN3_IMAGE, CNN3_AUDIO, CENTRAL_AUDIO
+    kind = UNI_KINDS.get(kind, kind)
+    lin = None
+    if kind == "image_simple":
+        br = Branch(cnn3_stack(CNN3_IMAGE, f"{prefix}.encoder"), f"{prefix}.encoder.14")
+        lin = f"{prefix}.projection.0"
+    elif kind == "spectrogram_simple":
+        br = Branch(cnn3_stack(CNN3_AUDIO, f"{prefix}.encoder"), f"{prefix}.encoder.18")
+    elif kind == "spectrogram_central":
+        br = Branch(lenet_stack(CENTRAL_AUDIO, f"{prefix}.encoder.0"), f"{prefix}.encoder.1")
+    else:
+        raise ValueError(kind)
+
+    def fwd(P, x, G):
+        f, c = br.forward(P, x, G)
+        if lin is None:
+            return f, (f, c)
+        return linear_fwd(f, P[lin + ".weight"], P[lin + ".bias"]), (f, c)
+
+    def bwd(P, dout, cache, grads):
+        f, c = cache
+        if lin is not None:
+            dout, dw, db = linear_bwd(dout, f, P[lin + ".weight"])
+            _acc(grads, lin + ".weight", dw)
+            _acc(grads, lin + ".bias", db)
+        return br.backward(P, dout, c, grads)
+
+    return fwd, bwd
+
+
+def unimodal_step(P, batch, hp, modality="image", cos_alpha=0.0, masks=None, encoder=None):
+    """One UniModalDINO training step (UniModalDINO.forward dino.py:1319-1398,
+    UniModalDINOLightning.dino_loss 1596-1635 + cosine consistency 1575-1594 when
+    cos_alpha > 0, training_step 1637-1668): forward -> loss -> EMA -> backward.
+    Views: g_* [B,G,1,H,W] (+ l_* [B,L,...]) of the chosen modality.  Returns loss, outputs,
+    live-student grads, centre and the new state (EMA, centre, BN running stats)."""
+    masks = masks or {}
     P = {k: np.asarray(v, F64) if np.asarray(v).dtype != np.int64 else np.asarray(v) for k, v in P.items()}
-    g_img = batch["g_img"]
-    B, G = g_img.shape[:2]
-    x = _views_to_rows(g_img).astype(F64)
-
-    def enc(prefix):
-        return Branch(cnn3_stack(CNN3_IMAGE, f"{prefix}.encoder"), f"{prefix}.encoder.14")
-
-    def run(prefix, x):
-        e = enc(prefix)
-        f, c = e.forward(P, x, G)
-        o = linear_fwd(f, P[f"{prefix}.projection.0.weight"], P[f"{prefix}.projection.0.bias"])
-        return o, (e, f, c)
-
-    s_feat, (se, sf, sc) = run("student", x)
-    t_feat, _ = run("teacher", x)
+    key = "img" if UNI_KINDS.get(modality, modality) == "image_simple" else "aud"
+    g = batch["g_" + key]
+    B, G = g.shape[:2]
+    l = batch.get("l_" + key)
+    L = 0 if l is None else l.shape[1]
+    V = G + L
+    x = _views_to_rows(g).astype(F64)
+    if L:
+        x = np.concatenate([x, _views_to_rows(l).astype(F64)])
+    kind = encoder or modality
+    sf, sb = uni_encoder(kind, "student")
+    tf, _ = uni_encoder(kind, "teacher")
+    s_feat, s_cache = sf(P, x, V)
+    t_feat, t_cache = tf(P, x[:G * B], G)
     sp, tp = ProjHead("student_projection"), ProjHead("teacher_projection")
-    s_proj, spc = sp.forward(P, s_feat)
-    t_proj, _ = tp.forward(P, t_feat)
+    s_proj, spc = sp.forward(P, s_feat, 1, masks.get("proj_s"))
+    t_proj, tpc = tp.forward(P, t_feat)
     t_c = t_proj - P["center"]
-    s_out = s_proj.reshape(G, B, -1)
+    s_out = s_proj.reshape(V, B, -1)
     t_out = t_c.reshape(G, B, -1)
-    loss, ds = dino_loss(s_out, t_out, hp["tau_s"], hp["tau_t"], center_teacher=True)
+    dino, ds = dino_loss(s_out, t_out, hp["tau_s"], hp["tau_t"], center_teacher=True)
     grads = {}
-    dsf = sp.backward(P, ds.reshape(G * B, -1), spc, grads)
-    df, dw, db = linear_bwd(dsf, sf, P["student.projection.0.weight"])
-    _acc(grads, "student.projection.0.weight", dw)
-    _acc(grads, "student.projection.0.bias", db)
-    se.backward(P, df, sc, grads)
+    dsf = sp.backward(P, ds.reshape(V * B, -1), spc, grads)
+    cos = 0.0
+    if cos_alpha > 0:
+        cos, demb = cosine_consistency_loss(s_feat.reshape(V, B, -1))
+        dsf = dsf + cos_alpha * demb.reshape(V * B, -1)
+    sb(P, dsf, s_cache, grads)
     new_center = P["center"] * hp["center_momentum"] + t_proj.mean(axis=0, keepdims=True) * (1 - hp["center_momentum"])
-    return {"loss": loss, "s_out": s_out, "t_out": t_out, "grads": grads, "center_after": new_center}
+    new = dict(P)
+    m = hp["momentum"]
+    for k in P:
+        if k.startswith("teacher") and not (k.endswith("running_mean") or k.endswith("running_var")
+                                            or k.endswith("num_batches_tracked")):
+            new[k] = ema(P[k], P["student" + k[len("teacher"):]], m)
+    new["center"] = new_center
+    bn_stats = (list(_branch_stats(s_cache[1])) + [("student_projection.mlp.1", spc[-1])]
+                + list(_branch_stats(t_cache[1])) + [("teacher_projection.mlp.1", tpc[-1])])
+    for bk, st in bn_stats:
+        rm, rv = bn_running_update(new[bk + ".running_mean"], new[bk + ".running_var"], st)
+        new[bk + ".running_mean"], new[bk + ".running_var"] = rm, rv
+        new[bk + ".num_batches_tracked"] = np.asarray(new[bk + ".num_batches_tracked"]) + st[0].shape[0]
+    return {"loss": dino + cos_alpha * cos, "dino_loss": dino, "cos_loss": cos, "s_out": s_out,
+            "t_out": t_out, "emb": s_feat.reshape(V, B, -1), "grads": grads,
+            "center_after": new_center, "state": new}
+
+
+def unimodal_image_step(P, batch, hp):
+    """UniModalDINO(ImageEncoder), 2 global / 0 local views, no cosine term (BASELINE config 1)."""
+    return unimodal_step(P, batch, hp, "image", 0.0)
 
 
 def simclr_step(P, batch, mode, temperature=0.07):

@@ -119,6 +119,30 @@ def unimodal_image_dino_spec(D=256, P=128):
     return sd
 
 
+def spectrogram_central_spec(sd, prefix, out_dim):
+    """SpectrogramEncoderCentral (models/dino.py:515-523): CentralUnimodalAudio + Linear(3136,out)."""
+    central_lenet_spec(sd, f"{prefix}.encoder.0", CENTRAL_AUDIO)
+    _dense(sd, f"{prefix}.encoder.1", out_dim, 64 * 7 * 7)
+
+
+def unimodal_dino_spec(modality="image", D=256, P=128):
+    """UniModalDINO (models/dino.py:1257-1297) over an UNIMODAL_MODEL_MAP encoder
+    (run_dino.py:542-550): "image"/"image_simple", "audio"/"spectrogram_simple",
+    "spectrogram_central"."""
+    kind = {"image": "image_simple", "audio": "spectrogram_simple"}.get(modality, modality)
+    if kind == "image_simple":
+        return unimodal_image_dino_spec(D, P)
+    build = {"spectrogram_simple": spectrogram_encoder_spec,
+             "spectrogram_central": spectrogram_central_spec}[kind]
+    sd = OrderedDict()
+    sd["center"] = ((1, P), "center")
+    build(sd, "student", D)
+    build(sd, "teacher", D)
+    projection_head_spec(sd, "student_projection", D, P)
+    projection_head_spec(sd, "teacher_projection", D, P)
+    return sd
+
+
 def simclr_spec(D=256, P=256):
     sd = OrderedDict()
     image_encoder_spec(sd, "image_encoder", D)

@@ -204,15 +204,18 @@ def multimodal_case(name, mode, E, D, P, B, G, L, pseed, bseed, steps, out_dir, 
     print(f"{name}: loss={out['loss']:.8f} curve={np.array(curve)}")
 
 
-def unimodal_case(name, D, P, B, pseed, bseed, steps, out_dir, dt="float32"):
+def unimodal_case(name, D, P, B, pseed, bseed, steps, out_dir, dt="float32", modality="image",
+                  L=0, cos_alpha=0.0):
     import torch
     dt = getattr(torch, dt)
     import models.dino as rd
     torch.manual_seed(0)
-    model = rd.UniModalDINO(encoder_class=rd.ImageEncoder, output_dim=D, projection_dim=P,
+    enc = {"image": rd.ImageEncoder, "audio": rd.SpectrogramEncoder,
+           "spectrogram_central": rd.SpectrogramEncoderCentral}[modality]
+    model = rd.UniModalDINO(encoder_class=enc, output_dim=D, projection_dim=P,
                             momentum=HP["momentum"], center_momentum=HP["center_momentum"],
                             dropout=0.0)
-    spec = ospec.unimodal_image_dino_spec(D, P)
+    spec = ospec.unimodal_dino_spec(modality, D, P)
     state = make_state(spec, pseed)
     load_into(model, spec, state)
     zero_dropout(model)
@@ -220,13 +223,18 @@ def unimodal_case(name, D, P, B, pseed, bseed, steps, out_dir, dt="float32"):
     model.train()
     selfns = types.SimpleNamespace(student_temperature=HP["tau_s"], teacher_temperature=HP["tau_t"])
     opt = torch.optim.Adam(model.parameters(), lr=HP["lr"], weight_decay=HP["wd"])
-    out = {"meta_dims": np.array([D, P, B, 2, 0, pseed, bseed])}
+    out = {"meta_dims": np.array([D, P, B, 2, L, pseed, bseed]), "meta_modality": np.array(modality),
+           "meta_cos_alpha": np.float64(cos_alpha)}
     curve = []
     for step in range(steps):
-        b = make_multimodal_batch(B, 2, 0, bseed + step, with_originals=False)
+        b = make_multimodal_batch(B, 2, L, bseed + step, with_originals=False)
         t = {k: torch.from_numpy(v).to(dt) for k, v in b.items()}
         s_out, t_out, emb = model((t["g_img"], t["g_aud"], t["l_img"], t["l_aud"]))
+        # UniModalDINOLightning.training_step (dino.py:1637-1668), replayed unbound
         loss = rd.UniModalDINOLightning.dino_loss(selfns, s_out, t_out)
+        if cos_alpha > 0:
+            cos = rd.UniModalDINOLightning._cosine_consistency_loss(selfns, emb)
+            loss = loss + cos_alpha * cos
         model.update_teacher()
         opt.zero_grad()
         loss.backward()
@@ -245,6 +253,10 @@ def unimodal_case(name, D, P, B, pseed, bseed, steps, out_dir, dt="float32"):
                     summarize("rs/" + k, v.numpy(), out)
                 elif k == "center":
                     out["center_after"] = v.numpy().astype(STORE["dtype"])
+                elif k.startswith("teacher") and not k.endswith("num_batches_tracked"):
+                    summarize("ema/" + k, v.numpy(), out)
+                elif not k.endswith("num_batches_tracked"):
+                    summarize("post/" + k, v.numpy(), out)
         curve.append(loss.item())
     out["curve"] = np.array(curve, np.float64)
     np.savez_compressed(os.path.join(out_dir, name + ".npz"), **out)
@@ -292,22 +304,37 @@ def simclr_case(name, D, P, B, pseed, bseed, out_dir, dt="float32"):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=HERE)
+    ap.add_argument("--only", default="", help="comma-separated case names (default: all)")
     args = ap.parse_args()
     write_stubs()
     import torch
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     o = args.out
+    only = set(args.only.split(",")) if args.only else None
+    # Each case twice: the reference executed in fp32 (its CPU numerics) and in float64
+    # (the same algorithm without rounding noise: the tight pin for the oracle).
+    cases = [
+        ("mm_mse_small", multimodal_case, ("mse", 32, 32, 16, 4, 2, 4, 101, 1001, 5), {}),
+        ("mm_default_small", multimodal_case, ("default", 32, 32, 16, 4, 2, 4, 102, 1002, 3), {}),
+        ("mm_infonce_small", multimodal_case, ("infonce", 32, 32, 16, 4, 2, 4, 103, 1003, 3), {}),
+        ("mm_semi_small", multimodal_case, ("semi_supervised", 32, 32, 16, 4, 2, 4, 104, 1004, 3), {}),
+        ("mm_mse_full", multimodal_case, ("mse", 256, 256, 128, 2, 2, 4, 105, 1005, 2), {}),
+        ("uni_image_g2l0", unimodal_case, (256, 128, 8, 106, 1006, 3), {}),
+        ("uni_image_g2l4_cos", unimodal_case, (64, 32, 6, 108, 1008, 3),
+         dict(modality="image", L=4, cos_alpha=0.3)),
+        ("uni_audio_g2l2_cos", unimodal_case, (64, 32, 3, 109, 1009, 2),
+         dict(modality="audio", L=2, cos_alpha=0.3)),
+        ("uni_speccentral_g2l2", unimodal_case, (32, 16, 3, 110, 1010, 2),
+         dict(modality="spectrogram_central", L=2, cos_alpha=0.0)),
+        ("simclr_small", simclr_case, (256, 256, 4, 107, 1007), {}),
+    ]
     # Each case twice: the reference executed in fp32 (its CPU numerics) and in float64
     # (the same algorithm without rounding noise: the tight pin for the oracle).
     for dt, sfx, store in (("float32", "", np.float32), ("float64", "_f64", np.float64)):
         STORE["dtype"] = store
-        multimodal_case("mm_mse_small" + sfx, "mse", 32, 32, 16, 4, 2, 4, 101, 1001, 5, o, dt)
-        multimodal_case("mm_default_small" + sfx, "default", 32, 32, 16, 4, 2, 4, 102, 1002, 3, o, dt)
-        multimodal_case("mm_infonce_small" + sfx, "infonce", 32, 32, 16, 4, 2, 4, 103, 1003, 3, o, dt)
-        multimodal_case("mm_semi_small" + sfx, "semi_supervised", 32, 32, 16, 4, 2, 4, 104, 1004, 3, o, dt)
-        multimodal_case("mm_mse_full" + sfx, "mse", 256, 256, 128, 2, 2, 4, 105, 1005, 2, o, dt)
-        unimodal_case("uni_image_g2l0" + sfx, 256, 128, 8, 106, 1006, 3, o, dt)
-        simclr_case("simclr_small" + sfx, 256, 256, 4, 107, 1007, o, dt)
+        for name, fn, a, kw in cases:
+            if only is None or name in only:
+                fn(name + sfx, *a, out_dir=o, dt=dt, **kw)
 
 
 if __name__ == "__main__":

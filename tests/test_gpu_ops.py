@@ -436,6 +436,48 @@ def test_ema_adam(ops):
     assert rel(host(tp), pr) < 1e-7
 
 
+def test_adamw(ops):
+    g = np.random.default_rng(9)
+    n = 257 * 4
+    p = g.normal(size=n).astype(np.float32)
+    gr = g.normal(size=n).astype(np.float32)
+    tp, tg = dev(p), dev(gr)
+    m, v = torch.zeros_like(tp), torch.zeros_like(tp)
+    pr, mr, vr = p.astype(np.float64), np.zeros(n), np.zeros(n)
+    for step in (1, 2, 3):
+        ops.adamw(tp, tg, m, v, n, 1e-3, 0.9, 0.999, 1e-8, 1e-2, 1 - 0.9 ** step, 1 - 0.999 ** step)
+        pr, mr, vr = O.adamw_step(pr, gr.astype(np.float64), mr, vr, step, 1e-3, 1e-2)
+    assert rel(host(tp), pr) < 1e-7
+
+
+def test_xent_offsets_global_rows(ops):
+    """Shard view of a global-batch CE: rows r0..r0+R of S [R, C] with target / masked column
+    at r + offset equal the corresponding rows of the full-batch loss (NT-Xent / InfoNCE with
+    all-gathered negatives)."""
+    g = np.random.default_rng(10)
+    C, R, r0 = 24, 6, 12
+    S = g.normal(size=(C, C)).astype(np.float32)
+    # full NT-Xent style rows: mask diagonal, targets (i + C/2) % C
+    full = S.astype(np.float64).copy()
+    np.fill_diagonal(full, -np.inf)
+    lab = (np.arange(C) + C // 2) % C
+    lref, dref = O.cross_entropy(full, lab)
+    rows = dev(S[r0:r0 + R])
+    lp, d = torch.empty(R, device="cuda"), torch.empty(R, C, device="cuda")
+    tgt = dev(lab[r0:r0 + R].astype(np.int64))
+    ops.softmax_xent(rows, C, R, C, tgt, 0, False, True, 1.0 / C, lp, d, C, False, mask_off=r0)
+    per_row = -O.log_softmax(full)[np.arange(C), lab]
+    assert np.abs(host(lp) - per_row[r0:r0 + R]).max() < 1e-5
+    dfull = dref.copy()
+    np.fill_diagonal(dfull, 0.0)
+    assert rel(host(d), dfull[r0:r0 + R]) < 1e-5
+    # InfoNCE diagonal target with offset, no mask
+    lp2 = torch.empty(R, device="cuda")
+    ops.softmax_xent(rows, C, R, C, None, 1, False, False, 1.0, lp2, None, C, False, tgt_off=r0)
+    ls = O.log_softmax(S.astype(np.float64))
+    assert np.abs(host(lp2) + ls[np.arange(r0, r0 + R), np.arange(r0, r0 + R)]).max() < 1e-5
+
+
 def test_stage_views(ops):
     g = np.random.default_rng(8)
     B, G, L = 3, 2, 4

@@ -128,6 +128,45 @@ def test_unimodal_image_config1_matches_reference(variant):
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("case", ["uni_image_g2l4_cos", "uni_audio_g2l2_cos", "uni_speccentral_g2l2"])
+def test_unimodal_local_views_cosine_matches_reference(case, variant):
+    """UniModalDINO (image / spectrogram encoder) with local views and the cosine-consistency
+    term at the reference's default cosine_loss_alpha=0.3: loss, outputs, gradients, EMA'd
+    teacher, BN running stats, centre and the post-Adam student (dino.py:1257-1398,
+    1575-1668)."""
+    fx = gu.load(case + variant)
+    lt, orel, grel, srel, floor, _ = TOL[variant]
+    D, P, B, G, L, pseed, bseed = [int(x) for x in fx["meta_dims"]]
+    modality, alpha = str(fx["meta_modality"]), float(fx["meta_cos_alpha"])
+    state = make_state(S.unimodal_dino_spec(modality, D, P), pseed)
+    batch = make_multimodal_batch(B, G, L, bseed, with_originals=False)
+    r = O.unimodal_step(state, batch, HP, modality, alpha)
+    assert abs(r["loss"] - fx["loss"]) < lt, (r["loss"], fx["loss"])
+    _check_all(fx, [("s_out", r["s_out"]), ("t_out", r["t_out"])], orel)
+    live = [str(k) for k in fx["live_keys"]]
+    assert sorted(live) == sorted(r["grads"].keys())
+    zero = _zero(case)
+    # gradients that nearly cancel through the projection head's BatchNorm1d (|g| ~ 1e-5: the
+    # Linear bias under it gets only the cosine term) sit at the fp32 reference's rounding
+    # noise (~8e-6, measured on the mathematically-zero mlp.0 bias); the _f64 pin checks them
+    small = set() if variant == "_f64" else {
+        k for k, v in gu.load(case + "_f64").items()
+        if k.startswith("grad/") and "@" not in k and np.linalg.norm(v) < 1e-4}
+    _check_all(fx, [("grad/" + k, r["grads"][k]) for k in live], grel,
+               floor_fn=lambda k: floor if k in zero else (1e-4 if k in small else 0.0))
+    _check_all(fx, [("center_after", r["center_after"])], orel)
+    new = r["state"]
+    _check_all(fx, [(k, new[k[3:]]) for k in fx if k.startswith("rs/") and "@" not in k]
+               + [(k[:-5], new[k[3:-5]]) for k in fx if k.startswith("rs/") and k.endswith("@norm")], srel)
+    _check_all(fx, [(k, new[k[4:]]) for k in fx if k.startswith("ema/") and "@" not in k]
+               + [(k[:-5], new[k[4:-5]]) for k in fx if k.startswith("ema/") and k.endswith("@norm")], srel)
+    if variant == "_f64":
+        post = O.adam_update_state(new, r["grads"], {}, 1, HP)
+        items = [("post/" + k, post[k]) for k in live if ("grad/" + k) not in zero]
+        _check_all(fx, items, 1e-8)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])
 def test_simclr_config4_matches_reference(mode, variant):
     fx = gu.load("simclr_small" + variant)
