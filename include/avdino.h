@@ -101,11 +101,13 @@ int avd_conv2d_wgrad(const void* x, int xdt, const void* dy, int dydt, float* dw
  * shift = beta - mean*scale).  If running_mean != NULL, applies the reference's sequential
  * per-call update for g = 0..G-1: rm = 0.9 rm + 0.1 mean_g, rv = 0.9 rv + 0.1 var_g*n/(n-1)
  * (nn.BatchNorm momentum 0.1; group order = the reference's call order, dino.py:680-704).
- * parts is consumed: the chunked first pass writes f64 chunk sums over it. */
+ * parts is consumed: the chunked first pass writes f64 chunk sums over it.
+ * pivot [G,C] (nullable): the partials are sums of (x - pivot) and (x - pivot)^2 (shifted sums
+ * from avd_colstats: no cancellation in the variance when |mean| >> std). */
 int avd_bn_finalize(float* parts, int G, int R, int C, long long count,
                     const float* gamma, const float* beta, float eps, float momentum,
                     float* mean, float* invstd, float* scale, float* shift,
-                    float* running_mean, float* running_var, void* stream);
+                    float* running_mean, float* running_var, const float* pivot, void* stream);
 
 /* out = maxpool2(relu(scale*y + shift))  [N,C,H/2,W/2]  (floor mode)      pool_mode 0
  * out = mean_hw(maxpool2(relu(...)))        [N,C]   f32 (AdaptiveAvgPool2d(1)) pool_mode 1
@@ -210,9 +212,12 @@ int avd_sum_rows(const float* in, int rows, int cols, long long ld, float* out, 
                  void* stream);
 
 /* Column partial statistics of x [rows, C] f32 for BatchNorm1d: parts [C, G, R, 2] with
- * R = avd_colstats_parts(rows/G) row-chunks per group. */
+ * R = avd_colstats_parts(rows/G) row-chunks per group.  pivot [G,C] (nullable) receives
+ * the first row of each group; the partials are then taken about it (pass it on to
+ * avd_bn_finalize). */
 int avd_colstats_parts(int rows_per_group);
-int avd_colstats(const float* x, int rows, int G, int C, float* parts, void* stream);
+int avd_colstats(const float* x, int rows, int G, int C, float* parts, float* pivot,
+                 void* stream);
 
 /* Elementwise activation with optional dropout (keep mask from a counter hash of
  * (seed, index), scaled by 1/(1-p)); act 0 = ReLU (fusion, dino.py:222-227),

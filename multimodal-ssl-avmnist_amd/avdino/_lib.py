@@ -27,7 +27,7 @@ PROTOS = {
     "avd_conv2d_dgrad": [P, P, P, I, I, I, I, I, I, I, I, P],
     "avd_conv2d_wgrad_chunks": [I, I, I, I],
     "avd_conv2d_wgrad": [P, I, P, I, P, I, I, I, I, I, I, I, P],
-    "avd_bn_finalize": [P, I, I, I, L, P, P, F, F, P, P, P, P, P, P, P],
+    "avd_bn_finalize": [P, I, I, I, L, P, P, F, F, P, P, P, P, P, P, P, P],
     "avd_bn_relu_pool": [P, I, P, P, P, I, I, I, I, I, I, I, P],
     "avd_bn_bwd_reduce": [P, I, P, I, I, P, P, P, P, P, I, I, I, I, I, P],
     "avd_bn_bwd_finalize": [P, I, I, I, L, P, P, P, P, P, P, P, I, P],
@@ -47,7 +47,7 @@ PROTOS = {
     "avd_cl_bn_bwd_apply": [P, I, P, I, P, P, P, P, I, I, I, I, I, P],
     "avd_sum_rows": [P, I, I, L, P, I, P],
     "avd_colstats_parts": [I],
-    "avd_colstats": [P, I, I, I, P, P],
+    "avd_colstats": [P, I, I, I, P, P, P],
     "avd_act_fwd": [P, P, I, P, P, I, I, I, F, U64, P],
     "avd_act_bwd": [P, P, P, I, P, P, I, I, I, F, U64, P],
     "avd_bn1d_bwd_reduce": [P, P, P, P, I, I, I, P, P],

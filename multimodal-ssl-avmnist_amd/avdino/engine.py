@@ -154,43 +154,48 @@ class ProjHead:
         self.gm = gemm_mode
 
     def forward(self, ws, store, tag, x, rows, out, drop_p=0.0, seed=0, x_ld=None, x_off=0,
-                update_running=True):
+                update_running=True, G=1):
+        """G > 1: the rows are G separate calls of the head (BatchNorm1d statistics and running
+        updates per call, in order), e.g. SimCLR's image-image mode."""
         p, Hd = self.p, self.h
+        rpg = rows // G
         h = ws.get(f"{tag}.h", rows * Hd)
         ops.linear_fwd(x, store[p + ".mlp.0.weight"], store[p + ".mlp.0.bias"], h, rows,
                        x_ld=x_ld, x_off=x_off, mode=self.gm)
-        R = ops.colstats_parts(rows)
-        parts = ws.get("stat_parts", Hd * R * 2)
-        ops.colstats(h, rows, 1, Hd, parts)
-        st = ws.get(f"{tag}.bn", 4 * Hd).view(4, Hd)
-        ops.bn_finalize(parts, 1, R, Hd, rows, store[p + ".mlp.1.weight"], store[p + ".mlp.1.bias"],
+        R = ops.colstats_parts(rpg)
+        parts = ws.get("stat_parts", Hd * G * R * 2)
+        pivot = ws.get(f"{tag}.pivot", G * Hd)
+        ops.colstats(h, rows, G, Hd, parts, pivot)
+        st = ws.get(f"{tag}.bn", 4 * G * Hd).view(4, G * Hd)
+        ops.bn_finalize(parts, G, R, Hd, rpg, store[p + ".mlp.1.weight"], store[p + ".mlp.1.bias"],
                         st[0], st[1], st[2], st[3],
                         store[p + ".mlp.1.running_mean"] if update_running else None,
-                        store[p + ".mlp.1.running_var"] if update_running else None)
+                        store[p + ".mlp.1.running_var"] if update_running else None, pivot=pivot)
         if update_running:
-            store.buffers[p + ".mlp.1.num_batches_tracked"] += 1
+            store.buffers[p + ".mlp.1.num_batches_tracked"] += G
         a = ws.get(f"{tag}.a", rows * Hd)
-        ops.act_fwd(h, a, 1, st[2], st[3], rows, 1, Hd, drop_p, seed)
+        ops.act_fwd(h, a, 1, st[2], st[3], rows, G, Hd, drop_p, seed)
         ops.linear_fwd(a, store[p + ".mlp.4.weight"], store[p + ".mlp.4.bias"], out, rows, mode=self.gm)
         return {"x": x, "x_ld": x_ld if x_ld is not None else self.i, "x_off": x_off, "h": h,
-                "a": a, "st": st, "rows": rows, "drop_p": drop_p, "seed": seed}
+                "a": a, "st": st, "rows": rows, "G": G, "drop_p": drop_p, "seed": seed}
 
     def backward(self, ws, store, ctx, dout, dx, dx_ld=None, dx_off=0):
-        p, Hd, rows = self.p, self.h, ctx["rows"]
+        p, Hd, rows, G = self.p, self.h, ctx["rows"], ctx["G"]
+        rpg = rows // G
         da = ws.get("head_da", rows * Hd)
         ops.linear_bwd(dout, ctx["a"], store[p + ".mlp.4.weight"], store.grad_of(p + ".mlp.4.weight"),
                        store.grad_of(p + ".mlp.4.bias"), da, rows, mode=self.gm)
         st = ctx["st"]
         dz = ws.get("head_dz", rows * Hd)
-        ops.act_bwd(ctx["h"], da, dz, 1, st[2], st[3], rows, 1, Hd, ctx["drop_p"], ctx["seed"])
-        R = ops.colstats_parts(rows)
-        parts = ws.get("bwd_parts", Hd * R * 2)
-        ops.bn1d_bwd_reduce(ctx["h"], dz, st[0], st[1], rows, 1, Hd, parts)
-        coef = ws.get("bwd_coef", Hd * 3)
-        ops.bn_bwd_finalize(parts, 1, R, Hd, rows, store[p + ".mlp.1.weight"], st[0], st[1], coef,
+        ops.act_bwd(ctx["h"], da, dz, 1, st[2], st[3], rows, G, Hd, ctx["drop_p"], ctx["seed"])
+        R = ops.colstats_parts(rpg)
+        parts = ws.get("bwd_parts", Hd * G * R * 2)
+        ops.bn1d_bwd_reduce(ctx["h"], dz, st[0], st[1], rows, G, Hd, parts)
+        coef = ws.get("bwd_coef", G * Hd * 3)
+        ops.bn_bwd_finalize(parts, G, R, Hd, rpg, store[p + ".mlp.1.weight"], st[0], st[1], coef,
                             store.grad_of(p + ".mlp.1.weight"), store.grad_of(p + ".mlp.1.bias"), None)
         dh = ws.get("head_dh", rows * Hd)
-        ops.bn1d_bwd_apply(ctx["h"], dz, coef, dh, rows, 1, Hd)
+        ops.bn1d_bwd_apply(ctx["h"], dz, coef, dh, rows, G, Hd)
         ops.linear_bwd(dh, ctx["x"], store[p + ".mlp.0.weight"], store.grad_of(p + ".mlp.0.weight"),
                        store.grad_of(p + ".mlp.0.bias"), dx, rows, x_ld=ctx["x_ld"],
                        x_off=ctx["x_off"], dx_ld=dx_ld, dx_off=dx_off, mode=self.gm)

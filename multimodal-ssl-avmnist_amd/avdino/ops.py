@@ -142,9 +142,9 @@ def conv2d_wgrad(x, dy, parts, N, Cin, H, W, Cout, K, pad):
 
 
 def bn_finalize(parts, G, R, C, count, gamma, beta, mean, invstd, scale, shift, rm=None, rv=None,
-                eps=1e-5, momentum=0.1):
+                eps=1e-5, momentum=0.1, pivot=None):
     call("avd_bn_finalize", p(parts), G, R, C, count, p(gamma), p(beta), eps, momentum, p(mean),
-         p(invstd), p(scale), p(shift), p(rm), p(rv), stream())
+         p(invstd), p(scale), p(shift), p(rm), p(rv), p(pivot), stream())
 
 
 def bn_relu_pool(y, scale, shift, out, pool_mode, N, B, C, H, W):
@@ -347,8 +347,8 @@ def colstats_parts(rows_per_group):
     return lib.avd_colstats_parts(rows_per_group)
 
 
-def colstats(x, rows, G, C, parts):
-    call("avd_colstats", p(x), rows, G, C, p(parts), stream())
+def colstats(x, rows, G, C, parts, pivot=None):
+    call("avd_colstats", p(x), rows, G, C, p(parts), p(pivot), stream())
 
 
 def act_fwd(x, out, act, scale, shift, rows, G, C, drop_p, seed):

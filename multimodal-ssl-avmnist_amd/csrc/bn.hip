@@ -71,7 +71,8 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(float* __restrict
 __global__ __launch_bounds__(64) void bn_finalize_kernel(
     const float* __restrict__ parts, int G, int R, int C, int S, int chunk, long long count,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
-    float* mean_o, float* invstd_o, float* scale_o, float* shift_o, float* rm, float* rv) {
+    float* mean_o, float* invstd_o, float* scale_o, float* shift_o, float* rm, float* rv,
+    const float* __restrict__ pivot) {
   const int c = blockIdx.x * 64 + threadIdx.x;
   if (c >= C) return;
   double rmean = rm ? (double)rm[c] : 0.0, rvar = rv ? (double)rv[c] : 0.0;
@@ -88,8 +89,9 @@ __global__ __launch_bounds__(64) void bn_finalize_kernel(
       sum += d[0];
       sq += d[1];
     }
-    const double mean = sum / n;
-    double var = sq / n - mean * mean;
+    const double ms = sum / n;                       // mean of (x - K)
+    const double mean = (pivot ? (double)pivot[(size_t)g * C + c] : 0.0) + ms;
+    double var = sq / n - ms * ms;
     if (var < 0) var = 0;
     const double invstd = 1.0 / sqrt(var + (double)eps);
     const double sc = (double)gamma[c] * invstd;
@@ -450,15 +452,21 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_q4_kernel(
 // ----------------------------------------------------------------------------- BN1d / dense
 constexpr int CS_ROWS = 64;
 
+// Shifted sums: every partial is taken about the pivot K = x[first row of the group][c]
+// (stored in pivot[g, c] for avd_bn_finalize), so var = E[(x-K)^2] - E[x-K]^2 does not cancel
+// when |mean| >> std (BatchNorm1d over ReLU'd, pooled encoder features).
 __global__ __launch_bounds__(256) void colstats_kernel(const float* __restrict__ x, int rpg, int G,
-                                                       int C, int R, float* __restrict__ parts) {
+                                                       int C, int R, float* __restrict__ parts,
+                                                       float* __restrict__ pivot) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   const int r = blockIdx.y, g = blockIdx.z;
   if (c >= C) return;
   const int r0 = r * CS_ROWS, r1 = min(rpg, r0 + CS_ROWS);
+  const float K = pivot ? x[(size_t)g * rpg * C + c] : 0.f;
+  if (pivot && r == 0) pivot[(size_t)g * C + c] = K;
   float s = 0.f, q = 0.f;
   for (int row = r0; row < r1; ++row) {
-    const float v = x[((size_t)g * rpg + row) * C + c];
+    const float v = x[((size_t)g * rpg + row) * C + c] - K;
     s += v;
     q += v * v;
   }
@@ -597,7 +605,7 @@ extern "C" {
 int avd_bn_finalize(float* parts, int G, int R, int C, long long count, const float* gamma,
                     const float* beta, float eps, float momentum, float* mean, float* invstd,
                     float* scale, float* shift, float* running_mean, float* running_var,
-                    void* stream) {
+                    const float* pivot, void* stream) {
   if (!parts || !gamma || !beta || !mean || !invstd || !scale || !shift) return AVD_ERR_ARG;
   if (G <= 0 || R <= 0 || C <= 0 || count <= 1) return AVD_ERR_SHAPE;
   if ((running_mean == nullptr) != (running_var == nullptr)) return AVD_ERR_ARG;
@@ -611,7 +619,7 @@ int avd_bn_finalize(float* parts, int G, int R, int C, long long count, const fl
   }
   bn_finalize_kernel<<<avd_cdiv(C, 64), 64, 0, st>>>(parts, G, R, C, S, chunk, count, gamma, beta,
                                                     eps, momentum, mean, invstd, scale, shift,
-                                                    running_mean, running_var);
+                                                    running_mean, running_var, pivot);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
@@ -726,12 +734,13 @@ int avd_bn_bwd_apply(const void* y, int ydt, const void* gout, int gdt, int pool
 
 int avd_colstats_parts(int rows_per_group) { return avd_cdiv(rows_per_group, CS_ROWS); }
 
-int avd_colstats(const float* x, int rows, int G, int C, float* parts, void* stream) {
+int avd_colstats(const float* x, int rows, int G, int C, float* parts, float* pivot,
+                 void* stream) {
   if (!x || !parts) return AVD_ERR_ARG;
   if (rows <= 0 || G <= 0 || rows % G || C <= 0) return AVD_ERR_SHAPE;
   const int rpg = rows / G, R = avd_colstats_parts(rpg);
   dim3 grid(avd_cdiv(C, 256), R, G);
-  colstats_kernel<<<grid, 256, 0, avd_stream(stream)>>>(x, rpg, G, C, R, parts);
+  colstats_kernel<<<grid, 256, 0, avd_stream(stream)>>>(x, rpg, G, C, R, parts, pivot);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

@@ -314,9 +314,10 @@ def test_projection_head_pieces(ops):
     th = dev(h)
     R = ops.colstats_parts(rows)
     parts = torch.empty(C * R * 2, device="cuda")
-    ops.colstats(th, rows, 1, C, parts)
+    piv = torch.empty(C, device="cuda")
+    ops.colstats(th, rows, 1, C, parts, piv)
     st = torch.empty(4, C, device="cuda")
-    ops.bn_finalize(parts, 1, R, C, rows, dev(gamma), dev(beta), st[0], st[1], st[2], st[3])
+    ops.bn_finalize(parts, 1, R, C, rows, dev(gamma), dev(beta), st[0], st[1], st[2], st[3], pivot=piv)
     a = torch.empty_like(th)
     ops.act_fwd(th, a, 1, st[2], st[3], rows, 1, C, 0.0, 0)
     assert rel(host(a), a_ref) < 1e-5
@@ -332,6 +333,25 @@ def test_projection_head_pieces(ops):
     ops.bn1d_bwd_apply(th, dz, coef, dh, rows, 1, C)
     assert rel(host(dg), dg_ref) < 1e-5 and rel(host(db), db_ref) < 1e-5
     assert rel(host(dh), dh_ref) < 1e-4
+
+
+@pytest.mark.parametrize("G", [1, 3])
+def test_bn1d_stats_offset_columns(ops, G):
+    """BatchNorm1d statistics of columns whose mean is 100x their std (ReLU'd, pooled encoder
+    features): the pivot-shifted sums keep the variance exact to f32 rounding."""
+    g = np.random.default_rng(12)
+    rpg, C = 40, 300
+    h = (g.normal(0, 1, (G * rpg, C)) * 0.05 + g.uniform(2, 8, C)).astype(np.float32)
+    R = ops.colstats_parts(rpg)
+    parts = torch.empty(C * G * R * 2, device="cuda")
+    piv = torch.empty(G * C, device="cuda")
+    ops.colstats(dev(h), G * rpg, G, C, parts, piv)
+    st = torch.empty(4, G * C, device="cuda")
+    one, zero = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
+    ops.bn_finalize(parts, G, R, C, rpg, one, zero, st[0], st[1], st[2], st[3], pivot=piv)
+    hs = h.astype(np.float64).reshape(G, rpg, C)
+    assert rel(host(st[0]), hs.mean(1).ravel()) < 1e-7
+    assert rel(host(st[1]), 1 / np.sqrt(hs.var(1) + 1e-5).ravel()) < 2e-6
 
 
 def test_dropout_mask_statistics_and_consistency(ops):
