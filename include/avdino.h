@@ -313,6 +313,10 @@ int avd_adam(float* p, const float* g, float* m, float* v, long long n, float lr
 int avd_adamw(float* p, const float* g, float* m, float* v, long long n, float lr, float b1,
               float b2, float eps, float wd, float bc1, float bc2, void* stream);
 
+/* y += a*x over n floats (16-byte aligned): folds a scattered gradient slab into the local one
+ * (global-negative contrastive losses, avdino/contrastive.py). */
+int avd_axpy(float* y, const float* x, long long n, float a, void* stream);
+
 /* out = sum(in[0..n)) in fixed order (loss reduction); out is one float. */
 int avd_sum(const float* in, int n, float scale, float* out, void* stream);
 

@@ -61,6 +61,7 @@ PROTOS = {
     "avd_ema": [P, P, L, F, P],
     "avd_adam": [P, P, P, P, L, F, F, F, F, F, F, F, P],
     "avd_adamw": [P, P, P, P, L, F, F, F, F, F, F, F, P],
+    "avd_axpy": [P, P, L, F, P],
     "avd_sum": [P, I, F, P, P],
     "avd_stage_views": [P, I, P, I, P, I, I, P, I, P],
 }

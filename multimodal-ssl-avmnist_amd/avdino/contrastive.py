@@ -1,0 +1,109 @@
+"""Contrastive heads with local or GLOBAL negatives.
+
+* InfoNCE of MultiModalDINOWithINFONCELightning.infoNCE_loss (dino.py:1091-1128; same math
+  other_ssl/info_nce/info_nce.py:75-112): S = n(i) n(a)^T / tau, (CE(S, diag) + CE(S^T, diag))/2.
+* NT-Xent of MultiModalSimCLRLightning.nt_xent_loss (multimodal_simclr.py:74-89):
+  reps = [z1; z2], S = n n^T / tau with the diagonal masked, targets (i + B) mod 2B.
+
+With world W > 1 (one process per GPU, torch.distributed over RCCL) every rank keeps its own
+B rows and all-gathers the L2-normalised rows of the other ranks as negatives, so rank r's rows
+of S are exactly rows r*B.. of the single-device S over the global W*B batch.  Each rank's
+loss is the mean over ITS rows; DDP's gradient averaging (x 1/W) then yields the gradient of
+the global-batch loss.  The column side of dS (how my rows act as other ranks' negatives /
+positives) is reduce-scattered back to the owning rank (avdino.dist).  W == 1 is the
+reference's single-device loss exactly.
+
+Compute is libavdino: l2norm, MFMA GEMMs, softmax-CE with offset targets / masks, axpy.
+"""
+from . import dist, ops
+
+
+class _Norm:
+    def __init__(self, ws, tag, x, rows, P):
+        self.y = ws.get(tag + ".n", rows * P)
+        self.r = ws.get(tag + ".r", rows)
+        self.rows, self.P = rows, P
+        ops.l2norm_fwd(x, self.y, self.r, rows, P)
+
+    def backward(self, dy, dx):
+        ops.l2norm_bwd(self.y, self.r, dy, dx, self.rows, self.P)
+
+
+def _world(local, group):
+    if local:
+        return 1, 0
+    return dist.world(group), dist.rank(group)
+
+
+def infonce(ws, zi, za, B, P, dzi, dza, loss_parts, temperature=0.07, gm=ops.GEMM_F32_MFMA,
+            group=None, local=False):
+    """zi, za [B, P] (this rank's rows) -> loss_parts [2B] per-row CE (this rank's loss =
+    sum(loss_parts) * 0.5 / B), dzi, dza [B, P] (d of that loss).  Returns the scale."""
+    W, r = _world(local, group)
+    inv_t = 1.0 / temperature
+    ni, na = _Norm(ws, "nce.i", zi, B, P), _Norm(ws, "nce.a", za, B, P)
+    ni_all = ni.y if W == 1 else dist.gather_rows(ni.y.view(B, P), group).reshape(-1)
+    na_all = na.y if W == 1 else dist.gather_rows(na.y.view(B, P), group).reshape(-1)
+    C = W * B
+    S1, S2 = ws.get("nce.S1", B * C), ws.get("nce.S2", B * C)
+    ops.gemm(B, C, P, ni.y, P, 1, na_all, 1, P, S1, C, alpha=inv_t, mode=gm)   # image rows
+    ops.gemm(B, C, P, na.y, P, 1, ni_all, 1, P, S2, C, alpha=inv_t, mode=gm)   # audio rows
+    dS1, dS2 = ws.get("nce.dS1", B * C), ws.get("nce.dS2", B * C)
+    ops.softmax_xent(S1, C, B, C, None, 1, False, False, 0.5 / B, loss_parts[:B], dS1, C, False,
+                     tgt_off=r * B)
+    ops.softmax_xent(S2, C, B, C, None, 1, False, False, 0.5 / B, loss_parts[B:2 * B], dS2, C,
+                     False, tgt_off=r * B)
+    dni, dna = ws.get("nce.dni", B * P), ws.get("nce.dna", B * P)
+    ops.gemm(B, P, C, dS1, C, 1, na_all, P, 1, dni, P, alpha=inv_t, mode=gm)   # row side
+    ops.gemm(B, P, C, dS2, C, 1, ni_all, P, 1, dna, P, alpha=inv_t, mode=gm)
+    # column side: d(na_all) from S1, d(ni_all) from S2, each [C, P], owned rows scattered home
+    cA, cI = ws.get("nce.colA", C * P), ws.get("nce.colI", C * P)
+    ops.gemm(C, P, B, dS1, 1, C, ni.y, P, 1, cA, P, alpha=inv_t, mode=gm)
+    ops.gemm(C, P, B, dS2, 1, C, na.y, P, 1, cI, P, alpha=inv_t, mode=gm)
+    if W == 1:
+        ops.axpy(dna, cA)
+        ops.axpy(dni, cI)
+    else:
+        ops.axpy(dna, dist.scatter_rows_grad(cA.view(C, P), group).reshape(-1))
+        ops.axpy(dni, dist.scatter_rows_grad(cI.view(C, P), group).reshape(-1))
+    ni.backward(dni, dzi)
+    na.backward(dna, dza)
+    return 0.5 / B
+
+
+def nt_xent(ws, reps, B, P, dreps, loss_parts, temperature=0.07, gm=ops.GEMM_F32_MFMA, group=None,
+            local=False):
+    """reps [2B, P] = [z1; z2] of this rank -> loss_parts [2B] per-row CE (this rank's loss =
+    sum(loss_parts) / 2B), dreps [2B, P].  Returns the scale."""
+    W, r = _world(local, group)
+    inv_t = 1.0 / temperature
+    n = _Norm(ws, "ntx", reps, 2 * B, P)
+    nv = n.y.view(2 * B, P)
+    if W == 1:
+        n_all = n.y
+    else:   # global layout [z1 of every rank; z2 of every rank]
+        n_all = ws.get("ntx.all", 2 * W * B * P)
+        n_all.view(2, W * B, P)[0].copy_(dist.gather_rows(nv[:B], group))
+        n_all.view(2, W * B, P)[1].copy_(dist.gather_rows(nv[B:], group))
+    C = 2 * W * B
+    S = ws.get("ntx.S", 2 * B * C)
+    ops.gemm(2 * B, C, P, n.y, P, 1, n_all, 1, P, S, C, alpha=inv_t, mode=gm)
+    dS = ws.get("ntx.dS", 2 * B * C)
+    g = 1.0 / (2 * B)
+    # z1 rows: global row r*B + i, positive W*B + r*B + i; z2 rows: W*B + r*B + i -> r*B + i
+    ops.softmax_xent(S, C, B, C, None, 1, False, True, g, loss_parts[:B], dS, C, False,
+                     tgt_off=W * B + r * B, mask_off=r * B)
+    ops.softmax_xent(S[B * C:], C, B, C, None, 1, False, True, g, loss_parts[B:2 * B], dS[B * C:],
+                     C, False, tgt_off=r * B, mask_off=W * B + r * B)
+    dn = ws.get("ntx.dn", 2 * B * P)
+    ops.gemm(2 * B, P, C, dS, C, 1, n_all, P, 1, dn, P, alpha=inv_t, mode=gm)   # row side
+    col = ws.get("ntx.col", C * P)
+    ops.gemm(C, P, 2 * B, dS, 1, C, n.y, P, 1, col, P, alpha=inv_t, mode=gm)   # column side
+    if W == 1:
+        ops.axpy(dn, col)
+    else:
+        cv = col.view(2, W * B, P)
+        ops.axpy(dn[:B * P], dist.scatter_rows_grad(cv[0], group).reshape(-1))
+        ops.axpy(dn[B * P:], dist.scatter_rows_grad(cv[1], group).reshape(-1))
+    n.backward(dn, dreps)
+    return g

@@ -20,12 +20,12 @@ import torch
 import torch.distributed as dist
 
 
-def world():
-    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+def world(group=None):
+    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
 
 
-def rank():
-    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+def rank(group=None):
+    return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
 
 
 def grad_allreduce_hook(group=None):
@@ -60,6 +60,10 @@ def gather_rows(x, group=None):
     out = torch.empty((n * x.shape[0],) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
     if x.device.type == "cuda" and dist.get_backend(group) == "nccl":
         dist.all_gather_into_tensor(out, x.contiguous(), group=group)
+    elif x.device.type == "cuda":   # gloo (the 1-GPU rehearsal): stage through host memory
+        h = torch.empty(out.shape, dtype=x.dtype)
+        dist.all_gather(list(h.chunk(n)), x.detach().cpu().contiguous(), group=group)
+        out.copy_(h)
     else:
         dist.all_gather(list(out.chunk(n)), x.contiguous(), group=group)
     return out
@@ -77,7 +81,7 @@ def scatter_rows_grad(dx_all, group=None):
         dist.reduce_scatter_tensor(out, dx_all.contiguous(), op=dist.ReduceOp.SUM, group=group)
         return out
     # gloo has no reduce_scatter: all-reduce then keep my slice (same result, test backend)
-    t = dx_all.contiguous().clone()
+    t = dx_all.detach().cpu().contiguous().clone()
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     r = dist.get_rank(group)
-    return t[r * B:(r + 1) * B].clone()
+    return t[r * B:(r + 1) * B].to(dx_all.device)

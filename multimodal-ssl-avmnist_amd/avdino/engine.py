@@ -21,7 +21,7 @@ MI355X-native restructuring (results identical up to fp32 rounding):
 """
 import torch
 
-from . import ops
+from . import contrastive, ops
 from .spec import (CENTRAL_AUDIO_CONVS, CENTRAL_IMAGE_CONVS, CNN3_AUDIO_CONVS, CNN3_IMAGE_CONVS,
                    HEAD_NAMES, PROJ_HIDDEN, UNI_ALIASES, UNI_ENCODERS, central_stack, cnn3_stack)
 
@@ -233,7 +233,7 @@ class MultiCentralEngine:
     semi_supervised}``)."""
 
     def __init__(self, store, mode, E, D, P, hp, act_dtype=F32, grad_hook=None, seed=0,
-                 buffer_hook=None):
+                 buffer_hook=None, negatives="global", group=None):
         self.store, self.mode, self.E, self.D, self.P, self.hp = store, mode, E, D, P, hp
         self.act = act_dtype
         # Linear layers: bf16 MFMA in the bf16 mode (like the reference's fp16 autocast),
@@ -253,6 +253,9 @@ class MultiCentralEngine:
             self.heads = (ProjHead(hi, E, out, gemm_mode=self.gm), ProjHead(ha, E, out, gemm_mode=self.gm))
         self.grad_hook = grad_hook      # e.g. DDP all-reduce of store.grad (avdino.dist)
         self.buffer_hook = buffer_hook  # e.g. rank-0 buffer broadcast before each forward
+        # InfoNCE negatives under DDP: "global" = all-gathered (single-device loss over the
+        # global batch), "local" = this rank's batch only (the reference's DDP)
+        self.negatives, self.group = negatives, group
         self.seed = seed
         self.step_idx = 0
         self.last = {}
@@ -370,25 +373,13 @@ class MultiCentralEngine:
         return loss
 
     def _infonce(self, zi, za, B, P, aux, dzi, dza, temperature=0.07):
-        """infoNCE_loss (dino.py:1091-1128): symmetric CE over S = n(i) n(a)^T / tau."""
-        ws = self.ws
-        ni, na = ws.get("nce.ni", B * P), ws.get("nce.na", B * P)
-        nri, nra = ws.get("nce.nri", B), ws.get("nce.nra", B)
-        ops.l2norm_fwd(zi, ni, nri, B, P)
-        ops.l2norm_fwd(za, na, nra, B, P)
-        S = ws.get("nce.S", B * B)
-        ops.gemm(B, B, P, ni, P, 1, na, 1, P, S, B, alpha=1.0 / temperature, mode=self.gm)
-        dS = ws.get("nce.dS", B * B)
-        parts = ws.get("nce.parts", 2 * B)
-        ops.softmax_xent(S, B, B, B, None, 1, False, False, 0.5 / B, parts[:B], dS, B, False)
-        ops.softmax_xent(S, B, B, B, None, 1, True, False, 0.5 / B, parts[B:], dS, B, True)
-        ops.sum_to(parts, 2 * B, 0.5 / B, aux[:1])
+        """infoNCE_loss (dino.py:1091-1128): symmetric CE over S = n(i) n(a)^T / tau, with the
+        other ranks' rows as extra negatives when negatives == "global" (contrastive.py)."""
+        parts = self.ws.get("nce.parts", 2 * B)
+        scale = contrastive.infonce(self.ws, zi, za, B, P, dzi, dza, parts, temperature, self.gm,
+                                    self.group, local=self.negatives == "local")
+        ops.sum_to(parts, 2 * B, scale, aux[:1])
         aux[1:].zero_()
-        dni, dna = ws.get("nce.dni", B * P), ws.get("nce.dna", B * P)
-        ops.gemm(B, P, B, dS, B, 1, na, P, 1, dni, P, alpha=1.0 / temperature, mode=self.gm)
-        ops.gemm(B, P, B, dS, 1, B, ni, P, 1, dna, P, alpha=1.0 / temperature, mode=self.gm)
-        ops.l2norm_bwd(ni, nri, dni, dzi, B, P)
-        ops.l2norm_bwd(na, nra, dna, dza, B, P)
 
     def _supervised(self, zi, za, labels, B, C, aux, dzi, dza):
         """supervised_loss (dino.py:1001-1025): CE(image) + CE(audio), mean over the batch."""
@@ -606,3 +597,118 @@ class UniModalEngine:
         B, V, G, P = c["B"], c["V"], c["G"], self.P
         return (c["s_proj"].view(V, B, P), c["t_proj"].view(G, B, P) - self.store["center"].view(1, 1, P),
                 c["emb"].view(V, B, -1))
+
+
+# ============================================================================ multimodal SimCLR
+class SimCLREngine:
+    """Training step of MultiModalSimCLRLightning (other_ssl/multimodal_simclr/
+    multimodal_simclr.py:22-112): a host-drawn modality pair per step (0 image/image,
+    1 audio/audio, 2 image/audio, 3 audio/image; torch.randint(0, 4), line 34), the towers
+    ImageEncoder / SpectrogramEncoder + ProjectionHead(D, P) (lines 12-20), NT-Xent over
+    [z1; z2] (tau 0.07, lines 74-89) with local or all-gathered global negatives
+    (contrastive.py), and Adam without weight decay (lines 103-112) stepped ONLY on the tower(s)
+    used this step: torch.optim.Adam skips parameters whose grad is None, each keeping its own
+    step count, so the image and audio arenas carry separate bias-correction counters.
+    Same-tower modes run both views through one launch per layer with two BatchNorm groups
+    (two separate module calls in the reference)."""
+
+    GROUPS = ("image_", "audio_")
+
+    def __init__(self, store, D, P, hp, act_dtype=F32, temperature=0.07, negatives="global",
+                 group=None, grad_hook=None, seed=1234):
+        self.store, self.D, self.P, self.hp = store, D, P, hp
+        self.act = act_dtype
+        self.gm = ops.GEMM_BF16_MFMA if act_dtype == torch.bfloat16 else ops.GEMM_F32_MFMA
+        self.ws = Workspace(store.device)
+        self.towers = (
+            (UniEncoder("image_simple", "image_encoder", act_dtype, self.gm),
+             ProjHead("image_projection_head", D, P, gemm_mode=self.gm)),
+            (UniEncoder("spectrogram_simple", "audio_encoder", act_dtype, self.gm),
+             ProjHead("audio_projection_head", D, P, gemm_mode=self.gm)))
+        self.temperature, self.negatives, self.group = temperature, negatives, group
+        self.grad_hook = grad_hook
+        self.gen = torch.Generator().manual_seed(seed)
+        self.adam_t = [0, 0]
+        self.ranges = [store.group_range(i) for i in range(2)]
+        self.last = {}
+
+    def draw_mode(self):
+        return int(torch.randint(0, 4, (1,), generator=self.gen).item())
+
+    def _stage(self, tag, views, tower):
+        enc = self.towers[tower][0]
+        HW = enc.hw * enc.hw
+        B = views[0].shape[0]
+        x = self.ws.get(tag, len(views) * B * HW, self.act)
+        ops.stage_views(views[0].contiguous(), 1, views[1].contiguous() if len(views) > 1 else None,
+                        len(views) - 1, None, B, HW, x)
+        return x
+
+    def forward(self, batch, mode=None):
+        """batch: img1/spec1/img2/spec2 device tensors [B,1,H,W].  Returns the loss tensor."""
+        ws, st, P = self.ws, self.store, self.P
+        mode = self.draw_mode() if mode is None else int(mode)
+        B = batch["img1"].shape[0]
+        reps = ws.get("reps", 2 * B * P)
+        calls = []   # (tower, rows slice start, n rows, groups, encoder ctx, head ctx)
+        if mode in (0, 1):
+            t = mode
+            k1, k2 = ("img1", "img2") if t == 0 else ("spec1", "spec2")
+            x = self._stage("in.x0", (batch[k1], batch[k2]), t)
+            enc, head = self.towers[t]
+            emb, ectx = enc.forward(ws, st, "e0", x, 2 * B, 2, need_dgrad=True)
+            hctx = head.forward(ws, st, "h0", emb, 2 * B, reps, 0.0, 0, G=2)
+            calls.append((t, 0, 2 * B, ectx, hctx))
+        else:
+            order = (0, 1) if mode == 2 else (1, 0)
+            for j, t in enumerate(order):
+                key = ("img" if t == 0 else "spec") + str(j + 1)
+                x = self._stage(f"in.x{j}", (batch[key],), t)
+                enc, head = self.towers[t]
+                emb, ectx = enc.forward(ws, st, f"e{j}", x, B, 1, need_dgrad=True)
+                hctx = head.forward(ws, st, f"h{j}", emb, B, reps[j * B * P:(j + 1) * B * P], 0.0, 0)
+                calls.append((t, j * B, B, ectx, hctx))
+        parts = ws.get("ntx.parts", 2 * B)
+        dreps = ws.get("dreps", 2 * B * P)
+        scale = contrastive.nt_xent(ws, reps, B, P, dreps, parts, self.temperature, self.gm,
+                                    self.group, local=self.negatives == "local")
+        loss = ws.get("loss", 1)
+        ops.sum_to(parts, 2 * B, scale, loss)
+        self.last = dict(B=B, mode=mode, calls=calls, reps=reps, dreps=dreps, loss=loss)
+        return loss
+
+    def backward(self):
+        ws, st, c = self.ws, self.store, self.last
+        P, D = self.P, self.D
+        for t, r0, n, ectx, hctx in c["calls"]:
+            enc, head = self.towers[t]
+            demb = ws.get("demb", n * D)
+            head.backward(ws, st, hctx, c["dreps"][r0 * P:(r0 + n) * P], demb)
+            enc.backward(ws, st, ectx, demb)
+
+    def used_towers(self):
+        return sorted({t for t, *_ in self.last["calls"]})
+
+    def adam(self):
+        """Adam(lr), no weight decay, on the used towers with their own step counters."""
+        b1, b2 = self.hp.betas
+        st = self.store
+        for t in self.used_towers():
+            self.adam_t[t] += 1
+            k = self.adam_t[t]
+            o, n = self.ranges[t]
+            ops.adam(st.student[o:o + n], st.grad[o:o + n], st.adam_m[o:o + n], st.adam_v[o:o + n],
+                     n, self.hp.lr, b1, b2, self.hp.eps, 0.0, 1 - b1 ** k, 1 - b2 ** k)
+
+    def step(self, batch, mode=None):
+        loss = self.forward(batch, mode)
+        self.backward()
+        if self.grad_hook is not None:
+            self.grad_hook(self.store.grad)
+        self.adam()
+        return loss
+
+    def outputs(self):
+        c = self.last
+        B, P = c["B"], self.P
+        return c["reps"][:B * P].view(B, P), c["reps"][B * P:].view(B, P)

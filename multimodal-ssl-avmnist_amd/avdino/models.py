@@ -22,9 +22,9 @@ import math
 import torch
 
 from . import ops
-from .engine import Hyper, MultiCentralEngine, UniModalEngine, adam_step, ema_step
+from .engine import Hyper, MultiCentralEngine, SimCLREngine, UniModalEngine, adam_step, ema_step
 from .params import ParamStore
-from .spec import HEAD_NAMES, multimodal_dino_sd, unimodal_dino_sd
+from .spec import HEAD_NAMES, multimodal_dino_sd, simclr_sd, unimodal_dino_sd
 
 _DT = {"bf16": torch.bfloat16, "16-mixed": torch.bfloat16, "bf16-mixed": torch.bfloat16,
        "32": torch.float32, "fp32": torch.float32, "f32": torch.float32}
@@ -574,3 +574,131 @@ class UniModalDINOLightning(MultiModalDINOLightning):
 
 UNIMODAL_MODEL_MAP = {"image_simple": ImageEncoder, "spectrogram_simple": SpectrogramEncoder,
                       "spectrogram_central": SpectrogramEncoderCentral}
+
+
+
+# ============================================================================ multimodal SimCLR
+class MultiModalSimCLRModel:
+    """other_ssl/multimodal_simclr/multimodal_simclr.py:12-47 on the HIP engine: ImageEncoder +
+    SpectrogramEncoder towers with ProjectionHead(output_dim, projection_dim) each."""
+
+    def __init__(self, output_dim=256, projection_dim=256, device=None, precision="bf16", seed=0,
+                 negatives="global", mode_seed=1234):
+        self.output_dim, self.projection_dim = output_dim, projection_dim
+        self.device = _device(device)
+        self.store = ParamStore(simclr_sd(output_dim, projection_dim), self.device, seed=seed,
+                                has_teacher=False, groups=SimCLREngine.GROUPS)
+        self.hp = Hyper(weight_decay=0.0)
+        self.engine = None
+        if self.device.type == "cuda":
+            self.engine = SimCLREngine(self.store, output_dim, projection_dim, self.hp,
+                                       act_dtype=_DT[precision], negatives=negatives, seed=mode_seed)
+        self.training = True
+
+    train, eval = MultiModalDINO.train, MultiModalDINO.eval
+    state_dict, load_state_dict = MultiModalDINO.state_dict, MultiModalDINO.load_state_dict
+    named_parameters, parameters = MultiModalDINO.named_parameters, MultiModalDINO.parameters
+    _need_engine = MultiModalDINO._need_engine
+
+    @staticmethod
+    def _batch_dict(batch):
+        img1, spec1, img2, spec2 = batch
+        return {"img1": img1, "spec1": spec1, "img2": img2, "spec2": spec2}
+
+    def forward(self, batch, mode=None):
+        """batch = (aug_img1, aug_spec1, aug_img2, aug_spec2) -> (z1, z2) [B, projection_dim]."""
+        eng = self._need_engine()
+        eng.forward({k: v.to(self.device).float() for k, v in self._batch_dict(batch).items()}, mode)
+        z1, z2 = eng.outputs()
+        return z1.clone(), z2.clone()
+
+    __call__ = forward
+
+
+class _NtXentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, reps, temperature):
+        from . import contrastive
+        from .engine import Workspace
+        N, P = reps.shape
+        B = N // 2
+        ws = Workspace(reps.device)
+        parts = torch.empty(N, device=reps.device)
+        d = torch.empty(N * P, device=reps.device)
+        scale = contrastive.nt_xent(ws, reps.detach().float().contiguous().view(-1), B, P, d, parts,
+                                    temperature, local=True)
+        loss = torch.empty(1, device=reps.device)
+        ops.sum_to(parts, N, scale, loss)
+        ctx.save_for_backward(d.view(N, P))
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        (d,) = ctx.saved_tensors
+        return d * g, None
+
+
+class MultiModalSimCLRLightning:
+    """multimodal_simclr.py:49-112: training_step = forward (random modality pair) + NT-Xent;
+    backward_and_step() = backward + Adam(lr) on the used towers (Lightning's automatic
+    optimisation); CosineAnnealingLR(T_max=num_epochs) per epoch."""
+
+    def __init__(self, projection_dim=256, output_dim=256, learning_rate=0.0001, num_epochs=100,
+                 use_mixed_precision=True, device=None, precision=None, seed=0, negatives="global",
+                 mode_seed=1234):
+        self.hparams = dict(projection_dim=projection_dim, output_dim=output_dim,
+                            learning_rate=learning_rate, num_epochs=num_epochs,
+                            use_mixed_precision=use_mixed_precision)
+        self.output_dim, self.projection_dim = output_dim, projection_dim
+        self.learning_rate, self.num_epochs = learning_rate, num_epochs
+        self.precision = precision or ("bf16" if use_mixed_precision else "32")
+        self.model = MultiModalSimCLRModel(output_dim, projection_dim, device, self.precision, seed,
+                                           negatives, mode_seed)
+        self.model.hp.lr = learning_rate
+        self.logged = {}
+        self._optim = None
+
+    def forward(self, batch):
+        return self.model(batch)
+
+    def nt_xent_loss(self, reps, temperature=0.07):
+        """multimodal_simclr.py:74-89 (fused HIP kernels; differentiable w.r.t. reps)."""
+        return _NtXentFn.apply(reps, temperature)
+
+    def log(self, name, value, **kw):
+        self.logged[name] = value
+
+    def training_step(self, batch, batch_idx):
+        eng = self.model._need_engine()
+        b = {k: v.to(self.model.device, non_blocking=True).float()
+             for k, v in self.model._batch_dict(batch).items()}
+        loss = eng.forward(b)
+        self.log("train_loss", loss)
+        return loss
+
+    def backward_and_step(self, optimizer=None):
+        eng = self.model._need_engine()
+        eng.backward()
+        if eng.grad_hook is not None:
+            eng.grad_hook(self.model.store.grad)
+        opt = optimizer or self.configure_optimizers()["optimizer"]
+        self.model.hp.lr = opt.param_groups[0]["lr"]
+        eng.adam()
+
+    def configure_optimizers(self):
+        if self._optim is None:
+            opt = FlatAdam(self.model.store, self.model.hp)
+            self._optim = {"optimizer": opt,
+                           "lr_scheduler": {"scheduler": CosineAnnealingLR(opt, T_max=self.num_epochs),
+                                            "monitor": "train_loss"}}
+        return self._optim
+
+    def state_dict(self):
+        return {"model." + k: v for k, v in self.model.state_dict().items()}
+
+    def load_state_dict(self, sd, strict=True):
+        self.model.load_state_dict({k[len("model."):]: v for k, v in sd.items() if k.startswith("model.")},
+                                   strict)
+
+    def parameters(self):
+        return self.model.parameters()

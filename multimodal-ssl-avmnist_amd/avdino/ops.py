@@ -417,6 +417,12 @@ def adamw(p_, g, m, v, n, lr, b1, b2, eps, wd, bc1, bc2):
     call("avd_adamw", p(p_), p(g), p(m), p(v), n, lr, b1, b2, eps, wd, bc1, bc2, stream())
 
 
+def axpy(y, x, a=1.0):
+    """y += a*x (contiguous f32, same numel)."""
+    _need(y.numel() == x.numel() and y.dtype == x.dtype == torch.float32, "axpy operands")
+    call("avd_axpy", p(y), p(x), y.numel(), a, stream())
+
+
 def sum_to(x, n, scale, out):
     call("avd_sum", p(x), n, scale, p(out), stream())
 

@@ -45,7 +45,10 @@ def _teacher_of(key):
 
 
 class ParamStore:
-    def __init__(self, sd_spec, device, seed=0, has_teacher=True):
+    def __init__(self, sd_spec, device, seed=0, has_teacher=True, groups=None):
+        """groups: optional list of key prefixes; the head parameters are laid out group by
+        group in that order (each group one contiguous range, see group_range), e.g. SimCLR's
+        image and audio towers, which Adam steps independently."""
         self.spec = OrderedDict(sd_spec)
         self.device = torch.device(device)
         keys = [k for k, (_s, kind) in self.spec.items() if _is_param(kind)]
@@ -63,6 +66,14 @@ class ParamStore:
                 o += -(-n // ALIGN) * ALIGN
             return offs, o
 
+        self.groups = list(groups or [])
+        if self.groups:
+            def gidx(k):
+                for i, g in enumerate(self.groups):
+                    if k.startswith(g):
+                        return i
+                return len(self.groups)
+            heads = sorted(heads, key=gidx)   # stable: spec order inside a group
         s_order = heads + ema_live + ema_dead
         self.s_offs, s_total = layout(s_order)
         self.n_heads = sum(-(-self.s_offs[k][1] // ALIGN) * ALIGN for k in heads)
@@ -93,6 +104,13 @@ class ParamStore:
             elif kind == "nbt":
                 self.buffers[k] = torch.zeros(shape, dtype=torch.int64, device=self.device)
         self.reset_parameters(seed)
+
+    def group_range(self, i):
+        """(offset, length) of head group i in the student / grad / Adam arenas."""
+        keys = [k for k in self.live_keys if k.startswith(self.groups[i])]
+        lo = min(self.s_offs[k][0] for k in keys)
+        hi = max(self.s_offs[k][0] + -(-self.s_offs[k][1] // ALIGN) * ALIGN for k in keys)
+        return lo, hi - lo
 
     # ------------------------------------------------------------------ views
     def _view(self, arena, offs, key):

@@ -73,6 +73,22 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     adam1<DECOUPLED>(p[i], g[i], m[i], v[i], lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2);
 }
 
+__global__ __launch_bounds__(256) void axpy_kernel(float* __restrict__ y, const float* __restrict__ x,
+                                                   long long n, float a) {
+  const long long n4 = n / 4;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    float4 yy = reinterpret_cast<float4*>(y)[i];
+    const float4 xx = reinterpret_cast<const float4*>(x)[i];
+    yy.x = fmaf(a, xx.x, yy.x);
+    yy.y = fmaf(a, xx.y, yy.y);
+    yy.z = fmaf(a, xx.z, yy.z);
+    yy.w = fmaf(a, xx.w, yy.w);
+    reinterpret_cast<float4*>(y)[i] = yy;
+  }
+  for (long long i = n4 * 4 + blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    y[i] = fmaf(a, x[i], y[i]);
+}
+
 inline int stream_grid(long long n) {
   long long b = (n / 4 + 255) / 256;
   if (b > 4096) b = 4096;
@@ -106,6 +122,15 @@ int avd_adam(float* p, const float* g, float* m, float* v, long long n, float lr
   if (n == 0) return AVD_OK;
   adam_kernel<false><<<stream_grid(n), 256, 0, avd_stream(stream)>>>(p, g, m, v, n, lr, b1, b2, eps,
                                                                      wd, 1.f / bc1, 1.f / sqrtf(bc2));
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_axpy(float* y, const float* x, long long n, float a, void* stream) {
+  if (!y || !x) return AVD_ERR_ARG;
+  if (n < 0 || !aligned16(y) || !aligned16(x)) return AVD_ERR_SHAPE;
+  if (n == 0) return AVD_OK;
+  axpy_kernel<<<stream_grid(n), 256, 0, avd_stream(stream)>>>(y, x, n, a);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

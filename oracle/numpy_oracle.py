@@ -677,12 +677,19 @@ def unimodal_image_step(P, batch, hp):
     return unimodal_step(P, batch, hp, "image", 0.0)
 
 
-def simclr_step(P, batch, mode, temperature=0.07):
+def simclr_step(P, batch, mode, temperature=0.07, shards=1):
     """MultiModalSimCLRModel.forward + nt_xent_loss (multimodal_simclr.py:22-47, 74-89)
-    for a pinned modality mode (0 img/img, 1 aud/aud, 2 img/aud, 3 aud/img)."""
+    for a pinned modality mode (0 img/img, 1 aud/aud, 2 img/aud, 3 aud/img).
+
+    shards > 1 restates the data-parallel run with GLOBAL negatives: the batch
+    is split into `shards` rank-local batches, each encoded with its own BatchNorm statistics,
+    NT-Xent is taken over the concatenated global [z1 of all shards; z2 of all shards], and
+    the parameter gradient is the sum over shards (= DDP's average of per-rank local-mean
+    losses).  bn_stats lists, per encoder call in call order, (bn key, stats) pairs."""
     from .spec import CNN3_IMAGE, CNN3_AUDIO
     P = {k: np.asarray(v, F64) if np.asarray(v).dtype != np.int64 else np.asarray(v) for k, v in P.items()}
     grads = {}
+    stats = []
 
     def image_enc(x):
         e = Branch(cnn3_stack(CNN3_IMAGE, "image_encoder.encoder"), "image_encoder.encoder.14")
@@ -690,6 +697,7 @@ def simclr_step(P, batch, mode, temperature=0.07):
         o = linear_fwd(f, P["image_encoder.projection.0.weight"], P["image_encoder.projection.0.bias"])
         h = ProjHead("image_projection_head")
         z, hc = h.forward(P, o)
+        stats.append(list(_branch_stats(c)) + [("image_projection_head.mlp.1", hc[-1])])
 
         def bwd(dz):
             do = h.backward(P, dz, hc, grads)
@@ -704,20 +712,31 @@ def simclr_step(P, batch, mode, temperature=0.07):
         f, c = e.forward(P, x, 1)
         h = ProjHead("audio_projection_head")
         z, hc = h.forward(P, f)
+        stats.append(list(_branch_stats(c)) + [("audio_projection_head.mlp.1", hc[-1])])
 
         def bwd(dz):
             do = h.backward(P, dz, hc, grads)
             e.backward(P, do, c, grads)
         return z, bwd
 
-    i1, s1 = batch["img1"].astype(F64), batch["spec1"].astype(F64)
-    i2, s2 = batch["img2"].astype(F64), batch["spec2"].astype(F64)
     f1 = image_enc if mode in (0, 2) else audio_enc
     f2 = image_enc if mode in (0, 3) else audio_enc
-    z1, b1 = f1(i1 if f1 is image_enc else s1)
-    z2, b2 = f2(i2 if f2 is image_enc else s2)
-    B = z1.shape[0]
-    loss, dr = nt_xent_loss(np.concatenate([z1, z2]), temperature)
-    b1(dr[:B])
-    b2(dr[B:])
-    return {"loss": loss, "z1": z1, "z2": z2, "grads": grads}
+    Bt = batch["img1"].shape[0]
+    B = Bt // shards
+    z1s, z2s, bw = [], [], []
+    for r in range(shards):
+        sl = slice(r * B, (r + 1) * B)
+        i1, s1 = batch["img1"][sl].astype(F64), batch["spec1"][sl].astype(F64)
+        i2, s2 = batch["img2"][sl].astype(F64), batch["spec2"][sl].astype(F64)
+        z1, b1 = f1(i1 if f1 is image_enc else s1)
+        z2, b2 = f2(i2 if f2 is image_enc else s2)
+        z1s.append(z1)
+        z2s.append(z2)
+        bw.append((b1, b2))
+    Z1, Z2 = np.concatenate(z1s), np.concatenate(z2s)
+    loss, dr = nt_xent_loss(np.concatenate([Z1, Z2]), temperature)
+    # per-shard local-mean losses averaged by DDP == the global mean: dr is already global
+    for r, (b1, b2) in enumerate(bw):
+        b1(dr[r * B:(r + 1) * B])
+        b2(dr[Bt + r * B:Bt + (r + 1) * B])
+    return {"loss": loss, "z1": Z1, "z2": Z2, "grads": grads, "bn_stats": stats}
