@@ -280,6 +280,11 @@ int avd_softmax_xent(const float* logits, long long ld, int R, int C, const int6
                      float* loss_parts, float* dlogits, long long ldd, int accumulate,
                      void* stream);
 
+/* correct[r] = 1.0f if argmax_j logits[r*ld + j] (first maximum, as torch.max) == targets[r],
+ * else 0.0f -- the probe accuracy of evaluate() (dino.py:913-947). */
+int avd_argmax_correct(const float* logits, long long ld, int R, int C, const int64_t* targets,
+                       float* correct, void* stream);
+
 /* Cosine-consistency term of the unimodal DINO loss (UniModalDINOLightning.
  * _cosine_consistency_loss, dino.py:1575-1594) over view-major embeddings emb [V*B, D]:
  * loss_parts [B] = alpha * per-sample share of mean_{i<j} mean_b (1 - n_i.n_j)^2 with
@@ -312,6 +317,12 @@ int avd_adam(float* p, const float* g, float* m, float* v, long long n, float lr
  * the optimiser of the epoch-end linear probe (on_train_epoch_end, dino.py:898, 1678). */
 int avd_adamw(float* p, const float* g, float* m, float* v, long long n, float lr, float b1,
               float b2, float eps, float wd, float bc1, float bc2, void* stream);
+
+/* Eval-mode BatchNorm coefficients from running statistics: scale = gamma / sqrt(rv + eps),
+ * shift = beta - rm * scale, [C] each (feed avd_cl_bn_relu_pool with G = 1). */
+int avd_bn_eval_coef(const float* gamma, const float* beta, const float* running_mean,
+                     const float* running_var, float eps, int C, float* scale, float* shift,
+                     void* stream);
 
 /* y += a*x over n floats (16-byte aligned): folds a scattered gradient slab into the local one
  * (global-negative contrastive losses, avdino/contrastive.py). */

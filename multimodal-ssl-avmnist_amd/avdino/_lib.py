@@ -62,6 +62,8 @@ PROTOS = {
     "avd_adam": [P, P, P, P, L, F, F, F, F, F, F, F, P],
     "avd_adamw": [P, P, P, P, L, F, F, F, F, F, F, F, P],
     "avd_axpy": [P, P, L, F, P],
+    "avd_bn_eval_coef": [P, P, P, P, F, I, P, P, P],
+    "avd_argmax_correct": [P, L, I, I, P, P, P],
     "avd_sum": [P, I, F, P, P],
     "avd_stage_views": [P, I, P, I, P, I, I, P, I, P],
 }

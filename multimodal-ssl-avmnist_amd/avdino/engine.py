@@ -112,6 +112,31 @@ class ConvBranch:
             h = out
         return h.view(N, -1), ctx
 
+    def forward_eval(self, ws, store, tag, x, N):
+        """Eval-mode forward (nn.Module.eval(): BatchNorm from the running statistics, no
+        statistics pass, nothing saved) -> features f32 [N, F]."""
+        wts = self.prepare(ws, store, tag, False)
+        h = x
+        nl = len(self.stack.convs)
+        for i, (ci, co, k, pad) in enumerate(self.stack.convs):
+            H, Ho, Hp = self.dims[i]
+            y = ws.get(f"{tag}.y{i}", N * Ho * Ho * co, self.act)
+            ops.cl_conv_fwd(h, wts[i][0], store[self.stack.conv_keys[i] + ".bias"], y, None,
+                            N, N, ci, H, H, co, k, pad)
+            bk = self.stack.bn_keys[i]
+            coef = ws.get(f"{tag}.ev{i}", 2 * co).view(2, co)
+            ops.bn_eval_coef(store[bk + ".weight"], store[bk + ".bias"], store[bk + ".running_mean"],
+                             store[bk + ".running_var"], coef[0], coef[1])
+            if i == nl - 1:
+                mode = self._tail_mode()
+                out = ws.get(f"{tag}.feat", N * co * (1 if mode == 1 else Hp * Hp), F32)
+            else:
+                mode = 0
+                out = ws.get(f"{tag}.x{i + 1}", N * Hp * Hp * co, self.act)
+            ops.cl_bn_relu_pool(y, coef[0], coef[1], out, mode, N, N, co, Ho, Ho)
+            h = out
+        return h.view(N, -1)
+
     def backward(self, ws, store, ctx, dfeat):
         """dfeat: f32 [N, F] gradient of the features; writes conv/BN parameter grads."""
         N, G = ctx["N"], ctx["G"]
@@ -487,6 +512,15 @@ class UniEncoder:
             acts.append(out)
             h = out
         return h.view(N, -1), (ctx, acts)
+
+    def forward_eval(self, ws, store, tag, x, N):
+        h = self.branch.forward_eval(ws, store, tag, x, N)
+        for i, k in enumerate(self.lins):
+            w = store[k + ".weight"]
+            out = ws.get(f"{tag}.lin{i}", N * w.shape[0])
+            ops.linear_fwd(h, w, store[k + ".bias"], out, N, mode=self.gm)
+            h = out
+        return h.view(N, -1)
 
     def backward(self, ws, store, ctx, dout):
         bctx, acts = ctx

@@ -366,6 +366,27 @@ class MultiModalDINOLightning:
     def forward(self, batch):
         return self.model(batch)
 
+    def _probe_kind(self):
+        enc = self.model.student_spec
+        return getattr(enc, "kind", None) or enc.arch
+
+    def on_train_epoch_end(self, traindata=None, validdata=None):
+        """Linear probe (dino.py:878-951 / 1670-1735) over iterables of (images, audios,
+        labels) device batches (the reference's AVMNIST loaders, batch 128); logs val_loss and
+        mlp_acc.  No data: nothing to do (the on-disk loader is outside the hot path)."""
+        if traindata is None or validdata is None:
+            return None
+        from .probe import LinearProbe
+        m = self.model
+        probe = LinearProbe(m.store, self._probe_kind(), m.output_dim,
+                            getattr(m, "encoder_output_dim", None), lr=self.learning_rate,
+                            act_dtype=_DT[self.precision],
+                            fusion_dropout=getattr(m.hp, "fusion_dropout", 0.3))
+        out = probe.run_epoch(traindata, validdata)
+        self.log("val_loss", out["val_loss"])
+        self.log("mlp_acc", out["mlp_acc"])
+        return out
+
     def state_dict(self):
         return {"model." + k: v for k, v in self.model.state_dict().items()}
 

@@ -417,6 +417,18 @@ def adamw(p_, g, m, v, n, lr, b1, b2, eps, wd, bc1, bc2):
     call("avd_adamw", p(p_), p(g), p(m), p(v), n, lr, b1, b2, eps, wd, bc1, bc2, stream())
 
 
+def bn_eval_coef(gamma, beta, rm, rv, scale, shift, eps=1e-5):
+    C = gamma.numel()
+    _need(all(t.numel() >= C for t in (beta, rm, rv, scale, shift)), "bn eval coef")
+    call("avd_bn_eval_coef", p(gamma), p(beta), p(rm), p(rv), eps, C, p(scale), p(shift), stream())
+
+
+def argmax_correct(logits, ld, R, C, targets, correct):
+    _need(logits.numel() >= (R - 1) * ld + C and targets.numel() >= R and correct.numel() >= R,
+          "argmax shapes")
+    call("avd_argmax_correct", p(logits), ld, R, C, p(targets), p(correct), stream())
+
+
 def axpy(y, x, a=1.0):
     """y += a*x (contiguous f32, same numel)."""
     _need(y.numel() == x.numel() and y.dtype == x.dtype == torch.float32, "axpy operands")

@@ -1,0 +1,193 @@
+"""Epoch-end linear probe (BASELINE config 5's "linear-probe eval"):
+``on_train_epoch_end`` of the DINO Lightning modules (models/dino.py:878-951 multimodal,
+1670-1735 unimodal) with ``DownstreamClassifier`` (1764-1814), on libavdino kernels.
+
+Reference semantics kept:
+  * the encoder is a frozen DEEP COPY of the student (here: a second ParamStore filled from the
+    student arena and buffer arena) -- nothing the probe does touches the trained model;
+  * ``model_downstream.train()`` puts the copy in TRAIN mode for the probe epoch: batch-stat
+    BatchNorm whose running statistics update the copy, and the CentralNet fusion dropout
+    (0.3) active; the copy gets no gradient (torch.no_grad);
+  * classifier Linear(output_dim, 128) - ReLU - Linear(128, 10), default init, trained with
+    AdamW(lr = learning_rate, weight_decay 0.01) one step per batch; ``val_loss`` = the mean
+    training loss of the epoch;
+  * ``evaluate()`` puts the copy in EVAL mode (running statistics, no dropout): mean CE over
+    the batches and ``mlp_acc`` = 100 * correct / total with torch.max's first-maximum argmax.
+The reference runs the probe under fp16 autocast + GradScaler on CUDA; here the classifier is
+fp32 (the GradScaler only matters on overflow) and the encoder copy runs in the engine's
+activation dtype.  Per-batch losses stay on the device (no host sync inside the epoch).
+"""
+import torch
+
+from . import ops
+from .engine import F32, ConvBranch, UniEncoder, Workspace
+from .params import ParamStore
+from .spec import CENTRAL_AUDIO_CONVS, CENTRAL_IMAGE_CONVS, UNI_ALIASES, UNI_ENCODERS, central_stack
+
+from collections import OrderedDict
+
+
+def classifier_sd(D, hidden=128, num_classes=10):
+    sd = OrderedDict()
+    sd["classifier.0.weight"] = ((hidden, D), "w")
+    sd["classifier.0.bias"] = ((hidden,), "b")
+    sd["classifier.2.weight"] = ((num_classes, hidden), "w")
+    sd["classifier.2.bias"] = ((num_classes,), "b")
+    return sd
+
+
+class _CentralEncoder:
+    """The multimodal student (CentralMultiModalEncoder.forward, dino.py:229-234, 454-468)
+    without gradients: both LeNet branches, their Linears into the cat buffer, fusion."""
+
+    def __init__(self, E, D, act, gm, fusion_dropout):
+        self.E, self.D, self.gm, self.p = E, D, gm, fusion_dropout
+        self.img = ConvBranch(central_stack("student.image_encoder.0", CENTRAL_IMAGE_CONVS, 28), act)
+        self.aud = ConvBranch(central_stack("student.audio_encoder.0", CENTRAL_AUDIO_CONVS, 112), act)
+
+    def __call__(self, ws, st, x_img, x_aud, N, train, seed):
+        E = self.E
+        if train:
+            fi, _ = self.img.forward(ws, st, "pi", x_img, N, 1, True, False)
+            fa, _ = self.aud.forward(ws, st, "pa", x_aud, N, 1, True, False)
+        else:
+            fi = self.img.forward_eval(ws, st, "pi", x_img, N)
+            fa = self.aud.forward_eval(ws, st, "pa", x_aud, N)
+        cat = ws.get("p.cat", N * 2 * E)
+        ops.linear_fwd(fi, st["student.image_encoder.1.weight"], st["student.image_encoder.1.bias"],
+                       cat, N, out_ld=2 * E, out_off=0, mode=self.gm)
+        ops.linear_fwd(fa, st["student.audio_encoder.1.weight"], st["student.audio_encoder.1.bias"],
+                       cat, N, out_ld=2 * E, out_off=E, mode=self.gm)
+        h = ws.get("p.fh", N * E)
+        ops.linear_fwd(cat, st["student.fusion.0.weight"], st["student.fusion.0.bias"], h, N,
+                       x_ld=2 * E, mode=self.gm)
+        r = ws.get("p.fr", N * E)
+        ops.act_fwd(h, r, 0, None, None, N, 1, E, self.p if train else 0.0, seed)
+        out = ws.get("p.feat", N * self.D)
+        ops.linear_fwd(r, st["student.fusion.3.weight"], st["student.fusion.3.bias"], out, N,
+                       mode=self.gm)
+        return out
+
+
+class _UniEncoder:
+    def __init__(self, kind, act, gm):
+        self.enc = UniEncoder(kind, "student", act, gm)
+
+    def __call__(self, ws, st, x, N, train):
+        if train:
+            out, _ = self.enc.forward(ws, st, "pu", x, N, 1, False)
+            return out
+        return self.enc.forward_eval(ws, st, "pu", x, N)
+
+
+class LinearProbe:
+    """One probe epoch over a trained DINO model's student.
+
+    source: the trained model's ParamStore (MultiModalDINO*.store / UniModalDINO.store);
+    kind: "multi_central" or an UNIMODAL_MODEL_MAP key; E/D: encoder_output_dim / output_dim.
+    """
+
+    def __init__(self, source, kind, D, E=None, lr=1e-4, weight_decay=0.01, act_dtype=F32,
+                 fusion_dropout=0.3, seed=0, classifier_state=None):
+        dev = source.device
+        self.store = ParamStore(source.spec, dev, has_teacher=source.teacher is not None)
+        self.store.student.copy_(source.student)          # copy.deepcopy(model.student)
+        self.store.buf_arena.copy_(source.buf_arena)
+        for k, b in source.buffers.items():
+            if k.endswith("num_batches_tracked"):
+                self.store.buffers[k].copy_(b)
+        self.kind = UNI_ALIASES.get(kind, kind)
+        self.D = D
+        self.gm = ops.GEMM_BF16_MFMA if act_dtype == torch.bfloat16 else ops.GEMM_F32_MFMA
+        self.act = act_dtype
+        self.ws = Workspace(dev)
+        if self.kind == "multi_central":
+            self.enc = _CentralEncoder(E, D, act_dtype, self.gm, fusion_dropout)
+        else:
+            self.enc = _UniEncoder(self.kind, act_dtype, self.gm)
+            self.modality = UNI_ENCODERS[self.kind][0]
+        self.cls = ParamStore(classifier_sd(D), dev, seed=seed, has_teacher=False)
+        if classifier_state is not None:
+            self.cls.load_state_dict(classifier_state)
+        self.lr, self.wd = lr, weight_decay
+        self.t = 0
+        self.seed = seed
+
+    def _features(self, images, audios, train):
+        ws, N = self.ws, images.shape[0]
+        if self.kind == "multi_central":
+            xi = ws.get("p.in.img", N * 784, self.act)
+            xa = ws.get("p.in.aud", N * 12544, self.act)
+            ops.stage_views(images.contiguous(), 1, None, 0, None, N, 784, xi)
+            ops.stage_views(audios.contiguous(), 1, None, 0, None, N, 12544, xa)
+            return self.enc(ws, self.store, xi, xa, N, train, self.seed * 7919 + self.t)
+        src, HW = (images, 784) if self.modality == "image" else (audios, 12544)
+        x = ws.get("p.in.x", N * HW, self.act)
+        ops.stage_views(src.contiguous(), 1, None, 0, None, N, HW, x)
+        return self.enc(ws, self.store, x, N, train)
+
+    def _logits(self, feat, N):
+        ws, c = self.ws, self.cls
+        h = ws.get("p.h", N * 128)
+        ops.linear_fwd(feat, c["classifier.0.weight"], c["classifier.0.bias"], h, N)
+        r = ws.get("p.r", N * 128)
+        ops.act_fwd(h, r, 0, None, None, N, 1, 128, 0.0, 0)
+        logits = ws.get("p.logits", N * 10)
+        ops.linear_fwd(r, c["classifier.2.weight"], c["classifier.2.bias"], logits, N)
+        return h, r, logits
+
+    def train_batch(self, images, audios, labels, loss_out):
+        """One classifier step; loss_out: 1-element device slot for this batch's mean CE."""
+        ws, c = self.ws, self.cls
+        N = images.shape[0]
+        feat = self._features(images, audios, True)
+        h, r, logits = self._logits(feat, N)
+        parts, dl = ws.get("p.parts", N), ws.get("p.dl", N * 10)
+        ops.softmax_xent(logits, 10, N, 10, labels, 0, False, False, 1.0 / N, parts, dl, 10, False)
+        ops.sum_to(parts, N, 1.0 / N, loss_out)
+        dr = ws.get("p.dr", N * 128)
+        ops.linear_bwd(dl, r, c["classifier.2.weight"], c.grad_of("classifier.2.weight"),
+                       c.grad_of("classifier.2.bias"), dr, N)
+        dh = ws.get("p.dh", N * 128)
+        ops.act_bwd(h, dr, dh, 0, None, None, N, 1, 128, 0.0, 0)
+        ops.linear_bwd(dh, feat, c["classifier.0.weight"], c.grad_of("classifier.0.weight"),
+                       c.grad_of("classifier.0.bias"), None, N)
+        self.t += 1
+        b1, b2 = 0.9, 0.999
+        ops.adamw(c.student, c.grad, c.adam_m, c.adam_v, c.n_live, self.lr, b1, b2, 1e-8, self.wd,
+                  1 - b1 ** self.t, 1 - b2 ** self.t)
+
+    def evaluate(self, batches):
+        """evaluate() (dino.py:913-947): eval-mode copy; returns (mean loss, accuracy %, logits)."""
+        ws = self.ws
+        losses, correct, logits_all, n = [], [], [], 0
+        for images, audios, labels in batches:
+            N = images.shape[0]
+            feat = self._features(images, audios, False)
+            _, _, logits = self._logits(feat, N)
+            parts = ws.get("p.parts", N)
+            ops.softmax_xent(logits, 10, N, 10, labels, 0, False, False, 1.0 / N, parts, None, 10,
+                             False)
+            l1 = torch.empty(1, device=logits.device)
+            ops.sum_to(parts, N, 1.0 / N, l1)
+            ok = torch.empty(N, device=logits.device)
+            ops.argmax_correct(logits, 10, N, 10, labels, ok)
+            c1 = torch.empty(1, device=logits.device)
+            ops.sum_to(ok, N, 1.0, c1)
+            losses.append(l1)
+            correct.append(c1)
+            logits_all.append(logits.view(N, 10).clone())
+            n += N
+        loss = torch.cat(losses).mean().item()
+        acc = 100.0 * torch.cat(correct).sum().item() / n
+        return loss, acc, torch.cat(logits_all)
+
+    def run_epoch(self, train_batches, valid_batches):
+        """on_train_epoch_end: returns {"val_loss", "mlp_acc", "eval_loss", "train_losses"}."""
+        train_batches = list(train_batches)
+        losses = torch.empty(len(train_batches), device=self.store.device)
+        for i, (images, audios, labels) in enumerate(train_batches):
+            self.train_batch(images, audios, labels, losses[i:i + 1])
+        ev_loss, acc, logits = self.evaluate(valid_batches)
+        return {"val_loss": losses.mean().item(), "mlp_acc": acc, "eval_loss": ev_loss,
+                "train_losses": losses, "logits": logits}

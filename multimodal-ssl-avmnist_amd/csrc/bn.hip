@@ -598,6 +598,20 @@ inline int grid_for(long long total) {
   return (int)b;
 }
 
+// Eval-mode BatchNorm (running statistics) as the per-channel affine the BN/ReLU/pool kernels
+// apply: scale = gamma / sqrt(rv + eps), shift = beta - rm * scale (nn.BatchNorm eval mode; the
+// linear probe's evaluate(), dino.py:913-947).
+__global__ void bn_eval_coef_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                    const float* __restrict__ rm, const float* __restrict__ rv,
+                                    float eps, int C, float* __restrict__ scale,
+                                    float* __restrict__ shift) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const double sc = (double)gamma[c] / sqrt((double)rv[c] + (double)eps);
+  scale[c] = (float)sc;
+  shift[c] = (float)((double)beta[c] - (double)rm[c] * sc);
+}
+
 }  // namespace
 
 extern "C" {
@@ -802,6 +816,17 @@ int avd_sum_rows(const float* in, int rows, int cols, long long ld, float* out, 
   else
     sum_rows_kernel<64><<<avd_cdiv(cols, 64), 1024, 0, avd_stream(stream)>>>(in, rows, cols, ld, out,
                                                                             accumulate);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_bn_eval_coef(const float* gamma, const float* beta, const float* running_mean,
+                     const float* running_var, float eps, int C, float* scale, float* shift,
+                     void* stream) {
+  if (!gamma || !beta || !running_mean || !running_var || !scale || !shift) return AVD_ERR_ARG;
+  if (C <= 0) return AVD_ERR_SHAPE;
+  bn_eval_coef_kernel<<<avd_cdiv(C, 256), 256, 0, avd_stream(stream)>>>(
+      gamma, beta, running_mean, running_var, eps, C, scale, shift);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

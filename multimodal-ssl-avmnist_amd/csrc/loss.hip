@@ -363,6 +363,29 @@ __global__ __launch_bounds__(256) void cosine_consistency_kernel(
   }
 }
 
+// correct[r] = 1 if argmax_j logits[r, j] (first maximum, torch.max semantics) == targets[r]
+__global__ __launch_bounds__(256) void argmax_correct_kernel(const float* __restrict__ logits,
+                                                             long long ld, int R, int C,
+                                                             const int64_t* __restrict__ targets,
+                                                             float* __restrict__ correct) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int l = lane_id();
+  if (r >= R) return;
+  float best = -INFINITY;
+  int bi = C;
+  for (int j = l; j < C; j += 64) {
+    const float v = logits[(size_t)r * ld + j];
+    if (v > best) { best = v; bi = j; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  if (l == 0) correct[r] = bi == (int)targets[r] ? 1.f : 0.f;
+}
+
 }  // namespace
 
 extern "C" {
@@ -425,6 +448,16 @@ int avd_softmax_xent(const float* logits, long long ld, int R, int C, const int6
   softmax_xent_kernel<<<avd_cdiv(R, 4), 256, 0, avd_stream(stream)>>>(
       logits, ld, R, C, targets, target_mode, tgt_off, col_major, mask_off, gscale, loss_parts,
       dlogits, ldd, accumulate);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_argmax_correct(const float* logits, long long ld, int R, int C, const int64_t* targets,
+                       float* correct, void* stream) {
+  if (!logits || !targets || !correct) return AVD_ERR_ARG;
+  if (R <= 0 || C <= 0 || ld < C) return AVD_ERR_SHAPE;
+  argmax_correct_kernel<<<avd_cdiv(R, 4), 256, 0, avd_stream(stream)>>>(logits, ld, R, C, targets,
+                                                                         correct);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

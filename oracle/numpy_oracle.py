@@ -75,6 +75,13 @@ def bn_train_fwd(x, gamma, beta, G, axes):
     return y.reshape(x.shape), cache, stats
 
 
+def bn_eval_fwd(x, gamma, beta, rm, rv):
+    """nn.BatchNorm2d/1d in eval mode: running statistics, channel axis 1."""
+    shape = (1, -1) + (1,) * (x.ndim - 2)
+    return (x - rm.reshape(shape)) / np.sqrt(rv.reshape(shape) + BN_EPS) * gamma.reshape(shape) \
+        + beta.reshape(shape)
+
+
 def bn_train_bwd(dy, cache):
     xhat, invstd, gamma, G, red, shape, xshape = cache
     dys = dy.reshape(xhat.shape)
@@ -180,12 +187,18 @@ class ConvStack:
         self.arch = arch
         self.prefix_fmt = prefix_fmt  # callable(i) -> (conv_key, bn_key)
 
-    def forward(self, P, x, G):
+    def forward(self, P, x, G, eval_mode=False):
+        """eval_mode: BatchNorm from the running statistics (nn.Module.eval()); forward only."""
         caches, stats = [], []
         h = x
         for i, (ci, co, k, pad) in enumerate(self.arch["convs"]):
             ck, bk = self.prefix_fmt(i)
             y, win = conv2d_fwd(h, P[ck + ".weight"], P[ck + ".bias"], pad)
+            if eval_mode:
+                z = bn_eval_fwd(y, P[bk + ".weight"], P[bk + ".bias"], P[bk + ".running_mean"],
+                                P[bk + ".running_var"])
+                h, _ = maxpool2_fwd(np.maximum(z, 0.0))
+                continue
             z, bnc, st = bn_train_fwd(y, P[bk + ".weight"], P[bk + ".bias"], G, axes=(2, 3))
             r = np.maximum(z, 0.0)
             p, pc = maxpool2_fwd(r)
@@ -244,8 +257,8 @@ class Branch:
         self.stack = stack
         self.lin = lin_key
 
-    def forward(self, P, x, G):
-        feat, sc = self.stack.forward(P, x, G)
+    def forward(self, P, x, G, eval_mode=False):
+        feat, sc = self.stack.forward(P, x, G, eval_mode)
         out = linear_fwd(feat, P[self.lin + ".weight"], P[self.lin + ".bias"])
         return out, (feat, sc)
 
@@ -267,9 +280,9 @@ class CentralMultiModal:
         self.img = Branch(lenet_stack(CENTRAL_IMAGE, f"{prefix}.image_encoder.0"), f"{prefix}.image_encoder.1")
         self.aud = Branch(lenet_stack(CENTRAL_AUDIO, f"{prefix}.audio_encoder.0"), f"{prefix}.audio_encoder.1")
 
-    def forward(self, P, img, aud, G, drop_mask=None):
-        fi, ci = self.img.forward(P, img, G)
-        fa, ca = self.aud.forward(P, aud, G)
+    def forward(self, P, img, aud, G, drop_mask=None, eval_mode=False):
+        fi, ci = self.img.forward(P, img, G, eval_mode)
+        fa, ca = self.aud.forward(P, aud, G, eval_mode)
         cat = np.concatenate([fi, fa], axis=1)
         h = linear_fwd(cat, P[self.p + ".fusion.0.weight"], P[self.p + ".fusion.0.bias"])
         r = np.maximum(h, 0.0)
@@ -600,8 +613,8 @@ def uni_encoder(kind, prefix):
     else:
         raise ValueError(kind)
 
-    def fwd(P, x, G):
-        f, c = br.forward(P, x, G)
+    def fwd(P, x, G, eval_mode=False):
+        f, c = br.forward(P, x, G, eval_mode)
         if lin is None:
             return f, (f, c)
         return linear_fwd(f, P[lin + ".weight"], P[lin + ".bias"]), (f, c)
@@ -740,3 +753,64 @@ def simclr_step(P, batch, mode, temperature=0.07, shards=1):
         b1(dr[r * B:(r + 1) * B])
         b2(dr[Bt + r * B:Bt + (r + 1) * B])
     return {"loss": loss, "z1": Z1, "z2": Z2, "grads": grads, "bn_stats": stats}
+
+
+def linear_probe(P, kind, train_batches, valid_batches, cls, lr, wd=0.01):
+    """on_train_epoch_end's linear probe (multimodal dino.py:878-951, unimodal 1670-1735) with
+    DownstreamClassifier (1764-1814): a frozen deep copy of the student encoder, run in TRAIN
+    mode during the probe epoch (batch-stat BatchNorm whose running statistics update the copy;
+    fusion dropout p=0 here), classifier Linear(D,128)-ReLU-Linear(128,10) trained with
+    AdamW(lr, weight_decay=wd) one step per batch, then evaluate() with the copy in eval mode
+    (running statistics).  kind: "multi_central" or an UNIMODAL_MODEL_MAP key.
+    batches: lists of dicts image [B,1,28,28], audio [B,1,112,112], label [B].
+    cls: classifier.{0,2}.{weight,bias}.  Returns per-batch train losses, val_loss (their mean),
+    eval loss / accuracy / logits, the final classifier and the copy's running statistics."""
+    P = {k: np.asarray(v, F64) if np.asarray(v).dtype != np.int64 else np.asarray(v) for k, v in P.items()}
+    C = {k: np.asarray(v, F64) for k, v in cls.items()}
+    if kind == "multi_central":
+        enc = CentralMultiModal("student")
+
+        def run(b, eval_mode):
+            out, cache = enc.forward(P, b["image"].astype(F64), b["audio"].astype(F64), 1,
+                                     eval_mode=eval_mode)
+            return out, (None if eval_mode else _stack_stats(cache))
+    else:
+        fwd, _ = uni_encoder(kind, "student")
+        img = UNI_KINDS.get(kind, kind) == "image_simple"
+
+        def run(b, eval_mode):
+            x = (b["image"] if img else b["audio"]).astype(F64)
+            out, cache = fwd(P, x, 1, eval_mode)
+            return out, (None if eval_mode else _branch_stats(cache[1]))
+    m = {k: np.zeros_like(v) for k, v in C.items()}
+    v = {k: np.zeros_like(x) for k, x in C.items()}
+    losses = []
+    for step, b in enumerate(train_batches, 1):
+        feat, stats = run(b, False)
+        for bk, st in stats:   # the copy's running statistics (train-mode forward)
+            P[bk + ".running_mean"], P[bk + ".running_var"] = bn_running_update(
+                P[bk + ".running_mean"], P[bk + ".running_var"], st)
+        h = linear_fwd(feat, C["classifier.0.weight"], C["classifier.0.bias"])
+        r = np.maximum(h, 0)
+        logits = linear_fwd(r, C["classifier.2.weight"], C["classifier.2.bias"])
+        loss, dl = cross_entropy(logits, b["label"])
+        losses.append(loss)
+        dr, dw2, db2 = linear_bwd(dl, r, C["classifier.2.weight"])
+        _, dw0, db0 = linear_bwd(dr * (h > 0), feat, C["classifier.0.weight"])
+        g = {"classifier.0.weight": dw0, "classifier.0.bias": db0, "classifier.2.weight": dw2,
+             "classifier.2.bias": db2}
+        for k in C:
+            C[k], m[k], v[k] = adamw_step(C[k], g[k], m[k], v[k], step, lr, wd)
+    ev_loss, correct, total, all_logits = 0.0, 0, 0, []
+    for b in valid_batches:
+        feat, _ = run(b, True)
+        h = linear_fwd(feat, C["classifier.0.weight"], C["classifier.0.bias"])
+        logits = linear_fwd(np.maximum(h, 0), C["classifier.2.weight"], C["classifier.2.bias"])
+        ev_loss += cross_entropy(logits, b["label"])[0]
+        correct += int((logits.argmax(1) == b["label"]).sum())
+        total += len(b["label"])
+        all_logits.append(logits)
+    rs = {k: P[k] for k in P if k.endswith(("running_mean", "running_var")) and k.startswith("student.")}
+    return {"train_losses": np.array(losses), "val_loss": float(np.mean(losses)),
+            "eval_loss": ev_loss / len(valid_batches), "mlp_acc": 100.0 * correct / total,
+            "logits": np.concatenate(all_logits), "classifier": C, "running": rs}

@@ -159,3 +159,11 @@ def is_live_student(key, mode):
     if key.startswith("teacher") or key == "center":
         return False
     return True
+
+
+def classifier_spec(D, hidden=128, num_classes=10):
+    """DownstreamClassifier.classifier (models/dino.py:1782-1786): Linear(D,128)-ReLU-Linear(128,10)."""
+    sd = OrderedDict()
+    _dense(sd, "classifier.0", hidden, D)
+    _dense(sd, "classifier.2", num_classes, hidden)
+    return sd

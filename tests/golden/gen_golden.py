@@ -301,6 +301,75 @@ def simclr_case(name, D, P, B, pseed, bseed, out_dir, dt="float32"):
     np.savez_compressed(os.path.join(out_dir, name + ".npz"), **out)
 
 
+def probe_case(name, kind, E, D, P, B, nb_train, nb_valid, pseed, bseed, out_dir, dt="float32",
+               lr=1e-3):
+    """on_train_epoch_end's linear probe (dino.py:878-951 / 1670-1735): DownstreamClassifier
+    over a frozen copy of the student, the copy in train mode for the probe epoch, AdamW on the
+    classifier, then evaluate() in eval mode.  Replayed on CPU without the CUDA-only fp16
+    autocast / GradScaler; the copy's dropout set to 0."""
+    import torch
+    import torch.nn as nn
+    dt = getattr(torch, dt)
+    import models.dino as rd
+    torch.manual_seed(0)
+    if kind == "multi_central":
+        model = rd.MultiModalDINO(encoder_class=rd.CentralMultiModalEncoder, output_dim=D,
+                                  encoder_output_dim=E, projection_dim=P, dropout=0.0)
+        spec = ospec.multimodal_dino_spec("default", E, D, P)
+    else:
+        enc = {"image_simple": rd.ImageEncoder, "spectrogram_simple": rd.SpectrogramEncoder}[kind]
+        model = rd.UniModalDINO(encoder_class=enc, output_dim=D, projection_dim=P, dropout=0.0)
+        spec = ospec.unimodal_dino_spec(kind, D, P)
+    state = make_state(spec, pseed)
+    load_into(model, spec, state)
+    model = model.to(dt)
+    clf = rd.DownstreamClassifier(model, trainable_encoder=False).to(dt)
+    zero_dropout(clf)
+    cspec = ospec.classifier_spec(D)
+    cstate = make_state(cspec, pseed + 1)
+    with torch.no_grad():
+        for k, v in cstate.items():
+            dict(clf.named_parameters())[k].copy_(torch.from_numpy(v).to(dt))
+    crit = nn.CrossEntropyLoss()
+    opt = torch.optim.AdamW(clf.classifier.parameters(), lr=lr)
+    clf.train()
+    out = {"meta_dims": np.array([E, D, P, B, nb_train, nb_valid, pseed, bseed]),
+           "meta_kind": np.array(kind), "meta_lr": np.float64(lr)}
+    losses = []
+    for i in range(nb_train):
+        b = make_multimodal_batch(B, 1, 0, bseed + i)
+        im, au = torch.from_numpy(b["image"]).to(dt), torch.from_numpy(b["audio"]).to(dt)
+        opt.zero_grad()
+        loss = crit(clf(im, au), torch.from_numpy(b["label"]))
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    out["train_losses"] = np.array(losses, np.float64)
+    clf.eval()
+    tot, correct, n, logits = 0.0, 0, 0, []
+    with torch.no_grad():
+        for i in range(nb_valid):
+            b = make_multimodal_batch(B, 1, 0, bseed + 1000 + i)
+            im, au = torch.from_numpy(b["image"]).to(dt), torch.from_numpy(b["audio"]).to(dt)
+            o = clf(im, au)
+            lab = torch.from_numpy(b["label"])
+            tot += crit(o, lab).item()
+            correct += int((o.argmax(1) == lab).sum())
+            n += len(lab)
+            logits.append(o.numpy())
+    out["eval_loss"] = np.float64(tot / nb_valid)
+    out["mlp_acc"] = np.float64(100.0 * correct / n)
+    summarize("logits", np.concatenate(logits), out)
+    for k, v in clf.named_parameters():
+        if k.startswith("classifier"):
+            summarize("cls/" + k, v.detach().numpy(), out)
+    for k, v in clf.encoder.state_dict().items():
+        if k.endswith("running_mean") or k.endswith("running_var"):
+            summarize("rs/student." + k, v.numpy(), out)
+    np.savez_compressed(os.path.join(out_dir, name + ".npz"), **out)
+    print(f"{name}: train losses {np.array(losses)} eval {out['eval_loss']:.6f} acc {out['mlp_acc']}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=HERE)
@@ -326,6 +395,8 @@ def main():
          dict(modality="audio", L=2, cos_alpha=0.3)),
         ("uni_speccentral_g2l2", unimodal_case, (32, 16, 3, 110, 1010, 2),
          dict(modality="spectrogram_central", L=2, cos_alpha=0.0)),
+        ("probe_multi_central", probe_case, ("multi_central", 32, 32, 16, 6, 3, 2, 111, 1011), {}),
+        ("probe_image_simple", probe_case, ("image_simple", 0, 64, 32, 6, 3, 2, 112, 1012), {}),
         ("simclr_small", simclr_case, (256, 256, 4, 107, 1007), {}),
     ]
     # Each case twice: the reference executed in fp32 (its CPU numerics) and in float64

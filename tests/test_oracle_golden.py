@@ -179,3 +179,27 @@ def test_simclr_config4_matches_reference(mode, variant):
     zero = _zero("simclr_small")
     _check_all(fx, [(f"m{mode}/grad/" + k, g) for k, g in r["grads"].items()], grel,
                floor_fn=lambda k: floor if k in zero else 0.0)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("case", ["probe_multi_central", "probe_image_simple"])
+def test_linear_probe_matches_reference(case, variant):
+    """Epoch-end linear probe (A15): DownstreamClassifier over a frozen train-mode copy of the
+    student + AdamW, then eval-mode evaluate() (dino.py:878-951, 1670-1735, 1764-1814)."""
+    fx = gu.load(case + variant)
+    lt, orel, grel, srel, floor, _ = TOL[variant]
+    E, D, P, B, nt, nv, pseed, bseed = [int(x) for x in fx["meta_dims"]]
+    kind, lr = str(fx["meta_kind"]), float(fx["meta_lr"])
+    spec = (S.multimodal_dino_spec("default", E, D, P) if kind == "multi_central"
+            else S.unimodal_dino_spec(kind, D, P))
+    state = make_state(spec, pseed)
+    cls = make_state(S.classifier_spec(D), pseed + 1)
+    train = [make_multimodal_batch(B, 1, 0, bseed + i) for i in range(nt)]
+    valid = [make_multimodal_batch(B, 1, 0, bseed + 1000 + i) for i in range(nv)]
+    r = O.linear_probe(state, kind, train, valid, cls, lr)
+    np.testing.assert_allclose(r["train_losses"], fx["train_losses"], atol=lt, rtol=0)
+    assert abs(r["eval_loss"] - float(fx["eval_loss"])) < lt
+    assert r["mlp_acc"] == float(fx["mlp_acc"])
+    _check_all(fx, [("logits", r["logits"])], orel)
+    _check_all(fx, [("cls/" + k, v) for k, v in r["classifier"].items()], srel)
+    _check_all(fx, [("rs/" + k, v) for k, v in r["running"].items()], srel)
