@@ -37,8 +37,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=1024, help="pairs per GPU per step")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="pairs per GPU per step (default: the workload's BASELINE config)")
     ap.add_argument("--mode", default="mse", choices=["default", "mse", "infonce", "semi_supervised"])
+    ap.add_argument("--workload", default="dino", choices=["dino", "uni", "simclr"],
+                    help="dino = MultiModalDINO* (--mode; config 2 mse / config 3 infonce with "
+                         "all-gathered negatives / config 5 semi_supervised); uni = UniModalDINO "
+                         "ImageEncoder 2 global views B=64 (config 1); simclr = multimodal SimCLR "
+                         "with all-gathered NT-Xent negatives, B=2048/GPU (config 4)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -81,6 +87,59 @@ def synthetic_pool(n, B, G, L, device, seed):
                      "image": px(B, 1, 28, 28), "audio": px(B, 1, 112, 112),
                      "label": torch.randint(0, 10, (B,), generator=gen, device=device)})
     return pool
+
+
+def build_workload(args, device, act, world, rank, avdist):
+    """(engine, device batch pool, pairs per GPU per step, config text, model name)."""
+    from avdino.engine import Hyper, MultiCentralEngine, SimCLREngine, UniModalEngine
+    from avdino.params import ParamStore
+    from avdino.spec import multimodal_dino_sd, simclr_sd, unimodal_dino_sd
+    hook = avdist.grad_allreduce_hook() if world > 1 else None
+    if args.workload == "uni":
+        B, D, P = args.batch or 64, 256, 128
+        store = ParamStore(unimodal_dino_sd("image_simple", D, P), device, seed=0)
+        if world > 1:
+            avdist.broadcast_parameters(store)
+        eng = UniModalEngine(store, "image_simple", D, P, Hyper(), act_dtype=act, cos_alpha=0.0,
+                             grad_hook=hook, buffer_hook=avdist.broadcast_buffers if world > 1 else None,
+                             seed=rank)
+        pool = synthetic_pool(2, B, 2, 0, device, 1234 + rank)
+        return (eng, pool, B, f"UniModalDINO ImageEncoder, 2 global views, B={B}/GPU, D={D}, P={P} "
+                              f"(BASELINE config 1)", "image_simple")
+    if args.workload == "simclr":
+        B, D, P = args.batch or 2048, 256, 256
+        store = ParamStore(simclr_sd(D, P), device, seed=0, has_teacher=False,
+                           groups=SimCLREngine.GROUPS)
+        if world > 1:
+            avdist.broadcast_parameters(store)
+        eng = SimCLREngine(store, D, P, Hyper(weight_decay=0.0), act_dtype=act, negatives="global",
+                           grad_hook=hook)
+        gen = torch.Generator(device=device).manual_seed(1234 + rank)
+
+        def px(*shape):
+            return torch.randint(0, 256, shape, generator=gen, device=device, dtype=torch.int32).float() / 255.0
+
+        pool = [{"img1": px(B, 1, 28, 28), "spec1": px(B, 1, 112, 112), "img2": px(B, 1, 28, 28),
+                 "spec2": px(B, 1, 112, 112)} for _ in range(2)]
+        return (eng, pool, B, f"multimodal SimCLR, random modality pair per step, NT-Xent over "
+                              f"all-gathered negatives, B={B}/GPU, D=P={D} (BASELINE config 4)",
+                "multimodal_simclr")
+    E, D, P, G, L = 256, 256, 128, 2, 4
+    B = args.batch or (4096 if args.mode == "semi_supervised" else 1024)
+    store = ParamStore(multimodal_dino_sd(args.mode, E, D, P), device, seed=0)
+    if world > 1:
+        avdist.broadcast_parameters(store)
+    # DDP semantics of the reference's multi-GPU run: rank-0 buffers broadcast before each
+    # forward, one averaged all-reduce of the flat live-gradient arena after backward
+    eng = MultiCentralEngine(store, args.mode, E, D, P, Hyper(), act_dtype=act, grad_hook=hook,
+                             buffer_hook=avdist.broadcast_buffers if world > 1 else None, seed=rank,
+                             negatives="global")
+    pool = synthetic_pool(2, B, G, L, device, 1234 + rank)
+    cfg = {"mse": "BASELINE config 2", "infonce": "BASELINE config 3 shape, all-gathered negatives",
+           "semi_supervised": "BASELINE config 5 shape, bf16 (no fp8 path yet)",
+           "default": "default mode"}[args.mode]
+    return (eng, pool, B, f"multi_central {args.mode} training step, B={B}/GPU, {G} global + {L} "
+                          f"local views, E=D={E}, P={P} ({cfg})", "multi_central")
 
 
 def cpu_baseline(batch, seconds):
@@ -133,23 +192,9 @@ def main():
             dist.init_process_group("gloo")
 
     from avdino import ops
-    from avdino.engine import Hyper, MultiCentralEngine
-    from avdino.params import ParamStore
-    from avdino.spec import multimodal_dino_sd
-
-    E, D, P, G, L, B = 256, 256, 128, 2, 4, args.batch
-    act = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    store = ParamStore(multimodal_dino_sd(args.mode, E, D, P), device, seed=0)
-
     from avdino import dist as avdist
-    if world > 1:
-        avdist.broadcast_parameters(store)
-    # DDP semantics of the reference's multi-GPU run: rank-0 buffers broadcast before each
-    # forward, one averaged all-reduce of the flat live-gradient arena after backward
-    eng = MultiCentralEngine(store, args.mode, E, D, P, Hyper(), act_dtype=act,
-                             grad_hook=avdist.grad_allreduce_hook() if world > 1 else None,
-                             buffer_hook=avdist.broadcast_buffers if world > 1 else None, seed=rank)
-    pool = synthetic_pool(2, B, G, L, device, 1234 + rank)
+    act = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    eng, pool, B, workload, model = build_workload(args, device, act, world, rank, avdist)
 
     # warm-up, timing every instrumented kernel once to find the dominant one
     ops.TIMER = ops.KernelTimer()
@@ -220,14 +265,14 @@ def main():
         "ms_per_step": round(elapsed * 1e3 / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
         "data": "synthetic: randint(0,256)/255 AVMNIST-shaped views resident in HBM; random-init weights",
-        "config": {"workload": f"multi_central {args.mode} training step, B={B}/GPU, {G} global + {L} local "
-                               f"views, E=D={E}, P={P} (BASELINE config 2)",
-                   "model": "multi_central", "global_batch": world * B, "seq_len": None,
+        "config": {"workload": workload,
+                   "model": model, "global_batch": world * B, "seq_len": None,
                    "parallelism": f"dp{world}"},
         "roofline": roof,
         "final_loss": round(lv, 6),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "dino" \
+            and args.mode == "mse":
         out["cpu_baseline"] = cpu_baseline(args.cpu_batch, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)

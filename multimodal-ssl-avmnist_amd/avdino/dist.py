@@ -48,7 +48,8 @@ def broadcast_parameters(store, src=0, group=None):
     """Initial replication (DDP does this once at wrap time): student + teacher arenas."""
     if dist.get_world_size(group) > 1:
         dist.broadcast(store.student, src=src, group=group)
-        dist.broadcast(store.teacher, src=src, group=group)
+        if store.teacher is not None:
+            dist.broadcast(store.teacher, src=src, group=group)
 
 
 def gather_rows(x, group=None):

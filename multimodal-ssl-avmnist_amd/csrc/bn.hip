@@ -305,7 +305,7 @@ __device__ __forceinline__ void unpack8(u4v v, float (&f)[8]) {
   f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
 }
 __device__ __forceinline__ unsigned pack2(float a, float b) {
-  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+  return pack_bf16x2(a, b);
 }
 
 // per window k = 0..3 of the quad: first-max argmax over relu(z) and the max

@@ -33,7 +33,7 @@ template <> struct Vec<bf16> {
   static __device__ __forceinline__ void st(bf16* p, const float (&f)[8]) {
     unsigned w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = (unsigned)f2bf(f[2 * i]) | ((unsigned)f2bf(f[2 * i + 1]) << 16);
+    for (int i = 0; i < 4; ++i) w[i] = pack_bf16x2(f[2 * i], f[2 * i + 1]);
     *reinterpret_cast<u4*>(p) = u4{w[0], w[1], w[2], w[3]};
   }
 };

@@ -58,12 +58,7 @@ __device__ __forceinline__ f4 mma(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// 4 consecutive channels of one pixel
-__device__ __forceinline__ void store4(bf16* p, const float (&v)[4]) {
-  const unsigned lo = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-  const unsigned hi = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
-  *reinterpret_cast<uint2*>(p) = make_uint2(lo, hi);
-}
+// 4 consecutive channels of one pixel (the bf16 store is inlined in conv_store)
 __device__ __forceinline__ void store4(float* p, const float (&v)[4]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
 }
@@ -117,14 +112,30 @@ __device__ __forceinline__ void conv_store(const f4 (&acc)[GPW][NT], const Tile&
     for (int t = 0; t < NT; ++t) {
       const int cob = co0 + 16 * t + 4 * g;
       if (!pv || cob >= Cout) continue;
-      float v[4];
+      if constexpr (sizeof(T) == 2) {
+        // one v_cvt_pk_bf16_f32 per pair; the statistics are taken on the stored (rounded)
+        // values, recovered from the packed bits
+        const uint32_t lo = pack_bf16x2(acc[j][t][0] + bv[t][0], acc[j][t][1] + bv[t][1]);
+        const uint32_t hi = pack_bf16x2(acc[j][t][2] + bv[t][2], acc[j][t][3] + bv[t][3]);
+        const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                            __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        v[i] = io<T>::rnd(acc[j][t][i] + bv[t][i]);
-        ss[t][i] += v[i];
-        sq[t][i] += v[i] * v[i];
+        for (int i = 0; i < 4; ++i) {
+          ss[t][i] += v[i];
+          sq[t][i] = fmaf(v[i], v[i], sq[t][i]);
+        }
+        *reinterpret_cast<uint2*>(y + (((size_t)n * Ho + oy) * Wo + ox) * Cout + cob) =
+            make_uint2(lo, hi);
+      } else {
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = acc[j][t][i] + bv[t][i];
+          ss[t][i] += v[i];
+          sq[t][i] += v[i] * v[i];
+        }
+        store4(y + (((size_t)n * Ho + oy) * Wo + ox) * Cout + cob, v);
       }
-      store4(y + (((size_t)n * Ho + oy) * Wo + ox) * Cout + cob, v);
     }
   }
 }

@@ -398,8 +398,8 @@ __global__ __launch_bounds__(256) void conv_fwd_mfma_kernel(
         bf16* row = y + (((size_t)n * Cout + co) * Ho + oy) * Wo;
         const int ox0 = tx0 + 4 * g;
         if (even && ox0 + 3 < Wo) {
-          const unsigned p0 = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-          const unsigned p1 = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+          const unsigned p0 = pack_bf16x2(v[0], v[1]);
+          const unsigned p1 = pack_bf16x2(v[2], v[3]);
           reinterpret_cast<unsigned*>(row + ox0)[0] = p0;
           reinterpret_cast<unsigned*>(row + ox0)[1] = p1;
         } else {

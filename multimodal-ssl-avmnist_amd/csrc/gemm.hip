@@ -186,8 +186,8 @@ __device__ __forceinline__ void store_tile(const TileRegs<ROWS>& t, long long sr
       typename GemmT<MODE>::T* d = S + r * LDK + k;
       if constexpr (MODE == 2) {
         // 4 bf16 = one 8-byte LDS store
-        const unsigned lo = (unsigned)f2bf(t.v[4 * i]) | ((unsigned)f2bf(t.v[4 * i + 1]) << 16);
-        const unsigned hi = (unsigned)f2bf(t.v[4 * i + 2]) | ((unsigned)f2bf(t.v[4 * i + 3]) << 16);
+        const unsigned lo = pack_bf16x2(t.v[4 * i], t.v[4 * i + 1]);
+        const unsigned hi = pack_bf16x2(t.v[4 * i + 2], t.v[4 * i + 3]);
         *reinterpret_cast<uint2*>(d) = make_uint2(lo, hi);
       } else {
 #pragma unroll
