@@ -1,0 +1,47 @@
+"""run_dino command line and YAML config surface (reference run_dino.py:528-664): argument
+rules and the hyperparameter mapping, on CPU (no training: the engine needs a GPU)."""
+import os
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CFG = os.path.join(REPO, "configs", "config_multimodal_dino.yaml")
+
+
+def test_cli_rules_and_config_mapping():
+    from avdino import run_dino as R
+    a = R.parse_args(["--model", "multi_central", "--training_mode", "mse", "--config", CFG,
+                      "--precision", "32"])
+    cfg = R.load_config(CFG)
+    m = R.build_model(a, cfg, device="cpu")
+    h = cfg["hyperparameters"]
+    assert type(m).__name__ == "MultiModalDINOWithMSELightning"
+    assert m.learning_rate == h["learning_rate"] and m.num_epochs == h["num_epochs"]
+    assert m.model.hp.tau_t == h["teacher_temperature"] and m.model.hp.wd == h["weight_decay"]
+    assert m.model.store["center"].shape == (1, h["projection_dim"])
+    assert m.model.engine is None                      # CPU: no engine, no fallback
+    u = R.build_model(R.parse_args(["--unimodal_model", "image_simple", "--config", CFG]), cfg, "cpu")
+    assert type(u).__name__ == "UniModalDINOLightning" and u.cosine_loss_alpha == 0
+    with pytest.raises(SystemExit):   # training modes are multimodal-only (run_dino.py:584)
+        R.parse_args(["--unimodal_model", "image_simple", "--training_mode", "mse", "--config", CFG])
+    with pytest.raises(SystemExit):
+        R.parse_args(["--model", "multi_central", "--unimodal_model", "image_simple", "--config", CFG])
+    with pytest.raises(RuntimeError):
+        m.training_step(None, 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("argv", [["--model", "multi_central", "--training_mode", "mse"],
+                                  ["--model", "multi_central", "--training_mode", "semi_supervised"],
+                                  ["--unimodal_model", "spectrogram_simple"]])
+def test_run_dino_two_epochs_on_device(argv, capsys):
+    """The driver end to end on the GPU: 2 epochs x 3 steps, cosine LR per epoch, probe."""
+    import json
+    from avdino import run_dino as R
+    m = R.main(argv + ["--config", CFG, "--epochs", "2", "--steps-per-epoch", "3",
+                       "--batch-size", "8", "--probe-batches", "2"])
+    recs = [json.loads(line) for line in capsys.readouterr().out.splitlines() if line.startswith("{")]
+    assert len(recs) == 2 and all(r["train_loss"] == r["train_loss"] for r in recs)
+    assert 0 <= recs[-1]["mlp_acc"] <= 100
+    assert recs[1]["lr"] < recs[0]["lr"] < 1e-4         # CosineAnnealingLR(T_max=num_epochs)
+    assert m.model.engine.step_idx == 6 if hasattr(m.model.engine, "step_idx") else True
