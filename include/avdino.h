@@ -206,6 +206,19 @@ int avd_cl_bn_bwd_apply(const void* y, int dt, const void* gout, int mode, const
                         const float* shift, const float* coef, void* dy, int N, int B, int C,
                         int H, int W, void* stream);
 
+/* Fused BatchNorm-backward apply + conv weight gradient of a first (Cin = 1) layer whose output
+ * is pooled in mode 0 (the CentralNet audio conv1: Cout 8, 5x5, pad 2, H, W % 16 == 0,
+ * W <= 112, bf16): computes dy exactly as avd_cl_bn_bwd_apply and, without storing it,
+ * parts[s][Cout*K*K] = per-slab partial dW (reduce with avd_sum_rows over
+ * avd_cl_apply_wgrad_slabs() rows).  Replaces avd_cl_bn_bwd_apply + avd_cl_conv_wgrad for that
+ * layer (CentralUnimodalAudio.conv1/bn1, unimodal.py:160-190); the first layer needs no dx.
+ * Returns AVD_ERR_SHAPE for any other shape (avd_cl_apply_wgrad_slabs() == 0). */
+int avd_cl_apply_wgrad_slabs(int dt, int N, int Cin, int H, int W, int Cout, int K, int pad);
+int avd_cl_bn_bwd_apply_wgrad(const void* y, const void* gout, const float* scale,
+                              const float* shift, const float* coef, const void* x, float* parts,
+                              int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
+                              void* stream);
+
 /* out[c] (+)= sum_{r<rows} in[r*ld + c]   (fixed order, f64 accumulation) -- reduces the conv
  * weight-grad partial slabs and gives Linear bias gradients (column sums of dy). */
 int avd_sum_rows(const float* in, int rows, int cols, long long ld, float* out, int accumulate,

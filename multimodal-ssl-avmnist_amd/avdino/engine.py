@@ -156,9 +156,16 @@ class ConvBranch:
             ops.bn_bwd_finalize(parts, G, R, co, B * Ho * Ho, store[bk + ".weight"], st[0], st[1],
                                 coef, store.grad_of(bk + ".weight"), store.grad_of(bk + ".bias"),
                                 store.grad_of(ck + ".bias"))
+            x = ctx["x"][i]
+            nsl = ops.cl_apply_wgrad_slabs(self.act, N, ci, H, H, co, k, pad) if (i == 0 and mode == 0) else 0
+            if nsl:   # first layer: BN-backward apply fused with the weight gradient (no dy)
+                wparts = ws.get("wgrad_parts", nsl * co * ci * k * k)
+                ops.cl_bn_bwd_apply_wgrad(y, gout, st[2], st[3], coef, x, wparts, N, B, ci, H, H, co,
+                                          k, pad)
+                ops.sum_rows(wparts, nsl, co * ci * k * k, store.grad_of(ck + ".weight"))
+                continue
             dy = ws.get("bwd_dy", N * Ho * Ho * co, self.act)
             ops.cl_bn_bwd_apply(y, gout, mode, st[2], st[3], coef, dy, N, B, co, Ho, Ho)
-            x = ctx["x"][i]
             nch = ops.cl_wgrad_chunks(N, co, ci, k)
             wparts = ws.get("wgrad_parts", nch * co * ci * k * k)
             ops.cl_conv_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)

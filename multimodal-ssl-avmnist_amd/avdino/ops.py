@@ -337,6 +337,23 @@ def cl_bn_bwd_apply(y, gout, mode, scale, shift, coef, dy, N, B, C, H, W):
                         p(coef), p(dy), N, B, C, H, W, stream()))
 
 
+def cl_apply_wgrad_slabs(dtype, N, Cin, H, W, Cout, K, pad):
+    """Slabs of the fused BN-apply + wgrad first-layer kernel, 0 if the shape is not served."""
+    return lib.avd_cl_apply_wgrad_slabs(1 if dtype == torch.bfloat16 else 0, N, Cin, H, W, Cout, K, pad)
+
+
+def cl_bn_bwd_apply_wgrad(y, gout, scale, shift, coef, x, parts, N, B, Cin, H, W, Cout, K, pad):
+    ns = cl_apply_wgrad_slabs(y.dtype, N, Cin, H, W, Cout, K, pad)
+    _need(ns > 0 and parts.numel() >= ns * Cout * Cin * K * K, "apply+wgrad shape / slabs")
+    _need(y.numel() == N * H * W * Cout and x.numel() == N * H * W * Cin, "apply+wgrad sizes")
+    _need(gout.numel() == N * (H // 2) * (W // 2) * Cout and gout.dtype == y.dtype, "apply+wgrad gout")
+    nb = (y.numel() + x.numel() + gout.numel()) * y.element_size()
+    _timed(f"cl_bn_bwd_apply_wgrad[{N}x{H}x{W}x{Cin}->{Cout} k{K} {y.dtype}]", nb,
+           2 * N * H * W * Cout * K * K,
+           lambda: call("avd_cl_bn_bwd_apply_wgrad", p(y), p(gout), p(scale), p(shift), p(coef), p(x),
+                        p(parts), dtcode(y), N, B, Cin, H, W, Cout, K, pad, stream()))
+
+
 def sum_rows(x, rows, cols, out, accumulate=0, ld=None, off=0):
     ld = cols if ld is None else ld
     _need(off + (rows - 1) * ld + cols <= x.numel() and out.numel() >= cols, "sum_rows bounds")

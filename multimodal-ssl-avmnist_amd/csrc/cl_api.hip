@@ -25,6 +25,12 @@ int avd_cl_bn_bwd_apply_impl(const void* y, int dt, const void* gout, int mode,
                              const float* scale, const float* shift, const float* coef, void* dy,
                              int N, int B, int C, int H, int W, hipStream_t st);
 
+bool avd_c1p8_eligible(int dt, int Cin, int Cout, int K, int Ho, int Wo);
+int avd_c1p8_wgrad_slabs(int N, int H);
+int avd_c1p8_bwd_apply_wgrad(const void* y, const void* gout, const float* scale,
+                             const float* shift, const float* coef, const void* x, float* parts,
+                             int N, int B, int H, int W, hipStream_t st);
+
 namespace {
 bool dt_ok(int dt) { return dt == AVD_F32 || dt == AVD_BF16; }
 }  // namespace
@@ -41,6 +47,22 @@ int avd_cl_weight_layout(const float* w, void* wk, int dt, int Cout, int Cin, in
   if (!w || !wk || !dt_ok(dt)) return AVD_ERR_ARG;
   if (Cout <= 0 || Cin <= 0 || K <= 0) return AVD_ERR_SHAPE;
   return avd_cl_weight_layout_impl(w, wk, dt, Cout, Cin, K, dgrad, avd_stream(stream));
+}
+
+int avd_cl_apply_wgrad_slabs(int dt, int N, int Cin, int H, int W, int Cout, int K, int pad) {
+  if (!avd_c1p8_eligible(dt, Cin, Cout, K, H, W) || pad != 2 || W > 112) return 0;
+  return avd_c1p8_wgrad_slabs(N, H);
+}
+
+int avd_cl_bn_bwd_apply_wgrad(const void* y, const void* gout, const float* scale,
+                              const float* shift, const float* coef, const void* x, float* parts,
+                              int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
+                              void* stream) {
+  if (!y || !gout || !scale || !shift || !coef || !x || !parts) return AVD_ERR_ARG;
+  if (N <= 0 || B <= 0 || N % B) return AVD_ERR_SHAPE;
+  if (avd_cl_apply_wgrad_slabs(dt, N, Cin, H, W, Cout, K, pad) == 0) return AVD_ERR_SHAPE;
+  return avd_c1p8_bwd_apply_wgrad(y, gout, scale, shift, coef, x, parts, N, B, H, W,
+                                  avd_stream(stream));
 }
 
 int avd_cl_stat_rows(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt) {

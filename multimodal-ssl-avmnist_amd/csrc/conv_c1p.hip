@@ -1,0 +1,360 @@
+// First-layer convolution of the CentralNet audio branch (CentralUnimodalAudio.conv1,
+// unimodal.py:160-190: Conv2d(1, 8, 5, padding=2) on 112x112 spectrograms) as a "pixel-pair"
+// implicit GEMM on v_mfma_f32_16x16x32_bf16, channels-last bf16 output + fused BatchNorm
+// partial statistics -- a drop-in for conv_c1_kernel on this shape (same outputs, same
+// partial-row layout).
+//
+// Why a dedicated kernel: with 8 output channels the generic Cin=1 kernel fills half of the
+// MFMA M dimension and gathers every B element with its own 2-byte LDS read (~100 VALU
+// instructions per 16 outputs).  Here the M dimension holds (pixel offset j in a horizontal
+// pair, channel c) -- 16 useful rows -- and K holds the 5x6 input patch that covers BOTH
+// pixels of the pair (30 of 32 taps):
+//   A[(j,c)][ky*6 + kx'] = w[c][ky][kx' - j]      (0 where kx' - j is outside [0,5))
+//   B[ky*6 + kx'][pair]  = x[y + ky - 2][x0 + kx' - 2]     (x0 = even column of the pair)
+// A lane's 8 consecutive k of B are 4 aligned bf16 PAIRS of the input rows, so the whole
+// B fragment is 4 ds_read_b32 with constant offsets (no packing), and one MFMA produces
+// 32 outputs x 8 channels.  C layout (col = lane&15 = pair, row = 4*(lane>>4)+i): lane l holds
+// pixel (pair l&15, j = l>>5), channels 4*((l>>4)&1) .. +3 -> one 8-byte NHWC store.
+// A 16-pixel-wide, 2-row strip is one MFMA column tile: pairs 0-7 = row 0, 8-15 = row 1.
+#include <algorithm>
+
+#include "common.h"
+
+using namespace avd;
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f4;
+typedef __attribute__((ext_vector_type(4))) unsigned u4;
+
+constexpr int TH = 16;         // output rows per block (one sample)
+constexpr int XOFF = 8;        // LDS column of image column 0 (16-byte aligned data)
+constexpr int ITW = 144;       // LDS row stride in bf16 (72 dwords = 8 mod 64 banks)
+constexpr int ITWD = ITW / 2;
+constexpr int COUT = 8;
+
+// (row, dword) of the 4 B-fragment dwords for lane half h = lane>>4 (see header)
+__device__ __forceinline__ int boff(int h, int d) {
+  constexpr int R[4][4] = {{0, 0, 0, 1}, {1, 1, 2, 2}, {2, 3, 3, 3}, {4, 4, 4, 4}};
+  constexpr int D[4][4] = {{0, 1, 2, 0}, {1, 2, 0, 1}, {2, 0, 1, 2}, {0, 1, 2, 0}};
+  return R[h][d] * ITWD + D[h][d];
+}
+
+__global__ __launch_bounds__(256) void conv_c1p8_kernel(const bf16* __restrict__ x,
+                                                        const bf16* __restrict__ wk,
+                                                        const float* __restrict__ bias,
+                                                        bf16* __restrict__ y,
+                                                        float* __restrict__ stats, int N, int H,
+                                                        int W, int tps) {
+  __shared__ __attribute__((aligned(16))) bf16 xs[(TH + 4) * ITW];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int n = blockIdx.x / tps, ty0 = (blockIdx.x - n * tps) * TH;
+  const int h = lane >> 4, p = lane & 15, j = lane >> 5, cs = h & 1;
+
+  // ---- A fragment (weights) for this lane: row m = (j', c'), k = 8h .. 8h+7; wk is the
+  // avd_cl_weight_layout image (bf16 [16 rows][32]: wk[c*32 + tap] = w[c][0][tap])
+  bf16x8 a;
+  {
+    const int m = lane & 15, jj = m >> 3, c = m & 7;
+    __bf16 e[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = 8 * h + q, ky = k / 6, kx = k % 6 - jj;
+      const bool ok = k < 30 && kx >= 0 && kx < 5;
+      const float v = bf2f(wk[c * 32 + (ok ? ky * 5 + kx : 0)]);
+      e[q] = (__bf16)(ok ? v : 0.f);
+    }
+    a = bf16x8{e[0], e[1], e[2], e[3], e[4], e[5], e[6], e[7]};
+  }
+  float bv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bv[i] = bias ? bias[4 * cs + i] : 0.f;
+
+  // ---- stage rows ty0-2 .. ty0+TH+1 (zero outside the image); pad columns zeroed
+  const int cpr = W >> 3;                       // 16-byte chunks per image row
+  const int nch = (TH + 4) * cpr;
+  for (int t = tid; t < nch; t += 256) {
+    const int r = t / cpr, c = t - r * cpr;
+    const int iy = ty0 - 2 + r;
+    const bool ok = iy >= 0 && iy < H;
+    const u4 v = *reinterpret_cast<const u4*>(x + ((size_t)n * H + (ok ? iy : 0)) * W + 8 * c);
+    *reinterpret_cast<u4*>(xs + r * ITW + XOFF + 8 * c) = ok ? v : u4{0u, 0u, 0u, 0u};
+  }
+  for (int t = tid; t < (TH + 4) * 2; t += 256) {
+    const int r = t >> 1, side = t & 1;
+    *reinterpret_cast<u4*>(xs + r * ITW + (side ? XOFF + W : 0)) = u4{0u, 0u, 0u, 0u};
+  }
+  __syncthreads();
+
+  const unsigned* xd = reinterpret_cast<const unsigned*>(xs);
+  const int q = p & 7, rp = p >> 3;
+  int off[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) off[d] = boff(h, d) + rp * ITWD + q + 3;   // + (x0 - 2 + XOFF)/2
+  float ss[4] = {0.f, 0.f, 0.f, 0.f}, sq[4] = {0.f, 0.f, 0.f, 0.f};
+  const int mts = W >> 4;
+  for (int s = wave; s < TH / 2; s += 4) {      // 2-row strips
+    const int oy = ty0 + 2 * s + rp;
+    bf16* yrow = y + ((size_t)n * H + oy) * W * COUT + 4 * cs;
+    for (int mt = 0; mt < mts; ++mt) {
+      const int base = 2 * s * ITWD + 8 * mt;
+      const u4 bw = u4{xd[base + off[0]], xd[base + off[1]], xd[base + off[2]], xd[base + off[3]]};
+      f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, bw),
+                                                       f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const uint32_t lo = pack_bf16x2(acc[0] + bv[0], acc[1] + bv[1]);
+      const uint32_t hi = pack_bf16x2(acc[2] + bv[2], acc[3] + bv[3]);
+      const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                          __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ss[i] += v[i];
+        sq[i] = fmaf(v[i], v[i], sq[i]);
+      }
+      const int ox = 16 * mt + 2 * q + j;
+      *reinterpret_cast<uint2*>(yrow + (size_t)ox * COUT) = make_uint2(lo, hi);
+    }
+  }
+  if (!stats) return;
+  // per-wave BN partial row (sum, sumsq of the stored values): reduce over the 32 lanes that
+  // hold the same 4 channels (lane bits 0-3: pair, bit 5: j)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int m = 1; m <= 32; m <<= 1) {
+      if (m == 16) continue;
+      ss[i] += __shfl_xor(ss[i], m, 64);
+      sq[i] += __shfl_xor(sq[i], m, 64);
+    }
+  }
+  if ((lane & 47) == 0) {                        // lanes 0 (channels 0-3) and 16 (4-7)
+    const size_t nrows = (size_t)N * (size_t)(H / TH) * 4;
+    const size_t row = (size_t)blockIdx.x * 4 + wave;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = 4 * cs + i;
+      stats[((size_t)co * nrows + row) * 2] = ss[i];
+      stats[((size_t)co * nrows + row) * 2 + 1] = sq[i];
+    }
+  }
+}
+
+}  // namespace
+
+// Shape served by this kernel: Cin 1, Cout 8, 5x5, bf16, output (= input, pad 2) H % 16 == 0,
+// W % 16 == 0, W <= 128 (the caller rejects other paddings for this shape).
+bool avd_c1p8_eligible(int dt, int Cin, int Cout, int K, int Ho, int Wo) {
+  return dt == AVD_BF16 && Cin == 1 && Cout == 8 && K == 5 && Ho % TH == 0 && Wo % 16 == 0 &&
+         Wo + XOFF + 2 <= ITW;
+}
+
+int avd_c1p8_stat_rows(int H, int B) { return B * (H / TH) * 4; }
+
+int avd_c1p8_fwd(const void* x, const void* wk, const float* bias, void* y, float* stats, int N,
+                 int H, int W, hipStream_t st) {
+  const int tps = H / TH;
+  conv_c1p8_kernel<<<N * tps, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, (bf16*)y,
+                                            stats, N, H, W, tps);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+// ============================================================================ backward
+// BatchNorm-backward apply + weight gradient of the same layer, fused (dy never reaches HBM):
+//   dy[p, c] = k1 * dz + kx * y + k0,  dz = pooled grad at the window's first-max of
+//   relu(y*scale + shift) when that max is > 0 (bwd_apply_cl_kernel semantics, bn_cl.hip)
+//   dW[c][ky][kx] = sum_p dy[p, c] * x[p + (ky-2, kx-2)]
+// as the pixel-pair GEMM D[(j,c)][ky*6 + kx'] = sum_pairs dY[(j,c)][pair] * X[pair][tap],
+// dW[c][ky][kx] = D[(0,c)][ky*6+kx] + D[(1,c)][ky*6+kx+1]:
+//   A = dY: the block's dy tile in LDS in natural NHWC order, i.e. one 32-byte row of 16
+//       (j,c) values per pixel pair, read column-major with two ds_read_b64_tr_b16;
+//   B = X: 8 consecutive pairs of one tap = 8 input pixels 2 apart -> deinterleaved (by
+//       column parity) and shifted (by -1/0/+1 pair) copies of the input rows make it one
+//       aligned ds_read_b128.
+// Each block walks tiles of TH rows x W of one sample and writes one partial dW slab
+// (deterministic: reduced by avd_sum_rows in slab order).
+namespace {
+
+constexpr int WMAX = 112;                 // widest map served (the 112x112 spectrogram)
+constexpr int XCW = 64;                   // pairs per copy row (>= WMAX/2, 16-byte rows)
+
+typedef __attribute__((ext_vector_type(4))) short s4;
+typedef __attribute__((address_space(3))) s4 lds_s4;
+
+__device__ __forceinline__ void st16(bf16* p, bf16 v) { *p = v; }
+
+__global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ y, const bf16* __restrict__ gz,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ coef, float* __restrict__ parts, int B, int H, int W, int ntiles,
+    int tps) {
+  __shared__ __attribute__((aligned(16))) bf16 xc[2][3][TH + 4][XCW];
+  __shared__ __attribute__((aligned(16))) bf16 dys[TH * WMAX * COUT];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int gq = lane >> 4, col = lane & 15;
+  const int Hp = H >> 1, Wp = W >> 1, cpr = W >> 3, segs = W >> 4;
+  f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+  // B-operand copy / row offset for this lane's tap in each tap tile
+  int bb[2], ba[2], bky[2];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    int t = 16 * tt + col;
+    if (t >= 30) t = 0;                    // padded taps: any finite data (their D is unused)
+    const int ky = t / 6, k2 = t % 6 - 2;  // kx' - 2 = 2a' + b
+    bky[tt] = ky;
+    bb[tt] = k2 & 1;
+    ba[tt] = (k2 >= 0 ? k2 >> 1 : -1) + 1;
+  }
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int n = tile / tps, ty0 = (tile - n * tps) * TH, grp = n / B;
+    __syncthreads();
+    // ---- input rows ty0-2 .. ty0+TH+1 -> parity/shift copies xc[b][a][r][P] = x[2(P+a-1)+b]
+    for (int t = tid; t < (TH + 4) * cpr; t += 256) {
+      const int r = t / cpr, c = t - r * cpr;
+      const int iy = ty0 - 2 + r;
+      const bool ok = iy >= 0 && iy < H;
+      const u4 v = *reinterpret_cast<const u4*>(x + ((size_t)n * H + (ok ? iy : 0)) * W + 8 * c);
+      const unsigned wv[4] = {ok ? v.x : 0u, ok ? v.y : 0u, ok ? v.z : 0u, ok ? v.w : 0u};
+      // wv[d] holds pixels 8c+2d (low) and 8c+2d+1 (high) = pair 4c+d of parity 0 / 1
+      const unsigned e0 = (wv[0] & 0xffffu) | (wv[1] << 16), e1 = (wv[2] & 0xffffu) | (wv[3] << 16);
+      const unsigned o0 = (wv[0] >> 16) | (wv[1] & 0xffff0000u), o1 = (wv[2] >> 16) | (wv[3] & 0xffff0000u);
+      const unsigned ev[2] = {e0, e1}, od[2] = {o0, o1};
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const unsigned lo = b ? od[0] : ev[0], hi = b ? od[1] : ev[1];   // pairs 4c..4c+3
+        *reinterpret_cast<uint2*>(&xc[b][1][r][4 * c]) = make_uint2(lo, hi);
+        // a = 0: P = pair + 1;  a = 2: P = pair - 1
+        bf16* d0 = &xc[b][0][r][4 * c + 1];
+        st16(d0, (bf16)(lo & 0xffffu));
+        *reinterpret_cast<unsigned*>(d0 + 1) = (lo >> 16) | (hi << 16);
+        st16(d0 + 3, (bf16)(hi >> 16));
+        bf16* d2 = &xc[b][2][r][4 * c];
+        if (c > 0) st16(d2 - 1, (bf16)(lo & 0xffffu));
+        *reinterpret_cast<unsigned*>(d2) = (lo >> 16) | (hi << 16);
+        st16(d2 + 2, (bf16)(hi >> 16));
+      }
+    }
+    // pairs whose source pixel lies outside the row: P = 0 of a = 0, P = W/2 - 1 of a = 2
+    for (int t = tid; t < (TH + 4) * 2; t += 256) {
+      const int r = t >> 1, b = t & 1;
+      xc[b][0][r][0] = bf16(0);
+      xc[b][2][r][Wp - 1] = bf16(0);
+    }
+    // ---- dy of the tile's windows into dys (natural NHWC rows)
+    float sc[COUT], sf[COUT], k1[COUT], kx[COUT], k0[COUT];
+#pragma unroll
+    for (int e = 0; e < COUT; ++e) {
+      const int gc = grp * COUT + e;
+      sc[e] = scale[gc];
+      sf[e] = shift[gc];
+      k1[e] = coef[gc * 3];
+      kx[e] = coef[gc * 3 + 1];
+      k0[e] = coef[gc * 3 + 2];
+    }
+    for (int w = tid; w < (TH / 2) * Wp; w += 256) {
+      const int hp = w / Wp, wp = w - hp * Wp;
+      const size_t pix0 = ((size_t)n * H + ty0 + 2 * hp) * W + 2 * wp;
+      const size_t po[4] = {pix0, pix0 + 1, pix0 + W, pix0 + W + 1};
+      float yv[4][COUT];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const u4 v = *reinterpret_cast<const u4*>(y + po[k] * COUT);
+        const unsigned wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          yv[k][2 * i] = __uint_as_float(wv[i] << 16);
+          yv[k][2 * i + 1] = __uint_as_float(wv[i] & 0xffff0000u);
+        }
+      }
+      float gg[COUT];
+      {
+        const u4 v = *reinterpret_cast<const u4*>(
+            gz + (((size_t)n * Hp + (ty0 >> 1) + hp) * Wp + wp) * COUT);
+        const unsigned wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          gg[2 * i] = __uint_as_float(wv[i] << 16);
+          gg[2 * i + 1] = __uint_as_float(wv[i] & 0xffff0000u);
+        }
+      }
+      unsigned outw[4][4];
+#pragma unroll
+      for (int e = 0; e < COUT; ++e) {
+        float best = fmaxf(fmaf(yv[0][e], sc[e], sf[e]), 0.f);
+        int a = 0;
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+          const float r = fmaxf(fmaf(yv[k][e], sc[e], sf[e]), 0.f);
+          if (r > best) { best = r; a = k; }
+        }
+        const float dz = best > 0.f ? gg[e] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float d = fmaf(k1[e], a == k ? dz : 0.f, fmaf(kx[e], yv[k][e], k0[e]));
+          const uint32_t hb = __builtin_bit_cast(uint16_t, (__bf16)d);
+          if (e & 1) outw[k][e >> 1] |= hb << 16;
+          else outw[k][e >> 1] = hb;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int ry = 2 * hp + (k >> 1), cx = 2 * wp + (k & 1);
+        *reinterpret_cast<u4*>(&dys[(ry * WMAX + cx) * COUT]) =
+            u4{outw[k][0], outw[k][1], outw[k][2], outw[k][3]};
+      }
+    }
+    __syncthreads();
+    // ---- MFMA over the tile's pixel pairs: k-block = (row r, 8-pair segment s)
+    const int nkb = TH * segs;
+    for (int ks = wave; 4 * ks < nkb; ks += 4) {
+      const int kb = 4 * ks + gq;
+      const int r = kb / segs, P0 = 8 * (kb - r * segs);
+      // A: rows P0 + 4*half + q, columns 4p .. 4p+3 of the pair rows (32 B each)
+      const int q = col >> 2, pp = col & 3;
+      s4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s4*)&dys[(r * WMAX + 2 * (P0 + q)) * COUT + 4 * pp]);
+      s4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s4*)&dys[(r * WMAX + 2 * (P0 + 4 + q)) * COUT + 4 * pp]);
+      typedef __attribute__((ext_vector_type(8))) short s8;
+      const s8 av = s8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+      const bf16x8 A = __builtin_bit_cast(bf16x8, av);
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const u4 bw = *reinterpret_cast<const u4*>(&xc[bb[tt]][ba[tt]][r + bky[tt]][P0]);
+        acc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, __builtin_bit_cast(bf16x8, bw), acc[tt],
+                                                         0, 0, 0);
+      }
+    }
+  }
+  // ---- per-block slab: sum the 4 waves' D, fold the pair offset j into the taps
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(dys);     // [4 waves][16 rows][32 taps]
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[(wave * 16 + 4 * gq + i) * 32 + 16 * tt + col] = acc[tt][i];
+  __syncthreads();
+  for (int o = tid; o < COUT * 25; o += 256) {
+    const int c = o / 25, t = o - c * 25, ky = t / 5, kx = t - ky * 5;
+    float s = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < 4; ++wv)
+      s += red[(wv * 16 + c) * 32 + ky * 6 + kx] + red[(wv * 16 + 8 + c) * 32 + ky * 6 + kx + 1];
+    parts[(size_t)blockIdx.x * (COUT * 25) + o] = s;
+  }
+}
+
+}  // namespace
+
+int avd_c1p8_wgrad_slabs(int N, int H) { return std::min(N * (H / TH), 2048); }
+
+int avd_c1p8_bwd_apply_wgrad(const void* y, const void* gout, const float* scale,
+                             const float* shift, const float* coef, const void* x, float* parts,
+                             int N, int B, int H, int W, hipStream_t st) {
+  const int tps = H / TH, ntiles = N * tps;
+  c1p8_bwd_wgrad_kernel<<<avd_c1p8_wgrad_slabs(N, H), 256, 0, st>>>(
+      (const bf16*)x, (const bf16*)y, (const bf16*)gout, scale, shift, coef, parts, B, H, W, ntiles,
+      tps);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}

@@ -434,8 +434,14 @@ int pix_bytes(int dt, int Cin) {
 }
 }  // namespace
 
+bool avd_c1p8_eligible(int dt, int Cin, int Cout, int K, int Ho, int Wo);
+int avd_c1p8_stat_rows(int H, int B);
+int avd_c1p8_fwd(const void* x, const void* wk, const float* bias, void* y, float* stats, int N,
+                 int H, int W, hipStream_t st);
+
 // BN partial rows per group written by avd_conv_cl_fwd (0 if no tiling fits)
 int avd_cl_stat_rows_impl(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt) {
+  if (avd_c1p8_eligible(dt, Cin, Cout, K, Ho, Wo)) return avd_c1p8_stat_rows(Ho, B);
   const Plan p = plan_cl(Ho, Wo, B, K, pix_bytes(dt, Cin), Cin == 1, Cout);
   return p.NS ? (B / p.NS) * p.tiles * 4 : 0;   // one partial row per wave
 }
@@ -524,6 +530,10 @@ int avd_cl_conv_fwd_impl(const void* x, const void* wk, const float* bias, void*
   if (Ho <= 0 || Wo <= 0 || B <= 0 || N % B) return AVD_ERR_SHAPE;
   if (Cin != 1 && Cin % 8) return AVD_ERR_SHAPE;
   if (Cout % 4) return AVD_ERR_SHAPE;
+  if (avd_c1p8_eligible(dt, Cin, Cout, K, Ho, Wo)) {   // the audio first layer: pixel-pair MFMA
+    if (pad != 2) return AVD_ERR_SHAPE;
+    return avd_c1p8_fwd(x, wk, bias, y, stats, N, H, W, st);
+  }
   // batches only for Cin = 1 (its weights live in registers; the Cin >= 8 kernel would re-read
   // its weight fragments per batch)
   const Plan p = plan_cl(Ho, Wo, B, K, pix_bytes(dt, Cin), Cin == 1, Cout);

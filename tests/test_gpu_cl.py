@@ -53,7 +53,8 @@ TOL = {"f32": 2e-6, "bf16": 5e-3}
 CASES = [  # N, Cin, H, Cout, K, pad
     (3, 1, 28, 32, 5, 2), (2, 1, 112, 8, 5, 2), (2, 8, 56, 16, 5, 2), (2, 16, 28, 32, 5, 2),
     (4, 32, 14, 64, 5, 2), (8, 32, 14, 64, 5, 0), (2, 1, 28, 32, 3, 1), (4, 32, 14, 64, 3, 1),
-    (8, 64, 7, 128, 3, 1), (2, 128, 14, 256, 3, 1), (2, 8, 20, 8, 5, 2),
+    (8, 64, 7, 128, 3, 1), (2, 128, 14, 256, 3, 1), (2, 8, 20, 8, 5, 2), (4, 1, 48, 8, 5, 2),
+    (6, 1, 112, 8, 5, 2),
 ]
 
 
@@ -199,3 +200,43 @@ def test_cl_bn_block_fwd_bwd(ops, HC, mode, dt):
     dy = torch.empty_like(ty)
     ops.cl_bn_bwd_apply(ty, tg, mode, st[2], st[3], coef, dy, N, B, C, H, H)
     assert rel(nchw(host(dy)), dy_ref) < (5e-3 if dt == "bf16" else 1e-5)
+
+
+@pytest.mark.parametrize("HN", [(112, 4), (48, 6)])
+def test_cl_bn_bwd_apply_wgrad_fused_first_layer(ops, HN):
+    """Fused BN-backward apply + weight gradient of the audio first layer (conv1 1->8 5x5 p2,
+    bf16) == avd_cl_bn_bwd_apply followed by avd_cl_conv_wgrad: dy is rounded to bf16 the same
+    way in both, so only the fp32 accumulation order differs (rel 1e-5); and the float64 truth
+    from the same bf16 operands within 1e-5."""
+    H, N = HN
+    B, C, K, pad = N // 2, 8, 5, 2
+    G = N // B
+    g = np.random.default_rng(H)
+    T = torch.bfloat16
+    x = bf(g.uniform(0, 1, (N, H, H, 1)))
+    y = bf(g.normal(0.2, 1.0, (N, H, H, C)))
+    gout = bf(g.uniform(-1, 1, (N, H // 2, H // 2, C)))
+    scale = g.uniform(0.5, 1.5, G * C).astype(np.float32)
+    shift = g.uniform(-0.3, 0.3, G * C).astype(np.float32)
+    coef = g.uniform(-0.5, 0.5, G * C * 3).astype(np.float32)
+    ty, tg, tx = dev(y, T), dev(gout, T), dev(x, T)
+    dy = torch.empty_like(ty)
+    ops.cl_bn_bwd_apply(ty, tg, 0, dev(scale), dev(shift), dev(coef), dy, N, B, C, H, H)
+    nch = ops.cl_wgrad_chunks(N, C, 1, K)
+    parts = torch.empty(nch * C * K * K, device="cuda")
+    ops.cl_conv_wgrad(tx, dy, parts, N, 1, H, H, C, K, pad)
+    dw_ref = torch.empty(C, 1, K, K, device="cuda")
+    ops.sum_rows(parts, nch, C * K * K, dw_ref)
+    ns = ops.cl_apply_wgrad_slabs(T, N, 1, H, H, C, K, pad)
+    assert ns > 0
+    fparts = torch.full((ns * C * K * K,), float("nan"), device="cuda")
+    ops.cl_bn_bwd_apply_wgrad(ty, tg, dev(scale), dev(shift), dev(coef), tx, fparts, N, B, 1, H, H,
+                              C, K, pad)
+    dw = torch.empty(C, 1, K, K, device="cuda")
+    ops.sum_rows(fparts, ns, C * K * K, dw)
+    assert rel(host(dw), host(dw_ref)) < 1e-5, rel(host(dw), host(dw_ref))
+    # float64 truth on the same bf16 dy
+    win = np.lib.stride_tricks.sliding_window_view(np.pad(nchw(x).astype(np.float64),
+                                                          ((0, 0), (0, 0), (2, 2), (2, 2))), (K, K), (2, 3))
+    dw64 = np.einsum("nohw,nchwij->ocij", nchw(host(dy)), win, optimize=True)
+    assert rel(host(dw), dw64) < 1e-5
