@@ -219,6 +219,25 @@ int avd_cl_bn_bwd_apply_wgrad(const void* y, const void* gout, const float* scal
                               int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
                               void* stream);
 
+/* The same first layer WITHOUT storing its conv output: every pass recomputes y = conv(x) + b
+ * (bf16-rounded, bit-identical across passes) into an on-chip tile from the 8x smaller input.
+ *   pass 0 (stats):  out = BN partial rows [Cout][G][R][2] of the rounded y
+ *                    (R = avd_cl_c1_recompute_rows(0, ...); feed avd_bn_finalize);
+ *   pass 1 (apply):  z = maxpool2(relu(y*scale + shift)) NHWC [N][H/2][W/2][Cout] (bf16);
+ *   pass 2 (reduce): out = BN-backward partial rows (sum dz, sum dz*xhat) as
+ *                    avd_cl_bn_bwd_reduce (mode 0), gz = pooled gradient;
+ *   pass 3 (wgrad):  out = dW partial slabs as avd_cl_bn_bwd_apply_wgrad.
+ * scale/shift/mean/invstd [G][Cout] from avd_bn_finalize, coef from avd_bn_bwd_finalize.
+ * Shape as avd_cl_bn_bwd_apply_wgrad; rows() == 0 otherwise (CentralUnimodalAudio conv1+bn1+
+ * pool, unimodal.py:160-190). */
+int avd_cl_c1_recompute_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cout,
+                             int K, int pad);
+int avd_cl_c1_recompute(int pass, const void* x, const void* wk, const float* bias,
+                        const float* scale, const float* shift, const float* mean,
+                        const float* invstd, const float* coef, const void* gz, void* z,
+                        float* out, int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
+                        int pad, void* stream);
+
 /* out[c] (+)= sum_{r<rows} in[r*ld + c]   (fixed order, f64 accumulation) -- reduces the conv
  * weight-grad partial slabs and gives Linear bias gradients (column sums of dy). */
 int avd_sum_rows(const float* in, int rows, int cols, long long ld, float* out, int accumulate,

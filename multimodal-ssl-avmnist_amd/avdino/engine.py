@@ -19,6 +19,8 @@ MI355X-native restructuring (results identical up to fp32 rounding):
   * cat() of image/audio features is a strided GEMM write; slices are pointer offsets;
   * EMA / Adam / grad all-reduce run on flat arenas (params.py).
 """
+import os
+
 import torch
 
 from . import contrastive, ops
@@ -85,6 +87,9 @@ class ConvBranch:
         nl = len(self.stack.convs)
         for i, (ci, co, k, pad) in enumerate(self.stack.convs):
             H, Ho, Hp = self.dims[i]
+            if i == 0 and nl > 1 and self._recompute_ok(N, B, ci, H, co, k, pad):
+                h = self._first_layer_recompute_fwd(ws, store, tag, ctx, h, N, G, B, update_running)
+                continue
             R = ops.cl_stat_rows(Ho, Ho, B, k, ci, co, self.act)
             y = ws.get(f"{tag}.y{i}", N * Ho * Ho * co, self.act)
             parts = ws.get("stat_parts", co * G * R * 2)
@@ -137,6 +142,59 @@ class ConvBranch:
             h = out
         return h.view(N, -1)
 
+    # ---- first layer without a stored conv output (avd_cl_c1_recompute): the audio conv1
+    # Off by default: measured slower than storing y (r1: the recomputing backward passes are
+    # VALU-bound); AVDINO_L1_RECOMPUTE=1 turns it on for experiments.
+    RECOMPUTE = os.environ.get("AVDINO_L1_RECOMPUTE", "0") == "1"
+
+    def _recompute_ok(self, N, B, ci, H, co, k, pad):
+        return (self.RECOMPUTE and self.act == torch.bfloat16 and
+                ops.cl_c1_recompute_rows(ops.C1_STATS, self.act, N, B, ci, H, H, co, k, pad) > 0)
+
+    def _first_layer_recompute_fwd(self, ws, store, tag, ctx, x, N, G, B, update_running):
+        ci, co, k, pad = self.stack.convs[0]
+        H, Ho, Hp = self.dims[0]
+        wk = ctx["wts"][0][0]
+        bias = store[self.stack.conv_keys[0] + ".bias"]
+        R = ops.cl_c1_recompute_rows(ops.C1_STATS, self.act, N, B, ci, H, H, co, k, pad)
+        parts = ws.get("stat_parts", co * G * R * 2)
+        ops.cl_c1_recompute(ops.C1_STATS, x, wk, bias, N, B, ci, H, H, co, k, pad, out=parts)
+        st = ws.get(f"{tag}.bn0", 4 * G * co).view(4, G * co)
+        bk = self.stack.bn_keys[0]
+        ops.bn_finalize(parts, G, R, co, B * Ho * Ho, store[bk + ".weight"], store[bk + ".bias"],
+                        st[0], st[1], st[2], st[3],
+                        store[bk + ".running_mean"] if update_running else None,
+                        store[bk + ".running_var"] if update_running else None)
+        if update_running:
+            store.buffers[bk + ".num_batches_tracked"] += G
+        out = ws.get(f"{tag}.x1", N * Hp * Hp * co, self.act)
+        ops.cl_c1_recompute(ops.C1_APPLY, x, wk, bias, N, B, ci, H, H, co, k, pad, scale=st[2],
+                            shift=st[3], z=out)
+        ctx["y"].append(None)          # never stored: the backward recomputes it
+        ctx["stats"].append(st)
+        ctx["x"].append(out)
+        return out
+
+    def _first_layer_recompute_bwd(self, ws, store, ctx, gout, N, G, B):
+        ci, co, k, pad = self.stack.convs[0]
+        H, Ho, Hp = self.dims[0]
+        x, wk, st = ctx["x"][0], ctx["wts"][0][0], ctx["stats"][0]
+        bk, ck = self.stack.bn_keys[0], self.stack.conv_keys[0]
+        bias = store[ck + ".bias"]
+        R = ops.cl_c1_recompute_rows(ops.C1_REDUCE, self.act, N, B, ci, H, H, co, k, pad)
+        parts = ws.get("bwd_parts", co * G * R * 2)
+        ops.cl_c1_recompute(ops.C1_REDUCE, x, wk, bias, N, B, ci, H, H, co, k, pad, scale=st[2],
+                            shift=st[3], mean=st[0], invstd=st[1], gz=gout, out=parts)
+        coef = ws.get("bwd_coef", G * co * 3)
+        ops.bn_bwd_finalize(parts, G, R, co, B * Ho * Ho, store[bk + ".weight"], st[0], st[1],
+                            coef, store.grad_of(bk + ".weight"), store.grad_of(bk + ".bias"),
+                            store.grad_of(ck + ".bias"))
+        nsl = ops.cl_c1_recompute_rows(ops.C1_WGRAD, self.act, N, B, ci, H, H, co, k, pad)
+        wparts = ws.get("wgrad_parts", nsl * co * ci * k * k)
+        ops.cl_c1_recompute(ops.C1_WGRAD, x, wk, bias, N, B, ci, H, H, co, k, pad, scale=st[2],
+                            shift=st[3], coef=coef, gz=gout, out=wparts)
+        ops.sum_rows(wparts, nsl, co * ci * k * k, store.grad_of(ck + ".weight"))
+
     def backward(self, ws, store, ctx, dfeat):
         """dfeat: f32 [N, F] gradient of the features; writes conv/BN parameter grads."""
         N, G = ctx["N"], ctx["G"]
@@ -147,6 +205,9 @@ class ConvBranch:
             ci, co, k, pad = self.stack.convs[i]
             H, Ho, Hp = self.dims[i]
             y, st = ctx["y"][i], ctx["stats"][i]
+            if y is None:              # recompute-path first layer
+                self._first_layer_recompute_bwd(ws, store, ctx, gout, N, G, B)
+                continue
             mode = self._tail_mode() if i == nl - 1 else 0
             bk, ck = self.stack.bn_keys[i], self.stack.conv_keys[i]
             R = ops.cl_bn_bwd_rows(B, co, Ho, Ho, self.act)

@@ -354,6 +354,37 @@ def cl_bn_bwd_apply_wgrad(y, gout, scale, shift, coef, x, parts, N, B, Cin, H, W
                         p(parts), dtcode(y), N, B, Cin, H, W, Cout, K, pad, stream()))
 
 
+C1_STATS, C1_APPLY, C1_REDUCE, C1_WGRAD = 0, 1, 2, 3
+
+
+def cl_c1_recompute_rows(pas, dtype, N, B, Cin, H, W, Cout, K, pad):
+    return lib.avd_cl_c1_recompute_rows(pas, 1 if dtype == torch.bfloat16 else 0, N, B, Cin, H, W,
+                                        Cout, K, pad)
+
+
+def cl_c1_recompute(pas, x, wk, bias, N, B, Cin, H, W, Cout, K, pad, scale=None, shift=None,
+                    mean=None, invstd=None, coef=None, gz=None, z=None, out=None):
+    """Recompute-y passes of the audio first layer (include/avdino.h avd_cl_c1_recompute)."""
+    rows = cl_c1_recompute_rows(pas, x.dtype, N, B, Cin, H, W, Cout, K, pad)
+    _need(rows > 0 and x.numel() == N * H * W * Cin, "c1 recompute shape")
+    G = N // B
+    if pas in (C1_STATS, C1_REDUCE):
+        _need(out is not None and out.numel() >= Cout * G * rows * 2, "c1 recompute rows")
+    if pas == C1_WGRAD:
+        _need(out is not None and out.numel() >= rows * Cout * Cin * K * K, "c1 recompute slabs")
+    npool = N * (H // 2) * (W // 2) * Cout
+    if pas == C1_APPLY:
+        _need(z is not None and z.numel() == npool and z.dtype == x.dtype, "c1 recompute z")
+    if pas in (C1_REDUCE, C1_WGRAD):
+        _need(gz is not None and gz.numel() == npool and gz.dtype == x.dtype, "c1 recompute gz")
+    nb = x.numel() * x.element_size() + (npool * 2 if pas != C1_STATS else 0)
+    name = ["stats", "apply", "reduce", "wgrad"][pas]
+    _timed(f"cl_c1_recompute_{name}[{N}x{H}x{W}x{Cin}->{Cout} k{K}]", nb, 2 * N * H * W * Cout * K * K,
+           lambda: call("avd_cl_c1_recompute", pas, p(x), p(wk), p(bias), p(scale), p(shift), p(mean),
+                        p(invstd), p(coef), p(gz), p(z), p(out), dtcode(x), N, B, Cin, H, W, Cout, K,
+                        pad, stream()))
+
+
 def sum_rows(x, rows, cols, out, accumulate=0, ld=None, off=0):
     ld = cols if ld is None else ld
     _need(off + (rows - 1) * ld + cols <= x.numel() and out.numel() >= cols, "sum_rows bounds")

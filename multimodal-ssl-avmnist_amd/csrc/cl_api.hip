@@ -31,6 +31,12 @@ int avd_c1p8_bwd_apply_wgrad(const void* y, const void* gout, const float* scale
                              const float* shift, const float* coef, const void* x, float* parts,
                              int N, int B, int H, int W, hipStream_t st);
 
+int avd_c1r_rows(int pass, int N, int B, int H);
+int avd_c1r_launch(int pass, const void* x, const void* wk, const float* bias, const float* scale,
+                   const float* shift, const float* mean, const float* invstd, const float* coef,
+                   const void* gz, void* z, float* out, int N, int B, int H, int W,
+                   hipStream_t st);
+
 namespace {
 bool dt_ok(int dt) { return dt == AVD_F32 || dt == AVD_BF16; }
 }  // namespace
@@ -63,6 +69,28 @@ int avd_cl_bn_bwd_apply_wgrad(const void* y, const void* gout, const float* scal
   if (avd_cl_apply_wgrad_slabs(dt, N, Cin, H, W, Cout, K, pad) == 0) return AVD_ERR_SHAPE;
   return avd_c1p8_bwd_apply_wgrad(y, gout, scale, shift, coef, x, parts, N, B, H, W,
                                   avd_stream(stream));
+}
+
+int avd_cl_c1_recompute_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cout,
+                             int K, int pad) {
+  if (pass < 0 || pass > 3 || B <= 0 || N % B) return 0;
+  if (!avd_c1p8_eligible(dt, Cin, Cout, K, H, W) || pad != 2 || W > 112) return 0;
+  return avd_c1r_rows(pass, N, B, H);
+}
+
+int avd_cl_c1_recompute(int pass, const void* x, const void* wk, const float* bias,
+                        const float* scale, const float* shift, const float* mean,
+                        const float* invstd, const float* coef, const void* gz, void* z,
+                        float* out, int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
+                        int pad, void* stream) {
+  if (!x || !wk) return AVD_ERR_ARG;
+  if (avd_cl_c1_recompute_rows(pass, dt, N, B, Cin, H, W, Cout, K, pad) == 0) return AVD_ERR_SHAPE;
+  const bool need_bn = pass != 0, need_g = pass >= 2;
+  if ((need_bn && (!scale || !shift)) || (pass == 1 && !z) || (pass != 1 && !out) ||
+      (need_g && !gz) || (pass == 2 && (!mean || !invstd)) || (pass == 3 && !coef))
+    return AVD_ERR_ARG;
+  return avd_c1r_launch(pass, x, wk, bias, scale, shift, mean, invstd, coef, gz, z, out, N, B, H,
+                        W, avd_stream(stream));
 }
 
 int avd_cl_stat_rows(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt) {

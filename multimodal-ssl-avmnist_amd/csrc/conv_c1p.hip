@@ -33,6 +33,7 @@ constexpr int XOFF = 8;        // LDS column of image column 0 (16-byte aligned 
 constexpr int ITW = 144;       // LDS row stride in bf16 (72 dwords = 8 mod 64 banks)
 constexpr int ITWD = ITW / 2;
 constexpr int COUT = 8;
+constexpr int MTMAX = 7;       // 16-pixel column tiles per strip (W <= 112)
 
 // (row, dword) of the 4 B-fragment dwords for lane half h = lane>>4 (see header)
 __device__ __forceinline__ int boff(int h, int d) {
@@ -49,7 +50,7 @@ __global__ __launch_bounds__(256) void conv_c1p8_kernel(const bf16* __restrict__
                                                         int W, int tps) {
   __shared__ __attribute__((aligned(16))) bf16 xs[(TH + 4) * ITW];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int n = blockIdx.x / tps, ty0 = (blockIdx.x - n * tps) * TH;
+  const int n = blockIdx.x;                     // one block = one sample, all its row tiles
   const int h = lane >> 4, p = lane & 15, j = lane >> 5, cs = h & 1;
 
   // ---- A fragment (weights) for this lane: row m = (j', c'), k = 8h .. 8h+7; wk is the
@@ -70,49 +71,49 @@ __global__ __launch_bounds__(256) void conv_c1p8_kernel(const bf16* __restrict__
   float bv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) bv[i] = bias ? bias[4 * cs + i] : 0.f;
-
-  // ---- stage rows ty0-2 .. ty0+TH+1 (zero outside the image); pad columns zeroed
-  const int cpr = W >> 3;                       // 16-byte chunks per image row
-  const int nch = (TH + 4) * cpr;
-  for (int t = tid; t < nch; t += 256) {
-    const int r = t / cpr, c = t - r * cpr;
-    const int iy = ty0 - 2 + r;
-    const bool ok = iy >= 0 && iy < H;
-    const u4 v = *reinterpret_cast<const u4*>(x + ((size_t)n * H + (ok ? iy : 0)) * W + 8 * c);
-    *reinterpret_cast<u4*>(xs + r * ITW + XOFF + 8 * c) = ok ? v : u4{0u, 0u, 0u, 0u};
-  }
-  for (int t = tid; t < (TH + 4) * 2; t += 256) {
-    const int r = t >> 1, side = t & 1;
-    *reinterpret_cast<u4*>(xs + r * ITW + (side ? XOFF + W : 0)) = u4{0u, 0u, 0u, 0u};
-  }
-  __syncthreads();
-
   const unsigned* xd = reinterpret_cast<const unsigned*>(xs);
   const int q = p & 7, rp = p >> 3;
   int off[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) off[d] = boff(h, d) + rp * ITWD + q + 3;   // + (x0 - 2 + XOFF)/2
   float ss[4] = {0.f, 0.f, 0.f, 0.f}, sq[4] = {0.f, 0.f, 0.f, 0.f};
-  const int mts = W >> 4;
-  for (int s = wave; s < TH / 2; s += 4) {      // 2-row strips
-    const int oy = ty0 + 2 * s + rp;
-    bf16* yrow = y + ((size_t)n * H + oy) * W * COUT + 4 * cs;
-    for (int mt = 0; mt < mts; ++mt) {
-      const int base = 2 * s * ITWD + 8 * mt;
-      const u4 bw = u4{xd[base + off[0]], xd[base + off[1]], xd[base + off[2]], xd[base + off[3]]};
-      f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, bw),
-                                                       f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      const uint32_t lo = pack_bf16x2(acc[0] + bv[0], acc[1] + bv[1]);
-      const uint32_t hi = pack_bf16x2(acc[2] + bv[2], acc[3] + bv[3]);
-      const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
-                          __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+  const int mts = W >> 4, cpr = W >> 3;
+  for (int tile = 0; tile < tps; ++tile) {
+    const int ty0 = tile * TH;
+    if (tile) __syncthreads();
+    // ---- stage rows ty0-2 .. ty0+TH+1 (zero outside the image); pad columns zeroed
+    for (int t = tid; t < (TH + 4) * cpr; t += 256) {
+      const int r = t / cpr, c = t - r * cpr;
+      const int iy = ty0 - 2 + r;
+      const bool ok = iy >= 0 && iy < H;
+      const u4 v = *reinterpret_cast<const u4*>(x + ((size_t)n * H + (ok ? iy : 0)) * W + 8 * c);
+      *reinterpret_cast<u4*>(xs + r * ITW + XOFF + 8 * c) = ok ? v : u4{0u, 0u, 0u, 0u};
+    }
+    if (tid < (TH + 4) * 2) {
+      const int r = tid >> 1, side = tid & 1;
+      *reinterpret_cast<u4*>(xs + r * ITW + (side ? XOFF + W : 0)) = u4{0u, 0u, 0u, 0u};
+    }
+    __syncthreads();
+    for (int s = wave; s < TH / 2; s += 4) {      // 2-row strips
+      const int oy = ty0 + 2 * s + rp;
+      bf16* yrow = y + ((size_t)n * H + oy) * W * COUT + 4 * cs;
+      for (int mt = 0; mt < mts; ++mt) {
+        const int base = 2 * s * ITWD + 8 * mt;
+        const u4 bw = u4{xd[base + off[0]], xd[base + off[1]], xd[base + off[2]], xd[base + off[3]]};
+        f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, bw),
+                                                         f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const uint32_t lo = pack_bf16x2(acc[0] + bv[0], acc[1] + bv[1]);
+        const uint32_t hi = pack_bf16x2(acc[2] + bv[2], acc[3] + bv[3]);
+        const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                            __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        ss[i] += v[i];
-        sq[i] = fmaf(v[i], v[i], sq[i]);
+        for (int i = 0; i < 4; ++i) {
+          ss[i] += v[i];
+          sq[i] = fmaf(v[i], v[i], sq[i]);
+        }
+        const int ox = 16 * mt + 2 * q + j;
+        *reinterpret_cast<uint2*>(yrow + (size_t)ox * COUT) = make_uint2(lo, hi);
       }
-      const int ox = 16 * mt + 2 * q + j;
-      *reinterpret_cast<uint2*>(yrow + (size_t)ox * COUT) = make_uint2(lo, hi);
     }
   }
   if (!stats) return;
@@ -128,7 +129,7 @@ __global__ __launch_bounds__(256) void conv_c1p8_kernel(const bf16* __restrict__
     }
   }
   if ((lane & 47) == 0) {                        // lanes 0 (channels 0-3) and 16 (4-7)
-    const size_t nrows = (size_t)N * (size_t)(H / TH) * 4;
+    const size_t nrows = (size_t)N * 4;             // one row per (sample, wave)
     const size_t row = (size_t)blockIdx.x * 4 + wave;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -145,16 +146,16 @@ __global__ __launch_bounds__(256) void conv_c1p8_kernel(const bf16* __restrict__
 // W % 16 == 0, W <= 128 (the caller rejects other paddings for this shape).
 bool avd_c1p8_eligible(int dt, int Cin, int Cout, int K, int Ho, int Wo) {
   return dt == AVD_BF16 && Cin == 1 && Cout == 8 && K == 5 && Ho % TH == 0 && Wo % 16 == 0 &&
-         Wo + XOFF + 2 <= ITW;
+         Wo <= 16 * MTMAX;
 }
 
-int avd_c1p8_stat_rows(int H, int B) { return B * (H / TH) * 4; }
+int avd_c1p8_stat_rows(int H, int B) { (void)H; return B * 4; }
 
 int avd_c1p8_fwd(const void* x, const void* wk, const float* bias, void* y, float* stats, int N,
                  int H, int W, hipStream_t st) {
   const int tps = H / TH;
-  conv_c1p8_kernel<<<N * tps, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, (bf16*)y,
-                                            stats, N, H, W, tps);
+  conv_c1p8_kernel<<<N, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, (bf16*)y, stats, N,
+                                      H, W, tps);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
@@ -355,6 +356,312 @@ int avd_c1p8_bwd_apply_wgrad(const void* y, const void* gout, const float* scale
   c1p8_bwd_wgrad_kernel<<<avd_c1p8_wgrad_slabs(N, H), 256, 0, st>>>(
       (const bf16*)x, (const bf16*)y, (const bf16*)gout, scale, shift, coef, parts, B, H, W, ntiles,
       tps);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+// ============================================================================ recompute path
+// The same layer without ever storing its conv output y (1.44 GB per config-2 step): every
+// pass re-derives y from the 180 MB input with the pixel-pair MFMA (4 ds_read_b32 + 1 MFMA per
+// 32 outputs, bit-identical bf16 values in every pass) into an LDS tile, then runs its own
+// epilogue:
+//   RC_STATS   BN partial (sum, sumsq) rows of the rounded values  (= conv_c1p8_kernel's)
+//   RC_APPLY   BN -> ReLU -> 2x2 max-pool -> z (the next layer's input; avd_cl_bn_relu_pool)
+//   RC_REDUCE  BN-backward partials (sum dz, sum dz*xhat) rows      (= avd_cl_bn_bwd_reduce)
+//   RC_WGRAD   BN-backward apply + weight gradient slabs            (= avd_cl_bn_bwd_apply_wgrad)
+namespace {
+
+enum { RC_STATS = 0, RC_APPLY = 1, RC_REDUCE = 2, RC_WGRAD = 3 };
+
+__device__ __forceinline__ void unpack8(u4 v, float (&f)[8]) {
+  const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+template <int PASS>
+__global__ __launch_bounds__(256) void c1p8_recompute_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ wk, const float* __restrict__ bias,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ coef, const bf16* __restrict__ gz, bf16* __restrict__ z,
+    float* __restrict__ out, int B, int H, int W, int ntiles, int tps) {
+  constexpr bool NEED_Y = PASS != RC_STATS;
+  constexpr bool WG = PASS == RC_WGRAD;
+  __shared__ __attribute__((aligned(16))) bf16 xs[(TH + 4) * ITW];
+  __shared__ __attribute__((aligned(16))) bf16 ys[NEED_Y ? TH * WMAX * COUT : 8];
+  __shared__ __attribute__((aligned(16))) bf16 xc[WG ? 2 : 1][WG ? 3 : 1][WG ? TH + 4 : 1][XCW];
+  __shared__ float red[WG ? 4 * 16 * 32 : 4 * 16];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int h = lane >> 4, p = lane & 15, j = lane >> 5, cs = h & 1;
+  const int q = p & 7, rp = p >> 3;
+  const int Hp = H >> 1, Wp = W >> 1, cpr = W >> 3, mts = W >> 4;
+
+  bf16x8 a;
+  {
+    const int m = lane & 15, jj = m >> 3, c = m & 7;
+    __bf16 e[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int k = 8 * h + t, ky = k / 6, kx = k % 6 - jj;
+      const bool ok = k < 30 && kx >= 0 && kx < 5;
+      const float v = bf2f(wk[c * 32 + (ok ? ky * 5 + kx : 0)]);
+      e[t] = (__bf16)(ok ? v : 0.f);
+    }
+    a = bf16x8{e[0], e[1], e[2], e[3], e[4], e[5], e[6], e[7]};
+  }
+  float bv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bv[i] = bias ? bias[4 * cs + i] : 0.f;
+  int off[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) off[d] = boff(h, d) + rp * ITWD + q + 3;
+
+  float ss[4] = {0.f, 0.f, 0.f, 0.f}, sq[4] = {0.f, 0.f, 0.f, 0.f};   // STATS
+  float s1[COUT], s2[COUT];                                           // REDUCE
+#pragma unroll
+  for (int e = 0; e < COUT; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};      // WGRAD
+  int bb[2], ba[2], bky[2];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    int t = 16 * tt + p;
+    if (t >= 30) t = 0;
+    const int ky = t / 6, k2 = t % 6 - 2;
+    bky[tt] = ky;
+    bb[tt] = k2 & 1;
+    ba[tt] = (k2 >= 0 ? k2 >> 1 : -1) + 1;
+  }
+
+  // WGRAD: blocks stride over all tiles (one dW slab each); the other passes: one block = one
+  // sample (its tps row tiles), so the per-block setup is amortised and rows are per sample
+  const int t_begin = WG ? (int)blockIdx.x : (int)blockIdx.x * tps;
+  const int t_end = WG ? ntiles : t_begin + tps;
+  const int t_step = WG ? (int)gridDim.x : 1;
+  for (int tile = t_begin; tile < t_end; tile += t_step) {
+    const int n = tile / tps, ty0 = (tile - n * tps) * TH, grp = n / B;
+    __syncthreads();
+    // ---- input tile (natural layout, zero pads)
+    for (int t = tid; t < (TH + 4) * cpr; t += 256) {
+      const int r = t / cpr, c = t - r * cpr;
+      const int iy = ty0 - 2 + r;
+      const bool ok = iy >= 0 && iy < H;
+      const u4 v = *reinterpret_cast<const u4*>(x + ((size_t)n * H + (ok ? iy : 0)) * W + 8 * c);
+      *reinterpret_cast<u4*>(xs + r * ITW + XOFF + 8 * c) = ok ? v : u4{0u, 0u, 0u, 0u};
+    }
+    for (int t = tid; t < (TH + 4) * 2; t += 256) {
+      const int r = t >> 1, side = t & 1;
+      *reinterpret_cast<u4*>(xs + r * ITW + (side ? XOFF + W : 0)) = u4{0u, 0u, 0u, 0u};
+    }
+    __syncthreads();
+    // ---- recompute y (rounded to bf16 exactly as the stored-y path)
+    const unsigned* xd = reinterpret_cast<const unsigned*>(xs);
+    for (int s = wave; s < TH / 2; s += 4) {
+      for (int mt = 0; mt < mts; ++mt) {
+        const int base = 2 * s * ITWD + 8 * mt;
+        const u4 bw = u4{xd[base + off[0]], xd[base + off[1]], xd[base + off[2]], xd[base + off[3]]};
+        const f4 r4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, bw),
+                                                              f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const uint32_t lo = pack_bf16x2(r4[0] + bv[0], r4[1] + bv[1]);
+        const uint32_t hi = pack_bf16x2(r4[2] + bv[2], r4[3] + bv[3]);
+        if constexpr (PASS == RC_STATS) {
+          const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                              __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            ss[i] += v[i];
+            sq[i] = fmaf(v[i], v[i], sq[i]);
+          }
+        } else {
+          const int ox = 16 * mt + 2 * q + j;
+          *reinterpret_cast<uint2*>(&ys[((2 * s + rp) * WMAX + ox) * COUT + 4 * cs]) =
+              make_uint2(lo, hi);
+        }
+      }
+    }
+    if constexpr (!NEED_Y) continue;
+    __syncthreads();
+    // ---- per-window epilogues (one thread = one 2x2 window, all 8 channels)
+    float sc[COUT], sf[COUT];
+#pragma unroll
+    for (int e = 0; e < COUT; ++e) {
+      sc[e] = scale[grp * COUT + e];
+      sf[e] = shift[grp * COUT + e];
+    }
+    for (int w = tid; w < (TH / 2) * Wp; w += 256) {
+      const int hp = w / Wp, wp = w - hp * Wp;
+      float yv[4][COUT];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        unpack8(*reinterpret_cast<const u4*>(
+                    &ys[((2 * hp + (k >> 1)) * WMAX + 2 * wp + (k & 1)) * COUT]), yv[k]);
+      float best[COUT];
+      int arg[COUT];
+#pragma unroll
+      for (int e = 0; e < COUT; ++e) {
+        best[e] = fmaxf(fmaf(yv[0][e], sc[e], sf[e]), 0.f);
+        arg[e] = 0;
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+          const float r = fmaxf(fmaf(yv[k][e], sc[e], sf[e]), 0.f);
+          if (r > best[e]) { best[e] = r; arg[e] = k; }
+        }
+      }
+      const size_t pw = ((size_t)n * Hp + (ty0 >> 1) + hp) * Wp + wp;
+      if constexpr (PASS == RC_APPLY) {
+        unsigned o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = pack_bf16x2(best[2 * i], best[2 * i + 1]);
+        *reinterpret_cast<u4*>(z + pw * COUT) = u4{o[0], o[1], o[2], o[3]};
+      } else {
+        float gg[COUT];
+        unpack8(*reinterpret_cast<const u4*>(gz + pw * COUT), gg);
+        if constexpr (PASS == RC_REDUCE) {
+#pragma unroll
+          for (int e = 0; e < COUT; ++e) {
+            const int ag = arg[e];
+            const float ya = ag == 0 ? yv[0][e] : ag == 1 ? yv[1][e] : ag == 2 ? yv[2][e] : yv[3][e];
+            const float dz = best[e] > 0.f ? gg[e] : 0.f;
+            s1[e] += dz;
+            s2[e] += dz * (ya - mean[grp * COUT + e]) * invstd[grp * COUT + e];
+          }
+        } else {   // RC_WGRAD: dy in place of the window's y
+          unsigned ow[4][4];
+#pragma unroll
+          for (int e = 0; e < COUT; ++e) {
+            const int gc = (grp * COUT + e) * 3;
+            const float k1 = coef[gc], kx = coef[gc + 1], k0 = coef[gc + 2];
+            const float dz = best[e] > 0.f ? gg[e] : 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const float d = fmaf(k1, arg[e] == k ? dz : 0.f, fmaf(kx, yv[k][e], k0));
+              const uint32_t hb = __builtin_bit_cast(uint16_t, (__bf16)d);
+              if (e & 1) ow[k][e >> 1] |= hb << 16;
+              else ow[k][e >> 1] = hb;
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            *reinterpret_cast<u4*>(&ys[((2 * hp + (k >> 1)) * WMAX + 2 * wp + (k & 1)) * COUT]) =
+                u4{ow[k][0], ow[k][1], ow[k][2], ow[k][3]};
+        }
+      }
+    }
+    if constexpr (WG) {
+      // parity/shift copies of the input rows, from the natural tile:
+      // xc[b][a][r][P] = x[2(P+a-1)+b] = xs[r][XOFF + 2(P+a-1) + b]  (pads are zero)
+      for (int t = tid; t < (TH + 4) * 3 * (Wp >> 1); t += 256) {
+        const int r = t / (3 * (Wp >> 1)), rem = t - r * 3 * (Wp >> 1);
+        const int aa = rem / (Wp >> 1), P = 2 * (rem - aa * (Wp >> 1));
+        const unsigned* src = reinterpret_cast<const unsigned*>(xs + r * ITW + XOFF) + (P + aa - 1);
+        const unsigned d0 = src[0], d1 = src[1];
+        *reinterpret_cast<unsigned*>(&xc[0][aa][r][P]) = (d0 & 0xffffu) | (d1 << 16);
+        *reinterpret_cast<unsigned*>(&xc[1][aa][r][P]) = (d0 >> 16) | (d1 & 0xffff0000u);
+      }
+      __syncthreads();
+      const int segs = W >> 4, nkb = TH * segs;
+      for (int ks = wave; 4 * ks < nkb; ks += 4) {
+        const int kb = 4 * ks + h;
+        const int r = kb / segs, P0 = 8 * (kb - r * segs);
+        const int qq = p >> 2, pp = p & 3;
+        s4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s4*)&ys[(r * WMAX + 2 * (P0 + qq)) * COUT + 4 * pp]);
+        s4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s4*)&ys[(r * WMAX + 2 * (P0 + 4 + qq)) * COUT + 4 * pp]);
+        typedef __attribute__((ext_vector_type(8))) short s8;
+        const bf16x8 A = __builtin_bit_cast(bf16x8, s8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]});
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          const u4 bw = *reinterpret_cast<const u4*>(&xc[bb[tt]][ba[tt]][r + bky[tt]][P0]);
+          acc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, __builtin_bit_cast(bf16x8, bw),
+                                                           acc[tt], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  if constexpr (PASS == RC_STATS || PASS == RC_REDUCE) {
+    // per-wave partial rows [C][G][R][2], R = B * 4 (one block = one sample)
+    const int n = blockIdx.x, grp = n / B;
+    const size_t R = (size_t)B * 4;
+    const size_t row = (size_t)(n - grp * B) * 4 + wave;
+    const int G = ntiles / (B * tps);
+    if constexpr (PASS == RC_STATS) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int m = 1; m <= 32; m <<= 1) {
+          if (m == 16) continue;
+          ss[i] += __shfl_xor(ss[i], m, 64);
+          sq[i] += __shfl_xor(sq[i], m, 64);
+        }
+      if ((lane & 47) == 0)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int co = 4 * cs + i;
+          out[(((size_t)co * G + grp) * R + row) * 2] = ss[i];
+          out[(((size_t)co * G + grp) * R + row) * 2 + 1] = sq[i];
+        }
+    } else {
+#pragma unroll
+      for (int e = 0; e < COUT; ++e) {
+        s1[e] = wave_sum(s1[e]);
+        s2[e] = wave_sum(s2[e]);
+      }
+      if (lane == 0)
+#pragma unroll
+        for (int e = 0; e < COUT; ++e) {
+          out[(((size_t)e * G + grp) * R + row) * 2] = s1[e];
+          out[(((size_t)e * G + grp) * R + row) * 2 + 1] = s2[e];
+        }
+    }
+  }
+  if constexpr (WG) {
+    __syncthreads();
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[(wave * 16 + 4 * h + i) * 32 + 16 * tt + p] = acc[tt][i];
+    __syncthreads();
+    for (int o = tid; o < COUT * 25; o += 256) {
+      const int c = o / 25, t = o - c * 25, ky = t / 5, kx = t - ky * 5;
+      float s = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < 4; ++wv)
+        s += red[(wv * 16 + c) * 32 + ky * 6 + kx] + red[(wv * 16 + 8 + c) * 32 + ky * 6 + kx + 1];
+      out[(size_t)blockIdx.x * (COUT * 25) + o] = s;
+    }
+  }
+}
+
+}  // namespace
+
+// rows per BN group (stats / reduce passes) or slabs (wgrad pass)
+int avd_c1r_rows(int pass, int N, int B, int H) {
+  return pass == RC_WGRAD ? avd_c1p8_wgrad_slabs(N, H) : B * 4;
+}
+
+int avd_c1r_launch(int pass, const void* x, const void* wk, const float* bias, const float* scale,
+                   const float* shift, const float* mean, const float* invstd, const float* coef,
+                   const void* gz, void* z, float* out, int N, int B, int H, int W,
+                   hipStream_t st) {
+  const int tps = H / TH, ntiles = N * tps;
+  const int grid = pass == RC_WGRAD ? avd_c1p8_wgrad_slabs(N, H) : N;
+#define AVD_RC(PS)                                                                             \
+  c1p8_recompute_kernel<PS><<<grid, 256, 0, st>>>(                                             \
+      (const bf16*)x, (const bf16*)wk, bias, scale, shift, mean, invstd, coef, (const bf16*)gz, \
+      (bf16*)z, out, B, H, W, ntiles, tps)
+  switch (pass) {
+    case RC_STATS: AVD_RC(RC_STATS); break;
+    case RC_APPLY: AVD_RC(RC_APPLY); break;
+    case RC_REDUCE: AVD_RC(RC_REDUCE); break;
+    case RC_WGRAD: AVD_RC(RC_WGRAD); break;
+    default: return AVD_ERR_ARG;
+  }
+#undef AVD_RC
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

@@ -240,3 +240,67 @@ def test_cl_bn_bwd_apply_wgrad_fused_first_layer(ops, HN):
                                                           ((0, 0), (0, 0), (2, 2), (2, 2))), (K, K), (2, 3))
     dw64 = np.einsum("nohw,nchwij->ocij", nchw(host(dy)), win, optimize=True)
     assert rel(host(dw), dw64) < 1e-5
+
+
+@pytest.mark.parametrize("HN", [(112, 4), (48, 6)])
+def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN):
+    """avd_cl_c1_recompute (the audio conv1 without a stored conv output) against the stored-y
+    kernels on the same bf16 operands: identical pooled output (bit-exact: same rounded y), and
+    the statistics / BN-backward partials / weight gradient to fp32 summation order."""
+    H, N = HN
+    B, Cin, C, K, pad = N // 2, 1, 8, 5, 2
+    G = N // B
+    T = torch.bfloat16
+    g = np.random.default_rng(H + 1)
+    x = bf(g.uniform(0, 1, (N, H, H, 1)))
+    w = bf(g.uniform(-1, 1, (C, 1, K, K)) / 5)
+    b = g.uniform(-0.1, 0.1, C).astype(np.float32)
+    tx, tb = dev(x, T), dev(b)
+    wk = torch.empty(ops.cl_weight_elems(C, 1, K, 0), device="cuda", dtype=T)
+    ops.cl_weight_layout(dev(w), wk, 0)
+    # stored-y path
+    y = torch.empty(N, H, H, C, device="cuda", dtype=T)
+    R0 = ops.cl_stat_rows(H, H, B, K, 1, C, T)
+    st0 = torch.empty(C * G * R0 * 2, device="cuda")
+    ops.cl_conv_fwd(tx, wk, tb, y, st0, N, B, 1, H, H, C, K, pad)
+    R1 = ops.cl_c1_recompute_rows(ops.C1_STATS, T, N, B, 1, H, H, C, K, pad)
+    st1 = torch.empty(C * G * R1 * 2, device="cuda")
+    ops.cl_c1_recompute(ops.C1_STATS, tx, wk, tb, N, B, 1, H, H, C, K, pad, out=st1)
+    s0 = host(st0).reshape(C, G, R0, 2).sum(2)
+    s1 = host(st1).reshape(C, G, R1, 2).sum(2)
+    assert rel(s1, s0) < 1e-6
+    gamma = (1 + g.uniform(-.2, .2, C)).astype(np.float32)
+    beta = g.uniform(-.2, .2, C).astype(np.float32)
+    bn = torch.empty(4, G * C, device="cuda")
+    ops.bn_finalize(st0, G, R0, C, B * H * H, dev(gamma), dev(beta), bn[0], bn[1], bn[2], bn[3])
+    z0 = torch.empty(N, H // 2, H // 2, C, device="cuda", dtype=T)
+    ops.cl_bn_relu_pool(y, bn[2], bn[3], z0, 0, N, B, C, H, H)
+    z1 = torch.empty_like(z0)
+    ops.cl_c1_recompute(ops.C1_APPLY, tx, wk, tb, N, B, 1, H, H, C, K, pad, scale=bn[2],
+                        shift=bn[3], z=z1)
+    assert torch.equal(z0, z1)
+    gz = dev(bf(g.uniform(-1, 1, (N, H // 2, H // 2, C))), T)
+    Rb = ops.cl_bn_bwd_rows(B, C, H, H, T)
+    p0 = torch.empty(C * G * Rb * 2, device="cuda")
+    ops.cl_bn_bwd_reduce(y, gz, 0, bn[2], bn[3], bn[0], bn[1], p0, N, B, C, H, H)
+    Rr = ops.cl_c1_recompute_rows(ops.C1_REDUCE, T, N, B, 1, H, H, C, K, pad)
+    p1 = torch.empty(C * G * Rr * 2, device="cuda")
+    ops.cl_c1_recompute(ops.C1_REDUCE, tx, wk, tb, N, B, 1, H, H, C, K, pad, scale=bn[2],
+                        shift=bn[3], mean=bn[0], invstd=bn[1], gz=gz, out=p1)
+    r0 = host(p0).reshape(C, G, Rb, 2).sum(2)
+    r1 = host(p1).reshape(C, G, Rr, 2).sum(2)
+    assert rel(r1, r0) < 1e-5, rel(r1, r0)
+    coef = torch.empty(G * C * 3, device="cuda")
+    dg, dbt = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    ops.bn_bwd_finalize(p0, G, Rb, C, B * H * H, dev(gamma), bn[0], bn[1], coef, dg, dbt, None)
+    ns = ops.cl_apply_wgrad_slabs(T, N, 1, H, H, C, K, pad)
+    f0 = torch.empty(ns * C * K * K, device="cuda")
+    ops.cl_bn_bwd_apply_wgrad(y, gz, bn[2], bn[3], coef, tx, f0, N, B, 1, H, H, C, K, pad)
+    nw = ops.cl_c1_recompute_rows(ops.C1_WGRAD, T, N, B, 1, H, H, C, K, pad)
+    f1 = torch.empty(nw * C * K * K, device="cuda")
+    ops.cl_c1_recompute(ops.C1_WGRAD, tx, wk, tb, N, B, 1, H, H, C, K, pad, scale=bn[2],
+                        shift=bn[3], coef=coef, gz=gz, out=f1)
+    d0, d1 = torch.empty(C * K * K, device="cuda"), torch.empty(C * K * K, device="cuda")
+    ops.sum_rows(f0, ns, C * K * K, d0)
+    ops.sum_rows(f1, nw, C * K * K, d1)
+    assert rel(host(d1), host(d0)) < 1e-6
