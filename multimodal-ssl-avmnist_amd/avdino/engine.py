@@ -326,7 +326,7 @@ class MultiCentralEngine:
     semi_supervised}``)."""
 
     def __init__(self, store, mode, E, D, P, hp, act_dtype=F32, grad_hook=None, seed=0,
-                 buffer_hook=None, negatives="global", group=None):
+                 buffer_hook=None, negatives="global", group=None, concurrent=True):
         self.store, self.mode, self.E, self.D, self.P, self.hp = store, mode, E, D, P, hp
         self.act = act_dtype
         # Linear layers: bf16 MFMA in the bf16 mode (like the reference's fp16 autocast),
@@ -344,6 +344,12 @@ class MultiCentralEngine:
             hi, ha = HEAD_NAMES[mode]
             out = 10 if mode == "semi_supervised" else P
             self.heads = (ProjHead(hi, E, out, gemm_mode=self.gm), ProjHead(ha, E, out, gemm_mode=self.gm))
+        # teacher forward and the image-branch backward run on a side stream with their own
+        # scratch (Workspace, split-K GEMM buffer), joined by events; concurrent=False keeps
+        # everything on the caller's stream
+        self.side = torch.cuda.Stream(store.device) if (concurrent and store.device.type == "cuda") else None
+        self.tws = Workspace(store.device) if self.side is not None else self.ws
+        self.iws = Workspace(store.device) if self.side is not None else self.ws
         self.grad_hook = grad_hook      # e.g. DDP all-reduce of store.grad (avdino.dist)
         self.buffer_hook = buffer_hook  # e.g. rank-0 buffer broadcast before each forward
         # InfoNCE negatives under DDP: "global" = all-gathered (single-device loss over the
@@ -353,10 +359,29 @@ class MultiCentralEngine:
         self.step_idx = 0
         self.last = {}
 
+    # -------------------------------------------------------------- streams
+    def _on_side(self, fn):
+        """Run fn() on the side stream after everything queued so far on the current stream;
+        returns (fn's result, completion event), or runs inline without a side stream."""
+        if self.side is None:
+            return fn(), None
+        main = torch.cuda.current_stream(self.store.device)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            out = fn()
+            done = torch.cuda.Event()
+            done.record(self.side)
+        return out, done
+
+    def _join(self, done):
+        if done is not None:
+            torch.cuda.current_stream(self.store.device).wait_event(done)
+
     # -------------------------------------------------------------- pieces
-    def _encoder_fwd(self, prefix, ib, ab, x_img, x_aud, N, G, tag, need_dgrad, update_running=True):
+    def _encoder_fwd(self, prefix, ib, ab, x_img, x_aud, N, G, tag, need_dgrad, update_running=True,
+                     ws=None):
         """Image + audio conv stacks and their Linear(., E) into one [N, 2E] buffer (= the cat)."""
-        ws, st, E = self.ws, self.store, self.E
+        ws, st, E = ws or self.ws, self.store, self.E
         fi, ci = ib.forward(ws, st, tag + ".img", x_img, N, G, update_running, need_dgrad)
         fa, ca = ab.forward(ws, st, tag + ".aud", x_aud, N, G, update_running, need_dgrad)
         cat = ws.get(tag + ".cat", N * 2 * E)
@@ -366,9 +391,9 @@ class MultiCentralEngine:
                        cat, N, out_ld=2 * E, out_off=E, mode=self.gm)
         return cat, (fi, ci, fa, ca)
 
-    def _fusion_fwd(self, prefix, cat, rows, tag, seed):
+    def _fusion_fwd(self, prefix, cat, rows, tag, seed, ws=None):
         """fusion: Linear(2E,E) -> ReLU -> Dropout(0.3, hard-coded dino.py:204/215) -> Linear(E,D)."""
-        ws, st, E, D = self.ws, self.store, self.E, self.D
+        ws, st, E, D = ws or self.ws, self.store, self.E, self.D
         h = ws.get(tag + ".fh", rows * E)
         ops.linear_fwd(cat, st[prefix + ".fusion.0.weight"], st[prefix + ".fusion.0.bias"], h, rows,
                        x_ld=2 * E, mode=self.gm)
@@ -408,18 +433,26 @@ class MultiCentralEngine:
         N = NG * B
         base = (self.seed * 1000003 + self.step_idx * 16) & 0xFFFFFFFFFFFF
 
+        # teacher: global views (prefix of the staged buffers), train-mode BN, no grad -- on a
+        # side stream, concurrently with the student (independent until the loss)
+        def teacher():
+            tws = self.tws
+            tcat, _ = self._encoder_fwd("teacher", self.t_img, self.t_aud, x_img[:G * B * 784],
+                                        x_aud[:G * B * 12544], G * B, G, "t", need_dgrad=False,
+                                        ws=tws)
+            tout, _ = self._fusion_fwd("teacher", tcat, G * B, "t", base + 2, ws=tws)
+            t_proj = tws.get("t_proj", G * B * P)
+            self.tproj.forward(tws, st, "tp", tout, G * B, t_proj, 0.0, 0)
+            return t_proj
+
+        t_proj, t_done = self._on_side(teacher)
         # student: all views (+ originals) in one pass per conv layer
         cat, senc = self._encoder_fwd("student", self.img, self.aud, x_img, x_aud, N, NG, "s",
                                       need_dgrad=training)
         fout, sfus = self._fusion_fwd("student", cat, V * B, "s", base + 1)
-        # teacher: global views (prefix of the staged buffers), train-mode BN, no grad
-        tcat, _ = self._encoder_fwd("teacher", self.t_img, self.t_aud, x_img[:G * B * 784],
-                                    x_aud[:G * B * 12544], G * B, G, "t", need_dgrad=False)
-        tout, _ = self._fusion_fwd("teacher", tcat, G * B, "t", base + 2)
         s_proj = ws.get("s_proj", V * B * P)
         spc = self.sproj.forward(ws, st, "sp", fout, V * B, s_proj, hp.dropout, base + 3)
-        t_proj = ws.get("t_proj", G * B * P)
-        self.tproj.forward(ws, st, "tp", tout, G * B, t_proj, 0.0, 0)
+        self._join(t_done)
 
         # DINO loss (+ centring and centre EMA) -- forward and d/ds in one pass
         loss_parts = ws.get("loss_parts", V * B + B)
@@ -511,17 +544,24 @@ class MultiCentralEngine:
             hi.backward(ws, st, ci, dzi, dcat, dx_ld=2 * E, dx_off=off)
             ha.backward(ws, st, ca, dza, dcat, dx_ld=2 * E, dx_off=off + E)
         fi, cimg, fa, caud = c["senc"]
-        dfi = ws.get("dfeat_img", N * fi.shape[1])
-        ops.linear_bwd(dcat, fi, st["student.image_encoder.1.weight"],
-                       st.grad_of("student.image_encoder.1.weight"),
-                       st.grad_of("student.image_encoder.1.bias"), dfi, N, dout_ld=2 * E, mode=self.gm)
-        self.img.backward(ws, st, cimg, dfi)
+
+        def image_branch():      # independent of the audio branch: side stream
+            iws = self.iws
+            dfi = iws.get("dfeat_img", N * fi.shape[1])
+            ops.linear_bwd(dcat, fi, st["student.image_encoder.1.weight"],
+                           st.grad_of("student.image_encoder.1.weight"),
+                           st.grad_of("student.image_encoder.1.bias"), dfi, N, dout_ld=2 * E,
+                           mode=self.gm)
+            self.img.backward(iws, st, cimg, dfi)
+
+        _, i_done = self._on_side(image_branch)
         dfa = ws.get("dfeat_aud", N * fa.shape[1])
         ops.linear_bwd(dcat, fa, st["student.audio_encoder.1.weight"],
                        st.grad_of("student.audio_encoder.1.weight"),
                        st.grad_of("student.audio_encoder.1.bias"), dfa, N, dout_ld=2 * E, dout_off=E,
                        mode=self.gm)
         self.aud.backward(ws, st, caud, dfa)
+        self._join(i_done)
 
     def step(self, batch):
         """One full training step; returns the loss as a device tensor (no host sync)."""

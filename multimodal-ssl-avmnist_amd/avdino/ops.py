@@ -209,12 +209,14 @@ _GEMM_WS = {}
 
 
 def _gemm_workspace(device, n):
-    """Split-K partial-tile scratch, one per device, grown on demand (stream-ordered reuse:
-    every GEMM on the stream finishes its reduce before the next one writes)."""
-    t = _GEMM_WS.get(device)
+    """Split-K partial-tile scratch, one per (device, stream), grown on demand (stream-ordered
+    reuse: every GEMM on a stream finishes its reduce before the next one writes; engines that
+    run branches on side streams get their own)."""
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    t = _GEMM_WS.get(key)
     if t is None or t.numel() < n:
         t = torch.empty(max(n, 1 << 20), device=device, dtype=torch.float32)
-        _GEMM_WS[device] = t
+        _GEMM_WS[key] = t
     return t
 
 

@@ -379,6 +379,10 @@ __global__ void weight_layout_cl_kernel(const float* __restrict__ w, T* __restri
 
 // ----------------------------------------------------------------------------- host plan
 struct Plan { int TH, TW, NS, GPW, NB, tilesX, tiles; };
+// widest output-channel block that may use 7 pixel groups per wave (AGPR budget / occupancy)
+#ifndef GPW7_MAX_COUT
+#define GPW7_MAX_COUT 32
+#endif
 
 // Tiling of an Ho x Wo output map into blocks of 64*GPW*NB pixels (GPW in {4, 7}; NB batches,
 // only when all input channels fit one LDS chunk).  Whole small maps are packed NS per block
@@ -389,7 +393,7 @@ Plan plan_cl(int Ho, int Wo, int B, int K, int pix_bytes, bool batches, int Cout
   Plan best{0, 0, 0, 0, 0, 0, 0};
   double bsc = -1, bh = 1e9;
   for (int gpw : {4, 7}) {
-    if (gpw == 7 && Cout > 32) continue;   // NT = 4: 7 groups would cost occupancy (AGPRs)
+    if (gpw == 7 && Cout > GPW7_MAX_COUT) continue;   // 7 groups x NT>1 tiles cost occupancy
     for (int nb = 1; nb <= (batches ? 8 : 1); ++nb) {
       const int cap = gpw * 64 * nb;
       if (cap > 2048) continue;
