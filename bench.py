@@ -56,6 +56,9 @@ def parse():
                     help="after warm-up, replay only the dominant launch K times and exit "
                          "(run under rocprofv3 --pmc; tools/pmc_traffic.py turns the last K "
                          "dispatches into the roofline's per-launch HBM traffic)")
+    ap.add_argument("--dominant", default=None, metavar="KEY",
+                    help="use this launch key as the roofline kernel instead of the warm-up's "
+                         "most expensive one (tools/gpu_pmc.sh passes the bench line's key)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"),
                     help="PMC traffic table written by tools/pmc_traffic.py")
     return ap.parse_args()
@@ -202,6 +205,10 @@ def main():
         eng.step(pool[i % len(pool)])
     summ = ops.TIMER.summary() if args.warmup else {}
     dominant = max(summ, key=lambda k: summ[k]["ms"]) if summ else None
+    if args.dominant:
+        if args.dominant not in summ:
+            raise SystemExit(f"--dominant {args.dominant!r}: no such launch key")
+        dominant = args.dominant
     ops.TIMER = ops.KernelTimer(only=dominant)
 
     if args.probe_dominant:

@@ -5,9 +5,13 @@ TAG=$1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 K=20
+# the roofline kernel of this round's bench line (gpu_round.sh writes it), so the counters
+# measure exactly the launch the bench reports
+DOM=$(python -c "import json,sys; print(json.loads(open('gpurun_out/bench_$TAG.json').readline())['roofline']['kernel'])")
+echo "dominant: $DOM"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcF_$TAG -o run -- \
-    python bench.py --steps 1 --warmup 2 --no-cpu-baseline --probe-dominant $K > gpurun_out/probeF_$TAG.json 2> gpurun_out/probeF_$TAG.err \
+    python bench.py --steps 1 --warmup 2 --no-cpu-baseline --probe-dominant $K --dominant "$DOM" > gpurun_out/probeF_$TAG.json 2> gpurun_out/probeF_$TAG.err \
 && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcW_$TAG -o run -- \
-    python bench.py --steps 1 --warmup 2 --no-cpu-baseline --probe-dominant $K > gpurun_out/probeW_$TAG.json 2> gpurun_out/probeW_$TAG.err \
+    python bench.py --steps 1 --warmup 2 --no-cpu-baseline --probe-dominant $K --dominant "$DOM" > gpurun_out/probeW_$TAG.json 2> gpurun_out/probeW_$TAG.err \
 && python tools/pmc_traffic.py gpurun_out/probeF_$TAG.json gpurun_out/pmcF_$TAG gpurun_out/pmcW_$TAG gpurun_out/traffic_$TAG.json
 echo "pmc rc=$?"
