@@ -444,7 +444,15 @@ int avd_c1p8_fwd(const void* x, const void* wk, const float* bias, void* y, floa
                  int H, int W, hipStream_t st);
 
 // BN partial rows per group written by avd_conv_cl_fwd (0 if no tiling fits)
+int avd_ws_stat_rows(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt);
+int avd_ws_conv_fwd(const void* x, const void* wk, const float* bias, void* y, float* stats,
+                    int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
+                    hipStream_t st);
+int avd_ws_conv_dgrad(const void* dy, const void* wk_d, void* dx, int dt, int N, int Cin, int H,
+                      int W, int Cout, int K, int pad, hipStream_t st);
+
 int avd_cl_stat_rows_impl(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt) {
+  if (const int r = avd_ws_stat_rows(Ho, Wo, B, K, Cin, Cout, dt)) return r;
   if (avd_c1p8_eligible(dt, Cin, Cout, K, Ho, Wo)) return avd_c1p8_stat_rows(Ho, B);
   const Plan p = plan_cl(Ho, Wo, B, K, pix_bytes(dt, Cin), Cin == 1, Cout);
   return p.NS ? (B / p.NS) * p.tiles * 4 : 0;   // one partial row per wave
@@ -538,6 +546,9 @@ int avd_cl_conv_fwd_impl(const void* x, const void* wk, const float* bias, void*
     if (pad != 2) return AVD_ERR_SHAPE;
     return avd_c1p8_fwd(x, wk, bias, y, stats, N, H, W, st);
   }
+  // the mid-layer shapes: weights-stationary persistent kernel (conv_ws.hip)
+  if (const int r = avd_ws_conv_fwd(x, wk, bias, y, stats, dt, N, B, Cin, H, W, Cout, K, pad, st))
+    return r > 0 ? AVD_OK : r;
   // batches only for Cin = 1 (its weights live in registers; the Cin >= 8 kernel would re-read
   // its weight fragments per batch)
   const Plan p = plan_cl(Ho, Wo, B, K, pix_bytes(dt, Cin), Cin == 1, Cout);
@@ -553,6 +564,8 @@ int avd_cl_conv_dgrad_impl(const void* dy, const void* wk_d, void* dx, int dt, i
                            int H, int W, int Cout, int K, int pad, hipStream_t st) {
   const int Ho = H + 2 * pad - K + 1, Wo = W + 2 * pad - K + 1;
   if (Ho <= 0 || Wo <= 0 || Cout % 8 || Cin % 4 || K - 1 - pad < 0) return AVD_ERR_SHAPE;
+  if (const int r = avd_ws_conv_dgrad(dy, wk_d, dx, dt, N, Cin, H, W, Cout, K, pad, st))
+    return r > 0 ? AVD_OK : r;
   const Plan p = plan_cl(H, W, N, K, pix_bytes(dt, Cout), false, Cin);
   if (!p.NS) return AVD_ERR_SHAPE;
   if (dt == AVD_BF16)

@@ -1,0 +1,435 @@
+// Weights-stationary, persistent NHWC convolution (bf16, v_mfma_f32_16x16x32_bf16) for the
+// fixed mid-layer shapes of the CentralNet encoders (unimodal.py:105-221): audio conv2-4
+// (56x56 8->16, 28x28 16->32, 14x14 32->64, 5x5 p2) and the image conv2 (14x14 32->64, 5x5 p0),
+// forward (bias + BatchNorm partials in the epilogue) and input gradient (flipped weights).
+//
+// Why a second conv kernel: the generic conv_cl_kernel re-reads its weight fragments from L2
+// on every k-step in every wave and stages each tile synchronously, so it spends most cycles
+// waiting (SQ_WAIT_ANY 56-75 %).  Here
+//   * every wave loads its slice of the weights ONCE into registers (A fragments, up to 200
+//     VGPRs) and keeps them for the whole launch;
+//   * a persistent block walks a contiguous range of tiles (neighbouring row strips of one
+//     sample stay on one XCD, so their halo rows hit L2);
+//   * the next tile's input is loaded into registers while the MFMAs run on the current one
+//     (one LDS buffer: barrier, write, barrier, issue next loads, compute).
+// GEMM view per tile: M = output channels (A = weights [co][tap*CIN + c]), N = 16-pixel groups,
+// K = (tap, channel); the B fragment (8 channels of one pixel and tap) is one ds_read_b128 of
+// the channels-last LDS tile.  The K order and per-k-step accumulation order are those of
+// conv_cl_kernel, so for CIN <= 32 both kernels return bit-identical maps.
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
+
+#include "common.h"
+
+using namespace avd;
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f4;
+typedef __attribute__((ext_vector_type(4))) unsigned u4;
+
+__device__ const u4 kZero16 = {0u, 0u, 0u, 0u};
+
+constexpr int cdv(int a, int b) { return (a + b - 1) / b; }
+
+// One layer shape.  Tiles are TH full-width output rows of NS samples.  The 4 waves of a block
+// split NCW ways over output channels, NKW ways over K (halves of the (tap, channel) range,
+// summed through LDS in fixed order) and NPW = 4 / (NCW NKW) ways over the tile's pixel
+// groups; a wave processes GB groups at a time (GB x NTW independent accumulator chains).
+template <int CIN_, int COUT_, int K_, int PAD_, int H_, int W_, int TH_, int NS_, int NCW_,
+          int NKW_, int GB_, int OCC_, int PF_ = 2>
+struct Ws {
+  static constexpr int OCC = OCC_;                         // target waves per SIMD
+  static constexpr int PF = PF_;                           // k-steps of B reads in flight
+  static constexpr int CIN = CIN_, COUT = COUT_, K = K_, PAD = PAD_, H = H_, W = W_;
+  static constexpr int HO = H + 2 * PAD - K + 1, WO = W + 2 * PAD - K + 1;
+  static constexpr int TH = TH_, TW = WO, NS = NS_;
+  static constexpr int ITH = TH + K - 1, ITW = TW + K - 1;
+  static constexpr int TPS = HO / TH;                      // tiles per sample group
+  static constexpr int VPP = CIN / 8;                      // 16-byte vectors per pixel
+  // LDS image [NS][ITH][RS][PS]: the pixel stride (PS elements) and the row pad (RS - ITW
+  // pixels) make the B-fragment ds_read_b128 conflict-free across its four 16-lane groups for
+  // every tap (found by simulating the gfx950 lane groups over all k-steps: ~4.2 LDS cycles per
+  // read instead of 8-11.5 with the odd-16-byte strides)
+  static constexpr int PS = VPP <= 2 ? CIN : CIN + 16;
+  static constexpr int RS = ITW + (VPP == 1 ? 8 : 4);
+  static constexpr int KK = K * K, KPAD = cdv(KK * CIN, 32) * 32, KS = KPAD / 32;
+  static constexpr int NT = COUT <= 16 ? 1 : COUT / 16;
+  static constexpr int NCW = NCW_, NKW = NKW_, NTW = NT / NCW, NPW = 4 / (NCW * NKW);
+  static constexpr int KSH = cdv(KS, NKW);                 // k-steps per wave
+  static constexpr int PIX = NS * TH * TW, G = cdv(PIX, 16), GW = cdv(G, NPW);
+  static constexpr int GB = GB_;
+  static constexpr int TASKS = NS * ITH * ITW * VPP, SLOTS = cdv(TASKS, 256);
+  static constexpr int LDS_ELEMS = NS * ITH * RS * PS;
+  static constexpr int RED = NKW > 1 ? 2 * NCW * GB * NTW * 64 : 1;   // f4 partial-sum slots
+  static_assert(HO % TH == 0, "strips must tile the map");
+  static_assert(NT % NCW == 0 && 4 % (NCW * NKW) == 0, "wave split");
+  static_assert(NKW == 1 || CIN >= 32, "K split only where tap offsets are compile-time");
+  static_assert(LDS_ELEMS * 2 + RED * 16 <= 96 * 1024, "LDS");
+};
+
+template <int V> using IC = std::integral_constant<int, V>;
+
+__device__ __forceinline__ f4 mma(bf16x8 a, bf16x8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Element offset, inside a pixel tile, of the B fragment of k-step ks for lane group g:
+// tap (kh, kw) and channel chunk.  Padded k-groups (tap >= K*K) read tap 0 (weights are 0).
+template <class L>
+__device__ __forceinline__ int koff(int ks, int g) {
+  const unsigned k0 = (unsigned)(4 * ks + g) * 8u;
+  unsigned tap = k0 / (unsigned)L::CIN, c = k0 % (unsigned)L::CIN;
+  if (tap >= (unsigned)L::KK) { tap = 0; c = 0; }
+  return (int)(((tap / L::K) * L::RS + tap % L::K) * L::PS + c);
+}
+
+template <class L, bool FWD>
+__global__ __launch_bounds__(256, L::OCC) void conv_ws_kernel(const bf16* __restrict__ x,
+                                                      const bf16* __restrict__ wk,
+                                                      const float* __restrict__ bias,
+                                                      bf16* __restrict__ y,
+                                                      float* __restrict__ stats, int ntiles,
+                                                      int nrows) {
+  __shared__ __attribute__((aligned(16))) bf16 xs[L::LDS_ELEMS];
+  __shared__ f4 red[L::RED];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int wc = wave % L::NCW, kw = (wave / L::NCW) % L::NKW, wp = wave / (L::NCW * L::NKW);
+  const int cob = wc * L::NTW * 16;
+
+  // ---- this wave's weight slice (k-steps kw*KSH ...), resident for the whole launch
+  bf16x8 a[L::KSH][L::NTW];
+  auto load_w = [&](auto kwc) {
+    constexpr int KW = decltype(kwc)::value;
+#pragma unroll
+    for (int j = 0; j < L::KSH; ++j)
+#pragma unroll
+      for (int t = 0; t < L::NTW; ++t) {
+        constexpr bf16x8 z = {};
+        a[j][t] = KW * L::KSH + j < L::KS
+                      ? *reinterpret_cast<const bf16x8*>(wk + (size_t)(cob + 16 * t + r16) * L::KPAD +
+                                                         32 * (KW * L::KSH + j) + 8 * g)
+                      : z;
+      }
+  };
+  if constexpr (L::NKW == 1) load_w(IC<0>{});
+  else if (kw == 0) load_w(IC<0>{});
+  else load_w(IC<1>{});
+  // per-lane tap offsets: for CIN >= 32 the lane part is just its channel chunk (8 g) and the
+  // k-step part folds into the LDS read's immediate offset
+  int toff[L::CIN >= 32 ? 1 : L::KS];
+  if constexpr (L::CIN < 32) {
+#pragma unroll
+    for (int ks = 0; ks < L::KS; ++ks) toff[ks] = koff<L>(ks, g);
+  } else {
+    toff[0] = 8 * g;
+  }
+  float bv[L::NTW][4];
+#pragma unroll
+  for (int t = 0; t < L::NTW; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = cob + 16 * t + 4 * g + i;
+      bv[t][i] = (FWD && bias && co < L::COUT) ? bias[co] : 0.f;
+    }
+
+  // ---- contiguous tile range of this block
+  const int per = ntiles / (int)gridDim.x, extra = ntiles % (int)gridDim.x;
+  const int t0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
+  const int t1 = t0 + per + ((int)blockIdx.x < extra ? 1 : 0);
+
+  u4 pre[L::SLOTS];
+  auto load_tile = [&](int ti) {
+    const int sg = ti / L::TPS, tt = ti - sg * L::TPS;
+    const int n0 = sg * L::NS, ty0 = tt * L::TH;
+#pragma unroll
+    for (int i = 0; i < L::SLOTS; ++i) {
+      const int task = tid + 256 * i;
+      const int q = task % L::VPP, pix = task / L::VPP;
+      const int c = pix % L::ITW, rs = pix / L::ITW;
+      const int r = rs % L::ITH, s = rs / L::ITH;
+      const int iy = ty0 - L::PAD + r, ix = c - L::PAD;
+      const bool ok = task < L::TASKS && iy >= 0 && iy < L::H && ix >= 0 && ix < L::W;
+      // halo / padding lanes load from a zero vector: no select on the loaded value, so
+      // nothing waits for these loads before the next tile's LDS write
+      const u4* src = ok ? reinterpret_cast<const u4*>(
+                               x + (((size_t)(n0 + s) * L::H + iy) * L::W + ix) * L::CIN + 8 * q)
+                         : &kZero16;
+      pre[i] = *src;
+    }
+  };
+
+  if (t0 < t1) load_tile(t0);
+  for (int ti = t0; ti < t1; ++ti) {
+    __syncthreads();   // every wave is done reading the previous tile
+#pragma unroll
+    for (int i = 0; i < L::SLOTS; ++i) {
+      const int task = tid + 256 * i;
+      if (task < L::TASKS) {
+        const int q = task % L::VPP, pix = task / L::VPP;
+        const int rs = pix / L::ITW, c = pix - rs * L::ITW;
+        *reinterpret_cast<u4*>(xs + (rs * L::RS + c) * L::PS + 8 * q) = pre[i];
+      }
+    }
+    __syncthreads();
+    if (ti + 1 < t1) load_tile(ti + 1);   // in flight under this tile's MFMAs
+
+    const int sg = ti / L::TPS, tt = ti - sg * L::TPS;
+    const int n0 = sg * L::NS, ty0 = tt * L::TH;
+    float ss[L::NTW][4], sq[L::NTW][4];
+#pragma unroll
+    for (int t = 0; t < L::NTW; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { ss[t][i] = 0.f; sq[t][i] = 0.f; }
+
+    for (int i0 = 0; i0 < L::GW; i0 += L::GB) {
+      int base[L::GB], opix[L::GB];
+      bool gv[L::GB];
+#pragma unroll
+      for (int b = 0; b < L::GB; ++b) {
+        const int p = (wp + L::NPW * (i0 + b)) * 16 + r16;
+        gv[b] = i0 + b < L::GW && p < L::PIX;
+        const int s = p / (L::TH * L::TW), rem = p - s * (L::TH * L::TW);
+        const int ry = rem / L::TW, rx = rem - ry * L::TW;
+        base[b] = gv[b] ? ((s * L::ITH + ry) * L::RS + rx) * L::PS : 0;
+        opix[b] = ((n0 + s) * L::HO + ty0 + ry) * L::WO + rx;
+      }
+      f4 acc[L::GB][L::NTW];
+#pragma unroll
+      for (int b = 0; b < L::GB; ++b)
+#pragma unroll
+        for (int t = 0; t < L::NTW; ++t) acc[b][t] = f4{0.f, 0.f, 0.f, 0.f};
+      // k-loop: B fragments PF k-steps ahead of their MFMAs
+      auto kloop = [&](auto kwc) {
+        constexpr int KW = decltype(kwc)::value;
+        constexpr int PF = L::PF;
+        bf16x8 bq[PF + 1][L::GB];
+        auto ld = [&](bf16x8 (&dst)[L::GB], int j) {
+#pragma unroll
+          for (int b = 0; b < L::GB; ++b) {
+            const int o = L::CIN >= 32 ? base[b] + toff[0] + koff<L>(KW * L::KSH + j, 0)
+                                       : base[b] + toff[L::CIN >= 32 ? 0 : j];
+            dst[b] = *reinterpret_cast<const bf16x8*>(xs + o);
+          }
+        };
+#pragma unroll
+        for (int j = 0; j < PF && j < L::KSH; ++j) ld(bq[j], j);
+#pragma unroll
+        for (int j = 0; j < L::KSH; ++j) {
+          if (j + PF < L::KSH) ld(bq[(j + PF) % (PF + 1)], j + PF);
+#pragma unroll
+          for (int b = 0; b < L::GB; ++b)
+#pragma unroll
+            for (int t = 0; t < L::NTW; ++t)
+              acc[b][t] = mma(a[j][t], bq[j % (PF + 1)][b], acc[b][t]);
+        }
+      };
+      if constexpr (L::NKW == 1) {
+        kloop(IC<0>{});
+      } else {
+        if (kw == 0) kloop(IC<0>{});
+        else kloop(IC<1>{});
+        // second K half -> first, through a double-buffered LDS slot (one barrier per batch)
+        f4* r = red + (((i0 / L::GB) & 1) * L::NCW + wc) * L::GB * L::NTW * 64;
+        if (kw == 1) {
+#pragma unroll
+          for (int b = 0; b < L::GB; ++b)
+#pragma unroll
+            for (int t = 0; t < L::NTW; ++t) r[(b * L::NTW + t) * 64 + lane] = acc[b][t];
+        }
+        __syncthreads();
+        if (kw == 0) {
+#pragma unroll
+          for (int b = 0; b < L::GB; ++b)
+#pragma unroll
+            for (int t = 0; t < L::NTW; ++t) acc[b][t] += r[(b * L::NTW + t) * 64 + lane];
+        }
+      }
+      if (kw != 0) continue;
+      // ---- epilogue: (bias,) bf16 rounding, NHWC store of 4 channels per lane, BN partials
+#pragma unroll
+      for (int b = 0; b < L::GB; ++b) {
+        if (!gv[b]) continue;
+#pragma unroll
+        for (int t = 0; t < L::NTW; ++t) {
+          const int co = cob + 16 * t + 4 * g;
+          if (co >= L::COUT) continue;
+          uint32_t lo, hi;
+          if constexpr (FWD) {
+            lo = pack_bf16x2(acc[b][t][0] + bv[t][0], acc[b][t][1] + bv[t][1]);
+            hi = pack_bf16x2(acc[b][t][2] + bv[t][2], acc[b][t][3] + bv[t][3]);
+            const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                                __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              ss[t][i] += v[i];
+              sq[t][i] = fmaf(v[i], v[i], sq[t][i]);
+            }
+          } else {
+            lo = pack_bf16x2(acc[b][t][0], acc[b][t][1]);
+            hi = pack_bf16x2(acc[b][t][2], acc[b][t][3]);
+          }
+          *reinterpret_cast<uint2*>(y + (size_t)opix[b] * L::COUT + co) = make_uint2(lo, hi);
+        }
+      }
+    }
+    if constexpr (FWD) {
+      if (stats && kw == 0) {   // partial row ti * NPW + wp of [COUT][nrows][2]
+        const int row = ti * L::NPW + wp;
+#pragma unroll
+        for (int t = 0; t < L::NTW; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float s1 = ss[t][i], s2 = sq[t][i];
+#pragma unroll
+            for (int m = 1; m < 16; m <<= 1) {
+              s1 += __shfl_xor(s1, m, 64);
+              s2 += __shfl_xor(s2, m, 64);
+            }
+            const int co = cob + 16 * t + 4 * g + i;
+            if (r16 == 0 && co < L::COUT) {
+              stats[((size_t)co * nrows + row) * 2] = s1;
+              stats[((size_t)co * nrows + row) * 2 + 1] = s2;
+            }
+          }
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- layer table
+//        CIN COUT K PAD  H   W  TH NS NCW NKW GB OCC
+#ifndef WS_VARIANT
+#define WS_VARIANT 0
+#endif
+#if WS_VARIANT == 0   // per-layer best of the measured variants (opbench, B=1024 step shapes)
+typedef Ws<8, 16, 5, 2, 56, 56, 14, 1, 1, 1, 2, 2, 4> FwdA2;  // audio conv2        273 us
+typedef Ws<16, 32, 5, 2, 28, 28, 14, 1, 1, 1, 1, 2, 4> FwdA3; // audio conv3        231 us
+typedef Ws<32, 64, 5, 2, 14, 14, 14, 1, 4, 1, 2, 2> FwdA4;    // audio conv4        168 us
+typedef Ws<32, 64, 5, 0, 14, 14, 10, 2, 4, 1, 2, 2> FwdI2;    // image conv2         87 us
+typedef Ws<16, 8, 5, 2, 56, 56, 8, 1, 1, 1, 1, 3> DgrA2;      // audio conv2 dgrad  275 us
+typedef Ws<32, 16, 5, 2, 28, 28, 14, 1, 1, 1, 2, 2> DgrA3;    // audio conv3 dgrad  145 us
+typedef Ws<64, 32, 5, 2, 14, 14, 14, 1, 2, 2, 2, 2> DgrA4;    // audio conv4 dgrad  158 us
+typedef Ws<64, 32, 5, 4, 10, 10, 14, 1, 2, 2, 2, 2> DgrI2;    // image conv2 dgrad  154 us
+#elif WS_VARIANT == 1
+typedef Ws<8, 16, 5, 2, 56, 56, 14, 1, 1, 1, 4, 2> FwdA2;
+typedef Ws<16, 32, 5, 2, 28, 28, 14, 1, 1, 1, 2, 2> FwdA3;
+typedef Ws<32, 64, 5, 2, 14, 14, 14, 1, 2, 2, 2, 2> FwdA4;
+typedef Ws<32, 64, 5, 0, 14, 14, 10, 2, 2, 2, 2, 2> FwdI2;
+typedef Ws<16, 8, 5, 2, 56, 56, 14, 1, 1, 1, 2, 2> DgrA2;
+typedef Ws<32, 16, 5, 2, 28, 28, 14, 1, 1, 1, 4, 2> DgrA3;
+typedef Ws<64, 32, 5, 2, 14, 14, 14, 1, 2, 2, 2, 2> DgrA4;
+typedef Ws<64, 32, 5, 4, 10, 10, 14, 1, 2, 2, 2, 2> DgrI2;
+#elif WS_VARIANT == 2
+typedef Ws<8, 16, 5, 2, 56, 56, 8, 1, 1, 1, 1, 3> FwdA2;
+typedef Ws<16, 32, 5, 2, 28, 28, 7, 1, 1, 1, 1, 3> FwdA3;
+typedef Ws<32, 64, 5, 2, 14, 14, 14, 1, 4, 1, 2, 2> FwdA4;
+typedef Ws<32, 64, 5, 0, 14, 14, 10, 2, 4, 1, 2, 2> FwdI2;
+typedef Ws<16, 8, 5, 2, 56, 56, 8, 1, 1, 1, 1, 3> DgrA2;
+typedef Ws<32, 16, 5, 2, 28, 28, 7, 1, 1, 1, 1, 3> DgrA3;
+typedef Ws<64, 32, 5, 2, 14, 14, 14, 1, 2, 2, 1, 3> DgrA4;
+typedef Ws<64, 32, 5, 4, 10, 10, 14, 1, 2, 2, 1, 3> DgrI2;
+#else
+typedef Ws<8, 16, 5, 2, 56, 56, 14, 1, 1, 1, 2, 2, 4> FwdA2;
+typedef Ws<16, 32, 5, 2, 28, 28, 14, 1, 1, 1, 1, 2, 4> FwdA3;
+typedef Ws<32, 64, 5, 2, 14, 14, 14, 1, 2, 2, 1, 2, 4> FwdA4;
+typedef Ws<32, 64, 5, 0, 14, 14, 10, 2, 2, 2, 1, 2, 4> FwdI2;
+typedef Ws<16, 8, 5, 2, 56, 56, 8, 1, 1, 1, 2, 3, 4> DgrA2;
+typedef Ws<32, 16, 5, 2, 28, 28, 14, 1, 1, 1, 2, 2, 4> DgrA3;
+typedef Ws<64, 32, 5, 2, 14, 14, 14, 1, 2, 2, 1, 2, 4> DgrA4;
+typedef Ws<64, 32, 5, 4, 10, 10, 14, 1, 2, 2, 1, 2, 4> DgrI2;
+#endif
+
+bool ws_disabled() {
+  const char* e = getenv("AVDINO_CONV_LEGACY");
+  return e && e[0] == '1';
+}
+
+int num_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+template <class L, bool FWD>
+int launch_ws(const void* x, const void* wk, const float* bias, void* y, float* stats, int N,
+              int B, hipStream_t st) {
+  if (N % L::NS || (FWD && stats && B % L::NS)) return AVD_ERR_SHAPE;
+  static int occ = 0;
+  if (!occ) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv_ws_kernel<L, FWD>, 256, 0) !=
+            hipSuccess || occ <= 0)
+      occ = 1;
+  }
+  const int ntiles = (N / L::NS) * L::TPS;
+  const int grid = std::min(ntiles, num_cus() * occ);
+  conv_ws_kernel<L, FWD><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, (bf16*)y,
+                                               stats, ntiles, ntiles * L::NPW);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+template <class L>
+bool is(int Cin, int H, int W, int Cout, int K, int pad) {
+  return Cin == L::CIN && Cout == L::COUT && K == L::K && pad == L::PAD && H == L::H && W == L::W;
+}
+
+template <class L>
+bool out_is(int Cin, int Ho, int Wo, int Cout, int K) {
+  return Cin == L::CIN && Cout == L::COUT && K == L::K && Ho == L::HO && Wo == L::WO;
+}
+
+}  // namespace
+
+// Rows of BN partials per group written by the weights-stationary forward, 0 if it does not
+// serve the shape (bf16 only).
+int avd_ws_stat_rows(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt) {
+  if (dt != AVD_BF16 || ws_disabled()) return 0;
+  auto rows = [&](auto l) -> int {
+    typedef decltype(l) L;
+    return B % L::NS ? 0 : (B / L::NS) * L::TPS * L::NPW;
+  };
+  if (out_is<FwdA2>(Cin, Ho, Wo, Cout, K)) return rows(FwdA2{});
+  if (out_is<FwdA3>(Cin, Ho, Wo, Cout, K)) return rows(FwdA3{});
+  if (out_is<FwdA4>(Cin, Ho, Wo, Cout, K)) return rows(FwdA4{});
+  if (out_is<FwdI2>(Cin, Ho, Wo, Cout, K)) return rows(FwdI2{});
+  return 0;
+}
+
+// 1 = launched, 0 = shape not served (caller falls back), < 0 = error
+int avd_ws_conv_fwd(const void* x, const void* wk, const float* bias, void* y, float* stats,
+                    int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
+                    hipStream_t st) {
+  if (dt != AVD_BF16 || ws_disabled()) return 0;
+  int r = 0;
+  if (is<FwdA2>(Cin, H, W, Cout, K, pad)) r = launch_ws<FwdA2, true>(x, wk, bias, y, stats, N, B, st);
+  else if (is<FwdA3>(Cin, H, W, Cout, K, pad)) r = launch_ws<FwdA3, true>(x, wk, bias, y, stats, N, B, st);
+  else if (is<FwdA4>(Cin, H, W, Cout, K, pad)) r = launch_ws<FwdA4, true>(x, wk, bias, y, stats, N, B, st);
+  else if (is<FwdI2>(Cin, H, W, Cout, K, pad)) r = launch_ws<FwdI2, true>(x, wk, bias, y, stats, N, B, st);
+  else return 0;
+  return r == AVD_OK ? 1 : (r == AVD_ERR_SHAPE ? 0 : r);
+}
+
+// dgrad of a forward conv (Cin -> Cout over H x W, pad): the kernel runs on dY (Cout channels,
+// Ho x Wo) with the flipped weights and padding K-1-pad, producing dX (Cin channels, H x W).
+int avd_ws_conv_dgrad(const void* dy, const void* wk_d, void* dx, int dt, int N, int Cin, int H,
+                      int W, int Cout, int K, int pad, hipStream_t st) {
+  if (dt != AVD_BF16 || ws_disabled()) return 0;
+  const int Ho = H + 2 * pad - K + 1, Wo = W + 2 * pad - K + 1, dp = K - 1 - pad;
+  int r = 0;
+  if (is<DgrA2>(Cout, Ho, Wo, Cin, K, dp)) r = launch_ws<DgrA2, false>(dy, wk_d, nullptr, dx, nullptr, N, N, st);
+  else if (is<DgrA3>(Cout, Ho, Wo, Cin, K, dp)) r = launch_ws<DgrA3, false>(dy, wk_d, nullptr, dx, nullptr, N, N, st);
+  else if (is<DgrA4>(Cout, Ho, Wo, Cin, K, dp)) r = launch_ws<DgrA4, false>(dy, wk_d, nullptr, dx, nullptr, N, N, st);
+  else if (is<DgrI2>(Cout, Ho, Wo, Cin, K, dp)) r = launch_ws<DgrI2, false>(dy, wk_d, nullptr, dx, nullptr, N, N, st);
+  else return 0;
+  return r == AVD_OK ? 1 : (r == AVD_ERR_SHAPE ? 0 : r);
+}

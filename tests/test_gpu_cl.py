@@ -304,3 +304,78 @@ def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN):
     ops.sum_rows(f0, ns, C * K * K, d0)
     ops.sum_rows(f1, nw, C * K * K, d1)
     assert rel(host(d1), host(d0)) < 1e-6
+
+
+# The bench's mid-layer convs are served by the weights-stationary kernel (conv_ws.hip) in bf16;
+# AVDINO_CONV_LEGACY=1 routes them to conv_cl_kernel.  The 56x56 and 28x28 layers keep the
+# legacy K order and accumulation order: bit-identical maps.  The 14x14 layers split K over two
+# waves (summed in fixed order), so there the two differ by bf16 rounding only; both paths are
+# also checked against float64.
+WS_SHAPES = [  # N, B, Cin, H, Cout, K, pad
+    (48, 24, 8, 56, 16, 5, 2), (48, 24, 16, 28, 32, 5, 2), (48, 24, 32, 14, 64, 5, 2),
+    (48, 24, 32, 14, 64, 5, 0)]
+
+
+def _both_paths(monkeypatch, fn):
+    monkeypatch.setenv("AVDINO_CONV_LEGACY", "0")
+    a = fn()
+    monkeypatch.setenv("AVDINO_CONV_LEGACY", "1")
+    b = fn()
+    monkeypatch.delenv("AVDINO_CONV_LEGACY")
+    return a, b
+
+
+@pytest.mark.parametrize("shape", WS_SHAPES)
+def test_ws_conv_fwd_matches_legacy(ops, shape, monkeypatch):
+    N, B, Cin, H, Cout, K, pad = shape
+    G = N // B
+    x, w, b = _inputs((N, Cin, H, Cout, K, pad), "bf16", 11)
+    Ho = H + 2 * pad - K + 1
+    T = torch.bfloat16
+    wk = torch.empty(ops.cl_weight_elems(Cout, Cin, K, 0), device="cuda", dtype=T)
+    ops.cl_weight_layout(dev(w), wk, 0)
+    xd, bd = dev(nhwc(x), T), dev(b)
+
+    def run():
+        y = torch.empty(N, Ho, Ho, Cout, device="cuda", dtype=T)
+        R = ops.cl_stat_rows(Ho, Ho, B, K, Cin, Cout, T)
+        st = torch.full((Cout * G * R * 2,), float("nan"), device="cuda")
+        ops.cl_conv_fwd(xd, wk, bd, y, st, N, B, Cin, H, H, Cout, K, pad)
+        torch.cuda.synchronize()
+        return host(y), host(st).reshape(Cout, G, R, 2).sum(2)
+
+    (y1, s1), (y0, s0) = _both_paths(monkeypatch, run)
+    if H > 14:
+        assert np.array_equal(y1, y0)
+        assert rel(s1, s0) < 1e-6
+    else:   # statistics of two differently rounded maps
+        assert rel(y1, y0) < 4e-3
+        assert rel(s1, s0) < 1e-3
+    y_ref, _ = O.conv2d_fwd(x.astype(np.float64), w.astype(np.float64), b.astype(np.float64), pad)
+    assert rel(nchw(y1), y_ref) < TOL["bf16"]
+
+
+@pytest.mark.parametrize("shape", WS_SHAPES)
+def test_ws_conv_dgrad_matches_legacy(ops, shape, monkeypatch):
+    N, _, Cin, H, Cout, K, pad = shape
+    x, w, _ = _inputs((N, Cin, H, Cout, K, pad), "bf16", 12)
+    y_ref, win = O.conv2d_fwd(x.astype(np.float64), w.astype(np.float64), np.zeros(Cout), pad)
+    dy = bf(np.random.default_rng(13).uniform(-1, 1, y_ref.shape))
+    T = torch.bfloat16
+    wd = torch.empty(ops.cl_weight_elems(Cout, Cin, K, 1), device="cuda", dtype=T)
+    ops.cl_weight_layout(dev(w), wd, 1)
+    dyd = dev(nhwc(dy), T)
+
+    def run():
+        dx = torch.empty(N, H, H, Cin, device="cuda", dtype=T)
+        ops.cl_conv_dgrad(dyd, wd, dx, N, Cin, H, H, Cout, K, pad)
+        torch.cuda.synchronize()
+        return host(dx)
+
+    d1, d0 = _both_paths(monkeypatch, run)
+    if H > 14:
+        assert np.array_equal(d1, d0)
+    else:
+        assert rel(d1, d0) < 4e-3
+    dx_ref, _, _ = O.conv2d_bwd(dy.astype(np.float64), win, w.astype(np.float64), x.shape, pad)
+    assert rel(nchw(d1), dx_ref) < TOL["bf16"]
