@@ -141,23 +141,33 @@ __global__ __launch_bounds__(256, L::OCC) void conv_ws_kernel(const bf16* __rest
   const int t0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
   const int t1 = t0 + per + ((int)blockIdx.x < extra ? 1 : 0);
 
+  // staging slots: tile-invariant parts of each 16-byte task (source offset relative to the
+  // tile's first sample and first input row incl. halo, LDS offset, halo row)
+  int goff[L::SLOTS], loff[L::SLOTS], srow[L::SLOTS];
+#pragma unroll
+  for (int i = 0; i < L::SLOTS; ++i) {
+    const int task = tid + 256 * i;
+    const int q = task % L::VPP, pix = task / L::VPP;
+    const int c = pix % L::ITW, rs = pix / L::ITW;
+    const int r = rs % L::ITH, s = rs / L::ITH;
+    const int ix = c - L::PAD;
+    srow[i] = r;
+    loff[i] = (rs * L::RS + c) * L::PS + 8 * q;
+    goff[i] = (task < L::TASKS && ix >= 0 && ix < L::W)
+                  ? ((s * L::H + r) * L::W + ix) * L::CIN + 8 * q : -1;
+  }
   u4 pre[L::SLOTS];
   auto load_tile = [&](int ti) {
     const int sg = ti / L::TPS, tt = ti - sg * L::TPS;
     const int n0 = sg * L::NS, ty0 = tt * L::TH;
+    // row ty0 - PAD of sample n0 (only dereferenced for in-range rows)
+    const bf16* bx = x + ((long long)n0 * L::H + ty0 - L::PAD) * L::W * L::CIN;
 #pragma unroll
     for (int i = 0; i < L::SLOTS; ++i) {
-      const int task = tid + 256 * i;
-      const int q = task % L::VPP, pix = task / L::VPP;
-      const int c = pix % L::ITW, rs = pix / L::ITW;
-      const int r = rs % L::ITH, s = rs / L::ITH;
-      const int iy = ty0 - L::PAD + r, ix = c - L::PAD;
-      const bool ok = task < L::TASKS && iy >= 0 && iy < L::H && ix >= 0 && ix < L::W;
       // halo / padding lanes load from a zero vector: no select on the loaded value, so
       // nothing waits for these loads before the next tile's LDS write
-      const u4* src = ok ? reinterpret_cast<const u4*>(
-                               x + (((size_t)(n0 + s) * L::H + iy) * L::W + ix) * L::CIN + 8 * q)
-                         : &kZero16;
+      const bool ok = goff[i] >= 0 && (unsigned)(ty0 - L::PAD + srow[i]) < (unsigned)L::H;
+      const u4* src = ok ? reinterpret_cast<const u4*>(bx + goff[i]) : &kZero16;
       pre[i] = *src;
     }
   };
@@ -166,14 +176,8 @@ __global__ __launch_bounds__(256, L::OCC) void conv_ws_kernel(const bf16* __rest
   for (int ti = t0; ti < t1; ++ti) {
     __syncthreads();   // every wave is done reading the previous tile
 #pragma unroll
-    for (int i = 0; i < L::SLOTS; ++i) {
-      const int task = tid + 256 * i;
-      if (task < L::TASKS) {
-        const int q = task % L::VPP, pix = task / L::VPP;
-        const int rs = pix / L::ITW, c = pix - rs * L::ITW;
-        *reinterpret_cast<u4*>(xs + (rs * L::RS + c) * L::PS + 8 * q) = pre[i];
-      }
-    }
+    for (int i = 0; i < L::SLOTS; ++i)
+      if (tid + 256 * i < L::TASKS) *reinterpret_cast<u4*>(xs + loff[i]) = pre[i];
     __syncthreads();
     if (ti + 1 < t1) load_tile(ti + 1);   // in flight under this tile's MFMAs
 

@@ -431,7 +431,14 @@ int dispatch_wgrad(const void* x, const void* dy, float* parts, int N, int Cin, 
 
 // Sample chunks (= partial slabs) of avd_cl_conv_wgrad: >= ~4 blocks per CU in flight while
 // keeping the slabs (chunks * Cout*Cin*K*K f32) small next to the activations.
+int avd_wg_chunks(int N, int Cout, int Cin, int K);
+int avd_wg_conv_wgrad(const void* x, const void* dy, int dt, float* parts, int N, int Cin, int H,
+                      int W, int Cout, int K, int pad, hipStream_t st);
+
 int avd_cl_wgrad_chunks_impl(int N, int Cout, int Cin, int K) {
+  // the mid-layer shapes use one slab per persistent block of wgrad_ws.hip (the legacy kernel
+  // takes any slab count, so a fallback launch for another H sizes its slabs the same way)
+  if (const int c = avd_wg_chunks(N, Cout, Cin, K)) return c;
   const long long per = (long long)Cout * Cin * K * K;
   long long c = (1ll << 24) / std::max(per, 1ll);
   c = std::max(128ll, std::min(c, Cin == 1 ? 4096ll : 1024ll));
@@ -442,6 +449,8 @@ int avd_cl_conv_wgrad_impl(const void* x, const void* dy, int dt, float* parts, 
                            int H, int W, int Cout, int K, int pad, hipStream_t st) {
   if (Cin != 1 && Cin % 8) return AVD_ERR_SHAPE;
   if (Cout % 8) return AVD_ERR_SHAPE;
+  if (const int r = avd_wg_conv_wgrad(x, dy, dt, parts, N, Cin, H, W, Cout, K, pad, st))
+    return r > 0 ? AVD_OK : r;
   const int chunks = avd_cl_wgrad_chunks_impl(N, Cout, Cin, K);
   if (dt == AVD_BF16)
     return dispatch_wgrad<bf16>(x, dy, parts, N, Cin, H, W, Cout, K, pad, chunks, st);

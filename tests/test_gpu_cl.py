@@ -379,3 +379,31 @@ def test_ws_conv_dgrad_matches_legacy(ops, shape, monkeypatch):
         assert rel(d1, d0) < 4e-3
     dx_ref, _, _ = O.conv2d_bwd(dy.astype(np.float64), win, w.astype(np.float64), x.shape, pad)
     assert rel(nchw(d1), dx_ref) < TOL["bf16"]
+
+
+@pytest.mark.parametrize("shape", WS_SHAPES)
+def test_ws_conv_wgrad_matches_legacy(ops, shape, monkeypatch):
+    """wgrad_ws.hip (one block = all weight columns of its sample chunk) vs the legacy kernel
+    and float64: exact bf16 products, fp32 sums in another order."""
+    N, _, Cin, H, Cout, K, pad = shape
+    x, _, _ = _inputs((N, Cin, H, Cout, K, pad), "bf16", 14)
+    Ho = H + 2 * pad - K + 1
+    dy = bf(np.random.default_rng(15).uniform(-1, 1, (N, Cout, Ho, Ho)))
+    T = torch.bfloat16
+    xd, dyd = dev(nhwc(x), T), dev(nhwc(dy), T)
+
+    def run():
+        nch = ops.cl_wgrad_chunks(N, Cout, Cin, K)
+        parts = torch.full((nch * Cout * Cin * K * K,), float("nan"), device="cuda")
+        ops.cl_conv_wgrad(xd, dyd, parts, N, Cin, H, H, Cout, K, pad)
+        dw = torch.empty(Cout, Cin, K, K, device="cuda")
+        ops.sum_rows(parts, nch, Cout * Cin * K * K, dw)
+        torch.cuda.synchronize()
+        return host(dw)
+
+    w1, w0 = _both_paths(monkeypatch, run)
+    wz = np.zeros((Cout, Cin, K, K))
+    _, win = O.conv2d_fwd(x.astype(np.float64), wz, np.zeros(Cout), pad)
+    _, dw_ref, _ = O.conv2d_bwd(dy.astype(np.float64), win, wz, x.shape, pad)
+    assert rel(w1, dw_ref) < 1e-5
+    assert rel(w0, dw_ref) < 1e-5

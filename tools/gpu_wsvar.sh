@@ -7,7 +7,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_cl.py -q -m gpu -x --timeou
 rc=$?; echo "tests rc=$rc"; grep -E "^E  |passed|failed|FAILED" gpurun_out/t_$TAG.log | cut -c1-300 | head -20
 [ $rc -eq 0 ] || exit $rc
 for v in "$@"; do
-  AVDINO_LIB=multimodal-ssl-avmnist_amd/avdino/variants/libavdino_$v.so timeout -k 10 300 python tools/opbench.py --filter cl_conv_ > gpurun_out/opbench_${TAG}_$v.txt 2>&1
-  rc=$?; echo "== $v rc=$rc"; grep -v wgrad gpurun_out/opbench_${TAG}_$v.txt | grep -v amdgpu.ids
+  AVDINO_LIB=multimodal-ssl-avmnist_amd/avdino/variants/libavdino_$v.so timeout -k 10 300 python tools/opbench.py --filter ${FILT:-cl_conv_} > gpurun_out/opbench_${TAG}_$v.txt 2>&1
+  rc=$?; echo "== $v rc=$rc"; grep -v "2048x\|x1->" gpurun_out/opbench_${TAG}_$v.txt | grep -v amdgpu.ids
   [ $rc -eq 0 ] || exit $rc
 done
