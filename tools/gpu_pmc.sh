@@ -7,7 +7,8 @@ mkdir -p gpurun_out
 K=20
 # the roofline kernel of this round's bench line (gpu_round.sh writes it), so the counters
 # measure exactly the launch the bench reports
-DOM=$(python -c "import json,sys; print(json.loads(open('gpurun_out/bench_$TAG.json').readline())['roofline']['kernel'])")
+# (or pass it as DOM=... when the bench ran in another call: gpurun_out/ does not travel)
+DOM=${DOM:-$(python -c "import json,sys; print(json.loads(open('gpurun_out/bench_$TAG.json').readline())['roofline']['kernel'])")}
 echo "dominant: $DOM"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmcF_$TAG -o run -- \
     python bench.py --steps 1 --warmup 2 --no-cpu-baseline --probe-dominant $K --dominant "$DOM" > gpurun_out/probeF_$TAG.json 2> gpurun_out/probeF_$TAG.err \
