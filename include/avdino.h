@@ -219,6 +219,26 @@ int avd_cl_bn_bwd_apply_wgrad(const void* y, const void* gout, const float* scal
                               int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
                               void* stream);
 
+/* BatchNorm-backward apply fused into BOTH consumers of dy, for the mid-layer convs (bf16):
+ * the input- and weight-gradient kernels read the conv output y [N,Ho,Wo,Cout] and the pooled
+ * gradient gout (layout gmode: 0 = pooled NHWC in dt, 2 = f32 [N][Cout*Ho/2*Wo/2] in (c,h,w)
+ * flatten order) and form dy = avd_cl_bn_bwd_apply(y, gout, gmode, scale, shift, coef) tile by
+ * tile on chip, so dy is never written or read (replaces avd_cl_bn_bwd_apply +
+ * avd_cl_conv_wgrad + avd_cl_conv_dgrad for CentralUnimodalAudio conv2-4 / bn2-4 and
+ * CentralUnimodalImage conv2 / bn2, unimodal.py:127-221).  B = samples per BN group (N/B <= 8).
+ * avd_cl_bnapply_ok() = 1 when both kernels serve the shape, else use the three unfused calls
+ * (AVD_ERR_SHAPE from either entry point otherwise).  Bit-identical to the unfused calls. */
+int avd_cl_bnapply_ok(int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
+                      int gmode);
+int avd_cl_conv_dgrad_bnapply(const void* y, const void* gout, int gmode, const float* scale,
+                              const float* shift, const float* coef, const void* wk_d, void* dx,
+                              int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
+                              int pad, void* stream);
+int avd_cl_conv_wgrad_bnapply(const void* x, const void* y, const void* gout, int gmode,
+                              const float* scale, const float* shift, const float* coef, int dt,
+                              float* dw_parts, int N, int B, int Cin, int H, int W, int Cout,
+                              int K, int pad, void* stream);
+
 /* The same first layer WITHOUT storing its conv output: every pass recomputes y = conv(x) + b
  * (bf16-rounded, bit-identical across passes) into an on-chip tile from the 8x smaller input.
  *   pass 0 (stats):  out = BN partial rows [Cout][G][R][2] of the rounded y

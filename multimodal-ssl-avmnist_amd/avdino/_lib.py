@@ -41,6 +41,9 @@ PROTOS = {
     "avd_cl_conv_dgrad": [P, P, P, I, I, I, I, I, I, I, I, P],
     "avd_cl_wgrad_chunks": [I, I, I, I],
     "avd_cl_conv_wgrad": [P, P, I, P, I, I, I, I, I, I, I, P],
+    "avd_cl_bnapply_ok": [I, I, I, I, I, I, I, I, I, I],
+    "avd_cl_conv_dgrad_bnapply": [P, P, I, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "avd_cl_conv_wgrad_bnapply": [P, P, P, I, P, P, P, I, P, I, I, I, I, I, I, I, I, P],
     "avd_cl_bn_relu_pool": [P, I, P, P, P, I, I, I, I, I, I, P],
     "avd_cl_bn_bwd_rows": [I, I, I, I, I],
     "avd_cl_bn_bwd_reduce": [P, I, P, I, P, P, P, P, P, I, I, I, I, I, P],

@@ -195,6 +195,12 @@ class ConvBranch:
                             shift=st[3], coef=coef, gz=gout, out=wparts)
         ops.sum_rows(wparts, nsl, co * ci * k * k, store.grad_of(ck + ".weight"))
 
+    # BN-backward apply fused into the dgrad/wgrad staging (avd_cl_conv_*_bnapply, bit-identical
+    # to the unfused chain).  Off by default: measured slower (r1_27: 2.62 ms fused vs 2.17 ms
+    # apply + dgrad + wgrad for the four mid layers) -- the window math in the staging phase costs
+    # registers (occupancy 2 -> 1) and is not hidden behind the MFMAs.  AVDINO_BNAPPLY_FUSED=1.
+    BNAPPLY_FUSED = os.environ.get("AVDINO_BNAPPLY_FUSED", "0") == "1"
+
     def backward(self, ws, store, ctx, dfeat):
         """dfeat: f32 [N, F] gradient of the features; writes conv/BN parameter grads."""
         N, G = ctx["N"], ctx["G"]
@@ -225,10 +231,21 @@ class ConvBranch:
                                           k, pad)
                 ops.sum_rows(wparts, nsl, co * ci * k * k, store.grad_of(ck + ".weight"))
                 continue
-            dy = ws.get("bwd_dy", N * Ho * Ho * co, self.act)
-            ops.cl_bn_bwd_apply(y, gout, mode, st[2], st[3], coef, dy, N, B, co, Ho, Ho)
             nch = ops.cl_wgrad_chunks(N, co, ci, k)
             wparts = ws.get("wgrad_parts", nch * co * ci * k * k)
+            if (self.BNAPPLY_FUSED and i > 0 and mode in (0, 2) and
+                    ops.cl_bnapply_ok(self.act, N, B, ci, H, H, co, k, pad, mode)):
+                # dy = BN-backward apply is formed inside both consumers (no dy tensor)
+                ops.cl_conv_wgrad_bnapply(x, y, gout, mode, st[2], st[3], coef, wparts, N, B, ci, H, H,
+                                          co, k, pad)
+                ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
+                dx = ws.get("bwd_dx", N * H * H * ci, self.act)
+                ops.cl_conv_dgrad_bnapply(y, gout, mode, st[2], st[3], coef, ctx["wts"][i][1], dx, N, B,
+                                          ci, H, H, co, k, pad)
+                gout = dx
+                continue
+            dy = ws.get("bwd_dy", N * Ho * Ho * co, self.act)
+            ops.cl_bn_bwd_apply(y, gout, mode, st[2], st[3], coef, dy, N, B, co, Ho, Ho)
             ops.cl_conv_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
             ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
             if i > 0:

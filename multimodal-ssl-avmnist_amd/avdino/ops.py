@@ -306,6 +306,45 @@ def cl_conv_wgrad(x, dy, parts, N, Cin, H, W, Cout, K, pad):
                         K, pad, stream()))
 
 
+def cl_bnapply_ok(dtype, N, B, Cin, H, W, Cout, K, pad, gmode):
+    """True when the input- and weight-gradient kernels can apply the layer's BatchNorm backward
+    themselves (avd_cl_bnapply_ok): then no dy tensor is needed."""
+    return bool(lib.avd_cl_bnapply_ok(_DT[dtype], N, B, Cin, H, W, Cout, K, pad, gmode))
+
+
+def _gout_check(gout, gmode, y, N, Ho, Wo, Cout):
+    want = N * (Ho // 2) * (Wo // 2) * Cout
+    _need(gout.numel() == want and (gout.dtype == y.dtype if gmode == 0 else gout.dtype == torch.float32),
+          "bnapply gout")
+
+
+def cl_conv_dgrad_bnapply(y, gout, gmode, scale, shift, coef, wk_d, dx, N, B, Cin, H, W, Cout, K, pad):
+    """dx = input gradient of the conv for dy = bn_bwd_apply(y, gout, ...) formed on chip."""
+    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
+    _need(y.numel() == N * Ho * Wo * Cout and dx.numel() == N * H * W * Cin, "bnapply dgrad sizes")
+    _need(y.dtype == dx.dtype == wk_d.dtype, "bnapply dgrad dtypes")
+    _gout_check(gout, gmode, y, N, Ho, Wo, Cout)
+    nb = (y.numel() + dx.numel()) * y.element_size() + gout.numel() * gout.element_size()
+    fl = 2 * N * Cin * H * W * Cout * K * K
+    _timed(f"cl_conv_dgrad_bnapply[{N}x{Ho}x{Wo}x{Cout}->{Cin} k{K}p{pad} g{gmode} {y.dtype}]", nb, fl,
+           lambda: call("avd_cl_conv_dgrad_bnapply", p(y), p(gout), gmode, p(scale), p(shift), p(coef),
+                        p(wk_d), p(dx), dtcode(y), N, B, Cin, H, W, Cout, K, pad, stream()))
+
+
+def cl_conv_wgrad_bnapply(x, y, gout, gmode, scale, shift, coef, parts, N, B, Cin, H, W, Cout, K, pad):
+    """Weight-gradient slabs (as cl_conv_wgrad) for dy = bn_bwd_apply(y, gout, ...) formed on chip."""
+    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
+    _need(x.numel() == N * H * W * Cin and y.numel() == N * Ho * Wo * Cout, "bnapply wgrad sizes")
+    _need(x.dtype == y.dtype, "bnapply wgrad dtypes")
+    _gout_check(gout, gmode, y, N, Ho, Wo, Cout)
+    _need(parts.numel() >= cl_wgrad_chunks(N, Cout, Cin, K) * Cout * Cin * K * K, "bnapply wgrad parts")
+    nb = (x.numel() + y.numel()) * x.element_size() + gout.numel() * gout.element_size()
+    fl = 2 * y.numel() * Cin * K * K
+    _timed(f"cl_conv_wgrad_bnapply[{N}x{H}x{W}x{Cin}->{Cout} k{K}p{pad} g{gmode} {x.dtype}]", nb, fl,
+           lambda: call("avd_cl_conv_wgrad_bnapply", p(x), p(y), p(gout), gmode, p(scale), p(shift),
+                        p(coef), dtcode(x), p(parts), N, B, Cin, H, W, Cout, K, pad, stream()))
+
+
 def cl_bn_relu_pool(y, scale, shift, out, mode, N, B, C, H, W):
     """mode 0: NHWC pooled (y dtype); 1: GAP f32 [N,C]; 2: f32 (c,h,w)-flattened pooled map."""
     _need(y.numel() == N * H * W * C, "cl pool y")

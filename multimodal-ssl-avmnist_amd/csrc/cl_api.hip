@@ -41,6 +41,19 @@ namespace {
 bool dt_ok(int dt) { return dt == AVD_F32 || dt == AVD_BF16; }
 }  // namespace
 
+int avd_ws_dgrad_bnapply_serves(int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
+                                int pad, int gmode);
+int avd_ws_conv_dgrad_bnapply(const void* y, const void* gout, int gmode, const float* scale,
+                              const float* shift, const float* coef, const void* wk_d, void* dx,
+                              int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
+                              hipStream_t st);
+int avd_wg_bnapply_serves(int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
+                          int gmode);
+int avd_wg_conv_wgrad_ex(const void* x, const void* dy, int dt, float* parts, int N, int Cin,
+                         int H, int W, int Cout, int K, int pad, int gmode, const void* gout,
+                         const float* scale, const float* shift, const float* coef, int B,
+                         hipStream_t st);
+
 extern "C" {
 
 int avd_cl_weight_elems(int Cout, int Cin, int K, int dgrad) {
@@ -111,6 +124,33 @@ int avd_cl_conv_dgrad(const void* dy, const void* wk_d, void* dx, int dt, int N,
   if (!dy || !wk_d || !dx || !dt_ok(dt)) return AVD_ERR_ARG;
   if (N <= 0 || (K != 3 && K != 5)) return AVD_ERR_SHAPE;
   return avd_cl_conv_dgrad_impl(dy, wk_d, dx, dt, N, Cin, H, W, Cout, K, pad, avd_stream(stream));
+}
+
+int avd_cl_bnapply_ok(int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
+                      int gmode) {
+  return avd_ws_dgrad_bnapply_serves(dt, N, B, Cin, H, W, Cout, K, pad, gmode) &&
+         avd_wg_bnapply_serves(dt, N, B, Cin, H, W, Cout, K, pad, gmode);
+}
+
+int avd_cl_conv_dgrad_bnapply(const void* y, const void* gout, int gmode, const float* scale,
+                              const float* shift, const float* coef, const void* wk_d, void* dx,
+                              int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
+                              int pad, void* stream) {
+  if (!y || !gout || !scale || !shift || !coef || !wk_d || !dx || !dt_ok(dt)) return AVD_ERR_ARG;
+  const int r = avd_ws_conv_dgrad_bnapply(y, gout, gmode, scale, shift, coef, wk_d, dx, dt, N, B,
+                                          Cin, H, W, Cout, K, pad, avd_stream(stream));
+  return r > 0 ? AVD_OK : (r == 0 ? AVD_ERR_SHAPE : r);
+}
+
+int avd_cl_conv_wgrad_bnapply(const void* x, const void* y, const void* gout, int gmode,
+                              const float* scale, const float* shift, const float* coef, int dt,
+                              float* dw_parts, int N, int B, int Cin, int H, int W, int Cout,
+                              int K, int pad, void* stream) {
+  if (!x || !y || !gout || !scale || !shift || !coef || !dw_parts || !dt_ok(dt)) return AVD_ERR_ARG;
+  if (gmode < 0) return AVD_ERR_ARG;
+  const int r = avd_wg_conv_wgrad_ex(x, y, dt, dw_parts, N, Cin, H, W, Cout, K, pad, gmode, gout,
+                                     scale, shift, coef, B, avd_stream(stream));
+  return r > 0 ? AVD_OK : (r == 0 ? AVD_ERR_SHAPE : r);
 }
 
 int avd_cl_wgrad_chunks(int N, int Cout, int Cin, int K) {

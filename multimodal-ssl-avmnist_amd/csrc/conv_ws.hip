@@ -21,6 +21,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "bnapply.h"
 
 using namespace avd;
 
@@ -86,15 +87,19 @@ __device__ __forceinline__ int koff(int ks, int g) {
   return (int)(((tap / L::K) * L::RS + tap % L::K) * L::PS + c);
 }
 
-template <class L, bool FWD>
-__global__ __launch_bounds__(256, L::OCC) void conv_ws_kernel(const bf16* __restrict__ x,
+// AP (input gradient only): 0 = x is the staged operand itself (dY); 1 / 2 = x is the conv
+// output y of the layer whose gradient this is, and the staging applies that layer's
+// BatchNorm backward (bnapply.h) to produce dY in LDS, with the pooled gradient in layout 0 / 2
+template <class L, bool FWD, int AP = 0>
+__global__ __launch_bounds__(256, AP ? (L::OCC > 1 ? L::OCC - 1 : 1) : L::OCC) void conv_ws_kernel(const bf16* __restrict__ x,
                                                       const bf16* __restrict__ wk,
                                                       const float* __restrict__ bias,
                                                       bf16* __restrict__ y,
                                                       float* __restrict__ stats, int ntiles,
-                                                      int nrows) {
+                                                      int nrows, ApplyArgs aa) {
   __shared__ __attribute__((aligned(16))) bf16 xs[L::LDS_ELEMS];
   __shared__ f4 red[L::RED];
+  __shared__ __attribute__((aligned(16))) float ctab[AP ? APPLY_GMAX * 5 * L::CIN : 4];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int g = lane >> 4, r16 = lane & 15;
   const int wc = wave % L::NCW, kw = (wave / L::NCW) % L::NKW, wp = wave / (L::NCW * L::NKW);
@@ -141,7 +146,7 @@ __global__ __launch_bounds__(256, L::OCC) void conv_ws_kernel(const bf16* __rest
   const int t0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
   const int t1 = t0 + per + ((int)blockIdx.x < extra ? 1 : 0);
 
-  // staging slots: tile-invariant parts of each 16-byte task (source offset relative to the
+  // staging slots (AP = 0): tile-invariant parts of each 16-byte task (source offset relative to the
   // tile's first sample and first input row incl. halo, LDS offset, halo row)
   int goff[L::SLOTS], loff[L::SLOTS], srow[L::SLOTS];
 #pragma unroll
@@ -156,12 +161,13 @@ __global__ __launch_bounds__(256, L::OCC) void conv_ws_kernel(const bf16* __rest
     goff[i] = (task < L::TASKS && ix >= 0 && ix < L::W)
                   ? ((s * L::H + r) * L::W + ix) * L::CIN + 8 * q : -1;
   }
-  u4 pre[L::SLOTS];
+  u4 pre[AP ? 1 : L::SLOTS];
   auto load_tile = [&](int ti) {
     const int sg = ti / L::TPS, tt = ti - sg * L::TPS;
     const int n0 = sg * L::NS, ty0 = tt * L::TH;
     // row ty0 - PAD of sample n0 (only dereferenced for in-range rows)
     const bf16* bx = x + ((long long)n0 * L::H + ty0 - L::PAD) * L::W * L::CIN;
+    if constexpr (AP) return;
 #pragma unroll
     for (int i = 0; i < L::SLOTS; ++i) {
       // halo / padding lanes load from a zero vector: no select on the loaded value, so
@@ -172,14 +178,89 @@ __global__ __launch_bounds__(256, L::OCC) void conv_ws_kernel(const bf16* __rest
     }
   };
 
-  if (t0 < t1) load_tile(t0);
-  for (int ti = t0; ti < t1; ++ti) {
-    __syncthreads();   // every wave is done reading the previous tile
+  // staging slots (AP != 0): one task = one 2x2 pooling window x 8 channels of y (windows
+  // are aligned: PAD and the tile rows are even), its pooled gradient, 4 dY vectors out
+  constexpr int HP = L::H / 2, WP = L::W / 2;
+  constexpr int WT = AP ? L::NS * (L::ITH / 2) * (L::ITW / 2) * L::VPP : 0;
+  constexpr int WSL = AP ? cdv(WT, 256) : 1;
+  int wgo[WSL], wgg[WSL], wlo[WSL], wrow[WSL];
+  WinIn prew[WSL];
+  if constexpr (AP) {
+    static_assert(L::PAD % 2 == 0 && L::TH % 2 == 0 && L::H % 2 == 0 && L::W % 2 == 0, "windows");
+    apply_load_ctab<L::CIN>(ctab, aa, tid, 256);
 #pragma unroll
-    for (int i = 0; i < L::SLOTS; ++i)
-      if (tid + 256 * i < L::TASKS) *reinterpret_cast<u4*>(xs + loff[i]) = pre[i];
+    for (int i = 0; i < WSL; ++i) {
+      const int task = tid + 256 * i;
+      const int q = task % L::VPP, w = task / L::VPP;
+      const int wc2 = w % (L::ITW / 2), t = w / (L::ITW / 2);
+      const int wr = t % (L::ITH / 2), s = t / (L::ITH / 2);
+      const int r = 2 * wr, c = 2 * wc2, ix = c - L::PAD;
+      wrow[i] = r;
+      wlo[i] = ((s * L::ITH + r) * L::RS + c) * L::PS + 8 * q;
+      wgo[i] = (task < WT && ix >= 0 && ix < L::W) ? ((s * L::H + r) * L::W + ix) * L::CIN + 8 * q : -1;
+      wgg[i] = AP == 1 ? ((s * HP + wr) * WP + ix / 2) * L::CIN + 8 * q
+                       : (s * L::CIN + 8 * q) * HP * WP + wr * WP + ix / 2;
+    }
+  }
+  auto load_win_tile = [&](int ti) {
+    const int sg = ti / L::TPS, tt = ti - sg * L::TPS;
+    const int n0 = sg * L::NS, ty0 = tt * L::TH;
+    const bf16* by = x + ((long long)n0 * L::H + ty0 - L::PAD) * L::W * L::CIN;
+    const long long prow = (ty0 - L::PAD) / 2;   // exact: both even
+#pragma unroll
+    for (int i = 0; i < WSL; ++i) {
+      const bool ok = wgo[i] >= 0 && (unsigned)(ty0 - L::PAD + wrow[i]) < (unsigned)L::H;
+      const bf16* p = by + (ok ? wgo[i] : 0);
+      prew[i].y[0] = *(ok ? reinterpret_cast<const u4*>(p) : &kZero16);
+      prew[i].y[1] = *(ok ? reinterpret_cast<const u4*>(p + L::CIN) : &kZero16);
+      prew[i].y[2] = *(ok ? reinterpret_cast<const u4*>(p + L::W * L::CIN) : &kZero16);
+      prew[i].y[3] = *(ok ? reinterpret_cast<const u4*>(p + (L::W + 1) * L::CIN) : &kZero16);
+      if constexpr (AP == 1) {
+        const bf16* gb = reinterpret_cast<const bf16*>(aa.gout) + ((long long)n0 * HP + prow) * WP * L::CIN;
+        prew[i].g0 = *(ok ? reinterpret_cast<const u4*>(gb + wgg[i]) : &kZero16);
+      } else {
+        const float* gb = reinterpret_cast<const float*>(aa.gout) + (long long)n0 * L::CIN * HP * WP + prow * WP;
+        const float* gp = gb + (ok ? wgg[i] : 0);
+        float gv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gv[e] = ok ? gp[(size_t)e * HP * WP] : 0.f;
+        prew[i].g0 = u4{__float_as_uint(gv[0]), __float_as_uint(gv[1]), __float_as_uint(gv[2]), __float_as_uint(gv[3])};
+        prew[i].g1 = u4{__float_as_uint(gv[4]), __float_as_uint(gv[5]), __float_as_uint(gv[6]), __float_as_uint(gv[7])};
+      }
+    }
+  };
+  auto store_win_tile = [&](int ti) {
+    const int sg = ti / L::TPS, tt = ti - sg * L::TPS;
+    const int n0 = sg * L::NS, ty0 = tt * L::TH;
+    const float* ct = ctab + (n0 / aa.B) * 5 * L::CIN;
+#pragma unroll
+    for (int i = 0; i < WSL; ++i) {
+      const int task = tid + 256 * i;
+      if (task >= WT) continue;
+      u4 o[4] = {u4{0u, 0u, 0u, 0u}, u4{0u, 0u, 0u, 0u}, u4{0u, 0u, 0u, 0u}, u4{0u, 0u, 0u, 0u}};
+      if (wgo[i] >= 0 && (unsigned)(ty0 - L::PAD + wrow[i]) < (unsigned)L::H)
+        apply_window<AP == 1 ? 0 : 2, L::CIN>(prew[i], ct + 8 * (task % L::VPP), o);
+      *reinterpret_cast<u4*>(xs + wlo[i]) = o[0];
+      *reinterpret_cast<u4*>(xs + wlo[i] + L::PS) = o[1];
+      *reinterpret_cast<u4*>(xs + wlo[i] + L::RS * L::PS) = o[2];
+      *reinterpret_cast<u4*>(xs + wlo[i] + (L::RS + 1) * L::PS) = o[3];
+    }
+  };
+
+  if (t0 < t1) { if constexpr (AP) load_win_tile(t0); else load_tile(t0); }
+  for (int ti = t0; ti < t1; ++ti) {
+    __syncthreads();   // every wave is done reading the previous tile (and ctab is written)
+    if constexpr (AP) {
+      store_win_tile(ti);
+    } else {
+#pragma unroll
+      for (int i = 0; i < L::SLOTS; ++i)
+        if (tid + 256 * i < L::TASKS) *reinterpret_cast<u4*>(xs + loff[i]) = pre[i];
+    }
     __syncthreads();
-    if (ti + 1 < t1) load_tile(ti + 1);   // in flight under this tile's MFMAs
+    if (ti + 1 < t1) {   // in flight under this tile's MFMAs
+      if constexpr (AP) load_win_tile(ti + 1); else load_tile(ti + 1);
+    }
 
     const int sg = ti / L::TPS, tt = ti - sg * L::TPS;
     const int n0 = sg * L::NS, ty0 = tt * L::TH;
@@ -364,20 +445,21 @@ int num_cus() {
   return cus;
 }
 
-template <class L, bool FWD>
+template <class L, bool FWD, int AP = 0>
 int launch_ws(const void* x, const void* wk, const float* bias, void* y, float* stats, int N,
-              int B, hipStream_t st) {
+              int B, hipStream_t st, const ApplyArgs& aa = ApplyArgs{}) {
   if (N % L::NS || (FWD && stats && B % L::NS)) return AVD_ERR_SHAPE;
+  if (AP && (aa.B % L::NS || aa.G > APPLY_GMAX || aa.G * aa.B != N)) return AVD_ERR_SHAPE;
   static int occ = 0;
   if (!occ) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv_ws_kernel<L, FWD>, 256, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv_ws_kernel<L, FWD, AP>, 256, 0) !=
             hipSuccess || occ <= 0)
       occ = 1;
   }
   const int ntiles = (N / L::NS) * L::TPS;
   const int grid = std::min(ntiles, num_cus() * occ);
-  conv_ws_kernel<L, FWD><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, (bf16*)y,
-                                               stats, ntiles, ntiles * L::NPW);
+  conv_ws_kernel<L, FWD, AP><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, (bf16*)y,
+                                                   stats, ntiles, ntiles * L::NPW, aa);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
@@ -436,4 +518,39 @@ int avd_ws_conv_dgrad(const void* dy, const void* wk_d, void* dx, int dt, int N,
   else if (is<DgrI2>(Cout, Ho, Wo, Cin, K, dp)) r = launch_ws<DgrI2, false>(dy, wk_d, nullptr, dx, nullptr, N, N, st);
   else return 0;
   return r == AVD_OK ? 1 : (r == AVD_ERR_SHAPE ? 0 : r);
+}
+
+// Input gradient of a forward conv (Cin -> Cout over H x W) whose output y went through
+// BatchNorm -> ReLU -> 2x2 max-pool: dY = BN-backward-apply(y, pooled gradient gout, coef) is
+// formed while staging (bnapply.h), so no dY tensor is read or written.  gmode: layout of gout
+// (0 = pooled NHWC bf16, 2 = f32 (c,h,w) flatten).  1 = launched, 0 = not served, < 0 = error.
+int avd_ws_conv_dgrad_bnapply(const void* y, const void* gout, int gmode, const float* scale,
+                              const float* shift, const float* coef, const void* wk_d, void* dx,
+                              int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
+                              hipStream_t st) {
+  if (dt != AVD_BF16 || ws_disabled() || (gmode != 0 && gmode != 2) || B <= 0 || N % B) return 0;
+  const int Ho = H + 2 * pad - K + 1, Wo = W + 2 * pad - K + 1, dp = K - 1 - pad;
+  const ApplyArgs aa{gout, scale, shift, coef, B, N / B};
+  int r = 0;
+#define AVD_DA(LL)                                                                               \
+  if (is<LL>(Cout, Ho, Wo, Cin, K, dp)) {                                                       \
+    r = gmode == 0 ? launch_ws<LL, false, 1>(y, wk_d, nullptr, dx, nullptr, N, N, st, aa)       \
+                   : launch_ws<LL, false, 2>(y, wk_d, nullptr, dx, nullptr, N, N, st, aa);      \
+    return r == AVD_OK ? 1 : (r == AVD_ERR_SHAPE ? 0 : r);                                      \
+  }
+  AVD_DA(DgrA2) AVD_DA(DgrA3) AVD_DA(DgrA4) AVD_DA(DgrI2)
+#undef AVD_DA
+  return 0;
+}
+
+int avd_ws_dgrad_bnapply_serves(int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
+                                int pad, int gmode) {
+  if (dt != AVD_BF16 || ws_disabled() || (gmode != 0 && gmode != 2) || B <= 0 || N % B ||
+      N / B > APPLY_GMAX)
+    return 0;
+  const int Ho = H + 2 * pad - K + 1, Wo = W + 2 * pad - K + 1, dp = K - 1 - pad;
+#define AVD_DS(LL) if (is<LL>(Cout, Ho, Wo, Cin, K, dp)) return B % LL::NS == 0 && N % LL::NS == 0;
+  AVD_DS(DgrA2) AVD_DS(DgrA3) AVD_DS(DgrA4) AVD_DS(DgrI2)
+#undef AVD_DS
+  return 0;
 }

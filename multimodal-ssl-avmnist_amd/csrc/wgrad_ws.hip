@@ -24,6 +24,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "bnapply.h"
 
 // diagnostics builds (wrong results): WG_VARIANT 10 = no staging, 11 = no MFMA loop,
 // 12 = no staging + B fragments read once per k-step only for column 0, 13 = no staging + no MFMA
@@ -110,12 +111,16 @@ __device__ __forceinline__ f4 mma(bf16x8 a, bf16x8 b, f4 c) {
 // pixel (within a 32-pixel k-step) of k = 8 g + 4 h + q: half-waves read 8 consecutive pixels
 __device__ __forceinline__ int kpix(int g, int h, int q) { return 16 * (g >> 1) + 8 * h + 4 * (g & 1) + q; }
 
-template <class L>
+// AP: 0 = dy is the conv-output gradient; 1 / 2 = dy is the conv output y and the staging
+// applies the layer's BatchNorm backward (bnapply.h) with the pooled gradient in layout 0 / 2
+template <class L, int AP = 0>
 __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* __restrict__ x,
                                                                    const bf16* __restrict__ dy,
                                                                    float* __restrict__ parts,
-                                                                   int N, int chunks) {
+                                                                   int N, int chunks,
+                                                                   ApplyArgs aa) {
   __shared__ __attribute__((aligned(16))) bf16 smem[L::SMEM];
+  __shared__ __attribute__((aligned(16))) float ctab[AP ? APPLY_GMAX * 5 * L::COUT : 4];
   bf16* dys = smem;                       // [DYP][DYS]: pixel (s * TR + r) * WO8 + ox
   bf16* xs = smem + L::DY_ELEMS;          // [NSS][XR][XW][XS]: X[y0 - PAD + r][c - PAD]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -183,6 +188,7 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* _
   }
   u4 pre[L::SLOTS];
   auto load_strip = [&](int st) {
+    if constexpr (AP) return;
     const int sg = st / L::SPS, y0 = (st - sg * L::SPS) * L::TR;
     const int n = sg * L::NSS;
     const bf16* bdy = dy + ((size_t)n * L::HO + y0) * L::WO * L::COUT;
@@ -204,15 +210,103 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* _
       if (tid + L::NTHR * i < L::DY_T + L::X_T) *reinterpret_cast<u4*>(smem + loff[i]) = pre[i];
   };
 
-  if (st0 < st1) load_strip(st0);
+  // AP: dY comes from windows of y (2x2 x 8 channels + the pooled gradient -> 4 dY vectors);
+  // X keeps its 16-byte tasks in their own slots
+  constexpr int HOP = L::HO / 2, WOP = L::WO / 2;
+  constexpr int WT = AP ? L::NSS * (L::TR / 2) * WOP * (L::COUT / 8) : 0;
+  constexpr int WSL = AP ? cdv(WT, L::NTHR) : 1;
+  constexpr int XSL = AP ? cdv(L::X_T, L::NTHR) : 1;
+  int wgo[WSL], wgg[WSL], wlo[WSL];
+  int xgo[XSL], xlo[XSL], xrw[XSL];
+  WinIn wpre[WSL];
+  u4 xpre[XSL];
+  if constexpr (AP) {
+    static_assert(L::TR % 2 == 0 && L::HO % 2 == 0 && L::WO % 2 == 0, "windows");
+    apply_load_ctab<L::COUT>(ctab, aa, tid, L::NTHR);
+#pragma unroll
+    for (int i = 0; i < WSL; ++i) {
+      const int task = tid + L::NTHR * i;
+      constexpr int V = L::COUT / 8;
+      const int q = task % V, w = task / V;
+      const int wc2 = w % WOP, t = w / WOP;
+      const int wr = t % (L::TR / 2), sm = t / (L::TR / 2);
+      wgo[i] = task < WT ? ((sm * L::HO + 2 * wr) * L::WO + 2 * wc2) * L::COUT + 8 * q : -1;
+      wlo[i] = ((sm * L::TR + 2 * wr) * L::WO8 + 2 * wc2) * L::DYS + 8 * q;
+      wgg[i] = AP == 1 ? ((sm * HOP + wr) * WOP + wc2) * L::COUT + 8 * q
+                       : (sm * L::COUT + 8 * q) * HOP * WOP + wr * WOP + wc2;
+    }
+#pragma unroll
+    for (int i = 0; i < XSL; ++i) {
+      const int t = tid + L::NTHR * i;
+      constexpr int V = L::CIN / 8;
+      const int q = t % V, pix = t / V;
+      const int rs = pix / L::XW, c = pix - rs * L::XW;
+      const int sm = rs / L::XR, r = rs - sm * L::XR;
+      const int ix = c - L::PAD;
+      xlo[i] = L::DY_ELEMS + pix * L::XS + 8 * q;
+      xrw[i] = r;
+      xgo[i] = (t < L::X_T && ix >= 0 && ix < L::W) ? ((sm * L::H + r) * L::W + ix) * L::CIN + 8 * q : -1;
+    }
+  }
+  auto load_strip_ap = [&](int st) {
+    const int sg = st / L::SPS, y0 = (st - sg * L::SPS) * L::TR;
+    const int n = sg * L::NSS;
+    const bf16* by = dy + ((size_t)n * L::HO + y0) * L::WO * L::COUT;
+    const bf16* bx = x + ((long long)n * L::H + y0 - L::PAD) * L::W * L::CIN;
+#pragma unroll
+    for (int i = 0; i < WSL; ++i) {
+      const bool ok = wgo[i] >= 0;
+      const bf16* p = by + (ok ? wgo[i] : 0);
+      wpre[i].y[0] = *(ok ? reinterpret_cast<const u4*>(p) : &kZeroW);
+      wpre[i].y[1] = *(ok ? reinterpret_cast<const u4*>(p + L::COUT) : &kZeroW);
+      wpre[i].y[2] = *(ok ? reinterpret_cast<const u4*>(p + L::WO * L::COUT) : &kZeroW);
+      wpre[i].y[3] = *(ok ? reinterpret_cast<const u4*>(p + (L::WO + 1) * L::COUT) : &kZeroW);
+      if constexpr (AP == 1) {
+        const bf16* gb = reinterpret_cast<const bf16*>(aa.gout) + ((size_t)n * HOP + y0 / 2) * WOP * L::COUT;
+        wpre[i].g0 = *(ok ? reinterpret_cast<const u4*>(gb + wgg[i]) : &kZeroW);
+      } else {
+        const float* gp = reinterpret_cast<const float*>(aa.gout) + (size_t)n * L::COUT * HOP * WOP +
+                          (size_t)(y0 / 2) * WOP + (ok ? wgg[i] : 0);
+        float gv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gv[e] = ok ? gp[(size_t)e * HOP * WOP] : 0.f;
+        wpre[i].g0 = u4{__float_as_uint(gv[0]), __float_as_uint(gv[1]), __float_as_uint(gv[2]), __float_as_uint(gv[3])};
+        wpre[i].g1 = u4{__float_as_uint(gv[4]), __float_as_uint(gv[5]), __float_as_uint(gv[6]), __float_as_uint(gv[7])};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < XSL; ++i) {
+      const bool ok = xgo[i] >= 0 && (unsigned)(y0 - L::PAD + xrw[i]) < (unsigned)L::H;
+      xpre[i] = *(ok ? reinterpret_cast<const u4*>(bx + xgo[i]) : &kZeroW);
+    }
+  };
+  auto store_strip_ap = [&](int st) {
+    const int n = (st / L::SPS) * L::NSS;
+    const float* ct = ctab + (n / aa.B) * 5 * L::COUT;
+#pragma unroll
+    for (int i = 0; i < WSL; ++i) {
+      if (wgo[i] < 0) continue;
+      u4 o[4];
+      apply_window<AP == 1 ? 0 : 2, L::COUT>(wpre[i], ct + 8 * ((tid + L::NTHR * i) % (L::COUT / 8)), o);
+      *reinterpret_cast<u4*>(smem + wlo[i]) = o[0];
+      *reinterpret_cast<u4*>(smem + wlo[i] + L::DYS) = o[1];
+      *reinterpret_cast<u4*>(smem + wlo[i] + L::WO8 * L::DYS) = o[2];
+      *reinterpret_cast<u4*>(smem + wlo[i] + (L::WO8 + 1) * L::DYS) = o[3];
+    }
+#pragma unroll
+    for (int i = 0; i < XSL; ++i)
+      if (tid + L::NTHR * i < L::X_T) *reinterpret_cast<u4*>(smem + xlo[i]) = xpre[i];
+  };
+
+  if (st0 < st1) { if constexpr (AP) load_strip_ap(st0); else load_strip(st0); }
   for (int st = st0; st < st1; ++st) {
 #ifndef WG_NOSTAGE
     __syncthreads();
-    store_strip();
+    if constexpr (AP) store_strip_ap(st); else store_strip();
     __syncthreads();
 #endif
 #ifndef WG_NOSTAGE
-    if (st + 1 < st1) load_strip(st + 1);
+    if (st + 1 < st1) { if constexpr (AP) load_strip_ap(st + 1); else load_strip(st + 1); }
 #endif
 #ifdef WG_NOMFMA
     continue;
@@ -405,19 +499,47 @@ int avd_wg_chunks(int N, int Cout, int Cin, int K) {
 }
 
 // 1 = launched, 0 = not served, < 0 = error.  parts must hold avd_wg_chunks(...) slabs.
-int avd_wg_conv_wgrad(const void* x, const void* dy, int dt, float* parts, int N, int Cin, int H,
-                      int W, int Cout, int K, int pad, hipStream_t st) {
+// With gmode >= 0, dy is the conv output y and dY = BN-backward-apply(y, gout, coef) is formed
+// while staging (bnapply.h; gmode = layout of gout, B = samples per BN group).
+int avd_wg_conv_wgrad_ex(const void* x, const void* dy, int dt, float* parts, int N, int Cin,
+                         int H, int W, int Cout, int K, int pad, int gmode, const void* gout,
+                         const float* scale, const float* shift, const float* coef, int B,
+                         hipStream_t st) {
   if (dt != AVD_BF16 || wg_disabled()) return 0;
+  if (gmode >= 0 && (gmode == 1 || gmode > 2 || B <= 0 || N % B || N / B > APPLY_GMAX)) return 0;
   const int chunks = avd_wg_chunks(N, Cout, Cin, K);
   if (!chunks) return 0;
+  const ApplyArgs aa{gout, scale, shift, coef, B, B > 0 ? N / B : 0};
 #define AVD_WG(LL)                                                                              \
   if (wg_is<LL>(Cin, H, W, Cout, K, pad)) {                                                    \
-    if (N % LL::NSS) return 0;                                                                  \
-    wgrad_ws_kernel<LL><<<chunks, LL::NTHR, 0, st>>>((const bf16*)x, (const bf16*)dy, parts, N, chunks); \
+    if (N % LL::NSS || (gmode >= 0 && B % LL::NSS)) return 0;                                  \
+    if (gmode < 0)                                                                             \
+      wgrad_ws_kernel<LL, 0><<<chunks, LL::NTHR, 0, st>>>((const bf16*)x, (const bf16*)dy, parts, N, chunks, aa); \
+    else if (gmode == 0)                                                                       \
+      wgrad_ws_kernel<LL, 1><<<chunks, LL::NTHR, 0, st>>>((const bf16*)x, (const bf16*)dy, parts, N, chunks, aa); \
+    else                                                                                       \
+      wgrad_ws_kernel<LL, 2><<<chunks, LL::NTHR, 0, st>>>((const bf16*)x, (const bf16*)dy, parts, N, chunks, aa); \
     AVD_CHECK_LAUNCH();                                                                         \
     return 1;                                                                                   \
   }
   AVD_WG(WgA2) AVD_WG(WgA3) AVD_WG(WgA4) AVD_WG(WgI2)
 #undef AVD_WG
+  return 0;
+}
+
+int avd_wg_conv_wgrad(const void* x, const void* dy, int dt, float* parts, int N, int Cin, int H,
+                      int W, int Cout, int K, int pad, hipStream_t st) {
+  return avd_wg_conv_wgrad_ex(x, dy, dt, parts, N, Cin, H, W, Cout, K, pad, -1, nullptr, nullptr,
+                              nullptr, nullptr, 0, st);
+}
+
+int avd_wg_bnapply_serves(int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
+                          int gmode) {
+  if (dt != AVD_BF16 || wg_disabled() || (gmode != 0 && gmode != 2) || B <= 0 || N % B ||
+      N / B > APPLY_GMAX || !avd_wg_chunks(N, Cout, Cin, K))
+    return 0;
+#define AVD_WS(LL) if (wg_is<LL>(Cin, H, W, Cout, K, pad)) return N % LL::NSS == 0 && B % LL::NSS == 0;
+  AVD_WS(WgA2) AVD_WS(WgA3) AVD_WS(WgA4) AVD_WS(WgI2)
+#undef AVD_WS
   return 0;
 }

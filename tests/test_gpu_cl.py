@@ -407,3 +407,54 @@ def test_ws_conv_wgrad_matches_legacy(ops, shape, monkeypatch):
     _, dw_ref, _ = O.conv2d_bwd(dy.astype(np.float64), win, wz, x.shape, pad)
     assert rel(w1, dw_ref) < 1e-5
     assert rel(w0, dw_ref) < 1e-5
+
+
+# BatchNorm-backward apply fused into the dgrad / wgrad staging (bnapply.h): must equal the
+# unfused avd_cl_bn_bwd_apply -> avd_cl_conv_wgrad / avd_cl_conv_dgrad chain bit for bit.
+BNAPPLY_SHAPES = [  # N, B, Cin, H, Cout, K, pad, gmode (0: pooled NHWC bf16, 2: f32 flatten)
+    (48, 24, 8, 56, 16, 5, 2, 0), (48, 24, 16, 28, 32, 5, 2, 0), (48, 24, 32, 14, 64, 5, 2, 2),
+    (48, 24, 32, 14, 64, 5, 0, 2), (48, 16, 32, 14, 64, 5, 2, 0)]
+
+
+@pytest.mark.parametrize("shape", BNAPPLY_SHAPES)
+def test_bnapply_fused_dgrad_wgrad_match_unfused(ops, shape):
+    N, B, Cin, H, Cout, K, pad, gmode = shape
+    G = N // B
+    T = torch.bfloat16
+    Ho = H + 2 * pad - K + 1
+    assert ops.cl_bnapply_ok(T, N, B, Cin, H, H, Cout, K, pad, gmode)
+    g = torch.Generator(device="cuda").manual_seed(21)
+
+    def rnd(*shape, dtype=torch.float32, lo=-1.0, hi=1.0):
+        return (torch.rand(*shape, generator=g, device="cuda") * (hi - lo) + lo).to(dtype)
+
+    x = rnd(N, H, H, Cin, dtype=T)
+    y = rnd(N, Ho, Ho, Cout, dtype=T)
+    gout = rnd(N, Ho // 2, Ho // 2, Cout, dtype=T) if gmode == 0 else rnd(N * Cout * (Ho // 2) ** 2)
+    scale, shift = rnd(G * Cout, lo=0.5, hi=1.5), rnd(G * Cout, lo=-0.2, hi=0.2)
+    coef = rnd(G * Cout * 3, lo=-0.5, hi=0.5)
+    w = rnd(Cout, Cin, K, K) / (Cin * K * K) ** 0.5
+    wd = torch.empty(ops.cl_weight_elems(Cout, Cin, K, 1), device="cuda", dtype=T)
+    ops.cl_weight_layout(w, wd, 1)
+    nch = ops.cl_wgrad_chunks(N, Cout, Cin, K)
+
+    def wsum(parts):
+        dw = torch.empty(Cout * Cin * K * K, device="cuda")
+        ops.sum_rows(parts, nch, Cout * Cin * K * K, dw)
+        return dw
+
+    # unfused chain
+    dy = torch.empty_like(y)
+    ops.cl_bn_bwd_apply(y, gout, gmode, scale, shift, coef, dy, N, B, Cout, Ho, Ho)
+    p0 = torch.full((nch * Cout * Cin * K * K,), float("nan"), device="cuda")
+    ops.cl_conv_wgrad(x, dy, p0, N, Cin, H, H, Cout, K, pad)
+    dx0 = torch.empty(N, H, H, Cin, device="cuda", dtype=T)
+    ops.cl_conv_dgrad(dy, wd, dx0, N, Cin, H, H, Cout, K, pad)
+    # fused
+    p1 = torch.full_like(p0, float("nan"))
+    ops.cl_conv_wgrad_bnapply(x, y, gout, gmode, scale, shift, coef, p1, N, B, Cin, H, H, Cout, K, pad)
+    dx1 = torch.full_like(dx0, float("nan"))
+    ops.cl_conv_dgrad_bnapply(y, gout, gmode, scale, shift, coef, wd, dx1, N, B, Cin, H, H, Cout, K, pad)
+    torch.cuda.synchronize()
+    assert torch.equal(wsum(p1), wsum(p0))
+    assert torch.equal(dx1, dx0)
