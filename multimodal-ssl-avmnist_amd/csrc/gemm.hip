@@ -113,7 +113,7 @@ struct GemmT<2> { typedef bf16 T; static constexpr int LDK = 40; };
 enum { LAY_K = 0, LAY_R = 1, LAY_S = 2 };
 
 template <int ROWS>
-struct TileRegs { float v[ROWS / 8]; };   // ROWS*32 elements over 256 threads
+struct TileRegs { float v[ROWS / 8 > 16 ? ROWS / 8 : 16]; };   // ROWS*32 elements over 256 threads
 
 template <int ROWS, int LAY>
 __device__ __forceinline__ void load_tile(const float* __restrict__ X, long long sr, long long sk,
@@ -138,22 +138,29 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ X, long long
       t.v[4 * i] = v.x; t.v[4 * i + 1] = v.y; t.v[4 * i + 2] = v.z; t.v[4 * i + 3] = v.w;
     }
   } else if constexpr (LAY == LAY_R) {
+    // a 4 (k) x 4 (rows) block per thread: four float4 loads along the rows, transposed in
+    // registers so store_tile writes 4 consecutive k of a row at once
 #pragma unroll
-    for (int i = 0; i < ROWS / 32; ++i) {
-      const int e4 = tid + 256 * i;
-      const int k = e4 / (ROWS / 4), r = (e4 % (ROWS / 4)) * 4;
-      const int gr = r0 + r, gk = k0 + k;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (gk < kend) {
-        const float* p = X + (size_t)gk * sk + gr;
-        if (gr + 3 < rows) v = *reinterpret_cast<const float4*>(p);
-        else {
-          if (gr < rows) v.x = p[0];
-          if (gr + 1 < rows) v.y = p[1];
-          if (gr + 2 < rows) v.z = p[2];
+    for (int i = 0; i < (ROWS + 127) / 128; ++i) {
+      const int b = tid + 256 * i;
+      const int kb = b / (ROWS / 4), r = (b % (ROWS / 4)) * 4;
+      const int gr = r0 + r;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int gk = k0 + 4 * kb + kk;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (b < 2 * ROWS && gk < kend) {
+          const float* p = X + (size_t)gk * sk + gr;
+          if (gr + 3 < rows) v = *reinterpret_cast<const float4*>(p);
+          else {
+            if (gr < rows) v.x = p[0];
+            if (gr + 1 < rows) v.y = p[1];
+            if (gr + 2 < rows) v.z = p[2];
+          }
         }
+        t.v[16 * i + kk] = v.x; t.v[16 * i + 4 + kk] = v.y;
+        t.v[16 * i + 8 + kk] = v.z; t.v[16 * i + 12 + kk] = v.w;
       }
-      t.v[4 * i] = v.x; t.v[4 * i + 1] = v.y; t.v[4 * i + 2] = v.z; t.v[4 * i + 3] = v.w;
     }
   } else {
     const bool kfast = sk <= sr;
@@ -196,11 +203,21 @@ __device__ __forceinline__ void store_tile(const TileRegs<ROWS>& t, long long sr
     }
   } else if constexpr (LAY == LAY_R) {
 #pragma unroll
-    for (int i = 0; i < ROWS / 32; ++i) {
-      const int e4 = tid + 256 * i;
-      const int k = e4 / (ROWS / 4), r = (e4 % (ROWS / 4)) * 4;
+    for (int i = 0; i < (ROWS + 127) / 128; ++i) {
+      const int b = tid + 256 * i;
+      if (b >= 2 * ROWS) continue;
+      const int kb = b / (ROWS / 4), r = (b % (ROWS / 4)) * 4;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) lds_put<MODE>(S + (r + j) * LDK + k, t.v[4 * i + j]);
+      for (int j = 0; j < 4; ++j) {
+        typename GemmT<MODE>::T* d = S + (r + j) * LDK + 4 * kb;
+        const float* v = &t.v[16 * i + 4 * j];
+        if constexpr (MODE == 2) {
+          *reinterpret_cast<uint2*>(d) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) d[kk] = v[kk];
+        }
+      }
     }
   } else {
     const bool kfast = sk <= sr;
@@ -341,6 +358,18 @@ struct Plan { int bm, bn, splits, kchunk; };
 
 Plan plan_for(int M, int N, int K) {
   auto tiles = [&](int bm, int bn) { return (long long)avd_cdiv(M, bm) * avd_cdiv(N, bn); };
+  // encoder Linear forward (x [rows, 1600 / 3136] x W^T, N = 256): one 256-wide column tile so
+  // the f32 activations stream from HBM once (128x64 tiles re-read them 4x), split-K for blocks
+  if (N > 128 && N <= 256 && K >= 1024 && M >= 4096) {
+    Plan p{128, 256, 1, K};
+    const long long t = tiles(128, 256);
+    const int s = (int)std::max(1ll, std::min<long long>(avd_cdiv(224, t), K / 128));
+    if (s > 1) {
+      p.kchunk = avd_cdiv(avd_cdiv(K, s), 32) * 32;
+      p.splits = avd_cdiv(K, p.kchunk);
+    }
+    return p;
+  }
   Plan p{64, 64, 1, K};
   if (tiles(128, 128) >= 224) p = {128, 128, 1, K};
   else if (tiles(128, 64) >= 224) p = {128, 64, 1, K};
@@ -368,7 +397,7 @@ void launch_gemm(const Plan& pl, int M, int N, int K, const float* A, long long 
   if (pl.bm == BM_ && pl.bn == BN_)                                                            \
     gemm_mfma_kernel<MODE, BM_, BN_, LA, LB><<<grid, 256, 0, st>>>(                            \
         M, N, K, pl.kchunk, A, sam, sak, B, sbk, sbn, C, ldc, bias, alpha, beta, w);
-  AVD_G(128, 128) else AVD_G(128, 64) else AVD_G(64, 64)
+  AVD_G(128, 256) else AVD_G(128, 128) else AVD_G(128, 64) else AVD_G(64, 64)
 #undef AVD_G
   if (pl.splits > 1) {
     const long long MN = (long long)M * N;
