@@ -219,6 +219,17 @@ int avd_cl_bn_bwd_apply_wgrad(const void* y, const void* gout, const float* scal
                               int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
                               void* stream);
 
+/* The partial sums of avd_cl_bn_bwd_reduce (same rows and layout, for avd_bn_bwd_finalize)
+ * from the POOLED output p = maxpool2(relu(y*scale + shift)) instead of y: at the window's
+ * argmax z = gamma*xhat + beta = p, so xhat = (p - beta)/gamma wherever the gradient is routed
+ * (p > 0).  pooled has gout's layout (mode 0: NHWC dt = the next conv's input; mode 2: f32
+ * (c,h,w) flatten = the encoder Linear's input); y is read only for channels with gamma == 0.
+ * Reads 2/4 of y's bytes instead of 5/4.  Modes 0 and 2, even H and W. */
+int avd_cl_bn_bwd_reduce_pooled(const void* y, int dt, const void* pooled, const void* gout,
+                                int mode, const float* gamma, const float* beta, const float* mean,
+                                const float* invstd, float* parts, int N, int B, int C, int H,
+                                int W, void* stream);
+
 /* BatchNorm-backward apply fused into BOTH consumers of dy, for the mid-layer convs (bf16):
  * the input- and weight-gradient kernels read the conv output y [N,Ho,Wo,Cout] and the pooled
  * gradient gout (layout gmode: 0 = pooled NHWC in dt, 2 = f32 [N][Cout*Ho/2*Wo/2] in (c,h,w)

@@ -114,6 +114,8 @@ class ConvBranch:
             ops.cl_bn_relu_pool(y, st[2], st[3], out, mode, N, B, co, Ho, Ho)
             if i < nl - 1:
                 ctx["x"].append(out)
+            else:
+                ctx["feat"] = out     # the tail's pooled output (the backward's BN reduce reads it)
             h = out
         return h.view(N, -1), ctx
 
@@ -218,7 +220,13 @@ class ConvBranch:
             bk, ck = self.stack.bn_keys[i], self.stack.conv_keys[i]
             R = ops.cl_bn_bwd_rows(B, co, Ho, Ho, self.act)
             parts = ws.get("bwd_parts", co * G * R * 2)
-            ops.cl_bn_bwd_reduce(y, gout, mode, st[2], st[3], st[0], st[1], parts, N, B, co, Ho, Ho)
+            pooled = ctx["x"][i + 1] if i < nl - 1 else ctx.get("feat")
+            if mode in (0, 2) and pooled is not None and Ho % 2 == 0:
+                # from the pooled output (2/4 of y's bytes): xhat = (p - beta)/gamma at the argmax
+                ops.cl_bn_bwd_reduce_pooled(y, pooled, gout, mode, store[bk + ".weight"],
+                                            store[bk + ".bias"], st[0], st[1], parts, N, B, co, Ho, Ho)
+            else:
+                ops.cl_bn_bwd_reduce(y, gout, mode, st[2], st[3], st[0], st[1], parts, N, B, co, Ho, Ho)
             coef = ws.get("bwd_coef", G * co * 3)
             ops.bn_bwd_finalize(parts, G, R, co, B * Ho * Ho, store[bk + ".weight"], st[0], st[1],
                                 coef, store.grad_of(bk + ".weight"), store.grad_of(bk + ".bias"),

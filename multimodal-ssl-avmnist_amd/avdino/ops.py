@@ -370,6 +370,19 @@ def cl_bn_bwd_reduce(y, gout, mode, scale, shift, mean, invstd, parts, N, B, C, 
                         p(mean), p(invstd), p(parts), N, B, C, H, W, stream()))
 
 
+def cl_bn_bwd_reduce_pooled(y, pooled, gout, mode, gamma, beta, mean, invstd, parts, N, B, C, H, W):
+    """cl_bn_bwd_reduce's partial rows from the pooled output (xhat = (p - beta)/gamma at the
+    argmax): reads pooled + gout instead of y + gout."""
+    R = cl_bn_bwd_rows(B, C, H, W, y.dtype)
+    _need(parts.numel() >= C * (N // B) * R * 2, "cl bwd parts")
+    _need(mode in (0, 2) and pooled.numel() == gout.numel() and pooled.dtype == gout.dtype,
+          "pooled bwd reduce layout")
+    nb = pooled.numel() * pooled.element_size() + gout.numel() * gout.element_size()
+    _timed(f"cl_bn_bwd_reduce_pooled[{N}x{H}x{W}x{C} m{mode} {y.dtype}]", nb, 0,
+           lambda: call("avd_cl_bn_bwd_reduce_pooled", p(y), dtcode(y), p(pooled), p(gout), mode,
+                        p(gamma), p(beta), p(mean), p(invstd), p(parts), N, B, C, H, W, stream()))
+
+
 def cl_bn_bwd_apply(y, gout, mode, scale, shift, coef, dy, N, B, C, H, W):
     _need(dy.numel() == y.numel() and dy.dtype == y.dtype, "cl bwd dy")
     nb = 2 * y.numel() * y.element_size() + gout.numel() * gout.element_size()

@@ -237,6 +237,72 @@ __global__ __launch_bounds__(256) void bwd_reduce_cl_kernel(
   }
 }
 
+// The same partial sums from the POOLED output p = max_k relu(y_k*scale + shift) (the next
+// layer's input, already in memory) instead of the 4x larger conv output y: at a window's
+// argmax a, z_a = gamma*xhat_a + beta = p, so where the gradient is routed (p > 0)
+// xhat_a = (p - beta) / gamma.  Reads p + gout (2/4 of y's bytes) instead of y + gout.
+// A channel with gamma == 0 has every z equal (= relu(beta)), so the first-max pixel is the
+// window's first one: its xhat is taken from y (read only for such channels).
+template <typename T>
+__global__ __launch_bounds__(256) void bwd_reduce_pooled_cl_kernel(
+    const T* __restrict__ y, const void* __restrict__ pooled, const void* __restrict__ gout,
+    int mode, const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ parts,
+    int G, int B, int C, int H, int W, int R, long long per) {
+  constexpr int V = Vec<T>::V;
+  __shared__ float sh[256][2 * V + 1];
+  const int Hp = H / 2, Wp = W / 2, CV = C / V;
+  const int slots = 256 / CV;
+  const int cv = threadIdx.x % CV, slot = threadIdx.x / CV;
+  const int r = blockIdx.x, g = blockIdx.y;
+  const int c0 = cv * V;
+  const long long nwin = (long long)B * Hp * Wp;
+  const long long w0 = r * per, w1 = std::min(nwin, w0 + per);
+  float ig[V], be[V], mu[V], is[V], s1[V], s2[V];
+  bool any0 = false;
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    const float ga = gamma[c0 + e];
+    ig[e] = ga != 0.f ? 1.f / ga : 0.f;
+    any0 |= ga == 0.f;
+    be[e] = beta[c0 + e];
+    s1[e] = 0.f; s2[e] = 0.f;
+  }
+  load_coef<V>(mean, g * C + c0, mu);
+  load_coef<V>(invstd, g * C + c0, is);
+  if (slot < slots) {
+    for (long long wi = w0 + slot; wi < w1; wi += slots) {
+      const int wp = (int)(wi % Wp), hp = (int)((wi / Wp) % Hp);
+      const int n = g * B + (int)(wi / ((long long)Wp * Hp));
+      float gg[V], pv[V];
+      load_gout<T, V>(gout, mode, n, hp, wp, Hp, Wp, C, c0, gg);
+      load_gout<T, V>(pooled, mode, n, hp, wp, Hp, Wp, C, c0, pv);
+      float y0[V];
+      if (any0) Vec<T>::ld(y + (((size_t)n * H + 2 * hp) * W + 2 * wp) * C + c0, y0);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float dz = pv[e] > 0.f ? gg[e] : 0.f;
+        const float xh = ig[e] != 0.f ? (pv[e] - be[e]) * ig[e] : (any0 ? (y0[e] - mu[e]) * is[e] : 0.f);
+        s1[e] += dz;
+        s2[e] += dz * xh;
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    sh[threadIdx.x][2 * e] = s1[e];
+    sh[threadIdx.x][2 * e + 1] = s2[e];
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < C * 2; o += 256) {
+    const int c = o >> 1, k = o & 1;
+    const int ocv = c / V, e = c % V;
+    float t = 0.f;
+    for (int s = 0; s < slots; ++s) t += sh[s * CV + ocv][2 * e + k];
+    parts[(((size_t)c * G + g) * R + r) * 2 + k] = t;
+  }
+}
+
 // dy = k1 * dz + kx * y + k0 for every pixel (incl. rows/cols outside the floor-mode windows)
 template <typename T>
 __global__ __launch_bounds__(256) void bwd_apply_cl_kernel(
@@ -362,6 +428,32 @@ int avd_cl_bn_bwd_apply_impl(const void* y, int dt, const void* gout, int mode,
     bwd_apply_cl_kernel<float><<<grid_for(total), 256, 0, st>>>((const float*)y, gout, mode, scale,
                                                                 shift, coef, (float*)dy, total, B,
                                                                 C, H, W);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+// BN-backward partial sums from the pooled output (bwd_reduce_pooled_cl_kernel); same rows as
+// avd_cl_bn_bwd_reduce.  pooled has gout's layout (mode 0: NHWC dt, mode 2: f32 (c,h,w)).
+int avd_cl_bn_bwd_reduce_pooled_impl(const void* y, int dt, const void* pooled, const void* gout,
+                                     int mode, const float* gamma, const float* beta,
+                                     const float* mean, const float* invstd, float* parts, int N,
+                                     int B, int C, int H, int W, hipStream_t st) {
+  const int V = dt == AVD_BF16 ? 8 : 4;
+  if (C % V || C / V > 256 || N % B || (mode != 0 && mode != 2) || (H & 1) || (W & 1))
+    return AVD_ERR_SHAPE;
+  const int G = N / B;
+  const int R = avd_cl_bn_bwd_rows_impl(B, C, H, W, dt);
+  const long long nwin = (long long)B * (H / 2) * (W / 2);
+  const long long per = (nwin + R - 1) / R;
+  dim3 grid(R, G);
+  if (dt == AVD_BF16)
+    bwd_reduce_pooled_cl_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)y, pooled, gout, mode, gamma,
+                                                            beta, mean, invstd, parts, G, B, C, H, W,
+                                                            R, per);
+  else
+    bwd_reduce_pooled_cl_kernel<float><<<grid, 256, 0, st>>>((const float*)y, pooled, gout, mode, gamma,
+                                                             beta, mean, invstd, parts, G, B, C, H, W,
+                                                             R, per);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

@@ -54,6 +54,11 @@ int avd_wg_conv_wgrad_ex(const void* x, const void* dy, int dt, float* parts, in
                          const float* scale, const float* shift, const float* coef, int B,
                          hipStream_t st);
 
+int avd_cl_bn_bwd_reduce_pooled_impl(const void* y, int dt, const void* pooled, const void* gout,
+                                     int mode, const float* gamma, const float* beta,
+                                     const float* mean, const float* invstd, float* parts, int N,
+                                     int B, int C, int H, int W, hipStream_t st);
+
 extern "C" {
 
 int avd_cl_weight_elems(int Cout, int Cin, int K, int dgrad) {
@@ -124,6 +129,17 @@ int avd_cl_conv_dgrad(const void* dy, const void* wk_d, void* dx, int dt, int N,
   if (!dy || !wk_d || !dx || !dt_ok(dt)) return AVD_ERR_ARG;
   if (N <= 0 || (K != 3 && K != 5)) return AVD_ERR_SHAPE;
   return avd_cl_conv_dgrad_impl(dy, wk_d, dx, dt, N, Cin, H, W, Cout, K, pad, avd_stream(stream));
+}
+
+int avd_cl_bn_bwd_reduce_pooled(const void* y, int dt, const void* pooled, const void* gout,
+                                int mode, const float* gamma, const float* beta, const float* mean,
+                                const float* invstd, float* parts, int N, int B, int C, int H,
+                                int W, void* stream) {
+  if (!y || !pooled || !gout || !gamma || !beta || !mean || !invstd || !parts || !dt_ok(dt))
+    return AVD_ERR_ARG;
+  if (N <= 0 || B <= 0 || H < 2 || W < 2) return AVD_ERR_SHAPE;
+  return avd_cl_bn_bwd_reduce_pooled_impl(y, dt, pooled, gout, mode, gamma, beta, mean, invstd,
+                                          parts, N, B, C, H, W, avd_stream(stream));
 }
 
 int avd_cl_bnapply_ok(int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
