@@ -21,6 +21,21 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
+// 16-byte load through the global address space.  A pointer selected between a tensor and a
+// __device__ zero vector is otherwise a generic pointer, i.e. a flat_load, which also counts in
+// lgkmcnt: every later LDS wait would then wait for the (prefetch) loads to land as well.
+typedef __attribute__((ext_vector_type(4))) unsigned u4v;
+#ifndef AVD_LDG_FLAT
+#define AVD_LDG_FLAT 0   // 1: generic (flat) loads, for A/B builds (tools/build_ws_variants.sh)
+#endif
+__device__ __forceinline__ u4v ldg16(const void* p) {
+#if AVD_LDG_FLAT
+  return *(const u4v*)p;
+#else
+  return *(const __attribute__((address_space(1))) u4v*)p;
+#endif
+}
+
 template <typename T> struct io;
 template <> struct io<float> {
   static __device__ __forceinline__ float ld(const float* p, size_t i) { return p[i]; }

@@ -183,6 +183,7 @@ typedef __attribute__((ext_vector_type(4))) short s4;
 typedef __attribute__((address_space(3))) s4 lds_s4;
 
 __device__ __forceinline__ void st16(bf16* p, bf16 v) { *p = v; }
+__device__ const u4 kZeroC1 = {0u, 0u, 0u, 0u};
 
 __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ y, const bf16* __restrict__ gz,
@@ -206,16 +207,49 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
     bb[tt] = k2 & 1;
     ba[tt] = (k2 >= 0 ? k2 >> 1 : -1) + 1;
   }
+  // every global load of a tile is issued before the block's barrier (the previous tile's
+  // MFMAs may still read LDS): per thread <= 2 input-row vectors and <= 2 pooling windows
+  // (W <= WMAX), past-the-end slots read a zero vector (no select on the loaded data)
+  const int nxt = (TH + 4) * cpr, nwin = (TH / 2) * Wp;
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int n = tile / tps, ty0 = (tile - n * tps) * TH, grp = n / B;
-    __syncthreads();
-    // ---- input rows ty0-2 .. ty0+TH+1 -> parity/shift copies xc[b][a][r][P] = x[2(P+a-1)+b]
-    for (int t = tid; t < (TH + 4) * cpr; t += 256) {
+    u4 xv[2], yv4[2][4], gv[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int t = tid + 256 * s;
       const int r = t / cpr, c = t - r * cpr;
       const int iy = ty0 - 2 + r;
-      const bool ok = iy >= 0 && iy < H;
-      const u4 v = *reinterpret_cast<const u4*>(x + ((size_t)n * H + (ok ? iy : 0)) * W + 8 * c);
-      const unsigned wv[4] = {ok ? v.x : 0u, ok ? v.y : 0u, ok ? v.z : 0u, ok ? v.w : 0u};
+      const bool ok = t < nxt && iy >= 0 && iy < H;
+      xv[s] = ldg16(ok ? (const void*)(x + ((size_t)n * H + iy) * W + 8 * c) : &kZeroC1);
+      const int w = tid + 256 * s;
+      const bool wok = w < nwin;
+      const int hp = w / Wp, wp = w - hp * Wp;
+      const size_t pix0 = ((size_t)n * H + ty0 + 2 * hp) * W + 2 * wp;
+      const size_t po[4] = {pix0, pix0 + 1, pix0 + W, pix0 + W + 1};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        yv4[s][k] = ldg16(wok ? (const void*)(y + po[k] * COUT) : &kZeroC1);
+      gv[s] = ldg16(wok ? (const void*)(gz + (((size_t)n * Hp + (ty0 >> 1) + hp) * Wp + wp) * COUT)
+                        : &kZeroC1);
+    }
+    float sc[COUT], sf[COUT], k1[COUT], kx[COUT], k0[COUT];
+#pragma unroll
+    for (int e = 0; e < COUT; ++e) {
+      const int gc = grp * COUT + e;
+      sc[e] = scale[gc];
+      sf[e] = shift[gc];
+      k1[e] = coef[gc * 3];
+      kx[e] = coef[gc * 3 + 1];
+      k0[e] = coef[gc * 3 + 2];
+    }
+    __syncthreads();
+    // ---- input rows ty0-2 .. ty0+THB+1 -> parity/shift copies xc[b][a][r][P] = x[2(P+a-1)+b]
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int t = tid + 256 * s;
+      if (t >= nxt) continue;
+      const int r = t / cpr, c = t - r * cpr;
+      const unsigned wv[4] = {xv[s].x, xv[s].y, xv[s].z, xv[s].w};
       // wv[d] holds pixels 8c+2d (low) and 8c+2d+1 (high) = pair 4c+d of parity 0 / 1
       const unsigned e0 = (wv[0] & 0xffffu) | (wv[1] << 16), e1 = (wv[2] & 0xffffu) | (wv[3] << 16);
       const unsigned o0 = (wv[0] >> 16) | (wv[1] & 0xffff0000u), o1 = (wv[2] >> 16) | (wv[3] & 0xffff0000u);
@@ -236,31 +270,21 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
       }
     }
     // pairs whose source pixel lies outside the row: P = 0 of a = 0, P = W/2 - 1 of a = 2
-    for (int t = tid; t < (TH + 4) * 2; t += 256) {
-      const int r = t >> 1, b = t & 1;
+    if (tid < (TH + 4) * 2) {
+      const int r = tid >> 1, b = tid & 1;
       xc[b][0][r][0] = bf16(0);
       xc[b][2][r][Wp - 1] = bf16(0);
     }
     // ---- dy of the tile's windows into dys (natural NHWC rows)
-    float sc[COUT], sf[COUT], k1[COUT], kx[COUT], k0[COUT];
 #pragma unroll
-    for (int e = 0; e < COUT; ++e) {
-      const int gc = grp * COUT + e;
-      sc[e] = scale[gc];
-      sf[e] = shift[gc];
-      k1[e] = coef[gc * 3];
-      kx[e] = coef[gc * 3 + 1];
-      k0[e] = coef[gc * 3 + 2];
-    }
-    for (int w = tid; w < (TH / 2) * Wp; w += 256) {
+    for (int s = 0; s < 2; ++s) {
+      const int w = tid + 256 * s;
+      if (w >= nwin) continue;
       const int hp = w / Wp, wp = w - hp * Wp;
-      const size_t pix0 = ((size_t)n * H + ty0 + 2 * hp) * W + 2 * wp;
-      const size_t po[4] = {pix0, pix0 + 1, pix0 + W, pix0 + W + 1};
       float yv[4][COUT];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const u4 v = *reinterpret_cast<const u4*>(y + po[k] * COUT);
-        const unsigned wv[4] = {v.x, v.y, v.z, v.w};
+        const unsigned wv[4] = {yv4[s][k].x, yv4[s][k].y, yv4[s][k].z, yv4[s][k].w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           yv[k][2 * i] = __uint_as_float(wv[i] << 16);
@@ -269,9 +293,7 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
       }
       float gg[COUT];
       {
-        const u4 v = *reinterpret_cast<const u4*>(
-            gz + (((size_t)n * Hp + (ty0 >> 1) + hp) * Wp + wp) * COUT);
-        const unsigned wv[4] = {v.x, v.y, v.z, v.w};
+        const unsigned wv[4] = {gv[s].x, gv[s].y, gv[s].z, gv[s].w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           gg[2 * i] = __uint_as_float(wv[i] << 16);
@@ -347,7 +369,24 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
 
 }  // namespace
 
-int avd_c1p8_wgrad_slabs(int N, int H) { return std::min(N * (H / TH), 2048); }
+// one resident wave of blocks (CUs x blocks per CU): the blocks walk the tiles in step,
+// with no tail round of partly filled CUs
+int avd_c1p8_wgrad_slabs(int N, int H) {
+  static int resident = 0;
+  if (!resident) {
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, c1p8_bwd_wgrad_kernel, 256, 0) !=
+            hipSuccess || per <= 0)
+      per = 3;
+    resident = cus * per;
+  }
+  return std::min(N * (H / TH), resident);
+}
+static int rc_wgrad_slabs(int N, int H) { return std::min(N * (H / TH), 2048); }
 
 int avd_c1p8_bwd_apply_wgrad(const void* y, const void* gout, const float* scale,
                              const float* shift, const float* coef, const void* x, float* parts,
@@ -641,7 +680,7 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
 
 // rows per BN group (stats / reduce passes) or slabs (wgrad pass)
 int avd_c1r_rows(int pass, int N, int B, int H) {
-  return pass == RC_WGRAD ? avd_c1p8_wgrad_slabs(N, H) : B * 4;
+  return pass == RC_WGRAD ? rc_wgrad_slabs(N, H) : B * 4;
 }
 
 int avd_c1r_launch(int pass, const void* x, const void* wk, const float* bias, const float* scale,
@@ -649,7 +688,7 @@ int avd_c1r_launch(int pass, const void* x, const void* wk, const float* bias, c
                    const void* gz, void* z, float* out, int N, int B, int H, int W,
                    hipStream_t st) {
   const int tps = H / TH, ntiles = N * tps;
-  const int grid = pass == RC_WGRAD ? avd_c1p8_wgrad_slabs(N, H) : N;
+  const int grid = pass == RC_WGRAD ? rc_wgrad_slabs(N, H) : N;
 #define AVD_RC(PS)                                                                             \
   c1p8_recompute_kernel<PS><<<grid, 256, 0, st>>>(                                             \
       (const bf16*)x, (const bf16*)wk, bias, scale, shift, mean, invstd, coef, (const bf16*)gz, \

@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256, AP ? (L::OCC > 1 ? L::OCC - 1 : 1) : L::OCC) v
       // nothing waits for these loads before the next tile's LDS write
       const bool ok = goff[i] >= 0 && (unsigned)(ty0 - L::PAD + srow[i]) < (unsigned)L::H;
       const u4* src = ok ? reinterpret_cast<const u4*>(bx + goff[i]) : &kZero16;
-      pre[i] = *src;
+      pre[i] = ldg16(src);
     }
   };
 
@@ -211,13 +211,13 @@ __global__ __launch_bounds__(256, AP ? (L::OCC > 1 ? L::OCC - 1 : 1) : L::OCC) v
     for (int i = 0; i < WSL; ++i) {
       const bool ok = wgo[i] >= 0 && (unsigned)(ty0 - L::PAD + wrow[i]) < (unsigned)L::H;
       const bf16* p = by + (ok ? wgo[i] : 0);
-      prew[i].y[0] = *(ok ? reinterpret_cast<const u4*>(p) : &kZero16);
-      prew[i].y[1] = *(ok ? reinterpret_cast<const u4*>(p + L::CIN) : &kZero16);
-      prew[i].y[2] = *(ok ? reinterpret_cast<const u4*>(p + L::W * L::CIN) : &kZero16);
-      prew[i].y[3] = *(ok ? reinterpret_cast<const u4*>(p + (L::W + 1) * L::CIN) : &kZero16);
+      prew[i].y[0] = ldg16(ok ? (const void*)(p) : &kZero16);
+      prew[i].y[1] = ldg16(ok ? (const void*)(p + L::CIN) : &kZero16);
+      prew[i].y[2] = ldg16(ok ? (const void*)(p + L::W * L::CIN) : &kZero16);
+      prew[i].y[3] = ldg16(ok ? (const void*)(p + (L::W + 1) * L::CIN) : &kZero16);
       if constexpr (AP == 1) {
         const bf16* gb = reinterpret_cast<const bf16*>(aa.gout) + ((long long)n0 * HP + prow) * WP * L::CIN;
-        prew[i].g0 = *(ok ? reinterpret_cast<const u4*>(gb + wgg[i]) : &kZero16);
+        prew[i].g0 = ldg16(ok ? (const void*)(gb + wgg[i]) : &kZero16);
       } else {
         const float* gb = reinterpret_cast<const float*>(aa.gout) + (long long)n0 * L::CIN * HP * WP + prow * WP;
         const float* gp = gb + (ok ? wgg[i] : 0);

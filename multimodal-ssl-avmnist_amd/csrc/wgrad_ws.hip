@@ -201,7 +201,7 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* _
       } else if (goff[i] >= 0 && (unsigned)(y0 - L::PAD + xrow[i]) < (unsigned)L::H) {
         src = reinterpret_cast<const u4*>(bx + goff[i]);
       }
-      pre[i] = *src;
+      pre[i] = ldg16(src);
     }
   };
   auto store_strip = [&]() {
@@ -257,13 +257,13 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* _
     for (int i = 0; i < WSL; ++i) {
       const bool ok = wgo[i] >= 0;
       const bf16* p = by + (ok ? wgo[i] : 0);
-      wpre[i].y[0] = *(ok ? reinterpret_cast<const u4*>(p) : &kZeroW);
-      wpre[i].y[1] = *(ok ? reinterpret_cast<const u4*>(p + L::COUT) : &kZeroW);
-      wpre[i].y[2] = *(ok ? reinterpret_cast<const u4*>(p + L::WO * L::COUT) : &kZeroW);
-      wpre[i].y[3] = *(ok ? reinterpret_cast<const u4*>(p + (L::WO + 1) * L::COUT) : &kZeroW);
+      wpre[i].y[0] = ldg16(ok ? (const void*)(p) : &kZeroW);
+      wpre[i].y[1] = ldg16(ok ? (const void*)(p + L::COUT) : &kZeroW);
+      wpre[i].y[2] = ldg16(ok ? (const void*)(p + L::WO * L::COUT) : &kZeroW);
+      wpre[i].y[3] = ldg16(ok ? (const void*)(p + (L::WO + 1) * L::COUT) : &kZeroW);
       if constexpr (AP == 1) {
         const bf16* gb = reinterpret_cast<const bf16*>(aa.gout) + ((size_t)n * HOP + y0 / 2) * WOP * L::COUT;
-        wpre[i].g0 = *(ok ? reinterpret_cast<const u4*>(gb + wgg[i]) : &kZeroW);
+        wpre[i].g0 = ldg16(ok ? (const void*)(gb + wgg[i]) : &kZeroW);
       } else {
         const float* gp = reinterpret_cast<const float*>(aa.gout) + (size_t)n * L::COUT * HOP * WOP +
                           (size_t)(y0 / 2) * WOP + (ok ? wgg[i] : 0);
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* _
 #pragma unroll
     for (int i = 0; i < XSL; ++i) {
       const bool ok = xgo[i] >= 0 && (unsigned)(y0 - L::PAD + xrw[i]) < (unsigned)L::H;
-      xpre[i] = *(ok ? reinterpret_cast<const u4*>(bx + xgo[i]) : &kZeroW);
+      xpre[i] = ldg16(ok ? (const void*)(bx + xgo[i]) : &kZeroW);
     }
   };
   auto store_strip_ap = [&](int st) {
