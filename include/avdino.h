@@ -274,6 +274,14 @@ int avd_cl_c1_recompute(int pass, const void* x, const void* wk, const float* bi
 int avd_sum_rows(const float* in, int rows, int cols, long long ld, float* out, int accumulate,
                  void* stream);
 
+/* The same sum in two passes for tall, narrow inputs (Linear bias gradients over thousands of
+ * rows, conv weight-grad slabs): avd_sum_rows_chunks(rows, cols) row chunks are summed in
+ * parallel into work[chunk][cols] (work_elems >= chunks*cols), then reduced in chunk order.
+ * chunks depends on the shape only (deterministic everywhere); 1 = single pass, work unused. */
+int avd_sum_rows_chunks(int rows, int cols);
+int avd_sum_rows_split(const float* in, int rows, int cols, long long ld, float* out,
+                       int accumulate, float* work, long long work_elems, void* stream);
+
 /* Column partial statistics of x [rows, C] f32 for BatchNorm1d: parts [C, G, R, 2] with
  * R = avd_colstats_parts(rows/G) row-chunks per group.  pivot [G,C] (nullable) receives
  * the first row of each group; the partials are then taken about it (pass it on to

@@ -54,6 +54,8 @@ PROTOS = {
     "avd_cl_c1_recompute": [I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "avd_cl_bn_bwd_apply_wgrad": [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "avd_sum_rows": [P, I, I, L, P, I, P],
+    "avd_sum_rows_chunks": [I, I],
+    "avd_sum_rows_split": [P, I, I, L, P, I, P, L, P],
     "avd_colstats_parts": [I],
     "avd_colstats": [P, I, I, I, P, P, P],
     "avd_act_fwd": [P, P, I, P, P, I, I, I, F, U64, P],

@@ -102,7 +102,7 @@ class ConvBranch:
                             store[bk + ".running_mean"] if update_running else None,
                             store[bk + ".running_var"] if update_running else None)
             if update_running:
-                store.buffers[bk + ".num_batches_tracked"] += G
+                store.bump_nbt(bk + ".num_batches_tracked", G)
             ctx["y"].append(y)
             ctx["stats"].append(st)
             if i == nl - 1:
@@ -168,7 +168,7 @@ class ConvBranch:
                         store[bk + ".running_mean"] if update_running else None,
                         store[bk + ".running_var"] if update_running else None)
         if update_running:
-            store.buffers[bk + ".num_batches_tracked"] += G
+            store.bump_nbt(bk + ".num_batches_tracked", G)
         out = ws.get(f"{tag}.x1", N * Hp * Hp * co, self.act)
         ops.cl_c1_recompute(ops.C1_APPLY, x, wk, bias, N, B, ci, H, H, co, k, pad, scale=st[2],
                             shift=st[3], z=out)
@@ -290,7 +290,7 @@ class ProjHead:
                         store[p + ".mlp.1.running_mean"] if update_running else None,
                         store[p + ".mlp.1.running_var"] if update_running else None, pivot=pivot)
         if update_running:
-            store.buffers[p + ".mlp.1.num_batches_tracked"] += G
+            store.bump_nbt(p + ".mlp.1.num_batches_tracked", G)
         a = ws.get(f"{tag}.a", rows * Hd)
         ops.act_fwd(h, a, 1, st[2], st[3], rows, G, Hd, drop_p, seed)
         ops.linear_fwd(a, store[p + ".mlp.4.weight"], store[p + ".mlp.4.bias"], out, rows, mode=self.gm)
@@ -521,6 +521,7 @@ class MultiCentralEngine:
         self.last = dict(B=B, G=G, L=L, V=V, NG=NG, N=N, cat=cat, senc=senc, sfus=sfus, spc=spc,
                          ds=ds, hctx=hctx, center_new=center_new, loss=loss, s_proj=s_proj,
                          t_proj=t_proj, training=training, head_out=head_out)
+        st.flush_nbt()
         return loss
 
     def _infonce(self, zi, za, B, P, aux, dzi, dza, temperature=0.07):
@@ -730,6 +731,7 @@ class UniModalEngine:
         ops.sum_to(loss_parts, loss_parts.numel(), 1.0, loss)
         self.last = dict(B=B, G=G, L=L, V=V, emb=emb, sctx=sctx, spc=spc, ds=ds, cos=cos,
                          center_new=center_new, s_proj=s_proj, t_proj=t_proj, loss=loss)
+        st.flush_nbt()
         return loss
 
     def update_center(self):
@@ -842,6 +844,7 @@ class SimCLREngine:
         loss = ws.get("loss", 1)
         ops.sum_to(parts, 2 * B, scale, loss)
         self.last = dict(B=B, mode=mode, calls=calls, reps=reps, dreps=dreps, loss=loss)
+        st.flush_nbt()
         return loss
 
     def backward(self):

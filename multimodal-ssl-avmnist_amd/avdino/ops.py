@@ -4,6 +4,8 @@ Every function takes torch tensors that live on the HIP device, checks shapes/dt
 host, and launches on torch's current stream.  PyTorch is used here only for device memory
 and streams; all arithmetic happens in libavdino.so.
 """
+import os
+
 import torch
 
 from ._lib import BF16, F32, call, lib
@@ -439,10 +441,25 @@ def cl_c1_recompute(pas, x, wk, bias, N, B, Cin, H, W, Cout, K, pad, scale=None,
                         pad, stream()))
 
 
+_SUM_WS = {}
+_SUM_SPLIT = os.environ.get("AVDINO_SUMROWS_SPLIT", "1") == "1"   # 0: single pass (A/B runs)
+
+
 def sum_rows(x, rows, cols, out, accumulate=0, ld=None, off=0):
+    """out[c] (+)= sum_r x[off + r*ld + c]: avd_sum_rows_split (row chunks in parallel, then
+    the chunk partials in fixed order) with a per-(device, stream) scratch."""
     ld = cols if ld is None else ld
     _need(off + (rows - 1) * ld + cols <= x.numel() and out.numel() >= cols, "sum_rows bounds")
-    call("avd_sum_rows", x.data_ptr() + 4 * off, rows, cols, ld, p(out), accumulate, stream())
+    if not _SUM_SPLIT:
+        call("avd_sum_rows", x.data_ptr() + 4 * off, rows, cols, ld, p(out), accumulate, stream())
+        return
+    n = lib.avd_sum_rows_chunks(rows, cols) * cols
+    key = (x.device, torch.cuda.current_stream(x.device).cuda_stream)
+    w = _SUM_WS.get(key)
+    if w is None or w.numel() < n:
+        w = _SUM_WS[key] = torch.empty(max(n, 1 << 16), device=x.device, dtype=torch.float32)
+    call("avd_sum_rows_split", x.data_ptr() + 4 * off, rows, cols, ld, p(out), accumulate, p(w),
+         w.numel(), stream())
 
 
 def colstats_parts(rows_per_group):

@@ -98,11 +98,18 @@ class ParamStore:
         self.buf_offs, nbuf = layout(fkeys)
         self.buf_arena = torch.zeros(max(nbuf, ALIGN), dtype=torch.float32, device=self.device)
         self.buffers = OrderedDict()
+        # num_batches_tracked counters: one int64 arena, bumped once per forward for all BN
+        # layers (bump_nbt / flush_nbt) instead of one add launch per layer
+        nkeys = [k for k, (_s, kind) in self.spec.items() if kind == "nbt"]
+        self.nbt_index = {k: i for i, k in enumerate(nkeys)}
+        self.nbt_arena = torch.zeros(max(len(nkeys), 1), dtype=torch.int64, device=self.device)
+        self._nbt_pending, self._nbt_cache = {}, {}
         for k, (shape, kind) in self.spec.items():
             if kind in ("rm", "rv", "center"):
                 self.buffers[k] = self._view(self.buf_arena, self.buf_offs, k)
             elif kind == "nbt":
-                self.buffers[k] = torch.zeros(shape, dtype=torch.int64, device=self.device)
+                i = self.nbt_index[k]
+                self.buffers[k] = self.nbt_arena[i:i + 1].view(shape)
         self.reset_parameters(seed)
 
     def group_range(self, i):
@@ -124,6 +131,24 @@ class ParamStore:
         if key in self.t_offs:
             return self._view(self.teacher, self.t_offs, key)
         return self.buffers[key]
+
+    def bump_nbt(self, key, inc):
+        """Record num_batches_tracked += inc for one BN layer (applied by flush_nbt)."""
+        self._nbt_pending[key] = self._nbt_pending.get(key, 0) + inc
+
+    def flush_nbt(self):
+        """Apply the recorded counter increments: one index_add_ on the current stream (the
+        index / value tensors are cached per increment pattern, so no host copy per step)."""
+        if not self._nbt_pending:
+            return
+        sig = tuple(sorted(self._nbt_pending.items()))
+        self._nbt_pending = {}
+        c = self._nbt_cache.get(sig)
+        if c is None:
+            idx = torch.tensor([self.nbt_index[k] for k, _ in sig], dtype=torch.int64, device=self.device)
+            val = torch.tensor([v for _, v in sig], dtype=torch.int64, device=self.device)
+            c = self._nbt_cache[sig] = (idx, val)
+        self.nbt_arena.index_add_(0, c[0], c[1])
 
     def grad_of(self, key):
         o, n = self.s_offs[key]
@@ -159,6 +184,7 @@ class ParamStore:
         self.adam_step = 0
 
     def state_dict(self):
+        self.flush_nbt()
         return OrderedDict((k, self[k]) for k in self.spec)
 
     def load_state_dict(self, sd, strict=True):

@@ -50,6 +50,7 @@ class _CentralEncoder:
         if train:
             fi, _ = self.img.forward(ws, st, "pi", x_img, N, 1, True, False)
             fa, _ = self.aud.forward(ws, st, "pa", x_aud, N, 1, True, False)
+            st.flush_nbt()
         else:
             fi = self.img.forward_eval(ws, st, "pi", x_img, N)
             fa = self.aud.forward_eval(ws, st, "pa", x_aud, N)
@@ -76,6 +77,7 @@ class _UniEncoder:
     def __call__(self, ws, st, x, N, train):
         if train:
             out, _ = self.enc.forward(ws, st, "pu", x, N, 1, False)
+            st.flush_nbt()
             return out
         return self.enc.forward_eval(ws, st, "pu", x, N)
 
@@ -93,9 +95,8 @@ class LinearProbe:
         self.store = ParamStore(source.spec, dev, has_teacher=source.teacher is not None)
         self.store.student.copy_(source.student)          # copy.deepcopy(model.student)
         self.store.buf_arena.copy_(source.buf_arena)
-        for k, b in source.buffers.items():
-            if k.endswith("num_batches_tracked"):
-                self.store.buffers[k].copy_(b)
+        source.flush_nbt()
+        self.store.nbt_arena.copy_(source.nbt_arena)
         self.kind = UNI_ALIASES.get(kind, kind)
         self.D = D
         self.gm = ops.GEMM_BF16_MFMA if act_dtype == torch.bfloat16 else ops.GEMM_F32_MFMA

@@ -552,20 +552,26 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(
 template <int CW>
 __global__ __launch_bounds__(1024) void sum_rows_kernel(const float* __restrict__ in, int rows,
                                                         int cols, long long ld,
-                                                        float* __restrict__ out, int accumulate) {
+                                                        float* __restrict__ out, int accumulate,
+                                                        int rows_per_chunk) {
+  // block (x, y) sums rows [y * rows_per_chunk, +rows_per_chunk) of its CW columns into row y
+  // of out (leading dimension cols); a single chunk is the whole reduction
   constexpr int PH = 1024 / CW;
   __shared__ double sh[PH][CW];
   const int lc = threadIdx.x % CW, ph = threadIdx.x / CW;
   const int col = blockIdx.x * CW + lc;
+  const int r0 = blockIdx.y * rows_per_chunk;
+  const int r1 = min(rows, r0 + rows_per_chunk);
+  out += (size_t)blockIdx.y * cols;
   double s = 0.0;
   if (col < cols) {
-    int r = ph;
-    for (; r + 3 * PH < rows; r += 4 * PH) {
+    int r = r0 + ph;
+    for (; r + 3 * PH < r1; r += 4 * PH) {
       const float a = in[(size_t)r * ld + col], b = in[(size_t)(r + PH) * ld + col];
       const float c = in[(size_t)(r + 2 * PH) * ld + col], d = in[(size_t)(r + 3 * PH) * ld + col];
       s += (double)a + (double)b + (double)c + (double)d;
     }
-    for (; r < rows; r += PH) s += in[(size_t)r * ld + col];
+    for (; r < r1; r += PH) s += in[(size_t)r * ld + col];
   }
   sh[ph][lc] = s;
   __syncthreads();
@@ -806,16 +812,51 @@ int avd_bn1d_bwd_apply(const float* x, const float* dz, const float* coef, float
   return AVD_OK;
 }
 
+static void launch_sum_rows(const float* in, int rows, int cols, long long ld, float* out,
+                            int accumulate, int chunks, hipStream_t st) {
+  const int rpc = avd_cdiv(rows, chunks);
+  if (cols <= 2048)
+    sum_rows_kernel<16><<<dim3(avd_cdiv(cols, 16), chunks), 1024, 0, st>>>(in, rows, cols, ld, out,
+                                                                          accumulate, rpc);
+  else
+    sum_rows_kernel<64><<<dim3(avd_cdiv(cols, 64), chunks), 1024, 0, st>>>(in, rows, cols, ld, out,
+                                                                          accumulate, rpc);
+}
+
 int avd_sum_rows(const float* in, int rows, int cols, long long ld, float* out, int accumulate,
                  void* stream) {
   if (!in || !out) return AVD_ERR_ARG;
   if (rows <= 0 || cols <= 0 || ld < cols) return AVD_ERR_SHAPE;
-  if (cols <= 2048)
-    sum_rows_kernel<16><<<avd_cdiv(cols, 16), 1024, 0, avd_stream(stream)>>>(in, rows, cols, ld, out,
-                                                                            accumulate);
-  else
-    sum_rows_kernel<64><<<avd_cdiv(cols, 64), 1024, 0, avd_stream(stream)>>>(in, rows, cols, ld, out,
-                                                                            accumulate);
+  launch_sum_rows(in, rows, cols, ld, out, accumulate, 1, avd_stream(stream));
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+// Row chunks for avd_sum_rows_split: enough blocks to cover the chip (>= 1024) with >= 4 row
+// phases of work per thread; 1 = no split.  A function of the shape only, so the summation
+// order (and the result) is the same on every device.
+int avd_sum_rows_chunks(int rows, int cols) {
+  if (rows <= 0 || cols <= 0) return 1;
+  const int cw = cols <= 2048 ? 16 : 64, ph = 1024 / cw;
+  const int cb = avd_cdiv(cols, cw);
+  const int want = avd_cdiv(1024, cb), most = rows / (4 * ph);
+  const int c = want < most ? want : most;
+  return c > 1 ? c : 1;
+}
+
+int avd_sum_rows_split(const float* in, int rows, int cols, long long ld, float* out,
+                       int accumulate, float* work, long long work_elems, void* stream) {
+  if (!in || !out) return AVD_ERR_ARG;
+  if (rows <= 0 || cols <= 0 || ld < cols) return AVD_ERR_SHAPE;
+  const int chunks = avd_sum_rows_chunks(rows, cols);
+  hipStream_t st = avd_stream(stream);
+  if (chunks == 1) {
+    launch_sum_rows(in, rows, cols, ld, out, accumulate, 1, st);
+  } else {
+    if (!work || work_elems < (long long)chunks * cols) return AVD_ERR_ARG;
+    launch_sum_rows(in, rows, cols, ld, work, 0, chunks, st);        // chunk partials
+    launch_sum_rows(work, chunks, cols, cols, out, accumulate, 1, st);   // fixed-order total
+  }
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

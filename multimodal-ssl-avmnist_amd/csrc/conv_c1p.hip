@@ -185,12 +185,29 @@ typedef __attribute__((address_space(3))) s4 lds_s4;
 __device__ __forceinline__ void st16(bf16* p, bf16 v) { *p = v; }
 __device__ const u4 kZeroC1 = {0u, 0u, 0u, 0u};
 
+// parity/shift input copies of the backward kernel: element offset of (b, a, r, P).  Row /
+// copy strides of 80 / 1648 / 5056 elements (160 / 3296 / 10112 B) spread the 16 taps of a
+// B-fragment read over distinct 16-byte bank windows: 13.1 instead of 52 LDS cycles per
+// pair of ds_read_b128 (tools/lds_bank_sim.py); 20.2 KB instead of 15.4 KB
+constexpr int XB_RS = 80, XB_CA = 1648, XB_CB = 5056;
+__device__ __forceinline__ int xbo(int b, int a, int r, int P) {
+  return b * XB_CB + a * XB_CA + r * XB_RS + P;
+}
+// dy tile column of pixel cx in tile row ry: in the odd k-blocks (kb = ry * segs + cx / 16)
+// the two 8-pixel halves of the 16-pixel segment trade places, so the 4 k-blocks one MFMA
+// step reads (kb = 4ks .. 4ks+3, 256 B apart) fall on both halves of the 64 banks:
+// no 2-way conflict between the lane halves of ds_read_b64_tr_b16
+__device__ __forceinline__ int dys_px(int ry, int cx, int segs) {
+  return cx ^ (((ry * segs + (cx >> 4)) & 1) << 3);
+}
+
 __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ y, const bf16* __restrict__ gz,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ coef, float* __restrict__ parts, int B, int H, int W, int ntiles,
     int tps) {
-  __shared__ __attribute__((aligned(16))) bf16 xc[2][3][TH + 4][XCW];
+  static_assert(XB_CA >= (TH + 4) * XB_RS && XB_CB >= 3 * XB_CA && XB_RS >= WMAX / 2, "xc strides");
+  __shared__ __attribute__((aligned(16))) bf16 xc[2 * XB_CB];
   __shared__ __attribute__((aligned(16))) bf16 dys[TH * WMAX * COUT];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int gq = lane >> 4, col = lane & 15;
@@ -257,13 +274,13 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const unsigned lo = b ? od[0] : ev[0], hi = b ? od[1] : ev[1];   // pairs 4c..4c+3
-        *reinterpret_cast<uint2*>(&xc[b][1][r][4 * c]) = make_uint2(lo, hi);
+        *reinterpret_cast<uint2*>(&xc[xbo(b, 1, r, 4 * c)]) = make_uint2(lo, hi);
         // a = 0: P = pair + 1;  a = 2: P = pair - 1
-        bf16* d0 = &xc[b][0][r][4 * c + 1];
+        bf16* d0 = &xc[xbo(b, 0, r, 4 * c + 1)];
         st16(d0, (bf16)(lo & 0xffffu));
         *reinterpret_cast<unsigned*>(d0 + 1) = (lo >> 16) | (hi << 16);
         st16(d0 + 3, (bf16)(hi >> 16));
-        bf16* d2 = &xc[b][2][r][4 * c];
+        bf16* d2 = &xc[xbo(b, 2, r, 4 * c)];
         if (c > 0) st16(d2 - 1, (bf16)(lo & 0xffffu));
         *reinterpret_cast<unsigned*>(d2) = (lo >> 16) | (hi << 16);
         st16(d2 + 2, (bf16)(hi >> 16));
@@ -272,8 +289,8 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
     // pairs whose source pixel lies outside the row: P = 0 of a = 0, P = W/2 - 1 of a = 2
     if (tid < (TH + 4) * 2) {
       const int r = tid >> 1, b = tid & 1;
-      xc[b][0][r][0] = bf16(0);
-      xc[b][2][r][Wp - 1] = bf16(0);
+      xc[xbo(b, 0, r, 0)] = bf16(0);
+      xc[xbo(b, 2, r, Wp - 1)] = bf16(0);
     }
     // ---- dy of the tile's windows into dys (natural NHWC rows)
 #pragma unroll
@@ -300,7 +317,7 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
           gg[2 * i + 1] = __uint_as_float(wv[i] & 0xffff0000u);
         }
       }
-      unsigned outw[4][4];
+      float dv[4][COUT];
 #pragma unroll
       for (int e = 0; e < COUT; ++e) {
         float best = fmaxf(fmaf(yv[0][e], sc[e], sf[e]), 0.f);
@@ -312,18 +329,15 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
         }
         const float dz = best > 0.f ? gg[e] : 0.f;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float d = fmaf(k1[e], a == k ? dz : 0.f, fmaf(kx[e], yv[k][e], k0[e]));
-          const uint32_t hb = __builtin_bit_cast(uint16_t, (__bf16)d);
-          if (e & 1) outw[k][e >> 1] |= hb << 16;
-          else outw[k][e >> 1] = hb;
-        }
+        for (int k = 0; k < 4; ++k)
+          dv[k][e] = fmaf(k1[e], a == k ? dz : 0.f, fmaf(kx[e], yv[k][e], k0[e]));
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int ry = 2 * hp + (k >> 1), cx = 2 * wp + (k & 1);
-        *reinterpret_cast<u4*>(&dys[(ry * WMAX + cx) * COUT]) =
-            u4{outw[k][0], outw[k][1], outw[k][2], outw[k][3]};
+        *reinterpret_cast<u4*>(&dys[(ry * WMAX + dys_px(ry, cx, segs)) * COUT]) =
+            u4{pack_bf16x2(dv[k][0], dv[k][1]), pack_bf16x2(dv[k][2], dv[k][3]),
+               pack_bf16x2(dv[k][4], dv[k][5]), pack_bf16x2(dv[k][6], dv[k][7])};
       }
     }
     __syncthreads();
@@ -334,16 +348,18 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
       const int r = kb / segs, P0 = 8 * (kb - r * segs);
       // A: rows P0 + 4*half + q, columns 4p .. 4p+3 of the pair rows (32 B each)
       const int q = col >> 2, pp = col & 3;
+      // (the segment's two 128-byte halves swapped when kb is odd, see dys_px)
+      const int hsw = (kb & 1) << 3;
       s4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (lds_s4*)&dys[(r * WMAX + 2 * (P0 + q)) * COUT + 4 * pp]);
+          (lds_s4*)&dys[(r * WMAX + 2 * P0 + ((2 * q) ^ hsw)) * COUT + 4 * pp]);
       s4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (lds_s4*)&dys[(r * WMAX + 2 * (P0 + 4 + q)) * COUT + 4 * pp]);
+          (lds_s4*)&dys[(r * WMAX + 2 * P0 + ((8 + 2 * q) ^ hsw)) * COUT + 4 * pp]);
       typedef __attribute__((ext_vector_type(8))) short s8;
       const s8 av = s8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
       const bf16x8 A = __builtin_bit_cast(bf16x8, av);
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
-        const u4 bw = *reinterpret_cast<const u4*>(&xc[bb[tt]][ba[tt]][r + bky[tt]][P0]);
+        const u4 bw = *reinterpret_cast<const u4*>(&xc[xbo(bb[tt], ba[tt], r + bky[tt], P0)]);
         acc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, __builtin_bit_cast(bf16x8, bw), acc[tt],
                                                          0, 0, 0);
       }

@@ -509,3 +509,27 @@ def test_stage_views(ops):
     ref = np.concatenate([gv.transpose(1, 0, 2, 3, 4).reshape(-1, 784), lv.transpose(1, 0, 2, 3, 4).reshape(-1, 784),
                           orig.reshape(-1, 784)])
     assert np.array_equal(host(out), ref)
+
+
+@pytest.mark.parametrize("rows,cols,ld,off", [(7168, 256, 512, 256), (512, 3200, 3200, 0),
+                                              (256, 51200, 51200, 0), (7, 5, 9, 3), (6144, 512, 512, 0)])
+def test_sum_rows_split_matches_f64(ops, rows, cols, ld, off):
+    """avd_sum_rows_split (row chunks in parallel, chunk partials summed in fixed order) against
+    the float64 column sums, with and without accumulation; bitwise equal across runs."""
+    from avdino._lib import lib
+    g = np.random.default_rng(rows + cols)
+    x = g.standard_normal(off + (rows - 1) * ld + cols).astype(np.float32)
+    base = g.standard_normal(cols).astype(np.float32)
+    xm = np.pad(x[off:], (0, rows * ld - (x.size - off))).reshape(rows, ld)[:, :cols]
+    want = xm.astype(np.float64).sum(0)
+    tx = dev(x)
+    out = torch.empty(cols, device="cuda")
+    ops.sum_rows(tx, rows, cols, out, ld=ld, off=off)
+    assert rel(host(out), want) < 1e-6
+    out2 = torch.empty(cols, device="cuda")
+    ops.sum_rows(tx, rows, cols, out2, ld=ld, off=off)
+    assert torch.equal(out, out2)
+    acc = dev(base.copy())
+    ops.sum_rows(tx, rows, cols, acc, accumulate=1, ld=ld, off=off)
+    assert rel(host(acc), want + base) < 1e-6
+    assert lib.avd_sum_rows_chunks(rows, cols) >= 1
