@@ -87,7 +87,7 @@ class ConvBranch:
         nl = len(self.stack.convs)
         for i, (ci, co, k, pad) in enumerate(self.stack.convs):
             H, Ho, Hp = self.dims[i]
-            if i == 0 and nl > 1 and self._recompute_ok(N, B, ci, H, co, k, pad):
+            if i == 0 and nl > 1 and self._recompute_ok(N, B, ci, H, co, k, pad, need_dgrad):
                 h = self._first_layer_recompute_fwd(ws, store, tag, ctx, h, N, G, B, update_running)
                 continue
             R = ops.cl_stat_rows(Ho, Ho, B, k, ci, co, self.act)
@@ -111,7 +111,13 @@ class ConvBranch:
             else:
                 mode = 0
                 out = ws.get(f"{tag}.x{i + 1}", N * Hp * Hp * co, self.act)
-            ops.cl_bn_relu_pool(y, st[2], st[3], out, mode, N, B, co, Ho, Ho)
+            if (i == 0 and mode == 0 and self.RC_APPLY and self.act == torch.bfloat16 and
+                    ops.cl_c1_recompute_rows(ops.C1_APPLY, self.act, N, B, ci, H, H, co, k, pad) > 0):
+                # BN -> ReLU -> pool from the conv recomputed out of x (bit-identical y)
+                ops.cl_c1_recompute(ops.C1_APPLY, h, wts[0][0], store[self.stack.conv_keys[0] + ".bias"],
+                                    N, B, ci, H, H, co, k, pad, scale=st[2], shift=st[3], z=out)
+            else:
+                ops.cl_bn_relu_pool(y, st[2], st[3], out, mode, N, B, co, Ho, Ho)
             if i < nl - 1:
                 ctx["x"].append(out)
             else:
@@ -145,12 +151,18 @@ class ConvBranch:
         return h.view(N, -1)
 
     # ---- first layer without a stored conv output (avd_cl_c1_recompute): the audio conv1
-    # Off by default: measured slower than storing y (r1: the recomputing backward passes are
-    # VALU-bound); AVDINO_L1_RECOMPUTE=1 turns it on for experiments.
+    # For a training forward, off by default: measured slower than storing y (the recomputing
+    # backward passes are VALU-bound); AVDINO_L1_RECOMPUTE=1 turns it on for experiments.
     RECOMPUTE = os.environ.get("AVDINO_L1_RECOMPUTE", "0") == "1"
+    # forwards without a backward (the teacher): y is never needed, so never stored -- stats
+    # and apply passes recompute it from the 8x smaller input (r1_34: +1.5 % step rate)
+    RC_NOGRAD = os.environ.get("AVDINO_L1_RC_NOGRAD", "1") == "1"
+    # stored-y forward whose BN -> ReLU -> pool recomputes y from x instead of reading the
+    # 1.44 GB it just wrote (bit-identical y; r1_34: +0.5 %)
+    RC_APPLY = os.environ.get("AVDINO_L1_RC_APPLY", "1") == "1"
 
-    def _recompute_ok(self, N, B, ci, H, co, k, pad):
-        return (self.RECOMPUTE and self.act == torch.bfloat16 and
+    def _recompute_ok(self, N, B, ci, H, co, k, pad, need_dgrad=True):
+        return ((self.RECOMPUTE or (self.RC_NOGRAD and not need_dgrad)) and self.act == torch.bfloat16 and
                 ops.cl_c1_recompute_rows(ops.C1_STATS, self.act, N, B, ci, H, H, co, k, pad) > 0)
 
     def _first_layer_recompute_fwd(self, ws, store, tag, ctx, x, N, G, B, update_running):
