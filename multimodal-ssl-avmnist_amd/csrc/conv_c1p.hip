@@ -189,6 +189,9 @@ __device__ const u4 kZeroC1 = {0u, 0u, 0u, 0u};
 // copy strides of 80 / 1648 / 5056 elements (160 / 3296 / 10112 B) spread the 16 taps of a
 // B-fragment read over distinct 16-byte bank windows: 13.1 instead of 52 LDS cycles per
 // pair of ds_read_b128 (tools/lds_bank_sim.py); 20.2 KB instead of 15.4 KB
+#ifndef C1B_DIAG
+#define C1B_DIAG 0   // diagnostic builds only (tools/build_ws_variants.sh SRC=conv_c1p MACRO=C1B_DIAG)
+#endif
 constexpr int XB_RS = 80, XB_CA = 1648, XB_CB = 5056;
 __device__ __forceinline__ int xbo(int b, int a, int r, int P) {
   return b * XB_CB + a * XB_CA + r * XB_RS + P;
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
   static_assert(XB_CA >= (TH + 4) * XB_RS && XB_CB >= 3 * XB_CA && XB_RS >= WMAX / 2, "xc strides");
   __shared__ __attribute__((aligned(16))) bf16 xc[2 * XB_CB];
   __shared__ __attribute__((aligned(16))) bf16 dys[TH * WMAX * COUT];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int gq = lane >> 4, col = lane & 15;
   const int Hp = H >> 1, Wp = W >> 1, cpr = W >> 3, segs = W >> 4;
   f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
@@ -228,26 +231,36 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
   // MFMAs may still read LDS): per thread <= 2 input-row vectors and <= 2 pooling windows
   // (W <= WMAX), past-the-end slots read a zero vector (no select on the loaded data)
   const int nxt = (TH + 4) * cpr, nwin = (TH / 2) * Wp;
+  // tile-invariant per-lane offsets (elements, relative to the tile's first row): the loads
+  // are then a block-uniform base + one 32-bit offset
+  int xr[2], xoff[2], yoff[2], goff[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int t = tid + 256 * s;
+    const int r = t / cpr, c = t - r * cpr;
+    xr[s] = t < nxt ? r : -(1 << 20);         // out-of-slot lanes: never a valid row
+    xoff[s] = (r - 2) * W + 8 * c;
+    const int w = min(tid + 256 * s, nwin - 1);   // out-of-slot windows re-read the last one
+    const int hp = w / Wp, wp = w - hp * Wp;
+    yoff[s] = (2 * hp * W + 2 * wp) * COUT;
+    goff[s] = (hp * Wp + wp) * COUT;
+  }
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int n = tile / tps, ty0 = (tile - n * tps) * TH, grp = n / B;
+    const bf16* xb = x + ((size_t)n * H + ty0) * W;
+    const bf16* yb = y + ((size_t)n * H + ty0) * W * COUT;
+    const bf16* gb = gz + ((size_t)n * Hp + (ty0 >> 1)) * Wp * COUT;
     u4 xv[2], yv4[2][4], gv[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int t = tid + 256 * s;
-      const int r = t / cpr, c = t - r * cpr;
-      const int iy = ty0 - 2 + r;
-      const bool ok = t < nxt && iy >= 0 && iy < H;
-      xv[s] = ldg16(ok ? (const void*)(x + ((size_t)n * H + iy) * W + 8 * c) : &kZeroC1);
-      const int w = tid + 256 * s;
-      const bool wok = w < nwin;
-      const int hp = w / Wp, wp = w - hp * Wp;
-      const size_t pix0 = ((size_t)n * H + ty0 + 2 * hp) * W + 2 * wp;
-      const size_t po[4] = {pix0, pix0 + 1, pix0 + W, pix0 + W + 1};
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        yv4[s][k] = ldg16(wok ? (const void*)(y + po[k] * COUT) : &kZeroC1);
-      gv[s] = ldg16(wok ? (const void*)(gz + (((size_t)n * Hp + (ty0 >> 1) + hp) * Wp + wp) * COUT)
-                        : &kZeroC1);
+      const bool ok = (unsigned)(ty0 - 2 + xr[s]) < (unsigned)H;
+      xv[s] = ldg16(ok ? (const void*)(xb + xoff[s]) : &kZeroC1);
+      const bf16* p = yb + yoff[s];
+      yv4[s][0] = ldg16(p);
+      yv4[s][1] = ldg16(p + COUT);
+      yv4[s][2] = ldg16(p + W * COUT);
+      yv4[s][3] = ldg16(p + (W + 1) * COUT);
+      gv[s] = ldg16(gb + goff[s]);
     }
     float sc[COUT], sf[COUT], k1[COUT], kx[COUT], k0[COUT];
 #pragma unroll
@@ -298,6 +311,11 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
       const int w = tid + 256 * s;
       if (w >= nwin) continue;
       const int hp = w / Wp, wp = w - hp * Wp;
+#if C1B_DIAG & 1   // diagnostic: no window math (y copied as dy)
+      for (int k = 0; k < 4; ++k)
+        *reinterpret_cast<u4*>(&dys[((2 * hp + (k >> 1)) * WMAX + dys_px(2 * hp + (k >> 1), 2 * wp + (k & 1), segs)) * COUT]) = yv4[s][k] ^ gv[s];
+      continue;
+#endif
       float yv[4][COUT];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -320,17 +338,19 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
       float dv[4][COUT];
 #pragma unroll
       for (int e = 0; e < COUT; ++e) {
-        float best = fmaxf(fmaf(yv[0][e], sc[e], sf[e]), 0.f);
-        int a = 0;
+        // first max of relu(y*scale + shift) over the window (max-pool's tie rule) as lane
+        // masks: the first k whose value equals the maximum
+        float rv[4];
 #pragma unroll
-        for (int k = 1; k < 4; ++k) {
-          const float r = fmaxf(fmaf(yv[k][e], sc[e], sf[e]), 0.f);
-          if (r > best) { best = r; a = k; }
-        }
-        const float dz = best > 0.f ? gg[e] : 0.f;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          dv[k][e] = fmaf(k1[e], a == k ? dz : 0.f, fmaf(kx[e], yv[k][e], k0[e]));
+        for (int k = 0; k < 4; ++k) rv[k] = fmaxf(fmaf(yv[k][e], sc[e], sf[e]), 0.f);
+        const float m = fmaxf(fmaxf(rv[0], rv[1]), fmaxf(rv[2], rv[3]));
+        const bool e0 = rv[0] == m, e1 = !e0 && rv[1] == m, e2 = !e0 && !e1 && rv[2] == m;
+        const bool e3 = !e0 && !e1 && !e2;
+        const float dz = m > 0.f ? gg[e] : 0.f;
+        dv[0][e] = fmaf(k1[e], e0 ? dz : 0.f, fmaf(kx[e], yv[0][e], k0[e]));
+        dv[1][e] = fmaf(k1[e], e1 ? dz : 0.f, fmaf(kx[e], yv[1][e], k0[e]));
+        dv[2][e] = fmaf(k1[e], e2 ? dz : 0.f, fmaf(kx[e], yv[2][e], k0[e]));
+        dv[3][e] = fmaf(k1[e], e3 ? dz : 0.f, fmaf(kx[e], yv[3][e], k0[e]));
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -341,27 +361,46 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
       }
     }
     __syncthreads();
-    // ---- MFMA over the tile's pixel pairs: k-block = (row r, 8-pair segment s)
-    const int nkb = TH * segs;
-    for (int ks = wave; 4 * ks < nkb; ks += 4) {
-      const int kb = 4 * ks + gq;
-      const int r = kb / segs, P0 = 8 * (kb - r * segs);
-      // A: rows P0 + 4*half + q, columns 4p .. 4p+3 of the pair rows (32 B each)
-      const int q = col >> 2, pp = col & 3;
-      // (the segment's two 128-byte halves swapped when kb is odd, see dys_px)
-      const int hsw = (kb & 1) << 3;
-      s4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (lds_s4*)&dys[(r * WMAX + 2 * P0 + ((2 * q) ^ hsw)) * COUT + 4 * pp]);
-      s4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (lds_s4*)&dys[(r * WMAX + 2 * P0 + ((8 + 2 * q) ^ hsw)) * COUT + 4 * pp]);
+    // ---- MFMA over the tile's pixel pairs: k-block kb = (row r, 8-pair segment sg); wave w
+    // takes kb = 4 ks + gq for ks = w, w + 4, ... (kb advances by 16: its parity, i.e. the
+    // dys half swap, is fixed per lane).  The next k-block's operands are read before the
+    // current MFMAs issue.
+    const int nkb = (C1B_DIAG & 2) ? 0 : TH * segs;   // diagnostic 2: no MFMA
+    if (4 * wave < nkb) {
       typedef __attribute__((ext_vector_type(8))) short s8;
-      const s8 av = s8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-      const bf16x8 A = __builtin_bit_cast(bf16x8, av);
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        const u4 bw = *reinterpret_cast<const u4*>(&xc[xbo(bb[tt], ba[tt], r + bky[tt], P0)]);
-        acc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, __builtin_bit_cast(bf16x8, bw), acc[tt],
-                                                         0, 0, 0);
+      const int q = col >> 2, pp = col & 3;
+      const int kb0 = 4 * wave + gq;
+      int r = kb0 / segs, sg = kb0 - r * segs;
+      const int hsw = (kb0 & 1) << 3;
+      // A: rows P0 + 4*half + q, columns 4p .. 4p+3 of the pair rows (32 B each)
+      const int aoff0 = ((2 * q) ^ hsw) * COUT + 4 * pp, aoff1 = ((8 + 2 * q) ^ hsw) * COUT + 4 * pp;
+      const int boff0 = xbo(bb[0], ba[0], bky[0], 0), boff1 = xbo(bb[1], ba[1], bky[1], 0);
+      const int dr = 16 / segs, dsg = 16 - dr * segs;
+      s4 h0, h1;
+      u4 w0, w1;
+      auto load = [&](s4& a0, s4& a1, u4& c0, u4& c1) {
+        const int P0 = 8 * sg, ab = (r * WMAX + 2 * P0) * COUT, bs = r * XB_RS + P0;
+        a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)&dys[ab + aoff0]);
+        a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)&dys[ab + aoff1]);
+        c0 = *reinterpret_cast<const u4*>(&xc[bs + boff0]);
+        c1 = *reinterpret_cast<const u4*>(&xc[bs + boff1]);
+      };
+      load(h0, h1, w0, w1);
+      for (int ks = wave;; ks += 4) {
+        const bool more = 4 * (ks + 4) < nkb;
+        s4 n0, n1;
+        u4 v0, v1;
+        if (more) {            // past the end: re-read the current block (stays in LDS bounds)
+          sg += dsg;
+          r += dr;
+          if (sg >= segs) { sg -= segs; ++r; }
+        }
+        load(n0, n1, v0, v1);  // unconditional: straight-line code keeps the wait partial
+        const bf16x8 A = __builtin_bit_cast(bf16x8, s8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]});
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, __builtin_bit_cast(bf16x8, w0), acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, __builtin_bit_cast(bf16x8, w1), acc[1], 0, 0, 0);
+        if (!more) break;
+        h0 = n0; h1 = n1; w0 = v0; w1 = v1;
       }
     }
   }
