@@ -535,21 +535,45 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
   const int t_begin = WG ? (int)blockIdx.x : (int)blockIdx.x * tps;
   const int t_end = WG ? ntiles : t_begin + tps;
   const int t_step = WG ? (int)gridDim.x : 1;
+  // input rows of a tile: <= 2 16-byte vectors per thread (W <= WMAX), register-prefetched one
+  // tile ahead (issued before the current tile's MFMAs and epilogue)
+  const int nxt = (TH + 4) * cpr;
+  int xr[2], xoff[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int t = tid + 256 * s;
+    const int r = t / cpr, c = t - r * cpr;
+    xr[s] = t < nxt ? r : -(1 << 20);
+    xoff[s] = (r - 2) * W + 8 * c;
+  }
+  u4 xv[2];
+  auto load_x = [&](int tl) {
+    const int n = tl / tps, ty0 = (tl - n * tps) * TH;
+    const bf16* xb = x + ((size_t)n * H + ty0) * W;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bool ok = (unsigned)(ty0 - 2 + xr[s]) < (unsigned)H;
+      xv[s] = ldg16(ok ? (const void*)(xb + xoff[s]) : &kZeroC1);
+    }
+  };
+  if (t_begin < t_end) load_x(t_begin);
   for (int tile = t_begin; tile < t_end; tile += t_step) {
     const int n = tile / tps, ty0 = (tile - n * tps) * TH, grp = n / B;
     __syncthreads();
     // ---- input tile (natural layout, zero pads)
-    for (int t = tid; t < (TH + 4) * cpr; t += 256) {
-      const int r = t / cpr, c = t - r * cpr;
-      const int iy = ty0 - 2 + r;
-      const bool ok = iy >= 0 && iy < H;
-      const u4 v = *reinterpret_cast<const u4*>(x + ((size_t)n * H + (ok ? iy : 0)) * W + 8 * c);
-      *reinterpret_cast<u4*>(xs + r * ITW + XOFF + 8 * c) = ok ? v : u4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int t = tid + 256 * s;
+      if (t < nxt) {
+        const int r = t / cpr, c = t - r * cpr;
+        *reinterpret_cast<u4*>(xs + r * ITW + XOFF + 8 * c) = xv[s];
+      }
     }
     for (int t = tid; t < (TH + 4) * 2; t += 256) {
       const int r = t >> 1, side = t & 1;
       *reinterpret_cast<u4*>(xs + r * ITW + (side ? XOFF + W : 0)) = u4{0u, 0u, 0u, 0u};
     }
+    if (tile + t_step < t_end) load_x(tile + t_step);
     __syncthreads();
     // ---- recompute y (rounded to bf16 exactly as the stored-y path)
     const unsigned* xd = reinterpret_cast<const unsigned*>(xs);
