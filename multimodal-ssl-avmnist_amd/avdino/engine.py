@@ -486,13 +486,51 @@ class MultiCentralEngine:
         # student: all views (+ originals) in one pass per conv layer
         cat, senc = self._encoder_fwd("student", self.img, self.aud, x_img, x_aud, N, NG, "s",
                                       need_dgrad=training)
+        loss_parts = ws.get("loss_parts", V * B + B)
+        head_out = None
+        hctx = None
+        h_done = None
+        n_parts = V * B
+        if with_orig:
+            # the originals' heads and their loss depend only on the cat rows [V*B, N): on the
+            # side stream (its own scratch), concurrently with fusion, projection and DINO loss.
+            # InfoNCE stays on this stream (its collectives keep one order per rank).
+            def heads():
+                hws = self.iws if self.mode != "infonce" else ws
+                hi, ha = self.heads
+                no = hi.o
+                zi = hws.get("zi", B * no)
+                za = hws.get("za", B * no)
+                off = V * B * 2 * E
+                ci = hi.forward(hws, st, "hi", cat, B, zi, 0.0, 0, x_ld=2 * E, x_off=off)
+                ca = ha.forward(hws, st, "ha", cat, B, za, 0.0, 0, x_ld=2 * E, x_off=off + E)
+                dzi = hws.get("dzi", B * no)
+                dza = hws.get("dza", B * no)
+                aux = loss_parts[V * B:V * B + B]
+                if self.mode == "mse":
+                    ops.mse_loss(zi, za, B, no, aux, dzi, dza)
+                    # mse parts are already divided by B*P; loss = sum
+                elif self.mode == "infonce":
+                    self._infonce(zi, za, B, no, aux, dzi, dza)
+                else:
+                    self._supervised(zi, za, batch["label"], B, no, aux, dzi, dza, hws)
+                if hp.alpha != 1.0:
+                    aux.mul_(hp.alpha)
+                    dzi.mul_(hp.alpha)
+                    dza.mul_(hp.alpha)
+                return (zi, za), (ci, ca, dzi, dza)
+
+            if self.mode == "infonce":
+                head_out, hctx = heads()
+            else:
+                (head_out, hctx), h_done = self._on_side(heads)
+            n_parts = V * B + B
         fout, sfus = self._fusion_fwd("student", cat, V * B, "s", base + 1)
         s_proj = ws.get("s_proj", V * B * P)
         spc = self.sproj.forward(ws, st, "sp", fout, V * B, s_proj, hp.dropout, base + 3)
         self._join(t_done)
 
         # DINO loss (+ centring and centre EMA) -- forward and d/ds in one pass
-        loss_parts = ws.get("loss_parts", V * B + B)
         ds = ws.get("ds", V * B * P)
         center_new = ws.get("center_new", P)
         work = ws.get("dino_work", (B + G * B) * P)
@@ -500,34 +538,7 @@ class MultiCentralEngine:
         ops.dino_loss(s_proj, t_proj, center, V, G, B, P, hp.tau_s, hp.tau_t, hp.center_momentum,
                       False, loss_parts[:V * B], ds, center_new, work)
         t_out = ws.get("t_out", G * B * P)  # centred teacher output (API only; the loss used t_raw)
-        head_out = None
-        hctx = None
-        n_parts = V * B
-        if with_orig:
-            hi, ha = self.heads
-            no = hi.o
-            zi = ws.get("zi", B * no)
-            za = ws.get("za", B * no)
-            off = V * B * 2 * E
-            ci = hi.forward(ws, st, "hi", cat, B, zi, 0.0, 0, x_ld=2 * E, x_off=off)
-            ca = ha.forward(ws, st, "ha", cat, B, za, 0.0, 0, x_ld=2 * E, x_off=off + E)
-            dzi = ws.get("dzi", B * no)
-            dza = ws.get("dza", B * no)
-            aux = loss_parts[V * B:V * B + B]
-            if self.mode == "mse":
-                ops.mse_loss(zi, za, B, no, aux, dzi, dza)
-                # mse parts are already divided by B*P; loss = sum
-            elif self.mode == "infonce":
-                self._infonce(zi, za, B, no, aux, dzi, dza)
-            else:
-                self._supervised(zi, za, batch["label"], B, no, aux, dzi, dza)
-            if hp.alpha != 1.0:
-                aux.mul_(hp.alpha)
-                dzi.mul_(hp.alpha)
-                dza.mul_(hp.alpha)
-            n_parts = V * B + B
-            head_out = (zi, za)
-            hctx = (ci, ca, dzi, dza)
+        self._join(h_done)
         loss = ws.get("loss", 1)
         ops.sum_to(loss_parts, n_parts, 1.0, loss)
         self.last = dict(B=B, G=G, L=L, V=V, NG=NG, N=N, cat=cat, senc=senc, sfus=sfus, spc=spc,
@@ -545,9 +556,9 @@ class MultiCentralEngine:
         ops.sum_to(parts, 2 * B, scale, aux[:1])
         aux[1:].zero_()
 
-    def _supervised(self, zi, za, labels, B, C, aux, dzi, dza):
+    def _supervised(self, zi, za, labels, B, C, aux, dzi, dza, ws=None):
         """supervised_loss (dino.py:1001-1025): CE(image) + CE(audio), mean over the batch."""
-        ws = self.ws
+        ws = ws or self.ws
         parts = ws.get("sup.parts", 2 * B)
         ops.softmax_xent(zi, C, B, C, labels, 0, False, False, 1.0 / B, parts[:B], dzi, C, False)
         ops.softmax_xent(za, C, B, C, labels, 0, False, False, 1.0 / B, parts[B:], dza, C, False)
@@ -563,6 +574,19 @@ class MultiCentralEngine:
         B, V, N = c["B"], c["V"], c["N"]
         # d cat buffer [N, 2E]: rows [0, V*B) from the fusion, rows [V*B, N) from the heads
         dcat = ws.get("dcat", N * 2 * E)
+        h_done = None
+        if c["hctx"] is not None:
+            # the heads' backward (disjoint dcat rows and parameters) on the side stream,
+            # concurrently with the projection / fusion backward
+            def heads_bwd():
+                ci, ca, dzi, dza = c["hctx"]
+                hi, ha = self.heads
+                off = V * B * 2 * E
+                hws = self.iws
+                hi.backward(hws, st, ci, dzi, dcat, dx_ld=2 * E, dx_off=off)
+                ha.backward(hws, st, ca, dza, dcat, dx_ld=2 * E, dx_off=off + E)
+
+            _, h_done = self._on_side(heads_bwd)
         dfout = ws.get("dfout", V * B * D)
         self.sproj.backward(ws, st, c["spc"], c["ds"], dfout)
         h, r = c["sfus"]
@@ -575,12 +599,7 @@ class MultiCentralEngine:
         ops.linear_bwd(dh, c["cat"], st["student.fusion.0.weight"], st.grad_of("student.fusion.0.weight"),
                        st.grad_of("student.fusion.0.bias"), dcat, V * B, x_ld=2 * E, dx_ld=2 * E,
                        mode=self.gm)
-        if c["hctx"] is not None:
-            ci, ca, dzi, dza = c["hctx"]
-            hi, ha = self.heads
-            off = V * B * 2 * E
-            hi.backward(ws, st, ci, dzi, dcat, dx_ld=2 * E, dx_off=off)
-            ha.backward(ws, st, ca, dza, dcat, dx_ld=2 * E, dx_off=off + E)
+        self._join(h_done)
         fi, cimg, fa, caud = c["senc"]
 
         def image_branch():      # independent of the audio branch: side stream

@@ -832,11 +832,12 @@ int avd_sum_rows(const float* in, int rows, int cols, long long ld, float* out, 
   return AVD_OK;
 }
 
-// Row chunks for avd_sum_rows_split: enough blocks to cover the chip (>= 1024) with >= 4 row
-// phases of work per thread; 1 = no split.  A function of the shape only, so the summation
+// Row chunks for avd_sum_rows_split (inputs of >= 2^20 elements): enough blocks to cover the
+// chip (>= 1024) with >= 4 row phases of work per thread; 1 = no split.  A function of the shape only, so the summation
 // order (and the result) is the same on every device.
 int avd_sum_rows_chunks(int rows, int cols) {
-  if (rows <= 0 || cols <= 0) return 1;
+  // small inputs: one launch (a second one costs more than the single pass takes)
+  if (rows <= 0 || cols <= 0 || (long long)rows * cols < (1ll << 20)) return 1;
   const int cw = cols <= 2048 ? 16 : 64, ph = 1024 / cw;
   const int cb = avd_cdiv(cols, cw);
   const int want = avd_cdiv(1024, cb), most = rows / (4 * ph);

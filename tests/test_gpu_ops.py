@@ -511,7 +511,7 @@ def test_stage_views(ops):
     assert np.array_equal(host(out), ref)
 
 
-@pytest.mark.parametrize("rows,cols,ld,off", [(7168, 256, 512, 256), (512, 3200, 3200, 0),
+@pytest.mark.parametrize("rows,cols,ld,off", [(7168, 256, 512, 256), (512, 3200, 3200, 0), (64, 320, 320, 0),
                                               (256, 51200, 51200, 0), (7, 5, 9, 3), (6144, 512, 512, 0)])
 def test_sum_rows_split_matches_f64(ops, rows, cols, ld, off):
     """avd_sum_rows_split (row chunks in parallel, chunk partials summed in fixed order) against
