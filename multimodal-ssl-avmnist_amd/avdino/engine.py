@@ -396,6 +396,11 @@ class MultiCentralEngine:
         self.step_idx = 0
         self.last = {}
 
+    # student image branch on the side stream, concurrently with the audio branch: measured
+    # slower (r1_39: 149.7k vs 152.4k pairs/s -- both branches' launches fill the chip, so
+    # they only contend), kept for experiments
+    IMAGE_SIDE = os.environ.get("AVDINO_IMAGE_SIDE", "0") == "1"
+
     # -------------------------------------------------------------- streams
     def _on_side(self, fn):
         """Run fn() on the side stream after everything queued so far on the current stream;
@@ -419,13 +424,27 @@ class MultiCentralEngine:
                      ws=None):
         """Image + audio conv stacks and their Linear(., E) into one [N, 2E] buffer (= the cat)."""
         ws, st, E = ws or self.ws, self.store, self.E
-        fi, ci = ib.forward(ws, st, tag + ".img", x_img, N, G, update_running, need_dgrad)
-        fa, ca = ab.forward(ws, st, tag + ".aud", x_aud, N, G, update_running, need_dgrad)
         cat = ws.get(tag + ".cat", N * 2 * E)
-        ops.linear_fwd(fi, st[prefix + ".image_encoder.1.weight"], st[prefix + ".image_encoder.1.bias"],
-                       cat, N, out_ld=2 * E, out_off=0, mode=self.gm)
+
+        def image():
+            iws = self.iws if side_image else ws
+            fi, ci = ib.forward(iws, st, tag + ".img", x_img, N, G, update_running, need_dgrad)
+            ops.linear_fwd(fi, st[prefix + ".image_encoder.1.weight"],
+                           st[prefix + ".image_encoder.1.bias"], cat, N, out_ld=2 * E, out_off=0,
+                           mode=self.gm)
+            return fi, ci
+
+        # the student's image branch (cat columns [0, E)) on the side stream, concurrently with
+        # its audio branch (columns [E, 2E)); the teacher runs there already, so never for it
+        side_image = self.IMAGE_SIDE and prefix == "student" and self.side is not None
+        if side_image:
+            (fi, ci), i_done = self._on_side(image)
+        else:
+            (fi, ci), i_done = image(), None
+        fa, ca = ab.forward(ws, st, tag + ".aud", x_aud, N, G, update_running, need_dgrad)
         ops.linear_fwd(fa, st[prefix + ".audio_encoder.1.weight"], st[prefix + ".audio_encoder.1.bias"],
                        cat, N, out_ld=2 * E, out_off=E, mode=self.gm)
+        self._join(i_done)
         return cat, (fi, ci, fa, ca)
 
     def _fusion_fwd(self, prefix, cat, rows, tag, seed, ws=None):
