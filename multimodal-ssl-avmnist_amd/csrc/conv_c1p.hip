@@ -42,6 +42,8 @@ __device__ __forceinline__ int boff(int h, int d) {
   return R[h][d] * ITWD + D[h][d];
 }
 
+__device__ const u4 kZeroF = {0u, 0u, 0u, 0u};
+
 __global__ __launch_bounds__(256) void conv_c1p8_kernel(const bf16* __restrict__ x,
                                                         const bf16* __restrict__ wk,
                                                         const float* __restrict__ bias,
@@ -78,21 +80,44 @@ __global__ __launch_bounds__(256) void conv_c1p8_kernel(const bf16* __restrict__
   for (int d = 0; d < 4; ++d) off[d] = boff(h, d) + rp * ITWD + q + 3;   // + (x0 - 2 + XOFF)/2
   float ss[4] = {0.f, 0.f, 0.f, 0.f}, sq[4] = {0.f, 0.f, 0.f, 0.f};
   const int mts = W >> 4, cpr = W >> 3;
+  // input rows: <= 2 16-byte vectors per thread (W <= 128), register-prefetched one tile ahead
+  // so their latency hides under the current tile's MFMAs and stores
+  const int nxt = (TH + 4) * cpr;
+  int xr[2], xoff[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int t = tid + 256 * s;
+    const int r = t / cpr, c = t - r * cpr;
+    xr[s] = t < nxt ? r : -(1 << 20);
+    xoff[s] = (r - 2) * W + 8 * c;
+  }
+  u4 xv[2];
+  auto load_x = [&](int ty0) {
+    const bf16* xb = x + ((size_t)n * H + ty0) * W;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bool ok = (unsigned)(ty0 - 2 + xr[s]) < (unsigned)H;
+      xv[s] = ldg16(ok ? (const void*)(xb + xoff[s]) : &kZeroF);
+    }
+  };
+  load_x(0);
   for (int tile = 0; tile < tps; ++tile) {
     const int ty0 = tile * TH;
     if (tile) __syncthreads();
     // ---- stage rows ty0-2 .. ty0+TH+1 (zero outside the image); pad columns zeroed
-    for (int t = tid; t < (TH + 4) * cpr; t += 256) {
-      const int r = t / cpr, c = t - r * cpr;
-      const int iy = ty0 - 2 + r;
-      const bool ok = iy >= 0 && iy < H;
-      const u4 v = *reinterpret_cast<const u4*>(x + ((size_t)n * H + (ok ? iy : 0)) * W + 8 * c);
-      *reinterpret_cast<u4*>(xs + r * ITW + XOFF + 8 * c) = ok ? v : u4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int t = tid + 256 * s;
+      if (t < nxt) {
+        const int r = t / cpr, c = t - r * cpr;
+        *reinterpret_cast<u4*>(xs + r * ITW + XOFF + 8 * c) = xv[s];
+      }
     }
     if (tid < (TH + 4) * 2) {
       const int r = tid >> 1, side = tid & 1;
       *reinterpret_cast<u4*>(xs + r * ITW + (side ? XOFF + W : 0)) = u4{0u, 0u, 0u, 0u};
     }
+    if (tile + 1 < tps) load_x(ty0 + TH);
     __syncthreads();
     for (int s = wave; s < TH / 2; s += 4) {      // 2-row strips
       const int oy = ty0 + 2 * s + rp;
