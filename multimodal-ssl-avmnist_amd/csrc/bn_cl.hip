@@ -270,7 +270,33 @@ __global__ __launch_bounds__(256) void bwd_reduce_pooled_cl_kernel(
   }
   load_coef<V>(mean, g * C + c0, mu);
   load_coef<V>(invstd, g * C + c0, is);
-  if (slot < slots) {
+  if (slot < slots && mode == 0 && !any0) {
+    // NHWC pooled maps: window wi of group g sits at ((g*B*Hp*Wp + wi) * C + c0) -- no index
+    // division; 4 windows' loads in flight per thread, summed in the same order as below
+    const size_t gbase = (size_t)g * B * Hp * Wp;
+    const T* gp = reinterpret_cast<const T*>(gout) + c0;
+    const T* pp = reinterpret_cast<const T*>(pooled) + c0;
+    for (long long wi = w0 + slot; wi < w1; wi += 4ll * slots) {
+      float gg[4][V], pv[4][V];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const long long wk = wi + (long long)k * slots;
+        const size_t off = (gbase + (size_t)(wk < w1 ? wk : wi)) * C;
+        Vec<T>::ld(gp + off, gg[k]);
+        Vec<T>::ld(pp + off, pv[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (wi + (long long)k * slots >= w1) break;
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          const float dz = pv[k][e] > 0.f ? gg[k][e] : 0.f;
+          s1[e] += dz;
+          s2[e] += dz * ((pv[k][e] - be[e]) * ig[e]);
+        }
+      }
+    }
+  } else if (slot < slots) {
     for (long long wi = w0 + slot; wi < w1; wi += slots) {
       const int wp = (int)(wi % Wp), hp = (int)((wi / Wp) % Hp);
       const int n = g * B + (int)(wi / ((long long)Wp * Hp));
