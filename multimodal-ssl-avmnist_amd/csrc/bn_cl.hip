@@ -97,14 +97,17 @@ __device__ __forceinline__ void load_coef(const float* __restrict__ a, int idx, 
 template <typename T>
 __global__ __launch_bounds__(256) void relu_pool_cl_kernel(
     const T* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
-    void* __restrict__ out, int mode, long long total, int B, int C, int H, int W) {
+    void* __restrict__ out, int mode, long long total, int B, int C, int H, int W, U32Div dcv,
+    U32Div dwp, U32Div dhp) {
   constexpr int V = Vec<T>::V;
   const int Hp = H / 2, Wp = W / 2, CV = C / V;
+  // total < 2^32 (host-checked): 32-bit index decomposition by exact reciprocal multiplies
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int cv = (int)(i % CV);
-    const long long pw = i / CV;                      // pooled pixel index
-    const int wp = (int)(pw % Wp), hp = (int)((pw / Wp) % Hp);
-    const int n = (int)(pw / ((long long)Wp * Hp));
+    const unsigned pw = dcv.div((unsigned)i);         // pooled pixel index
+    const int cv = (int)((unsigned)i - pw * CV);
+    const unsigned ph = dwp.div(pw);
+    const int wp = (int)(pw - ph * Wp);
+    const int n = (int)dhp.div(ph), hp = (int)(ph - (unsigned)n * Hp);
     const int g = n / B, c0 = cv * V;
     float sc[V], sf[V];
     load_coef<V>(scale, g * C + c0, sc);
@@ -335,15 +338,17 @@ __global__ __launch_bounds__(256) void bwd_apply_cl_kernel(
     const T* __restrict__ y, const void* __restrict__ gout, int mode,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ coef, T* __restrict__ dy, long long total, int B, int C, int H,
-    int W) {
+    int W, U32Div dcv, U32Div dwc, U32Div dhc) {
   constexpr int V = Vec<T>::V;
   const int Hp = H / 2, Wp = W / 2, CV = C / V;
   const int Hc = (H + 1) / 2, Wc = (W + 1) / 2;      // windows covering every pixel
+  // total < 2^32 (host-checked): 32-bit index decomposition by exact reciprocal multiplies
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int cv = (int)(i % CV);
-    const long long pw = i / CV;
-    const int wc = (int)(pw % Wc), hc = (int)((pw / Wc) % Hc);
-    const int n = (int)(pw / ((long long)Wc * Hc));
+    const unsigned pw = dcv.div((unsigned)i);
+    const int cv = (int)((unsigned)i - pw * CV);
+    const unsigned ph = dwc.div(pw);
+    const int wc = (int)(pw - ph * Wc);
+    const int n = (int)dhc.div(ph), hc = (int)(ph - (unsigned)n * Hc);
     const int g = n / B, c0 = cv * V;
     float sc[V], sf[V], k1[V], kx[V], k0[V];
     load_coef<V>(scale, g * C + c0, sc);
@@ -397,12 +402,16 @@ int avd_cl_bn_relu_pool_impl(const void* y, int dt, const float* scale, const fl
                                                                       (float*)out, total, B, C, H, W);
   } else if (mode == 0 || mode == 2) {
     const long long total = (long long)N * (H / 2) * (W / 2) * (C / V);
+    if (total >= (1ll << 32)) return AVD_ERR_SHAPE;
+    const U32Div dcv = U32Div::make(C / V), dwp = U32Div::make(W / 2), dhp = U32Div::make(H / 2);
     if (dt == AVD_BF16)
       relu_pool_cl_kernel<bf16><<<grid_for(total), 256, 0, st>>>((const bf16*)y, scale, shift, out,
-                                                                 mode, total, B, C, H, W);
+                                                                 mode, total, B, C, H, W, dcv, dwp,
+                                                                 dhp);
     else
       relu_pool_cl_kernel<float><<<grid_for(total), 256, 0, st>>>((const float*)y, scale, shift, out,
-                                                                  mode, total, B, C, H, W);
+                                                                  mode, total, B, C, H, W, dcv, dwp,
+                                                                  dhp);
   } else {
     return AVD_ERR_ARG;
   }
@@ -446,14 +455,17 @@ int avd_cl_bn_bwd_apply_impl(const void* y, int dt, const void* gout, int mode,
   const int V = dt == AVD_BF16 ? 8 : 4;
   if (C % V || N % B || mode < 0 || mode > 2) return AVD_ERR_SHAPE;
   const long long total = (long long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / V);
+  if (total >= (1ll << 32)) return AVD_ERR_SHAPE;
+  const U32Div dcv = U32Div::make(C / V), dwc = U32Div::make((W + 1) / 2),
+               dhc = U32Div::make((H + 1) / 2);
   if (dt == AVD_BF16)
     bwd_apply_cl_kernel<bf16><<<grid_for(total), 256, 0, st>>>((const bf16*)y, gout, mode, scale,
                                                                shift, coef, (bf16*)dy, total, B, C,
-                                                               H, W);
+                                                               H, W, dcv, dwc, dhc);
   else
     bwd_apply_cl_kernel<float><<<grid_for(total), 256, 0, st>>>((const float*)y, gout, mode, scale,
                                                                 shift, coef, (float*)dy, total, B,
-                                                                C, H, W);
+                                                                C, H, W, dcv, dwc, dhc);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
