@@ -47,6 +47,10 @@ class KernelTimer:
         self.fns = {}       # key -> last launch closure (tools/opbench.py replays them)
 
     def wrap(self, key, nbytes, flops, fn):
+        # launches of one op and shape from different streams are different call sites (e.g.
+        # the audio conv3 and image conv1 BN-backward apply share a shape): keyed apart
+        if torch.cuda.current_stream() != torch.cuda.default_stream():
+            key += " @side"
         if self.only is not None and key != self.only:
             return fn()
         if self.only is not None:
