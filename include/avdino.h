@@ -373,6 +373,40 @@ int avd_cosine_consistency(const float* emb, int V, int B, int D, float alpha, f
 int avd_stage_views(const float* g, int G, const float* l, int L, const float* orig, int B,
                     int HW, void* out, int odt, void* stream);
 
+/* ------------------------------------------------------------------ data path */
+
+/* Device-side view augmentation: replaces the per-sample CPU transform chains of
+ * MultiModalAugmentation.__call__ (utils/get_data.py:233-257; chains at 122-193).  One record
+ * of AVD_AUG_REC floats per (sample b, view v) holds the already-drawn random parameters (the
+ * host samples them, avdino/augment.py); the kernel applies, in the reference's order,
+ *   RandomResizedCrop (bilinear, edge-clamped; the crops only up-sample, so antialias is a
+ *   no-op) -> TimeWarpWithStretch (get_data.py:29-58: |phase_vocoder| = linear interpolation
+ *   of magnitudes at t*rate, zero beyond) -> Frequency/TimeMasking (zero bands) ->
+ *   RandomRotation -> RandomAffine (nearest, zero fill, torchvision's centred inverse matrix)
+ *   -> RandomErasing (zero box) -> GaussianNoise (get_data.py:21-27; counter-hash normals) ->
+ *   GroupedMasking (get_data.py:60-108; 4x4 groups, bitmask row gm[rec[AVD_AUG_GM]]).
+ * src_u8 [N, H*W] raw dataset pixels, idx [B] int64 rows of src (the batch's sample ids),
+ * lut [256] f32 = the dataset's normalisation of each byte value (get_data.py:464-467),
+ * rec [B*V, AVD_AUG_REC], gm [*, gm_words] u32.  out f32: order 0 -> [B, V, H, W] (the
+ * reference's collated views), order 1 -> [V, B, H, W] (view-major, the engine's layout). */
+#define AVD_AUG_REC 28
+enum {
+  AVD_AUG_CROP = 0,    /* 0..3: top, left, h, w of the crop box */
+  AVD_AUG_AFF = 4,     /* 4..9: RandomAffine inverse [m0 m1 m2; m3 m4 m5], centred coords */
+  AVD_AUG_ROT = 10,    /* 10..15: RandomRotation inverse, same form */
+  AVD_AUG_RATE = 16,   /* time-stretch rate */
+  AVD_AUG_FMASK = 17,  /* 17,18: rows [f0, f1) zeroed */
+  AVD_AUG_TMASK = 19,  /* 19,20: cols [t0, t1) zeroed */
+  AVD_AUG_NOISE = 21,  /* gaussian noise std (0: none) */
+  AVD_AUG_GM = 22,     /* grouped-mask bitmask row, < 0: none */
+  AVD_AUG_FLAGS = 23,  /* bit 0 crop, 1 affine, 2 rotation, 3 time stretch */
+  AVD_AUG_ERASE = 24   /* 24..27: top, left, h, w of the erased box (h = 0: none) */
+};
+int avd_augment_views(const uint8_t* src_u8, const int64_t* idx, long long n_src, int B, int V,
+                      int H, int W, const float* lut, const float* rec, const uint32_t* gm,
+                      int gm_words, int group, unsigned long long seed, int order, float* out,
+                      void* stream);
+
 /* ------------------------------------------------------------------ optimiser / EMA */
 
 /* teacher = m*teacher + (1-m)*student over n floats (MultiModalDINO.update_teacher,

@@ -76,6 +76,7 @@ PROTOS = {
     "avd_argmax_correct": [P, L, I, I, P, P, P],
     "avd_sum": [P, I, F, P, P],
     "avd_stage_views": [P, I, P, I, P, I, I, P, I, P],
+    "avd_augment_views": [P, P, L, I, I, I, I, P, P, P, I, I, U64, I, P, P],
 }
 
 

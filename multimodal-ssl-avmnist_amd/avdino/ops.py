@@ -567,3 +567,23 @@ def stage_views(g, G, l, L, orig, B, HW, out):
     _need(orig is None or orig.numel() == B * HW, "stage orig")
     _need(out.numel() == (G + L + (orig is not None)) * B * HW, "stage out")
     call("avd_stage_views", p(g), G, p(l), L, p(orig), B, HW, p(out), dtcode(out), stream())
+
+
+AUG_REC = 28  # floats per (sample, view) record, include/avdino.h AVD_AUG_REC
+
+
+def augment_views(src_u8, idx, lut, rec, gm, group, seed, V, H, W, out, order=0):
+    """Device view augmentation (avd_augment_views): src_u8 [N, H*W] u8, idx [B] int64, lut [256]
+    f32, rec [B*V, AUG_REC] f32, gm [R, words] int32/uint32 or None, out f32 [B,V,H,W] (order 0)
+    or [V,B,H,W] (order 1).  Sample ids and bitmask rows are range-checked by the caller on the
+    host arrays before upload (avdino.augment.ViewAugmenter)."""
+    B = idx.numel()
+    _need(src_u8.dtype == torch.uint8 and src_u8.dim() == 2 and src_u8.shape[1] == H * W, "aug src")
+    _need(idx.dtype == torch.int64 and lut.numel() == 256 and lut.dtype == torch.float32, "aug idx/lut")
+    _need(rec.dtype == torch.float32 and rec.shape == (B * V, AUG_REC), "aug records")
+    _need(out.dtype == torch.float32 and out.numel() == B * V * H * W, "aug out")
+    for t in (src_u8, idx, lut, rec, out) + ((gm,) if gm is not None else ()):
+        _need(t.is_contiguous() and t.device == out.device, "aug operands contiguous, one device")
+    words = gm.shape[1] if gm is not None else 0
+    call("avd_augment_views", p(src_u8), p(idx), src_u8.shape[0], B, V, H, W, p(lut), p(rec),
+         p(gm), words, group, seed & (2**64 - 1), order, p(out), stream())

@@ -1,0 +1,188 @@
+// Device-side view augmentation: the per-sample CPU transform chains of
+// MultiModalAugmentation (AVMNIST_Experiments/utils/get_data.py:110-257) as one gather kernel.
+//
+// The host draws every random parameter (avdino/augment.py follows torchvision's / torchaudio's
+// get_params rules) into one record per (sample, view); the device does the pixel work.  One
+// block builds one output view: the sample's source row (H*W bytes) is gathered by its dataset
+// index, normalised through the dataset's byte->f32 table and staged in LDS once, then every
+// output pixel walks the chain backwards (output -> affine -> rotation -> masks -> time stretch
+// -> crop -> source) with the reference's interpolation at each stage.  HBM traffic per view is
+// H*W source bytes + 4*H*W output bytes; the kernel is write-bound.
+//
+// Floating-point contraction is off so the coordinate and interpolation arithmetic rounds the
+// way the numpy restatement in oracle/augment.py does (bit-identical outside the noise term).
+#include "common.h"
+
+using namespace avd;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxHW = 112 * 112;
+
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebull;
+  x ^= x >> 31;
+  return x;
+}
+
+// Standard normal from (seed, record, pixel): Box-Muller over a 64-bit counter hash.
+__device__ __forceinline__ float gauss(unsigned long long seed, unsigned rec, unsigned pix) {
+#pragma clang fp contract(off)
+  const unsigned long long r = mix64(seed ^ mix64(((unsigned long long)rec << 32) | pix));
+  const float u1 = (float)((r >> 40) + 1ull) * 5.9604644775390625e-8f;  // (0, 1]
+  const float u2 = (float)((r >> 16) & 0xFFFFFFull) * 5.9604644775390625e-8f;
+  return sqrtf(-2.0f * logf(u1)) * cosf(6.2831855f * u2);
+}
+
+// Nearest-neighbour inverse map of a torchvision affine / rotation (grid_sample, zero padding,
+// align_corners=False): src = M (p - c) + t + c, c = ((W-1)/2, (H-1)/2), rounded half-to-even.
+__device__ __forceinline__ bool affine_nearest(const float* m, float cx, float cy, int W, int H,
+                                               int& x, int& y) {
+#pragma clang fp contract(off)
+  const float dx = (float)x - cx, dy = (float)y - cy;
+  const float sx = ((m[0] * dx + m[1] * dy) + m[2]) + cx;
+  const float sy = ((m[3] * dx + m[4] * dy) + m[5]) + cy;
+  const float rx = rintf(sx), ry = rintf(sy);
+  if (!(rx >= 0.0f && rx <= (float)(W - 1) && ry >= 0.0f && ry <= (float)(H - 1))) return false;
+  x = (int)rx;
+  y = (int)ry;
+  return true;
+}
+
+struct View {
+  const float* img;   // LDS, [H, W] normalised source
+  int H, W;
+  bool crop;
+  int top, left, ch, cw;
+  float sh, sw;       // ch / H, cw / W
+};
+
+// RandomResizedCrop output pixel (r, c): bilinear (align_corners=False, source index clamped
+// at 0 and at the crop's last row/column) inside the integer crop box.
+__device__ __forceinline__ float crop_sample(const View& v, int r, int c) {
+#pragma clang fp contract(off)
+  if (!v.crop) return v.img[r * v.W + c];
+  float sy = ((float)r + 0.5f) * v.sh - 0.5f;
+  float sx = ((float)c + 0.5f) * v.sw - 0.5f;
+  sy = sy < 0.0f ? 0.0f : sy;
+  sx = sx < 0.0f ? 0.0f : sx;
+  const int y0 = (int)sy, x0 = (int)sx;
+  const int y1 = y0 + 1 < v.ch ? y0 + 1 : v.ch - 1;
+  const int x1 = x0 + 1 < v.cw ? x0 + 1 : v.cw - 1;
+  const float ly = sy - (float)y0, lx = sx - (float)x0;
+  const float hy = 1.0f - ly, hx = 1.0f - lx;
+  const float* p0 = v.img + (v.top + y0) * v.W + v.left;
+  const float* p1 = v.img + (v.top + y1) * v.W + v.left;
+  return hy * (hx * p0[x0] + lx * p0[x1]) + ly * (hx * p1[x0] + lx * p1[x1]);
+}
+
+__global__ __launch_bounds__(kThreads) void augment_kernel(
+    const uint8_t* __restrict__ src, const int64_t* __restrict__ idx, int V, int B, int H, int W,
+    const float* __restrict__ lut, const float* __restrict__ recs, const uint32_t* __restrict__ gm,
+    int gm_words, int group, unsigned long long seed, int order, float* __restrict__ out) {
+#pragma clang fp contract(off)
+  __shared__ float s_img[kMaxHW];
+  __shared__ float s_lut[256];
+  const int rid = blockIdx.x;  // record = b * V + v
+  const int b = rid / V, v = rid - b * V;
+  const int HW = H * W;
+  const float* rec = recs + (size_t)rid * AVD_AUG_REC;
+
+  s_lut[threadIdx.x] = lut[threadIdx.x];
+  __syncthreads();
+  const uint32_t* row = reinterpret_cast<const uint32_t*>(src + (size_t)idx[b] * HW);
+  for (int i = threadIdx.x; i < HW / 4; i += kThreads) {
+    const uint32_t w4 = row[i];
+    s_img[4 * i + 0] = s_lut[w4 & 0xFF];
+    s_img[4 * i + 1] = s_lut[(w4 >> 8) & 0xFF];
+    s_img[4 * i + 2] = s_lut[(w4 >> 16) & 0xFF];
+    s_img[4 * i + 3] = s_lut[w4 >> 24];
+  }
+  __syncthreads();
+
+  const int flags = (int)rec[AVD_AUG_FLAGS];
+  View vw;
+  vw.img = s_img;
+  vw.H = H;
+  vw.W = W;
+  vw.crop = flags & 1;
+  vw.top = (int)rec[AVD_AUG_CROP + 0];
+  vw.left = (int)rec[AVD_AUG_CROP + 1];
+  vw.ch = (int)rec[AVD_AUG_CROP + 2];
+  vw.cw = (int)rec[AVD_AUG_CROP + 3];
+  vw.sh = (float)vw.ch / (float)H;
+  vw.sw = (float)vw.cw / (float)W;
+  const bool aff = flags & 2, rot = flags & 4, tw = flags & 8;
+  float maff[6], mrot[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    maff[k] = rec[AVD_AUG_AFF + k];
+    mrot[k] = rec[AVD_AUG_ROT + k];
+  }
+  const float rate = rec[AVD_AUG_RATE];
+  const int f0 = (int)rec[AVD_AUG_FMASK], f1 = (int)rec[AVD_AUG_FMASK + 1];
+  const int t0 = (int)rec[AVD_AUG_TMASK], t1 = (int)rec[AVD_AUG_TMASK + 1];
+  const float nstd = rec[AVD_AUG_NOISE];
+  const int gmrow = (int)rec[AVD_AUG_GM];
+  const int et = (int)rec[AVD_AUG_ERASE], el = (int)rec[AVD_AUG_ERASE + 1];
+  const int eh = (int)rec[AVD_AUG_ERASE + 2], ew = (int)rec[AVD_AUG_ERASE + 3];
+  const float cx = (float)(W - 1) * 0.5f, cy = (float)(H - 1) * 0.5f;
+  const uint32_t* gmr = (gm && gmrow >= 0) ? gm + (size_t)gmrow * gm_words : nullptr;
+  const int gw = group > 0 ? W / group : 1;
+  float* o = out + (order == 0 ? (size_t)rid : (size_t)v * B + b) * HW;
+
+  for (int p = threadIdx.x; p < HW; p += kThreads) {
+    const int y = p / W, x = p - y * W;
+    int qx = x, qy = y;
+    bool ok = true;
+    if (aff) ok = affine_nearest(maff, cx, cy, W, H, qx, qy);
+    if (ok && rot) ok = affine_nearest(mrot, cx, cy, W, H, qx, qy);
+    float val = 0.0f;
+    if (ok && !(qy >= f0 && qy < f1) && !(qx >= t0 && qx < t1)) {
+      if (tw) {
+        // |phase_vocoder(spec, rate)|[c] = a*|s[i0+1]| + (1-a)*|s[i0]|, t = c*rate, zero past
+        // the input's end (torchaudio pads two zero frames); ceil(W/rate) output frames.
+        const float t = (float)qx * rate;
+        if (t < (float)W) {
+          const int i0 = (int)t;
+          const float a = t - (float)i0;
+          const float s0 = fabsf(crop_sample(vw, qy, i0));
+          const float s1 = i0 + 1 < W ? fabsf(crop_sample(vw, qy, i0 + 1)) : 0.0f;
+          val = a * s1 + (1.0f - a) * s0;
+        }
+      } else {
+        val = crop_sample(vw, qy, qx);
+      }
+    }
+    if (eh > 0 && y >= et && y < et + eh && x >= el && x < el + ew) val = 0.0f;
+    if (nstd != 0.0f) val = val + gauss(seed, (unsigned)rid, (unsigned)p) * nstd;
+    if (gmr) {
+      const int g = (y / group) * gw + x / group;
+      if ((gmr[g >> 5] >> (g & 31)) & 1u) val = val * 0.0f;
+    }
+    o[p] = val;
+  }
+}
+
+}  // namespace
+
+extern "C" int avd_augment_views(const uint8_t* src_u8, const int64_t* idx, long long n_src, int B,
+                                 int V, int H, int W, const float* lut, const float* rec,
+                                 const uint32_t* gm, int gm_words, int group,
+                                 unsigned long long seed, int order, float* out, void* stream) {
+  if (!src_u8 || !idx || !lut || !rec || !out) return AVD_ERR_ARG;
+  if (B <= 0 || V <= 0 || H <= 0 || W <= 0 || n_src <= 0) return AVD_ERR_SHAPE;
+  if ((long long)H * W > kMaxHW || (H * W) % 4 || order < 0 || order > 1) return AVD_ERR_SHAPE;
+  if (gm && (group <= 0 || H % group || W % group ||
+             gm_words * 32 < (H / group) * (W / group)))
+    return AVD_ERR_SHAPE;
+  (void)n_src;  // sample ids are range-checked by the host wrapper (avdino.ops.augment_views)
+  augment_kernel<<<B * V, kThreads, 0, avd_stream(stream)>>>(src_u8, idx, V, B, H, W, lut, rec, gm,
+                                                             gm_words, group, seed, order, out);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
