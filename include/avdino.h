@@ -436,6 +436,26 @@ int avd_axpy(float* y, const float* x, long long n, float a, void* stream);
 /* out = sum(in[0..n)) in fixed order (loss reduction); out is one float. */
 int avd_sum(const float* in, int n, float scale, float* out, void* stream);
 
+/* ------------------------------------------------------------------ downstream evaluation
+ * (training_structures/dino_train.py:47-102, 349-369) */
+
+/* out[j] = sum_k x[j*D + k]^2 (the train-side term of the kNN distance). */
+int avd_row_sqnorm(const float* x, int N, int D, float* out, void* stream);
+
+/* kNN selection and vote (train_knn_classifier, dino_train.py:349-369: sklearn
+ * KNeighborsClassifier(n_neighbors=K), brute-force euclidean, uniform weights).  For test row
+ * i the distance to train row j ranks as xnorm[j] + S[i*ldS + j] where S = -2 Q X^T comes
+ * from avd_gemm (the test row's own norm is common to the row).  nbr [M, K] (may be NULL)
+ * receives the K nearest train indices in increasing distance (ties: smaller index); pred [M]
+ * the class with the most votes among labels[nbr] (ties: the smallest class, as sklearn's
+ * argmax over class counts).  K <= 16, C <= 64. */
+int avd_knn_select(const float* S, long long ldS, const float* xnorm, int M, int N, int K,
+                   const int64_t* labels, int C, int64_t* nbr, int64_t* pred, void* stream);
+
+/* idx[r] = argmax_j logits[r*ld + j], first maximum (torch.max(outputs, 1) in
+ * compute_classification_metrics, dino_train.py:76). */
+int avd_argmax_rows(const float* logits, long long ld, int R, int C, int64_t* idx, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -312,3 +312,24 @@ class MultiModalAugmentation:
         li = self.image(idx, self.local_transforms["image"], L) if L else None
         la = self.audio(idx, self.local_transforms["audio"], L) if L else None
         return gi, ga, li, la
+
+
+def process_augment_config(config, trial=None, is_hyperparameter_search=False):
+    """process_augment_config's final-training branch (hyperparameter_tuning/
+    objective_augment.py:68-96): the config's ``best_augments`` split into
+    {"augmentations": kwargs without p, "augmentation_probabilities": p} per view setting.
+    The Optuna search branch is out of scope."""
+    if is_hyperparameter_search:
+        raise NotImplementedError("Optuna augmentation search is outside the MI355X hot path")
+    if "best_augments" not in config:
+        raise ValueError("best_augments not found in config for final training")
+    augmentations = {"global_views": {}, "local_views": {}}
+    probabilities = {"global_views": {}, "local_views": {}}
+    for view in ("global_views", "local_views"):
+        for aug, params in config["best_augments"][view].items():
+            kw = {k: v for k, v in params.items() if k != "p"}
+            if kw:
+                augmentations[view][aug] = kw
+            if "p" in params:
+                probabilities[view][aug] = params["p"]
+    return {"augmentations": augmentations, "augmentation_probabilities": probabilities}

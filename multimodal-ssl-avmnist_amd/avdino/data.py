@@ -131,16 +131,19 @@ class AVMNISTDinoLoader:
         n = len(arrays)
         self.seed = seed
         gen = torch.Generator().manual_seed(seed)
-        if split == "train" and train_size + val_size == n:
+        if split == "train":   # random_split raises on a size mismatch (get_data.py:606-609)
             self.train_idx, self.val_idx = random_split_indices(n, [train_size, val_size], gen)
         else:
             self.train_idx, self.val_idx = np.arange(n), np.arange(0)
         self.batch_size, self.shuffle, self.rank, self.world = batch_size, shuffle, rank, world
         self.mode = multimodal_mode
         self.aug = augmentations or MultiModalAugmentation(n_global_views, n_local_views)
-        self.aug.bind(ViewAugmenter(self.dev["image"], self.dev["lut_image"], *IMG_HW, seed=seed),
+        # augmentation streams differ per rank (each rank's worker RNGs do in the reference);
+        # the shuffle order (seed) stays shared so the rank strides partition one permutation
+        aseed = seed + 2 * rank
+        self.aug.bind(ViewAugmenter(self.dev["image"], self.dev["lut_image"], *IMG_HW, seed=aseed),
                       ViewAugmenter(self.dev["audio"], self.dev["lut_audio"], *AUD_HW,
-                                    seed=seed + 1))
+                                    seed=aseed + 1))
         self.epoch = 0
 
     def _order(self):
@@ -171,3 +174,44 @@ class AVMNISTDinoLoader:
         self.epoch += 1
         for s in range(0, len(order), self.batch_size):
             yield self.batch(order[s:s + self.batch_size])
+
+
+class AVMNISTLabelledLoader:
+    """``AVMNISTDataModule``'s loaders (get_data.py:592-620, batch 128): (images [B,1,28,28],
+    audios [B,1,112,112], labels [B]) device batches, un-augmented and normalised by the byte
+    tables.  split "train"/"val" = the two parts of random_split(55000, 5000) of the train
+    files, "test" = the test files (the reference's random_split(test, [10000, 0]) only
+    permutes them, and its test loader does not shuffle); the train split shuffles per epoch."""
+
+    def __init__(self, data_dir, batch_size=128, type="burst_noise", device="cuda", split="train",
+                 train_size=55000, val_size=5000, seed=0, shuffle=None):
+        paths = avmnist_paths(data_dir, type)["test" if split == "test" else "train"]
+        for path in paths:
+            if not os.path.exists(path):
+                raise FileNotFoundError(f"Data file not found: {path}")
+        arrays = AVMNISTArrays(*paths)
+        self.dev = arrays.to_device(device)
+        n = len(arrays)
+        if split == "test":
+            self.idx = np.arange(n)
+        else:
+            tr, va = random_split_indices(n, [train_size, val_size], torch.Generator().manual_seed(seed))
+            self.idx = tr if split == "train" else va
+        self.batch_size, self.seed, self.epoch = batch_size, seed, 0
+        self.shuffle = (split == "train") if shuffle is None else shuffle
+        self.image = ViewAugmenter(self.dev["image"], self.dev["lut_image"], *IMG_HW, seed=seed)
+        self.audio = ViewAugmenter(self.dev["audio"], self.dev["lut_audio"], *AUD_HW, seed=seed)
+
+    def __len__(self):
+        return -(-len(self.idx) // self.batch_size)
+
+    def __iter__(self):
+        idx = self.idx
+        if self.shuffle:
+            g = torch.Generator().manual_seed(self.seed + 1000003 * (self.epoch + 1))
+            idx = idx[torch.randperm(len(idx), generator=g).numpy()]
+        self.epoch += 1
+        for s in range(0, len(idx), self.batch_size):
+            b = idx[s:s + self.batch_size]
+            lab = self.dev["labels"][torch.from_numpy(np.asarray(b, np.int64)).to(self.dev["labels"].device)]
+            yield self.image.identity(b), self.audio.identity(b), lab

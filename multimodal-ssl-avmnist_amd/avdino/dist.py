@@ -39,9 +39,12 @@ def grad_allreduce_hook(group=None):
 
 
 def broadcast_buffers(store, src=0, group=None):
-    """Rank ``src``'s buffer arena (centre, BN running stats, counters) to every rank."""
+    """Rank ``src``'s buffers to every rank: the f32 arena (centre, BN running stats) and the
+    int64 num_batches_tracked counters (pending increments applied first)."""
     if dist.get_world_size(group) > 1:
         dist.broadcast(store.buf_arena, src=src, group=group)
+        store.flush_nbt()
+        dist.broadcast(store.nbt_arena, src=src, group=group)
 
 
 def broadcast_parameters(store, src=0, group=None):

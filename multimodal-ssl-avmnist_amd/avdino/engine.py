@@ -394,6 +394,7 @@ class MultiCentralEngine:
         self.negatives, self.group = negatives, group
         self.seed = seed
         self.step_idx = 0
+        self.fwd_count = 0     # forwards so far (a backward belongs to the latest one)
         self.last = {}
 
     # student image branch on the side stream, concurrently with the audio branch: measured
@@ -560,6 +561,7 @@ class MultiCentralEngine:
         self._join(h_done)
         loss = ws.get("loss", 1)
         ops.sum_to(loss_parts, n_parts, 1.0, loss)
+        self.fwd_count += 1
         self.last = dict(B=B, G=G, L=L, V=V, NG=NG, N=N, cat=cat, senc=senc, sfus=sfus, spc=spc,
                          ds=ds, hctx=hctx, center_new=center_new, loss=loss, s_proj=s_proj,
                          t_proj=t_proj, training=training, head_out=head_out)
@@ -587,10 +589,16 @@ class MultiCentralEngine:
     def update_center(self):
         self.store["center"].copy_(self.last["center_new"].view(1, -1))
 
-    def backward(self):
+    def backward(self, ds=None, dheads=None):
+        """Backward of the last forward into the gradient arena (overwritten, not accumulated).
+        Seeds: the fused losses' own d/ds and d/d(head outputs) by default; ``ds`` [V*B*P]
+        and ``dheads`` = (d image head, d audio head) [B*out] replace them when the loss was
+        computed outside the engine (the differentiable ``MultiModalDINO.forward`` path)."""
         ws, st, E, D, P = self.ws, self.store, self.E, self.D, self.P
         c = self.last
         B, V, N = c["B"], c["V"], c["N"]
+        if ds is not None:
+            c["ds"] = ds
         # d cat buffer [N, 2E]: rows [0, V*B) from the fusion, rows [V*B, N) from the heads
         dcat = ws.get("dcat", N * 2 * E)
         h_done = None
@@ -599,6 +607,8 @@ class MultiCentralEngine:
             # concurrently with the projection / fusion backward
             def heads_bwd():
                 ci, ca, dzi, dza = c["hctx"]
+                if dheads is not None:
+                    dzi, dza = dheads
                 hi, ha = self.heads
                 off = V * B * 2 * E
                 hws = self.iws
@@ -743,6 +753,7 @@ class UniModalEngine:
         self.tproj = ProjHead("teacher_projection", D, P, gemm_mode=self.gm)
         self.grad_hook, self.buffer_hook = grad_hook, buffer_hook
         self.seed, self.step_idx = seed, 0
+        self.fwd_count = 0
         self.last = {}
 
     def stage(self, batch):
@@ -779,6 +790,7 @@ class UniModalEngine:
             ops.cosine_consistency(emb, V, B, D, self.cos_alpha, loss_parts[V * B:], None)
         loss = ws.get("loss", 1)
         ops.sum_to(loss_parts, loss_parts.numel(), 1.0, loss)
+        self.fwd_count += 1
         self.last = dict(B=B, G=G, L=L, V=V, emb=emb, sctx=sctx, spc=spc, ds=ds, cos=cos,
                          center_new=center_new, s_proj=s_proj, t_proj=t_proj, loss=loss)
         st.flush_nbt()
@@ -787,14 +799,19 @@ class UniModalEngine:
     def update_center(self):
         self.store["center"].copy_(self.last["center_new"].view(1, -1))
 
-    def backward(self):
+    def backward(self, ds=None, demb=None):
+        """Backward into the gradient arena.  ``ds`` [V*B*P] replaces the fused DINO loss's
+        d/ds and ``demb`` [V*B*D] the cosine term's d/d(embeddings) (then added to the
+        projection's input gradient) when the losses were computed outside the engine."""
         ws, st, c = self.ws, self.store, self.last
         B, V, D = c["B"], c["V"], self.D
-        demb = ws.get("demb", V * B * D)
-        self.sproj.backward(ws, st, c["spc"], c["ds"], demb)
-        if c["cos"]:
-            ops.cosine_consistency(c["emb"], V, B, D, self.cos_alpha, None, demb)
-        self.enc.backward(ws, st, c["sctx"], demb)
+        g = ws.get("demb", V * B * D)
+        self.sproj.backward(ws, st, c["spc"], c["ds"] if ds is None else ds, g)
+        if demb is not None:
+            g.add_(demb.reshape(-1))
+        elif ds is None and c["cos"]:
+            ops.cosine_consistency(c["emb"], V, B, D, self.cos_alpha, None, g)
+        self.enc.backward(ws, st, c["sctx"], g)
 
     def step(self, batch):
         if self.buffer_hook is not None:
@@ -849,6 +866,7 @@ class SimCLREngine:
         self.gen = torch.Generator().manual_seed(seed)
         self.adam_t = [0, 0]
         self.ranges = [store.group_range(i) for i in range(2)]
+        self.fwd_count = 0
         self.last = {}
 
     def draw_mode(self):
@@ -893,17 +911,21 @@ class SimCLREngine:
                                     self.group, local=self.negatives == "local")
         loss = ws.get("loss", 1)
         ops.sum_to(parts, 2 * B, scale, loss)
+        self.fwd_count += 1
         self.last = dict(B=B, mode=mode, calls=calls, reps=reps, dreps=dreps, loss=loss)
         st.flush_nbt()
         return loss
 
-    def backward(self):
+    def backward(self, dreps=None):
+        """Backward into the used towers' gradient ranges; ``dreps`` [2B*P] replaces the fused
+        NT-Xent's d/d[z1; z2] when the loss was computed outside the engine."""
         ws, st, c = self.ws, self.store, self.last
         P, D = self.P, self.D
+        dr = c["dreps"] if dreps is None else dreps.reshape(-1)
         for t, r0, n, ectx, hctx in c["calls"]:
             enc, head = self.towers[t]
             demb = ws.get("demb", n * D)
-            head.backward(ws, st, hctx, c["dreps"][r0 * P:(r0 + n) * P], demb)
+            head.backward(ws, st, hctx, dr[r0 * P:(r0 + n) * P], demb)
             enc.backward(ws, st, ectx, demb)
 
     def used_towers(self):

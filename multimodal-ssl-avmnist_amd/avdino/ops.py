@@ -552,6 +552,27 @@ def argmax_correct(logits, ld, R, C, targets, correct):
     call("avd_argmax_correct", p(logits), ld, R, C, p(targets), p(correct), stream())
 
 
+def argmax_rows(logits, ld, R, C, idx):
+    _need(logits.numel() >= (R - 1) * ld + C and idx.numel() >= R and idx.dtype == torch.int64,
+          "argmax_rows shapes")
+    call("avd_argmax_rows", p(logits), ld, R, C, p(idx), stream())
+
+
+def row_sqnorm(x, N, D, out):
+    _need(x.dtype == torch.float32 and x.numel() >= N * D and out.numel() >= N, "row_sqnorm shapes")
+    call("avd_row_sqnorm", p(x), N, D, p(out), stream())
+
+
+def knn_select(S, ldS, xnorm, M, N, K, labels, C, nbr, pred):
+    """S [M, ldS] = -2 Q X^T (f32), xnorm [N], labels [N] int64 -> pred [M] int64 (+ nbr [M, K])."""
+    _need(S.dtype == torch.float32 and S.numel() >= (M - 1) * ldS + N and xnorm.numel() >= N, "knn S")
+    _need(labels.dtype == torch.int64 and labels.numel() >= N, "knn labels")
+    _need(pred.dtype == torch.int64 and pred.numel() >= M, "knn pred")
+    _need(nbr is None or (nbr.dtype == torch.int64 and nbr.numel() >= M * K), "knn nbr")
+    _need(1 <= K <= 16 and K <= N and 1 <= C <= 64, "knn K <= 16, C <= 64")
+    call("avd_knn_select", p(S), ldS, p(xnorm), M, N, K, p(labels), C, p(nbr), p(pred), stream())
+
+
 def axpy(y, x, a=1.0):
     """y += a*x (contiguous f32, same numel)."""
     _need(y.numel() == x.numel() and y.dtype == x.dtype == torch.float32, "axpy operands")

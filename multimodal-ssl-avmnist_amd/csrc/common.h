@@ -2,10 +2,24 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/avdino.h"
 
 namespace avd {
+
+// Test hook for the persistent kernels (conv_ws, wgrad_ws, c1p8 wgrad / recompute-wgrad):
+// AVDINO_GRID_CAP=n caps their grid at n blocks, so at test sizes every block walks several
+// tiles -- the cross-tile loop, the LDS reuse barrier and the next-tile prefetch run exactly
+// as at bench size.  Unset (the default) it changes nothing.
+inline int grid_cap(int grid) {
+  const char* e = getenv("AVDINO_GRID_CAP");
+  if (e) {
+    const int c = atoi(e);
+    if (c > 0 && c < grid) return c;
+  }
+  return grid;
+}
 
 typedef uint16_t bf16;
 

@@ -464,9 +464,9 @@ int avd_c1p8_wgrad_slabs(int N, int H) {
       per = 3;
     resident = cus * per;
   }
-  return std::min(N * (H / TH), resident);
+  return grid_cap(std::min(N * (H / TH), resident));
 }
-static int rc_wgrad_slabs(int N, int H) { return std::min(N * (H / TH), 2048); }
+static int rc_wgrad_slabs(int N, int H) { return grid_cap(std::min(N * (H / TH), 2048)); }
 
 int avd_c1p8_bwd_apply_wgrad(const void* y, const void* gout, const float* scale,
                              const float* shift, const float* coef, const void* x, float* parts,

@@ -457,7 +457,7 @@ int launch_ws(const void* x, const void* wk, const float* bias, void* y, float* 
       occ = 1;
   }
   const int ntiles = (N / L::NS) * L::TPS;
-  const int grid = std::min(ntiles, num_cus() * occ);
+  const int grid = grid_cap(std::min(ntiles, num_cus() * occ));
   conv_ws_kernel<L, FWD, AP><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, (bf16*)y,
                                                    stats, ntiles, ntiles * L::NPW, aa);
   AVD_CHECK_LAUNCH();

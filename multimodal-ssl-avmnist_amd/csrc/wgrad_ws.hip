@@ -495,7 +495,7 @@ int avd_wg_chunks(int N, int Cout, int Cin, int K) {
   else if (Cin == 16 && Cout == 32 && K == 5) occ = WgA3::OCC;
   else if (Cin == 32 && Cout == 64 && K == 5) occ = WgA4::OCC;
   else return 0;
-  return std::max(1, std::min(N, wg_cus() * occ));
+  return std::max(1, grid_cap(std::min(N, wg_cus() * occ)));
 }
 
 // 1 = launched, 0 = not served, < 0 = error.  parts must hold avd_wg_chunks(...) slabs.

@@ -755,6 +755,81 @@ def simclr_step(P, batch, mode, temperature=0.07, shards=1):
     return {"loss": loss, "z1": Z1, "z2": Z2, "grads": grads, "bn_stats": stats}
 
 
+class _ProbeModel:
+    """DownstreamClassifier (models/dino.py:1764-1814) over a deep copy of the student:
+    ``features(b, eval_mode)`` runs the copy (train mode updates its BN running statistics),
+    the classifier is Linear(D,128)-ReLU-Linear(128,10) trained with AdamW."""
+
+    def __init__(self, P, kind, cls):
+        self.P = {k: np.asarray(v, F64) if np.asarray(v).dtype != np.int64 else np.asarray(v)
+                  for k, v in P.items()}
+        self.C = {k: np.asarray(v, F64) for k, v in cls.items()}
+        self.m = {k: np.zeros_like(v) for k, v in self.C.items()}
+        self.v = {k: np.zeros_like(x) for k, x in self.C.items()}
+        self.t = 0
+        if kind == "multi_central":
+            enc = CentralMultiModal("student")
+
+            def run(b, eval_mode):
+                out, cache = enc.forward(self.P, b["image"].astype(F64), b["audio"].astype(F64), 1,
+                                         eval_mode=eval_mode)
+                return out, (None if eval_mode else _stack_stats(cache))
+        else:
+            fwd, _ = uni_encoder(kind, "student")
+            img = UNI_KINDS.get(kind, kind) == "image_simple"
+
+            def run(b, eval_mode):
+                x = (b["image"] if img else b["audio"]).astype(F64)
+                out, cache = fwd(self.P, x, 1, eval_mode)
+                return out, (None if eval_mode else _branch_stats(cache[1]))
+        self.run = run
+
+    def features(self, b, eval_mode):
+        feat, stats = self.run(b, eval_mode)
+        if not eval_mode:
+            for bk, st in stats:   # the copy's running statistics (train-mode forward)
+                self.P[bk + ".running_mean"], self.P[bk + ".running_var"] = bn_running_update(
+                    self.P[bk + ".running_mean"], self.P[bk + ".running_var"], st)
+        return feat
+
+    def logits(self, feat):
+        C = self.C
+        h = linear_fwd(feat, C["classifier.0.weight"], C["classifier.0.bias"])
+        return h, linear_fwd(np.maximum(h, 0), C["classifier.2.weight"], C["classifier.2.bias"])
+
+    def train_batch(self, b, lr, wd):
+        """One optimizer step on the classifier; returns the batch's mean CE."""
+        C = self.C
+        feat = self.features(b, False)
+        h, logits = self.logits(feat)
+        r = np.maximum(h, 0)
+        loss, dl = cross_entropy(logits, b["label"])
+        dr, dw2, db2 = linear_bwd(dl, r, C["classifier.2.weight"])
+        _, dw0, db0 = linear_bwd(dr * (h > 0), feat, C["classifier.0.weight"])
+        g = {"classifier.0.weight": dw0, "classifier.0.bias": db0, "classifier.2.weight": dw2,
+             "classifier.2.bias": db2}
+        self.t += 1
+        for k in C:
+            C[k], self.m[k], self.v[k] = adamw_step(C[k], g[k], self.m[k], self.v[k], self.t, lr, wd)
+        return loss
+
+    def evaluate(self, batches):
+        """evaluate() in eval mode: (mean per-batch CE, accuracy %, logits, predictions)."""
+        ev_loss, correct, total, all_logits = 0.0, 0, 0, []
+        for b in batches:
+            _, logits = self.logits(self.features(b, True))
+            ev_loss += cross_entropy(logits, b["label"])[0]
+            correct += int((logits.argmax(1) == b["label"]).sum())
+            total += len(b["label"])
+            all_logits.append(logits)
+        lg = np.concatenate(all_logits)
+        return ev_loss / len(batches), 100.0 * correct / total, lg, lg.argmax(1)
+
+    def running(self):
+        return {k: self.P[k].copy() for k in self.P
+                if k.endswith(("running_mean", "running_var")) and k.startswith("student.")}
+
+
 def linear_probe(P, kind, train_batches, valid_batches, cls, lr, wd=0.01):
     """on_train_epoch_end's linear probe (multimodal dino.py:878-951, unimodal 1670-1735) with
     DownstreamClassifier (1764-1814): a frozen deep copy of the student encoder, run in TRAIN
@@ -765,52 +840,53 @@ def linear_probe(P, kind, train_batches, valid_batches, cls, lr, wd=0.01):
     batches: lists of dicts image [B,1,28,28], audio [B,1,112,112], label [B].
     cls: classifier.{0,2}.{weight,bias}.  Returns per-batch train losses, val_loss (their mean),
     eval loss / accuracy / logits, the final classifier and the copy's running statistics."""
-    P = {k: np.asarray(v, F64) if np.asarray(v).dtype != np.int64 else np.asarray(v) for k, v in P.items()}
-    C = {k: np.asarray(v, F64) for k, v in cls.items()}
-    if kind == "multi_central":
-        enc = CentralMultiModal("student")
-
-        def run(b, eval_mode):
-            out, cache = enc.forward(P, b["image"].astype(F64), b["audio"].astype(F64), 1,
-                                     eval_mode=eval_mode)
-            return out, (None if eval_mode else _stack_stats(cache))
-    else:
-        fwd, _ = uni_encoder(kind, "student")
-        img = UNI_KINDS.get(kind, kind) == "image_simple"
-
-        def run(b, eval_mode):
-            x = (b["image"] if img else b["audio"]).astype(F64)
-            out, cache = fwd(P, x, 1, eval_mode)
-            return out, (None if eval_mode else _branch_stats(cache[1]))
-    m = {k: np.zeros_like(v) for k, v in C.items()}
-    v = {k: np.zeros_like(x) for k, x in C.items()}
-    losses = []
-    for step, b in enumerate(train_batches, 1):
-        feat, stats = run(b, False)
-        for bk, st in stats:   # the copy's running statistics (train-mode forward)
-            P[bk + ".running_mean"], P[bk + ".running_var"] = bn_running_update(
-                P[bk + ".running_mean"], P[bk + ".running_var"], st)
-        h = linear_fwd(feat, C["classifier.0.weight"], C["classifier.0.bias"])
-        r = np.maximum(h, 0)
-        logits = linear_fwd(r, C["classifier.2.weight"], C["classifier.2.bias"])
-        loss, dl = cross_entropy(logits, b["label"])
-        losses.append(loss)
-        dr, dw2, db2 = linear_bwd(dl, r, C["classifier.2.weight"])
-        _, dw0, db0 = linear_bwd(dr * (h > 0), feat, C["classifier.0.weight"])
-        g = {"classifier.0.weight": dw0, "classifier.0.bias": db0, "classifier.2.weight": dw2,
-             "classifier.2.bias": db2}
-        for k in C:
-            C[k], m[k], v[k] = adamw_step(C[k], g[k], m[k], v[k], step, lr, wd)
-    ev_loss, correct, total, all_logits = 0.0, 0, 0, []
-    for b in valid_batches:
-        feat, _ = run(b, True)
-        h = linear_fwd(feat, C["classifier.0.weight"], C["classifier.0.bias"])
-        logits = linear_fwd(np.maximum(h, 0), C["classifier.2.weight"], C["classifier.2.bias"])
-        ev_loss += cross_entropy(logits, b["label"])[0]
-        correct += int((logits.argmax(1) == b["label"]).sum())
-        total += len(b["label"])
-        all_logits.append(logits)
-    rs = {k: P[k] for k in P if k.endswith(("running_mean", "running_var")) and k.startswith("student.")}
+    pm = _ProbeModel(P, kind, cls)
+    losses = [pm.train_batch(b, lr, wd) for b in train_batches]
+    ev_loss, acc, logits, _ = pm.evaluate(valid_batches)
     return {"train_losses": np.array(losses), "val_loss": float(np.mean(losses)),
-            "eval_loss": ev_loss / len(valid_batches), "mlp_acc": 100.0 * correct / total,
-            "logits": np.concatenate(all_logits), "classifier": C, "running": rs}
+            "eval_loss": ev_loss, "mlp_acc": acc, "logits": logits, "classifier": pm.C,
+            "running": pm.running()}
+
+
+def cosine_annealing_lr(base_lr, epoch, T_max, eta_min=0.0):
+    """torch.optim.lr_scheduler.CosineAnnealingLR's value after ``epoch`` steps (closed form)."""
+    return eta_min + (base_lr - eta_min) * (1 + math.cos(math.pi * epoch / T_max)) / 2
+
+
+def train_downstream(P, kind, train_batches, valid_batches, test_batches, cls, num_epochs=10,
+                     lr=1e-3, wd=0.01):
+    """training_structures/dino_train.py:188-329: DownstreamClassifier trained num_epochs with
+    AdamW(classifier, lr) (torch default weight_decay 0.01) + CosineAnnealingLR(T_max=num_epochs)
+    stepped per epoch; the copy in train mode for training epochs, eval mode for evaluate();
+    the checkpoint of the first epoch with the highest validation accuracy (strict >, starting
+    from 0) -- classifier AND the copy's running statistics -- is reloaded for the test set."""
+    import copy
+    pm = _ProbeModel(P, kind, cls)
+    best_acc, best, history = 0.0, None, []
+    for epoch in range(num_epochs):
+        lr_e = cosine_annealing_lr(lr, epoch, num_epochs)
+        losses = [pm.train_batch(b, lr_e, wd) for b in train_batches]
+        val_loss, val_acc, _, _ = pm.evaluate(valid_batches)
+        history.append((float(np.mean(losses)), val_loss, val_acc))
+        if val_acc > best_acc:
+            best_acc, best = val_acc, (epoch, copy.deepcopy(pm.C), copy.deepcopy(pm.P))
+    if best is not None:
+        pm.C, pm.P = best[1], best[2]
+    test_loss, test_acc, logits, preds = pm.evaluate(test_batches)
+    return {"history": np.array(history), "best_epoch": -1 if best is None else best[0],
+            "test_loss": test_loss, "test_acc": test_acc, "test_logits": logits,
+            "test_preds": preds, "classifier": pm.C, "running": pm.running()}
+
+
+def knn_classify(train_x, train_y, test_x, k=5):
+    """sklearn KNeighborsClassifier(n_neighbors=k).fit(train_x, train_y).predict(test_x) as
+    train_knn_classifier uses it (dino_train.py:362-366): brute-force euclidean distances in
+    float64, the k nearest with ties to the smaller train index, uniform-weight vote with ties
+    to the smallest class (argmax over sorted classes_).  Returns (predictions, neighbours)."""
+    tx, qx = np.asarray(train_x, F64), np.asarray(test_x, F64)
+    d = (qx * qx).sum(1)[:, None] - 2 * qx @ tx.T + (tx * tx).sum(1)[None, :]
+    nbr = np.argsort(d, axis=1, kind="stable")[:, :k]
+    classes, yi = np.unique(np.asarray(train_y), return_inverse=True)
+    votes = np.zeros((len(qx), len(classes)), np.int64)
+    np.add.at(votes, (np.repeat(np.arange(len(qx)), k), yi[nbr].ravel()), 1)
+    return classes[votes.argmax(1)], nbr

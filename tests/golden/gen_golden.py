@@ -69,6 +69,7 @@ STUBS = {
         f"class {n}:\n    def __init__(self, *a, **k): pass\n"
         for n in ["TimeStretch", "FrequencyMasking", "TimeMasking", "Spectrogram"]),
     "torchmetrics/__init__.py": "",
+    "torchinfo/__init__.py": "def summary(*a, **k): raise RuntimeError('stub')\n",
     "torchmetrics/classification.py": "class Accuracy:\n    def __init__(self, *a, **k): pass\n",
 }
 
@@ -370,6 +371,102 @@ def probe_case(name, kind, E, D, P, B, nb_train, nb_valid, pseed, bseed, out_dir
     print(f"{name}: train losses {np.array(losses)} eval {out['eval_loss']:.6f} acc {out['mlp_acc']}")
 
 
+def downstream_case(name, kind, E, D, P, B, nb_train, nb_valid, nb_test, epochs, pseed, bseed,
+                    out_dir, dt="float32", lr=1e-3):
+    """compute_accuracies' two evaluations (run_dino.py:481-501), by calling the reference's
+    own training_structures/dino_train.py functions on CPU:
+      train_knn_classifier (349-369): FeatureExtractor + sklearn KNeighborsClassifier(5);
+      train_downstream (188-329): DownstreamClassifier, AdamW + CosineAnnealingLR, best-val
+        checkpoint, test evaluation (the CUDA-only autocast / GradScaler disable themselves).
+    Harness-only changes: DownstreamClassifier / FeatureExtractor are subclassed inside
+    dino_train's namespace to (a) load the classifier weights from oracle/params.py instead of
+    torch's RNG and (b) cast the inputs to the run dtype (the functions cast them to float32);
+    the model's dropout is set to 0."""
+    import csv as _csv
+    import tempfile
+    import torch
+    from torch.utils.data import DataLoader, TensorDataset
+    dtt = getattr(torch, dt)
+    import models.dino as rd
+    import training_structures.dino_train as tdt
+    torch.manual_seed(0)
+    if kind == "multi_central":
+        model = rd.MultiModalDINO(encoder_class=rd.CentralMultiModalEncoder, output_dim=D,
+                                  encoder_output_dim=E, projection_dim=P, dropout=0.0)
+        spec = ospec.multimodal_dino_spec("default", E, D, P)
+    else:
+        enc = {"image_simple": rd.ImageEncoder, "spectrogram_simple": rd.SpectrogramEncoder}[kind]
+        model = rd.UniModalDINO(encoder_class=enc, output_dim=D, projection_dim=P, dropout=0.0)
+        spec = ospec.unimodal_dino_spec(kind, D, P)
+    state = make_state(spec, pseed)
+    load_into(model, spec, state)
+    zero_dropout(model)
+    model = model.to(dtt)
+    cstate = make_state(ospec.classifier_spec(D), pseed + 1)
+
+    class DC(rd.DownstreamClassifier):
+        def __init__(self, *a, **k):
+            super().__init__(*a, **k)
+            self.to(dtt)
+            with torch.no_grad():
+                for kk, v in cstate.items():
+                    dict(self.named_parameters())[kk].copy_(torch.from_numpy(v).to(dtt))
+
+        def forward(self, images, spectrograms=None):
+            return super().forward(images.to(dtt), None if spectrograms is None else spectrograms.to(dtt))
+
+    class FE(rd.FeatureExtractor):
+        def forward(self, images, spectrograms=None):
+            return super().forward(images.to(dtt), None if spectrograms is None else spectrograms.to(dtt))
+
+    tdt.DownstreamClassifier, tdt.FeatureExtractor = DC, FE
+
+    def loader(n, seed):
+        bs = [make_multimodal_batch(B, 1, 0, seed + i) for i in range(n)]
+        cat = lambda k: torch.from_numpy(np.concatenate([b[k] for b in bs]))  # noqa: E731
+        return DataLoader(TensorDataset(cat("image"), cat("audio"), cat("label")), batch_size=B,
+                          shuffle=False)
+
+    tr, va, te = loader(nb_train, bseed), loader(nb_valid, bseed + 1000), loader(nb_test, bseed + 2000)
+    out = {"meta_dims": np.array([E, D, P, B, nb_train, nb_valid, nb_test, epochs, pseed, bseed]),
+           "meta_kind": np.array(kind), "meta_lr": np.float64(lr)}
+    knn, acc = tdt.train_knn_classifier(model, tr, te, n_neighbors=5, device="cpu")
+    fe = FE(model)
+    trf, _ = tdt.feature_extraction_loop("cpu", fe, tr)
+    tef, tel = tdt.feature_extraction_loop("cpu", fe, te)
+    out["knn_acc"] = np.float64(acc)
+    out["knn_pred"] = knn.predict(tef).astype(np.int64)
+    out["knn_nbr"] = knn.kneighbors(tef, return_distance=False).astype(np.int64)
+    summarize("feat_train", trf, out)
+    summarize("feat_test", tef, out)
+    with tempfile.TemporaryDirectory() as tmp:
+        clf = tdt.train_downstream(model, tr, va, te, num_epochs=epochs, device="cpu",
+                                   learning_rate=lr, save_path=f"{tmp}/d/m.pt",
+                                   train_log_path=f"{tmp}/d/train.csv",
+                                   test_log_path=f"{tmp}/d/test.csv")
+        logs = sorted(os.listdir(f"{tmp}/d"))
+        tr_log = [f for f in logs if f.startswith("train")][0]
+        te_log = [f for f in logs if f.startswith("test")][0]
+        with open(f"{tmp}/d/{tr_log}") as f:
+            rows = list(_csv.reader(f))[1:]
+        out["history"] = np.array([[float(r[1]), float(r[2]), float(r[3])] for r in rows], np.float64)
+        with open(f"{tmp}/d/{te_log}") as f:
+            rows = list(_csv.reader(f))[1:]
+        out["test_preds"] = np.array([int(r[1]) for r in rows], np.int64)
+        out["test_labels"] = np.array([int(r[0]) for r in rows], np.int64)
+    met = tdt.compute_classification_metrics(clf, te, device="cpu")
+    out["test_acc"] = np.float64(met["accuracy"])
+    out["confusion_matrix"] = met["confusion_matrix"].astype(np.int64)
+    for k, v in clf.named_parameters():
+        if k.startswith("classifier"):
+            summarize("cls/" + k, v.detach().numpy(), out)
+    for k, v in clf.encoder.state_dict().items():
+        if k.endswith("running_mean") or k.endswith("running_var"):
+            summarize("rs/student." + k, v.numpy(), out)
+    np.savez_compressed(os.path.join(out_dir, name + ".npz"), **out)
+    print(f"{name}: knn {acc:.2f}% history {out['history'].tolist()} test {out['test_acc']:.2f}%")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=HERE)
@@ -398,6 +495,10 @@ def main():
         ("probe_multi_central", probe_case, ("multi_central", 32, 32, 16, 6, 3, 2, 111, 1011), {}),
         ("probe_image_simple", probe_case, ("image_simple", 0, 64, 32, 6, 3, 2, 112, 1012), {}),
         ("simclr_small", simclr_case, (256, 256, 4, 107, 1007), {}),
+        ("downstream_multi_central", downstream_case,
+         ("multi_central", 32, 32, 16, 8, 4, 2, 2, 3, 113, 1013), {}),
+        ("downstream_image_simple", downstream_case,
+         ("image_simple", 0, 64, 32, 8, 4, 2, 2, 3, 114, 1014), {}),
     ]
     # Each case twice: the reference executed in fp32 (its CPU numerics) and in float64
     # (the same algorithm without rounding noise: the tight pin for the oracle).

@@ -1,0 +1,330 @@
+"""The production bf16 conv kernels at the shapes the bench runs (VERDICT r1 "what's weak" 1).
+
+bench.py's config-2 step (B=1024, 2 global + 4 local views + the originals) runs the audio
+conv1 kernels at N = 7 x 1024 = 7168 samples (student) and 2048 (teacher), and the mid-layer
+weights-stationary kernels (conv_ws / wgrad_ws) at the same N.  Those kernels are persistent:
+grid = min(tiles, resident blocks), so at bench size every block walks tens of tiles through
+the cross-tile loop, the LDS-reuse barrier and the next-tile register prefetch -- paths the
+small-N tests (one tile per block) never reach.  Here they run:
+
+  * at bench size, against a float64 reference computed on the GPU with torch (a tap loop of
+    f64 matmuls -- no MIOpen, no libavdino) from the SAME bf16 operands;
+  * at small N with AVDINO_GRID_CAP forcing a few blocks (many tiles each), against the
+    uncapped launch: forward / dgrad tiles are independent of the block that computes them
+    (bit-identical), weight gradients are fp32 sums in another order (rel 1e-6).
+
+Tolerances: stored bf16 maps rel-L2 5e-3 (one bf16 rounding of the output); f32 reductions of
+stored values (BN statistics, weight gradients) 1e-5 vs float64.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+F = pytest.importorskip("torch.nn.functional")
+
+T = torch.bfloat16
+F64 = torch.float64
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from avdino import ops as _ops
+    return _ops
+
+
+def grel(a, b):
+    a, b = a.to(F64).reshape(-1), b.to(F64).reshape(-1)
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def rnd(g, shape, lo=-1.0, hi=1.0, dtype=torch.float32):
+    return (torch.rand(*shape, generator=g, device="cuda") * (hi - lo) + lo).to(dtype)
+
+
+def _chunks(N, per_sample_elems, budget=2 ** 27):
+    step = max(1, budget // max(per_sample_elems, 1))
+    return [(s, min(N, s + step)) for s in range(0, N, step)]
+
+
+def conv_ref(x, w, pad):
+    """NHWC float64 conv: x [N,H,W,Ci], w [Co,Ci,K,K] -> [N,Ho,Wo,Co] (tap loop of matmuls)."""
+    N, H, W, Ci = x.shape
+    Co, _, K, _ = w.shape
+    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
+    w = w.to(F64)
+    y = torch.empty(N, Ho, Wo, Co, device="cuda", dtype=F64)
+    for a, b in _chunks(N, (H + 2 * pad) * (W + 2 * pad) * max(Ci, Co) * 3):
+        xp = F.pad(x[a:b].to(F64), (0, 0, pad, pad, pad, pad))
+        acc = torch.zeros(b - a, Ho, Wo, Co, device="cuda", dtype=F64)
+        for i in range(K):
+            for j in range(K):
+                acc += xp[:, i:i + Ho, j:j + Wo, :] @ w[:, :, i, j].T
+        y[a:b] = acc
+    return y
+
+
+def wgrad_ref(x, dy, K, pad):
+    """dW[o,c,i,j] = sum_{n,h,w} dy[n,h,w,o] x_pad[n,h+i,w+j,c], float64."""
+    N, H, W, Ci = x.shape
+    _, Ho, Wo, Co = dy.shape
+    dw = torch.zeros(Co, Ci, K, K, device="cuda", dtype=F64)
+    for a, b in _chunks(N, (H + 2 * pad) * (W + 2 * pad) * (Ci + Co) * 2):
+        xp = F.pad(x[a:b].to(F64), (0, 0, pad, pad, pad, pad))
+        d = dy[a:b].to(F64).reshape(-1, Co)
+        for i in range(K):
+            for j in range(K):
+                dw[:, :, i, j] += d.T @ xp[:, i:i + Ho, j:j + Wo, :].reshape(-1, Ci)
+    return dw
+
+
+def dgrad_ref(dy, w, pad):
+    """dX = conv(dy, w flipped and transposed, K-1-pad), float64."""
+    K = w.shape[2]
+    w2 = w.to(F64).flip(2, 3).transpose(0, 1).contiguous()
+    return conv_ref(dy, w2, K - 1 - pad)
+
+
+def layout(ops, w, dgrad):
+    Co, Ci, K, _ = w.shape
+    wk = torch.empty(ops.cl_weight_elems(Co, Ci, K, dgrad), device="cuda", dtype=T)
+    ops.cl_weight_layout(w.float().contiguous(), wk, dgrad)
+    return wk
+
+
+# ---------------------------------------------------------------------------- audio conv1
+N_STUDENT, N_TEACHER, B_BENCH = 7 * 1024, 2 * 1024, 1024
+
+
+def test_conv1_forward_stats_bench_size(ops):
+    """Audio conv1 (1->8, 5x5 p2, 112x112) forward + BN partial sums at N = 7168."""
+    N, B, H, C, K, pad = N_STUDENT, B_BENCH, 112, 8, 5, 2
+    G = N // B
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = rnd(g, (N, H, H, 1), 0, 1, T)
+    w = rnd(g, (C, 1, K, K)).to(T).float() / 5
+    bias = rnd(g, (C,), -0.1, 0.1)
+    y = torch.empty(N, H, H, C, device="cuda", dtype=T)
+    R = ops.cl_stat_rows(H, H, B, K, 1, C, T)
+    st = torch.full((C * G * R * 2,), float("nan"), device="cuda")
+    ops.cl_conv_fwd(x, layout(ops, w, 0), bias, y, st, N, B, 1, H, H, C, K, pad)
+    y_ref = conv_ref(x, w, pad) + bias.to(F64)
+    assert grel(y, y_ref) < 5e-3
+    s = st.view(C, G, R, 2).to(F64).sum(2)
+    yv = y.to(F64).view(G, B * H * H, C)
+    assert grel(s[..., 0], yv.sum(1).T) < 1e-5
+    assert grel(s[..., 1], (yv ** 2).sum(1).T) < 1e-5
+
+
+def _bn_setup(g, G, C):
+    scale = rnd(g, (G * C,), 0.5, 1.5)
+    shift = rnd(g, (G * C,), -0.3, 0.3)
+    coef = rnd(g, (G * C * 3,), -0.5, 0.5)
+    return scale, shift, coef
+
+
+def test_conv1_bwd_apply_wgrad_bench_size(ops):
+    """c1p8_bwd_wgrad_kernel (BN-backward apply fused with conv1's weight gradient), the
+    bench's dominant launch, at N = 7168: 65 tiles per persistent block on MI355X."""
+    N, B, H, C, K, pad = N_STUDENT, B_BENCH, 112, 8, 5, 2
+    G = N // B
+    g = torch.Generator(device="cuda").manual_seed(2)
+    x = rnd(g, (N, H, H, 1), 0, 1, T)
+    y = (torch.randn(N, H, H, C, generator=g, device="cuda") * 0.8 + 0.1).to(T)
+    gout = rnd(g, (N, H // 2, H // 2, C), dtype=T)
+    scale, shift, coef = _bn_setup(g, G, C)
+    ns = ops.cl_apply_wgrad_slabs(T, N, 1, H, H, C, K, pad)
+    assert 0 < ns < N * (H // 16), "persistent grid expected at bench size"
+    parts = torch.full((ns * C * K * K,), float("nan"), device="cuda")
+    ops.cl_bn_bwd_apply_wgrad(y, gout, scale, shift, coef, x, parts, N, B, 1, H, H, C, K, pad)
+    dw = torch.empty(C * K * K, device="cuda")
+    ops.sum_rows(parts, ns, C * K * K, dw)
+    # the same bf16 dy from the unfused apply kernel, then float64
+    dy = torch.empty_like(y)
+    ops.cl_bn_bwd_apply(y, gout, 0, scale, shift, coef, dy, N, B, C, H, H)
+    dw64 = wgrad_ref(x, dy, K, pad)
+    assert grel(dw, dw64) < 1e-5, grel(dw, dw64)
+
+
+def test_conv1_recompute_bench_size(ops):
+    """The stored-y-free conv1 passes the bench runs: teacher statistics (N = 2048, C1_STATS)
+    and the student's BN -> ReLU -> pool recomputed from x (N = 7168, C1_APPLY) equal the
+    stored-y kernels (bit-exact pooled maps, statistics to fp32 order)."""
+    H, C, K, pad, B = 112, 8, 5, 2, B_BENCH
+    g = torch.Generator(device="cuda").manual_seed(3)
+    w = rnd(g, (C, 1, K, K)).to(T).float() / 5
+    bias = rnd(g, (C,), -0.1, 0.1)
+    wk = layout(ops, w, 0)
+    for N, pas in ((N_TEACHER, ops.C1_STATS), (N_STUDENT, ops.C1_APPLY)):
+        G = N // B
+        x = rnd(g, (N, H, H, 1), 0, 1, T)
+        y = torch.empty(N, H, H, C, device="cuda", dtype=T)
+        R0 = ops.cl_stat_rows(H, H, B, K, 1, C, T)
+        st0 = torch.empty(C * G * R0 * 2, device="cuda")
+        ops.cl_conv_fwd(x, wk, bias, y, st0, N, B, 1, H, H, C, K, pad)
+        if pas == ops.C1_STATS:
+            R1 = ops.cl_c1_recompute_rows(ops.C1_STATS, T, N, B, 1, H, H, C, K, pad)
+            st1 = torch.empty(C * G * R1 * 2, device="cuda")
+            ops.cl_c1_recompute(ops.C1_STATS, x, wk, bias, N, B, 1, H, H, C, K, pad, out=st1)
+            assert grel(st1.view(C, G, R1, 2).to(F64).sum(2), st0.view(C, G, R0, 2).to(F64).sum(2)) < 1e-6
+        else:
+            scale, shift, _ = _bn_setup(g, G, C)
+            z0 = torch.empty(N, H // 2, H // 2, C, device="cuda", dtype=T)
+            ops.cl_bn_relu_pool(y, scale, shift, z0, 0, N, B, C, H, H)
+            z1 = torch.full_like(z0, float("nan"))
+            ops.cl_c1_recompute(ops.C1_APPLY, x, wk, bias, N, B, 1, H, H, C, K, pad, scale=scale,
+                                shift=shift, z=z1)
+            assert torch.equal(z0, z1)
+
+
+# ---------------------------------------------------------------------------- mid layers
+# (Cin, H, Cout, K, pad, N): the CentralNet audio conv2-4 and image conv2 at bench-scale N
+WS_BENCH = [(8, 56, 16, 5, 2, 2048), (16, 28, 32, 5, 2, 2048), (32, 14, 64, 5, 2, 4096),
+            (32, 14, 64, 5, 0, 4096)]
+
+
+@pytest.mark.parametrize("shape", WS_BENCH)
+def test_ws_kernels_bench_size(ops, shape):
+    """conv_ws forward (+ stats), conv_ws dgrad and wgrad_ws at bench-scale N vs float64."""
+    Ci, H, Co, K, pad, N = shape
+    B = 1024
+    G = N // B
+    Ho = H + 2 * pad - K + 1
+    g = torch.Generator(device="cuda").manual_seed(4 + H + pad)
+    x = rnd(g, (N, H, H, Ci), dtype=T)
+    w = (rnd(g, (Co, Ci, K, K)) / (Ci * K * K) ** 0.5).to(T).float()
+    bias = rnd(g, (Co,), -0.1, 0.1)
+    y = torch.empty(N, Ho, Ho, Co, device="cuda", dtype=T)
+    R = ops.cl_stat_rows(Ho, Ho, B, K, Ci, Co, T)
+    st = torch.full((Co * G * R * 2,), float("nan"), device="cuda")
+    ops.cl_conv_fwd(x, layout(ops, w, 0), bias, y, st, N, B, Ci, H, H, Co, K, pad)
+    assert grel(y, conv_ref(x, w, pad) + bias.to(F64)) < 5e-3
+    s = st.view(Co, G, R, 2).to(F64).sum(2)
+    yv = y.to(F64).view(G, B * Ho * Ho, Co)
+    assert grel(s[..., 0], yv.sum(1).T) < 1e-5
+    assert grel(s[..., 1], (yv ** 2).sum(1).T) < 1e-5
+    dy = rnd(g, (N, Ho, Ho, Co), dtype=T)
+    dx = torch.empty(N, H, H, Ci, device="cuda", dtype=T)
+    ops.cl_conv_dgrad(dy, layout(ops, w, 1), dx, N, Ci, H, H, Co, K, pad)
+    assert grel(dx, dgrad_ref(dy, w, pad)) < 5e-3
+    nch = ops.cl_wgrad_chunks(N, Co, Ci, K)
+    parts = torch.full((nch * Co * Ci * K * K,), float("nan"), device="cuda")
+    ops.cl_conv_wgrad(x, dy, parts, N, Ci, H, H, Co, K, pad)
+    dw = torch.empty(Co * Ci * K * K, device="cuda")
+    ops.sum_rows(parts, nch, Co * Ci * K * K, dw)
+    assert grel(dw, wgrad_ref(x, dy, K, pad)) < 1e-5
+
+
+# ---------------------------------------------------------------------------- forced small grids
+def _capped(monkeypatch, cap, fn):
+    monkeypatch.delenv("AVDINO_GRID_CAP", raising=False)
+    a = fn()
+    monkeypatch.setenv("AVDINO_GRID_CAP", str(cap))
+    b = fn()
+    monkeypatch.delenv("AVDINO_GRID_CAP")
+    return a, b
+
+
+@pytest.mark.parametrize("shape", [(8, 56, 16, 5, 2, 48), (16, 28, 32, 5, 2, 48),
+                                   (32, 14, 64, 5, 2, 96), (32, 14, 64, 5, 0, 96)])
+@pytest.mark.parametrize("cap", [1, 3, 7])
+def test_ws_kernels_many_tiles_per_block(ops, shape, cap, monkeypatch):
+    Ci, H, Co, K, pad, N = shape
+    B = N // 2
+    G = 2
+    Ho = H + 2 * pad - K + 1
+    g = torch.Generator(device="cuda").manual_seed(50 + H)
+    x = rnd(g, (N, H, H, Ci), dtype=T)
+    w = (rnd(g, (Co, Ci, K, K)) / (Ci * K * K) ** 0.5).to(T).float()
+    bias = rnd(g, (Co,), -0.1, 0.1)
+    dy = rnd(g, (N, Ho, Ho, Co), dtype=T)
+    wk, wd = layout(ops, w, 0), layout(ops, w, 1)
+    R = ops.cl_stat_rows(Ho, Ho, B, K, Ci, Co, T)
+
+    def run():
+        y = torch.full((N, Ho, Ho, Co), float("nan"), device="cuda", dtype=T)
+        st = torch.full((Co * G * R * 2,), float("nan"), device="cuda")
+        ops.cl_conv_fwd(x, wk, bias, y, st, N, B, Ci, H, H, Co, K, pad)
+        dx = torch.full((N, H, H, Ci), float("nan"), device="cuda", dtype=T)
+        ops.cl_conv_dgrad(dy, wd, dx, N, Ci, H, H, Co, K, pad)
+        nch = ops.cl_wgrad_chunks(N, Co, Ci, K)
+        parts = torch.full((nch * Co * Ci * K * K,), float("nan"), device="cuda")
+        ops.cl_conv_wgrad(x, dy, parts, N, Ci, H, H, Co, K, pad)
+        dw = torch.empty(Co * Ci * K * K, device="cuda")
+        ops.sum_rows(parts, nch, Co * Ci * K * K, dw)
+        torch.cuda.synchronize()
+        return y, st.view(Co, G, R, 2).to(F64).sum(2), dx, dw
+
+    (y0, s0, dx0, dw0), (y1, s1, dx1, dw1) = _capped(monkeypatch, cap, run)
+    assert torch.equal(y0, y1) and torch.equal(dx0, dx1)
+    assert grel(s1, s0) < 1e-6 and grel(dw1, dw0) < 1e-6
+    assert grel(dw1, wgrad_ref(x, dy, K, pad)) < 1e-5
+
+
+@pytest.mark.parametrize("cap", [1, 5])
+def test_conv1_wgrad_many_tiles_per_block(ops, cap, monkeypatch):
+    N, B, H, C, K, pad = 12, 6, 112, 8, 5, 2
+    G = N // B
+    g = torch.Generator(device="cuda").manual_seed(60 + cap)
+    x = rnd(g, (N, H, H, 1), 0, 1, T)
+    y = torch.randn(N, H, H, C, generator=g, device="cuda").to(T)
+    gout = rnd(g, (N, H // 2, H // 2, C), dtype=T)
+    scale, shift, coef = _bn_setup(g, G, C)
+
+    def run():
+        ns = ops.cl_apply_wgrad_slabs(T, N, 1, H, H, C, K, pad)
+        parts = torch.full((ns * C * K * K,), float("nan"), device="cuda")
+        ops.cl_bn_bwd_apply_wgrad(y, gout, scale, shift, coef, x, parts, N, B, 1, H, H, C, K, pad)
+        dw = torch.empty(C * K * K, device="cuda")
+        ops.sum_rows(parts, ns, C * K * K, dw)
+        torch.cuda.synchronize()
+        return ns, dw
+
+    (n0, dw0), (n1, dw1) = _capped(monkeypatch, cap, run)
+    assert n1 == cap < n0
+    assert grel(dw1, dw0) < 1e-6
+
+
+# ---------------------------------------------------------------------------- whole step
+def test_bf16_step_vs_fp32_step_config2(capsys):
+    """The benchmarked bf16 step at config-2 size (B = 1024, 2 global + 4 local views, mse,
+    E = D = 256, P = 128) against the fp32 engine from identical parameters and inputs.  The
+    bf16 path rounds every stored activation and conv operand once (2^-9 relative); the bounds
+    below are what that rounding allows for a 4-layer conv stack with batch statistics (the
+    measured errors are printed): loss 2e-3 relative, per-tensor gradient rel-L2 median 2e-2 and
+    worst 1e-1 over tensors with a non-negligible gradient."""
+    from avdino.engine import Hyper, MultiCentralEngine
+    from avdino.params import ParamStore
+    from avdino.spec import multimodal_dino_sd
+    from oracle.params import make_state
+    from oracle import spec as OS
+    E = D = 256
+    P, B, G, L = 128, 1024, 2, 4
+    state = make_state(OS.multimodal_dino_spec("mse", E, D, P), 301)
+    g = torch.Generator(device="cuda").manual_seed(302)
+
+    def px(*s):
+        return torch.randint(0, 256, s, generator=g, device="cuda", dtype=torch.int32).float() / 255
+
+    batch = dict(g_img=px(B, G, 1, 28, 28), g_aud=px(B, G, 1, 112, 112), l_img=px(B, L, 1, 28, 28),
+                 l_aud=px(B, L, 1, 112, 112), image=px(B, 1, 28, 28), audio=px(B, 1, 112, 112))
+    out = {}
+    for name, act in (("f32", torch.float32), ("bf16", torch.bfloat16)):
+        store = ParamStore(multimodal_dino_sd("mse", E, D, P), "cuda")
+        store.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state.items()})
+        eng = MultiCentralEngine(store, "mse", E, D, P, Hyper(dropout=0.0, fusion_dropout=0.0),
+                                 act_dtype=act)
+        loss = eng.forward(batch).item()
+        eng.backward()
+        out[name] = (loss, {k: store.grad_of(k).detach().to(F64).clone() for k in store.live_keys})
+    (l32, g32), (l16, g16) = out["f32"], out["bf16"]
+    errs = {k: grel(g16[k], g32[k]) for k in g32 if g32[k].norm().item() > 1e-6 * max(
+        v.norm().item() for v in g32.values())}
+    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:6]
+    med = float(np.median(list(errs.values())))
+    with capsys.disabled():
+        print(f"\nbf16 vs fp32 step (B=1024): loss {l16:.6f} vs {l32:.6f} "
+              f"(rel {abs(l16 - l32) / abs(l32):.2e}); grad rel-L2 median {med:.2e}; worst {worst}")
+    assert abs(l16 - l32) / abs(l32) < 2e-3
+    assert med < 2e-2
+    assert worst[0][1] < 1e-1, worst

@@ -110,9 +110,18 @@ def test_simclr_mode_draw_and_lightning_api():
     assert set(modes) == {0, 1, 2, 3}
     b = make_simclr_batch(4, 5)
     batch = tuple(torch.from_numpy(b[k]) for k in ("img1", "spec1", "img2", "spec2"))
-    loss = m.training_step(batch, 0)
-    m.backward_and_step()
+    opt = m.configure_optimizers()["optimizer"]
+    loss = m.training_step(batch, 0, mode=2)
+    opt.zero_grad()
+    loss.backward()
+    opt.step()
     assert np.isfinite(loss.item())
+    assert m.model.arena_image.grad is not None and m.model.arena_audio.grad is not None
+    loss = m.training_step(batch, 1, mode=0)        # image/image: the audio tower gets no grad
+    opt.zero_grad(set_to_none=True)
+    loss.backward()
+    assert m.model.arena_image.grad is not None and m.model.arena_audio.grad is None
+    opt.step()
     reps = torch.randn(8, 32, device="cuda", requires_grad=True)
     lv = m.nt_xent_loss(reps)
     lv.backward()

@@ -180,16 +180,22 @@ def test_unimodal_bf16_step_close_to_oracle(kind):
 
 
 def test_lightning_api_unimodal():
-    """UniModalDINOLightning surface: training_step -> backward_and_step, cosine loss API."""
+    """UniModalDINOLightning surface: training_step -> zero_grad -> backward -> optimizer.step
+    (Lightning's automatic optimisation), cosine loss API."""
     from avdino.models import UNIMODAL_MODEL_MAP, UniModalDINOLightning
     m = UniModalDINOLightning(encoder_class=UNIMODAL_MODEL_MAP["image_simple"], output_dim=64,
                               projection_dim=32, dropout=0.0, precision="32", device="cuda",
                               cosine_loss_alpha=0.3)
     b = make_multimodal_batch(4, 2, 2, 77, with_originals=False)
     views = tuple(torch.from_numpy(b[k]) for k in ("g_img", "g_aud", "l_img", "l_aud"))
+    opt = m.configure_optimizers()["optimizer"]
+    pre = m.model.store.student.clone()
     loss = m.training_step(views, 0)
-    m.backward_and_step()
+    opt.zero_grad()
+    loss.backward()
+    opt.step()
     assert np.isfinite(loss.item())
+    assert m.model.arena.grad is not None and not torch.equal(pre, m.model.store.student)
     e = torch.randn(4, 5, 16, device="cuda", requires_grad=True)
     c = m._cosine_consistency_loss(e)
     c.backward()

@@ -39,9 +39,11 @@ def test_run_dino_two_epochs_on_device(argv, capsys):
     import json
     from avdino import run_dino as R
     m = R.main(argv + ["--config", CFG, "--epochs", "2", "--steps-per-epoch", "3",
-                       "--batch-size", "8", "--probe-batches", "2"])
+                       "--batch-size", "8", "--probe-batches", "2", "--synthetic"])
     recs = [json.loads(line) for line in capsys.readouterr().out.splitlines() if line.startswith("{")]
     assert len(recs) == 2 and all(r["train_loss"] == r["train_loss"] for r in recs)
     assert 0 <= recs[-1]["mlp_acc"] <= 100
-    assert recs[1]["lr"] < recs[0]["lr"] < 1e-4         # CosineAnnealingLR(T_max=num_epochs)
-    assert m.model.engine.step_idx == 6 if hasattr(m.model.engine, "step_idx") else True
+    # lr used in each epoch: CosineAnnealingLR(T_max=num_epochs) stepped per epoch
+    assert recs[1]["lr"] < recs[0]["lr"] == pytest.approx(1e-4)
+    assert m.model.engine.step_idx == 6
+    assert m.trainer_.global_step == 6
