@@ -257,7 +257,7 @@ def test_ws_kernels_many_tiles_per_block(ops, shape, cap, monkeypatch):
 
     (y0, s0, dx0, dw0), (y1, s1, dx1, dw1) = _capped(monkeypatch, cap, run)
     assert torch.equal(y0, y1) and torch.equal(dx0, dx1)
-    assert grel(s1, s0) < 1e-6 and grel(dw1, dw0) < 1e-6
+    assert grel(s1, s0) < 1e-6 and grel(dw1, dw0) < 5e-6     # fp32 sum order
     assert grel(dw1, wgrad_ref(x, dy, K, pad)) < 1e-5
 
 
@@ -286,13 +286,32 @@ def test_conv1_wgrad_many_tiles_per_block(ops, cap, monkeypatch):
 
 
 # ---------------------------------------------------------------------------- whole step
+def _ref_grads(state, batch, E, D, P, autocast_dtype):
+    """The reference's step (oracle/torch_port.py restates its modules and ops) on the GPU,
+    fp32 or under torch.autocast(dtype) -- the reference's own mixed-precision mode is
+    '16-mixed' (run_dino.py:360); bf16 autocast is the same recipe in our storage type."""
+    from oracle import torch_port as TP
+    torch.manual_seed(0)
+    m = TP.DinoMSE(E, D, P, dropout=0.0, fusion_dropout=0.0).cuda()
+    m.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state.items()}, strict=True)
+    b = batch
+    with torch.autocast("cuda", dtype=autocast_dtype or torch.float32, enabled=autocast_dtype is not None):
+        fi, fa, s_, t_ = m(b["image"], b["audio"], b["g_img"], b["g_aud"], b["l_img"], b["l_aud"])
+        loss = TP.dino_loss(s_.float(), t_.float()) + TP.mse_loss(fi.float(), fa.float())
+    loss.backward()
+    return loss.item(), {k: p.grad.detach().to(F64).clone() for k, p in m.named_parameters()
+                         if p.grad is not None}
+
+
 def test_bf16_step_vs_fp32_step_config2(capsys):
     """The benchmarked bf16 step at config-2 size (B = 1024, 2 global + 4 local views, mse,
-    E = D = 256, P = 128) against the fp32 engine from identical parameters and inputs.  The
-    bf16 path rounds every stored activation and conv operand once (2^-9 relative); the bounds
-    below are what that rounding allows for a 4-layer conv stack with batch statistics (the
-    measured errors are printed): loss 2e-3 relative, per-tensor gradient rel-L2 median 2e-2 and
-    worst 1e-1 over tensors with a non-negligible gradient."""
+    E = D = 256, P = 128) against the fp32 engine from identical parameters and inputs, with
+    per-tensor bounds taken from the REFERENCE's own mixed precision: the same step in the
+    reference's ops (torch_port) under bf16 autocast vs fp32, on the GPU.  At initialisation
+    the conv-weight / BN gradients are small sums of large cancelling terms, so one bf16
+    rounding of the stored maps moves them by ~10 % -- in the reference's recipe as in ours.
+    Bounds: loss 1e-3 relative; every tensor within 2x the reference's bf16-autocast error
+    (floor 1e-2); the median within 1.25x; printed with the fp16-autocast ('16-mixed') errors."""
     from avdino.engine import Hyper, MultiCentralEngine
     from avdino.params import ParamStore
     from avdino.spec import multimodal_dino_sd
@@ -317,14 +336,26 @@ def test_bf16_step_vs_fp32_step_config2(capsys):
         loss = eng.forward(batch).item()
         eng.backward()
         out[name] = (loss, {k: store.grad_of(k).detach().to(F64).clone() for k in store.live_keys})
+    ref = {n: _ref_grads(state, batch, E, D, P, a) for n, a in
+           (("f32", None), ("bf16", torch.bfloat16), ("f16", torch.float16))}
     (l32, g32), (l16, g16) = out["f32"], out["bf16"]
-    errs = {k: grel(g16[k], g32[k]) for k in g32 if g32[k].norm().item() > 1e-6 * max(
-        v.norm().item() for v in g32.values())}
-    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:6]
-    med = float(np.median(list(errs.values())))
+    big = max(v.norm().item() for v in g32.values())
+    keys = [k for k in g32 if g32[k].norm().item() > 1e-6 * big]
+    ours = {k: grel(g16[k], g32[k]) for k in keys}
+    rbf = {k: grel(ref["bf16"][1][k], ref["f32"][1][k]) for k in keys}
+    rfp = {k: grel(ref["f16"][1][k], ref["f32"][1][k]) for k in keys}
+    ratio = sorted(((ours[k] / max(rbf[k], 1e-2), k) for k in keys), reverse=True)
+    med = (float(np.median(list(ours.values()))), float(np.median(list(rbf.values()))),
+           float(np.median(list(rfp.values()))))
     with capsys.disabled():
         print(f"\nbf16 vs fp32 step (B=1024): loss {l16:.6f} vs {l32:.6f} "
-              f"(rel {abs(l16 - l32) / abs(l32):.2e}); grad rel-L2 median {med:.2e}; worst {worst}")
-    assert abs(l16 - l32) / abs(l32) < 2e-3
-    assert med < 2e-2
-    assert worst[0][1] < 1e-1, worst
+              f"(rel {abs(l16 - l32) / abs(l32):.2e}); fp32 engine vs fp32 reference loss "
+              f"{abs(l32 - ref['f32'][0]):.2e}")
+        print(f"grad rel-L2 median: ours bf16 {med[0]:.3e}, reference bf16-autocast {med[1]:.3e}, "
+              f"reference fp16-autocast {med[2]:.3e}")
+        for r, k in ratio[:8]:
+            print(f"  {k}: ours {ours[k]:.3e} ref-bf16 {rbf[k]:.3e} ref-fp16 {rfp[k]:.3e}")
+    assert abs(l32 - ref["f32"][0]) < 1e-4
+    assert abs(l16 - l32) / abs(l32) < 1e-3
+    assert ratio[0][0] < 2.0, ratio[:4]
+    assert med[0] < 1.25 * med[1], med

@@ -203,3 +203,65 @@ def test_linear_probe_matches_reference(case, variant):
     _check_all(fx, [("logits", r["logits"])], orel)
     _check_all(fx, [("cls/" + k, v) for k, v in r["classifier"].items()], srel)
     _check_all(fx, [("rs/" + k, v) for k, v in r["running"].items()], srel)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("case", ["downstream_multi_central", "downstream_image_simple"])
+def test_downstream_matches_reference(case, variant):
+    """compute_accuracies' evaluations (run_dino.py:481-501), fixtures from the reference's own
+    train_knn_classifier + train_downstream + compute_classification_metrics
+    (dino_train.py:47-102, 188-369): frozen eval-mode features, sklearn kNN(5) predictions and
+    neighbours, the 3-epoch AdamW + cosine-LR MLP probe's per-epoch (train loss, val loss, val
+    accuracy), the best-val checkpoint's test predictions / accuracy / classifier / copy
+    running statistics."""
+    fx = gu.load(case + variant)
+    lt, orel, grel, srel, floor, _ = TOL[variant]
+    E, D, P, B, nt, nv, ne, epochs, pseed, bseed = [int(x) for x in fx["meta_dims"]]
+    kind, lr = str(fx["meta_kind"]), float(fx["meta_lr"])
+    spec = (S.multimodal_dino_spec("default", E, D, P) if kind == "multi_central"
+            else S.unimodal_dino_spec(kind, D, P))
+    state = make_state(spec, pseed)
+    cls = make_state(S.classifier_spec(D), pseed + 1)
+    train = [make_multimodal_batch(B, 1, 0, bseed + i) for i in range(nt)]
+    valid = [make_multimodal_batch(B, 1, 0, bseed + 1000 + i) for i in range(nv)]
+    test = [make_multimodal_batch(B, 1, 0, bseed + 2000 + i) for i in range(ne)]
+    fe = O._ProbeModel(state, kind, cls)
+    trf = np.concatenate([fe.features(b, True) for b in train])
+    tef = np.concatenate([fe.features(b, True) for b in test])
+    _check_all(fx, [("feat_train", trf), ("feat_test", tef)], orel)
+    pred, nbr = O.knn_classify(trf, np.concatenate([b["label"] for b in train]), tef, 5)
+    np.testing.assert_array_equal(pred, fx["knn_pred"])
+    np.testing.assert_array_equal(nbr, fx["knn_nbr"])
+    tel = np.concatenate([b["label"] for b in test])
+    assert 100 * np.mean(pred == tel) == pytest.approx(float(fx["knn_acc"]))
+    r = O.train_downstream(state, kind, train, valid, test, cls, epochs, lr)
+    np.testing.assert_allclose(r["history"][:, :2], fx["history"][:, :2], atol=lt, rtol=0)
+    np.testing.assert_array_equal(r["history"][:, 2], fx["history"][:, 2])
+    np.testing.assert_array_equal(r["test_preds"], fx["test_preds"])
+    np.testing.assert_array_equal(tel, fx["test_labels"])
+    assert r["test_acc"] == pytest.approx(float(fx["test_acc"]))
+    _check_all(fx, [("cls/" + k, v) for k, v in r["classifier"].items()], srel)
+    _check_all(fx, [("rs/" + k, v) for k, v in r["running"].items()], srel)
+
+
+def test_knn_oracle_matches_sklearn():
+    """The kNN restatement == sklearn.neighbors.KNeighborsClassifier(5) (the library the
+    reference calls, dino_train.py:362) on its brute-force path (what 'auto' picks for more
+    than 15 feature dimensions -- the reference's features are 256-dim), incl. 2-2-1 vote ties
+    (to the smallest class).  Exact distance ties (measure zero for continuous features) are
+    outside the contract: sklearn resolves them in its heap's order, not by index."""
+    sk = pytest.importorskip("sklearn.neighbors")
+    g = np.random.default_rng(7)
+    ties = 0
+    for n, m, d, c in ((200, 120, 32, 10), (300, 400, 16, 4), (120, 300, 20, 3), (500, 500, 256, 10)):
+        X = g.normal(size=(n, d))
+        Q = g.normal(size=(m, d))
+        y = g.integers(0, c, n)
+        knn = sk.KNeighborsClassifier(n_neighbors=5).fit(X, y)
+        assert knn._fit_method == "brute"
+        pred, nbr = O.knn_classify(X, y, Q, 5)
+        np.testing.assert_array_equal(pred, knn.predict(Q))
+        np.testing.assert_array_equal(nbr, knn.kneighbors(Q, return_distance=False))
+        votes = np.stack([np.bincount(y[r], minlength=c) for r in nbr])
+        ties += int(((votes == votes.max(1, keepdims=True)).sum(1) > 1).sum())
+    assert ties > 50        # the vote tie-break was exercised
