@@ -30,12 +30,19 @@ import torch  # noqa: E402
 METRIC = "AVMNIST audio-image pairs/sec (multimodal DINO step) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_PEAK_TFS = {"bf16": 2500.0, "f32": 157.3}   # dense, no sparsity
+# SURVEY 8(d) "BN-barrier" algorithmic HBM bytes per pair of a whole training step (inputs read
+# once, each train-mode-BN'd conv output written once and read once forward, saved output read
+# + its gradient written / read backward; weights amortised), bf16 storage; f32 doubles them
+STEP_BYTES_PER_PAIR_BF16 = {"mse": 17.37e6, "infonce": 17.37e6, "semi_supervised": 17.37e6,
+                            "default": 15.15e6, "simclr": 8.0e6, "uni": 1.24e6}
+STEP_FLOPS_PER_PAIR = {"mse": 1794.6e6, "infonce": 1794.6e6, "semi_supervised": 1793.9e6,
+                       "default": 1561.1e6, "simclr": 1104.3e6, "uni": 124.6e6}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None,
                     help="pairs per GPU per step (default: the workload's BASELINE config)")
@@ -47,10 +54,14 @@ def parse():
                          "with all-gathered NT-Xent negatives, B=2048/GPU (config 4)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="launch every kernel from Python each step instead of replaying the "
+                         "captured hipGraph of the step")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) for real runs; gloo only to rehearse N>1 with several "
                          "ranks sharing one GPU")
-    ap.add_argument("--cpu-batch", type=int, default=32)
+    ap.add_argument("--cpu-batch", type=int, default=1024,
+                    help="pairs per CPU step (config 2's B; the sample is >= 2 timed steps)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--probe-dominant", type=int, default=0, metavar="K",
                     help="after warm-up, replay only the dominant launch K times and exit "
@@ -158,10 +169,13 @@ def cpu_baseline(batch, seconds):
     def px(*shape):
         return torch.randint(0, 256, shape, generator=g).float() / 255.0
 
-    b = {"g_img": px(batch, 2, 1, 28, 28), "g_aud": px(batch, 2, 1, 112, 112),
-         "l_img": px(batch, 4, 1, 28, 28), "l_aud": px(batch, 4, 1, 112, 112),
-         "image": px(batch, 1, 28, 28), "audio": px(batch, 1, 112, 112)}
-    TP.train_step(model, opt, b)  # warm-up
+    def mk(n):
+        return {"g_img": px(n, 2, 1, 28, 28), "g_aud": px(n, 2, 1, 112, 112),
+                "l_img": px(n, 4, 1, 28, 28), "l_aud": px(n, 4, 1, 112, 112),
+                "image": px(n, 1, 28, 28), "audio": px(n, 1, 112, 112)}
+
+    TP.train_step(model, opt, mk(32))  # warm-up (code paths, allocator) on a small batch
+    b = mk(batch)
     n, t0 = 0, time.perf_counter()
     while True:
         TP.train_step(model, opt, b)
@@ -171,8 +185,9 @@ def cpu_baseline(batch, seconds):
             break
     return {"value": round(batch * n / el, 2), "unit": "pairs/s", "cores": torch.get_num_threads(),
             "kind": "port",
-            "sample": f"oracle/torch_port.py multi_central mse step, fp32, B={batch}, 2 global + 4 local "
-                      f"views, {n} timed steps ({el:.1f} s) after 1 warm-up, torch CPU "
+            "sample": f"oracle/torch_port.py multi_central mse step (the reference's Lightning "
+                      f"training_step ops, dino.py:1214-1238), fp32, B={batch}, 2 global + 4 local "
+                      f"views, {n} timed steps ({el:.1f} s) after a B=32 warm-up step, torch CPU "
                       f"{torch.get_num_threads()} threads"}
 
 
@@ -199,22 +214,25 @@ def main():
     act = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     eng, pool, B, workload, model = build_workload(args, device, act, world, rank, avdist)
 
-    # warm-up, timing every instrumented kernel to find the dominant one (from the second
-    # warm-up step on: the first one's launches are cold)
+    # warm-up: eager steps (the second one times every instrumented kernel to find the dominant
+    # one; the first one's launches are cold), then -- graph mode -- the step's capture
+    use_graph = not args.no_graph and not args.probe_dominant
+    eng.use_graph = use_graph
+    eng.graph.warmup = min(2, max(args.warmup - 1, 0))
     ops.TIMER = None
     for i in range(args.warmup):
-        if i == min(1, args.warmup - 1):
-            ops.TIMER = ops.KernelTimer()
+        ops.TIMER = ops.KernelTimer() if i == min(1, args.warmup - 1) else None
         eng.step(pool[i % len(pool)])
-    summ = ops.TIMER.summary() if args.warmup else {}
+    summ = ops.TIMER.summary() if (args.warmup and ops.TIMER is not None) else {}
     dominant = max(summ, key=lambda k: summ[k]["ms"]) if summ else None
     if args.dominant:
         if args.dominant not in summ:
             raise SystemExit(f"--dominant {args.dominant!r}: no such launch key")
         dominant = args.dominant
-    ops.TIMER = ops.KernelTimer(only=dominant)
+    ops.TIMER = None if use_graph else ops.KernelTimer(only=dominant)
 
     if args.probe_dominant:
+        ops.TIMER = ops.KernelTimer(only=dominant)
         eng.step(pool[0])                 # captures the dominant launch (inputs stay live)
         torch.cuda.synchronize()
         fn = ops.TIMER.replay
@@ -233,6 +251,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = eng.step(pool[i % len(pool)])
+    t_issue = time.perf_counter() - t0
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -244,6 +263,14 @@ def main():
     lv = loss.item()
     if not math.isfinite(lv):
         raise SystemExit(f"non-finite loss {lv}")
+    if use_graph:
+        # the dominant launch's duration, HIP events around it, from eager steps after the
+        # timed region (inside a replayed graph there is no per-launch host hook)
+        eng.use_graph = False
+        ops.TIMER = ops.KernelTimer(only=dominant)
+        for i in range(3):
+            eng.step(pool[i % len(pool)])
+        torch.cuda.synchronize()
 
     timed = ops.TIMER.summary()
     if dominant is None and timed:
@@ -265,10 +292,25 @@ def main():
                 "traffic": load_traffic(args.traffic, dominant),
                 "avg_launch_us": round(avg_s * 1e6, 2),
                 "algorithmic_bytes": int(nb), "algorithmic_flops": int(fl),
-                "kernel_share_of_step": round(d["ms"] / (elapsed * 1e3), 4)}
+                "kernel_share_of_step": round(d["ms"] / (3 if use_graph else args.steps) /
+                                              (elapsed * 1e3 / args.steps), 4)}
 
     total_pairs = world * B * args.steps
     value = total_pairs / elapsed
+    # whole-step roofline: pairs/s per GPU against min(HBM ceiling, MFMA ceiling)
+    key = args.mode if args.workload == "dino" else args.workload
+    bpp = STEP_BYTES_PER_PAIR_BF16[key] * (1 if args.dtype == "bf16" else 2)
+    fpp = STEP_FLOPS_PER_PAIR[key]
+    ceil_hbm = HBM_PEAK_GBS * 1e9 / bpp
+    ceil_mfma = MFMA_PEAK_TFS[args.dtype] * 1e12 / fpp
+    per_gpu = value / world
+    step_roof = {"bound": "hbm" if ceil_hbm <= ceil_mfma else "mfma",
+                 "bytes_per_pair": bpp, "flops_per_pair": fpp,
+                 "ceiling_pairs_per_s_per_gpu": round(min(ceil_hbm, ceil_mfma), 1),
+                 "achieved_GBps": round(per_gpu * bpp / 1e9, 1),
+                 "achieved_TFLOPs": round(per_gpu * fpp / 1e12, 2),
+                 "frac": round(per_gpu / min(ceil_hbm, ceil_mfma), 4),
+                 "traffic_bytes_per_pair": load_traffic(args.traffic, "step:" + key)}
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "pairs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -279,6 +321,10 @@ def main():
                    "model": model, "global_batch": world * B, "seq_len": None,
                    "parallelism": f"dp{world}"},
         "roofline": roof,
+        "step_roofline": step_roof,
+        "timed_region_s": round(elapsed, 4),
+        "host_issue_ms_per_step": round(t_issue * 1e3 / args.steps, 3),
+        "graph": use_graph,
         "final_loss": round(lv, 6),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "dino" \

@@ -304,6 +304,15 @@ int avd_act_bwd(const float* x, const float* dout, float* dx, int act, const flo
                 const float* shift, int rows, int G, int C, float p, unsigned long long seed,
                 void* stream);
 
+/* The same with the dropout seed offset by *seed_off (device memory; the step state of
+ * avd_step_begin), so a captured step (hipGraph) draws fresh masks on every replay. */
+int avd_act_fwd_dev(const float* x, float* out, int act, const float* scale, const float* shift,
+                    int rows, int G, int C, float p, unsigned long long seed,
+                    const unsigned long long* seed_off, void* stream);
+int avd_act_bwd_dev(const float* x, const float* dout, float* dx, int act, const float* scale,
+                    const float* shift, int rows, int G, int C, float p, unsigned long long seed,
+                    const unsigned long long* seed_off, void* stream);
+
 /* BatchNorm1d backward partials: parts [C, G, R, 2] = (sum dz, sum dz*xhat) per row chunk. */
 int avd_bn1d_bwd_reduce(const float* x, const float* dz, const float* mean, const float* invstd,
                         int rows, int G, int C, float* parts, void* stream);
@@ -423,6 +432,21 @@ int avd_adam(float* p, const float* g, float* m, float* v, long long n, float lr
 int avd_adamw(float* p, const float* g, float* m, float* v, long long n, float lr, float b1,
               float b2, float eps, float wd, float bc1, float bc2, void* stream);
 
+/* Device step state of a graph-replayable training step (the engine's per-step scalars live
+ * in device memory, so one captured hipGraph replays every step):
+ *   t        [1] int64 -- optimizer steps taken; avd_step_begin increments it,
+ *   hyp      [4] f32   -- {lr (written by the host when the schedule moves), 1-b1^t, 1-b2^t, -}
+ *                         (bias corrections in double, rounded once, as the host computes them),
+ *   seed_off [1] u64   -- t_before * seed_stride, the dropout counter offset of this step
+ *                         (may be NULL).
+ * avd_adam_dev / avd_adamw_dev read lr and the bias corrections from hyp. */
+int avd_step_begin(long long* t, float* hyp, unsigned long long* seed_off, double b1, double b2,
+                   unsigned long long seed_stride, void* stream);
+int avd_adam_dev(float* p, const float* g, float* m, float* v, long long n, const float* hyp,
+                 float b1, float b2, float eps, float wd, void* stream);
+int avd_adamw_dev(float* p, const float* g, float* m, float* v, long long n, const float* hyp,
+                  float b1, float b2, float eps, float wd, void* stream);
+
 /* Eval-mode BatchNorm coefficients from running statistics: scale = gamma / sqrt(rv + eps),
  * shift = beta - rm * scale, [C] each (feed avd_cl_bn_relu_pool with G = 1). */
 int avd_bn_eval_coef(const float* gamma, const float* beta, const float* running_mean,
@@ -445,12 +469,15 @@ int avd_row_sqnorm(const float* x, int N, int D, float* out, void* stream);
 /* kNN selection and vote (train_knn_classifier, dino_train.py:349-369: sklearn
  * KNeighborsClassifier(n_neighbors=K), brute-force euclidean, uniform weights).  For test row
  * i the distance to train row j ranks as xnorm[j] + S[i*ldS + j] where S = -2 Q X^T comes
- * from avd_gemm (the test row's own norm is common to the row).  nbr [M, K] (may be NULL)
- * receives the K nearest train indices in increasing distance (ties: smaller index); pred [M]
- * the class with the most votes among labels[nbr] (ties: the smallest class, as sklearn's
- * argmax over class counts).  K <= 16, C <= 64. */
+ * from avd_gemm (the test row's own norm is common to the row).  With Q [M, D] / X [N, D]
+ * (may be NULL) the min(16, N) best candidates of that ranking are re-ranked by their direct
+ * distance sum_k (q_k - x_jk)^2 (no norm cancellation).  nbr [M, K] (may be NULL) receives the
+ * K nearest train indices in increasing distance (ties: smaller index); pred [M] the class
+ * with the most votes among labels[nbr] (ties: the smallest class, as sklearn's argmax over
+ * class counts).  K <= 16, C <= 64; labels are class indices 0..C-1. */
 int avd_knn_select(const float* S, long long ldS, const float* xnorm, int M, int N, int K,
-                   const int64_t* labels, int C, int64_t* nbr, int64_t* pred, void* stream);
+                   const float* Q, const float* X, int D, const int64_t* labels, int C,
+                   int64_t* nbr, int64_t* pred, void* stream);
 
 /* idx[r] = argmax_j logits[r*ld + j], first maximum (torch.max(outputs, 1) in
  * compute_classification_metrics, dino_train.py:76). */

@@ -16,6 +16,7 @@ I = ctypes.c_int
 L = ctypes.c_longlong
 F = ctypes.c_float
 U64 = ctypes.c_ulonglong
+D = ctypes.c_double
 
 # name -> argtypes (restype is always c_int except where noted)
 PROTOS = {
@@ -60,6 +61,11 @@ PROTOS = {
     "avd_colstats": [P, I, I, I, P, P, P],
     "avd_act_fwd": [P, P, I, P, P, I, I, I, F, U64, P],
     "avd_act_bwd": [P, P, P, I, P, P, I, I, I, F, U64, P],
+    "avd_act_fwd_dev": [P, P, I, P, P, I, I, I, F, U64, P, P],
+    "avd_act_bwd_dev": [P, P, P, I, P, P, I, I, I, F, U64, P, P],
+    "avd_step_begin": [P, P, P, D, D, U64, P],
+    "avd_adam_dev": [P, P, P, P, L, P, F, F, F, F, P],
+    "avd_adamw_dev": [P, P, P, P, L, P, F, F, F, F, P],
     "avd_bn1d_bwd_reduce": [P, P, P, P, I, I, I, P, P],
     "avd_bn1d_bwd_apply": [P, P, P, P, I, I, I, P],
     "avd_dino_loss": [P, P, P, I, I, I, I, F, F, F, I, P, P, P, P, P],
@@ -78,7 +84,7 @@ PROTOS = {
     "avd_stage_views": [P, I, P, I, P, I, I, P, I, P],
     "avd_augment_views": [P, P, L, I, I, I, I, P, P, P, I, I, U64, I, P, P],
     "avd_row_sqnorm": [P, I, I, P, P],
-    "avd_knn_select": [P, L, P, I, I, I, P, I, P, P, P],
+    "avd_knn_select": [P, L, P, I, I, I, P, P, I, P, I, P, P, P],
     "avd_argmax_rows": [P, L, I, I, P, P],
 }
 

@@ -135,8 +135,9 @@ class DownstreamClassifier(nn.Module):
 class KNeighborsClassifier:
     """sklearn.neighbors.KNeighborsClassifier(n_neighbors) with algorithm='brute',
     metric='euclidean', weights='uniform' (what 'auto' picks for 256-dim features), on the
-    device: ranking by |x_j|^2 - 2 q.x_j from one exact-f32 MFMA GEMM per query chunk, top-k
-    (ties to the smaller train index) and majority vote (ties to the smallest class)."""
+    device: candidates by |x_j|^2 - 2 q.x_j from one exact-f32 MFMA GEMM per query chunk, the
+    best 16 re-ranked by their direct distance, top-k (ties to the smaller train index) and
+    majority vote (ties to the smallest class)."""
 
     def __init__(self, n_neighbors=5, query_chunk=4096):
         self.n_neighbors = n_neighbors
@@ -170,7 +171,8 @@ class KNeighborsClassifier:
             ops.gemm(m, N, D, Q, D, 1, self._X, 1, D, S, N, alpha=-2.0, a_off=a * D,
                      mode=ops.GEMM_F32_MFMA)
             ops.knn_select(S, N, self._xnorm, m, N, K, self._y, len(self.classes_),
-                           None if nbr is None else nbr[a:a + m], pred[a:a + m])
+                           None if nbr is None else nbr[a:a + m], pred[a:a + m],
+                           Q=Q[a:a + m], X=self._X, D=D)
         return pred, nbr
 
     def predict(self, Q):

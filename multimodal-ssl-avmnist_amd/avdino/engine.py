@@ -284,7 +284,7 @@ class ProjHead:
         self.gm = gemm_mode
 
     def forward(self, ws, store, tag, x, rows, out, drop_p=0.0, seed=0, x_ld=None, x_off=0,
-                update_running=True, G=1):
+                update_running=True, G=1, seed_off=None):
         """G > 1: the rows are G separate calls of the head (BatchNorm1d statistics and running
         updates per call, in order), e.g. SimCLR's image-image mode."""
         p, Hd = self.p, self.h
@@ -304,10 +304,11 @@ class ProjHead:
         if update_running:
             store.bump_nbt(p + ".mlp.1.num_batches_tracked", G)
         a = ws.get(f"{tag}.a", rows * Hd)
-        ops.act_fwd(h, a, 1, st[2], st[3], rows, G, Hd, drop_p, seed)
+        ops.act_fwd(h, a, 1, st[2], st[3], rows, G, Hd, drop_p, seed, seed_off)
         ops.linear_fwd(a, store[p + ".mlp.4.weight"], store[p + ".mlp.4.bias"], out, rows, mode=self.gm)
         return {"x": x, "x_ld": x_ld if x_ld is not None else self.i, "x_off": x_off, "h": h,
-                "a": a, "st": st, "rows": rows, "G": G, "drop_p": drop_p, "seed": seed}
+                "a": a, "st": st, "rows": rows, "G": G, "drop_p": drop_p, "seed": seed,
+                "seed_off": seed_off}
 
     def backward(self, ws, store, ctx, dout, dx, dx_ld=None, dx_off=0):
         p, Hd, rows, G = self.p, self.h, ctx["rows"], ctx["G"]
@@ -317,7 +318,8 @@ class ProjHead:
                        store.grad_of(p + ".mlp.4.bias"), da, rows, mode=self.gm)
         st = ctx["st"]
         dz = ws.get("head_dz", rows * Hd)
-        ops.act_bwd(ctx["h"], da, dz, 1, st[2], st[3], rows, G, Hd, ctx["drop_p"], ctx["seed"])
+        ops.act_bwd(ctx["h"], da, dz, 1, st[2], st[3], rows, G, Hd, ctx["drop_p"], ctx["seed"],
+                    ctx.get("seed_off"))
         R = ops.colstats_parts(rpg)
         parts = ws.get("bwd_parts", Hd * G * R * 2)
         ops.bn1d_bwd_reduce(ctx["h"], dz, st[0], st[1], rows, G, Hd, parts)
@@ -341,6 +343,75 @@ class Hyper:
         self.dropout, self.fusion_dropout = dropout, fusion_dropout
         self.alpha = alpha
         self.betas, self.eps = betas, eps
+
+
+SEED_MASK = 0xFFFFFFFFFFFF
+
+
+class StepState:
+    """The per-step scalars of a training step in device memory (avd_step_begin): the optimizer
+    step count, lr and Adam bias corrections, and the dropout counter offset.  Kernels read them
+    from there, so a step captured once as a hipGraph replays every later step exactly as the
+    eager step would run it (fresh dropout masks, the right bias corrections).  The host keeps
+    no copy that can drift: ``t`` and ``seed_off`` advance only on the device."""
+
+    SEED_STRIDE = 16
+
+    def __init__(self, device, lr, betas=(0.9, 0.999)):
+        self.t = torch.zeros(1, dtype=torch.int64, device=device)
+        self.seed_off = torch.zeros(1, dtype=torch.int64, device=device)
+        self.hyp = torch.zeros(4, dtype=torch.float32, device=device)
+        self.b1, self.b2 = betas
+        self.lr = None
+        self.set_lr(lr)
+
+    def set_lr(self, lr):
+        """Host-side schedule change (eager, outside any captured graph)."""
+        if lr != self.lr:
+            self.hyp[0:1].fill_(lr)
+            self.lr = lr
+
+    def begin(self, seed=True):
+        """seed_off = t * 16; t += 1; hyp[1:3] = 1 - beta^t."""
+        ops.step_begin(self.t, self.hyp, self.seed_off if seed else None, self.b1, self.b2,
+                       self.SEED_STRIDE)
+
+
+def adam_step_dev(store, hp, sstate, lo=0, n=None):
+    """adam_step with lr / bias corrections from the device StepState (graph-replayable)."""
+    n = store.n_live - lo if n is None else n
+    b1, b2 = hp.betas
+    ops.adam_dev(store.student[lo:lo + n], store.grad[lo:lo + n], store.adam_m[lo:lo + n],
+                 store.adam_v[lo:lo + n], n, sstate.hyp, b1, b2, hp.eps, hp.wd)
+
+
+class GraphedStep:
+    """A training step's device work captured once per input shape as a hipGraph
+    (torch.cuda.CUDAGraph over HIP stream capture, side streams joined by events) and replayed:
+    one host call per step instead of ~230 launches.  The first ``warmup`` calls per shape run
+    eagerly (they size every workspace), the next one captures."""
+
+    def __init__(self, warmup=2):
+        self.warmup = warmup
+        self.graphs = {}
+        self.seen = {}
+
+    def run(self, key, body):
+        g = self.graphs.get(key)
+        if g is not None:
+            g.replay()
+            return
+        n = self.seen.get(key, 0)
+        if n < self.warmup:
+            self.seen[key] = n + 1
+            body()
+            return
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="relaxed"):
+            body()
+        self.graphs[key] = g
+        g.replay()          # the capture itself executed nothing
 
 
 def adam_step(store, hp):
@@ -396,6 +467,9 @@ class MultiCentralEngine:
         self.step_idx = 0
         self.fwd_count = 0     # forwards so far (a backward belongs to the latest one)
         self.last = {}
+        self.sstate = StepState(store.device, hp.lr, hp.betas)
+        self.use_graph = False     # step(): capture the device work once, replay it (bench)
+        self.graph = GraphedStep()
 
     # student image branch on the side stream, concurrently with the audio branch: measured
     # slower (r1_39: 149.7k vs 152.4k pairs/s -- both branches' launches fill the chip, so
@@ -455,14 +529,16 @@ class MultiCentralEngine:
         ops.linear_fwd(cat, st[prefix + ".fusion.0.weight"], st[prefix + ".fusion.0.bias"], h, rows,
                        x_ld=2 * E, mode=self.gm)
         r = ws.get(tag + ".fr", rows * E)
-        ops.act_fwd(h, r, 0, None, None, rows, 1, E, self.hp.fusion_dropout, seed)
+        ops.act_fwd(h, r, 0, None, None, rows, 1, E, self.hp.fusion_dropout, seed,
+                    self.sstate.seed_off)
         out = ws.get(tag + ".fout", rows * D)
         ops.linear_fwd(r, st[prefix + ".fusion.3.weight"], st[prefix + ".fusion.3.bias"], out, rows,
                        mode=self.gm)
         return out, (h, r)
 
     def stage(self, batch, with_orig):
-        """Device batch dict -> view-major staged image/audio inputs (act dtype)."""
+        """Device batch dict -> view-major staged image/audio inputs (act dtype) and the labels,
+        in fixed workspace buffers (what a captured step reads)."""
         ws = self.ws
         g_img, l_img = batch["g_img"], batch["l_img"]
         B, G = g_img.shape[:2]
@@ -474,21 +550,30 @@ class MultiCentralEngine:
                         batch["image"].contiguous() if with_orig else None, B, 784, x_img)
         ops.stage_views(batch["g_aud"].contiguous(), G, batch["l_aud"].contiguous() if L else None, L,
                         batch["audio"].contiguous() if with_orig else None, B, 12544, x_aud)
-        return x_img, x_aud, B, G, L
+        labels = None
+        if self.mode == "semi_supervised":
+            labels = ws.get("in.label", B, torch.int64)
+            labels.copy_(batch["label"].reshape(-1))
+        return x_img, x_aud, B, G, L, labels
 
     # -------------------------------------------------------------- the step
     def forward(self, batch, training=True):
         # training=False skips the input-grad weight layouts (forward-only use of the API)
         """Forward of the whole step; fills self.last with everything backward needs.
-        Returns device tensors (s_out [V,B,P], t_out [G,B,P] centred, head outputs or None)."""
+        Returns the loss (a device scalar in the workspace)."""
+        return self._forward_staged(self.stage(batch, self.heads is not None), training)
+
+    def _forward_staged(self, staged, training=True):
         hp, ws, st = self.hp, self.ws, self.store
         E, D, P = self.E, self.D, self.P
         with_orig = self.heads is not None
-        x_img, x_aud, B, G, L = self.stage(batch, with_orig)
+        x_img, x_aud, B, G, L, labels = staged
         V = G + L
         NG = V + (1 if with_orig else 0)   # BN groups of the student pass
         N = NG * B
-        base = (self.seed * 1000003 + self.step_idx * 16) & 0xFFFFFFFFFFFF
+        if training:
+            self.sstate.begin()        # dropout offset of this step, optimizer step count
+        base = (self.seed * 1000003) & SEED_MASK
 
         # teacher: global views (prefix of the staged buffers), train-mode BN, no grad -- on a
         # side stream, concurrently with the student (independent until the loss)
@@ -533,7 +618,7 @@ class MultiCentralEngine:
                 elif self.mode == "infonce":
                     self._infonce(zi, za, B, no, aux, dzi, dza)
                 else:
-                    self._supervised(zi, za, batch["label"], B, no, aux, dzi, dza, hws)
+                    self._supervised(zi, za, labels, B, no, aux, dzi, dza, hws)
                 if hp.alpha != 1.0:
                     aux.mul_(hp.alpha)
                     dzi.mul_(hp.alpha)
@@ -547,7 +632,8 @@ class MultiCentralEngine:
             n_parts = V * B + B
         fout, sfus = self._fusion_fwd("student", cat, V * B, "s", base + 1)
         s_proj = ws.get("s_proj", V * B * P)
-        spc = self.sproj.forward(ws, st, "sp", fout, V * B, s_proj, hp.dropout, base + 3)
+        spc = self.sproj.forward(ws, st, "sp", fout, V * B, s_proj, hp.dropout, base + 3,
+                                 seed_off=self.sstate.seed_off)
         self._join(t_done)
 
         # DINO loss (+ centring and centre EMA) -- forward and d/ds in one pass
@@ -624,7 +710,7 @@ class MultiCentralEngine:
                        st.grad_of("student.fusion.3.bias"), dr, V * B, mode=self.gm)
         dh = ws.get("fus_dh", V * B * E)
         ops.act_bwd(h, dr, dh, 0, None, None, V * B, 1, E, self.hp.fusion_dropout,
-                    (self.seed * 1000003 + self.step_idx * 16 + 1) & 0xFFFFFFFFFFFF)
+                    ((self.seed * 1000003) & SEED_MASK) + 1, self.sstate.seed_off)
         ops.linear_bwd(dh, c["cat"], st["student.fusion.0.weight"], st.grad_of("student.fusion.0.weight"),
                        st.grad_of("student.fusion.0.bias"), dcat, V * B, x_ld=2 * E, dx_ld=2 * E,
                        mode=self.gm)
@@ -649,19 +735,38 @@ class MultiCentralEngine:
         self.aud.backward(ws, st, caud, dfa)
         self._join(i_done)
 
+    def _graphable(self):
+        # InfoNCE's global negatives put collectives inside the forward: eager there
+        from . import dist as avdist
+        return not (self.mode == "infonce" and self.negatives != "local" and avdist.world(self.group) > 1)
+
     def step(self, batch):
-        """One full training step; returns the loss as a device tensor (no host sync)."""
+        """One full training step; returns the loss as a device tensor (no host sync).
+        With ``use_graph`` everything after the input staging (and around the data-parallel
+        collectives) is a captured hipGraph replayed per step."""
         if self.buffer_hook is not None:
             self.buffer_hook(self.store)
-        loss = self.forward(batch, training=True)
-        self.update_center()
-        ema_step(self.store, self.hp.momentum)     # update_teacher: pre-step student
-        self.backward()
+        self.sstate.set_lr(self.hp.lr)
+        staged = self.stage(batch, self.heads is not None)
+
+        def body():
+            self._forward_staged(staged, training=True)
+            self.update_center()
+            ema_step(self.store, self.hp.momentum)     # update_teacher: pre-step student
+            self.backward()
+            if self.grad_hook is None:
+                adam_step_dev(self.store, self.hp, self.sstate)
+
+        if self.use_graph and self._graphable():
+            self.graph.run(staged[2:5], body)
+        else:
+            body()
         if self.grad_hook is not None:
             self.grad_hook(self.store.grad)
-        adam_step(self.store, self.hp)
+            adam_step_dev(self.store, self.hp, self.sstate)
+        self.store.adam_step += 1
         self.step_idx += 1
-        return loss
+        return self.last["loss"]
 
     def last_head_outputs(self):
         """(image head output, audio head output) [B, P or classes] of the last forward."""
@@ -755,6 +860,9 @@ class UniModalEngine:
         self.seed, self.step_idx = seed, 0
         self.fwd_count = 0
         self.last = {}
+        self.sstate = StepState(store.device, hp.lr, hp.betas)
+        self.use_graph = False
+        self.graph = GraphedStep()
 
     def stage(self, batch):
         key = "img" if self.modality == "image" else "aud"
@@ -768,15 +876,21 @@ class UniModalEngine:
         return x, B, G, L
 
     def forward(self, batch, training=True):
+        return self._forward_staged(self.stage(batch), training)
+
+    def _forward_staged(self, staged, training=True):
         hp, ws, st, D, P = self.hp, self.ws, self.store, self.D, self.P
-        x, B, G, L = self.stage(batch)
+        x, B, G, L = staged
         V = G + L
         HW = self.enc.hw * self.enc.hw
-        base = (self.seed * 1000003 + self.step_idx * 16) & 0xFFFFFFFFFFFF
+        if training:
+            self.sstate.begin()
+        base = (self.seed * 1000003) & SEED_MASK
         emb, sctx = self.enc.forward(ws, st, "s", x, V * B, V, need_dgrad=training)
         temb, _ = self.t_enc.forward(ws, st, "t", x[:G * B * HW], G * B, G, need_dgrad=False)
         s_proj = ws.get("s_proj", V * B * P)
-        spc = self.sproj.forward(ws, st, "sp", emb, V * B, s_proj, hp.dropout, base + 3)
+        spc = self.sproj.forward(ws, st, "sp", emb, V * B, s_proj, hp.dropout, base + 3,
+                                 seed_off=self.sstate.seed_off)
         t_proj = ws.get("t_proj", G * B * P)
         self.tproj.forward(ws, st, "tp", temb, G * B, t_proj, 0.0, 0)
         cos = self.cos_alpha > 0 and V >= 2
@@ -816,15 +930,27 @@ class UniModalEngine:
     def step(self, batch):
         if self.buffer_hook is not None:
             self.buffer_hook(self.store)
-        loss = self.forward(batch, training=True)
-        self.update_center()
-        ema_step(self.store, self.hp.momentum)
-        self.backward()
+        self.sstate.set_lr(self.hp.lr)
+        staged = self.stage(batch)
+
+        def body():
+            self._forward_staged(staged, training=True)
+            self.update_center()
+            ema_step(self.store, self.hp.momentum)
+            self.backward()
+            if self.grad_hook is None:
+                adam_step_dev(self.store, self.hp, self.sstate)
+
+        if self.use_graph:
+            self.graph.run(staged[1:], body)
+        else:
+            body()
         if self.grad_hook is not None:
             self.grad_hook(self.store.grad)
-        adam_step(self.store, self.hp)
+            adam_step_dev(self.store, self.hp, self.sstate)
+        self.store.adam_step += 1
         self.step_idx += 1
-        return loss
+        return self.last["loss"]
 
     def outputs(self):
         """(s_out [V,B,P], t_out [G,B,P] centred with the pre-update centre, embeddings [V,B,D])
@@ -868,6 +994,10 @@ class SimCLREngine:
         self.ranges = [store.group_range(i) for i in range(2)]
         self.fwd_count = 0
         self.last = {}
+        # one optimizer step count per tower (torch.optim.Adam keeps per-parameter steps)
+        self.sstates = [StepState(store.device, hp.lr, hp.betas) for _ in range(2)]
+        self.use_graph = False
+        self.graph = GraphedStep()
 
     def draw_mode(self):
         return int(torch.randint(0, 4, (1,), generator=self.gen).item())
@@ -881,17 +1011,27 @@ class SimCLREngine:
                         len(views) - 1, None, B, HW, x)
         return x
 
+    def stage(self, batch, mode):
+        """The mode's input views into fixed workspace buffers."""
+        if mode in (0, 1):
+            k1, k2 = ("img1", "img2") if mode == 0 else ("spec1", "spec2")
+            return (self._stage("in.x0", (batch[k1], batch[k2]), mode),)
+        order = (0, 1) if mode == 2 else (1, 0)
+        return tuple(self._stage(f"in.x{j}", (batch[("img" if t == 0 else "spec") + str(j + 1)],), t)
+                     for j, t in enumerate(order))
+
     def forward(self, batch, mode=None):
         """batch: img1/spec1/img2/spec2 device tensors [B,1,H,W].  Returns the loss tensor."""
-        ws, st, P = self.ws, self.store, self.P
         mode = self.draw_mode() if mode is None else int(mode)
-        B = batch["img1"].shape[0]
+        return self._forward_staged(self.stage(batch, mode), mode, batch["img1"].shape[0])
+
+    def _forward_staged(self, xs, mode, B):
+        ws, st, P = self.ws, self.store, self.P
         reps = ws.get("reps", 2 * B * P)
         calls = []   # (tower, rows slice start, n rows, groups, encoder ctx, head ctx)
         if mode in (0, 1):
             t = mode
-            k1, k2 = ("img1", "img2") if t == 0 else ("spec1", "spec2")
-            x = self._stage("in.x0", (batch[k1], batch[k2]), t)
+            x = xs[0]
             enc, head = self.towers[t]
             emb, ectx = enc.forward(ws, st, "e0", x, 2 * B, 2, need_dgrad=True)
             hctx = head.forward(ws, st, "h0", emb, 2 * B, reps, 0.0, 0, G=2)
@@ -899,8 +1039,7 @@ class SimCLREngine:
         else:
             order = (0, 1) if mode == 2 else (1, 0)
             for j, t in enumerate(order):
-                key = ("img" if t == 0 else "spec") + str(j + 1)
-                x = self._stage(f"in.x{j}", (batch[key],), t)
+                x = xs[j]
                 enc, head = self.towers[t]
                 emb, ectx = enc.forward(ws, st, f"e{j}", x, B, 1, need_dgrad=True)
                 hctx = head.forward(ws, st, f"h{j}", emb, B, reps[j * B * P:(j + 1) * B * P], 0.0, 0)
@@ -932,23 +1071,44 @@ class SimCLREngine:
         return sorted({t for t, *_ in self.last["calls"]})
 
     def adam(self):
-        """Adam(lr), no weight decay, on the used towers with their own step counters."""
+        """Adam(lr), no weight decay, on the used towers with their own step counters (device
+        step state per tower: graph-replayable)."""
         b1, b2 = self.hp.betas
         st = self.store
         for t in self.used_towers():
-            self.adam_t[t] += 1
-            k = self.adam_t[t]
+            ss = self.sstates[t]
+            ss.begin(seed=False)
             o, n = self.ranges[t]
-            ops.adam(st.student[o:o + n], st.grad[o:o + n], st.adam_m[o:o + n], st.adam_v[o:o + n],
-                     n, self.hp.lr, b1, b2, self.hp.eps, 0.0, 1 - b1 ** k, 1 - b2 ** k)
+            ops.adam_dev(st.student[o:o + n], st.grad[o:o + n], st.adam_m[o:o + n], st.adam_v[o:o + n],
+                         n, ss.hyp, b1, b2, self.hp.eps, 0.0)
+
+    def _graphable(self):
+        from . import dist as avdist
+        return self.negatives == "local" or avdist.world(self.group) == 1
 
     def step(self, batch, mode=None):
-        loss = self.forward(batch, mode)
-        self.backward()
+        mode = self.draw_mode() if mode is None else int(mode)
+        for ss in self.sstates:
+            ss.set_lr(self.hp.lr)
+        B = batch["img1"].shape[0]
+        xs = self.stage(batch, mode)
+
+        def body():
+            self._forward_staged(xs, mode, B)
+            self.backward()
+            if self.grad_hook is None:
+                self.adam()
+
+        if self.use_graph and self._graphable():
+            self.graph.run((mode, B), body)
+        else:
+            body()
         if self.grad_hook is not None:
             self.grad_hook(self.store.grad)
-        self.adam()
-        return loss
+            self.adam()
+        for t in self.used_towers():
+            self.adam_t[t] += 1
+        return self.last["loss"]
 
     def outputs(self):
         c = self.last

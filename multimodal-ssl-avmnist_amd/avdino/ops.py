@@ -474,11 +474,20 @@ def colstats(x, rows, G, C, parts, pivot=None):
     call("avd_colstats", p(x), rows, G, C, p(parts), p(pivot), stream())
 
 
-def act_fwd(x, out, act, scale, shift, rows, G, C, drop_p, seed):
-    call("avd_act_fwd", p(x), p(out), act, p(scale), p(shift), rows, G, C, drop_p, seed, stream())
+def act_fwd(x, out, act, scale, shift, rows, G, C, drop_p, seed, seed_off=None):
+    """seed_off: optional device u64 [1] added to seed (the engine's StepState.seed_off)."""
+    if seed_off is None:
+        call("avd_act_fwd", p(x), p(out), act, p(scale), p(shift), rows, G, C, drop_p, seed, stream())
+    else:
+        call("avd_act_fwd_dev", p(x), p(out), act, p(scale), p(shift), rows, G, C, drop_p, seed,
+             p(seed_off), stream())
 
 
-def act_bwd(x, dout, dx, act, scale, shift, rows, G, C, drop_p, seed):
+def act_bwd(x, dout, dx, act, scale, shift, rows, G, C, drop_p, seed, seed_off=None):
+    if seed_off is not None:
+        call("avd_act_bwd_dev", p(x), p(dout), p(dx), act, p(scale), p(shift), rows, G, C, drop_p,
+             seed, p(seed_off), stream())
+        return
     call("avd_act_bwd", p(x), p(dout), p(dx), act, p(scale), p(shift), rows, G, C, drop_p, seed,
          stream())
 
@@ -536,6 +545,19 @@ def adam(p_, g, m, v, n, lr, b1, b2, eps, wd, bc1, bc2):
     call("avd_adam", p(p_), p(g), p(m), p(v), n, lr, b1, b2, eps, wd, bc1, bc2, stream())
 
 
+def step_begin(t, hyp, seed_off, b1, b2, seed_stride):
+    """Device step state: seed_off = t * stride; t += 1; hyp[1:3] = bias corrections of t."""
+    _need(t.dtype == torch.int64 and hyp.dtype == torch.float32 and hyp.numel() >= 3, "step state")
+    call("avd_step_begin", p(t), p(hyp), p(seed_off), float(b1), float(b2), seed_stride, stream())
+
+
+def adam_dev(p_, g, m, v, n, hyp, b1, b2, eps, wd, decoupled=False):
+    """Adam / AdamW reading lr and the bias corrections from the device step state hyp."""
+    _need(p_.numel() >= n and g.numel() >= n and hyp.numel() >= 3, "adam_dev sizes")
+    call("avd_adamw_dev" if decoupled else "avd_adam_dev", p(p_), p(g), p(m), p(v), n, p(hyp), b1, b2,
+         eps, wd, stream())
+
+
 def adamw(p_, g, m, v, n, lr, b1, b2, eps, wd, bc1, bc2):
     call("avd_adamw", p(p_), p(g), p(m), p(v), n, lr, b1, b2, eps, wd, bc1, bc2, stream())
 
@@ -563,14 +585,17 @@ def row_sqnorm(x, N, D, out):
     call("avd_row_sqnorm", p(x), N, D, p(out), stream())
 
 
-def knn_select(S, ldS, xnorm, M, N, K, labels, C, nbr, pred):
-    """S [M, ldS] = -2 Q X^T (f32), xnorm [N], labels [N] int64 -> pred [M] int64 (+ nbr [M, K])."""
+def knn_select(S, ldS, xnorm, M, N, K, labels, C, nbr, pred, Q=None, X=None, D=0):
+    """S [M, ldS] = -2 Q X^T (f32), xnorm [N], labels [N] int64 -> pred [M] int64 (+ nbr [M, K]);
+    Q [M, D] / X [N, D]: re-rank the best 16 candidates by direct distance."""
+    _need(Q is None or (Q.numel() >= M * D and X is not None and X.numel() >= N * D), "knn Q/X")
     _need(S.dtype == torch.float32 and S.numel() >= (M - 1) * ldS + N and xnorm.numel() >= N, "knn S")
     _need(labels.dtype == torch.int64 and labels.numel() >= N, "knn labels")
     _need(pred.dtype == torch.int64 and pred.numel() >= M, "knn pred")
     _need(nbr is None or (nbr.dtype == torch.int64 and nbr.numel() >= M * K), "knn nbr")
     _need(1 <= K <= 16 and K <= N and 1 <= C <= 64, "knn K <= 16, C <= 64")
-    call("avd_knn_select", p(S), ldS, p(xnorm), M, N, K, p(labels), C, p(nbr), p(pred), stream())
+    call("avd_knn_select", p(S), ldS, p(xnorm), M, N, K, p(Q), p(X), D, p(labels), C, p(nbr), p(pred),
+         stream())
 
 
 def axpy(y, x, a=1.0):

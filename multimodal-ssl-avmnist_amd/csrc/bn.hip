@@ -514,7 +514,8 @@ __device__ __forceinline__ float gelu_d(float z) {
 __global__ __launch_bounds__(256) void act_fwd_kernel(
     const float* __restrict__ x, float* __restrict__ out, int act, const float* __restrict__ scale,
     const float* __restrict__ shift, long long total, int rpg, int C, float p,
-    unsigned long long seed) {
+    unsigned long long seed, const unsigned long long* __restrict__ seed_off) {
+  if (seed_off) seed += seed_off[0];
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
     float v = x[i];
     if (act == 0) {
@@ -531,7 +532,8 @@ __global__ __launch_bounds__(256) void act_fwd_kernel(
 __global__ __launch_bounds__(256) void act_bwd_kernel(
     const float* __restrict__ x, const float* __restrict__ dout, float* __restrict__ dx, int act,
     const float* __restrict__ scale, const float* __restrict__ shift, long long total, int rpg,
-    int C, float p, unsigned long long seed) {
+    int C, float p, unsigned long long seed, const unsigned long long* __restrict__ seed_off) {
+  if (seed_off) seed += seed_off[0];
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
     const float d = dout[i] * dropout_scale(seed, (unsigned long long)i, p);
     const float v = x[i];
@@ -765,13 +767,33 @@ int avd_colstats(const float* x, int rows, int G, int C, float* parts, float* pi
   return AVD_OK;
 }
 
-int avd_act_fwd(const float* x, float* out, int act, const float* scale, const float* shift,
-                int rows, int G, int C, float p, unsigned long long seed, void* stream) {
+int avd_act_fwd_dev(const float* x, float* out, int act, const float* scale, const float* shift,
+                    int rows, int G, int C, float p, unsigned long long seed,
+                    const unsigned long long* seed_off, void* stream) {
   if (!x || !out || (act == 1 && (!scale || !shift)) || (act != 0 && act != 1)) return AVD_ERR_ARG;
   if (rows <= 0 || G <= 0 || rows % G || p < 0.f || p >= 1.f) return AVD_ERR_SHAPE;
   const long long total = (long long)rows * C;
   act_fwd_kernel<<<grid_for(total), 256, 0, avd_stream(stream)>>>(x, out, act, scale, shift, total,
-                                                                  rows / G, C, p, seed);
+                                                                  rows / G, C, p, seed, seed_off);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_act_fwd(const float* x, float* out, int act, const float* scale, const float* shift,
+                int rows, int G, int C, float p, unsigned long long seed, void* stream) {
+  return avd_act_fwd_dev(x, out, act, scale, shift, rows, G, C, p, seed, nullptr, stream);
+}
+
+int avd_act_bwd_dev(const float* x, const float* dout, float* dx, int act, const float* scale,
+                    const float* shift, int rows, int G, int C, float p, unsigned long long seed,
+                    const unsigned long long* seed_off, void* stream) {
+  if (!x || !dout || !dx || (act == 1 && (!scale || !shift)) || (act != 0 && act != 1))
+    return AVD_ERR_ARG;
+  if (rows <= 0 || G <= 0 || rows % G || p < 0.f || p >= 1.f) return AVD_ERR_SHAPE;
+  const long long total = (long long)rows * C;
+  act_bwd_kernel<<<grid_for(total), 256, 0, avd_stream(stream)>>>(x, dout, dx, act, scale, shift,
+                                                                  total, rows / G, C, p, seed,
+                                                                  seed_off);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
@@ -779,14 +801,7 @@ int avd_act_fwd(const float* x, float* out, int act, const float* scale, const f
 int avd_act_bwd(const float* x, const float* dout, float* dx, int act, const float* scale,
                 const float* shift, int rows, int G, int C, float p, unsigned long long seed,
                 void* stream) {
-  if (!x || !dout || !dx || (act == 1 && (!scale || !shift)) || (act != 0 && act != 1))
-    return AVD_ERR_ARG;
-  if (rows <= 0 || G <= 0 || rows % G || p < 0.f || p >= 1.f) return AVD_ERR_SHAPE;
-  const long long total = (long long)rows * C;
-  act_bwd_kernel<<<grid_for(total), 256, 0, avd_stream(stream)>>>(x, dout, dx, act, scale, shift,
-                                                                  total, rows / G, C, p, seed);
-  AVD_CHECK_LAUNCH();
-  return AVD_OK;
+  return avd_act_bwd_dev(x, dout, dx, act, scale, shift, rows, G, C, p, seed, nullptr, stream);
 }
 
 int avd_bn1d_bwd_reduce(const float* x, const float* dz, const float* mean, const float* invstd,

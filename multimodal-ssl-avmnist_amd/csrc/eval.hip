@@ -22,11 +22,16 @@ __device__ __forceinline__ bool knn_less(float da, int ja, float db, int jb) {
 
 // One workgroup per test row i.  d_j = xnorm[j] + S[i, j], with S = -2 q_i . x_j from the GEMM
 // (|q_i|^2 is the same for every j of the row, so the ranking does not need it).  Each thread
-// keeps a sorted top-K of its strided columns in LDS; 8 pairwise merge rounds reduce the 256
-// lists; thread 0 votes.
+// keeps a sorted top-KS of its strided columns in LDS; 8 pairwise merge rounds reduce the 256
+// lists.  The GEMM form cancels |q|^2 + |x|^2 against 2 q.x, so its f32 error is relative to
+// the norms, not to the distance: with Q/X given, the KS = min(16, N) candidates are re-ranked
+// by their direct distance sum_k (q_k - x_jk)^2 (error relative to the distance itself, as
+// sklearn's float64 path ranks them) before the first K are kept.  Thread 0 votes.
 __global__ __launch_bounds__(KNN_T) void knn_select_kernel(
     const float* __restrict__ S, long long ldS, const float* __restrict__ xnorm, int N, int K,
+    int KS, const float* __restrict__ Q, const float* __restrict__ X, int D,
     const int64_t* __restrict__ labels, int C, int64_t* __restrict__ nbr, int64_t* __restrict__ pred) {
+  __shared__ float rd[KNN_KMAX];
   __shared__ float sd[KNN_T * KNN_KMAX];
   __shared__ int sj[KNN_T * KNN_KMAX];
   __shared__ float td[KNN_T / 2 * KNN_KMAX];   // merge outputs
@@ -34,35 +39,62 @@ __global__ __launch_bounds__(KNN_T) void knn_select_kernel(
   __shared__ int cnt[KNN_CMAX];
   const int t = threadIdx.x;
   const int i = blockIdx.x;
-  float* d = sd + t * K;
-  int* jj = sj + t * K;
-  for (int k = 0; k < K; ++k) { d[k] = INFINITY; jj[k] = 0x7fffffff; }
+  float* d = sd + t * KS;
+  int* jj = sj + t * KS;
+  for (int k = 0; k < KS; ++k) { d[k] = INFINITY; jj[k] = 0x7fffffff; }
   float worst = INFINITY;
   int worst_j = 0x7fffffff;
   const float* row = S + (size_t)i * ldS;
   for (int j = t; j < N; j += KNN_T) {
     const float v = xnorm[j] + row[j];
     if (knn_less(v, j, worst, worst_j)) {      // insert into the sorted list, drop the last
-      int p = K - 1;
+      int p = KS - 1;
       while (p > 0 && knn_less(v, j, d[p - 1], jj[p - 1])) { d[p] = d[p - 1]; jj[p] = jj[p - 1]; --p; }
       d[p] = v; jj[p] = j;
-      worst = d[K - 1]; worst_j = jj[K - 1];
+      worst = d[KS - 1]; worst_j = jj[KS - 1];
     }
   }
   __syncthreads();
   for (int s = KNN_T / 2; s > 0; s >>= 1) {
-    if (t < s) {   // merge lists t and t + s (both sorted) -> the K smallest into list t
-      float* a = sd + t * K;   int* aj = sj + t * K;
-      const float* b = sd + (t + s) * K; const int* bj = sj + (t + s) * K;
-      float* od = td + t * K; int* oj = tj + t * K;
+    if (t < s) {   // merge lists t and t + s (both sorted) -> the KS smallest into list t
+      float* a = sd + t * KS;   int* aj = sj + t * KS;
+      const float* b = sd + (t + s) * KS; const int* bj = sj + (t + s) * KS;
+      float* od = td + t * KS; int* oj = tj + t * KS;
       int x = 0, y = 0;
-      for (int k = 0; k < K; ++k) {
+      for (int k = 0; k < KS; ++k) {
         if (knn_less(a[x], aj[x], b[y], bj[y])) { od[k] = a[x]; oj[k] = aj[x]; ++x; }
         else { od[k] = b[y]; oj[k] = bj[y]; ++y; }
       }
-      for (int k = 0; k < K; ++k) { a[k] = od[k]; aj[k] = oj[k]; }
+      for (int k = 0; k < KS; ++k) { a[k] = od[k]; aj[k] = oj[k]; }
     }
     __syncthreads();
+  }
+  if (Q) {   // re-rank the KS candidates by their direct distances: 16 lanes per candidate
+    const int c = t >> 4, l = t & 15;
+    float acc = 0.f;
+    const int j = c < KS ? sj[c] : 0x7fffffff;
+    if (c < KS && j < N) {
+      const float* q = Q + (size_t)i * D;
+      const float* x = X + (size_t)j * D;
+      for (int k = l; k < D; k += 16) {
+        const float df = q[k] - x[k];
+        acc = fmaf(df, df, acc);
+      }
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 16);
+    __syncthreads();
+    if (c < KS && l == 0) rd[c] = j < N ? acc : INFINITY;
+    __syncthreads();
+    if (t == 0) {   // insertion sort of the KS (distance, index) pairs
+      for (int a = 1; a < KS; ++a) {
+        const float dv = rd[a];
+        const int jv = sj[a];
+        int b = a;
+        while (b > 0 && knn_less(dv, jv, rd[b - 1], sj[b - 1])) { rd[b] = rd[b - 1]; sj[b] = sj[b - 1]; --b; }
+        rd[b] = dv; sj[b] = jv;
+      }
+    }
   }
   if (t < C) cnt[t] = 0;
   __syncthreads();
@@ -131,11 +163,15 @@ int avd_row_sqnorm(const float* x, int N, int D, float* out, void* stream) {
 }
 
 int avd_knn_select(const float* S, long long ldS, const float* xnorm, int M, int N, int K,
-                   const int64_t* labels, int C, int64_t* nbr, int64_t* pred, void* stream) {
-  if (!S || !xnorm || !labels || !pred) return AVD_ERR_ARG;
-  if (M <= 0 || N <= 0 || K <= 0 || K > KNN_KMAX || K > N || C <= 0 || C > KNN_CMAX || ldS < N)
+                   const float* Q, const float* X, int D, const int64_t* labels, int C,
+                   int64_t* nbr, int64_t* pred, void* stream) {
+  if (!S || !xnorm || !labels || !pred || (Q && !X)) return AVD_ERR_ARG;
+  if (M <= 0 || N <= 0 || K <= 0 || K > KNN_KMAX || K > N || C <= 0 || C > KNN_CMAX || ldS < N ||
+      (Q && D <= 0))
     return AVD_ERR_SHAPE;
-  knn_select_kernel<<<M, KNN_T, 0, avd_stream(stream)>>>(S, ldS, xnorm, N, K, labels, C, nbr, pred);
+  const int KS = Q ? (N < KNN_KMAX ? N : KNN_KMAX) : K;
+  knn_select_kernel<<<M, KNN_T, 0, avd_stream(stream)>>>(S, ldS, xnorm, N, K, KS, Q, X, D, labels, C,
+                                                         nbr, pred);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

@@ -54,7 +54,13 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    long long n, float lr, float b1, float b2,
                                                    float eps, float wd, float inv_bc1,
-                                                   float inv_sqrt_bc2) {
+                                                   float inv_sqrt_bc2,
+                                                   const float* __restrict__ hyp) {
+  if (hyp) {   // per-step scalars from the device step state (graph-replayable steps)
+    lr = hyp[0];
+    inv_bc1 = 1.f / hyp[1];
+    inv_sqrt_bc2 = 1.f / sqrtf(hyp[2]);
+  }
   const long long n4 = n / 4;
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
     float4 pp = reinterpret_cast<float4*>(p)[i];
@@ -98,6 +104,19 @@ inline int stream_grid(long long n) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// One thread: the device step state of a graph-replayable training step (see avdino.h).
+__global__ void step_begin_kernel(long long* __restrict__ t, float* __restrict__ hyp,
+                                  unsigned long long* __restrict__ seed_off, double b1, double b2,
+                                  unsigned long long stride) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const long long done = t[0];
+  if (seed_off) seed_off[0] = (unsigned long long)done * stride;
+  const long long k = done + 1;
+  t[0] = k;
+  hyp[1] = (float)(1.0 - pow(b1, (double)k));
+  hyp[2] = (float)(1.0 - pow(b2, (double)k));
+}
+
 }  // namespace
 
 extern "C" {
@@ -121,7 +140,7 @@ int avd_adam(float* p, const float* g, float* m, float* v, long long n, float lr
   if (n < 0 || !aligned16(p) || !aligned16(g) || !aligned16(m) || !aligned16(v)) return AVD_ERR_SHAPE;
   if (n == 0) return AVD_OK;
   adam_kernel<false><<<stream_grid(n), 256, 0, avd_stream(stream)>>>(p, g, m, v, n, lr, b1, b2, eps,
-                                                                     wd, 1.f / bc1, 1.f / sqrtf(bc2));
+                                                                     wd, 1.f / bc1, 1.f / sqrtf(bc2), nullptr);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
@@ -141,9 +160,42 @@ int avd_adamw(float* p, const float* g, float* m, float* v, long long n, float l
   if (n < 0 || !aligned16(p) || !aligned16(g) || !aligned16(m) || !aligned16(v)) return AVD_ERR_SHAPE;
   if (n == 0) return AVD_OK;
   adam_kernel<true><<<stream_grid(n), 256, 0, avd_stream(stream)>>>(p, g, m, v, n, lr, b1, b2, eps,
-                                                                    wd, 1.f / bc1, 1.f / sqrtf(bc2));
+                                                                    wd, 1.f / bc1, 1.f / sqrtf(bc2), nullptr);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
+}
+
+int avd_step_begin(long long* t, float* hyp, unsigned long long* seed_off, double b1, double b2,
+                   unsigned long long seed_stride, void* stream) {
+  if (!t || !hyp) return AVD_ERR_ARG;
+  step_begin_kernel<<<1, 64, 0, avd_stream(stream)>>>(t, hyp, seed_off, b1, b2, seed_stride);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+static int adam_dev(bool decoupled, float* p, const float* g, float* m, float* v, long long n,
+                    const float* hyp, float b1, float b2, float eps, float wd, void* stream) {
+  if (!p || !g || !m || !v || !hyp) return AVD_ERR_ARG;
+  if (n < 0 || !aligned16(p) || !aligned16(g) || !aligned16(m) || !aligned16(v)) return AVD_ERR_SHAPE;
+  if (n == 0) return AVD_OK;
+  if (decoupled)
+    adam_kernel<true><<<stream_grid(n), 256, 0, avd_stream(stream)>>>(p, g, m, v, n, 0.f, b1, b2, eps,
+                                                                      wd, 1.f, 1.f, hyp);
+  else
+    adam_kernel<false><<<stream_grid(n), 256, 0, avd_stream(stream)>>>(p, g, m, v, n, 0.f, b1, b2, eps,
+                                                                       wd, 1.f, 1.f, hyp);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_adam_dev(float* p, const float* g, float* m, float* v, long long n, const float* hyp,
+                 float b1, float b2, float eps, float wd, void* stream) {
+  return adam_dev(false, p, g, m, v, n, hyp, b1, b2, eps, wd, stream);
+}
+
+int avd_adamw_dev(float* p, const float* g, float* m, float* v, long long n, const float* hyp,
+                  float b1, float b2, float eps, float wd, void* stream) {
+  return adam_dev(true, p, g, m, v, n, hyp, b1, b2, eps, wd, stream);
 }
 
 }  // extern "C"

@@ -1,0 +1,107 @@
+"""Graph-replayed training steps (engine.GraphedStep + StepState): a step captured once as a
+hipGraph and replayed must be the eager step, bit for bit, on every later step -- fresh dropout
+masks (the counter offset lives in device memory), the right Adam bias corrections (device step
+count), BN running statistics / counters, centre, teacher EMA -- for the three engines."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+from oracle import spec as OS  # noqa: E402
+from oracle.params import make_multimodal_batch, make_simclr_batch, make_state  # noqa: E402
+
+
+def _dev(b):
+    return {k: torch.from_numpy(v).cuda() for k, v in b.items()}
+
+
+def _run_multi(mode, graph, steps=5, precision=torch.bfloat16):
+    from avdino.engine import Hyper, MultiCentralEngine
+    from avdino.params import ParamStore
+    from avdino.spec import multimodal_dino_sd
+    E, D, P, B, G, L = 32, 32, 16, 8, 2, 4
+    store = ParamStore(multimodal_dino_sd(mode, E, D, P), "cuda")
+    store.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in
+                           make_state(OS.multimodal_dino_spec(mode, E, D, P), 401).items()})
+    eng = MultiCentralEngine(store, mode, E, D, P, Hyper(dropout=0.3, fusion_dropout=0.3),
+                             act_dtype=precision, seed=3)
+    eng.use_graph = graph
+    batches = [_dev(make_multimodal_batch(B, G, L, 4000 + i)) for i in range(2)]
+    losses = [eng.step(batches[i % 2]).item() for i in range(steps)]
+    return store, losses, eng
+
+
+@pytest.mark.parametrize("mode", ["mse", "semi_supervised", "default"])
+def test_graph_replay_equals_eager_multimodal(mode):
+    s0, l0, _ = _run_multi(mode, False)
+    s1, l1, e1 = _run_multi(mode, True)
+    assert len(e1.graph.graphs) == 1           # captured once, replayed for steps 4, 5
+    assert l0 == l1, (l0, l1)
+    assert len(set(l1[2:])) > 1 or len(set(l1)) > 1
+    assert torch.equal(s0.student, s1.student)
+    assert torch.equal(s0.teacher, s1.teacher)
+    assert torch.equal(s0.buf_arena, s1.buf_arena)
+    s0.flush_nbt()
+    s1.flush_nbt()
+    assert torch.equal(s0.nbt_arena, s1.nbt_arena)
+    assert torch.equal(s0.adam_m, s1.adam_m) and torch.equal(s0.adam_v, s1.adam_v)
+    assert int(e1.sstate.t.item()) == 5
+
+
+def test_graph_dropout_masks_change_per_replay():
+    """The same batch every step: with the device seed offset, replays differ (fresh masks)
+    exactly as eager steps do; with dropout 0 the only change is the parameter update."""
+    from avdino.engine import Hyper, MultiCentralEngine
+    from avdino.params import ParamStore
+    from avdino.spec import multimodal_dino_sd
+    E, D, P, B, G, L = 32, 32, 16, 8, 2, 4
+    outs = []
+    for graph in (False, True):
+        store = ParamStore(multimodal_dino_sd("mse", E, D, P), "cuda", seed=5)
+        eng = MultiCentralEngine(store, "mse", E, D, P, Hyper(lr=0.0, weight_decay=0.0, dropout=0.5,
+                                                              fusion_dropout=0.5, momentum=1.0),
+                                 act_dtype=torch.float32, seed=9)
+        eng.use_graph = graph
+        b = _dev(make_multimodal_batch(B, G, L, 4100))
+        outs.append([eng.step(b).item() for _ in range(6)])
+    assert outs[0] == outs[1]
+    assert len(set(outs[1])) == 6     # lr 0, EMA off: only the masks (and BN running stats) move
+
+
+def test_graph_replay_equals_eager_unimodal():
+    from avdino.engine import Hyper, UniModalEngine
+    from avdino.params import ParamStore
+    from avdino.spec import unimodal_dino_sd
+    res = []
+    for graph in (False, True):
+        store = ParamStore(unimodal_dino_sd("image_simple", 64, 32), "cuda", seed=2)
+        eng = UniModalEngine(store, "image_simple", 64, 32, Hyper(dropout=0.3),
+                             act_dtype=torch.bfloat16, cos_alpha=0.3, seed=4)
+        eng.use_graph = graph
+        bs = [_dev(make_multimodal_batch(16, 2, 2, 4200 + i, with_originals=False)) for i in range(2)]
+        res.append(([eng.step(bs[i % 2]).item() for i in range(5)], store))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1].student, res[1][1].student)
+    assert torch.equal(res[0][1].teacher, res[1][1].teacher)
+
+
+def test_graph_replay_equals_eager_simclr():
+    from avdino.engine import Hyper, SimCLREngine
+    from avdino.params import ParamStore
+    from avdino.spec import simclr_sd
+    modes = [0, 2, 1, 3, 2, 0, 3, 2, 2, 1]
+    res = []
+    for graph in (False, True):
+        store = ParamStore(simclr_sd(64, 32), "cuda", seed=3, has_teacher=False,
+                           groups=SimCLREngine.GROUPS)
+        eng = SimCLREngine(store, 64, 32, Hyper(weight_decay=0.0), act_dtype=torch.bfloat16,
+                           negatives="local")
+        eng.use_graph = graph
+        b = make_simclr_batch(8, 4300)
+        b = {k: torch.from_numpy(v).cuda() for k, v in b.items()}
+        res.append(([eng.step(b, m).item() for m in modes], store, eng))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1].student, res[1][1].student)
+    assert res[1][2].adam_t == res[0][2].adam_t
+    assert [int(s.t.item()) for s in res[1][2].sstates] == res[0][2].adam_t
