@@ -116,10 +116,11 @@ def build_workload(args, device, act, world, rank, avdist):
             avdist.broadcast_parameters(store)
         eng = UniModalEngine(store, "image_simple", D, P, Hyper(), act_dtype=act, cos_alpha=0.0,
                              grad_hook=hook, buffer_hook=avdist.broadcast_buffers if world > 1 else None,
-                             seed=rank)
+                             seed=rank, step_order="pretrain")
         pool = synthetic_pool(2, B, 2, 0, device, 1234 + rank)
-        return (eng, pool, B, f"UniModalDINO ImageEncoder, 2 global views, B={B}/GPU, D={D}, P={P} "
-                              f"(BASELINE config 1)", "image_simple")
+        return (eng, pool, B, f"UniModalDINO ImageEncoder, 2 global views, B={B}/GPU, D={D}, P={P}, "
+                              f"training_structures.pretrain_dino step (AdamW, EMA after the step; "
+                              f"BASELINE config 1)", "image_simple")
     if args.workload == "simclr":
         B, D, P = args.batch or 2048, 256, 256
         store = ParamStore(simclr_sd(D, P), device, seed=0, has_teacher=False,
@@ -154,6 +155,31 @@ def build_workload(args, device, act, world, rank, avdist):
            "default": "default mode"}[args.mode]
     return (eng, pool, B, f"multi_central {args.mode} training step, B={B}/GPU, {G} global + {L} "
                           f"local views, E=D={E}, P={P} ({cfg})", "multi_central")
+
+
+def cpu_baseline_uni(batch, seconds):
+    """Config 1's reference path on the host cores: training_structures.pretrain_dino's step
+    (oracle/torch_port.py UniImageDINO + pretrain_step: AdamW, EMA after the step), fp32."""
+    from oracle import torch_port as TP
+    torch.manual_seed(0)
+    model = TP.UniImageDINO()
+    model.train()
+    opt = torch.optim.AdamW(list(model.parameters()), lr=1e-4)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randint(0, 256, (batch, 2, 1, 28, 28), generator=g).float() / 255.0
+    TP.pretrain_step(model, opt, x)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        TP.pretrain_step(model, opt, x)
+        n += 1
+        el = time.perf_counter() - t0
+        if (n >= 2 and el >= seconds) or n >= 2000:
+            break
+    return {"value": round(batch * n / el, 2), "unit": "pairs/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle/torch_port.py UniImageDINO training_structures.pretrain_dino step "
+                      f"(dino_train.py:143-161), fp32, B={batch}, 2 global views, {n} timed steps "
+                      f"({el:.1f} s) after 1 warm-up, torch CPU {torch.get_num_threads()} threads"}
 
 
 def cpu_baseline(batch, seconds):
@@ -330,6 +356,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "dino" \
             and args.mode == "mse":
         out["cpu_baseline"] = cpu_baseline(args.cpu_batch, args.cpu_seconds)
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "uni":
+        out["cpu_baseline"] = cpu_baseline_uni(B, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -844,7 +844,14 @@ class UniModalEngine:
     teacher EMA (before backward, dino.py:1661), backward, Adam with L2 weight decay."""
 
     def __init__(self, store, kind, D, P, hp, act_dtype=F32, cos_alpha=0.0, grad_hook=None,
-                 buffer_hook=None, seed=0):
+                 buffer_hook=None, seed=0, step_order="lightning"):
+        """step_order "lightning": UniModalDINOLightning.training_step + Adam(L2) (EMA before
+        backward); "pretrain": training_structures.pretrain_dino (dino_train.py:137-166):
+        AdamW (weight_decay 0.01) and the EMA AFTER the optimizer step, loss = the unimodal
+        DINO loss only."""
+        if step_order not in ("lightning", "pretrain"):
+            raise ValueError(step_order)
+        self.step_order = step_order
         self.store, self.D, self.P, self.hp = store, D, P, hp
         self.kind = UNI_ALIASES.get(kind, kind)
         self.act = act_dtype
@@ -933,13 +940,26 @@ class UniModalEngine:
         self.sstate.set_lr(self.hp.lr)
         staged = self.stage(batch)
 
+        pre = self.step_order == "pretrain"
+
+        def opt_and_ema():
+            if pre:     # AdamW, then the EMA sees the post-step student
+                b1, b2 = self.hp.betas
+                st = self.store
+                ops.adam_dev(st.student, st.grad, st.adam_m, st.adam_v, st.n_live, self.sstate.hyp,
+                             b1, b2, self.hp.eps, 0.01, decoupled=True)
+                ema_step(st, self.hp.momentum)
+            else:
+                adam_step_dev(self.store, self.hp, self.sstate)
+
         def body():
             self._forward_staged(staged, training=True)
             self.update_center()
-            ema_step(self.store, self.hp.momentum)
+            if not pre:
+                ema_step(self.store, self.hp.momentum)
             self.backward()
             if self.grad_hook is None:
-                adam_step_dev(self.store, self.hp, self.sstate)
+                opt_and_ema()
 
         if self.use_graph:
             self.graph.run(staged[1:], body)
@@ -947,7 +967,7 @@ class UniModalEngine:
             body()
         if self.grad_hook is not None:
             self.grad_hook(self.store.grad)
-            adam_step_dev(self.store, self.hp, self.sstate)
+            opt_and_ema()
         self.store.adam_step += 1
         self.step_idx += 1
         return self.last["loss"]

@@ -261,14 +261,19 @@ __global__ __launch_bounds__(256) void bwd_reduce_pooled_cl_kernel(
   const int c0 = cv * V;
   const long long nwin = (long long)B * Hp * Wp;
   const long long w0 = r * per, w1 = std::min(nwin, w0 + per);
-  float ig[V], be[V], mu[V], is[V], s1[V], s2[V];
+  float ig[V], be[V], mu[V], is[V], s1[V], s2[V], gs[V];
   bool any0 = false;
 #pragma unroll
   for (int e = 0; e < V; ++e) {
-    const float ga = gamma[c0 + e];
-    ig[e] = ga != 0.f ? 1.f / ga : 0.f;
-    any0 |= ga == 0.f;
-    be[e] = beta[c0 + e];
+    // xhat = (p - beta) / gamma carries the stored p's rounding amplified by |beta / gamma|:
+    // such channels (and gamma == 0) take xhat from y at the argmax instead -- bound: the
+    // error stays under 8 ulps of the storage type in xhat units
+    const float ga = gamma[c0 + e], bb = beta[c0 + e];
+    const bool use_y = ga == 0.f || fabsf(bb) > (sizeof(T) == 2 ? 8.f : 4096.f) * fabsf(ga);
+    ig[e] = use_y ? 0.f : 1.f / ga;
+    gs[e] = ga > 0.f ? 1.f : (ga < 0.f ? -1.f : 0.f);
+    any0 |= use_y;
+    be[e] = bb;
     s1[e] = 0.f; s2[e] = 0.f;
   }
   load_coef<V>(mean, g * C + c0, mu);
@@ -306,12 +311,33 @@ __global__ __launch_bounds__(256) void bwd_reduce_pooled_cl_kernel(
       float gg[V], pv[V];
       load_gout<T, V>(gout, mode, n, hp, wp, Hp, Wp, C, c0, gg);
       load_gout<T, V>(pooled, mode, n, hp, wp, Hp, Wp, C, c0, pv);
-      float y0[V];
-      if (any0) Vec<T>::ld(y + (((size_t)n * H + 2 * hp) * W + 2 * wp) * C + c0, y0);
+      // y-path channels: the window's argmax of gamma * xhat + beta is the max of xhat for
+      // gamma > 0, its min for gamma < 0 (first of equals); gamma == 0 makes every element
+      // equal, and the forward's max keeps the first (top-left) one
+      float y0[V], y1[V], y2[V], y3[V];
+      if (any0) {
+        const T* yw = y + (((size_t)n * H + 2 * hp) * W + 2 * wp) * C + c0;
+        Vec<T>::ld(yw, y0);
+        Vec<T>::ld(yw + C, y1);
+        Vec<T>::ld(yw + (size_t)W * C, y2);
+        Vec<T>::ld(yw + (size_t)W * C + C, y3);
+      }
 #pragma unroll
       for (int e = 0; e < V; ++e) {
         const float dz = pv[e] > 0.f ? gg[e] : 0.f;
-        const float xh = ig[e] != 0.f ? (pv[e] - be[e]) * ig[e] : (any0 ? (y0[e] - mu[e]) * is[e] : 0.f);
+        float xh = 0.f;
+        if (ig[e] != 0.f) {
+          xh = (pv[e] - be[e]) * ig[e];
+        } else if (any0) {
+          xh = (y0[e] - mu[e]) * is[e];
+          if (gs[e] != 0.f) {
+            const float c1 = (y1[e] - mu[e]) * is[e], c2 = (y2[e] - mu[e]) * is[e],
+                        c3 = (y3[e] - mu[e]) * is[e];
+            if (gs[e] * c1 > gs[e] * xh) xh = c1;
+            if (gs[e] * c2 > gs[e] * xh) xh = c2;
+            if (gs[e] * c3 > gs[e] * xh) xh = c3;
+          }
+        }
         s1[e] += dz;
         s2[e] += dz * xh;
       }

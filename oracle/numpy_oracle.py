@@ -452,7 +452,7 @@ def _views_to_rows(v):
     return np.ascontiguousarray(v.transpose(1, 0, 2, 3, 4).reshape(V * B, *v.shape[2:]))
 
 
-def multimodal_step(P, batch, mode, hp, masks=None):
+def multimodal_step(P, batch, mode, hp, masks=None, aux_fn=None):
     """One MultiModalDINO* training step in the reference's order:
     forward -> losses -> EMA (pre-step student) -> backward -> Adam.
 
@@ -461,6 +461,8 @@ def multimodal_step(P, batch, mode, hp, masks=None):
     masks: optional dropout masks (already scaled by 1/(1-p)) for the fusion of the
     student ('fusion_s' [V*B,E]), teacher ('fusion_t' [G*B,E]), heads ('fusion_o' [B,E])
     and the student projection ('proj_s' [V*B,512]); None = p 0.
+    aux_fn: optional (zi, za) -> (aux loss, d zi, d za) replacing the mode's own head loss
+    (multimodal_step_ddp's global-negative InfoNCE).
     """
     masks = masks or {}
     P = {k: np.asarray(v, F64) if np.asarray(v).dtype != np.int64 else np.asarray(v) for k, v in P.items()}
@@ -508,7 +510,9 @@ def multimodal_step(P, batch, mode, hp, masks=None):
         hI, hA = ProjHead(hi), ProjHead(ha)
         zi, zic = hI.forward(P, fi)
         za, zac = hA.forward(P, fa)
-        if mode == "mse":
+        if aux_fn is not None:
+            aux, dzi, dza = aux_fn(zi, za)
+        elif mode == "mse":
             aux, dzi, dza = mse_loss(zi, za)
         elif mode == "infonce":
             aux, dzi, dza = infonce_loss(zi, za)
@@ -547,6 +551,40 @@ def multimodal_step(P, batch, mode, hp, masks=None):
     out["grads"] = grads
     out["state"] = new
     return out
+
+
+def multimodal_step_ddp(P, batch, mode, hp, world, global_negatives=True):
+    """The reference's DDP step over ``world`` ranks, simulated in one process (SURVEY 8(e)
+    "parity for N ranks"): rank r owns batch rows r*B..(r+1)*B (DistributedSampler shards),
+    runs the forward with its OWN BatchNorm statistics (no SyncBN), updates its own centre and
+    running statistics, and the gradients are averaged (DDP all-reduce / world) before Adam;
+    every rank starts from rank 0's buffers (broadcast_buffers).  InfoNCE with
+    global_negatives: each rank's loss is the mean over ITS rows of the InfoNCE over the
+    all-gathered batch, and its head gradient is the one the all-gather's adjoint delivers, so
+    the averaged gradient is the single-device gradient of the global-batch InfoNCE.
+    Returns per-rank step dicts and the averaged gradients."""
+    Bt = batch["g_img"].shape[0]
+    B = Bt // world
+    shard = [{k: v[r * B:(r + 1) * B] for k, v in batch.items()} for r in range(world)]
+    aux = [None] * world
+    if mode == "infonce" and global_negatives and world > 1:
+        zs = [multimodal_step(P, shard[r], mode, hp) for r in range(world)]
+        Zi = np.concatenate([z["f_img"] for z in zs])
+        Za = np.concatenate([z["f_aud"] for z in zs])
+        _, dZi, dZa = infonce_loss(Zi, Za)
+        inn, _ = l2norm_fwd(Zi)
+        an, _ = l2norm_fwd(Za)
+        S = inn @ an.T / 0.07
+        lab = np.arange(Bt)
+        ls1 = -log_softmax(S)[lab, lab]
+        ls2 = -log_softmax(S.T)[lab, lab]
+        for r in range(world):
+            sl = slice(r * B, (r + 1) * B)
+            lr_ = 0.5 * (ls1[sl].mean() + ls2[sl].mean())
+            aux[r] = (lambda a, b, lr_=lr_, sl=sl: (lr_, world * dZi[sl], world * dZa[sl]))
+    outs = [multimodal_step(P, shard[r], mode, hp, aux_fn=aux[r]) for r in range(world)]
+    grads = {k: sum(o["grads"][k] for o in outs) / world for k in outs[0]["grads"]}
+    return outs, grads
 
 
 def _stack_stats(enc_cache):
@@ -683,6 +721,39 @@ def unimodal_step(P, batch, hp, modality="image", cos_alpha=0.0, masks=None, enc
     return {"loss": dino + cos_alpha * cos, "dino_loss": dino, "cos_loss": cos, "s_out": s_out,
             "t_out": t_out, "emb": s_feat.reshape(V, B, -1), "grads": grads,
             "center_after": new_center, "state": new}
+
+
+def pretrain_dino(P, batches, epochs, lr=1e-4, hp=None, wd=0.01, modality="image"):
+    """training_structures/dino_train.py:104-186 (BASELINE config 1's CPU path): AdamW over
+    every parameter with a gradient (torch default weight_decay 0.01), and per batch
+    forward -> dino_loss(tau_s 0.1, tau_t 0.04; the unimodal loss) -> backward -> AdamW.step ->
+    update_teacher, i.e. the teacher EMA sees the POST-step student (the Lightning path EMAs
+    before backward).  batches: per epoch, the same list of unimodal batch dicts.  Returns the
+    per-step losses, per-epoch mean losses and the final state."""
+    hp = dict(hp or {})
+    hp.setdefault("tau_s", 0.1)
+    hp.setdefault("tau_t", 0.04)
+    P = {k: np.asarray(v, F64) if np.asarray(v).dtype != np.int64 else np.asarray(v) for k, v in P.items()}
+    opt, t, losses, epoch_losses = {}, 0, [], []
+    for _ in range(epochs):
+        el = []
+        for b in batches:
+            r = unimodal_step(P, b, hp, modality, 0.0)
+            new = r["state"]
+            t += 1
+            for k, g in r["grads"].items():
+                m, v = opt.get(k, (np.zeros_like(g), np.zeros_like(g)))
+                new[k], m, v = adamw_step(P[k], g, m, v, t, lr, wd)
+                opt[k] = (m, v)
+            for k in P:     # EMA after the optimizer step: old teacher, NEW student
+                if k.startswith("teacher") and not k.endswith(("running_mean", "running_var",
+                                                                "num_batches_tracked")):
+                    new[k] = ema(P[k], new["student" + k[len("teacher"):]], hp["momentum"])
+            P = new
+            losses.append(r["loss"])
+            el.append(r["loss"])
+        epoch_losses.append(float(np.mean(el)))
+    return {"step_losses": np.array(losses), "epoch_losses": np.array(epoch_losses), "state": P}
 
 
 def unimodal_image_step(P, batch, hp):

@@ -131,3 +131,77 @@ def train_step(model, opt, batch):
     loss.backward()
     opt.step()
     return loss.detach()
+
+
+# ---------------------------------------------------------------------------- config 1
+def _cnn3(chans):
+    layers = []
+    for ci, co in zip(chans[:-1], chans[1:]):
+        layers += [nn.Conv2d(ci, co, 3, padding=1), nn.BatchNorm2d(co), nn.ReLU(), nn.MaxPool2d(2)]
+    return layers
+
+
+class ImageEnc(nn.Module):
+    """ImageEncoder (dino.py:18-42, 483-499): 3x[conv3x3 -> BN -> ReLU -> pool] 1->32->64->128,
+    GAP, Linear(128, 512), projection Linear(512, D)."""
+
+    def __init__(self, D):
+        super().__init__()
+        self.encoder = nn.Sequential(*_cnn3([1, 32, 64, 128]), nn.AdaptiveAvgPool2d(1), nn.Flatten(),
+                                     nn.Linear(128, 512))
+        self.projection = nn.Sequential(nn.Linear(512, D))
+
+    def forward(self, x):
+        return self.projection(self.encoder(x))
+
+
+class UniImageDINO(nn.Module):
+    """UniModalDINO(ImageEncoder) (dino.py:1257-1398); state-dict keys as the reference."""
+
+    def __init__(self, D=256, P=128, dropout=0.3):
+        super().__init__()
+        self.student, self.teacher = ImageEnc(D), ImageEnc(D)
+        self.teacher.load_state_dict(self.student.state_dict())
+        self.student_projection, self.teacher_projection = head(D, P, dropout), head(D, P)
+        self.teacher_projection.load_state_dict(self.student_projection.state_dict())
+        for p in list(self.teacher.parameters()) + list(self.teacher_projection.parameters()):
+            p.requires_grad = False
+        self.register_buffer("center", torch.zeros(1, P))
+
+    update_teacher = DinoMSE.update_teacher
+
+    def forward(self, g_img, cm=0.9):
+        G = g_img.shape[1]
+        sp = self.student_projection.mlp(torch.cat([self.student(g_img[:, v]) for v in range(G)]))
+        with torch.no_grad():
+            tp = self.teacher_projection.mlp(torch.cat([self.teacher(g_img[:, v]) for v in range(G)]))
+            tc = tp - self.center
+            self.center = self.center * cm + tp.mean(0, keepdim=True) * (1 - cm)
+        B = g_img.shape[0]
+        return sp.view(G, B, -1), tc.view(G, B, -1)
+
+
+def unimodal_dino_loss(s, t, tau_s=0.1, tau_t=0.04):
+    """UniModalDINOLightning.dino_loss (dino.py:1596-1635): after L2-normalising, the teacher
+    is also centred by its per-view batch mean."""
+    s = F.normalize(s, p=2, dim=-1)
+    t = F.normalize(t, p=2, dim=-1)
+    pt = F.softmax((t - t.mean(dim=1, keepdim=True)) / tau_t, dim=-1)
+    ls = F.log_softmax(s / tau_s, dim=-1)
+    total = 0
+    for i in range(s.shape[0]):
+        for j in range(t.shape[0]):
+            total = total + (-(pt[j] * ls[i]).sum(-1).mean())
+    return total / (s.shape[0] * t.shape[0])
+
+
+def pretrain_step(model, opt, g_img):
+    """training_structures.pretrain_dino's inner loop (dino_train.py:143-161): zero_grad ->
+    forward -> dino_loss -> backward -> AdamW.step -> update_teacher."""
+    opt.zero_grad()
+    s, t = model(g_img)
+    loss = unimodal_dino_loss(s, t)
+    loss.backward()
+    opt.step()
+    model.update_teacher()
+    return loss.detach()

@@ -467,6 +467,74 @@ def downstream_case(name, kind, E, D, P, B, nb_train, nb_valid, nb_test, epochs,
     print(f"{name}: knn {acc:.2f}% history {out['history'].tolist()} test {out['test_acc']:.2f}%")
 
 
+def pretrain_case(name, D, P, B, pseed, bseed, epochs, nb, out_dir, dt="float32", lr=1e-4):
+    """training_structures/dino_train.py:104-186 pretrain_dino (BASELINE config 1's CPU path),
+    by calling the reference's own function on CPU: AdamW(model.parameters(), lr) (torch's
+    default weight_decay 0.01), per batch zero_grad -> forward -> dino_loss(tau_s=0.1,
+    tau_t=0.04) -> backward -> step -> update_teacher (EMA AFTER the step, unlike the Lightning
+    path), epochs x nb batches of UniModalDINO(ImageEncoder) over 2 global views.
+    Harness-only adapters: the reference's current UniModalDINO.forward returns (student,
+    teacher, embeddings) while pretrain_dino unpacks two values, so a wrapper returns the first
+    two; dino_loss is UniModalDINOLightning.dino_loss called unbound with the given
+    temperatures (recording each step's loss); dropout 0."""
+    import csv as _csv
+    import tempfile
+    import torch
+    from torch.utils.data import DataLoader, TensorDataset
+    dtt = getattr(torch, dt)
+    import models.dino as rd
+    import training_structures.dino_train as tdt
+    torch.manual_seed(0)
+    model = rd.UniModalDINO(encoder_class=rd.ImageEncoder, output_dim=D, projection_dim=P,
+                            momentum=HP["momentum"], center_momentum=HP["center_momentum"], dropout=0.0)
+    spec = ospec.unimodal_dino_spec("image", D, P)
+    state = make_state(spec, pseed)
+    load_into(model, spec, state)
+    zero_dropout(model)
+    model = model.to(dtt)
+
+    class Two(torch.nn.Module):
+        def __init__(self, m):
+            super().__init__()
+            self.m = m
+
+        def forward(self, batch):
+            s_out, t_out, _ = self.m(batch)
+            return s_out, t_out
+
+        def update_teacher(self):
+            self.m.update_teacher()
+
+    losses = []
+
+    def dino_loss(s_out, t_out, tau_s=0.1, tau_t=0.04):
+        ns = types.SimpleNamespace(student_temperature=tau_s, teacher_temperature=tau_t)
+        loss = rd.UniModalDINOLightning.dino_loss(ns, s_out, t_out)
+        losses.append(loss.item())
+        return loss
+
+    bs = [make_multimodal_batch(B, 2, 0, bseed + i, with_originals=False) for i in range(nb)]
+    cat = lambda k: torch.from_numpy(np.concatenate([b[k] for b in bs])).to(dtt)  # noqa: E731
+    loader = DataLoader(TensorDataset(cat("g_img"), cat("g_aud"), cat("l_img"), cat("l_aud")),
+                        batch_size=B, shuffle=False)
+    with tempfile.TemporaryDirectory() as tmp:
+        tdt.pretrain_dino(Two(model), loader, dino_loss, num_epochs=epochs, learning_rate=lr,
+                          save_path=f"{tmp}/p/m.pt", log_path=f"{tmp}/p/log.csv")
+        log = [f for f in os.listdir(f"{tmp}/p") if f.startswith("log")][0]
+        with open(f"{tmp}/p/{log}") as f:
+            rows = list(_csv.reader(f))[1:]
+    out = {"meta_dims": np.array([D, P, B, epochs, nb, pseed, bseed]), "meta_lr": np.float64(lr),
+           "step_losses": np.array(losses, np.float64),
+           "epoch_losses": np.array([float(r[1]) for r in rows], np.float64)}
+    for k, v in model.state_dict().items():
+        if k == "center":
+            out["center"] = v.numpy().astype(STORE["dtype"])
+        elif not k.endswith("num_batches_tracked"):
+            summarize("state/" + k, v.numpy(), out)
+    np.savez_compressed(os.path.join(out_dir, name + ".npz"), **out)
+    print(f"{name}: step losses {np.array(losses)} epochs {out['epoch_losses']}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=HERE)
@@ -495,6 +563,7 @@ def main():
         ("probe_multi_central", probe_case, ("multi_central", 32, 32, 16, 6, 3, 2, 111, 1011), {}),
         ("probe_image_simple", probe_case, ("image_simple", 0, 64, 32, 6, 3, 2, 112, 1012), {}),
         ("simclr_small", simclr_case, (256, 256, 4, 107, 1007), {}),
+        ("pretrain_image_simple", pretrain_case, (64, 32, 8, 115, 1015, 2, 2), {}),
         ("downstream_multi_central", downstream_case,
          ("multi_central", 32, 32, 16, 8, 4, 2, 2, 3, 113, 1013), {}),
         ("downstream_image_simple", downstream_case,

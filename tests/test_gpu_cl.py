@@ -499,3 +499,44 @@ def test_bn_bwd_reduce_pooled_matches_y_path(ops, HC, mode, dt):
     assert np.allclose(s1[..., 0], s0[..., 0], rtol=1e-5, atol=1e-4)     # sum dz: identical routing
     tol = 2e-6 if dt == "f32" else 4e-3                                  # bf16: rounding of p
     assert rel(s1[..., 1], s0[..., 1]) < tol
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("mode", [0, 2])
+def test_bn_bwd_reduce_pooled_small_gamma(ops, mode, dt):
+    """channels whose |beta / gamma| would amplify the stored pooled value's rounding
+    (gamma 1e-2, beta 1 here) take xhat from y; the sums then match the y-path kernel."""
+    H, C, N, B = 28, 32, 6, 3
+    G = N // B
+    T = DT[dt]
+    g = torch.Generator(device="cuda").manual_seed(37)
+    y = torch.randn(N, H, H, C, generator=g, device="cuda").to(T)
+    gamma = torch.rand(C, generator=g, device="cuda") + 0.5
+    beta = torch.randn(C, generator=g, device="cuda") * 0.1
+    gamma[:8] = 1e-2
+    beta[:8] = 1.0
+    gamma[8] = -2e-3
+    beta[8] = -0.5
+    yf = y.float().view(G, B * H * H, C)
+    mean = yf.mean(1).reshape(-1).contiguous()
+    invstd = (yf.var(1, unbiased=False) + 1e-5).rsqrt().reshape(-1).contiguous()
+    scale = (gamma.view(1, C) * invstd.view(G, C)).reshape(-1).contiguous()
+    shift = (beta.view(1, C) - mean.view(G, C) * scale.view(G, C)).reshape(-1).contiguous()
+    Hp = H // 2
+    if mode == 0:
+        pooled = torch.empty(N, Hp, Hp, C, device="cuda", dtype=T)
+        gout = torch.randn(N, Hp, Hp, C, generator=g, device="cuda").to(T)
+    else:
+        pooled = torch.empty(N * C * Hp * Hp, device="cuda")
+        gout = torch.randn(N * C * Hp * Hp, generator=g, device="cuda")
+    ops.cl_bn_relu_pool(y, scale, shift, pooled, mode, N, B, C, H, H)
+    R = ops.cl_bn_bwd_rows(B, C, H, H, T)
+    p0 = torch.zeros(C * G * R * 2, device="cuda")
+    p1 = torch.zeros(C * G * R * 2, device="cuda")
+    ops.cl_bn_bwd_reduce(y, gout, mode, scale, shift, mean, invstd, p0, N, B, C, H, H)
+    ops.cl_bn_bwd_reduce_pooled(y, pooled, gout, mode, gamma, beta, mean, invstd, p1, N, B, C, H, H)
+    s0 = host(p0).reshape(C, G, R, 2).sum(2)
+    s1 = host(p1).reshape(C, G, R, 2).sum(2)
+    for c in range(9):       # the small-gamma channels: xhat from y, as the y-path kernel
+        assert rel(s1[c, :, 1], s0[c, :, 1]) < 5e-5, c
+    assert rel(s1[9:, :, 1], s0[9:, :, 1]) < (2e-6 if dt == "f32" else 4e-3)
