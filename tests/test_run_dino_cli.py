@@ -47,3 +47,23 @@ def test_run_dino_two_epochs_on_device(argv, capsys):
     assert recs[1]["lr"] < recs[0]["lr"] == pytest.approx(1e-4)
     assert m.model.engine.step_idx == 6
     assert m.trainer_.global_step == 6
+
+
+def test_submit_models_surface(tmp_path):
+    """batch_files/submit_models.py's command line: one run_dino job per model, unsupported
+    encoders rejected, torchrun with nproc = hardware.num_gpus when > 1."""
+    import yaml
+    from avdino import submit_models as SM
+    cmds = SM.main(["--models", "multi_central", "image_simple", "--training_mode", "mse",
+                    "--config", CFG, "--dry-run"])
+    assert cmds[0][1:] == ["-m", "avdino.run_dino", "--model", "multi_central", "--config", CFG,
+                           "--metric", "mlp_acc", "--training_mode", "mse"]
+    assert "--unimodal_model" in cmds[1] and "--training_mode" not in cmds[1]
+    with pytest.raises(SystemExit):
+        SM.main(["--models", "multi_vit", "--config", CFG, "--dry-run"])
+    cfg = yaml.safe_load(open(CFG))
+    cfg["hardware"]["num_gpus"] = 8
+    p8 = tmp_path / "c8.yaml"
+    p8.write_text(yaml.safe_dump(cfg))
+    c8 = SM.main(["--models", "multi_central", "--config", str(p8), "--dry-run"])[0]
+    assert "torch.distributed.run" in c8 and "--nproc-per-node=8" in c8
