@@ -1,0 +1,439 @@
+// 3x3 convolutions (pad 1) of the SimCLR / unimodal image and spectrogram encoders
+// (models/dino.py:18-73 image_encoder / audio_encoder: 32..256 channels on 56x56 .. 7x7 maps)
+// as an implicit GEMM on v_mfma_f32_16x16x32_bf16, NHWC bf16, forward (+ bias and the fused
+// BatchNorm partial statistics) and input gradient (the same kernel on dY with the flipped,
+// channel-swapped weights).
+//
+// Why not conv_cl_kernel for these: it reads its weight fragments from global memory inside
+// the k-loop and keeps small pixel tiles, which for 32..256-channel 3x3 layers leaves the
+// MFMAs at 8-13 % of peak (config 4 profile, r2).  Here a block owns a tile of up to 448 output
+// pixels (TR rows of one sample, or NS whole small maps) x 64 output channels, and for each
+// 32-channel input chunk stages
+//   * the input tile + 1-pixel halo, 32 channels = one 64-byte row per pixel,
+//   * the 64 x 9 x 32 weight slice, one 64-byte row per (tap, output channel),
+// into LDS once; every tap of the chunk then reads both operands from LDS.  64-byte rows carry
+// their four 16-byte chunks XOR-swizzled by (row >> 2) & 3, so the 16 rows one MFMA fragment
+// read touches land on 16 distinct 4-bank groups (conflict-free ds_read_b128).
+//   A = weights  [16 output channels][32 input channels of one tap]
+//   B = input    [32 input channels][16 output pixels], shifted by the tap
+//   C: lane holds 4 consecutive output channels of one pixel -> one 8-byte NHWC store.
+// Each wave owns GPW 16-pixel groups (interleaved over the waves) x NT 16-channel tiles.
+#include <algorithm>
+
+#include "common.h"
+
+using namespace avd;
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f4;
+typedef __attribute__((ext_vector_type(4))) unsigned u4;
+
+constexpr int CH = 32;            // input channels per LDS chunk (one MFMA k-step per tap)
+constexpr int ROWB = CH * 2;      // bytes per LDS row
+
+__device__ const u4 kZero3 = {0u, 0u, 0u, 0u};
+
+// element offset of 16-byte chunk q (0..3) of LDS row r
+__device__ __forceinline__ int swz(int r, int q) { return r * CH + ((q ^ ((r >> 2) & 3)) << 3); }
+
+template <int NT, int GPW>
+__global__ __launch_bounds__(256, 2) void conv3_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ wk, const float* __restrict__ bias,
+    bf16* __restrict__ y, float* __restrict__ stats, int N, int H, int W, int C, int O, int Kpad,
+    int TR, int NS, int tilesPS, int nrows) {
+  extern __shared__ __attribute__((aligned(16))) bf16 smem[];
+  constexpr int BO = NT * 16;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int ti = blockIdx.x;
+  const int sg = ti / tilesPS, tt = ti - sg * tilesPS;
+  const int n0 = sg * NS, y0 = tt * TR;
+  const int o0 = blockIdx.z * BO;
+  const int IW = W + 2, IR = TR + 2;
+  const int npix = NS * IR * IW;           // staged input pixels (tile + halo)
+  bf16* xs = smem;                         // [npix] rows
+  bf16* ws = smem + npix * CH;             // [9][BO] rows
+  const int TP = NS * TR * W;              // tile output pixels
+
+  // this lane's pixels: groups wave + 4j, pixel r16 of each
+  int base[GPW];
+  bool pv[GPW];
+  int pn[GPW], py[GPW], px[GPW];
+#pragma unroll
+  for (int j = 0; j < GPW; ++j) {
+    const int p = (wave + 4 * j) * 16 + r16;
+    const int s = p / (TR * W), rem = p - s * (TR * W);
+    const int r = rem / W, xx = rem - r * W;
+    pv[j] = p < TP && y0 + r < H;
+    base[j] = pv[j] ? (s * IR + r) * IW + xx : 0;    // input row of tap (0, 0)
+    pn[j] = n0 + s; py[j] = y0 + r; px[j] = xx;
+  }
+  f4 acc[GPW][NT];
+#pragma unroll
+  for (int j = 0; j < GPW; ++j)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[j][t] = f4{0.f, 0.f, 0.f, 0.f};
+
+  for (int c0 = 0; c0 < C; c0 += CH) {
+    if (c0) __syncthreads();
+    // ---- stage the input tile + halo (zero outside the image) and the weight slice
+    for (int t = tid; t < npix * 4; t += 256) {
+      const int q = t & 3, pix = t >> 2;
+      const int sr = pix / IW, ix = pix - sr * IW - 1;
+      const int s = sr / IR, iy = y0 + sr - s * IR - 1;
+      const int n = n0 + s;
+      const bool ok = n < N && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      const u4 v = ldg16(ok ? (const void*)(x + (((size_t)n * H + iy) * W + ix) * C + c0 + 8 * q)
+                            : (const void*)&kZero3);
+      *reinterpret_cast<u4*>(xs + swz(pix, q)) = v;
+    }
+    for (int t = tid; t < 9 * BO * 4; t += 256) {
+      const int q = t & 3, row = t >> 2;
+      const int tap = row / BO, o = row - tap * BO;
+      *reinterpret_cast<u4*>(ws + swz(row, q)) =
+          ldg16(wk + (size_t)(o0 + o) * Kpad + tap * C + c0 + 8 * q);
+    }
+    __syncthreads();
+    // ---- 9 taps x NT x GPW MFMAs from LDS
+#pragma unroll 3
+    for (int tap = 0; tap < 9; ++tap) {
+      const int toff = (tap / 3) * IW + tap % 3;
+      bf16x8 a[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        a[t] = *reinterpret_cast<const bf16x8*>(ws + swz(tap * BO + 16 * t + r16, g));
+#pragma unroll
+      for (int j = 0; j < GPW; ++j) {
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(xs + swz(base[j] + toff, g));
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t], b, acc[j][t], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue: bias, bf16 rounding, NHWC store, BN partial sums of the stored values
+  float ss[NT][4], sq[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int co = o0 + 16 * t + 4 * g;
+    float bv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bv[i] = bias ? bias[co + i] : 0.f;
+      ss[t][i] = 0.f;
+      sq[t][i] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < GPW; ++j) {
+      if (!pv[j]) continue;
+      const uint32_t lo = pack_bf16x2(acc[j][t][0] + bv[0], acc[j][t][1] + bv[1]);
+      const uint32_t hi = pack_bf16x2(acc[j][t][2] + bv[2], acc[j][t][3] + bv[3]);
+      const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                          __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ss[t][i] += v[i];
+        sq[t][i] = fmaf(v[i], v[i], sq[t][i]);
+      }
+      *reinterpret_cast<uint2*>(y + (((size_t)pn[j] * H + py[j]) * W + px[j]) * O + co) =
+          make_uint2(lo, hi);
+    }
+  }
+  if (!stats) return;
+  const int row = ti * 4 + wave;     // one partial row per (tile, wave)
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float a = ss[t][i], q = sq[t][i];
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) {
+        a += __shfl_xor(a, m, 64);
+        q += __shfl_xor(q, m, 64);
+      }
+      if (r16 == 0) {
+        const int co = o0 + 16 * t + 4 * g + i;
+        stats[((size_t)co * nrows + row) * 2] = a;
+        stats[((size_t)co * nrows + row) * 2 + 1] = q;
+      }
+    }
+}
+
+struct Plan3 { int TR, NS, GPW, tilesPS; };
+
+// The tile with the best utilisation of GPW*64 pixel slots (ties: more pixels); whole small
+// maps are packed NS per block with NS | B (a tile never straddles two BatchNorm groups) and
+// the staged input stays <= 40 KB (with the 36 KB weight slice: 2 blocks per CU).
+Plan3 plan3(int H, int W, int B) {
+  Plan3 best{0, 0, 0, 0};
+  double bu = -1;
+  const char* fg = getenv("AVDINO_C3_GPW");      // A/B experiments: force the pixel groups
+  for (int gpw : {4, 7}) {
+    if (fg && atoi(fg) != gpw) continue;
+    const int cap = gpw * 64;
+    auto consider = [&](int TR, int NS) {
+      if (TR <= 0 || NS <= 0 || TR * W * NS > cap) return;
+      if ((size_t)NS * (TR + 2) * (W + 2) * ROWB > 40 * 1024) return;
+      const int tps = avd_cdiv(H, TR);
+      const double u = (double)H * W * NS / ((double)tps * cap);
+      if (u > bu + 1e-9 || (u > bu - 1e-9 && TR * NS > best.TR * best.NS)) {
+        bu = u;
+        best = Plan3{TR, NS, gpw, tps};
+      }
+    };
+    if (H * W <= cap)
+      for (int ns = cap / (H * W); ns >= 1; --ns)
+        if (B % ns == 0) consider(H, ns);
+    for (int tr = 1; tr <= H && tr * W <= cap; ++tr) consider(tr, 1);
+  }
+  return best;
+}
+
+template <int NT, int GPW>
+int launch3(const Plan3& p, const void* x, const void* wk, const float* bias, void* y, float* stats,
+            int N, int H, int W, int C, int O, hipStream_t st) {
+  constexpr int BO = NT * 16;
+  const size_t lds = ((size_t)p.NS * (p.TR + 2) * (W + 2) + 9 * BO) * ROWB;
+  const int total = avd_cdiv(N, p.NS) * p.tilesPS;
+  dim3 grid(total, 1, O / BO);
+  conv3_kernel<NT, GPW><<<grid, 256, lds, st>>>((const bf16*)x, (const bf16*)wk, bias, (bf16*)y,
+                                                stats, N, H, W, C, O, 9 * C, p.TR, p.NS, p.tilesPS,
+                                                total * 4);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+}  // namespace
+
+// Served: bf16, 3x3, pad 1, C (input channels of the executed conv) % 32 == 0, O % 32 == 0.
+bool avd_c3_serves(int dt, int C, int O, int K, int pad) {
+  if (getenv("AVDINO_C3_OFF")) return false;
+  return dt == AVD_BF16 && K == 3 && pad == 1 && C % CH == 0 && C >= CH && O % 32 == 0;
+}
+
+// BN partial rows per group of avd_c3_conv (fwd): 4 per tile
+int avd_c3_stat_rows(int H, int W, int B) {
+  const Plan3 p = plan3(H, W, B);
+  return p.NS ? (B / p.NS) * p.tilesPS * 4 : 0;
+}
+
+// y = conv3x3(x) (+ bias, + stats) over NHWC bf16 maps; x [N][H][W][C], wk the avd_cl weight
+// layout ([O][9*C], tap-major) of the executed conv (the dgrad layout for an input gradient).
+int avd_c3_conv(const void* x, const void* wk, const float* bias, void* y, float* stats, int N,
+                int B, int H, int W, int C, int O, hipStream_t st) {
+  const Plan3 p = plan3(H, W, B);
+  if (!p.NS || N % p.NS) return AVD_ERR_SHAPE;
+  const char* fn = getenv("AVDINO_C3_NT");       // A/B experiments: force the channel tiles
+  const int NT = fn ? atoi(fn) : (O % 64 == 0 ? 4 : 2);
+#define AVD_L(NTT, G) \
+  if (NT == NTT && p.GPW == G) return launch3<NTT, G>(p, x, wk, bias, y, stats, N, H, W, C, O, st);
+  AVD_L(4, 4) AVD_L(4, 7) AVD_L(2, 4) AVD_L(2, 7)
+#undef AVD_L
+  return AVD_ERR_SHAPE;
+}
+
+// ============================================================================ weight gradient
+// dW[co][ci][tap] = sum_p dY[p][co] * X[p + tap][ci] for the same 3x3 layers, as a GEMM
+// M = co (a group of BO), N = (tap, ci) of one 32-channel input group = 18 column tiles,
+// K = output pixels, split over pixel chunks (deterministic slabs, summed by avd_sum_rows).
+// A block stages one strip (TR output rows of one sample) at a time: dY [pixels][BO] and
+// X [halo rows][halo cols][32]; both MFMA operands are pixel-major there, so their fragments
+// come from ds_read_b64_tr_b16 (4 pixels x 4 channels per read, two reads per fragment; the
+// k-step's 32 pixels are ordered so that each half-wave reads 8 consecutive pixels: the
+// wgrad_ws.hip scheme).  Pixel rows are padded to WO8 (multiple of 8) so a 4-pixel run never
+// crosses a row; the pad pixels' dY stays zero.  The groups (co, ci) of one pixel chunk are
+// consecutive logical blocks mapped onto one XCD, so its strips are re-read from that XCD's L2.
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) short s4w;
+typedef __attribute__((ext_vector_type(2))) unsigned u2w;
+
+__device__ __forceinline__ u2w trd(const bf16* p) {
+  const s4w v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s4w*)(reinterpret_cast<uintptr_t>(p)));
+  return __builtin_bit_cast(u2w, v);
+}
+__device__ __forceinline__ bf16x8 fr8(u2w lo, u2w hi) {
+  return __builtin_bit_cast(bf16x8, u4{lo.x, lo.y, hi.x, hi.y});
+}
+__device__ __forceinline__ int kpx(int g, int h, int q) { return 16 * (g >> 1) + 8 * h + 4 * (g & 1) + q; }
+
+constexpr int XS3 = CH + 16;     // X LDS pixel stride (elements)
+
+template <int BO>
+__global__ __launch_bounds__(256, 2) void wgrad3_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ dy, float* __restrict__ parts, int N,
+    int H, int W, int Cin, int Cout, int TR, int nchunk, int ngroup) {
+  constexpr int DYS = BO + 16;               // dY LDS pixel stride (elements)
+  constexpr int MTW = BO / 32;               // o-tiles per wave (2 wave rows)
+  constexpr int NW = 9;                      // column tiles per wave (2 wave columns of 9)
+  extern __shared__ __attribute__((aligned(16))) bf16 smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4, r16 = lane & 15, q4 = r16 >> 2, p4 = r16 & 3;
+  const int wo = wave & 1, wc = wave >> 1;
+  // XCD-aware: logical block L = (hw block % 8) * (grid / 8) + hw block / 8 (grid % 8 == 0)
+  const int nb = gridDim.x;
+  const int L = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);
+  const int chunk = L / ngroup, grp = L - chunk * ngroup;
+  const int ngo = Cout / BO;
+  const int o0 = (grp % ngo) * BO, c0 = (grp / ngo) * CH;
+  const int WO8 = (W + 7) & ~7, XW = WO8 + 2, XR = TR + 2;
+  const int SP = TR * WO8;                   // strip pixels (incl. row pads)
+  const int KST = (SP + 31) / 32;
+  bf16* dys = smem;                          // [KST*32][DYS]
+  bf16* xs = smem + KST * 32 * DYS;          // [XR][XW][XS3]
+  const int sps = H / TR;
+  const int nstrip = N * sps;
+  const int st0 = (int)((long long)chunk * nstrip / nchunk);
+  const int st1 = (int)((long long)(chunk + 1) * nstrip / nchunk);
+
+  // pad pixels (ox >= W, and the k tail) of dY stay zero for the whole launch
+  for (int i = tid; i < KST * 32 * (DYS / 8); i += 256) {
+    const int pix = i / (DYS / 8), ox = pix % WO8;
+    if (ox >= W || pix >= SP) *reinterpret_cast<u4*>(dys + (size_t)i * 8) = u4{0u, 0u, 0u, 0u};
+  }
+  // this lane's column tiles: ct = wc*9 + j -> tap = ct >> 1, ci tile = ct & 1
+  int xo[NW];
+#pragma unroll
+  for (int j = 0; j < NW; ++j) {
+    const int ct = wc * NW + j, tap = ct >> 1;
+    xo[j] = ((tap / 3) * XW + tap % 3) * XS3 + 16 * (ct & 1) + 4 * p4;
+  }
+  f4 acc[MTW][NW];
+#pragma unroll
+  for (int m = 0; m < MTW; ++m)
+#pragma unroll
+    for (int j = 0; j < NW; ++j) acc[m][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  for (int st = st0; st < st1; ++st) {
+    const int n = st / sps, y0 = (st - n * sps) * TR;
+    __syncthreads();
+    // dY strip: TR rows x W pixels x BO channels (16-byte tasks)
+    const int dtask = TR * W * (BO / 8);
+    for (int t = tid; t < dtask; t += 256) {
+      const int q = t % (BO / 8), pix = t / (BO / 8);
+      const int r = pix / W, ox = pix - r * W;
+      *reinterpret_cast<u4*>(dys + (r * WO8 + ox) * DYS + 8 * q) =
+          ldg16(dy + (((size_t)n * H + y0 + r) * W + ox) * Cout + o0 + 8 * q);
+    }
+    // X strip + halo: rows y0-1 .. y0+TR, cols -1 .. WO8 (zero outside the image)
+    const int xtask = XR * XW * (CH / 8);
+    for (int t = tid; t < xtask; t += 256) {
+      const int q = t & 3, pix = t >> 2;
+      const int r = pix / XW, c = pix - r * XW;
+      const int iy = y0 - 1 + r, ix = c - 1;
+      const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      *reinterpret_cast<u4*>(xs + pix * XS3 + 8 * q) =
+          ldg16(ok ? (const void*)(x + (((size_t)n * H + iy) * W + ix) * Cin + c0 + 8 * q)
+                   : (const void*)&kZero3);
+    }
+    __syncthreads();
+    for (int ks = 0; ks < KST; ++ks) {
+      const int P0 = 32 * ks;
+      bf16x8 a[MTW];
+#pragma unroll
+      for (int m = 0; m < MTW; ++m) {
+        const int co = 16 * (wo * MTW + m) + 4 * p4;
+        a[m] = fr8(trd(dys + (P0 + kpx(g, 0, q4)) * DYS + co),
+                   trd(dys + (P0 + kpx(g, 1, q4)) * DYS + co));
+      }
+      int xb[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int P = min(P0 + kpx(g, h, q4), SP - 1);     // k tail: dY is 0 there
+        const int r = P / WO8, ox = P - r * WO8;
+        xb[h] = (r * XW + ox) * XS3;
+      }
+#pragma unroll
+      for (int j = 0; j < NW; ++j) {
+        const bf16x8 b = fr8(trd(xs + xb[0] + xo[j]), trd(xs + xb[1] + xo[j]));
+#pragma unroll
+        for (int m = 0; m < MTW; ++m)
+          acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], b, acc[m][j], 0, 0, 0);
+      }
+    }
+  }
+
+  // slab write [co][ci][tap] through LDS, one o-tile per wave row per pass (32 rows of
+  // 32 x 9 floats), so the rows leave as contiguous float4 stores
+  float* tb = reinterpret_cast<float*>(smem);   // [32][32 * 9]
+  constexpr int PER = CH * 9;
+  float* out = parts + (size_t)chunk * Cout * Cin * 9;
+#pragma unroll
+  for (int m = 0; m < MTW; ++m) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+      const int ct = wc * NW + j, tap = ct >> 1, ci = 16 * (ct & 1) + r16;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) tb[(16 * wo + 4 * g + i) * PER + ci * 9 + tap] = acc[m][j][i];
+    }
+    __syncthreads();
+    for (int e = tid; e < 32 * PER / 4; e += 256) {
+      const int row = e / (PER / 4), c4 = e - row * (PER / 4);
+      const int co = 16 * ((row >> 4) * MTW + m) + (row & 15);
+      reinterpret_cast<float4*>(out + ((size_t)(o0 + co) * Cin + c0) * 9)[c4] =
+          reinterpret_cast<const float4*>(tb)[e];
+    }
+  }
+}
+
+size_t wg3_lds(int TR, int W, int BO) {
+  const int wo8 = (W + 7) & ~7, kst = (TR * wo8 + 31) / 32;
+  return std::max((size_t)kst * 32 * (BO + 16) * 2 + (size_t)(TR + 2) * (wo8 + 2) * XS3 * 2,
+                  (size_t)32 * CH * 9 * 4);
+}
+
+// strip rows for a map of H x W: the largest divisor of H whose strip fits 72 KB of LDS
+// (two blocks per CU) within 256 pixels (AVDINO_C3_TR overrides)
+int tr3(int H, int W, int BO) {
+  if (const char* e = getenv("AVDINO_C3_TR")) {
+    const int t = atoi(e);
+    if (t > 0 && H % t == 0) return t;
+  }
+  const int wo8 = (W + 7) & ~7;
+  int best = 1;
+  for (int tr = 1; tr <= H; ++tr)
+    if (H % tr == 0 && tr * wo8 <= 256 && wg3_lds(tr, W, BO) <= 72 * 1024) best = tr;
+  return best;
+}
+
+int wg3_bo(int Cout) { return Cout % 128 == 0 ? 128 : 64; }
+
+}  // namespace
+
+// Slabs of avd_c3_wgrad for (N, Cout, Cin), or 0 if not served.
+int avd_c3_wgrad_chunks(int N, int Cout, int Cin, int K) {
+  if (getenv("AVDINO_C3_OFF") || K != 3 || Cin % CH || Cout % 64) return 0;
+  const int groups = (Cout / wg3_bo(Cout)) * (Cin / CH);
+  static const int target = getenv("AVDINO_C3_WBLK") ? atoi(getenv("AVDINO_C3_WBLK")) : 512;
+  int nchunk = std::max(1, target / groups);
+  nchunk = std::min(nchunk, N);
+  // the grid (nchunk * groups) must be a multiple of 8 for the XCD remap
+  while ((nchunk * groups) % 8) ++nchunk;
+  return nchunk;
+}
+
+// 1 = launched, 0 = not served, < 0 = error.  parts holds avd_c3_wgrad_chunks slabs.
+int avd_c3_wgrad(const void* x, const void* dy, int dt, float* parts, int N, int Cin, int H, int W,
+                 int Cout, int K, int pad, hipStream_t st) {
+  if (dt != AVD_BF16 || pad != 1) return 0;
+  const int nchunk = avd_c3_wgrad_chunks(N, Cout, Cin, K);
+  if (!nchunk) return 0;
+  const int BO = wg3_bo(Cout), TR = tr3(H, W, BO);
+  const int groups = (Cout / BO) * (Cin / CH);
+  const size_t lds = wg3_lds(TR, W, BO);
+  if (lds > 80 * 1024) return 0;
+  const int grid = nchunk * groups;
+  if (BO == 128)
+    wgrad3_kernel<128><<<grid, 256, lds, st>>>((const bf16*)x, (const bf16*)dy, parts, N, H, W,
+                                               Cin, Cout, TR, nchunk, groups);
+  else
+    wgrad3_kernel<64><<<grid, 256, lds, st>>>((const bf16*)x, (const bf16*)dy, parts, N, H, W,
+                                              Cin, Cout, TR, nchunk, groups);
+  AVD_CHECK_LAUNCH();
+  return 1;
+}

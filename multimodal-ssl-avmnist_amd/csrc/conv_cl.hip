@@ -451,7 +451,14 @@ int avd_ws_conv_fwd(const void* x, const void* wk, const float* bias, void* y, f
 int avd_ws_conv_dgrad(const void* dy, const void* wk_d, void* dx, int dt, int N, int Cin, int H,
                       int W, int Cout, int K, int pad, hipStream_t st);
 
+bool avd_c3_serves(int dt, int C, int O, int K, int pad);
+int avd_c3_stat_rows(int H, int W, int B);
+int avd_c3_conv(const void* x, const void* wk, const float* bias, void* y, float* stats, int N,
+                int B, int H, int W, int C, int O, hipStream_t st);
+
 int avd_cl_stat_rows_impl(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt) {
+  // 3x3 layers are pad 1 throughout (the conv entry point rejects other paddings there)
+  if (avd_c3_serves(dt, Cin, Cout, K, 1)) return avd_c3_stat_rows(Ho, Wo, B);
   if (const int r = avd_ws_stat_rows(Ho, Wo, B, K, Cin, Cout, dt)) return r;
   if (avd_c1p8_eligible(dt, Cin, Cout, K, Ho, Wo)) return avd_c1p8_stat_rows(Ho, B);
   const Plan p = plan_cl(Ho, Wo, B, K, pix_bytes(dt, Cin), Cin == 1, Cout);
@@ -546,6 +553,11 @@ int avd_cl_conv_fwd_impl(const void* x, const void* wk, const float* bias, void*
     if (pad != 2) return AVD_ERR_SHAPE;
     return avd_c1p8_fwd(x, wk, bias, y, stats, N, H, W, st);
   }
+  // the 32..256-channel 3x3 layers: LDS-staged implicit GEMM (conv3.hip)
+  if (avd_c3_serves(dt, Cin, Cout, K, 1)) {
+    if (pad != 1) return AVD_ERR_SHAPE;
+    return avd_c3_conv(x, wk, bias, y, stats, N, B, H, W, Cin, Cout, st);
+  }
   // the mid-layer shapes: weights-stationary persistent kernel (conv_ws.hip)
   if (const int r = avd_ws_conv_fwd(x, wk, bias, y, stats, dt, N, B, Cin, H, W, Cout, K, pad, st))
     return r > 0 ? AVD_OK : r;
@@ -564,6 +576,8 @@ int avd_cl_conv_dgrad_impl(const void* dy, const void* wk_d, void* dx, int dt, i
                            int H, int W, int Cout, int K, int pad, hipStream_t st) {
   const int Ho = H + 2 * pad - K + 1, Wo = W + 2 * pad - K + 1;
   if (Ho <= 0 || Wo <= 0 || Cout % 8 || Cin % 4 || K - 1 - pad < 0) return AVD_ERR_SHAPE;
+  if (avd_c3_serves(dt, Cout, Cin, K, K - 1 - pad) && Ho == H && Wo == W)
+    return avd_c3_conv(dy, wk_d, nullptr, dx, nullptr, N, N, H, W, Cout, Cin, st);
   if (const int r = avd_ws_conv_dgrad(dy, wk_d, dx, dt, N, Cin, H, W, Cout, K, pad, st))
     return r > 0 ? AVD_OK : r;
   const Plan p = plan_cl(H, W, N, K, pix_bytes(dt, Cout), false, Cin);

@@ -435,7 +435,12 @@ int avd_wg_chunks(int N, int Cout, int Cin, int K);
 int avd_wg_conv_wgrad(const void* x, const void* dy, int dt, float* parts, int N, int Cin, int H,
                       int W, int Cout, int K, int pad, hipStream_t st);
 
+int avd_c3_wgrad_chunks(int N, int Cout, int Cin, int K);
+int avd_c3_wgrad(const void* x, const void* dy, int dt, float* parts, int N, int Cin, int H, int W,
+                 int Cout, int K, int pad, hipStream_t st);
+
 int avd_cl_wgrad_chunks_impl(int N, int Cout, int Cin, int K) {
+  if (const int c = avd_c3_wgrad_chunks(N, Cout, Cin, K)) return c;   // 3x3 layers (conv3.hip)
   // the mid-layer shapes use one slab per persistent block of wgrad_ws.hip (the legacy kernel
   // takes any slab count, so a fallback launch for another H sizes its slabs the same way)
   if (const int c = avd_wg_chunks(N, Cout, Cin, K)) return c;
@@ -450,6 +455,8 @@ int avd_cl_conv_wgrad_impl(const void* x, const void* dy, int dt, float* parts, 
   if (Cin != 1 && Cin % 8) return AVD_ERR_SHAPE;
   if (Cout % 8) return AVD_ERR_SHAPE;
   if (const int r = avd_wg_conv_wgrad(x, dy, dt, parts, N, Cin, H, W, Cout, K, pad, st))
+    return r > 0 ? AVD_OK : r;
+  if (const int r = avd_c3_wgrad(x, dy, dt, parts, N, Cin, H, W, Cout, K, pad, st))
     return r > 0 ? AVD_OK : r;
   const int chunks = avd_cl_wgrad_chunks_impl(N, Cout, Cin, K);
   if (dt == AVD_BF16)

@@ -181,11 +181,15 @@ def test_conv1_recompute_bench_size(ops):
 # (Cin, H, Cout, K, pad, N): the CentralNet audio conv2-4 and image conv2 at bench-scale N
 WS_BENCH = [(8, 56, 16, 5, 2, 2048), (16, 28, 32, 5, 2, 2048), (32, 14, 64, 5, 2, 4096),
             (32, 14, 64, 5, 0, 4096)]
+# the 3x3 layers of the SimCLR / unimodal encoders at BASELINE config 4's B = 2048 (conv3.hip)
+C3_BENCH = [(32, 56, 64, 3, 1, 2048), (64, 28, 128, 3, 1, 2048), (128, 14, 256, 3, 1, 2048),
+            (32, 14, 64, 3, 1, 2048), (64, 7, 128, 3, 1, 2048)]
 
 
-@pytest.mark.parametrize("shape", WS_BENCH)
+@pytest.mark.parametrize("shape", WS_BENCH + C3_BENCH)
 def test_ws_kernels_bench_size(ops, shape):
-    """conv_ws forward (+ stats), conv_ws dgrad and wgrad_ws at bench-scale N vs float64."""
+    """conv_ws / conv3 forward (+ stats), dgrad and weight gradient at bench-scale N vs
+    float64."""
     Ci, H, Co, K, pad, N = shape
     B = 1024
     G = N // B

@@ -1,0 +1,55 @@
+"""Time the 3x3 conv kernels (fwd / dgrad / wgrad) of config 4 per shape with HIP events.
+    AVDINO_C3_NT=2 AVDINO_C3_GPW=4 python tools/c3bench.py"""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "multimodal-ssl-avmnist_amd")]
+from avdino import ops  # noqa: E402
+
+T = torch.bfloat16
+SHAPES = [(32, 56, 64), (64, 28, 128), (128, 14, 256), (32, 14, 64), (64, 7, 128)]
+
+
+def timeit(fn, n=10):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(n):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n * 1e3
+
+
+def main():
+    N, B = 2048, 1024
+    tag = f"NT={os.environ.get('AVDINO_C3_NT', '-')} GPW={os.environ.get('AVDINO_C3_GPW', '-')}"
+    for Ci, H, Co in SHAPES:
+        x = torch.randn(N, H, H, Ci, device="cuda").to(T)
+        w = torch.randn(Co, Ci, 3, 3, device="cuda") * 0.05
+        wk = torch.empty(ops.cl_weight_elems(Co, Ci, 3, 0), device="cuda", dtype=T)
+        wd = torch.empty(ops.cl_weight_elems(Co, Ci, 3, 1), device="cuda", dtype=T)
+        ops.cl_weight_layout(w, wk, 0)
+        ops.cl_weight_layout(w, wd, 1)
+        bias = torch.zeros(Co, device="cuda")
+        y = torch.empty(N, H, H, Co, device="cuda", dtype=T)
+        R = ops.cl_stat_rows(H, H, B, 3, Ci, Co, T)
+        st = torch.empty(Co * (N // B) * R * 2, device="cuda")
+        dx = torch.empty_like(x)
+        fl = 2.0 * N * H * H * Co * Ci * 9
+        tf = timeit(lambda: ops.cl_conv_fwd(x, wk, bias, y, st, N, B, Ci, H, H, Co, 3, 1))
+        td = timeit(lambda: ops.cl_conv_dgrad(y, wd, dx, N, Ci, H, H, Co, 3, 1))
+        nch = ops.cl_wgrad_chunks(N, Co, Ci, 3)
+        parts = torch.empty(nch * Co * Ci * 9, device="cuda")
+        tw = timeit(lambda: ops.cl_conv_wgrad(x, y, parts, N, Ci, H, H, Co, 3, 1), 3)
+        print(f"{tag} {Ci:4d}->{Co:4d} @{H:3d}: fwd {tf:8.1f} us ({fl / tf / 1e6:6.1f} TF/s)  "
+              f"dgrad {td:8.1f} us ({fl / td / 1e6:6.1f})  wgrad {tw:8.1f} us ({fl / tw / 1e6:6.1f})",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

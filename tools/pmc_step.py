@@ -43,18 +43,29 @@ def main():
     json.dump({"step:mse": {"traffic_bytes": step / B, "fetch_raw_bytes_per_step": res["FETCH_SIZE"],
                             "write_bytes_per_step": res["WRITE_SIZE"], "unit": "bytes per pair"}},
               open(os.path.join(root, f"traffic_step_{tag}.json"), "w"), indent=1)
+    def short(name):
+        return name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:72]
+
     per = {}
     for r in rows(os.path.join(root, f"pmc_sq_{tag}")):
-        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:70]
-        d = per.setdefault(k, {})
+        d = per.setdefault(short(r["Kernel_Name"]), {})
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-        d["dispatches"] = d.get("dispatches", 0)
-    print("\nper kernel (2 warm-up + 1 timed step, eager): MFMA busy / SQ busy cycles, bf16 MOPS")
-    for k, d in sorted(per.items(), key=lambda kv: -kv[1].get("SQ_VALU_MFMA_BUSY_CYCLES", 0))[:30]:
-        busy = d.get("SQ_BUSY_CYCLES", 0)
-        mf = d.get("SQ_VALU_MFMA_BUSY_CYCLES", 0)
-        print(f"{mf:14.4g} {busy:14.4g}  util {mf / busy if busy else 0:6.3f}  "
-              f"mops_bf16 {d.get('SQ_INSTS_VALU_MFMA_MOPS_BF16', 0):12.4g}  {k}")
+    dur = {}
+    for f in glob.glob(os.path.join(root, f"pmc_sq_{tag}", "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            dur[k] = dur.get(k, 0.0) + (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    peak = 2.5e15
+    print("\nper kernel over one counter run (2 warm-up + 1 step, eager, serialised by the counter "
+          "pass): bf16 MFMA FLOPs = SQ_INSTS_VALU_MFMA_MOPS_BF16 x 512, over the kernels' summed "
+          "duration, as a fraction of the 2.5 PFLOP/s dense bf16 peak; MFMA-busy cycles raw")
+    print(f"{'TFLOP/s':>9} {'of peak':>8} {'time ms':>8} {'MOPS bf16':>11} {'MFMA busy':>11}  kernel")
+    for k, d in sorted(per.items(), key=lambda kv: -kv[1].get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0))[:30]:
+        fl = d.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0) * 512
+        t = dur.get(k, 0.0)
+        tf = fl / t / 1e12 if t else 0.0
+        print(f"{tf:9.1f} {tf * 1e12 / peak:8.3f} {t * 1e3:8.3f} {d.get('SQ_INSTS_VALU_MFMA_MOPS_BF16', 0):11.4g} "
+              f"{d.get('SQ_VALU_MFMA_BUSY_CYCLES', 0):11.4g}  {k}")
 
 
 if __name__ == "__main__":
