@@ -28,7 +28,11 @@ def timeit(fn, n=10):
 def main():
     N, B = 2048, 1024
     tag = f"NT={os.environ.get('AVDINO_C3_NT', '-')} GPW={os.environ.get('AVDINO_C3_GPW', '-')}"
-    for Ci, H, Co in SHAPES:
+    only = os.environ.get("C3B_ONLY")            # profiling: one op ("fwd"/"dgrad"/"wgrad")
+    pick = os.environ.get("C3B_SHAPE")           # profiling: one shape index
+    for si, (Ci, H, Co) in enumerate(SHAPES):
+        if pick is not None and si != int(pick):
+            continue
         x = torch.randn(N, H, H, Ci, device="cuda").to(T)
         w = torch.randn(Co, Ci, 3, 3, device="cuda") * 0.05
         wk = torch.empty(ops.cl_weight_elems(Co, Ci, 3, 0), device="cuda", dtype=T)
@@ -41,11 +45,15 @@ def main():
         st = torch.empty(Co * (N // B) * R * 2, device="cuda")
         dx = torch.empty_like(x)
         fl = 2.0 * N * H * H * Co * Ci * 9
-        tf = timeit(lambda: ops.cl_conv_fwd(x, wk, bias, y, st, N, B, Ci, H, H, Co, 3, 1))
-        td = timeit(lambda: ops.cl_conv_dgrad(y, wd, dx, N, Ci, H, H, Co, 3, 1))
         nch = ops.cl_wgrad_chunks(N, Co, Ci, 3)
         parts = torch.empty(nch * Co * Ci * 9, device="cuda")
-        tw = timeit(lambda: ops.cl_conv_wgrad(x, y, parts, N, Ci, H, H, Co, 3, 1), 3)
+        tf = td = tw = float("nan")
+        if only in (None, "fwd"):
+            tf = timeit(lambda: ops.cl_conv_fwd(x, wk, bias, y, st, N, B, Ci, H, H, Co, 3, 1))
+        if only in (None, "dgrad"):
+            td = timeit(lambda: ops.cl_conv_dgrad(y, wd, dx, N, Ci, H, H, Co, 3, 1))
+        if only in (None, "wgrad"):
+            tw = timeit(lambda: ops.cl_conv_wgrad(x, y, parts, N, Ci, H, H, Co, 3, 1), 3)
         print(f"{tag} {Ci:4d}->{Co:4d} @{H:3d}: fwd {tf:8.1f} us ({fl / tf / 1e6:6.1f} TF/s)  "
               f"dgrad {td:8.1f} us ({fl / td / 1e6:6.1f})  wgrad {tw:8.1f} us ({fl / tw / 1e6:6.1f})",
               flush=True)
