@@ -35,6 +35,36 @@ constexpr int ROWB = CH * 2;      // bytes per LDS row
 
 __device__ const u4 kZero3 = {0u, 0u, 0u, 0u};
 
+// a / b for 0 <= a < 2^22 through the f32 reciprocal rb = 1 / b (exact after one correction):
+// a handful of VALU instructions instead of the ~30 of a runtime integer division
+__device__ __forceinline__ int fdivi(int a, int b, float rb) {
+  int q = (int)((float)a * rb);
+  const int r = a - q * b;
+  q += (r >= b) - (r < 0);
+  return q;
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)reinterpret_cast<uintptr_t>(p);
+}
+__device__ __forceinline__ bf16x8 lds16(uint32_t a) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(a);
+}
+
+// sum over each 16-lane row (the MFMA C columns) with DPP adds: quad swaps, half-row and
+// row mirrors; no LDS traffic (a __shfl_xor is a ds_bpermute)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);     // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);     // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);    // row_half_mirror
+  v += dpp_f<0x140>(v);    // row_mirror
+  return v;
+}
+
 // one 16-byte LDS-DMA per lane: lane l's global 16 bytes land at lds_wave + 16 * l
 __device__ __forceinline__ void glds16(const void* g, const bf16* lds_wave) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(
@@ -48,155 +78,263 @@ __device__ __forceinline__ void glds16(const void* g, const bf16* lds_wave) {
 // moves b by 1..2*IW+2): conflict-free, where (r >> 2) & 3 was 2-way for b % 16 != 4.
 __device__ __forceinline__ int swz(int r, int q) { return r * CH + ((q ^ ((r >> 1) & 2)) << 3); }
 
-template <int NT, int GPW>
-__global__ __launch_bounds__(256, 2) void conv3_kernel(
+// Persistent, double-buffered: one block of 8 waves per CU walks a contiguous range of work
+// items (tile, 64- or 32-channel output group); each item runs one unit per 32-channel input
+// chunk, and the LDS-DMA of unit u+1 (input tile + halo, weight slice) is in flight while unit
+// u's MFMAs run.  Waves 0-3 / 4-7 own the two halves of the output group's channel tiles, wave
+// & 3 the pixel groups (wave & 3) + 4j.  Input rows are padded to IW8 (multiple of 16) pixels, so
+// a tap's row shift ky * IW8 keeps the swizzle phase and becomes an immediate offset: after a
+// per-unit base add, every fragment read is an immediate-offset ds_read_b128.
+constexpr int XPAD = 16;
+
+template <int BO, int GPW, int IW8>
+__global__ __launch_bounds__(512, 1) void conv3p_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ wk, const float* __restrict__ bias,
-    bf16* __restrict__ y, float* __restrict__ stats, int N, int H, int W, int C, int O, int Kpad,
-    int TR, int NS, int tilesPS, int nrows) {
+    bf16* __restrict__ y, float* __restrict__ stats, int N, int H, int W, int C, int O, int TR,
+    int NS, int tilesPS, int xrows, int nitems, int G, int diag) {
+  constexpr int NTW = BO / 32;                 // 16-channel tiles per wave
+  constexpr int WROWS = 9 * BO;                // weight rows per unit
   extern __shared__ __attribute__((aligned(16))) bf16 smem[];
-  constexpr int BO = NT * 16;
+  float* bs = reinterpret_cast<float*>(smem);  // [O <= 256] bias
+  bf16* buf = smem + 512;                      // 2 x {input [xrows][32], weights [9*BO][32]}
+  const int bufE = (xrows + WROWS) * CH;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const int g = lane >> 4, r16 = lane & 15;
-  const int ti = blockIdx.x;
-  const int sg = ti / tilesPS, tt = ti - sg * tilesPS;
-  const int n0 = sg * NS, y0 = tt * TR;
-  const int o0 = blockIdx.z * BO;
-  const int IW = W + 2, IR = TR + 2;
-  const int npix = NS * IR * IW;           // staged input pixels (tile + halo)
-  bf16* xs = smem;                         // [npix] rows
-  bf16* ws = smem + npix * CH;             // [9][BO] rows
-  const int TP = NS * TR * W;              // tile output pixels
+  const int wp = wave & 3, wt = wave >> 2;
+  const int IR = TR + 2, TRW = TR * W, TP = NS * TRW;
+  const int ngo = O / BO, nch = C / CH;
+  const int tiles = nitems / ngo, tilesPG = tiles / G;   // items are (og, tile), og-major
+  const int it0 = (int)((long long)blockIdx.x * nitems / gridDim.x);
+  const int it1 = (int)((long long)(blockIdx.x + 1) * nitems / gridDim.x);
+  const float rW = 1.f / W, rTRW = 1.f / TRW, rIR = 1.f / IR;
 
-  // this lane's pixels: groups wave + 4j, pixel r16 of each
-  int base[GPW];
-  bool pv[GPW];
-  int pn[GPW], py[GPW], px[GPW];
+  for (int i = tid; i < O; i += 512) bs[i] = bias ? bias[i] : 0.f;
+
+  // lane geometry (the same for every tile): B-read byte offsets for kx = 0..2, and (s, r, xx)
+  int xoff[GPW][3], pos[GPW];
 #pragma unroll
   for (int j = 0; j < GPW; ++j) {
-    const int p = (wave + 4 * j) * 16 + r16;
-    const int s = p / (TR * W), rem = p - s * (TR * W);
-    const int r = rem / W, xx = rem - r * W;
-    pv[j] = p < TP && y0 + r < H;
-    base[j] = pv[j] ? (s * IR + r) * IW + xx : 0;    // input row of tap (0, 0)
-    pn[j] = n0 + s; py[j] = y0 + r; px[j] = xx;
+    const int p = (wp + 4 * j) * 16 + r16;
+    const int sN = fdivi(p, TRW, rTRW), rem = p - sN * TRW;
+    const int r = fdivi(rem, W, rW), xx = rem - r * W;
+    const int base = (sN * IR + r) * IW8 + xx;
+    pos[j] = p < TP ? (sN << 16) | (r << 8) | xx : -1;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int row = p < TP ? base + kx : kx;
+      xoff[j][kx] = row * 64 + ((g ^ ((row >> 1) & 2)) << 4);
+    }
   }
-  f4 acc[GPW][NT];
+  const int aoff = (16 * NTW * wt + r16) * 64 + ((g ^ ((r16 >> 1) & 2)) << 4);
+
+  auto stage = [&](int item, int c, int b) {
+    bf16* xb = buf + b * bufE;
+    bf16* wb = xb + xrows * CH;
+    const int og = item / tiles, ti = item - og * tiles;
+    const int sg = ti / tilesPS, tt = ti - sg * tilesPS;
+    const int n0 = sg * NS, y0 = tt * TR, o0 = og * BO, c0 = c * CH;
+    // input: rows of IW8 * 4 slots (a multiple of 64: whole wave instructions)
+    const int nin = NS * IR * IW8 / 16;
+    for (int k = wave_u; k < nin; k += 8) {
+      const int row = (64 * k) / (IW8 * 4);
+      const int ls = 64 * k - row * (IW8 * 4) + lane;
+      const int px = ls >> 2, q = (ls & 3) ^ ((px >> 1) & 2);
+      const int sN = fdivi(row, IR, rIR), iy = y0 + row - sN * IR - 1, n = n0 + sN, ix = px - 1;
+      const bool ok = n < N && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      glds16(ok ? (const void*)(x + (((size_t)n * H + iy) * W + ix) * C + c0 + 8 * q)
+                : (const void*)&kZero3, xb + 64 * k * 8);
+    }
+    for (int k = wave_u; k < WROWS / 16; k += 8) {
+      const int sl = 64 * k + lane, row = sl >> 2, q = (sl & 3) ^ ((row >> 1) & 2);
+      const int tap = row / BO, m = row - tap * BO;
+      // A row (tile T, m) holds channel T*16+m, or with two tiles per wave the channel that puts
+      // 8 consecutive channels into each lane's two accumulators (one 16-byte store)
+      const int T = m >> 4, mm = m & 15;
+      const int o = NTW == 2 ? 32 * (T >> 1) + 8 * (mm >> 2) + 4 * (T & 1) + (mm & 3) : m;
+      glds16(wk + (size_t)(o0 + o) * (9 * C) + tap * C + c0 + 8 * q, wb + 64 * k * 8);
+    }
+  };
+
+  f4 acc[GPW][NTW];
 #pragma unroll
   for (int j = 0; j < GPW; ++j)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[j][t] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NTW; ++t) acc[j][t] = f4{0.f, 0.f, 0.f, 0.f};
 
-  for (int c0 = 0; c0 < C; c0 += CH) {
-    if (c0) __syncthreads();
-    // ---- stage the input tile + halo (zero outside the image) and the weight slice by
-    // LDS-DMA: a wave instruction fills 64 consecutive 16-byte slots (slot = row * 4 + physical
-    // chunk); the swizzle is applied on the source side (the chunk a slot holds is
-    // qs ^ ((row >> 1) & 2), the same involution swz() reads with).  All loads are in flight
-    // together; the barrier below waits for them.
-    for (int s0 = 64 * wave_u; s0 < npix * 4; s0 += 256) {
-      const int sl = s0 + lane, pix = sl >> 2, q = (sl & 3) ^ ((pix >> 1) & 2);
-      if (pix < npix) {
-        const int sr = pix / IW, ix = pix - sr * IW - 1;
-        const int s = sr / IR, iy = y0 + sr - s * IR - 1;
-        const int n = n0 + s;
-        const bool ok = n < N && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-        glds16(ok ? (const void*)(x + (((size_t)n * H + iy) * W + ix) * C + c0 + 8 * q)
-                  : (const void*)&kZero3, xs + s0 * 8);
-      }
-    }
-    for (int s0 = 64 * wave_u; s0 < 9 * BO * 4; s0 += 256) {
-      const int sl = s0 + lane, row = sl >> 2, q = (sl & 3) ^ ((row >> 1) & 2);
-      const int tap = row / BO, o = row - tap * BO;
-      glds16(wk + (size_t)(o0 + o) * Kpad + tap * C + c0 + 8 * q, ws + s0 * 8);
-    }
-    __syncthreads();
-    // ---- 9 taps x NT x GPW MFMAs from LDS
-#pragma unroll 3
-    for (int tap = 0; tap < 9; ++tap) {
-      const int toff = (tap / 3) * IW + tap % 3;
-      bf16x8 a[NT];
+  // BatchNorm partial sums: rows [blockIdx.x * 4 + wp] of R = gridDim.x * 4 per group
+  float run_s[NTW][4], run_q[NTW][4];
+  int cur_pair = -1;
+  const int srow = blockIdx.x * 4 + wp, R = gridDim.x * 4;
+  auto coff = [](int t, int i) { return (NTW == 2 ? 4 * t : 0) + i; };
+  auto flush = [&](int pr) {
+    if (r16) return;
+    const int ogp = pr / G, gp = pr - ogp * G;
+    const int cwp = ogp * BO + 16 * NTW * wt + 4 * NTW * g;
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-        a[t] = *reinterpret_cast<const bf16x8*>(ws + swz(tap * BO + 16 * t + r16, g));
-#pragma unroll
-      for (int j = 0; j < GPW; ++j) {
-        const bf16x8 b = *reinterpret_cast<const bf16x8*>(xs + swz(base[j] + toff, g));
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-          acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t], b, acc[j][t], 0, 0, 0);
-      }
-    }
-  }
-
-  // ---- epilogue: bias, bf16 rounding, NHWC store, BN partial sums of the stored values
-  float ss[NT][4], sq[NT][4];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int co = o0 + 16 * t + 4 * g;
-    float bv[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bv[i] = bias ? bias[co + i] : 0.f;
-      ss[t][i] = 0.f;
-      sq[t][i] = 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < GPW; ++j) {
-      if (!pv[j]) continue;
-      const uint32_t lo = pack_bf16x2(acc[j][t][0] + bv[0], acc[j][t][1] + bv[1]);
-      const uint32_t hi = pack_bf16x2(acc[j][t][2] + bv[2], acc[j][t][3] + bv[3]);
-      const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
-                          __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+    for (int t = 0; t < NTW; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        ss[t][i] += v[i];
-        sq[t][i] = fmaf(v[i], v[i], sq[t][i]);
+        const size_t o = (((size_t)(cwp + coff(t, i)) * G + gp) * R + srow) * 2;
+        *reinterpret_cast<float2*>(stats + o) = make_float2(run_s[t][i], run_q[t][i]);
       }
-      *reinterpret_cast<uint2*>(y + (((size_t)pn[j] * H + py[j]) * W + px[j]) * O + co) =
-          make_uint2(lo, hi);
+  };
+
+  // units u = (item, chunk) in order; the barrier after unit u's MFMAs retires unit u+1's
+  // DMA (issued before those MFMAs) and the previous epilogue's stores, so neither is waited
+  // for right after being issued; unit u+2's DMA then refills the buffer unit u just left
+  const int nunits = (it1 - it0) * nch;
+  if (nunits > 0) stage(it0, 0, 0);
+  __syncthreads();
+  if (nunits > 1) stage(it0 + (nch == 1), nch == 1 ? 0 : 1, 1);
+  for (int u = 0; u < nunits; ++u) {
+    const int item = it0 + u / nch, c = u - (u / nch) * nch;
+    // ---- 9 taps x NTW x GPW MFMAs; 32-bit LDS addresses with immediate tap offsets, the
+    // next tap's fragments read while this tap's MFMAs run
+    {
+      const uint32_t xb = lds_addr(buf + (u & 1) * bufE);
+      const uint32_t ab = xb + xrows * CH * 2 + aoff;
+      uint32_t bp[GPW][3];
+#pragma unroll
+      for (int j = 0; j < GPW; ++j)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) bp[j][kx] = xb + xoff[j][kx];
+      bf16x8 a[2][NTW], bv[2][GPW];
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) a[0][t] = lds16(ab + 16 * t * 64);
+#pragma unroll
+      for (int j = 0; j < GPW; ++j) bv[0][j] = lds16(bp[j][0]);
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int cur = tap & 1, nxt = cur ^ 1;
+        if (tap < 8) {
+          const int ky = (tap + 1) / 3, kx = (tap + 1) % 3;
+#pragma unroll
+          for (int t = 0; t < NTW; ++t) a[nxt][t] = lds16(ab + ((tap + 1) * BO + 16 * t) * 64);
+#pragma unroll
+          for (int j = 0; j < GPW; ++j) bv[nxt][j] = lds16(bp[j][kx] + ky * IW8 * 64);
+        }
+        __builtin_amdgcn_sched_barrier(0);     // keep the prefetch ahead of this tap's MFMAs
+#pragma unroll
+        for (int j = 0; j < GPW; ++j)
+#pragma unroll
+          for (int t = 0; t < NTW; ++t)
+            acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cur][t], bv[cur][j], acc[j][t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (u + 2 < nunits && !(diag & 1)) stage(it0 + (u + 2) / nch, (u + 2) % nch, u & 1);
+    if (c == nch - 1 && !(diag & 2)) {
+      // ---- epilogue: bias, bf16 rounding, NHWC store, BN sums of the stored values
+      const int og = item / tiles, ti = item - og * tiles;
+      const int sg = ti / tilesPS, tt = ti - sg * tilesPS;
+      const int n0 = sg * NS, y0 = tt * TR;
+      const int cw = og * BO + 16 * NTW * wt + 4 * NTW * g;
+      float bv[NTW][4], ss[NTW][4], sq[NTW][4];
+#pragma unroll
+      for (int t = 0; t < NTW; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          bv[t][i] = bs[cw + coff(t, i)];
+          ss[t][i] = 0.f;
+          sq[t][i] = 0.f;
+        }
+#pragma unroll
+      for (int j = 0; j < GPW; ++j) {
+        const int ps = pos[j];
+        const int sN = ps >> 16, r = (ps >> 8) & 255, xx = ps & 255;
+        if (ps < 0 || y0 + r >= H) continue;
+        bf16* yp = y + ((((size_t)(n0 + sN) * H + y0 + r) * W + xx) * O + cw);
+        uint32_t pk[NTW][2];
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) {
+          const uint32_t lo = pack_bf16x2(acc[j][t][0] + bv[t][0], acc[j][t][1] + bv[t][1]);
+          const uint32_t hi = pack_bf16x2(acc[j][t][2] + bv[t][2], acc[j][t][3] + bv[t][3]);
+          const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                              __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            ss[t][i] += v[i];
+            sq[t][i] = fmaf(v[i], v[i], sq[t][i]);
+          }
+          pk[t][0] = lo;
+          pk[t][1] = hi;
+        }
+        if (!(diag & 4)) {
+          if constexpr (NTW == 2)
+            *reinterpret_cast<u4*>(yp) = u4{pk[0][0], pk[0][1], pk[1][0], pk[1][1]};
+          else
+            *reinterpret_cast<uint2*>(yp) = make_uint2(pk[0][0], pk[0][1]);
+        }
+      }
+      if (stats && !(diag & 8)) {
+        // per-block running sums over the tiles of one (og, BatchNorm group): written once per
+        // such run (and zeros for the pairs the block never reaches) into row blockIdx*4 + wp
+        const int pair = og * G + ti / tilesPG;
+        if (pair != cur_pair) {
+          if (cur_pair >= 0) flush(cur_pair);
+          cur_pair = pair;
+#pragma unroll
+          for (int t = 0; t < NTW; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { run_s[t][i] = 0.f; run_q[t][i] = 0.f; }
+        }
+#pragma unroll
+        for (int t = 0; t < NTW; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            run_s[t][i] += row16_sum(ss[t][i]);
+            run_q[t][i] += row16_sum(sq[t][i]);
+          }
+      }
+#pragma unroll
+      for (int j = 0; j < GPW; ++j)
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) acc[j][t] = f4{0.f, 0.f, 0.f, 0.f};
     }
   }
-  if (!stats) return;
-  const int row = ti * 4 + wave;     // one partial row per (tile, wave)
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float a = ss[t][i], q = sq[t][i];
-#pragma unroll
-      for (int m = 1; m < 16; m <<= 1) {
-        a += __shfl_xor(a, m, 64);
-        q += __shfl_xor(q, m, 64);
-      }
-      if (r16 == 0) {
-        const int co = o0 + 16 * t + 4 * g + i;
-        stats[((size_t)co * nrows + row) * 2] = a;
-        stats[((size_t)co * nrows + row) * 2 + 1] = q;
-      }
+  if (stats && !(diag & 8)) {
+    if (cur_pair >= 0) flush(cur_pair);
+    // the (og, group) pairs this block never reached: zero rows.  The reached pairs are the
+    // contiguous interval [first, last] of the og-major order.
+    int first = 0, last = -1;
+    if (it0 < it1) {
+      first = (it0 / tiles) * G + (it0 % tiles) / tilesPG;
+      last = ((it1 - 1) / tiles) * G + ((it1 - 1) % tiles) / tilesPG;
     }
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { run_s[t][i] = 0.f; run_q[t][i] = 0.f; }
+    for (int pr = 0; pr < ngo * G; ++pr)
+      if (pr < first || pr > last) flush(pr);
+  }
 }
 
-struct Plan3 { int TR, NS, GPW, tilesPS; };
+struct Plan3 { int TR, NS, GPW, tilesPS, IW8, xrows; };
+
+int iw8_of(int W) { return (W + 2 + XPAD - 1) / XPAD * XPAD; }
 
 // The tile with the best utilisation of GPW*64 pixel slots (ties: more pixels); whole small
-// maps are packed NS per block with NS | B (a tile never straddles two BatchNorm groups) and
-// the staged input stays <= 40 KB (with the 36 KB weight slice: 2 blocks per CU).
+// maps are packed NS per block with NS | B (a tile never straddles two BatchNorm groups); the
+// two LDS buffers (input rows + a 64-channel weight slice) and the bias fit 160 KB.
 Plan3 plan3(int H, int W, int B) {
-  Plan3 best{0, 0, 0, 0};
+  Plan3 best{0, 0, 0, 0, 0, 0};
   double bu = -1;
+  const int IW8 = iw8_of(W);
   const char* fg = getenv("AVDINO_C3_GPW");      // A/B experiments: force the pixel groups
   for (int gpw : {4, 7}) {
     if (fg && atoi(fg) != gpw) continue;
     const int cap = gpw * 64;
     auto consider = [&](int TR, int NS) {
-      if (TR <= 0 || NS <= 0 || TR * W * NS > cap) return;
-      if ((size_t)NS * (TR + 2) * (W + 2) * ROWB > 40 * 1024) return;
+      if (TR <= 0 || NS <= 0 || TR * W * NS > cap || TR > 255) return;
+      const int xrows = NS * (TR + 2) * IW8;
+      if (2 * (xrows + 9 * 64) * ROWB + 1024 > 160 * 1024) return;
       const int tps = avd_cdiv(H, TR);
       const double u = (double)H * W * NS / ((double)tps * cap);
       if (u > bu + 1e-9 || (u > bu - 1e-9 && TR * NS > best.TR * best.NS)) {
         bu = u;
-        best = Plan3{TR, NS, gpw, tps};
+        best = Plan3{TR, NS, gpw, tps, IW8, xrows};
       }
     };
     if (H * W <= cap)
@@ -207,32 +345,52 @@ Plan3 plan3(int H, int W, int B) {
   return best;
 }
 
-template <int NT, int GPW>
+int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// diagnostics (wrong results): AVDINO_C3_DIAG bit 0 = no staging after the first two units,
+// bit 1 = no epilogue, bit 2 = no y stores, bit 3 = no statistics
+int diag3() {
+  static const int d = getenv("AVDINO_C3_DIAG") ? atoi(getenv("AVDINO_C3_DIAG")) : 0;
+  return d;
+}
+
+template <int BO, int GPW, int IW8>
 int launch3(const Plan3& p, const void* x, const void* wk, const float* bias, void* y, float* stats,
-            int N, int H, int W, int C, int O, hipStream_t st) {
-  constexpr int BO = NT * 16;
-  const size_t lds = ((size_t)p.NS * (p.TR + 2) * (W + 2) + 9 * BO) * ROWB;
-  const int total = avd_cdiv(N, p.NS) * p.tilesPS;
-  dim3 grid(total, 1, O / BO);
-  conv3_kernel<NT, GPW><<<grid, 256, lds, st>>>((const bf16*)x, (const bf16*)wk, bias, (bf16*)y,
-                                                stats, N, H, W, C, O, 9 * C, p.TR, p.NS, p.tilesPS,
-                                                total * 4);
+            int N, int B, int H, int W, int C, int O, hipStream_t st) {
+  const size_t lds = 1024 + 2 * (size_t)(p.xrows + 9 * BO) * ROWB;
+  const int tiles = (N / p.NS) * p.tilesPS;
+  const int nitems = tiles * (O / BO);
+  // with statistics every CU's block owns 4 partial rows per group (avd_c3_stat_rows)
+  const int grid = stats ? num_cus() : std::min(nitems, num_cus());
+  conv3p_kernel<BO, GPW, IW8><<<grid, 512, lds, st>>>(
+      (const bf16*)x, (const bf16*)wk, bias, (bf16*)y, stats, N, H, W, C, O, p.TR, p.NS,
+      p.tilesPS, p.xrows, nitems, N / B, diag3());
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
 
 }  // namespace
 
-// Served: bf16, 3x3, pad 1, C (input channels of the executed conv) % 32 == 0, O % 32 == 0.
+// Served: bf16, 3x3, pad 1, C (input channels of the executed conv) % 32 == 0, O % 32 == 0,
+// O <= 256, maps up to 62 pixels wide.
 bool avd_c3_serves(int dt, int C, int O, int K, int pad) {
   if (getenv("AVDINO_C3_OFF")) return false;
-  return dt == AVD_BF16 && K == 3 && pad == 1 && C % CH == 0 && C >= CH && O % 32 == 0;
+  return dt == AVD_BF16 && K == 3 && pad == 1 && C % CH == 0 && C >= CH && O % 32 == 0 && O <= 256;
 }
 
-// BN partial rows per group of avd_c3_conv (fwd): 4 per tile
+// BN partial rows per group of avd_c3_conv (fwd): 4 per CU (each block's running sums)
 int avd_c3_stat_rows(int H, int W, int B) {
   const Plan3 p = plan3(H, W, B);
-  return p.NS ? (B / p.NS) * p.tilesPS * 4 : 0;
+  return p.NS ? 4 * num_cus() : 0;
 }
 
 // y = conv3x3(x) (+ bias, + stats) over NHWC bf16 maps; x [N][H][W][C], wk the avd_cl weight
@@ -240,12 +398,13 @@ int avd_c3_stat_rows(int H, int W, int B) {
 int avd_c3_conv(const void* x, const void* wk, const float* bias, void* y, float* stats, int N,
                 int B, int H, int W, int C, int O, hipStream_t st) {
   const Plan3 p = plan3(H, W, B);
-  if (!p.NS || N % p.NS) return AVD_ERR_SHAPE;
-  const char* fn = getenv("AVDINO_C3_NT");       // A/B experiments: force the channel tiles
-  const int NT = fn ? atoi(fn) : (O % 64 == 0 ? 4 : 2);
-#define AVD_L(NTT, G) \
-  if (NT == NTT && p.GPW == G) return launch3<NTT, G>(p, x, wk, bias, y, stats, N, H, W, C, O, st);
-  AVD_L(4, 4) AVD_L(4, 7) AVD_L(2, 4) AVD_L(2, 7)
+  if (!p.NS || N % p.NS || N % B || B % p.NS || O > 256) return AVD_ERR_SHAPE;
+#define AVD_L(BO_, G, I)                                                                     \
+  if (O % BO_ == 0 && p.GPW == G && p.IW8 == I)                                              \
+    return launch3<BO_, G, I>(p, x, wk, bias, y, stats, N, B, H, W, C, O, st);
+  AVD_L(64, 7, 64) AVD_L(64, 7, 32) AVD_L(64, 7, 16) AVD_L(64, 4, 64) AVD_L(64, 4, 32)
+  AVD_L(64, 4, 16) AVD_L(32, 7, 64) AVD_L(32, 7, 32) AVD_L(32, 7, 16) AVD_L(32, 4, 64)
+  AVD_L(32, 4, 32) AVD_L(32, 4, 16)
 #undef AVD_L
   return AVD_ERR_SHAPE;
 }

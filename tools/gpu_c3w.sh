@@ -8,7 +8,7 @@ tail -3 gpurun_out/c3w_bench_tests.log
 timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
   tests/test_gpu_cl.py tests/test_gpu_simclr.py tests/test_gpu_uni.py > gpurun_out/c3w_cl_tests.log 2>&1 || { tail -30 gpurun_out/c3w_cl_tests.log; exit 1; }
 tail -3 gpurun_out/c3w_cl_tests.log
-for cfg in "" "AVDINO_C3_NT=2"; do
+for cfg in "" "AVDINO_C3_GPW=4"; do
   echo "== $cfg"
   env $cfg timeout -k 10 300 python tools/c3bench.py || exit $?
 done
