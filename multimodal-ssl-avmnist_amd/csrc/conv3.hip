@@ -261,9 +261,13 @@ __global__ __launch_bounds__(512, 1) void conv3p_kernel(
           pk[t][1] = hi;
         }
         if (!(diag & 4)) {
-          if constexpr (NTW == 2)
-            *reinterpret_cast<u4*>(yp) = u4{pk[0][0], pk[0][1], pk[1][0], pk[1][1]};
-          else
+          if constexpr (NTW == 2) {
+            const u4 v = u4{pk[0][0], pk[0][1], pk[1][0], pk[1][1]};
+            if (diag & 16)
+              __builtin_nontemporal_store(v, reinterpret_cast<u4*>(yp));
+            else
+              *reinterpret_cast<u4*>(yp) = v;
+          } else
             *reinterpret_cast<uint2*>(yp) = make_uint2(pk[0][0], pk[0][1]);
         }
       }
@@ -357,7 +361,8 @@ int num_cus() {
 }
 
 // diagnostics (wrong results): AVDINO_C3_DIAG bit 0 = no staging after the first two units,
-// bit 1 = no epilogue, bit 2 = no y stores, bit 3 = no statistics
+// bit 1 = no epilogue, bit 2 = no y stores, bit 3 = no statistics; bit 4 (correct results):
+// non-temporal y stores
 int diag3() {
   static const int d = getenv("AVDINO_C3_DIAG") ? atoi(getenv("AVDINO_C3_DIAG")) : 0;
   return d;
