@@ -108,6 +108,69 @@ __global__ __launch_bounds__(64) void bn_finalize_kernel(
   }
 }
 
+// Single pass, one block per channel, for partial lists up to FIN1_MAXROWS rows per group:
+// thread t sums rows t / G, t / G + 256 / G, ... of group t % G (every group's loads in flight
+// together), the per-thread partials of a group are then folded in fixed order by thread g.
+constexpr int FIN1_MAXROWS = 8192;
+
+__device__ __forceinline__ void group_sums(const float* __restrict__ parts, int G, int R, int c,
+                                           double* sh1, double* sh2) {
+  const int tid = threadIdx.x, per = 256 / G, gq = tid % G, j = tid / G;
+  double s1 = 0.0, s2 = 0.0;
+  if (j < per) {
+    const float2* p = reinterpret_cast<const float2*>(parts) + ((size_t)c * G + gq) * R;
+    for (int r = j; r < R; r += per) {
+      const float2 v = p[r];
+      s1 += v.x;
+      s2 += v.y;
+    }
+  }
+  sh1[tid] = s1;
+  sh2[tid] = s2;
+  __syncthreads();
+  if (tid < G) {
+    double a = 0.0, b = 0.0;
+    for (int k = 0; k < per; ++k) {
+      a += sh1[k * G + tid];
+      b += sh2[k * G + tid];
+    }
+    sh1[256 + tid] = a;
+    sh2[256 + tid] = b;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void bn_finalize1_kernel(
+    const float* __restrict__ parts, int G, int R, int C, long long count,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
+    float* mean_o, float* invstd_o, float* scale_o, float* shift_o, float* rm, float* rv,
+    const float* __restrict__ pivot) {
+  __shared__ double sh1[512], sh2[512];
+  const int c = blockIdx.x;
+  group_sums(parts, G, R, c, sh1, sh2);
+  if (threadIdx.x != 0) return;
+  double rmean = rm ? (double)rm[c] : 0.0, rvar = rv ? (double)rv[c] : 0.0;
+  const double n = (double)count;
+  for (int g = 0; g < G; ++g) {
+    const double ms = sh1[256 + g] / n;
+    const double mean = (pivot ? (double)pivot[(size_t)g * C + c] : 0.0) + ms;
+    double var = sh2[256 + g] / n - ms * ms;
+    if (var < 0) var = 0;
+    const double invstd = 1.0 / sqrt(var + (double)eps);
+    const double sc = (double)gamma[c] * invstd;
+    mean_o[g * C + c] = (float)mean;
+    invstd_o[g * C + c] = (float)invstd;
+    scale_o[g * C + c] = (float)sc;
+    shift_o[g * C + c] = (float)((double)beta[c] - mean * sc);
+    rmean = (1.0 - momentum) * rmean + momentum * mean;
+    rvar = (1.0 - momentum) * rvar + momentum * var * n / (n - 1.0);
+  }
+  if (rm) {
+    rm[c] = (float)rmean;
+    rv[c] = (float)rvar;
+  }
+}
+
 // ----------------------------------------------------------------------------- relu + pool
 template <typename TY, typename TO>
 __global__ __launch_bounds__(256) void bn_relu_pool_kernel(
@@ -226,31 +289,28 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
     const float* __restrict__ gamma, const float* __restrict__ mean,
     const float* __restrict__ invstd, float* coef, float* dgamma, float* dbeta, float* dbias,
     int accumulate) {
-  __shared__ double sh[4];
+  __shared__ double sh1[512], sh2[512];
   const int c = blockIdx.x;
+  group_sums(parts, G, R, c, sh1, sh2);
+  if (threadIdx.x != 0) return;
   double dg = 0.0, db = 0.0, dbi = 0.0;
   const double n = (double)count;
   for (int g = 0; g < G; ++g) {
-    double s1, s2;
-    reduce_pairs(parts + ((size_t)c * G + g) * R * 2, R, sh, s1, s2);
-    if (threadIdx.x == 0) {
-      const double is = invstd[g * C + c], mu = mean[g * C + c], ga = gamma[c];
-      const double k1 = ga * is;
-      const double kx = -ga * is * is * s2 / n;
-      const double k0 = -ga * is * s1 / n + ga * is * is * mu * s2 / n;
-      coef[(g * C + c) * 3 + 0] = (float)k1;
-      coef[(g * C + c) * 3 + 1] = (float)kx;
-      coef[(g * C + c) * 3 + 2] = (float)k0;
-      dg += s2;
-      db += s1;
-      dbi += k1 * s1 + kx * mu * n + k0 * n;  // = sum of dy over the group (analytically 0)
-    }
+    const double s1 = sh1[256 + g], s2 = sh2[256 + g];
+    const double is = invstd[g * C + c], mu = mean[g * C + c], ga = gamma[c];
+    const double k1 = ga * is;
+    const double kx = -ga * is * is * s2 / n;
+    const double k0 = -ga * is * s1 / n + ga * is * is * mu * s2 / n;
+    coef[(g * C + c) * 3 + 0] = (float)k1;
+    coef[(g * C + c) * 3 + 1] = (float)kx;
+    coef[(g * C + c) * 3 + 2] = (float)k0;
+    dg += s2;
+    db += s1;
+    dbi += k1 * s1 + kx * mu * n + k0 * n;  // = sum of dy over the group (analytically 0)
   }
-  if (threadIdx.x == 0) {
-    if (dgamma) dgamma[c] = (float)(accumulate ? dgamma[c] + dg : dg);
-    if (dbeta) dbeta[c] = (float)(accumulate ? dbeta[c] + db : db);
-    if (dbias) dbias[c] = (float)(accumulate ? dbias[c] + dbi : dbi);
-  }
+  if (dgamma) dgamma[c] = (float)(accumulate ? dgamma[c] + dg : dg);
+  if (dbeta) dbeta[c] = (float)(accumulate ? dbeta[c] + db : db);
+  if (dbias) dbias[c] = (float)(accumulate ? dbias[c] + dbi : dbi);
 }
 
 template <typename TY, typename TG, typename TD>
@@ -632,6 +692,12 @@ int avd_bn_finalize(float* parts, int G, int R, int C, long long count, const fl
   if (G <= 0 || R <= 0 || C <= 0 || count <= 1) return AVD_ERR_SHAPE;
   if ((running_mean == nullptr) != (running_var == nullptr)) return AVD_ERR_ARG;
   hipStream_t st = avd_stream(stream);
+  if (G <= 256 && R <= FIN1_MAXROWS) {
+    bn_finalize1_kernel<<<C, 256, 0, st>>>(parts, G, R, C, count, gamma, beta, eps, momentum, mean,
+                                           invstd, scale, shift, running_mean, running_var, pivot);
+    AVD_CHECK_LAUNCH();
+    return AVD_OK;
+  }
   // ~2048 partial rows per block, >= 2 rows per chunk (room for the in-place doubles)
   int S = 0, chunk = 1;
   if (R >= 2) {
@@ -716,7 +782,7 @@ int avd_bn_bwd_finalize(const float* parts, int G, int R, int C, long long count
                         const float* gamma, const float* mean, const float* invstd, float* coef,
                         float* dgamma, float* dbeta, float* dbias, int accumulate, void* stream) {
   if (!parts || !gamma || !mean || !invstd || !coef) return AVD_ERR_ARG;
-  if (G <= 0 || R <= 0 || C <= 0 || count <= 0) return AVD_ERR_SHAPE;
+  if (G <= 0 || G > 256 || R <= 0 || C <= 0 || count <= 0) return AVD_ERR_SHAPE;
   bn_bwd_finalize_kernel<<<C, 256, 0, avd_stream(stream)>>>(parts, G, R, C, count, gamma, mean,
                                                              invstd, coef, dgamma, dbeta, dbias,
                                                              accumulate);

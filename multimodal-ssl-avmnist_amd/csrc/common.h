@@ -144,6 +144,21 @@ __device__ __forceinline__ float dropout_scale(unsigned long long seed, unsigned
   return u >= p ? 1.f / (1.f - p) : 0.f;
 }
 
+// sum over each 16-lane row (the MFMA C columns) with DPP adds: quad swaps, half-row and
+// row mirrors; no LDS traffic (a __shfl_xor is a ds_bpermute)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);     // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);     // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);    // row_half_mirror
+  v += dpp_f<0x140>(v);    // row_mirror
+  return v;
+}
+
+
 }  // namespace avd
 
 #define AVD_CHECK_LAUNCH()                                  \

@@ -51,20 +51,6 @@ __device__ __forceinline__ bf16x8 lds16(uint32_t a) {
   return *reinterpret_cast<const __attribute__((address_space(3))) bf16x8*>(a);
 }
 
-// sum over each 16-lane row (the MFMA C columns) with DPP adds: quad swaps, half-row and
-// row mirrors; no LDS traffic (a __shfl_xor is a ds_bpermute)
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
-}
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dpp_f<0xB1>(v);     // quad_perm [1,0,3,2]
-  v += dpp_f<0x4E>(v);     // quad_perm [2,3,0,1]
-  v += dpp_f<0x141>(v);    // row_half_mirror
-  v += dpp_f<0x140>(v);    // row_mirror
-  return v;
-}
-
 // one 16-byte LDS-DMA per lane: lane l's global 16 bytes land at lds_wave + 16 * l
 __device__ __forceinline__ void glds16(const void* g, const bf16* lds_wave) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(

@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256, AP ? (L::OCC > 1 ? L::OCC - 1 : 1) : L::OCC) v
                                                       const float* __restrict__ bias,
                                                       bf16* __restrict__ y,
                                                       float* __restrict__ stats, int ntiles,
-                                                      int nrows, ApplyArgs aa) {
+                                                      int ngroups, ApplyArgs aa) {
   __shared__ __attribute__((aligned(16))) bf16 xs[L::LDS_ELEMS];
   __shared__ f4 red[L::RED];
   __shared__ __attribute__((aligned(16))) float ctab[AP ? APPLY_GMAX * 5 * L::CIN : 4];
@@ -247,6 +247,31 @@ __global__ __launch_bounds__(256, AP ? (L::OCC > 1 ? L::OCC - 1 : 1) : L::OCC) v
     }
   };
 
+  // BN partial sums (forward): per-block running sums over the block's tiles of one
+  // BatchNorm group, one row per (block, pixel wave set) and group: [COUT][G][R = grid*NPW][2]
+  float run_s[L::NTW][4], run_q[L::NTW][4];
+  int cur_g = -1;
+  const int tilesPG = ntiles / ngroups, R = (int)gridDim.x * L::NPW;
+  auto zero_run = [&]() {
+#pragma unroll
+    for (int t = 0; t < L::NTW; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { run_s[t][i] = 0.f; run_q[t][i] = 0.f; }
+  };
+  auto flush = [&](int gp) {
+    if (r16 != 0 || kw != 0) return;
+#pragma unroll
+    for (int t = 0; t < L::NTW; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = cob + 16 * t + 4 * g + i;
+        if (co < L::COUT)
+          *reinterpret_cast<float2*>(stats + (((size_t)co * ngroups + gp) * R + blockIdx.x * L::NPW + wp) * 2) =
+              make_float2(run_s[t][i], run_q[t][i]);
+      }
+  };
+  zero_run();
+
   if (t0 < t1) { if constexpr (AP) load_win_tile(t0); else load_tile(t0); }
   for (int ti = t0; ti < t1; ++ti) {
     __syncthreads();   // every wave is done reading the previous tile (and ctab is written)
@@ -362,25 +387,31 @@ __global__ __launch_bounds__(256, AP ? (L::OCC > 1 ? L::OCC - 1 : 1) : L::OCC) v
       }
     }
     if constexpr (FWD) {
-      if (stats && kw == 0) {   // partial row ti * NPW + wp of [COUT][nrows][2]
-        const int row = ti * L::NPW + wp;
+      if (stats && kw == 0) {
+        const int gi = ti / tilesPG;
+        if (gi != cur_g) {
+          if (cur_g >= 0) flush(cur_g);
+          cur_g = gi;
+          zero_run();
+        }
 #pragma unroll
         for (int t = 0; t < L::NTW; ++t)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            float s1 = ss[t][i], s2 = sq[t][i];
-#pragma unroll
-            for (int m = 1; m < 16; m <<= 1) {
-              s1 += __shfl_xor(s1, m, 64);
-              s2 += __shfl_xor(s2, m, 64);
-            }
-            const int co = cob + 16 * t + 4 * g + i;
-            if (r16 == 0 && co < L::COUT) {
-              stats[((size_t)co * nrows + row) * 2] = s1;
-              stats[((size_t)co * nrows + row) * 2 + 1] = s2;
-            }
+            run_s[t][i] += row16_sum(ss[t][i]);
+            run_q[t][i] += row16_sum(sq[t][i]);
           }
       }
+    }
+  }
+  if constexpr (FWD) {
+    if (stats) {
+      if (cur_g >= 0) flush(cur_g);
+      // groups this block never reached (its tiles cover groups [first, last]): zero rows
+      const int first = t0 < t1 ? t0 / tilesPG : 0, last = t0 < t1 ? (t1 - 1) / tilesPG : -1;
+      zero_run();
+      for (int gp = 0; gp < ngroups; ++gp)
+        if (gp < first || gp > last) flush(gp);
     }
   }
 }
@@ -445,6 +476,18 @@ int num_cus() {
   return cus;
 }
 
+// the forward's grid when it writes BatchNorm partials: one resident wave of blocks
+template <class L>
+int ws_stat_grid() {
+  static int occ = 0;
+  if (!occ) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv_ws_kernel<L, true, 0>, 256, 0) !=
+            hipSuccess || occ <= 0)
+      occ = 1;
+  }
+  return grid_cap(num_cus() * occ);
+}
+
 template <class L, bool FWD, int AP = 0>
 int launch_ws(const void* x, const void* wk, const float* bias, void* y, float* stats, int N,
               int B, hipStream_t st, const ApplyArgs& aa = ApplyArgs{}) {
@@ -457,9 +500,10 @@ int launch_ws(const void* x, const void* wk, const float* bias, void* y, float* 
       occ = 1;
   }
   const int ntiles = (N / L::NS) * L::TPS;
-  const int grid = grid_cap(std::min(ntiles, num_cus() * occ));
+  // with statistics the grid is fixed (avd_ws_stat_rows: R = grid * NPW rows per group)
+  const int grid = FWD && stats ? ws_stat_grid<L>() : grid_cap(std::min(ntiles, num_cus() * occ));
   conv_ws_kernel<L, FWD, AP><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, (bf16*)y,
-                                                   stats, ntiles, ntiles * L::NPW, aa);
+                                                   stats, ntiles, FWD && stats ? N / B : 1, aa);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
@@ -482,7 +526,7 @@ int avd_ws_stat_rows(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt) {
   if (dt != AVD_BF16 || ws_disabled()) return 0;
   auto rows = [&](auto l) -> int {
     typedef decltype(l) L;
-    return B % L::NS ? 0 : (B / L::NS) * L::TPS * L::NPW;
+    return B % L::NS ? 0 : ws_stat_grid<L>() * L::NPW;
   };
   if (out_is<FwdA2>(Cin, Ho, Wo, Cout, K)) return rows(FwdA2{});
   if (out_is<FwdA3>(Cin, Ho, Wo, Cout, K)) return rows(FwdA3{});

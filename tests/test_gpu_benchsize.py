@@ -243,9 +243,10 @@ def test_ws_kernels_many_tiles_per_block(ops, shape, cap, monkeypatch):
     bias = rnd(g, (Co,), -0.1, 0.1)
     dy = rnd(g, (N, Ho, Ho, Co), dtype=T)
     wk, wd = layout(ops, w, 0), layout(ops, w, 1)
-    R = ops.cl_stat_rows(Ho, Ho, B, K, Ci, Co, T)
 
     def run():
+        # the forward's partial rows are per resident block: the count follows the grid cap
+        R = ops.cl_stat_rows(Ho, Ho, B, K, Ci, Co, T)
         y = torch.full((N, Ho, Ho, Co), float("nan"), device="cuda", dtype=T)
         st = torch.full((Co * G * R * 2,), float("nan"), device="cuda")
         ops.cl_conv_fwd(x, wk, bias, y, st, N, B, Ci, H, H, Co, K, pad)
