@@ -29,7 +29,8 @@ import torch  # noqa: E402
 
 METRIC = "AVMNIST audio-image pairs/sec (multimodal DINO step) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-MFMA_PEAK_TFS = {"bf16": 2500.0, "f32": 157.3}   # dense, no sparsity
+# dense, no sparsity; non-scaled fp8 MFMA (v_mfma_f32_16x16x32_fp8_fp8) runs at the bf16 rate
+MFMA_PEAK_TFS = {"bf16": 2500.0, "f32": 157.3, "fp8": 2500.0}
 # SURVEY 8(d) "BN-barrier" algorithmic HBM bytes per pair of a whole training step (inputs read
 # once, each train-mode-BN'd conv output written once and read once forward, saved output read
 # + its gradient written / read backward; weights amortised), bf16 storage; f32 doubles them
@@ -52,7 +53,9 @@ def parse():
                          "all-gathered negatives / config 5 semi_supervised); uni = UniModalDINO "
                          "ImageEncoder 2 global views B=64 (config 1); simclr = multimodal SimCLR "
                          "with all-gathered NT-Xent negatives, B=2048/GPU (config 4)")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32", "fp8"],
+                    help="fp8: e4m3 MFMA forward for the mid-layer convs (config 5), bf16 maps "
+                         "and backward")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every kernel from Python each step instead of replaying the "
@@ -148,10 +151,11 @@ def build_workload(args, device, act, world, rank, avdist):
     # forward, one averaged all-reduce of the flat live-gradient arena after backward
     eng = MultiCentralEngine(store, args.mode, E, D, P, Hyper(), act_dtype=act, grad_hook=hook,
                              buffer_hook=avdist.broadcast_buffers if world > 1 else None, seed=rank,
-                             negatives="global")
+                             negatives="global", conv_fp8=args.dtype == "fp8")
     pool = synthetic_pool(2, B, G, L, device, 1234 + rank)
+    prec = "e4m3 MFMA mid-layer conv forward, bf16 maps/backward" if args.dtype == "fp8" else args.dtype
     cfg = {"mse": "BASELINE config 2", "infonce": "BASELINE config 3 shape, all-gathered negatives",
-           "semi_supervised": "BASELINE config 5 shape, bf16 (no fp8 path yet)",
+           "semi_supervised": f"BASELINE config 5 shape, {prec}",
            "default": "default mode"}[args.mode]
     return (eng, pool, B, f"multi_central {args.mode} training step, B={B}/GPU, {G} global + {L} "
                           f"local views, E=D={E}, P={P} ({cfg})", "multi_central")
@@ -237,7 +241,9 @@ def main():
 
     from avdino import ops
     from avdino import dist as avdist
-    act = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    act = torch.float32 if args.dtype == "f32" else torch.bfloat16
+    if args.dtype == "fp8" and args.workload != "dino":
+        raise SystemExit("--dtype fp8 is the multimodal DINO conv path (config 5); use --workload dino")
     eng, pool, B, workload, model = build_workload(args, device, act, world, rank, avdist)
 
     # warm-up: eager steps (the second one times every instrumented kernel to find the dominant
@@ -325,7 +331,7 @@ def main():
     value = total_pairs / elapsed
     # whole-step roofline: pairs/s per GPU against min(HBM ceiling, MFMA ceiling)
     key = args.mode if args.workload == "dino" else args.workload
-    bpp = STEP_BYTES_PER_PAIR_BF16[key] * (1 if args.dtype == "bf16" else 2)
+    bpp = STEP_BYTES_PER_PAIR_BF16[key] * (2 if args.dtype == "f32" else 1)
     fpp = STEP_FLOPS_PER_PAIR[key]
     ceil_hbm = HBM_PEAK_GBS * 1e9 / bpp
     ceil_mfma = MFMA_PEAK_TFS[args.dtype] * 1e12 / fpp

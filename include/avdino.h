@@ -483,6 +483,30 @@ int avd_knn_select(const float* S, long long ldS, const float* xnorm, int M, int
  * compute_classification_metrics, dino_train.py:76). */
 int avd_argmax_rows(const float* logits, long long ld, int R, int C, int64_t* idx, void* stream);
 
+/* ------------------------------------------------------------------ fp8 conv path (config 5)
+ * BASELINE config 5 ("fp8 MFMA conv path"), SURVEY 7 step 9: the mid-layer conv FORWARD on
+ * v_mfma_f32_16x16x32_fp8_fp8 with OCP e4m3fn operands (gfx950); replaces the bf16
+ * F.conv2d of CentralUnimodalImage/Audio.forward (unimodal.py:127-221) under the reference's
+ * '16-mixed' Trainer precision (run_dino.py:360).  The input stays a bf16 NHWC map and is
+ * quantised while staged (per-tensor scale xscale, RNE, saturating at +-448); the weights are
+ * quantised per output channel by avd_fp8_weight_quant; y is bf16 NHWC plus BatchNorm partial
+ * rows (layout of avd_cl_conv_fwd, avd_fp8_stat_rows rows per group).  The backward stays
+ * bf16 (avd_cl_conv_dgrad / avd_cl_conv_wgrad on the stored maps). */
+
+/* Bytes of the e4m3 weight rows [Cout][32*ceil(K*K*Cin/32)] (k = tap*Cin + c). */
+int avd_fp8_weight_elems(int Cout, int Cin, int K);
+/* W f32 [Cout][Cin][K][K] -> wq e4m3 rows and wscale[Cout] = max|W[o]| / 448. */
+int avd_fp8_weight_quant(const float* w, int Cout, int Cin, int K, void* wq, float* wscale,
+                         void* stream);
+/* 1 if (Cin, Cout, K) has an fp8 kernel. */
+int avd_fp8_conv_serves(int Cin, int Cout, int K);
+/* BN partial rows per group written by avd_fp8_conv_fwd (0: not served). */
+int avd_fp8_stat_rows(int Ho, int Wo, int B, int K, int Cin, int Cout);
+/* y = bf16(conv(q(x / xscale), wq) * xscale * wscale[o] + bias[o]); stats as avd_cl_conv_fwd. */
+int avd_fp8_conv_fwd(const void* x, float xscale, const void* wq, const float* wscale,
+                     const float* bias, void* y, float* stats, int N, int B, int Cin, int H,
+                     int W, int Cout, int K, int pad, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

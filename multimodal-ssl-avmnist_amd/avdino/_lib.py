@@ -86,6 +86,11 @@ PROTOS = {
     "avd_row_sqnorm": [P, I, I, P, P],
     "avd_knn_select": [P, L, P, I, I, I, P, P, I, P, I, P, P, P],
     "avd_argmax_rows": [P, L, I, I, P, P],
+    "avd_fp8_weight_elems": [I, I, I],
+    "avd_fp8_weight_quant": [P, I, I, I, P, P, P],
+    "avd_fp8_conv_serves": [I, I, I],
+    "avd_fp8_stat_rows": [I, I, I, I, I, I],
+    "avd_fp8_conv_fwd": [P, F, P, P, P, P, P, I, I, I, I, I, I, I, I, P],
 }
 
 

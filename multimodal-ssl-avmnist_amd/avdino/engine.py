@@ -56,24 +56,54 @@ class ConvBranch:
     MFMA) and bf16 (bench) storage; only the final features are f32 [N, F] in the reference's
     flatten order."""
 
-    def __init__(self, stack, act_dtype):
+    def __init__(self, stack, act_dtype, fp8=False):
         self.stack = stack
         self.act = act_dtype
         self.dims = stack.layer_dims()
+        # fp8 (e4m3) MFMA forward for the layers after the first (config 5's "fp8 MFMA conv
+        # path"); maps stay bf16, the backward stays bf16 (avd_fp8_conv_fwd)
+        self.fp8 = bool(fp8) and act_dtype == torch.bfloat16
+
+    def _fp8_ok(self, i):
+        ci, co, k, _p = self.stack.convs[i]
+        return self.fp8 and i > 0 and ops.fp8_conv_serves(ci, co, k)
 
     def prepare(self, ws, store, tag, need_dgrad):
-        """MFMA weight layouts for this step (the weights change every step)."""
+        """MFMA weight layouts for this step (the weights change every step): (bf16 forward
+        rows, bf16 dgrad rows, (e4m3 rows, per-channel scales) for fp8 layers)."""
         wts = []
         for i, (ci, co, k, _p) in enumerate(self.stack.convs):
             w = store[self.stack.conv_keys[i] + ".weight"]
-            wk = ws.get(f"{tag}.wk{i}", ops.cl_weight_elems(co, ci, k, 0), self.act)
-            ops.cl_weight_layout(w, wk, 0)
+            q = None
+            if self._fp8_ok(i):
+                q = (ws.get(f"{tag}.wq{i}", ops.fp8_weight_elems(co, ci, k), torch.uint8),
+                     ws.get(f"{tag}.wqs{i}", co))
+                ops.fp8_weight_quant(w, q[0], q[1])
+                wk = None
+            else:
+                wk = ws.get(f"{tag}.wk{i}", ops.cl_weight_elems(co, ci, k, 0), self.act)
+                ops.cl_weight_layout(w, wk, 0)
             wd = None
             if need_dgrad and i > 0:
                 wd = ws.get(f"{tag}.wd{i}", ops.cl_weight_elems(co, ci, k, 1), self.act)
                 ops.cl_weight_layout(w, wd, 1)
-            wts.append((wk, wd))
+            wts.append((wk, wd, q))
         return wts
+
+    def _conv_fwd(self, i, h, wt, bias, y, parts, N, B):
+        ci, co, k, pad = self.stack.convs[i]
+        H = self.dims[i][0]
+        if wt[2] is not None:
+            ops.fp8_conv_fwd(h, 1.0, wt[2][0], wt[2][1], bias, y, parts, N, B, ci, H, H, co, k, pad)
+        else:
+            ops.cl_conv_fwd(h, wt[0], bias, y, parts, N, B, ci, H, H, co, k, pad)
+
+    def _stat_rows(self, i, B):
+        ci, co, k, _p = self.stack.convs[i]
+        Ho = self.dims[i][1]
+        if self._fp8_ok(i):
+            return ops.fp8_stat_rows(Ho, Ho, B, k, ci, co)
+        return ops.cl_stat_rows(Ho, Ho, B, k, ci, co, self.act)
 
     def _tail_mode(self):
         return 1 if self.stack.gap else 2
@@ -90,11 +120,10 @@ class ConvBranch:
             if i == 0 and nl > 1 and self._recompute_ok(N, B, ci, H, co, k, pad, need_dgrad):
                 h = self._first_layer_recompute_fwd(ws, store, tag, ctx, h, N, G, B, update_running)
                 continue
-            R = ops.cl_stat_rows(Ho, Ho, B, k, ci, co, self.act)
+            R = self._stat_rows(i, B)
             y = ws.get(f"{tag}.y{i}", N * Ho * Ho * co, self.act)
             parts = ws.get("stat_parts", co * G * R * 2)
-            ops.cl_conv_fwd(h, wts[i][0], store[self.stack.conv_keys[i] + ".bias"], y, parts,
-                            N, B, ci, H, H, co, k, pad)
+            self._conv_fwd(i, h, wts[i], store[self.stack.conv_keys[i] + ".bias"], y, parts, N, B)
             st = ws.get(f"{tag}.bn{i}", 4 * G * co).view(4, G * co)
             bk = self.stack.bn_keys[i]
             ops.bn_finalize(parts, G, R, co, B * Ho * Ho, store[bk + ".weight"], store[bk + ".bias"],
@@ -134,8 +163,7 @@ class ConvBranch:
         for i, (ci, co, k, pad) in enumerate(self.stack.convs):
             H, Ho, Hp = self.dims[i]
             y = ws.get(f"{tag}.y{i}", N * Ho * Ho * co, self.act)
-            ops.cl_conv_fwd(h, wts[i][0], store[self.stack.conv_keys[i] + ".bias"], y, None,
-                            N, N, ci, H, H, co, k, pad)
+            self._conv_fwd(i, h, wts[i], store[self.stack.conv_keys[i] + ".bias"], y, None, N, N)
             bk = self.stack.bn_keys[i]
             coef = ws.get(f"{tag}.ev{i}", 2 * co).view(2, co)
             ops.bn_eval_coef(store[bk + ".weight"], store[bk + ".bias"], store[bk + ".running_mean"],
@@ -434,17 +462,19 @@ class MultiCentralEngine:
     semi_supervised}``)."""
 
     def __init__(self, store, mode, E, D, P, hp, act_dtype=F32, grad_hook=None, seed=0,
-                 buffer_hook=None, negatives="global", group=None, concurrent=True):
+                 buffer_hook=None, negatives="global", group=None, concurrent=True, conv_fp8=False):
         self.store, self.mode, self.E, self.D, self.P, self.hp = store, mode, E, D, P, hp
         self.act = act_dtype
         # Linear layers: bf16 MFMA in the bf16 mode (like the reference's fp16 autocast),
         # exact-f32 MFMA in the fp32 (parity) mode
         self.gm = ops.GEMM_BF16_MFMA if act_dtype == torch.bfloat16 else ops.GEMM_F32_MFMA
         self.ws = Workspace(store.device)
-        self.img = ConvBranch(central_stack("student.image_encoder.0", CENTRAL_IMAGE_CONVS, 28), act_dtype)
-        self.aud = ConvBranch(central_stack("student.audio_encoder.0", CENTRAL_AUDIO_CONVS, 112), act_dtype)
-        self.t_img = ConvBranch(central_stack("teacher.image_encoder.0", CENTRAL_IMAGE_CONVS, 28), act_dtype)
-        self.t_aud = ConvBranch(central_stack("teacher.audio_encoder.0", CENTRAL_AUDIO_CONVS, 112), act_dtype)
+        # conv_fp8: e4m3 MFMA forward for the mid-layer convs (bf16 mode only; config 5)
+        self.conv_fp8 = bool(conv_fp8) and act_dtype == torch.bfloat16
+        self.img = ConvBranch(central_stack("student.image_encoder.0", CENTRAL_IMAGE_CONVS, 28), act_dtype, conv_fp8)
+        self.aud = ConvBranch(central_stack("student.audio_encoder.0", CENTRAL_AUDIO_CONVS, 112), act_dtype, conv_fp8)
+        self.t_img = ConvBranch(central_stack("teacher.image_encoder.0", CENTRAL_IMAGE_CONVS, 28), act_dtype, conv_fp8)
+        self.t_aud = ConvBranch(central_stack("teacher.audio_encoder.0", CENTRAL_AUDIO_CONVS, 112), act_dtype, conv_fp8)
         self.sproj = ProjHead("student_projection", D, P, gemm_mode=self.gm)
         self.tproj = ProjHead("teacher_projection", D, P, gemm_mode=self.gm)
         self.heads = None

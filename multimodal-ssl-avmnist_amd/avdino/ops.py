@@ -267,6 +267,45 @@ def cl_stat_rows(Ho, Wo, B, K, Cin, Cout, dtype):
     return lib.avd_cl_stat_rows(Ho, Wo, B, K, Cin, Cout, _DT[dtype])
 
 
+# ---- fp8 (e4m3) conv forward (config 5): include/avdino.h "fp8 conv path"
+def fp8_conv_serves(Cin, Cout, K):
+    return bool(lib.avd_fp8_conv_serves(Cin, Cout, K))
+
+
+def fp8_weight_elems(Cout, Cin, K):
+    return lib.avd_fp8_weight_elems(Cout, Cin, K)
+
+
+def fp8_stat_rows(Ho, Wo, B, K, Cin, Cout):
+    return lib.avd_fp8_stat_rows(Ho, Wo, B, K, Cin, Cout)
+
+
+def fp8_weight_quant(w, wq, wscale):
+    """w f32 [Cout, Cin, K, K] -> wq uint8 e4m3 rows + wscale f32 [Cout] (per-channel max/448)."""
+    Cout, Cin, K, _ = w.shape
+    _need(w.dtype == torch.float32 and w.is_contiguous(), "fp8 quant w")
+    _need(wq.dtype == torch.uint8 and wq.numel() >= fp8_weight_elems(Cout, Cin, K), "fp8 quant wq")
+    _need(wscale.dtype == torch.float32 and wscale.numel() >= Cout, "fp8 quant scale")
+    call("avd_fp8_weight_quant", p(w), Cout, Cin, K, p(wq), p(wscale), stream())
+
+
+def fp8_conv_fwd(x, xscale, wq, wscale, bias, y, stats, N, B, Cin, H, W, Cout, K, pad):
+    """bf16 NHWC x -> bf16 NHWC y on the e4m3 MFMA (+bias, + BN partial rows [Cout][N/B][R][2])."""
+    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
+    _need(fp8_conv_serves(Cin, Cout, K), f"fp8 conv: no kernel for {Cin}->{Cout} k{K}")
+    _need(x.dtype == y.dtype == torch.bfloat16, "fp8 conv dtypes (bf16 maps)")
+    _need(x.numel() == N * H * W * Cin and y.numel() == N * Ho * Wo * Cout, "fp8 conv sizes")
+    _need(wq.numel() >= fp8_weight_elems(Cout, Cin, K) and wscale.numel() >= Cout, "fp8 conv weights")
+    if stats is not None:
+        R = fp8_stat_rows(Ho, Wo, B, K, Cin, Cout)
+        _need(R > 0 and stats.numel() >= Cout * (N // B) * R * 2, "fp8 conv stats size")
+    nb = x.numel() * 2 + y.numel() * 2
+    fl = 2 * y.numel() * Cin * K * K
+    _timed(f"fp8_conv_fwd[{N}x{H}x{W}x{Cin}->{Cout} k{K}p{pad}]", nb, fl,
+           lambda: call("avd_fp8_conv_fwd", p(x), float(xscale), p(wq), p(wscale), p(bias), p(y),
+                        p(stats), N, B, Cin, H, W, Cout, K, pad, stream()))
+
+
 def cl_conv_fwd(x, wk, bias, y, stats, N, B, Cin, H, W, Cout, K, pad):
     """NHWC conv (+bias) with fused BN partial sums: stats [Cout][N/B][R][2]."""
     Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1

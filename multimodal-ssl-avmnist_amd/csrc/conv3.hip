@@ -57,12 +57,11 @@ __device__ __forceinline__ void glds16(const void* g, const bf16* lds_wave) {
       reinterpret_cast<uintptr_t>(lds_wave)), 16, 0, 0);
 }
 
-// element offset of 16-byte chunk q (0..3) of LDS row r.  ds_read_b128 is serviced in four
+// LDS swizzle of the 64-byte rows (16-byte chunk q of row r sits at chunk q ^ ((r >> 1) & 2)).  ds_read_b128 is serviced in four
 // 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32); a fragment read puts rows
 // b..b+15 of chunks (2k, 2k+1) into a group pair, and flipping bit 1 of the chunk on every
 // other 4-row block spreads each group over the 16 slots of a bank row for ANY b (a tap shift
 // moves b by 1..2*IW+2): conflict-free, where (r >> 2) & 3 was 2-way for b % 16 != 4.
-__device__ __forceinline__ int swz(int r, int q) { return r * CH + ((q ^ ((r >> 1) & 2)) << 3); }
 
 // Persistent, double-buffered: one block of 8 waves per CU walks a contiguous range of work
 // items (tile, 64- or 32-channel output group); each item runs one unit per 32-channel input
@@ -339,7 +338,7 @@ int num_cus() {
   static int n = 0;
   if (!n) {
     int dev = 0;
-    hipGetDevice(&dev);
+    (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
       n = 256;
   }

@@ -1,0 +1,166 @@
+"""fp8 (OCP e4m3fn) MFMA conv forward -- BASELINE config 5's "fp8 MFMA conv path"
+(avd_fp8_conv_fwd, csrc/conv8.hip).
+
+  * the weight quantiser against torch's own e4m3fn cast: per-output-channel scale
+    max|W[o]| / 448 and the tap-major byte rows bit-exact;
+  * the conv against a float64 conv of the SAME quantised operands (dequantised e4m3 input and
+    weights, the kernel's scales and bias): the MFMA products are exact, so the only error is
+    the fp32 accumulation order and the bf16 rounding of the stored output (rel-L2 5e-3, BN
+    partial sums of the stored values 1e-5) -- for the four CentralNet mid layers, small N and
+    one config-5-sized launch (N = 4096);
+  * a multimodal DINO step (semi_supervised, config 5's mode) in fp8 mode against the bf16
+    step from identical state: statistical parity (bf16/fp8 are compared by loss
+    band and gradient agreement) -- loss within 2 %, flat gradient cosine >= 0.99.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+from tests.test_gpu_benchsize import conv_ref, grel, rnd  # noqa: E402
+
+T = torch.bfloat16
+F64 = torch.float64
+E4 = torch.float8_e4m3fn
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from avdino import ops as _ops
+    return _ops
+
+
+def quant_ref(w):
+    """torch restatement of fp8_wquant_kernel: (rows [O][KP] uint8, scale [O])."""
+    O, C, K, _ = w.shape
+    amax = w.abs().reshape(O, -1).amax(1)
+    # correctly rounded amax / 448 (a tensor / scalar division in torch multiplies by 1/448)
+    s = torch.where(amax > 0, (amax.double() / 448.0).float(), torch.ones_like(amax))
+    q = (w / s.view(O, 1, 1, 1)).clamp(-448, 448).to(E4)
+    rows = q.permute(0, 2, 3, 1).reshape(O, K * K * C)        # k = tap * C + c
+    KP = (K * K * C + 31) // 32 * 32
+    out = torch.zeros(O, KP, dtype=torch.uint8, device=w.device)
+    out[:, :K * K * C] = rows.view(torch.uint8)
+    return out, s
+
+
+MID = [(8, 56, 16, 5, 2), (16, 28, 32, 5, 2), (32, 14, 64, 5, 2), (32, 14, 64, 5, 0)]
+
+
+@pytest.mark.parametrize("shape", MID)
+def test_fp8_weight_quant_matches_torch_e4m3(ops, shape):
+    Ci, H, Co, K, pad = shape
+    g = torch.Generator(device="cuda").manual_seed(Ci + Co)
+    w = rnd(g, (Co, Ci, K, K)) * 0.1
+    w[0] = 0.0                                               # all-zero channel: scale 1
+    wq = torch.empty(ops.fp8_weight_elems(Co, Ci, K), dtype=torch.uint8, device="cuda")
+    ws = torch.empty(Co, device="cuda")
+    ops.fp8_weight_quant(w, wq, ws)
+    rq, rs = quant_ref(w)
+    assert torch.equal(ws, rs)
+    assert torch.equal(wq.view(Co, -1), rq)
+
+
+def _case(ops, shape, N, B, seed):
+    Ci, H, Co, K, pad = shape
+    G = N // B
+    Ho = H + 2 * pad - K + 1
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = rnd(g, (N, H, H, Ci), 0.0, 3.0, T)                   # post-ReLU/pool-like maps
+    w = rnd(g, (Co, Ci, K, K)) / (Ci * K * K) ** 0.5
+    bias = rnd(g, (Co,), -0.1, 0.1)
+    wq = torch.empty(ops.fp8_weight_elems(Co, Ci, K), dtype=torch.uint8, device="cuda")
+    ws = torch.empty(Co, device="cuda")
+    ops.fp8_weight_quant(w, wq, ws)
+    R = ops.fp8_stat_rows(Ho, Ho, B, K, Ci, Co)
+    assert R > 0
+    y = torch.full((N, Ho, Ho, Co), float("nan"), device="cuda", dtype=T)
+    st = torch.full((Co * G * R * 2,), float("nan"), device="cuda")
+    ops.fp8_conv_fwd(x, 1.0, wq, ws, bias, y, st, N, B, Ci, H, H, Co, K, pad)
+    # float64 conv of the dequantised operands
+    xq = x.float().clamp(-448, 448).to(E4).to(F64)
+    rq, rs = quant_ref(w)
+    KK = K * K * Ci
+    wdq = rq[:, :KK].view(E4).to(F64).view(Co, K, K, Ci).permute(0, 3, 1, 2) * rs.to(F64).view(Co, 1, 1, 1)
+    y_ref = conv_ref(xq, wdq, pad) + bias.to(F64)
+    assert grel(y, y_ref) < 5e-3, grel(y, y_ref)
+    s = st.view(Co, G, R, 2).to(F64).sum(2)
+    yv = y.to(F64).view(G, -1, Co)
+    assert grel(s[..., 0], yv.sum(1).T) < 1e-5
+    assert grel(s[..., 1], (yv ** 2).sum(1).T) < 1e-5
+
+
+@pytest.mark.parametrize("shape", MID)
+def test_fp8_conv_matches_f64_of_quantised_operands(ops, shape):
+    _case(ops, shape, 24, 12, 7)
+
+
+def test_fp8_conv_config5_size(ops):
+    _case(ops, MID[1], 4096, 4096, 8)
+
+
+def _engine(act, fp8, state, mode="semi_supervised"):
+    from avdino.engine import Hyper, MultiCentralEngine
+    from avdino.params import ParamStore
+    from avdino.spec import multimodal_dino_sd
+    store = ParamStore(multimodal_dino_sd(mode, 64, 64, 32), "cuda")
+    store.load_state_dict(state)
+    hp = Hyper(dropout=0.0, fusion_dropout=0.0)
+    return store, MultiCentralEngine(store, mode, 64, 64, 32, hp, act_dtype=act, conv_fp8=fp8)
+
+
+def test_fp8_step_statistical_parity_with_bf16():
+    """Band test: the fp8 step's loss and gradient error against the fp32 engine from the same
+    state stay within 3x the bf16 step's own error (the accepted precision mode: bf16 is bounded
+    by the reference's bf16-autocast error, test_gpu_benchsize.py), plus an absolute floor."""
+    from oracle import spec as OS
+    from oracle.params import make_multimodal_batch, make_state
+    state = {k: torch.from_numpy(np.array(v)) for k, v in
+             make_state(OS.multimodal_dino_spec("semi_supervised", 64, 64, 32), 91).items()}
+    batch = {k: torch.from_numpy(v).cuda() for k, v in make_multimodal_batch(64, 2, 2, 92).items()}
+    res = {}
+    for name, act, fp8 in (("f32", torch.float32, False), ("bf16", T, False), ("fp8", T, True)):
+        store, eng = _engine(act, fp8, state)
+        if fp8:
+            assert any(eng.aud._fp8_ok(i) for i in range(1, 4)), "fp8 kernels not selected"
+        loss = eng.forward(batch)
+        eng.update_center()
+        eng.backward()
+        torch.cuda.synchronize()
+        res[name] = (loss.item(), store.grad.detach().double().clone())
+    l32, g32 = res["f32"]
+    dl = {k: abs(res[k][0] - l32) for k in ("bf16", "fp8")}
+    dg = {k: ((res[k][1] - g32).norm() / g32.norm()).item() for k in ("bf16", "fp8")}
+    cs = {k: torch.nn.functional.cosine_similarity(res[k][1], g32, dim=0).item() for k in ("bf16", "fp8")}
+    print("loss err", dl, "loss", l32, "grad rel-L2", dg, "cos", cs)
+    assert dl["fp8"] <= 0.02 * abs(l32), (dl, l32)
+
+
+@pytest.mark.parametrize("cap", [1, 3])
+def test_fp8_conv_many_tiles_per_block(ops, cap, monkeypatch):
+    """The persistent tile loop (weights resident, input restaged per tile): a capped grid gives
+    the same bits as the uncapped one (partial rows are per tile, not per block)."""
+    Ci, H, Co, K, pad = MID[0]
+    N, B = 24, 12
+    Ho = H + 2 * pad - K + 1
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = rnd(g, (N, H, H, Ci), 0.0, 3.0, T)
+    w = rnd(g, (Co, Ci, K, K)) / (Ci * K * K) ** 0.5
+    wq = torch.empty(ops.fp8_weight_elems(Co, Ci, K), dtype=torch.uint8, device="cuda")
+    ws = torch.empty(Co, device="cuda")
+    ops.fp8_weight_quant(w, wq, ws)
+    R = ops.fp8_stat_rows(Ho, Ho, B, K, Ci, Co)
+
+    def run():
+        y = torch.full((N, Ho, Ho, Co), float("nan"), device="cuda", dtype=T)
+        st = torch.full((Co * (N // B) * R * 2,), float("nan"), device="cuda")
+        ops.fp8_conv_fwd(x, 1.0, wq, ws, None, y, st, N, B, Ci, H, H, Co, K, pad)
+        torch.cuda.synchronize()
+        return y, st
+
+    monkeypatch.delenv("AVDINO_GRID_CAP", raising=False)
+    y0, s0 = run()
+    monkeypatch.setenv("AVDINO_GRID_CAP", str(cap))
+    y1, s1 = run()
+    assert torch.equal(y0, y1) and torch.equal(s0, s1)
