@@ -415,6 +415,29 @@ int avd_augment_views(const uint8_t* src_u8, const int64_t* idx, long long n_src
                       int H, int W, const float* lut, const float* rec, const uint32_t* gm,
                       int gm_words, int group, unsigned long long seed, int order, float* out,
                       void* stream);
+/* The same with out in odt (AVD_F32 or AVD_BF16): with order 1 and bf16 the views land
+ * straight in the engine's staged view-major input (no f32 round trip through
+ * avd_stage_views). */
+int avd_augment_views_dt(const uint8_t* src_u8, const int64_t* idx, long long n_src, int B,
+                         int V, int H, int W, const float* lut, const float* rec,
+                         const uint32_t* gm, int gm_words, int group, unsigned long long seed,
+                         int order, void* out, int odt, void* stream);
+
+/* The records' random parameters drawn on the device (the get_params rules of each transform:
+ * RandomResizedCrop / RandomErasing 10 attempts + fallback, RandomRotation / RandomAffine
+ * inverse matrices, torchaudio mask_along_axis bands, time-stretch rate, noise std,
+ * GroupedMasking's randperm(ng)[:k] as the k smallest of ng counter-hash keys).  stages is a
+ * HOST array [nstages <= 8][8] of {kind, p, params...}:
+ *   kind 0 crop {scale0, scale1, ratio0, ratio1}, 1 time stretch {min, max},
+ *   2 frequency mask {param}, 3 time mask {param}, 4 rotation {degrees},
+ *   5 affine {degrees, translate_x (< 0: none), translate_y, scale0 (<= 0: none), scale1},
+ *   6 erasing {scale0, scale1, ratio0, ratio1}, 7 gaussian noise {std},
+ *   8 grouped masking {mask_ratio} (group size = group);
+ * each stage draws U < p (applied) first, as RandomApply.  rec [n, AVD_AUG_REC] (record r's
+ * grouped-mask row is r), gm [n, gm_words] (NULL without grouped masking; ng <= 1024). */
+int avd_augment_records(const float* stages, int nstages, int n, int H, int W, int group,
+                        unsigned long long seed, float* rec, uint32_t* gm, int gm_words,
+                        void* stream);
 
 /* ------------------------------------------------------------------ optimiser / EMA */
 

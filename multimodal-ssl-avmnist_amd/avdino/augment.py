@@ -217,6 +217,47 @@ def sample_records(rng, chain, n, H, W, group=4):
     return rec, gm
 
 
+# ----------------------------------------------------------------------------- device draws
+_SK = {"crop": 0, "time_warp": 1, "frequency_mask": 2, "time_mask": 3, "rotation": 4,
+       "affine": 5, "erasing": 6, "gaussian_noise": 7, "grouped_masking": 8}
+
+
+def chain_stages(chain, group=4):
+    """A chain as avd_augment_records' host stage table [S, 8] f32: {kind, p, params...}
+    (include/avdino.h)."""
+    validate_chain(chain)
+    st = np.zeros((len(chain), ops.AUG_STAGE_F), np.float32)
+    for i, (kind, kw, pr) in enumerate(chain):
+        q = st[i, 2:]
+        st[i, 0], st[i, 1] = _SK[kind], pr
+        if kind == "crop":
+            q[0:2] = kw.get("scale", (0.08, 1.0))
+            q[2:4] = kw.get("ratio", (3.0 / 4.0, 4.0 / 3.0))
+        elif kind == "erasing":
+            q[0:2] = kw.get("scale", (0.02, 0.33))
+            q[2:4] = kw.get("ratio", (0.3, 3.3))
+        elif kind == "time_warp":
+            q[0], q[1] = kw.get("min_factor", 0.8), kw.get("max_factor", 1.2)
+        elif kind == "frequency_mask":
+            q[0] = kw["freq_mask_param"]
+        elif kind == "time_mask":
+            q[0] = kw["time_mask_param"]
+        elif kind == "rotation":
+            q[0] = kw["degrees"]
+        elif kind == "affine":
+            q[0] = kw.get("degrees", 0)
+            tr, sc = kw.get("translate"), kw.get("scale")
+            q[1], q[2] = tr if tr else (-1.0, -1.0)
+            q[3], q[4] = sc if sc else (0.0, 0.0)
+        elif kind == "gaussian_noise":
+            q[0] = kw.get("std", 0.1)
+        elif kind == "grouped_masking":
+            if kw.get("group_size", 4) != group:
+                raise ValueError("grouped masking group size must match the kernel's group")
+            q[0] = kw.get("mask_ratio", 0.5)
+    return st
+
+
 # ----------------------------------------------------------------------------- the device op
 
 class ViewAugmenter:
@@ -225,11 +266,34 @@ class ViewAugmenter:
     ``src_u8`` [N, H*W] uint8 on the device, ``lut`` [256] f32 (the dataset's normalisation).
     ``__call__(idx, chain, n_views)`` -> f32 [B, n_views, 1, H, W] on the device."""
 
-    def __init__(self, src_u8, lut, H, W, seed=0):
+    def __init__(self, src_u8, lut, H, W, seed=0, device_params=True):
         self.src, self.lut, self.H, self.W = src_u8, lut, H, W
         self.rng = np.random.default_rng(seed)
         self.seed = seed
         self.calls = 0
+        # parameters drawn by avd_augment_records (default) or by numpy on the host
+        self.device_params = device_params
+        self._stage_cache = {}
+
+    def records_dev(self, chain, B, n_views, group=4):
+        """(rec [B*n_views, REC], gm [B*n_views, words] or None) drawn on the device."""
+        key = id(chain)
+        st = self._stage_cache.get(key)
+        if st is None or st[0] is not chain:
+            st = (chain, chain_stages(chain, group))
+            self._stage_cache[key] = st
+        stages = st[1]
+        n = B * n_views
+        dev = self.src.device
+        rec = torch.empty(n, REC, dtype=torch.float32, device=dev)
+        gm = None
+        if any(k == "grouped_masking" for k, _, _ in chain):
+            words = ((self.H // group) * (self.W // group) + 31) // 32
+            gm = torch.empty(n, words, dtype=torch.int32, device=dev)
+        self.calls += 1
+        rseed = (self.seed * 0xD1B54A32D192ED03 + 0x5EED * self.calls) & (2**64 - 1)
+        ops.augment_records(stages, n, self.H, self.W, group, rseed, rec, gm)
+        return rec, gm
 
     def records(self, chain, B, n_views):
         rec = np.zeros((B, n_views, REC), np.float32)
@@ -245,14 +309,18 @@ class ViewAugmenter:
 
     def __call__(self, idx, chain, n_views, out=None, order=0):
         idx = np.asarray(idx, np.int64)
-        rec, gm = self.records(chain, idx.shape[0], n_views)
+        if self.device_params:
+            rec, gm = self.records_dev(chain, idx.shape[0], n_views)
+        else:
+            rec, gm = self.records(chain, idx.shape[0], n_views)
         return self.apply(idx, rec, gm, n_views, out, order)
 
     def apply(self, idx, rec, gm, n_views, out=None, order=0):
         idx = np.asarray(idx, np.int64)
         if idx.size == 0 or idx.min() < 0 or idx.max() >= self.src.shape[0]:
             raise IndexError("sample id outside the dataset")
-        if gm is not None and rec[:, 22].max() >= gm.shape[0]:
+        on_dev = isinstance(rec, torch.Tensor)   # avd_augment_records: gm row r for record r
+        if not on_dev and gm is not None and rec[:, 22].max() >= gm.shape[0]:
             raise IndexError("grouped-mask row outside the bitmask table")
         dev = self.src.device
         B = idx.shape[0]
@@ -260,8 +328,11 @@ class ViewAugmenter:
         if out is None:
             out = torch.empty(shape, dtype=torch.float32, device=dev)
         idx_d = torch.from_numpy(idx).to(dev)
-        rec_d = torch.from_numpy(np.ascontiguousarray(rec, np.float32)).to(dev)
-        gm_d = None if gm is None else torch.from_numpy(gm.view(np.int32)).to(dev)
+        if on_dev:
+            rec_d, gm_d = rec, gm
+        else:
+            rec_d = torch.from_numpy(np.ascontiguousarray(rec, np.float32)).to(dev)
+            gm_d = None if gm is None else torch.from_numpy(gm.view(np.int32)).to(dev)
         self.calls += 1
         seed = (self.seed * 0x9E3779B97F4A7C15 + self.calls) & (2**64 - 1)
         ops.augment_views(self.src, idx_d, self.lut, rec_d, gm_d, 4, seed, n_views, self.H,
@@ -312,6 +383,23 @@ class MultiModalAugmentation:
         li = self.image(idx, self.local_transforms["image"], L) if L else None
         la = self.audio(idx, self.local_transforms["audio"], L) if L else None
         return gi, ga, li, la
+
+    def stage(self, idx, x_img, x_aud, with_orig):
+        """Build the views straight into the engine's staged view-major inputs (bf16 or f32
+        [(G + L [+1]) * B, H, W]): global views rows [0, G*B), local views [G*B, (G+L)*B), the
+        un-augmented originals (the Extended dataset's image / audio) the last B rows -- the
+        layout avd_stage_views would produce from the collated f32 views, without them."""
+        idx = np.asarray(idx, np.int64)
+        B, G, L = idx.shape[0], self.n_global_views, self.n_local_views
+        for aug, x, hw in ((self.image, x_img, 784), (self.audio, x_aud, 12544)):
+            key = "image" if aug is self.image else "audio"
+            nv = G + L + (1 if with_orig else 0)
+            xv = x.view(nv, B * hw)
+            aug(idx, self.global_transforms[key], G, out=xv[:G].view(-1), order=1)
+            if L:
+                aug(idx, self.local_transforms[key], L, out=xv[G:G + L].view(-1), order=1)
+            if with_orig:
+                aug.identity(idx, out=xv[G + L].view(-1))
 
 
 def process_augment_config(config, trial=None, is_hyperparameter_search=False):

@@ -169,11 +169,24 @@ class AVMNISTDinoLoader:
         lab = self.dev["labels"][torch.from_numpy(np.asarray(idx, np.int64)).to(img.device)]
         return img, aud, lab, views
 
+    def staged_batch(self, idx):
+        """Engine fast path: {"aug", "idx", "label"} -- MultiCentralEngine.stage builds the views
+        straight into its staged bf16 inputs (no collated f32 views)."""
+        lab = self.dev["labels"][torch.from_numpy(np.asarray(idx, np.int64)).to(self.dev["labels"].device)]
+        return {"aug": self.aug, "idx": np.asarray(idx, np.int64), "label": lab}
+
     def __iter__(self):
         order = self._order()
         self.epoch += 1
         for s in range(0, len(order), self.batch_size):
             yield self.batch(order[s:s + self.batch_size])
+
+    def iter_staged(self):
+        """One epoch of engine fast-path batches (staged_batch)."""
+        order = self._order()
+        self.epoch += 1
+        for s in range(0, len(order), self.batch_size):
+            yield self.staged_batch(order[s:s + self.batch_size])
 
 
 class AVMNISTLabelledLoader:

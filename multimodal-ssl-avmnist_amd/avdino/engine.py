@@ -570,16 +570,26 @@ class MultiCentralEngine:
         """Device batch dict -> view-major staged image/audio inputs (act dtype) and the labels,
         in fixed workspace buffers (what a captured step reads)."""
         ws = self.ws
-        g_img, l_img = batch["g_img"], batch["l_img"]
-        B, G = g_img.shape[:2]
-        L = l_img.shape[1]
-        nv = G + L + (1 if with_orig else 0)
-        x_img = ws.get("in.img", nv * B * 784, self.act)
-        x_aud = ws.get("in.aud", nv * B * 12544, self.act)
-        ops.stage_views(g_img.contiguous(), G, l_img.contiguous() if L else None, L,
-                        batch["image"].contiguous() if with_orig else None, B, 784, x_img)
-        ops.stage_views(batch["g_aud"].contiguous(), G, batch["l_aud"].contiguous() if L else None, L,
-                        batch["audio"].contiguous() if with_orig else None, B, 12544, x_aud)
+        if "aug" in batch:
+            # real-data path: the device augmentation writes the views straight into the staged
+            # inputs ({"aug": MultiModalAugmentation, "idx": sample ids, "label": ...})
+            aug, idx = batch["aug"], batch["idx"]
+            B, G, L = len(idx), aug.n_global_views, aug.n_local_views
+            nv = G + L + (1 if with_orig else 0)
+            x_img = ws.get("in.img", nv * B * 784, self.act)
+            x_aud = ws.get("in.aud", nv * B * 12544, self.act)
+            aug.stage(idx, x_img, x_aud, with_orig)
+        else:
+            g_img, l_img = batch["g_img"], batch["l_img"]
+            B, G = g_img.shape[:2]
+            L = l_img.shape[1]
+            nv = G + L + (1 if with_orig else 0)
+            x_img = ws.get("in.img", nv * B * 784, self.act)
+            x_aud = ws.get("in.aud", nv * B * 12544, self.act)
+            ops.stage_views(g_img.contiguous(), G, l_img.contiguous() if L else None, L,
+                            batch["image"].contiguous() if with_orig else None, B, 784, x_img)
+            ops.stage_views(batch["g_aud"].contiguous(), G, batch["l_aud"].contiguous() if L else None, L,
+                            batch["audio"].contiguous() if with_orig else None, B, 12544, x_aud)
         labels = None
         if self.mode == "semi_supervised":
             labels = ws.get("in.label", B, torch.int64)

@@ -658,17 +658,38 @@ AUG_REC = 28  # floats per (sample, view) record, include/avdino.h AVD_AUG_REC
 
 
 def augment_views(src_u8, idx, lut, rec, gm, group, seed, V, H, W, out, order=0):
-    """Device view augmentation (avd_augment_views): src_u8 [N, H*W] u8, idx [B] int64, lut [256]
-    f32, rec [B*V, AUG_REC] f32, gm [R, words] int32/uint32 or None, out f32 [B,V,H,W] (order 0)
-    or [V,B,H,W] (order 1).  Sample ids and bitmask rows are range-checked by the caller on the
-    host arrays before upload (avdino.augment.ViewAugmenter)."""
+    """Device view augmentation (avd_augment_views_dt): src_u8 [N, H*W] u8, idx [B] int64, lut
+    [256] f32, rec [B*V, AUG_REC] f32, gm [R, words] int32/uint32 or None, out f32 or bf16
+    [B,V,H,W] (order 0) or [V,B,H,W] (order 1; a bf16 out may be a row range of the engine's
+    staged view-major input).  Sample ids and bitmask rows are range-checked by the caller
+    (avdino.augment.ViewAugmenter)."""
     B = idx.numel()
     _need(src_u8.dtype == torch.uint8 and src_u8.dim() == 2 and src_u8.shape[1] == H * W, "aug src")
     _need(idx.dtype == torch.int64 and lut.numel() == 256 and lut.dtype == torch.float32, "aug idx/lut")
     _need(rec.dtype == torch.float32 and rec.shape == (B * V, AUG_REC), "aug records")
-    _need(out.dtype == torch.float32 and out.numel() == B * V * H * W, "aug out")
+    _need(out.dtype in (torch.float32, torch.bfloat16) and out.numel() == B * V * H * W, "aug out")
     for t in (src_u8, idx, lut, rec, out) + ((gm,) if gm is not None else ()):
         _need(t.is_contiguous() and t.device == out.device, "aug operands contiguous, one device")
     words = gm.shape[1] if gm is not None else 0
-    call("avd_augment_views", p(src_u8), p(idx), src_u8.shape[0], B, V, H, W, p(lut), p(rec),
-         p(gm), words, group, seed & (2**64 - 1), order, p(out), stream())
+    call("avd_augment_views_dt", p(src_u8), p(idx), src_u8.shape[0], B, V, H, W, p(lut), p(rec),
+         p(gm), words, group, seed & (2**64 - 1), order, p(out), dtcode(out), stream())
+
+
+AUG_STAGE_F = 8       # floats per chain stage of avd_augment_records
+AUG_MAX_STAGES = 8
+
+
+def augment_records(stages, n, H, W, group, seed, rec, gm):
+    """Device parameter draws (avd_augment_records): stages float32 numpy [S, 8] (host),
+    rec f32 [n, AUG_REC] and gm int32 [n, words] (or None without grouped masking) on the
+    device."""
+    import numpy as _np
+    st = _np.ascontiguousarray(stages, _np.float32)
+    _need(st.ndim == 2 and st.shape[1] == AUG_STAGE_F and st.shape[0] <= AUG_MAX_STAGES, "aug stages")
+    _need(rec.dtype == torch.float32 and rec.shape == (n, AUG_REC) and rec.is_contiguous(), "aug rec out")
+    words = 0
+    if gm is not None:
+        _need(gm.dim() == 2 and gm.shape[0] == n and gm.is_contiguous(), "aug gm out")
+        words = gm.shape[1]
+    call("avd_augment_records", st.ctypes.data, st.shape[0], n, H, W, group, seed & (2**64 - 1),
+         p(rec), p(gm), words, stream())

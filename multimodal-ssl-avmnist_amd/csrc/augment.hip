@@ -80,10 +80,11 @@ __device__ __forceinline__ float crop_sample(const View& v, int r, int c) {
   return hy * (hx * p0[x0] + lx * p0[x1]) + ly * (hx * p1[x0] + lx * p1[x1]);
 }
 
+template <typename TO>
 __global__ __launch_bounds__(kThreads) void augment_kernel(
     const uint8_t* __restrict__ src, const int64_t* __restrict__ idx, int V, int B, int H, int W,
     const float* __restrict__ lut, const float* __restrict__ recs, const uint32_t* __restrict__ gm,
-    int gm_words, int group, unsigned long long seed, int order, float* __restrict__ out) {
+    int gm_words, int group, unsigned long long seed, int order, TO* __restrict__ out) {
 #pragma clang fp contract(off)
   __shared__ float s_img[kMaxHW];
   __shared__ float s_lut[256];
@@ -133,7 +134,7 @@ __global__ __launch_bounds__(kThreads) void augment_kernel(
   const float cx = (float)(W - 1) * 0.5f, cy = (float)(H - 1) * 0.5f;
   const uint32_t* gmr = (gm && gmrow >= 0) ? gm + (size_t)gmrow * gm_words : nullptr;
   const int gw = group > 0 ? W / group : 1;
-  float* o = out + (order == 0 ? (size_t)rid : (size_t)v * B + b) * HW;
+  TO* o = out + (order == 0 ? (size_t)rid : (size_t)v * B + b) * HW;
 
   for (int p = threadIdx.x; p < HW; p += kThreads) {
     const int y = p / W, x = p - y * W;
@@ -164,8 +165,167 @@ __global__ __launch_bounds__(kThreads) void augment_kernel(
       const int g = (y / group) * gw + x / group;
       if ((gmr[g >> 5] >> (g & 31)) & 1u) val = val * 0.0f;
     }
-    o[p] = val;
+    if constexpr (sizeof(TO) == 4)
+      o[p] = val;
+    else
+      o[p] = f2bf(val);     // bf16 straight into the engine's staged view-major input
   }
+}
+
+// ----------------------------------------------------------------------------- parameter draws
+// The chain's random parameters drawn on the device (what ViewAugmenter.records draws with
+// numpy): one block per (sample, view) record; thread 0 walks the stages in order with a
+// counter-hash uniform stream (seed, record, draw index); the grouped mask picks exactly k of
+// the ng groups as the k smallest of ng hashed keys (block-wide bitonic sort in LDS), i.e. a
+// uniformly random k-subset like randperm(ng)[:k].
+enum { SK_CROP = 0, SK_TWARP, SK_FMASK, SK_TMASK, SK_ROT, SK_AFF, SK_ERASE, SK_NOISE, SK_GMASK };
+constexpr int kMaxStages = 8, kStageF = 8, kMaxGroups = 1024;
+struct Chain { float st[kMaxStages * kStageF]; int n; };
+
+struct Urng {
+  unsigned long long seed;
+  unsigned rec, ctr;
+  __device__ float u() {       // [0, 1), 24 bits
+    const unsigned long long r = mix64(seed ^ mix64(((unsigned long long)rec << 32) | ctr++));
+    return (float)(r >> 40) * 5.9604644775390625e-8f;
+  }
+  __device__ float uni(float a, float b) { return a + (b - a) * u(); }
+  __device__ int below(int n) {  // uniform integer in [0, n)
+    const int k = (int)(u() * (float)n);
+    return k < n ? k : n - 1;
+  }
+};
+
+// torchvision _get_inverse_affine_matrix, centre (0, 0), no shear
+__device__ void inv_affine(float angle_deg, float tx, float ty, float s, float* m) {
+  const float r = angle_deg * 0.017453292519943295f;
+  const float c = cosf(r), sn = sinf(r);
+  m[0] = c / s; m[1] = sn / s; m[2] = 0.f; m[3] = -sn / s; m[4] = c / s; m[5] = 0.f;
+  m[2] += m[0] * (-tx) + m[1] * (-ty);
+  m[5] += m[3] * (-tx) + m[4] * (-ty);
+}
+
+__global__ __launch_bounds__(256) void aug_records_kernel(Chain ch, int H, int W, int group,
+                                                          unsigned long long seed,
+                                                          float* __restrict__ recs,
+                                                          uint32_t* __restrict__ gm, int gm_words) {
+  __shared__ unsigned long long keys[kMaxGroups];
+  __shared__ int s_k, s_on;
+  const int rid = blockIdx.x;
+  float* rec = recs + (size_t)rid * AVD_AUG_REC;
+  Urng rng{seed, (unsigned)rid, 0u};
+  if (threadIdx.x == 0) {
+    float r[AVD_AUG_REC];
+    for (int i = 0; i < AVD_AUG_REC; ++i) r[i] = 0.f;
+    r[AVD_AUG_GM] = -1.f;
+    int flags = 0, gk = -1, gon = 0;
+    const float area = (float)(H * W);
+    for (int si = 0; si < ch.n; ++si) {
+      const float* a = ch.st + si * kStageF;
+      const int kind = (int)a[0];
+      const bool on = rng.u() < a[1];
+      const float* q = a + 2;
+      if (kind == SK_CROP || kind == SK_ERASE) {
+        // RandomResizedCrop / RandomErasing get_params: 10 attempts, then the fallback
+        const bool crop = kind == SK_CROP;
+        const float l0 = logf(q[2]), l1 = logf(q[3]);
+        int h = 0, w = 0, i = 0, j = 0;
+        bool found = false;
+        for (int t = 0; t < 10 && !found; ++t) {
+          const float ta = area * rng.uni(q[0], q[1]);
+          const float ar = expf(rng.uni(l0, l1));
+          const int ww = (int)rintf(sqrtf(crop ? ta * ar : ta / ar));
+          const int hh = (int)rintf(sqrtf(crop ? ta / ar : ta * ar));
+          found = crop ? (ww > 0 && ww <= W && hh > 0 && hh <= H) : (hh < H && ww < W);
+          if (found) { h = hh; w = ww; }
+        }
+        if (found) {
+          i = rng.below(H - h + 1);
+          j = rng.below(W - w + 1);
+        } else if (crop) {      // centre crop at the nearest admissible aspect
+          const float inr = (float)W / (float)H;
+          if (inr < q[2]) { w = W; h = (int)rintf((float)W / q[2]); }
+          else if (inr > q[3]) { h = H; w = (int)rintf((float)H * q[3]); }
+          else { w = W; h = H; }
+          i = (H - h) / 2;
+          j = (W - w) / 2;
+        }
+        if (on) {
+          const int o = crop ? AVD_AUG_CROP : AVD_AUG_ERASE;
+          r[o] = (float)i; r[o + 1] = (float)j; r[o + 2] = (float)h; r[o + 3] = (float)w;
+          if (crop) flags |= 1;
+        }
+      } else if (kind == SK_ROT) {
+        float m[6];
+        inv_affine(-rng.uni(-q[0], q[0]), 0.f, 0.f, 1.f, m);
+        if (on) { for (int k = 0; k < 6; ++k) r[AVD_AUG_ROT + k] = m[k]; flags |= 4; }
+      } else if (kind == SK_AFF) {
+        const float ang = rng.uni(-q[0], q[0]);
+        const float tx = q[1] >= 0.f ? rintf(rng.uni(-q[1] * W, q[1] * W)) : 0.f;
+        const float ty = q[1] >= 0.f ? rintf(rng.uni(-q[2] * H, q[2] * H)) : 0.f;
+        const float sc = q[3] > 0.f ? rng.uni(q[3], q[4]) : 1.f;
+        float m[6];
+        inv_affine(ang, tx, ty, sc, m);
+        if (on) { for (int k = 0; k < 6; ++k) r[AVD_AUG_AFF + k] = m[k]; flags |= 2; }
+      } else if (kind == SK_TWARP) {
+        const float rate = rng.uni(q[0], q[1]);
+        if (on) { r[AVD_AUG_RATE] = rate; flags |= 8; }
+      } else if (kind == SK_FMASK || kind == SK_TMASK) {
+        const int size = kind == SK_FMASK ? H : W;
+        const float value = rng.u() * q[0];
+        const float minv = rng.u() * ((float)size - value);
+        const int st = (int)floorf(minv), en = st + (int)floorf(value);
+        const int o = kind == SK_FMASK ? AVD_AUG_FMASK : AVD_AUG_TMASK;
+        if (on) { r[o] = (float)st; r[o + 1] = (float)en; }
+      } else if (kind == SK_NOISE) {
+        if (on) r[AVD_AUG_NOISE] = q[0];
+      } else if (kind == SK_GMASK) {
+        const int ng = (H / group) * (W / group);
+        gk = (int)(q[0] * (float)ng);
+        gon = on;
+        if (on) r[AVD_AUG_GM] = (float)rid;
+      }
+    }
+    r[AVD_AUG_FLAGS] = (float)flags;
+    for (int i = 0; i < AVD_AUG_REC; ++i) rec[i] = r[i];
+    s_k = gk;
+    s_on = gon;
+  }
+  __syncthreads();
+  const int k = s_k;
+  if (k < 0 || !gm) return;
+  // exactly k distinct groups: the k smallest of ng random keys (index in the low bits)
+  const int ng = (H / group) * (W / group);
+  int n2 = 1;
+  while (n2 < ng) n2 <<= 1;
+  for (int i = threadIdx.x; i < n2; i += 256)
+    keys[i] = i < ng ? ((mix64(seed ^ mix64(((unsigned long long)(rid | 0x80000000u) << 32) | i))
+                         & ~0x3FFull) | (unsigned long long)i)
+                     : ~0ull;
+  __syncthreads();
+  for (int size = 2; size <= n2; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < n2; i += 256) {
+        const int jx = i ^ stride;
+        if (jx > i) {
+          const bool up = (i & size) == 0;
+          const unsigned long long a = keys[i], b = keys[jx];
+          if ((a > b) == up) { keys[i] = b; keys[jx] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  __shared__ uint32_t bits[kMaxGroups / 32];
+  for (int wd = threadIdx.x; wd < kMaxGroups / 32; wd += 256) bits[wd] = 0u;
+  __syncthreads();
+  if (s_on)
+    for (int i = threadIdx.x; i < k; i += 256) {
+      const int gidx = (int)(keys[i] & 0x3FFull);
+      atomicOr(&bits[gidx >> 5], 1u << (gidx & 31));     // LDS
+    }
+  __syncthreads();
+  uint32_t* row = gm + (size_t)rid * gm_words;
+  for (int wd = threadIdx.x; wd < gm_words; wd += 256) row[wd] = wd < kMaxGroups / 32 ? bits[wd] : 0u;
 }
 
 }  // namespace
@@ -181,8 +341,51 @@ extern "C" int avd_augment_views(const uint8_t* src_u8, const int64_t* idx, long
              gm_words * 32 < (H / group) * (W / group)))
     return AVD_ERR_SHAPE;
   (void)n_src;  // sample ids are range-checked by the host wrapper (avdino.ops.augment_views)
-  augment_kernel<<<B * V, kThreads, 0, avd_stream(stream)>>>(src_u8, idx, V, B, H, W, lut, rec, gm,
-                                                             gm_words, group, seed, order, out);
+  augment_kernel<float><<<B * V, kThreads, 0, avd_stream(stream)>>>(src_u8, idx, V, B, H, W, lut, rec, gm,
+                                                                    gm_words, group, seed, order, out);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+extern "C" int avd_augment_views_dt(const uint8_t* src_u8, const int64_t* idx, long long n_src,
+                                    int B, int V, int H, int W, const float* lut, const float* rec,
+                                    const uint32_t* gm, int gm_words, int group,
+                                    unsigned long long seed, int order, void* out, int odt,
+                                    void* stream) {
+  if (odt == AVD_F32)
+    return avd_augment_views(src_u8, idx, n_src, B, V, H, W, lut, rec, gm, gm_words, group, seed,
+                             order, (float*)out, stream);
+  if (odt != AVD_BF16) return AVD_ERR_DTYPE;
+  if (!src_u8 || !idx || !lut || !rec || !out) return AVD_ERR_ARG;
+  if (B <= 0 || V <= 0 || H <= 0 || W <= 0 || n_src <= 0) return AVD_ERR_SHAPE;
+  if ((long long)H * W > kMaxHW || (H * W) % 4 || order < 0 || order > 1) return AVD_ERR_SHAPE;
+  if (gm && (group <= 0 || H % group || W % group ||
+             gm_words * 32 < (H / group) * (W / group)))
+    return AVD_ERR_SHAPE;
+  augment_kernel<bf16><<<B * V, kThreads, 0, avd_stream(stream)>>>(src_u8, idx, V, B, H, W, lut, rec, gm,
+                                                                   gm_words, group, seed, order,
+                                                                   (bf16*)out);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+extern "C" int avd_augment_records(const float* stages, int nstages, int n, int H, int W,
+                                   int group, unsigned long long seed, float* rec, uint32_t* gm,
+                                   int gm_words, void* stream) {
+  if (!stages || !rec) return AVD_ERR_ARG;
+  if (nstages < 0 || nstages > kMaxStages || n <= 0 || H <= 0 || W <= 0) return AVD_ERR_SHAPE;
+  Chain ch{};
+  ch.n = nstages;
+  bool has_gm = false;
+  for (int i = 0; i < nstages * kStageF; ++i) ch.st[i] = stages[i];
+  for (int i = 0; i < nstages; ++i) has_gm |= (int)stages[i * kStageF] == SK_GMASK;
+  if (has_gm) {
+    if (!gm || group <= 0 || H % group || W % group) return AVD_ERR_SHAPE;
+    const int ng = (H / group) * (W / group);
+    if (ng > kMaxGroups || gm_words * 32 < ng) return AVD_ERR_SHAPE;
+  }
+  aug_records_kernel<<<n, 256, 0, avd_stream(stream)>>>(ch, H, W, group, seed, rec,
+                                                        has_gm ? gm : nullptr, gm_words);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

@@ -83,3 +83,120 @@ def test_loader_batches_feed_a_training_step(tmp_path):
     batch = dict(image=img, audio=aud, label=lab, g_img=gi, g_aud=ga, l_img=li, l_aud=la)
     loss = eng.step(batch).item()
     assert np.isfinite(loss)
+
+
+# ---------------------------------------------------------------------- device parameter draws
+def _dev_records(chain, n, H, W, seed):
+    src = torch.zeros(1, H * W, dtype=torch.uint8, device="cuda")
+    aug = A.ViewAugmenter(src, torch.zeros(256, device="cuda"), H, W, seed=seed)
+    rec, gm = aug.records_dev(chain, n, 1)
+    return rec.cpu().numpy(), None if gm is None else gm.cpu().numpy().view(np.uint32)
+
+
+def _stats(rec, gm, H, W):
+    fl = rec[:, 23].astype(np.int64)
+    crop, aff, rot, tw = (fl & 1) > 0, (fl & 2) > 0, (fl & 4) > 0, (fl & 8) > 0
+    er = rec[:, 26] > 0
+    out = {"p_crop": crop.mean(), "p_aff": aff.mean(), "p_rot": rot.mean(), "p_tw": tw.mean(),
+           "p_erase": er.mean(), "p_noise": (rec[:, 21] != 0).mean(), "p_gm": (rec[:, 22] >= 0).mean(),
+           "p_fmask": (rec[:, 18] > rec[:, 17]).mean(), "p_tmask": (rec[:, 20] > rec[:, 19]).mean()}
+    if crop.any():
+        out["crop_area"] = (rec[crop, 2] * rec[crop, 3]).mean() / (H * W)
+        out["crop_top"] = rec[crop, 0].mean() / H
+    if aff.any():
+        out["aff_scale"] = np.hypot(rec[aff, 4], rec[aff, 5]).mean()
+        out["aff_tx"] = np.abs(rec[aff, 6]).mean() / W
+    if rot.any():
+        out["rot_sin"] = np.abs(rec[rot, 11]).mean()
+    if tw.any():
+        out["rate"] = rec[tw, 16].mean()
+    if er.any():
+        out["erase_area"] = (rec[er, 26] * rec[er, 27]).mean() / (H * W)
+    fm = rec[:, 18] > rec[:, 17]
+    if fm.any():
+        out["fmask_w"] = (rec[fm, 18] - rec[fm, 17]).mean()
+    return out
+
+
+@pytest.mark.parametrize("view,mod", [("global", "image"), ("local", "image"),
+                                      ("global", "audio"), ("local", "audio")])
+def test_device_param_draws_match_the_host_distributions(view, mod):
+    """avd_augment_records vs the numpy sampler (the get_params rules): 20000 draws each;
+    probabilities within 0.015, mean box areas / scales / rates within 3 % (the streams differ,
+    the distributions must not)."""
+    H = W = 28 if mod == "image" else 112
+    chain = A.default_chains()[view][mod]
+    n = 20000
+    drec, dgm = _dev_records(chain, n, H, W, 77)
+    hrec, hgm = _records(chain, n, 1, H, W, 78)
+    ds, hs = _stats(drec, dgm, H, W), _stats(hrec, hgm, H, W)
+    assert ds.keys() == hs.keys()
+    for k in ds:
+        if k.startswith("p_"):
+            assert abs(ds[k] - hs[k]) < 0.015, (k, ds[k], hs[k])
+        else:
+            assert abs(ds[k] - hs[k]) <= 0.03 * max(abs(hs[k]), 1e-3) + 0.002, (k, ds[k], hs[k])
+
+
+def test_device_param_draws_bounds_and_exact_masks():
+    chain = A.default_chains()["local"]["audio"]
+    H = W = 112
+    rec, gm = _dev_records(chain, 4096, H, W, 5)
+    crop = (rec[:, 23].astype(np.int64) & 1) > 0
+    t, l_, h, w = rec[crop, 0], rec[crop, 1], rec[crop, 2], rec[crop, 3]
+    assert (h > 0).all() and (w > 0).all() and (t >= 0).all() and (l_ >= 0).all()
+    assert (t + h <= H).all() and (l_ + w <= W).all()
+    ng = (H // 4) * (W // 4)
+    k = int(0.6 * ng)
+    on = rec[:, 22] >= 0
+    pop = np.array([bin(int(x)).count("1") for x in gm.reshape(-1)]).reshape(gm.shape).sum(1)
+    assert (pop[on] == k).all() and (pop[~on] == 0).all()
+    assert (rec[on, 22] == np.nonzero(on)[0]).all()
+    # deterministic in the seed
+    rec2, gm2 = _dev_records(chain, 4096, H, W, 5)
+    assert np.array_equal(rec, rec2) and np.array_equal(gm, gm2)
+
+
+def test_staged_bf16_views_equal_the_f32_views_rounded():
+    """The views written straight into the staged bf16 input equal the f32 views (same
+    records, same noise seed) rounded to bf16."""
+    rng = np.random.default_rng(6)
+    src = torch.from_numpy(rng.integers(0, 256, (9, 12544), dtype=np.uint8)).cuda()
+    lut = torch.from_numpy(OA.normalise_lut("audio")).cuda()
+    chain = A.default_chains()["local"]["audio"]
+    idx = np.array([3, 1, 8, 0])
+    a32 = A.ViewAugmenter(src, lut, 112, 112, seed=2)
+    a16 = A.ViewAugmenter(src, lut, 112, 112, seed=2)
+    v32 = a32(idx, chain, 3, order=1)
+    out = torch.empty(3 * 4 * 12544, dtype=torch.bfloat16, device="cuda")
+    a16(idx, chain, 3, out=out, order=1)
+    assert torch.equal(out.view_as(v32), v32.to(torch.bfloat16))
+
+
+def test_engine_step_from_staged_augmentation_equals_collated_views(tmp_path):
+    """MultiCentralEngine.stage({"aug", "idx"}) builds the views in place; the same seeds
+    through the collated f32 views + avd_stage_views give the same staged bits and loss."""
+    from avdino.data import AVMNISTDinoLoader
+    from avdino.engine import Hyper, MultiCentralEngine
+    from avdino.params import ParamStore
+    from avdino.spec import multimodal_dino_sd
+    root = _fake_avmnist(tmp_path, n=40)
+    mk = lambda: AVMNISTDinoLoader(root, batch_size=8, train_size=36, val_size=4, seed=3,  # noqa: E731
+                                   multimodal_mode="mse", device="cuda", shuffle=False)
+    la, lb = mk(), mk()
+    idx = la._order()[:8]
+    E, D, P = 32, 32, 16
+    res = []
+    for batch in (la.staged_batch(idx), None):
+        store = ParamStore(multimodal_dino_sd("mse", E, D, P), "cuda:0", seed=1)
+        eng = MultiCentralEngine(store, "mse", E, D, P, Hyper(dropout=0.0, fusion_dropout=0.0),
+                                 act_dtype=torch.bfloat16)
+        if batch is None:
+            img, aud, lab, (gi, ga, li, la_) = lb.batch(idx)
+            batch = dict(image=img, audio=aud, label=lab, g_img=gi, g_aud=ga, l_img=li, l_aud=la_)
+        staged = eng.stage(batch, True)
+        loss = eng._forward_staged(staged, training=True).item()
+        res.append((staged[0].clone(), staged[1].clone(), loss))
+    (xi0, xa0, l0), (xi1, xa1, l1) = res
+    assert torch.equal(xi0, xi1) and torch.equal(xa0, xa1)
+    assert l0 == l1

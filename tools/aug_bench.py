@@ -1,10 +1,17 @@
-"""Time the device data path (avd_augment_views) on one config-2 batch: B=1024 pairs, 2 global +
-4 local views of both modalities plus the originals, against its HBM roofline.
+"""Time the device data path on config-2 batches (B=1024 pairs, 2 global + 4 local views of both
+modalities plus the originals) and the real-data training step it feeds.
 
-Algorithmic bytes per launch = outputs written (4 B x H x W per view) + each source row read
-once (H x W bytes per sample; later views of a sample hit L2).  Timed with HIP events on the
-current stream around `iters` repetitions of the same launches; parameter draws (host) are
-made once, outside the timed region, and reported separately."""
+  collated_f32  host numpy parameter draws + avd_augment_views (f32 collated views) +
+                avd_stage_views (f32 -> bf16 staged input): the round-1 path
+  staged_bf16   avd_augment_records (device draws) + avd_augment_views_dt writing bf16 straight
+                into the engine's staged view-major input (MultiModalAugmentation.stage)
+  step_*        MultiCentralEngine (mse, bf16, graph replay) steps fed by staged_bf16 batches of
+                a synthetic AVMNIST-shaped uint8 dataset resident in HBM, vs the same engine on
+                pre-built synthetic views (bench.py's input)
+
+Algorithmic bytes of the staged path per batch: the staged bf16 views written once
+(2 B x H x W x views) + each source row read once per modality.  Times from HIP events on the
+current stream; one JSON line per measurement."""
 import json
 import sys
 import time
@@ -19,51 +26,88 @@ from avdino import augment as A  # noqa: E402
 from avdino import ops  # noqa: E402
 
 
-def main(B=1024, N=55000, iters=20):
+def timed(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters, (time.perf_counter() - t0) * 1e3 / iters
+
+
+def main(B=1024, N=55000, G=2, L=4, iters=20):
     dev = torch.device("cuda")
     rng = np.random.default_rng(0)
     src = {"image": torch.from_numpy(rng.integers(0, 256, (N, 784), dtype=np.uint8)).to(dev),
            "audio": torch.from_numpy(rng.integers(0, 256, (N, 12544), dtype=np.uint8)).to(dev)}
     lut = torch.arange(256, dtype=torch.float32, device=dev) / 255.0
     idx = rng.choice(N, B, replace=False)
-    ch = A.default_chains()
-    plan = []
-    t0 = time.perf_counter()
-    for mod, HW in (("image", 28), ("audio", 112)):
-        aug = A.ViewAugmenter(src[mod], lut, HW, HW, seed=1)
-        for grp, V in (("global", 2), ("local", 4)):
-            rec, gm = aug.records(ch[grp][mod], B, V)
-            plan.append((aug, rec, gm, V, HW))
-        ident = np.zeros((B, A.REC), np.float32)
-        ident[:, 22] = -1
-        plan.append((aug, ident, None, 1, HW))
-    host_ms = (time.perf_counter() - t0) * 1e3
-    staged = []
-    for aug, rec, gm, V, HW in plan:
-        staged.append((aug.src, torch.from_numpy(idx).to(dev), torch.from_numpy(rec).to(dev),
-                       None if gm is None else torch.from_numpy(gm.view(np.int32)).to(dev), V, HW,
-                       torch.empty((B, V, HW, HW), device=dev)))
-    nbytes = sum(B * V * HW * HW * 4 + B * HW * HW for *_, V, HW, _ in staged)
+    nv = G + L + 1
+    x_img = torch.empty(nv * B * 784, dtype=torch.bfloat16, device=dev)
+    x_aud = torch.empty(nv * B * 12544, dtype=torch.bfloat16, device=dev)
 
-    def run():
-        for s, i, r, g, V, HW, out in staged:
-            ops.augment_views(s, i, lut, r, g, 4, 7, V, HW, HW, out, 0)
+    def make_aug(device_params):
+        aug = A.MultiModalAugmentation(G, L)
+        return aug.bind(A.ViewAugmenter(src["image"], lut, 28, 28, seed=1, device_params=device_params),
+                        A.ViewAugmenter(src["audio"], lut, 112, 112, seed=2, device_params=device_params))
 
-    run()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(iters):
-        run()
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / iters
-    gbs = nbytes / (ms * 1e-3) / 1e9
-    print(json.dumps({"what": "device augmentation, config-2 batch (B=1024, 2+4 views + originals, "
-                      "both modalities, 6 launches)", "ms_per_batch": round(ms, 4),
-                      "pairs_per_s": round(B / (ms * 1e-3), 1), "algorithmic_bytes": nbytes,
-                      "achieved_GBps": round(gbs, 1), "peak_GBps": 8000.0,
-                      "frac": round(gbs / 8000.0, 4), "host_param_draw_ms": round(host_ms, 2)}))
+    host = make_aug(False)
+
+    def collated():
+        gi, ga, li, la = host(idx)
+        img = host.image.identity(idx)
+        aud = host.audio.identity(idx)
+        ops.stage_views(gi, G, li, L, img, B, 784, x_img)
+        ops.stage_views(ga, G, la, L, aud, B, 12544, x_aud)
+
+    devp = make_aug(True)
+
+    def staged():
+        devp.stage(idx, x_img, x_aud, True)
+
+    nbytes = nv * B * (784 + 12544) * 2 + B * (784 + 12544)
+    for name, fn in (("collated_f32", collated), ("staged_bf16", staged)):
+        gpu_ms, wall_ms = timed(fn, iters)
+        print(json.dumps({"bench": "augment_batch", "path": name, "B": B, "views": nv,
+                          "gpu_ms": round(gpu_ms, 3), "wall_ms": round(wall_ms, 3),
+                          "pairs_per_s": round(B / (max(gpu_ms, wall_ms) / 1e3), 1),
+                          "staged_GBps": round(nbytes / (gpu_ms / 1e3) / 1e9, 1)}), flush=True)
+
+    # the training step fed by the device data path vs pre-built synthetic views
+    from avdino.engine import Hyper, MultiCentralEngine
+    from avdino.params import ParamStore
+    from avdino.spec import multimodal_dino_sd
+    E, D, P = 256, 256, 128
+    store = ParamStore(multimodal_dino_sd("mse", E, D, P), dev, seed=0)
+    eng = MultiCentralEngine(store, "mse", E, D, P, Hyper(), act_dtype=torch.bfloat16)
+    eng.use_graph = True
+    eng.graph.warmup = 2
+    labels = torch.zeros(B, dtype=torch.int64, device=dev)
+    batches = [{"aug": devp, "idx": rng.choice(N, B, replace=False), "label": labels}
+               for _ in range(4)]
+    px = lambda *s: torch.rand(*s, device=dev)  # noqa: E731
+    synth = {"image": px(B, 1, 28, 28), "audio": px(B, 1, 112, 112), "label": labels,
+             "g_img": px(B, G, 1, 28, 28), "g_aud": px(B, G, 1, 112, 112),
+             "l_img": px(B, L, 1, 28, 28), "l_aud": px(B, L, 1, 112, 112)}
+    for name, feed in (("step_synthetic_views", lambda i: synth),
+                       ("step_device_augmented", lambda i: batches[i % len(batches)])):
+        for i in range(4):
+            eng.step(feed(i))
+        torch.cuda.synchronize()
+        k = [0]
+
+        def one():
+            eng.step(feed(k[0]))
+            k[0] += 1
+
+        gpu_ms, wall_ms = timed(one, iters)
+        print(json.dumps({"bench": "train_step", "path": name, "B": B, "mode": "mse", "dtype": "bf16",
+                          "ms_per_step": round(max(gpu_ms, wall_ms), 3),
+                          "pairs_per_s": round(B / (max(gpu_ms, wall_ms) / 1e3), 1)}), flush=True)
 
 
 if __name__ == "__main__":
