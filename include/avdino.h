@@ -207,8 +207,10 @@ int avd_cl_bn_bwd_apply(const void* y, int dt, const void* gout, int mode, const
                         int H, int W, void* stream);
 
 /* Fused BatchNorm-backward apply + conv weight gradient of a first (Cin = 1) layer whose output
- * is pooled in mode 0 (the CentralNet audio conv1: Cout 8, 5x5, pad 2, H, W % 16 == 0,
- * W <= 112, bf16): computes dy exactly as avd_cl_bn_bwd_apply and, without storing it,
+ * is pooled in mode 0 -- the CentralNet audio conv1 (Cout 8, 5x5, pad 2, H, W % 16 == 0,
+ * W <= 112) and the first 3x3 layer of the SimCLR / unimodal encoders (Cout 16/32, 3x3, pad 1,
+ * H % 4 == 0, W even; models/dino.py:18-73), bf16: computes dy exactly as
+ * avd_cl_bn_bwd_apply and, without storing it,
  * parts[s][Cout*K*K] = per-slab partial dW (reduce with avd_sum_rows over
  * avd_cl_apply_wgrad_slabs() rows).  Replaces avd_cl_bn_bwd_apply + avd_cl_conv_wgrad for that
  * layer (CentralUnimodalAudio.conv1/bn1, unimodal.py:160-190); the first layer needs no dx.

@@ -73,7 +73,14 @@ int avd_cl_weight_layout(const float* w, void* wk, int dt, int Cout, int Cin, in
   return avd_cl_weight_layout_impl(w, wk, dt, Cout, Cin, K, dgrad, avd_stream(stream));
 }
 
+int avd_c1w3_slabs(int dt, int N, int Cin, int H, int W, int Cout, int K, int pad);
+int avd_c1w3_apply_wgrad(const void* y, const void* gout, const float* scale, const float* shift,
+                         const float* coef, const void* x, float* parts, int N, int B, int H,
+                         int W, int Cout, hipStream_t st);
+
 int avd_cl_apply_wgrad_slabs(int dt, int N, int Cin, int H, int W, int Cout, int K, int pad) {
+  // the first 3x3 layer of the SimCLR / unimodal encoders (c1w3.hip)
+  if (const int s = avd_c1w3_slabs(dt, N, Cin, H, W, Cout, K, pad)) return s;
   if (!avd_c1p8_eligible(dt, Cin, Cout, K, H, W) || pad != 2 || W > 112) return 0;
   return avd_c1p8_wgrad_slabs(N, H);
 }
@@ -85,6 +92,9 @@ int avd_cl_bn_bwd_apply_wgrad(const void* y, const void* gout, const float* scal
   if (!y || !gout || !scale || !shift || !coef || !x || !parts) return AVD_ERR_ARG;
   if (N <= 0 || B <= 0 || N % B) return AVD_ERR_SHAPE;
   if (avd_cl_apply_wgrad_slabs(dt, N, Cin, H, W, Cout, K, pad) == 0) return AVD_ERR_SHAPE;
+  if (avd_c1w3_slabs(dt, N, Cin, H, W, Cout, K, pad))
+    return avd_c1w3_apply_wgrad(y, gout, scale, shift, coef, x, parts, N, B, H, W, Cout,
+                                avd_stream(stream));
   return avd_c1p8_bwd_apply_wgrad(y, gout, scale, shift, coef, x, parts, N, B, H, W,
                                   avd_stream(stream));
 }

@@ -364,3 +364,26 @@ def test_bf16_step_vs_fp32_step_config2(capsys):
     assert abs(l16 - l32) / abs(l32) < 1e-3
     assert ratio[0][0] < 2.0, ratio[:4]
     assert med[0] < 1.25 * med[1], med
+
+
+def test_simclr_conv1_bwd_apply_wgrad_bench_size(ops):
+    """c1w3_kernel (the 3x3 encoders' conv1 1->32 p1 BN-backward apply fused with dW) at
+    config 4's N = 2048 spectrograms (112x112): against the unfused apply + weight gradient
+    (same bf16 dy) and float64."""
+    N, B, H, C, K, pad = 2048, 2048, 112, 32, 3, 1
+    G = N // B
+    g = torch.Generator(device="cuda").manual_seed(21)
+    x = rnd(g, (N, H, H, 1), 0, 1, T)
+    y = (torch.randn(N, H, H, C, generator=g, device="cuda") * 0.8 + 0.1).to(T)
+    gout = rnd(g, (N, H // 2, H // 2, C), dtype=T)
+    scale, shift, coef = _bn_setup(g, G, C)
+    ns = ops.cl_apply_wgrad_slabs(T, N, 1, H, H, C, K, pad)
+    assert 0 < ns < N * (H // 4), "persistent grid expected at bench size"
+    parts = torch.full((ns * C * K * K,), float("nan"), device="cuda")
+    ops.cl_bn_bwd_apply_wgrad(y, gout, scale, shift, coef, x, parts, N, B, 1, H, H, C, K, pad)
+    dw = torch.empty(C * K * K, device="cuda")
+    ops.sum_rows(parts, ns, C * K * K, dw)
+    dy = torch.empty_like(y)
+    ops.cl_bn_bwd_apply(y, gout, 0, scale, shift, coef, dy, N, B, C, H, H)
+    dw64 = wgrad_ref(x, dy, K, pad)
+    assert grel(dw, dw64) < 1e-5, grel(dw, dw64)

@@ -202,14 +202,16 @@ def test_cl_bn_block_fwd_bwd(ops, HC, mode, dt):
     assert rel(nchw(host(dy)), dy_ref) < (5e-3 if dt == "bf16" else 1e-5)
 
 
-@pytest.mark.parametrize("HN", [(112, 4), (48, 6)])
+@pytest.mark.parametrize("HN", [(112, 4, 8, 5, 2), (48, 6, 8, 5, 2), (112, 4, 32, 3, 1),
+                                (28, 24, 32, 3, 1), (56, 6, 16, 3, 1)])
 def test_cl_bn_bwd_apply_wgrad_fused_first_layer(ops, HN):
-    """Fused BN-backward apply + weight gradient of the audio first layer (conv1 1->8 5x5 p2,
-    bf16) == avd_cl_bn_bwd_apply followed by avd_cl_conv_wgrad: dy is rounded to bf16 the same
-    way in both, so only the fp32 accumulation order differs (rel 1e-5); and the float64 truth
-    from the same bf16 operands within 1e-5."""
-    H, N = HN
-    B, C, K, pad = N // 2, 8, 5, 2
+    """Fused BN-backward apply + weight gradient of a first layer -- the CentralNet audio conv1
+    (1->8 5x5 p2, c1p8) and the 3x3 encoders' conv1 (1->16/32 3x3 p1, c1w3), bf16 ==
+    avd_cl_bn_bwd_apply followed by avd_cl_conv_wgrad: dy is rounded to bf16 the same way in
+    both, so only the fp32 accumulation order differs (rel 1e-5); and the float64 truth from
+    the same bf16 operands within 1e-5."""
+    H, N, C, K, pad = HN
+    B = N // 2
     G = N // B
     g = np.random.default_rng(H)
     T = torch.bfloat16
@@ -237,7 +239,7 @@ def test_cl_bn_bwd_apply_wgrad_fused_first_layer(ops, HN):
     assert rel(host(dw), host(dw_ref)) < 1e-5, rel(host(dw), host(dw_ref))
     # float64 truth on the same bf16 dy
     win = np.lib.stride_tricks.sliding_window_view(np.pad(nchw(x).astype(np.float64),
-                                                          ((0, 0), (0, 0), (2, 2), (2, 2))), (K, K), (2, 3))
+                                                          ((0, 0), (0, 0), (pad, pad), (pad, pad))), (K, K), (2, 3))
     dw64 = np.einsum("nohw,nchwij->ocij", nchw(host(dy)), win, optimize=True)
     assert rel(host(dw), dw64) < 1e-5
 
