@@ -36,15 +36,6 @@ __device__ __forceinline__ bf16x8 fr8(u2w lo, u2w hi) {
 }
 __device__ __forceinline__ int kpx(int g, int h, int q) { return 16 * (g >> 1) + 8 * h + 4 * (g & 1) + q; }
 
-__device__ __forceinline__ void ld8(const bf16* p, float (&v)[8]) {
-  const u4 w = *reinterpret_cast<const u4*>(p);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[2 * i] = __uint_as_float(w[i] << 16);
-    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-  }
-}
-
 constexpr int XS9 = 16;      // x9 pixel stride (taps)
 constexpr int TRW = 4;       // tile rows (two window rows)
 
@@ -81,49 +72,96 @@ __global__ __launch_bounds__(256, 2) void c1w3_kernel(
   for (int i = TP * (XS9 / 8) + tid; i < TPP * (XS9 / 8); i += 256)
     *reinterpret_cast<u4*>(x9 + (size_t)i * 8) = u4{0u, 0u, 0u, 0u};
 
+  // this thread's window tasks t = tid + 256 i all have channel group q = tid % VQ; its 8
+  // channels' BN coefficients are held in registers (reloaded when the BN group changes)
+  constexpr int TPT = 2;                      // window tasks per thread (TRW=4: 2*Wp*VQ <= 512)
+  const int q = tid % VQ, c0 = 8 * q;
+  const int ntask = (TRW / 2) * Wp * VQ;
+  float sc[8], sf[8], k1[8], kx[8], k0[8];
+  int cur_g = -1;
+  // next tile's operands, loaded while the current tile's MFMAs run
+  u4 py[TPT][4], pg[TPT];
+  bf16 px[3];
+  auto load = [&](int ti) {
+    const int n = ti / tps, y0 = (ti - n * tps) * TRW;
+#pragma unroll
+    for (int i = 0; i < TPT; ++i) {
+      const int t = tid + 256 * i;
+      const int w = t / VQ, wc = w % Wp, wr = w / Wp;
+      const bool ok = t < ntask;
+      const int yy = y0 + 2 * wr;
+      const size_t pix0 = ok ? ((size_t)n * H + yy) * W + 2 * wc : 0;
+      const size_t g0 = ok ? (((size_t)n * Hp + yy / 2) * Wp + wc) * C + c0 : 0;
+      py[i][0] = *reinterpret_cast<const u4*>(y + pix0 * C + c0);
+      py[i][1] = *reinterpret_cast<const u4*>(y + (pix0 + 1) * C + c0);
+      py[i][2] = *reinterpret_cast<const u4*>(y + (pix0 + W) * C + c0);
+      py[i][3] = *reinterpret_cast<const u4*>(y + (pix0 + W + 1) * C + c0);
+      pg[i] = *reinterpret_cast<const u4*>(gout + g0);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int e = tid + 256 * i;
+      const int r = e / XW, c = e - r * XW, iy = y0 - 1 + r, ix = c - 1;
+      const bool ok = e < (TRW + 2) * XW && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      px[i] = x[ok ? ((size_t)n * H + iy) * W + ix : 0];
+    }
+  };
+  auto unpack = [](u4 w, float (&v)[8]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  };
+  if (t0 < t1) load(t0);
+
   for (int ti = t0; ti < t1; ++ti) {
     const int n = ti / tps, y0 = (ti - n * tps) * TRW, gb = n / B;
-    __syncthreads();                          // the previous tile's reads are done
-    // ---- x rows y0-1 .. y0+TRW (zero outside the image)
-    for (int i = tid; i < (TRW + 2) * XW; i += 256) {
-      const int r = i / XW, c = i - r * XW, iy = y0 - 1 + r, ix = c - 1;
-      xr[i] = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-                  ? x[((size_t)n * H + iy) * W + ix] : f2bf(0.f);
-    }
-    // ---- dy per pooling window x 8 channels into dys
-    const int ntask = (TRW / 2) * Wp * VQ;
-    for (int t = tid; t < ntask; t += 256) {
-      const int q = t % VQ, w = t / VQ;
-      const int wc = w % Wp, wr = w / Wp;
-      const int c0 = 8 * q;
-      const int yy = y0 + 2 * wr, hp = yy / 2;
-      const size_t pix0 = ((size_t)n * H + yy) * W + 2 * wc;
-      float v[4][8], gg[8];
-      ld8(y + pix0 * C + c0, v[0]);
-      ld8(y + (pix0 + 1) * C + c0, v[1]);
-      ld8(y + (pix0 + W) * C + c0, v[2]);
-      ld8(y + (pix0 + W + 1) * C + c0, v[3]);
-      ld8(gout + (((size_t)n * Hp + hp) * Wp + wc) * C + c0, gg);
-      uint32_t o[4][4];
+    if (gb != cur_g) {
+      cur_g = gb;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int gc = gb * C + c0 + e;
-        const float sc = scale[gc], sf = shift[gc];
-        const float k1 = coef[gc * 3], kx = coef[gc * 3 + 1], k0 = coef[gc * 3 + 2];
-        float best = fmaxf(fmaf(v[0][e], sc, sf), 0.f);
+        sc[e] = scale[gc]; sf[e] = shift[gc];
+        k1[e] = coef[gc * 3]; kx[e] = coef[gc * 3 + 1]; k0[e] = coef[gc * 3 + 2];
+      }
+    }
+    __syncthreads();                          // the previous tile's reads are done
+    // ---- x rows y0-1 .. y0+TRW (zero outside the image) and dy per window x 8 channels
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int e = tid + 256 * i;
+      if (e < (TRW + 2) * XW) {
+        const int r = e / XW, c = e - r * XW, iy = y0 - 1 + r, ix = c - 1;
+        xr[e] = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) ? px[i] : f2bf(0.f);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TPT; ++i) {
+      const int t = tid + 256 * i;
+      if (t >= ntask) continue;
+      const int w = t / VQ, wc = w % Wp, wr = w / Wp;
+      float v[4][8], gg[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) unpack(py[i][k], v[k]);
+      unpack(pg[i], gg);
+      uint32_t o[4][4];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float best = fmaxf(fmaf(v[0][e], sc[e], sf[e]), 0.f);
         int a = 0;
 #pragma unroll
         for (int k = 1; k < 4; ++k) {
-          const float r = fmaxf(fmaf(v[k][e], sc, sf), 0.f);
+          const float r = fmaxf(fmaf(v[k][e], sc[e], sf[e]), 0.f);
           if (r > best) { best = r; a = k; }
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const float dz = (a == k && best > 0.f) ? gg[e] : 0.f;
-          const float d = fmaf(k1, dz, fmaf(kx, v[k][e], k0));
-          const uint32_t b = __builtin_bit_cast(uint16_t, f2bf(d));
-          if (e & 1) o[k][e >> 1] |= b << 16;
-          else o[k][e >> 1] = b;
+          const float d = fmaf(k1[e], dz, fmaf(kx[e], v[k][e], k0[e]));
+          const uint32_t bb = __builtin_bit_cast(uint16_t, f2bf(d));
+          if (e & 1) o[k][e >> 1] |= bb << 16;
+          else o[k][e >> 1] = bb;
         }
       }
       const int p0 = (2 * wr) * W + 2 * wc;
@@ -132,6 +170,7 @@ __global__ __launch_bounds__(256, 2) void c1w3_kernel(
       for (int k = 0; k < 4; ++k)
         *reinterpret_cast<u4*>(dys + pk[k] * DYS + c0) = u4{o[k][0], o[k][1], o[k][2], o[k][3]};
     }
+    if (ti + 1 < t1) load(ti + 1);            // in flight under this tile's im2col and MFMAs
     __syncthreads();                          // xr ready
     // ---- im2col: x9[p][tap] = x[p + (ky - 1, kx - 1)], taps 9..15 zero
     for (int p = tid; p < TP; p += 256) {
@@ -206,7 +245,8 @@ int avd_c1w3_slabs(int dt, int N, int Cin, int H, int W, int Cout, int K, int pa
   if (getenv("AVDINO_C1W3_OFF")) return 0;
   if (dt != AVD_BF16 || Cin != 1 || K != 3 || pad != 1) return 0;
   if (Cout != 16 && Cout != 32 && Cout != 64) return 0;
-  if (H % TRW || W % 2 || W > 128) return 0;
+  if (H % TRW || W % 2 || W > 128 || (TRW / 2) * (W / 2) * (Cout / 8) > 512 || (TRW + 2) * (W + 2) > 768)
+    return 0;
   if (c1w3_lds(Cout, W) > 80 * 1024) return 0;
   return grid_cap(std::min(N * (H / TRW), 2 * ncu_c1w3()));
 }
