@@ -169,6 +169,11 @@ int avd_gemm(int M, int N, int K, const float* A, long long sam, long long sak,
 int avd_cl_weight_elems(int Cout, int Cin, int K, int dgrad);
 int avd_cl_weight_layout(const float* w, void* wk, int dt, int Cout, int Cin, int K, int dgrad,
                          void* stream);
+/* n <= 16 layouts in one launch (a conv stack's per-step weights): HOST arrays of n entries,
+ * entry e = avd_cl_weight_layout(w[e], wk[e], dt, cout[e], cin[e], k[e], dgrad[e]). */
+int avd_cl_weight_layout_batch(int n, const float* const* w, void* const* wk, const int* cout,
+                               const int* cin, const int* k, const int* dgrad, int dt,
+                               void* stream);
 
 /* y = conv2d(x, w) + bias (stride 1, zero padding pad), x [N,H,W,Cin] -> y [N,Ho,Wo,Cout].
  * stats != NULL: BatchNorm partial (sum, sumsq) of the stored y values, [Cout][G][R][2] with

@@ -37,6 +37,7 @@ PROTOS = {
     "avd_gemm_ws_elems": [I, I, I, I],
     "avd_cl_weight_elems": [I, I, I, I],
     "avd_cl_weight_layout": [P, P, I, I, I, I, I, P],
+    "avd_cl_weight_layout_batch": [I, P, P, P, P, P, P, I, P],
     "avd_cl_stat_rows": [I, I, I, I, I, I, I],
     "avd_cl_conv_fwd": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "avd_cl_conv_dgrad": [P, P, P, I, I, I, I, I, I, I, I, P],

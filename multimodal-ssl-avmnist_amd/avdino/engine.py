@@ -71,7 +71,7 @@ class ConvBranch:
     def prepare(self, ws, store, tag, need_dgrad):
         """MFMA weight layouts for this step (the weights change every step): (bf16 forward
         rows, bf16 dgrad rows, (e4m3 rows, per-channel scales) for fp8 layers)."""
-        wts = []
+        wts, batch = [], []
         for i, (ci, co, k, _p) in enumerate(self.stack.convs):
             w = store[self.stack.conv_keys[i] + ".weight"]
             q = None
@@ -82,12 +82,14 @@ class ConvBranch:
                 wk = None
             else:
                 wk = ws.get(f"{tag}.wk{i}", ops.cl_weight_elems(co, ci, k, 0), self.act)
-                ops.cl_weight_layout(w, wk, 0)
+                batch.append((w, wk, 0))
             wd = None
             if need_dgrad and i > 0:
                 wd = ws.get(f"{tag}.wd{i}", ops.cl_weight_elems(co, ci, k, 1), self.act)
-                ops.cl_weight_layout(w, wd, 1)
+                batch.append((w, wd, 1))
             wts.append((wk, wd, q))
+        if batch:       # every layout of the stack in one launch
+            ops.cl_weight_layout_batch(batch)
         return wts
 
     def _conv_fwd(self, i, h, wt, bias, y, parts, N, B):

@@ -263,6 +263,27 @@ def cl_weight_layout(w, wk, dgrad):
     call("avd_cl_weight_layout", p(w), p(wk), dtcode(wk), Cout, Cin, K, int(dgrad), stream())
 
 
+def cl_weight_layout_batch(entries):
+    """entries: [(w f32 [Cout,Cin,K,K], wk, dgrad)] (<= 16, one dtype) -> one launch
+    (avd_cl_weight_layout_batch)."""
+    import ctypes as _ct
+    n = len(entries)
+    _need(0 < n <= 16, "weight layout batch size")
+    dt = entries[0][1].dtype
+    for w, wk, dg in entries:
+        Co, Ci, K, _ = w.shape
+        _need(w.dtype == torch.float32 and w.is_contiguous(), "layout batch w")
+        _need(wk.dtype == dt and wk.numel() >= cl_weight_elems(Co, Ci, K, dg), "layout batch wk")
+    PA, IA = _ct.c_void_p * n, _ct.c_int * n
+    ws = PA(*[w.data_ptr() for w, _, _ in entries])
+    wks = PA(*[wk.data_ptr() for _, wk, _ in entries])
+    co = IA(*[w.shape[0] for w, _, _ in entries])
+    ci = IA(*[w.shape[1] for w, _, _ in entries])
+    kk = IA(*[w.shape[2] for w, _, _ in entries])
+    dg = IA(*[int(d) for _, _, d in entries])
+    call("avd_cl_weight_layout_batch", n, ws, wks, co, ci, kk, dg, _DT[dt], stream())
+
+
 def cl_stat_rows(Ho, Wo, B, K, Cin, Cout, dtype):
     return lib.avd_cl_stat_rows(Ho, Wo, B, K, Cin, Cout, _DT[dtype])
 

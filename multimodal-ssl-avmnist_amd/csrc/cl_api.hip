@@ -5,6 +5,9 @@ int avd_cl_layout_rows_impl(int O);
 int avd_cl_stat_rows_impl(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt);
 int avd_cl_weight_layout_impl(const float* w, void* wk, int dt, int Cout, int Cin, int K,
                               int dgrad, hipStream_t st);
+int avd_cl_weight_layout_batch_impl(int n, const float* const* w, void* const* wk,
+                                    const int* cout, const int* cin, const int* k,
+                                    const int* dgrad, int dt, hipStream_t st);
 int avd_cl_conv_fwd_impl(const void* x, const void* wk, const float* bias, void* y, float* stats,
                          int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
                          hipStream_t st);
@@ -71,6 +74,15 @@ int avd_cl_weight_layout(const float* w, void* wk, int dt, int Cout, int Cin, in
   if (!w || !wk || !dt_ok(dt)) return AVD_ERR_ARG;
   if (Cout <= 0 || Cin <= 0 || K <= 0) return AVD_ERR_SHAPE;
   return avd_cl_weight_layout_impl(w, wk, dt, Cout, Cin, K, dgrad, avd_stream(stream));
+}
+
+int avd_cl_weight_layout_batch(int n, const float* const* w, void* const* wk, const int* cout,
+                               const int* cin, const int* k, const int* dgrad, int dt,
+                               void* stream) {
+  if (!w || !wk || !cout || !cin || !k || !dgrad || !dt_ok(dt)) return AVD_ERR_ARG;
+  for (int e = 0; e < n; ++e)
+    if (cout[e] <= 0 || cin[e] <= 0 || k[e] <= 0) return AVD_ERR_SHAPE;
+  return avd_cl_weight_layout_batch_impl(n, w, wk, cout, cin, k, dgrad, dt, avd_stream(stream));
 }
 
 int avd_c1w3_slabs(int dt, int N, int Cin, int H, int W, int Cout, int K, int pad);

@@ -377,6 +377,32 @@ __global__ void weight_layout_cl_kernel(const float* __restrict__ w, T* __restri
   io<T>::st(wk, i, v);
 }
 
+// Several layouts in one launch (blockIdx.y = entry): the per-step weight layouts of a conv stack
+constexpr int WLB_MAX = 16;
+struct WLBatch {
+  const float* w[WLB_MAX];
+  void* wk[WLB_MAX];
+  int cout[WLB_MAX], cin[WLB_MAX], kk[WLB_MAX], dgrad[WLB_MAX], rows[WLB_MAX], kpad[WLB_MAX];
+};
+
+template <typename T>
+__global__ void weight_layout_batch_kernel(WLBatch b) {
+  const int e = blockIdx.y;
+  const int dg = b.dgrad[e], Cout = b.cout[e], Cin = b.cin[e], KK = b.kk[e], Kpad = b.kpad[e];
+  const int O = dg ? Cin : Cout, C = dg ? Cout : Cin, n = b.rows[e] * Kpad;
+  const float* w = b.w[e];
+  T* wk = reinterpret_cast<T*>(b.wk[e]);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int o = i / Kpad, k = i % Kpad;
+    float v = 0.f;
+    if (o < O && k < KK * C) {
+      const int tap = k / C, c = k % C;
+      v = dg ? w[((size_t)c * Cin + o) * KK + (KK - 1 - tap)] : w[((size_t)o * Cin + c) * KK + tap];
+    }
+    io<T>::st(wk, i, v);
+  }
+}
+
 // ----------------------------------------------------------------------------- host plan
 struct Plan { int TH, TW, NS, GPW, NB, tilesX, tiles; };
 // widest output-channel block that may use 7 pixel groups per wave (AGPR budget / occupancy)
@@ -463,6 +489,32 @@ int avd_cl_stat_rows_impl(int Ho, int Wo, int B, int K, int Cin, int Cout, int d
   if (avd_c1p8_eligible(dt, Cin, Cout, K, Ho, Wo)) return avd_c1p8_stat_rows(Ho, B);
   const Plan p = plan_cl(Ho, Wo, B, K, pix_bytes(dt, Cin), Cin == 1, Cout);
   return p.NS ? (B / p.NS) * p.tiles * 4 : 0;   // one partial row per wave
+}
+
+int avd_cl_weight_layout_batch_impl(int n, const float* const* w, void* const* wk,
+                                    const int* cout, const int* cin, const int* k,
+                                    const int* dgrad, int dt, hipStream_t st) {
+  if (n <= 0 || n > WLB_MAX) return AVD_ERR_SHAPE;
+  WLBatch b{};
+  int most = 0;
+  for (int e = 0; e < n; ++e) {
+    if (!w[e] || !wk[e]) return AVD_ERR_ARG;
+    const int O = dgrad[e] ? cin[e] : cout[e], C = dgrad[e] ? cout[e] : cin[e];
+    b.w[e] = w[e];
+    b.wk[e] = wk[e];
+    b.cout[e] = cout[e];
+    b.cin[e] = cin[e];
+    b.kk[e] = k[e] * k[e];
+    b.dgrad[e] = dgrad[e];
+    b.kpad[e] = avd_cdiv(k[e] * k[e] * C, 32) * 32;
+    b.rows[e] = avd_cl_layout_rows_impl(O);
+    most = std::max(most, b.rows[e] * b.kpad[e]);
+  }
+  dim3 grid(std::min(avd_cdiv(most, 256), 256), n);
+  if (dt == AVD_BF16) weight_layout_batch_kernel<bf16><<<grid, 256, 0, st>>>(b);
+  else weight_layout_batch_kernel<float><<<grid, 256, 0, st>>>(b);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
 }
 
 int avd_cl_weight_layout_impl(const float* w, void* wk, int dt, int Cout, int Cin, int K,
