@@ -245,12 +245,16 @@ class ConvBranch:
     # registers (occupancy 2 -> 1) and is not hidden behind the MFMAs.  AVDINO_BNAPPLY_FUSED=1.
     BNAPPLY_FUSED = os.environ.get("AVDINO_BNAPPLY_FUSED", "0") == "1"
 
-    def backward(self, ws, store, ctx, dfeat):
-        """dfeat: f32 [N, F] gradient of the features; writes conv/BN parameter grads."""
+    def backward(self, ws, store, ctx, dfeat, wstream=None):
+        """dfeat: f32 [N, F] gradient of the features; writes conv/BN parameter grads.
+        wstream: a second stream for the mid layers' weight gradients (they only read dy and
+        the layer input, so they overlap the input-gradient chain); joined before returning."""
         N, G = ctx["N"], ctx["G"]
         B = N // G
         gout = dfeat
         nl = len(self.stack.convs)
+        main = torch.cuda.current_stream(dfeat.device) if wstream is not None else None
+        wdone = []
         for i in reversed(range(nl)):
             ci, co, k, pad = self.stack.convs[i]
             H, Ho, Hp = self.dims[i]
@@ -294,14 +298,26 @@ class ConvBranch:
                                           ci, H, H, co, k, pad)
                 gout = dx
                 continue
-            dy = ws.get("bwd_dy", N * Ho * Ho * co, self.act)
+            dy = ws.get(f"bwd_dy{i}" if wstream is not None else "bwd_dy", N * Ho * Ho * co, self.act)
             ops.cl_bn_bwd_apply(y, gout, mode, st[2], st[3], coef, dy, N, B, co, Ho, Ho)
-            ops.cl_conv_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
-            ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
+            if wstream is not None and i > 0:
+                wparts = ws.get(f"wgrad_parts{i}", nch * co * ci * k * k)
+                wstream.wait_stream(main)
+                with torch.cuda.stream(wstream):
+                    ops.cl_conv_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
+                    ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
+                    ev = torch.cuda.Event()
+                    ev.record(wstream)
+                wdone.append(ev)
+            else:
+                ops.cl_conv_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
+                ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
             if i > 0:
                 dx = ws.get("bwd_dx", N * H * H * ci, self.act)
                 ops.cl_conv_dgrad(dy, ctx["wts"][i][1], dx, N, ci, H, H, co, k, pad)
                 gout = dx
+        for ev in wdone:
+            main.wait_event(ev)
 
 
 # ============================================================================ dense heads
@@ -488,6 +504,9 @@ class MultiCentralEngine:
         # scratch (Workspace, split-K GEMM buffer), joined by events; concurrent=False keeps
         # everything on the caller's stream
         self.side = torch.cuda.Stream(store.device) if (concurrent and store.device.type == "cuda") else None
+        # the audio branch's mid-layer weight gradients on a third stream (AVDINO_WGRAD_SIDE=0: off)
+        self.wside = (torch.cuda.Stream(store.device) if (self.side is not None and
+                      os.environ.get("AVDINO_WGRAD_SIDE", "1") == "1") else None)
         self.tws = Workspace(store.device) if self.side is not None else self.ws
         self.iws = Workspace(store.device) if self.side is not None else self.ws
         self.grad_hook = grad_hook      # e.g. DDP all-reduce of store.grad (avdino.dist)
@@ -774,7 +793,7 @@ class MultiCentralEngine:
                        st.grad_of("student.audio_encoder.1.weight"),
                        st.grad_of("student.audio_encoder.1.bias"), dfa, N, dout_ld=2 * E, dout_off=E,
                        mode=self.gm)
-        self.aud.backward(ws, st, caud, dfa)
+        self.aud.backward(ws, st, caud, dfa, wstream=self.wside)
         self._join(i_done)
 
     def _graphable(self):
