@@ -450,7 +450,10 @@ int avd_cl_bn_bwd_rows_impl(int B, int C, int H, int W, int dt) {
   const int V = dt == AVD_BF16 ? 8 : 4;
   const long long nwin = (long long)B * (H / 2) * (W / 2);
   const int slots = 256 / std::max(1, C / V);
-  const long long r = (nwin + (long long)slots * 16 - 1) / ((long long)slots * 16);
+  // windows per slot (thread) of a partial row: long enough that the block's fixed reduction is
+  // amortised over several rounds of 4 in-flight windows (AVDINO_BWD_WPS overrides)
+  static const int wps = getenv("AVDINO_BWD_WPS") ? std::max(1, atoi(getenv("AVDINO_BWD_WPS"))) : 16;
+  const long long r = (nwin + (long long)slots * wps - 1) / ((long long)slots * wps);
   return (int)std::max(1ll, std::min(r, 4096ll));
 }
 
