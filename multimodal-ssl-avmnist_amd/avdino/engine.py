@@ -190,9 +190,13 @@ class ConvBranch:
     # stored-y forward whose BN -> ReLU -> pool recomputes y from x instead of reading the
     # 1.44 GB it just wrote (bit-identical y; r1_34: +0.5 %)
     RC_APPLY = os.environ.get("AVDINO_L1_RC_APPLY", "1") == "1"
+    # 3x3 first layers (the SimCLR / unimodal encoders): recompute passes c1r3_kernel, whose y
+    # is one MFMA per 16 channels x 16 pixels from the staged input tile
+    RECOMPUTE3 = os.environ.get("AVDINO_L1_RECOMPUTE3", "0") == "1"
 
     def _recompute_ok(self, N, B, ci, H, co, k, pad, need_dgrad=True):
-        return ((self.RECOMPUTE or (self.RC_NOGRAD and not need_dgrad)) and self.act == torch.bfloat16 and
+        rc = self.RECOMPUTE or (self.RECOMPUTE3 and k == 3) or (self.RC_NOGRAD and not need_dgrad)
+        return (rc and self.act == torch.bfloat16 and
                 ops.cl_c1_recompute_rows(ops.C1_STATS, self.act, N, B, ci, H, H, co, k, pad) > 0)
 
     def _first_layer_recompute_fwd(self, ws, store, tag, ctx, x, N, G, B, update_running):

@@ -111,9 +111,17 @@ int avd_cl_bn_bwd_apply_wgrad(const void* y, const void* gout, const float* scal
                                   avd_stream(stream));
 }
 
+int avd_c1r3_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad);
+int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, const float* scale,
+                    const float* shift, const float* mean, const float* invstd, const float* coef,
+                    const void* gz, void* z, float* out, int N, int B, int H, int W, int Cout,
+                    hipStream_t st);
+
 int avd_cl_c1_recompute_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cout,
                              int K, int pad) {
   if (pass < 0 || pass > 3 || B <= 0 || N % B) return 0;
+  // the 3x3 encoders' first layer (c1w3.hip)
+  if (const int r = avd_c1r3_rows(pass, dt, N, B, Cin, H, W, Cout, K, pad)) return r;
   if (!avd_c1p8_eligible(dt, Cin, Cout, K, H, W) || pad != 2 || W > 112) return 0;
   return avd_c1r_rows(pass, N, B, H);
 }
@@ -129,6 +137,9 @@ int avd_cl_c1_recompute(int pass, const void* x, const void* wk, const float* bi
   if ((need_bn && (!scale || !shift)) || (pass == 1 && !z) || (pass != 1 && !out) ||
       (need_g && !gz) || (pass == 2 && (!mean || !invstd)) || (pass == 3 && !coef))
     return AVD_ERR_ARG;
+  if (avd_c1r3_rows(pass, dt, N, B, Cin, H, W, Cout, K, pad))
+    return avd_c1r3_launch(pass, x, wk, bias, scale, shift, mean, invstd, coef, gz, z, out, N, B,
+                           H, W, Cout, avd_stream(stream));
   return avd_c1r_launch(pass, x, wk, bias, scale, shift, mean, invstd, coef, gz, z, out, N, B, H,
                         W, avd_stream(stream));
 }

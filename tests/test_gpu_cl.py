@@ -244,18 +244,21 @@ def test_cl_bn_bwd_apply_wgrad_fused_first_layer(ops, HN):
     assert rel(host(dw), dw64) < 1e-5
 
 
-@pytest.mark.parametrize("HN", [(112, 4), (48, 6)])
+@pytest.mark.parametrize("HN", [(112, 4, 8, 5, 2), (48, 6, 8, 5, 2),
+                                # the 3x3 encoders' first layer (c1r3_kernel, c1w3.hip)
+                                (112, 4, 32, 3, 1), (112, 6, 16, 3, 1), (56, 4, 64, 3, 1),
+                                (48, 6, 32, 3, 1), (8, 4, 16, 3, 1)])
 def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN):
     """avd_cl_c1_recompute (the audio conv1 without a stored conv output) against the stored-y
     kernels on the same bf16 operands: identical pooled output (bit-exact: same rounded y), and
     the statistics / BN-backward partials / weight gradient to fp32 summation order."""
-    H, N = HN
-    B, Cin, C, K, pad = N // 2, 1, 8, 5, 2
+    H, N, C, K, pad = HN
+    B, Cin = N // 2, 1
     G = N // B
     T = torch.bfloat16
-    g = np.random.default_rng(H + 1)
+    g = np.random.default_rng(H + C + K)
     x = bf(g.uniform(0, 1, (N, H, H, 1)))
-    w = bf(g.uniform(-1, 1, (C, 1, K, K)) / 5)
+    w = bf(g.uniform(-1, 1, (C, 1, K, K)) / K)
     b = g.uniform(-0.1, 0.1, C).astype(np.float32)
     tx, tb = dev(x, T), dev(b)
     wk = torch.empty(ops.cl_weight_elems(C, 1, K, 0), device="cuda", dtype=T)
@@ -266,6 +269,7 @@ def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN):
     st0 = torch.empty(C * G * R0 * 2, device="cuda")
     ops.cl_conv_fwd(tx, wk, tb, y, st0, N, B, 1, H, H, C, K, pad)
     R1 = ops.cl_c1_recompute_rows(ops.C1_STATS, T, N, B, 1, H, H, C, K, pad)
+    assert R1 > 0
     st1 = torch.empty(C * G * R1 * 2, device="cuda")
     ops.cl_c1_recompute(ops.C1_STATS, tx, wk, tb, N, B, 1, H, H, C, K, pad, out=st1)
     s0 = host(st0).reshape(C, G, R0, 2).sum(2)
