@@ -54,6 +54,7 @@ PROTOS = {
     "avd_cl_apply_wgrad_slabs": [I, I, I, I, I, I, I, I],
     "avd_cl_c1_recompute_rows": [I, I, I, I, I, I, I, I, I, I],
     "avd_cl_c1_recompute": [I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "avd_cl_c1_recompute_combine": [P, P, P, P, P, I, I, P],
     "avd_cl_bn_bwd_apply_wgrad": [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "avd_sum_rows": [P, I, I, L, P, I, P],
     "avd_sum_rows_chunks": [I, I],

@@ -192,7 +192,10 @@ class ConvBranch:
     RC_APPLY = os.environ.get("AVDINO_L1_RC_APPLY", "1") == "1"
     # 3x3 first layers (the SimCLR / unimodal encoders): recompute passes c1r3_kernel, whose y
     # is one MFMA per 16 channels x 16 pixels from the staged input tile
-    RECOMPUTE3 = os.environ.get("AVDINO_L1_RECOMPUTE3", "0") == "1"
+    RECOMPUTE3 = os.environ.get("AVDINO_L1_RECOMPUTE3", "1") == "1"
+    # their backward as one pass (avd_cl_c1_recompute pass 4) + a tiny combine: dW is linear in
+    # dy = k1 dz + kx y + k0, so the pass accumulates sum dz x9 and the Gram matrix of x9
+    RC_MOMENTS = os.environ.get("AVDINO_L1_RC_MOMENTS", "1") == "1"
 
     def _recompute_ok(self, N, B, ci, H, co, k, pad, need_dgrad=True):
         rc = self.RECOMPUTE or (self.RECOMPUTE3 and k == 3) or (self.RC_NOGRAD and not need_dgrad)
@@ -229,6 +232,21 @@ class ConvBranch:
         x, wk, st = ctx["x"][0], ctx["wts"][0][0], ctx["stats"][0]
         bk, ck = self.stack.bn_keys[0], self.stack.conv_keys[0]
         bias = store[ck + ".bias"]
+        R4 = ops.cl_c1_recompute_rows(ops.C1_REDUCE_MOMENTS, self.act, N, B, ci, H, H, co, k, pad)
+        if self.RC_MOMENTS and R4 > 0:
+            # one pass: BN-backward sums + the moments dW is linear in (3x3 layers)
+            mc = ops.c1_moment_cols(co)
+            parts = ws.get("bwd_parts_m", co * G * R4 * 2 + R4 * G * mc)
+            ops.cl_c1_recompute(ops.C1_REDUCE_MOMENTS, x, wk, bias, N, B, ci, H, H, co, k, pad,
+                                scale=st[2], shift=st[3], mean=st[0], invstd=st[1], gz=gout, out=parts)
+            coef = ws.get("bwd_coef", G * co * 3)
+            ops.bn_bwd_finalize(parts, G, R4, co, B * Ho * Ho, store[bk + ".weight"], st[0], st[1],
+                                coef, store.grad_of(bk + ".weight"), store.grad_of(bk + ".bias"),
+                                store.grad_of(ck + ".bias"))
+            mom = ws.get("c1_moments", G * mc)
+            ops.sum_rows(parts, R4, G * mc, mom, off=co * G * R4 * 2)
+            ops.cl_c1_recompute_combine(mom, coef, wk, bias, store.grad_of(ck + ".weight"), G, co)
+            return
         R = ops.cl_c1_recompute_rows(ops.C1_REDUCE, self.act, N, B, ci, H, H, co, k, pad)
         parts = ws.get("bwd_parts", co * G * R * 2)
         ops.cl_c1_recompute(ops.C1_REDUCE, x, wk, bias, N, B, ci, H, H, co, k, pad, scale=st[2],

@@ -474,7 +474,12 @@ def cl_bn_bwd_apply_wgrad(y, gout, scale, shift, coef, x, parts, N, B, Cin, H, W
                         p(parts), dtcode(y), N, B, Cin, H, W, Cout, K, pad, stream()))
 
 
-C1_STATS, C1_APPLY, C1_REDUCE, C1_WGRAD = 0, 1, 2, 3
+C1_STATS, C1_APPLY, C1_REDUCE, C1_WGRAD, C1_REDUCE_MOMENTS = 0, 1, 2, 3, 4
+
+
+def c1_moment_cols(Cout):
+    """Columns of one pass-4 moment row: sum dz x9 [Cout][9] + Gram rows [9][10]."""
+    return Cout * 9 + 90
 
 
 def cl_c1_recompute_rows(pas, dtype, N, B, Cin, H, W, Cout, K, pad):
@@ -490,19 +495,30 @@ def cl_c1_recompute(pas, x, wk, bias, N, B, Cin, H, W, Cout, K, pad, scale=None,
     G = N // B
     if pas in (C1_STATS, C1_REDUCE):
         _need(out is not None and out.numel() >= Cout * G * rows * 2, "c1 recompute rows")
+    if pas == C1_REDUCE_MOMENTS:
+        _need(out is not None and out.numel() >= G * rows * (Cout * 2 + c1_moment_cols(Cout)),
+              "c1 recompute rows + moments")
+        _need(mean is not None and invstd is not None, "c1 recompute mean/invstd")
     if pas == C1_WGRAD:
         _need(out is not None and out.numel() >= rows * Cout * Cin * K * K, "c1 recompute slabs")
     npool = N * (H // 2) * (W // 2) * Cout
     if pas == C1_APPLY:
         _need(z is not None and z.numel() == npool and z.dtype == x.dtype, "c1 recompute z")
-    if pas in (C1_REDUCE, C1_WGRAD):
+    if pas in (C1_REDUCE, C1_WGRAD, C1_REDUCE_MOMENTS):
         _need(gz is not None and gz.numel() == npool and gz.dtype == x.dtype, "c1 recompute gz")
     nb = x.numel() * x.element_size() + (npool * 2 if pas != C1_STATS else 0)
-    name = ["stats", "apply", "reduce", "wgrad"][pas]
+    name = ["stats", "apply", "reduce", "wgrad", "reduce_moments"][pas]
     _timed(f"cl_c1_recompute_{name}[{N}x{H}x{W}x{Cin}->{Cout} k{K}]", nb, 2 * N * H * W * Cout * K * K,
            lambda: call("avd_cl_c1_recompute", pas, p(x), p(wk), p(bias), p(scale), p(shift), p(mean),
                         p(invstd), p(coef), p(gz), p(z), p(out), dtcode(x), N, B, Cin, H, W, Cout, K,
                         pad, stream()))
+
+
+def cl_c1_recompute_combine(moments, coef, wk, bias, dw, G, Cout):
+    """dW of the 3x3 first layer from pass 4's row-summed moments (avd_cl_c1_recompute_combine)."""
+    _need(moments.numel() >= G * c1_moment_cols(Cout) and coef.numel() >= G * Cout * 3 and
+          dw.numel() >= Cout * 9, "c1 recompute combine shape")
+    call("avd_cl_c1_recompute_combine", p(moments), p(coef), p(wk), p(bias), p(dw), G, Cout, stream())
 
 
 _SUM_WS = {}

@@ -271,24 +271,33 @@ int avd_c1w3_apply_wgrad(const void* y, const void* gout, const float* scale, co
 
 // ============================================================================ recompute passes
 // The same first layer WITHOUT a stored conv output (avd_cl_c1_recompute for 3x3 / Cin 1):
-// every pass rebuilds y = bf16(conv(x) + b) for a tile from the staged input (x rows -> the
-// im2col tile x9 in LDS -> one v_mfma_f32_16x16x32_bf16 per 16 channels x 16 pixels with the
-// weight rows as A, the same code in every pass, so y is bit-identical across passes) and then
+// every pass rebuilds y = bf16(conv(x) + b) for a tile of TRW rows from the staged input rows
+// (one v_mfma_f32_16x16x32_bf16 per 16 channels x 16 pixels, weights as A, k = tap as in the
+// stored-y forward, so y is bit-identical to it and across passes) and then
 //   pass 0: BN partial sums of y (per-block running sums, rows [C][G][4 * grid][2]);
 //   pass 1: z = maxpool2(relu(y * scale + shift)) NHWC bf16;
 //   pass 2: BN-backward partial sums (sum dz, sum dz * xhat) like avd_cl_bn_bwd_reduce;
-//   pass 3: dy in LDS and the weight gradient, as c1w3_kernel.
+//   pass 3: dy in LDS and the weight gradient, as c1w3_kernel (plus the im2col tile x9).
 // A 16-pixel MFMA column group is a 2-row x 8-column patch (W % 8 == 0), so a pooling window
 // is the lanes {n, n^1, n^8, n^9} of a 16-lane row: DPP quad_perm / row_ror:8 exchanges.
+// The next tile's input rows (and pooled gradient, passes 2-3) are register-prefetched into a
+// second LDS buffer while the current tile computes: one barrier per tile (two in pass 3).
 namespace {
 
 template <int CTRL>
-__device__ __forceinline__ float dppf(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+__device__ __forceinline__ int dppi(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
 }
+typedef __attribute__((ext_vector_type(2))) float f2;
+typedef __attribute__((ext_vector_type(2))) short s2v;
+
+constexpr int RXO = 8;                          // xr: column ix at RXO + ix, zero pads both sides
+
+// blocks per CU (register budget: 512 / (4 x bpc) VGPRs per lane, no spills)
+__host__ __device__ constexpr int c1r3_bpc(int P, int C) { return (P >= 3 || (P == 2 && C == 64)) ? 2 : (P == 2 || C == 64) ? 3 : 4; }
 
 template <int P, int C>
-__global__ __launch_bounds__(256, 2) void c1r3_kernel(
+__global__ __launch_bounds__(256, c1r3_bpc(P, C)) void c1r3_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ wk, const float* __restrict__ bias,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -296,48 +305,120 @@ __global__ __launch_bounds__(256, 2) void c1r3_kernel(
     float* __restrict__ out, int N, int B, int H, int W) {
   constexpr int NT = C / 16;
   constexpr int DYS = C == 16 ? 16 : C + 16;
+  constexpr bool GZ = P >= 2;
+  constexpr bool RED = P == 2 || P == 4;            // BN-backward partial sums
+  constexpr bool WG = P >= 3;                       // im2col tile + weight-gradient MFMAs
   extern __shared__ __attribute__((aligned(16))) bf16 sm[];
   const int TP = TRW * W;
   const int KST = (TP + 31) / 32, TPP = KST * 32;
-  bf16* x9 = sm;                              // [TPP][XS9]
-  bf16* xr = x9 + TPP * XS9;                  // [TRW + 2][W + 2]
-  bf16* dys = xr + (((TRW + 2) * (W + 2) + 7) & ~7);   // [TPP][DYS] (pass 3)
-  const int XW = W + 2;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int g = lane >> 4, r16 = lane & 15, q4 = r16 >> 2, p4 = r16 & 3;
+  const int XS = W + 2 * RXO;                       // xr row stride
+  const int XB = (TRW + 2) * XS;                    // one xr buffer
   const int Hp = H / 2, Wp = W / 2;
+  const int GB = (TRW / 2) * Wp * C;                // one gz buffer (a tile's pooled gradient)
+  bf16* xr = sm;                                    // [2][TRW + 2][XS]
+  bf16* gzs = xr + 2 * XB;                          // [2][GB]
+  bf16* x9 = gzs + (GZ ? 2 * GB : 0);               // [TPP][XS9] (pass 3)
+  bf16* dys = x9 + TPP * XS9;                       // [TPP][DYS] (pass 3)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15, q4 = r16 >> 2, p4 = r16 & 3;
   const int tps = H / TRW, ntiles = N * tps, G = N / B, tilesPG = ntiles / G;
   const int per = ntiles / (int)gridDim.x, extra = ntiles % (int)gridDim.x;
   const int t0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
   const int t1 = t0 + per + ((int)blockIdx.x < extra ? 1 : 0);
-  const int ngroups16 = (TRW / 2) * (W / 8);  // 16-pixel column groups per tile
+  const int ngroups16 = (TRW / 2) * (W / 8);        // 16-pixel column groups per tile
+  // a 16-pixel column group is 2 rows x 8 columns: lane r16 -> pixel (r16 >> 3, r16 & 7)
+  const int plane = (r16 >> 3) * W + (r16 & 7);                 // pixel within the group's rows
+  const int xlane = (r16 >> 3) * (W + 2 * RXO) + (r16 & 7) + RXO - 1;
+  const int mn = r16 & 9;                                       // position in the 2x2 window
+  const int e1 = mn & 1, e8 = mn >> 3;                          // earlier-partner tie breaks
+  const int wlane = ((r16 & 7) >> 1) * C + 4 * g;               // window column, channel quad
 
-  // weight rows (A): lane holds w[16 t + r16][8 g .. 8 g + 7] (taps >= 9 are zero rows of wk)
+  // weight rows (A): lane holds w[16 t + r16][8 g .. 8 g + 7] (taps >= 9 are zero in wk)
   bf16x8 aw[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) aw[t] = *reinterpret_cast<const bf16x8*>(wk + (16 * t + r16) * 32 + 8 * g);
-  float bv[NT][4];
+  f2 bv2[NT][2];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bv[t][i] = bias ? bias[16 * t + 4 * g + i] : 0.f;
+    for (int h = 0; h < 2; ++h)
+      bv2[t][h] = bias ? f2{bias[16 * t + 4 * g + 2 * h], bias[16 * t + 4 * g + 2 * h + 1]} : f2{0.f, 0.f};
 
-  // per-block running sums (passes 0, 2): rows blockIdx*4 + wave of R = 4 * grid per group
+  // ---- staging: input rows y0-1 .. y0+TRW (16-byte vectors, one per thread) and gz
+  const int cpr = W / 8, nxv = (TRW + 2) * cpr;
+  const int xrow = tid / cpr, xcol = tid - xrow * cpr;
+  u4 xv = u4{0u, 0u, 0u, 0u};
+  u4 gv4[NT];
+  auto load = [&](int tl) {
+    const int n = tl / tps, y0 = (tl - n * tps) * TRW;
+    const int iy = y0 - 1 + xrow;
+    if (tid < nxv)
+      xv = (unsigned)iy < (unsigned)H
+               ? *reinterpret_cast<const u4*>(x + ((size_t)n * H + iy) * W + 8 * xcol)
+               : u4{0u, 0u, 0u, 0u};
+    if constexpr (GZ) {
+      const bf16* gb = gz + ((size_t)n * Hp + y0 / 2) * Wp * C;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int e = tid + 256 * j;
+        if (8 * e < GB) gv4[j] = *reinterpret_cast<const u4*>(gb + 8 * e);
+      }
+    }
+  };
+  auto put = [&](int buf) {
+    if (tid < nxv) *reinterpret_cast<u4*>(xr + buf * XB + xrow * XS + RXO + 8 * xcol) = xv;
+    if constexpr (GZ) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int e = tid + 256 * j;
+        if (8 * e < GB) *reinterpret_cast<u4*>(gzs + buf * GB + 8 * e) = gv4[j];
+      }
+    }
+  };
+
+  // per-block running sums (passes 0, 2, 4): rows blockIdx*4 + wave of R = 4 * grid per group
   float rs[NT][4], rq[NT][4];
+  f2 rs2[NT][2], rq2[NT][2];                        // pass 0 keeps its sums packed
   int cur_g = -1;
   const int R = 4 * (int)gridDim.x, srow = blockIdx.x * 4 + wave;
   auto zero_run = [&]() {
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int t = 0; t < NT; ++t) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) { rs[t][i] = 0.f; rq[t][i] = 0.f; }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) { rs2[t][h] = f2{0.f, 0.f}; rq2[t][h] = f2{0.f, 0.f}; }
+    }
   };
+  f4 acc3[NT], gacc;
+  const int WSZ = C * 9 + 90;                       // pass 4 moments per (row, group)
+  float* wmo = out + (size_t)C * G * R * 2;         // pass 4: [R][G][WSZ] after the sums
   auto flush = [&](int gp) {
+    if constexpr (P == 4) {
+      // this wave's moments of group gp: sum dz x9 [C][9], then the Gram rows of x9 [9][10]
+      // (column 9 is the ones tap: sum x9)
+      float* o = wmo + ((size_t)srow * G + gp) * WSZ;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (r16 < 9) o[(16 * t + 4 * g + i) * 9 + r16] = acc3[t][i];
+          acc3[t][i] = 0.f;
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (4 * g + i < 9 && r16 < 10) o[C * 9 + (4 * g + i) * 10 + r16] = gacc[i];
+        gacc[i] = 0.f;
+      }
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float a = row16_sum(rs[t][i]), b = row16_sum(rq[t][i]);
+        const float sa = P == 0 ? rs2[t][i >> 1][i & 1] : rs[t][i];
+        const float sb = P == 0 ? rq2[t][i >> 1][i & 1] : rq[t][i];
+        const float a = row16_sum(sa), b = row16_sum(sb);
         if (r16 == 0)
           *reinterpret_cast<float2*>(out + (((size_t)(16 * t + 4 * g + i) * G + gp) * R + srow) * 2) =
               make_float2(a, b);
@@ -345,21 +426,29 @@ __global__ __launch_bounds__(256, 2) void c1r3_kernel(
   };
   zero_run();
   // BN coefficients of the current group (passes 1-3): channels 16 t + 4 g + i
-  float sc[NT][4], sf[NT][4], mu[NT][4], is[NT][4], k1[NT][4], kx[NT][4], k0[NT][4];
+  f2 sc2[NT][2], sf2[NT][2];
+  float c2[NT][4], c3[NT][4], c4[NT][4];
   int cg = -1;
-  f4 acc3[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc3[t] = f4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (P == 3) {
+  gacc = f4{0.f, 0.f, 0.f, 0.f};
+
+  // zero both xr buffers (pads stay zero) and the padding pixels of the im2col / dy tiles
+  for (int i = tid; i < 2 * XB / 8; i += 256) reinterpret_cast<u4*>(xr)[i] = u4{0u, 0u, 0u, 0u};
+  if constexpr (WG) {
     for (int i = TP * (DYS / 8) + tid; i < TPP * (DYS / 8); i += 256)
       *reinterpret_cast<u4*>(dys + (size_t)i * 8) = u4{0u, 0u, 0u, 0u};
+    for (int i = TP * (XS9 / 8) + tid; i < TPP * (XS9 / 8); i += 256)
+      *reinterpret_cast<u4*>(x9 + (size_t)i * 8) = u4{0u, 0u, 0u, 0u};
   }
-  for (int i = TP * (XS9 / 8) + tid; i < TPP * (XS9 / 8); i += 256)
-    *reinterpret_cast<u4*>(x9 + (size_t)i * 8) = u4{0u, 0u, 0u, 0u};
+  if (t0 < t1) load(t0);
+  __syncthreads();
+  if (t0 < t1) put(t0 & 1);
+  if (t0 + 1 < t1) load(t0 + 1);
 
   for (int ti = t0; ti < t1; ++ti) {
-    const int n = ti / tps, y0 = (ti - n * tps) * TRW, gb = n / B;
-    if constexpr (P == 0 || P == 2) {
+    const int n = ti / tps, y0 = (ti - n * tps) * TRW, gb = n / B, buf = ti & 1;
+    if constexpr (P == 0 || RED) {
       const int gi = ti / tilesPG;
       if (gi != cur_g) {
         if (cur_g >= 0) flush(cur_g);
@@ -375,110 +464,128 @@ __global__ __launch_bounds__(256, 2) void c1r3_kernel(
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int gc = gb * C + 16 * t + 4 * g + i;
-            sc[t][i] = scale[gc]; sf[t][i] = shift[gc];
-            if constexpr (P == 2) { mu[t][i] = mean[gc]; is[t][i] = invstd[gc]; }
-            if constexpr (P == 3) { k1[t][i] = coef[gc * 3]; kx[t][i] = coef[gc * 3 + 1]; k0[t][i] = coef[gc * 3 + 2]; }
+            sc2[t][i >> 1][i & 1] = scale[gc]; sf2[t][i >> 1][i & 1] = shift[gc];
+            if constexpr (RED) { c2[t][i] = mean[gc]; c3[t][i] = invstd[gc]; }
+            if constexpr (P == 3) { c2[t][i] = coef[gc * 3]; c3[t][i] = coef[gc * 3 + 1]; c4[t][i] = coef[gc * 3 + 2]; }
           }
       }
     }
-    __syncthreads();
-    for (int i = tid; i < (TRW + 2) * XW; i += 256) {
-      const int r = i / XW, c = i - r * XW, iy = y0 - 1 + r, ix = c - 1;
-      xr[i] = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-                  ? x[((size_t)n * H + iy) * W + ix] : f2bf(0.f);
-    }
-    __syncthreads();
-    for (int p = tid; p < TP; p += 256) {
-      const int r = p / W, c = p - r * W;
-      uint32_t w8[8];
+    __syncthreads();                    // buffer `buf` complete; the other one and x9/dys free
+    if (ti + 1 < t1) put(buf ^ 1);
+    if (ti + 2 < t1) load(ti + 2);      // in flight under this tile's work
+    const bf16* xb = xr + buf * XB;
+    if constexpr (WG) {
+      // im2col x9[p][tap] for the weight-gradient MFMAs (taps 9..15 zero; pass 4: tap 9 = 1)
+      for (int p = tid; p < TP; p += 256) {
+        const int r = p / W, c = p - r * W;
+        uint32_t w8[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) w8[k] = 0u;
+        for (int k = 0; k < 8; ++k) w8[k] = 0u;
+        if constexpr (P == 4) w8[4] = 0x3F800000u;   // bf16 1.0 at tap 9
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const uint32_t b = __builtin_bit_cast(uint16_t, xr[(r + t / 3) * XW + c + t % 3]);
-        w8[t >> 1] |= (t & 1) ? b << 16 : b;
+        for (int t = 0; t < 9; ++t) {
+          const uint32_t b = __builtin_bit_cast(uint16_t, xb[(r + t / 3) * XS + RXO - 1 + c + t % 3]);
+          w8[t >> 1] |= (t & 1) ? b << 16 : b;
+        }
+        *reinterpret_cast<u4*>(x9 + p * XS9) = u4{w8[0], w8[1], w8[2], w8[3]};
+        *reinterpret_cast<u4*>(x9 + p * XS9 + 8) = u4{w8[4], w8[5], w8[6], w8[7]};
       }
-      *reinterpret_cast<u4*>(x9 + p * XS9) = u4{w8[0], w8[1], w8[2], w8[3]};
-      *reinterpret_cast<u4*>(x9 + p * XS9 + 8) = u4{w8[4], w8[5], w8[6], w8[7]};
     }
-    __syncthreads();
-    // ---- y for the wave's column groups, pass epilogues
+    // ---- y for the wave's column groups, straight from the staged rows; pass epilogues
+    const bf16* gzt = gzs + buf * GB;
+    const size_t zt = ((size_t)n * Hp + y0 / 2) * Wp * C;            // tile's first pooled row
     for (int q = wave; q < ngroups16; q += 4) {
-      const int gr = q / (W / 8), gc8 = q - gr * (W / 8);
-      const int prow = 2 * gr + (r16 >> 3), pcol = 8 * gc8 + (r16 & 7);   // pixel of this lane
-      const int p = prow * W + pcol;
-      const bf16x8 bx = g < 2 ? *reinterpret_cast<const bf16x8*>(x9 + p * XS9 + 8 * g)
-                              : bf16x8{};
-      float yv[NT][4];
+      const int gr = q / (W / 8), gc8 = q - gr * (W / 8);              // wave-uniform
+      const bf16* xp = xb + 2 * gr * XS + 8 * gc8 + xlane;
+      typedef __attribute__((ext_vector_type(8))) unsigned short us8;   // raw bf16 bits
+      us8 bs = us8{};
+      if (g == 0) {
+        bs[0] = xp[0]; bs[1] = xp[1]; bs[2] = xp[2];
+        bs[3] = xp[XS]; bs[4] = xp[XS + 1]; bs[5] = xp[XS + 2];
+        bs[6] = xp[2 * XS]; bs[7] = xp[2 * XS + 1];
+      } else if (g == 1) {
+        bs[0] = xp[2 * XS + 2];
+      }
+      const bf16x8 bx = __builtin_bit_cast(bf16x8, bs);
+      const int wg = (gr * Wp + 4 * gc8) * C + wlane;                  // window (lane part in wlane)
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const f4 a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[t], bx, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[t], bx, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        // y = bf16(acc + b) for the lane's 4 channels, as two packed pairs
+        f2 y2[2];
+        uint32_t yb[2];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) yv[t][i] = bf2f(f2bf(a[i] + bv[t][i]));
-      }
-      if constexpr (P == 0) {
+        for (int h = 0; h < 2; ++h) {
+          const f2 s2 = f2{acc[2 * h], acc[2 * h + 1]} + bv2[t][h];
+          yb[h] = pack_bf16x2(s2.x, s2.y);
+          y2[h] = f2{__uint_as_float(yb[h] << 16), __uint_as_float(yb[h] & 0xffff0000u)};
+        }
+        if constexpr (P == 0) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            rs[t][i] += yv[t][i];
-            rq[t][i] = fmaf(yv[t][i], yv[t][i], rq[t][i]);
+          for (int h = 0; h < 2; ++h) {
+            rs2[t][h] += y2[h];
+            rq2[t][h] = __builtin_elementwise_fma(y2[h], y2[h], rq2[t][h]);
           }
-      } else {
-        // window = lanes {L, L^1, L^8, L^9}, L = r16 & ~9; k order (0,0),(0,1),(1,0),(1,1)
-        const int mn = r16 & 9;
-        const int wy = y0 / 2 + gr, wx = 4 * gc8 + ((r16 & 7) >> 1);
-        const size_t wpix = ((size_t)n * Hp + wy) * Wp + wx;
+        } else if constexpr (P == 1) {
+          // relu(bn(y)) rounded to bf16 (monotone: the max of the rounded values is the rounded
+          // max), window max over lanes ^1 then ^8 on packed non-negative bf16 as int16
+          uint32_t m[2];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          float gv[4] = {0.f, 0.f, 0.f, 0.f};
-          if constexpr (P >= 2) {
-            const uint2 w2 = *reinterpret_cast<const uint2*>(gz + wpix * C + 16 * t + 4 * g);
-            gv[0] = __uint_as_float(w2.x << 16); gv[1] = __uint_as_float(w2.x & 0xffff0000u);
-            gv[2] = __uint_as_float(w2.y << 16); gv[3] = __uint_as_float(w2.y & 0xffff0000u);
+          for (int h = 0; h < 2; ++h) {
+            const f2 v = __builtin_elementwise_fma(y2[h], sc2[t][h], sf2[t][h]);
+            s2v r = __builtin_elementwise_max(__builtin_bit_cast(s2v, pack_bf16x2(v.x, v.y)), s2v{0, 0});
+            r = __builtin_elementwise_max(r, __builtin_bit_cast(s2v, dppi<0xB1>(__builtin_bit_cast(int, r))));
+            r = __builtin_elementwise_max(r, __builtin_bit_cast(s2v, dppi<0x128>(__builtin_bit_cast(int, r))));
+            m[h] = __builtin_bit_cast(uint32_t, r);
           }
-          float zo[4];
+          if (mn == 0)
+            *reinterpret_cast<uint2*>(z + zt + wg + 16 * t) = make_uint2(m[0], m[1]);
+        } else {
+          // first argmax of the window (k order (0,0),(0,1),(1,0),(1,1); lane L^m holds
+          // k = 2 (m >> 3) + (m & 1)) on bn(y) as signed ints: ordered like the floats wherever
+          // one side is > 0, and only a positive maximum carries the gradient.  The lane wins
+          // iff it beats its earlier partners strictly and its later ones or ties:
+          // v > u  <=>  v >= u + 1 (ints), the +1 only toward earlier partners.
+          const uint2 gw = *reinterpret_cast<const uint2*>(gzt + wg + 16 * t);
+          const float gg[4] = {__uint_as_float(gw.x << 16), __uint_as_float(gw.x & 0xffff0000u),
+                               __uint_as_float(gw.y << 16), __uint_as_float(gw.y & 0xffff0000u)};
+          float dz[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float zz = fmaxf(fmaf(yv[t][i], sc[t][i], sf[t][i]), 0.f);
-            const float z1 = dppf<0xB1>(zz), z8 = dppf<0x128>(zz), z9 = dppf<0x128>(z1);
-            if constexpr (P == 1) {
-              zo[i] = fmaxf(fmaxf(zz, z1), fmaxf(z8, z9));
-            } else {
-              // the window's values in k order: lane L^m holds k = (m >> 3) * 2 + (m & 1)
-              float wv[4];
-              wv[0] = mn == 0 ? zz : mn == 1 ? z1 : mn == 8 ? z8 : z9;   // lane L
-              wv[1] = mn == 1 ? zz : mn == 0 ? z1 : mn == 9 ? z8 : z9;   // L^1
-              wv[2] = mn == 8 ? zz : mn == 9 ? z1 : mn == 0 ? z8 : z9;   // L^8
-              wv[3] = mn == 9 ? zz : mn == 8 ? z1 : mn == 1 ? z8 : z9;   // L^9
-              float best = wv[0];
-              int a = 0;
+          for (int h = 0; h < 2; ++h) {
+            const f2 v = __builtin_elementwise_fma(y2[h], sc2[t][h], sf2[t][h]);
 #pragma unroll
-              for (int k = 1; k < 4; ++k)
-                if (wv[k] > best) { best = wv[k]; a = k; }
-              const int kn = (mn >> 3) * 2 + (mn & 1);
-              const float dz = (a == kn && best > 0.f) ? gv[i] : 0.f;
-              if constexpr (P == 2) {
-                const float xh = (yv[t][i] - mu[t][i]) * is[t][i];
-                rs[t][i] += dz;
-                rq[t][i] = fmaf(dz, xh, rq[t][i]);
-              } else {
-                zo[i] = fmaf(k1[t][i], dz, fmaf(kx[t][i], yv[t][i], k0[t][i]));   // dy
-              }
+            for (int e = 0; e < 2; ++e) {
+              const int vi = __float_as_int(v[e]);
+              const int u1 = dppi<0xB1>(vi) + e1, u8 = dppi<0x128>(vi) + e8,
+                        u9 = dppi<0x128>(dppi<0xB1>(vi)) + e8;
+              const int thr = max(max(u1, u8), max(u9, 1));
+              dz[2 * h + e] = vi >= thr ? gg[2 * h + e] : 0.f;
             }
           }
-          if constexpr (P == 1) {
-            if ((r16 & 9) == 0)
-              *reinterpret_cast<uint2*>(z + wpix * C + 16 * t + 4 * g) =
-                  make_uint2(pack_bf16x2(zo[0], zo[1]), pack_bf16x2(zo[2], zo[3]));
+          if constexpr (RED) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float yy = y2[i >> 1][i & 1];
+              const float xh = (yy - c2[t][i]) * c3[t][i];
+              rs[t][i] += dz[i];
+              rq[t][i] = fmaf(dz[i], xh, rq[t][i]);
+            }
+          }
+          if constexpr (P == 4) {     // dz (exact in bf16: a pooled gradient or zero)
+            *reinterpret_cast<uint2*>(dys + (2 * gr * W + 8 * gc8 + plane) * DYS + 16 * t + 4 * g) =
+                make_uint2(pack_bf16x2(dz[0], dz[1]), pack_bf16x2(dz[2], dz[3]));
           } else if constexpr (P == 3) {
-            *reinterpret_cast<uint2*>(dys + p * DYS + 16 * t + 4 * g) =
-                make_uint2(pack_bf16x2(zo[0], zo[1]), pack_bf16x2(zo[2], zo[3]));
+            float d[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              d[i] = fmaf(c2[t][i], dz[i], fmaf(c3[t][i], y2[i >> 1][i & 1], c4[t][i]));   // dy
+            *reinterpret_cast<uint2*>(dys + (2 * gr * W + 8 * gc8 + plane) * DYS + 16 * t + 4 * g) =
+                make_uint2(pack_bf16x2(d[0], d[1]), pack_bf16x2(d[2], d[3]));
           }
         }
       }
     }
-    if constexpr (P == 3) {
+    if constexpr (WG) {
       __syncthreads();
       for (int ks = wave; ks < KST; ks += 4) {
         const int P0 = 32 * ks;
@@ -489,11 +596,13 @@ __global__ __launch_bounds__(256, 2) void c1r3_kernel(
           const bf16x8 av = fr8(trd(dys + pa * DYS + 16 * t + 4 * p4), trd(dys + pb * DYS + 16 * t + 4 * p4));
           acc3[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bvv, acc3[t], 0, 0, 0);
         }
+        // the same fragment is the A operand of the x9 Gram matrix (rows: taps, k: pixels)
+        if constexpr (P == 4) gacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bvv, bvv, gacc, 0, 0, 0);
       }
     }
   }
 
-  if constexpr (P == 0 || P == 2) {
+  if constexpr (P == 0 || RED) {
     if (cur_g >= 0) flush(cur_g);
     const int first = t0 < t1 ? t0 / tilesPG : 0, last = t0 < t1 ? (t1 - 1) / tilesPG : -1;
     zero_run();
@@ -519,18 +628,45 @@ __global__ __launch_bounds__(256, 2) void c1r3_kernel(
   }
 }
 
-size_t c1r3_lds(int C, int W) {
-  const int DYS = C == 16 ? 16 : C + 16;
-  const size_t tpp = (size_t)(TRW * W + 31) / 32 * 32;
-  const size_t xrw = ((size_t)(TRW + 2) * (W + 2) + 7) & ~(size_t)7;
-  const size_t a = (tpp * XS9 + xrw + tpp * DYS) * 2;
-  return std::max(a, (size_t)4 * C * 16 * 4);
+size_t c1r3_lds(int P, int C, int W) {
+  const size_t XB = (size_t)(TRW + 2) * (W + 2 * RXO);
+  const size_t GB = P >= 2 ? (size_t)(TRW / 2) * (W / 2) * C : 0;
+  size_t e = 2 * XB + 2 * GB;
+  if (P >= 3) {
+    const int DYS = C == 16 ? 16 : C + 16;
+    const size_t tpp = (size_t)(TRW * W + 31) / 32 * 32;
+    e += tpp * (XS9 + DYS);
+  }
+  return std::max(e * 2, P == 3 ? (size_t)4 * C * 16 * 4 : (size_t)0);
 }
 
-int c1r3_grid(int N, int H) {
-  (void)N;
-  (void)H;
-  return grid_cap(2 * ncu_c1w3());
+int c1r3_grid(int P, int C) { return grid_cap(c1r3_bpc(P, C) * ncu_c1w3()); }
+
+// dW of pass 4 from the row-summed moments m [G][C * 9 + 90] and the BN-backward coefficients:
+//   dW[c][t] = sum_g k1 sum(dz x9_t) + kx sum(y x9_t) + k0 sum(x9_t),
+//   sum(y x9_t) = sum_t' w[c][t'] Gram[t'][t] + b[c] sum(x9_t)   (y = w . x9 + b)
+__global__ void c1r3_combine_kernel(const float* __restrict__ m, const float* __restrict__ coef,
+                                    const bf16* __restrict__ wk, const float* __restrict__ bias,
+                                    float* __restrict__ dw, int G, int C) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= C * 9) return;
+  const int c = e / 9, t = e - c * 9, WSZ = C * 9 + 90;
+  float wr[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) wr[k] = bf2f(wk[c * 32 + k]);
+  const float b = bias ? bias[c] : 0.f;
+  float acc = 0.f;
+  for (int g = 0; g < G; ++g) {
+    const float* mg = m + (size_t)g * WSZ;
+    const float* gram = mg + C * 9;
+    const float sx = gram[t * 10 + 9];
+    float sy = b * sx;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) sy = fmaf(wr[k], gram[k * 10 + t], sy);
+    const float* k3 = coef + ((size_t)g * C + c) * 3;
+    acc += k3[0] * mg[e] + k3[1] * sy + k3[2] * sx;
+  }
+  dw[e] = acc;
 }
 
 }  // namespace
@@ -542,32 +678,35 @@ int avd_c1r3_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cou
   if (getenv("AVDINO_C1R3_OFF")) return 0;
   if (dt != AVD_BF16 || Cin != 1 || K != 3 || pad != 1 || B <= 0 || N % B) return 0;
   if (Cout != 16 && Cout != 32 && Cout != 64) return 0;
-  if (H % TRW || W % 8 || W > 128) return 0;
-  if (c1r3_lds(Cout, W) > 80 * 1024) return 0;
-  const int grid = c1r3_grid(N, H);
-  switch (pass) {
-    case 0: case 2: return 4 * grid;
-    case 1: return 1;
-    case 3: return grid;
-    default: return 0;
-  }
+  if (H % TRW || W % 8 || W > 128 || pass < 0 || pass > 4) return 0;
+  if (c1r3_lds(3, Cout, W) > 80 * 1024) return 0;     // every pass served, or none
+  const int grid = c1r3_grid(pass, Cout);
+  return pass == 1 ? 1 : pass == 3 ? grid : 4 * grid;   // pass 4: rows R of both its outputs
 }
 
 int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, const float* scale,
                     const float* shift, const float* mean, const float* invstd, const float* coef,
                     const void* gz, void* z, float* out, int N, int B, int H, int W, int Cout,
                     hipStream_t st) {
-  const int grid = c1r3_grid(N, H);
-  const size_t lds = c1r3_lds(Cout, W);
+  const int grid = c1r3_grid(pass, Cout);
+  const size_t lds = c1r3_lds(pass, Cout, W);
 #define AVD_P(P_, C_)                                                                          \
   if (pass == P_ && Cout == C_)                                                                \
     c1r3_kernel<P_, C_><<<grid, 256, lds, st>>>((const bf16*)x, (const bf16*)wk, bias, scale,   \
                                                 shift, mean, invstd, coef, (const bf16*)gz,    \
                                                 (bf16*)z, out, N, B, H, W);
-#define AVD_PC(C_) AVD_P(0, C_) else AVD_P(1, C_) else AVD_P(2, C_) else AVD_P(3, C_)
+#define AVD_PC(C_) AVD_P(0, C_) else AVD_P(1, C_) else AVD_P(2, C_) else AVD_P(3, C_) else AVD_P(4, C_)
   AVD_PC(16) else AVD_PC(32) else AVD_PC(64) else return AVD_ERR_SHAPE;
 #undef AVD_PC
 #undef AVD_P
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_c1r3_combine(const float* m, const float* coef, const void* wk, const float* bias,
+                     float* dw, int G, int Cout, hipStream_t st) {
+  c1r3_combine_kernel<<<avd_cdiv(Cout * 9, 64), 64, 0, st>>>(m, coef, (const bf16*)wk, bias, dw, G,
+                                                             Cout);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

@@ -117,11 +117,15 @@ int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, 
                     const void* gz, void* z, float* out, int N, int B, int H, int W, int Cout,
                     hipStream_t st);
 
+int avd_c1r3_combine(const float* m, const float* coef, const void* wk, const float* bias,
+                     float* dw, int G, int Cout, hipStream_t st);
+
 int avd_cl_c1_recompute_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cout,
                              int K, int pad) {
-  if (pass < 0 || pass > 3 || B <= 0 || N % B) return 0;
-  // the 3x3 encoders' first layer (c1w3.hip)
+  if (pass < 0 || pass > 4 || B <= 0 || N % B) return 0;
+  // the 3x3 encoders' first layer (c1w3.hip); pass 4 (reduce + weight-gradient moments) only there
   if (const int r = avd_c1r3_rows(pass, dt, N, B, Cin, H, W, Cout, K, pad)) return r;
+  if (pass == 4) return 0;
   if (!avd_c1p8_eligible(dt, Cin, Cout, K, H, W) || pad != 2 || W > 112) return 0;
   return avd_c1r_rows(pass, N, B, H);
 }
@@ -135,13 +139,20 @@ int avd_cl_c1_recompute(int pass, const void* x, const void* wk, const float* bi
   if (avd_cl_c1_recompute_rows(pass, dt, N, B, Cin, H, W, Cout, K, pad) == 0) return AVD_ERR_SHAPE;
   const bool need_bn = pass != 0, need_g = pass >= 2;
   if ((need_bn && (!scale || !shift)) || (pass == 1 && !z) || (pass != 1 && !out) ||
-      (need_g && !gz) || (pass == 2 && (!mean || !invstd)) || (pass == 3 && !coef))
+      (need_g && !gz) || ((pass == 2 || pass == 4) && (!mean || !invstd)) || (pass == 3 && !coef))
     return AVD_ERR_ARG;
   if (avd_c1r3_rows(pass, dt, N, B, Cin, H, W, Cout, K, pad))
     return avd_c1r3_launch(pass, x, wk, bias, scale, shift, mean, invstd, coef, gz, z, out, N, B,
                            H, W, Cout, avd_stream(stream));
   return avd_c1r_launch(pass, x, wk, bias, scale, shift, mean, invstd, coef, gz, z, out, N, B, H,
                         W, avd_stream(stream));
+}
+
+int avd_cl_c1_recompute_combine(const float* moments, const float* coef, const void* wk,
+                                const float* bias, float* dw, int G, int Cout, void* stream) {
+  if (!moments || !coef || !wk || !dw) return AVD_ERR_ARG;
+  if (G <= 0 || (Cout != 16 && Cout != 32 && Cout != 64)) return AVD_ERR_SHAPE;
+  return avd_c1r3_combine(moments, coef, wk, bias, dw, G, Cout, avd_stream(stream));
 }
 
 int avd_cl_stat_rows(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt) {
