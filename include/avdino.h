@@ -237,6 +237,25 @@ int avd_cl_bn_bwd_reduce_pooled(const void* y, int dt, const void* pooled, const
                                 const float* invstd, float* parts, int N, int B, int C, int H,
                                 int W, void* stream);
 
+/* avd_cl_conv_dgrad fused with the NEXT backward step's avd_cl_bn_bwd_reduce_pooled (bf16, the
+ * 5x5 mid-layer convs of CentralUnimodalAudio conv2-4 / CentralUnimodalImage conv2): dx is the
+ * gradient of this conv's input `pooled` [N,H,W,Cin] = maxpool2(relu(bn(yprev))) with yprev
+ * [N,2H,2W,Cin] the previous layer's conv output, so the dgrad epilogue forms that layer's
+ * BatchNorm-backward partial sums from dx while it is in registers -- dx is not read back.
+ * parts [Cin][N/B][R][2], R = avd_cl_dgrad_bnreduce_rows() (0 = shape not served: use the two
+ * unfused calls); gamma/beta/mean/invstd are the previous layer's.  A channel whose xhat needs y
+ * (gamma == 0 or |beta| > 8|gamma|) triggers a second pass inside this call that rewrites the
+ * rows from yprev.  Same sums as the unfused pair up to fp32 summation order; dx bit-identical
+ * to avd_cl_conv_dgrad.  Replaces the tail of nn.BatchNorm2d's backward behind
+ * unimodal.py:160-221 (autograd of the reference). */
+int avd_cl_dgrad_bnreduce_rows(int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
+                               int pad);
+int avd_cl_conv_dgrad_bnreduce(const void* dy, const void* wk_d, void* dx, const void* pooled,
+                               const void* yprev, const float* gamma, const float* beta,
+                               const float* mean, const float* invstd, float* parts, int dt, int N,
+                               int B, int Cin, int H, int W, int Cout, int K, int pad,
+                               void* stream);
+
 /* BatchNorm-backward apply fused into BOTH consumers of dy, for the mid-layer convs (bf16):
  * the input- and weight-gradient kernels read the conv output y [N,Ho,Wo,Cout] and the pooled
  * gradient gout (layout gmode: 0 = pooled NHWC in dt, 2 = f32 [N][Cout*Ho/2*Wo/2] in (c,h,w)

@@ -266,6 +266,19 @@ class ConvBranch:
     # apply + dgrad + wgrad for the four mid layers) -- the window math in the staging phase costs
     # registers (occupancy 2 -> 1) and is not hidden behind the MFMAs.  AVDINO_BNAPPLY_FUSED=1.
     BNAPPLY_FUSED = os.environ.get("AVDINO_BNAPPLY_FUSED", "0") == "1"
+    # the previous layer's BN-backward partial sums formed in the dgrad epilogue
+    # (avd_cl_conv_dgrad_bnreduce): the pooled gradient is not read back by a reduce pass
+    DGRAD_BNREDUCE = os.environ.get("AVDINO_DGRAD_BNREDUCE", "1") == "1"
+
+    def _dgrad_reduce_rows(self, ctx, i, N, B):
+        """Rows of the fused dgrad + previous-layer reduce at layer i (> 0), 0 = unfused."""
+        if not self.DGRAD_BNREDUCE or self.act != torch.bfloat16 or ctx["y"][i - 1] is None:
+            return 0
+        ci, co, k, pad = self.stack.convs[i]
+        H = self.dims[i][0]
+        if self.dims[i - 1][1] != 2 * H:
+            return 0
+        return ops.cl_dgrad_bnreduce_rows(self.act, N, B, ci, H, H, co, k, pad)
 
     def backward(self, ws, store, ctx, dfeat, wstream=None):
         """dfeat: f32 [N, F] gradient of the features; writes conv/BN parameter grads.
@@ -277,6 +290,7 @@ class ConvBranch:
         nl = len(self.stack.convs)
         main = torch.cuda.current_stream(dfeat.device) if wstream is not None else None
         wdone = []
+        fused = None       # (parts, R) this layer's reduce already formed by the dgrad above it
         for i in reversed(range(nl)):
             ci, co, k, pad = self.stack.convs[i]
             H, Ho, Hp = self.dims[i]
@@ -289,7 +303,10 @@ class ConvBranch:
             R = ops.cl_bn_bwd_rows(B, co, Ho, Ho, self.act)
             parts = ws.get("bwd_parts", co * G * R * 2)
             pooled = ctx["x"][i + 1] if i < nl - 1 else ctx.get("feat")
-            if mode in (0, 2) and pooled is not None and Ho % 2 == 0:
+            if fused is not None:
+                parts, R = fused
+                fused = None
+            elif mode in (0, 2) and pooled is not None and Ho % 2 == 0:
                 # from the pooled output (2/4 of y's bytes): xhat = (p - beta)/gamma at the argmax
                 ops.cl_bn_bwd_reduce_pooled(y, pooled, gout, mode, store[bk + ".weight"],
                                             store[bk + ".bias"], st[0], st[1], parts, N, B, co, Ho, Ho)
@@ -336,7 +353,17 @@ class ConvBranch:
                 ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
             if i > 0:
                 dx = ws.get("bwd_dx", N * H * H * ci, self.act)
-                ops.cl_conv_dgrad(dy, ctx["wts"][i][1], dx, N, ci, H, H, co, k, pad)
+                Rf = self._dgrad_reduce_rows(ctx, i, N, B)
+                if Rf:
+                    pk = self.stack.bn_keys[i - 1]
+                    pst = ctx["stats"][i - 1]
+                    fparts = ws.get("bwd_parts_rd", ci * G * Rf * 2)
+                    ops.cl_conv_dgrad_bnreduce(dy, ctx["wts"][i][1], dx, ctx["x"][i], ctx["y"][i - 1],
+                                               store[pk + ".weight"], store[pk + ".bias"], pst[0], pst[1],
+                                               fparts, N, B, ci, H, H, co, k, pad)
+                    fused = (fparts, Rf)
+                else:
+                    ops.cl_conv_dgrad(dy, ctx["wts"][i][1], dx, N, ci, H, H, co, k, pad)
                 gout = dx
         for ev in wdone:
             main.wait_event(ev)

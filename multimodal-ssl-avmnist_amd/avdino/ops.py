@@ -449,6 +449,31 @@ def cl_bn_bwd_reduce_pooled(y, pooled, gout, mode, gamma, beta, mean, invstd, pa
                         p(gamma), p(beta), p(mean), p(invstd), p(parts), N, B, C, H, W, stream()))
 
 
+def cl_dgrad_bnreduce_rows(dtype, N, B, Cin, H, W, Cout, K, pad):
+    """Rows per group of avd_cl_conv_dgrad_bnreduce's partial sums; 0 = shape not served."""
+    return lib.avd_cl_dgrad_bnreduce_rows(_DT[dtype], N, B, Cin, H, W, Cout, K, pad)
+
+
+def cl_conv_dgrad_bnreduce(dy, wk_d, dx, pooled, yprev, gamma, beta, mean, invstd, parts, N, B,
+                           Cin, H, W, Cout, K, pad):
+    """cl_conv_dgrad + the previous layer's cl_bn_bwd_reduce_pooled (gout = dx, pooled = this
+    conv's input) in one pass: the sums are formed in the dgrad epilogue."""
+    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
+    R = cl_dgrad_bnreduce_rows(dy.dtype, N, B, Cin, H, W, Cout, K, pad)
+    _need(R > 0, "dgrad_bnreduce: shape not served")
+    _need(dy.numel() == N * Ho * Wo * Cout and dx.numel() == N * H * W * Cin, "dgrad_bnreduce sizes")
+    _need(pooled.numel() == dx.numel() and yprev.numel() == 4 * dx.numel(), "dgrad_bnreduce maps")
+    _need(dy.dtype == dx.dtype == wk_d.dtype == pooled.dtype == yprev.dtype, "dgrad_bnreduce dtypes")
+    _need(parts.numel() >= Cin * (N // B) * R * 2, "dgrad_bnreduce parts")
+    nb = (dy.numel() + dx.numel() + pooled.numel()) * dy.element_size()
+    fl = 2 * N * Cin * H * W * Cout * K * K
+    _timed(f"cl_conv_dgrad_bnreduce[{N}x{Ho}x{Wo}x{Cout}->{Cin} k{K}p{pad} {dy.dtype}]", nb, fl,
+           lambda: call("avd_cl_conv_dgrad_bnreduce", p(dy), p(wk_d), p(dx), p(pooled), p(yprev),
+                        p(gamma), p(beta), p(mean), p(invstd), p(parts), dtcode(dy), N, B, Cin, H, W,
+                        Cout, K, pad, stream()))
+    return R
+
+
 def cl_bn_bwd_apply(y, gout, mode, scale, shift, coef, dy, N, B, C, H, W):
     _need(dy.numel() == y.numel() and dy.dtype == y.dtype, "cl bwd dy")
     nb = 2 * y.numel() * y.element_size() + gout.numel() * gout.element_size()

@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256) void bwd_reduce_pooled_cl_kernel(
     const T* __restrict__ y, const void* __restrict__ pooled, const void* __restrict__ gout,
     int mode, const float* __restrict__ gamma, const float* __restrict__ beta,
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ parts,
-    int G, int B, int C, int H, int W, int R, long long per) {
+    int G, int B, int C, int H, int W, int R, long long per, int fixup) {
   constexpr int V = Vec<T>::V;
   __shared__ float sh[256][2 * V + 1];
   const int Hp = H / 2, Wp = W / 2, CV = C / V;
@@ -261,6 +261,16 @@ __global__ __launch_bounds__(256) void bwd_reduce_pooled_cl_kernel(
   const int c0 = cv * V;
   const long long nwin = (long long)B * Hp * Wp;
   const long long w0 = r * per, w1 = std::min(nwin, w0 + per);
+  if (fixup) {
+    // fix-up pass after a dgrad that formed these sums in its epilogue (conv_ws.hip, RD): only
+    // when some channel needs xhat from y are the rows rewritten (all of them, by this kernel)
+    bool need = false;
+    for (int c = 0; c < C; ++c) {
+      const float ga = gamma[c], bb = beta[c];
+      need |= ga == 0.f || fabsf(bb) > (sizeof(T) == 2 ? 8.f : 4096.f) * fabsf(ga);
+    }
+    if (!need) return;
+  }
   float ig[V], be[V], mu[V], is[V], s1[V], s2[V], gs[V];
   bool any0 = false;
 #pragma unroll
@@ -516,11 +526,29 @@ int avd_cl_bn_bwd_reduce_pooled_impl(const void* y, int dt, const void* pooled, 
   if (dt == AVD_BF16)
     bwd_reduce_pooled_cl_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)y, pooled, gout, mode, gamma,
                                                             beta, mean, invstd, parts, G, B, C, H, W,
-                                                            R, per);
+                                                            R, per, 0);
   else
     bwd_reduce_pooled_cl_kernel<float><<<grid, 256, 0, st>>>((const float*)y, pooled, gout, mode, gamma,
                                                              beta, mean, invstd, parts, G, B, C, H, W,
-                                                             R, per);
+                                                             R, per, 0);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+// Fix-up pass of avd_cl_conv_dgrad_bnreduce (bf16, NHWC pooled maps): R rows as the dgrad
+// wrote them; every block returns at once unless a channel needs xhat from y.
+int avd_cl_bn_bwd_reduce_pooled_fixup_impl(const void* y, const void* pooled, const void* gout,
+                                           const float* gamma, const float* beta,
+                                           const float* mean, const float* invstd, float* parts,
+                                           int R, int N, int B, int C, int H, int W,
+                                           hipStream_t st) {
+  if (C % 8 || C / 8 > 256 || N % B || (H & 1) || (W & 1) || R <= 0) return AVD_ERR_SHAPE;
+  const int G = N / B;
+  const long long nwin = (long long)B * (H / 2) * (W / 2);
+  const long long per = (nwin + R - 1) / R;
+  bwd_reduce_pooled_cl_kernel<bf16><<<dim3(R, G), 256, 0, st>>>((const bf16*)y, pooled, gout, 0, gamma,
+                                                                beta, mean, invstd, parts, G, B, C, H,
+                                                                W, R, per, 1);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

@@ -62,7 +62,41 @@ int avd_cl_bn_bwd_reduce_pooled_impl(const void* y, int dt, const void* pooled, 
                                      const float* mean, const float* invstd, float* parts, int N,
                                      int B, int C, int H, int W, hipStream_t st);
 
+int avd_ws_dgrad_bnreduce_rows(int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad);
+int avd_ws_conv_dgrad_bnreduce(const void* dy, const void* wk_d, void* dx, const void* pooled,
+                               const float* gamma, const float* beta, float* parts, int dt, int N,
+                               int B, int Cin, int H, int W, int Cout, int K, int pad,
+                               hipStream_t st);
+int avd_cl_bn_bwd_reduce_pooled_fixup_impl(const void* y, const void* pooled, const void* gout,
+                                           const float* gamma, const float* beta,
+                                           const float* mean, const float* invstd, float* parts,
+                                           int R, int N, int B, int C, int H, int W,
+                                           hipStream_t st);
+
 extern "C" {
+
+int avd_cl_dgrad_bnreduce_rows(int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
+                               int pad) {
+  return avd_ws_dgrad_bnreduce_rows(dt, N, B, Cin, H, W, Cout, K, pad);
+}
+
+int avd_cl_conv_dgrad_bnreduce(const void* dy, const void* wk_d, void* dx, const void* pooled,
+                               const void* yprev, const float* gamma, const float* beta,
+                               const float* mean, const float* invstd, float* parts, int dt, int N,
+                               int B, int Cin, int H, int W, int Cout, int K, int pad,
+                               void* stream) {
+  if (!dy || !wk_d || !dx || !pooled || !yprev || !gamma || !beta || !mean || !invstd || !parts)
+    return AVD_ERR_ARG;
+  const int R = avd_ws_dgrad_bnreduce_rows(dt, N, B, Cin, H, W, Cout, K, pad);
+  if (R <= 0) return AVD_ERR_SHAPE;
+  const hipStream_t st = avd_stream(stream);
+  const int r = avd_ws_conv_dgrad_bnreduce(dy, wk_d, dx, pooled, gamma, beta, parts, dt, N, B, Cin,
+                                           H, W, Cout, K, pad, st);
+  if (r <= 0) return r == 0 ? AVD_ERR_SHAPE : r;
+  // the previous layer's conv output yprev is N x 2H x 2W x Cin
+  return avd_cl_bn_bwd_reduce_pooled_fixup_impl(yprev, pooled, dx, gamma, beta, mean, invstd, parts,
+                                                R, N, B, Cin, 2 * H, 2 * W, st);
+}
 
 int avd_cl_weight_elems(int Cout, int Cin, int K, int dgrad) {
   const int O = dgrad ? Cin : Cout, C = dgrad ? Cout : Cin;

@@ -90,8 +90,19 @@ __device__ __forceinline__ int koff(int ks, int g) {
 // AP (input gradient only): 0 = x is the staged operand itself (dY); 1 / 2 = x is the conv
 // output y of the layer whose gradient this is, and the staging applies that layer's
 // BatchNorm backward (bnapply.h) to produce dY in LDS, with the pooled gradient in layout 0 / 2
-template <class L, bool FWD, int AP = 0>
-__global__ __launch_bounds__(256, AP ? (L::OCC > 1 ? L::OCC - 1 : 1) : L::OCC) void conv_ws_kernel(const bf16* __restrict__ x,
+//
+// RD (input gradient only, AP = 0): the epilogue also forms the BatchNorm-backward partial sums of
+// the PREVIOUS layer, whose pooled output p is this conv's input and whose pooled gradient is
+// the dX this kernel writes (what bwd_reduce_pooled_cl_kernel, bn_cl.hip, reads back from HBM):
+// per channel sum dz and sum dz * xhat with dz = (p > 0 ? dX : 0) and xhat = (p - beta) / gamma
+// (aa.gout = p, aa.scale = gamma, aa.shift = beta; sum dz * p is accumulated and turned into the
+// xhat sum per row at the flush, so no per-channel constants occupy registers in the tile loop),
+// as per-block running sums per BN group into
+// stats [C][G][R = grid * NPW][2].  Channels with |beta| >> |gamma| contribute 0 to the second sum
+// here; the launcher follows with bwd_reduce_pooled's fix-up pass, which rewrites every row
+// from y when any channel needs it.
+template <class L, bool FWD, int AP = 0, bool RD = false>
+__global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::OCC - 1 : 1) : L::OCC) void conv_ws_kernel(const bf16* __restrict__ x,
                                                       const bf16* __restrict__ wk,
                                                       const float* __restrict__ bias,
                                                       bf16* __restrict__ y,
@@ -140,6 +151,7 @@ __global__ __launch_bounds__(256, AP ? (L::OCC > 1 ? L::OCC - 1 : 1) : L::OCC) v
       const int co = cob + 16 * t + 4 * g + i;
       bv[t][i] = (FWD && bias && co < L::COUT) ? bias[co] : 0.f;
     }
+  constexpr bool STATS = FWD || RD;
 
   // ---- contiguous tile range of this block
   const int per = ntiles / (int)gridDim.x, extra = ntiles % (int)gridDim.x;
@@ -258,16 +270,31 @@ __global__ __launch_bounds__(256, AP ? (L::OCC > 1 ? L::OCC - 1 : 1) : L::OCC) v
 #pragma unroll
       for (int i = 0; i < 4; ++i) { run_s[t][i] = 0.f; run_q[t][i] = 0.f; }
   };
-  auto flush = [&](int gp) {
-    if (r16 != 0 || kw != 0) return;
+  auto flush = [&](int gp) {   // wave-uniform call: the row sums are DPP across the 16 lanes
+    if (kw != 0) return;
+#pragma unroll
+    for (int t = 0; t < L::NTW; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        run_s[t][i] = row16_sum(run_s[t][i]);
+        run_q[t][i] = row16_sum(run_q[t][i]);
+      }
+    if (r16 != 0) return;
 #pragma unroll
     for (int t = 0; t < L::NTW; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int co = cob + 16 * t + 4 * g + i;
-        if (co < L::COUT)
+        if (co < L::COUT) {
+          float q = run_q[t][i];
+          if constexpr (RD) {
+            // sum dz * xhat = (sum dz * p - beta * sum dz) / gamma; 0 for the fix-up channels
+            const float ga = aa.scale[co], bb = aa.shift[co];
+            q = (ga == 0.f || fabsf(bb) > 8.f * fabsf(ga)) ? 0.f : (q - bb * run_s[t][i]) / ga;
+          }
           *reinterpret_cast<float2*>(stats + (((size_t)co * ngroups + gp) * R + blockIdx.x * L::NPW + wp) * 2) =
-              make_float2(run_s[t][i], run_q[t][i]);
+              make_float2(run_s[t][i], q);
+        }
       }
   };
   zero_run();
@@ -289,11 +316,20 @@ __global__ __launch_bounds__(256, AP ? (L::OCC > 1 ? L::OCC - 1 : 1) : L::OCC) v
 
     const int sg = ti / L::TPS, tt = ti - sg * L::TPS;
     const int n0 = sg * L::NS, ty0 = tt * L::TH;
-    float ss[L::NTW][4], sq[L::NTW][4];
-#pragma unroll
-    for (int t = 0; t < L::NTW; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { ss[t][i] = 0.f; sq[t][i] = 0.f; }
+    // statistics: a new BN group starts a new running sum (lane-local over the block's tiles
+    // of that group; summed across the 16 pixel lanes once, at the flush)
+    if constexpr (STATS) {
+      if (stats && kw == 0) {
+        const int gi = ti / tilesPG;
+        if (gi != cur_g) {
+          if (cur_g >= 0) flush(cur_g);
+          cur_g = gi;
+          zero_run();
+        }
+      }
+    }
+    auto& ss = run_s;
+    auto& sq = run_q;
 
     for (int i0 = 0; i0 < L::GW; i0 += L::GB) {
       int base[L::GB], opix[L::GB];
@@ -306,6 +342,20 @@ __global__ __launch_bounds__(256, AP ? (L::OCC > 1 ? L::OCC - 1 : 1) : L::OCC) v
         const int ry = rem / L::TW, rx = rem - ry * L::TW;
         base[b] = gv[b] ? ((s * L::ITH + ry) * L::RS + rx) * L::PS : 0;
         opix[b] = ((n0 + s) * L::HO + ty0 + ry) * L::WO + rx;
+      }
+      // RD: the pooled map at this wave's output elements, in flight under the MFMAs
+      uint2 pq[RD ? L::GB : 1][RD ? L::NTW : 1];
+      if constexpr (RD) {
+#pragma unroll
+        for (int b = 0; b < L::GB; ++b)
+#pragma unroll
+          for (int t = 0; t < L::NTW; ++t) {
+            const int co = cob + 16 * t + 4 * g;
+            pq[b][t] = (kw == 0 && gv[b] && co < L::COUT)
+                           ? *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(aa.gout) +
+                                                             (size_t)opix[b] * L::COUT + co)
+                           : make_uint2(0u, 0u);
+          }
       }
       f4 acc[L::GB][L::NTW];
 #pragma unroll
@@ -381,30 +431,25 @@ __global__ __launch_bounds__(256, AP ? (L::OCC > 1 ? L::OCC - 1 : 1) : L::OCC) v
           } else {
             lo = pack_bf16x2(acc[b][t][0], acc[b][t][1]);
             hi = pack_bf16x2(acc[b][t][2], acc[b][t][3]);
+            if constexpr (RD) {   // sums over the stored (rounded) gradient, as the reduce reads it
+              const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                                  __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+              const float pv[4] = {__uint_as_float(pq[b][t].x << 16), __uint_as_float(pq[b][t].x & 0xffff0000u),
+                                   __uint_as_float(pq[b][t].y << 16), __uint_as_float(pq[b][t].y & 0xffff0000u)};
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {   // sum dz and sum dz * p (xhat applied at the flush)
+                const float dz = pv[i] > 0.f ? v[i] : 0.f;
+                ss[t][i] += dz;
+                sq[t][i] = fmaf(dz, pv[i], sq[t][i]);
+              }
+            }
           }
           *reinterpret_cast<uint2*>(y + (size_t)opix[b] * L::COUT + co) = make_uint2(lo, hi);
         }
       }
     }
-    if constexpr (FWD) {
-      if (stats && kw == 0) {
-        const int gi = ti / tilesPG;
-        if (gi != cur_g) {
-          if (cur_g >= 0) flush(cur_g);
-          cur_g = gi;
-          zero_run();
-        }
-#pragma unroll
-        for (int t = 0; t < L::NTW; ++t)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            run_s[t][i] += row16_sum(ss[t][i]);
-            run_q[t][i] += row16_sum(sq[t][i]);
-          }
-      }
-    }
   }
-  if constexpr (FWD) {
+  if constexpr (STATS) {
     if (stats) {
       if (cur_g >= 0) flush(cur_g);
       // groups this block never reached (its tiles cover groups [first, last]): zero rows
@@ -476,34 +521,37 @@ int num_cus() {
   return cus;
 }
 
-// the forward's grid when it writes BatchNorm partials: one resident wave of blocks
-template <class L>
-int ws_stat_grid() {
+// resident blocks per CU of one instantiation (cached per instantiation: the device's CU
+// count and register file are the same for every device of a homogeneous node)
+template <class L, bool FWD, int AP, bool RD>
+int ws_occ() {
   static int occ = 0;
   if (!occ) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv_ws_kernel<L, true, 0>, 256, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv_ws_kernel<L, FWD, AP, RD>, 256, 0) !=
             hipSuccess || occ <= 0)
       occ = 1;
   }
-  return grid_cap(num_cus() * occ);
+  return occ;
 }
 
-template <class L, bool FWD, int AP = 0>
+// the grid of a launch that writes BatchNorm partials (forward statistics, or the RD dgrad's
+// backward sums): one resident wave of blocks, so R = grid * NPW rows per group is fixed
+template <class L, bool FWD = true, bool RD = false>
+int ws_stat_grid() {
+  return grid_cap(num_cus() * ws_occ<L, FWD, 0, RD>());
+}
+
+template <class L, bool FWD, int AP = 0, bool RD = false>
 int launch_ws(const void* x, const void* wk, const float* bias, void* y, float* stats, int N,
               int B, hipStream_t st, const ApplyArgs& aa = ApplyArgs{}) {
-  if (N % L::NS || (FWD && stats && B % L::NS)) return AVD_ERR_SHAPE;
+  constexpr bool STATS = FWD || RD;
+  if (N % L::NS || (STATS && stats && B % L::NS)) return AVD_ERR_SHAPE;
   if (AP && (aa.B % L::NS || aa.G > APPLY_GMAX || aa.G * aa.B != N)) return AVD_ERR_SHAPE;
-  static int occ = 0;
-  if (!occ) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv_ws_kernel<L, FWD, AP>, 256, 0) !=
-            hipSuccess || occ <= 0)
-      occ = 1;
-  }
   const int ntiles = (N / L::NS) * L::TPS;
-  // with statistics the grid is fixed (avd_ws_stat_rows: R = grid * NPW rows per group)
-  const int grid = FWD && stats ? ws_stat_grid<L>() : grid_cap(std::min(ntiles, num_cus() * occ));
-  conv_ws_kernel<L, FWD, AP><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, (bf16*)y,
-                                                   stats, ntiles, FWD && stats ? N / B : 1, aa);
+  const int grid = STATS && stats ? ws_stat_grid<L, FWD, RD>()
+                                  : grid_cap(std::min(ntiles, num_cus() * ws_occ<L, FWD, AP, RD>()));
+  conv_ws_kernel<L, FWD, AP, RD><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, (bf16*)y,
+                                                       stats, ntiles, STATS && stats ? N / B : 1, aa);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
@@ -584,6 +632,38 @@ int avd_ws_conv_dgrad_bnapply(const void* y, const void* gout, int gmode, const 
   }
   AVD_DA(DgrA2) AVD_DA(DgrA3) AVD_DA(DgrA4) AVD_DA(DgrI2)
 #undef AVD_DA
+  return 0;
+}
+
+// Input gradient + the previous layer's BatchNorm-backward partial sums (RD above).  The
+// previous layer: BN over Cin channels, ReLU, 2x2 max-pool whose output `pooled` (N x H x W x Cin,
+// NHWC bf16) is this conv's input.  parts [Cin][N/B][R][2], R = avd_ws_dgrad_bnreduce_rows.
+// 1 = launched, 0 = not served, < 0 = error.  (The fix-up pass is the caller's: cl_api.hip.)
+int avd_ws_dgrad_bnreduce_rows(int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad) {
+  if (dt != AVD_BF16 || ws_disabled() || B <= 0 || N % B) return 0;
+  const int Ho = H + 2 * pad - K + 1, Wo = W + 2 * pad - K + 1, dp = K - 1 - pad;
+#define AVD_RR(LL) \
+  if (is<LL>(Cout, Ho, Wo, Cin, K, dp)) return B % LL::NS ? 0 : ws_stat_grid<LL, false, true>() * LL::NPW;
+  AVD_RR(DgrA2) AVD_RR(DgrA3) AVD_RR(DgrA4) AVD_RR(DgrI2)
+#undef AVD_RR
+  return 0;
+}
+
+int avd_ws_conv_dgrad_bnreduce(const void* dy, const void* wk_d, void* dx, const void* pooled,
+                               const float* gamma, const float* beta, float* parts, int dt, int N,
+                               int B, int Cin, int H, int W, int Cout, int K, int pad,
+                               hipStream_t st) {
+  if (!avd_ws_dgrad_bnreduce_rows(dt, N, B, Cin, H, W, Cout, K, pad)) return 0;
+  const int Ho = H + 2 * pad - K + 1, Wo = W + 2 * pad - K + 1, dp = K - 1 - pad;
+  const ApplyArgs aa{pooled, gamma, beta, nullptr, B, N / B};
+  int r = 0;
+#define AVD_RD(LL)                                                                              \
+  if (is<LL>(Cout, Ho, Wo, Cin, K, dp)) {                                                      \
+    r = launch_ws<LL, false, 0, true>(dy, wk_d, nullptr, dx, parts, N, B, st, aa);             \
+    return r == AVD_OK ? 1 : (r == AVD_ERR_SHAPE ? 0 : r);                                     \
+  }
+  AVD_RD(DgrA2) AVD_RD(DgrA3) AVD_RD(DgrA4) AVD_RD(DgrI2)
+#undef AVD_RD
   return 0;
 }
 

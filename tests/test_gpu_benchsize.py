@@ -219,6 +219,74 @@ def test_ws_kernels_bench_size(ops, shape):
     assert grel(dw, wgrad_ref(x, dy, K, pad)) < 1e-5
 
 
+# ------------------------------------------------------- dgrad + previous layer's BN-backward sums
+def _prev_layer(ops, g, N, B, Ci, H, small_gamma=False):
+    """The previous layer's BN -> ReLU -> pool over a random conv output yprev [N,2H,2H,Ci]:
+    (yprev, pooled, gamma, beta, mean, invstd) with per-(group, channel) statistics."""
+    G = N // B
+    yprev = (torch.randn(N, 2 * H, 2 * H, Ci, generator=g, device="cuda") * 0.7 + 0.2).to(T)
+    yv = yprev.to(F64).view(G, -1, Ci)
+    mean = yv.mean(1)
+    invstd = 1.0 / torch.sqrt(yv.var(1, unbiased=False) + 1e-5)
+    gamma = rnd(g, (Ci,), 0.5, 1.5)
+    beta = rnd(g, (Ci,), -0.3, 0.3)
+    if small_gamma:            # |beta| >> |gamma|: xhat must come from y (the fix-up pass)
+        gamma[1], beta[1] = 1e-2, 1.0
+        gamma[Ci - 1] = 0.0
+    scale = (gamma.to(F64) * invstd)
+    shift = beta.to(F64) - mean * scale
+    pooled = torch.empty(N, H, H, Ci, device="cuda", dtype=T)
+    ops.cl_bn_relu_pool(yprev, scale.float().reshape(-1).contiguous(), shift.float().reshape(-1).contiguous(),
+                        pooled, 0, N, B, Ci, 2 * H, 2 * H)
+    return yprev, pooled, gamma, beta, mean.float().reshape(-1).contiguous(), invstd.float().reshape(-1).contiguous()
+
+
+# (Cin, H, Cout, K, pad, N): the four conv_ws dgrad layers, N with many tiles per block
+RD_BENCH = [(8, 56, 16, 5, 2, 2048), (16, 28, 32, 5, 2, 2048), (32, 14, 64, 5, 2, 4096),
+            (32, 14, 64, 5, 0, 4096)]
+
+
+@pytest.mark.parametrize("small_gamma", [False, True])
+@pytest.mark.parametrize("shape", RD_BENCH)
+def test_dgrad_bnreduce_bench_size(ops, shape, small_gamma):
+    """avd_cl_conv_dgrad_bnreduce: dx bit-identical to avd_cl_conv_dgrad, and the previous
+    layer's BN-backward partial sums equal avd_cl_bn_bwd_reduce_pooled's (fp32 sum order, 1e-5)
+    and float64 of sum dz, sum dz * xhat.  small_gamma: channels whose xhat needs y go through
+    the fix-up pass (gamma = 1e-2 with beta = 1, and gamma = 0)."""
+    Ci, H, Co, K, pad, N = shape
+    B = 1024
+    G = N // B
+    Ho = H + 2 * pad - K + 1
+    g = torch.Generator(device="cuda").manual_seed(90 + H + pad + small_gamma)
+    w = (rnd(g, (Co, Ci, K, K)) / (Ci * K * K) ** 0.5).to(T).float()
+    wd = layout(ops, w, 1)
+    dy = rnd(g, (N, Ho, Ho, Co), dtype=T)
+    yprev, pooled, gamma, beta, mean, invstd = _prev_layer(ops, g, N, B, Ci, H, small_gamma)
+    Rf = ops.cl_dgrad_bnreduce_rows(T, N, B, Ci, H, H, Co, K, pad)
+    assert Rf > 0
+    dx1 = torch.full((N, H, H, Ci), float("nan"), device="cuda", dtype=T)
+    pf = torch.full((Ci * G * Rf * 2,), float("nan"), device="cuda")
+    ops.cl_conv_dgrad_bnreduce(dy, wd, dx1, pooled, yprev, gamma, beta, mean, invstd, pf, N, B,
+                               Ci, H, H, Co, K, pad)
+    dx0 = torch.empty_like(dx1)
+    ops.cl_conv_dgrad(dy, wd, dx0, N, Ci, H, H, Co, K, pad)
+    assert torch.equal(dx0, dx1)
+    R0 = ops.cl_bn_bwd_rows(B, Ci, 2 * H, 2 * H, T)
+    p0 = torch.empty(Ci * G * R0 * 2, device="cuda")
+    ops.cl_bn_bwd_reduce_pooled(yprev, pooled, dx0, 0, gamma, beta, mean, invstd, p0, N, B, Ci,
+                                2 * H, 2 * H)
+    s1 = pf.view(Ci, G, Rf, 2).to(F64).sum(2)
+    s0 = p0.view(Ci, G, R0, 2).to(F64).sum(2)
+    assert grel(s1[..., 0], s0[..., 0]) < 1e-5
+    assert grel(s1[..., 1], s0[..., 1]) < 1e-5
+    if not small_gamma:        # float64 from the pooled map: xhat = (p - beta) / gamma
+        pv, dv = pooled.to(F64).view(G, -1, Ci), dx0.to(F64).view(G, -1, Ci)
+        dz = torch.where(pv > 0, dv, torch.zeros_like(dv))
+        xh = (pv - beta.to(F64)) / gamma.to(F64)
+        assert grel(s1[..., 0], dz.sum(1).T) < 1e-5
+        assert grel(s1[..., 1], (dz * xh).sum(1).T) < 1e-5
+
+
 # ---------------------------------------------------------------------------- forced small grids
 def _capped(monkeypatch, cap, fn):
     monkeypatch.delenv("AVDINO_GRID_CAP", raising=False)
