@@ -284,9 +284,11 @@ int avd_cl_conv_wgrad_bnapply(const void* x, const void* y, const void* gout, in
  *   pass 2 (reduce): out = BN-backward partial rows (sum dz, sum dz*xhat) as
  *                    avd_cl_bn_bwd_reduce (mode 0), gz = pooled gradient;
  *   pass 3 (wgrad):  out = dW partial slabs as avd_cl_bn_bwd_apply_wgrad.
- *   pass 4 (3x3 only: reduce + weight-gradient moments in one pass): out = pass 2's rows
- *                    [Cout][G][R][2], then [R][G][Cout*9 + 90] moments (sum dz x9 per
- *                    channel/tap, Gram rows of the im2col x9 with a ones tap); dW is linear in
+ *   pass 4 (reduce + weight-gradient moments in one pass): out = pass 2's rows
+ *                    [Cout][G][R][2], then [R][G][avd_cl_c1_moment_cols(Cout)] moments:
+ *                    3x3 layers: sum dz x9 per channel/tap, Gram rows of the im2col x9 with a
+ *                    ones tap (Cout*9 + 90); the 5x5 audio conv1 (Cout 8): sum dz x25 [8][25],
+ *                    the x25 Gram matrix [25][25], sum x25 [25] (850).  dW is linear in
  *                    dy = k1 dz + kx y + k0, so after avd_bn_bwd_finalize and avd_sum_rows of
  *                    the moments, avd_cl_c1_recompute_combine forms dW (y taken unrounded).
  * scale/shift/mean/invstd [G][Cout] from avd_bn_finalize, coef from avd_bn_bwd_finalize.
@@ -299,8 +301,10 @@ int avd_cl_c1_recompute(int pass, const void* x, const void* wk, const float* bi
                         const float* invstd, const float* coef, const void* gz, void* z,
                         float* out, int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
                         int pad, void* stream);
-/* dW [Cout][1][3][3] = sum_g k1 M_dz + kx (w . Gram + b sum x9) + k0 sum x9 from pass 4's
- * row-summed moments [G][Cout*9 + 90] and coef [G][Cout][3]; wk = the forward layout. */
+/* dW [Cout][1][K][K] = sum_g k1 M_dz + kx (w . Gram + b sum x) + k0 sum x from pass 4's
+ * row-summed moments [G][avd_cl_c1_moment_cols(Cout)] and coef [G][Cout][3]; wk = the forward
+ * layout.  Cout 8: the 5x5 audio conv1; Cout 16/32/64: the 3x3 first layers. */
+int avd_cl_c1_moment_cols(int Cout);
 int avd_cl_c1_recompute_combine(const float* moments, const float* coef, const void* wk,
                                 const float* bias, float* dw, int G, int Cout, void* stream);
 

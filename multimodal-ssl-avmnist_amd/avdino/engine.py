@@ -196,9 +196,14 @@ class ConvBranch:
     # their backward as one pass (avd_cl_c1_recompute pass 4) + a tiny combine: dW is linear in
     # dy = k1 dz + kx y + k0, so the pass accumulates sum dz x9 and the Gram matrix of x9
     RC_MOMENTS = os.environ.get("AVDINO_L1_RC_MOMENTS", "1") == "1"
+    # the 5x5 audio conv1 in training: no stored y either -- its backward is the one moments
+    # pass (x and the pooled gradient in, BN-backward sums + dW moments out) and a combine
+    MOMENTS5 = os.environ.get("AVDINO_L1_MOMENTS5", "0") == "1"
 
     def _recompute_ok(self, N, B, ci, H, co, k, pad, need_dgrad=True):
         rc = self.RECOMPUTE or (self.RECOMPUTE3 and k == 3) or (self.RC_NOGRAD and not need_dgrad)
+        if not rc and self.MOMENTS5 and self.RC_MOMENTS and k == 5 and self.act == torch.bfloat16:
+            rc = ops.cl_c1_recompute_rows(ops.C1_REDUCE_MOMENTS, self.act, N, B, ci, H, H, co, k, pad) > 0
         return (rc and self.act == torch.bfloat16 and
                 ops.cl_c1_recompute_rows(ops.C1_STATS, self.act, N, B, ci, H, H, co, k, pad) > 0)
 
@@ -268,7 +273,7 @@ class ConvBranch:
     BNAPPLY_FUSED = os.environ.get("AVDINO_BNAPPLY_FUSED", "0") == "1"
     # the previous layer's BN-backward partial sums formed in the dgrad epilogue
     # (avd_cl_conv_dgrad_bnreduce): the pooled gradient is not read back by a reduce pass
-    DGRAD_BNREDUCE = os.environ.get("AVDINO_DGRAD_BNREDUCE", "1") == "1"
+    DGRAD_BNREDUCE = os.environ.get("AVDINO_DGRAD_BNREDUCE", "0") == "1"
 
     def _dgrad_reduce_rows(self, ctx, i, N, B):
         """Rows of the fused dgrad + previous-layer reduce at layer i (> 0), 0 = unfused."""

@@ -503,8 +503,12 @@ C1_STATS, C1_APPLY, C1_REDUCE, C1_WGRAD, C1_REDUCE_MOMENTS = 0, 1, 2, 3, 4
 
 
 def c1_moment_cols(Cout):
-    """Columns of one pass-4 moment row: sum dz x9 [Cout][9] + Gram rows [9][10]."""
-    return Cout * 9 + 90
+    """Columns of one pass-4 moment row (avd_cl_c1_moment_cols): 3x3 layers sum dz x9
+    [Cout][9] + Gram rows [9][10]; the 5x5 audio conv1 (Cout 8) sum dz x25 [8][25] + Gram
+    [25][25] + sum x25 [25]."""
+    n = lib.avd_cl_c1_moment_cols(Cout)
+    _need(n > 0, f"no pass-4 moments for Cout {Cout}")
+    return n
 
 
 def cl_c1_recompute_rows(pas, dtype, N, B, Cin, H, W, Cout, K, pad):
@@ -540,9 +544,10 @@ def cl_c1_recompute(pas, x, wk, bias, N, B, Cin, H, W, Cout, K, pad, scale=None,
 
 
 def cl_c1_recompute_combine(moments, coef, wk, bias, dw, G, Cout):
-    """dW of the 3x3 first layer from pass 4's row-summed moments (avd_cl_c1_recompute_combine)."""
+    """dW of a first layer from pass 4's row-summed moments (avd_cl_c1_recompute_combine): the
+    3x3 layers (Cout 16/32/64) and the 5x5 audio conv1 (Cout 8)."""
     _need(moments.numel() >= G * c1_moment_cols(Cout) and coef.numel() >= G * Cout * 3 and
-          dw.numel() >= Cout * 9, "c1 recompute combine shape")
+          dw.numel() >= Cout * (25 if Cout == 8 else 9), "c1 recompute combine shape")
     call("avd_cl_c1_recompute_combine", p(moments), p(coef), p(wk), p(bias), p(dw), G, Cout, stream())
 
 

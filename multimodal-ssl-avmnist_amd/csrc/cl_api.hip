@@ -1,4 +1,6 @@
 // C ABI of the channels-last (NHWC) conv-block path (include/avdino.h, "avd_cl_*").
+#include <cstdlib>
+
 #include "common.h"
 
 int avd_cl_layout_rows_impl(int O);
@@ -35,6 +37,9 @@ int avd_c1p8_bwd_apply_wgrad(const void* y, const void* gout, const float* scale
                              int N, int B, int H, int W, hipStream_t st);
 
 int avd_c1r_rows(int pass, int N, int B, int H);
+int avd_c1p8_moment_cols();
+int avd_c1p8_combine(const float* m, const float* coef, const void* wk, const float* bias,
+                     float* dw, int G, hipStream_t st);
 int avd_c1r_launch(int pass, const void* x, const void* wk, const float* bias, const float* scale,
                    const float* shift, const float* mean, const float* invstd, const float* coef,
                    const void* gz, void* z, float* out, int N, int B, int H, int W,
@@ -159,8 +164,8 @@ int avd_cl_c1_recompute_rows(int pass, int dt, int N, int B, int Cin, int H, int
   if (pass < 0 || pass > 4 || B <= 0 || N % B) return 0;
   // the 3x3 encoders' first layer (c1w3.hip); pass 4 (reduce + weight-gradient moments) only there
   if (const int r = avd_c1r3_rows(pass, dt, N, B, Cin, H, W, Cout, K, pad)) return r;
-  if (pass == 4) return 0;
   if (!avd_c1p8_eligible(dt, Cin, Cout, K, H, W) || pad != 2 || W > 112) return 0;
+  if (pass == 4 && getenv("AVDINO_C1P8_MOMENTS_OFF")) return 0;
   return avd_c1r_rows(pass, N, B, H);
 }
 
@@ -185,8 +190,16 @@ int avd_cl_c1_recompute(int pass, const void* x, const void* wk, const float* bi
 int avd_cl_c1_recompute_combine(const float* moments, const float* coef, const void* wk,
                                 const float* bias, float* dw, int G, int Cout, void* stream) {
   if (!moments || !coef || !wk || !dw) return AVD_ERR_ARG;
-  if (G <= 0 || (Cout != 16 && Cout != 32 && Cout != 64)) return AVD_ERR_SHAPE;
+  if (G <= 0 || (Cout != 8 && Cout != 16 && Cout != 32 && Cout != 64)) return AVD_ERR_SHAPE;
+  if (Cout == 8)   // the 5x5 audio conv1 (conv_c1p.hip)
+    return avd_c1p8_combine(moments, coef, wk, bias, dw, G, avd_stream(stream));
   return avd_c1r3_combine(moments, coef, wk, bias, dw, G, Cout, avd_stream(stream));
+}
+
+int avd_cl_c1_moment_cols(int Cout) {
+  if (Cout == 8) return avd_c1p8_moment_cols();
+  if (Cout == 16 || Cout == 32 || Cout == 64) return Cout * 9 + 90;
+  return 0;
 }
 
 int avd_cl_stat_rows(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt) {

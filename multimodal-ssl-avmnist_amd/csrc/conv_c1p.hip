@@ -780,11 +780,379 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------- moments pass
+// Backward of the layer in ONE pass that reads only the input x and the pooled gradient gz
+// (no stored y, no dy): dy = k1 dz + kx y + k0 is linear in (dz, y, 1) and y = w . x25 + b, so
+//   dW[c][t] = sum_g k1 M[g][c][t] + kx (sum_t' w[c][t'] G[g][t'][t] + b[c] S[g][t]) + k0 S[g][t]
+// with, per BN group g, M = sum dz x25 (dz = the routed pooled gradient), G = sum x25 x25^T (the
+// patch Gram matrix) and S = sum x25 -- none of which needs the BN-backward coefficients, so the
+// same pass also forms the BN-backward sums (sum dz, sum dz xhat) those coefficients come from
+// (avd_bn_bwd_finalize) and a tiny combine kernel finishes dW.  Per tile: x rows staged twice
+// (natural rows for the y recompute, parity/shift copies for the B operand), y recomputed by
+// the pixel-pair MFMA into LDS (bit-identical bf16 values), one thread per pooling window forms
+// dz in place of y, then per k-block of pixel pairs: D += dZ X (2 MFMAs, the wgrad kernel's
+// operands) and the Gram tiles X^T X (3 MFMAs; the B fragment doubles as the A fragment, and
+// pair column 30 reads ones so its Gram column is S).  Blocks own contiguous tile ranges of
+// one BN group; outputs per block row r of group g:
+//   out[((c * G + g) * R + r) * 2 + {0, 1}]                 BN sums of channel c
+//   out[C * G * R * 2 + (r * G + g) * MOM5 + ...]             M [8][25] | G [25][25] | S [25]
+constexpr int MOM5 = COUT * 25 + 25 * 25 + 25;
+#ifndef C1M_DIAG
+#define C1M_DIAG 0   // diagnostic builds only: 1 no window math, 2 no Gram MFMAs, 4 no y MFMA, 8 no k-loop
+#endif
+
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
+}
+
+__global__ __launch_bounds__(256) void c1p8_moments_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ wk, const float* __restrict__ bias,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ mean, const float* __restrict__ invstd,
+    const bf16* __restrict__ gz, float* __restrict__ out, int B, int G, int R, int H, int W,
+    int tps) {
+  __shared__ __attribute__((aligned(16))) bf16 xs[(TH + 4) * ITW];
+  __shared__ __attribute__((aligned(16))) bf16 xc[2 * XB_CB];
+  __shared__ __attribute__((aligned(16))) bf16 dys[TH * WMAX * COUT];
+  __shared__ __attribute__((aligned(16))) bf16 gzs[(TH / 2) * (WMAX / 2) * COUT];
+  __shared__ float bsum[4][2 * COUT];
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int gq = lane >> 4, col = lane & 15;
+  const int Hp = H >> 1, Wp = W >> 1, cpr = W >> 3, segs = W >> 4, mts = W >> 4;
+  const int grp = (int)blockIdx.x / R, rr = (int)blockIdx.x - grp * R;
+  const long long tpg = (long long)B * tps;                 // tiles of one BN group
+  const int t_begin = (int)(grp * tpg + (tpg * rr) / R), t_end = (int)(grp * tpg + (tpg * (rr + 1)) / R);
+
+  // y recompute: A = weights (rows (j, c)), B = 4 dwords of the natural rows (conv_c1p8_kernel);
+  // D lane = pixel (pair q + 8 rp, j) of a 2-row strip, channels 4 cs .. 4 cs + 3
+  bf16x8 aw;
+  {
+    const int m = lane & 15, jj = m >> 3, c = m & 7;
+    __bf16 e[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = 8 * gq + q, ky = k / 6, kx = k % 6 - jj;
+      const bool ok = k < 30 && kx >= 0 && kx < 5;
+      const float v = bf2f(wk[c * 32 + (ok ? ky * 5 + kx : 0)]);
+      e[q] = (__bf16)(ok ? v : 0.f);
+    }
+    aw = bf16x8{e[0], e[1], e[2], e[3], e[4], e[5], e[6], e[7]};
+  }
+  const int cs = gq & 1, jy = lane >> 5, qy = col & 7, rp = col >> 3;
+  float bv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bv[i] = bias ? bias[4 * cs + i] : 0.f;
+  int yo[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) yo[d] = boff(gq, d) + rp * ITWD + qy + 3;
+  // this block's group: BN coefficients of the lane's 4 channels
+  float sc[4], sf[4], mu[4], is[4], s1[4], s2[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int gc = grp * COUT + 4 * cs + i;
+    sc[i] = scale[gc]; sf[i] = shift[gc]; mu[i] = mean[gc]; is[i] = invstd[gc];
+    s1[i] = 0.f; s2[i] = 0.f;
+  }
+  // window position k = 2 rp + j of the lane's pixel; its partners k^1 (lane ^ 32), k^2
+  // (lane ^ 8, DPP row_ror:8), k^3: the lane routes the gradient iff its BN value is > 0, beats
+  // its earlier partners strictly and its later ones or ties (max-pool's first-max rule), as
+  // ints (ordered like the floats wherever one side is > 0): v > u <=> v >= u + 1
+  const int e1 = jy, e2 = rp;
+  // wgrad / Gram operands (c1p8_bwd_wgrad_kernel's): tap tiles tt = 0, 1
+  int bb[2], ba[2], bky[2];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    int t = 16 * tt + col;
+    if (t >= 30) t = 0;
+    const int ky = t / 6, k2 = t % 6 - 2;
+    bky[tt] = ky;
+    bb[tt] = k2 & 1;
+    ba[tt] = (k2 >= 0 ? k2 >> 1 : -1) + 1;
+  }
+  const bool ones = col == 14;                               // pair column 30: constant 1
+  // fp32 MFMA accumulators per tile, folded into float64 after every tile (the combine's
+  // cancellation amplifies the accumulation error of long fp32 chains)
+  double dacc[5][4];
+#pragma unroll
+  for (int b = 0; b < 5; ++b)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dacc[b][i] = 0.0;
+
+  // global loads one tile ahead: <= 2 input-row vectors and <= 2 pooled-gradient vectors
+  const int nxt = (TH + 4) * cpr, nwin = (TH / 2) * Wp;
+  int xr[2], xoff[2], goff[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int t = tid + 256 * s;
+    const int r = t / cpr, c = t - r * cpr;
+    xr[s] = t < nxt ? r : -(1 << 20);
+    xoff[s] = (r - 2) * W + 8 * c;
+    goff[s] = min(t, nwin - 1) * COUT;        // window (hp, wp) of the tile = row-major index
+  }
+  u4 xv[2], gv[2];
+  auto load = [&](int tile) {
+    const int n = tile / tps, ty0 = (tile - n * tps) * TH;
+    const bf16* xb = x + ((size_t)n * H + ty0) * W;
+    const bf16* gb = gz + ((size_t)n * Hp + (ty0 >> 1)) * Wp * COUT;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bool ok = (unsigned)(ty0 - 2 + xr[s]) < (unsigned)H;
+      xv[s] = ldg16(ok ? (const void*)(xb + xoff[s]) : &kZeroC1);
+      gv[s] = ldg16(gb + goff[s]);
+    }
+  };
+  if (t_begin < t_end) load(t_begin);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    __syncthreads();                     // the previous tile's MFMAs are done with LDS
+    // ---- natural rows (y recompute), parity/shift copies (B operand), pooled gradients
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int t = tid + 256 * s;
+      if (t < nwin) *reinterpret_cast<u4*>(&gzs[t * COUT]) = gv[s];
+      if (t >= nxt) continue;
+      const int r = t / cpr, c = t - r * cpr;
+      *reinterpret_cast<u4*>(xs + r * ITW + XOFF + 8 * c) = xv[s];
+      const unsigned wv[4] = {xv[s].x, xv[s].y, xv[s].z, xv[s].w};
+      const unsigned e0 = (wv[0] & 0xffffu) | (wv[1] << 16), ee1 = (wv[2] & 0xffffu) | (wv[3] << 16);
+      const unsigned o0 = (wv[0] >> 16) | (wv[1] & 0xffff0000u), o1 = (wv[2] >> 16) | (wv[3] & 0xffff0000u);
+      const unsigned ev[2] = {e0, ee1}, od[2] = {o0, o1};
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const unsigned lo = b ? od[0] : ev[0], hi = b ? od[1] : ev[1];
+        *reinterpret_cast<uint2*>(&xc[xbo(b, 1, r, 4 * c)]) = make_uint2(lo, hi);
+        bf16* d0 = &xc[xbo(b, 0, r, 4 * c + 1)];
+        st16(d0, (bf16)(lo & 0xffffu));
+        *reinterpret_cast<unsigned*>(d0 + 1) = (lo >> 16) | (hi << 16);
+        st16(d0 + 3, (bf16)(hi >> 16));
+        bf16* d2 = &xc[xbo(b, 2, r, 4 * c)];
+        if (c > 0) st16(d2 - 1, (bf16)(lo & 0xffffu));
+        *reinterpret_cast<unsigned*>(d2) = (lo >> 16) | (hi << 16);
+        st16(d2 + 2, (bf16)(hi >> 16));
+      }
+    }
+    if (tid < (TH + 4) * 2) {
+      const int r = tid >> 1, b = tid & 1;
+      xc[xbo(b, 0, r, 0)] = bf16(0);
+      xc[xbo(b, 2, r, Wp - 1)] = bf16(0);
+      *reinterpret_cast<u4*>(xs + r * ITW + (b ? XOFF + W : 0)) = u4{0u, 0u, 0u, 0u};
+    }
+    if (tile + 1 < t_end) load(tile + 1);   // in flight under this tile's work
+    __syncthreads();
+    // ---- y (bf16, as every other pass rounds it), the window's first-max routing across the
+    // 4 lanes of a window, BN sums on the routing lane, dz into dys (the wgrad A operand)
+    if (!(C1M_DIAG & 4)) {
+      const unsigned* xd = reinterpret_cast<const unsigned*>(xs);
+      for (int s = wave; s < TH / 2; s += 4) {
+        const int ry = 2 * s + rp;
+        for (int mt = 0; mt < mts; ++mt) {
+          const int base = 2 * s * ITWD + 8 * mt;
+          const u4 bw = u4{xd[base + yo[0]], xd[base + yo[1]], xd[base + yo[2]], xd[base + yo[3]]};
+          const f4 r4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, __builtin_bit_cast(bf16x8, bw),
+                                                                f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          const uint2 gw = *reinterpret_cast<const uint2*>(&gzs[(s * Wp + 8 * mt + qy) * COUT + 4 * cs]);
+          const float gg[4] = {__uint_as_float(gw.x << 16), __uint_as_float(gw.x & 0xffff0000u),
+                               __uint_as_float(gw.y << 16), __uint_as_float(gw.y & 0xffff0000u)};
+          float dz[4];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const uint32_t yb = pack_bf16x2(r4[2 * h] + bv[2 * h], r4[2 * h + 1] + bv[2 * h + 1]);
+            const float yy[2] = {__uint_as_float(yb << 16), __uint_as_float(yb & 0xffff0000u)};
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const int i = 2 * h + e;
+              const int vi = __float_as_int(fmaf(yy[e], sc[i], sf[i]));
+              const int p1 = __shfl_xor(vi, 32, 64);
+              const int u1 = p1 + e1, u2 = dpp_i<0x128>(vi) + e2, u3 = dpp_i<0x128>(p1) + e2;
+              const bool win = vi >= max(max(u1, u2), max(u3, 1));
+              dz[i] = win ? gg[i] : 0.f;
+              s1[i] += dz[i];
+              s2[i] = fmaf(dz[i], (yy[e] - mu[i]) * is[i], s2[i]);
+            }
+          }
+          const int cx = 16 * mt + 2 * qy + jy;
+          *reinterpret_cast<uint2*>(&dys[(ry * WMAX + dys_px(ry, cx, segs)) * COUT + 4 * cs]) =
+              make_uint2(pack_bf16x2(dz[0], dz[1]), pack_bf16x2(dz[2], dz[3]));
+        }
+      }
+    }
+    __syncthreads();
+    // ---- k-blocks of pixel pairs: D += dZ X (tap tiles 0, 1) and the Gram tiles (0,0) (0,1) (1,1)
+    const int nkb = (C1M_DIAG & 8) ? 0 : TH * segs;
+    f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+    f4 ga[3] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+    if (4 * wave < nkb) {
+      typedef __attribute__((ext_vector_type(8))) short s8;
+      const int q = col >> 2, pp = col & 3;
+      const int kb0 = 4 * wave + gq;
+      int r = kb0 / segs, sg = kb0 - r * segs;
+      const int hsw = (kb0 & 1) << 3;
+      const int aoff0 = ((2 * q) ^ hsw) * COUT + 4 * pp, aoff1 = ((8 + 2 * q) ^ hsw) * COUT + 4 * pp;
+      const int boff0 = xbo(bb[0], ba[0], bky[0], 0), boff1 = xbo(bb[1], ba[1], bky[1], 0);
+      const int dr = 16 / segs, dsg = 16 - dr * segs;
+      const u4 one4 = u4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+      s4 h0, h1;
+      u4 w0, w1;
+      auto ld = [&](s4& a0, s4& a1, u4& c0, u4& c1) {
+        const int P0 = 8 * sg, ab = (r * WMAX + 2 * P0) * COUT, bs = r * XB_RS + P0;
+        a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)&dys[ab + aoff0]);
+        a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)&dys[ab + aoff1]);
+        c0 = *reinterpret_cast<const u4*>(&xc[bs + boff0]);
+        c1 = *reinterpret_cast<const u4*>(&xc[bs + boff1]);
+      };
+      ld(h0, h1, w0, w1);
+      for (int ks = wave;; ks += 4) {
+        const bool more = 4 * (ks + 4) < nkb;
+        s4 n0, n1;
+        u4 v0, v1;
+        if (more) {
+          sg += dsg;
+          r += dr;
+          if (sg >= segs) { sg -= segs; ++r; }
+        }
+        ld(n0, n1, v0, v1);
+        const bf16x8 A = __builtin_bit_cast(bf16x8, s8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]});
+        const bf16x8 X0 = __builtin_bit_cast(bf16x8, w0);
+        const bf16x8 X1 = __builtin_bit_cast(bf16x8, ones ? one4 : w1);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, X0, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, X1, acc[1], 0, 0, 0);
+        if (!(C1M_DIAG & 2)) {
+          ga[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X0, X0, ga[0], 0, 0, 0);
+          ga[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X0, X1, ga[1], 0, 0, 0);
+          ga[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X1, X1, ga[2], 0, 0, 0);
+        }
+        if (!more) break;
+        h0 = n0; h1 = n1; w0 = v0; w1 = v1;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      dacc[0][i] += acc[0][i]; dacc[1][i] += acc[1][i];
+      dacc[2][i] += ga[0][i]; dacc[3][i] += ga[1][i]; dacc[4][i] += ga[2][i];
+    }
+  }
+  // ---- block outputs: BN sums (one row), then M / Gram / S folded from pairs to taps
+  // lanes of one channel half cs = (lane >> 4) & 1: sum over lane bits 0-3 and 5
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int m = 1; m <= 32; m <<= 1) {
+      if (m == 16) continue;
+      s1[i] += __shfl_xor(s1[i], m, 64);
+      s2[i] += __shfl_xor(s2[i], m, 64);
+    }
+  if ((lane & 47) == 0)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { bsum[wave][4 * cs + i] = s1[i]; bsum[wave][COUT + 4 * cs + i] = s2[i]; }
+  __syncthreads();                        // also: every wave is done with dys / xc
+  float* red = reinterpret_cast<float*>(dys);        // [4][16][32]  D
+  float* g6 = red + 4 * 16 * 32;                     // [4][32][32]  Gram tiles (upper blocks)
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[(wave * 16 + 4 * gq + i) * 32 + 16 * tt + col] = (float)dacc[tt][i];
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const int ti = b == 2 ? 1 : 0, tj = b == 0 ? 0 : 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      g6[(wave * 32 + 16 * ti + 4 * gq + i) * 32 + 16 * tj + col] = (float)dacc[2 + b][i];
+  }
+  __syncthreads();
+  if (tid < 2 * COUT) {
+    const int e = tid % COUT, k = tid / COUT;
+    const float v = bsum[0][tid] + bsum[1][tid] + bsum[2][tid] + bsum[3][tid];
+    out[(((size_t)e * G + grp) * R + rr) * 2 + k] = v;
+  }
+  float* o = out + (size_t)COUT * G * R * 2 + ((size_t)rr * G + grp) * MOM5;
+  auto g6v = [&](int t1, int t2) {        // the lower block (1,0) is the transpose of (0,1)
+    if (t1 >= 16 && t2 < 16) { const int tmp = t1; t1 = t2; t2 = tmp; }
+    float v = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < 4; ++wv) v += g6[(wv * 32 + t1) * 32 + t2];
+    return v;
+  };
+  for (int e = tid; e < MOM5; e += 256) {
+    float v;
+    if (e < COUT * 25) {
+      const int c = e / 25, t = e - c * 25, ky = t / 5, kx = t - ky * 5;
+      v = 0.f;
+#pragma unroll
+      for (int wv = 0; wv < 4; ++wv)
+        v += red[(wv * 16 + c) * 32 + ky * 6 + kx] + red[(wv * 16 + 8 + c) * 32 + ky * 6 + kx + 1];
+    } else if (e < COUT * 25 + 625) {
+      const int a = (e - COUT * 25) / 25, b = (e - COUT * 25) % 25;
+      const int pa = (a / 5) * 6 + a % 5, pb = (b / 5) * 6 + b % 5;
+      v = g6v(pa, pb) + g6v(pa + 1, pb + 1);      // even pixel of the pair, then the odd one
+    } else {
+      const int a = e - COUT * 25 - 625, pa = (a / 5) * 6 + a % 5;
+      v = g6v(pa, 30) + g6v(pa + 1, 30);
+    }
+    o[e] = v;
+  }
+}
+
+// dW [8][25] from the row-summed moments m [G][MOM5] and the BN-backward coefficients
+__global__ void c1p8_combine_kernel(const float* __restrict__ m, const float* __restrict__ coef,
+                                    const bf16* __restrict__ wk, const float* __restrict__ bias,
+                                    float* __restrict__ dw, int G) {
+  // float64: the kx and k0 terms are large and cancel (dy is centred by the BN backward), so
+  // they are formed and summed in double (fp32 here cost ~1e-3 relative in dW at bench size)
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= COUT * 25) return;
+  const int c = e / 25, t = e - c * 25;
+  double wr[25];
+#pragma unroll
+  for (int k = 0; k < 25; ++k) wr[k] = (double)bf2f(wk[c * 32 + k]);
+  const double b = bias ? (double)bias[c] : 0.0;
+  double acc = 0.0;
+  for (int g = 0; g < G; ++g) {
+    const float* mg = m + (size_t)g * MOM5;
+    const float* gram = mg + COUT * 25;
+    const double sx = gram[625 + t];
+    double sy = b * sx;
+#pragma unroll
+    for (int k = 0; k < 25; ++k) sy = fma(wr[k], (double)gram[k * 25 + t], sy);
+    const float* k3 = coef + ((size_t)g * COUT + c) * 3;
+    acc += (double)k3[0] * mg[e] + (double)k3[1] * sy + (double)k3[2] * sx;
+  }
+  dw[e] = (float)acc;
+}
+
+int c1p8_moment_rows(int N, int B) {
+  static int resident = 0;
+  if (!resident) {
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, c1p8_moments_kernel, 256, 0) !=
+            hipSuccess || per <= 0)
+      per = 2;
+    resident = cus * per;
+  }
+  const int G = N / B;
+  return std::max(1, std::min(grid_cap(resident) / G, B));   // one resident wave of blocks
+}
+
 }  // namespace
 
-// rows per BN group (stats / reduce passes) or slabs (wgrad pass)
+// rows per BN group (stats / reduce passes; moments pass 4: rows of both its outputs) or slabs
+// (wgrad pass)
 int avd_c1r_rows(int pass, int N, int B, int H) {
+  if (pass == 4) return c1p8_moment_rows(N, B);
   return pass == RC_WGRAD ? rc_wgrad_slabs(N, H) : B * 4;
+}
+
+int avd_c1p8_moment_cols() { return MOM5; }
+
+int avd_c1p8_combine(const float* m, const float* coef, const void* wk, const float* bias,
+                     float* dw, int G, hipStream_t st) {
+  c1p8_combine_kernel<<<avd_cdiv(COUT * 25, 64), 64, 0, st>>>(m, coef, (const bf16*)wk, bias, dw, G);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
 }
 
 int avd_c1r_launch(int pass, const void* x, const void* wk, const float* bias, const float* scale,
@@ -792,6 +1160,13 @@ int avd_c1r_launch(int pass, const void* x, const void* wk, const float* bias, c
                    const void* gz, void* z, float* out, int N, int B, int H, int W,
                    hipStream_t st) {
   const int tps = H / TH, ntiles = N * tps;
+  if (pass == 4) {
+    const int G = N / B, R = c1p8_moment_rows(N, B);
+    c1p8_moments_kernel<<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, scale, shift,
+                                               mean, invstd, (const bf16*)gz, out, B, G, R, H, W, tps);
+    AVD_CHECK_LAUNCH();
+    return AVD_OK;
+  }
   const int grid = pass == RC_WGRAD ? rc_wgrad_slabs(N, H) : N;
 #define AVD_RC(PS)                                                                             \
   c1p8_recompute_kernel<PS><<<grid, 256, 0, st>>>(                                             \

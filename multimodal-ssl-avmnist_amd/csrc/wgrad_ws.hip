@@ -495,7 +495,10 @@ int avd_wg_chunks(int N, int Cout, int Cin, int K) {
   else if (Cin == 16 && Cout == 32 && K == 5) occ = WgA3::OCC;
   else if (Cin == 32 && Cout == 64 && K == 5) occ = WgA4::OCC;
   else return 0;
-  return std::max(1, grid_cap(std::min(N, wg_cus() * occ)));
+  // AVDINO_WG_CU_PCT: percent of the CUs the persistent grid occupies (it runs on a side stream
+  // beside the input-gradient chain; fewer slabs leave CUs to that chain's kernels)
+  static const int pct = getenv("AVDINO_WG_CU_PCT") ? std::min(100, std::max(1, atoi(getenv("AVDINO_WG_CU_PCT")))) : 100;
+  return std::max(1, grid_cap(std::min(N, std::max(1, wg_cus() * pct / 100) * occ)));
 }
 
 // 1 = launched, 0 = not served, < 0 = error.  parts must hold avd_wg_chunks(...) slabs.

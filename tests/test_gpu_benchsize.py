@@ -177,6 +177,95 @@ def test_conv1_recompute_bench_size(ops):
             assert torch.equal(z0, z1)
 
 
+def test_conv1_moments_pass_bench_size(ops):
+    """The training backward of the audio conv1 without a stored y (pass 4 of
+    avd_cl_c1_recompute + combine) at N = 7168, ~100 tiles per block: its BN-backward sums equal
+    avd_cl_bn_bwd_reduce's (fp32 order), its patch Gram matrix and patch sums equal float64, and
+    dW is within the stored-y path's bf16 rounding of dy."""
+    N, B, H, C, K, pad = N_STUDENT, B_BENCH, 112, 8, 5, 2
+    G = N // B
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = rnd(g, (N, H, H, 1), 0, 1, T)
+    w = rnd(g, (C, 1, K, K)).to(T).float() / 5
+    bias = rnd(g, (C,), -0.1, 0.1)
+    wk = layout(ops, w, 0)
+    y = torch.empty(N, H, H, C, device="cuda", dtype=T)
+    R0 = ops.cl_stat_rows(H, H, B, K, 1, C, T)
+    st0 = torch.empty(C * G * R0 * 2, device="cuda")
+    ops.cl_conv_fwd(x, wk, bias, y, st0, N, B, 1, H, H, C, K, pad)
+    gamma, beta = rnd(g, (C,), 0.8, 1.2), rnd(g, (C,), -0.2, 0.2)
+    bn = torch.empty(4, G * C, device="cuda")
+    ops.bn_finalize(st0, G, R0, C, B * H * H, gamma, beta, bn[0], bn[1], bn[2], bn[3])
+    gz = rnd(g, (N, H // 2, H // 2, C), dtype=T)
+    Rb = ops.cl_bn_bwd_rows(B, C, H, H, T)
+    p0 = torch.empty(C * G * Rb * 2, device="cuda")
+    ops.cl_bn_bwd_reduce(y, gz, 0, bn[2], bn[3], bn[0], bn[1], p0, N, B, C, H, H)
+    coef = torch.empty(G * C * 3, device="cuda")
+    dg, dbt = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    ops.bn_bwd_finalize(p0, G, Rb, C, B * H * H, gamma, bn[0], bn[1], coef, dg, dbt, None)
+    ns = ops.cl_apply_wgrad_slabs(T, N, 1, H, H, C, K, pad)
+    f0 = torch.empty(ns * C * K * K, device="cuda")
+    ops.cl_bn_bwd_apply_wgrad(y, gz, bn[2], bn[3], coef, x, f0, N, B, 1, H, H, C, K, pad)
+    d0 = torch.empty(C * K * K, device="cuda")
+    ops.sum_rows(f0, ns, C * K * K, d0)
+    R4 = ops.cl_c1_recompute_rows(ops.C1_REDUCE_MOMENTS, T, N, B, 1, H, H, C, K, pad)
+    assert 0 < R4 and G * R4 * 20 < N * (H // 16), "persistent blocks with many tiles expected"
+    mc = ops.c1_moment_cols(C)
+    m4 = torch.full((C * G * R4 * 2 + R4 * G * mc,), float("nan"), device="cuda")
+    ops.cl_c1_recompute(ops.C1_REDUCE_MOMENTS, x, wk, bias, N, B, 1, H, H, C, K, pad, scale=bn[2],
+                        shift=bn[3], mean=bn[0], invstd=bn[1], gz=gz, out=m4)
+    r4 = m4[:C * G * R4 * 2].view(C, G, R4, 2).to(F64).sum(2)
+    r0 = p0.view(C, G, Rb, 2).to(F64).sum(2)
+    assert grel(r4, r0) < 1e-5, grel(r4, r0)
+    mom = torch.empty(G * mc, device="cuda")
+    ops.sum_rows(m4, R4, G * mc, mom, off=C * G * R4 * 2)
+    mh = mom.view(G, mc).to(F64)
+    # float64 moments: M = sum dz x25 (dz routed at the first max of relu(bn(y)) of the same
+    # bf16 y), Gram = sum x25 x25^T, S = sum x25, per BN group
+    gram = torch.zeros(G, 25, 25, device="cuda", dtype=F64)
+    sx = torch.zeros(G, 25, device="cuda", dtype=F64)
+    mz = torch.zeros(G, C, 25, device="cuda", dtype=F64)
+    sc, sf = bn[2].view(G, C).to(F64), bn[3].view(G, C).to(F64)
+    for a, b in _chunks(N, H * H * 25 * 2):
+        u = F.unfold(x[a:b].permute(0, 3, 1, 2).to(F64), K, padding=pad)     # [n, 25, H*H]
+        for gi in range(a // B, (b - 1) // B + 1):
+            lo, hi = max(a, gi * B) - a, min(b, (gi + 1) * B) - a
+            n = hi - lo
+            gram[gi] += torch.einsum("nip,njp->ij", u[lo:hi], u[lo:hi])
+            sx[gi] += u[lo:hi].sum((0, 2))
+            z = torch.relu(y[a + lo:a + hi].to(F64) * sc[gi] + sf[gi])
+            zw = z.view(n, H // 2, 2, H // 2, 2, C).permute(0, 1, 3, 5, 2, 4).reshape(n, H // 2, H // 2, C, 4)
+            best, am = zw.max(-1)
+            gzw = gz[a + lo:a + hi].to(F64)
+            dzw = torch.where((torch.arange(4, device="cuda") == am[..., None]) & (best[..., None] > 0),
+                              gzw[..., None], torch.zeros((), device="cuda", dtype=F64))
+            dz = dzw.view(n, H // 2, H // 2, C, 2, 2).permute(0, 1, 4, 2, 5, 3).reshape(n, H * H, C)
+            mz[gi] += torch.einsum("npc,ntp->ct", dz, u[lo:hi])
+    assert grel(mh[:, C * 25:C * 25 + 625].view(G, 25, 25), gram) < 1e-5
+    assert grel(mh[:, C * 25 + 625:], sx) < 1e-5
+    assert grel(mh[:, :C * 25].view(G, C, 25), mz) < 1e-5
+    d4 = torch.empty(C * K * K, device="cuda")
+    ops.cl_c1_recompute_combine(mom, coef, wk, bias, d4, G, C)
+    # dW of the moments formula in float64 (y = w . x25 + b unrounded in the kx term)
+    k3 = coef.view(G, C, 3).to(F64)
+    w64 = w.view(C, 25).to(T).to(F64)          # the bf16 weights both paths compute with
+    sy = torch.einsum("ct,gts->gcs", w64, gram) + bias.to(F64)[None, :, None] * sx[:, None, :]
+    dw64 = (k3[..., 0:1] * mz + k3[..., 1:2] * sy + k3[..., 2:3] * sx[:, None, :]).sum(0)
+    # the same formula on the kernel's moments (isolates the combine from the moment sums)
+    km, kg, ks = mh[:, :C * 25].view(G, C, 25), mh[:, C * 25:C * 25 + 625].view(G, 25, 25), mh[:, C * 25 + 625:]
+    ksy = torch.einsum("ct,gts->gcs", w64, kg) + bias.to(F64)[None, :, None] * ks[:, None, :]
+    dwk = (k3[..., 0:1] * km + k3[..., 1:2] * ksy + k3[..., 2:3] * ks[:, None, :]).sum(0)
+    print("moments rel: M", grel(km, mz), "Gram", grel(kg, gram), "S", grel(ks, sx),
+          "| dW: combine vs f64 formula on kernel moments", grel(d4, dwk), "kernel-moment dW vs f64",
+          grel(dwk, dw64), "vs stored-y", grel(d4, d0), "stored-y vs f64", grel(d0, dw64))
+    assert grel(d4, dw64) < 1e-4, grel(d4, dw64)
+    # the stored-y path rounds dy to bf16 before its weight gradient; dy is centred, so over
+    # 90M pixels that rounding shows in dW amplified by the cancellation (2.5 % measured): the
+    # moments pass is the more accurate of the two
+    assert grel(d4, d0) < 5e-2, grel(d4, d0)
+    assert grel(d0, dw64) < 5e-2
+
+
 # ---------------------------------------------------------------------------- mid layers
 # (Cin, H, Cout, K, pad, N): the CentralNet audio conv2-4 and image conv2 at bench-scale N
 WS_BENCH = [(8, 56, 16, 5, 2, 2048), (16, 28, 32, 5, 2, 2048), (32, 14, 64, 5, 2, 4096),
@@ -330,7 +419,9 @@ def test_ws_kernels_many_tiles_per_block(ops, shape, cap, monkeypatch):
 
     (y0, s0, dx0, dw0), (y1, s1, dx1, dw1) = _capped(monkeypatch, cap, run)
     assert torch.equal(y0, y1) and torch.equal(dx0, dx1)
-    assert grel(s1, s0) < 1e-6 and grel(dw1, dw0) < 5e-6     # fp32 sum order
+    # fp32 sum order: statistics are lane-local running sums over a block's tiles, so a cap of
+    # one block sums ~10^4 values per lane (sum of signed values: 2.2e-6 measured at cap 1)
+    assert grel(s1, s0) < 1e-5 and grel(dw1, dw0) < 5e-6
     assert grel(dw1, wgrad_ref(x, dy, K, pad)) < 1e-5
 
 

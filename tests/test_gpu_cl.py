@@ -311,12 +311,12 @@ def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN):
     ops.sum_rows(f1, nw, C * K * K, d1)
     assert rel(host(d1), host(d0)) < 1e-6
     R4 = ops.cl_c1_recompute_rows(ops.C1_REDUCE_MOMENTS, T, N, B, 1, H, H, C, K, pad)
-    if K != 3:
-        assert R4 == 0
-        return
+    assert R4 > 0
     # pass 4: the reduce rows of pass 2 plus the moments; dW = combine(moments, coef)
+    # (3x3: [C*9 | Gram rows 9 x 10 with the ones tap]; 5x5 audio conv1: [C*25 | 25 x 25 | 25])
+    KK = K * K
     mc = ops.c1_moment_cols(C)
-    m4 = torch.empty(C * G * R4 * 2 + R4 * G * mc, device="cuda")
+    m4 = torch.full((C * G * R4 * 2 + R4 * G * mc,), float("nan"), device="cuda")
     ops.cl_c1_recompute(ops.C1_REDUCE_MOMENTS, tx, wk, tb, N, B, 1, H, H, C, K, pad, scale=bn[2],
                         shift=bn[3], mean=bn[0], invstd=bn[1], gz=gz, out=m4)
     r4 = host(m4[:C * G * R4 * 2]).reshape(C, G, R4, 2).sum(2)
@@ -324,16 +324,20 @@ def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN):
     mom = torch.empty(G * mc, device="cuda")
     ops.sum_rows(m4, R4, G * mc, mom, off=C * G * R4 * 2)
     mh = host(mom).reshape(G, mc)
-    # the Gram block against float64 (exact products, f32 sums): sum x9_t x9_t' and sum x9_t
+    # the Gram block against float64 (exact products, f32 sums): sum xk_t xk_t' and sum xk_t
     win = np.lib.stride_tricks.sliding_window_view(
-        np.pad(nchw(x).astype(np.float64), ((0, 0), (0, 0), (1, 1), (1, 1))), (3, 3), (2, 3))
-    x9 = win.reshape(G, B, H, H, 9)
-    gram = np.einsum("gbhwi,gbhwj->gij", x9, x9)
-    assert rel(mh[:, C * 9:].reshape(G, 9, 10)[:, :, :9], gram) < 1e-5
-    assert rel(mh[:, C * 9:].reshape(G, 9, 10)[:, :, 9], x9.sum((1, 2, 3))) < 1e-5
-    d4 = torch.empty(C * 9, device="cuda")
-    ops.cl_c1_recompute_combine(mom, coef, wk, tb, d4, G, C)
-    # dW from the unrounded dy = k1 dz + kx y + k0 (y = w . x9 + b unrounded in the kx term):
+        np.pad(nchw(x).astype(np.float64), ((0, 0), (0, 0), (pad, pad), (pad, pad))), (K, K), (2, 3))
+    xk = win.reshape(G, B, H, H, KK)
+    gram = np.einsum("gbhwi,gbhwj->gij", xk, xk)
+    if K == 3:
+        gk, sk = mh[:, C * 9:].reshape(G, 9, 10)[:, :, :9], mh[:, C * 9:].reshape(G, 9, 10)[:, :, 9]
+    else:
+        gk, sk = mh[:, C * KK:C * KK + KK * KK].reshape(G, KK, KK), mh[:, C * KK + KK * KK:]
+    assert rel(gk, gram) < 1e-5, rel(gk, gram)
+    assert rel(sk, xk.sum((1, 2, 3))) < 1e-5
+    dk = torch.empty(C * KK, device="cuda")
+    ops.cl_c1_recompute_combine(mom, coef, wk, tb, dk, G, C)
+    # dW from the unrounded dy = k1 dz + kx y + k0 (y = w . xk + b unrounded in the kx term):
     # against float64 of exactly that, and within the bf16 rounding of dy of the stored-y path
     # (dy is centred, so its rounding shows in dW amplified by the cancellation: ~0.5 %)
     yb = host(y).astype(np.float64).reshape(G, B, H, H, C)
@@ -344,12 +348,13 @@ def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN):
     gzh = host(gz).astype(np.float64).reshape(G, B, H // 2, H // 2, C)
     dzw = np.where((np.arange(4) == am[..., None]) & (best[..., None] > 0), gzh[..., None], 0.0)
     dz = dzw.reshape(G, B, H // 2, H // 2, C, 2, 2).transpose(0, 1, 2, 5, 3, 6, 4).reshape(G, B, H, H, C)
-    yex = np.einsum("gbhwt,ct->gbhwc", x9, w.reshape(C, 9).astype(np.float64)) + b.astype(np.float64)
+    assert rel(mh[:, :C * KK].reshape(G, C, KK), np.einsum("gbhwc,gbhwt->gct", dz, xk)) < 1e-5
+    yex = np.einsum("gbhwt,ct->gbhwc", xk, w.reshape(C, KK).astype(np.float64)) + b.astype(np.float64)
     k3 = host(coef).astype(np.float64).reshape(G, 1, 1, 1, C, 3)
     dy64 = k3[..., 0] * dz + k3[..., 1] * yex + k3[..., 2]
-    dw64 = np.einsum("gbhwc,gbhwt->ct", dy64, x9)
-    e64 = rel(host(d4), dw64.reshape(-1))
-    err = rel(host(d4), host(d0))
+    dw64 = np.einsum("gbhwc,gbhwt->ct", dy64, xk)
+    e64 = rel(host(dk), dw64.reshape(-1))
+    err = rel(host(dk), host(d0))
     print("pass-4 dW rel: vs float64", e64, "vs stored-y path", err)
     assert e64 < 1e-4, e64
     assert err < 1e-2, err
