@@ -198,7 +198,7 @@ class ConvBranch:
     RC_MOMENTS = os.environ.get("AVDINO_L1_RC_MOMENTS", "1") == "1"
     # the 5x5 audio conv1 in training: no stored y either -- its backward is the one moments
     # pass (x and the pooled gradient in, BN-backward sums + dW moments out) and a combine
-    MOMENTS5 = os.environ.get("AVDINO_L1_MOMENTS5", "0") == "1"
+    MOMENTS5 = os.environ.get("AVDINO_L1_MOMENTS5", "1") == "1"
 
     def _recompute_ok(self, N, B, ci, H, co, k, pad, need_dgrad=True):
         rc = self.RECOMPUTE or (self.RECOMPUTE3 and k == 3) or (self.RC_NOGRAD and not need_dgrad)

@@ -802,12 +802,14 @@ constexpr int MOM5 = COUT * 25 + 25 * 25 + 25;
 #define C1M_DIAG 0   // diagnostic builds only: 1 no window math, 2 no Gram MFMAs, 4 no y MFMA, 8 no k-loop
 #endif
 
+typedef __attribute__((ext_vector_type(2))) float f2;
+
 template <int CTRL>
 __device__ __forceinline__ int dpp_i(int v) {
   return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
 }
 
-__global__ __launch_bounds__(256) void c1p8_moments_kernel(
+__global__ __launch_bounds__(256, 2) void c1p8_moments_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ wk, const float* __restrict__ bias,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -848,12 +850,12 @@ __global__ __launch_bounds__(256) void c1p8_moments_kernel(
 #pragma unroll
   for (int d = 0; d < 4; ++d) yo[d] = boff(gq, d) + rp * ITWD + qy + 3;
   // this block's group: BN coefficients of the lane's 4 channels
-  float sc[4], sf[4], mu[4], is[4], s1[4], s2[4];
+  float sc[4], sf[4];
+  f2 s1v[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}}, s2v[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int gc = grp * COUT + 4 * cs + i;
-    sc[i] = scale[gc]; sf[i] = shift[gc]; mu[i] = mean[gc]; is[i] = invstd[gc];
-    s1[i] = 0.f; s2[i] = 0.f;
+    sc[i] = scale[gc]; sf[i] = shift[gc];
   }
   // window position k = 2 rp + j of the lane's pixel; its partners k^1 (lane ^ 32), k^2
   // (lane ^ 8, DPP row_ror:8), k^3: the lane routes the gradient iff its BN value is > 0, beats
@@ -943,33 +945,54 @@ __global__ __launch_bounds__(256) void c1p8_moments_kernel(
     // ---- y (bf16, as every other pass rounds it), the window's first-max routing across the
     // 4 lanes of a window, BN sums on the routing lane, dz into dys (the wgrad A operand)
     if (!(C1M_DIAG & 4)) {
+      // per 2-row strip: every column tile's operands first (LDS reads in flight together),
+      // then the MFMAs, then the routing VALU -- the column-tile loop is unrolled (MTMAX)
       const unsigned* xd = reinterpret_cast<const unsigned*>(xs);
       for (int s = wave; s < TH / 2; s += 4) {
         const int ry = 2 * s + rp;
-        for (int mt = 0; mt < mts; ++mt) {
+        u4 bw[MTMAX];
+        uint2 gw[MTMAX];
+#pragma unroll
+        for (int mt = 0; mt < MTMAX; ++mt) {
+          if (mt >= mts) break;
           const int base = 2 * s * ITWD + 8 * mt;
-          const u4 bw = u4{xd[base + yo[0]], xd[base + yo[1]], xd[base + yo[2]], xd[base + yo[3]]};
-          const f4 r4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, __builtin_bit_cast(bf16x8, bw),
-                                                                f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          const uint2 gw = *reinterpret_cast<const uint2*>(&gzs[(s * Wp + 8 * mt + qy) * COUT + 4 * cs]);
-          const float gg[4] = {__uint_as_float(gw.x << 16), __uint_as_float(gw.x & 0xffff0000u),
-                               __uint_as_float(gw.y << 16), __uint_as_float(gw.y & 0xffff0000u)};
+          bw[mt] = u4{xd[base + yo[0]], xd[base + yo[1]], xd[base + yo[2]], xd[base + yo[3]]};
+          gw[mt] = *reinterpret_cast<const uint2*>(&gzs[(s * Wp + 8 * mt + qy) * COUT + 4 * cs]);
+        }
+        f4 r4[MTMAX];
+#pragma unroll
+        for (int mt = 0; mt < MTMAX; ++mt) {
+          if (mt >= mts) break;
+          r4[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, __builtin_bit_cast(bf16x8, bw[mt]),
+                                                           f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        }
+#pragma unroll
+        for (int mt = 0; mt < MTMAX; ++mt) {
+          if (mt >= mts) break;
+          const float gg[4] = {__uint_as_float(gw[mt].x << 16), __uint_as_float(gw[mt].x & 0xffff0000u),
+                               __uint_as_float(gw[mt].y << 16), __uint_as_float(gw[mt].y & 0xffff0000u)};
           float dz[4];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const uint32_t yb = pack_bf16x2(r4[2 * h] + bv[2 * h], r4[2 * h + 1] + bv[2 * h + 1]);
-            const float yy[2] = {__uint_as_float(yb << 16), __uint_as_float(yb & 0xffff0000u)};
+            const uint32_t yb = pack_bf16x2(r4[mt][2 * h] + bv[2 * h], r4[mt][2 * h + 1] + bv[2 * h + 1]);
+            const f2 yy = f2{__uint_as_float(yb << 16), __uint_as_float(yb & 0xffff0000u)};
+            const f2 bnv = __builtin_elementwise_fma(yy, f2{sc[2 * h], sc[2 * h + 1]}, f2{sf[2 * h], sf[2 * h + 1]});
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
               const int i = 2 * h + e;
-              const int vi = __float_as_int(fmaf(yy[e], sc[i], sf[i]));
-              const int p1 = __shfl_xor(vi, 32, 64);
+              const int vi = __float_as_int(bnv[e]);
+              // lane ^ 32 by the half swap: lanes < 32 get the upper half's value in r[1],
+              // lanes >= 32 the lower half's in r[0]
+              const auto sw = __builtin_amdgcn_permlane32_swap(vi, vi, false, false);
+              const int p1 = jy ? (int)sw[0] : (int)sw[1];
               const int u1 = p1 + e1, u2 = dpp_i<0x128>(vi) + e2, u3 = dpp_i<0x128>(p1) + e2;
               const bool win = vi >= max(max(u1, u2), max(u3, 1));
               dz[i] = win ? gg[i] : 0.f;
-              s1[i] += dz[i];
-              s2[i] = fmaf(dz[i], (yy[e] - mu[i]) * is[i], s2[i]);
             }
+            // sum dz and sum dz * y (xhat applied once at the end: (sum dz y - mean sum dz) * invstd)
+            const f2 d2 = f2{dz[2 * h], dz[2 * h + 1]};
+            s1v[h] += d2;
+            s2v[h] = __builtin_elementwise_fma(d2, yy, s2v[h]);
           }
           const int cx = 16 * mt + 2 * qy + jy;
           *reinterpret_cast<uint2*>(&dys[(ry * WMAX + dys_px(ry, cx, segs)) * COUT + 4 * cs]) =
@@ -1033,6 +1056,13 @@ __global__ __launch_bounds__(256) void c1p8_moments_kernel(
     }
   }
   // ---- block outputs: BN sums (one row), then M / Gram / S folded from pairs to taps
+  float s1[4], s2[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int gc = grp * COUT + 4 * cs + i;
+    s1[i] = s1v[i >> 1][i & 1];
+    s2[i] = (s2v[i >> 1][i & 1] - mean[gc] * s1[i]) * invstd[gc];
+  }
   // lanes of one channel half cs = (lane >> 4) & 1: sum over lane bits 0-3 and 5
 #pragma unroll
   for (int i = 0; i < 4; ++i)
