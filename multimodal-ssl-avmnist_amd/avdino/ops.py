@@ -41,7 +41,8 @@ class KernelTimer:
     timing to one key (the dominant kernel) so the timed region stays undisturbed."""
 
     def __init__(self, only=None):
-        self.only = only
+        # None: every instrumented launch; else one key or a set of keys
+        self.only = {only} if isinstance(only, str) else (set(only) if only is not None else None)
         self.rec = []  # (key, bytes, flops, start_event, end_event)
         self.replay = None  # last launch closure of the ``only`` key (bench --probe-dominant)
         self.fns = {}       # key -> last launch closure (tools/opbench.py replays them)
@@ -51,7 +52,7 @@ class KernelTimer:
         # the audio conv3 and image conv1 BN-backward apply share a shape): keyed apart
         if torch.cuda.current_stream() != torch.cuda.default_stream():
             key += " @side"
-        if self.only is not None and key != self.only:
+        if self.only is not None and key not in self.only:
             return fn()
         if self.only is not None:
             self.replay = fn
@@ -537,7 +538,12 @@ def cl_c1_recompute(pas, x, wk, bias, N, B, Cin, H, W, Cout, K, pad, scale=None,
         _need(gz is not None and gz.numel() == npool and gz.dtype == x.dtype, "c1 recompute gz")
     nb = x.numel() * x.element_size() + (npool * 2 if pas != C1_STATS else 0)
     name = ["stats", "apply", "reduce", "wgrad", "reduce_moments"][pas]
-    _timed(f"cl_c1_recompute_{name}[{N}x{H}x{W}x{Cin}->{Cout} k{K}]", nb, 2 * N * H * W * Cout * K * K,
+    # MFMA work: the y recompute; the weight-gradient passes also dY x (or dz x), and pass 4 the
+    # patch Gram matrix (KK x (KK + 1) per output pixel, the ones column included)
+    KK = K * K
+    fl = 2 * N * H * W * (Cout * KK * (2 if pas in (C1_WGRAD, C1_REDUCE_MOMENTS) else 1) +
+                          (KK * (KK + 1) if pas == C1_REDUCE_MOMENTS else 0))
+    _timed(f"cl_c1_recompute_{name}[{N}x{H}x{W}x{Cin}->{Cout} k{K}]", nb, fl,
            lambda: call("avd_cl_c1_recompute", pas, p(x), p(wk), p(bias), p(scale), p(shift), p(mean),
                         p(invstd), p(coef), p(gz), p(z), p(out), dtcode(x), N, B, Cin, H, W, Cout, K,
                         pad, stream()))
