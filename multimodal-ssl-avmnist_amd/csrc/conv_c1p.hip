@@ -17,6 +17,7 @@
 // pixel (pair l&15, j = l>>5), channels 4*((l>>4)&1) .. +3 -> one 8-byte NHWC store.
 // A 16-pixel-wide, 2-row strip is one MFMA column tile: pairs 0-7 = row 0, 8-15 = row 1.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -1163,8 +1164,11 @@ int c1p8_moment_rows(int N, int B) {
       per = 2;
     resident = cus * per;
   }
+  // several waves of blocks: beside the concurrent streams' persistent kernels a block may start
+  // late, and shorter blocks bound that tail (AVDINO_C1M_WAVES, default 8)
+  static const int waves = getenv("AVDINO_C1M_WAVES") ? std::max(1, atoi(getenv("AVDINO_C1M_WAVES"))) : 8;
   const int G = N / B;
-  return std::max(1, std::min(grid_cap(resident) / G, B));   // one resident wave of blocks
+  return std::max(1, std::min(grid_cap(resident * waves) / G, B));
 }
 
 }  // namespace
