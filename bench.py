@@ -252,10 +252,12 @@ def main():
     eng.use_graph = use_graph
     eng.graph.warmup = min(2, max(args.warmup - 1, 0))
     ops.TIMER = None
+    wtimer = None
     for i in range(args.warmup):
         ops.TIMER = ops.KernelTimer() if i == min(1, args.warmup - 1) else None
+        wtimer = ops.TIMER or wtimer
         eng.step(pool[i % len(pool)])
-    summ = ops.TIMER.summary() if (args.warmup and ops.TIMER is not None) else {}
+    summ = wtimer.summary() if wtimer is not None else {}
     dominant = max(summ, key=lambda k: summ[k]["ms"]) if summ else None
     if args.dominant:
         if args.dominant not in summ:
