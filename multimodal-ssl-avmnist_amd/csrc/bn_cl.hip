@@ -9,6 +9,7 @@
 //   mode 2: out = pooled map flattened in the reference's (c, h, w) order, f32 [N][C*Hp*Wp]
 //           (the input of the encoder's Linear, dino.py:459-468)
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -368,6 +369,96 @@ __global__ __launch_bounds__(256) void bwd_reduce_pooled_cl_kernel(
   }
 }
 
+__device__ __forceinline__ float to_f(bf16 v) { return bf2f(v); }
+__device__ __forceinline__ float to_f(float v) { return v; }
+
+// Mode 2 of the kernel above (pooled map and gradient f32 in the (c, h, w) flatten order of the
+// encoder Linear's input): one wave per channel, lanes over the channel's Hp*Wp <= 64 pooled
+// positions -- each sample's plane is a contiguous 4*Hp*Wp-byte run, so the loads coalesce
+// (the generic path reads 8 planes 4*Hp*Wp bytes apart per thread, with 64-bit index
+// divisions).  Block (r, g, channel quad): samples [r*B/R, (r+1)*B/R) of group g, same rows as
+// bwd_reduce_pooled_cl_kernel.  Channels whose xhat needs y take it at the window argmax of y.
+template <typename T>
+__global__ __launch_bounds__(256) void bwd_reduce_pooled_m2_kernel(
+    const T* __restrict__ y, const float* __restrict__ pooled, const float* __restrict__ gout,
+    const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ parts,
+    int G, int B, int C, int H, int W, int R) {
+  const int lane = threadIdx.x & 63, c = blockIdx.z * 4 + (threadIdx.x >> 6);
+  const int r = blockIdx.x, g = blockIdx.y;
+  const int Hp = H / 2, Wp = W / 2, HW = Hp * Wp;
+  if (c >= C) return;
+  const int n0 = g * B + (int)(((long long)r * B) / R), n1 = g * B + (int)(((long long)(r + 1) * B) / R);
+  const float ga = gamma[c], bb = beta[c];
+  const bool use_y = ga == 0.f || fabsf(bb) > (sizeof(T) == 2 ? 8.f : 4096.f) * fabsf(ga);
+  const float ig = use_y ? 0.f : 1.f / ga, gs = ga > 0.f ? 1.f : (ga < 0.f ? -1.f : 0.f);
+  const float mu = mean[g * C + c], is = invstd[g * C + c];
+  float s1 = 0.f, s2 = 0.f;
+  for (int p0 = 0; p0 < HW; p0 += 64) {
+    const int p = p0 + lane;
+    if (p >= HW) continue;
+    const int hp = p / Wp, wp = p - hp * Wp;
+    int n = n0;
+    // 4 samples' loads in flight per lane, summed in sample order
+    for (; n + 4 <= n1; n += 4) {
+      float pv[4], gv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const size_t o = ((size_t)(n + k) * C + c) * HW + p;
+        pv[k] = pooled[o];
+        gv[k] = gout[o];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float dz = pv[k] > 0.f ? gv[k] : 0.f;
+        float xh = (pv[k] - bb) * ig;
+        if (use_y) {
+          const T* yw = y + (((size_t)(n + k) * H + 2 * hp) * W + 2 * wp) * C + c;
+          float yv[4];
+          yv[0] = to_f(yw[0]); yv[1] = to_f(yw[C]);
+          yv[2] = to_f(yw[(size_t)W * C]); yv[3] = to_f(yw[(size_t)W * C + C]);
+          xh = (yv[0] - mu) * is;
+          if (gs != 0.f)
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+              const float cq = (yv[q] - mu) * is;
+              if (gs * cq > gs * xh) xh = cq;
+            }
+        }
+        s1 += dz;
+        s2 += dz * xh;
+      }
+    }
+    for (; n < n1; ++n) {
+      const size_t o = ((size_t)n * C + c) * HW + p;
+      const float pv = pooled[o], gv = gout[o];
+      const float dz = pv > 0.f ? gv : 0.f;
+      float xh = (pv - bb) * ig;
+      if (use_y) {
+        const T* yw = y + (((size_t)n * H + 2 * hp) * W + 2 * wp) * C + c;
+        float yv[4];
+        yv[0] = to_f(yw[0]); yv[1] = to_f(yw[C]);
+        yv[2] = to_f(yw[(size_t)W * C]); yv[3] = to_f(yw[(size_t)W * C + C]);
+        xh = (yv[0] - mu) * is;
+        if (gs != 0.f)
+#pragma unroll
+          for (int q = 1; q < 4; ++q) {
+            const float cq = (yv[q] - mu) * is;
+            if (gs * cq > gs * xh) xh = cq;
+          }
+      }
+      s1 += dz;
+      s2 += dz * xh;
+    }
+  }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (lane == 0) {
+    parts[(((size_t)c * G + g) * R + r) * 2] = s1;
+    parts[(((size_t)c * G + g) * R + r) * 2 + 1] = s2;
+  }
+}
+
 // dy = k1 * dz + kx * y + k0 for every pixel (incl. rows/cols outside the floor-mode windows)
 template <typename T>
 __global__ __launch_bounds__(256) void bwd_apply_cl_kernel(
@@ -523,6 +614,19 @@ int avd_cl_bn_bwd_reduce_pooled_impl(const void* y, int dt, const void* pooled, 
   const long long nwin = (long long)B * (H / 2) * (W / 2);
   const long long per = (nwin + R - 1) / R;
   dim3 grid(R, G);
+  if (mode == 2 && R <= B && !getenv("AVDINO_REDUCE_M2_GENERIC")) {
+    const dim3 g2(R, G, (C + 3) / 4);
+    if (dt == AVD_BF16)
+      bwd_reduce_pooled_m2_kernel<bf16><<<g2, 256, 0, st>>>((const bf16*)y, (const float*)pooled,
+                                                            (const float*)gout, gamma, beta, mean,
+                                                            invstd, parts, G, B, C, H, W, R);
+    else
+      bwd_reduce_pooled_m2_kernel<float><<<g2, 256, 0, st>>>((const float*)y, (const float*)pooled,
+                                                             (const float*)gout, gamma, beta, mean,
+                                                             invstd, parts, G, B, C, H, W, R);
+    AVD_CHECK_LAUNCH();
+    return AVD_OK;
+  }
   if (dt == AVD_BF16)
     bwd_reduce_pooled_cl_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)y, pooled, gout, mode, gamma,
                                                             beta, mean, invstd, parts, G, B, C, H, W,

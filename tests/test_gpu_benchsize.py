@@ -308,6 +308,41 @@ def test_ws_kernels_bench_size(ops, shape):
     assert grel(dw, wgrad_ref(x, dy, K, pad)) < 1e-5
 
 
+@pytest.mark.parametrize("HC", [(14, 64), (10, 64)])
+def test_bn_bwd_reduce_pooled_mode2_bench_size(ops, HC, monkeypatch):
+    """The encoder tails' BN-backward sums from the (c, h, w)-flattened pooled map and gradient
+    (bwd_reduce_pooled_m2_kernel: a wave per channel, coalesced planes) at N = 7168 against the
+    generic pooled kernel and float64 of sum dz, sum dz * xhat."""
+    H, C = HC
+    N, B = N_STUDENT, B_BENCH
+    G, Hp = N // B, H // 2
+    g = torch.Generator(device="cuda").manual_seed(11 + H)
+    y = (torch.randn(N, H, H, C, generator=g, device="cuda") * 0.8).to(T)
+    gamma, beta = rnd(g, (C,), 0.5, 1.5), rnd(g, (C,), -0.2, 0.2)
+    yf = y.to(F64).view(G, -1, C)
+    mean = yf.mean(1).float().reshape(-1).contiguous()
+    invstd = (yf.var(1, unbiased=False) + 1e-5).rsqrt().float().reshape(-1).contiguous()
+    scale = (gamma.view(1, C) * invstd.view(G, C)).reshape(-1).contiguous()
+    shift = (beta.view(1, C) - mean.view(G, C) * scale.view(G, C)).reshape(-1).contiguous()
+    pooled = torch.empty(N * C * Hp * Hp, device="cuda")
+    ops.cl_bn_relu_pool(y, scale, shift, pooled, 2, N, B, C, H, H)
+    gout = torch.randn(N * C * Hp * Hp, generator=g, device="cuda")
+    R = ops.cl_bn_bwd_rows(B, C, H, H, T)
+    p1 = torch.full((C * G * R * 2,), float("nan"), device="cuda")
+    ops.cl_bn_bwd_reduce_pooled(y, pooled, gout, 2, gamma, beta, mean, invstd, p1, N, B, C, H, H)
+    monkeypatch.setenv("AVDINO_REDUCE_M2_GENERIC", "1")
+    p0 = torch.full((C * G * R * 2,), float("nan"), device="cuda")
+    ops.cl_bn_bwd_reduce_pooled(y, pooled, gout, 2, gamma, beta, mean, invstd, p0, N, B, C, H, H)
+    s1 = p1.view(C, G, R, 2).to(F64).sum(2)
+    s0 = p0.view(C, G, R, 2).to(F64).sum(2)
+    assert grel(s1, s0) < 1e-5, grel(s1, s0)
+    pv, gv = pooled.to(F64).view(G, B, C, -1), gout.to(F64).view(G, B, C, -1)
+    dz = torch.where(pv > 0, gv, torch.zeros_like(gv))
+    xh = (pv - beta.to(F64).view(1, 1, C, 1)) / gamma.to(F64).view(1, 1, C, 1)
+    assert grel(s1[..., 0], dz.sum((1, 3)).T) < 1e-5
+    assert grel(s1[..., 1], (dz * xh).sum((1, 3)).T) < 1e-5
+
+
 # ------------------------------------------------------- dgrad + previous layer's BN-backward sums
 def _prev_layer(ops, g, N, B, Ci, H, small_gamma=False):
     """The previous layer's BN -> ReLU -> pool over a random conv output yprev [N,2H,2H,Ci]:

@@ -1,0 +1,10 @@
+#!/bin/bash
+# mode-2 pooled BN-backward reduce: tests and same-box A/B vs the generic kernel
+TAG=$1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
+    tests/test_gpu_cl.py -k "reduce_pooled" tests/test_gpu_benchsize.py -k "mode2 or reduce_pooled" tests/test_gpu_step.py > gpurun_out/t_$TAG.log 2>&1
+rc=$?; echo "tests rc=$rc"; grep -aE "^E  |passed|failed|FAILED" gpurun_out/t_$TAG.log | cut -c1-300 | head -20
+[ $rc -eq 0 ] || exit $rc
+bash tools/gpu_ab3.sh $TAG - AVDINO_REDUCE_M2_GENERIC=1
