@@ -850,19 +850,15 @@ __global__ __launch_bounds__(256, 2) void c1p8_moments_kernel(
   int yo[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) yo[d] = boff(gq, d) + rp * ITWD + qy + 3;
-  // this block's group: BN coefficients of the lane's 4 channels
-  float sc[4], sf[4];
-  f2 s1v[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}}, s2v[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
+  // this block's group: BN coefficients; per-thread sums over its pooling windows (all 8
+  // channels): sum dz and sum dz * y (xhat applied once at the end)
+  float sc[COUT], sf[COUT], s1[COUT], s2[COUT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int gc = grp * COUT + 4 * cs + i;
-    sc[i] = scale[gc]; sf[i] = shift[gc];
+  for (int e = 0; e < COUT; ++e) {
+    sc[e] = scale[grp * COUT + e];
+    sf[e] = shift[grp * COUT + e];
+    s1[e] = 0.f; s2[e] = 0.f;
   }
-  // window position k = 2 rp + j of the lane's pixel; its partners k^1 (lane ^ 32), k^2
-  // (lane ^ 8, DPP row_ror:8), k^3: the lane routes the gradient iff its BN value is > 0, beats
-  // its earlier partners strictly and its later ones or ties (max-pool's first-max rule), as
-  // ints (ordered like the floats wherever one side is > 0): v > u <=> v >= u + 1
-  const int e1 = jy, e2 = rp;
   // wgrad / Gram operands (c1p8_bwd_wgrad_kernel's): tap tiles tt = 0, 1
   int bb[2], ba[2], bky[2];
 #pragma unroll
@@ -943,63 +939,85 @@ __global__ __launch_bounds__(256, 2) void c1p8_moments_kernel(
     }
     if (tile + 1 < t_end) load(tile + 1);   // in flight under this tile's work
     __syncthreads();
-    // ---- y (bf16, as every other pass rounds it), the window's first-max routing across the
-    // 4 lanes of a window, BN sums on the routing lane, dz into dys (the wgrad A operand)
+    // ---- y (bf16, as every other pass rounds it) into dys at the wgrad A-operand positions:
+    // per 2-row strip every column tile's operands first, then the MFMAs, then the stores
     if (!(C1M_DIAG & 4)) {
-      // per 2-row strip: every column tile's operands first (LDS reads in flight together),
-      // then the MFMAs, then the routing VALU -- the column-tile loop is unrolled (MTMAX)
       const unsigned* xd = reinterpret_cast<const unsigned*>(xs);
       for (int s = wave; s < TH / 2; s += 4) {
         const int ry = 2 * s + rp;
         u4 bw[MTMAX];
-        uint2 gw[MTMAX];
 #pragma unroll
         for (int mt = 0; mt < MTMAX; ++mt) {
           if (mt >= mts) break;
           const int base = 2 * s * ITWD + 8 * mt;
           bw[mt] = u4{xd[base + yo[0]], xd[base + yo[1]], xd[base + yo[2]], xd[base + yo[3]]};
-          gw[mt] = *reinterpret_cast<const uint2*>(&gzs[(s * Wp + 8 * mt + qy) * COUT + 4 * cs]);
-        }
-        f4 r4[MTMAX];
-#pragma unroll
-        for (int mt = 0; mt < MTMAX; ++mt) {
-          if (mt >= mts) break;
-          r4[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, __builtin_bit_cast(bf16x8, bw[mt]),
-                                                           f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         }
 #pragma unroll
         for (int mt = 0; mt < MTMAX; ++mt) {
           if (mt >= mts) break;
-          const float gg[4] = {__uint_as_float(gw[mt].x << 16), __uint_as_float(gw[mt].x & 0xffff0000u),
-                               __uint_as_float(gw[mt].y << 16), __uint_as_float(gw[mt].y & 0xffff0000u)};
-          float dz[4];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const uint32_t yb = pack_bf16x2(r4[mt][2 * h] + bv[2 * h], r4[mt][2 * h + 1] + bv[2 * h + 1]);
-            const f2 yy = f2{__uint_as_float(yb << 16), __uint_as_float(yb & 0xffff0000u)};
-            const f2 bnv = __builtin_elementwise_fma(yy, f2{sc[2 * h], sc[2 * h + 1]}, f2{sf[2 * h], sf[2 * h + 1]});
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const int i = 2 * h + e;
-              const int vi = __float_as_int(bnv[e]);
-              // lane ^ 32 by the half swap: lanes < 32 get the upper half's value in r[1],
-              // lanes >= 32 the lower half's in r[0]
-              const auto sw = __builtin_amdgcn_permlane32_swap(vi, vi, false, false);
-              const int p1 = jy ? (int)sw[0] : (int)sw[1];
-              const int u1 = p1 + e1, u2 = dpp_i<0x128>(vi) + e2, u3 = dpp_i<0x128>(p1) + e2;
-              const bool win = vi >= max(max(u1, u2), max(u3, 1));
-              dz[i] = win ? gg[i] : 0.f;
-            }
-            // sum dz and sum dz * y (xhat applied once at the end: (sum dz y - mean sum dz) * invstd)
-            const f2 d2 = f2{dz[2 * h], dz[2 * h + 1]};
-            s1v[h] += d2;
-            s2v[h] = __builtin_elementwise_fma(d2, yy, s2v[h]);
-          }
+          const f4 r4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, __builtin_bit_cast(bf16x8, bw[mt]),
+                                                                f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
           const int cx = 16 * mt + 2 * qy + jy;
           *reinterpret_cast<uint2*>(&dys[(ry * WMAX + dys_px(ry, cx, segs)) * COUT + 4 * cs]) =
-              make_uint2(pack_bf16x2(dz[0], dz[1]), pack_bf16x2(dz[2], dz[3]));
+              make_uint2(pack_bf16x2(r4[0] + bv[0], r4[1] + bv[1]), pack_bf16x2(r4[2] + bv[2], r4[3] + bv[3]));
         }
       }
+    }
+    __syncthreads();
+    // ---- one thread per pooling window: first-max routing, BN sums, dz in place of y
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int w = tid + 256 * s;
+      if (w >= nwin || (C1M_DIAG & 1)) continue;
+      const int hp = w / Wp, wp = w - hp * Wp;
+      int po[4];
+      float yv[4][COUT];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int ry = 2 * hp + (k >> 1), cx = 2 * wp + (k & 1);
+        po[k] = (ry * WMAX + dys_px(ry, cx, segs)) * COUT;
+        const u4 v = *reinterpret_cast<const u4*>(&dys[po[k]]);
+        const unsigned wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          yv[k][2 * i] = __uint_as_float(wv[i] << 16);
+          yv[k][2 * i + 1] = __uint_as_float(wv[i] & 0xffff0000u);
+        }
+      }
+      const u4 gvw = *reinterpret_cast<const u4*>(&gzs[w * COUT]);
+      float gg[COUT];
+      {
+        const unsigned wv[4] = {gvw.x, gvw.y, gvw.z, gvw.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          gg[2 * i] = __uint_as_float(wv[i] << 16);
+          gg[2 * i + 1] = __uint_as_float(wv[i] & 0xffff0000u);
+        }
+      }
+      uint32_t ow[4][4];
+#pragma unroll
+      for (int e = 0; e < COUT; ++e) {
+        float rv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rv[k] = fmaxf(fmaf(yv[k][e], sc[e], sf[e]), 0.f);
+        const float m = fmaxf(fmaxf(rv[0], rv[1]), fmaxf(rv[2], rv[3]));
+        const bool e0 = rv[0] == m, e1 = !e0 && rv[1] == m, e2 = !e0 && !e1 && rv[2] == m;
+        const float dz = m > 0.f ? gg[e] : 0.f;
+        const float ya = e0 ? yv[0][e] : e1 ? yv[1][e] : e2 ? yv[2][e] : yv[3][e];
+        s1[e] += dz;
+        s2[e] = fmaf(dz, ya, s2[e]);
+        // dz (exact in bf16: a pooled gradient or zero) at the first max, 0 elsewhere
+        const uint32_t db = __float_as_uint(dz) >> 16;
+        const uint32_t d[4] = {e0 ? db : 0u, e1 ? db : 0u, e2 ? db : 0u, (!e0 && !e1 && !e2) ? db : 0u};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (e & 1) ow[k][e >> 1] |= d[k] << 16;
+          else ow[k][e >> 1] = d[k];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        *reinterpret_cast<u4*>(&dys[po[k]]) = u4{ow[k][0], ow[k][1], ow[k][2], ow[k][3]};
     }
     __syncthreads();
     // ---- k-blocks of pixel pairs: D += dZ X (tap tiles 0, 1) and the Gram tiles (0,0) (0,1) (1,1)
@@ -1057,25 +1075,16 @@ __global__ __launch_bounds__(256, 2) void c1p8_moments_kernel(
     }
   }
   // ---- block outputs: BN sums (one row), then M / Gram / S folded from pairs to taps
-  float s1[4], s2[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int gc = grp * COUT + 4 * cs + i;
-    s1[i] = s1v[i >> 1][i & 1];
-    s2[i] = (s2v[i >> 1][i & 1] - mean[gc] * s1[i]) * invstd[gc];
+  for (int e = 0; e < COUT; ++e) {
+    const int gc = grp * COUT + e;
+    const float a1 = wave_sum(s1[e]), a2 = wave_sum(s2[e]);
+    s1[e] = a1;
+    s2[e] = (a2 - mean[gc] * a1) * invstd[gc];       // sum dz * xhat
   }
-  // lanes of one channel half cs = (lane >> 4) & 1: sum over lane bits 0-3 and 5
+  if (lane == 0)
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int m = 1; m <= 32; m <<= 1) {
-      if (m == 16) continue;
-      s1[i] += __shfl_xor(s1[i], m, 64);
-      s2[i] += __shfl_xor(s2[i], m, 64);
-    }
-  if ((lane & 47) == 0)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { bsum[wave][4 * cs + i] = s1[i]; bsum[wave][COUT + 4 * cs + i] = s2[i]; }
+    for (int e = 0; e < COUT; ++e) { bsum[wave][e] = s1[e]; bsum[wave][COUT + e] = s2[e]; }
   __syncthreads();                        // also: every wave is done with dys / xc
   float* red = reinterpret_cast<float*>(dys);        // [4][16][32]  D
   float* g6 = red + 4 * 16 * 32;                     // [4][32][32]  Gram tiles (upper blocks)
@@ -1151,6 +1160,125 @@ __global__ void c1p8_combine_kernel(const float* __restrict__ m, const float* __
   dw[e] = (float)acc;
 }
 
+// The forward BN -> ReLU -> 2x2 max-pool pass (RC_APPLY) with the pooling done in registers:
+// y by the pixel-pair MFMA, relu(y * scale + shift) and the window max across the 4 lanes that
+// hold the window's pixels (v_permlane32_swap + DPP row_ror:8, as the moments pass), bf16
+// rounding of the max (= the max of the rounded values: rounding is monotone), one 8-byte store
+// per window and channel half -- no y tile in LDS, no per-window thread phase.  One block per
+// sample; bit-identical z to c1p8_recompute_kernel<RC_APPLY>.
+__global__ __launch_bounds__(256) void c1p8_apply_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ wk, const float* __restrict__ bias,
+    const float* __restrict__ scale, const float* __restrict__ shift, bf16* __restrict__ z,
+    int B, int H, int W, int tps) {
+  __shared__ __attribute__((aligned(16))) bf16 xs[(TH + 4) * ITW];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int gq = lane >> 4, col = lane & 15;
+  const int n = blockIdx.x, grp = n / B;
+  const int Hp = H >> 1, Wp = W >> 1, cpr = W >> 3, mts = W >> 4;
+  bf16x8 aw;
+  {
+    const int m = lane & 15, jj = m >> 3, c = m & 7;
+    __bf16 e[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = 8 * gq + q, ky = k / 6, kx = k % 6 - jj;
+      const bool ok = k < 30 && kx >= 0 && kx < 5;
+      const float v = bf2f(wk[c * 32 + (ok ? ky * 5 + kx : 0)]);
+      e[q] = (__bf16)(ok ? v : 0.f);
+    }
+    aw = bf16x8{e[0], e[1], e[2], e[3], e[4], e[5], e[6], e[7]};
+  }
+  const int cs = gq & 1, jy = lane >> 5, qy = col & 7, rp = col >> 3;
+  float bv[4], sc[4], sf[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    bv[i] = bias ? bias[4 * cs + i] : 0.f;
+    sc[i] = scale[grp * COUT + 4 * cs + i];
+    sf[i] = shift[grp * COUT + 4 * cs + i];
+  }
+  int yo[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) yo[d] = boff(gq, d) + rp * ITWD + qy + 3;
+  const bool writer = jy == 0 && rp == 0;        // window pixel (0, 0) stores the max
+  const int nxt = (TH + 4) * cpr;
+  int xr[2], xoff[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int t = tid + 256 * s;
+    const int r = t / cpr, c = t - r * cpr;
+    xr[s] = t < nxt ? r : -(1 << 20);
+    xoff[s] = (r - 2) * W + 8 * c;
+  }
+  u4 xv[2];
+  auto load_x = [&](int ty0) {
+    const bf16* xb = x + ((size_t)n * H + ty0) * W;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bool ok = (unsigned)(ty0 - 2 + xr[s]) < (unsigned)H;
+      xv[s] = ldg16(ok ? (const void*)(xb + xoff[s]) : &kZeroC1);
+    }
+  };
+  load_x(0);
+  for (int tile = 0; tile < tps; ++tile) {
+    const int ty0 = tile * TH;
+    if (tile) __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int t = tid + 256 * s;
+      if (t < nxt) {
+        const int r = t / cpr, c = t - r * cpr;
+        *reinterpret_cast<u4*>(xs + r * ITW + XOFF + 8 * c) = xv[s];
+      }
+    }
+    if (tid < (TH + 4) * 2) {
+      const int r = tid >> 1, side = tid & 1;
+      *reinterpret_cast<u4*>(xs + r * ITW + (side ? XOFF + W : 0)) = u4{0u, 0u, 0u, 0u};
+    }
+    if (tile + 1 < tps) load_x(ty0 + TH);
+    __syncthreads();
+    const unsigned* xd = reinterpret_cast<const unsigned*>(xs);
+    for (int s = wave; s < TH / 2; s += 4) {
+      u4 bw[MTMAX];
+#pragma unroll
+      for (int mt = 0; mt < MTMAX; ++mt) {
+        if (mt >= mts) break;
+        const int base = 2 * s * ITWD + 8 * mt;
+        bw[mt] = u4{xd[base + yo[0]], xd[base + yo[1]], xd[base + yo[2]], xd[base + yo[3]]};
+      }
+      f4 r4[MTMAX];
+#pragma unroll
+      for (int mt = 0; mt < MTMAX; ++mt) {
+        if (mt >= mts) break;
+        r4[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, __builtin_bit_cast(bf16x8, bw[mt]),
+                                                         f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      }
+      bf16* zrow = z + ((size_t)n * Hp + (ty0 >> 1) + s) * Wp * COUT + 4 * cs;
+#pragma unroll
+      for (int mt = 0; mt < MTMAX; ++mt) {
+        if (mt >= mts) break;
+        float m[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t yb = pack_bf16x2(r4[mt][2 * h] + bv[2 * h], r4[mt][2 * h + 1] + bv[2 * h + 1]);
+          const float yy[2] = {__uint_as_float(yb << 16), __uint_as_float(yb & 0xffff0000u)};
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int i = 2 * h + e;
+            const float v = fmaxf(fmaf(yy[e], sc[i], sf[i]), 0.f);
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+            const float p1 = __uint_as_float(jy ? sw[0] : sw[1]);
+            const float m2 = fmaxf(v, p1);
+            m[i] = fmaxf(m2, __int_as_float(dpp_i<0x128>(__float_as_int(m2))));
+          }
+        }
+        if (writer)
+          *reinterpret_cast<uint2*>(zrow + (size_t)(8 * mt + qy) * COUT) =
+              make_uint2(pack_bf16x2(m[0], m[1]), pack_bf16x2(m[2], m[3]));
+      }
+    }
+  }
+}
+
 int c1p8_moment_rows(int N, int B) {
   static int resident = 0;
   if (!resident) {
@@ -1198,6 +1326,14 @@ int avd_c1r_launch(int pass, const void* x, const void* wk, const float* bias, c
     const int G = N / B, R = c1p8_moment_rows(N, B);
     c1p8_moments_kernel<<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, scale, shift,
                                                mean, invstd, (const bf16*)gz, out, B, G, R, H, W, tps);
+    AVD_CHECK_LAUNCH();
+    return AVD_OK;
+  }
+  // the in-register pooling variant measured slower (361 vs 268 us at N = 7168: ~5 VALU per
+  // element for the cross-lane max against 0.75 in the per-window threads): opt-in only
+  if (pass == RC_APPLY && getenv("AVDINO_C1_APPLY_REG")) {
+    c1p8_apply_kernel<<<N, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, scale, shift,
+                                          (bf16*)z, B, H, W, tps);
     AVD_CHECK_LAUNCH();
     return AVD_OK;
   }

@@ -209,7 +209,7 @@ def test_conv1_moments_pass_bench_size(ops):
     d0 = torch.empty(C * K * K, device="cuda")
     ops.sum_rows(f0, ns, C * K * K, d0)
     R4 = ops.cl_c1_recompute_rows(ops.C1_REDUCE_MOMENTS, T, N, B, 1, H, H, C, K, pad)
-    assert 0 < R4 and G * R4 * 20 < N * (H // 16), "persistent blocks with many tiles expected"
+    assert 0 < R4 and G * R4 * 8 < N * (H // 16), "blocks with many tiles each expected"
     mc = ops.c1_moment_cols(C)
     m4 = torch.full((C * G * R4 * 2 + R4 * G * mc,), float("nan"), device="cuda")
     ops.cl_c1_recompute(ops.C1_REDUCE_MOMENTS, x, wk, bias, N, B, 1, H, H, C, K, pad, scale=bn[2],
