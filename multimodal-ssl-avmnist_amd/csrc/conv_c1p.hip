@@ -995,11 +995,21 @@ __global__ __launch_bounds__(256, 2) void c1p8_moments_kernel(
         }
       }
       uint32_t ow[4][4];
+      // BN values of the window, two channels per packed FMA; the first max of relu(v) routes
+      // the gradient only when it is > 0, where it is the first max of v itself (no relu needed)
+      float bnv[4][COUT];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < COUT; e += 2) {
+          const f2 v = __builtin_elementwise_fma(f2{yv[k][e], yv[k][e + 1]}, f2{sc[e], sc[e + 1]},
+                                                 f2{sf[e], sf[e + 1]});
+          bnv[k][e] = v[0];
+          bnv[k][e + 1] = v[1];
+        }
 #pragma unroll
       for (int e = 0; e < COUT; ++e) {
-        float rv[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) rv[k] = fmaxf(fmaf(yv[k][e], sc[e], sf[e]), 0.f);
+        const float rv[4] = {bnv[0][e], bnv[1][e], bnv[2][e], bnv[3][e]};
         const float m = fmaxf(fmaxf(rv[0], rv[1]), fmaxf(rv[2], rv[3]));
         const bool e0 = rv[0] == m, e1 = !e0 && rv[1] == m, e2 = !e0 && !e1 && rv[2] == m;
         const float dz = m > 0.f ? gg[e] : 0.f;
