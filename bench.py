@@ -248,15 +248,23 @@ def main():
 
     # warm-up: eager steps (the second one times every instrumented kernel to find the dominant
     # one; the first one's launches are cold), then -- graph mode -- the step's capture
-    use_graph = not args.no_graph and not args.probe_dominant
+    # graph replay needs one eager warm-up step (it sizes every workspace) and the capture
+    # inside the warm-up: with fewer than 2 warm-up steps the bench runs eagerly
+    use_graph = not args.no_graph and not args.probe_dominant and args.warmup >= 2
     eng.use_graph = use_graph
     eng.graph.warmup = min(2, max(args.warmup - 1, 0))
     ops.TIMER = None
     wtimer = None
+    # the timed warm-up step must run eagerly: with graphs, calls >= graph.warmup capture (and
+    # events recorded inside a capture have no timestamps)
+    t_idx = min(1, args.warmup - 1)
+    if use_graph and t_idx >= eng.graph.warmup:
+        t_idx = -1
     for i in range(args.warmup):
-        ops.TIMER = ops.KernelTimer() if i == min(1, args.warmup - 1) else None
+        ops.TIMER = ops.KernelTimer() if i == t_idx else None
         wtimer = ops.TIMER or wtimer
         eng.step(pool[i % len(pool)])
+    ops.TIMER = None
     summ = wtimer.summary() if wtimer is not None else {}
     dominant = max(summ, key=lambda k: summ[k]["ms"]) if summ else None
     if args.dominant:

@@ -502,6 +502,12 @@ int avd_adamw(float* p, const float* g, float* m, float* v, long long n, float l
  *   seed_off [1] u64   -- t_before * seed_stride, the dropout counter offset of this step
  *                         (may be NULL).
  * avd_adam_dev / avd_adamw_dev read lr and the bias corrections from hyp. */
+/* arena[idx[i]] += val[i] for i < n, int64, distinct indices: the num_batches_tracked
+ * increments of one forward for every BatchNorm layer at once (nn.BatchNorm*d.forward in
+ * training mode, num_batches_tracked += 1 per call; dino.py:680-704 calls each layer per view). */
+int avd_counters_add(long long* arena, const long long* idx, const long long* val, int n,
+                     void* stream);
+
 int avd_step_begin(long long* t, float* hyp, unsigned long long* seed_off, double b1, double b2,
                    unsigned long long seed_stride, void* stream);
 int avd_adam_dev(float* p, const float* g, float* m, float* v, long long n, const float* hyp,

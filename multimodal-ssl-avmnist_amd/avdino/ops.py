@@ -450,6 +450,13 @@ def cl_bn_bwd_reduce_pooled(y, pooled, gout, mode, gamma, beta, mean, invstd, pa
                         p(gamma), p(beta), p(mean), p(invstd), p(parts), N, B, C, H, W, stream()))
 
 
+def counters_add(arena, idx, val):
+    """arena[idx[i]] += val[i] (int64, distinct indices): avd_counters_add."""
+    _need(arena.dtype == idx.dtype == val.dtype == torch.int64 and idx.numel() == val.numel(),
+          "counters_add operands")
+    call("avd_counters_add", p(arena), p(idx), p(val), idx.numel(), stream())
+
+
 def cl_dgrad_bnreduce_rows(dtype, N, B, Cin, H, W, Cout, K, pad):
     """Rows per group of avd_cl_conv_dgrad_bnreduce's partial sums; 0 = shape not served."""
     return lib.avd_cl_dgrad_bnreduce_rows(_DT[dtype], N, B, Cin, H, W, Cout, K, pad)

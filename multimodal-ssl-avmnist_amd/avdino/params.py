@@ -137,8 +137,9 @@ class ParamStore:
         self._nbt_pending[key] = self._nbt_pending.get(key, 0) + inc
 
     def flush_nbt(self):
-        """Apply the recorded counter increments: one index_add_ on the current stream (the
-        index / value tensors are cached per increment pattern, so no host copy per step)."""
+        """Apply the recorded counter increments: one avd_counters_add launch on the current
+        stream (the index / value tensors are cached per increment pattern, so no host copy per
+        step)."""
         if not self._nbt_pending:
             return
         sig = tuple(sorted(self._nbt_pending.items()))
@@ -148,7 +149,11 @@ class ParamStore:
             idx = torch.tensor([self.nbt_index[k] for k, _ in sig], dtype=torch.int64, device=self.device)
             val = torch.tensor([v for _, v in sig], dtype=torch.int64, device=self.device)
             c = self._nbt_cache[sig] = (idx, val)
-        self.nbt_arena.index_add_(0, c[0], c[1])
+        if self.nbt_arena.device.type != "cuda":     # host-side store (checkpoint / state-dict work)
+            self.nbt_arena.index_add_(0, c[0], c[1])
+            return
+        from . import ops
+        ops.counters_add(self.nbt_arena, c[0], c[1])
 
     def grad_of(self, key):
         o, n = self.s_offs[key]

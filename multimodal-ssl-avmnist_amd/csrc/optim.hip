@@ -117,9 +117,27 @@ __global__ void step_begin_kernel(long long* __restrict__ t, float* __restrict__
   hyp[2] = (float)(1.0 - pow(b2, (double)k));
 }
 
+// BatchNorm num_batches_tracked increments of one forward, all layers at once:
+// arena[idx[i]] += val[i] (distinct indices; one thread each)
+__global__ void counters_add_kernel(long long* __restrict__ arena, const long long* __restrict__ idx,
+                                    const long long* __restrict__ val, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) arena[idx[i]] += val[i];
+}
+
 }  // namespace
 
 extern "C" {
+
+int avd_counters_add(long long* arena, const long long* idx, const long long* val, int n,
+                     void* stream) {
+  if (!arena || !idx || !val) return AVD_ERR_ARG;
+  if (n < 0) return AVD_ERR_SHAPE;
+  if (n == 0) return AVD_OK;
+  counters_add_kernel<<<avd_cdiv(n, 64), 64, 0, avd_stream(stream)>>>(arena, idx, val, n);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
 
 int avd_version(void) { return (0 << 16) | 1; }
 
