@@ -892,13 +892,10 @@ __global__ __launch_bounds__(256, 2) void c1p8_moments_kernel(
     ba[tt] = (k2 >= 0 ? k2 >> 1 : -1) + 1;
   }
   const bool ones = col == 14;                               // pair column 30: constant 1
-  // fp32 MFMA accumulators per tile, folded into float64 after every tile (the combine's
-  // cancellation amplifies the accumulation error of long fp32 chains)
-  double dacc[5][4];
-#pragma unroll
-  for (int b = 0; b < 5; ++b)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dacc[b][i] = 0.0;
+  // fp32 MFMA accumulators over the block's tiles (8 waves of blocks: ~12 tiles each at bench
+  // size; moments within 1e-7 of float64 there)
+  f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+  f4 ga[3] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
 
   // global loads one tile ahead: <= 2 input-row vectors and <= 2 pooled-gradient vectors
   const int nxt = (TH + 4) * cpr, nwin = (TH / 2) * Wp;
@@ -1053,8 +1050,6 @@ __global__ __launch_bounds__(256, 2) void c1p8_moments_kernel(
     __syncthreads();
     // ---- k-blocks of pixel pairs: D += dZ X (tap tiles 0, 1) and the Gram tiles (0,0) (0,1) (1,1)
     const int nkb = (C1M_DIAG & 8) ? 0 : TH * segs;
-    f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
-    f4 ga[3] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
     if (4 * wave < nkb) {
       typedef __attribute__((ext_vector_type(8))) short s8;
       const int q = col >> 2, pp = col & 3;
@@ -1074,17 +1069,26 @@ __global__ __launch_bounds__(256, 2) void c1p8_moments_kernel(
         c0 = *reinterpret_cast<const u4*>(&xc[bs + boff0]);
         c1 = *reinterpret_cast<const u4*>(&xc[bs + boff1]);
       };
-      ld(h0, h1, w0, w1);
-      for (int ks = wave;; ks += 4) {
-        const bool more = 4 * (ks + 4) < nkb;
-        s4 n0, n1;
-        u4 v0, v1;
-        if (more) {
+      // two k-blocks of operand reads ahead of the MFMAs (past the end: re-read the last
+      // block, in LDS bounds)
+      auto adv = [&](bool go) {
+        if (go) {
           sg += dsg;
           r += dr;
           if (sg >= segs) { sg -= segs; ++r; }
         }
-        ld(n0, n1, v0, v1);
+      };
+      ld(h0, h1, w0, w1);
+      s4 n0, n1;
+      u4 v0, v1;
+      adv(4 * (wave + 4) < nkb);
+      ld(n0, n1, v0, v1);
+      for (int ks = wave;; ks += 4) {
+        const bool more = 4 * (ks + 4) < nkb;
+        s4 m0, m1;
+        u4 x0v, x1v;
+        adv(4 * (ks + 8) < nkb);
+        ld(m0, m1, x0v, x1v);
         const bf16x8 A = __builtin_bit_cast(bf16x8, s8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]});
         const bf16x8 X0 = __builtin_bit_cast(bf16x8, w0);
         const bf16x8 X1 = __builtin_bit_cast(bf16x8, ones ? one4 : w1);
@@ -1097,12 +1101,8 @@ __global__ __launch_bounds__(256, 2) void c1p8_moments_kernel(
         }
         if (!more) break;
         h0 = n0; h1 = n1; w0 = v0; w1 = v1;
+        n0 = m0; n1 = m1; v0 = x0v; v1 = x1v;
       }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      dacc[0][i] += acc[0][i]; dacc[1][i] += acc[1][i];
-      dacc[2][i] += ga[0][i]; dacc[3][i] += ga[1][i]; dacc[4][i] += ga[2][i];
     }
   }
   // ---- block outputs: BN sums (one row), then M / Gram / S folded from pairs to taps
@@ -1122,13 +1122,13 @@ __global__ __launch_bounds__(256, 2) void c1p8_moments_kernel(
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) red[(wave * 16 + 4 * gq + i) * 32 + 16 * tt + col] = (float)dacc[tt][i];
+    for (int i = 0; i < 4; ++i) red[(wave * 16 + 4 * gq + i) * 32 + 16 * tt + col] = acc[tt][i];
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
     const int ti = b == 2 ? 1 : 0, tj = b == 0 ? 0 : 1;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      g6[(wave * 32 + 16 * ti + 4 * gq + i) * 32 + 16 * tj + col] = (float)dacc[2 + b][i];
+      g6[(wave * 32 + 16 * ti + 4 * gq + i) * 32 + 16 * tj + col] = ga[b][i];
   }
   __syncthreads();
   if (tid < 2 * COUT) {
