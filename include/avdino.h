@@ -49,52 +49,6 @@ const char* avd_last_error(void);
  * (models/unimodal.py:127-153 and 185-211; models/dino.py:18-73).
  */
 
-/* Number of partial-statistic rows per sample written by avd_conv2d_fwd. */
-int avd_conv2d_stat_tiles(int Ho, int Wo);
-
-/* Re-lay a conv weight w [Cout,Cin,K,K] (f32) for the kernels:
- * mode 0 (f32 forward):    wt[ci][tap][co] = w[co][ci][tap]        (f32)
- * mode 1 (f32 input-grad): wt[co][tap][ci] = w[co][ci][K*K-1-tap] (f32)
- *   (VALU kernels: per tap the weights a workgroup needs are contiguous and uniform, so
- *    they arrive through scalar loads)
- * mode 2 (bf16 forward, MFMA):    wk[co][tap*Cin + ci] = w[co][ci][tap]          (bf16)
- * mode 3 (bf16 input-grad, MFMA): wk[ci][tap*Cout + co] = w[co][ci][K*K-1-tap]   (bf16)
- *   (rows padded with zeros to a multiple of 32 k and of 16/64 output channels: the MFMA
- *    B-operand fragment of a lane is one 16-byte load)
- * avd_conv_weight_layout_elems gives the element count of wt for a mode. */
-int avd_conv_weight_layout_elems(int Cout, int Cin, int K, int mode);
-int avd_conv_weight_layout(const float* w, void* wt, int Cout, int Cin, int K, int mode,
-                           void* stream);
-
-/* y = conv2d(x, w) + bias   (nn.Conv2d forward, unimodal.py:113-176)
- * x [N,Cin,H,W] (xdt), bias [Cout] f32 (NULL = 0),
- * wt = avd_conv_weight_layout(w, mode 2) when x and y are bf16, Cin % 8 == 0, Cin <= 256 (MFMA
- *      implicit GEMM, v_mfma_f32_16x16x32_bf16), else mode 0 (VALU direct conv),
- * y [N,Cout,Ho,Wo] (ydt),
- * Ho = H + 2*pad - K + 1.  If stats != NULL, writes per-(channel, sample, tile) partial
- * (sum, sum of squares) of the stored y: stats [Cout, N, T, 2] f32, T = avd_conv2d_stat_tiles.
- * K in {3, 5}. */
-int avd_conv2d_fwd(const void* x, int xdt, const void* wt, const float* bias, void* y, int ydt,
-                   float* stats, int N, int Cin, int H, int W, int Cout, int K, int pad,
-                   void* stream);
-
-/* dx = conv2d_input_grad(dy, w)   (autograd of nn.Conv2d w.r.t. its input)
- * dy [N,Cout,Ho,Wo] (dt), dx [N,Cin,H,W] (dt),
- * wt_dgrad = avd_conv_weight_layout(w, mode 3) for bf16 with Cout % 8 == 0, Cout <= 256 (MFMA),
- * mode 1 otherwise (f32 VALU). */
-int avd_conv2d_dgrad(const void* dy, const void* wt_dgrad, void* dx, int dt,
-                     int N, int Cin, int H, int W, int Cout, int K, int pad, void* stream);
-
-/* Number of sample chunks (partial slabs) avd_conv2d_wgrad writes for N samples. */
-int avd_conv2d_wgrad_chunks(int N, int Cout, int Cin, int K);
-
-/* dw_parts[c] = sum over the samples of chunk c of conv2d_weight_grad(x, dy)
- * x [N,Cin,H,W] (xdt), dy [N,Cout,Ho,Wo] (dydt), dw_parts [chunks, Cout, Cin*K*K] f32.
- * bf16 x/dy run on MFMA (v_mfma_f32_16x16x32_bf16, fp32 accumulate); f32 on the VALU.
- * Reduce with avd_sum_rows. */
-int avd_conv2d_wgrad(const void* x, int xdt, const void* dy, int dydt, float* dw_parts,
-                     int N, int Cin, int H, int W, int Cout, int K, int pad, void* stream);
-
 /* BatchNorm2d / BatchNorm1d train-mode statistics, per (group, channel):
  * parts [C, G, R, 2] f32 partial (sum, sumsq) rows, channel-major (R rows per group: for
  * conv stats R = B*T), count = elements per (group, channel).  Outputs mean/invstd/scale/shift [G,C] (scale = gamma*invstd,
@@ -109,21 +63,6 @@ int avd_bn_finalize(float* parts, int G, int R, int C, long long count,
                     float* mean, float* invstd, float* scale, float* shift,
                     float* running_mean, float* running_var, const float* pivot, void* stream);
 
-/* out = maxpool2(relu(scale*y + shift))  [N,C,H/2,W/2]  (floor mode)      pool_mode 0
- * out = mean_hw(maxpool2(relu(...)))        [N,C]   f32 (AdaptiveAvgPool2d(1)) pool_mode 1
- * y [N,C,H,W] (ydt); scale/shift [G,C]; B samples per group. */
-int avd_bn_relu_pool(const void* y, int ydt, const float* scale, const float* shift,
-                     void* out, int odt, int pool_mode, int N, int B, int C, int H, int W,
-                     void* stream);
-
-/* Backward of maxpool2(relu(BN(y))) up to the BN-output gradient dz, reduced:
- * parts [C, N, 2] f32 = per-sample (sum dz, sum dz*xhat)  (= [C, G, B, 2]).
- * gout: grad of the block output: pool_mode 0 [N,C,H/2,W/2] (gdt); pool_mode 1 [N,C] f32. */
-int avd_bn_bwd_reduce(const void* y, int ydt, const void* gout, int gdt, int pool_mode,
-                      const float* scale, const float* shift, const float* mean,
-                      const float* invstd, float* parts, int N, int B, int C, int H, int W,
-                      void* stream);
-
 /* From the partials [C, G, R, 2] build the input-gradient coefficients
  * coef [G, C, 3] (dy = k1*dz + kx*y + k0) and write dgamma/dbeta/dbias [C] (sums over
  * groups; dbias = sum of dy = the grad of a bias feeding this BN, NULL to skip).
@@ -132,12 +71,6 @@ int avd_bn_bwd_finalize(const float* parts, int G, int R, int C, long long count
                         const float* gamma, const float* mean, const float* invstd,
                         float* coef, float* dgamma, float* dbeta, float* dbias, int accumulate,
                         void* stream);
-
-/* dy [N,C,H,W] (dt) = gradient w.r.t. the conv output y of the whole block
- * (maxpool2 + ReLU + BN backward), using coef from avd_bn_bwd_finalize. */
-int avd_bn_bwd_apply(const void* y, int ydt, const void* gout, int gdt, int pool_mode,
-                     const float* scale, const float* shift, const float* coef,
-                     void* dy, int dt, int N, int B, int C, int H, int W, void* stream);
 
 /* ------------------------------------------------------------------ dense layers */
 

@@ -21,18 +21,8 @@ D = ctypes.c_double
 # name -> argtypes (restype is always c_int except where noted)
 PROTOS = {
     "avd_version": [],
-    "avd_conv2d_stat_tiles": [I, I],
-    "avd_conv_weight_layout": [P, P, I, I, I, I, P],
-    "avd_conv_weight_layout_elems": [I, I, I, I],
-    "avd_conv2d_fwd": [P, I, P, P, P, I, P, I, I, I, I, I, I, I, P],
-    "avd_conv2d_dgrad": [P, P, P, I, I, I, I, I, I, I, I, P],
-    "avd_conv2d_wgrad_chunks": [I, I, I, I],
-    "avd_conv2d_wgrad": [P, I, P, I, P, I, I, I, I, I, I, I, P],
     "avd_bn_finalize": [P, I, I, I, L, P, P, F, F, P, P, P, P, P, P, P, P],
-    "avd_bn_relu_pool": [P, I, P, P, P, I, I, I, I, I, I, I, P],
-    "avd_bn_bwd_reduce": [P, I, P, I, I, P, P, P, P, P, I, I, I, I, I, P],
     "avd_bn_bwd_finalize": [P, I, I, I, L, P, P, P, P, P, P, P, I, P],
-    "avd_bn_bwd_apply": [P, I, P, I, I, P, P, P, P, I, I, I, I, I, I, P],
     "avd_gemm": [I, I, I, P, L, L, P, L, L, P, L, P, F, F, I, P, L, P],
     "avd_gemm_ws_elems": [I, I, I, I],
     "avd_cl_weight_elems": [I, I, I, I],

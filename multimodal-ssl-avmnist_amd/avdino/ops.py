@@ -91,102 +91,17 @@ def _need(cond, msg):
         raise ValueError(msg)
 
 
-# ---------------------------------------------------------------- conv blocks
-def conv_stat_tiles(Ho, Wo):
-    return lib.avd_conv2d_stat_tiles(Ho, Wo)
-
-
-def conv_weight_layout_elems(Cout, Cin, K, mode):
-    return lib.avd_conv_weight_layout_elems(Cout, Cin, K, mode)
-
-
-def conv_weight_layout(w, wt, mode):
-    """mode 0/1: f32 VALU layouts (fwd / input-grad); 2/3: bf16 MFMA layouts."""
-    Cout, Cin, K, _ = w.shape
-    _need(wt.numel() >= conv_weight_layout_elems(Cout, Cin, K, mode), "wt size")
-    _need(wt.dtype == (torch.bfloat16 if mode >= 2 else torch.float32), "wt dtype")
-    call("avd_conv_weight_layout", p(w), p(wt), Cout, Cin, K, mode, stream())
-
-
-def mfma_conv(x_dtype, cin):
-    """True when avd_conv2d_fwd / _dgrad take the MFMA path (and want layouts 2 / 3)."""
-    return x_dtype == torch.bfloat16 and cin % 8 == 0 and cin <= 256
-
-
-def conv2d_fwd(x, wt, bias, y, stats, N, Cin, H, W, Cout, K, pad):
-    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
-    _need(x.numel() == N * Cin * H * W, "conv x size")
-    _need(y.numel() == N * Cout * Ho * Wo, "conv y size")
-    if stats is not None:
-        _need(stats.numel() >= Cout * N * conv_stat_tiles(Ho, Wo) * 2, "conv stats size")
-    nb = x.numel() * x.element_size() + y.numel() * y.element_size()
-    fl = 2 * N * Cout * Ho * Wo * Cin * K * K
-    _timed(f"conv2d_fwd[{N}x{Cin}x{H}x{W}->{Cout} k{K}p{pad} {x.dtype}]", nb, fl,
-           lambda: call("avd_conv2d_fwd", p(x), dtcode(x), p(wt), p(bias), p(y), dtcode(y),
-                        p(stats), N, Cin, H, W, Cout, K, pad, stream()))
-
-
-def conv2d_dgrad(dy, wt_d, dx, N, Cin, H, W, Cout, K, pad):
-    _need(dx.numel() == N * Cin * H * W and dx.dtype == dy.dtype, "dgrad dx")
-    nb = (dy.numel() + dx.numel()) * dy.element_size()
-    fl = 2 * N * Cin * H * W * Cout * K * K
-    _timed(f"conv2d_dgrad[{N}x{Cout}->{Cin}x{H}x{W} k{K}p{pad} {dy.dtype}]", nb, fl,
-           lambda: call("avd_conv2d_dgrad", p(dy), p(wt_d), p(dx), dtcode(dy), N, Cin, H, W, Cout,
-                        K, pad, stream()))
-
-
-def wgrad_chunks(N, Cout, Cin, K):
-    return lib.avd_conv2d_wgrad_chunks(N, Cout, Cin, K)
-
-
-def conv2d_wgrad(x, dy, parts, N, Cin, H, W, Cout, K, pad):
-    _need(parts.numel() >= wgrad_chunks(N, Cout, Cin, K) * Cout * Cin * K * K, "wgrad parts")
-    nb = x.numel() * x.element_size() + dy.numel() * dy.element_size()
-    fl = 2 * dy.numel() * Cin * K * K
-    _timed(f"conv2d_wgrad[{N}x{Cin}x{H}x{W}->{Cout} k{K}p{pad} {x.dtype}]", nb, fl,
-           lambda: call("avd_conv2d_wgrad", p(x), dtcode(x), p(dy), dtcode(dy), p(parts), N, Cin,
-                        H, W, Cout, K, pad, stream()))
-
-
+# ---------------------------------------------------------------- BatchNorm statistics
 def bn_finalize(parts, G, R, C, count, gamma, beta, mean, invstd, scale, shift, rm=None, rv=None,
                 eps=1e-5, momentum=0.1, pivot=None):
     call("avd_bn_finalize", p(parts), G, R, C, count, p(gamma), p(beta), eps, momentum, p(mean),
          p(invstd), p(scale), p(shift), p(rm), p(rv), p(pivot), stream())
 
 
-def bn_relu_pool(y, scale, shift, out, pool_mode, N, B, C, H, W):
-    _need(y.numel() == N * C * H * W and scale.numel() >= (N // B) * C, "bn_relu_pool y")
-    _need(out.numel() == (N * C if pool_mode else N * C * (H // 2) * (W // 2)), "bn_relu_pool out")
-    nb = y.numel() * y.element_size() + out.numel() * out.element_size()
-    _timed(f"bn_relu_pool[{N}x{C}x{H}x{W} {y.dtype}]", nb, 0,
-           lambda: call("avd_bn_relu_pool", p(y), dtcode(y), p(scale), p(shift), p(out),
-                        dtcode(out), pool_mode, N, B, C, H, W, stream()))
-
-
-def bn_bwd_reduce(y, gout, pool_mode, scale, shift, mean, invstd, parts, N, B, C, H, W):
-    _need(y.numel() == N * C * H * W and parts.numel() >= C * N * 2, "bn_bwd_reduce sizes")
-    _need(gout.numel() == (N * C if pool_mode else N * C * (H // 2) * (W // 2)), "bn_bwd gout")
-    nb = y.numel() * y.element_size() + gout.numel() * gout.element_size()
-    _timed(f"bn_bwd_reduce[{N}x{C}x{H}x{W} {y.dtype}]", nb, 0,
-           lambda: call("avd_bn_bwd_reduce", p(y), dtcode(y), p(gout), dtcode(gout), pool_mode,
-                        p(scale), p(shift), p(mean), p(invstd), p(parts), N, B, C, H, W, stream()))
-
-
 def bn_bwd_finalize(parts, G, R, C, count, gamma, mean, invstd, coef, dgamma, dbeta, dbias,
                     accumulate=0):
     call("avd_bn_bwd_finalize", p(parts), G, R, C, count, p(gamma), p(mean), p(invstd), p(coef),
          p(dgamma), p(dbeta), p(dbias), accumulate, stream())
-
-
-def bn_bwd_apply(y, gout, pool_mode, scale, shift, coef, dy, N, B, C, H, W):
-    _need(y.numel() == N * C * H * W and dy.numel() == y.numel(), "bn_bwd_apply sizes")
-    _need(gout.numel() == (N * C if pool_mode else N * C * (H // 2) * (W // 2)), "bn_bwd gout")
-    _need(coef.numel() >= (N // B) * C * 3, "bn_bwd coef")
-    nb = (y.numel() * y.element_size() + gout.numel() * gout.element_size()
-          + dy.numel() * dy.element_size())
-    _timed(f"bn_bwd_apply[{N}x{C}x{H}x{W} {y.dtype}]", nb, 0,
-           lambda: call("avd_bn_bwd_apply", p(y), dtcode(y), p(gout), dtcode(gout), pool_mode,
-                        p(scale), p(shift), p(coef), p(dy), dtcode(dy), N, B, C, H, W, stream()))
 
 
 # ---------------------------------------------------------------- dense

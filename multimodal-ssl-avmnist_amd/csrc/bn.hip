@@ -171,119 +171,6 @@ __global__ __launch_bounds__(256) void bn_finalize1_kernel(
   }
 }
 
-// ----------------------------------------------------------------------------- relu + pool
-template <typename TY, typename TO>
-__global__ __launch_bounds__(256) void bn_relu_pool_kernel(
-    const TY* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
-    TO* __restrict__ out, long long total, int B, int C, int H, int W) {
-  const int Hp = H / 2, Wp = W / 2;
-  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int wp = (int)(i % Wp);
-    const int hp = (int)((i / Wp) % Hp);
-    const long long nc = i / ((long long)Hp * Wp);
-    const int c = (int)(nc % C);
-    const int n = (int)(nc / C);
-    const int g = n / B;
-    const float sc = scale[g * C + c], sf = shift[g * C + c];
-    const size_t base = ((size_t)nc * H + 2 * hp) * W + 2 * wp;
-    float m = 0.f;  // relu output >= 0
-    m = fmaxf(m, fmaf(io<TY>::ld(y, base), sc, sf));
-    m = fmaxf(m, fmaf(io<TY>::ld(y, base + 1), sc, sf));
-    m = fmaxf(m, fmaf(io<TY>::ld(y, base + W), sc, sf));
-    m = fmaxf(m, fmaf(io<TY>::ld(y, base + W + 1), sc, sf));
-    io<TO>::st(out, i, m);
-  }
-}
-
-template <typename TY>
-__global__ __launch_bounds__(256) void bn_relu_pool_gap_kernel(
-    const TY* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
-    float* __restrict__ out, long long total, int B, int C, int H, int W) {
-  const int Hp = H / 2, Wp = W / 2;
-  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int c = (int)(i % C);
-    const int n = (int)(i / C);
-    const int g = n / B;
-    const float sc = scale[g * C + c], sf = shift[g * C + c];
-    float acc = 0.f;
-    for (int hp = 0; hp < Hp; ++hp)
-      for (int wp = 0; wp < Wp; ++wp) {
-        const size_t base = ((size_t)i * H + 2 * hp) * W + 2 * wp;
-        float m = 0.f;
-        m = fmaxf(m, fmaf(io<TY>::ld(y, base), sc, sf));
-        m = fmaxf(m, fmaf(io<TY>::ld(y, base + 1), sc, sf));
-        m = fmaxf(m, fmaf(io<TY>::ld(y, base + W), sc, sf));
-        m = fmaxf(m, fmaf(io<TY>::ld(y, base + W + 1), sc, sf));
-        acc += m;
-      }
-    out[i] = acc / (float)(Hp * Wp);
-  }
-}
-
-// Window helper: z values of the 2x2 window, first-max argmax and the max of relu(z).
-struct Win {
-  float y[4];
-  int arg;
-  float zmax;
-};
-template <typename TY>
-__device__ __forceinline__ Win load_win(const TY* y, size_t base, int W, float sc, float sf) {
-  Win w;
-  w.y[0] = io<TY>::ld(y, base);
-  w.y[1] = io<TY>::ld(y, base + 1);
-  w.y[2] = io<TY>::ld(y, base + W);
-  w.y[3] = io<TY>::ld(y, base + W + 1);
-  // max over relu(z) with first-max tie-break in row-major window order (scan with '>')
-  float best = fmaxf(fmaf(w.y[0], sc, sf), 0.f);
-  int arg = 0;
-#pragma unroll
-  for (int k = 1; k < 4; ++k) {
-    const float r = fmaxf(fmaf(w.y[k], sc, sf), 0.f);
-    if (r > best) { best = r; arg = k; }
-  }
-  w.arg = arg;
-  w.zmax = best;
-  return w;
-}
-
-template <typename TG>
-__device__ __forceinline__ float gout_at(const TG* gout, int pool_mode, long long nc, int q, int HpWp) {
-  if (pool_mode == 0) return io<TG>::ld(gout, (size_t)nc * HpWp + q);
-  return reinterpret_cast<const float*>(gout)[nc] / (float)HpWp;
-}
-
-// ----------------------------------------------------------------------------- backward reduce
-template <typename TY, typename TG>
-__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
-    const TY* __restrict__ y, const TG* __restrict__ gout, int pool_mode,
-    const float* __restrict__ scale, const float* __restrict__ shift,
-    const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ parts,
-    int N, int B, int C, int H, int W) {
-  const int Hp = H / 2, Wp = W / 2, HpWp = Hp * Wp;
-  const long long nc = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (nc >= (long long)N * C) return;
-  const int c = (int)(nc % C), n = (int)(nc / C), g = n / B;
-  const float sc = scale[g * C + c], sf = shift[g * C + c];
-  const float mu = mean[g * C + c], is = invstd[g * C + c];
-  float s1 = 0.f, s2 = 0.f;
-  for (int q = lane; q < HpWp; q += 64) {
-    const int hp = q / Wp, wp = q % Wp;
-    const Win w = load_win<TY>(y, ((size_t)nc * H + 2 * hp) * W + 2 * wp, W, sc, sf);
-    if (w.zmax > 0.f) {
-      const float d = gout_at<TG>(gout, pool_mode, nc, q, HpWp);
-      s1 += d;
-      s2 += d * (w.y[w.arg] - mu) * is;
-    }
-  }
-  s1 = wave_sum(s1);
-  s2 = wave_sum(s2);
-  if (lane == 0) {
-    parts[((size_t)c * N + n) * 2] = s1;
-    parts[((size_t)c * N + n) * 2 + 1] = s2;
-  }
-}
-
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
     const float* __restrict__ parts, int G, int R, int C, long long count,
     const float* __restrict__ gamma, const float* __restrict__ mean,
@@ -311,202 +198,6 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
   if (dgamma) dgamma[c] = (float)(accumulate ? dgamma[c] + dg : dg);
   if (dbeta) dbeta[c] = (float)(accumulate ? dbeta[c] + db : db);
   if (dbias) dbias[c] = (float)(accumulate ? dbias[c] + dbi : dbi);
-}
-
-template <typename TY, typename TG, typename TD>
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
-    const TY* __restrict__ y, const TG* __restrict__ gout, int pool_mode,
-    const float* __restrict__ scale, const float* __restrict__ shift,
-    const float* __restrict__ coef, TD* __restrict__ dy, long long total, int B, int C, int H,
-    int W) {
-  const int Hp = H / 2, Wp = W / 2, HpWp = Hp * Wp;
-  const int Hc = (H + 1) / 2, Wc = (W + 1) / 2;  // windows incl. floor-mode leftovers
-  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int wc = (int)(i % Wc);
-    const int hc = (int)((i / Wc) % Hc);
-    const long long nc = i / ((long long)Hc * Wc);
-    const int c = (int)(nc % C), n = (int)(nc / C), g = n / B;
-    const float sc = scale[g * C + c], sf = shift[g * C + c];
-    const float k1 = coef[(g * C + c) * 3], kx = coef[(g * C + c) * 3 + 1],
-                k0 = coef[(g * C + c) * 3 + 2];
-    const int h0 = 2 * hc, w0 = 2 * wc;
-    const size_t base = ((size_t)nc * H + h0) * W + w0;
-    if (hc < Hp && wc < Wp) {
-      const Win w = load_win<TY>(y, base, W, sc, sf);
-      const float d = w.zmax > 0.f ? gout_at<TG>(gout, pool_mode, nc, hc * Wp + wc, HpWp) : 0.f;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float dz = (k == w.arg) ? d : 0.f;
-        const size_t o = base + (k >> 1) * W + (k & 1);
-        io<TD>::st(dy, o, fmaf(k1, dz, fmaf(kx, w.y[k], k0)));
-      }
-    } else {  // incomplete window (odd H/W): no gradient flows through pooling
-      for (int a = 0; a < 2; ++a)
-        for (int b = 0; b < 2; ++b)
-          if (h0 + a < H && w0 + b < W) {
-            const size_t o = base + a * W + b;
-            io<TD>::st(dy, o, fmaf(kx, io<TY>::ld(y, o), k0));
-          }
-    }
-  }
-}
-
-// ----------------------------------------------------------------------------- bf16 x4 paths
-// bf16 maps whose row width is a multiple of 8: one thread handles 4 consecutive pooling
-// windows of an output row -> two 16-byte loads of y (the two input rows), 8-byte gradient
-// loads/stores.  (f32 maps and other widths take the scalar kernels above.)
-typedef __attribute__((ext_vector_type(4))) unsigned u4v;
-typedef __attribute__((ext_vector_type(2))) unsigned u2v;
-
-__device__ __forceinline__ void unpack8(u4v v, float (&f)[8]) {
-  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
-  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
-  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
-  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
-}
-__device__ __forceinline__ unsigned pack2(float a, float b) {
-  return pack_bf16x2(a, b);
-}
-
-// per window k = 0..3 of the quad: first-max argmax over relu(z) and the max
-__device__ __forceinline__ void quad_windows(const float (&r0)[8], const float (&r1)[8], float sc,
-                                             float sf, int (&arg)[4], float (&mx)[4]) {
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float v[4] = {r0[2 * k], r0[2 * k + 1], r1[2 * k], r1[2 * k + 1]};
-    float best = fmaxf(fmaf(v[0], sc, sf), 0.f);
-    int a = 0;
-#pragma unroll
-    for (int j = 1; j < 4; ++j) {
-      const float r = fmaxf(fmaf(v[j], sc, sf), 0.f);
-      if (r > best) { best = r; a = j; }
-    }
-    arg[k] = a;
-    mx[k] = best;
-  }
-}
-
-__global__ __launch_bounds__(256) void bn_relu_pool_q4_kernel(
-    const bf16* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
-    bf16* __restrict__ out, long long total4, int B, int C, int H, int W) {
-  const int Hp = H / 2, Wp = W / 2, Q = Wp / 4;
-  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total4; i += (long long)gridDim.x * 256) {
-    const int q = (int)(i % Q);
-    const int hp = (int)((i / Q) % Hp);
-    const long long nc = i / ((long long)Q * Hp);
-    const int c = (int)(nc % C), g = (int)(nc / C) / B;
-    const float sc = scale[g * C + c], sf = shift[g * C + c];
-    const size_t base = ((size_t)nc * H + 2 * hp) * W + 8 * q;
-    float r0[8], r1[8];
-    unpack8(*reinterpret_cast<const u4v*>(y + base), r0);
-    unpack8(*reinterpret_cast<const u4v*>(y + base + W), r1);
-    int arg[4];
-    float mx[4];
-    quad_windows(r0, r1, sc, sf, arg, mx);
-    *reinterpret_cast<u2v*>(out + ((size_t)nc * Hp + hp) * Wp + 4 * q) =
-        u2v{pack2(mx[0], mx[1]), pack2(mx[2], mx[3])};
-  }
-}
-
-__global__ __launch_bounds__(256) void bn_bwd_reduce_q4_kernel(
-    const bf16* __restrict__ y, const bf16* __restrict__ gout, const float* __restrict__ scale,
-    const float* __restrict__ shift, const float* __restrict__ mean,
-    const float* __restrict__ invstd, float* __restrict__ parts, int N, int B, int C, int H, int W) {
-  const int Hp = H / 2, Wp = W / 2, Q = Wp / 4, HQ = Hp * Q;
-  const long long nc = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (nc >= (long long)N * C) return;
-  const int c = (int)(nc % C), n = (int)(nc / C), g = n / B;
-  const float sc = scale[g * C + c], sf = shift[g * C + c];
-  const float mu = mean[g * C + c], is = invstd[g * C + c];
-  float s1 = 0.f, s2 = 0.f;
-  const bf16* yp = y + (size_t)nc * H * W;
-  const bf16* gp = gout + (size_t)nc * Hp * Wp;
-  // 4 quads per lane per pass with every load issued before any math: a wave-per-plane
-  // reduction is bound by load latency, not bandwidth
-  for (int t0 = lane; t0 < HQ; t0 += 256) {
-    u4v a0[4], a1[4];
-    u2v gv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int t = t0 + 64 * u;
-      if (t < HQ) {
-        const int hp = t / Q, q = t - hp * Q;
-        const size_t base = (size_t)(2 * hp) * W + 8 * q;
-        a0[u] = *reinterpret_cast<const u4v*>(yp + base);
-        a1[u] = *reinterpret_cast<const u4v*>(yp + base + W);
-        gv[u] = *reinterpret_cast<const u2v*>(gp + (size_t)hp * Wp + 4 * q);
-      } else {   // zero gradient: contributes nothing
-        a0[u] = u4v{0u, 0u, 0u, 0u};
-        a1[u] = u4v{0u, 0u, 0u, 0u};
-        gv[u] = u2v{0u, 0u};
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      float r0[8], r1[8];
-      unpack8(a0[u], r0);
-      unpack8(a1[u], r1);
-      const float gg[4] = {__uint_as_float(gv[u].x << 16), __uint_as_float(gv[u].x & 0xffff0000u),
-                           __uint_as_float(gv[u].y << 16), __uint_as_float(gv[u].y & 0xffff0000u)};
-      int arg[4];
-      float mx[4];
-      quad_windows(r0, r1, sc, sf, arg, mx);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int a = arg[k];   // selects, not a runtime register index
-        const float ya = a == 0 ? r0[2 * k] : a == 1 ? r0[2 * k + 1] : a == 2 ? r1[2 * k] : r1[2 * k + 1];
-        const float gk = mx[k] > 0.f ? gg[k] : 0.f;
-        s1 += gk;
-        s2 += gk * (ya - mu) * is;
-      }
-    }
-  }
-  s1 = wave_sum(s1);
-  s2 = wave_sum(s2);
-  if (lane == 0) {
-    parts[((size_t)c * N + n) * 2] = s1;
-    parts[((size_t)c * N + n) * 2 + 1] = s2;
-  }
-}
-
-__global__ __launch_bounds__(256) void bn_bwd_apply_q4_kernel(
-    const bf16* __restrict__ y, const bf16* __restrict__ gout, const float* __restrict__ scale,
-    const float* __restrict__ shift, const float* __restrict__ coef, bf16* __restrict__ dy,
-    long long total4, int B, int C, int H, int W) {
-  const int Hp = H / 2, Wp = W / 2, Q = Wp / 4;
-  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total4; i += (long long)gridDim.x * 256) {
-    const int q = (int)(i % Q);
-    const int hp = (int)((i / Q) % Hp);
-    const long long nc = i / ((long long)Q * Hp);
-    const int c = (int)(nc % C), g = (int)(nc / C) / B;
-    const float sc = scale[g * C + c], sf = shift[g * C + c];
-    const float k1 = coef[(g * C + c) * 3], kx = coef[(g * C + c) * 3 + 1],
-                k0 = coef[(g * C + c) * 3 + 2];
-    const size_t base = ((size_t)nc * H + 2 * hp) * W + 8 * q;
-    float r0[8], r1[8];
-    unpack8(*reinterpret_cast<const u4v*>(y + base), r0);
-    unpack8(*reinterpret_cast<const u4v*>(y + base + W), r1);
-    const u2v gv = *reinterpret_cast<const u2v*>(gout + ((size_t)nc * Hp + hp) * Wp + 4 * q);
-    const float gg[4] = {__uint_as_float(gv.x << 16), __uint_as_float(gv.x & 0xffff0000u),
-                         __uint_as_float(gv.y << 16), __uint_as_float(gv.y & 0xffff0000u)};
-    int arg[4];
-    float mx[4];
-    quad_windows(r0, r1, sc, sf, arg, mx);
-    float d0[8], d1[8];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float d = mx[k] > 0.f ? gg[k] : 0.f;
-      d0[2 * k] = fmaf(k1, arg[k] == 0 ? d : 0.f, fmaf(kx, r0[2 * k], k0));
-      d0[2 * k + 1] = fmaf(k1, arg[k] == 1 ? d : 0.f, fmaf(kx, r0[2 * k + 1], k0));
-      d1[2 * k] = fmaf(k1, arg[k] == 2 ? d : 0.f, fmaf(kx, r1[2 * k], k0));
-      d1[2 * k + 1] = fmaf(k1, arg[k] == 3 ? d : 0.f, fmaf(kx, r1[2 * k + 1], k0));
-    }
-    *reinterpret_cast<u4v*>(dy + base) =
-        u4v{pack2(d0[0], d0[1]), pack2(d0[2], d0[3]), pack2(d0[4], d0[5]), pack2(d0[6], d0[7])};
-    *reinterpret_cast<u4v*>(dy + base + W) =
-        u4v{pack2(d1[0], d1[1]), pack2(d1[2], d1[3]), pack2(d1[4], d1[5]), pack2(d1[6], d1[7])};
-  }
 }
 
 // ----------------------------------------------------------------------------- BN1d / dense
@@ -717,72 +408,6 @@ int avd_bn_finalize(float* parts, int G, int R, int C, long long count, const fl
   return AVD_OK;
 }
 
-int avd_bn_relu_pool(const void* y, int ydt, const float* scale, const float* shift, void* out,
-                     int odt, int pool_mode, int N, int B, int C, int H, int W, void* stream) {
-  if (!y || !scale || !shift || !out) return AVD_ERR_ARG;
-  if (N <= 0 || B <= 0 || N % B || H < 2 || W < 2) return AVD_ERR_SHAPE;
-  hipStream_t st = avd_stream(stream);
-  if (pool_mode == 0 && ydt == AVD_BF16 && odt == AVD_BF16 && W % 8 == 0 && H % 2 == 0) {
-    const long long total4 = (long long)N * C * (H / 2) * (W / 8);
-    bn_relu_pool_q4_kernel<<<grid_for(total4), 256, 0, st>>>((const bf16*)y, scale, shift,
-                                                             (bf16*)out, total4, B, C, H, W);
-  } else if (pool_mode == 0) {
-    const long long total = (long long)N * C * (H / 2) * (W / 2);
-#define AVD_P(TY, TO)                                                                     \
-  bn_relu_pool_kernel<TY, TO><<<grid_for(total), 256, 0, st>>>((const TY*)y, scale, shift, \
-                                                              (TO*)out, total, B, C, H, W);
-    if (ydt == AVD_F32 && odt == AVD_F32) { AVD_P(float, float) }
-    else if (ydt == AVD_F32 && odt == AVD_BF16) { AVD_P(float, bf16) }
-    else if (ydt == AVD_BF16 && odt == AVD_BF16) { AVD_P(bf16, bf16) }
-    else if (ydt == AVD_BF16 && odt == AVD_F32) { AVD_P(bf16, float) }
-    else return AVD_ERR_DTYPE;
-#undef AVD_P
-  } else if (pool_mode == 1) {
-    if (odt != AVD_F32) return AVD_ERR_DTYPE;
-    const long long total = (long long)N * C;
-    if (ydt == AVD_F32)
-      bn_relu_pool_gap_kernel<float><<<grid_for(total), 256, 0, st>>>((const float*)y, scale, shift,
-                                                                      (float*)out, total, B, C, H, W);
-    else if (ydt == AVD_BF16)
-      bn_relu_pool_gap_kernel<bf16><<<grid_for(total), 256, 0, st>>>((const bf16*)y, scale, shift,
-                                                                     (float*)out, total, B, C, H, W);
-    else return AVD_ERR_DTYPE;
-  } else {
-    return AVD_ERR_ARG;
-  }
-  AVD_CHECK_LAUNCH();
-  return AVD_OK;
-}
-
-int avd_bn_bwd_reduce(const void* y, int ydt, const void* gout, int gdt, int pool_mode,
-                      const float* scale, const float* shift, const float* mean,
-                      const float* invstd, float* parts, int N, int B, int C, int H, int W,
-                      void* stream) {
-  if (!y || !gout || !scale || !shift || !mean || !invstd || !parts) return AVD_ERR_ARG;
-  if (N <= 0 || B <= 0 || N % B || (pool_mode != 0 && pool_mode != 1)) return AVD_ERR_SHAPE;
-  if (pool_mode == 1 && gdt != AVD_F32) return AVD_ERR_DTYPE;
-  hipStream_t st = avd_stream(stream);
-  const int grid = avd_cdiv((long long)N * C, 4);
-  if (pool_mode == 0 && ydt == AVD_BF16 && gdt == AVD_BF16 && W % 8 == 0 && H % 2 == 0) {
-    bn_bwd_reduce_q4_kernel<<<grid, 256, 0, st>>>((const bf16*)y, (const bf16*)gout, scale, shift,
-                                                  mean, invstd, parts, N, B, C, H, W);
-    AVD_CHECK_LAUNCH();
-    return AVD_OK;
-  }
-#define AVD_R(TY, TG)                                                                         \
-  bn_bwd_reduce_kernel<TY, TG><<<grid, 256, 0, st>>>((const TY*)y, (const TG*)gout, pool_mode, \
-                                                     scale, shift, mean, invstd, parts, N, B,  \
-                                                     C, H, W);
-  if (ydt == AVD_F32 && gdt == AVD_F32) { AVD_R(float, float) }
-  else if (ydt == AVD_BF16 && gdt == AVD_BF16) { AVD_R(bf16, bf16) }
-  else if (ydt == AVD_BF16 && gdt == AVD_F32) { AVD_R(bf16, float) }
-  else if (ydt == AVD_F32 && gdt == AVD_BF16) { AVD_R(float, bf16) }
-  else return AVD_ERR_DTYPE;
-#undef AVD_R
-  AVD_CHECK_LAUNCH();
-  return AVD_OK;
-}
-
 int avd_bn_bwd_finalize(const float* parts, int G, int R, int C, long long count,
                         const float* gamma, const float* mean, const float* invstd, float* coef,
                         float* dgamma, float* dbeta, float* dbias, int accumulate, void* stream) {
@@ -791,36 +416,6 @@ int avd_bn_bwd_finalize(const float* parts, int G, int R, int C, long long count
   bn_bwd_finalize_kernel<<<C, 256, 0, avd_stream(stream)>>>(parts, G, R, C, count, gamma, mean,
                                                              invstd, coef, dgamma, dbeta, dbias,
                                                              accumulate);
-  AVD_CHECK_LAUNCH();
-  return AVD_OK;
-}
-
-int avd_bn_bwd_apply(const void* y, int ydt, const void* gout, int gdt, int pool_mode,
-                     const float* scale, const float* shift, const float* coef, void* dy, int dt,
-                     int N, int B, int C, int H, int W, void* stream) {
-  if (!y || !gout || !scale || !shift || !coef || !dy) return AVD_ERR_ARG;
-  if (N <= 0 || B <= 0 || N % B || (pool_mode != 0 && pool_mode != 1)) return AVD_ERR_SHAPE;
-  if (pool_mode == 1 && gdt != AVD_F32) return AVD_ERR_DTYPE;
-  hipStream_t st = avd_stream(stream);
-  if (pool_mode == 0 && ydt == AVD_BF16 && gdt == AVD_BF16 && dt == AVD_BF16 && W % 8 == 0 &&
-      H % 2 == 0) {
-    const long long total4 = (long long)N * C * (H / 2) * (W / 8);
-    bn_bwd_apply_q4_kernel<<<grid_for(total4), 256, 0, st>>>((const bf16*)y, (const bf16*)gout, scale,
-                                                             shift, coef, (bf16*)dy, total4, B, C, H,
-                                                             W);
-    AVD_CHECK_LAUNCH();
-    return AVD_OK;
-  }
-  const long long total = (long long)N * C * ((H + 1) / 2) * ((W + 1) / 2);
-#define AVD_A(TY, TG, TD)                                                                       \
-  bn_bwd_apply_kernel<TY, TG, TD><<<grid_for(total), 256, 0, st>>>(                            \
-      (const TY*)y, (const TG*)gout, pool_mode, scale, shift, coef, (TD*)dy, total, B, C, H, W);
-  if (ydt == AVD_F32 && gdt == AVD_F32 && dt == AVD_F32) { AVD_A(float, float, float) }
-  else if (ydt == AVD_BF16 && gdt == AVD_BF16 && dt == AVD_BF16) { AVD_A(bf16, bf16, bf16) }
-  else if (ydt == AVD_BF16 && gdt == AVD_F32 && dt == AVD_BF16) { AVD_A(bf16, float, bf16) }
-  else if (ydt == AVD_F32 && gdt == AVD_BF16 && dt == AVD_F32) { AVD_A(float, bf16, float) }
-  else return AVD_ERR_DTYPE;
-#undef AVD_A
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

@@ -19,7 +19,7 @@ def header_functions():
 
 def test_header_declares_functions():
     fns = header_functions()
-    assert "avd_conv2d_fwd" in fns and "avd_adam" in fns and len(fns) >= 25
+    assert "avd_cl_conv_fwd" in fns and "avd_adam" in fns and len(fns) >= 25
 
 
 def test_library_exports_every_declared_symbol():
@@ -37,21 +37,21 @@ def test_ctypes_prototypes_cover_header():
 def test_host_helpers():
     from avdino._lib import lib
     assert lib.avd_version() >= 1
-    assert lib.avd_conv2d_stat_tiles(112, 112) == 49
-    assert lib.avd_conv2d_stat_tiles(10, 10) == 1
-    assert lib.avd_conv2d_wgrad_chunks(7168, 16, 8, 5) == 1024
-    assert lib.avd_conv2d_wgrad_chunks(7168, 64, 32, 5) == 327
-    assert lib.avd_conv2d_wgrad_chunks(12, 16, 8, 5) == 12
+    assert lib.avd_cl_stat_rows(112, 112, 512, 5, 8, 16, 1) == 57344
+    assert lib.avd_cl_stat_rows(14, 14, 512, 3, 32, 64, 1) == 1024
+    assert lib.avd_cl_wgrad_chunks(7168, 16, 8, 5) == 512
+    assert lib.avd_cl_wgrad_chunks(7168, 64, 32, 5) == 256
+    assert lib.avd_cl_wgrad_chunks(12, 16, 8, 5) == 12
     assert lib.avd_colstats_parts(6144) == 96
 
 
 def test_argument_validation_without_launch():
     from avdino._lib import lib
     # null pointers -> AVD_ERR_ARG; bad shapes -> AVD_ERR_SHAPE; bad dtype -> AVD_ERR_DTYPE
-    assert lib.avd_conv2d_fwd(None, 0, None, None, None, 0, None, 1, 1, 28, 28, 8, 5, 2, None) == -4
+    assert lib.avd_cl_conv_fwd(None, None, None, None, None, 1, 1, 1, 8, 28, 28, 16, 5, 2, None) == -4
     dummy = ctypes.c_void_p(16)
-    assert lib.avd_conv2d_fwd(dummy, 0, dummy, None, dummy, 0, None, 1, 1, 28, 28, 8, 7, 2, None) == -1
-    assert lib.avd_conv2d_fwd(dummy, 7, dummy, None, dummy, 0, None, 1, 1, 28, 28, 8, 5, 2, None) == -2
+    assert lib.avd_cl_conv_fwd(dummy, dummy, None, dummy, None, 1, 1, 1, 8, 28, 28, 16, 7, 2, None) == -1
+    assert lib.avd_cl_conv_fwd(dummy, dummy, None, dummy, None, 7, 1, 1, 8, 28, 28, 16, 5, 2, None) == -4
     assert lib.avd_bn_finalize(dummy, 0, 1, 1, 2, dummy, dummy, 1e-5, 0.1, dummy, dummy, dummy,
                                dummy, None, None, None, None) == -1
     assert lib.avd_stage_views(dummy, 2, None, 1, None, 4, 784, dummy, 0, None) == -4
