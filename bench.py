@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every kernel from Python each step instead of replaying the "
                          "captured hipGraph of the step")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="multimodal DINO: run each step's teacher forward under the previous "
+                         "step's backward (engine.pipeline; same losses, measured no faster)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) for real runs; gloo only to rehearse N>1 with several "
                          "ranks sharing one GPU")
@@ -152,6 +155,7 @@ def build_workload(args, device, act, world, rank, avdist):
     eng = MultiCentralEngine(store, args.mode, E, D, P, Hyper(), act_dtype=act, grad_hook=hook,
                              buffer_hook=avdist.broadcast_buffers if world > 1 else None, seed=rank,
                              negatives="global", conv_fp8=args.dtype == "fp8")
+    eng.pipeline = args.pipeline
     pool = synthetic_pool(2, B, G, L, device, 1234 + rank)
     prec = "e4m3 MFMA mid-layer conv forward, bf16 maps/backward" if args.dtype == "fp8" else args.dtype
     cfg = {"mse": "BASELINE config 2", "infonce": "BASELINE config 3 shape, all-gathered negatives",
@@ -246,6 +250,13 @@ def main():
         raise SystemExit("--dtype fp8 is the multimodal DINO conv path (config 5); use --workload dino")
     eng, pool, B, workload, model = build_workload(args, device, act, world, rank, avdist)
 
+    def step(i):
+        """Step i of the run over the batch pool (multimodal DINO: the next batch rides along
+        for the pipelined teacher forward)."""
+        if getattr(eng, "pipeline", False):
+            return eng.step(pool[i % len(pool)], next_batch=pool[(i + 1) % len(pool)])
+        return eng.step(pool[i % len(pool)])
+
     # warm-up: eager steps (the second one times every instrumented kernel to find the dominant
     # one; the first one's launches are cold), then -- graph mode -- the step's capture
     # graph replay needs one eager warm-up step (it sizes every workspace) and the capture
@@ -263,7 +274,7 @@ def main():
     for i in range(args.warmup):
         ops.TIMER = ops.KernelTimer() if i == t_idx else None
         wtimer = ops.TIMER or wtimer
-        eng.step(pool[i % len(pool)])
+        step(i)
     ops.TIMER = None
     summ = wtimer.summary() if wtimer is not None else {}
     dominant = max(summ, key=lambda k: summ[k]["ms"]) if summ else None
@@ -297,8 +308,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = eng.step(pool[i % len(pool)])
+    for i in range(args.warmup, args.warmup + args.steps):
+        loss = step(i)
     t_issue = time.perf_counter() - t0
     torch.cuda.synchronize()
     if dist is not None:
@@ -316,8 +327,8 @@ def main():
         # timed region (inside a replayed graph there is no per-launch host hook)
         eng.use_graph = False
         ops.TIMER = ops.KernelTimer(only=watch)
-        for i in range(3):
-            eng.step(pool[i % len(pool)])
+        for i in range(args.warmup + args.steps, args.warmup + args.steps + 3):
+            step(i)
         torch.cuda.synchronize()
 
     timed = ops.TIMER.summary()
@@ -379,6 +390,7 @@ def main():
         "timed_region_s": round(elapsed, 4),
         "host_issue_ms_per_step": round(t_issue * 1e3 / args.steps, 3),
         "graph": use_graph,
+        "teacher_pipelined": bool(getattr(eng, "pipeline", False)),
         "final_loss": round(lv, 6),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "dino" \

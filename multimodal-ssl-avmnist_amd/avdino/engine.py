@@ -575,6 +575,19 @@ class MultiCentralEngine:
         self.sstate = StepState(store.device, hp.lr, hp.betas)
         self.use_graph = False     # step(): capture the device work once, replay it (bench)
         self.graph = GraphedStep()
+        # pipeline=True: step(batch, next_batch) runs the teacher forward of next_batch on a
+        # fourth stream under this step's backward (it only needs the EMA'd teacher and the next
+        # batch's global views), so the next step's loss finds the teacher output ready.  Same
+        # losses and parameters as the sequential step; the teacher's BN running statistics and
+        # counters run one batch ahead between steps (train-mode BN normalises with the batch's
+        # own statistics, so no output depends on them; under DDP the rank-0 buffer broadcast
+        # of the next step then carries rank 0's already-updated teacher statistics).  Measured
+        # no faster on the config-2 step (profiles/r2f_ab.txt: the chip is already shared by
+        # three streams), so off by default.
+        self.pipeline = False
+        self.tside = None
+        self._t_ready = None       # (id(batch), B, G) of the teacher output waiting in t_proj
+        self._tseed = None
 
     # student image branch on the side stream, concurrently with the audio branch: measured
     # slower (r1_39: 149.7k vs 152.4k pairs/s -- both branches' launches fill the chip, so
@@ -627,15 +640,15 @@ class MultiCentralEngine:
         self._join(i_done)
         return cat, (fi, ci, fa, ca)
 
-    def _fusion_fwd(self, prefix, cat, rows, tag, seed, ws=None):
+    def _fusion_fwd(self, prefix, cat, rows, tag, seed, ws=None, seed_off=None):
         """fusion: Linear(2E,E) -> ReLU -> Dropout(0.3, hard-coded dino.py:204/215) -> Linear(E,D)."""
         ws, st, E, D = ws or self.ws, self.store, self.E, self.D
+        seed_off = self.sstate.seed_off if seed_off is None else seed_off
         h = ws.get(tag + ".fh", rows * E)
         ops.linear_fwd(cat, st[prefix + ".fusion.0.weight"], st[prefix + ".fusion.0.bias"], h, rows,
                        x_ld=2 * E, mode=self.gm)
         r = ws.get(tag + ".fr", rows * E)
-        ops.act_fwd(h, r, 0, None, None, rows, 1, E, self.hp.fusion_dropout, seed,
-                    self.sstate.seed_off)
+        ops.act_fwd(h, r, 0, None, None, rows, 1, E, self.hp.fusion_dropout, seed, seed_off)
         out = ws.get(tag + ".fout", rows * D)
         ops.linear_fwd(r, st[prefix + ".fusion.3.weight"], st[prefix + ".fusion.3.bias"], out, rows,
                        mode=self.gm)
@@ -671,6 +684,47 @@ class MultiCentralEngine:
             labels.copy_(batch["label"].reshape(-1))
         return x_img, x_aud, B, G, L, labels
 
+    def stage_teacher(self, batch):
+        """The global views of a (pre-augmented) batch into the teacher's own staged inputs
+        (pipelined step: the student of the current step still reads its staged buffers)."""
+        if "aug" in batch:
+            raise ValueError("pipelined teacher: needs the batch's views ({'g_img', 'g_aud', ...})")
+        g_img, g_aud = batch["g_img"], batch["g_aud"]
+        B, G = g_img.shape[:2]
+        x_img = self.ws.get("tin.img", G * B * 784, self.act)
+        x_aud = self.ws.get("tin.aud", G * B * 12544, self.act)
+        ops.stage_views(g_img.contiguous(), G, None, 0, None, B, 784, x_img)
+        ops.stage_views(g_aud.contiguous(), G, None, 0, None, B, 12544, x_aud)
+        return x_img, x_aud, B, G
+
+    def _teacher_fwd(self, x_img, x_aud, B, G, seed_off=None):
+        """Teacher: global views, train-mode BN, no grad, into t_proj [G*B, P] (its workspace)."""
+        tws, st = self.tws, self.store
+        base = (self.seed * 1000003) & SEED_MASK
+        tcat, _ = self._encoder_fwd("teacher", self.t_img, self.t_aud, x_img[:G * B * 784],
+                                    x_aud[:G * B * 12544], G * B, G, "t", need_dgrad=False, ws=tws)
+        tout, _ = self._fusion_fwd("teacher", tcat, G * B, "t", base + 2, ws=tws, seed_off=seed_off)
+        t_proj = tws.get("t_proj", G * B * self.P)
+        self.tproj.forward(tws, st, "tp", tout, G * B, t_proj, 0.0, 0)
+        return t_proj
+
+    def _teacher_next(self, tin):
+        """Pipelined step: the teacher forward of the next batch on the fourth stream, after
+        everything queued so far on this one (the EMA'd teacher, the loss that read t_proj);
+        its fusion dropout uses the next step's counter offset.  Returns the completion event."""
+        main = torch.cuda.current_stream(self.store.device)
+        if self.tside is None:
+            self.tside = torch.cuda.Stream(self.store.device)
+            self._tseed = torch.zeros_like(self.sstate.seed_off)
+        self.tside.wait_stream(main)
+        with torch.cuda.stream(self.tside):
+            torch.add(self.sstate.seed_off, StepState.SEED_STRIDE, out=self._tseed)
+            x_img, x_aud, B, G = tin
+            self._teacher_fwd(x_img, x_aud, B, G, seed_off=self._tseed)
+            done = torch.cuda.Event()
+            done.record(self.tside)
+        return done
+
     # -------------------------------------------------------------- the step
     def forward(self, batch, training=True):
         # training=False skips the input-grad weight layouts (forward-only use of the API)
@@ -678,7 +732,7 @@ class MultiCentralEngine:
         Returns the loss (a device scalar in the workspace)."""
         return self._forward_staged(self.stage(batch, self.heads is not None), training)
 
-    def _forward_staged(self, staged, training=True):
+    def _forward_staged(self, staged, training=True, teacher_ready=False):
         hp, ws, st = self.hp, self.ws, self.store
         E, D, P = self.E, self.D, self.P
         with_orig = self.heads is not None
@@ -691,18 +745,12 @@ class MultiCentralEngine:
         base = (self.seed * 1000003) & SEED_MASK
 
         # teacher: global views (prefix of the staged buffers), train-mode BN, no grad -- on a
-        # side stream, concurrently with the student (independent until the loss)
-        def teacher():
-            tws = self.tws
-            tcat, _ = self._encoder_fwd("teacher", self.t_img, self.t_aud, x_img[:G * B * 784],
-                                        x_aud[:G * B * 12544], G * B, G, "t", need_dgrad=False,
-                                        ws=tws)
-            tout, _ = self._fusion_fwd("teacher", tcat, G * B, "t", base + 2, ws=tws)
-            t_proj = tws.get("t_proj", G * B * P)
-            self.tproj.forward(tws, st, "tp", tout, G * B, t_proj, 0.0, 0)
-            return t_proj
-
-        t_proj, t_done = self._on_side(teacher)
+        # side stream, concurrently with the student (independent until the loss); pipelined
+        # steps find it computed under the previous step's backward
+        if teacher_ready:
+            t_proj, t_done = self.tws.get("t_proj", G * B * P), None
+        else:
+            t_proj, t_done = self._on_side(lambda: self._teacher_fwd(x_img, x_aud, B, G))
         # student: all views (+ originals) in one pass per conv layer
         cat, senc = self._encoder_fwd("student", self.img, self.aud, x_img, x_aud, N, NG, "s",
                                       need_dgrad=training)
@@ -855,25 +903,35 @@ class MultiCentralEngine:
         from . import dist as avdist
         return not (self.mode == "infonce" and self.negatives != "local" and avdist.world(self.group) > 1)
 
-    def step(self, batch):
+    def step(self, batch, next_batch=None):
         """One full training step; returns the loss as a device tensor (no host sync).
         With ``use_graph`` everything after the input staging (and around the data-parallel
-        collectives) is a captured hipGraph replayed per step."""
+        collectives) is a captured hipGraph replayed per step.  With ``pipeline`` and the next
+        step's batch, that batch's teacher forward runs under this step's backward."""
         if self.buffer_hook is not None:
             self.buffer_hook(self.store)
         self.sstate.set_lr(self.hp.lr)
         staged = self.stage(batch, self.heads is not None)
+        B, G = staged[2], staged[3]
+        ready = self._t_ready == (id(batch), B, G)   # the previous step ran this batch's teacher
+        tin = None
+        if self.pipeline and next_batch is not None and self.side is not None:
+            tin = self.stage_teacher(next_batch)
 
         def body():
-            self._forward_staged(staged, training=True)
+            self._forward_staged(staged, training=True, teacher_ready=ready)
             self.update_center()
             ema_step(self.store, self.hp.momentum)     # update_teacher: pre-step student
+            t_done = self._teacher_next(tin) if tin is not None else None
             self.backward()
             if self.grad_hook is None:
                 adam_step_dev(self.store, self.hp, self.sstate)
+            self._join(t_done)
+            self.store.flush_nbt()
 
+        self._t_ready = (id(next_batch),) + tin[2:4] if tin is not None else None
         if self.use_graph and self._graphable():
-            self.graph.run(staged[2:5], body)
+            self.graph.run(staged[2:5] + (ready, tin is not None), body)
         else:
             body()
         if self.grad_hook is not None:

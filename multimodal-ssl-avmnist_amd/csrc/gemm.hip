@@ -376,9 +376,12 @@ Plan plan_for(int M, int N, int K) {
   else if (K >= 1024)   // deep K: the split below restores the block count
     p = (M >= 128 && N >= 128) ? Plan{128, 128, 1, K} : (M >= 128 ? Plan{128, 64, 1, K} : p);
   const long long t = tiles(p.bm, p.bn);
+  // split target (blocks) and minimum K rows per split: AVDINO_GEMM_SPLIT / AVDINO_GEMM_KMIN
+  static const int target = getenv("AVDINO_GEMM_SPLIT") ? atoi(getenv("AVDINO_GEMM_SPLIT")) : 512;
+  static const int kmin = getenv("AVDINO_GEMM_KMIN") ? atoi(getenv("AVDINO_GEMM_KMIN")) : 256;
   if (t < 224 && K >= 512) {
-    int s = (int)std::min<long long>(avd_cdiv(512, t), K / 256);
-    s = std::max(1, std::min(s, 64));
+    int s = (int)std::min<long long>(avd_cdiv(target, t), K / kmin);
+    s = std::max(1, std::min(s, 128));
     if (s > 1) {
       p.kchunk = avd_cdiv(avd_cdiv(K, s), 32) * 32;
       p.splits = avd_cdiv(K, p.kchunk);

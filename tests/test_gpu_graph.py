@@ -105,3 +105,42 @@ def test_graph_replay_equals_eager_simclr():
     assert torch.equal(res[0][1].student, res[1][1].student)
     assert res[1][2].adam_t == res[0][2].adam_t
     assert [int(s.t.item()) for s in res[1][2].sstates] == res[0][2].adam_t
+
+
+@pytest.mark.parametrize("graph", [False, True])
+@pytest.mark.parametrize("mode", ["mse", "semi_supervised"])
+def test_pipelined_teacher_equals_sequential(mode, graph):
+    """engine.pipeline: the next batch's teacher forward under this step's backward (fourth
+    stream, the next step's dropout offset) gives the sequential step's losses and parameters
+    bit for bit; only the teacher's BN running statistics run one batch ahead."""
+    from avdino.engine import Hyper, MultiCentralEngine
+    from avdino.params import ParamStore
+    from avdino.spec import multimodal_dino_sd
+    E, D, P, B, G, L = 32, 32, 16, 8, 2, 4
+    res = []
+    for pipe in (False, True):
+        store = ParamStore(multimodal_dino_sd(mode, E, D, P), "cuda")
+        store.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in
+                               make_state(OS.multimodal_dino_spec(mode, E, D, P), 402).items()})
+        eng = MultiCentralEngine(store, mode, E, D, P, Hyper(dropout=0.3, fusion_dropout=0.3),
+                                 act_dtype=torch.bfloat16, seed=5)
+        eng.use_graph = graph
+        eng.pipeline = pipe
+        batches = [_dev(make_multimodal_batch(B, G, L, 4200 + i)) for i in range(2)]
+        losses = [eng.step(batches[i % 2], next_batch=batches[(i + 1) % 2]).item()
+                  for i in range(6)]
+        res.append((store, losses, eng))
+    (s0, l0, _), (s1, l1, e1) = res
+    assert l0 == l1, (l0, l1)
+    assert len(set(l1)) > 1
+    if graph:
+        assert len(e1.graph.graphs) == 1
+    assert torch.equal(s0.student, s1.student)
+    assert torch.equal(s0.teacher, s1.teacher)
+    assert torch.equal(s0.adam_m, s1.adam_m) and torch.equal(s0.adam_v, s1.adam_v)
+    # the student's BN buffers match; the pipelined teacher has seen one more batch
+    sb = [k for k in s0.buffers if k.startswith("student.") or k == "center"]
+    assert sb
+    for k in sb:
+        assert torch.equal(s0[k], s1[k]), k
+    assert e1._t_ready is not None
