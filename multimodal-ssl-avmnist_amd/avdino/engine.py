@@ -557,6 +557,7 @@ class MultiCentralEngine:
         # teacher forward and the image-branch backward run on a side stream with their own
         # scratch (Workspace, split-K GEMM buffer), joined by events; concurrent=False keeps
         # everything on the caller's stream
+        concurrent = concurrent and os.environ.get("AVDINO_SINGLE_STREAM", "0") != "1"
         self.side = torch.cuda.Stream(store.device) if (concurrent and store.device.type == "cuda") else None
         # the audio branch's mid-layer weight gradients on a third stream (AVDINO_WGRAD_SIDE=0: off)
         self.wside = (torch.cuda.Stream(store.device) if (self.side is not None and
