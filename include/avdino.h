@@ -197,13 +197,15 @@ int avd_cl_conv_dgrad_bnreduce(const void* dy, const void* wk_d, void* dx, const
  * avd_cl_conv_wgrad + avd_cl_conv_dgrad for CentralUnimodalAudio conv2-4 / bn2-4 and
  * CentralUnimodalImage conv2 / bn2, unimodal.py:127-221).  B = samples per BN group (N/B <= 8).
  * avd_cl_bnapply_ok() = 1 when both kernels serve the shape, else use the three unfused calls
- * (AVD_ERR_SHAPE from either entry point otherwise).  Bit-identical to the unfused calls. */
+ * (AVD_ERR_SHAPE from either entry point otherwise).  Bit-identical to the unfused calls.
+ * avd_cl_conv_dgrad_bnapply's dy (nullable, NHWC like y, not aliasing y or dx) also receives the
+ * dy it forms, so a plain avd_cl_conv_wgrad can follow without a separate apply pass. */
 int avd_cl_bnapply_ok(int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
                       int gmode);
 int avd_cl_conv_dgrad_bnapply(const void* y, const void* gout, int gmode, const float* scale,
                               const float* shift, const float* coef, const void* wk_d, void* dx,
-                              int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
-                              int pad, void* stream);
+                              void* dy, int dt, int N, int B, int Cin, int H, int W, int Cout,
+                              int K, int pad, void* stream);
 int avd_cl_conv_wgrad_bnapply(const void* x, const void* y, const void* gout, int gmode,
                               const float* scale, const float* shift, const float* coef, int dt,
                               float* dw_parts, int N, int B, int Cin, int H, int W, int Cout,

@@ -39,7 +39,7 @@ PROTOS = {
     "avd_cl_c1_moment_cols": [I],
     "avd_counters_add": [P, P, P, I, P],
     "avd_cl_conv_dgrad_bnreduce": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
-    "avd_cl_conv_dgrad_bnapply": [P, P, I, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "avd_cl_conv_dgrad_bnapply": [P, P, I, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "avd_cl_conv_wgrad_bnapply": [P, P, P, I, P, P, P, I, P, I, I, I, I, I, I, I, I, P],
     "avd_cl_bn_relu_pool": [P, I, P, P, P, I, I, I, I, I, I, P],
     "avd_cl_bn_bwd_rows": [I, I, I, I, I],

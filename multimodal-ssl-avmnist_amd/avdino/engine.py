@@ -285,6 +285,9 @@ class ConvBranch:
             return 0
         return ops.cl_dgrad_bnreduce_rows(self.act, N, B, ci, H, H, co, k, pad)
 
+    # input-gradient kernel forms the BN-backward apply and stores dy (AVDINO_DGRAD_APPLY=1)
+    DGRAD_APPLY = os.environ.get("AVDINO_DGRAD_APPLY", "0") == "1"
+
     def backward(self, ws, store, ctx, dfeat, wstream=None):
         """dfeat: f32 [N, F] gradient of the features; writes conv/BN parameter grads.
         wstream: a second stream for the mid layers' weight gradients (they only read dy and
@@ -343,6 +346,27 @@ class ConvBranch:
                 gout = dx
                 continue
             dy = ws.get(f"bwd_dy{i}" if wstream is not None else "bwd_dy", N * Ho * Ho * co, self.act)
+            if (self.DGRAD_APPLY and i > 0 and mode in (0, 2) and not self._dgrad_reduce_rows(ctx, i, N, B)
+                    and ops.cl_bnapply_ok(self.act, N, B, ci, H, H, co, k, pad, mode)):
+                # BN-backward apply formed in the input-gradient kernel's staging, which also
+                # stores dy for the weight gradient (no separate apply pass re-reading y)
+                dx = ws.get(f"bwd_dx{i % 2}", N * H * H * ci, self.act)   # != gout (bwd_dx{(i+1) % 2})
+                ops.cl_conv_dgrad_bnapply(y, gout, mode, st[2], st[3], coef, ctx["wts"][i][1], dx, N, B,
+                                          ci, H, H, co, k, pad, dy=dy)
+                if wstream is not None:
+                    wparts = ws.get(f"wgrad_parts{i}", nch * co * ci * k * k)
+                    wstream.wait_stream(main)
+                    with torch.cuda.stream(wstream):
+                        ops.cl_conv_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
+                        ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
+                        ev = torch.cuda.Event()
+                        ev.record(wstream)
+                    wdone.append(ev)
+                else:
+                    ops.cl_conv_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
+                    ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
+                gout = dx
+                continue
             ops.cl_bn_bwd_apply(y, gout, mode, st[2], st[3], coef, dy, N, B, co, Ho, Ho)
             if wstream is not None and i > 0:
                 wparts = ws.get(f"wgrad_parts{i}", nch * co * ci * k * k)

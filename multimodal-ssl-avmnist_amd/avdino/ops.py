@@ -300,17 +300,22 @@ def _gout_check(gout, gmode, y, N, Ho, Wo, Cout):
           "bnapply gout")
 
 
-def cl_conv_dgrad_bnapply(y, gout, gmode, scale, shift, coef, wk_d, dx, N, B, Cin, H, W, Cout, K, pad):
-    """dx = input gradient of the conv for dy = bn_bwd_apply(y, gout, ...) formed on chip."""
+def cl_conv_dgrad_bnapply(y, gout, gmode, scale, shift, coef, wk_d, dx, N, B, Cin, H, W, Cout, K, pad,
+                          dy=None):
+    """dx = input gradient of the conv for dy = bn_bwd_apply(y, gout, ...) formed on chip;
+    ``dy`` (optional, like y) also receives that dy (for the weight gradient)."""
     Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
     _need(y.numel() == N * Ho * Wo * Cout and dx.numel() == N * H * W * Cin, "bnapply dgrad sizes")
     _need(y.dtype == dx.dtype == wk_d.dtype, "bnapply dgrad dtypes")
+    _need(dy is None or (dy.numel() == y.numel() and dy.dtype == y.dtype), "bnapply dgrad dy")
     _gout_check(gout, gmode, y, N, Ho, Wo, Cout)
-    nb = (y.numel() + dx.numel()) * y.element_size() + gout.numel() * gout.element_size()
+    nb = ((y.numel() + dx.numel() + (0 if dy is None else dy.numel())) * y.element_size()
+          + gout.numel() * gout.element_size())
     fl = 2 * N * Cin * H * W * Cout * K * K
-    _timed(f"cl_conv_dgrad_bnapply[{N}x{Ho}x{Wo}x{Cout}->{Cin} k{K}p{pad} g{gmode} {y.dtype}]", nb, fl,
+    _timed(f"cl_conv_dgrad_bnapply{'' if dy is None else '+dy'}[{N}x{Ho}x{Wo}x{Cout}->{Cin} k{K}p{pad} "
+           f"g{gmode} {y.dtype}]", nb, fl,
            lambda: call("avd_cl_conv_dgrad_bnapply", p(y), p(gout), gmode, p(scale), p(shift), p(coef),
-                        p(wk_d), p(dx), dtcode(y), N, B, Cin, H, W, Cout, K, pad, stream()))
+                        p(wk_d), p(dx), p(dy), dtcode(y), N, B, Cin, H, W, Cout, K, pad, stream()))
 
 
 def cl_conv_wgrad_bnapply(x, y, gout, gmode, scale, shift, coef, parts, N, B, Cin, H, W, Cout, K, pad):

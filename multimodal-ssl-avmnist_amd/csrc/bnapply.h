@@ -26,6 +26,7 @@ struct ApplyArgs {
   const float* coef;   // [G*C][3] = (k1, kx, k0)
   int B;               // samples per BN group
   int G;               // groups (<= APPLY_GMAX)
+  void* dy = nullptr;  // input-gradient kernel only: also store the dY it forms (tile interiors)
 };
 constexpr int APPLY_GMAX = 8;
 

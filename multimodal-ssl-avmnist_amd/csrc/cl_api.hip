@@ -53,8 +53,8 @@ int avd_ws_dgrad_bnapply_serves(int dt, int N, int B, int Cin, int H, int W, int
                                 int pad, int gmode);
 int avd_ws_conv_dgrad_bnapply(const void* y, const void* gout, int gmode, const float* scale,
                               const float* shift, const float* coef, const void* wk_d, void* dx,
-                              int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
-                              hipStream_t st);
+                              void* dy, int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
+                              int pad, hipStream_t st);
 int avd_wg_bnapply_serves(int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
                           int gmode);
 int avd_wg_conv_wgrad_ex(const void* x, const void* dy, int dt, float* parts, int N, int Cin,
@@ -241,11 +241,12 @@ int avd_cl_bnapply_ok(int dt, int N, int B, int Cin, int H, int W, int Cout, int
 
 int avd_cl_conv_dgrad_bnapply(const void* y, const void* gout, int gmode, const float* scale,
                               const float* shift, const float* coef, const void* wk_d, void* dx,
-                              int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
-                              int pad, void* stream) {
+                              void* dy, int dt, int N, int B, int Cin, int H, int W, int Cout,
+                              int K, int pad, void* stream) {
   if (!y || !gout || !scale || !shift || !coef || !wk_d || !dx || !dt_ok(dt)) return AVD_ERR_ARG;
-  const int r = avd_ws_conv_dgrad_bnapply(y, gout, gmode, scale, shift, coef, wk_d, dx, dt, N, B,
-                                          Cin, H, W, Cout, K, pad, avd_stream(stream));
+  if (dy && (dy == y || dy == dx)) return AVD_ERR_ARG;
+  const int r = avd_ws_conv_dgrad_bnapply(y, gout, gmode, scale, shift, coef, wk_d, dx, dy, dt, N,
+                                          B, Cin, H, W, Cout, K, pad, avd_stream(stream));
   return r > 0 ? AVD_OK : (r == 0 ? AVD_ERR_SHAPE : r);
 }
 

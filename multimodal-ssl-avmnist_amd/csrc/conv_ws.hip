@@ -250,8 +250,18 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
       const int task = tid + 256 * i;
       if (task >= WT) continue;
       u4 o[4] = {u4{0u, 0u, 0u, 0u}, u4{0u, 0u, 0u, 0u}, u4{0u, 0u, 0u, 0u}, u4{0u, 0u, 0u, 0u}};
-      if (wgo[i] >= 0 && (unsigned)(ty0 - L::PAD + wrow[i]) < (unsigned)L::H)
+      if (wgo[i] >= 0 && (unsigned)(ty0 - L::PAD + wrow[i]) < (unsigned)L::H) {
         apply_window<AP == 1 ? 0 : 2, L::CIN>(prew[i], ct + 8 * (task % L::VPP), o);
+        // dY out for the weight gradient: each window of the map once, from the tile whose
+        // interior rows [PAD, PAD + TH) of the staged strip hold it (windows never straddle)
+        if (aa.dy && (unsigned)(wrow[i] - L::PAD) < (unsigned)L::TH) {
+          bf16* d = reinterpret_cast<bf16*>(aa.dy) + ((long long)n0 * L::H + ty0 - L::PAD) * L::W * L::CIN + wgo[i];
+          *reinterpret_cast<u4*>(d) = o[0];
+          *reinterpret_cast<u4*>(d + L::CIN) = o[1];
+          *reinterpret_cast<u4*>(d + L::W * L::CIN) = o[2];
+          *reinterpret_cast<u4*>(d + (L::W + 1) * L::CIN) = o[3];
+        }
+      }
       *reinterpret_cast<u4*>(xs + wlo[i]) = o[0];
       *reinterpret_cast<u4*>(xs + wlo[i] + L::PS) = o[1];
       *reinterpret_cast<u4*>(xs + wlo[i] + L::RS * L::PS) = o[2];
@@ -618,11 +628,11 @@ int avd_ws_conv_dgrad(const void* dy, const void* wk_d, void* dx, int dt, int N,
 // (0 = pooled NHWC bf16, 2 = f32 (c,h,w) flatten).  1 = launched, 0 = not served, < 0 = error.
 int avd_ws_conv_dgrad_bnapply(const void* y, const void* gout, int gmode, const float* scale,
                               const float* shift, const float* coef, const void* wk_d, void* dx,
-                              int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
-                              hipStream_t st) {
+                              void* dy, int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
+                              int pad, hipStream_t st) {
   if (dt != AVD_BF16 || ws_disabled() || (gmode != 0 && gmode != 2) || B <= 0 || N % B) return 0;
   const int Ho = H + 2 * pad - K + 1, Wo = W + 2 * pad - K + 1, dp = K - 1 - pad;
-  const ApplyArgs aa{gout, scale, shift, coef, B, N / B};
+  const ApplyArgs aa{gout, scale, shift, coef, B, N / B, dy};
   int r = 0;
 #define AVD_DA(LL)                                                                               \
   if (is<LL>(Cout, Ho, Wo, Cin, K, dp)) {                                                       \

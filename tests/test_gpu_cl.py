@@ -509,9 +509,19 @@ def test_bnapply_fused_dgrad_wgrad_match_unfused(ops, shape):
     ops.cl_conv_wgrad_bnapply(x, y, gout, gmode, scale, shift, coef, p1, N, B, Cin, H, H, Cout, K, pad)
     dx1 = torch.full_like(dx0, float("nan"))
     ops.cl_conv_dgrad_bnapply(y, gout, gmode, scale, shift, coef, wd, dx1, N, B, Cin, H, H, Cout, K, pad)
+    # dgrad that also stores the dy it forms (AVDINO_DGRAD_APPLY), then the plain weight gradient
+    dx2 = torch.full_like(dx0, float("nan"))
+    dy2 = torch.full_like(dy, float("nan"))
+    ops.cl_conv_dgrad_bnapply(y, gout, gmode, scale, shift, coef, wd, dx2, N, B, Cin, H, H, Cout, K,
+                              pad, dy=dy2)
+    p2 = torch.full_like(p0, float("nan"))
+    ops.cl_conv_wgrad(x, dy2, p2, N, Cin, H, H, Cout, K, pad)
     torch.cuda.synchronize()
     assert torch.equal(wsum(p1), wsum(p0))
     assert torch.equal(dx1, dx0)
+    assert torch.equal(dy2, dy)
+    assert torch.equal(dx2, dx0)
+    assert torch.equal(wsum(p2), wsum(p0))
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
