@@ -287,6 +287,8 @@ class ConvBranch:
 
     # input-gradient kernel forms the BN-backward apply and stores dy (AVDINO_DGRAD_APPLY=1)
     DGRAD_APPLY = os.environ.get("AVDINO_DGRAD_APPLY", "0") == "1"
+    # layers whose weight gradient stays on the main stream (A/B: AVDINO_WGRAD_MAIN=3,2)
+    WGRAD_MAIN = {int(v) for v in os.environ.get("AVDINO_WGRAD_MAIN", "").split(",") if v.strip()}
 
     def backward(self, ws, store, ctx, dfeat, wstream=None):
         """dfeat: f32 [N, F] gradient of the features; writes conv/BN parameter grads.
@@ -368,7 +370,7 @@ class ConvBranch:
                 gout = dx
                 continue
             ops.cl_bn_bwd_apply(y, gout, mode, st[2], st[3], coef, dy, N, B, co, Ho, Ho)
-            if wstream is not None and i > 0:
+            if wstream is not None and i > 0 and i not in self.WGRAD_MAIN:
                 wparts = ws.get(f"wgrad_parts{i}", nch * co * ci * k * k)
                 wstream.wait_stream(main)
                 with torch.cuda.stream(wstream):
