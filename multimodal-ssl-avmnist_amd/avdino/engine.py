@@ -620,15 +620,22 @@ class MultiCentralEngine:
     # slower (r1_39: 149.7k vs 152.4k pairs/s -- both branches' launches fill the chip, so
     # they only contend), kept for experiments
     IMAGE_SIDE = os.environ.get("AVDINO_IMAGE_SIDE", "0") == "1"
+    # capture order of the heads' backward (A/B: AVDINO_HEADS_LATE=0 queues it first)
+    HEADS_LATE = os.environ.get("AVDINO_HEADS_LATE", "1") == "1"
+    FHEADS_LATE = os.environ.get("AVDINO_FHEADS_LATE", "1") == "1"
 
     # -------------------------------------------------------------- streams
-    def _on_side(self, fn):
-        """Run fn() on the side stream after everything queued so far on the current stream;
-        returns (fn's result, completion event), or runs inline without a side stream."""
+    def _on_side(self, fn, after=None):
+        """Run fn() on the side stream after everything queued so far on the current stream (or
+        after the event ``after`` recorded on it earlier); returns (fn's result, completion
+        event), or runs inline without a side stream."""
         if self.side is None:
             return fn(), None
         main = torch.cuda.current_stream(self.store.device)
-        self.side.wait_stream(main)
+        if after is not None:
+            self.side.wait_event(after)
+        else:
+            self.side.wait_stream(main)
         with torch.cuda.stream(self.side):
             out = fn()
             done = torch.cuda.Event()
@@ -815,8 +822,14 @@ class MultiCentralEngine:
                     dza.mul_(hp.alpha)
                 return (zi, za), (ci, ca, dzi, dza)
 
+            f_after = None
             if self.mode == "infonce":
                 head_out, hctx = heads()
+            elif self.FHEADS_LATE and self.side is not None:
+                # queued (captured) after the fusion / projection below, depending only on
+                # what is queued so far (the cat)
+                f_after = torch.cuda.Event()
+                f_after.record(torch.cuda.current_stream(st.device))
             else:
                 (head_out, hctx), h_done = self._on_side(heads)
             n_parts = V * B + B
@@ -824,6 +837,8 @@ class MultiCentralEngine:
         s_proj = ws.get("s_proj", V * B * P)
         spc = self.sproj.forward(ws, st, "sp", fout, V * B, s_proj, hp.dropout, base + 3,
                                  seed_off=self.sstate.seed_off)
+        if with_orig and f_after is not None:
+            (head_out, hctx), h_done = self._on_side(heads, after=f_after)
         self._join(t_done)
 
         # DINO loss (+ centring and centre EMA) -- forward and d/ds in one pass
@@ -878,6 +893,12 @@ class MultiCentralEngine:
         # d cat buffer [N, 2E]: rows [0, V*B) from the fusion, rows [V*B, N) from the heads
         dcat = ws.get("dcat", N * 2 * E)
         h_done = None
+        # the heads' backward depends only on what is queued so far; queued (captured) after the
+        # main chain below so a replayed graph submits the critical path's launches first
+        h_after = None
+        if c["hctx"] is not None and self.HEADS_LATE and self.side is not None:
+            h_after = torch.cuda.Event()
+            h_after.record(torch.cuda.current_stream(self.store.device))
         if c["hctx"] is not None:
             # the heads' backward (disjoint dcat rows and parameters) on the side stream,
             # concurrently with the projection / fusion backward
@@ -891,7 +912,8 @@ class MultiCentralEngine:
                 hi.backward(hws, st, ci, dzi, dcat, dx_ld=2 * E, dx_off=off)
                 ha.backward(hws, st, ca, dza, dcat, dx_ld=2 * E, dx_off=off + E)
 
-            _, h_done = self._on_side(heads_bwd)
+            if h_after is None:
+                _, h_done = self._on_side(heads_bwd)
         dfout = ws.get("dfout", V * B * D)
         self.sproj.backward(ws, st, c["spc"], c["ds"], dfout)
         h, r = c["sfus"]
@@ -904,6 +926,8 @@ class MultiCentralEngine:
         ops.linear_bwd(dh, c["cat"], st["student.fusion.0.weight"], st.grad_of("student.fusion.0.weight"),
                        st.grad_of("student.fusion.0.bias"), dcat, V * B, x_ld=2 * E, dx_ld=2 * E,
                        mode=self.gm)
+        if h_after is not None:
+            _, h_done = self._on_side(heads_bwd, after=h_after)
         self._join(h_done)
         fi, cimg, fa, caud = c["senc"]
 
