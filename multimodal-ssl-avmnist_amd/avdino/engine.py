@@ -437,15 +437,23 @@ class ProjHead:
                 "seed_off": seed_off}
 
     def backward(self, ws, store, ctx, dout, dx, dx_ld=None, dx_off=0):
+        for _ in self.backward_steps(ws, store, ctx, dout, dx, dx_ld, dx_off):
+            pass
+
+    def backward_steps(self, ws, store, ctx, dout, dx, dx_ld=None, dx_off=0):
+        """backward() as a generator that yields between its launch groups (so two heads'
+        backward passes on two streams can be queued interleaved)."""
         p, Hd, rows, G = self.p, self.h, ctx["rows"], ctx["G"]
         rpg = rows // G
         da = ws.get("head_da", rows * Hd)
         ops.linear_bwd(dout, ctx["a"], store[p + ".mlp.4.weight"], store.grad_of(p + ".mlp.4.weight"),
                        store.grad_of(p + ".mlp.4.bias"), da, rows, mode=self.gm)
+        yield
         st = ctx["st"]
         dz = ws.get("head_dz", rows * Hd)
         ops.act_bwd(ctx["h"], da, dz, 1, st[2], st[3], rows, G, Hd, ctx["drop_p"], ctx["seed"],
                     ctx.get("seed_off"))
+        yield
         R = ops.colstats_parts(rpg)
         parts = ws.get("bwd_parts", Hd * G * R * 2)
         ops.bn1d_bwd_reduce(ctx["h"], dz, st[0], st[1], rows, G, Hd, parts)
@@ -454,6 +462,7 @@ class ProjHead:
                             store.grad_of(p + ".mlp.1.weight"), store.grad_of(p + ".mlp.1.bias"), None)
         dh = ws.get("head_dh", rows * Hd)
         ops.bn1d_bwd_apply(ctx["h"], dz, coef, dh, rows, G, Hd)
+        yield
         ops.linear_bwd(dh, ctx["x"], store[p + ".mlp.0.weight"], store.grad_of(p + ".mlp.0.weight"),
                        store.grad_of(p + ".mlp.0.bias"), dx, rows, x_ld=ctx["x_ld"],
                        x_off=ctx["x_off"], dx_ld=dx_ld, dx_off=dx_off, mode=self.gm)
@@ -620,8 +629,8 @@ class MultiCentralEngine:
     # slower (r1_39: 149.7k vs 152.4k pairs/s -- both branches' launches fill the chip, so
     # they only contend), kept for experiments
     IMAGE_SIDE = os.environ.get("AVDINO_IMAGE_SIDE", "0") == "1"
-    # capture order of the heads' backward (A/B: AVDINO_HEADS_LATE=0 queues it first)
-    HEADS_LATE = os.environ.get("AVDINO_HEADS_LATE", "1") == "1"
+    # the heads' backward queued interleaved with the main chain's (else after it)
+    INTERLEAVE = os.environ.get("AVDINO_INTERLEAVE", "1") == "1"
     FHEADS_LATE = os.environ.get("AVDINO_FHEADS_LATE", "1") == "1"
 
     # -------------------------------------------------------------- streams
@@ -893,41 +902,62 @@ class MultiCentralEngine:
         # d cat buffer [N, 2E]: rows [0, V*B) from the fusion, rows [V*B, N) from the heads
         dcat = ws.get("dcat", N * 2 * E)
         h_done = None
-        # the heads' backward depends only on what is queued so far; queued (captured) after the
-        # main chain below so a replayed graph submits the critical path's launches first
-        h_after = None
-        if c["hctx"] is not None and self.HEADS_LATE and self.side is not None:
+
+        # the heads' backward (disjoint dcat rows and parameters) on the side stream, beside
+        # the projection / fusion backward on this one; both chains are generators yielding
+        # between launch groups and are queued interleaved (INTERLEAVE), so a replayed graph
+        # -- whose launches go out in capture order -- runs them side by side
+        def heads_steps():
+            ci, ca, dzi, dza = c["hctx"]
+            if dheads is not None:
+                dzi, dza = dheads
+            hi, ha = self.heads
+            off = V * B * 2 * E
+            hws = self.iws
+            yield from hi.backward_steps(hws, st, ci, dzi, dcat, dx_ld=2 * E, dx_off=off)
+            yield from ha.backward_steps(hws, st, ca, dza, dcat, dx_ld=2 * E, dx_off=off + E)
+
+        def main_steps():
+            dfout = ws.get("dfout", V * B * D)
+            yield from self.sproj.backward_steps(ws, st, c["spc"], c["ds"], dfout)
+            h, r = c["sfus"]
+            dr = ws.get("fus_dr", V * B * E)
+            ops.linear_bwd(dfout, r, st["student.fusion.3.weight"], st.grad_of("student.fusion.3.weight"),
+                           st.grad_of("student.fusion.3.bias"), dr, V * B, mode=self.gm)
+            yield
+            dh = ws.get("fus_dh", V * B * E)
+            ops.act_bwd(h, dr, dh, 0, None, None, V * B, 1, E, self.hp.fusion_dropout,
+                        ((self.seed * 1000003) & SEED_MASK) + 1, self.sstate.seed_off)
+            yield
+            ops.linear_bwd(dh, c["cat"], st["student.fusion.0.weight"], st.grad_of("student.fusion.0.weight"),
+                           st.grad_of("student.fusion.0.bias"), dcat, V * B, x_ld=2 * E, dx_ld=2 * E,
+                           mode=self.gm)
+
+        def drain(gen):
+            for _ in gen:
+                pass
+
+        if c["hctx"] is None:
+            drain(main_steps())
+        elif self.side is None:
+            drain(heads_steps())
+            drain(main_steps())
+        elif self.INTERLEAVE:
+            main = torch.cuda.current_stream(self.store.device)
+            self.side.wait_stream(main)
+            gens = [(main_steps(), main), (heads_steps(), self.side)]
+            while gens:
+                for g in list(gens):
+                    with torch.cuda.stream(g[1]):
+                        if next(g[0], StopIteration) is StopIteration:
+                            gens.remove(g)
+            h_done = torch.cuda.Event()
+            h_done.record(self.side)
+        else:
             h_after = torch.cuda.Event()
             h_after.record(torch.cuda.current_stream(self.store.device))
-        if c["hctx"] is not None:
-            # the heads' backward (disjoint dcat rows and parameters) on the side stream,
-            # concurrently with the projection / fusion backward
-            def heads_bwd():
-                ci, ca, dzi, dza = c["hctx"]
-                if dheads is not None:
-                    dzi, dza = dheads
-                hi, ha = self.heads
-                off = V * B * 2 * E
-                hws = self.iws
-                hi.backward(hws, st, ci, dzi, dcat, dx_ld=2 * E, dx_off=off)
-                ha.backward(hws, st, ca, dza, dcat, dx_ld=2 * E, dx_off=off + E)
-
-            if h_after is None:
-                _, h_done = self._on_side(heads_bwd)
-        dfout = ws.get("dfout", V * B * D)
-        self.sproj.backward(ws, st, c["spc"], c["ds"], dfout)
-        h, r = c["sfus"]
-        dr = ws.get("fus_dr", V * B * E)
-        ops.linear_bwd(dfout, r, st["student.fusion.3.weight"], st.grad_of("student.fusion.3.weight"),
-                       st.grad_of("student.fusion.3.bias"), dr, V * B, mode=self.gm)
-        dh = ws.get("fus_dh", V * B * E)
-        ops.act_bwd(h, dr, dh, 0, None, None, V * B, 1, E, self.hp.fusion_dropout,
-                    ((self.seed * 1000003) & SEED_MASK) + 1, self.sstate.seed_off)
-        ops.linear_bwd(dh, c["cat"], st["student.fusion.0.weight"], st.grad_of("student.fusion.0.weight"),
-                       st.grad_of("student.fusion.0.bias"), dcat, V * B, x_ld=2 * E, dx_ld=2 * E,
-                       mode=self.gm)
-        if h_after is not None:
-            _, h_done = self._on_side(heads_bwd, after=h_after)
+            drain(main_steps())
+            _, h_done = self._on_side(lambda: drain(heads_steps()), after=h_after)
         self._join(h_done)
         fi, cimg, fa, caud = c["senc"]
 
