@@ -622,7 +622,7 @@ class MultiCentralEngine:
         # three streams), so off by default.
         self.pipeline = False
         self.tside = None
-        self._t_ready = None       # (id(batch), B, G) of the teacher output waiting in t_proj
+        self._t_ready = None       # (batch, B, G) of the teacher output waiting in t_proj
         self._tseed = None
 
     # student image branch on the side stream, concurrently with the audio branch: measured
@@ -994,7 +994,9 @@ class MultiCentralEngine:
         self.sstate.set_lr(self.hp.lr)
         staged = self.stage(batch, self.heads is not None)
         B, G = staged[2], staged[3]
-        ready = self._t_ready == (id(batch), B, G)   # the previous step ran this batch's teacher
+        # the previous step ran this batch's teacher (the reference held in _t_ready keeps the
+        # object alive, so identity cannot be a recycled id)
+        ready = self._t_ready is not None and self._t_ready[0] is batch and self._t_ready[1:] == (B, G)
         tin = None
         if self.pipeline and next_batch is not None and self.side is not None:
             tin = self.stage_teacher(next_batch)
@@ -1010,7 +1012,7 @@ class MultiCentralEngine:
             self._join(t_done)
             self.store.flush_nbt()
 
-        self._t_ready = (id(next_batch),) + tin[2:4] if tin is not None else None
+        self._t_ready = (next_batch,) + tin[2:4] if tin is not None else None
         if self.use_graph and self._graphable():
             self.graph.run(staged[2:5] + (ready, tin is not None), body)
         else:
