@@ -56,12 +56,15 @@ const char* avd_last_error(void);
  * per-call update for g = 0..G-1: rm = 0.9 rm + 0.1 mean_g, rv = 0.9 rv + 0.1 var_g*n/(n-1)
  * (nn.BatchNorm momentum 0.1; group order = the reference's call order, dino.py:680-704).
  * parts is consumed: the chunked first pass writes f64 chunk sums over it.
- * pivot [G,C] (nullable): the partials are sums of (x - pivot) and (x - pivot)^2 (shifted sums
- * from avd_colstats: no cancellation in the variance when |mean| >> std). */
+ * pivot (nullable): the partials are sums of (x - K) and (x - K)^2 with K = pivot[g * pivot_gs + c]
+ * (shifted sums: no cancellation in the variance when |mean| >> std).  pivot_gs = C for a
+ * per-(group, channel) pivot [G,C] (avd_colstats), 0 for one pivot per channel [C] -- which may
+ * be running_mean itself (avd_cl_conv_fwd_pv's pivot: read before the running update). */
 int avd_bn_finalize(float* parts, int G, int R, int C, long long count,
                     const float* gamma, const float* beta, float eps, float momentum,
                     float* mean, float* invstd, float* scale, float* shift,
-                    float* running_mean, float* running_var, const float* pivot, void* stream);
+                    float* running_mean, float* running_var, const float* pivot, int pivot_gs,
+                    void* stream);
 
 /* From the partials [C, G, R, 2] build the input-gradient coefficients
  * coef [G, C, 3] (dy = k1*dz + kx*y + k0) and write dgamma/dbeta/dbias [C] (sums over
@@ -116,6 +119,17 @@ int avd_cl_stat_rows(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt);
 int avd_cl_conv_fwd(const void* x, const void* wk, const float* bias, void* y, float* stats,
                     int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
                     void* stream);
+/* 1 if the statistics producer of this shape takes a pivot (the persistent weights-stationary
+ * mid layers, whose lane-local running sums span thousands of values per BN group). */
+int avd_cl_stat_pivot(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt);
+/* avd_cl_conv_fwd with statistics about a per-channel pivot [Cout] (nullable; only where
+ * avd_cl_stat_pivot, else AVD_ERR_ARG): the partials are sums of (y - pivot[c]) and
+ * (y - pivot[c])^2 -- finalize with avd_bn_finalize(..., pivot, pivot_gs = 0).  The engine
+ * passes the layer's BatchNorm running mean: near every batch's mean once it has tracked a few
+ * batches, so the variance keeps full precision when |mean| >> std. */
+int avd_cl_conv_fwd_pv(const void* x, const void* wk, const float* bias, const float* pivot,
+                       void* y, float* stats, int dt, int N, int B, int Cin, int H, int W, int Cout,
+                       int K, int pad, void* stream);
 
 /* dx [N,H,W,Cin] = input gradient of the conv for dy [N,Ho,Wo,Cout]; wk_d = dgrad layout. */
 int avd_cl_conv_dgrad(const void* dy, const void* wk_d, void* dx, int dt, int N, int Cin, int H,

@@ -21,7 +21,7 @@ D = ctypes.c_double
 # name -> argtypes (restype is always c_int except where noted)
 PROTOS = {
     "avd_version": [],
-    "avd_bn_finalize": [P, I, I, I, L, P, P, F, F, P, P, P, P, P, P, P, P],
+    "avd_bn_finalize": [P, I, I, I, L, P, P, F, F, P, P, P, P, P, P, P, I, P],
     "avd_bn_bwd_finalize": [P, I, I, I, L, P, P, P, P, P, P, P, I, P],
     "avd_gemm": [I, I, I, P, L, L, P, L, L, P, L, P, F, F, I, P, L, P],
     "avd_gemm_ws_elems": [I, I, I, I],
@@ -30,6 +30,8 @@ PROTOS = {
     "avd_cl_weight_layout_batch": [I, P, P, P, P, P, P, I, P],
     "avd_cl_stat_rows": [I, I, I, I, I, I, I],
     "avd_cl_conv_fwd": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "avd_cl_stat_pivot": [I, I, I, I, I, I, I],
+    "avd_cl_conv_fwd_pv": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "avd_cl_conv_dgrad": [P, P, P, I, I, I, I, I, I, I, I, P],
     "avd_cl_wgrad_chunks": [I, I, I, I],
     "avd_cl_conv_wgrad": [P, P, I, P, I, I, I, I, I, I, I, P],

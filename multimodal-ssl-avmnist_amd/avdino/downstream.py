@@ -35,6 +35,7 @@ import torch.nn as nn
 
 from . import ops
 from .probe import LinearProbe
+from .trainer import cosine_lr
 
 
 def _source(pretrained_model, is_dino_based=True):
@@ -258,8 +259,6 @@ def train_downstream(pretrained_model, trainloader, validloader, testloader, num
     test result)."""
     model = DownstreamClassifier(pretrained_model, is_dino_based=is_dino_based, lr=learning_rate,
                                  weight_decay=0.01, seed=seed, classifier_state=classifier_state)
-    sched = torch.optim.lr_scheduler.CosineAnnealingLR(
-        torch.optim.SGD([torch.zeros(1, requires_grad=True)], lr=learning_rate), T_max=num_epochs)
     stamp = datetime.now().strftime("%Y-%m-%d %H-%M-%S")
     if write_logs:
         for path in (save_path, train_log_path, test_log_path):
@@ -277,17 +276,23 @@ def train_downstream(pretrained_model, trainloader, validloader, testloader, num
     history = []
     for epoch in range(num_epochs):
         model.train()
-        model.lr = sched.get_last_lr()[0]
-        batches = list(trainloader)
-        losses = torch.empty(len(batches), device=device)
-        for i, batch in enumerate(batches):
+        # CosineAnnealingLR(T_max=num_epochs) stepped once per epoch, in closed form
+        model.lr = cosine_lr(learning_rate, epoch, num_epochs)
+        # the loader is streamed (one batch alive at a time); the per-batch losses stay in one
+        # device buffer, sized from len(loader) when it has one (no host sync inside the epoch)
+        n = len(trainloader) if hasattr(trainloader, "__len__") else 0
+        losses = torch.empty(max(n, 1), device=device)
+        i = 0
+        for batch in trainloader:
+            if i >= losses.numel():
+                losses = torch.cat([losses, torch.empty(losses.numel(), device=device)])
             images, audios, lab = _as_batch(batch, device)
             model.train_step(images, audios, lab, losses[i:i + 1])
-        sched.step()
-        train_loss = losses.mean().item()
+            i += 1
+        train_loss = losses[:i].mean().item()
         val_loss, val_acc, *_ = _evaluate(model, validloader, device)
         history.append({"epoch": epoch + 1, "train_loss": train_loss, "val_loss": val_loss,
-                        "val_accuracy": val_acc, "train_losses": losses.cpu().numpy()})
+                        "val_accuracy": val_acc, "train_losses": losses[:i].cpu().numpy()})
         if write_logs:
             with open(train_log_path, "a", newline="") as f:
                 csv.writer(f).writerow([epoch + 1, train_loss, val_loss, val_acc])

@@ -24,14 +24,15 @@ import os
 import torch
 
 from . import contrastive, ops
-from .spec import (CENTRAL_AUDIO_CONVS, CENTRAL_IMAGE_CONVS, CNN3_AUDIO_CONVS, CNN3_IMAGE_CONVS,
-                   HEAD_NAMES, PROJ_HIDDEN, UNI_ALIASES, UNI_ENCODERS, central_stack, cnn3_stack)
+from .spec import HEAD_NAMES, MULTI_ENCODERS, PROJ_HIDDEN, UNI_ALIASES, UNI_ENCODERS
 
 F32 = torch.float32
 
 
 class Workspace:
-    """Named device scratch buffers, grown on demand and reused across steps."""
+    """Named device scratch buffers, grown on demand and reused across steps.  Every
+    (re)allocation bumps ops' allocation epoch, so graphs captured over the old buffers are
+    retired (GraphedStep)."""
 
     def __init__(self, device):
         self.device = device
@@ -42,6 +43,7 @@ class Workspace:
         if b is None or b.numel() < numel or b.dtype != dtype:
             b = torch.empty(max(numel, 1), dtype=dtype, device=self.device)
             self.bufs[name] = b
+            ops.bump_alloc_epoch()
         return b[:numel]
 
     def nbytes(self):
@@ -92,13 +94,25 @@ class ConvBranch:
             ops.cl_weight_layout_batch(batch)
         return wts
 
-    def _conv_fwd(self, i, h, wt, bias, y, parts, N, B):
+    def _conv_fwd(self, i, h, wt, bias, y, parts, N, B, pivot=None):
         ci, co, k, pad = self.stack.convs[i]
         H = self.dims[i][0]
         if wt[2] is not None:
             ops.fp8_conv_fwd(h, 1.0, wt[2][0], wt[2][1], bias, y, parts, N, B, ci, H, H, co, k, pad)
         else:
-            ops.cl_conv_fwd(h, wt[0], bias, y, parts, N, B, ci, H, H, co, k, pad)
+            ops.cl_conv_fwd(h, wt[0], bias, y, parts, N, B, ci, H, H, co, k, pad, pivot=pivot)
+
+    # A/B switch for the statistics pivot (AVDINO_NO_PIVOT=1: raw sums, as before round 3)
+    NO_PIVOT = os.environ.get("AVDINO_NO_PIVOT", "0") == "1"
+
+    def _stat_pivot(self, store, i, B):
+        """The BN running mean as the statistics pivot where the producer takes one (the
+        persistent mid layers: avd_cl_stat_pivot) -- None elsewhere."""
+        ci, co, k, _p = self.stack.convs[i]
+        Ho = self.dims[i][1]
+        if self.NO_PIVOT or self._fp8_ok(i) or not ops.cl_stat_pivot(Ho, Ho, B, k, ci, co, self.act):
+            return None
+        return store[self.stack.bn_keys[i] + ".running_mean"]
 
     def _stat_rows(self, i, B):
         ci, co, k, _p = self.stack.convs[i]
@@ -125,13 +139,15 @@ class ConvBranch:
             R = self._stat_rows(i, B)
             y = ws.get(f"{tag}.y{i}", N * Ho * Ho * co, self.act)
             parts = ws.get("stat_parts", co * G * R * 2)
-            self._conv_fwd(i, h, wts[i], store[self.stack.conv_keys[i] + ".bias"], y, parts, N, B)
+            pv = self._stat_pivot(store, i, B)
+            self._conv_fwd(i, h, wts[i], store[self.stack.conv_keys[i] + ".bias"], y, parts, N, B, pv)
             st = ws.get(f"{tag}.bn{i}", 4 * G * co).view(4, G * co)
             bk = self.stack.bn_keys[i]
             ops.bn_finalize(parts, G, R, co, B * Ho * Ho, store[bk + ".weight"], store[bk + ".bias"],
                             st[0], st[1], st[2], st[3],
                             store[bk + ".running_mean"] if update_running else None,
-                            store[bk + ".running_var"] if update_running else None)
+                            store[bk + ".running_var"] if update_running else None,
+                            pivot=pv, pivot_gs=0)
             if update_running:
                 store.bump_nbt(bk + ".num_batches_tracked", G)
             ctx["y"].append(y)
@@ -524,18 +540,28 @@ class GraphedStep:
     """A training step's device work captured once per input shape as a hipGraph
     (torch.cuda.CUDAGraph over HIP stream capture, side streams joined by events) and replayed:
     one host call per step instead of ~230 launches.  The first ``warmup`` calls per shape run
-    eagerly (they size every workspace), the next one captures."""
+    eagerly (they size every workspace), the next one captures.
+
+    A graph holds the device pointers of the scratch buffers it was captured over; when any of
+    them is reallocated later (a larger key's eager warm-up grows a shared buffer, e.g. SimCLR's
+    image/image mode captured before its audio/audio mode was first seen) the graph is stale:
+    each graph records the allocation epoch after its capture and is dropped and re-captured
+    instead of replayed once the epoch has moved."""
 
     def __init__(self, warmup=2):
         self.warmup = warmup
-        self.graphs = {}
+        self.graphs = {}     # key -> (graph, allocation epoch after its capture)
         self.seen = {}
+        self.captures = 0
 
     def run(self, key, body):
-        g = self.graphs.get(key)
-        if g is not None:
-            g.replay()
-            return
+        ent = self.graphs.get(key)
+        if ent is not None:
+            if ent[1] == ops.alloc_epoch():
+                ent[0].replay()
+                return
+            del self.graphs[key]            # captured over buffers that have since moved
+            self.seen[key] = self.warmup - 1
         n = self.seen.get(key, 0)
         if n < self.warmup:
             self.seen[key] = n + 1
@@ -545,7 +571,8 @@ class GraphedStep:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="relaxed"):
             body()
-        self.graphs[key] = g
+        self.graphs[key] = (g, ops.alloc_epoch())
+        self.captures += 1
         g.replay()          # the capture itself executed nothing
 
 
@@ -565,11 +592,15 @@ def ema_step(store, m):
 # ============================================================================ multimodal DINO
 class MultiCentralEngine:
     """Training step of MultiModalDINO{,WithMSE,WithINFONCE,SemiSupervised} over
-    CentralMultiModalEncoder (``--model multi_central --training_mode {default,mse,infonce,
-    semi_supervised}``)."""
+    CentralMultiModalEncoder (``--model multi_central``, dino.py:454-468) or
+    SimpleMultiModalEncoder (``--model multi_simple``, dino.py:214-234: the 3x3 image_encoder /
+    audio_encoder with global average pooling), ``--training_mode {default,mse,infonce,
+    semi_supervised}``.  Both encoders are the same dataflow -- two conv branches, each a
+    Linear to E, cat, fusion -- so only the stacks and the Linear keys differ."""
 
     def __init__(self, store, mode, E, D, P, hp, act_dtype=F32, grad_hook=None, seed=0,
-                 buffer_hook=None, negatives="global", group=None, concurrent=True, conv_fp8=False):
+                 buffer_hook=None, negatives="global", group=None, concurrent=True, conv_fp8=False,
+                 encoder="multi_central"):
         self.store, self.mode, self.E, self.D, self.P, self.hp = store, mode, E, D, P, hp
         self.act = act_dtype
         # Linear layers: bf16 MFMA in the bf16 mode (like the reference's fp16 autocast),
@@ -578,10 +609,12 @@ class MultiCentralEngine:
         self.ws = Workspace(store.device)
         # conv_fp8: e4m3 MFMA forward for the mid-layer convs (bf16 mode only; config 5)
         self.conv_fp8 = bool(conv_fp8) and act_dtype == torch.bfloat16
-        self.img = ConvBranch(central_stack("student.image_encoder.0", CENTRAL_IMAGE_CONVS, 28), act_dtype, conv_fp8)
-        self.aud = ConvBranch(central_stack("student.audio_encoder.0", CENTRAL_AUDIO_CONVS, 112), act_dtype, conv_fp8)
-        self.t_img = ConvBranch(central_stack("teacher.image_encoder.0", CENTRAL_IMAGE_CONVS, 28), act_dtype, conv_fp8)
-        self.t_aud = ConvBranch(central_stack("teacher.audio_encoder.0", CENTRAL_AUDIO_CONVS, 112), act_dtype, conv_fp8)
+        self.encoder = encoder
+        istack, self.img_lin, astack, self.aud_lin, _sd = MULTI_ENCODERS[encoder]
+        self.img = ConvBranch(istack("student"), act_dtype, conv_fp8)
+        self.aud = ConvBranch(astack("student"), act_dtype, conv_fp8)
+        self.t_img = ConvBranch(istack("teacher"), act_dtype, conv_fp8)
+        self.t_aud = ConvBranch(astack("teacher"), act_dtype, conv_fp8)
         self.sproj = ProjHead("student_projection", D, P, gemm_mode=self.gm)
         self.tproj = ProjHead("teacher_projection", D, P, gemm_mode=self.gm)
         self.heads = None
@@ -665,8 +698,8 @@ class MultiCentralEngine:
         def image():
             iws = self.iws if side_image else ws
             fi, ci = ib.forward(iws, st, tag + ".img", x_img, N, G, update_running, need_dgrad)
-            ops.linear_fwd(fi, st[prefix + ".image_encoder.1.weight"],
-                           st[prefix + ".image_encoder.1.bias"], cat, N, out_ld=2 * E, out_off=0,
+            lin = f"{prefix}.{self.img_lin}"
+            ops.linear_fwd(fi, st[lin + ".weight"], st[lin + ".bias"], cat, N, out_ld=2 * E, out_off=0,
                            mode=self.gm)
             return fi, ci
 
@@ -678,8 +711,8 @@ class MultiCentralEngine:
         else:
             (fi, ci), i_done = image(), None
         fa, ca = ab.forward(ws, st, tag + ".aud", x_aud, N, G, update_running, need_dgrad)
-        ops.linear_fwd(fa, st[prefix + ".audio_encoder.1.weight"], st[prefix + ".audio_encoder.1.bias"],
-                       cat, N, out_ld=2 * E, out_off=E, mode=self.gm)
+        lin = f"{prefix}.{self.aud_lin}"
+        ops.linear_fwd(fa, st[lin + ".weight"], st[lin + ".bias"], cat, N, out_ld=2 * E, out_off=E, mode=self.gm)
         self._join(i_done)
         return cat, (fi, ci, fa, ca)
 
@@ -964,17 +997,17 @@ class MultiCentralEngine:
         def image_branch():      # independent of the audio branch: side stream
             iws = self.iws
             dfi = iws.get("dfeat_img", N * fi.shape[1])
-            ops.linear_bwd(dcat, fi, st["student.image_encoder.1.weight"],
-                           st.grad_of("student.image_encoder.1.weight"),
-                           st.grad_of("student.image_encoder.1.bias"), dfi, N, dout_ld=2 * E,
+            lin = "student." + self.img_lin
+            ops.linear_bwd(dcat, fi, st[lin + ".weight"], st.grad_of(lin + ".weight"),
+                           st.grad_of(lin + ".bias"), dfi, N, dout_ld=2 * E,
                            mode=self.gm)
             self.img.backward(iws, st, cimg, dfi)
 
         _, i_done = self._on_side(image_branch)
         dfa = ws.get("dfeat_aud", N * fa.shape[1])
-        ops.linear_bwd(dcat, fa, st["student.audio_encoder.1.weight"],
-                       st.grad_of("student.audio_encoder.1.weight"),
-                       st.grad_of("student.audio_encoder.1.bias"), dfa, N, dout_ld=2 * E, dout_off=E,
+        lin = "student." + self.aud_lin
+        ops.linear_bwd(dcat, fa, st[lin + ".weight"], st.grad_of(lin + ".weight"),
+                       st.grad_of(lin + ".bias"), dfa, N, dout_ld=2 * E, dout_off=E,
                        mode=self.gm)
         self.aud.backward(ws, st, caud, dfa, wstream=self.wside)
         self._join(i_done)
@@ -995,8 +1028,14 @@ class MultiCentralEngine:
         staged = self.stage(batch, self.heads is not None)
         B, G = staged[2], staged[3]
         # the previous step ran this batch's teacher (the reference held in _t_ready keeps the
-        # object alive, so identity cannot be a recycled id)
-        ready = self._t_ready is not None and self._t_ready[0] is batch and self._t_ready[1:] == (B, G)
+        # object alive, so identity cannot be a recycled id).  Contract of the pipelined step:
+        # ``batch`` IS the previous call's ``next_batch``, not mutated since -- that teacher
+        # forward already updated the teacher's BN running statistics, so a different batch
+        # here cannot be served without drifting from the sequential run: refuse it.
+        if self._t_ready is not None and not (self._t_ready[0] is batch and self._t_ready[1:] == (B, G)):
+            raise ValueError("pipelined step: batch must be the previous step's next_batch (its "
+                             "teacher forward already ran); set pipeline=False to change batches")
+        ready = self._t_ready is not None
         tin = None
         if self.pipeline and next_batch is not None and self.side is not None:
             tin = self.stage_teacher(next_batch)
@@ -1107,6 +1146,10 @@ class UniModalEngine:
         DINO loss only."""
         if step_order not in ("lightning", "pretrain"):
             raise ValueError(step_order)
+        if step_order == "pretrain" and float(cos_alpha) > 0:
+            # pretrain_dino (dino_train.py:137-166) optimises the unimodal DINO loss alone
+            raise ValueError("step_order='pretrain' runs pretrain_dino's loss, which has no "
+                             "cosine-consistency term: cos_alpha must be 0")
         self.step_order = step_order
         self.store, self.D, self.P, self.hp = store, D, P, hp
         self.kind = UNI_ALIASES.get(kind, kind)

@@ -4,6 +4,7 @@ Class names, constructor arguments, forward() signatures/returns and state-dict 
 the reference (paths relative to its AVMNIST_Experiments/):
 
   CentralMultiModalEncoder          models/dino.py:454-468   (``--model multi_central``)
+  SimpleMultiModalEncoder           models/dino.py:214-234   (``--model multi_simple``)
   ProjectionHead                    models/dino.py:1240-1254
   MultiModalDINO                    models/dino.py:588-727
   MultiModalDINOWithMSE             models/dino.py:1156-1171
@@ -38,7 +39,7 @@ import torch.nn as nn
 from . import contrastive, ops
 from .engine import Hyper, MultiCentralEngine, SimCLREngine, UniModalEngine, Workspace, ema_step
 from .params import ParamStore
-from .spec import multimodal_dino_sd, simclr_sd, unimodal_dino_sd
+from .spec import MULTI_ENCODERS, multimodal_dino_sd, simclr_sd, unimodal_dino_sd
 
 try:  # a real drop-in under Lightning's Trainer where Lightning is installed
     from lightning.pytorch import LightningModule as _LightningBase
@@ -61,6 +62,14 @@ class BaseMultiModalEncoder:
         self.output_dim = output_dim
         self.encoder_output_dim = encoder_output_dim
         self.fusion_dropout = fusion_dropout
+
+
+class SimpleMultiModalEncoder(BaseMultiModalEncoder):
+    """image_encoder(E) (3x3 CNN 1->32->64->128, GAP, Linear(128,E)) and audio_encoder(E)
+    (1->32->64->128->256, GAP, Linear(256,E)), concat fusion Linear(2E,E)-ReLU-
+    Dropout(fusion_dropout)-Linear(E,D) (models/dino.py:18-73, 214-234)."""
+
+    arch = "multi_simple"
 
 
 class CentralMultiModalEncoder(BaseMultiModalEncoder):
@@ -109,7 +118,7 @@ class SpectrogramEncoderCentral(SpectrogramEncoder):
     kind = "spectrogram_central"
 
 
-MODEL_MAP = {"multi_central": CentralMultiModalEncoder}
+MODEL_MAP = {"multi_simple": SimpleMultiModalEncoder, "multi_central": CentralMultiModalEncoder}
 UNIMODAL_MODEL_MAP = {"image_simple": ImageEncoder, "spectrogram_simple": SpectrogramEncoder,
                       "spectrogram_central": SpectrogramEncoderCentral}
 
@@ -319,18 +328,18 @@ class MultiModalDINO(_ArenaModule):
         encoder_kwargs["output_dim"] = output_dim
         encoder_kwargs["encoder_output_dim"] = encoder_output_dim
         enc = encoder_class(**encoder_kwargs)
-        if getattr(enc, "arch", None) != "multi_central":
+        if getattr(enc, "arch", None) not in MULTI_ENCODERS:
             raise NotImplementedError(
-                f"{encoder_class.__name__}: only CentralMultiModalEncoder (multi_central) runs on the "
-                f"MI355X engine in this release (BASELINE hot path)")
+                f"{encoder_class.__name__}: the MI355X engine runs {sorted(MULTI_ENCODERS)} "
+                f"(SimpleMultiModalEncoder / CentralMultiModalEncoder)")
         self.student_spec = enc
         self.projection_dim, self.output_dim = projection_dim, output_dim
         self.encoder_output_dim = encoder_output_dim
         self.momentum, self.center_momentum, self.dropout = momentum, center_momentum, dropout
         self.device = _device(device)
         self.precision = precision
-        store = ParamStore(multimodal_dino_sd(self.mode, encoder_output_dim, output_dim, projection_dim),
-                           self.device, seed=seed)
+        store = ParamStore(multimodal_dino_sd(self.mode, encoder_output_dim, output_dim, projection_dim,
+                                              encoder=enc.arch), self.device, seed=seed)
         self._bind(store, [("arena", 0, store.n_live)])
         self.hp = Hyper(momentum=momentum, center_momentum=center_momentum, dropout=dropout,
                         fusion_dropout=enc.fusion_dropout)
@@ -338,7 +347,7 @@ class MultiModalDINO(_ArenaModule):
         if self.device.type == "cuda":
             self.engine = MultiCentralEngine(store, self.mode, encoder_output_dim, output_dim,
                                              projection_dim, self.hp, act_dtype=_DT[precision], seed=seed,
-                                             negatives=negatives, group=group)
+                                             negatives=negatives, group=group, encoder=enc.arch)
         self.student = _StudentView(self, enc.arch, output_dim, encoder_output_dim)
 
     def arena_ranges(self):

@@ -86,6 +86,20 @@ def _timed(key, nbytes, flops, fn):
     return TIMER.wrap(key, nbytes, flops, fn)
 
 
+# Scratch allocation epoch: bumped whenever a workspace / scratch buffer is (re)allocated.  A
+# captured hipGraph bakes in the device pointers it saw, so a graph captured in an earlier epoch
+# may address freed memory and must not be replayed (engine.GraphedStep checks this).
+_ALLOC_EPOCH = [0]
+
+
+def bump_alloc_epoch():
+    _ALLOC_EPOCH[0] += 1
+
+
+def alloc_epoch():
+    return _ALLOC_EPOCH[0]
+
+
 def _need(cond, msg):
     if not cond:
         raise ValueError(msg)
@@ -93,9 +107,13 @@ def _need(cond, msg):
 
 # ---------------------------------------------------------------- BatchNorm statistics
 def bn_finalize(parts, G, R, C, count, gamma, beta, mean, invstd, scale, shift, rm=None, rv=None,
-                eps=1e-5, momentum=0.1, pivot=None):
+                eps=1e-5, momentum=0.1, pivot=None, pivot_gs=None):
+    """pivot [G, C] (pivot_gs = C, avd_colstats) or [C] (pivot_gs = 0, avd_cl_conv_fwd_pv)."""
+    if pivot is not None:
+        pivot_gs = C if pivot_gs is None else pivot_gs
+        _need(pivot.numel() >= (G - 1) * pivot_gs + C, "bn_finalize pivot size")
     call("avd_bn_finalize", p(parts), G, R, C, count, p(gamma), p(beta), eps, momentum, p(mean),
-         p(invstd), p(scale), p(shift), p(rm), p(rv), p(pivot), stream())
+         p(invstd), p(scale), p(shift), p(rm), p(rv), p(pivot), int(pivot_gs or 0), stream())
 
 
 def bn_bwd_finalize(parts, G, R, C, count, gamma, mean, invstd, coef, dgamma, dbeta, dbias,
@@ -139,6 +157,7 @@ def _gemm_workspace(device, n):
     if t is None or t.numel() < n:
         t = torch.empty(max(n, 1 << 20), device=device, dtype=torch.float32)
         _GEMM_WS[key] = t
+        bump_alloc_epoch()
     return t
 
 
@@ -243,8 +262,13 @@ def fp8_conv_fwd(x, xscale, wq, wscale, bias, y, stats, N, B, Cin, H, W, Cout, K
                         p(stats), N, B, Cin, H, W, Cout, K, pad, stream()))
 
 
-def cl_conv_fwd(x, wk, bias, y, stats, N, B, Cin, H, W, Cout, K, pad):
-    """NHWC conv (+bias) with fused BN partial sums: stats [Cout][N/B][R][2]."""
+def cl_stat_pivot(Ho, Wo, B, K, Cin, Cout, dtype):
+    return bool(lib.avd_cl_stat_pivot(Ho, Wo, B, K, Cin, Cout, _DT[dtype]))
+
+
+def cl_conv_fwd(x, wk, bias, y, stats, N, B, Cin, H, W, Cout, K, pad, pivot=None):
+    """NHWC conv (+bias) with fused BN partial sums: stats [Cout][N/B][R][2]; with ``pivot``
+    [Cout] (where cl_stat_pivot) sums about it (avd_cl_conv_fwd_pv)."""
     Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
     _need(x.numel() == N * H * W * Cin and y.numel() == N * Ho * Wo * Cout, "cl conv sizes")
     _need(x.dtype == y.dtype == wk.dtype, "cl conv dtypes")
@@ -252,11 +276,14 @@ def cl_conv_fwd(x, wk, bias, y, stats, N, B, Cin, H, W, Cout, K, pad):
     if stats is not None:
         R = cl_stat_rows(Ho, Wo, B, K, Cin, Cout, x.dtype)
         _need(R > 0 and stats.numel() >= Cout * (N // B) * R * 2, "cl conv stats size")
+    if pivot is not None:
+        _need(stats is not None and pivot.numel() >= Cout and pivot.dtype == torch.float32 and
+              cl_stat_pivot(Ho, Wo, B, K, Cin, Cout, x.dtype), "cl conv pivot")
     nb = x.numel() * x.element_size() + y.numel() * y.element_size()
     fl = 2 * N * Cout * Ho * Wo * Cin * K * K
     _timed(f"cl_conv_fwd[{N}x{H}x{W}x{Cin}->{Cout} k{K}p{pad} {x.dtype}]", nb, fl,
-           lambda: call("avd_cl_conv_fwd", p(x), p(wk), p(bias), p(y), p(stats), dtcode(x), N, B,
-                        Cin, H, W, Cout, K, pad, stream()))
+           lambda: call("avd_cl_conv_fwd_pv", p(x), p(wk), p(bias), p(pivot), p(y), p(stats), dtcode(x),
+                        N, B, Cin, H, W, Cout, K, pad, stream()))
 
 
 def cl_conv_dgrad(dy, wk_d, dx, N, Cin, H, W, Cout, K, pad):
@@ -501,6 +528,7 @@ def sum_rows(x, rows, cols, out, accumulate=0, ld=None, off=0):
     w = _SUM_WS.get(key)
     if w is None or w.numel() < n:
         w = _SUM_WS[key] = torch.empty(max(n, 1 << 16), device=x.device, dtype=torch.float32)
+        bump_alloc_epoch()
     call("avd_sum_rows_split", x.data_ptr() + 4 * off, rows, cols, ld, p(out), accumulate, p(w),
          w.numel(), stream())
 

@@ -22,7 +22,7 @@ import torch
 from . import ops
 from .engine import F32, ConvBranch, UniEncoder, Workspace
 from .params import ParamStore
-from .spec import CENTRAL_AUDIO_CONVS, CENTRAL_IMAGE_CONVS, UNI_ALIASES, UNI_ENCODERS, central_stack
+from .spec import MULTI_ENCODERS, UNI_ALIASES, UNI_ENCODERS
 
 from collections import OrderedDict
 
@@ -36,14 +36,17 @@ def classifier_sd(D, hidden=128, num_classes=10):
     return sd
 
 
-class _CentralEncoder:
-    """The multimodal student (CentralMultiModalEncoder.forward, dino.py:229-234, 454-468)
-    without gradients: both LeNet branches, their Linears into the cat buffer, fusion."""
+class _MultiEncoder:
+    """The multimodal student (SimpleMultiModalEncoder.forward, dino.py:229-234; the
+    CentralMultiModalEncoder of 454-468 or the 3x3 encoders of 214-227) without gradients:
+    both conv branches, their Linears into the cat buffer, fusion."""
 
-    def __init__(self, E, D, act, gm, fusion_dropout):
+    def __init__(self, arch, E, D, act, gm, fusion_dropout):
         self.E, self.D, self.gm, self.p = E, D, gm, fusion_dropout
-        self.img = ConvBranch(central_stack("student.image_encoder.0", CENTRAL_IMAGE_CONVS, 28), act)
-        self.aud = ConvBranch(central_stack("student.audio_encoder.0", CENTRAL_AUDIO_CONVS, 112), act)
+        istack, ilin, astack, alin, _sd = MULTI_ENCODERS[arch]
+        self.img = ConvBranch(istack("student"), act)
+        self.aud = ConvBranch(astack("student"), act)
+        self.ilin, self.alin = "student." + ilin, "student." + alin
 
     def __call__(self, ws, st, x_img, x_aud, N, train, seed):
         E = self.E
@@ -55,9 +58,9 @@ class _CentralEncoder:
             fi = self.img.forward_eval(ws, st, "pi", x_img, N)
             fa = self.aud.forward_eval(ws, st, "pa", x_aud, N)
         cat = ws.get("p.cat", N * 2 * E)
-        ops.linear_fwd(fi, st["student.image_encoder.1.weight"], st["student.image_encoder.1.bias"],
+        ops.linear_fwd(fi, st[self.ilin + ".weight"], st[self.ilin + ".bias"],
                        cat, N, out_ld=2 * E, out_off=0, mode=self.gm)
-        ops.linear_fwd(fa, st["student.audio_encoder.1.weight"], st["student.audio_encoder.1.bias"],
+        ops.linear_fwd(fa, st[self.alin + ".weight"], st[self.alin + ".bias"],
                        cat, N, out_ld=2 * E, out_off=E, mode=self.gm)
         h = ws.get("p.fh", N * E)
         ops.linear_fwd(cat, st["student.fusion.0.weight"], st["student.fusion.0.bias"], h, N,
@@ -86,7 +89,8 @@ class LinearProbe:
     """One probe epoch over a trained DINO model's student.
 
     source: the trained model's ParamStore (MultiModalDINO*.store / UniModalDINO.store);
-    kind: "multi_central" or an UNIMODAL_MODEL_MAP key; E/D: encoder_output_dim / output_dim.
+    kind: a MODEL_MAP key ("multi_central", "multi_simple") or an UNIMODAL_MODEL_MAP key;
+    E/D: encoder_output_dim / output_dim.
     """
 
     def __init__(self, source, kind, D, E=None, lr=1e-4, weight_decay=0.01, act_dtype=F32,
@@ -102,8 +106,9 @@ class LinearProbe:
         self.gm = ops.GEMM_BF16_MFMA if act_dtype == torch.bfloat16 else ops.GEMM_F32_MFMA
         self.act = act_dtype
         self.ws = Workspace(dev)
-        if self.kind == "multi_central":
-            self.enc = _CentralEncoder(E, D, act_dtype, self.gm, fusion_dropout)
+        self.multimodal = self.kind in MULTI_ENCODERS
+        if self.multimodal:
+            self.enc = _MultiEncoder(self.kind, E, D, act_dtype, self.gm, fusion_dropout)
         else:
             self.enc = _UniEncoder(self.kind, act_dtype, self.gm)
             self.modality = UNI_ENCODERS[self.kind][0]
@@ -116,7 +121,7 @@ class LinearProbe:
 
     def _features(self, images, audios, train):
         ws, N = self.ws, images.shape[0]
-        if self.kind == "multi_central":
+        if self.multimodal:
             xi = ws.get("p.in.img", N * 784, self.act)
             xa = ws.get("p.in.aud", N * 12544, self.act)
             ops.stage_views(images.contiguous(), 1, None, 0, None, N, 784, xi)

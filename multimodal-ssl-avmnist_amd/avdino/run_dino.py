@@ -22,6 +22,7 @@ or no files) batches are synthetic AVMNIST-shaped device tensors (pixel values r
 --hyperparameter_tune / --hyperparameter_tune_augments (Optuna) are out of scope.
 """
 import argparse
+import math
 import json
 import os
 
@@ -42,8 +43,10 @@ def parse_args(argv=None):
     p.add_argument("--hyperparameter_tune", action="store_true")
     p.add_argument("--hyperparameter_tune_augments", action="store_true")
     p.add_argument("--epochs", type=int, default=None, help="override num_epochs")
-    p.add_argument("--steps-per-epoch", type=int, default=20,
-                   help="batches per epoch (synthetic data; caps the real loader too)")
+    p.add_argument("--steps-per-epoch", type=int, default=None,
+                   help="batches per epoch: synthetic data default 20; with real data the "
+                        "loader's full epoch (the reference's Trainer has no batch limit) unless "
+                        "given, then it caps the epoch like limit_train_batches")
     p.add_argument("--batch-size", type=int, default=None, help="override batch_size")
     p.add_argument("--probe-batches", type=int, default=4,
                    help="labelled batches for the epoch-end probe (synthetic data)")
@@ -163,12 +166,112 @@ class _EpochPrinter:
         print(json.dumps(rec), flush=True)
 
 
+def _stack_macs(stack):
+    """Multiply-adds of one sample through a conv stack (Conv2d: Ho*Wo*Cout*Cin*K*K)."""
+    macs = 0
+    for (ci, co, k, _p), (_h, ho, _hp) in zip(stack.convs, stack.layer_dims()):
+        macs += ho * ho * co * ci * k * k
+    return macs
+
+
+def model_stats(model, G, L):
+    """(GFLOPs per sample, parameter count) for run_dino's performance summary
+    (calculate_gflops, run_dino.py:243-283: torchinfo's total_mult_adds of the eval-mode forward
+    over one batch / batch size, and total_params).  Analytic here (no torchinfo): Conv2d and
+    Linear multiply-adds of the student over the G+L views, the teacher over the G global views,
+    their projection heads and, for the modes with heads, the originals through the student
+    branches and both heads; parameters = every parameter tensor of the state dict (student,
+    teacher, heads, incl. the CentralNet fc1/fc2 the reference builds but never runs)."""
+    from .spec import MULTI_ENCODERS, UNI_ENCODERS
+    m = model.model
+    spec = m.store.spec
+    params = sum(int(math.prod(shp)) for k, (shp, kind) in spec.items()
+                 if kind in ("w", "b", "bn_w", "bn_b"))
+
+    def lin(key):
+        shp = spec[key + ".weight"][0]
+        return shp[0] * shp[1]
+
+    def head(prefix):
+        return lin(prefix + ".mlp.0") + lin(prefix + ".mlp.4")
+
+    arch = getattr(m.student_spec, "arch", None)
+    if arch in MULTI_ENCODERS:
+        ist, il, ast_, al, _ = MULTI_ENCODERS[arch]
+        branch_i = _stack_macs(ist("student")) + lin("student." + il)
+        branch_a = _stack_macs(ast_("student")) + lin("student." + al)
+        enc = branch_i + branch_a + lin("student.fusion.0") + lin("student.fusion.3")
+        macs = (G + L) * (enc + head("student_projection")) + G * (enc + head("teacher_projection"))
+        heads = [k[:-len(".mlp.0.weight")] for k in spec if k.endswith(".mlp.0.weight")
+                 and not k.startswith(("student_projection", "teacher_projection"))]
+        if heads:
+            macs += branch_i + branch_a + sum(head(h) for h in heads)
+    else:
+        kind = m.student_spec.kind
+        _mod, stack, lins, _sd = UNI_ENCODERS[kind]
+        enc = _stack_macs(stack("student")) + sum(lin(f"student.{k}") for k in lins)
+        macs = (G + L) * (enc + head("student_projection")) + G * (enc + head("teacher_projection"))
+    return macs / 1e9, params
+
+
+def write_run_summary(model, args, config, out, G, L, stats_cb, trainer, training_time,
+                      knn=None, mlp=None):
+    """run_dino.py:409-464: ``final_results_{model}.csv`` (one row, the reference's columns) and
+    ``performance_summary.txt`` (key: value lines + the augmentation summary)."""
+    import csv
+    from datetime import datetime
+    h = config["hyperparameters"]
+    gflops, params = model_stats(model, G, L)
+    name = config.get("model", {}).get("name") or (args.model or args.unimodal_model)
+    cm = trainer.callback_metrics
+    epoch_time, avg_batch = cm.get("epoch_time"), cm.get("avg_batch_time")
+    results = {
+        "model": name, "best_train_loss": cm.get("train_loss"), "best_mlp_acc": cm.get("mlp_acc"),
+        "learning_rate": h["learning_rate"], "batch_size": args.batch_size or h["batch_size"],
+        "momentum": h["momentum"], "center_momentum": h["center_momentum"],
+        "projection_dim": h["projection_dim"], "output_dim": h["output_dim"],
+        "data_augmentation": h.get("data_augmentation", "burst_noise"),
+        "n_global_views": G, "n_local_views": L, "gflops": gflops, "params": params,
+        "params_millions": params / 1e6, "total_training_time": training_time,
+        "avg_epoch_time": epoch_time, "avg_batch_time": avg_batch,
+        "timestamp": datetime.now().strftime("%Y-%m-%d %H:%M:%S")}
+    with open(os.path.join(out, f"final_results_{name}.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(results))
+        w.writeheader()
+        w.writerow(results)
+    metric = args.metric
+    perf = {
+        "model_name": name, "parameters": f"{params / 1e6:.2f}M", "gflops": f"{gflops:.2f}",
+        "n_global_views": G, "n_local_views": L,
+        "training_time_hours": f"{training_time / 3600:.2f}",
+        "avg_epoch_time_minutes": f"{epoch_time / 60:.2f}" if epoch_time else "N/A",
+        "best_train_loss": f"{float(cm.get('train_loss', 0) or 0):.4f}",
+        f"best_{metric}": f"{float(cm.get(metric, 0) or 0):.4f}",
+        "downstream_mlp_acc": f"{mlp:.4f}" if mlp is not None else "N/A",
+        "downstream_knn_accuracy": f"{knn:.4f}" if knn is not None else "N/A",
+        # one seed here (the reference averages 3 seeds): std over one run
+        "downstream_mlp_acc_std": f"{0.0:.4f}" if mlp is not None else "N/A",
+        "downstream_knn_accuracy_std": f"{0.0:.4f}" if knn is not None else "N/A",
+        # gate_image / gate_audio exist only on the gated encoders (not on the MI355X path)
+        "final_audio_gate": "N/A", "final_image_gate": "N/A",
+    }
+    with open(os.path.join(out, "performance_summary.txt"), "w") as f:
+        for k, v in perf.items():
+            f.write(f"{k}: {v}\n")
+        aug = getattr(model, "augment_summary", None)
+        if aug:
+            f.write("\n# Augmentation Summary\n" + str(aug) + "\n")
+    return results, perf
+
+
 def main(argv=None):
     import tempfile
 
     import torch
 
-    from .trainer import ModelCheckpoint, Trainer
+    import time
+
+    from .trainer import CSVLogger, ModelCheckpoint, ModelStatsCallback, Trainer
     args = parse_args(argv)
     config = load_config(args.config)
     h = config["hyperparameters"]
@@ -198,7 +301,7 @@ def main(argv=None):
         validdata = AVMNISTLabelledLoader(split="val", **lab)
         testdata = AVMNISTLabelledLoader(split="test", **lab)
     else:
-        loader = SyntheticDinoLoader(B, G, L, args.steps_per_epoch, dev, seed, mode)
+        loader = SyntheticDinoLoader(B, G, L, args.steps_per_epoch or 20, dev, seed, mode)
         traindata = synthetic_labelled(B, args.probe_batches, dev, seed + 1)
         validdata = testdata = traindata[:1]
     if args.probe_batches or real:
@@ -206,10 +309,17 @@ def main(argv=None):
     out = args.out or tempfile.mkdtemp(prefix="avdino_run_")
     ckpt = ModelCheckpoint(dirpath=out, monitor=args.metric, save_top_k=1,
                            mode="max" if args.metric == "mlp_acc" else "min")
+    stats_cb = ModelStatsCallback()
+    # run_dino.py:355-365: CSVLogger per seed, log_every_n_steps=10, [checkpoint, stats]
+    logger = CSVLogger(out, name=f"logs_seed{config['experiment']['seed']}") if rank == 0 else None
     trainer = Trainer(max_epochs=epochs, strategy="ddp" if ddp else "auto", precision="16-mixed",
-                      callbacks=[ckpt, _EpochPrinter()],
+                      callbacks=[ckpt, stats_cb, _EpochPrinter()], log_every_n_steps=10,
+                      logger=logger, deterministic=True,
                       limit_train_batches=args.steps_per_epoch if real else None)
+    t0 = time.time()
     trainer.fit(model, loader)
+    training_time = time.time() - t0
+    knn = mlp = None
     if args.downstream and trainer.is_global_zero and ckpt.best_model_path:
         from .downstream import compute_accuracies
         best = type(model).load_from_checkpoint(ckpt.best_model_path, device=dev,
@@ -217,7 +327,10 @@ def main(argv=None):
         knn, mlp, _ = compute_accuracies(best.model, traindata, validdata, testdata, out, "model",
                                          num_epochs=2 if not real else 10)
         print(json.dumps({"knn_acc": knn, "mlp_acc": mlp}), flush=True)
+    if trainer.is_global_zero:
+        write_run_summary(model, args, config, out, G, L, stats_cb, trainer, training_time, knn, mlp)
     model.trainer_ = trainer
+    model.out_dir_ = out
     return model
 
 

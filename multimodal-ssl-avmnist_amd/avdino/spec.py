@@ -5,6 +5,7 @@ checkpoints interoperate:
   CentralUnimodalImage/Audio      reference models/unimodal.py:105-221
   image_encoder / audio_encoder   models/dino.py:18-73
   CentralMultiModalEncoder        models/dino.py:454-468 (fusion: 214-234)
+  SimpleMultiModalEncoder         models/dino.py:214-234 (image_encoder / audio_encoder, 18-73)
   ProjectionHead                  models/dino.py:1240-1254
   MultiModalDINO*                 models/dino.py:588-632, 964-970, 1053-1058, 1156-1161
   UniModalDINO / ImageEncoder     models/dino.py:1257-1297, 483-499
@@ -98,6 +99,27 @@ def central_multimodal_sd(sd, prefix, E, D):
     _dense(sd, f"{prefix}.fusion.3", D, E)
 
 
+def simple_multimodal_sd(sd, prefix, E, D):
+    """SimpleMultiModalEncoder (``--model multi_simple``): image_encoder(E), audio_encoder(E)
+    (nn.Sequential 3x3 CNNs, Linear at index 14 / 18), fusion."""
+    _cnn3(sd, f"{prefix}.image_encoder", CNN3_IMAGE_CONVS, E)
+    _cnn3(sd, f"{prefix}.audio_encoder", CNN3_AUDIO_CONVS, E)
+    _dense(sd, f"{prefix}.fusion.0", E, 2 * E)
+    _dense(sd, f"{prefix}.fusion.3", D, E)
+
+
+# MODEL_MAP encoders that run on the engine (run_dino.py:530-540):
+#   arch -> (image stack(prefix), image Linear key, audio stack(prefix), audio Linear key, sd builder)
+MULTI_ENCODERS = {
+    "multi_central": (lambda p: central_stack(f"{p}.image_encoder.0", CENTRAL_IMAGE_CONVS, 28), "image_encoder.1",
+                      lambda p: central_stack(f"{p}.audio_encoder.0", CENTRAL_AUDIO_CONVS, 112), "audio_encoder.1",
+                      central_multimodal_sd),
+    "multi_simple": (lambda p: cnn3_stack(f"{p}.image_encoder", CNN3_IMAGE_CONVS, 28), "image_encoder.14",
+                     lambda p: cnn3_stack(f"{p}.audio_encoder", CNN3_AUDIO_CONVS, 112), "audio_encoder.18",
+                     simple_multimodal_sd),
+}
+
+
 def projection_head_sd(sd, prefix, in_dim, out_dim, hidden=PROJ_HIDDEN):
     _dense(sd, f"{prefix}.mlp.0", hidden, in_dim)
     _bn(sd, f"{prefix}.mlp.1", hidden)
@@ -109,11 +131,12 @@ HEAD_NAMES = {"mse": ("image_projection_head", "audio_projection_head"),
               "semi_supervised": ("image_classifier", "audio_classifier")}
 
 
-def multimodal_dino_sd(mode, E, D, P, num_classes=10):
+def multimodal_dino_sd(mode, E, D, P, num_classes=10, encoder="multi_central"):
+    build = MULTI_ENCODERS[encoder][4]
     sd = OrderedDict()
     sd["center"] = ((1, P), "center")
-    central_multimodal_sd(sd, "student", E, D)
-    central_multimodal_sd(sd, "teacher", E, D)
+    build(sd, "student", E, D)
+    build(sd, "teacher", E, D)
     projection_head_sd(sd, "student_projection", D, P)
     projection_head_sd(sd, "teacher_projection", D, P)
     if mode in HEAD_NAMES:

@@ -23,7 +23,7 @@ ALL_MODELS = ["multi_simple", "multi_simple_gated", "multi_lstm", "multi_vit", "
               "multi_mobile_vit", "multi_resnet", "multi_cross_attention", "multi_central",
               "image_simple", "spectrogram_simple", "spectrogram_central", "spectrogram_lstm",
               "spectrogram_resnet", "spectrogram_vit", "spectrogram_mobile_vit"]
-MULTIMODAL = {"multi_central"}
+MULTIMODAL = {"multi_central", "multi_simple"}
 UNIMODAL = {"image_simple", "spectrogram_simple", "spectrogram_central"}
 
 

@@ -23,15 +23,162 @@ GPU box, which have no lightning.
 """
 import math
 import os
+import time
 
+import numpy as np
 import torch
 
 from . import dist as avdist
 
 
 class Callback:
+    """lightning.pytorch.Callback's hooks that the reference's training path uses."""
+
+    def on_train_start(self, trainer, module):
+        pass
+
+    def on_train_epoch_start(self, trainer, module):
+        pass
+
+    def on_train_batch_start(self, trainer, module, batch, batch_idx):
+        pass
+
+    def on_train_batch_end(self, trainer, module, outputs, batch, batch_idx):
+        pass
+
     def on_train_epoch_end(self, trainer, module):
         pass
+
+    def on_train_end(self, trainer, module):
+        pass
+
+
+class _Clock:
+    """Stream-ordered timestamps: HIP events on the device (no host sync per batch; read back at
+    the epoch end), host perf_counter on CPU."""
+
+    def __init__(self, device):
+        self.dev = torch.device(device) if device is not None else torch.device("cpu")
+        self.gpu = self.dev.type == "cuda"
+
+    def mark(self):
+        if self.gpu:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(torch.cuda.current_stream(self.dev))
+            return e
+        return time.perf_counter()
+
+    def seconds(self, a, b):
+        if self.gpu:
+            b.synchronize()
+            return a.elapsed_time(b) / 1e3
+        return b - a
+
+
+class ModelStatsCallback(Callback):
+    """run_dino.py:191-225: per-epoch ``epoch_time`` and ``avg_batch_time`` (logged, so they
+    reach the CSV log and ``callback_metrics``), ``total_training_time`` at the end.  A batch's
+    time is the device time from its first launch to its last (HIP events recorded in stream
+    order), so the asynchronous engine is timed without a host synchronisation per batch --
+    what time.time() around a synchronous step measures in the reference."""
+
+    def __init__(self):
+        super().__init__()
+        self.batch_times = []
+        self._marks = []
+        self.epoch_start_time = None
+        self.training_start_time = None
+        self.total_training_time = None
+        self._clock = None
+
+    def on_train_start(self, trainer, module):
+        self._clock = _Clock(getattr(getattr(module, "model", None), "device", None))
+        self.training_start_time = time.time()
+
+    def on_train_epoch_start(self, trainer, module):
+        self.epoch_start_time = self._clock.mark()
+        self._marks = []
+        self.batch_times = []
+
+    def on_train_batch_start(self, trainer, module, batch, batch_idx):
+        self._marks.append([self._clock.mark(), None])
+
+    def on_train_batch_end(self, trainer, module, outputs, batch, batch_idx):
+        self._marks[-1][1] = self._clock.mark()
+
+    def on_train_epoch_end(self, trainer, module):
+        end = self._clock.mark()
+        epoch_time = self._clock.seconds(self.epoch_start_time, end)
+        self.batch_times = [self._clock.seconds(a, b) for a, b in self._marks if b is not None]
+        avg_batch_time = float(np.mean(self.batch_times)) if self.batch_times else 0.0
+        module.log("epoch_time", epoch_time)
+        module.log("avg_batch_time", avg_batch_time)
+
+    def on_train_end(self, trainer, module):
+        self.total_training_time = time.time() - self.training_start_time
+        if trainer.logger is not None:
+            trainer.logger.log_metrics({"total_training_time": self.total_training_time},
+                                       step=max(trainer.global_step - 1, 0))
+            trainer.logger.save()
+        else:
+            print(f"Total training time: {self.total_training_time:.2f} seconds")
+
+
+class CSVLogger:
+    """lightning CSVLogger(save_dir, name): ``{save_dir}/{name}/version_{n}/metrics.csv`` (one
+    row per ``log_metrics`` call with its ``step``; the header is the sorted union of every key
+    seen, the file rewritten when a new key appears, as Lightning's _ExperimentWriter does) and
+    ``hparams.yaml``.  run_dino.py:355 builds one per seed (``logs_seed{seed}``)."""
+
+    def __init__(self, save_dir, name="lightning_logs", version=None):
+        self.save_dir, self.name = str(save_dir), name
+        root = os.path.join(self.save_dir, name)
+        if version is None:
+            os.makedirs(root, exist_ok=True)
+            have = [int(d.split("_", 1)[1]) for d in os.listdir(root)
+                    if d.startswith("version_") and d.split("_", 1)[1].isdigit()]
+            version = max(have) + 1 if have else 0
+        self.version = version
+        self.log_dir = os.path.join(root, f"version_{version}")
+        self.metrics_file_path = os.path.join(self.log_dir, "metrics.csv")
+        self.metrics, self.metrics_keys = [], []
+        self.hparams = {}
+
+    def log_hyperparams(self, params):
+        self.hparams.update({k: v for k, v in dict(params).items()
+                             if isinstance(v, (int, float, str, bool, type(None)))})
+
+    def log_metrics(self, metrics, step=None):
+        row = {k: (v.item() if torch.is_tensor(v) else v) for k, v in metrics.items()}
+        row["step"] = len(self.metrics) if step is None else int(step)
+        self.metrics.append(row)
+
+    def save(self):
+        import csv
+        import yaml
+        os.makedirs(self.log_dir, exist_ok=True)
+        with open(os.path.join(self.log_dir, "hparams.yaml"), "w") as f:
+            yaml.safe_dump(self.hparams, f)
+        if not self.metrics:
+            return
+        new = sorted(set().union(*self.metrics) - set(self.metrics_keys))
+        exists = os.path.isfile(self.metrics_file_path)
+        if new:
+            self.metrics_keys = sorted(self.metrics_keys + new)
+            if exists:       # rewrite the rows already on disk under the wider header
+                with open(self.metrics_file_path, newline="") as f:
+                    old = list(csv.DictReader(f))
+                self.metrics = old + self.metrics
+                exists = False
+        with open(self.metrics_file_path, "a" if exists else "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=self.metrics_keys)
+            if not exists:
+                w.writeheader()
+            w.writerows(self.metrics)
+        self.metrics = []
+
+    def finalize(self, status="success"):
+        self.save()
 
 
 class ModelCheckpoint(Callback):
@@ -141,18 +288,23 @@ class Trainer:
         opt, sch = self._configure(model)
         loader = self._loader(train_dataloaders, datamodule)
         dev = model.model.device
+        if self.logger is not None and hasattr(self.logger, "log_hyperparams"):
+            self.logger.log_hyperparams(dict(getattr(model, "hparams", {}) or {}))
+        self._hook("on_train_start", model)
         for epoch in range(self.current_epoch, self.max_epochs):
             self.current_epoch = epoch
             model.train()
             model.logged_history = {}
             if hasattr(loader, "set_epoch"):
                 loader.set_epoch(epoch)
+            self._hook("on_train_epoch_start", model)
             n = self.limit_train_batches
-            losses = []
+            losses, first_step = [], self.global_step
             for i, batch in enumerate(loader):
                 if n is not None and i >= n:
                     break
                 out = {}
+                self._hook("on_train_batch_start", model, batch, i)
 
                 def closure(batch=batch, i=i):
                     loss = model.training_step(batch, i)
@@ -163,6 +315,7 @@ class Trainer:
 
                 opt.step(closure)
                 losses.append(out["loss"].detach().reshape(1))
+                self._hook("on_train_batch_end", model, out, batch, i)
                 self.global_step += 1
             self._epoch_metrics(model, losses, dev)
             for cb in self.callbacks:
@@ -175,10 +328,33 @@ class Trainer:
                     cb.on_train_epoch_end(self, model)
             for s in self.lr_schedulers:
                 s.step()
-            if self.logger is not None and hasattr(self.logger, "log_metrics"):
-                self.logger.log_metrics(dict(self.logged_metrics, epoch=epoch), step=self.global_step)
+            self._log_epoch(epoch, losses, first_step)
         self.current_epoch = self.max_epochs
+        self._hook("on_train_end", model)
+        if self.logger is not None and hasattr(self.logger, "save"):
+            self.logger.save()
         return self
+
+    def _hook(self, name, model, *args):
+        for cb in self.callbacks:
+            fn = getattr(cb, name, None)
+            if fn is not None:
+                fn(self, model, *args)
+
+    def _log_epoch(self, epoch, losses, first_step):
+        """Lightning's logger rows for ``self.log('train_loss', on_step=True, on_epoch=True)``:
+        ``train_loss_step`` every ``log_every_n_steps`` steps (step index s with (s+1) % n == 0),
+        then one epoch-end row with the epoch-level metrics.  The step losses stay on the device
+        during the epoch; they are read back here, once."""
+        if self.logger is None or not hasattr(self.logger, "log_metrics"):
+            return
+        if losses:
+            vals = torch.cat(losses).float().cpu().tolist()
+            for j, v in enumerate(vals):
+                s = first_step + j
+                if (s + 1) % max(self.log_every_n_steps, 1) == 0:
+                    self.logger.log_metrics({"train_loss_step": v, "epoch": epoch}, step=s)
+        self.logger.log_metrics(dict(self.logged_metrics, epoch=epoch), step=max(self.global_step - 1, 0))
 
     def _epoch_metrics(self, model, losses, dev):
         """on_epoch=True reduction of train_loss: the mean of this epoch's step losses (in DDP,

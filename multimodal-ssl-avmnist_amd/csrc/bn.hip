@@ -68,11 +68,19 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(float* __restrict
   }
 }
 
+// the pivot a producer subtracted (non-finite pivots are taken as 0 there, conv_ws.hip)
+__device__ __forceinline__ float pivot_of(const float* pivot, size_t i) {
+  const float k = pivot[i];
+  return isfinite(k) ? k : 0.f;
+}
+
 __global__ __launch_bounds__(64) void bn_finalize_kernel(
     const float* __restrict__ parts, int G, int R, int C, int S, int chunk, long long count,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
     float* mean_o, float* invstd_o, float* scale_o, float* shift_o, float* rm, float* rv,
-    const float* __restrict__ pivot) {
+    const float* pivot, int pivot_gs) {
+  // pivot may alias rm (the running mean as the pivot): every element is read by the thread that
+  // writes it, before the write -- hence no __restrict__ on either
   const int c = blockIdx.x * 64 + threadIdx.x;
   if (c >= C) return;
   double rmean = rm ? (double)rm[c] : 0.0, rvar = rv ? (double)rv[c] : 0.0;
@@ -90,7 +98,7 @@ __global__ __launch_bounds__(64) void bn_finalize_kernel(
       sq += d[1];
     }
     const double ms = sum / n;                       // mean of (x - K)
-    const double mean = (pivot ? (double)pivot[(size_t)g * C + c] : 0.0) + ms;
+    const double mean = (pivot ? (double)pivot_of(pivot, (size_t)g * pivot_gs + c) : 0.0) + ms;
     double var = sq / n - ms * ms;
     if (var < 0) var = 0;
     const double invstd = 1.0 / sqrt(var + (double)eps);
@@ -144,7 +152,7 @@ __global__ __launch_bounds__(256) void bn_finalize1_kernel(
     const float* __restrict__ parts, int G, int R, int C, long long count,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
     float* mean_o, float* invstd_o, float* scale_o, float* shift_o, float* rm, float* rv,
-    const float* __restrict__ pivot) {
+    const float* pivot, int pivot_gs) {
   __shared__ double sh1[512], sh2[512];
   const int c = blockIdx.x;
   group_sums(parts, G, R, c, sh1, sh2);
@@ -153,7 +161,7 @@ __global__ __launch_bounds__(256) void bn_finalize1_kernel(
   const double n = (double)count;
   for (int g = 0; g < G; ++g) {
     const double ms = sh1[256 + g] / n;
-    const double mean = (pivot ? (double)pivot[(size_t)g * C + c] : 0.0) + ms;
+    const double mean = (pivot ? (double)pivot_of(pivot, (size_t)g * pivot_gs + c) : 0.0) + ms;
     double var = sh2[256 + g] / n - ms * ms;
     if (var < 0) var = 0;
     const double invstd = 1.0 / sqrt(var + (double)eps);
@@ -378,7 +386,7 @@ extern "C" {
 int avd_bn_finalize(float* parts, int G, int R, int C, long long count, const float* gamma,
                     const float* beta, float eps, float momentum, float* mean, float* invstd,
                     float* scale, float* shift, float* running_mean, float* running_var,
-                    const float* pivot, void* stream) {
+                    const float* pivot, int pivot_gs, void* stream) {
   if (!parts || !gamma || !beta || !mean || !invstd || !scale || !shift) return AVD_ERR_ARG;
   if (G <= 0 || R <= 0 || C <= 0 || count <= 1) return AVD_ERR_SHAPE;
   if ((running_mean == nullptr) != (running_var == nullptr)) return AVD_ERR_ARG;
@@ -390,7 +398,8 @@ int avd_bn_finalize(float* parts, int G, int R, int C, long long count, const fl
       getenv("AVDINO_FIN1_ROWS") ? atoll(getenv("AVDINO_FIN1_ROWS")) : 0;
   if (G <= 256 && R <= FIN1_MAXROWS && (long long)G * R <= fin1_rows) {
     bn_finalize1_kernel<<<C, 256, 0, st>>>(parts, G, R, C, count, gamma, beta, eps, momentum, mean,
-                                           invstd, scale, shift, running_mean, running_var, pivot);
+                                           invstd, scale, shift, running_mean, running_var, pivot,
+                                           pivot_gs);
     AVD_CHECK_LAUNCH();
     return AVD_OK;
   }
@@ -403,7 +412,7 @@ int avd_bn_finalize(float* parts, int G, int R, int C, long long count, const fl
   }
   bn_finalize_kernel<<<avd_cdiv(C, 64), 64, 0, st>>>(parts, G, R, C, S, chunk, count, gamma, beta,
                                                     eps, momentum, mean, invstd, scale, shift,
-                                                    running_mean, running_var, pivot);
+                                                    running_mean, running_var, pivot, pivot_gs);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

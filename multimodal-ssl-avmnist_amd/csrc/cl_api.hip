@@ -12,7 +12,8 @@ int avd_cl_weight_layout_batch_impl(int n, const float* const* w, void* const* w
                                     const int* dgrad, int dt, hipStream_t st);
 int avd_cl_conv_fwd_impl(const void* x, const void* wk, const float* bias, void* y, float* stats,
                          int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
-                         hipStream_t st);
+                         hipStream_t st, const float* pivot);
+int avd_ws_stat_rows(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt);
 int avd_cl_conv_dgrad_impl(const void* dy, const void* wk_d, void* dx, int dt, int N, int Cin,
                            int H, int W, int Cout, int K, int pad, hipStream_t st);
 int avd_cl_wgrad_chunks_impl(int N, int Cout, int Cin, int K);
@@ -209,10 +210,21 @@ int avd_cl_stat_rows(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt) {
 int avd_cl_conv_fwd(const void* x, const void* wk, const float* bias, void* y, float* stats,
                     int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
                     void* stream) {
+  return avd_cl_conv_fwd_pv(x, wk, bias, nullptr, y, stats, dt, N, B, Cin, H, W, Cout, K, pad,
+                            stream);
+}
+
+int avd_cl_stat_pivot(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt) {
+  return avd_ws_stat_rows(Ho, Wo, B, K, Cin, Cout, dt) > 0;
+}
+
+int avd_cl_conv_fwd_pv(const void* x, const void* wk, const float* bias, const float* pivot,
+                       void* y, float* stats, int dt, int N, int B, int Cin, int H, int W, int Cout,
+                       int K, int pad, void* stream) {
   if (!x || !wk || !y || !dt_ok(dt)) return AVD_ERR_ARG;
   if (N <= 0 || B <= 0 || (K != 3 && K != 5)) return AVD_ERR_SHAPE;
   return avd_cl_conv_fwd_impl(x, wk, bias, y, stats, dt, N, B, Cin, H, W, Cout, K, pad,
-                              avd_stream(stream));
+                              avd_stream(stream), stats ? pivot : nullptr);
 }
 
 int avd_cl_conv_dgrad(const void* dy, const void* wk_d, void* dx, int dt, int N, int Cin, int H,

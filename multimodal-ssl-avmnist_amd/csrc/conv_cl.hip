@@ -473,7 +473,7 @@ int avd_c1p8_fwd(const void* x, const void* wk, const float* bias, void* y, floa
 int avd_ws_stat_rows(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt);
 int avd_ws_conv_fwd(const void* x, const void* wk, const float* bias, void* y, float* stats,
                     int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
-                    hipStream_t st);
+                    hipStream_t st, const float* pivot);
 int avd_ws_conv_dgrad(const void* dy, const void* wk_d, void* dx, int dt, int N, int Cin, int H,
                       int W, int Cout, int K, int pad, hipStream_t st);
 
@@ -596,9 +596,12 @@ int dispatch_cl(const Plan& p, const void* x, const void* wk, const float* bias,
 // stats != NULL).  x/y/wk in dt; wk = avd_cl_weight_layout(fwd).  B = samples per BN group.
 int avd_cl_conv_fwd_impl(const void* x, const void* wk, const float* bias, void* y, float* stats,
                          int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
-                         hipStream_t st) {
+                         hipStream_t st, const float* pivot) {
   const int Ho = H + 2 * pad - K + 1, Wo = W + 2 * pad - K + 1;
   if (Ho <= 0 || Wo <= 0 || B <= 0 || N % B) return AVD_ERR_SHAPE;
+  // a statistics pivot is taken only by the producers whose lane-local running sums are long
+  // (avd_cl_stat_pivot): anywhere else the caller must not pass one
+  if (pivot && !avd_ws_stat_rows(Ho, Wo, B, K, Cin, Cout, dt)) return AVD_ERR_ARG;
   if (Cin != 1 && Cin % 8) return AVD_ERR_SHAPE;
   if (Cout % 4) return AVD_ERR_SHAPE;
   if (avd_c1p8_eligible(dt, Cin, Cout, K, Ho, Wo)) {   // the audio first layer: pixel-pair MFMA
@@ -611,7 +614,8 @@ int avd_cl_conv_fwd_impl(const void* x, const void* wk, const float* bias, void*
     return avd_c3_conv(x, wk, bias, y, stats, N, B, H, W, Cin, Cout, st);
   }
   // the mid-layer shapes: weights-stationary persistent kernel (conv_ws.hip)
-  if (const int r = avd_ws_conv_fwd(x, wk, bias, y, stats, dt, N, B, Cin, H, W, Cout, K, pad, st))
+  if (const int r = avd_ws_conv_fwd(x, wk, bias, y, stats, dt, N, B, Cin, H, W, Cout, K, pad, st,
+                                   pivot))
     return r > 0 ? AVD_OK : r;
   // batches only for Cin = 1 (its weights live in registers; the Cin >= 8 kernel would re-read
   // its weight fragments per batch)

@@ -107,7 +107,8 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
                                                       const float* __restrict__ bias,
                                                       bf16* __restrict__ y,
                                                       float* __restrict__ stats, int ntiles,
-                                                      int ngroups, ApplyArgs aa) {
+                                                      int ngroups, ApplyArgs aa,
+                                                      const float* __restrict__ pivot) {
   __shared__ __attribute__((aligned(16))) bf16 xs[L::LDS_ELEMS];
   __shared__ f4 red[L::RED];
   __shared__ __attribute__((aligned(16))) float ctab[AP ? APPLY_GMAX * 5 * L::CIN : 4];
@@ -143,13 +144,18 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
   } else {
     toff[0] = 8 * g;
   }
-  float bv[L::NTW][4];
+  // bias, and the statistics pivot: forward partials are shifted sums of (y - K[c]) and
+  // (y - K[c])^2 about a per-channel K near the batch mean (the layer's running mean), so the
+  // variance E[(y-K)^2] - E[y-K]^2 does not cancel when |mean| >> std (avd_bn_finalize pivot)
+  float bv[L::NTW][4], pv[L::NTW][4];
 #pragma unroll
   for (int t = 0; t < L::NTW; ++t)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int co = cob + 16 * t + 4 * g + i;
       bv[t][i] = (FWD && bias && co < L::COUT) ? bias[co] : 0.f;
+      const float k = (FWD && pivot && co < L::COUT) ? pivot[co] : 0.f;
+      pv[t][i] = isfinite(k) ? k : 0.f;
     }
   constexpr bool STATS = FWD || RD;
 
@@ -435,8 +441,9 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
                                 __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              ss[t][i] += v[i];
-              sq[t][i] = fmaf(v[i], v[i], sq[t][i]);
+              const float d = v[i] - pv[t][i];
+              ss[t][i] += d;
+              sq[t][i] = fmaf(d, d, sq[t][i]);
             }
           } else {
             lo = pack_bf16x2(acc[b][t][0], acc[b][t][1]);
@@ -553,7 +560,7 @@ int ws_stat_grid() {
 
 template <class L, bool FWD, int AP = 0, bool RD = false>
 int launch_ws(const void* x, const void* wk, const float* bias, void* y, float* stats, int N,
-              int B, hipStream_t st, const ApplyArgs& aa = ApplyArgs{}) {
+              int B, hipStream_t st, const ApplyArgs& aa = ApplyArgs{}, const float* pivot = nullptr) {
   constexpr bool STATS = FWD || RD;
   if (N % L::NS || (STATS && stats && B % L::NS)) return AVD_ERR_SHAPE;
   if (AP && (aa.B % L::NS || aa.G > APPLY_GMAX || aa.G * aa.B != N)) return AVD_ERR_SHAPE;
@@ -561,7 +568,8 @@ int launch_ws(const void* x, const void* wk, const float* bias, void* y, float* 
   const int grid = STATS && stats ? ws_stat_grid<L, FWD, RD>()
                                   : grid_cap(std::min(ntiles, num_cus() * ws_occ<L, FWD, AP, RD>()));
   conv_ws_kernel<L, FWD, AP, RD><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, (bf16*)y,
-                                                       stats, ntiles, STATS && stats ? N / B : 1, aa);
+                                                       stats, ntiles, STATS && stats ? N / B : 1, aa,
+                                                       FWD ? pivot : nullptr);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
@@ -596,13 +604,14 @@ int avd_ws_stat_rows(int Ho, int Wo, int B, int K, int Cin, int Cout, int dt) {
 // 1 = launched, 0 = shape not served (caller falls back), < 0 = error
 int avd_ws_conv_fwd(const void* x, const void* wk, const float* bias, void* y, float* stats,
                     int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
-                    hipStream_t st) {
+                    hipStream_t st, const float* pivot) {
   if (dt != AVD_BF16 || ws_disabled()) return 0;
   int r = 0;
-  if (is<FwdA2>(Cin, H, W, Cout, K, pad)) r = launch_ws<FwdA2, true>(x, wk, bias, y, stats, N, B, st);
-  else if (is<FwdA3>(Cin, H, W, Cout, K, pad)) r = launch_ws<FwdA3, true>(x, wk, bias, y, stats, N, B, st);
-  else if (is<FwdA4>(Cin, H, W, Cout, K, pad)) r = launch_ws<FwdA4, true>(x, wk, bias, y, stats, N, B, st);
-  else if (is<FwdI2>(Cin, H, W, Cout, K, pad)) r = launch_ws<FwdI2, true>(x, wk, bias, y, stats, N, B, st);
+  const ApplyArgs aa{};
+  if (is<FwdA2>(Cin, H, W, Cout, K, pad)) r = launch_ws<FwdA2, true>(x, wk, bias, y, stats, N, B, st, aa, pivot);
+  else if (is<FwdA3>(Cin, H, W, Cout, K, pad)) r = launch_ws<FwdA3, true>(x, wk, bias, y, stats, N, B, st, aa, pivot);
+  else if (is<FwdA4>(Cin, H, W, Cout, K, pad)) r = launch_ws<FwdA4, true>(x, wk, bias, y, stats, N, B, st, aa, pivot);
+  else if (is<FwdI2>(Cin, H, W, Cout, K, pad)) r = launch_ws<FwdI2, true>(x, wk, bias, y, stats, N, B, st, aa, pivot);
   else return 0;
   return r == AVD_OK ? 1 : (r == AVD_ERR_SHAPE ? 0 : r);
 }

@@ -271,14 +271,23 @@ class Branch:
 
 
 class CentralMultiModal:
-    """CentralMultiModalEncoder forward (SimpleMultiModalEncoder.forward, dino.py:229-234):
-    cat(image_branch, audio_branch) -> Linear -> ReLU -> Dropout -> Linear."""
+    """CentralMultiModalEncoder / SimpleMultiModalEncoder forward (SimpleMultiModalEncoder.forward,
+    dino.py:229-234): cat(image_branch, audio_branch) -> Linear -> ReLU -> Dropout -> Linear.
+    encoder "multi_central": CentralNet LeNets + Linear (dino.py:454-468); "multi_simple": the
+    3x3 image_encoder / audio_encoder (dino.py:18-73, 214-227), whose Linear is Sequential index
+    14 / 18."""
 
-    def __init__(self, prefix):
-        from .spec import CENTRAL_IMAGE, CENTRAL_AUDIO
+    def __init__(self, prefix, encoder="multi_central"):
+        from .spec import CENTRAL_IMAGE, CENTRAL_AUDIO, CNN3_AUDIO, CNN3_IMAGE
         self.p = prefix
-        self.img = Branch(lenet_stack(CENTRAL_IMAGE, f"{prefix}.image_encoder.0"), f"{prefix}.image_encoder.1")
-        self.aud = Branch(lenet_stack(CENTRAL_AUDIO, f"{prefix}.audio_encoder.0"), f"{prefix}.audio_encoder.1")
+        if encoder == "multi_central":
+            self.img = Branch(lenet_stack(CENTRAL_IMAGE, f"{prefix}.image_encoder.0"), f"{prefix}.image_encoder.1")
+            self.aud = Branch(lenet_stack(CENTRAL_AUDIO, f"{prefix}.audio_encoder.0"), f"{prefix}.audio_encoder.1")
+        elif encoder == "multi_simple":
+            self.img = Branch(cnn3_stack(CNN3_IMAGE, f"{prefix}.image_encoder"), f"{prefix}.image_encoder.14")
+            self.aud = Branch(cnn3_stack(CNN3_AUDIO, f"{prefix}.audio_encoder"), f"{prefix}.audio_encoder.18")
+        else:
+            raise ValueError(encoder)
 
     def forward(self, P, img, aud, G, drop_mask=None, eval_mode=False):
         fi, ci = self.img.forward(P, img, G, eval_mode)
@@ -452,7 +461,7 @@ def _views_to_rows(v):
     return np.ascontiguousarray(v.transpose(1, 0, 2, 3, 4).reshape(V * B, *v.shape[2:]))
 
 
-def multimodal_step(P, batch, mode, hp, masks=None, aux_fn=None):
+def multimodal_step(P, batch, mode, hp, masks=None, aux_fn=None, encoder="multi_central"):
     """One MultiModalDINO* training step in the reference's order:
     forward -> losses -> EMA (pre-step student) -> backward -> Adam.
 
@@ -473,8 +482,8 @@ def multimodal_step(P, batch, mode, hp, masks=None, aux_fn=None):
     img_v = np.concatenate([_views_to_rows(g_img), _views_to_rows(l_img)]).astype(F64)
     aud_v = np.concatenate([_views_to_rows(g_aud), _views_to_rows(l_aud)]).astype(F64)
 
-    stu = CentralMultiModal("student")
-    tea = CentralMultiModal("teacher")
+    stu = CentralMultiModal("student", encoder)
+    tea = CentralMultiModal("teacher", encoder)
     sproj, tproj = ProjHead("student_projection"), ProjHead("teacher_projection")
 
     # student: all views (each view its own BN group)

@@ -11,6 +11,7 @@ shapes and order match its ``state_dict`` exactly:
   (conv5x5 -> BN2d -> ReLU -> maxpool2, headless; fc1/fc2 built but unused)
 * 3x3 CNNs           -- reference models/dino.py:18-73 (image_encoder / audio_encoder)
 * CentralMultiModalEncoder -- models/dino.py:454-468 (+ fusion from 214-234)
+* SimpleMultiModalEncoder  -- models/dino.py:214-234 (image_encoder / audio_encoder + fusion)
 * ProjectionHead     -- models/dino.py:1240-1254
 * MultiModalDINO(+MSE/INFONCE/SemiSupervised) -- models/dino.py:588-632, 964-970,
   1053-1058, 1156-1161
@@ -73,18 +74,32 @@ def central_multimodal_spec(sd, prefix, E, D):
     _dense(sd, f"{prefix}.fusion.3", D, E)
 
 
+def simple_multimodal_spec(sd, prefix, E, D):
+    """SimpleMultiModalEncoder (models/dino.py:214-234, ``--model multi_simple``):
+    image_encoder(E), audio_encoder(E), fusion -- registration order = state-dict order."""
+    cnn3_spec(sd, f"{prefix}.image_encoder", CNN3_IMAGE, E)
+    cnn3_spec(sd, f"{prefix}.audio_encoder", CNN3_AUDIO, E)
+    _dense(sd, f"{prefix}.fusion.0", E, 2 * E)
+    _dense(sd, f"{prefix}.fusion.3", D, E)
+
+
+MULTIMODAL_ENCODERS = {"multi_central": central_multimodal_spec, "multi_simple": simple_multimodal_spec}
+
+
 def projection_head_spec(sd, prefix, in_dim, out_dim, hidden=PROJ_HIDDEN):
     _dense(sd, f"{prefix}.mlp.0", hidden, in_dim)
     _bn(sd, f"{prefix}.mlp.1", hidden)
     _dense(sd, f"{prefix}.mlp.4", out_dim, hidden)
 
 
-def multimodal_dino_spec(mode="mse", E=256, D=256, P=128, num_classes=10):
-    """State-dict spec of MultiModalDINO* with CentralMultiModalEncoder (``multi_central``)."""
+def multimodal_dino_spec(mode="mse", E=256, D=256, P=128, num_classes=10, encoder="multi_central"):
+    """State-dict spec of MultiModalDINO* with CentralMultiModalEncoder (``multi_central``) or
+    SimpleMultiModalEncoder (``multi_simple``)."""
+    build = MULTIMODAL_ENCODERS[encoder]
     sd = OrderedDict()
     sd["center"] = ((1, P), "center")
-    central_multimodal_spec(sd, "student", E, D)
-    central_multimodal_spec(sd, "teacher", E, D)
+    build(sd, "student", E, D)
+    build(sd, "teacher", E, D)
     projection_head_spec(sd, "student_projection", D, P)
     projection_head_spec(sd, "teacher_projection", D, P)
     if mode in ("mse", "infonce"):

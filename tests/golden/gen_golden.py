@@ -124,7 +124,8 @@ def zero_dropout(model):
 HP = dict(lr=1e-4, wd=1e-6, momentum=0.996, center_momentum=0.9, tau_s=0.1, tau_t=0.04)
 
 
-def multimodal_case(name, mode, E, D, P, B, G, L, pseed, bseed, steps, out_dir, dt="float32"):
+def multimodal_case(name, mode, E, D, P, B, G, L, pseed, bseed, steps, out_dir, dt="float32",
+                    encoder="multi_central"):
     import torch
     dt = getattr(torch, dt)
     import torch.nn as nn
@@ -137,10 +138,12 @@ def multimodal_case(name, mode, E, D, P, B, G, L, pseed, bseed, steps, out_dir, 
             "infonce": rd.MultiModalDINOWithINFONCELightning,
             "semi_supervised": rd.MultiModalDINOSemiSupervisedLightning}[mode]
     torch.manual_seed(0)
-    model = cls(encoder_class=rd.CentralMultiModalEncoder, output_dim=D, encoder_output_dim=E,
+    enc = {"multi_central": rd.CentralMultiModalEncoder,
+           "multi_simple": rd.SimpleMultiModalEncoder}[encoder]   # run_dino.py:530-540
+    model = cls(encoder_class=enc, output_dim=D, encoder_output_dim=E,
                 projection_dim=P, momentum=HP["momentum"], center_momentum=HP["center_momentum"],
                 dropout=0.0)
-    spec = ospec.multimodal_dino_spec(mode, E, D, P)
+    spec = ospec.multimodal_dino_spec(mode, E, D, P, encoder=encoder)
     state = make_state(spec, pseed)
     load_into(model, spec, state)
     zero_dropout(model)
@@ -149,7 +152,8 @@ def multimodal_case(name, mode, E, D, P, B, G, L, pseed, bseed, steps, out_dir, 
     selfns = types.SimpleNamespace(student_temperature=HP["tau_s"], teacher_temperature=HP["tau_t"],
                                    alpha=1, ce_loss=nn.CrossEntropyLoss())
     opt = torch.optim.Adam(model.parameters(), lr=HP["lr"], weight_decay=HP["wd"])
-    out = {"meta_mode": np.array(mode), "meta_dims": np.array([E, D, P, B, G, L, pseed, bseed])}
+    out = {"meta_mode": np.array(mode), "meta_dims": np.array([E, D, P, B, G, L, pseed, bseed]),
+           "meta_encoder": np.array(encoder)}
     curve = []
     for step in range(steps):
         b = make_multimodal_batch(B, G, L, bseed + step)
@@ -552,7 +556,13 @@ def main():
         ("mm_default_small", multimodal_case, ("default", 32, 32, 16, 4, 2, 4, 102, 1002, 3), {}),
         ("mm_infonce_small", multimodal_case, ("infonce", 32, 32, 16, 4, 2, 4, 103, 1003, 3), {}),
         ("mm_semi_small", multimodal_case, ("semi_supervised", 32, 32, 16, 4, 2, 4, 104, 1004, 3), {}),
-        ("mm_mse_full", multimodal_case, ("mse", 256, 256, 128, 2, 2, 4, 105, 1005, 2), {}),
+        # full E=D=256, P=128 dims, a 5-step free-running curve (north_star's 1e-4 loss-curve bar)
+        ("mm_mse_full", multimodal_case, ("mse", 256, 256, 128, 2, 2, 4, 105, 1005, 5), {}),
+        # --model multi_simple (SimpleMultiModalEncoder over the 3x3 image/audio encoders)
+        ("mm_simple_mse_small", multimodal_case, ("mse", 32, 32, 16, 3, 2, 2, 116, 1016, 3),
+         dict(encoder="multi_simple")),
+        ("mm_simple_default_small", multimodal_case, ("default", 32, 32, 16, 3, 2, 2, 117, 1017, 2),
+         dict(encoder="multi_simple")),
         ("uni_image_g2l0", unimodal_case, (256, 128, 8, 106, 1006, 3), {}),
         ("uni_image_g2l4_cos", unimodal_case, (64, 32, 6, 108, 1008, 3),
          dict(modality="image", L=4, cos_alpha=0.3)),

@@ -53,7 +53,7 @@ def test_argument_validation_without_launch():
     assert lib.avd_cl_conv_fwd(dummy, dummy, None, dummy, None, 1, 1, 1, 8, 28, 28, 16, 7, 2, None) == -1
     assert lib.avd_cl_conv_fwd(dummy, dummy, None, dummy, None, 7, 1, 1, 8, 28, 28, 16, 5, 2, None) == -4
     assert lib.avd_bn_finalize(dummy, 0, 1, 1, 2, dummy, dummy, 1e-5, 0.1, dummy, dummy, dummy,
-                               dummy, None, None, None, None) == -1
+                               dummy, None, None, None, 0, None) == -1
     assert lib.avd_stage_views(dummy, 2, None, 1, None, 4, 784, dummy, 0, None) == -4
     assert lib.avd_stage_views(dummy, 2, None, 0, None, 4, 783, dummy, 0, None) == -1
     assert lib.avd_act_fwd(dummy, dummy, 0, None, None, 4, 1, 8, 1.0, 0, None) == -1

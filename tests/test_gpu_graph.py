@@ -144,3 +144,28 @@ def test_pipelined_teacher_equals_sequential(mode, graph):
     for k in sb:
         assert torch.equal(s0[k], s1[k]), k
     assert e1._t_ready is not None
+
+
+def test_graph_recaptured_after_workspace_growth_simclr():
+    """a graph captured for SimCLR's image/image mode (small staged input) before the
+    audio/audio mode is first seen must not be replayed after that mode's eager warm-up grows
+    the shared workspace buffers (the old graph would address freed memory): it is re-captured,
+    and every step equals the eager run bit for bit."""
+    from avdino.engine import Hyper, SimCLREngine
+    from avdino.params import ParamStore
+    from avdino.spec import simclr_sd
+    modes = [0, 0, 0, 0, 1, 1, 1, 0, 0, 3, 3, 3, 0, 1]
+    res = []
+    for graph in (False, True):
+        store = ParamStore(simclr_sd(64, 32), "cuda", seed=3, has_teacher=False,
+                           groups=SimCLREngine.GROUPS)
+        eng = SimCLREngine(store, 64, 32, Hyper(weight_decay=0.0), act_dtype=torch.bfloat16,
+                           negatives="local")
+        eng.use_graph = graph
+        b = {k: torch.from_numpy(v).cuda() for k, v in make_simclr_batch(8, 4400).items()}
+        res.append(([eng.step(b, m).item() for m in modes], store, eng))
+    assert res[0][0] == res[1][0], (res[0][0], res[1][0])
+    assert torch.equal(res[0][1].student, res[1][1].student)
+    g = res[1][2].graph
+    # mode 0 was captured before mode 1 grew the buffers, then captured again
+    assert g.captures > len(g.graphs), (g.captures, list(g.graphs))
