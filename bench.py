@@ -165,6 +165,35 @@ def build_workload(args, device, act, world, rank, avdist):
                           f"local views, E=D={E}, P={P} ({cfg})", "multi_central")
 
 
+def host_cpu():
+    """The host CPU the baseline ran on (lscpu's model name and core counts, read from
+    /proc/cpuinfo: lscpu may be absent on the GPU box): model, physical cores, logical CPUs, and
+    the CPUs this process may run on (the box's CPU share)."""
+    model, phys = None, set()
+    cur = {}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if not line.strip():
+                    if "physical id" in cur and "core id" in cur:
+                        phys.add((cur["physical id"], cur["core id"]))
+                    cur = {}
+                    continue
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                cur[k] = v
+                if k == "model name" and model is None:
+                    model = v
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"cpu_model": model, "physical_cores": len(phys) or None, "logical_cpus": os.cpu_count(),
+            "affinity_cpus": aff}
+
+
 def cpu_baseline_uni(batch, seconds):
     """Config 1's reference path on the host cores: training_structures.pretrain_dino's step
     (oracle/torch_port.py UniImageDINO + pretrain_step: AdamW, EMA after the step), fp32."""
@@ -184,7 +213,7 @@ def cpu_baseline_uni(batch, seconds):
         if (n >= 2 and el >= seconds) or n >= 2000:
             break
     return {"value": round(batch * n / el, 2), "unit": "pairs/s", "cores": torch.get_num_threads(),
-            "kind": "port",
+            "kind": "port", "host": host_cpu(),
             "sample": f"oracle/torch_port.py UniImageDINO training_structures.pretrain_dino step "
                       f"(dino_train.py:143-161), fp32, B={batch}, 2 global views, {n} timed steps "
                       f"({el:.1f} s) after 1 warm-up, torch CPU {torch.get_num_threads()} threads"}
@@ -218,7 +247,7 @@ def cpu_baseline(batch, seconds):
         if (n >= 2 and el >= seconds) or n >= 400:
             break
     return {"value": round(batch * n / el, 2), "unit": "pairs/s", "cores": torch.get_num_threads(),
-            "kind": "port",
+            "kind": "port", "host": host_cpu(),
             "sample": f"oracle/torch_port.py multi_central mse step (the reference's Lightning "
                       f"training_step ops, dino.py:1214-1238), fp32, B={batch}, 2 global + 4 local "
                       f"views, {n} timed steps ({el:.1f} s) after a B=32 warm-up step, torch CPU "

@@ -9,15 +9,29 @@
  * shows the binding.
  *
  * Contract (all functions):
- *   - plain pointers + sizes; the caller owns every buffer (including partial-sum
- *     workspaces, sized with the *_parts / *_chunks helpers); the library allocates nothing
- *     and keeps no mutable global state;
+ *   - plain pointers + sizes; the caller owns every device buffer (including partial-sum
+ *     workspaces, sized with the *_parts / *_chunks / *_rows helpers); the library allocates no
+ *     device memory;
+ *   - host-side state: per-process caches filled on first use and read-only afterwards -- the
+ *     CU count and the occupancy of each persistent kernel (hipOccupancy queries that size the
+ *     persistent grids, e.g. conv_ws.hip ws_occ, conv_c1p.hip, wgrad_ws.hip, conv3.hip, c1w3.hip,
+ *     conv8.hip) and the AVDINO_* environment switches, read once; no state depends on the
+ *     data, so calls are reentrant for distinct streams (the first calls race benignly: every
+ *     thread computes the same value);
  *   - `stream` is a hipStream_t (NULL = default stream); launches are asynchronous;
  *   - return AVD_OK (0) or a negative avd_status; shapes are validated before any launch;
- *   - tensors are dense row-major (NCHW for feature maps, N = G*B samples stored
- *     group-major: group g = view g owns samples g*B .. g*B+B-1);
+ *   - layouts: conv feature maps are channels-last NHWC ([N, H, W, C], bf16 or f32), N = G*B
+ *     samples stored group-major (group g = view g owns samples g*B .. g*B+B-1); a stack's last
+ *     pooled map can also be written as the reference's (c, h, w) flatten [N, C*H*W] (f32) for
+ *     the Linear that follows; dense-head tensors are row-major f32 [rows, features];
  *   - reductions are deterministic (fixed-order partial sums, no float atomics): the same
  *     inputs give bitwise-identical outputs run to run.
+ *
+ * SURVEY.md 8(b) sketched an `avd_tensor` descriptor ABI ({data, dtype, ndim, shape[5],
+ * stride[5]}); this header passes plain pointers, dtype codes and the few sizes each kernel
+ * needs instead -- every tensor on this path is dense, so strides carry no information, and a
+ * ctypes / cgo / JNI binding of scalars is simpler than of a struct.  Leading dimensions appear
+ * explicitly where a kernel reads or writes a strided slice (GEMM ld / offsets).
  */
 #ifndef AVDINO_H
 #define AVDINO_H
@@ -454,6 +468,35 @@ int avd_adamw(float* p, const float* g, float* m, float* v, long long n, float l
 /* arena[idx[i]] += val[i] for i < n, int64, distinct indices: the num_batches_tracked
  * increments of one forward for every BatchNorm layer at once (nn.BatchNorm*d.forward in
  * training mode, num_batches_tracked += 1 per call; dino.py:680-704 calls each layer per view). */
+/* ---- the audio conv1 backward routed by forward codes (conv_c1p.hip; CentralUnimodalAudio conv1
+ * -> bn1 -> relu -> maxpool, unimodal.py:185-190, 5x5 1->8 on 112x112, bf16).
+ * avd_cl_c1_apply_codes = avd_cl_c1_recompute pass 1 (BN -> ReLU -> 2x2 max-pool z from the
+ * recomputed y) that also writes codes [N][H/2][W/2] u32: nibble c (bits 4c..4c+3) = 1 + the
+ * first argmax of relu(bn(y)) over the window when that max is > 0, else 0 -- the max-pool
+ * indices of nn.MaxPool2d (first maximum) with ReLU's zero gradient folded in.
+ * avd_cl_c1_moments_codes: ONE pass over x, the pooled gradient gz [N][H/2][W/2][8] and the
+ * codes -> per (row r, group g) of avd_cl_c1_codes_rows rows: MOMC = avd_cl_c1_codes_cols()
+ * floats: M[8][25] = sum dz x25 | Gram[25][25] = sum x25 x25^T | S[25] = sum x25 | sum dz [8],
+ * out[(r * G + g) * MOMC + ...]; reduce the rows with avd_sum_rows.
+ * avd_cl_c1_codes_combine (one launch, float64): the BN backward of bn1 (dgamma, dbeta, coef
+ * [G][8][3] as avd_bn_bwd_finalize; sum dz y = w . M + b sum dz at the exact conv output), the
+ * conv bias gradient dbias (= sum dy) and dW [8][25] = sum_g k1 M + kx (w Gram + b S) + k0 S.
+ * count = B*H*W; coef / dgamma / dbeta / dbias nullable. */
+int avd_cl_c1_codes_rows(int N, int B, int H, int W);
+int avd_cl_c1_codes_cols(void);
+int avd_cl_c1_apply_codes(const void* x, const void* wk, const float* bias, const float* scale,
+                          const float* shift, void* z, unsigned* codes, int N, int B, int H, int W,
+                          void* stream);
+int avd_cl_c1_moments_codes(const void* x, const void* gz, const unsigned* codes, float* out,
+                            int N, int B, int H, int W, void* stream);
+int avd_cl_c1_codes_combine(const float* moments, const void* wk, const float* bias,
+                            const float* gamma, const float* mean, const float* invstd,
+                            long long count, float* dw, float* dgamma, float* dbeta, float* dbias,
+                            float* coef, int G, void* stream);
+
+/* Timeline mark: marks[idx] = the device real-time counter (100 MHz ticks) when the stream
+ * reaches this launch (tools: phase timing of a replayed step without a profiler). */
+int avd_mark(unsigned long long* marks, int idx, void* stream);
 int avd_counters_add(long long* arena, const long long* idx, const long long* val, int n,
                      void* stream);
 

@@ -39,7 +39,13 @@ PROTOS = {
     "avd_cl_bn_bwd_reduce_pooled": [P, I, P, P, I, P, P, P, P, P, I, I, I, I, I, P],
     "avd_cl_dgrad_bnreduce_rows": [I, I, I, I, I, I, I, I, I],
     "avd_cl_c1_moment_cols": [I],
+    "avd_cl_c1_codes_rows": [I, I, I, I],
+    "avd_cl_c1_codes_cols": [],
+    "avd_cl_c1_apply_codes": [P, P, P, P, P, P, P, I, I, I, I, P],
+    "avd_cl_c1_moments_codes": [P, P, P, P, I, I, I, I, P],
+    "avd_cl_c1_codes_combine": [P, P, P, P, P, P, L, P, P, P, P, P, I, P],
     "avd_counters_add": [P, P, P, I, P],
+    "avd_mark": [P, I, P],
     "avd_cl_conv_dgrad_bnreduce": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "avd_cl_conv_dgrad_bnapply": [P, P, I, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "avd_cl_conv_wgrad_bnapply": [P, P, P, I, P, P, P, I, P, I, I, I, I, I, I, I, I, P],

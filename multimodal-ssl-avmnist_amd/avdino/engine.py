@@ -134,7 +134,9 @@ class ConvBranch:
         for i, (ci, co, k, pad) in enumerate(self.stack.convs):
             H, Ho, Hp = self.dims[i]
             if i == 0 and nl > 1 and self._recompute_ok(N, B, ci, H, co, k, pad, need_dgrad):
-                h = self._first_layer_recompute_fwd(ws, store, tag, ctx, h, N, G, B, update_running)
+                h = self._first_layer_recompute_fwd(ws, store, tag, ctx, h, N, G, B, update_running,
+                                                    need_dgrad)
+                ops.mark(f"{tag}.f{i}")
                 continue
             R = self._stat_rows(i, B)
             y = ws.get(f"{tag}.y{i}", N * Ho * Ho * co, self.act)
@@ -170,6 +172,7 @@ class ConvBranch:
             else:
                 ctx["feat"] = out     # the tail's pooled output (the backward's BN reduce reads it)
             h = out
+            ops.mark(f"{tag}.f{i}")
         return h.view(N, -1), ctx
 
     def forward_eval(self, ws, store, tag, x, N):
@@ -223,7 +226,18 @@ class ConvBranch:
         return (rc and self.act == torch.bfloat16 and
                 ops.cl_c1_recompute_rows(ops.C1_STATS, self.act, N, B, ci, H, H, co, k, pad) > 0)
 
-    def _first_layer_recompute_fwd(self, ws, store, tag, ctx, x, N, G, B, update_running):
+    # the 5x5 audio conv1's backward from the forward's routing codes (avd_cl_c1_moments_codes):
+    # AVDINO_C1_CODES=0 keeps the recomputing moments pass (pass 4)
+    CODES = os.environ.get("AVDINO_C1_CODES", "1") == "1"
+
+    def _codes_ok(self, N, B, need_dgrad):
+        ci, co, k, pad = self.stack.convs[0]
+        H = self.dims[0][0]
+        return (self.CODES and need_dgrad and self.act == torch.bfloat16 and (ci, co, k, pad) == (1, 8, 5, 2)
+                and ops.c1_codes_rows(N, B, H, H) > 0)
+
+    def _first_layer_recompute_fwd(self, ws, store, tag, ctx, x, N, G, B, update_running,
+                                   need_dgrad=True):
         ci, co, k, pad = self.stack.convs[0]
         H, Ho, Hp = self.dims[0]
         wk = ctx["wts"][0][0]
@@ -240,8 +254,15 @@ class ConvBranch:
         if update_running:
             store.bump_nbt(bk + ".num_batches_tracked", G)
         out = ws.get(f"{tag}.x1", N * Hp * Hp * co, self.act)
-        ops.cl_c1_recompute(ops.C1_APPLY, x, wk, bias, N, B, ci, H, H, co, k, pad, scale=st[2],
-                            shift=st[3], z=out)
+        if self._codes_ok(N, B, need_dgrad):
+            # training forward: the pooling pass also records where each window's gradient goes
+            # (routing codes), so the backward needs neither y nor a recompute of it
+            codes = ws.get(f"{tag}.c1codes", N * Hp * Hp, torch.int32)
+            ops.c1_apply_codes(x, wk, bias, st[2], st[3], out, codes, N, B, H, H)
+            ctx["codes"] = codes
+        else:
+            ops.cl_c1_recompute(ops.C1_APPLY, x, wk, bias, N, B, ci, H, H, co, k, pad, scale=st[2],
+                                shift=st[3], z=out)
         ctx["y"].append(None)          # never stored: the backward recomputes it
         ctx["stats"].append(st)
         ctx["x"].append(out)
@@ -253,6 +274,18 @@ class ConvBranch:
         x, wk, st = ctx["x"][0], ctx["wts"][0][0], ctx["stats"][0]
         bk, ck = self.stack.bn_keys[0], self.stack.conv_keys[0]
         bias = store[ck + ".bias"]
+        if ctx.get("codes") is not None:
+            # one pass over x, the pooled gradient and the routing codes; a float64 combine forms
+            # the BN backward and dW from the moments (avd_cl_c1_codes_combine)
+            Rc, mc = ops.c1_codes_rows(N, B, H, H), ops.c1_codes_cols()
+            parts = ws.get("c1_codes_parts", Rc * G * mc)
+            ops.c1_moments_codes(x, gout, ctx["codes"], parts, N, B, H, H)
+            mom = ws.get("c1_codes_mom", G * mc)
+            ops.sum_rows(parts, Rc, G * mc, mom)
+            ops.c1_codes_combine(mom, wk, bias, store[bk + ".weight"], st[0], st[1], B * Ho * Ho,
+                                 store.grad_of(ck + ".weight"), store.grad_of(bk + ".weight"),
+                                 store.grad_of(bk + ".bias"), store.grad_of(ck + ".bias"), None, G)
+            return
         R4 = ops.cl_c1_recompute_rows(ops.C1_REDUCE_MOMENTS, self.act, N, B, ci, H, H, co, k, pad)
         if self.RC_MOMENTS and R4 > 0:
             # one pass: BN-backward sums + the moments dW is linear in (3x3 layers)
@@ -323,6 +356,7 @@ class ConvBranch:
             y, st = ctx["y"][i], ctx["stats"][i]
             if y is None:              # recompute-path first layer
                 self._first_layer_recompute_bwd(ws, store, ctx, gout, N, G, B)
+                ops.mark(f"b{i}")
                 continue
             mode = self._tail_mode() if i == nl - 1 else 0
             bk, ck = self.stack.bn_keys[i], self.stack.conv_keys[i]
@@ -349,6 +383,7 @@ class ConvBranch:
                 ops.cl_bn_bwd_apply_wgrad(y, gout, st[2], st[3], coef, x, wparts, N, B, ci, H, H, co,
                                           k, pad)
                 ops.sum_rows(wparts, nsl, co * ci * k * k, store.grad_of(ck + ".weight"))
+                ops.mark(f"b{i}")
                 continue
             nch = ops.cl_wgrad_chunks(N, co, ci, k)
             wparts = ws.get("wgrad_parts", nch * co * ci * k * k)
@@ -390,8 +425,10 @@ class ConvBranch:
                 wparts = ws.get(f"wgrad_parts{i}", nch * co * ci * k * k)
                 wstream.wait_stream(main)
                 with torch.cuda.stream(wstream):
+                    ops.mark(f"w{i}.begin")
                     ops.cl_conv_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
                     ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
+                    ops.mark(f"w{i}.end")
                     ev = torch.cuda.Event()
                     ev.record(wstream)
                 wdone.append(ev)
@@ -412,6 +449,7 @@ class ConvBranch:
                 else:
                     ops.cl_conv_dgrad(dy, ctx["wts"][i][1], dx, N, ci, H, H, co, k, pad)
                 gout = dx
+            ops.mark(f"b{i}")
         for ev in wdone:
             main.wait_event(ev)
 
@@ -777,11 +815,13 @@ class MultiCentralEngine:
         """Teacher: global views, train-mode BN, no grad, into t_proj [G*B, P] (its workspace)."""
         tws, st = self.tws, self.store
         base = (self.seed * 1000003) & SEED_MASK
+        ops.mark("t.begin")
         tcat, _ = self._encoder_fwd("teacher", self.t_img, self.t_aud, x_img[:G * B * 784],
                                     x_aud[:G * B * 12544], G * B, G, "t", need_dgrad=False, ws=tws)
         tout, _ = self._fusion_fwd("teacher", tcat, G * B, "t", base + 2, ws=tws, seed_off=seed_off)
         t_proj = tws.get("t_proj", G * B * self.P)
         self.tproj.forward(tws, st, "tp", tout, G * B, t_proj, 0.0, 0)
+        ops.mark("t.end")
         return t_proj
 
     def _teacher_next(self, tin):
@@ -818,6 +858,7 @@ class MultiCentralEngine:
         N = NG * B
         if training:
             self.sstate.begin()        # dropout offset of this step, optimizer step count
+        ops.mark("fwd.begin")
         base = (self.seed * 1000003) & SEED_MASK
 
         # teacher: global views (prefix of the staged buffers), train-mode BN, no grad -- on a
@@ -862,6 +903,7 @@ class MultiCentralEngine:
                     aux.mul_(hp.alpha)
                     dzi.mul_(hp.alpha)
                     dza.mul_(hp.alpha)
+                ops.mark("heads.fwd")
                 return (zi, za), (ci, ca, dzi, dza)
 
             f_after = None
@@ -875,10 +917,12 @@ class MultiCentralEngine:
             else:
                 (head_out, hctx), h_done = self._on_side(heads)
             n_parts = V * B + B
+        ops.mark("s.enc")
         fout, sfus = self._fusion_fwd("student", cat, V * B, "s", base + 1)
         s_proj = ws.get("s_proj", V * B * P)
         spc = self.sproj.forward(ws, st, "sp", fout, V * B, s_proj, hp.dropout, base + 3,
                                  seed_off=self.sstate.seed_off)
+        ops.mark("s.proj")
         if with_orig and f_after is not None:
             (head_out, hctx), h_done = self._on_side(heads, after=f_after)
         self._join(t_done)
@@ -891,9 +935,11 @@ class MultiCentralEngine:
         ops.dino_loss(s_proj, t_proj, center, V, G, B, P, hp.tau_s, hp.tau_t, hp.center_momentum,
                       False, loss_parts[:V * B], ds, center_new, work)
         t_out = ws.get("t_out", G * B * P)  # centred teacher output (API only; the loss used t_raw)
+        ops.mark("dino")
         self._join(h_done)
         loss = ws.get("loss", 1)
         ops.sum_to(loss_parts, n_parts, 1.0, loss)
+        ops.mark("loss")
         self.fwd_count += 1
         self.last = dict(B=B, G=G, L=L, V=V, NG=NG, N=N, cat=cat, senc=senc, sfus=sfus, spc=spc,
                          ds=ds, hctx=hctx, center_new=center_new, loss=loss, s_proj=s_proj,
@@ -991,10 +1037,13 @@ class MultiCentralEngine:
             h_after.record(torch.cuda.current_stream(self.store.device))
             drain(main_steps())
             _, h_done = self._on_side(lambda: drain(heads_steps()), after=h_after)
+        ops.mark("bwd.main_heads")
         self._join(h_done)
+        ops.mark("bwd.heads_joined")
         fi, cimg, fa, caud = c["senc"]
 
         def image_branch():      # independent of the audio branch: side stream
+            ops.mark("img.bwd.begin")
             iws = self.iws
             dfi = iws.get("dfeat_img", N * fi.shape[1])
             lin = "student." + self.img_lin
@@ -1002,6 +1051,7 @@ class MultiCentralEngine:
                            st.grad_of(lin + ".bias"), dfi, N, dout_ld=2 * E,
                            mode=self.gm)
             self.img.backward(iws, st, cimg, dfi)
+            ops.mark("img.bwd.end")
 
         _, i_done = self._on_side(image_branch)
         dfa = ws.get("dfeat_aud", N * fa.shape[1])
@@ -1010,6 +1060,7 @@ class MultiCentralEngine:
                        st.grad_of(lin + ".bias"), dfa, N, dout_ld=2 * E, dout_off=E,
                        mode=self.gm)
         self.aud.backward(ws, st, caud, dfa, wstream=self.wside)
+        ops.mark("aud.bwd.end")
         self._join(i_done)
 
     def _graphable(self):
@@ -1041,15 +1092,18 @@ class MultiCentralEngine:
             tin = self.stage_teacher(next_batch)
 
         def body():
+            ops.mark_reset()
             self._forward_staged(staged, training=True, teacher_ready=ready)
             self.update_center()
             ema_step(self.store, self.hp.momentum)     # update_teacher: pre-step student
+            ops.mark("ema")
             t_done = self._teacher_next(tin) if tin is not None else None
             self.backward()
             if self.grad_hook is None:
                 adam_step_dev(self.store, self.hp, self.sstate)
             self._join(t_done)
             self.store.flush_nbt()
+            ops.mark("end")
 
         self._t_ready = (next_batch,) + tin[2:4] if tin is not None else None
         if self.use_graph and self._graphable():

@@ -511,6 +511,49 @@ def cl_c1_recompute_combine(moments, coef, wk, bias, dw, G, Cout):
     call("avd_cl_c1_recompute_combine", p(moments), p(coef), p(wk), p(bias), p(dw), G, Cout, stream())
 
 
+# ---- the audio conv1 backward routed by forward codes (include/avdino.h avd_cl_c1_*codes*)
+def c1_codes_rows(N, B, H, W):
+    """Rows per BN group of avd_cl_c1_moments_codes (0 = shape not served)."""
+    return lib.avd_cl_c1_codes_rows(N, B, H, W)
+
+
+def c1_codes_cols():
+    return lib.avd_cl_c1_codes_cols()
+
+
+def c1_apply_codes(x, wk, bias, scale, shift, z, codes, N, B, H, W):
+    """BN -> ReLU -> 2x2 max-pool of the recomputed conv1 output (avd_cl_c1_recompute pass 1)
+    plus the routing codes [N, H/2, W/2] (int32 storage of the u32 nibble words)."""
+    npool = N * (H // 2) * (W // 2)
+    _need(c1_codes_rows(N, B, H, W) > 0 and x.numel() == N * H * W and x.dtype == torch.bfloat16,
+          "c1 codes shape")
+    _need(z.numel() == npool * 8 and z.dtype == x.dtype, "c1 codes z")
+    _need(codes.numel() >= npool and codes.element_size() == 4, "c1 codes buffer")
+    _timed(f"c1_apply_codes[{N}x{H}x{W}x1->8 k5]", x.numel() * 2 + npool * 20, 2 * N * H * W * 8 * 25,
+           lambda: call("avd_cl_c1_apply_codes", p(x), p(wk), p(bias), p(scale), p(shift), p(z),
+                        p(codes), N, B, H, W, stream()))
+
+
+def c1_moments_codes(x, gz, codes, out, N, B, H, W):
+    """One pass over x, the pooled gradient and the codes -> moment rows [R][G][MOMC]."""
+    R = c1_codes_rows(N, B, H, W)
+    npool = N * (H // 2) * (W // 2)
+    _need(R > 0 and x.numel() == N * H * W and x.dtype == torch.bfloat16, "c1 moments codes shape")
+    _need(gz.numel() == npool * 8 and gz.dtype == x.dtype and codes.numel() >= npool, "c1 moments gz/codes")
+    _need(out.numel() >= R * (N // B) * c1_codes_cols(), "c1 moments rows")
+    # algorithmic work: dz x (8 x 25 per pixel pair, dense over the routed tile) + the patch Gram
+    fl = 2 * N * H * W * (8 * 25 + 25 * 26)
+    _timed(f"c1_moments_codes[{N}x{H}x{W}x1->8 k5]", x.numel() * 2 + npool * 20, fl,
+           lambda: call("avd_cl_c1_moments_codes", p(x), p(gz), p(codes), p(out), N, B, H, W, stream()))
+
+
+def c1_codes_combine(moments, wk, bias, gamma, mean, invstd, count, dw, dgamma, dbeta, dbias, coef, G):
+    """bn1 backward + conv1 bias / weight gradients from the row-summed moments [G][MOMC]."""
+    _need(moments.numel() >= G * c1_codes_cols() and dw.numel() >= 200, "c1 codes combine")
+    call("avd_cl_c1_codes_combine", p(moments), p(wk), p(bias), p(gamma), p(mean), p(invstd), int(count),
+         p(dw), p(dgamma), p(dbeta), p(dbias), p(coef), G, stream())
+
+
 _SUM_WS = {}
 _SUM_SPLIT = os.environ.get("AVDINO_SUMROWS_SPLIT", "1") == "1"   # 0: single pass (A/B runs)
 
@@ -721,3 +764,45 @@ def augment_records(stages, n, H, W, group, seed, rec, gm):
         words = gm.shape[1]
     call("avd_augment_records", st.ctypes.data, st.shape[0], n, H, W, group, seed & (2**64 - 1),
          p(rec), p(gm), words, stream())
+
+
+# ---------------------------------------------------------------- timeline marks (tools)
+class Marks:
+    """Phase marks of a step (avd_mark): ``mark(name)`` records the device real-time counter
+    when the current stream reaches it.  Enabled by engine code through the module-level
+    MARKS (None = off, no launch).  ``read()`` -> [(name, stream id, t_us)] of the last pass."""
+
+    def __init__(self, device, cap=512):
+        self.buf = torch.zeros(cap, dtype=torch.int64, device=device)
+        self.names = []
+
+    def mark(self, name):
+        s = torch.cuda.current_stream()
+        i = len(self.names)
+        if i >= self.buf.numel():
+            return
+        self.names.append((name, s.cuda_stream))
+        call("avd_mark", p(self.buf), i, s.cuda_stream)
+
+    def reset(self):
+        self.names = []
+
+    def read(self):
+        torch.cuda.synchronize()
+        t = self.buf[:len(self.names)].cpu().tolist()
+        t0 = min(t) if t else 0
+        return [(n, s, (v - t0) / 100.0) for (n, s), v in zip(self.names, t)]
+
+
+MARKS = None
+
+
+def mark(name):
+    if MARKS is not None:
+        MARKS.mark(name)
+
+
+def mark_reset():
+    """Start of a (captured or eager) step: the marks are re-numbered from 0."""
+    if MARKS is not None:
+        MARKS.reset()

@@ -37,6 +37,18 @@ int avd_c1p8_bwd_apply_wgrad(const void* y, const void* gout, const float* scale
                              const float* shift, const float* coef, const void* x, float* parts,
                              int N, int B, int H, int W, hipStream_t st);
 
+int avd_c1_codes_rows(int N, int B);
+int avd_c1_codes_cols();
+int avd_c1_apply_codes_launch(const void* x, const void* wk, const float* bias, const float* scale,
+                              const float* shift, void* z, unsigned* codes, int N, int B, int H,
+                              int W, hipStream_t st);
+int avd_c1_moments_codes_launch(const void* x, const void* gz, const unsigned* codes, float* out,
+                                int N, int B, int H, int W, hipStream_t st);
+int avd_c1_codes_combine_launch(const float* m, const void* wk, const float* bias,
+                                const float* gamma, const float* mean, const float* invstd,
+                                long long count, float* dw, float* dgamma, float* dbeta,
+                                float* dbias, float* coef, int G, hipStream_t st);
+
 int avd_c1r_rows(int pass, int N, int B, int H);
 int avd_c1p8_moment_cols();
 int avd_c1p8_combine(const float* m, const float* coef, const void* wk, const float* bias,
@@ -195,6 +207,45 @@ int avd_cl_c1_recompute_combine(const float* moments, const float* coef, const v
   if (Cout == 8)   // the 5x5 audio conv1 (conv_c1p.hip)
     return avd_c1p8_combine(moments, coef, wk, bias, dw, G, avd_stream(stream));
   return avd_c1r3_combine(moments, coef, wk, bias, dw, G, Cout, avd_stream(stream));
+}
+
+namespace {
+bool c1_codes_shape(int N, int B, int H, int W) {
+  return N > 0 && B > 0 && N % B == 0 && avd_c1p8_eligible(AVD_BF16, 1, 8, 5, H, W) && W <= 112 &&
+         H % 2 == 0 && W % 2 == 0;
+}
+}  // namespace
+
+int avd_cl_c1_codes_rows(int N, int B, int H, int W) {
+  return c1_codes_shape(N, B, H, W) ? avd_c1_codes_rows(N, B) : 0;
+}
+
+int avd_cl_c1_codes_cols(void) { return avd_c1_codes_cols(); }
+
+int avd_cl_c1_apply_codes(const void* x, const void* wk, const float* bias, const float* scale,
+                          const float* shift, void* z, unsigned* codes, int N, int B, int H, int W,
+                          void* stream) {
+  if (!x || !wk || !scale || !shift || !z || !codes) return AVD_ERR_ARG;
+  if (!c1_codes_shape(N, B, H, W)) return AVD_ERR_SHAPE;
+  return avd_c1_apply_codes_launch(x, wk, bias, scale, shift, z, codes, N, B, H, W,
+                                   avd_stream(stream));
+}
+
+int avd_cl_c1_moments_codes(const void* x, const void* gz, const unsigned* codes, float* out,
+                            int N, int B, int H, int W, void* stream) {
+  if (!x || !gz || !codes || !out) return AVD_ERR_ARG;
+  if (!c1_codes_shape(N, B, H, W)) return AVD_ERR_SHAPE;
+  return avd_c1_moments_codes_launch(x, gz, codes, out, N, B, H, W, avd_stream(stream));
+}
+
+int avd_cl_c1_codes_combine(const float* moments, const void* wk, const float* bias,
+                            const float* gamma, const float* mean, const float* invstd,
+                            long long count, float* dw, float* dgamma, float* dbeta, float* dbias,
+                            float* coef, int G, void* stream) {
+  if (!moments || !wk || !gamma || !mean || !invstd || !dw) return AVD_ERR_ARG;
+  if (G <= 0 || count <= 1) return AVD_ERR_SHAPE;
+  return avd_c1_codes_combine_launch(moments, wk, bias, gamma, mean, invstd, count, dw, dgamma,
+                                     dbeta, dbias, coef, G, avd_stream(stream));
 }
 
 int avd_cl_c1_moment_cols(int Cout) {

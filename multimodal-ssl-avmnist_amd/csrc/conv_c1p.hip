@@ -508,7 +508,8 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ coef, const bf16* __restrict__ gz, bf16* __restrict__ z,
-    float* __restrict__ out, int B, int H, int W, int ntiles, int tps) {
+    float* __restrict__ out, int B, int H, int W, int ntiles, int tps,
+    unsigned* __restrict__ codes) {
   constexpr bool NEED_Y = PASS != RC_STATS;
   constexpr bool WG = PASS == RC_WGRAD;
   __shared__ __attribute__((aligned(16))) bf16 xs[(TH + 4) * ITW];
@@ -681,6 +682,12 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = pack_bf16x2(best[2 * i], best[2 * i + 1]);
         *reinterpret_cast<u4*>(z + pw * COUT) = u4{o[0], o[1], o[2], o[3]};
+        if (codes) {   // routing code of the window: nibble e = 1 + first argmax, 0 = no route
+          unsigned code = 0u;
+#pragma unroll
+          for (int e = 0; e < COUT; ++e) code |= (best[e] > 0.f ? (unsigned)(arg[e] + 1) : 0u) << (4 * e);
+          codes[pw] = code;
+        }
       } else {
         float gg[COUT];
         unpack8(*reinterpret_cast<const u4*>(gz + pw * COUT), gg);
@@ -1310,6 +1317,313 @@ __global__ __launch_bounds__(256) void c1p8_apply_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------- routed backward
+// The training backward of the layer from the forward's routing codes instead of a recomputed y.
+// The forward apply pass (RC_APPLY with codes) already decides, per pooling window and channel,
+// where the pooled gradient goes: codes[n][hp][wp] nibble e = 1 + the first argmax of
+// relu(bn(y)) when that max is > 0, else 0 (bwd_apply_cl_kernel's routing).  So this pass needs
+// neither y nor the BN coefficients: per tile it places dz = gz at the coded pixel (zero
+// elsewhere), then per k-block of pixel pairs D += dZ X and the Gram tiles X^T X (the moments
+// kernel's 5 MFMAs; pair column 30 reads ones, so D's column 30 is sum dz and the Gram's is S).
+// The BN-backward sum dz * y at the routed pixels is not accumulated at all: y = w . x25 + b, so
+// sum dz y = w . M + b sum dz, formed in float64 by the combine (c1p8_codes_combine_kernel)
+// with the exact (unrounded) conv output.  Per block row r of group g, MOMC floats:
+//   M [8][25] | Gram [25][25] | S [25] | sum dz [8]
+constexpr int MOMC = COUT * 25 + 25 * 25 + 25 + COUT;
+
+__global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ gz, const unsigned* __restrict__ codes,
+    float* __restrict__ out, int B, int G, int R, int H, int W, int tps) {
+  __shared__ __attribute__((aligned(16))) bf16 xc[2 * XB_CB];
+  __shared__ __attribute__((aligned(16))) bf16 dys[TH * WMAX * COUT];
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int gq = lane >> 4, col = lane & 15;
+  const int Hp = H >> 1, Wp = W >> 1, cpr = W >> 3, segs = W >> 4;
+  const int grp = (int)blockIdx.x / R, rr = (int)blockIdx.x - grp * R;
+  const long long tpg = (long long)B * tps;                 // tiles of one BN group
+  const int t_begin = (int)(grp * tpg + (tpg * rr) / R), t_end = (int)(grp * tpg + (tpg * (rr + 1)) / R);
+  int bb[2], ba[2], bky[2];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    int t = 16 * tt + col;
+    if (t >= 30) t = 0;
+    const int ky = t / 6, k2 = t % 6 - 2;
+    bky[tt] = ky;
+    bb[tt] = k2 & 1;
+    ba[tt] = (k2 >= 0 ? k2 >> 1 : -1) + 1;
+  }
+  const bool ones = col == 14;                               // pair column 30: constant 1
+  f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+  f4 ga[3] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+
+  // global loads one tile ahead: <= 2 input-row vectors, and the pooled gradients + codes of
+  // this thread's <= 2 windows
+  const int nxt = (TH + 4) * cpr, nwin = (TH / 2) * Wp;
+  int xr[2], xoff[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int t = tid + 256 * s;
+    const int r = t / cpr, c = t - r * cpr;
+    xr[s] = t < nxt ? r : -(1 << 20);
+    xoff[s] = (r - 2) * W + 8 * c;
+  }
+  u4 xv[2], gv[2];
+  unsigned cv[2];
+  auto load = [&](int tile) {
+    const int n = tile / tps, ty0 = (tile - n * tps) * TH;
+    const bf16* xb = x + ((size_t)n * H + ty0) * W;
+    const size_t w0 = ((size_t)n * Hp + (ty0 >> 1)) * Wp;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bool ok = (unsigned)(ty0 - 2 + xr[s]) < (unsigned)H;
+      xv[s] = ldg16(ok ? (const void*)(xb + xoff[s]) : &kZeroC1);
+      const int w = min(tid + 256 * s, nwin - 1);
+      gv[s] = ldg16(gz + (w0 + w) * COUT);
+      cv[s] = codes[w0 + w];
+    }
+  };
+  if (t_begin < t_end) load(t_begin);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    __syncthreads();                     // the previous tile's MFMAs are done with LDS
+    // ---- parity/shift copies of the input rows (B operand)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int t = tid + 256 * s;
+      if (t >= nxt) continue;
+      const int r = t / cpr, c = t - r * cpr;
+      const unsigned wv[4] = {xv[s].x, xv[s].y, xv[s].z, xv[s].w};
+      const unsigned e0 = (wv[0] & 0xffffu) | (wv[1] << 16), ee1 = (wv[2] & 0xffffu) | (wv[3] << 16);
+      const unsigned o0 = (wv[0] >> 16) | (wv[1] & 0xffff0000u), o1 = (wv[2] >> 16) | (wv[3] & 0xffff0000u);
+      const unsigned ev[2] = {e0, ee1}, od[2] = {o0, o1};
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const unsigned lo = b ? od[0] : ev[0], hi = b ? od[1] : ev[1];
+        *reinterpret_cast<uint2*>(&xc[xbo(b, 1, r, 4 * c)]) = make_uint2(lo, hi);
+        bf16* d0 = &xc[xbo(b, 0, r, 4 * c + 1)];
+        st16(d0, (bf16)(lo & 0xffffu));
+        *reinterpret_cast<unsigned*>(d0 + 1) = (lo >> 16) | (hi << 16);
+        st16(d0 + 3, (bf16)(hi >> 16));
+        bf16* d2 = &xc[xbo(b, 2, r, 4 * c)];
+        if (c > 0) st16(d2 - 1, (bf16)(lo & 0xffffu));
+        *reinterpret_cast<unsigned*>(d2) = (lo >> 16) | (hi << 16);
+        st16(d2 + 2, (bf16)(hi >> 16));
+      }
+    }
+    if (tid < (TH + 4) * 2) {
+      const int r = tid >> 1, b = tid & 1;
+      xc[xbo(b, 0, r, 0)] = bf16(0);
+      xc[xbo(b, 2, r, Wp - 1)] = bf16(0);
+    }
+    // ---- dz at the coded pixel of every window (4 pixels x 8 channels per window thread)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int w = tid + 256 * s;
+      if (w >= nwin) continue;
+      const int hp = w / Wp, wp = w - hp * Wp;
+      const unsigned gw[4] = {gv[s].x, gv[s].y, gv[s].z, gv[s].w}, code = cv[s];
+      unsigned ow[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const unsigned nl = (code >> (8 * i)) & 0xFu, nh = (code >> (8 * i + 4)) & 0xFu;
+        const unsigned glo = gw[i] & 0xffffu, ghi = gw[i] & 0xffff0000u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          ow[k][i] = (nl == (unsigned)(k + 1) ? glo : 0u) | (nh == (unsigned)(k + 1) ? ghi : 0u);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int ry = 2 * hp + (k >> 1), cx = 2 * wp + (k & 1);
+        *reinterpret_cast<u4*>(&dys[(ry * WMAX + dys_px(ry, cx, segs)) * COUT]) =
+            u4{ow[k][0], ow[k][1], ow[k][2], ow[k][3]};
+      }
+    }
+    if (tile + 1 < t_end) load(tile + 1);   // in flight under this tile's MFMAs
+    __syncthreads();
+    // ---- k-blocks of pixel pairs: D += dZ X (tap tiles 0, 1) and the Gram tiles (0,0) (0,1) (1,1)
+    const int nkb = TH * segs;
+    if (4 * wave < nkb) {
+      typedef __attribute__((ext_vector_type(8))) short s8;
+      const int q = col >> 2, pp = col & 3;
+      const int kb0 = 4 * wave + gq;
+      int r = kb0 / segs, sg = kb0 - r * segs;
+      const int hsw = (kb0 & 1) << 3;
+      const int aoff0 = ((2 * q) ^ hsw) * COUT + 4 * pp, aoff1 = ((8 + 2 * q) ^ hsw) * COUT + 4 * pp;
+      const int boff0 = xbo(bb[0], ba[0], bky[0], 0), boff1 = xbo(bb[1], ba[1], bky[1], 0);
+      const int dr = 16 / segs, dsg = 16 - dr * segs;
+      const u4 one4 = u4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+      s4 h0, h1;
+      u4 w0, w1;
+      auto ld = [&](s4& a0, s4& a1, u4& c0, u4& c1) {
+        const int P0 = 8 * sg, ab = (r * WMAX + 2 * P0) * COUT, bs = r * XB_RS + P0;
+        a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)&dys[ab + aoff0]);
+        a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)&dys[ab + aoff1]);
+        c0 = *reinterpret_cast<const u4*>(&xc[bs + boff0]);
+        c1 = *reinterpret_cast<const u4*>(&xc[bs + boff1]);
+      };
+      auto adv = [&](bool go) {
+        if (go) {
+          sg += dsg;
+          r += dr;
+          if (sg >= segs) { sg -= segs; ++r; }
+        }
+      };
+      ld(h0, h1, w0, w1);
+      s4 n0, n1;
+      u4 v0, v1;
+      adv(4 * (wave + 4) < nkb);
+      ld(n0, n1, v0, v1);
+      for (int ks = wave;; ks += 4) {
+        const bool more = 4 * (ks + 4) < nkb;
+        s4 m0, m1;
+        u4 x0v, x1v;
+        adv(4 * (ks + 8) < nkb);
+        ld(m0, m1, x0v, x1v);
+        const bf16x8 A = __builtin_bit_cast(bf16x8, s8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]});
+        const bf16x8 X0 = __builtin_bit_cast(bf16x8, w0);
+        const bf16x8 X1 = __builtin_bit_cast(bf16x8, ones ? one4 : w1);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, X0, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, X1, acc[1], 0, 0, 0);
+        ga[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X0, X0, ga[0], 0, 0, 0);
+        ga[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X0, X1, ga[1], 0, 0, 0);
+        ga[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X1, X1, ga[2], 0, 0, 0);
+        if (!more) break;
+        h0 = n0; h1 = n1; w0 = v0; w1 = v1;
+        n0 = m0; n1 = m1; v0 = x0v; v1 = x1v;
+      }
+    }
+  }
+  // ---- block outputs: M / Gram / S folded from pairs to taps, sum dz from D's column 30
+  __syncthreads();                        // every wave is done with dys / xc
+  float* red = reinterpret_cast<float*>(dys);        // [4][16][32]  D
+  float* g6 = red + 4 * 16 * 32;                     // [4][32][32]  Gram tiles (upper blocks)
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[(wave * 16 + 4 * gq + i) * 32 + 16 * tt + col] = acc[tt][i];
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const int ti = b == 2 ? 1 : 0, tj = b == 0 ? 0 : 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      g6[(wave * 32 + 16 * ti + 4 * gq + i) * 32 + 16 * tj + col] = ga[b][i];
+  }
+  __syncthreads();
+  float* o = out + ((size_t)rr * G + grp) * MOMC;
+  auto g6v = [&](int t1, int t2) {        // the lower block (1,0) is the transpose of (0,1)
+    if (t1 >= 16 && t2 < 16) { const int tmp = t1; t1 = t2; t2 = tmp; }
+    float v = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < 4; ++wv) v += g6[(wv * 32 + t1) * 32 + t2];
+    return v;
+  };
+  for (int e = tid; e < MOMC; e += 256) {
+    float v = 0.f;
+    if (e < COUT * 25) {
+      const int c = e / 25, t = e - c * 25, ky = t / 5, kx = t - ky * 5;
+#pragma unroll
+      for (int wv = 0; wv < 4; ++wv)
+        v += red[(wv * 16 + c) * 32 + ky * 6 + kx] + red[(wv * 16 + 8 + c) * 32 + ky * 6 + kx + 1];
+    } else if (e < COUT * 25 + 625) {
+      const int a = (e - COUT * 25) / 25, b = (e - COUT * 25) % 25;
+      const int pa = (a / 5) * 6 + a % 5, pb = (b / 5) * 6 + b % 5;
+      v = g6v(pa, pb) + g6v(pa + 1, pb + 1);      // even pixel of the pair, then the odd one
+    } else if (e < COUT * 25 + 650) {
+      const int a = e - COUT * 25 - 625, pa = (a / 5) * 6 + a % 5;
+      v = g6v(pa, 30) + g6v(pa + 1, 30);
+    } else {
+      const int c = e - (COUT * 25 + 650);
+#pragma unroll
+      for (int wv = 0; wv < 4; ++wv) v += red[(wv * 16 + c) * 32 + 30] + red[(wv * 16 + 8 + c) * 32 + 30];
+    }
+    o[e] = v;
+  }
+}
+
+// BN backward + dW of the layer from the row-summed routed moments m [G][MOMC] (float64):
+//   sum dz y = w . M + b sum dz  (the exact conv output at the routed pixels)
+//   sum dz xhat = (sum dz y - mean sum dz) invstd;  coef (k1, kx, k0) as avd_bn_bwd_finalize;
+//   dW[c][t] = sum_g k1 M + kx (sum_t' w[c][t'] Gram[t'][t] + b S[t]) + k0 S[t]
+// and dgamma / dbeta / dbias (= sum dy, analytically 0) summed over the groups.
+__global__ __launch_bounds__(256) void c1p8_codes_combine_kernel(
+    const float* __restrict__ m, const bf16* __restrict__ wk, const float* __restrict__ bias,
+    const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
+    long long count, float* __restrict__ dw, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    float* __restrict__ dbias, float* __restrict__ coef, int G) {
+  __shared__ double sk[32 * COUT][3];
+  __shared__ double s12[32 * COUT][2];
+  const int tid = threadIdx.x;
+  const double n = (double)count;
+  if (tid < G * COUT) {
+    const int g = tid / COUT, c = tid - g * COUT;
+    const float* mg = m + (size_t)g * MOMC;
+    const double b = bias ? (double)bias[c] : 0.0;
+    const double s1 = mg[COUT * 25 + 650 + c];
+    double sy = b * s1;
+    for (int t = 0; t < 25; ++t) sy = fma((double)bf2f(wk[c * 32 + t]), (double)mg[c * 25 + t], sy);
+    const double mu = mean[g * COUT + c], is = invstd[g * COUT + c], ga = gamma[c];
+    const double s2 = (sy - mu * s1) * is;                   // sum dz * xhat
+    const double k1 = ga * is, kx = -ga * is * is * s2 / n, k0 = -ga * is * s1 / n + ga * is * is * mu * s2 / n;
+    sk[tid][0] = k1; sk[tid][1] = kx; sk[tid][2] = k0;
+    s12[tid][0] = s1; s12[tid][1] = s2;
+    if (coef) {
+      coef[tid * 3 + 0] = (float)k1;
+      coef[tid * 3 + 1] = (float)kx;
+      coef[tid * 3 + 2] = (float)k0;
+    }
+  }
+  __syncthreads();
+  if (tid < COUT) {
+    double dg = 0.0, db = 0.0, dbi = 0.0;
+    for (int g = 0; g < G; ++g) {
+      const int i = g * COUT + tid;
+      const double mu = mean[i];
+      dg += s12[i][1];
+      db += s12[i][0];
+      dbi += sk[i][0] * s12[i][0] + sk[i][1] * mu * n + sk[i][2] * n;
+    }
+    if (dgamma) dgamma[tid] = (float)dg;
+    if (dbeta) dbeta[tid] = (float)db;
+    if (dbias) dbias[tid] = (float)dbi;
+  }
+  for (int e = tid; e < COUT * 25; e += 256) {
+    const int c = e / 25, t = e - c * 25;
+    double wr[25];
+#pragma unroll
+    for (int k = 0; k < 25; ++k) wr[k] = (double)bf2f(wk[c * 32 + k]);
+    const double b = bias ? (double)bias[c] : 0.0;
+    double acc = 0.0;
+    for (int g = 0; g < G; ++g) {
+      const float* mg = m + (size_t)g * MOMC;
+      const float* gram = mg + COUT * 25;
+      const double sx = gram[625 + t];
+      double sy = b * sx;
+#pragma unroll
+      for (int k = 0; k < 25; ++k) sy = fma(wr[k], (double)gram[k * 25 + t], sy);
+      const int i = g * COUT + c;
+      acc += sk[i][0] * mg[e] + sk[i][1] * sy + sk[i][2] * sx;
+    }
+    dw[e] = (float)acc;
+  }
+}
+
+int c1p8_codes_rows(int N, int B) {
+  static int resident = 0;
+  if (!resident) {
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, c1p8_moments_codes_kernel, 256, 0) !=
+            hipSuccess || per <= 0)
+      per = 2;
+    resident = cus * per;
+  }
+  static const int waves = getenv("AVDINO_C1M_WAVES") ? std::max(1, atoi(getenv("AVDINO_C1M_WAVES"))) : 8;
+  const int G = N / B;
+  return std::max(1, std::min(grid_cap(resident * waves) / G, B));
+}
+
 int c1p8_moment_rows(int N, int B) {
   static int resident = 0;
   if (!resident) {
@@ -1372,7 +1686,7 @@ int avd_c1r_launch(int pass, const void* x, const void* wk, const float* bias, c
 #define AVD_RC(PS)                                                                             \
   c1p8_recompute_kernel<PS><<<grid, 256, 0, st>>>(                                             \
       (const bf16*)x, (const bf16*)wk, bias, scale, shift, mean, invstd, coef, (const bf16*)gz, \
-      (bf16*)z, out, B, H, W, ntiles, tps)
+      (bf16*)z, out, B, H, W, ntiles, tps, nullptr)
   switch (pass) {
     case RC_STATS: AVD_RC(RC_STATS); break;
     case RC_APPLY: AVD_RC(RC_APPLY); break;
@@ -1381,6 +1695,41 @@ int avd_c1r_launch(int pass, const void* x, const void* wk, const float* bias, c
     default: return AVD_ERR_ARG;
   }
 #undef AVD_RC
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+// ---------------------------------------------------------------------------- routed backward API
+int avd_c1_codes_rows(int N, int B) { return c1p8_codes_rows(N, B); }
+int avd_c1_codes_cols() { return MOMC; }
+
+int avd_c1_apply_codes_launch(const void* x, const void* wk, const float* bias, const float* scale,
+                              const float* shift, void* z, unsigned* codes, int N, int B, int H,
+                              int W, hipStream_t st) {
+  const int tps = H / TH;
+  c1p8_recompute_kernel<RC_APPLY><<<N, 256, 0, st>>>(
+      (const bf16*)x, (const bf16*)wk, bias, scale, shift, nullptr, nullptr, nullptr, nullptr,
+      (bf16*)z, nullptr, B, H, W, N * tps, tps, codes);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_c1_moments_codes_launch(const void* x, const void* gz, const unsigned* codes, float* out,
+                                int N, int B, int H, int W, hipStream_t st) {
+  const int tps = H / TH, G = N / B, R = c1p8_codes_rows(N, B);
+  c1p8_moments_codes_kernel<<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)gz, codes, out, B, G,
+                                                   R, H, W, tps);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_c1_codes_combine_launch(const float* m, const void* wk, const float* bias,
+                                const float* gamma, const float* mean, const float* invstd,
+                                long long count, float* dw, float* dgamma, float* dbeta,
+                                float* dbias, float* coef, int G, hipStream_t st) {
+  if (G <= 0 || G > 32) return AVD_ERR_SHAPE;
+  c1p8_codes_combine_kernel<<<1, 256, 0, st>>>(m, (const bf16*)wk, bias, gamma, mean, invstd, count,
+                                               dw, dgamma, dbeta, dbias, coef, G);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

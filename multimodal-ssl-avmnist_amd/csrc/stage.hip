@@ -51,3 +51,20 @@ extern "C" int avd_stage_views(const float* g, int G, const float* l, int L, con
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
+
+// ---------------------------------------------------------------------------- timeline marks
+// One lane stores the GPU's constant-rate real-time counter (s_memrealtime, 100 MHz) into
+// marks[idx] when the stream reaches this launch: phase boundaries of a captured step, timed
+// without a profiler (whose per-dispatch tracing stretches a replayed graph's timeline).
+namespace {
+__global__ void mark_kernel(unsigned long long* __restrict__ marks, int idx) {
+  if (threadIdx.x == 0) marks[idx] = wall_clock64();
+}
+}  // namespace
+
+extern "C" int avd_mark(unsigned long long* marks, int idx, void* stream) {
+  if (!marks || idx < 0) return AVD_ERR_ARG;
+  mark_kernel<<<1, 64, 0, avd_stream(stream)>>>(marks, idx);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
