@@ -248,15 +248,18 @@ int avd_cl_conv_wgrad_bnapply(const void* x, const void* y, const void* gout, in
  *                    avd_cl_bn_bwd_reduce (mode 0), gz = pooled gradient;
  *   pass 3 (wgrad):  out = dW partial slabs as avd_cl_bn_bwd_apply_wgrad.
  *   pass 4 (reduce + weight-gradient moments in one pass): out = pass 2's rows
- *                    [Cout][G][R][2], then [R][G][avd_cl_c1_moment_cols(Cout)] moments:
- *                    3x3 layers: sum dz x9 per channel/tap, Gram rows of the im2col x9 with a
- *                    ones tap (Cout*9 + 90); the 5x5 audio conv1 (Cout 8): sum dz x25 [8][25],
- *                    the x25 Gram matrix [25][25], sum x25 [25] (850).  dW is linear in
+ *                    [Cout][G][R][2], then [R][G][avd_cl_c1_moment_cols(Cout, K)] moments:
+ *                    Cout 16/32/64 (c1w3.hip): sum dz xk per channel/tap [Cout][KK], Gram rows of
+ *                    the im2col xk with a ones tap [KK][KK+1] (KK = 9 for 3x3 pad 1, 25 for 5x5
+ *                    pad 2 -- the CentralNet image conv1); the 5x5 audio conv1 (Cout 8): sum dz x25
+ *                    [8][25], the x25 Gram matrix [25][25], sum x25 [25] (850).  dW is linear in
  *                    dy = k1 dz + kx y + k0, so after avd_bn_bwd_finalize and avd_sum_rows of
  *                    the moments, avd_cl_c1_recompute_combine forms dW (y taken unrounded).
  * scale/shift/mean/invstd [G][Cout] from avd_bn_finalize, coef from avd_bn_bwd_finalize.
- * Shape as avd_cl_bn_bwd_apply_wgrad; rows() == 0 otherwise (CentralUnimodalAudio conv1+bn1+
- * pool, unimodal.py:160-190). */
+ * Shapes: Cin 1, bf16, the 5x5 pad-2 1->8 audio conv1 at 112^2 (CentralUnimodalAudio conv1+bn1+
+ * pool, unimodal.py:160-190), and 1->16/32/64 3x3 pad 1 or 5x5 pad 2 with W % 4 == 0, W <= 128
+ * (the 3x3 encoders' first layers, dino.py:18-73; CentralUnimodalImage conv1+bn1+pool,
+ * unimodal.py:127-141); rows() == 0 otherwise. */
 int avd_cl_c1_recompute_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cout,
                              int K, int pad);
 int avd_cl_c1_recompute(int pass, const void* x, const void* wk, const float* bias,
@@ -265,11 +268,12 @@ int avd_cl_c1_recompute(int pass, const void* x, const void* wk, const float* bi
                         float* out, int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
                         int pad, void* stream);
 /* dW [Cout][1][K][K] = sum_g k1 M_dz + kx (w . Gram + b sum x) + k0 sum x from pass 4's
- * row-summed moments [G][avd_cl_c1_moment_cols(Cout)] and coef [G][Cout][3]; wk = the forward
- * layout.  Cout 8: the 5x5 audio conv1; Cout 16/32/64: the 3x3 first layers. */
-int avd_cl_c1_moment_cols(int Cout);
+ * row-summed moments [G][avd_cl_c1_moment_cols(Cout, K)] and coef [G][Cout][3] (float64);
+ * wk = the forward layout.  Cout 8: the 5x5 audio conv1; Cout 16/32/64: the 3x3 / 5x5 first
+ * layers. */
+int avd_cl_c1_moment_cols(int Cout, int K);
 int avd_cl_c1_recompute_combine(const float* moments, const float* coef, const void* wk,
-                                const float* bias, float* dw, int G, int Cout, void* stream);
+                                const float* bias, float* dw, int G, int Cout, int K, void* stream);
 
 /* out[c] (+)= sum_{r<rows} in[r*ld + c]   (fixed order, f64 accumulation) -- reduces the conv
  * weight-grad partial slabs and gives Linear bias gradients (column sums of dy). */

@@ -38,7 +38,7 @@ PROTOS = {
     "avd_cl_bnapply_ok": [I, I, I, I, I, I, I, I, I, I],
     "avd_cl_bn_bwd_reduce_pooled": [P, I, P, P, I, P, P, P, P, P, I, I, I, I, I, P],
     "avd_cl_dgrad_bnreduce_rows": [I, I, I, I, I, I, I, I, I],
-    "avd_cl_c1_moment_cols": [I],
+    "avd_cl_c1_moment_cols": [I, I],
     "avd_cl_c1_codes_rows": [I, I, I, I],
     "avd_cl_c1_codes_cols": [],
     "avd_cl_c1_apply_codes": [P, P, P, P, P, P, P, I, I, I, I, P],
@@ -56,7 +56,7 @@ PROTOS = {
     "avd_cl_apply_wgrad_slabs": [I, I, I, I, I, I, I, I],
     "avd_cl_c1_recompute_rows": [I, I, I, I, I, I, I, I, I, I],
     "avd_cl_c1_recompute": [I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
-    "avd_cl_c1_recompute_combine": [P, P, P, P, P, I, I, P],
+    "avd_cl_c1_recompute_combine": [P, P, P, P, P, I, I, I, P],
     "avd_cl_bn_bwd_apply_wgrad": [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "avd_sum_rows": [P, I, I, L, P, I, P],
     "avd_sum_rows_chunks": [I, I],

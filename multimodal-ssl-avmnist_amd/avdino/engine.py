@@ -289,7 +289,7 @@ class ConvBranch:
         R4 = ops.cl_c1_recompute_rows(ops.C1_REDUCE_MOMENTS, self.act, N, B, ci, H, H, co, k, pad)
         if self.RC_MOMENTS and R4 > 0:
             # one pass: BN-backward sums + the moments dW is linear in (3x3 layers)
-            mc = ops.c1_moment_cols(co)
+            mc = ops.c1_moment_cols(co, k)
             parts = ws.get("bwd_parts_m", co * G * R4 * 2 + R4 * G * mc)
             ops.cl_c1_recompute(ops.C1_REDUCE_MOMENTS, x, wk, bias, N, B, ci, H, H, co, k, pad,
                                 scale=st[2], shift=st[3], mean=st[0], invstd=st[1], gz=gout, out=parts)
@@ -299,7 +299,7 @@ class ConvBranch:
                                 store.grad_of(ck + ".bias"))
             mom = ws.get("c1_moments", G * mc)
             ops.sum_rows(parts, R4, G * mc, mom, off=co * G * R4 * 2)
-            ops.cl_c1_recompute_combine(mom, coef, wk, bias, store.grad_of(ck + ".weight"), G, co)
+            ops.cl_c1_recompute_combine(mom, coef, wk, bias, store.grad_of(ck + ".weight"), G, co, k)
             return
         R = ops.cl_c1_recompute_rows(ops.C1_REDUCE, self.act, N, B, ci, H, H, co, k, pad)
         parts = ws.get("bwd_parts", co * G * R * 2)

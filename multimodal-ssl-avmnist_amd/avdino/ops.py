@@ -457,11 +457,11 @@ def cl_bn_bwd_apply_wgrad(y, gout, scale, shift, coef, x, parts, N, B, Cin, H, W
 C1_STATS, C1_APPLY, C1_REDUCE, C1_WGRAD, C1_REDUCE_MOMENTS = 0, 1, 2, 3, 4
 
 
-def c1_moment_cols(Cout):
-    """Columns of one pass-4 moment row (avd_cl_c1_moment_cols): 3x3 layers sum dz x9
-    [Cout][9] + Gram rows [9][10]; the 5x5 audio conv1 (Cout 8) sum dz x25 [8][25] + Gram
+def c1_moment_cols(Cout, K):
+    """Columns of one pass-4 moment row (avd_cl_c1_moment_cols): Cout 16/32/64 sum dz xk
+    [Cout][KK] + Gram rows [KK][KK+1]; the 5x5 audio conv1 (Cout 8) sum dz x25 [8][25] + Gram
     [25][25] + sum x25 [25]."""
-    n = lib.avd_cl_c1_moment_cols(Cout)
+    n = lib.avd_cl_c1_moment_cols(Cout, K)
     _need(n > 0, f"no pass-4 moments for Cout {Cout}")
     return n
 
@@ -480,7 +480,7 @@ def cl_c1_recompute(pas, x, wk, bias, N, B, Cin, H, W, Cout, K, pad, scale=None,
     if pas in (C1_STATS, C1_REDUCE):
         _need(out is not None and out.numel() >= Cout * G * rows * 2, "c1 recompute rows")
     if pas == C1_REDUCE_MOMENTS:
-        _need(out is not None and out.numel() >= G * rows * (Cout * 2 + c1_moment_cols(Cout)),
+        _need(out is not None and out.numel() >= G * rows * (Cout * 2 + c1_moment_cols(Cout, K)),
               "c1 recompute rows + moments")
         _need(mean is not None and invstd is not None, "c1 recompute mean/invstd")
     if pas == C1_WGRAD:
@@ -503,12 +503,13 @@ def cl_c1_recompute(pas, x, wk, bias, N, B, Cin, H, W, Cout, K, pad, scale=None,
                         pad, stream()))
 
 
-def cl_c1_recompute_combine(moments, coef, wk, bias, dw, G, Cout):
+def cl_c1_recompute_combine(moments, coef, wk, bias, dw, G, Cout, K=None):
     """dW of a first layer from pass 4's row-summed moments (avd_cl_c1_recompute_combine): the
-    3x3 layers (Cout 16/32/64) and the 5x5 audio conv1 (Cout 8)."""
-    _need(moments.numel() >= G * c1_moment_cols(Cout) and coef.numel() >= G * Cout * 3 and
-          dw.numel() >= Cout * (25 if Cout == 8 else 9), "c1 recompute combine shape")
-    call("avd_cl_c1_recompute_combine", p(moments), p(coef), p(wk), p(bias), p(dw), G, Cout, stream())
+    3x3 / 5x5 layers (Cout 16/32/64) and the 5x5 audio conv1 (Cout 8)."""
+    K = (5 if Cout == 8 else 3) if K is None else K
+    _need(moments.numel() >= G * c1_moment_cols(Cout, K) and coef.numel() >= G * Cout * 3 and
+          dw.numel() >= Cout * K * K, "c1 recompute combine shape")
+    call("avd_cl_c1_recompute_combine", p(moments), p(coef), p(wk), p(bias), p(dw), G, Cout, K, stream())
 
 
 # ---- the audio conv1 backward routed by forward codes (include/avdino.h avd_cl_c1_*codes*)

@@ -270,18 +270,24 @@ int avd_c1w3_apply_wgrad(const void* y, const void* gout, const float* scale, co
 }  // extern "C"
 
 // ============================================================================ recompute passes
-// The same first layer WITHOUT a stored conv output (avd_cl_c1_recompute for 3x3 / Cin 1):
-// every pass rebuilds y = bf16(conv(x) + b) for a tile of TRW rows from the staged input rows
-// (one v_mfma_f32_16x16x32_bf16 per 16 channels x 16 pixels, weights as A, k = tap as in the
-// stored-y forward, so y is bit-identical to it and across passes) and then
+// The same first layer WITHOUT a stored conv output (avd_cl_c1_recompute for Cin = 1, 3x3 pad 1
+// -- the SimCLR / unimodal encoders' first layers -- and 5x5 pad 2 -- the CentralNet image
+// conv1, unimodal.py:127-141): every pass rebuilds y = bf16(conv(x) + b) for a tile of TRW rows
+// from the staged input rows (one v_mfma_f32_16x16x32_bf16 per 16 channels x 16 pixels, weights
+// as A, k = tap: all 9 or 25 taps in one K = 32 step, so y is bit-identical to the stored-y
+// forward and across passes) and then
 //   pass 0: BN partial sums of y (per-block running sums, rows [C][G][4 * grid][2]);
 //   pass 1: z = maxpool2(relu(y * scale + shift)) NHWC bf16;
 //   pass 2: BN-backward partial sums (sum dz, sum dz * xhat) like avd_cl_bn_bwd_reduce;
-//   pass 3: dy in LDS and the weight gradient, as c1w3_kernel (plus the im2col tile x9).
-// A 16-pixel MFMA column group is a 2-row x 8-column patch (W % 8 == 0), so a pooling window
-// is the lanes {n, n^1, n^8, n^9} of a 16-lane row: DPP quad_perm / row_ror:8 exchanges.
-// The next tile's input rows (and pooled gradient, passes 2-3) are register-prefetched into a
-// second LDS buffer while the current tile computes: one barrier per tile (two in pass 3).
+//   pass 3: dy in LDS and the weight gradient, as c1w3_kernel (plus the im2col tile xk);
+//   pass 4: pass 2's sums plus the moments dW is linear in: sum dz xk [C][KK] and the Gram rows
+//           of the im2col tile [KK][KK + 1] (column KK = the ones tap: sum xk).
+// A 16-pixel MFMA column group is a 2-row x 8-column patch, so a pooling window is the lanes
+// {n, n^1, n^8, n^9} of a 16-lane row: DPP quad_perm / row_ror:8 exchanges.  Widths that are 4
+// mod 8 (the 28-pixel image) run on WV = W + 4 virtual columns whose lanes are masked out of
+// every output, sum and moment.  The next tile's input rows (and pooled gradient, passes 2-4)
+// are register-prefetched into a second LDS buffer while the current tile computes: one barrier
+// per tile (two in passes 3-4).
 namespace {
 
 template <int CTRL>
@@ -290,14 +296,33 @@ __device__ __forceinline__ int dppi(int v) {
 }
 typedef __attribute__((ext_vector_type(2))) float f2;
 typedef __attribute__((ext_vector_type(2))) short s2v;
+typedef __attribute__((ext_vector_type(8))) unsigned short us8;   // raw bf16 bits
 
 constexpr int RXO = 8;                          // xr: column ix at RXO + ix, zero pads both sides
 
 // blocks per CU (register budget: 512 / (4 x bpc) VGPRs per lane, no spills)
-__host__ __device__ constexpr int c1r3_bpc(int P, int C) { return (P >= 3 || (P == 2 && C == 64)) ? 2 : (P == 2 || C == 64) ? 3 : 4; }
+__host__ __device__ constexpr int c1r3_bpc(int P, int C, int K) {
+  return K == 5 ? ((P >= 3 || C == 64) ? 2 : 3)
+                : (P >= 3 || (P == 2 && C == 64)) ? 2 : (P == 2 || C == 64) ? 3 : 4;
+}
+__host__ __device__ constexpr int c1r3_ntap(int K) { return K * K + 1 <= 16 ? 1 : 2; }   // tap tiles
 
-template <int P, int C>
-__global__ __launch_bounds__(256, c1r3_bpc(P, C)) void c1r3_kernel(
+// the 8 taps 8 G_ .. 8 G_ + 7 of a lane's B fragment (k = tap) from the staged rows
+template <int K, int G_>
+__device__ __forceinline__ void btaps(us8& bs, const bf16* xp, int XS) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    constexpr int KK = K * K;
+    const int t = 8 * G_ + q;
+    if (t < KK) bs[q] = xp[(t / K) * XS + t % K];
+  }
+}
+
+// TR: rows of one staged tile (4, or the whole sample for small maps: the 28x28 image, where a
+// 4-row tile is too little work to hide the staging loads); passes 3-4 run their im2col /
+// dy tiles and k-loop in chunks of TRW = 4 rows of it
+template <int P, int C, int K, int TR>
+__global__ __launch_bounds__(256, c1r3_bpc(P, C, K)) void c1r3_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ wk, const float* __restrict__ bias,
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -305,36 +330,40 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C)) void c1r3_kernel(
     float* __restrict__ out, int N, int B, int H, int W) {
   constexpr int NT = C / 16;
   constexpr int DYS = C == 16 ? 16 : C + 16;
+  constexpr int KK = K * K, PADK = K / 2, NTAP = c1r3_ntap(K), XSK = 16 * NTAP;
   constexpr bool GZ = P >= 2;
   constexpr bool RED = P == 2 || P == 4;            // BN-backward partial sums
   constexpr bool WG = P >= 3;                       // im2col tile + weight-gradient MFMAs
   extern __shared__ __attribute__((aligned(16))) bf16 sm[];
-  const int TP = TRW * W;
-  const int KST = (TP + 31) / 32, TPP = KST * 32;
-  const int XS = W + 2 * RXO;                       // xr row stride
-  const int XB = (TRW + 2) * XS;                    // one xr buffer
+  constexpr int NGZ = TR == TRW ? NT : 4;          // pooled-gradient vectors per thread
+  const int WV = (W + 7) & ~7;                      // virtual width (groups of 8 columns)
+  const int TP = TRW * WV;                          // pixels of one compute chunk
+  const int KST = TP / 32;                          // k-steps (TP is a multiple of 32)
+  const int XS = WV + 2 * RXO;                      // xr row stride
+  const int XB = (TR + K - 1) * XS;                 // one xr buffer
   const int Hp = H / 2, Wp = W / 2;
-  const int GB = (TRW / 2) * Wp * C;                // one gz buffer (a tile's pooled gradient)
-  bf16* xr = sm;                                    // [2][TRW + 2][XS]
+  const int GB = (TR / 2) * Wp * C;                 // one gz buffer (a tile's pooled gradient)
+  bf16* xr = sm;                                    // [2][TR + K - 1][XS]
   bf16* gzs = xr + 2 * XB;                          // [2][GB]
-  bf16* x9 = gzs + (GZ ? 2 * GB : 0);               // [TPP][XS9] (pass 3)
-  bf16* dys = x9 + TPP * XS9;                       // [TPP][DYS] (pass 3)
+  bf16* xk = gzs + (GZ ? 2 * GB : 0);               // [TP][XSK] (passes 3, 4)
+  bf16* dys = xk + TP * XSK;                        // [TP][DYS] (passes 3, 4)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15, q4 = r16 >> 2, p4 = r16 & 3;
-  const int tps = H / TRW, ntiles = N * tps, G = N / B, tilesPG = ntiles / G;
+  const int tps = H / TR, ntiles = N * tps, G = N / B, tilesPG = ntiles / G;
   const int per = ntiles / (int)gridDim.x, extra = ntiles % (int)gridDim.x;
   const int t0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
   const int t1 = t0 + per + ((int)blockIdx.x < extra ? 1 : 0);
-  const int ngroups16 = (TRW / 2) * (W / 8);        // 16-pixel column groups per tile
+  const int gpr = WV / 8;                           // 16-pixel column groups per row pair
   // a 16-pixel column group is 2 rows x 8 columns: lane r16 -> pixel (r16 >> 3, r16 & 7)
-  const int plane = (r16 >> 3) * W + (r16 & 7);                 // pixel within the group's rows
-  const int xlane = (r16 >> 3) * (W + 2 * RXO) + (r16 & 7) + RXO - 1;
+  const int plane = (r16 >> 3) * WV + (r16 & 7);                // pixel within the group's rows
+  const int xlane = (r16 >> 3) * XS + (r16 & 7) + RXO - PADK;
   const int mn = r16 & 9;                                       // position in the 2x2 window
   const int e1 = mn & 1, e8 = mn >> 3;                          // earlier-partner tie breaks
-  const int wlane = ((r16 & 7) >> 1) * C + 4 * g;               // window column, channel quad
+  const int wcol = (r16 & 7) >> 1;                              // window column within the group
+  const int wlane = wcol * C + 4 * g;                           // window column, channel quad
 
-  // weight rows (A): lane holds w[16 t + r16][8 g .. 8 g + 7] (taps >= 9 are zero in wk)
+  // weight rows (A): lane holds w[16 t + r16][8 g .. 8 g + 7] (taps >= KK are zero in wk)
   bf16x8 aw[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) aw[t] = *reinterpret_cast<const bf16x8*>(wk + (16 * t + r16) * 32 + 8 * g);
@@ -345,32 +374,43 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C)) void c1r3_kernel(
     for (int h = 0; h < 2; ++h)
       bv2[t][h] = bias ? f2{bias[16 * t + 4 * g + 2 * h], bias[16 * t + 4 * g + 2 * h + 1]} : f2{0.f, 0.f};
 
-  // ---- staging: input rows y0-1 .. y0+TRW (16-byte vectors, one per thread) and gz
-  const int cpr = W / 8, nxv = (TRW + 2) * cpr;
+  // ---- staging: input rows y0-PADK .. y0+TR+PADK-1 (one vector per thread: 16 bytes, or 8
+  // when W is 4 mod 8) and gz
+  const bool v16 = (W & 7) == 0;
+  const int cpr = v16 ? W / 8 : W / 4, nxv = (TR + K - 1) * cpr;
   const int xrow = tid / cpr, xcol = tid - xrow * cpr;
   u4 xv = u4{0u, 0u, 0u, 0u};
-  u4 gv4[NT];
+  u4 gv4[NGZ];
   auto load = [&](int tl) {
-    const int n = tl / tps, y0 = (tl - n * tps) * TRW;
-    const int iy = y0 - 1 + xrow;
-    if (tid < nxv)
-      xv = (unsigned)iy < (unsigned)H
-               ? *reinterpret_cast<const u4*>(x + ((size_t)n * H + iy) * W + 8 * xcol)
-               : u4{0u, 0u, 0u, 0u};
+    const int n = tl / tps, y0 = (tl - n * tps) * TR;
+    const int iy = y0 - PADK + xrow;
+    if (tid < nxv) {
+      const bool ok = (unsigned)iy < (unsigned)H;
+      const bf16* src = x + ((size_t)n * H + iy) * W;
+      if (v16) xv = ok ? *reinterpret_cast<const u4*>(src + 8 * xcol) : u4{0u, 0u, 0u, 0u};
+      else {
+        const uint2 v = ok ? *reinterpret_cast<const uint2*>(src + 4 * xcol) : make_uint2(0u, 0u);
+        xv = u4{v.x, v.y, 0u, 0u};
+      }
+    }
     if constexpr (GZ) {
       const bf16* gb = gz + ((size_t)n * Hp + y0 / 2) * Wp * C;
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
+      for (int j = 0; j < NGZ; ++j) {
         const int e = tid + 256 * j;
         if (8 * e < GB) gv4[j] = *reinterpret_cast<const u4*>(gb + 8 * e);
       }
     }
   };
   auto put = [&](int buf) {
-    if (tid < nxv) *reinterpret_cast<u4*>(xr + buf * XB + xrow * XS + RXO + 8 * xcol) = xv;
+    if (tid < nxv) {
+      bf16* d = xr + buf * XB + xrow * XS + RXO;
+      if (v16) *reinterpret_cast<u4*>(d + 8 * xcol) = xv;
+      else *reinterpret_cast<uint2*>(d + 4 * xcol) = make_uint2(xv.x, xv.y);
+    }
     if constexpr (GZ) {
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
+      for (int j = 0; j < NGZ; ++j) {
         const int e = tid + 256 * j;
         if (8 * e < GB) *reinterpret_cast<u4*>(gzs + buf * GB + 8 * e) = gv4[j];
       }
@@ -391,25 +431,36 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C)) void c1r3_kernel(
       for (int h = 0; h < 2; ++h) { rs2[t][h] = f2{0.f, 0.f}; rq2[t][h] = f2{0.f, 0.f}; }
     }
   };
-  f4 acc3[NT], gacc;
-  const int WSZ = C * 9 + 90;                       // pass 4 moments per (row, group)
+  constexpr int NG = NTAP == 1 ? 1 : 3;             // Gram tiles (0,0) [(0,1) (1,1)]
+  f4 acc3[NT][NTAP], gacc[NG];
+  const int WSZ = C * KK + KK * (KK + 1);           // pass 4 moments per (row, group)
   float* wmo = out + (size_t)C * G * R * 2;         // pass 4: [R][G][WSZ] after the sums
   auto flush = [&](int gp) {
     if constexpr (P == 4) {
-      // this wave's moments of group gp: sum dz x9 [C][9], then the Gram rows of x9 [9][10]
-      // (column 9 is the ones tap: sum x9)
+      // this wave's moments of group gp: sum dz xk [C][KK], then the Gram rows of xk
+      // [KK][KK + 1] (column KK is the ones tap: sum xk); the lower tile (1,0) by symmetry
       float* o = wmo + ((size_t)srow * G + gp) * WSZ;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (r16 < 9) o[(16 * t + 4 * g + i) * 9 + r16] = acc3[t][i];
-          acc3[t][i] = 0.f;
-        }
+        for (int nt = 0; nt < NTAP; ++nt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (4 * g + i < 9 && r16 < 10) o[C * 9 + (4 * g + i) * 10 + r16] = gacc[i];
-        gacc[i] = 0.f;
+          for (int i = 0; i < 4; ++i) {
+            const int tap = 16 * nt + r16;
+            if (tap < KK) o[(16 * t + 4 * g + i) * KK + tap] = acc3[t][nt][i];
+            acc3[t][nt][i] = 0.f;
+          }
+      float* gr = o + C * KK;
+#pragma unroll
+      for (int b = 0; b < NG; ++b) {
+        const int ti = b == 2 ? 1 : 0, tj = b == 0 ? 0 : 1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int a = 16 * ti + 4 * g + i, c = 16 * tj + r16;
+          if (a < KK && c <= KK) gr[a * (KK + 1) + c] = gacc[b][i];
+          if (b == 1 && c < KK && a < KK) gr[c * (KK + 1) + a] = gacc[b][i];
+          gacc[b][i] = 0.f;
+        }
       }
     }
 #pragma unroll
@@ -425,21 +476,23 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C)) void c1r3_kernel(
       }
   };
   zero_run();
-  // BN coefficients of the current group (passes 1-3): channels 16 t + 4 g + i
+  // BN coefficients of the current group (passes 1-4): channels 16 t + 4 g + i
   f2 sc2[NT][2], sf2[NT][2];
   float c2[NT][4], c3[NT][4], c4[NT][4];
   int cg = -1;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc3[t] = f4{0.f, 0.f, 0.f, 0.f};
-  gacc = f4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int nt = 0; nt < NTAP; ++nt) acc3[t][nt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int b = 0; b < NG; ++b) gacc[b] = f4{0.f, 0.f, 0.f, 0.f};
 
-  // zero both xr buffers (pads stay zero) and the padding pixels of the im2col / dy tiles
+  // zero both xr buffers (pads and virtual columns stay zero) and the dy tile (its virtual
+  // columns stay zero: dz / dy is written for the valid lanes only)
   for (int i = tid; i < 2 * XB / 8; i += 256) reinterpret_cast<u4*>(xr)[i] = u4{0u, 0u, 0u, 0u};
   if constexpr (WG) {
-    for (int i = TP * (DYS / 8) + tid; i < TPP * (DYS / 8); i += 256)
+    for (int i = tid; i < TP * (DYS / 8); i += 256)
       *reinterpret_cast<u4*>(dys + (size_t)i * 8) = u4{0u, 0u, 0u, 0u};
-    for (int i = TP * (XS9 / 8) + tid; i < TPP * (XS9 / 8); i += 256)
-      *reinterpret_cast<u4*>(x9 + (size_t)i * 8) = u4{0u, 0u, 0u, 0u};
   }
   if (t0 < t1) load(t0);
   __syncthreads();
@@ -447,7 +500,7 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C)) void c1r3_kernel(
   if (t0 + 1 < t1) load(t0 + 1);
 
   for (int ti = t0; ti < t1; ++ti) {
-    const int n = ti / tps, y0 = (ti - n * tps) * TRW, gb = n / B, buf = ti & 1;
+    const int n = ti / tps, y0 = (ti - n * tps) * TR, gb = n / B, buf = ti & 1;
     if constexpr (P == 0 || RED) {
       const int gi = ti / tilesPG;
       if (gi != cur_g) {
@@ -470,134 +523,158 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C)) void c1r3_kernel(
           }
       }
     }
-    __syncthreads();                    // buffer `buf` complete; the other one and x9/dys free
+    __syncthreads();                    // buffer `buf` complete; the other one and xk/dys free
     if (ti + 1 < t1) put(buf ^ 1);
     if (ti + 2 < t1) load(ti + 2);      // in flight under this tile's work
     const bf16* xb = xr + buf * XB;
-    if constexpr (WG) {
-      // im2col x9[p][tap] for the weight-gradient MFMAs (taps 9..15 zero; pass 4: tap 9 = 1)
-      for (int p = tid; p < TP; p += 256) {
-        const int r = p / W, c = p - r * W;
-        uint32_t w8[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) w8[k] = 0u;
-        if constexpr (P == 4) w8[4] = 0x3F800000u;   // bf16 1.0 at tap 9
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const uint32_t b = __builtin_bit_cast(uint16_t, xb[(r + t / 3) * XS + RXO - 1 + c + t % 3]);
-          w8[t >> 1] |= (t & 1) ? b << 16 : b;
-        }
-        *reinterpret_cast<u4*>(x9 + p * XS9) = u4{w8[0], w8[1], w8[2], w8[3]};
-        *reinterpret_cast<u4*>(x9 + p * XS9 + 8) = u4{w8[4], w8[5], w8[6], w8[7]};
-      }
-    }
-    // ---- y for the wave's column groups, straight from the staged rows; pass epilogues
     const bf16* gzt = gzs + buf * GB;
     const size_t zt = ((size_t)n * Hp + y0 / 2) * Wp * C;            // tile's first pooled row
-    for (int q = wave; q < ngroups16; q += 4) {
-      const int gr = q / (W / 8), gc8 = q - gr * (W / 8);              // wave-uniform
-      const bf16* xp = xb + 2 * gr * XS + 8 * gc8 + xlane;
-      typedef __attribute__((ext_vector_type(8))) unsigned short us8;   // raw bf16 bits
-      us8 bs = us8{};
-      if (g == 0) {
-        bs[0] = xp[0]; bs[1] = xp[1]; bs[2] = xp[2];
-        bs[3] = xp[XS]; bs[4] = xp[XS + 1]; bs[5] = xp[XS + 2];
-        bs[6] = xp[2 * XS]; bs[7] = xp[2 * XS + 1];
-      } else if (g == 1) {
-        bs[0] = xp[2 * XS + 2];
-      }
-      const bf16x8 bx = __builtin_bit_cast(bf16x8, bs);
-      const int wg = (gr * Wp + 4 * gc8) * C + wlane;                  // window (lane part in wlane)
+    // passes 0-2: the whole tile in one sweep; passes 3-4: chunks of TRW rows (im2col + dy
+    // tiles, then the k-loop)
+    constexpr int NCH = WG ? TR / TRW : 1;
+    for (int cr = 0; cr < NCH; ++cr) {
+      const int r0 = WG ? cr * TRW : 0;                                // first tile row of the sweep
+      if (WG && cr > 0) __syncthreads();                               // last chunk's k-loop is done
+      if constexpr (WG) {
+        // im2col xk[p][tap] for the weight-gradient MFMAs (taps KK.. zero; pass 4: tap KK = 1);
+        // virtual columns (c >= W) all zero
+        for (int p = tid; p < TP; p += 256) {
+          const int r = p / WV, c = p - r * WV;
+          uint32_t w8[XSK / 2];
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[t], bx, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        // y = bf16(acc + b) for the lane's 4 channels, as two packed pairs
-        f2 y2[2];
-        uint32_t yb[2];
+          for (int k = 0; k < XSK / 2; ++k) w8[k] = 0u;
+          if (c < W) {
+            if constexpr (P == 4) w8[KK >> 1] = (KK & 1) ? 0x3F800000u : 0x3F80u;   // bf16 1.0 at tap KK
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const f2 s2 = f2{acc[2 * h], acc[2 * h + 1]} + bv2[t][h];
-          yb[h] = pack_bf16x2(s2.x, s2.y);
-          y2[h] = f2{__uint_as_float(yb[h] << 16), __uint_as_float(yb[h] & 0xffff0000u)};
-        }
-        if constexpr (P == 0) {
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            rs2[t][h] += y2[h];
-            rq2[t][h] = __builtin_elementwise_fma(y2[h], y2[h], rq2[t][h]);
-          }
-        } else if constexpr (P == 1) {
-          // relu(bn(y)) rounded to bf16 (monotone: the max of the rounded values is the rounded
-          // max), window max over lanes ^1 then ^8 on packed non-negative bf16 as int16
-          uint32_t m[2];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const f2 v = __builtin_elementwise_fma(y2[h], sc2[t][h], sf2[t][h]);
-            s2v r = __builtin_elementwise_max(__builtin_bit_cast(s2v, pack_bf16x2(v.x, v.y)), s2v{0, 0});
-            r = __builtin_elementwise_max(r, __builtin_bit_cast(s2v, dppi<0xB1>(__builtin_bit_cast(int, r))));
-            r = __builtin_elementwise_max(r, __builtin_bit_cast(s2v, dppi<0x128>(__builtin_bit_cast(int, r))));
-            m[h] = __builtin_bit_cast(uint32_t, r);
-          }
-          if (mn == 0)
-            *reinterpret_cast<uint2*>(z + zt + wg + 16 * t) = make_uint2(m[0], m[1]);
-        } else {
-          // first argmax of the window (k order (0,0),(0,1),(1,0),(1,1); lane L^m holds
-          // k = 2 (m >> 3) + (m & 1)) on bn(y) as signed ints: ordered like the floats wherever
-          // one side is > 0, and only a positive maximum carries the gradient.  The lane wins
-          // iff it beats its earlier partners strictly and its later ones or ties:
-          // v > u  <=>  v >= u + 1 (ints), the +1 only toward earlier partners.
-          const uint2 gw = *reinterpret_cast<const uint2*>(gzt + wg + 16 * t);
-          const float gg[4] = {__uint_as_float(gw.x << 16), __uint_as_float(gw.x & 0xffff0000u),
-                               __uint_as_float(gw.y << 16), __uint_as_float(gw.y & 0xffff0000u)};
-          float dz[4];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const f2 v = __builtin_elementwise_fma(y2[h], sc2[t][h], sf2[t][h]);
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const int vi = __float_as_int(v[e]);
-              const int u1 = dppi<0xB1>(vi) + e1, u8 = dppi<0x128>(vi) + e8,
-                        u9 = dppi<0x128>(dppi<0xB1>(vi)) + e8;
-              const int thr = max(max(u1, u8), max(u9, 1));
-              dz[2 * h + e] = vi >= thr ? gg[2 * h + e] : 0.f;
+            for (int t = 0; t < KK; ++t) {
+              const uint32_t b = __builtin_bit_cast(uint16_t, xb[(r0 + r + t / K) * XS + RXO - PADK + c + t % K]);
+              w8[t >> 1] |= (t & 1) ? b << 16 : b;
             }
           }
-          if constexpr (RED) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float yy = y2[i >> 1][i & 1];
-              const float xh = (yy - c2[t][i]) * c3[t][i];
-              rs[t][i] += dz[i];
-              rq[t][i] = fmaf(dz[i], xh, rq[t][i]);
-            }
-          }
-          if constexpr (P == 4) {     // dz (exact in bf16: a pooled gradient or zero)
-            *reinterpret_cast<uint2*>(dys + (2 * gr * W + 8 * gc8 + plane) * DYS + 16 * t + 4 * g) =
-                make_uint2(pack_bf16x2(dz[0], dz[1]), pack_bf16x2(dz[2], dz[3]));
-          } else if constexpr (P == 3) {
-            float d[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-              d[i] = fmaf(c2[t][i], dz[i], fmaf(c3[t][i], y2[i >> 1][i & 1], c4[t][i]));   // dy
-            *reinterpret_cast<uint2*>(dys + (2 * gr * W + 8 * gc8 + plane) * DYS + 16 * t + 4 * g) =
-                make_uint2(pack_bf16x2(d[0], d[1]), pack_bf16x2(d[2], d[3]));
-          }
+          for (int v = 0; v < XSK / 8; ++v)
+            *reinterpret_cast<u4*>(xk + p * XSK + 8 * v) = u4{w8[4 * v], w8[4 * v + 1], w8[4 * v + 2], w8[4 * v + 3]};
         }
       }
-    }
-    if constexpr (WG) {
-      __syncthreads();
-      for (int ks = wave; ks < KST; ks += 4) {
-        const int P0 = 32 * ks;
-        const int pa = P0 + kpx(g, 0, q4), pb = P0 + kpx(g, 1, q4);
-        const bf16x8 bvv = fr8(trd(x9 + pa * XS9 + 4 * p4), trd(x9 + pb * XS9 + 4 * p4));
+      // ---- y for the wave's column groups, straight from the staged rows; pass epilogues
+      const int ngroups16 = ((WG ? TRW : TR) / 2) * gpr;
+      for (int q = wave; q < ngroups16; q += 4) {
+        const int grl = q / gpr, gc8 = q - grl * gpr;                   // wave-uniform
+        const int gr = r0 / 2 + grl;                                    // row pair within the tile
+        const bool vld = 8 * gc8 + (r16 & 7) < W;                       // a real (not virtual) column
+        const bool wvld = 4 * gc8 + wcol < Wp;                          // its pooling window
+        const bf16* xp = xb + 2 * gr * XS + 8 * gc8 + xlane;
+        us8 bs = us8{};
+        if (g == 0) btaps<K, 0>(bs, xp, XS);
+        else if (g == 1) btaps<K, 1>(bs, xp, XS);
+        else if (g == 2) btaps<K, 2>(bs, xp, XS);
+        else btaps<K, 3>(bs, xp, XS);
+        const bf16x8 bx = __builtin_bit_cast(bf16x8, bs);
+        const int wg = wvld ? (gr * Wp + 4 * gc8) * C + wlane : 0;     // window (lane part in wlane)
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-          const bf16x8 av = fr8(trd(dys + pa * DYS + 16 * t + 4 * p4), trd(dys + pb * DYS + 16 * t + 4 * p4));
-          acc3[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bvv, acc3[t], 0, 0, 0);
+          const f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[t], bx, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          // y = bf16(acc + b) for the lane's 4 channels, as two packed pairs
+          f2 y2[2];
+          uint32_t yb[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const f2 s2 = f2{acc[2 * h], acc[2 * h + 1]} + bv2[t][h];
+            yb[h] = pack_bf16x2(s2.x, s2.y);
+            y2[h] = f2{__uint_as_float(yb[h] << 16), __uint_as_float(yb[h] & 0xffff0000u)};
+          }
+          if constexpr (P == 0) {
+            if (vld) {
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                rs2[t][h] += y2[h];
+                rq2[t][h] = __builtin_elementwise_fma(y2[h], y2[h], rq2[t][h]);
+              }
+            }
+          } else if constexpr (P == 1) {
+            // relu(bn(y)) rounded to bf16 (monotone: the max of the rounded values is the rounded
+            // max), window max over lanes ^1 then ^8 on packed non-negative bf16 as int16
+            uint32_t m[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const f2 v = __builtin_elementwise_fma(y2[h], sc2[t][h], sf2[t][h]);
+              s2v r = __builtin_elementwise_max(__builtin_bit_cast(s2v, pack_bf16x2(v.x, v.y)), s2v{0, 0});
+              r = __builtin_elementwise_max(r, __builtin_bit_cast(s2v, dppi<0xB1>(__builtin_bit_cast(int, r))));
+              r = __builtin_elementwise_max(r, __builtin_bit_cast(s2v, dppi<0x128>(__builtin_bit_cast(int, r))));
+              m[h] = __builtin_bit_cast(uint32_t, r);
+            }
+            if (mn == 0 && wvld)
+              *reinterpret_cast<uint2*>(z + zt + wg + 16 * t) = make_uint2(m[0], m[1]);
+          } else {
+            // first argmax of the window (k order (0,0),(0,1),(1,0),(1,1); lane L^m holds
+            // k = 2 (m >> 3) + (m & 1)) on bn(y) as signed ints: ordered like the floats wherever
+            // one side is > 0, and only a positive maximum carries the gradient.  The lane wins
+            // iff it beats its earlier partners strictly and its later ones or ties:
+            // v > u  <=>  v >= u + 1 (ints), the +1 only toward earlier partners.
+            const uint2 gw = *reinterpret_cast<const uint2*>(gzt + wg + 16 * t);
+            const float gg[4] = {__uint_as_float(gw.x << 16), __uint_as_float(gw.x & 0xffff0000u),
+                                 __uint_as_float(gw.y << 16), __uint_as_float(gw.y & 0xffff0000u)};
+            float dz[4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const f2 v = __builtin_elementwise_fma(y2[h], sc2[t][h], sf2[t][h]);
+#pragma unroll
+              for (int e = 0; e < 2; ++e) {
+                const int vi = __float_as_int(v[e]);
+                const int u1 = dppi<0xB1>(vi) + e1, u8 = dppi<0x128>(vi) + e8,
+                          u9 = dppi<0x128>(dppi<0xB1>(vi)) + e8;
+                const int thr = max(max(u1, u8), max(u9, 1));
+                dz[2 * h + e] = (vi >= thr && vld) ? gg[2 * h + e] : 0.f;
+              }
+            }
+            if constexpr (RED) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const float yy = y2[i >> 1][i & 1];
+                const float xh = (yy - c2[t][i]) * c3[t][i];
+                rs[t][i] += dz[i];
+                rq[t][i] = fmaf(dz[i], xh, rq[t][i]);
+              }
+            }
+            if constexpr (P == 4) {     // dz (exact in bf16: a pooled gradient or zero)
+              *reinterpret_cast<uint2*>(dys + (2 * grl * WV + 8 * gc8 + plane) * DYS + 16 * t + 4 * g) =
+                  make_uint2(pack_bf16x2(dz[0], dz[1]), pack_bf16x2(dz[2], dz[3]));
+            } else if constexpr (P == 3) {
+              float d[4];
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                d[i] = vld ? fmaf(c2[t][i], dz[i], fmaf(c3[t][i], y2[i >> 1][i & 1], c4[t][i])) : 0.f;   // dy
+              *reinterpret_cast<uint2*>(dys + (2 * grl * WV + 8 * gc8 + plane) * DYS + 16 * t + 4 * g) =
+                  make_uint2(pack_bf16x2(d[0], d[1]), pack_bf16x2(d[2], d[3]));
+            }
+          }
         }
-        // the same fragment is the A operand of the x9 Gram matrix (rows: taps, k: pixels)
-        if constexpr (P == 4) gacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bvv, bvv, gacc, 0, 0, 0);
+      }
+      if constexpr (WG) {
+        __syncthreads();
+        for (int ks = wave; ks < KST; ks += 4) {
+          const int P0 = 32 * ks;
+          const int pa = P0 + kpx(g, 0, q4), pb = P0 + kpx(g, 1, q4);
+          bf16x8 bvv[NTAP];
+#pragma unroll
+          for (int nt = 0; nt < NTAP; ++nt)
+            bvv[nt] = fr8(trd(xk + pa * XSK + 16 * nt + 4 * p4), trd(xk + pb * XSK + 16 * nt + 4 * p4));
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            const bf16x8 av = fr8(trd(dys + pa * DYS + 16 * t + 4 * p4), trd(dys + pb * DYS + 16 * t + 4 * p4));
+#pragma unroll
+            for (int nt = 0; nt < NTAP; ++nt)
+              acc3[t][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bvv[nt], acc3[t][nt], 0, 0, 0);
+          }
+          // the same fragments are the A operands of the im2col Gram matrix (rows: taps, k: pixels)
+          if constexpr (P == 4) {
+            gacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bvv[0], bvv[0], gacc[0], 0, 0, 0);
+            if constexpr (NTAP == 2) {
+              gacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bvv[0], bvv[NTAP - 1], gacc[1], 0, 0, 0);
+              gacc[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bvv[NTAP - 1], bvv[NTAP - 1], gacc[2], 0, 0, 0);
+            }
+          }
+        }
       }
     }
   }
@@ -615,88 +692,105 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C)) void c1r3_kernel(
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) red[(wave * C + 16 * t + 4 * g + i) * 16 + r16] = acc3[t][i];
+      for (int nt = 0; nt < NTAP; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[(wave * C + 16 * t + 4 * g + i) * XSK + 16 * nt + r16] = acc3[t][nt][i];
     __syncthreads();
-    float* o = out + (size_t)blockIdx.x * C * 9;
-    for (int e = tid; e < C * 9; e += 256) {
-      const int c = e / 9, tap = e - c * 9;
+    float* o = out + (size_t)blockIdx.x * C * KK;
+    for (int e = tid; e < C * KK; e += 256) {
+      const int c = e / KK, tap = e - c * KK;
       float sacc = 0.f;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) sacc += red[(w * C + c) * 16 + tap];
+      for (int w = 0; w < 4; ++w) sacc += red[(w * C + c) * XSK + tap];
       o[e] = sacc;
     }
   }
 }
 
-size_t c1r3_lds(int P, int C, int W) {
-  const size_t XB = (size_t)(TRW + 2) * (W + 2 * RXO);
-  const size_t GB = P >= 2 ? (size_t)(TRW / 2) * (W / 2) * C : 0;
+// staged tile rows: the whole 28-row sample for the small image maps, else 4
+int c1r3_tr(int H, int W) { return (W <= 32 && H == 28) ? 28 : TRW; }
+
+size_t c1r3_lds(int P, int C, int W, int K, int TR) {
+  const int WV = (W + 7) & ~7;
+  const size_t XB = (size_t)(TR + K - 1) * (WV + 2 * RXO);
+  const size_t GB = P >= 2 ? (size_t)(TR / 2) * (W / 2) * C : 0;
   size_t e = 2 * XB + 2 * GB;
+  const int XSK = 16 * c1r3_ntap(K);
   if (P >= 3) {
     const int DYS = C == 16 ? 16 : C + 16;
-    const size_t tpp = (size_t)(TRW * W + 31) / 32 * 32;
-    e += tpp * (XS9 + DYS);
+    e += (size_t)TRW * WV * (XSK + DYS);
   }
-  return std::max(e * 2, P == 3 ? (size_t)4 * C * 16 * 4 : (size_t)0);
+  return std::max(e * 2, P == 3 ? (size_t)4 * C * XSK * 4 : (size_t)0);
 }
 
-int c1r3_grid(int P, int C) { return grid_cap(c1r3_bpc(P, C) * ncu_c1w3()); }
+int c1r3_grid(int P, int C, int K) {
+  const int bpc = K == 5 ? c1r3_bpc(P, C, 5) : c1r3_bpc(P, C, 3);
+  return grid_cap(bpc * ncu_c1w3());
+}
 
-// dW of pass 4 from the row-summed moments m [G][C * 9 + 90] and the BN-backward coefficients:
-//   dW[c][t] = sum_g k1 sum(dz x9_t) + kx sum(y x9_t) + k0 sum(x9_t),
-//   sum(y x9_t) = sum_t' w[c][t'] Gram[t'][t] + b[c] sum(x9_t)   (y = w . x9 + b)
+// dW of pass 4 from the row-summed moments m [G][C * KK + KK * (KK + 1)] and the BN-backward
+// coefficients, in float64 (the kx and k0 terms are large and cancel: dy is centred):
+//   dW[c][t] = sum_g k1 sum(dz xk_t) + kx sum(y xk_t) + k0 sum(xk_t),
+//   sum(y xk_t) = sum_t' w[c][t'] Gram[t'][t] + b[c] sum(xk_t)   (y = w . xk + b)
 __global__ void c1r3_combine_kernel(const float* __restrict__ m, const float* __restrict__ coef,
                                     const bf16* __restrict__ wk, const float* __restrict__ bias,
-                                    float* __restrict__ dw, int G, int C) {
+                                    float* __restrict__ dw, int G, int C, int KK) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= C * 9) return;
-  const int c = e / 9, t = e - c * 9, WSZ = C * 9 + 90;
-  float wr[9];
-#pragma unroll
-  for (int k = 0; k < 9; ++k) wr[k] = bf2f(wk[c * 32 + k]);
-  const float b = bias ? bias[c] : 0.f;
-  float acc = 0.f;
+  if (e >= C * KK) return;
+  const int c = e / KK, t = e - c * KK, WSZ = C * KK + KK * (KK + 1);
+  const double b = bias ? (double)bias[c] : 0.0;
+  double acc = 0.0;
   for (int g = 0; g < G; ++g) {
     const float* mg = m + (size_t)g * WSZ;
-    const float* gram = mg + C * 9;
-    const float sx = gram[t * 10 + 9];
-    float sy = b * sx;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) sy = fmaf(wr[k], gram[k * 10 + t], sy);
+    const float* gram = mg + C * KK;
+    const double sx = gram[t * (KK + 1) + KK];
+    double sy = b * sx;
+    for (int k = 0; k < KK; ++k) sy = fma((double)bf2f(wk[c * 32 + k]), (double)gram[k * (KK + 1) + t], sy);
     const float* k3 = coef + ((size_t)g * C + c) * 3;
-    acc += k3[0] * mg[e] + k3[1] * sy + k3[2] * sx;
+    acc += (double)k3[0] * mg[e] + (double)k3[1] * sy + (double)k3[2] * sx;
   }
-  dw[e] = acc;
+  dw[e] = (float)acc;
 }
 
 }  // namespace
 
 extern "C" {
 
-// rows / slabs of a recompute pass for a 3x3 Cin-1 first layer (0: not served)
+// rows / slabs of a recompute pass for a Cin-1 first layer, 3x3 pad 1 or 5x5 pad 2 (0: not served)
 int avd_c1r3_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad) {
   if (getenv("AVDINO_C1R3_OFF")) return 0;
-  if (dt != AVD_BF16 || Cin != 1 || K != 3 || pad != 1 || B <= 0 || N % B) return 0;
+  if (dt != AVD_BF16 || Cin != 1 || !((K == 3 && pad == 1) || (K == 5 && pad == 2)) || B <= 0 || N % B) return 0;
+  // the 5x5 image conv1 (1->32 at 28^2) is served on request only: its passes measure no faster
+  // than the stored-y chain at the bench's N (tools/c1bench.py: 98 + 112 + 332 us vs 542 us for
+  // conv + pool + reduce + apply + wgrad) -- the 25-tap B-fragment gather is the cost
+  if (K == 5 && !getenv("AVDINO_C1R5")) return 0;
   if (Cout != 16 && Cout != 32 && Cout != 64) return 0;
-  if (H % TRW || W % 8 || W > 128 || pass < 0 || pass > 4) return 0;
-  if (c1r3_lds(3, Cout, W) > 80 * 1024) return 0;     // every pass served, or none
-  const int grid = c1r3_grid(pass, Cout);
+  if (K == 5 && Cout != 32) return 0;                   // instantiated: the CentralNet image conv1
+  if (H % TRW || W % 4 || W > 128 || pass < 0 || pass > 4) return 0;
+  const int TR = c1r3_tr(H, W);
+  if (TR != TRW && ((W > 32) || Cout > 32)) return 0;   // whole-sample tiles: gz staging bound
+  if ((TR + K - 1) * (W % 8 ? W / 4 : W / 8) > 256) return 0;                // one x vector per thread
+  if (c1r3_lds(3, Cout, W, K, TR) > 80 * 1024 || c1r3_lds(4, Cout, W, K, TR) > 80 * 1024) return 0;   // every pass, or none
+  const int grid = c1r3_grid(pass, Cout, K);
   return pass == 1 ? 1 : pass == 3 ? grid : 4 * grid;   // pass 4: rows R of both its outputs
 }
 
 int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, const float* scale,
                     const float* shift, const float* mean, const float* invstd, const float* coef,
-                    const void* gz, void* z, float* out, int N, int B, int H, int W, int Cout,
+                    const void* gz, void* z, float* out, int N, int B, int H, int W, int Cout, int K,
                     hipStream_t st) {
-  const int grid = c1r3_grid(pass, Cout);
-  const size_t lds = c1r3_lds(pass, Cout, W);
-#define AVD_P(P_, C_)                                                                          \
-  if (pass == P_ && Cout == C_)                                                                \
-    c1r3_kernel<P_, C_><<<grid, 256, lds, st>>>((const bf16*)x, (const bf16*)wk, bias, scale,   \
-                                                shift, mean, invstd, coef, (const bf16*)gz,    \
-                                                (bf16*)z, out, N, B, H, W);
-#define AVD_PC(C_) AVD_P(0, C_) else AVD_P(1, C_) else AVD_P(2, C_) else AVD_P(3, C_) else AVD_P(4, C_)
-  AVD_PC(16) else AVD_PC(32) else AVD_PC(64) else return AVD_ERR_SHAPE;
+  const int grid = c1r3_grid(pass, Cout, K);
+  const int TR = c1r3_tr(H, W);
+  const size_t lds = c1r3_lds(pass, Cout, W, K, TR);
+#define AVD_P(P_, C_, K_, TR_)                                                                 \
+  if (pass == P_ && Cout == C_ && K == K_ && TR == TR_)                                        \
+    c1r3_kernel<P_, C_, K_, TR_><<<grid, 256, lds, st>>>((const bf16*)x, (const bf16*)wk, bias,   \
+                                                         scale, shift, mean, invstd, coef,      \
+                                                         (const bf16*)gz, (bf16*)z, out, N, B, H, W);
+#define AVD_PC(C_, K_, TR_) AVD_P(0, C_, K_, TR_) else AVD_P(1, C_, K_, TR_) else AVD_P(2, C_, K_, TR_) \
+  else AVD_P(3, C_, K_, TR_) else AVD_P(4, C_, K_, TR_)
+  AVD_PC(16, 3, 4) else AVD_PC(32, 3, 4) else AVD_PC(64, 3, 4) else AVD_PC(32, 5, 4)
+  else AVD_PC(16, 3, 28) else AVD_PC(32, 3, 28) else AVD_PC(32, 5, 28) else return AVD_ERR_SHAPE;
 #undef AVD_PC
 #undef AVD_P
   AVD_CHECK_LAUNCH();
@@ -704,9 +798,10 @@ int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, 
 }
 
 int avd_c1r3_combine(const float* m, const float* coef, const void* wk, const float* bias,
-                     float* dw, int G, int Cout, hipStream_t st) {
-  c1r3_combine_kernel<<<avd_cdiv(Cout * 9, 64), 64, 0, st>>>(m, coef, (const bf16*)wk, bias, dw, G,
-                                                             Cout);
+                     float* dw, int G, int Cout, int K, hipStream_t st) {
+  const int KK = K * K;
+  c1r3_combine_kernel<<<avd_cdiv(Cout * KK, 64), 64, 0, st>>>(m, coef, (const bf16*)wk, bias, dw, G,
+                                                              Cout, KK);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

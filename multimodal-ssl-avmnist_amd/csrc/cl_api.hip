@@ -166,11 +166,11 @@ int avd_cl_bn_bwd_apply_wgrad(const void* y, const void* gout, const float* scal
 int avd_c1r3_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad);
 int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, const float* scale,
                     const float* shift, const float* mean, const float* invstd, const float* coef,
-                    const void* gz, void* z, float* out, int N, int B, int H, int W, int Cout,
+                    const void* gz, void* z, float* out, int N, int B, int H, int W, int Cout, int K,
                     hipStream_t st);
 
 int avd_c1r3_combine(const float* m, const float* coef, const void* wk, const float* bias,
-                     float* dw, int G, int Cout, hipStream_t st);
+                     float* dw, int G, int Cout, int K, hipStream_t st);
 
 int avd_cl_c1_recompute_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cout,
                              int K, int pad) {
@@ -195,18 +195,19 @@ int avd_cl_c1_recompute(int pass, const void* x, const void* wk, const float* bi
     return AVD_ERR_ARG;
   if (avd_c1r3_rows(pass, dt, N, B, Cin, H, W, Cout, K, pad))
     return avd_c1r3_launch(pass, x, wk, bias, scale, shift, mean, invstd, coef, gz, z, out, N, B,
-                           H, W, Cout, avd_stream(stream));
+                           H, W, Cout, K, avd_stream(stream));
   return avd_c1r_launch(pass, x, wk, bias, scale, shift, mean, invstd, coef, gz, z, out, N, B, H,
                         W, avd_stream(stream));
 }
 
 int avd_cl_c1_recompute_combine(const float* moments, const float* coef, const void* wk,
-                                const float* bias, float* dw, int G, int Cout, void* stream) {
+                                const float* bias, float* dw, int G, int Cout, int K, void* stream) {
   if (!moments || !coef || !wk || !dw) return AVD_ERR_ARG;
-  if (G <= 0 || (Cout != 8 && Cout != 16 && Cout != 32 && Cout != 64)) return AVD_ERR_SHAPE;
+  if (G <= 0 || (Cout != 8 && Cout != 16 && Cout != 32 && Cout != 64) || (K != 3 && K != 5))
+    return AVD_ERR_SHAPE;
   if (Cout == 8)   // the 5x5 audio conv1 (conv_c1p.hip)
-    return avd_c1p8_combine(moments, coef, wk, bias, dw, G, avd_stream(stream));
-  return avd_c1r3_combine(moments, coef, wk, bias, dw, G, Cout, avd_stream(stream));
+    return K == 5 ? avd_c1p8_combine(moments, coef, wk, bias, dw, G, avd_stream(stream)) : AVD_ERR_SHAPE;
+  return avd_c1r3_combine(moments, coef, wk, bias, dw, G, Cout, K, avd_stream(stream));
 }
 
 namespace {
@@ -248,9 +249,9 @@ int avd_cl_c1_codes_combine(const float* moments, const void* wk, const float* b
                                      dbeta, dbias, coef, G, avd_stream(stream));
 }
 
-int avd_cl_c1_moment_cols(int Cout) {
-  if (Cout == 8) return avd_c1p8_moment_cols();
-  if (Cout == 16 || Cout == 32 || Cout == 64) return Cout * 9 + 90;
+int avd_cl_c1_moment_cols(int Cout, int K) {
+  if (Cout == 8) return K == 5 ? avd_c1p8_moment_cols() : 0;
+  if ((Cout == 16 || Cout == 32 || Cout == 64) && (K == 3 || K == 5)) return Cout * K * K + K * K * (K * K + 1);
   return 0;
 }
 

@@ -247,12 +247,18 @@ def test_cl_bn_bwd_apply_wgrad_fused_first_layer(ops, HN):
 @pytest.mark.parametrize("HN", [(112, 4, 8, 5, 2), (48, 6, 8, 5, 2),
                                 # the 3x3 encoders' first layer (c1r3_kernel, c1w3.hip)
                                 (112, 4, 32, 3, 1), (112, 6, 16, 3, 1), (56, 4, 64, 3, 1),
-                                (48, 6, 32, 3, 1), (8, 4, 16, 3, 1)])
-def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN):
+                                (48, 6, 32, 3, 1), (8, 4, 16, 3, 1),
+                                # widths 4 mod 8 (virtual columns) and the 5x5 CentralNet image
+                                # conv1 (1->32 at 28^2, unimodal.py:127-141)
+                                (28, 6, 32, 3, 1), (28, 6, 32, 5, 2), (20, 6, 32, 5, 2),
+                                (48, 4, 32, 5, 2)])
+def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN, monkeypatch):
     """avd_cl_c1_recompute (the audio conv1 without a stored conv output) against the stored-y
     kernels on the same bf16 operands: identical pooled output (bit-exact: same rounded y), and
     the statistics / BN-backward partials / weight gradient to fp32 summation order."""
     H, N, C, K, pad = HN
+    if K == 5 and C != 8:
+        monkeypatch.setenv("AVDINO_C1R5", "1")     # the 5x5 image conv1 passes (opt-in path)
     B, Cin = N // 2, 1
     G = N // B
     T = torch.bfloat16
@@ -300,8 +306,15 @@ def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN):
     dg, dbt = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
     ops.bn_bwd_finalize(p0, G, Rb, C, B * H * H, dev(gamma), bn[0], bn[1], coef, dg, dbt, None)
     ns = ops.cl_apply_wgrad_slabs(T, N, 1, H, H, C, K, pad)
-    f0 = torch.empty(ns * C * K * K, device="cuda")
-    ops.cl_bn_bwd_apply_wgrad(y, gz, bn[2], bn[3], coef, tx, f0, N, B, 1, H, H, C, K, pad)
+    if ns:   # the stored-y fused apply + wgrad (c1p8 / c1w3)
+        f0 = torch.empty(ns * C * K * K, device="cuda")
+        ops.cl_bn_bwd_apply_wgrad(y, gz, bn[2], bn[3], coef, tx, f0, N, B, 1, H, H, C, K, pad)
+    else:    # (5x5 Cout 32: no fused stored-y kernel) the unfused apply, then the weight gradient
+        dyk = torch.empty_like(y)
+        ops.cl_bn_bwd_apply(y, gz, 0, bn[2], bn[3], coef, dyk, N, B, C, H, H)
+        ns = ops.cl_wgrad_chunks(N, C, 1, K)
+        f0 = torch.empty(ns * C * K * K, device="cuda")
+        ops.cl_conv_wgrad(tx, dyk, f0, N, 1, H, H, C, K, pad)
     nw = ops.cl_c1_recompute_rows(ops.C1_WGRAD, T, N, B, 1, H, H, C, K, pad)
     f1 = torch.empty(nw * C * K * K, device="cuda")
     ops.cl_c1_recompute(ops.C1_WGRAD, tx, wk, tb, N, B, 1, H, H, C, K, pad, scale=bn[2],
@@ -315,7 +328,7 @@ def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN):
     # pass 4: the reduce rows of pass 2 plus the moments; dW = combine(moments, coef)
     # (3x3: [C*9 | Gram rows 9 x 10 with the ones tap]; 5x5 audio conv1: [C*25 | 25 x 25 | 25])
     KK = K * K
-    mc = ops.c1_moment_cols(C)
+    mc = ops.c1_moment_cols(C, K)
     m4 = torch.full((C * G * R4 * 2 + R4 * G * mc,), float("nan"), device="cuda")
     ops.cl_c1_recompute(ops.C1_REDUCE_MOMENTS, tx, wk, tb, N, B, 1, H, H, C, K, pad, scale=bn[2],
                         shift=bn[3], mean=bn[0], invstd=bn[1], gz=gz, out=m4)
@@ -329,14 +342,15 @@ def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN):
         np.pad(nchw(x).astype(np.float64), ((0, 0), (0, 0), (pad, pad), (pad, pad))), (K, K), (2, 3))
     xk = win.reshape(G, B, H, H, KK)
     gram = np.einsum("gbhwi,gbhwj->gij", xk, xk)
-    if K == 3:
-        gk, sk = mh[:, C * 9:].reshape(G, 9, 10)[:, :, :9], mh[:, C * 9:].reshape(G, 9, 10)[:, :, 9]
+    if C != 8:   # c1r3 layout: Gram rows with the ones tap [KK][KK + 1]
+        gk = mh[:, C * KK:].reshape(G, KK, KK + 1)[:, :, :KK]
+        sk = mh[:, C * KK:].reshape(G, KK, KK + 1)[:, :, KK]
     else:
         gk, sk = mh[:, C * KK:C * KK + KK * KK].reshape(G, KK, KK), mh[:, C * KK + KK * KK:]
     assert rel(gk, gram) < 1e-5, rel(gk, gram)
     assert rel(sk, xk.sum((1, 2, 3))) < 1e-5
     dk = torch.empty(C * KK, device="cuda")
-    ops.cl_c1_recompute_combine(mom, coef, wk, tb, dk, G, C)
+    ops.cl_c1_recompute_combine(mom, coef, wk, tb, dk, G, C, K)
     # dW from the unrounded dy = k1 dz + kx y + k0 (y = w . xk + b unrounded in the kx term):
     # against float64 of exactly that, and within the bf16 rounding of dy of the stored-y path
     # (dy is centred, so its rounding shows in dW amplified by the cancellation: ~0.5 %)

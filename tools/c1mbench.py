@@ -49,7 +49,7 @@ def main():
     R1 = ops.cl_c1_recompute_rows(ops.C1_STATS, T, N, B, 1, H, H, C, K, pad)
     st1 = torch.empty(C * G * R1 * 2, device="cuda")
     R4 = ops.cl_c1_recompute_rows(ops.C1_REDUCE_MOMENTS, T, N, B, 1, H, H, C, K, pad)
-    mc = ops.c1_moment_cols(C)
+    mc = ops.c1_moment_cols(C, K)
     m4 = torch.empty(C * G * R4 * 2 + R4 * G * mc, device="cuda")
 
     def fwd():
