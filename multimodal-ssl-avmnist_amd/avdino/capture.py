@@ -1,0 +1,125 @@
+"""hipGraph capture of a training step, in segments around host points.
+
+A step's device work is captured once per input shape and replayed (one host call per segment
+instead of ~200 launches).  Data-parallel steps have host points inside the step: a
+collective issued by the host (``torch.distributed`` over RCCL, or gloo in the rehearsal) that
+reads and writes FIXED device buffers -- the global-negative all-gather / reduce-scatter of
+InfoNCE (config 3) and NT-Xent (config 4), the early gradient bucket's all-reduce.  The step
+body calls :func:`host_point` there.  Eagerly that just runs the collective; while capturing it
+closes the current graph segment, executes it, runs the collective and opens the next segment,
+so a replay is ``graph_0, collective_0, graph_1, ..., graph_n`` on the caller's stream, every
+collective in the same order on every rank.  Work forked to side streams must be joined
+before a host point (a segment, like any captured graph, ends with every forked stream
+rejoined); callers join exactly there and nowhere else.
+"""
+import torch
+
+from . import ops
+
+_ACTIVE = None     # the _Capture in progress (host_point's target), else None
+
+
+class _Capture:
+    def __init__(self, pool):
+        self.pool, self.seq, self.g = pool, [], None
+
+    def begin(self):
+        self.g = torch.cuda.CUDAGraph()
+        self.g.capture_begin(pool=self.pool, capture_error_mode="relaxed")
+
+    def end(self):
+        self.g.capture_end()
+        self.seq.append(self.g)
+        self.g.replay()            # capturing executed nothing: run the segment now
+        self.g = None
+
+    def cut(self, fn):
+        self.end()
+        fn()
+        self.seq.append(fn)
+        self.begin()
+
+
+def host_point(fn):
+    """Run the host-issued collective ``fn()`` at this point of the step (see module doc).
+    ``fn`` must only touch buffers whose addresses are fixed across steps."""
+    if _ACTIVE is None:
+        fn()
+    else:
+        _ACTIVE.cut(fn)
+
+
+def capturing():
+    return _ACTIVE is not None
+
+
+class GraphedStep:
+    """A training step's device work captured once per input shape as a sequence of hipGraphs
+    (torch.cuda.CUDAGraph over HIP stream capture, side streams joined by events) separated by
+    host points, and replayed.  The first ``warmup`` calls per shape run eagerly (they size
+    every workspace), the next one captures.
+
+    A graph holds the device pointers of the scratch buffers it was captured over; when any of
+    them is reallocated later (a larger key's eager warm-up grows a shared buffer, e.g. SimCLR's
+    image/image mode captured before its audio/audio mode was first seen) the graph is stale:
+    each capture records the allocation epoch after it and is dropped and re-captured instead
+    of replayed once the epoch has moved."""
+
+    def __init__(self, warmup=2):
+        self.warmup = warmup
+        self.graphs = {}     # key -> (segments, allocation epoch after the capture)
+        self.seen = {}
+        self.captures = 0
+        self.pool = None
+        self.stream = None
+
+    def segments(self, key):
+        """Number of graph segments of the capture for ``key`` (None: not captured)."""
+        ent = self.graphs.get(key)
+        return None if ent is None else sum(1 for s in ent[0] if hasattr(s, "replay"))
+
+    def run(self, key, body):
+        global _ACTIVE
+        ent = self.graphs.get(key)
+        if ent is not None:
+            if ent[1] == ops.alloc_epoch():
+                for s in ent[0]:
+                    if hasattr(s, "replay"):
+                        s.replay()
+                    else:
+                        s()          # a host point's collective
+                return
+            del self.graphs[key]            # captured over buffers that have since moved
+            self.seen[key] = self.warmup - 1
+        n = self.seen.get(key, 0)
+        if n < self.warmup:
+            self.seen[key] = n + 1
+            body()
+            return
+        if _ACTIVE is not None:
+            raise RuntimeError("nested step capture")
+        torch.cuda.synchronize()
+        if self.pool is None:
+            self.pool = torch.cuda.graph_pool_handle()
+            self.stream = torch.cuda.Stream()
+        main = torch.cuda.current_stream()
+        self.stream.wait_stream(main)
+        cap = _Capture(self.pool)
+        with torch.cuda.stream(self.stream):
+            _ACTIVE = cap
+            try:
+                cap.begin()
+                body()
+                cap.end()
+            except BaseException:
+                if cap.g is not None:       # leave no stream in capture mode behind
+                    try:
+                        cap.g.capture_end()
+                    except Exception:
+                        pass
+                raise
+            finally:
+                _ACTIVE = None
+        main.wait_stream(self.stream)
+        self.graphs[key] = (cap.seq, ops.alloc_epoch())
+        self.captures += 1

@@ -11,11 +11,14 @@ of S are exactly rows r*B.. of the single-device S over the global W*B batch.  E
 loss is the mean over ITS rows; DDP's gradient averaging (x 1/W) then yields the gradient of
 the global-batch loss.  The column side of dS (how my rows act as other ranks' negatives /
 positives) is reduce-scattered back to the owning rank (avdino.dist).  W == 1 is the
-reference's single-device loss exactly.
+reference's single-device loss exactly.  The collectives are host points (avdino.capture) on
+fixed workspace buffers, so a global-negative step is still a captured graph -- three
+segments around the gather and the scatter.
 
 Compute is libavdino: l2norm, MFMA GEMMs, softmax-CE with offset targets / masks, axpy.
 """
 from . import dist, ops
+from .capture import host_point
 
 
 class _Norm:
@@ -42,9 +45,13 @@ def infonce(ws, zi, za, B, P, dzi, dza, loss_parts, temperature=0.07, gm=ops.GEM
     W, r = _world(local, group)
     inv_t = 1.0 / temperature
     ni, na = _Norm(ws, "nce.i", zi, B, P), _Norm(ws, "nce.a", za, B, P)
-    ni_all = ni.y if W == 1 else dist.gather_rows(ni.y.view(B, P), group).reshape(-1)
-    na_all = na.y if W == 1 else dist.gather_rows(na.y.view(B, P), group).reshape(-1)
     C = W * B
+    if W == 1:
+        ni_all, na_all = ni.y, na.y
+    else:   # host point: the all-gathers write fixed buffers the next graph segment reads
+        ni_all, na_all = ws.get("nce.ni_all", C * P), ws.get("nce.na_all", C * P)
+        host_point(lambda: (dist.gather_rows(ni.y.view(B, P), group, out=ni_all.view(C, P)),
+                            dist.gather_rows(na.y.view(B, P), group, out=na_all.view(C, P))))
     S1, S2 = ws.get("nce.S1", B * C), ws.get("nce.S2", B * C)
     ops.gemm(B, C, P, ni.y, P, 1, na_all, 1, P, S1, C, alpha=inv_t, mode=gm)   # image rows
     ops.gemm(B, C, P, na.y, P, 1, ni_all, 1, P, S2, C, alpha=inv_t, mode=gm)   # audio rows
@@ -64,8 +71,11 @@ def infonce(ws, zi, za, B, P, dzi, dza, loss_parts, temperature=0.07, gm=ops.GEM
         ops.axpy(dna, cA)
         ops.axpy(dni, cI)
     else:
-        ops.axpy(dna, dist.scatter_rows_grad(cA.view(C, P), group).reshape(-1))
-        ops.axpy(dni, dist.scatter_rows_grad(cI.view(C, P), group).reshape(-1))
+        rA, rI = ws.get("nce.rA", B * P), ws.get("nce.rI", B * P)
+        host_point(lambda: (dist.scatter_rows_grad(cA.view(C, P), group, out=rA.view(B, P)),
+                            dist.scatter_rows_grad(cI.view(C, P), group, out=rI.view(B, P))))
+        ops.axpy(dna, rA)
+        ops.axpy(dni, rI)
     ni.backward(dni, dzi)
     na.backward(dna, dza)
     return 0.5 / B
@@ -81,10 +91,11 @@ def nt_xent(ws, reps, B, P, dreps, loss_parts, temperature=0.07, gm=ops.GEMM_F32
     nv = n.y.view(2 * B, P)
     if W == 1:
         n_all = n.y
-    else:   # global layout [z1 of every rank; z2 of every rank]
+    else:   # global layout [z1 of every rank; z2 of every rank]; host point as in infonce
         n_all = ws.get("ntx.all", 2 * W * B * P)
-        n_all.view(2, W * B, P)[0].copy_(dist.gather_rows(nv[:B], group))
-        n_all.view(2, W * B, P)[1].copy_(dist.gather_rows(nv[B:], group))
+        av = n_all.view(2, W * B, P)
+        host_point(lambda: (dist.gather_rows(nv[:B], group, out=av[0]),
+                            dist.gather_rows(nv[B:], group, out=av[1])))
     C = 2 * W * B
     S = ws.get("ntx.S", 2 * B * C)
     ops.gemm(2 * B, C, P, n.y, P, 1, n_all, 1, P, S, C, alpha=inv_t, mode=gm)
@@ -103,7 +114,10 @@ def nt_xent(ws, reps, B, P, dreps, loss_parts, temperature=0.07, gm=ops.GEMM_F32
         ops.axpy(dn, col)
     else:
         cv = col.view(2, W * B, P)
-        ops.axpy(dn[:B * P], dist.scatter_rows_grad(cv[0], group).reshape(-1))
-        ops.axpy(dn[B * P:], dist.scatter_rows_grad(cv[1], group).reshape(-1))
+        rc = ws.get("ntx.rc", 2 * B * P)
+        rv = rc.view(2, B, P)
+        host_point(lambda: (dist.scatter_rows_grad(cv[0], group, out=rv[0]),
+                            dist.scatter_rows_grad(cv[1], group, out=rv[1])))
+        ops.axpy(dn, rc)
     n.backward(dn, dreps)
     return g

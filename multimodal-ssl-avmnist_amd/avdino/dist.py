@@ -2,10 +2,11 @@
 ``torch.distributed`` with backend ``nccl`` (= RCCL over xGMI) on MI355X, ``gloo`` in the CPU
 tests.  Nothing here computes model math; it moves the engine's flat arenas.
 
-* :func:`grad_allreduce_hook` -- the per-step gradient exchange: ONE all-reduce over the flat
-  live-gradient arena (2.12 M f32 = 8.5 MB for mse/infonce; the reference's DDP buckets the
-  same parameters, dead fc1/fc2 excluded because they have no gradient), then x 1/world
-  (DDP's gradient averaging).
+* :class:`GradAllReduce` -- the per-step gradient exchange over the flat live-gradient arena
+  (2.12 M f32 = 8.5 MB for mse/infonce; the reference's DDP buckets the same parameters, dead
+  fc1/fc2 excluded because they have no gradient), then x 1/world (DDP's gradient
+  averaging): the ranges the backward finishes first (heads, fusion, projection) go out as
+  an early bucket from inside the captured step, the conv branches after it.
 * :func:`broadcast_buffers` -- DDP ``broadcast_buffers=True`` semantics of the reference's
   Lightning DDP run: at the start of every forward rank 0's buffers (``center``, BN running
   stats, ``num_batches_tracked``) overwrite the other ranks' copies, so all ranks train from
@@ -28,14 +29,88 @@ def rank(group=None):
     return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
 
 
-def grad_allreduce_hook(group=None):
-    """fn(grad_arena) for MultiCentralEngine(grad_hook=...): all-reduce SUM then average."""
-    def hook(grad):
-        n = dist.get_world_size(group)
+class GradAllReduce:
+    """DDP's gradient averaging over the flat gradient arena, in buckets.
+
+    ``bucket(grad, ranges)`` all-reduces those ranges as soon as the step has produced them
+    (an engine calls it at a host point inside its captured step, avdino.capture): with RCCL
+    the collective runs on the process group's stream while the rest of the backward keeps
+    the compute stream busy.  ``hook(grad)`` -- after the step -- all-reduces whatever no
+    bucket covered (within ``ranges``, default the whole arena), waits for every bucket and
+    scales the reduced ranges by 1/world.  Every rank issues the same buckets in the same
+    order (same ranges, same step structure).  With no bucket it is one all-reduce over the
+    arena (the round-1/2 behaviour)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.pending, self.covered = [], []
+
+    def world(self):
+        return dist.get_world_size(self.group)
+
+    def bucket(self, grad, ranges):
+        if self.world() == 1:
+            return
+        # RCCL: asynchronous on the process group's stream.  gloo (the 1-GPU rehearsal)
+        # completes it here: its CUDA all-reduce stages through host memory on a worker thread,
+        # and left in flight under the next replayed graph segment it stalled each step ~20x
+        # (measured 167-215 ms vs 9-11 ms per 2-rank step)
+        overlap = dist.get_backend(self.group) == "nccl"
+        for lo, hi in ranges:
+            if hi > lo:
+                w = dist.all_reduce(grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
+                                    async_op=overlap)
+                if overlap:
+                    self.pending.append(w)
+                self.covered.append((lo, hi))
+
+    def __call__(self, grad, ranges=None):
+        n = self.world()
         if n > 1:
-            dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
-            grad.mul_(1.0 / n)
-    return hook
+            want = [(0, grad.numel())] if ranges is None else list(ranges)
+            rest = subtract_ranges(want, self.covered)
+            for lo, hi in rest:
+                self.pending.append(dist.all_reduce(grad[lo:hi], op=dist.ReduceOp.SUM,
+                                                    group=self.group, async_op=True))
+            for w in self.pending:
+                w.wait()
+            for lo, hi in merge_ranges(self.covered + rest):
+                grad[lo:hi].mul_(1.0 / n)
+        self.pending, self.covered = [], []
+
+
+def merge_ranges(ranges):
+    out = []
+    for lo, hi in sorted(r for r in ranges if r[1] > r[0]):
+        if out and lo <= out[-1][1]:
+            out[-1] = (out[-1][0], max(out[-1][1], hi))
+        else:
+            out.append((lo, hi))
+    return out
+
+
+def subtract_ranges(want, cut):
+    """Parts of the ranges ``want`` not covered by ``cut`` (both lists of [lo, hi))."""
+    cut = merge_ranges(cut)
+    out = []
+    for lo, hi in merge_ranges(want):
+        for clo, chi in cut:
+            if chi <= lo or clo >= hi:
+                continue
+            if clo > lo:
+                out.append((lo, clo))
+            lo = max(lo, chi)
+            if lo >= hi:
+                break
+        if lo < hi:
+            out.append((lo, hi))
+    return out
+
+
+def grad_allreduce_hook(group=None):
+    """fn(grad_arena) for the engines' ``grad_hook``: all-reduce SUM then average, with
+    optional early buckets (:class:`GradAllReduce`)."""
+    return GradAllReduce(group)
 
 
 def broadcast_buffers(store, src=0, group=None):
@@ -55,13 +130,18 @@ def broadcast_parameters(store, src=0, group=None):
             dist.broadcast(store.teacher, src=src, group=group)
 
 
-def gather_rows(x, group=None):
+def gather_rows(x, group=None, out=None):
     """[B, F] local rows -> [world*B, F] global rows in rank order (rank r owns rows
-    r*B:(r+1)*B).  Every rank must pass the same B."""
+    r*B:(r+1)*B).  Every rank must pass the same B.  ``out``: a fixed destination (what a
+    captured step's next segment reads, avdino.capture)."""
     n = dist.get_world_size(group)
     if n == 1:
+        if out is not None:
+            out.copy_(x)
+            return out
         return x
-    out = torch.empty((n * x.shape[0],) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
+    if out is None:
+        out = torch.empty((n * x.shape[0],) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
     if x.device.type == "cuda" and dist.get_backend(group) == "nccl":
         dist.all_gather_into_tensor(out, x.contiguous(), group=group)
     elif x.device.type == "cuda":   # gloo (the 1-GPU rehearsal): stage through host memory
@@ -73,19 +153,24 @@ def gather_rows(x, group=None):
     return out
 
 
-def scatter_rows_grad(dx_all, group=None):
+def scatter_rows_grad(dx_all, group=None, out=None):
     """d loss / d(global rows) [world*B, F] from this rank -> SUM over ranks of each rank's
-    contribution to MY rows [B, F] (the adjoint of :func:`gather_rows`)."""
+    contribution to MY rows [B, F] (the adjoint of :func:`gather_rows`); ``out`` as there."""
     n = dist.get_world_size(group)
     if n == 1:
+        if out is not None:
+            out.copy_(dx_all)
+            return out
         return dx_all
     B = dx_all.shape[0] // n
-    if dx_all.device.type == "cuda" and dist.get_backend(group) == "nccl":
+    if out is None:
         out = torch.empty((B,) + tuple(dx_all.shape[1:]), device=dx_all.device, dtype=dx_all.dtype)
+    if dx_all.device.type == "cuda" and dist.get_backend(group) == "nccl":
         dist.reduce_scatter_tensor(out, dx_all.contiguous(), op=dist.ReduceOp.SUM, group=group)
         return out
     # gloo has no reduce_scatter: all-reduce then keep my slice (same result, test backend)
     t = dx_all.detach().cpu().contiguous().clone()
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     r = dist.get_rank(group)
-    return t[r * B:(r + 1) * B].to(dx_all.device)
+    out.copy_(t[r * B:(r + 1) * B])
+    return out

@@ -24,9 +24,13 @@ import os
 import torch
 
 from . import contrastive, ops
+from .capture import GraphedStep, host_point  # noqa: F401  (GraphedStep re-exported)
 from .spec import HEAD_NAMES, MULTI_ENCODERS, PROJ_HIDDEN, UNI_ALIASES, UNI_ENCODERS
 
 F32 = torch.float32
+# early gradient buckets at a host point inside the step (AVDINO_GRAD_BUCKETS=0: one all-reduce
+# after the step)
+BUCKETS = os.environ.get("AVDINO_GRAD_BUCKETS", "1") == "1"
 
 
 class Workspace:
@@ -574,46 +578,6 @@ def adam_step_dev(store, hp, sstate, lo=0, n=None):
                  store.adam_v[lo:lo + n], n, sstate.hyp, b1, b2, hp.eps, hp.wd)
 
 
-class GraphedStep:
-    """A training step's device work captured once per input shape as a hipGraph
-    (torch.cuda.CUDAGraph over HIP stream capture, side streams joined by events) and replayed:
-    one host call per step instead of ~230 launches.  The first ``warmup`` calls per shape run
-    eagerly (they size every workspace), the next one captures.
-
-    A graph holds the device pointers of the scratch buffers it was captured over; when any of
-    them is reallocated later (a larger key's eager warm-up grows a shared buffer, e.g. SimCLR's
-    image/image mode captured before its audio/audio mode was first seen) the graph is stale:
-    each graph records the allocation epoch after its capture and is dropped and re-captured
-    instead of replayed once the epoch has moved."""
-
-    def __init__(self, warmup=2):
-        self.warmup = warmup
-        self.graphs = {}     # key -> (graph, allocation epoch after its capture)
-        self.seen = {}
-        self.captures = 0
-
-    def run(self, key, body):
-        ent = self.graphs.get(key)
-        if ent is not None:
-            if ent[1] == ops.alloc_epoch():
-                ent[0].replay()
-                return
-            del self.graphs[key]            # captured over buffers that have since moved
-            self.seen[key] = self.warmup - 1
-        n = self.seen.get(key, 0)
-        if n < self.warmup:
-            self.seen[key] = n + 1
-            body()
-            return
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode="relaxed"):
-            body()
-        self.graphs[key] = (g, ops.alloc_epoch())
-        self.captures += 1
-        g.replay()          # the capture itself executed nothing
-
-
 def adam_step(store, hp):
     """torch.optim.Adam over the live arena (params with grad=None are outside it)."""
     store.adam_step += 1
@@ -694,6 +658,7 @@ class MultiCentralEngine:
         self.pipeline = False
         self.tside = None
         self._t_ready = None       # (batch, B, G) of the teacher output waiting in t_proj
+        self.tin_pending = None    # the next batch's teacher inputs while its forward is queued
         self._tseed = None
 
     # student image branch on the side stream, concurrently with the audio branch: measured
@@ -908,6 +873,10 @@ class MultiCentralEngine:
 
             f_after = None
             if self.mode == "infonce":
+                if self._global_negatives():
+                    # its all-gather is a host point: no forked stream may be in flight there
+                    self._join(t_done)
+                    t_done = None
                 head_out, hctx = heads()
             elif self.FHEADS_LATE and self.side is not None:
                 # queued (captured) after the fusion / projection below, depending only on
@@ -1040,6 +1009,11 @@ class MultiCentralEngine:
         ops.mark("bwd.main_heads")
         self._join(h_done)
         ops.mark("bwd.heads_joined")
+        # every stream is joined here and the heads / fusion / projection gradients are final:
+        # their all-reduce goes out now (a host point), overlapping the conv-branch backward
+        if self._bucketed():
+            g = self.store.grad
+            host_point(lambda: self.grad_hook.bucket(g, self._early_ranges))
         fi, cimg, fa, caud = c["senc"]
 
         def image_branch():      # independent of the audio branch: side stream
@@ -1063,10 +1037,28 @@ class MultiCentralEngine:
         ops.mark("aud.bwd.end")
         self._join(i_done)
 
-    def _graphable(self):
-        # InfoNCE's global negatives put collectives inside the forward: eager there
+    def _global_negatives(self):
         from . import dist as avdist
-        return not (self.mode == "infonce" and self.negatives != "local" and avdist.world(self.group) > 1)
+        return self.negatives != "local" and avdist.world(self.group) > 1
+
+    def _bucketed(self):
+        """Early gradient bucket: a bucket-capable hook, world > 1, and no pipelined teacher
+        forward in flight on its own stream at the bucket's host point."""
+        from . import dist as avdist
+        return (hasattr(self.grad_hook, "bucket") and self.tin_pending is None and BUCKETS
+                and avdist.world(getattr(self.grad_hook, "group", None)) > 1)
+
+    @property
+    def _early_ranges(self):
+        """Gradient-arena ranges final once the heads / fusion / projection backward is done:
+        every live parameter outside the two conv branches (whose Linear to E included)."""
+        st = self.store
+        br = ("student." + self.img_lin.split(".")[0] + ".", "student." + self.aud_lin.split(".")[0] + ".")
+        from .dist import merge_ranges
+        from .params import ALIGN
+        live = set(st.live_keys)
+        return merge_ranges([(o, o + -(-n // ALIGN) * ALIGN) for k, (o, n) in st.s_offs.items()
+                             if k in live and not k.startswith(br)])
 
     def step(self, batch, next_batch=None):
         """One full training step; returns the loss as a device tensor (no host sync).
@@ -1106,10 +1098,12 @@ class MultiCentralEngine:
             ops.mark("end")
 
         self._t_ready = (next_batch,) + tin[2:4] if tin is not None else None
-        if self.use_graph and self._graphable():
+        self.tin_pending = tin
+        if self.use_graph:
             self.graph.run(staged[2:5] + (ready, tin is not None), body)
         else:
             body()
+        self.tin_pending = None
         if self.grad_hook is not None:
             self.grad_hook(self.store.grad)
             adam_step_dev(self.store, self.hp, self.sstate)
@@ -1434,11 +1428,18 @@ class SimCLREngine:
         ws, st, c = self.ws, self.store, self.last
         P, D = self.P, self.D
         dr = c["dreps"] if dreps is None else dreps.reshape(-1)
-        for t, r0, n, ectx, hctx in c["calls"]:
+        calls = c["calls"]
+        for i, (t, r0, n, ectx, hctx) in enumerate(calls):
             enc, head = self.towers[t]
             demb = ws.get("demb", n * D)
             head.backward(ws, st, hctx, dr[r0 * P:(r0 + n) * P], demb)
             enc.backward(ws, st, ectx, demb)
+            if i + 1 < len(calls) and self._bucketed():
+                # this tower's gradients are final (one stream): all-reduce them now, under
+                # the other tower's backward
+                o, m = self.ranges[t]
+                g = st.grad
+                host_point(lambda g=g, o=o, m=m: self.grad_hook.bucket(g, [(o, o + m)]))
 
     def used_towers(self):
         return sorted({t for t, *_ in self.last["calls"]})
@@ -1455,9 +1456,10 @@ class SimCLREngine:
             ops.adam_dev(st.student[o:o + n], st.grad[o:o + n], st.adam_m[o:o + n], st.adam_v[o:o + n],
                          n, ss.hyp, b1, b2, self.hp.eps, 0.0)
 
-    def _graphable(self):
+    def _bucketed(self):
         from . import dist as avdist
-        return self.negatives == "local" or avdist.world(self.group) == 1
+        return (hasattr(self.grad_hook, "bucket") and BUCKETS
+                and avdist.world(getattr(self.grad_hook, "group", None)) > 1)
 
     def step(self, batch, mode=None):
         mode = self.draw_mode() if mode is None else int(mode)
@@ -1472,12 +1474,18 @@ class SimCLREngine:
             if self.grad_hook is None:
                 self.adam()
 
-        if self.use_graph and self._graphable():
+        if self.use_graph:
             self.graph.run((mode, B), body)
         else:
             body()
         if self.grad_hook is not None:
-            self.grad_hook(self.store.grad)
+            if hasattr(self.grad_hook, "bucket"):
+                # only the used towers' ranges: every rank draws the same mode sequence (same
+                # generator seed, as the reference's seed_everything), so the sizes agree
+                self.grad_hook(self.store.grad, ranges=[(o, o + n) for o, n in
+                                                        (self.ranges[t] for t in self.used_towers())])
+            else:
+                self.grad_hook(self.store.grad)
             self.adam()
         for t in self.used_towers():
             self.adam_t[t] += 1

@@ -88,7 +88,7 @@ def _timed(key, nbytes, flops, fn):
 
 # Scratch allocation epoch: bumped whenever a workspace / scratch buffer is (re)allocated.  A
 # captured hipGraph bakes in the device pointers it saw, so a graph captured in an earlier epoch
-# may address freed memory and must not be replayed (engine.GraphedStep checks this).
+# may address freed memory and must not be replayed (capture.GraphedStep checks this).
 _ALLOC_EPOCH = [0]
 
 

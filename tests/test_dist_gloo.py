@@ -78,6 +78,43 @@ def test_grad_allreduce_and_buffer_broadcast():
         assert np.all(buf == 1.0)                 # rank 0's buffers everywhere
 
 
+def _bucketed(r, world):
+    """GradAllReduce with early buckets (overlapping, unordered) + the remainder == flat."""
+    from avdino import dist as D
+    g = torch.Generator().manual_seed(300 + r)
+    grad = torch.randn(1000, generator=g)
+    flat = grad.clone()
+    D.GradAllReduce()(flat)
+    b = grad.clone()
+    h = D.GradAllReduce()
+    h.bucket(b, [(600, 800), (0, 128)])
+    h.bucket(b, [(128, 200)])
+    h(b)
+    sub = grad.clone()                # only some ranges (SimCLR's used towers)
+    h2 = D.GradAllReduce()
+    h2.bucket(sub, [(0, 100)])
+    h2(sub, ranges=[(0, 300), (500, 700)])
+    return flat.numpy(), b.numpy(), sub.numpy(), grad.numpy()
+
+
+def test_bucketed_allreduce_equals_flat():
+    from avdino.dist import merge_ranges, subtract_ranges
+    assert subtract_ranges([(0, 100)], [(10, 20), (50, 60)]) == [(0, 10), (20, 50), (60, 100)]
+    assert subtract_ranges([(0, 10), (20, 30)], [(5, 25)]) == [(0, 5), (25, 30)]
+    assert subtract_ranges([(0, 10)], [(0, 10)]) == []
+    assert merge_ranges([(5, 6), (0, 5), (7, 9)]) == [(0, 6), (7, 9)]
+    res = _run(_bucketed)
+    raw = [x[1][3] for x in res]
+    for _, (flat, b, sub, grad) in res:
+        np.testing.assert_array_equal(flat, b)
+        mean = (raw[0] + raw[1]) / 2
+        np.testing.assert_allclose(flat, mean, rtol=1e-6, atol=1e-7)
+        inside = np.zeros(1000, bool)
+        inside[0:300] = inside[500:700] = True
+        np.testing.assert_array_equal(sub[inside], flat[inside])
+        np.testing.assert_array_equal(sub[~inside], grad[~inside])   # untouched outside
+
+
 # ----------------------------------------------------------------- global negatives
 class _Gather(torch.autograd.Function):
     """gather_rows with its adjoint (scatter_rows_grad) as the backward."""

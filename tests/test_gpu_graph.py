@@ -1,4 +1,4 @@
-"""Graph-replayed training steps (engine.GraphedStep + StepState): a step captured once as a
+"""Graph-replayed training steps (capture.GraphedStep + StepState): a step captured once as a
 hipGraph and replayed must be the eager step, bit for bit, on every later step -- fresh dropout
 masks (the counter offset lives in device memory), the right Adam bias corrections (device step
 count), BN running statistics / counters, centre, teacher EMA -- for the three engines."""

@@ -115,7 +115,7 @@ def test_graph_staleness_rule():
             FakeGraph.replays += 1
 
     g = GraphedStep(warmup=1)
-    g.graphs["k"] = (FakeGraph(), ops.alloc_epoch())
+    g.graphs["k"] = ([FakeGraph()], ops.alloc_epoch())
     g.seen["k"] = 1
     calls = []
     g.run("k", lambda: calls.append(1))
@@ -124,3 +124,29 @@ def test_graph_staleness_rule():
     g.warmup = 2                        # (keep the re-run eager: no capture on CPU)
     g.run("k", lambda: calls.append(1))
     assert "k" not in g.graphs and calls == [1] and FakeGraph.replays == 1
+
+
+def test_segmented_replay_order():
+    """A captured step with host points replays as graph, collective, graph, ... in order;
+    outside a capture a host point just runs its collective."""
+    from avdino import ops
+    from avdino.capture import GraphedStep, capturing, host_point
+    order = []
+
+    class Seg:
+        def __init__(self, i):
+            self.i = i
+
+        def replay(self):
+            order.append(("g", self.i))
+
+    g = GraphedStep(warmup=1)
+    g.graphs["k"] = ([Seg(0), lambda: order.append(("c", 0)), Seg(1),
+                      lambda: order.append(("c", 1)), Seg(2)], ops.alloc_epoch())
+    g.run("k", lambda: order.append("eager"))
+    assert order == [("g", 0), ("c", 0), ("g", 1), ("c", 1), ("g", 2)]
+    assert g.segments("k") == 3 and g.segments("x") is None
+    assert not capturing()
+    hit = []
+    host_point(lambda: hit.append(1))
+    assert hit == [1]
