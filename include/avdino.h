@@ -429,11 +429,23 @@ int avd_augment_views_dt(const uint8_t* src_u8, const int64_t* idx, long long n_
                          const uint32_t* gm, int gm_words, int group, unsigned long long seed,
                          int order, void* out, int odt, void* stream);
 
+/* The same views for a chain in ANY stage order (transforms.Compose order; the reference's own
+ * configs/config_multimodal_dino.yaml best_augments chains, get_data.py:195-231, put the masks
+ * and noise before the time stretch and the crop): kinds is a HOST array [nkinds <= 9] of
+ * stage kinds in application order (the avd_augment_records numbering below); each applied
+ * stage reads the previous stage's whole view (held in LDS), as each transform module reads its
+ * predecessor's output.  A chain in the avd_augment_views order gives bit-identical views. */
+int avd_augment_views_seq(const uint8_t* src_u8, const int64_t* idx, long long n_src, int B,
+                          int V, int H, int W, const float* lut, const float* rec,
+                          const uint32_t* gm, int gm_words, int group, unsigned long long seed,
+                          int order, const int* kinds, int nkinds, void* out, int odt,
+                          void* stream);
+
 /* The records' random parameters drawn on the device (the get_params rules of each transform:
  * RandomResizedCrop / RandomErasing 10 attempts + fallback, RandomRotation / RandomAffine
  * inverse matrices, torchaudio mask_along_axis bands, time-stretch rate, noise std,
  * GroupedMasking's randperm(ng)[:k] as the k smallest of ng counter-hash keys).  stages is a
- * HOST array [nstages <= 8][8] of {kind, p, params...}:
+ * HOST array [nstages <= 9][8] of {kind, p, params...}:
  *   kind 0 crop {scale0, scale1, ratio0, ratio1}, 1 time stretch {min, max},
  *   2 frequency mask {param}, 3 time mask {param}, 4 rotation {degrees},
  *   5 affine {degrees, translate_x (< 0: none), translate_y, scale0 (<= 0: none), scale1},

@@ -88,6 +88,7 @@ PROTOS = {
     "avd_stage_views": [P, I, P, I, P, I, I, P, I, P],
     "avd_augment_views": [P, P, L, I, I, I, I, P, P, P, I, I, U64, I, P, P],
     "avd_augment_views_dt": [P, P, L, I, I, I, I, P, P, P, I, I, U64, I, P, I, P],
+    "avd_augment_views_seq": [P, P, L, I, I, I, I, P, P, P, I, I, U64, I, P, I, P, I, P],
     "avd_augment_records": [P, I, I, I, I, I, U64, P, P, I, P],
     "avd_row_sqnorm": [P, I, I, P, P],
     "avd_knn_select": [P, L, P, I, I, I, P, P, I, P, I, P, P, P],

@@ -81,12 +81,30 @@ def custom_audio_chain(augmentations, probabilities):
 
 
 def validate_chain(chain):
-    """The kernel applies stages in one fixed order; a chain must be a sub-sequence of it."""
-    last, seen = -1, set()
+    """Every stage a known transform, each at most once (a record has one parameter slot per
+    transform kind).  Any order: transforms.Compose order is kept (avd_augment_views_seq)."""
+    seen = set()
     for kind, _, _ in chain:
-        if kind not in KIND_ORDER or kind in seen or KIND_ORDER[kind] < last:
-            raise NotImplementedError(f"transform order not supported on device: {chain}")
-        last, seen = KIND_ORDER[kind], seen | {kind}
+        if kind not in KIND_ORDER or kind in seen:
+            raise NotImplementedError(f"transform chain not supported on device: {chain}")
+        seen.add(kind)
+
+
+def fixed_order(chain):
+    """True when the chain is a sub-sequence of the gather kernel's order (avd_augment_views:
+    crop -> time stretch -> masks -> rotation -> affine -> erasing -> noise -> groups), so the
+    one-pass gather kernel applies it; other orders run stage by stage (avd_augment_views_seq)."""
+    last = -1
+    for kind, _, _ in chain:
+        if KIND_ORDER[kind] < last:
+            return False
+        last = KIND_ORDER[kind]
+    return True
+
+
+def chain_kinds(chain):
+    """The chain's stage kinds in application order (avd_augment_records numbering)."""
+    return [_SK[kind] for kind, _, _ in chain]
 
 
 # ----------------------------------------------------------------------------- parameter draws
@@ -266,8 +284,10 @@ class ViewAugmenter:
     ``src_u8`` [N, H*W] uint8 on the device, ``lut`` [256] f32 (the dataset's normalisation).
     ``__call__(idx, chain, n_views)`` -> f32 [B, n_views, 1, H, W] on the device."""
 
-    def __init__(self, src_u8, lut, H, W, seed=0, device_params=True):
+    def __init__(self, src_u8, lut, H, W, seed=0, device_params=True, sequential=False):
         self.src, self.lut, self.H, self.W = src_u8, lut, H, W
+        # sequential=True: every chain through the stage-by-stage kernel (tests compare the two)
+        self.sequential = sequential
         self.rng = np.random.default_rng(seed)
         self.seed = seed
         self.calls = 0
@@ -313,9 +333,12 @@ class ViewAugmenter:
             rec, gm = self.records_dev(chain, idx.shape[0], n_views)
         else:
             rec, gm = self.records(chain, idx.shape[0], n_views)
-        return self.apply(idx, rec, gm, n_views, out, order)
+        kinds = chain_kinds(chain) if (self.sequential or not fixed_order(chain)) else None
+        return self.apply(idx, rec, gm, n_views, out, order, kinds)
 
-    def apply(self, idx, rec, gm, n_views, out=None, order=0):
+    def apply(self, idx, rec, gm, n_views, out=None, order=0, kinds=None):
+        """kinds: the stage kinds in application order for avd_augment_views_seq (None: the
+        fixed-order gather kernel)."""
         idx = np.asarray(idx, np.int64)
         if idx.size == 0 or idx.min() < 0 or idx.max() >= self.src.shape[0]:
             raise IndexError("sample id outside the dataset")
@@ -327,7 +350,10 @@ class ViewAugmenter:
         shape = (B, n_views, 1, self.H, self.W) if order == 0 else (n_views, B, 1, self.H, self.W)
         if out is None:
             out = torch.empty(shape, dtype=torch.float32, device=dev)
-        idx_d = torch.from_numpy(idx).to(dev)
+        # pinned + non-blocking: a data-stream prefetch must not block the host on that stream
+        idx_t = torch.from_numpy(idx)
+        idx_d = (idx_t.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda"
+                 else idx_t.to(dev))
         if on_dev:
             rec_d, gm_d = rec, gm
         else:
@@ -336,7 +362,7 @@ class ViewAugmenter:
         self.calls += 1
         seed = (self.seed * 0x9E3779B97F4A7C15 + self.calls) & (2**64 - 1)
         ops.augment_views(self.src, idx_d, self.lut, rec_d, gm_d, 4, seed, n_views, self.H,
-                          self.W, out, order)
+                          self.W, out, order, kinds)
         return out
 
     def identity(self, idx, out=None):

@@ -91,6 +91,10 @@ class GraphedStep:
                 return
             del self.graphs[key]            # captured over buffers that have since moved
             self.seen[key] = self.warmup - 1
+            if not self.graphs:
+                # the last graph on the shared memory pool is gone, and with it the pool: the
+                # next capture needs a new one (the allocator refuses a pool nobody holds)
+                self.pool = None
         n = self.seen.get(key, 0)
         if n < self.warmup:
             self.seen[key] = n + 1

@@ -121,7 +121,7 @@ class AVMNISTDinoLoader:
     def __init__(self, data_dir, batch_size=32, n_global_views=2, n_local_views=4,
                  type="burst_noise", augmentations=None, device="cuda", split="train",
                  train_size=55000, val_size=5000, seed=0, multimodal_mode="mse", shuffle=True,
-                 rank=0, world=1):
+                 rank=0, world=1, staged=False):
         self.paths = avmnist_paths(data_dir, type)
         for path in self.paths[split]:
             if not os.path.exists(path):
@@ -137,6 +137,9 @@ class AVMNISTDinoLoader:
             self.train_idx, self.val_idx = np.arange(n), np.arange(0)
         self.batch_size, self.shuffle, self.rank, self.world = batch_size, shuffle, rank, world
         self.mode = multimodal_mode
+        # staged=True: iterate staged_batch dicts (the multimodal engines build the views in
+        # place and can prefetch them under the previous step) instead of collated views
+        self.staged = staged
         self.aug = augmentations or MultiModalAugmentation(n_global_views, n_local_views)
         # augmentation streams differ per rank (each rank's worker RNGs do in the reference);
         # the shuffle order (seed) stays shared so the rank strides partition one permutation
@@ -176,6 +179,9 @@ class AVMNISTDinoLoader:
         return {"aug": self.aug, "idx": np.asarray(idx, np.int64), "label": lab}
 
     def __iter__(self):
+        if self.staged:
+            yield from self.iter_staged()
+            return
         order = self._order()
         self.epoch += 1
         for s in range(0, len(order), self.batch_size):

@@ -657,6 +657,12 @@ class MultiCentralEngine:
         # three streams), so off by default.
         self.pipeline = False
         self.tside = None
+        # real-data input prefetch (prefetch()): data stream, the staging buffer set in use (0/1),
+        # the pending prefetch (batch, set, done event, staged) and the "other set is free" event
+        self.dstream = None
+        self._par = 0
+        self._pf = None
+        self._ev_free = None
         self._t_ready = None       # (batch, B, G) of the teacher output waiting in t_proj
         self.tin_pending = None    # the next batch's teacher inputs while its forward is queued
         self._tseed = None
@@ -733,19 +739,67 @@ class MultiCentralEngine:
                        mode=self.gm)
         return out, (h, r)
 
+    # the next real-data batch's device augmentation queued on a data stream under the current
+    # step (prefetch); AVDINO_AUG_PREFETCH=0 stages every batch synchronously
+    PREFETCH = os.environ.get("AVDINO_AUG_PREFETCH", "1") == "1"
+
+    def _aug_bufs(self, batch, with_orig, par):
+        """Staged-input buffers of set ``par`` (0/1) for a {"aug", "idx"} batch:
+        (x_img, x_aud, B, G, L)."""
+        aug, idx = batch["aug"], batch["idx"]
+        B, G, L = len(idx), aug.n_global_views, aug.n_local_views
+        nv = G + L + (1 if with_orig else 0)
+        sfx = "" if par == 0 else ".1"
+        return (self.ws.get("in.img" + sfx, nv * B * 784, self.act),
+                self.ws.get("in.aud" + sfx, nv * B * 12544, self.act), B, G, L)
+
+    def prefetch(self, batch):
+        """Queue the augmentation of the NEXT step's real-data batch ({"aug", "idx", ...}) on the
+        data stream, into the staging buffers the current step does not read, so it runs under
+        the step just queued instead of in front of the next one.  The next stage() of that same
+        batch object waits for it and takes those buffers.  Returns False when not applicable
+        (synthetic views, no side streams, prefetch off)."""
+        if not self.PREFETCH or "aug" not in batch or self.side is None:
+            return False
+        if self._pf is not None:
+            raise RuntimeError("prefetch: the previously prefetched batch was never consumed")
+        par = 1 - self._par
+        if self.dstream is None:
+            self.dstream = torch.cuda.Stream(self.store.device)
+        # the other buffers were last read by the step before the current one: free once the
+        # main stream is past the event stage() recorded in front of the current step
+        free = self._ev_free
+        if free is not None:
+            self.dstream.wait_event(free)
+        else:
+            self.dstream.wait_stream(torch.cuda.current_stream(self.store.device))
+        with_orig = self.heads is not None
+        staged = self._aug_bufs(batch, with_orig, par)      # allocated outside the data stream
+        with torch.cuda.stream(self.dstream):
+            batch["aug"].stage(batch["idx"], staged[0], staged[1], with_orig)
+            done = torch.cuda.Event()
+            done.record(self.dstream)
+        self._pf = (batch, par, done, staged)
+        return True
+
     def stage(self, batch, with_orig):
         """Device batch dict -> view-major staged image/audio inputs (act dtype) and the labels,
         in fixed workspace buffers (what a captured step reads)."""
         ws = self.ws
-        if "aug" in batch:
+        main = torch.cuda.current_stream(self.store.device) if self.store.device.type == "cuda" else None
+        pf, self._pf = self._pf, None
+        if pf is not None and pf[0] is batch:
+            # prefetched under the previous step: wait for the data stream, use its buffers
+            main.wait_event(pf[2])
+            self._par = pf[1]
+            x_img, x_aud, B, G, L = pf[3]
+        elif "aug" in batch:
             # real-data path: the device augmentation writes the views straight into the staged
             # inputs ({"aug": MultiModalAugmentation, "idx": sample ids, "label": ...})
-            aug, idx = batch["aug"], batch["idx"]
-            B, G, L = len(idx), aug.n_global_views, aug.n_local_views
-            nv = G + L + (1 if with_orig else 0)
-            x_img = ws.get("in.img", nv * B * 784, self.act)
-            x_aud = ws.get("in.aud", nv * B * 12544, self.act)
-            aug.stage(idx, x_img, x_aud, with_orig)
+            if pf is not None:         # a prefetched batch that was not the next one: drop it
+                main.wait_event(pf[2])
+            x_img, x_aud, B, G, L = self._aug_bufs(batch, with_orig, self._par)
+            batch["aug"].stage(batch["idx"], x_img, x_aud, with_orig)
         else:
             g_img, l_img = batch["g_img"], batch["l_img"]
             B, G = g_img.shape[:2]
@@ -757,10 +811,16 @@ class MultiCentralEngine:
                             batch["image"].contiguous() if with_orig else None, B, 784, x_img)
             ops.stage_views(batch["g_aud"].contiguous(), G, batch["l_aud"].contiguous() if L else None, L,
                             batch["audio"].contiguous() if with_orig else None, B, 12544, x_aud)
+            self._par = 0
         labels = None
         if self.mode == "semi_supervised":
-            labels = ws.get("in.label", B, torch.int64)
+            labels = ws.get("in.label" + ("" if self._par == 0 else ".1"), B, torch.int64)
             labels.copy_(batch["label"].reshape(-1))
+        if main is not None:
+            # everything queued on the main stream after this point reads THIS buffer set: the
+            # other one is free for a prefetch once the main stream passes here
+            self._ev_free = torch.cuda.Event()
+            self._ev_free.record(main)
         return x_img, x_aud, B, G, L, labels
 
     def stage_teacher(self, batch):
@@ -1080,7 +1140,7 @@ class MultiCentralEngine:
                              "teacher forward already ran); set pipeline=False to change batches")
         ready = self._t_ready is not None
         tin = None
-        if self.pipeline and next_batch is not None and self.side is not None:
+        if self.pipeline and next_batch is not None and self.side is not None and "aug" not in next_batch:
             tin = self.stage_teacher(next_batch)
 
         def body():
@@ -1100,10 +1160,12 @@ class MultiCentralEngine:
         self._t_ready = (next_batch,) + tin[2:4] if tin is not None else None
         self.tin_pending = tin
         if self.use_graph:
-            self.graph.run(staged[2:5] + (ready, tin is not None), body)
+            self.graph.run(staged[2:5] + (ready, tin is not None, self._par), body)
         else:
             body()
         self.tin_pending = None
+        if next_batch is not None and "aug" in next_batch:
+            self.prefetch(next_batch)
         if self.grad_hook is not None:
             self.grad_hook(self.store.grad)
             adam_step_dev(self.store, self.hp, self.sstate)

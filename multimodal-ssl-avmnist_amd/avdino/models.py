@@ -710,6 +710,8 @@ class MultiModalDINOLightning(_LightningShaped):
 
     # ---------------------------------------------------------------- step
     def _batch_dict(self, batch):
+        if isinstance(batch, dict) and "aug" in batch:
+            return batch       # AVMNISTDinoLoader(staged=True): the engine augments into its inputs
         if self.model.mode == "default":
             d = self.model._views_dict(batch)
         else:
@@ -717,6 +719,15 @@ class MultiModalDINOLightning(_LightningShaped):
             d = self.model._views_dict(views)
             d.update(image=image, audio=audio, label=labels)
         return {k: v.to(self.model.device, non_blocking=True) for k, v in d.items()}
+
+    def prefetch(self, batch):
+        """Trainer hook (after the optimizer step of the current batch): queue the NEXT batch's
+        device augmentation under the step just issued (MultiCentralEngine.prefetch); only for
+        staged real-data batches, a no-op otherwise."""
+        eng = getattr(self.model, "engine", None)
+        if isinstance(batch, dict) and "aug" in batch and hasattr(eng, "prefetch"):
+            return eng.prefetch(batch)
+        return False
 
     def training_step(self, batch, batch_idx):
         """Forward + losses (+ centre update) + teacher EMA before backward (dino.py:856-876,

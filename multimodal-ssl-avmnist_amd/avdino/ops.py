@@ -729,8 +729,9 @@ def stage_views(g, G, l, L, orig, B, HW, out):
 AUG_REC = 28  # floats per (sample, view) record, include/avdino.h AVD_AUG_REC
 
 
-def augment_views(src_u8, idx, lut, rec, gm, group, seed, V, H, W, out, order=0):
-    """Device view augmentation (avd_augment_views_dt): src_u8 [N, H*W] u8, idx [B] int64, lut
+def augment_views(src_u8, idx, lut, rec, gm, group, seed, V, H, W, out, order=0, kinds=None):
+    """Device view augmentation (avd_augment_views_dt; with ``kinds``, the chain's stage kinds in
+    application order, avd_augment_views_seq): src_u8 [N, H*W] u8, idx [B] int64, lut
     [256] f32, rec [B*V, AUG_REC] f32, gm [R, words] int32/uint32 or None, out f32 or bf16
     [B,V,H,W] (order 0) or [V,B,H,W] (order 1; a bf16 out may be a row range of the engine's
     staged view-major input).  Sample ids and bitmask rows are range-checked by the caller
@@ -743,12 +744,20 @@ def augment_views(src_u8, idx, lut, rec, gm, group, seed, V, H, W, out, order=0)
     for t in (src_u8, idx, lut, rec, out) + ((gm,) if gm is not None else ()):
         _need(t.is_contiguous() and t.device == out.device, "aug operands contiguous, one device")
     words = gm.shape[1] if gm is not None else 0
-    call("avd_augment_views_dt", p(src_u8), p(idx), src_u8.shape[0], B, V, H, W, p(lut), p(rec),
-         p(gm), words, group, seed & (2**64 - 1), order, p(out), dtcode(out), stream())
+    if kinds is None:
+        call("avd_augment_views_dt", p(src_u8), p(idx), src_u8.shape[0], B, V, H, W, p(lut), p(rec),
+             p(gm), words, group, seed & (2**64 - 1), order, p(out), dtcode(out), stream())
+        return
+    import numpy as _np
+    ks = _np.ascontiguousarray(kinds, _np.int32)
+    _need(ks.ndim == 1 and ks.shape[0] <= AUG_MAX_STAGES, "aug stage kinds")
+    call("avd_augment_views_seq", p(src_u8), p(idx), src_u8.shape[0], B, V, H, W, p(lut), p(rec),
+         p(gm), words, group, seed & (2**64 - 1), order, ks.ctypes.data, ks.shape[0], p(out),
+         dtcode(out), stream())
 
 
 AUG_STAGE_F = 8       # floats per chain stage of avd_augment_records
-AUG_MAX_STAGES = 8
+AUG_MAX_STAGES = 9
 
 
 def augment_records(stages, n, H, W, group, seed, rec, gm):

@@ -294,7 +294,8 @@ def main(argv=None):
         loader = AVMNISTDinoLoader(config["data"]["data_dir"], B, G, L,
                                    h.get("data_augmentation", "burst_noise"), aug, dev,
                                    seed=config["experiment"]["seed"], multimodal_mode=mode,
-                                   rank=rank, world=world)
+                                   rank=rank, world=world,
+                                   staged=hasattr(model, "prefetch") and mode is not None)
         lab = dict(data_dir=config["data"]["data_dir"], batch_size=128, device=dev,
                    type=h.get("data_augmentation", "burst_noise"), seed=config["experiment"]["seed"])
         traindata = AVMNISTLabelledLoader(split="train", **lab)

@@ -300,9 +300,13 @@ class Trainer:
             self._hook("on_train_epoch_start", model)
             n = self.limit_train_batches
             losses, first_step = [], self.global_step
-            for i, batch in enumerate(loader):
-                if n is not None and i >= n:
-                    break
+            # one batch of look-ahead: after a step is issued the module may queue the next
+            # batch's input work under it (model.prefetch: the device augmentation)
+            prefetch = getattr(model, "prefetch", None)
+            it = iter(loader)
+            batch, i = next(it, None), 0
+            while batch is not None and (n is None or i < n):
+                nxt = next(it, None) if (n is None or i + 1 < n) else None
                 out = {}
                 self._hook("on_train_batch_start", model, batch, i)
 
@@ -314,9 +318,12 @@ class Trainer:
                     return loss
 
                 opt.step(closure)
+                if nxt is not None and prefetch is not None:
+                    prefetch(nxt)
                 losses.append(out["loss"].detach().reshape(1))
                 self._hook("on_train_batch_end", model, out, batch, i)
                 self.global_step += 1
+                batch, i = nxt, i + 1
             self._epoch_metrics(model, losses, dev)
             for cb in self.callbacks:
                 if not getattr(cb, "monitoring", False):

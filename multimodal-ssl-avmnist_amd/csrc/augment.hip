@@ -172,14 +172,172 @@ __global__ __launch_bounds__(kThreads) void augment_kernel(
   }
 }
 
+enum { SK_CROP = 0, SK_TWARP, SK_FMASK, SK_TMASK, SK_ROT, SK_AFF, SK_ERASE, SK_NOISE, SK_GMASK };
+constexpr int kMaxStages = 9, kStageF = 8, kMaxGroups = 1024;
+
+// ----------------------------------------------------------------------------- any stage order
+// transforms.Compose applies a chain in its own order, and the reference's own config
+// (configs/config_multimodal_dino.yaml best_augments -> MultiModalAugmentation(augment_values=...),
+// get_data.py:195-231) orders its audio chains by YAML key: frequency mask, noise, time mask,
+// time stretch, crop, affine -- not the fixed order the gather kernel above walks backwards.
+// This kernel runs the chain forwards, one stage at a time, over the view held in LDS (f32):
+// each applied stage reads the previous stage's whole image, exactly as each torchvision /
+// torchaudio module reads its predecessor's output.  A thread owns pixels tid + k*256; the
+// resampling stages (crop, time stretch, rotation, affine) gather into registers, then a
+// barrier, then overwrite the image; the value stages (masks, erasing, noise, groups) update
+// their own pixels in place.  Same per-pixel formulas as the gather kernel, so a chain in the
+// fixed order gives bit-identical views either way.
+struct Prog { int kind[kMaxStages]; int n; };
+
+template <typename TO, int NPT>
+__global__ __launch_bounds__(kThreads) void augment_seq_kernel(
+    const uint8_t* __restrict__ src, const int64_t* __restrict__ idx, int V, int B, int H, int W,
+    const float* __restrict__ lut, const float* __restrict__ recs, const uint32_t* __restrict__ gm,
+    int gm_words, int group, unsigned long long seed, int order, Prog prog, TO* __restrict__ out) {
+#pragma clang fp contract(off)
+  __shared__ float s_img[kMaxHW];
+  __shared__ float s_lut[256];
+  const int rid = blockIdx.x;  // record = b * V + v
+  const int b = rid / V, v = rid - b * V;
+  const int HW = H * W;
+  const float* rec = recs + (size_t)rid * AVD_AUG_REC;
+
+  s_lut[threadIdx.x] = lut[threadIdx.x];
+  __syncthreads();
+  const uint32_t* row = reinterpret_cast<const uint32_t*>(src + (size_t)idx[b] * HW);
+  for (int i = threadIdx.x; i < HW / 4; i += kThreads) {
+    const uint32_t w4 = row[i];
+    s_img[4 * i + 0] = s_lut[w4 & 0xFF];
+    s_img[4 * i + 1] = s_lut[(w4 >> 8) & 0xFF];
+    s_img[4 * i + 2] = s_lut[(w4 >> 16) & 0xFF];
+    s_img[4 * i + 3] = s_lut[w4 >> 24];
+  }
+  __syncthreads();
+
+  const int flags = (int)rec[AVD_AUG_FLAGS];
+  View vw;               // the crop reads the current image
+  vw.img = s_img;
+  vw.H = H;
+  vw.W = W;
+  vw.crop = true;
+  vw.top = (int)rec[AVD_AUG_CROP + 0];
+  vw.left = (int)rec[AVD_AUG_CROP + 1];
+  vw.ch = (int)rec[AVD_AUG_CROP + 2];
+  vw.cw = (int)rec[AVD_AUG_CROP + 3];
+  vw.sh = (float)vw.ch / (float)H;
+  vw.sw = (float)vw.cw / (float)W;
+  const float cx = (float)(W - 1) * 0.5f, cy = (float)(H - 1) * 0.5f;
+  float acc[NPT];
+
+  for (int s = 0; s < prog.n; ++s) {
+    const int kind = prog.kind[s];
+    bool gather = false;
+    if (kind == SK_CROP) {
+      if (!(flags & 1)) continue;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const int p = threadIdx.x + k * kThreads;
+        if (p < HW) {
+          const int y = p / W;
+          acc[k] = crop_sample(vw, y, p - y * W);
+        }
+      }
+      gather = true;
+    } else if (kind == SK_TWARP) {
+      if (!(flags & 8)) continue;
+      const float rate = rec[AVD_AUG_RATE];
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const int p = threadIdx.x + k * kThreads;
+        if (p < HW) {
+          const int y = p / W, x = p - y * W;
+          const float t = (float)x * rate;
+          float val = 0.0f;
+          if (t < (float)W) {
+            const int i0 = (int)t;
+            const float a = t - (float)i0;
+            const float s0 = fabsf(s_img[y * W + i0]);
+            const float s1 = i0 + 1 < W ? fabsf(s_img[y * W + i0 + 1]) : 0.0f;
+            val = a * s1 + (1.0f - a) * s0;
+          }
+          acc[k] = val;
+        }
+      }
+      gather = true;
+    } else if (kind == SK_ROT || kind == SK_AFF) {
+      if (!(flags & (kind == SK_ROT ? 4 : 2))) continue;
+      float m[6];
+      const int o = kind == SK_ROT ? AVD_AUG_ROT : AVD_AUG_AFF;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) m[j] = rec[o + j];
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const int p = threadIdx.x + k * kThreads;
+        if (p < HW) {
+          int qy = p / W, qx = p - qy * W;
+          acc[k] = affine_nearest(m, cx, cy, W, H, qx, qy) ? s_img[qy * W + qx] : 0.0f;
+        }
+      }
+      gather = true;
+    } else if (kind == SK_FMASK || kind == SK_TMASK) {
+      const int o = kind == SK_FMASK ? AVD_AUG_FMASK : AVD_AUG_TMASK;
+      const int a0 = (int)rec[o], a1 = (int)rec[o + 1];
+      if (a1 <= a0) continue;
+      for (int p = threadIdx.x; p < HW; p += kThreads) {
+        const int y = p / W, c = kind == SK_FMASK ? y : p - y * W;
+        if (c >= a0 && c < a1) s_img[p] = 0.0f;
+      }
+    } else if (kind == SK_ERASE) {
+      const int et = (int)rec[AVD_AUG_ERASE], el = (int)rec[AVD_AUG_ERASE + 1];
+      const int eh = (int)rec[AVD_AUG_ERASE + 2], ew = (int)rec[AVD_AUG_ERASE + 3];
+      if (eh <= 0) continue;
+      for (int p = threadIdx.x; p < HW; p += kThreads) {
+        const int y = p / W, x = p - y * W;
+        if (y >= et && y < et + eh && x >= el && x < el + ew) s_img[p] = 0.0f;
+      }
+    } else if (kind == SK_NOISE) {
+      const float nstd = rec[AVD_AUG_NOISE];
+      if (nstd == 0.0f) continue;
+      for (int p = threadIdx.x; p < HW; p += kThreads)
+        s_img[p] = s_img[p] + gauss(seed, (unsigned)rid, (unsigned)p) * nstd;
+    } else if (kind == SK_GMASK) {
+      const int gmrow = (int)rec[AVD_AUG_GM];
+      if (!gm || gmrow < 0) continue;
+      const uint32_t* gmr = gm + (size_t)gmrow * gm_words;
+      const int gw = W / group;
+      for (int p = threadIdx.x; p < HW; p += kThreads) {
+        const int y = p / W, x = p - y * W;
+        const int g = (y / group) * gw + x / group;
+        if ((gmr[g >> 5] >> (g & 31)) & 1u) s_img[p] = s_img[p] * 0.0f;
+      }
+    } else {
+      continue;
+    }
+    __syncthreads();      // every read of the previous image (gathers) / every update is done
+    if (gather) {
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const int p = threadIdx.x + k * kThreads;
+        if (p < HW) s_img[p] = acc[k];
+      }
+      __syncthreads();
+    }
+  }
+  TO* o = out + (order == 0 ? (size_t)rid : (size_t)v * B + b) * HW;
+  for (int p = threadIdx.x; p < HW; p += kThreads) {
+    if constexpr (sizeof(TO) == 4)
+      o[p] = s_img[p];
+    else
+      o[p] = f2bf(s_img[p]);
+  }
+}
+
 // ----------------------------------------------------------------------------- parameter draws
 // The chain's random parameters drawn on the device (what ViewAugmenter.records draws with
 // numpy): one block per (sample, view) record; thread 0 walks the stages in order with a
 // counter-hash uniform stream (seed, record, draw index); the grouped mask picks exactly k of
 // the ng groups as the k smallest of ng hashed keys (block-wide bitonic sort in LDS), i.e. a
 // uniformly random k-subset like randperm(ng)[:k].
-enum { SK_CROP = 0, SK_TWARP, SK_FMASK, SK_TMASK, SK_ROT, SK_AFF, SK_ERASE, SK_NOISE, SK_GMASK };
-constexpr int kMaxStages = 8, kStageF = 8, kMaxGroups = 1024;
 struct Chain { float st[kMaxStages * kStageF]; int n; };
 
 struct Urng {
@@ -365,6 +523,45 @@ extern "C" int avd_augment_views_dt(const uint8_t* src_u8, const int64_t* idx, l
   augment_kernel<bf16><<<B * V, kThreads, 0, avd_stream(stream)>>>(src_u8, idx, V, B, H, W, lut, rec, gm,
                                                                    gm_words, group, seed, order,
                                                                    (bf16*)out);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+extern "C" int avd_augment_views_seq(const uint8_t* src_u8, const int64_t* idx, long long n_src,
+                                     int B, int V, int H, int W, const float* lut, const float* rec,
+                                     const uint32_t* gm, int gm_words, int group,
+                                     unsigned long long seed, int order, const int* kinds,
+                                     int nkinds, void* out, int odt, void* stream) {
+  if (!src_u8 || !idx || !lut || !rec || !out || (nkinds > 0 && !kinds)) return AVD_ERR_ARG;
+  if (B <= 0 || V <= 0 || H <= 0 || W <= 0 || n_src <= 0) return AVD_ERR_SHAPE;
+  if ((long long)H * W > kMaxHW || (H * W) % 4 || order < 0 || order > 1) return AVD_ERR_SHAPE;
+  if (nkinds < 0 || nkinds > kMaxStages) return AVD_ERR_SHAPE;
+  Prog prog{};
+  prog.n = nkinds;
+  bool has_gm = false;
+  for (int i = 0; i < nkinds; ++i) {
+    if (kinds[i] < SK_CROP || kinds[i] > SK_GMASK) return AVD_ERR_ARG;
+    prog.kind[i] = kinds[i];
+    has_gm |= kinds[i] == SK_GMASK;
+  }
+  if (gm && has_gm && (group <= 0 || H % group || W % group ||
+                       gm_words * 32 < (H / group) * (W / group)))
+    return AVD_ERR_SHAPE;
+  if (odt != AVD_F32 && odt != AVD_BF16) return AVD_ERR_DTYPE;
+  const int npt = avd_cdiv(H * W, kThreads);
+  hipStream_t st = avd_stream(stream);
+#define AVD_SEQ_LAUNCH(TO, N)                                                                  \
+  augment_seq_kernel<TO, N><<<B * V, kThreads, 0, st>>>(src_u8, idx, V, B, H, W, lut, rec, gm,  \
+                                                        gm_words, group, seed, order, prog,     \
+                                                        (TO*)out)
+  if (npt <= 4) {
+    if (odt == AVD_F32) AVD_SEQ_LAUNCH(float, 4); else AVD_SEQ_LAUNCH(bf16, 4);
+  } else if (npt <= 16) {
+    if (odt == AVD_F32) AVD_SEQ_LAUNCH(float, 16); else AVD_SEQ_LAUNCH(bf16, 16);
+  } else {
+    if (odt == AVD_F32) AVD_SEQ_LAUNCH(float, 49); else AVD_SEQ_LAUNCH(bf16, 49);
+  }
+#undef AVD_SEQ_LAUNCH
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

@@ -115,11 +115,35 @@ enum { LAY_K = 0, LAY_R = 1, LAY_S = 2 };
 template <int ROWS>
 struct TileRegs { float v[ROWS / 8 > 16 ? ROWS / 8 : 16]; };   // ROWS*32 elements over 256 threads
 
-template <int ROWS, int LAY>
+template <int ROWS, int LAY, bool EX = false>
 __device__ __forceinline__ void load_tile(const float* __restrict__ X, long long sr, long long sk,
                                           int r0, int k0, int rows, int kend, TileRegs<ROWS>& t) {
   const int tid = threadIdx.x;
-  if constexpr (LAY == LAY_K) {
+  if constexpr (EX && LAY == LAY_K) {
+    // whole tiles (the caller checked): unconditional loads, so the wait for one register stage
+    // leaves the younger stages' loads in flight (no branch for the waitcnt pass to merge over)
+#pragma unroll
+    for (int i = 0; i < ROWS / 32; ++i) {
+      const int e4 = tid + 256 * i;
+      const int r = e4 >> 3, k = (e4 & 7) * 4;
+      const float4 v = *reinterpret_cast<const float4*>(X + (size_t)(r0 + r) * sr + k0 + k);
+      t.v[4 * i] = v.x; t.v[4 * i + 1] = v.y; t.v[4 * i + 2] = v.z; t.v[4 * i + 3] = v.w;
+    }
+  } else if constexpr (EX && LAY == LAY_R) {
+#pragma unroll
+    for (int i = 0; i < (ROWS + 127) / 128; ++i) {
+      const int b = tid + 256 * i;
+      const int kb = b / (ROWS / 4), r = (b % (ROWS / 4)) * 4;
+      if (ROWS >= 128 || b < 2 * ROWS) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const float4 v = *reinterpret_cast<const float4*>(X + (size_t)(k0 + 4 * kb + kk) * sk + r0 + r);
+          t.v[16 * i + kk] = v.x; t.v[16 * i + 4 + kk] = v.y;
+          t.v[16 * i + 8 + kk] = v.z; t.v[16 * i + 12 + kk] = v.w;
+        }
+      }
+    }
+  } else if constexpr (LAY == LAY_K) {
 #pragma unroll
     for (int i = 0; i < ROWS / 32; ++i) {
       const int e4 = tid + 256 * i;
@@ -231,7 +255,13 @@ __device__ __forceinline__ void store_tile(const TileRegs<ROWS>& t, long long sr
   }
 }
 
-template <int MODE, int BM, int BN, int LA, int LB>
+// register prefetch depth: deeper for the small tiles (the heads' latency-bound GEMMs), within
+// the VGPR budget of the large ones (128x256: 48 + 128 accumulator registers per stage set)
+template <int BM, int BN>
+struct Depth { static constexpr int P = BM * BN >= 128 * 256 ? 1 : (BM * BN >= 128 * 64 ? 2 : 4); };
+
+template <int MODE, int BM, int BN, int LA, int LB, bool EX = false,
+          int P = EX ? Depth<BM, BN>::P : 1>
 __global__ __launch_bounds__(256) void gemm_mfma_kernel(
     int M, int N, int K, int kchunk, const float* __restrict__ A, long long sam, long long sak,
     const float* __restrict__ B, long long sbk, long long sbn, float* __restrict__ C, long long ldc,
@@ -254,20 +284,33 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  TileRegs<BM> ta;
-  TileRegs<BN> tb;
+  // P register stages of k-tiles in flight: tile kt+P is loaded while tile kt is stored to LDS
+  // and multiplied (the loop is latency-bound otherwise: one HBM round trip per 32-deep k-tile)
+  TileRegs<BM> ta[P];
+  TileRegs<BN> tb[P];
   const int nk = (kend - kbeg + 31) / 32;
-  load_tile<BM, LA>(A, sam, sak, m0, kbeg, M, kend, ta);
-  load_tile<BN, LB>(B, sbn, sbk, n0, kbeg, N, kend, tb);   // B^T tile: rows = n
-  store_tile<MODE, BM, LA>(ta, sam, sak, As[0]);
-  store_tile<MODE, BN, LB>(tb, sbn, sbk, Bs[0]);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
+  // EX: every tile whole; loads past the last k-tile re-read the last one (clamped, never used)
+  auto kt_at = [&](int kt) { return kbeg + 32 * (EX ? min(kt, nk - 1) : kt); };
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+    if (EX || p < nk) {
+      load_tile<BM, LA, EX>(A, sam, sak, m0, kt_at(p), M, kend, ta[p]);
+      load_tile<BN, LB, EX>(B, sbn, sbk, n0, kt_at(p), N, kend, tb[p]);   // B^T tile: rows = n
+    }
+  for (int kt0 = 0; kt0 < nk; kt0 += P) {
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int kt = kt0 + p;
+    if (kt >= nk) break;
     const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      load_tile<BM, LA>(A, sam, sak, m0, kbeg + 32 * (kt + 1), M, kend, ta);
-      load_tile<BN, LB>(B, sbn, sbk, n0, kbeg + 32 * (kt + 1), N, kend, tb);
+    // buffer cur was last read by tile kt-2's MFMAs, which every wave finished before the
+    // barrier of tile kt-1
+    store_tile<MODE, BM, LA>(ta[p], sam, sak, As[cur]);
+    store_tile<MODE, BN, LB>(tb[p], sbn, sbk, Bs[cur]);
+    __syncthreads();
+    if (EX || kt + P < nk) {
+      load_tile<BM, LA, EX>(A, sam, sak, m0, kt_at(kt + P), M, kend, ta[p]);
+      load_tile<BN, LB, EX>(B, sbn, sbk, n0, kt_at(kt + P), N, kend, tb[p]);
     }
     const T* as = As[cur] + (BM / 2 * wm + r16) * LDK;
     const T* bs = Bs[cur] + (BN / 2 * wn + r16) * LDK;
@@ -297,11 +340,7 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
       }
     }
-    if (more) {
-      store_tile<MODE, BM, LA>(ta, sam, sak, As[cur ^ 1]);
-      store_tile<MODE, BN, LB>(tb, sbn, sbk, Bs[cur ^ 1]);
-    }
-    __syncthreads();
+  }
   }
   float* part = ws ? ws + (size_t)blockIdx.z * M * N : nullptr;
 #pragma unroll
@@ -396,10 +435,21 @@ void launch_gemm(const Plan& pl, int M, int N, int K, const float* A, long long 
                  const float* bias, float alpha, float beta, float* ws, hipStream_t st) {
   dim3 grid(avd_cdiv(N, pl.bn), avd_cdiv(M, pl.bm), pl.splits);
   float* w = pl.splits > 1 ? ws : nullptr;
+  // whole tiles in every dimension (vector layouts, 16-byte aligned strides): the deep
+  // register-prefetch variant (AVDINO_GEMM_EX=1)
+  // (measured no faster than the checked variant at the step's shapes, profiles/r3_gemm_ab.txt: off)
+  static const bool ex_on = getenv("AVDINO_GEMM_EX") && atoi(getenv("AVDINO_GEMM_EX")) != 0;
+  const bool ex = ex_on && LA != LAY_S && LB != LAY_S && M % pl.bm == 0 && N % pl.bn == 0 &&
+                  K % 32 == 0 && pl.kchunk % 32 == 0;
 #define AVD_G(BM_, BN_)                                                                        \
-  if (pl.bm == BM_ && pl.bn == BN_)                                                            \
-    gemm_mfma_kernel<MODE, BM_, BN_, LA, LB><<<grid, 256, 0, st>>>(                            \
-        M, N, K, pl.kchunk, A, sam, sak, B, sbk, sbn, C, ldc, bias, alpha, beta, w);
+  if (pl.bm == BM_ && pl.bn == BN_) {                                                          \
+    if (ex)                                                                                    \
+      gemm_mfma_kernel<MODE, BM_, BN_, LA, LB, true><<<grid, 256, 0, st>>>(                    \
+          M, N, K, pl.kchunk, A, sam, sak, B, sbk, sbn, C, ldc, bias, alpha, beta, w);         \
+    else                                                                                       \
+      gemm_mfma_kernel<MODE, BM_, BN_, LA, LB, false><<<grid, 256, 0, st>>>(                   \
+          M, N, K, pl.kchunk, A, sam, sak, B, sbk, sbn, C, ldc, bias, alpha, beta, w);         \
+  }
   AVD_G(128, 256) else AVD_G(128, 128) else AVD_G(128, 64) else AVD_G(64, 64)
 #undef AVD_G
   if (pl.splits > 1) {

@@ -9,11 +9,19 @@ vocoder| of a zero-phase spectrogram, get_data.py:29-58) -> Frequency/TimeMaskin
 180-182) -> RandomRotation (124/129) -> RandomAffine (nearest, 125/130/152/185) -> RandomErasing
 (131) -> GaussianNoise (21-27, 189) -> GroupedMasking (60-108, 157/191).
 
-Parity status: torchvision / torchaudio (the libraries these transforms come from in the
-reference) are not installed in this image and the reference ships no fixture of augmented
-views, so agreement with *their* pixel output is "parity unpinned"; this oracle pins the
-device kernel to the stated maths (bit-exact outside the noise term, whose log/cos may differ
-by a few ulp).
+augment_one_seq restates the same stages for a chain in ANY order (transforms.Compose: each
+stage reads its predecessor's whole output), which avd_augment_views_seq follows; for a chain in
+the fixed order both restatements agree bit for bit (tests/test_augment_data.py).
+
+Parity status: pinned to the reference's own code where that code is plain torch
+(tests/test_augment_golden.py, fixtures by tests/golden/gen_augment_golden.py): the chain
+structure MultiModalAugmentation builds (default and from the shipped config's best_augments),
+__call__'s view/chain control flow, and the pixels of GroupedMasking and GaussianNoise ->
+GroupedMasking given the reference's randperm / randn draws (bit-identical).  The stages that
+call torchvision / torchaudio kernels (RandomResizedCrop, RandomRotation, RandomAffine,
+RandomErasing, TimeStretch, Frequency/TimeMasking) stay "parity unpinned": those libraries are
+not installed here; this oracle restates their published algorithms and pins the device
+kernels to that maths (bit-exact outside the noise term, whose log/cos may differ by a few ulp).
 """
 import numpy as np
 
@@ -112,8 +120,60 @@ def augment_one(img, rec, gm, seed, rid, group=4):
     return val.astype(f32)
 
 
-def augment_views(src_u8, idx, lut, rec, gm, V, H, W, seed, order=0, group=4):
-    """All records: out [B, V, H, W] (order 0) or [V, B, H, W] (order 1)."""
+# stage kinds (avd_augment_records numbering, avdino/augment.py _SK)
+K_CROP, K_TWARP, K_FMASK, K_TMASK, K_ROT, K_AFF, K_ERASE, K_NOISE, K_GMASK = range(9)
+
+
+def augment_one_seq(img, rec, gm, seed, rid, kinds, group=4, noise=None):
+    """One view through a chain in ANY order, one transform at a time over the whole image --
+    transforms.Compose semantics (get_data.py:134-231: each module reads its predecessor's
+    output), the restatement avd_augment_views_seq follows.  ``noise`` [H, W] replaces the
+    counter-hash normals (tests inject the reference's own torch.randn_like draws)."""
+    H, W = img.shape
+    cur = img.astype(f32).copy()
+    y, x = np.meshgrid(np.arange(H), np.arange(W), indexing="ij")
+    flags = int(rec[23])
+    for k in kinds:
+        if k == K_CROP and flags & 1:
+            cur = _crop_sample(cur, rec, y, x).astype(f32)
+        elif k == K_TWARP and flags & 8:
+            # |phase_vocoder| of a zero-phase spectrogram (get_data.py:42-58)
+            t = x.astype(f32) * f32(rec[16])
+            inr = t < f32(W)
+            tt = np.where(inr, t, f32(0))
+            i0 = tt.astype(np.int64)
+            a = tt - i0.astype(f32)
+            s0 = np.abs(cur[y, i0])
+            s1 = np.where(i0 + 1 < W, np.abs(cur[y, np.minimum(i0 + 1, W - 1)]), f32(0))
+            cur = np.where(inr, a * s1 + (f32(1) - a) * s0, f32(0)).astype(f32)
+        elif k in (K_ROT, K_AFF) and flags & (4 if k == K_ROT else 2):
+            m = rec[10:16] if k == K_ROT else rec[4:10]
+            ok, qx, qy = _affine_nearest(m, x, y, H, W)
+            cur = np.where(ok, cur[qy, qx], f32(0)).astype(f32)
+        elif k == K_FMASK and rec[18] > rec[17]:
+            cur = np.where((y >= int(rec[17])) & (y < int(rec[18])), f32(0), cur)
+        elif k == K_TMASK and rec[20] > rec[19]:
+            cur = np.where((x >= int(rec[19])) & (x < int(rec[20])), f32(0), cur)
+        elif k == K_ERASE and rec[26] > 0:
+            et, el, eh, ew = (int(v) for v in rec[24:28])
+            cur = np.where((y >= et) & (y < et + eh) & (x >= el) & (x < el + ew), f32(0), cur)
+        elif k == K_NOISE and rec[21] != 0:
+            # GaussianNoise.forward: x + randn_like(x) * std (get_data.py:26-27)
+            g = (gauss(seed, rid, (y * W + x).reshape(-1)).reshape(H, W) if noise is None
+                 else np.asarray(noise, f32))
+            cur = (cur + g * f32(rec[21])).astype(f32)
+        elif k == K_GMASK and gm is not None and rec[22] >= 0:
+            # GroupedMasking.forward: spectrogram * mask over 4x4 groups (get_data.py:98-106)
+            row = int(rec[22])
+            gi = (y // group) * (W // group) + x // group
+            bit = (gm[row][gi >> 5].astype(np.uint32) >> (gi & 31).astype(np.uint32)) & 1
+            cur = np.where(bit == 1, cur * f32(0), cur)
+    return cur.astype(f32)
+
+
+def augment_views(src_u8, idx, lut, rec, gm, V, H, W, seed, order=0, group=4, kinds=None):
+    """All records: out [B, V, H, W] (order 0) or [V, B, H, W] (order 1).  kinds: the chain's
+    stage order (augment_one_seq) instead of the fixed gather order (augment_one)."""
     B = len(idx)
     out = np.zeros((B, V, H, W) if order == 0 else (V, B, H, W), f32)
     lut = np.asarray(lut, f32)
@@ -121,7 +181,8 @@ def augment_views(src_u8, idx, lut, rec, gm, V, H, W, seed, order=0, group=4):
         img = lut[src_u8[idx[b]]].reshape(H, W)
         for v in range(V):
             rid = b * V + v
-            o = augment_one(img, rec[rid], gm, seed, rid, group)
+            o = (augment_one(img, rec[rid], gm, seed, rid, group) if kinds is None else
+                 augment_one_seq(img, rec[rid], gm, seed, rid, kinds, group))
             if order == 0:
                 out[b, v] = o
             else:

@@ -66,13 +66,18 @@ def test_random_split_partition():
         D.random_split_indices(60, [50, 5])
 
 
-def test_chain_order_validation():
+def test_chain_validation_and_order():
     for ch in A.default_chains()["global"].values():
         A.validate_chain(ch)
+        assert A.fixed_order(ch)          # the reference's default chains: the gather kernel
+    # any Compose order is accepted (the stage-by-stage kernel runs it) ...
+    A.validate_chain([("affine", {}, 1.0), ("crop", {}, 1.0)])
+    assert not A.fixed_order([("gaussian_noise", {}, 1.0), ("frequency_mask", {}, 1.0)])
+    # ... but a kind twice or an unknown kind is not (one record slot per transform kind)
     with pytest.raises(NotImplementedError):
-        A.validate_chain([("affine", {}, 1.0), ("crop", {}, 1.0)])
+        A.validate_chain([("crop", {}, 1.0), ("crop", {}, 1.0)])
     with pytest.raises(NotImplementedError):
-        A.validate_chain([("gaussian_noise", {}, 1.0), ("frequency_mask", {}, 1.0)])
+        A.validate_chain([("elastic", {}, 1.0)])
     custom = A.custom_audio_chain({"time_mask": {"time_mask_param": 10},
                                    "gaussian_noise": {"std": 0.05}},
                                   {"time_mask": 0.5, "gaussian_noise": 0.3})
@@ -163,3 +168,39 @@ def test_oracle_masks_time_stretch_and_groups():
 def test_oracle_noise_statistics():
     z = OA.gauss(12345, 7, np.arange(200000))
     assert abs(z.mean()) < 0.01 and abs(z.std() - 1.0) < 0.01
+
+
+def _random_record(rng, chain, H, W):
+    rec, gm = A.sample_records(rng, chain, 1, H, W)
+    return rec[0], gm
+
+
+@pytest.mark.parametrize("view", ["global", "local"])
+@pytest.mark.parametrize("mod", ["image", "audio"])
+def test_sequential_oracle_equals_gather_oracle_in_fixed_order(view, mod):
+    """A chain in the gather kernel's order gives the same views stage by stage (Compose
+    semantics) as walked backwards per output pixel: the two restatements agree bit for bit."""
+    H = 28 if mod == "image" else 112
+    rng = np.random.default_rng(11)
+    chain = [(k, kw, 1.0 if k != "erasing" else 0.5) for k, kw, _p in A.default_chains()[view][mod]]
+    kinds = A.chain_kinds(chain)
+    img = OA.normalise_lut("image")[rng.integers(0, 256, (H, H))]
+    for r in range(6):
+        rec, gm = _random_record(rng, chain, H, H)
+        if gm is not None:
+            rec[22] = 0
+        np.testing.assert_array_equal(OA.augment_one_seq(img, rec, gm, 5, r, kinds),
+                                      OA.augment_one(img, rec, gm, 5, r))
+
+
+def test_sequential_oracle_follows_the_chain_order():
+    """Masks before the time stretch are stretched with the image; after it they are not."""
+    img = np.arange(1, 112 * 112 + 1, dtype=np.float32).reshape(112, 112) / 12544.0
+    r = _rec()
+    r[19:21] = [40, 50]        # time mask, columns [40, 50)
+    r[16], r[23] = 2.0, 8      # time stretch by 2 (t = 2c)
+    K = OA
+    before = OA.augment_one_seq(img, r, None, 0, 0, [K.K_TMASK, K.K_TWARP])
+    after = OA.augment_one_seq(img, r, None, 0, 0, [K.K_TWARP, K.K_TMASK])
+    assert (before[:, 20:25] == 0).all() and (before[:, 25:56] > 0).all()
+    assert (after[:, 40:50] == 0).all() and (after[:, 20:25] > 0).all()

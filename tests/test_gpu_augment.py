@@ -200,3 +200,171 @@ def test_engine_step_from_staged_augmentation_equals_collated_views(tmp_path):
     (xi0, xa0, l0), (xi1, xa1, l1) = res
     assert torch.equal(xi0, xi1) and torch.equal(xa0, xa1)
     assert l0 == l1
+
+
+def _config_chains():
+    """The audio chains of the reference's own config (configs/config_multimodal_dino.yaml
+    best_augments through process_augment_config, get_data.py:195-231): YAML key order, i.e.
+    masks and noise BEFORE the time stretch and the crop -- not the gather kernel's order."""
+    import os
+    import yaml
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(here, "configs", "config_multimodal_dino.yaml")) as f:
+        cfg = yaml.safe_load(f)
+    aug = A.MultiModalAugmentation(2, 4, augment_values=A.process_augment_config(cfg))
+    return {"global": aug.global_transforms["audio"], "local": aug.local_transforms["audio"]}
+
+
+@pytest.mark.parametrize("view", ["global", "local"])
+@pytest.mark.parametrize("order", [0, 1])
+def test_sequential_kernel_matches_oracle_on_the_config_chains(view, order):
+    """avd_augment_views_seq vs the stage-by-stage restatement (OA.augment_one_seq) on the
+    reference config's chains (every stage forced on in half the records): bit-exact without
+    noise, |diff| <= 2e-5 with it (device logf/cosf, then interpolated by later stages)."""
+    chain = _config_chains()[view]
+    assert not A.fixed_order(chain)
+    H = W = 112
+    N, B, V = 9, 4, 3
+    rng = np.random.default_rng(21)
+    src = rng.integers(0, 256, (N, H * W), dtype=np.uint8)
+    idx = rng.integers(0, N, B)
+    lut = OA.normalise_lut("audio")
+    rec_on, gm = _records([(k, kw, 1.0) for k, kw, _p in chain], B, V, H, W, 3)
+    rec_p, _ = _records(chain, B, V, H, W, 4)
+    rec = np.where((np.arange(B * V) % 2 == 0)[:, None], rec_on, rec_p)
+    if gm is None:
+        rec[:, 22] = -1
+    kinds = A.chain_kinds(chain)
+    seed = 0x1234567
+    out = torch.empty((B, V, H, W) if order == 0 else (V, B, H, W), device="cuda")
+    ops.augment_views(torch.from_numpy(src).cuda(), torch.from_numpy(idx).cuda(),
+                      torch.from_numpy(lut).cuda(), torch.from_numpy(np.ascontiguousarray(rec)).cuda(),
+                      None if gm is None else torch.from_numpy(gm.view(np.int32)).cuda(),
+                      4, seed, V, H, W, out, order, kinds)
+    got = out.cpu().numpy()
+    ref = OA.augment_views(src, idx, lut, rec, gm, V, H, W, seed, order, kinds=kinds)
+    noisy = (rec[:, 21] != 0).reshape(B, V)
+    if order == 1:
+        noisy = noisy.T
+    np.testing.assert_array_equal(got[~noisy], ref[~noisy])
+    np.testing.assert_allclose(got[noisy], ref[noisy], rtol=0, atol=2e-5)
+
+
+@pytest.mark.parametrize("view,mod", [("global", "image"), ("local", "image"),
+                                      ("global", "audio"), ("local", "audio")])
+def test_sequential_kernel_equals_gather_kernel_in_fixed_order(view, mod):
+    """The default chains through both kernels: identical views, noise included."""
+    H = W = 28 if mod == "image" else 112
+    rng = np.random.default_rng(8)
+    src = torch.from_numpy(rng.integers(0, 256, (12, H * W), dtype=np.uint8)).cuda()
+    lut = torch.from_numpy(OA.normalise_lut(mod)).cuda()
+    chain = A.default_chains()[view][mod]
+    idx = np.array([3, 1, 8, 0, 11])
+    outs = []
+    for seq in (False, True):
+        aug = A.ViewAugmenter(src, lut, H, W, seed=7, sequential=seq)
+        outs.append(aug(idx, chain, 4, order=1))
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_config_chains_stage_bf16_views():
+    """MultiModalAugmentation(augment_values=the config's best_augments).stage: the staged bf16
+    views equal the f32 views of the same seeds rounded, originals included."""
+    rng = np.random.default_rng(9)
+    srcs = {"image": torch.from_numpy(rng.integers(0, 256, (10, 784), dtype=np.uint8)).cuda(),
+            "audio": torch.from_numpy(rng.integers(0, 256, (10, 12544), dtype=np.uint8)).cuda()}
+    luts = {k: torch.from_numpy(OA.normalise_lut(k)).cuda() for k in srcs}
+    ch = _config_chains()
+    idx = np.array([4, 9, 2])
+
+    def mk():
+        aug = A.MultiModalAugmentation(2, 4)
+        aug.global_transforms["audio"], aug.local_transforms["audio"] = ch["global"], ch["local"]
+        return aug.bind(A.ViewAugmenter(srcs["image"], luts["image"], 28, 28, seed=1),
+                        A.ViewAugmenter(srcs["audio"], luts["audio"], 112, 112, seed=2))
+
+    x_img = torch.empty(7 * 3 * 784, dtype=torch.bfloat16, device="cuda")
+    x_aud = torch.empty(7 * 3 * 12544, dtype=torch.bfloat16, device="cuda")
+    mk().stage(idx, x_img, x_aud, True)
+    a32 = mk()
+    gi, ga, li, la = a32(idx)
+    ref = torch.cat([ga.transpose(0, 1).reshape(-1), la.transpose(0, 1).reshape(-1),
+                     a32.audio.identity(idx).reshape(-1)])
+    assert torch.equal(x_aud, ref.to(torch.bfloat16))
+    assert torch.isfinite(ref).all() and (ref != 0).any()
+
+
+def test_grouped_masking_kernel_equals_the_references_output():
+    """avd_augment_views_seq with the reference's own randperm groups (tests/golden/
+    augment_ref.npz, GroupedMasking.forward run here, get_data.py:60-108): bit-identical."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "augment_ref.npz"))
+    src = z["src_u8"].reshape(6, 12544)
+    gms, refs = [], []
+    for r in range(3):
+        gm = np.zeros(25, np.uint32)
+        for g in z[f"gm{r}_idx"]:
+            gm[g >> 5] |= np.uint32(1) << np.uint32(g & 31)
+        gms.append(gm)
+        refs.append(z[f"gm{r}_out"])
+    rec = np.zeros((3, A.REC), np.float32)
+    rec[:, 22] = np.arange(3)
+    out = torch.empty((3, 1, 112, 112), device="cuda")
+    ops.augment_views(torch.from_numpy(src).cuda(), torch.arange(3, device="cuda"),
+                      torch.from_numpy(z["lut"]).cuda(), torch.from_numpy(rec).cuda(),
+                      torch.from_numpy(np.stack(gms).view(np.int32)).cuda(), 4, 0, 1, 112, 112, out, 0,
+                      [OA.K_GMASK])
+    np.testing.assert_array_equal(out.cpu().numpy()[:, 0], np.stack(refs))
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_prefetched_augmentation_steps_equal_serial_steps(tmp_path, graph):
+    """Real-data steps whose next batch is augmented on the data stream under the current step
+    (engine.prefetch, double-buffered staged inputs) give the same losses and parameters, bit
+    for bit, as steps that augment each batch in front of it -- eager and graph-replayed."""
+    from avdino.data import AVMNISTDinoLoader
+    from avdino.engine import Hyper, MultiCentralEngine
+    from avdino.params import ParamStore
+    from avdino.spec import multimodal_dino_sd
+    root = _fake_avmnist(tmp_path, n=40)
+    E, D, P = 32, 32, 16
+    res = []
+    for pre in (False, True):
+        ld = AVMNISTDinoLoader(root, batch_size=8, train_size=36, val_size=4, seed=3,
+                               multimodal_mode="semi_supervised", device="cuda", staged=True)
+        batches = list(ld)[:4] * 2
+        store = ParamStore(multimodal_dino_sd("semi_supervised", E, D, P), "cuda:0", seed=1)
+        eng = MultiCentralEngine(store, "semi_supervised", E, D, P, Hyper(dropout=0.0, fusion_dropout=0.0),
+                                 act_dtype=torch.bfloat16)
+        eng.use_graph = graph
+        eng.graph.warmup = 1
+        losses = []
+        for i, b in enumerate(batches):
+            nxt = batches[i + 1] if (pre and i + 1 < len(batches)) else None
+            losses.append(eng.step(b, next_batch=nxt).item())
+        assert eng._pf is None
+        res.append((losses, store.student.clone(), store.teacher.clone()))
+    (l0, s0, t0), (l1, s1, t1) = res
+    assert l0 == l1
+    assert torch.equal(s0, s1) and torch.equal(t0, t1)
+
+
+def test_trainer_prefetches_staged_batches(tmp_path):
+    """Trainer.fit over a staged loader (one batch of look-ahead, model.prefetch after each
+    optimizer step) equals the same fit over the collated views."""
+    from avdino.data import AVMNISTDinoLoader
+    from avdino.models import CentralMultiModalEncoder, MultiModalDINOWithMSELightning
+    from avdino.trainer import Trainer
+    root = _fake_avmnist(tmp_path, n=40)
+    out = []
+    for staged in (False, True):
+        ld = AVMNISTDinoLoader(root, batch_size=8, train_size=36, val_size=4, seed=3,
+                               multimodal_mode="mse", device="cuda", staged=staged)
+        torch.manual_seed(0)
+        m = MultiModalDINOWithMSELightning(encoder_class=CentralMultiModalEncoder, projection_dim=16,
+                                           output_dim=32, encoder_output_dim=32, dropout=0.0,
+                                           device="cuda", precision="bf16", seed=0)
+        tr = Trainer(max_epochs=1, limit_train_batches=3, logger=None)
+        tr.fit(m, ld)
+        out.append(m.model.store.student.clone())
+    assert torch.equal(out[0], out[1])

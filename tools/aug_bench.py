@@ -6,8 +6,10 @@ modalities plus the originals) and the real-data training step it feeds.
   staged_bf16   avd_augment_records (device draws) + avd_augment_views_dt writing bf16 straight
                 into the engine's staged view-major input (MultiModalAugmentation.stage)
   step_*        MultiCentralEngine (mse, bf16, graph replay) steps fed by staged_bf16 batches of
-                a synthetic AVMNIST-shaped uint8 dataset resident in HBM, vs the same engine on
-                pre-built synthetic views (bench.py's input)
+                a synthetic AVMNIST-shaped uint8 dataset resident in HBM (serially before each
+                step, or prefetched: the next batch's augmentation on the data stream under the
+                current step, engine.prefetch), vs the same engine on pre-built synthetic views
+                (bench.py's input)
 
 Algorithmic bytes of the staged path per batch: the staged bf16 views written once
 (2 B x H x W x views) + each source row read once per modality.  Times from HIP events on the
@@ -93,15 +95,17 @@ def main(B=1024, N=55000, G=2, L=4, iters=20):
     synth = {"image": px(B, 1, 28, 28), "audio": px(B, 1, 112, 112), "label": labels,
              "g_img": px(B, G, 1, 28, 28), "g_aud": px(B, G, 1, 112, 112),
              "l_img": px(B, L, 1, 28, 28), "l_aud": px(B, L, 1, 112, 112)}
-    for name, feed in (("step_synthetic_views", lambda i: synth),
-                       ("step_device_augmented", lambda i: batches[i % len(batches)])):
-        for i in range(4):
-            eng.step(feed(i))
+    for name, feed, nxt in (("step_synthetic_views", lambda i: synth, None),
+                            ("step_device_augmented", lambda i: batches[i % len(batches)], None),
+                            ("step_device_augmented_prefetched", lambda i: batches[i % len(batches)],
+                             lambda i: batches[(i + 1) % len(batches)])):
+        for i in range(6):
+            eng.step(feed(i), next_batch=nxt(i) if nxt else None)
         torch.cuda.synchronize()
-        k = [0]
+        k = [6]
 
         def one():
-            eng.step(feed(k[0]))
+            eng.step(feed(k[0]), next_batch=nxt(k[0]) if nxt else None)
             k[0] += 1
 
         gpu_ms, wall_ms = timed(one, iters)

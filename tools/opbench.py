@@ -37,6 +37,7 @@ def main():
     eng.step(pool[0])
     torch.cuda.synchronize()
     fns = ops.TIMER.fns
+    calls = {k: v["calls"] for k, v in ops.TIMER.summary().items()}
     ops.TIMER = None
     rows = []
     for key, (fn, nb, fl) in fns.items():
@@ -50,11 +51,17 @@ def main():
         e.record()
         torch.cuda.synchronize()
         us = s.elapsed_time(e) * 1e3 / a.reps
-        rows.append((us, key, nb / us / 1e3, fl / us / 1e6))
+        # roofline time of the launch: max(bytes / 8 TB/s, flops / 2.5 PF/s (bf16) or 157 TF/s)
+        roof = max(nb / 8e6, fl / (2.5e9 if act == torch.bfloat16 else 157e6))
+        rows.append((us * calls.get(key, 1), us, calls.get(key, 1), key, nb / us / 1e3, fl / us / 1e6,
+                     roof))
     tot = sum(r[0] for r in rows)
-    for us, key, gbs, tfs in sorted(rows, reverse=True):
-        print(f"{us:9.1f} us {100 * us / tot:5.1f}%  {gbs:7.0f} GB/s {tfs:7.1f} TF/s  {key}")
-    print(f"sum of distinct launches: {tot / 1e3:.2f} ms")
+    troof = sum(r[6] * r[2] for r in rows)
+    print("  per-step    us/launch  calls   share    GB/s    TF/s   roof us  x-roof  key")
+    for st, us, n, key, gbs, tfs, roof in sorted(rows, reverse=True):
+        print(f"{st:9.1f} us {us:9.1f} {n:5d} {100 * st / tot:6.1f}%  {gbs:7.0f} {tfs:7.1f} "
+              f"{roof:8.1f} {us / max(roof, 1e-3):7.2f}  {key}")
+    print(f"serial step (sum over launches x calls): {tot / 1e3:.3f} ms; roofline sum {troof / 1e3:.3f} ms")
 
 
 if __name__ == "__main__":
