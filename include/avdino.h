@@ -444,8 +444,8 @@ int avd_augment_views_seq(const uint8_t* src_u8, const int64_t* idx, long long n
 /* The records' random parameters drawn on the device (the get_params rules of each transform:
  * RandomResizedCrop / RandomErasing 10 attempts + fallback, RandomRotation / RandomAffine
  * inverse matrices, torchaudio mask_along_axis bands, time-stretch rate, noise std,
- * GroupedMasking's randperm(ng)[:k] as the k smallest of ng counter-hash keys).  stages is a
- * HOST array [nstages <= 9][8] of {kind, p, params...}:
+ * GroupedMasking's randperm(ng)[:k] as a uniformly random k-subset by Floyd's algorithm; one
+ * thread per record).  stages is a HOST array [nstages <= 9][8] of {kind, p, params...}:
  *   kind 0 crop {scale0, scale1, ratio0, ratio1}, 1 time stretch {min, max},
  *   2 frequency mask {param}, 3 time mask {param}, 4 rotation {degrees},
  *   5 affine {degrees, translate_x (< 0: none), translate_y, scale0 (<= 0: none), scale1},

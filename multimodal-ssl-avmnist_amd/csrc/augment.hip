@@ -29,13 +29,16 @@ __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
   return x;
 }
 
-// Standard normal from (seed, record, pixel): Box-Muller over a 64-bit counter hash.
-__device__ __forceinline__ float gauss(unsigned long long seed, unsigned rec, unsigned pix) {
+// Two standard normals for the pixel pair (2q, 2q+1) of a record: one Box-Muller draw over a
+// 64-bit counter hash of (seed, record, q) -- the cosine for the even pixel, the sine for the odd
+// one (independent N(0,1) values; one hash, one log, one sqrt per two pixels).
+__device__ __forceinline__ float2 gauss2(unsigned long long seed, unsigned rec, unsigned q) {
 #pragma clang fp contract(off)
-  const unsigned long long r = mix64(seed ^ mix64(((unsigned long long)rec << 32) | pix));
+  const unsigned long long r = mix64(seed ^ mix64(((unsigned long long)rec << 32) | q));
   const float u1 = (float)((r >> 40) + 1ull) * 5.9604644775390625e-8f;  // (0, 1]
   const float u2 = (float)((r >> 16) & 0xFFFFFFull) * 5.9604644775390625e-8f;
-  return sqrtf(-2.0f * logf(u1)) * cosf(6.2831855f * u2);
+  const float mag = sqrtf(-2.0f * logf(u1)), ang = 6.2831855f * u2;
+  return make_float2(mag * cosf(ang), mag * sinf(ang));
 }
 
 // Nearest-neighbour inverse map of a torchvision affine / rotation (grid_sample, zero padding,
@@ -136,39 +139,51 @@ __global__ __launch_bounds__(kThreads) void augment_kernel(
   const int gw = group > 0 ? W / group : 1;
   TO* o = out + (order == 0 ? (size_t)rid : (size_t)v * B + b) * HW;
 
-  for (int p = threadIdx.x; p < HW; p += kThreads) {
-    const int y = p / W, x = p - y * W;
-    int qx = x, qy = y;
-    bool ok = true;
-    if (aff) ok = affine_nearest(maff, cx, cy, W, H, qx, qy);
-    if (ok && rot) ok = affine_nearest(mrot, cx, cy, W, H, qx, qy);
-    float val = 0.0f;
-    if (ok && !(qy >= f0 && qy < f1) && !(qx >= t0 && qx < t1)) {
-      if (tw) {
-        // |phase_vocoder(spec, rate)|[c] = a*|s[i0+1]| + (1-a)*|s[i0]|, t = c*rate, zero past
-        // the input's end (torchaudio pads two zero frames); ceil(W/rate) output frames.
-        const float t = (float)qx * rate;
-        if (t < (float)W) {
-          const int i0 = (int)t;
-          const float a = t - (float)i0;
-          const float s0 = fabsf(crop_sample(vw, qy, i0));
-          const float s1 = i0 + 1 < W ? fabsf(crop_sample(vw, qy, i0 + 1)) : 0.0f;
-          val = a * s1 + (1.0f - a) * s0;
+  // a thread builds the pixel pair (2q, 2q+1): W is even, so a pair never straddles a row; it
+  // shares the row index, one noise draw and one (2 x bf16 / 2 x f32) store
+  const FastDiv divw(W / 2), divg(group > 0 ? group : 1);
+  for (int q = threadIdx.x; q < HW / 2; q += kThreads) {
+    const int y = divw.div(q), x0 = 2 * (q - y * (W / 2));
+    float2 g2 = make_float2(0.f, 0.f);
+    if (nstd != 0.0f) g2 = gauss2(seed, (unsigned)rid, (unsigned)q);
+    const int gy = gmr ? divg.div(y) * gw : 0;
+    float v2[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int x = x0 + e;
+      int qx = x, qy = y;
+      bool ok = true;
+      if (aff) ok = affine_nearest(maff, cx, cy, W, H, qx, qy);
+      if (ok && rot) ok = affine_nearest(mrot, cx, cy, W, H, qx, qy);
+      float val = 0.0f;
+      if (ok && !(qy >= f0 && qy < f1) && !(qx >= t0 && qx < t1)) {
+        if (tw) {
+          // |phase_vocoder(spec, rate)|[c] = a*|s[i0+1]| + (1-a)*|s[i0]|, t = c*rate, zero past
+          // the input's end (torchaudio pads two zero frames); ceil(W/rate) output frames.
+          const float t = (float)qx * rate;
+          if (t < (float)W) {
+            const int i0 = (int)t;
+            const float a = t - (float)i0;
+            const float s0 = fabsf(crop_sample(vw, qy, i0));
+            const float s1 = i0 + 1 < W ? fabsf(crop_sample(vw, qy, i0 + 1)) : 0.0f;
+            val = a * s1 + (1.0f - a) * s0;
+          }
+        } else {
+          val = crop_sample(vw, qy, qx);
         }
-      } else {
-        val = crop_sample(vw, qy, qx);
       }
-    }
-    if (eh > 0 && y >= et && y < et + eh && x >= el && x < el + ew) val = 0.0f;
-    if (nstd != 0.0f) val = val + gauss(seed, (unsigned)rid, (unsigned)p) * nstd;
-    if (gmr) {
-      const int g = (y / group) * gw + x / group;
-      if ((gmr[g >> 5] >> (g & 31)) & 1u) val = val * 0.0f;
+      if (eh > 0 && y >= et && y < et + eh && x >= el && x < el + ew) val = 0.0f;
+      if (nstd != 0.0f) val = val + (e ? g2.y : g2.x) * nstd;
+      if (gmr) {
+        const int g = gy + divg.div(x);
+        if ((gmr[g >> 5] >> (g & 31)) & 1u) val = val * 0.0f;
+      }
+      v2[e] = val;
     }
     if constexpr (sizeof(TO) == 4)
-      o[p] = val;
-    else
-      o[p] = f2bf(val);     // bf16 straight into the engine's staged view-major input
+      reinterpret_cast<float2*>(o)[q] = make_float2(v2[0], v2[1]);
+    else      // bf16 straight into the engine's staged view-major input
+      reinterpret_cast<uint32_t*>(o)[q] = pack_bf16x2(v2[0], v2[1]);
   }
 }
 
@@ -298,8 +313,11 @@ __global__ __launch_bounds__(kThreads) void augment_seq_kernel(
     } else if (kind == SK_NOISE) {
       const float nstd = rec[AVD_AUG_NOISE];
       if (nstd == 0.0f) continue;
-      for (int p = threadIdx.x; p < HW; p += kThreads)
-        s_img[p] = s_img[p] + gauss(seed, (unsigned)rid, (unsigned)p) * nstd;
+      for (int q = threadIdx.x; q < HW / 2; q += kThreads) {
+        const float2 g2 = gauss2(seed, (unsigned)rid, (unsigned)q);
+        s_img[2 * q] = s_img[2 * q] + g2.x * nstd;
+        s_img[2 * q + 1] = s_img[2 * q + 1] + g2.y * nstd;
+      }
     } else if (kind == SK_GMASK) {
       const int gmrow = (int)rec[AVD_AUG_GM];
       if (!gm || gmrow < 0) continue;
@@ -324,20 +342,21 @@ __global__ __launch_bounds__(kThreads) void augment_seq_kernel(
     }
   }
   TO* o = out + (order == 0 ? (size_t)rid : (size_t)v * B + b) * HW;
-  for (int p = threadIdx.x; p < HW; p += kThreads) {
+  for (int q = threadIdx.x; q < HW / 2; q += kThreads) {
     if constexpr (sizeof(TO) == 4)
-      o[p] = s_img[p];
+      reinterpret_cast<float2*>(o)[q] = make_float2(s_img[2 * q], s_img[2 * q + 1]);
     else
-      o[p] = f2bf(s_img[p]);
+      reinterpret_cast<uint32_t*>(o)[q] = pack_bf16x2(s_img[2 * q], s_img[2 * q + 1]);
   }
 }
 
 // ----------------------------------------------------------------------------- parameter draws
 // The chain's random parameters drawn on the device (what ViewAugmenter.records draws with
-// numpy): one block per (sample, view) record; thread 0 walks the stages in order with a
-// counter-hash uniform stream (seed, record, draw index); the grouped mask picks exactly k of
-// the ng groups as the k smallest of ng hashed keys (block-wide bitonic sort in LDS), i.e. a
-// uniformly random k-subset like randperm(ng)[:k].
+// numpy): one THREAD per (sample, view) record walks the stages in order with a counter-hash
+// uniform stream (seed, record, draw index) -- records are independent, so a launch is n lanes
+// of serial draws, not n blocks with one busy lane each; the grouped mask picks exactly k of the
+// ng groups with Floyd's algorithm (a uniformly random k-subset, like randperm(ng)[:k]) on a
+// per-thread bitmask in LDS.
 struct Chain { float st[kMaxStages * kStageF]; int n; };
 
 struct Urng {
@@ -363,127 +382,113 @@ __device__ void inv_affine(float angle_deg, float tx, float ty, float s, float* 
   m[5] += m[3] * (-tx) + m[4] * (-ty);
 }
 
-__global__ __launch_bounds__(256) void aug_records_kernel(Chain ch, int H, int W, int group,
-                                                          unsigned long long seed,
-                                                          float* __restrict__ recs,
-                                                          uint32_t* __restrict__ gm, int gm_words) {
-  __shared__ unsigned long long keys[kMaxGroups];
-  __shared__ int s_k, s_on;
-  const int rid = blockIdx.x;
+constexpr int kRecThreads = 64;
+
+__global__ __launch_bounds__(kRecThreads) void aug_records_kernel(Chain ch, int n, int H, int W,
+                                                                  int group,
+                                                                  unsigned long long seed,
+                                                                  float* __restrict__ recs,
+                                                                  uint32_t* __restrict__ gm,
+                                                                  int gm_words) {
+  // the grouped-mask bitmask of each thread: word-major [word][thread] (conflict-free when the
+  // lanes touch the same word index)
+  __shared__ uint32_t bits[kMaxGroups / 32][kRecThreads];
+  const int rid = blockIdx.x * kRecThreads + threadIdx.x;
+  if (rid >= n) return;       // no barrier below: lanes are independent
   float* rec = recs + (size_t)rid * AVD_AUG_REC;
   Urng rng{seed, (unsigned)rid, 0u};
-  if (threadIdx.x == 0) {
-    float r[AVD_AUG_REC];
-    for (int i = 0; i < AVD_AUG_REC; ++i) r[i] = 0.f;
-    r[AVD_AUG_GM] = -1.f;
-    int flags = 0, gk = -1, gon = 0;
-    const float area = (float)(H * W);
-    for (int si = 0; si < ch.n; ++si) {
-      const float* a = ch.st + si * kStageF;
-      const int kind = (int)a[0];
-      const bool on = rng.u() < a[1];
-      const float* q = a + 2;
-      if (kind == SK_CROP || kind == SK_ERASE) {
-        // RandomResizedCrop / RandomErasing get_params: 10 attempts, then the fallback
-        const bool crop = kind == SK_CROP;
-        const float l0 = logf(q[2]), l1 = logf(q[3]);
-        int h = 0, w = 0, i = 0, j = 0;
-        bool found = false;
-        for (int t = 0; t < 10 && !found; ++t) {
-          const float ta = area * rng.uni(q[0], q[1]);
-          const float ar = expf(rng.uni(l0, l1));
-          const int ww = (int)rintf(sqrtf(crop ? ta * ar : ta / ar));
-          const int hh = (int)rintf(sqrtf(crop ? ta / ar : ta * ar));
-          found = crop ? (ww > 0 && ww <= W && hh > 0 && hh <= H) : (hh < H && ww < W);
-          if (found) { h = hh; w = ww; }
-        }
-        if (found) {
-          i = rng.below(H - h + 1);
-          j = rng.below(W - w + 1);
-        } else if (crop) {      // centre crop at the nearest admissible aspect
-          const float inr = (float)W / (float)H;
-          if (inr < q[2]) { w = W; h = (int)rintf((float)W / q[2]); }
-          else if (inr > q[3]) { h = H; w = (int)rintf((float)H * q[3]); }
-          else { w = W; h = H; }
-          i = (H - h) / 2;
-          j = (W - w) / 2;
-        }
-        if (on) {
-          const int o = crop ? AVD_AUG_CROP : AVD_AUG_ERASE;
-          r[o] = (float)i; r[o + 1] = (float)j; r[o + 2] = (float)h; r[o + 3] = (float)w;
-          if (crop) flags |= 1;
-        }
-      } else if (kind == SK_ROT) {
-        float m[6];
-        inv_affine(-rng.uni(-q[0], q[0]), 0.f, 0.f, 1.f, m);
-        if (on) { for (int k = 0; k < 6; ++k) r[AVD_AUG_ROT + k] = m[k]; flags |= 4; }
-      } else if (kind == SK_AFF) {
-        const float ang = rng.uni(-q[0], q[0]);
-        const float tx = q[1] >= 0.f ? rintf(rng.uni(-q[1] * W, q[1] * W)) : 0.f;
-        const float ty = q[1] >= 0.f ? rintf(rng.uni(-q[2] * H, q[2] * H)) : 0.f;
-        const float sc = q[3] > 0.f ? rng.uni(q[3], q[4]) : 1.f;
-        float m[6];
-        inv_affine(ang, tx, ty, sc, m);
-        if (on) { for (int k = 0; k < 6; ++k) r[AVD_AUG_AFF + k] = m[k]; flags |= 2; }
-      } else if (kind == SK_TWARP) {
-        const float rate = rng.uni(q[0], q[1]);
-        if (on) { r[AVD_AUG_RATE] = rate; flags |= 8; }
-      } else if (kind == SK_FMASK || kind == SK_TMASK) {
-        const int size = kind == SK_FMASK ? H : W;
-        const float value = rng.u() * q[0];
-        const float minv = rng.u() * ((float)size - value);
-        const int st = (int)floorf(minv), en = st + (int)floorf(value);
-        const int o = kind == SK_FMASK ? AVD_AUG_FMASK : AVD_AUG_TMASK;
-        if (on) { r[o] = (float)st; r[o + 1] = (float)en; }
-      } else if (kind == SK_NOISE) {
-        if (on) r[AVD_AUG_NOISE] = q[0];
-      } else if (kind == SK_GMASK) {
-        const int ng = (H / group) * (W / group);
-        gk = (int)(q[0] * (float)ng);
-        gon = on;
-        if (on) r[AVD_AUG_GM] = (float)rid;
+  float r[AVD_AUG_REC];
+  for (int i = 0; i < AVD_AUG_REC; ++i) r[i] = 0.f;
+  r[AVD_AUG_GM] = -1.f;
+  int flags = 0, gk = -1, gon = 0;
+  const float area = (float)(H * W);
+  for (int si = 0; si < ch.n; ++si) {
+    const float* a = ch.st + si * kStageF;
+    const int kind = (int)a[0];
+    const bool on = rng.u() < a[1];
+    const float* q = a + 2;
+    if (kind == SK_CROP || kind == SK_ERASE) {
+      // RandomResizedCrop / RandomErasing get_params: 10 attempts, then the fallback
+      const bool crop = kind == SK_CROP;
+      const float l0 = logf(q[2]), l1 = logf(q[3]);
+      int h = 0, w = 0, i = 0, j = 0;
+      bool found = false;
+      for (int t = 0; t < 10 && !found; ++t) {
+        const float ta = area * rng.uni(q[0], q[1]);
+        const float ar = expf(rng.uni(l0, l1));
+        const int ww = (int)rintf(sqrtf(crop ? ta * ar : ta / ar));
+        const int hh = (int)rintf(sqrtf(crop ? ta / ar : ta * ar));
+        found = crop ? (ww > 0 && ww <= W && hh > 0 && hh <= H) : (hh < H && ww < W);
+        if (found) { h = hh; w = ww; }
       }
+      if (found) {
+        i = rng.below(H - h + 1);
+        j = rng.below(W - w + 1);
+      } else if (crop) {      // centre crop at the nearest admissible aspect
+        const float inr = (float)W / (float)H;
+        if (inr < q[2]) { w = W; h = (int)rintf((float)W / q[2]); }
+        else if (inr > q[3]) { h = H; w = (int)rintf((float)H * q[3]); }
+        else { w = W; h = H; }
+        i = (H - h) / 2;
+        j = (W - w) / 2;
+      }
+      if (on) {
+        const int o = crop ? AVD_AUG_CROP : AVD_AUG_ERASE;
+        r[o] = (float)i; r[o + 1] = (float)j; r[o + 2] = (float)h; r[o + 3] = (float)w;
+        if (crop) flags |= 1;
+      }
+    } else if (kind == SK_ROT) {
+      float m[6];
+      inv_affine(-rng.uni(-q[0], q[0]), 0.f, 0.f, 1.f, m);
+      if (on) { for (int k = 0; k < 6; ++k) r[AVD_AUG_ROT + k] = m[k]; flags |= 4; }
+    } else if (kind == SK_AFF) {
+      const float ang = rng.uni(-q[0], q[0]);
+      const float tx = q[1] >= 0.f ? rintf(rng.uni(-q[1] * W, q[1] * W)) : 0.f;
+      const float ty = q[1] >= 0.f ? rintf(rng.uni(-q[2] * H, q[2] * H)) : 0.f;
+      const float sc = q[3] > 0.f ? rng.uni(q[3], q[4]) : 1.f;
+      float m[6];
+      inv_affine(ang, tx, ty, sc, m);
+      if (on) { for (int k = 0; k < 6; ++k) r[AVD_AUG_AFF + k] = m[k]; flags |= 2; }
+    } else if (kind == SK_TWARP) {
+      const float rate = rng.uni(q[0], q[1]);
+      if (on) { r[AVD_AUG_RATE] = rate; flags |= 8; }
+    } else if (kind == SK_FMASK || kind == SK_TMASK) {
+      const int size = kind == SK_FMASK ? H : W;
+      const float value = rng.u() * q[0];
+      const float minv = rng.u() * ((float)size - value);
+      const int st = (int)floorf(minv), en = st + (int)floorf(value);
+      const int o = kind == SK_FMASK ? AVD_AUG_FMASK : AVD_AUG_TMASK;
+      if (on) { r[o] = (float)st; r[o + 1] = (float)en; }
+    } else if (kind == SK_NOISE) {
+      if (on) r[AVD_AUG_NOISE] = q[0];
+    } else if (kind == SK_GMASK) {
+      const int ng = (H / group) * (W / group);
+      gk = (int)(q[0] * (float)ng);
+      gon = on;
+      if (on) r[AVD_AUG_GM] = (float)rid;
     }
-    r[AVD_AUG_FLAGS] = (float)flags;
-    for (int i = 0; i < AVD_AUG_REC; ++i) rec[i] = r[i];
-    s_k = gk;
-    s_on = gon;
   }
-  __syncthreads();
-  const int k = s_k;
-  if (k < 0 || !gm) return;
-  // exactly k distinct groups: the k smallest of ng random keys (index in the low bits)
+  r[AVD_AUG_FLAGS] = (float)flags;
+  for (int i = 0; i < AVD_AUG_REC; ++i) rec[i] = r[i];
+  if (gk < 0 || !gm) return;
+  // exactly k distinct groups (Floyd): for j = ng-k .. ng-1 draw t uniform in [0, j]; take t,
+  // or j when t is taken already -- every k-subset equally likely
   const int ng = (H / group) * (W / group);
-  int n2 = 1;
-  while (n2 < ng) n2 <<= 1;
-  for (int i = threadIdx.x; i < n2; i += 256)
-    keys[i] = i < ng ? ((mix64(seed ^ mix64(((unsigned long long)(rid | 0x80000000u) << 32) | i))
-                         & ~0x3FFull) | (unsigned long long)i)
-                     : ~0ull;
-  __syncthreads();
-  for (int size = 2; size <= n2; size <<= 1)
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = threadIdx.x; i < n2; i += 256) {
-        const int jx = i ^ stride;
-        if (jx > i) {
-          const bool up = (i & size) == 0;
-          const unsigned long long a = keys[i], b = keys[jx];
-          if ((a > b) == up) { keys[i] = b; keys[jx] = a; }
-        }
-      }
-      __syncthreads();
+  const int words = (ng + 31) / 32;
+  const int tx = threadIdx.x;
+  for (int wd = 0; wd < words; ++wd) bits[wd][tx] = 0u;
+  if (gon) {
+    const unsigned long long key = (unsigned long long)(rid | 0x80000000u) << 32;
+    for (int j = ng - gk; j < ng; ++j) {
+      const unsigned h = (unsigned)(mix64(seed ^ mix64(key | (unsigned)j)) >> 32);
+      const int t = (int)(((unsigned long long)h * (unsigned)(j + 1)) >> 32);   // [0, j]
+      const bool taken = (bits[t >> 5][tx] >> (t & 31)) & 1u;
+      const int g = taken ? j : t;
+      bits[g >> 5][tx] |= 1u << (g & 31);
     }
-  __shared__ uint32_t bits[kMaxGroups / 32];
-  for (int wd = threadIdx.x; wd < kMaxGroups / 32; wd += 256) bits[wd] = 0u;
-  __syncthreads();
-  if (s_on)
-    for (int i = threadIdx.x; i < k; i += 256) {
-      const int gidx = (int)(keys[i] & 0x3FFull);
-      atomicOr(&bits[gidx >> 5], 1u << (gidx & 31));     // LDS
-    }
-  __syncthreads();
+  }
   uint32_t* row = gm + (size_t)rid * gm_words;
-  for (int wd = threadIdx.x; wd < gm_words; wd += 256) row[wd] = wd < kMaxGroups / 32 ? bits[wd] : 0u;
+  for (int wd = 0; wd < gm_words; ++wd) row[wd] = wd < words ? bits[wd][tx] : 0u;
 }
 
 }  // namespace
@@ -494,7 +499,7 @@ extern "C" int avd_augment_views(const uint8_t* src_u8, const int64_t* idx, long
                                  unsigned long long seed, int order, float* out, void* stream) {
   if (!src_u8 || !idx || !lut || !rec || !out) return AVD_ERR_ARG;
   if (B <= 0 || V <= 0 || H <= 0 || W <= 0 || n_src <= 0) return AVD_ERR_SHAPE;
-  if ((long long)H * W > kMaxHW || (H * W) % 4 || order < 0 || order > 1) return AVD_ERR_SHAPE;
+  if ((long long)H * W > kMaxHW || (H * W) % 4 || W % 2 || order < 0 || order > 1) return AVD_ERR_SHAPE;
   if (gm && (group <= 0 || H % group || W % group ||
              gm_words * 32 < (H / group) * (W / group)))
     return AVD_ERR_SHAPE;
@@ -516,7 +521,7 @@ extern "C" int avd_augment_views_dt(const uint8_t* src_u8, const int64_t* idx, l
   if (odt != AVD_BF16) return AVD_ERR_DTYPE;
   if (!src_u8 || !idx || !lut || !rec || !out) return AVD_ERR_ARG;
   if (B <= 0 || V <= 0 || H <= 0 || W <= 0 || n_src <= 0) return AVD_ERR_SHAPE;
-  if ((long long)H * W > kMaxHW || (H * W) % 4 || order < 0 || order > 1) return AVD_ERR_SHAPE;
+  if ((long long)H * W > kMaxHW || (H * W) % 4 || W % 2 || order < 0 || order > 1) return AVD_ERR_SHAPE;
   if (gm && (group <= 0 || H % group || W % group ||
              gm_words * 32 < (H / group) * (W / group)))
     return AVD_ERR_SHAPE;
@@ -534,7 +539,7 @@ extern "C" int avd_augment_views_seq(const uint8_t* src_u8, const int64_t* idx, 
                                      int nkinds, void* out, int odt, void* stream) {
   if (!src_u8 || !idx || !lut || !rec || !out || (nkinds > 0 && !kinds)) return AVD_ERR_ARG;
   if (B <= 0 || V <= 0 || H <= 0 || W <= 0 || n_src <= 0) return AVD_ERR_SHAPE;
-  if ((long long)H * W > kMaxHW || (H * W) % 4 || order < 0 || order > 1) return AVD_ERR_SHAPE;
+  if ((long long)H * W > kMaxHW || (H * W) % 4 || W % 2 || order < 0 || order > 1) return AVD_ERR_SHAPE;
   if (nkinds < 0 || nkinds > kMaxStages) return AVD_ERR_SHAPE;
   Prog prog{};
   prog.n = nkinds;
@@ -581,8 +586,8 @@ extern "C" int avd_augment_records(const float* stages, int nstages, int n, int 
     const int ng = (H / group) * (W / group);
     if (ng > kMaxGroups || gm_words * 32 < ng) return AVD_ERR_SHAPE;
   }
-  aug_records_kernel<<<n, 256, 0, avd_stream(stream)>>>(ch, H, W, group, seed, rec,
-                                                        has_gm ? gm : nullptr, gm_words);
+  aug_records_kernel<<<avd_cdiv(n, kRecThreads), kRecThreads, 0, avd_stream(stream)>>>(
+      ch, n, H, W, group, seed, rec, has_gm ? gm : nullptr, gm_words);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

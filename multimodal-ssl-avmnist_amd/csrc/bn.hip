@@ -209,7 +209,9 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
 }
 
 // ----------------------------------------------------------------------------- BN1d / dense
-constexpr int CS_ROWS = 64;
+// rows per partial of the column reductions: 16 keeps ~4 blocks per CU busy at the heads' shapes
+// ([6144, 512] per call; 64 rows per thread left the loop latency-bound, ~20 us per launch)
+constexpr int CS_ROWS = 16;
 
 // Shifted sums: every partial is taken about the pivot K = x[first row of the group][c]
 // (stored in pivot[g, c] for avd_bn_finalize), so var = E[(x-K)^2] - E[x-K]^2 does not cancel
@@ -224,6 +226,7 @@ __global__ __launch_bounds__(256) void colstats_kernel(const float* __restrict__
   const float K = pivot ? x[(size_t)g * rpg * C + c] : 0.f;
   if (pivot && r == 0) pivot[(size_t)g * C + c] = K;
   float s = 0.f, q = 0.f;
+#pragma unroll 16
   for (int row = r0; row < r1; ++row) {
     const float v = x[((size_t)g * rpg + row) * C + c] - K;
     s += v;
@@ -243,6 +246,7 @@ __global__ __launch_bounds__(256) void bn1d_bwd_reduce_kernel(
   const float mu = mean[g * C + c], is = invstd[g * C + c];
   const int r0 = r * CS_ROWS, r1 = min(rpg, r0 + CS_ROWS);
   float s1 = 0.f, s2 = 0.f;
+#pragma unroll 16
   for (int row = r0; row < r1; ++row) {
     const size_t o = ((size_t)g * rpg + row) * C + c;
     const float d = dz[o];

@@ -37,13 +37,16 @@ def _mix64(x):
 
 
 def gauss(seed, rec, pix):
-    """csrc/augment.hip gauss(): Box-Muller over a counter hash of (seed, record, pixel)."""
+    """csrc/augment.hip gauss2(): one Box-Muller draw over a counter hash of (seed, record,
+    pixel pair pix >> 1) -- its cosine for the even pixel, its sine for the odd one."""
+    pix = np.asarray(pix)
     with np.errstate(over="ignore"):
-        key = (np.uint64(rec) << np.uint64(32)) | pix.astype(np.uint64)
+        key = (np.uint64(rec) << np.uint64(32)) | (pix >> 1).astype(np.uint64)
         r = _mix64(np.uint64(seed) ^ _mix64(key))
     u1 = ((r >> np.uint64(40)) + np.uint64(1)).astype(f32) * f32(5.9604644775390625e-8)
     u2 = ((r >> np.uint64(16)) & np.uint64(0xFFFFFF)).astype(f32) * f32(5.9604644775390625e-8)
-    return np.sqrt(f32(-2.0) * np.log(u1)) * np.cos(f32(6.2831855) * u2)
+    mag, ang = np.sqrt(f32(-2.0) * np.log(u1)), f32(6.2831855) * u2
+    return np.where((pix & 1) == 0, mag * np.cos(ang), mag * np.sin(ang)).astype(f32)
 
 
 def _affine_nearest(m, x, y, H, W):
