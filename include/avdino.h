@@ -105,6 +105,17 @@ int avd_gemm(int M, int N, int K, const float* A, long long sam, long long sak,
              const float* bias, float alpha, float beta, int mode, float* ws,
              long long ws_elems, void* stream);
 
+/* nn.Linear backward's two GEMMs in ONE launch (modes 1/2): dW [O, In] = dout^T x and
+ * dX [rows, In] = dout W (W [O, In]); dout [rows, O] (leading dimension dout_ld), x [rows, In]
+ * (x_ld), dX leading dimension dx_ld.  Both read dout, neither depends on the other: their tile
+ * grids run side by side (one launch boundary, and two small grids fill the chip together);
+ * results are bitwise those of the two avd_gemm calls.  ws: avd_linear_bwd_ws_elems floats of
+ * split-K scratch (NULL: single passes over K).  The bias gradient stays avd_sum_rows. */
+long long avd_linear_bwd_ws_elems(int rows, int O, int In, int mode);
+int avd_linear_bwd(int rows, int O, int In, const float* dout, long long dout_ld, const float* x,
+                   long long x_ld, const float* W, float* dW, float* dX, long long dx_ld, int mode,
+                   float* ws, long long ws_elems, void* stream);
+
 /* ------------------------------------------------------------------ channels-last conv blocks
  * The training path's conv blocks on NHWC maps ([N][H][W][C]; Cin = 1 maps are the plain
  * images), on MFMA for both storage types: dt = AVD_BF16 (v_mfma_f32_16x16x32_bf16) or AVD_F32

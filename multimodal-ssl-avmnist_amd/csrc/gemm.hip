@@ -13,6 +13,8 @@ using namespace avd;
 
 namespace {
 
+__device__ __forceinline__ int avd_cdiv_d(int a, int b) { return (a + b - 1) / b; }
+
 constexpr int BM = 64, BN = 64, BK = 16;
 
 __global__ __launch_bounds__(256) void sgemm_kernel(int M, int N, int K, const float* __restrict__ A,
@@ -115,35 +117,11 @@ enum { LAY_K = 0, LAY_R = 1, LAY_S = 2 };
 template <int ROWS>
 struct TileRegs { float v[ROWS / 8 > 16 ? ROWS / 8 : 16]; };   // ROWS*32 elements over 256 threads
 
-template <int ROWS, int LAY, bool EX = false>
+template <int ROWS, int LAY>
 __device__ __forceinline__ void load_tile(const float* __restrict__ X, long long sr, long long sk,
                                           int r0, int k0, int rows, int kend, TileRegs<ROWS>& t) {
   const int tid = threadIdx.x;
-  if constexpr (EX && LAY == LAY_K) {
-    // whole tiles (the caller checked): unconditional loads, so the wait for one register stage
-    // leaves the younger stages' loads in flight (no branch for the waitcnt pass to merge over)
-#pragma unroll
-    for (int i = 0; i < ROWS / 32; ++i) {
-      const int e4 = tid + 256 * i;
-      const int r = e4 >> 3, k = (e4 & 7) * 4;
-      const float4 v = *reinterpret_cast<const float4*>(X + (size_t)(r0 + r) * sr + k0 + k);
-      t.v[4 * i] = v.x; t.v[4 * i + 1] = v.y; t.v[4 * i + 2] = v.z; t.v[4 * i + 3] = v.w;
-    }
-  } else if constexpr (EX && LAY == LAY_R) {
-#pragma unroll
-    for (int i = 0; i < (ROWS + 127) / 128; ++i) {
-      const int b = tid + 256 * i;
-      const int kb = b / (ROWS / 4), r = (b % (ROWS / 4)) * 4;
-      if (ROWS >= 128 || b < 2 * ROWS) {
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const float4 v = *reinterpret_cast<const float4*>(X + (size_t)(k0 + 4 * kb + kk) * sk + r0 + r);
-          t.v[16 * i + kk] = v.x; t.v[16 * i + 4 + kk] = v.y;
-          t.v[16 * i + 8 + kk] = v.z; t.v[16 * i + 12 + kk] = v.w;
-        }
-      }
-    }
-  } else if constexpr (LAY == LAY_K) {
+  if constexpr (LAY == LAY_K) {
 #pragma unroll
     for (int i = 0; i < ROWS / 32; ++i) {
       const int e4 = tid + 256 * i;
@@ -255,62 +233,66 @@ __device__ __forceinline__ void store_tile(const TileRegs<ROWS>& t, long long sr
   }
 }
 
-// register prefetch depth: deeper for the small tiles (the heads' latency-bound GEMMs), within
-// the VGPR budget of the large ones (128x256: 48 + 128 accumulator registers per stage set)
-template <int BM, int BN>
-struct Depth { static constexpr int P = BM * BN >= 128 * 256 ? 1 : (BM * BN >= 128 * 64 ? 2 : 4); };
+// One GEMM problem of a launch (the paired launch carries two).
+struct GemmArgs {
+  int M, N, K, kchunk;
+  const float* A;
+  long long sam, sak;
+  const float* B;
+  long long sbk, sbn;
+  float* C;
+  long long ldc;
+  const float* bias;
+  float alpha, beta;
+  float* ws;      // split-K partial tiles (nullptr: one pass over K)
+};
 
-template <int MODE, int BM, int BN, int LA, int LB, bool EX = false,
-          int P = EX ? Depth<BM, BN>::P : 1>
-__global__ __launch_bounds__(256) void gemm_mfma_kernel(
-    int M, int N, int K, int kchunk, const float* __restrict__ A, long long sam, long long sak,
-    const float* __restrict__ B, long long sbk, long long sbn, float* __restrict__ C, long long ldc,
-    const float* __restrict__ bias, float alpha, float beta, float* __restrict__ ws) {
+// LDS bytes of one tile body: double-buffered A and B k-tiles
+template <int MODE, int BM, int BN>
+struct GemmLds {
+  static constexpr int BYTES = 2 * (BM + BN) * GemmT<MODE>::LDK * (int)sizeof(typename GemmT<MODE>::T);
+};
+
+// One BM x BN output tile (tile column tn, tile row tm) over the k-chunk tz of problem p, staged
+// through the LDS block `smem` (GemmLds bytes).
+template <int MODE, int BM, int BN, int LA, int LB>
+__device__ __forceinline__ void gemm_tile(const GemmArgs& p, int tn, int tm, int tz, char* smem) {
   typedef typename GemmT<MODE>::T T;
   constexpr int LDK = GemmT<MODE>::LDK;
   constexpr int TI = BM / 32, TJ = BN / 32;   // MFMA tiles per wave
-  __shared__ __attribute__((aligned(16))) T As[2][BM * LDK];
-  __shared__ __attribute__((aligned(16))) T Bs[2][BN * LDK];
+  T (*As)[BM * LDK] = reinterpret_cast<T (*)[BM * LDK]>(smem);
+  T (*Bs)[BN * LDK] = reinterpret_cast<T (*)[BN * LDK]>(smem + 2 * BM * LDK * sizeof(T));
+  const int M = p.M, N = p.N, K = p.K;
+  const float* __restrict__ A = p.A;
+  const float* __restrict__ B = p.B;
+  const long long sam = p.sam, sak = p.sak, sbk = p.sbk, sbn = p.sbn;
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
   const int g = lane >> 4, r16 = lane & 15;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int kbeg = blockIdx.z * kchunk;
-  const int kend = min(K, kbeg + kchunk);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = tz * p.kchunk;
+  const int kend = min(K, kbeg + p.kchunk);
   f4 acc[TI][TJ];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  // P register stages of k-tiles in flight: tile kt+P is loaded while tile kt is stored to LDS
-  // and multiplied (the loop is latency-bound otherwise: one HBM round trip per 32-deep k-tile)
-  TileRegs<BM> ta[P];
-  TileRegs<BN> tb[P];
+  TileRegs<BM> ta;
+  TileRegs<BN> tb;
   const int nk = (kend - kbeg + 31) / 32;
-  // EX: every tile whole; loads past the last k-tile re-read the last one (clamped, never used)
-  auto kt_at = [&](int kt) { return kbeg + 32 * (EX ? min(kt, nk - 1) : kt); };
-#pragma unroll
-  for (int p = 0; p < P; ++p)
-    if (EX || p < nk) {
-      load_tile<BM, LA, EX>(A, sam, sak, m0, kt_at(p), M, kend, ta[p]);
-      load_tile<BN, LB, EX>(B, sbn, sbk, n0, kt_at(p), N, kend, tb[p]);   // B^T tile: rows = n
-    }
-  for (int kt0 = 0; kt0 < nk; kt0 += P) {
-#pragma unroll
-  for (int p = 0; p < P; ++p) {
-    const int kt = kt0 + p;
-    if (kt >= nk) break;
+  load_tile<BM, LA>(A, sam, sak, m0, kbeg, M, kend, ta);
+  load_tile<BN, LB>(B, sbn, sbk, n0, kbeg, N, kend, tb);   // B^T tile: rows = n
+  store_tile<MODE, BM, LA>(ta, sam, sak, As[0]);
+  store_tile<MODE, BN, LB>(tb, sbn, sbk, Bs[0]);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    // buffer cur was last read by tile kt-2's MFMAs, which every wave finished before the
-    // barrier of tile kt-1
-    store_tile<MODE, BM, LA>(ta[p], sam, sak, As[cur]);
-    store_tile<MODE, BN, LB>(tb[p], sbn, sbk, Bs[cur]);
-    __syncthreads();
-    if (EX || kt + P < nk) {
-      load_tile<BM, LA, EX>(A, sam, sak, m0, kt_at(kt + P), M, kend, ta[p]);
-      load_tile<BN, LB, EX>(B, sbn, sbk, n0, kt_at(kt + P), N, kend, tb[p]);
+    const bool more = kt + 1 < nk;
+    if (more) {
+      load_tile<BM, LA>(A, sam, sak, m0, kbeg + 32 * (kt + 1), M, kend, ta);
+      load_tile<BN, LB>(B, sbn, sbk, n0, kbeg + 32 * (kt + 1), N, kend, tb);
     }
     const T* as = As[cur] + (BM / 2 * wm + r16) * LDK;
     const T* bs = Bs[cur] + (BN / 2 * wn + r16) * LDK;
@@ -340,16 +322,20 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
       }
     }
+    if (more) {
+      store_tile<MODE, BM, LA>(ta, sam, sak, As[cur ^ 1]);
+      store_tile<MODE, BN, LB>(tb, sbn, sbk, Bs[cur ^ 1]);
+    }
+    __syncthreads();
   }
-  }
-  float* part = ws ? ws + (size_t)blockIdx.z * M * N : nullptr;
+  float* part = p.ws ? p.ws + (size_t)tz * M * N : nullptr;
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const int n = n0 + BN / 2 * wn + 16 * j + r16;
       if (n >= N) continue;
-      const float bv = (!part && bias) ? bias[n] : 0.f;
+      const float bv = (!part && p.bias) ? p.bias[n] : 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int m = m0 + BM / 2 * wm + 16 * i + 4 * g + e;
@@ -357,13 +343,37 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(
         if (part) {
           part[(size_t)m * N + n] = acc[i][j][e];
         } else {
-          float* c = C + (size_t)m * ldc + n;
-          float v = alpha * acc[i][j][e] + bv;
-          if (beta != 0.f) v += beta * *c;
+          float* c = p.C + (size_t)m * p.ldc + n;
+          float v = p.alpha * acc[i][j][e] + bv;
+          if (p.beta != 0.f) v += p.beta * *c;
           *c = v;
         }
       }
     }
+}
+
+template <int MODE, int BM, int BN, int LA, int LB>
+__global__ __launch_bounds__(256) void gemm_mfma_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) char smem[GemmLds<MODE, BM, BN>::BYTES];
+  gemm_tile<MODE, BM, BN, LA, LB>(p, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+}
+
+// Two independent problems in one grid (a Linear layer's weight gradient and input gradient
+// both read dout): blocks [0, nb1) run problem 1 on its (n1 x m1 x z1) tile grid, the rest
+// problem 2.  One launch boundary instead of two, and the two small grids fill the chip together.
+template <int MODE, int BM1, int BN1, int LA1, int LB1, int BM2, int BN2, int LA2, int LB2>
+__global__ __launch_bounds__(256) void gemm_pair_kernel(GemmArgs p1, int n1, int m1, GemmArgs p2,
+                                                        int n2, int m2) {
+  constexpr int L1 = GemmLds<MODE, BM1, BN1>::BYTES, L2 = GemmLds<MODE, BM2, BN2>::BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[L1 > L2 ? L1 : L2];
+  int b = blockIdx.x;
+  const int nb1 = n1 * m1 * (p1.ws ? avd_cdiv_d(p1.K, p1.kchunk) : 1);
+  if (b < nb1) {
+    gemm_tile<MODE, BM1, BN1, LA1, LB1>(p1, b % n1, (b / n1) % m1, b / (n1 * m1), smem);
+  } else {
+    b -= nb1;
+    gemm_tile<MODE, BM2, BN2, LA2, LB2>(p2, b % n2, (b / n2) % m2, b / (n2 * m2), smem);
+  }
 }
 
 // C = alpha * sum_{z < S} ws[z] (+bias) (+beta C), fixed split order
@@ -429,45 +439,37 @@ Plan plan_for(int M, int N, int K) {
   return p;
 }
 
-template <int MODE, int LA, int LB>
-void launch_gemm(const Plan& pl, int M, int N, int K, const float* A, long long sam, long long sak,
-                 const float* B, long long sbk, long long sbn, float* C, long long ldc,
-                 const float* bias, float alpha, float beta, float* ws, hipStream_t st) {
-  dim3 grid(avd_cdiv(N, pl.bn), avd_cdiv(M, pl.bm), pl.splits);
-  float* w = pl.splits > 1 ? ws : nullptr;
-  // whole tiles in every dimension (vector layouts, 16-byte aligned strides): the deep
-  // register-prefetch variant (AVDINO_GEMM_EX=1)
-  // (measured no faster than the checked variant at the step's shapes, profiles/r3_gemm_ab.txt: off)
-  static const bool ex_on = getenv("AVDINO_GEMM_EX") && atoi(getenv("AVDINO_GEMM_EX")) != 0;
-  const bool ex = ex_on && LA != LAY_S && LB != LAY_S && M % pl.bm == 0 && N % pl.bn == 0 &&
-                  K % 32 == 0 && pl.kchunk % 32 == 0;
-#define AVD_G(BM_, BN_)                                                                        \
-  if (pl.bm == BM_ && pl.bn == BN_) {                                                          \
-    if (ex)                                                                                    \
-      gemm_mfma_kernel<MODE, BM_, BN_, LA, LB, true><<<grid, 256, 0, st>>>(                    \
-          M, N, K, pl.kchunk, A, sam, sak, B, sbk, sbn, C, ldc, bias, alpha, beta, w);         \
-    else                                                                                       \
-      gemm_mfma_kernel<MODE, BM_, BN_, LA, LB, false><<<grid, 256, 0, st>>>(                   \
-          M, N, K, pl.kchunk, A, sam, sak, B, sbk, sbn, C, ldc, bias, alpha, beta, w);         \
+GemmArgs make_args(const Plan& pl, int M, int N, int K, const float* A, long long sam,
+                   long long sak, const float* B, long long sbk, long long sbn, float* C,
+                   long long ldc, const float* bias, float alpha, float beta, float* ws) {
+  return GemmArgs{M, N, K, pl.kchunk, A, sam, sak, B, sbk, sbn, C, ldc, bias, alpha, beta,
+                  pl.splits > 1 ? ws : nullptr};
+}
+
+void launch_splitk_reduce(const Plan& pl, const GemmArgs& a, hipStream_t st) {
+  if (pl.splits > 1) {
+    const long long MN = (long long)a.M * a.N;
+    const int blocks = (int)std::min<long long>(avd_cdiv(MN, 256), 4096);
+    splitk_reduce_kernel<<<blocks, 256, 0, st>>>(a.ws, pl.splits, a.M, a.N, a.C, a.ldc, a.bias,
+                                                 a.alpha, a.beta);
   }
+}
+
+template <int MODE, int LA, int LB>
+void launch_gemm(const Plan& pl, const GemmArgs& a, hipStream_t st) {
+  dim3 grid(avd_cdiv(a.N, pl.bn), avd_cdiv(a.M, pl.bm), pl.splits);
+#define AVD_G(BM_, BN_)                                                                        \
+  if (pl.bm == BM_ && pl.bn == BN_) gemm_mfma_kernel<MODE, BM_, BN_, LA, LB><<<grid, 256, 0, st>>>(a);
   AVD_G(128, 256) else AVD_G(128, 128) else AVD_G(128, 64) else AVD_G(64, 64)
 #undef AVD_G
-  if (pl.splits > 1) {
-    const long long MN = (long long)M * N;
-    const int blocks = (int)std::min<long long>(avd_cdiv(MN, 256), 4096);
-    splitk_reduce_kernel<<<blocks, 256, 0, st>>>(ws, pl.splits, M, N, C, ldc, bias, alpha, beta);
-  }
+  launch_splitk_reduce(pl, a, st);
 }
 
 // operand layouts are template parameters (the index math of the others would otherwise sit in
 // registers): K/R combinations get vector loads, anything with a scalar operand the generic path
 template <int MODE>
-void dispatch_gemm(const Plan& pl, int lA, int lB, int M, int N, int K, const float* A,
-                   long long sam, long long sak, const float* B, long long sbk, long long sbn,
-                   float* C, long long ldc, const float* bias, float alpha, float beta, float* ws,
-                   hipStream_t st) {
-#define AVD_L(LA_, LB_) launch_gemm<MODE, LA_, LB_>(pl, M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, \
-                                                   bias, alpha, beta, ws, st)
+void dispatch_gemm(const Plan& pl, int lA, int lB, const GemmArgs& a, hipStream_t st) {
+#define AVD_L(LA_, LB_) launch_gemm<MODE, LA_, LB_>(pl, a, st)
   if (lA == LAY_K && lB == LAY_K) AVD_L(LAY_K, LAY_K);
   else if (lA == LAY_K && lB == LAY_R) AVD_L(LAY_K, LAY_R);
   else if (lA == LAY_R && lB == LAY_R) AVD_L(LAY_R, LAY_R);
@@ -476,9 +478,75 @@ void dispatch_gemm(const Plan& pl, int lA, int lB, int M, int N, int K, const fl
 #undef AVD_L
 }
 
+// The paired Linear backward launch: problem 1 = dW [O, In] = dout^T x (A rows contiguous, B
+// rows contiguous), problem 2 = dX [rows, In] = dout W (A k-contiguous, B rows contiguous).
+// Tile plans served: dW 128x128 (every weight-gradient plan of the step), dX any of 128x128,
+// 128x64, 64x64; anything else returns false and the caller launches the two GEMMs separately.
+template <int MODE>
+bool launch_pair(const Plan& p1, const GemmArgs& a1, const Plan& p2, const GemmArgs& a2,
+                 hipStream_t st) {
+  if (p1.bm != 128 || p1.bn != 128) return false;
+  const int n1 = avd_cdiv(a1.N, p1.bn), m1 = avd_cdiv(a1.M, p1.bm);
+  const int n2 = avd_cdiv(a2.N, p2.bn), m2 = avd_cdiv(a2.M, p2.bm);
+  const int blocks = n1 * m1 * p1.splits + n2 * m2 * p2.splits;
+#define AVD_P(BM2_, BN2_)                                                                      \
+  if (p2.bm == BM2_ && p2.bn == BN2_) {                                                        \
+    gemm_pair_kernel<MODE, 128, 128, LAY_R, LAY_R, BM2_, BN2_, LAY_K, LAY_R>                   \
+        <<<blocks, 256, 0, st>>>(a1, n1, m1, a2, n2, m2);                                      \
+  }
+  AVD_P(128, 128) else AVD_P(128, 64) else AVD_P(64, 64) else return false;
+#undef AVD_P
+  launch_splitk_reduce(p1, a1, st);
+  launch_splitk_reduce(p2, a2, st);
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
+
+long long avd_linear_bwd_ws_elems(int rows, int O, int In, int mode) {
+  return avd_gemm_ws_elems(O, In, rows, mode) + avd_gemm_ws_elems(rows, In, O, mode);
+}
+
+int avd_linear_bwd(int rows, int O, int In, const float* dout, long long dout_ld, const float* x,
+                   long long x_ld, const float* W, float* dW, float* dX, long long dx_ld, int mode,
+                   float* ws, long long ws_elems, void* stream) {
+  if (!dout || !x || !W || !dW || !dX) return AVD_ERR_ARG;
+  if (rows <= 0 || O <= 0 || In <= 0 || dout_ld < O || x_ld < In || dx_ld < In) return AVD_ERR_SHAPE;
+  if (mode != 1 && mode != 2) return AVD_ERR_ARG;
+  hipStream_t st = avd_stream(stream);
+  Plan p1 = plan_for(O, In, rows), p2 = plan_for(rows, In, O);
+  const long long w1 = p1.splits > 1 ? (long long)p1.splits * O * In : 0;
+  const long long w2 = p2.splits > 1 ? (long long)p2.splits * rows * In : 0;
+  if (!ws || ws_elems < w1 + w2) {   // no (or too small a) workspace: single passes over K
+    if (p1.splits > 1) { p1.splits = 1; p1.kchunk = rows; }
+    if (p2.splits > 1) { p2.splits = 1; p2.kchunk = O; }
+  }
+  // dW[o, i] = sum_r dout[r, o] x[r, i]; dX[r, i] = sum_o dout[r, o] W[o, i]
+  const GemmArgs a1 = make_args(p1, O, In, rows, dout, 1, dout_ld, x, x_ld, 1, dW, In, nullptr,
+                                1.f, 0.f, ws);
+  const GemmArgs a2 = make_args(p2, rows, In, O, dout, dout_ld, 1, W, In, 1, dX, dx_ld, nullptr,
+                                1.f, 0.f, p1.splits > 1 ? ws + w1 : ws);
+  const bool lay = lay_of(dout, 1, dout_ld) == LAY_R && lay_of(x, 1, x_ld) == LAY_R &&
+                   lay_of(dout, dout_ld, 1) == LAY_K && lay_of(W, 1, In) == LAY_R;
+  bool done = false;
+  if (lay)
+    done = mode == 1 ? launch_pair<1>(p1, a1, p2, a2, st) : launch_pair<2>(p1, a1, p2, a2, st);
+  if (!done) {
+    const int l1a = lay_of(dout, 1, dout_ld), l1b = lay_of(x, 1, x_ld);
+    const int l2a = lay_of(dout, dout_ld, 1), l2b = lay_of(W, 1, In);
+    if (mode == 1) {
+      dispatch_gemm<1>(p1, l1a, l1b, a1, st);
+      dispatch_gemm<1>(p2, l2a, l2b, a2, st);
+    } else {
+      dispatch_gemm<2>(p1, l1a, l1b, a1, st);
+      dispatch_gemm<2>(p2, l2a, l2b, a2, st);
+    }
+  }
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
 
 long long avd_gemm_ws_elems(int M, int N, int K, int mode) {
   if (mode != 1 && mode != 2) return 0;
@@ -505,10 +573,11 @@ int avd_gemm(int M, int N, int K, const float* A, long long sam, long long sak, 
     }
     const int lA = lay_of(A, sam, sak);
     const int lB = lay_of(B, sbn, sbk);
+    const GemmArgs a = make_args(pl, M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, bias, alpha, beta, ws);
     if (mode == 1)
-      dispatch_gemm<1>(pl, lA, lB, M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, bias, alpha, beta, ws, st);
+      dispatch_gemm<1>(pl, lA, lB, a, st);
     else
-      dispatch_gemm<2>(pl, lA, lB, M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, bias, alpha, beta, ws, st);
+      dispatch_gemm<2>(pl, lA, lB, a, st);
   } else {
     return AVD_ERR_ARG;
   }

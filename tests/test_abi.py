@@ -42,7 +42,7 @@ def test_host_helpers():
     assert lib.avd_cl_wgrad_chunks(7168, 16, 8, 5) == 512
     assert lib.avd_cl_wgrad_chunks(7168, 64, 32, 5) == 256
     assert lib.avd_cl_wgrad_chunks(12, 16, 8, 5) == 12
-    assert lib.avd_colstats_parts(6144) == 96
+    assert lib.avd_colstats_parts(6144) == 384       # 16-row partials
 
 
 def test_argument_validation_without_launch():

@@ -374,3 +374,28 @@ def test_sum_rows_split_matches_f64(ops, rows, cols, ld, off):
     ops.sum_rows(tx, rows, cols, acc, accumulate=1, ld=ld, off=off)
     assert rel(host(acc), want + base) < 1e-6
     assert lib.avd_sum_rows_chunks(rows, cols) >= 1
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("rows,O_,In", [(1024, 128, 512), (1024, 512, 256), (6144, 256, 512),
+                                        (2048, 256, 1600)])
+def test_linear_bwd_pair_launch_equals_two_gemms(ops, monkeypatch, mode, rows, O_, In):
+    """avd_linear_bwd (dW and dX tile grids in one launch, split-K where the plans split) gives
+    bitwise the dW / dX / db of the two separate avd_gemm launches; dX lands in a column slice
+    of a wider buffer as the heads' backward writes it (dcat)."""
+    g = np.random.default_rng(rows + O_ + In + mode)
+    dout = dev(g.normal(size=(rows, O_)).astype(np.float32))
+    x = dev(g.normal(size=(rows, In)).astype(np.float32))
+    w = dev(g.normal(size=(O_, In)).astype(np.float32))
+    res = []
+    for pair in (False, True):
+        monkeypatch.setattr(ops, "PAIR_BWD", pair)
+        dw, db = torch.empty(O_, In, device="cuda"), torch.empty(O_, device="cuda")
+        dx = torch.zeros(rows, 2 * In, device="cuda")
+        ops.linear_bwd(dout, x, w, dw, db, dx, rows, dx_ld=2 * In, dx_off=In, mode=mode)
+        res.append((dw, db, dx))
+    (a, b, c), (a2, b2, c2) = res
+    assert torch.equal(a, a2) and torch.equal(b, b2) and torch.equal(c, c2)
+    assert c2[:, :In].abs().max().item() == 0
+    ref = host(dout).astype(np.float64).T @ host(x).astype(np.float64)
+    assert rel(host(a2), ref) < (1e-6 if mode == 1 else 1e-2)
