@@ -521,6 +521,28 @@ int avd_cl_c1_codes_combine(const float* moments, const void* wk, const float* b
                             long long count, float* dw, float* dgamma, float* dbeta, float* dbias,
                             float* coef, int G, void* stream);
 
+/* ---- the same routed backward for the IMAGE conv1 (c1w3.hip pass 1 + c1r5.hip; CentralUnimodalImage
+ * conv1 -> bn1 -> relu -> maxpool, unimodal.py:127-141, 5x5 1->32 on 28x28, bf16).
+ * avd_cl_c1r5_apply_codes = avd_cl_c1_recompute pass 1 that also writes codes [N][14][14][8] u16:
+ * word q of a window holds channels 4q..4q+3, nibble i (bits 4i..4i+3) = 1 + the window position
+ * ((0,0),(0,1),(1,0),(1,1)) of the first argmax of relu(bn(y)) when that max is > 0, else 0.
+ * avd_cl_c1r5_moments_codes: ONE pass over x, gz [N][14][14][32] and the codes -> per (row r,
+ * group g) of avd_cl_c1r5_codes_rows rows, avd_cl_c1r5_codes_cols() floats: M[32][25] |
+ * Gram[25][25] | S[25] | sum dz[32] at out[(r * G + g) * cols + ...] (reduce with avd_sum_rows);
+ * the taps come from shifted copies of the image (no im2col gather).
+ * avd_cl_c1r5_codes_combine: as avd_cl_c1_codes_combine for the 32 channels (G <= 8). */
+int avd_cl_c1r5_codes_rows(int N, int B, int H, int W);
+int avd_cl_c1r5_codes_cols(void);
+int avd_cl_c1r5_apply_codes(const void* x, const void* wk, const float* bias, const float* scale,
+                            const float* shift, void* z, unsigned short* codes, int N, int B, int H,
+                            int W, void* stream);
+int avd_cl_c1r5_moments_codes(const void* x, const void* gz, const unsigned short* codes, float* out,
+                              int N, int B, int H, int W, void* stream);
+int avd_cl_c1r5_codes_combine(const float* moments, const void* wk, const float* bias,
+                              const float* gamma, const float* mean, const float* invstd,
+                              long long count, float* dw, float* dgamma, float* dbeta, float* dbias,
+                              float* coef, int G, void* stream);
+
 /* Timeline mark: marks[idx] = the device real-time counter (100 MHz ticks) when the stream
  * reaches this launch (tools: phase timing of a replayed step without a profiler). */
 int avd_mark(unsigned long long* marks, int idx, void* stream);

@@ -230,15 +230,24 @@ class ConvBranch:
         return (rc and self.act == torch.bfloat16 and
                 ops.cl_c1_recompute_rows(ops.C1_STATS, self.act, N, B, ci, H, H, co, k, pad) > 0)
 
-    # the 5x5 audio conv1's backward from the forward's routing codes (avd_cl_c1_moments_codes):
-    # AVDINO_C1_CODES=0 keeps the recomputing moments pass (pass 4)
+    # the 5x5 conv1 backwards from the forward's routing codes: the audio conv1 (1->8 at 112^2,
+    # avd_cl_c1_moments_codes) and the image conv1 (1->32 at 28^2, avd_cl_c1r5_moments_codes);
+    # AVDINO_C1_CODES=0 keeps the recomputing moments pass (pass 4) for both
     CODES = os.environ.get("AVDINO_C1_CODES", "1") == "1"
 
     def _codes_ok(self, N, B, need_dgrad):
+        """"audio" / "image" when the first layer's training backward is the routed moments pass,
+        else None."""
         ci, co, k, pad = self.stack.convs[0]
         H = self.dims[0][0]
-        return (self.CODES and need_dgrad and self.act == torch.bfloat16 and (ci, co, k, pad) == (1, 8, 5, 2)
-                and ops.c1_codes_rows(N, B, H, H) > 0)
+        if not (self.CODES and need_dgrad and self.act == torch.bfloat16):
+            return None
+        if (ci, co, k, pad) == (1, 8, 5, 2) and ops.c1_codes_rows(N, B, H, H) > 0:
+            return "audio"
+        if ((ci, co, k, pad) == (1, 32, 5, 2) and ops.c1r5_codes_rows(N, B, H, H) > 0 and
+                ops.cl_c1_recompute_rows(ops.C1_APPLY, self.act, N, B, ci, H, H, co, k, pad) > 0):
+            return "image"
+        return None
 
     def _first_layer_recompute_fwd(self, ws, store, tag, ctx, x, N, G, B, update_running,
                                    need_dgrad=True):
@@ -258,12 +267,17 @@ class ConvBranch:
         if update_running:
             store.bump_nbt(bk + ".num_batches_tracked", G)
         out = ws.get(f"{tag}.x1", N * Hp * Hp * co, self.act)
-        if self._codes_ok(N, B, need_dgrad):
+        route = self._codes_ok(N, B, need_dgrad)
+        if route == "audio":
             # training forward: the pooling pass also records where each window's gradient goes
             # (routing codes), so the backward needs neither y nor a recompute of it
             codes = ws.get(f"{tag}.c1codes", N * Hp * Hp, torch.int32)
             ops.c1_apply_codes(x, wk, bias, st[2], st[3], out, codes, N, B, H, H)
-            ctx["codes"] = codes
+            ctx["codes"] = (route, codes)
+        elif route == "image":
+            codes = ws.get(f"{tag}.c1codes", N * Hp * Hp * 8, torch.int16)
+            ops.c1r5_apply_codes(x, wk, bias, st[2], st[3], out, codes, N, B, H, H)
+            ctx["codes"] = (route, codes)
         else:
             ops.cl_c1_recompute(ops.C1_APPLY, x, wk, bias, N, B, ci, H, H, co, k, pad, scale=st[2],
                                 shift=st[3], z=out)
@@ -280,15 +294,19 @@ class ConvBranch:
         bias = store[ck + ".bias"]
         if ctx.get("codes") is not None:
             # one pass over x, the pooled gradient and the routing codes; a float64 combine forms
-            # the BN backward and dW from the moments (avd_cl_c1_codes_combine)
-            Rc, mc = ops.c1_codes_rows(N, B, H, H), ops.c1_codes_cols()
+            # the BN backward and dW from the moments (avd_cl_c1_codes_combine / c1r5)
+            route, codes = ctx["codes"]
+            img = route == "image"
+            Rc = (ops.c1r5_codes_rows if img else ops.c1_codes_rows)(N, B, H, H)
+            mc = ops.c1r5_codes_cols() if img else ops.c1_codes_cols()
             parts = ws.get("c1_codes_parts", Rc * G * mc)
-            ops.c1_moments_codes(x, gout, ctx["codes"], parts, N, B, H, H)
+            (ops.c1r5_moments_codes if img else ops.c1_moments_codes)(x, gout, codes, parts, N, B, H, H)
             mom = ws.get("c1_codes_mom", G * mc)
             ops.sum_rows(parts, Rc, G * mc, mom)
-            ops.c1_codes_combine(mom, wk, bias, store[bk + ".weight"], st[0], st[1], B * Ho * Ho,
-                                 store.grad_of(ck + ".weight"), store.grad_of(bk + ".weight"),
-                                 store.grad_of(bk + ".bias"), store.grad_of(ck + ".bias"), None, G)
+            (ops.c1r5_codes_combine if img else ops.c1_codes_combine)(
+                mom, wk, bias, store[bk + ".weight"], st[0], st[1], B * Ho * Ho,
+                store.grad_of(ck + ".weight"), store.grad_of(bk + ".weight"),
+                store.grad_of(bk + ".bias"), store.grad_of(ck + ".bias"), None, G)
             return
         R4 = ops.cl_c1_recompute_rows(ops.C1_REDUCE_MOMENTS, self.act, N, B, ci, H, H, co, k, pad)
         if self.RC_MOMENTS and R4 > 0:

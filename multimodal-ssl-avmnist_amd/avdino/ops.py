@@ -577,6 +577,50 @@ def c1_codes_combine(moments, wk, bias, gamma, mean, invstd, count, dw, dgamma, 
          p(dw), p(dgamma), p(dbeta), p(dbias), p(coef), G, stream())
 
 
+# ---- the image conv1 backward routed by forward codes (include/avdino.h avd_cl_c1r5_*)
+def c1r5_codes_rows(N, B, H, W):
+    """Rows per BN group of avd_cl_c1r5_moments_codes (0 = shape not served)."""
+    return lib.avd_cl_c1r5_codes_rows(N, B, H, W)
+
+
+def c1r5_codes_cols():
+    return lib.avd_cl_c1r5_codes_cols()
+
+
+def c1r5_apply_codes(x, wk, bias, scale, shift, z, codes, N, B, H, W):
+    """BN -> ReLU -> 2x2 max-pool of the recomputed image conv1 output (c1r3 pass 1) plus the
+    routing codes [N, H/2, W/2, 8] (int16 storage of the u16 nibble words)."""
+    npool = N * (H // 2) * (W // 2)
+    _need(c1r5_codes_rows(N, B, H, W) > 0 and x.numel() == N * H * W and x.dtype == torch.bfloat16,
+          "c1r5 codes shape")
+    _need(z.numel() == npool * 32 and z.dtype == x.dtype, "c1r5 codes z")
+    _need(codes.numel() >= npool * 8 and codes.element_size() == 2, "c1r5 codes buffer")
+    _timed(f"c1r5_apply_codes[{N}x{H}x{W}x1->32 k5]", x.numel() * 2 + npool * 80, 2 * N * H * W * 32 * 25,
+           lambda: call("avd_cl_c1r5_apply_codes", p(x), p(wk), p(bias), p(scale), p(shift), p(z),
+                        p(codes), N, B, H, W, stream()))
+
+
+def c1r5_moments_codes(x, gz, codes, out, N, B, H, W):
+    """One pass over x, the pooled gradient and the codes -> moment rows [R][G][cols]."""
+    R = c1r5_codes_rows(N, B, H, W)
+    npool = N * (H // 2) * (W // 2)
+    _need(R > 0 and x.numel() == N * H * W and x.dtype == torch.bfloat16, "c1r5 moments codes shape")
+    _need(gz.numel() == npool * 32 and gz.dtype == x.dtype and codes.numel() >= npool * 8,
+          "c1r5 moments gz/codes")
+    _need(out.numel() >= R * (N // B) * c1r5_codes_cols(), "c1r5 moments rows")
+    # algorithmic work: dz x (32 x 26 per pixel, dense over the routed map) + the patch Gram
+    fl = 2 * N * H * W * (32 * 26 + 26 * 26)
+    _timed(f"c1r5_moments_codes[{N}x{H}x{W}x1->32 k5]", x.numel() * 2 + npool * 80, fl,
+           lambda: call("avd_cl_c1r5_moments_codes", p(x), p(gz), p(codes), p(out), N, B, H, W, stream()))
+
+
+def c1r5_codes_combine(moments, wk, bias, gamma, mean, invstd, count, dw, dgamma, dbeta, dbias, coef, G):
+    """bn1 backward + image conv1 bias / weight gradients from the row-summed moments."""
+    _need(moments.numel() >= G * c1r5_codes_cols() and dw.numel() >= 800 and G <= 8, "c1r5 codes combine")
+    call("avd_cl_c1r5_codes_combine", p(moments), p(wk), p(bias), p(gamma), p(mean), p(invstd),
+         int(count), p(dw), p(dgamma), p(dbeta), p(dbias), p(coef), G, stream())
+
+
 _SUM_WS = {}
 _SUM_SPLIT = os.environ.get("AVDINO_SUMROWS_SPLIT", "1") == "1"   # 0: single pass (A/B runs)
 

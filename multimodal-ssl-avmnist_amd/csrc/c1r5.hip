@@ -1,0 +1,381 @@
+// The CentralNet IMAGE conv1 backward routed by forward codes (CentralUnimodalImage conv1 -> bn1
+// -> relu -> maxpool, unimodal.py:127-141: Conv2d(1, 32, 5, padding=2) on 28x28 images, bf16).
+//
+// The forward's BN -> ReLU -> pool pass (c1r3_kernel pass 1 with codes, c1w3.hip) writes, per
+// pooling window and channel, where nn.MaxPool2d's gradient goes (nibble = 1 + the window
+// position of the first argmax of relu(bn(y)) when that max is > 0, else 0).  The backward of
+// conv1 + bn1 is then linear in three moments of the input patches x25 (as the audio conv1's,
+// conv_c1p.hip): dy = k1 dz + kx y + k0 and y = w . x25 + b give
+//   dW[c][t] = sum_g k1 M[g][c][t] + kx (sum_t' w[c][t'] Gram[g][t'][t] + b[c] S[g][t]) + k0 S[g][t]
+//   sum dz y = w . M + b sum dz     (the BN backward's second sum, at the exact conv output)
+// with M = sum dz x25, Gram = sum x25 x25^T, S = sum x25 per BN group.  This pass forms them with
+// no y, no argmax and no im2col gather (the recomputing pass 4 of c1r3_kernel spends its time
+// there: 25 scalar LDS reads per pixel):
+//   * GEMM view M = dZ^T X over K = pixels: a 32-pixel k-block is one image row on a 32-column
+//     virtual width (columns 28..31 zero), so a lane's 8 consecutive k of X for tap (ty, tx) are
+//     8 consecutive pixels of ONE row of a shifted copy of the image -- one aligned ds_read_b128
+//     from copy[tx][row + ty], no gather.  Five copies (tx = -2..2, columns >= 28 zeroed) plus a
+//     constant "ones" copy (tap 25: sum dz and S come out of the same MFMAs) are built per sample.
+//   * dZ is channel-major in LDS ([32][28][32]): dz = gz at the coded pixel of each window, 0 at
+//     the other three -- an A fragment is one ds_read_b128 of 8 pixels of one channel.
+//   * per image row: 2 channel tiles x 2 tap tiles of D += dZ X and the Gram tiles (0,0) (0,1)
+//     (1,1) (the X fragment is its own transpose's A operand): 7 MFMAs, 4 LDS reads.
+// Blocks own contiguous sample ranges of one BN group (G x R blocks); each writes one row of
+// MOMC5 = M [32][25] | Gram [25][25] | S [25] | sum dz [32] floats, reduced with avd_sum_rows.
+#include <algorithm>
+
+#include "common.h"
+
+using namespace avd;
+
+namespace {
+
+constexpr int C = 32, KK = 25, IH = 28, IW = 28, VW = 32;   // channels, taps, image, virtual width
+constexpr int HP = IH / 2, WP = IW / 2, NWIN = HP * WP;     // pooling windows per sample
+constexpr int MOMC5 = C * KK + KK * KK + KK + C;
+constexpr int NCOPY = 6, CROWS = IH + 4;                     // copies: tx = -2..2, ones; rows: pad 2
+constexpr int XS_R = IH + 4, XS_C = IW + 4 + 4;              // staged image, 2-pixel halo (+ pad)
+constexpr int LDS_X = XS_R * XS_C;                           // bf16 elements
+constexpr int LDS_CP = NCOPY * CROWS * VW;
+constexpr int LDS_DZ = C * IH * VW;
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f4;
+typedef __attribute__((ext_vector_type(4))) unsigned u4;
+
+// per-thread global vectors of one sample: x 98, gz 784, codes 196 (16-byte vectors)
+constexpr int NXV = IH * IW / 8, NGV = NWIN * C / 8, NCV = NWIN * 8 / 8;
+constexpr int NVEC = NXV + NGV + NCV, VPT = (NVEC + 255) / 256;
+
+__global__ __launch_bounds__(256, 2) void c1r5_moments_codes_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ gz, const unsigned short* __restrict__ codes,
+    float* __restrict__ out, int B, int G, int R) {
+  __shared__ __attribute__((aligned(16))) bf16 xs[LDS_X];
+  __shared__ __attribute__((aligned(16))) bf16 cp[LDS_CP];
+  __shared__ __attribute__((aligned(16))) bf16 dz[LDS_DZ];
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int grp = (int)blockIdx.x / R, rr = (int)blockIdx.x - grp * R;
+  const int s_begin = grp * B + (int)(((long long)B * rr) / R);
+  const int s_end = grp * B + (int)(((long long)B * (rr + 1)) / R);
+
+  // constant parts: zero halo of the staged image, zero virtual columns of dZ, the ones copy
+  for (int i = tid; i < LDS_X / 8; i += 256) reinterpret_cast<u4*>(xs)[i] = u4{0u, 0u, 0u, 0u};
+  for (int i = tid; i < LDS_DZ / 8; i += 256) reinterpret_cast<u4*>(dz)[i] = u4{0u, 0u, 0u, 0u};
+  for (int i = tid; i < CROWS * VW / 8; i += 256) {
+    const int row = i / (VW / 8), seg = i - row * (VW / 8);
+    const bool rv = row >= 2 && row < IH + 2;
+    u4 v;
+    unsigned* vw = reinterpret_cast<unsigned*>(&v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c0 = 8 * seg + 2 * k;
+      const unsigned lo = (rv && c0 < IW) ? 0x3F80u : 0u, hi = (rv && c0 + 1 < IW) ? 0x3F80u : 0u;
+      vw[k] = lo | (hi << 16);
+    }
+    reinterpret_cast<u4*>(cp + 5 * CROWS * VW)[i] = v;
+  }
+
+  // this lane's taps: tile 0 = taps 0..15, tile 1 = taps 16..31 (25 = ones, > 25 = zero)
+  int toff[2];
+  bool tzero[2];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const int t = 16 * tt + r16;
+    tzero[tt] = t > KK;
+    if (t < KK) {
+      const int ty = t / 5 - 2, tx = t % 5 - 2;
+      toff[tt] = (tx + 2) * CROWS * VW + (ty + 2) * VW + 8 * g;
+    } else {
+      toff[tt] = 5 * CROWS * VW + 2 * VW + 8 * g;   // ones copy, row offset 0 (rows start at 2)
+    }
+  }
+
+  f4 acc[2][2], ga[3];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int b = 0; b < 3; ++b) ga[b] = f4{0.f, 0.f, 0.f, 0.f};
+
+  u4 vv[VPT];
+  auto load = [&](int n) {
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int e = tid + 256 * j;
+      if (e < NXV) vv[j] = ldg16(x + (size_t)n * IH * IW + 8 * e);
+      else if (e < NXV + NGV) vv[j] = ldg16(gz + (size_t)n * NWIN * C + 8 * (e - NXV));
+      else if (e < NVEC) vv[j] = ldg16(codes + (size_t)n * NWIN * 8 + 8 * (e - NXV - NGV));
+    }
+  };
+  if (s_begin < s_end) load(s_begin);
+  __syncthreads();
+  for (int n = s_begin; n < s_end; ++n) {
+    // ---- the sample's image into the halo'd staging buffer; gz / codes stay in registers
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int e = tid + 256 * j;
+      if (e < NXV) {
+        // 8 pixels may straddle a row (28 = 3.5 vectors), a pixel pair never does (28 even):
+        // one dword store per pair, 4-byte aligned (XS_C and the column are even)
+        const unsigned w4[4] = {vv[j].x, vv[j].y, vv[j].z, vv[j].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int pix = 8 * e + 2 * k, r = pix / IW, c = pix - r * IW;
+          *reinterpret_cast<unsigned*>(xs + (r + 2) * XS_C + c + 2) = w4[k];
+        }
+      }
+    }
+    __syncthreads();                      // xs complete; the previous sample's k-loop is done
+    // the sample's codes to LDS (a gz vector's window codes sit in another thread's vector):
+    // 3136 B in the space of copies 3-4, which are rebuilt after the codes are consumed
+    unsigned short* cst = reinterpret_cast<unsigned short*>(cp + 3 * CROWS * VW);
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int e = tid + 256 * j;
+      if (e >= NXV + NGV && e < NVEC) reinterpret_cast<u4*>(cst)[e - NXV - NGV] = vv[j];
+    }
+    __syncthreads();
+    // dZ: the routed pooled gradient at the coded pixel of every (window, channel), 0 at the
+    // window's other three pixels (each gz vector = one window x 8 channels)
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int e = tid + 256 * j;
+      if (e >= NXV && e < NXV + NGV) {
+        const int q = e - NXV, w = q >> 2, c0 = 8 * (q & 3);
+        const int hp = w / WP, wp = w - hp * WP;
+        const unsigned gw[4] = {vv[j].x, vv[j].y, vv[j].z, vv[j].w};
+        const unsigned short k0 = cst[w * 8 + (c0 >> 2)], k1 = cst[w * 8 + (c0 >> 2) + 1];
+#pragma unroll
+        for (int cc = 0; cc < 8; ++cc) {
+          const unsigned nib = ((cc < 4 ? k0 : k1) >> (4 * (cc & 3))) & 0xFu;
+          const unsigned gv = (gw[cc >> 1] >> (16 * (cc & 1))) & 0xffffu;
+          bf16* d = dz + ((c0 + cc) * IH + 2 * hp) * VW + 2 * wp;
+          // row 2hp: positions 1, 2 (k = 0, 1); row 2hp+1: positions 3, 4 (k = 2, 3)
+          const unsigned r0 = (nib == 1u ? gv : 0u) | ((nib == 2u ? gv : 0u) << 16);
+          const unsigned r1 = (nib == 3u ? gv : 0u) | ((nib == 4u ? gv : 0u) << 16);
+          *reinterpret_cast<unsigned*>(d) = r0;
+          *reinterpret_cast<unsigned*>(d + VW) = r1;
+        }
+      }
+    }
+    __syncthreads();                      // codes consumed: copies 3-4 may be rebuilt
+    if (n + 1 < s_end) load(n + 1);       // in flight under this sample's copies and MFMAs
+    // ---- the five shifted copies: copy[tx][row][col] = col < 28 ? x[row - 2][col + tx] : 0
+    for (int i = tid; i < 5 * CROWS * (VW / 8); i += 256) {
+      const int ci = i / (CROWS * (VW / 8)), rem = i - ci * (CROWS * (VW / 8));
+      const int row = rem / (VW / 8), seg = rem - row * (VW / 8);
+      const bf16* srow = xs + row * XS_C + ci;                    // xs col = col + tx + 2
+      u4 v;
+      unsigned* vw = reinterpret_cast<unsigned*>(&v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c0 = 8 * seg + 2 * k;
+        const unsigned lo = c0 < IW ? (unsigned)srow[c0] : 0u;
+        const unsigned hi = c0 + 1 < IW ? (unsigned)srow[c0 + 1] : 0u;
+        vw[k] = lo | (hi << 16);
+      }
+      reinterpret_cast<u4*>(cp)[i] = v;
+    }
+    __syncthreads();
+    // ---- k-loop: image rows, a wave every fourth one
+    for (int r = wave; r < IH; r += 4) {
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(dz + (r16 * IH + r) * VW + 8 * g);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(dz + ((16 + r16) * IH + r) * VW + 8 * g);
+      const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(cp + toff[0] + r * VW);
+      bf16x8 x1 = *reinterpret_cast<const bf16x8*>(cp + toff[1] + r * VW);
+      if (tzero[1]) x1 = bf16x8{};
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, x0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, x1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, x0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, x1, acc[1][1], 0, 0, 0);
+      ga[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, x0, ga[0], 0, 0, 0);
+      ga[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, x1, ga[1], 0, 0, 0);
+      ga[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, x1, ga[2], 0, 0, 0);
+    }
+    __syncthreads();                      // the k-loop is done with cp / dz before the next sample
+  }
+
+  // ---- block row: reduce the four waves' accumulators through LDS (dz is free now)
+  float* red = reinterpret_cast<float*>(dz);          // [4][32 ch][32 taps]  D
+  float* gr = red + 4 * C * 32;                       // [4][32][32]          Gram tiles
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        red[(wave * C + 16 * a + 4 * g + i) * 32 + 16 * b + r16] = acc[a][b][i];
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const int ti = b == 2 ? 1 : 0, tj = b == 0 ? 0 : 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) gr[(wave * 32 + 16 * ti + 4 * g + i) * 32 + 16 * tj + r16] = ga[b][i];
+  }
+  __syncthreads();
+  auto gv = [&](int t1, int t2) {          // the lower block (1,0) is the transpose of (0,1)
+    if (t1 >= 16 && t2 < 16) { const int tmp = t1; t1 = t2; t2 = tmp; }
+    float v = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < 4; ++wv) v += gr[(wv * 32 + t1) * 32 + t2];
+    return v;
+  };
+  float* o = out + ((size_t)rr * G + grp) * MOMC5;
+  for (int e = tid; e < MOMC5; e += 256) {
+    float v = 0.f;
+    if (e < C * KK) {
+      const int c = e / KK, t = e - c * KK;
+#pragma unroll
+      for (int wv = 0; wv < 4; ++wv) v += red[(wv * C + c) * 32 + t];
+    } else if (e < C * KK + KK * KK) {
+      const int q = e - C * KK, a = q / KK, b = q - a * KK;
+      v = gv(a, b);
+    } else if (e < C * KK + KK * KK + KK) {
+      v = gv(e - C * KK - KK * KK, KK);
+    } else {
+      const int c = e - (C * KK + KK * KK + KK);
+#pragma unroll
+      for (int wv = 0; wv < 4; ++wv) v += red[(wv * C + c) * 32 + KK];
+    }
+    o[e] = v;
+  }
+}
+
+// BN backward + dW of the layer from the row-summed routed moments m [G][MOMC5], float64:
+//   sum dz y = w . M + b sum dz;  sum dz xhat = (sum dz y - mean sum dz) invstd;
+//   coef (k1, kx, k0) as avd_bn_bwd_finalize;  dW[c][t] = sum_g k1 M + kx (w Gram + b S) + k0 S;
+//   dgamma / dbeta / dbias (= sum dy) summed over the groups.
+__global__ __launch_bounds__(256) void c1r5_codes_combine_kernel(
+    const float* __restrict__ m, const bf16* __restrict__ wk, const float* __restrict__ bias,
+    const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
+    long long count, float* __restrict__ dw, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    float* __restrict__ dbias, float* __restrict__ coef, int G) {
+  __shared__ double sk[8 * C][3];
+  __shared__ double s12[8 * C][2];
+  const int tid = threadIdx.x;
+  const double n = (double)count;
+  if (tid < G * C) {
+    const int gq = tid / C, c = tid - gq * C;
+    const float* mg = m + (size_t)gq * MOMC5;
+    const double b = bias ? (double)bias[c] : 0.0;
+    const double s1 = mg[C * KK + KK * KK + KK + c];
+    double sy = b * s1;
+    for (int t = 0; t < KK; ++t) sy = fma((double)bf2f(wk[c * 32 + t]), (double)mg[c * KK + t], sy);
+    const double mu = mean[gq * C + c], is = invstd[gq * C + c], ga = gamma[c];
+    const double s2 = (sy - mu * s1) * is;                   // sum dz * xhat
+    const double k1 = ga * is, kx = -ga * is * is * s2 / n, k0 = -ga * is * s1 / n + ga * is * is * mu * s2 / n;
+    sk[tid][0] = k1; sk[tid][1] = kx; sk[tid][2] = k0;
+    s12[tid][0] = s1; s12[tid][1] = s2;
+    if (coef) {
+      coef[tid * 3 + 0] = (float)k1;
+      coef[tid * 3 + 1] = (float)kx;
+      coef[tid * 3 + 2] = (float)k0;
+    }
+  }
+  __syncthreads();
+  if (tid < C) {
+    double dg = 0.0, db = 0.0, dbi = 0.0;
+    for (int gq = 0; gq < G; ++gq) {
+      const int i = gq * C + tid;
+      const double mu = mean[i];
+      dg += s12[i][1];
+      db += s12[i][0];
+      dbi += sk[i][0] * s12[i][0] + sk[i][1] * mu * n + sk[i][2] * n;
+    }
+    if (dgamma) dgamma[tid] = (float)dg;
+    if (dbeta) dbeta[tid] = (float)db;
+    if (dbias) dbias[tid] = (float)dbi;
+  }
+  for (int e = tid; e < C * KK; e += 256) {
+    const int c = e / KK, t = e - c * KK;
+    double wr[KK];
+#pragma unroll
+    for (int k = 0; k < KK; ++k) wr[k] = (double)bf2f(wk[c * 32 + k]);
+    const double b = bias ? (double)bias[c] : 0.0;
+    double acc = 0.0;
+    for (int gq = 0; gq < G; ++gq) {
+      const float* mg = m + (size_t)gq * MOMC5;
+      const float* gram = mg + C * KK;
+      const double sx = gram[KK * KK + t];
+      double sy = b * sx;
+#pragma unroll
+      for (int k = 0; k < KK; ++k) sy = fma(wr[k], (double)gram[k * KK + t], sy);
+      const int i = gq * C + c;
+      acc += sk[i][0] * mg[e] + sk[i][1] * sy + sk[i][2] * sx;
+    }
+    dw[e] = (float)acc;
+  }
+}
+
+int c1r5_rows(int N, int B) {
+  static int resident = 0;
+  if (!resident) {
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, c1r5_moments_codes_kernel, 256, 0) !=
+            hipSuccess || per <= 0)
+      per = 2;
+    resident = cus * per;
+  }
+  const int G = N / B;
+  // one resident wave of blocks over the G groups, at least 4 samples per block
+  return std::max(1, std::min(grid_cap(resident) / G, B / 4));
+}
+
+}  // namespace
+
+extern "C" {
+
+// shape served: Cin 1, Cout 32, 5x5 pad 2 on 28x28, bf16 (the CentralNet image conv1)
+int avd_cl_c1r5_codes_rows(int N, int B, int H, int W) {
+  if (N <= 0 || B <= 0 || N % B || H != IH || W != IW || N / B > 8) return 0;
+  return c1r5_rows(N, B);
+}
+
+int avd_cl_c1r5_codes_cols(void) { return MOMC5; }
+
+int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, const float* scale,
+                    const float* shift, const float* mean, const float* invstd, const float* coef,
+                    const void* gz, void* z, float* out, int N, int B, int H, int W, int Cout, int K,
+                    hipStream_t st, unsigned short* codes);
+int avd_c1r3_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad);
+
+int avd_cl_c1r5_apply_codes(const void* x, const void* wk, const float* bias, const float* scale,
+                            const float* shift, void* z, unsigned short* codes, int N, int B, int H,
+                            int W, void* stream) {
+  if (!x || !wk || !scale || !shift || !z || !codes) return AVD_ERR_ARG;
+  if (!avd_cl_c1r5_codes_rows(N, B, H, W) || !avd_c1r3_rows(1, AVD_BF16, N, B, 1, H, W, C, 5, 2))
+    return AVD_ERR_SHAPE;
+  return avd_c1r3_launch(1, x, wk, bias, scale, shift, nullptr, nullptr, nullptr, nullptr, z,
+                         nullptr, N, B, H, W, C, 5, avd_stream(stream), codes);
+}
+
+int avd_cl_c1r5_moments_codes(const void* x, const void* gz, const unsigned short* codes, float* out,
+                              int N, int B, int H, int W, void* stream) {
+  if (!x || !gz || !codes || !out) return AVD_ERR_ARG;
+  const int R = avd_cl_c1r5_codes_rows(N, B, H, W);
+  if (!R) return AVD_ERR_SHAPE;
+  const int G = N / B;
+  c1r5_moments_codes_kernel<<<G * R, 256, 0, avd_stream(stream)>>>(
+      (const bf16*)x, (const bf16*)gz, codes, out, B, G, R);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_cl_c1r5_codes_combine(const float* moments, const void* wk, const float* bias,
+                              const float* gamma, const float* mean, const float* invstd,
+                              long long count, float* dw, float* dgamma, float* dbeta, float* dbias,
+                              float* coef, int G, void* stream) {
+  if (!moments || !wk || !gamma || !mean || !invstd || !dw) return AVD_ERR_ARG;
+  if (G <= 0 || G > 8 || count <= 1) return AVD_ERR_SHAPE;
+  c1r5_codes_combine_kernel<<<1, 256, 0, avd_stream(stream)>>>(moments, (const bf16*)wk, bias, gamma,
+                                                               mean, invstd, count, dw, dgamma, dbeta,
+                                                               dbias, coef, G);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+}  // extern "C"
