@@ -521,9 +521,10 @@ int avd_cl_c1_codes_combine(const float* moments, const void* wk, const float* b
                             long long count, float* dw, float* dgamma, float* dbeta, float* dbias,
                             float* coef, int G, void* stream);
 
-/* ---- the same routed backward for the IMAGE conv1 (c1w3.hip pass 1 + c1r5.hip; CentralUnimodalImage
+/* ---- the same routed backward for the IMAGE conv1 (c1r5.hip; CentralUnimodalImage
  * conv1 -> bn1 -> relu -> maxpool, unimodal.py:127-141, 5x5 1->32 on 28x28, bf16).
- * avd_cl_c1r5_apply_codes = avd_cl_c1_recompute pass 1 that also writes codes [N][14][14][8] u16:
+ * avd_cl_c1r5_apply_codes: the pooled map z of avd_cl_c1_recompute pass 1 (bit-identical; a
+ * pixel-major MFMA puts each pooling window in one lane) plus codes [N][14][14][8] u16:
  * word q of a window holds channels 4q..4q+3, nibble i (bits 4i..4i+3) = 1 + the window position
  * ((0,0),(0,1),(1,0),(1,1)) of the first argmax of relu(bn(y)) when that max is > 0, else 0.
  * avd_cl_c1r5_moments_codes: ONE pass over x, gz [N][14][14][32] and the codes -> per (row r,

@@ -1,7 +1,7 @@
 // The CentralNet IMAGE conv1 backward routed by forward codes (CentralUnimodalImage conv1 -> bn1
 // -> relu -> maxpool, unimodal.py:127-141: Conv2d(1, 32, 5, padding=2) on 28x28 images, bf16).
 //
-// The forward's BN -> ReLU -> pool pass (c1r3_kernel pass 1 with codes, c1w3.hip) writes, per
+// The forward's BN -> ReLU -> pool pass (c1r5_apply_kernel below) writes, per
 // pooling window and channel, where nn.MaxPool2d's gradient goes (nibble = 1 + the window
 // position of the first argmax of relu(bn(y)) when that max is > 0, else 0).  The backward of
 // conv1 + bn1 is then linear in three moments of the input patches x25 (as the audio conv1's,
@@ -42,6 +42,12 @@ constexpr int LDS_DZ = C * IH * VW;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f4;
 typedef __attribute__((ext_vector_type(4))) unsigned u4;
+typedef __attribute__((ext_vector_type(8))) unsigned short us8;   // raw bf16 bits
+
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
+}
 
 // per-thread global vectors of one sample: x 98, gz 784, codes 196 (16-byte vectors)
 constexpr int NXV = IH * IW / 8, NGV = NWIN * C / 8, NCV = NWIN * 8 / 8;
@@ -242,6 +248,118 @@ __global__ __launch_bounds__(256, 2) void c1r5_moments_codes_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------- forward apply
+// BN -> ReLU -> 2x2 max-pool of the recomputed conv output plus the routing codes, in one pass
+// over the 180 MB input (the layer's y is never stored).  The MFMA runs PIXEL-major: A = the
+// im2col fragment of 16 pixels (all 25 taps in one K = 32 step), B = the weights of 16 channels
+// (the same registers the channel-major passes use as A), so D lane l holds y for pixels
+// 4 (l / 16) .. +3 of one channel.  With the 16 pixels of a group ordered window by window
+// (pixel p = 4 w + k: window w of 4 side by side, k = (0,0) (0,1) (1,0) (1,1)), every lane holds
+// ONE whole pooling window of one channel: the max, the first argmax and the > 0 test are
+// in-lane integer compares of the f32 bn(y) bits -- no cross-lane exchange -- and y is the same
+// bf16(acc + b) as the stored-y conv's (bit-identical pooled map, tests/test_gpu_benchsize.py).
+constexpr int AP_XS = IW + 8, AP_XR = IH + 4;                // staged rows: 2-pixel halo + pad
+constexpr int AP_GROUPS = (IH / 2) * 4;                      // 16-pixel groups per sample
+
+__global__ __launch_bounds__(256) void c1r5_apply_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ wk, const float* __restrict__ bias,
+    const float* __restrict__ scale, const float* __restrict__ shift, bf16* __restrict__ z,
+    unsigned short* __restrict__ codes, int N, int B) {
+  __shared__ __attribute__((aligned(16))) bf16 xs[2][AP_XR * AP_XS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int per = N / (int)gridDim.x, extra = N % (int)gridDim.x;
+  const int s0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
+  const int s1 = s0 + per + ((int)blockIdx.x < extra ? 1 : 0);
+
+  bf16x8 aw[2];
+  float bv[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    aw[t] = *reinterpret_cast<const bf16x8*>(wk + (16 * t + r16) * 32 + 8 * g);
+    bv[t] = bias ? bias[16 * t + r16] : 0.f;
+  }
+  // this lane's A row: pixel r16 of a group = window r16 / 4, position r16 % 4; its taps
+  // 8 g .. 8 g + 7 (>= 25: zero)
+  const int pk = r16 & 3, pcol = 2 * (r16 >> 2) + (pk & 1), prow = pk >> 1;
+  int toff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int t = 8 * g + j;
+    toff[j] = t < KK ? (prow + t / 5) * AP_XS + pcol + t % 5 : -1;
+  }
+  for (int i = tid; i < 2 * AP_XR * AP_XS / 2; i += 256) reinterpret_cast<unsigned*>(xs)[i] = 0u;
+
+  u4 xv = u4{0u, 0u, 0u, 0u};
+  auto load = [&](int n) {
+    if (tid < NXV) xv = ldg16(x + (size_t)n * IH * IW + 8 * tid);
+  };
+  if (s0 < s1) load(s0);
+  __syncthreads();
+  int cg = -1;
+  float sc[2], sf[2];
+  for (int n = s0; n < s1; ++n) {
+    bf16* xb = xs[(n - s0) & 1];
+    if (tid < NXV) {
+      // a pixel pair never straddles a row (28 even): dword stores, 4-byte aligned
+      const unsigned w4[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int pix = 8 * tid + 2 * k, r = pix / IW, c = pix - r * IW;
+        *reinterpret_cast<unsigned*>(xb + (r + 2) * AP_XS + c + 2) = w4[k];
+      }
+    }
+    __syncthreads();                      // this buffer complete; every wave is past sample n-2
+    if (n + 1 < s1) load(n + 1);
+    if (n / B != cg) {
+      cg = n / B;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) { sc[t] = scale[cg * C + 16 * t + r16]; sf[t] = shift[cg * C + 16 * t + r16]; }
+    }
+    for (int q = wave; q < AP_GROUPS; q += 4) {
+      const int rp = q >> 2, cq = q & 3;                       // row pair, 8-column group
+      const bf16* xp = xb + 2 * rp * AP_XS + 8 * cq;
+      us8 bs;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bs[j] = toff[j] >= 0 ? xp[toff[j]] : (unsigned short)0;
+      const bf16x8 px = __builtin_bit_cast(bf16x8, bs);
+      const int wcol = 4 * cq + g;                             // the lane's window column
+      unsigned zw = 0u, cw = 0u;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(px, aw[t], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const uint32_t y01 = pack_bf16x2(acc[0] + bv[t], acc[1] + bv[t]);
+        const uint32_t y23 = pack_bf16x2(acc[2] + bv[t], acc[3] + bv[t]);
+        const float y[4] = {__uint_as_float(y01 << 16), __uint_as_float(y01 & 0xffff0000u),
+                            __uint_as_float(y23 << 16), __uint_as_float(y23 & 0xffff0000u)};
+        int v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = __float_as_int(fmaf(y[i], sc[t], sf[t]));
+        // signed-int order = float order where either side is > 0; max with 0 = the ReLU
+        const int mx = max(max(v[0], v[1]), max(v[2], max(v[3], 0)));
+        const int a = v[0] == mx ? 1 : v[1] == mx ? 2 : v[2] == mx ? 3 : 4;   // first argmax + 1
+        const unsigned nib = mx > 0 ? (unsigned)a : 0u;
+        zw |= (pack_bf16x2(__int_as_float(mx), 0.f) & 0xffffu) << (16 * t);
+        cw |= nib << (4 * pk + 16 * t);
+      }
+      // pooled map: lane pairs trade halves so each stores 2 adjacent channels (4 bytes):
+      // even r16 -> channels (r16, r16 + 1), odd r16 -> (15 + r16, 16 + r16)
+      const unsigned zo = (unsigned)dppi<0xB1>((int)zw);
+      const bool ev = (r16 & 1) == 0;
+      const unsigned word = ev ? (zw & 0xffffu) | (zo << 16) : (zo >> 16) | (zw & 0xffff0000u);
+      // codes: the 4 channels of a word sit in one lane quad
+      cw |= (unsigned)dppi<0xB1>((int)cw);
+      cw |= (unsigned)dppi<0x4E>((int)cw);
+      if (wcol < WP) {
+        const size_t win = (size_t)n * NWIN + rp * WP + wcol;
+        *reinterpret_cast<unsigned*>(z + win * C + (ev ? r16 : 15 + r16)) = word;
+        if (pk < 2) codes[win * 8 + 4 * pk + (r16 >> 2)] = (unsigned short)(cw >> (16 * pk));
+      }
+    }
+  }
+}
+
 // BN backward + dW of the layer from the row-summed routed moments m [G][MOMC5], float64:
 //   sum dz y = w . M + b sum dz;  sum dz xhat = (sum dz y - mean sum dz) invstd;
 //   coef (k1, kx, k0) as avd_bn_bwd_finalize;  dW[c][t] = sum_g k1 M + kx (w Gram + b S) + k0 S;
@@ -337,20 +455,27 @@ int avd_cl_c1r5_codes_rows(int N, int B, int H, int W) {
 
 int avd_cl_c1r5_codes_cols(void) { return MOMC5; }
 
-int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, const float* scale,
-                    const float* shift, const float* mean, const float* invstd, const float* coef,
-                    const void* gz, void* z, float* out, int N, int B, int H, int W, int Cout, int K,
-                    hipStream_t st, unsigned short* codes);
-int avd_c1r3_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad);
-
 int avd_cl_c1r5_apply_codes(const void* x, const void* wk, const float* bias, const float* scale,
                             const float* shift, void* z, unsigned short* codes, int N, int B, int H,
                             int W, void* stream) {
   if (!x || !wk || !scale || !shift || !z || !codes) return AVD_ERR_ARG;
-  if (!avd_cl_c1r5_codes_rows(N, B, H, W) || !avd_c1r3_rows(1, AVD_BF16, N, B, 1, H, W, C, 5, 2))
-    return AVD_ERR_SHAPE;
-  return avd_c1r3_launch(1, x, wk, bias, scale, shift, nullptr, nullptr, nullptr, nullptr, z,
-                         nullptr, N, B, H, W, C, 5, avd_stream(stream), codes);
+  if (!avd_cl_c1r5_codes_rows(N, B, H, W)) return AVD_ERR_SHAPE;
+  static int resident = 0;
+  if (!resident) {
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, c1r5_apply_kernel, 256, 0) != hipSuccess ||
+        per <= 0)
+      per = 2;
+    resident = cus * per;
+  }
+  const int grid = grid_cap(std::min(N, resident));
+  c1r5_apply_kernel<<<grid, 256, 0, avd_stream(stream)>>>((const bf16*)x, (const bf16*)wk, bias, scale,
+                                                          shift, (bf16*)z, codes, N, B);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
 }
 
 int avd_cl_c1r5_moments_codes(const void* x, const void* gz, const unsigned short* codes, float* out,

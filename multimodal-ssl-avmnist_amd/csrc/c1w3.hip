@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C, K)) void c1r3_kernel(
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ coef, const bf16* __restrict__ gz, bf16* __restrict__ z,
-    float* __restrict__ out, int N, int B, int H, int W, unsigned short* __restrict__ codes) {
+    float* __restrict__ out, int N, int B, int H, int W) {
   constexpr int NT = C / 16;
   constexpr int DYS = C == 16 ? 16 : C + 16;
   constexpr int KK = K * K, PADK = K / 2, NTAP = c1r3_ntap(K), XSK = 16 * NTAP;
@@ -605,29 +605,6 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C, K)) void c1r3_kernel(
             }
             if (mn == 0 && wvld)
               *reinterpret_cast<uint2*>(z + zt + wg + 16 * t) = make_uint2(m[0], m[1]);
-            if (codes) {
-              // routing codes for the backward (c1r5.hip): nibble i of this lane's 16-bit word =
-              // 1 + the window position (k order (0,0),(0,1),(1,0),(1,1)) of the first argmax of
-              // bn(y) for channel 16 t + 4 g + i when that max is > 0, else 0 -- the routing the
-              // recomputing passes 2-4 derive below, decided on the same f32 values
-              unsigned nib = 0u;
-#pragma unroll
-              for (int h = 0; h < 2; ++h) {
-                const f2 v = __builtin_elementwise_fma(y2[h], sc2[t][h], sf2[t][h]);
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                  const int vi = __float_as_int(v[e]);
-                  const int u1 = dppi<0xB1>(vi) + e1, u8 = dppi<0x128>(vi) + e8,
-                            u9 = dppi<0x128>(dppi<0xB1>(vi)) + e8;
-                  const int thr = max(max(u1, u8), max(u9, 1));
-                  if (vi >= thr && vld) nib |= (unsigned)(2 * e8 + e1 + 1) << (4 * (2 * h + e));
-                }
-              }
-              nib |= (unsigned)dppi<0xB1>((int)nib);
-              nib |= (unsigned)dppi<0x128>((int)nib);
-              if (mn == 0 && wvld)
-                codes[(size_t)zt / 4 + wg / 4 + 4 * t] = (unsigned short)nib;
-            }
           } else {
             // first argmax of the window (k order (0,0),(0,1),(1,0),(1,1); lane L^m holds
             // k = 2 (m >> 3) + (m & 1)) on bn(y) as signed ints: ordered like the floats wherever
@@ -804,7 +781,7 @@ int avd_c1r3_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cou
 int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, const float* scale,
                     const float* shift, const float* mean, const float* invstd, const float* coef,
                     const void* gz, void* z, float* out, int N, int B, int H, int W, int Cout, int K,
-                    hipStream_t st, unsigned short* codes) {
+                    hipStream_t st) {
   const int grid = c1r3_grid(pass, Cout, K);
   const int TR = c1r3_tr(H, W);
   const size_t lds = c1r3_lds(pass, Cout, W, K, TR);
@@ -812,8 +789,7 @@ int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, 
   if (pass == P_ && Cout == C_ && K == K_ && TR == TR_)                                        \
     c1r3_kernel<P_, C_, K_, TR_><<<grid, 256, lds, st>>>((const bf16*)x, (const bf16*)wk, bias,   \
                                                          scale, shift, mean, invstd, coef,      \
-                                                         (const bf16*)gz, (bf16*)z, out, N, B, H, W, \
-                                                         codes);
+                                                         (const bf16*)gz, (bf16*)z, out, N, B, H, W);
 #define AVD_PC(C_, K_, TR_) AVD_P(0, C_, K_, TR_) else AVD_P(1, C_, K_, TR_) else AVD_P(2, C_, K_, TR_) \
   else AVD_P(3, C_, K_, TR_) else AVD_P(4, C_, K_, TR_)
   AVD_PC(16, 3, 4) else AVD_PC(32, 3, 4) else AVD_PC(64, 3, 4) else AVD_PC(32, 5, 4)

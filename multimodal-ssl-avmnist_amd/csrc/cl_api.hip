@@ -167,7 +167,7 @@ int avd_c1r3_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cou
 int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, const float* scale,
                     const float* shift, const float* mean, const float* invstd, const float* coef,
                     const void* gz, void* z, float* out, int N, int B, int H, int W, int Cout, int K,
-                    hipStream_t st, unsigned short* codes);
+                    hipStream_t st);
 
 int avd_c1r3_combine(const float* m, const float* coef, const void* wk, const float* bias,
                      float* dw, int G, int Cout, int K, hipStream_t st);
@@ -195,7 +195,7 @@ int avd_cl_c1_recompute(int pass, const void* x, const void* wk, const float* bi
     return AVD_ERR_ARG;
   if (avd_c1r3_rows(pass, dt, N, B, Cin, H, W, Cout, K, pad))
     return avd_c1r3_launch(pass, x, wk, bias, scale, shift, mean, invstd, coef, gz, z, out, N, B,
-                           H, W, Cout, K, avd_stream(stream), nullptr);
+                           H, W, Cout, K, avd_stream(stream));
   return avd_c1r_launch(pass, x, wk, bias, scale, shift, mean, invstd, coef, gz, z, out, N, B, H,
                         W, avd_stream(stream));
 }
