@@ -49,6 +49,8 @@ PROTOS = {
     "avd_cl_c1r5_codes_rows": [I, I, I, I],
     "avd_cl_c1r5_codes_cols": [],
     "avd_cl_c1r5_apply_codes": [P, P, P, P, P, P, P, I, I, I, I, P],
+    "avd_cl_c1r5_stats_rows": [I, I, I, I],
+    "avd_cl_c1r5_stats": [P, P, P, P, I, I, I, I, P],
     "avd_cl_c1r5_moments_codes": [P, P, P, P, I, I, I, I, P],
     "avd_cl_c1r5_codes_combine": [P, P, P, P, P, P, L, P, P, P, P, P, I, P],
     "avd_counters_add": [P, P, P, I, P],

@@ -235,6 +235,17 @@ class ConvBranch:
     # AVDINO_C1_CODES=0 keeps the recomputing moments pass (pass 4) for both
     CODES = os.environ.get("AVDINO_C1_CODES", "1") == "1"
 
+    # the image conv1's forward passes (statistics; BN -> ReLU -> pool [+ codes]) on the
+    # pixel-major MFMA kernels of c1r5.hip (one pooling window per lane); AVDINO_C1R5_PM=0 runs
+    # them on c1r3 passes 0 / 1 instead (same pooled map; statistics summed in another order)
+    PIXEL_MAJOR = os.environ.get("AVDINO_C1R5_PM", "1") == "1"
+
+    def _pixel_major(self, N, B):
+        ci, co, k, pad = self.stack.convs[0]
+        H = self.dims[0][0]
+        return (self.PIXEL_MAJOR and (ci, co, k, pad) == (1, 32, 5, 2) and self.act == torch.bfloat16
+                and ops.c1r5_serves(N, B, H, H))
+
     def _codes_ok(self, N, B, need_dgrad):
         """"audio" / "image" when the first layer's training backward is the routed moments pass,
         else None."""
@@ -244,8 +255,7 @@ class ConvBranch:
             return None
         if (ci, co, k, pad) == (1, 8, 5, 2) and ops.c1_codes_rows(N, B, H, H) > 0:
             return "audio"
-        if ((ci, co, k, pad) == (1, 32, 5, 2) and ops.c1r5_codes_rows(N, B, H, H) > 0 and
-                ops.cl_c1_recompute_rows(ops.C1_APPLY, self.act, N, B, ci, H, H, co, k, pad) > 0):
+        if (ci, co, k, pad) == (1, 32, 5, 2) and ops.c1r5_codes_rows(N, B, H, H) > 0:
             return "image"
         return None
 
@@ -255,9 +265,15 @@ class ConvBranch:
         H, Ho, Hp = self.dims[0]
         wk = ctx["wts"][0][0]
         bias = store[self.stack.conv_keys[0] + ".bias"]
-        R = ops.cl_c1_recompute_rows(ops.C1_STATS, self.act, N, B, ci, H, H, co, k, pad)
-        parts = ws.get("stat_parts", co * G * R * 2)
-        ops.cl_c1_recompute(ops.C1_STATS, x, wk, bias, N, B, ci, H, H, co, k, pad, out=parts)
+        pm = self._pixel_major(N, B)
+        if pm:
+            R = ops.c1r5_stats_rows(N, B, H, H)
+            parts = ws.get("stat_parts", co * G * R * 2)
+            ops.c1r5_stats(x, wk, bias, parts, N, B, H, H)
+        else:
+            R = ops.cl_c1_recompute_rows(ops.C1_STATS, self.act, N, B, ci, H, H, co, k, pad)
+            parts = ws.get("stat_parts", co * G * R * 2)
+            ops.cl_c1_recompute(ops.C1_STATS, x, wk, bias, N, B, ci, H, H, co, k, pad, out=parts)
         st = ws.get(f"{tag}.bn0", 4 * G * co).view(4, G * co)
         bk = self.stack.bn_keys[0]
         ops.bn_finalize(parts, G, R, co, B * Ho * Ho, store[bk + ".weight"], store[bk + ".bias"],
@@ -278,6 +294,8 @@ class ConvBranch:
             codes = ws.get(f"{tag}.c1codes", N * Hp * Hp * 8, torch.int16)
             ops.c1r5_apply_codes(x, wk, bias, st[2], st[3], out, codes, N, B, H, H)
             ctx["codes"] = (route, codes)
+        elif pm:
+            ops.c1r5_apply_codes(x, wk, bias, st[2], st[3], out, None, N, B, H, H)
         else:
             ops.cl_c1_recompute(ops.C1_APPLY, x, wk, bias, N, B, ci, H, H, co, k, pad, scale=st[2],
                                 shift=st[3], z=out)

@@ -587,15 +587,37 @@ def c1r5_codes_cols():
     return lib.avd_cl_c1r5_codes_cols()
 
 
+def c1r5_serves(N, B, H, W):
+    """The pixel-major image conv1 passes (avd_cl_c1r5_stats / _apply_codes) serve this shape."""
+    return lib.avd_cl_c1r5_stats_rows(N, B, H, W) > 0
+
+
+def c1r5_stats_rows(N, B, H, W):
+    return lib.avd_cl_c1r5_stats_rows(N, B, H, W)
+
+
+def c1r5_stats(x, wk, bias, out, N, B, H, W):
+    """BN partial sums [32][G][R][2] of the recomputed image conv1 output (bf16 y)."""
+    R = c1r5_stats_rows(N, B, H, W)
+    _need(R > 0 and x.numel() == N * H * W and x.dtype == torch.bfloat16, "c1r5 stats shape")
+    _need(out.numel() >= 32 * (N // B) * R * 2, "c1r5 stats rows")
+    _timed(f"c1r5_stats[{N}x{H}x{W}x1->32 k5]", x.numel() * 2, 2 * N * H * W * 32 * 25,
+           lambda: call("avd_cl_c1r5_stats", p(x), p(wk), p(bias), p(out), N, B, H, W, stream()))
+
+
 def c1r5_apply_codes(x, wk, bias, scale, shift, z, codes, N, B, H, W):
-    """BN -> ReLU -> 2x2 max-pool of the recomputed image conv1 output (c1r3 pass 1) plus the
-    routing codes [N, H/2, W/2, 8] (int16 storage of the u16 nibble words)."""
+    """BN -> ReLU -> 2x2 max-pool of the recomputed image conv1 output (bit-identical to c1r3
+    pass 1) plus, when ``codes`` is given, the routing codes [N, H/2, W/2, 8] (int16 storage of
+    the u16 nibble words)."""
     npool = N * (H // 2) * (W // 2)
-    _need(c1r5_codes_rows(N, B, H, W) > 0 and x.numel() == N * H * W and x.dtype == torch.bfloat16,
-          "c1r5 codes shape")
-    _need(z.numel() == npool * 32 and z.dtype == x.dtype, "c1r5 codes z")
-    _need(codes.numel() >= npool * 8 and codes.element_size() == 2, "c1r5 codes buffer")
-    _timed(f"c1r5_apply_codes[{N}x{H}x{W}x1->32 k5]", x.numel() * 2 + npool * 80, 2 * N * H * W * 32 * 25,
+    _need(c1r5_serves(N, B, H, W) and x.numel() == N * H * W and x.dtype == torch.bfloat16,
+          "c1r5 apply shape")
+    _need(z.numel() == npool * 32 and z.dtype == x.dtype, "c1r5 apply z")
+    if codes is not None:
+        _need(codes.numel() >= npool * 8 and codes.element_size() == 2, "c1r5 codes buffer")
+    name = "c1r5_apply_codes" if codes is not None else "c1r5_apply"
+    _timed(f"{name}[{N}x{H}x{W}x1->32 k5]", x.numel() * 2 + npool * (80 if codes is not None else 64),
+           2 * N * H * W * 32 * 25,
            lambda: call("avd_cl_c1r5_apply_codes", p(x), p(wk), p(bias), p(scale), p(shift), p(z),
                         p(codes), N, B, H, W, stream()))
 

@@ -354,9 +354,99 @@ __global__ __launch_bounds__(256) void c1r5_apply_kernel(
       if (wcol < WP) {
         const size_t win = (size_t)n * NWIN + rp * WP + wcol;
         *reinterpret_cast<unsigned*>(z + win * C + (ev ? r16 : 15 + r16)) = word;
-        if (pk < 2) codes[win * 8 + 4 * pk + (r16 >> 2)] = (unsigned short)(cw >> (16 * pk));
+        if (codes && pk < 2) codes[win * 8 + 4 * pk + (r16 >> 2)] = (unsigned short)(cw >> (16 * pk));
       }
     }
+  }
+}
+
+// BatchNorm partial sums (sum y, sum y^2 of the bf16 y) of the same recomputed conv output, on
+// the same pixel-major MFMA: each lane accumulates its channel over its window's 4 pixels in
+// registers; the block's 16 lane partials per channel are summed through LDS in fixed order
+// into one row of parts [C][G][R][2] (avd_bn_finalize's layout).  Block (group, r) owns a
+// contiguous slice of one BN group, so every (group, row) is written exactly once.
+__global__ __launch_bounds__(256) void c1r5_stats_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ wk, const float* __restrict__ bias,
+    float* __restrict__ out, int B, int G, int R) {
+  __shared__ __attribute__((aligned(16))) bf16 xs[2][AP_XR * AP_XS];
+  __shared__ float red[4][4][2][16][2];   // [wave][lane group][t][channel r16][sum, sumsq]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r16 = lane & 15;
+  const int grp = (int)blockIdx.x / R, rr = (int)blockIdx.x - grp * R;
+  const int s0 = grp * B + (int)(((long long)B * rr) / R);
+  const int s1 = grp * B + (int)(((long long)B * (rr + 1)) / R);
+
+  bf16x8 aw[2];
+  float bv[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    aw[t] = *reinterpret_cast<const bf16x8*>(wk + (16 * t + r16) * 32 + 8 * g);
+    bv[t] = bias ? bias[16 * t + r16] : 0.f;
+  }
+  const int pk = r16 & 3, pcol = 2 * (r16 >> 2) + (pk & 1), prow = pk >> 1;
+  int toff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int t = 8 * g + j;
+    toff[j] = t < KK ? (prow + t / 5) * AP_XS + pcol + t % 5 : -1;
+  }
+  for (int i = tid; i < 2 * AP_XR * AP_XS / 2; i += 256) reinterpret_cast<unsigned*>(xs)[i] = 0u;
+  u4 xv = u4{0u, 0u, 0u, 0u};
+  auto load = [&](int n) {
+    if (tid < NXV) xv = ldg16(x + (size_t)n * IH * IW + 8 * tid);
+  };
+  if (s0 < s1) load(s0);
+  __syncthreads();
+  float sm[2] = {0.f, 0.f}, sq[2] = {0.f, 0.f};
+  for (int n = s0; n < s1; ++n) {
+    bf16* xb = xs[(n - s0) & 1];
+    if (tid < NXV) {
+      const unsigned w4[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int pix = 8 * tid + 2 * k, r = pix / IW, c = pix - r * IW;
+        *reinterpret_cast<unsigned*>(xb + (r + 2) * AP_XS + c + 2) = w4[k];
+      }
+    }
+    __syncthreads();
+    if (n + 1 < s1) load(n + 1);
+    for (int q = wave; q < AP_GROUPS; q += 4) {
+      const int rp = q >> 2, cq = q & 3;
+      const bool wv = 4 * cq + g < WP;                         // not virtual columns 28..31
+      const bf16* xp = xb + 2 * rp * AP_XS + 8 * cq;
+      us8 bs;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bs[j] = toff[j] >= 0 ? xp[toff[j]] : (unsigned short)0;
+      const bf16x8 px = __builtin_bit_cast(bf16x8, bs);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(px, aw[t], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const uint32_t y01 = pack_bf16x2(acc[0] + bv[t], acc[1] + bv[t]);
+        const uint32_t y23 = pack_bf16x2(acc[2] + bv[t], acc[3] + bv[t]);
+        const float y0 = __uint_as_float(y01 << 16), y1 = __uint_as_float(y01 & 0xffff0000u);
+        const float y2 = __uint_as_float(y23 << 16), y3 = __uint_as_float(y23 & 0xffff0000u);
+        if (wv) {   // after the MFMA: the whole wave issues it
+          sm[t] += (y0 + y1) + (y2 + y3);
+          sq[t] += fmaf(y0, y0, y1 * y1) + fmaf(y2, y2, y3 * y3);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    red[wave][g][t][r16][0] = sm[t];
+    red[wave][g][t][r16][1] = sq[t];
+  }
+  __syncthreads();
+  if (tid < 2 * C) {
+    const int c = tid >> 1, k = tid & 1, t = c >> 4, ch = c & 15;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) v += red[w][gg][t][ch][k];
+    out[(((size_t)c * G + grp) * R + rr) * 2 + k] = v;
   }
 }
 
@@ -455,11 +545,41 @@ int avd_cl_c1r5_codes_rows(int N, int B, int H, int W) {
 
 int avd_cl_c1r5_codes_cols(void) { return MOMC5; }
 
+// rows per BN group of avd_cl_c1r5_stats (0 = shape not served)
+int avd_cl_c1r5_stats_rows(int N, int B, int H, int W) {
+  if (N <= 0 || B <= 0 || N % B || H != IH || W != IW) return 0;
+  static int resident = 0;
+  if (!resident) {
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, c1r5_stats_kernel, 256, 0) != hipSuccess ||
+        per <= 0)
+      per = 2;
+    resident = cus * per;
+  }
+  const int G = N / B;
+  return std::max(1, std::min(grid_cap(resident) / G, std::max(1, B / 4)));
+}
+
+int avd_cl_c1r5_stats(const void* x, const void* wk, const float* bias, float* out, int N, int B,
+                      int H, int W, void* stream) {
+  if (!x || !wk || !out) return AVD_ERR_ARG;
+  const int R = avd_cl_c1r5_stats_rows(N, B, H, W);
+  if (!R) return AVD_ERR_SHAPE;
+  const int G = N / B;
+  c1r5_stats_kernel<<<G * R, 256, 0, avd_stream(stream)>>>((const bf16*)x, (const bf16*)wk, bias, out,
+                                                          B, G, R);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
 int avd_cl_c1r5_apply_codes(const void* x, const void* wk, const float* bias, const float* scale,
                             const float* shift, void* z, unsigned short* codes, int N, int B, int H,
                             int W, void* stream) {
-  if (!x || !wk || !scale || !shift || !z || !codes) return AVD_ERR_ARG;
-  if (!avd_cl_c1r5_codes_rows(N, B, H, W)) return AVD_ERR_SHAPE;
+  if (!x || !wk || !scale || !shift || !z) return AVD_ERR_ARG;   // codes may be null (no backward)
+  if (N <= 0 || B <= 0 || N % B || H != IH || W != IW) return AVD_ERR_SHAPE;
   static int resident = 0;
   if (!resident) {
     int dev = 0, cus = 0, per = 0;

@@ -797,6 +797,19 @@ def test_image_conv1_routed_backward(ops, N, B):
     codes = torch.full((N * Hp * Hp * 8,), -1, device="cuda", dtype=torch.int16)
     ops.c1r5_apply_codes(x, wk, bias, bn[2], bn[3], z1, codes, N, B, H, H)
     assert torch.equal(z0, z1)
+    z2 = torch.full_like(z0, float("nan"))
+    ops.c1r5_apply_codes(x, wk, bias, bn[2], bn[3], z2, None, N, B, H, H)     # no codes: same map
+    assert torch.equal(z0, z2)
+    # the pixel-major statistics pass: per-group sums of the bf16 y within 1e-5 of float64
+    Rs = ops.c1r5_stats_rows(N, B, H, H)
+    sp = torch.full((C * G * Rs * 2,), float("nan"), device="cuda")
+    ops.c1r5_stats(x, wk, bias, sp, N, B, H, H)
+    s64 = sp.view(C, G, Rs, 2).to(F64).sum(2)
+    y64 = y.to(F64).view(G, B * H * H, C)
+    assert grel(s64[..., 0], y64.sum(1).T) < 1e-5 and grel(s64[..., 1], (y64 * y64).sum(1).T) < 1e-5
+    bnp = torch.empty(4, G * C, device="cuda")
+    ops.bn_finalize(sp, G, Rs, C, B * H * H, gamma, beta, bnp[0], bnp[1], bnp[2], bnp[3])
+    assert grel(bnp, bn) < 1e-5
     gz = rnd(g, (N, Hp, Hp, C), dtype=T)
     Rc, mc = ops.c1r5_codes_rows(N, B, H, H), ops.c1r5_codes_cols()
     assert Rc > 0 and mc == C * 25 + 625 + 25 + C
