@@ -385,8 +385,38 @@ def main():
                 "kernel_share_of_step": round(d["ms"] / (3 if use_graph else args.steps) /
                                               (elapsed * 1e3 / args.steps), 4)}
 
+    def isolated(k, reps=10):
+        """The launch replayed alone (same inputs, its own stream idle otherwise), HIP events
+        around ``reps`` back-to-back replays: the kernel's own speed, free of the time-sharing
+        with the other streams' kernels that the in-step duration includes."""
+        ops.TIMER = ops.KernelTimer(only=[k])
+        step(args.warmup + args.steps + 3)
+        torch.cuda.synchronize()
+        fn, ops.TIMER = ops.TIMER.replay, None
+        if fn is None:
+            return None
+        fn()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) * 1e3 / reps
+
     roof = roofline_of(dominant)
     roof_hbm = roofline_of(hbm_dom) if hbm_dom is not None else None
+    for r in (roof, roof_hbm):
+        if r is None:
+            continue
+        iso = isolated(r["kernel"])
+        if iso:
+            d = timed[r["kernel"]]
+            amount = (d["bytes"] if r["unit"] == "GB/s" else d["flops"]) / d["calls"]
+            ach = amount / (iso * 1e-6) / (1e9 if r["unit"] == "GB/s" else 1e12)
+            r["isolated_avg_launch_us"] = round(iso, 2)
+            r["isolated_achieved"] = round(ach, 2)
+            r["isolated_frac"] = round(ach / r["peak"], 4)
 
     total_pairs = world * B * args.steps
     value = total_pairs / elapsed

@@ -145,7 +145,11 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ X, long long
 #pragma unroll
     for (int i = 0; i < (ROWS + 127) / 128; ++i) {
       const int b = tid + 256 * i;
-      const int kb = b / (ROWS / 4), r = (b % (ROWS / 4)) * 4;
+      // k-block fastest: 8 lanes cover one row's 32 k (64 LDS bytes) and the next 8 lanes the
+      // next 4 rows, so a 16-lane group of store_tile's 8-byte LDS writes is bank-conflict free
+      // (rows fastest put lanes 4 apart on one bank: 4-way); the global reads stay whole
+      // 128-byte row segments (8 lanes x 16 bytes per k row)
+      const int kb = b & 7, r = (b >> 3) * 4;
       const int gr = r0 + r;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
@@ -208,7 +212,7 @@ __device__ __forceinline__ void store_tile(const TileRegs<ROWS>& t, long long sr
     for (int i = 0; i < (ROWS + 127) / 128; ++i) {
       const int b = tid + 256 * i;
       if (b >= 2 * ROWS) continue;
-      const int kb = b / (ROWS / 4), r = (b % (ROWS / 4)) * 4;
+      const int kb = b & 7, r = (b >> 3) * 4;                   // as load_tile<LAY_R>
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         typename GemmT<MODE>::T* d = S + (r + j) * LDK + 4 * kb;
