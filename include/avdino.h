@@ -110,11 +110,14 @@ int avd_gemm(int M, int N, int K, const float* A, long long sam, long long sak,
  * (x_ld), dX leading dimension dx_ld.  Both read dout, neither depends on the other: their tile
  * grids run side by side (one launch boundary, and two small grids fill the chip together);
  * results are bitwise those of the two avd_gemm calls.  ws: avd_linear_bwd_ws_elems floats of
- * split-K scratch (NULL: single passes over K).  The bias gradient stays avd_sum_rows. */
+ * split-K scratch (NULL: single passes over K).  db (nullable) = the bias gradient
+ * sum_r dout[r, :], formed by extra blocks of the same launches (row-chunk partials in ws, then
+ * a fixed-order fold in the split-K reduce launch): deterministic, no separate reduction
+ * launches; needs ws (AVD_ERR_ARG without it). */
 long long avd_linear_bwd_ws_elems(int rows, int O, int In, int mode);
 int avd_linear_bwd(int rows, int O, int In, const float* dout, long long dout_ld, const float* x,
-                   long long x_ld, const float* W, float* dW, float* dX, long long dx_ld, int mode,
-                   float* ws, long long ws_elems, void* stream);
+                   long long x_ld, const float* W, float* dW, float* dX, long long dx_ld, float* db,
+                   int mode, float* ws, long long ws_elems, void* stream);
 
 /* ------------------------------------------------------------------ channels-last conv blocks
  * The training path's conv blocks on NHWC maps ([N][H][W][C]; Cin = 1 maps are the plain

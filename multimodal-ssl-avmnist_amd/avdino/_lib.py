@@ -25,7 +25,7 @@ PROTOS = {
     "avd_bn_bwd_finalize": [P, I, I, I, L, P, P, P, P, P, P, P, I, P],
     "avd_gemm": [I, I, I, P, L, L, P, L, L, P, L, P, F, F, I, P, L, P],
     "avd_gemm_ws_elems": [I, I, I, I],
-    "avd_linear_bwd": [I, I, I, P, L, P, L, P, P, P, L, I, P, L, P],
+    "avd_linear_bwd": [I, I, I, P, L, P, L, P, P, P, L, P, I, P, L, P],
     "avd_linear_bwd_ws_elems": [I, I, I, I],
     "avd_cl_weight_elems": [I, I, I, I],
     "avd_cl_weight_layout": [P, P, I, I, I, I, I, P],

@@ -182,22 +182,21 @@ def linear_bwd(dout, x, w, dw, db, dx, rows, dout_ld=None, dout_off=0, x_ld=None
     x_ld = In if x_ld is None else x_ld
     dx_ld = In if dx_ld is None else dx_ld
     if dx is not None and mode in (GEMM_F32_MFMA, GEMM_BF16_MFMA) and PAIR_BWD:
-        # dW and dX in one launch (avd_linear_bwd), then the bias gradient
+        # dW, dX and the bias gradient on the same launches (avd_linear_bwd)
         for t in (dout, x, w, dw, dx):
             _need(t.dtype == torch.float32 and t.is_contiguous(), "linear_bwd operands are contiguous f32")
         _need(dout_off + (rows - 1) * dout_ld + O <= dout.numel(), "linear_bwd dout bounds")
         _need(x_off + (rows - 1) * x_ld + In <= x.numel(), "linear_bwd x bounds")
         _need(dx_off + (rows - 1) * dx_ld + In <= dx.numel(), "linear_bwd dx bounds")
         _need(dw.numel() >= O * In, "linear_bwd dw size")
-        nws = lib.avd_linear_bwd_ws_elems(rows, O, In, mode)
-        ws = _gemm_workspace(dout.device, nws) if nws > 0 else None
+        nws = lib.avd_linear_bwd_ws_elems(rows, O, In, mode)   # > 0: includes the bias partials
+        ws = _gemm_workspace(dout.device, nws)
+        _need(db is None or db.numel() >= O, "linear_bwd db size")
         _timed(f"linear_bwd[{rows}x{O}x{In} m{mode}]",
                4 * (2 * rows * O + rows * In + O * In + O * In + rows * In), 4 * rows * O * In,
                lambda: call("avd_linear_bwd", rows, O, In, dout.data_ptr() + 4 * dout_off, dout_ld,
                             x.data_ptr() + 4 * x_off, x_ld, p(w), p(dw),
-                            dx.data_ptr() + 4 * dx_off, dx_ld, mode, p(ws), nws, stream()))
-        if db is not None:
-            sum_rows(dout, rows, O, db, ld=dout_ld, off=dout_off)
+                            dx.data_ptr() + 4 * dx_off, dx_ld, p(db), mode, p(ws), nws, stream()))
         return
     # dW[o, i] = sum_r dout[r, o] x[r, i]: A = dout^T (M=O, K=rows), B = x (K=rows, N=In)
     gemm(O, In, rows, dout, 1, dout_ld, x, x_ld, 1, dw, In, a_off=dout_off, b_off=x_off, mode=mode)

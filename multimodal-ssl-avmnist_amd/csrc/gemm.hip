@@ -362,32 +362,72 @@ __global__ __launch_bounds__(256) void gemm_mfma_kernel(GemmArgs p) {
   gemm_tile<MODE, BM, BN, LA, LB>(p, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
+// The bias gradient db[o] = sum_r dout[r, o] of a Linear backward, riding on the launches the
+// weight gradient makes anyway: the paired GEMM launch's extra blocks write column partial sums
+// of row chunks (block (chunk, 256-column strip)), the split-K reduce launch's extra blocks fold
+// them in fixed chunk order.  Deterministic; two launches fewer per layer than avd_sum_rows_split.
+struct DbArgs {
+  const float* dout;
+  long long ld;
+  int rows, O, chunk, nrc, strips;
+  float* part;   // [nrc][O]
+  float* db;     // nullptr: no bias gradient in these launches
+};
+
+__device__ __forceinline__ void db_partial(const DbArgs& d, int b) {
+  const int strip = b % d.strips, rc = b / d.strips, c = strip * 256 + (int)threadIdx.x;
+  if (c >= d.O) return;
+  const int r0 = rc * d.chunk, r1 = min(d.rows, r0 + d.chunk);
+  const float* p = d.dout + (size_t)r0 * d.ld + c;
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r, p += d.ld) s += *p;
+  d.part[(size_t)rc * d.O + c] = s;
+}
+
+__device__ __forceinline__ void db_final(const DbArgs& d, int b) {
+  const int c = b * 256 + (int)threadIdx.x;
+  if (c >= d.O) return;
+  float s = 0.f;
+  for (int rc = 0; rc < d.nrc; ++rc) s += d.part[(size_t)rc * d.O + c];
+  d.db[c] = s;
+}
+
 // Two independent problems in one grid (a Linear layer's weight gradient and input gradient
-// both read dout): blocks [0, nb1) run problem 1 on its (n1 x m1 x z1) tile grid, the rest
-// problem 2.  One launch boundary instead of two, and the two small grids fill the chip together.
+// both read dout): blocks [0, nb1) run problem 1 on its (n1 x m1 x z1) tile grid, the next nb2
+// problem 2, and the last (when d.db) the bias gradient's chunk partials.  One launch boundary
+// instead of three, and the small grids fill the chip together.
 template <int MODE, int BM1, int BN1, int LA1, int LB1, int BM2, int BN2, int LA2, int LB2>
 __global__ __launch_bounds__(256) void gemm_pair_kernel(GemmArgs p1, int n1, int m1, GemmArgs p2,
-                                                        int n2, int m2) {
+                                                        int n2, int m2, DbArgs d) {
   constexpr int L1 = GemmLds<MODE, BM1, BN1>::BYTES, L2 = GemmLds<MODE, BM2, BN2>::BYTES;
   __shared__ __attribute__((aligned(16))) char smem[L1 > L2 ? L1 : L2];
   int b = blockIdx.x;
   const int nb1 = n1 * m1 * (p1.ws ? avd_cdiv_d(p1.K, p1.kchunk) : 1);
+  const int nb2 = n2 * m2 * (p2.ws ? avd_cdiv_d(p2.K, p2.kchunk) : 1);
   if (b < nb1) {
     gemm_tile<MODE, BM1, BN1, LA1, LB1>(p1, b % n1, (b / n1) % m1, b / (n1 * m1), smem);
-  } else {
+  } else if (b < nb1 + nb2) {
     b -= nb1;
     gemm_tile<MODE, BM2, BN2, LA2, LB2>(p2, b % n2, (b / n2) % m2, b / (n2 * m2), smem);
+  } else {
+    db_partial(d, b - nb1 - nb2);
   }
 }
 
-// C = alpha * sum_{z < S} ws[z] (+bias) (+beta C), fixed split order
+// C = alpha * sum_{z < S} ws[z] (+bias) (+beta C), fixed split order; blocks >= nmain (when
+// the launch carries a bias gradient) fold its chunk partials instead
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S,
                                                             int M, int N, float* __restrict__ C,
                                                             long long ldc,
                                                             const float* __restrict__ bias,
-                                                            float alpha, float beta) {
+                                                            float alpha, float beta, int nmain,
+                                                            DbArgs d) {
+  if ((int)blockIdx.x >= nmain) {
+    db_final(d, (int)blockIdx.x - nmain);
+    return;
+  }
   const long long MN = (long long)M * N;
-  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < MN; i += (long long)gridDim.x * 256) {
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < MN; i += (long long)nmain * 256) {
     float s = 0.f;
     for (int z = 0; z < S; ++z) s += ws[(size_t)z * MN + i];
     const int m = (int)(i / N), n = (int)(i % N);
@@ -450,12 +490,19 @@ GemmArgs make_args(const Plan& pl, int M, int N, int K, const float* A, long lon
                   pl.splits > 1 ? ws : nullptr};
 }
 
-void launch_splitk_reduce(const Plan& pl, const GemmArgs& a, hipStream_t st) {
+__global__ __launch_bounds__(256) void db_final_kernel(DbArgs d) { db_final(d, (int)blockIdx.x); }
+
+// the split-K reduce of one problem (plus, with d.db, the bias gradient's final fold); with no
+// split and a bias gradient, the fold alone
+void launch_splitk_reduce(const Plan& pl, const GemmArgs& a, hipStream_t st, const DbArgs* d = nullptr) {
+  const int nd = (d && d->db) ? avd_cdiv(d->O, 256) : 0;
   if (pl.splits > 1) {
     const long long MN = (long long)a.M * a.N;
     const int blocks = (int)std::min<long long>(avd_cdiv(MN, 256), 4096);
-    splitk_reduce_kernel<<<blocks, 256, 0, st>>>(a.ws, pl.splits, a.M, a.N, a.C, a.ldc, a.bias,
-                                                 a.alpha, a.beta);
+    splitk_reduce_kernel<<<blocks + nd, 256, 0, st>>>(a.ws, pl.splits, a.M, a.N, a.C, a.ldc, a.bias,
+                                                      a.alpha, a.beta, blocks, d ? *d : DbArgs{});
+  } else if (nd) {
+    db_final_kernel<<<nd, 256, 0, st>>>(*d);
   }
 }
 
@@ -488,21 +535,38 @@ void dispatch_gemm(const Plan& pl, int lA, int lB, const GemmArgs& a, hipStream_
 // 128x64, 64x64; anything else returns false and the caller launches the two GEMMs separately.
 template <int MODE>
 bool launch_pair(const Plan& p1, const GemmArgs& a1, const Plan& p2, const GemmArgs& a2,
-                 hipStream_t st) {
+                 const DbArgs& d, hipStream_t st) {
   if (p1.bm != 128 || p1.bn != 128) return false;
   const int n1 = avd_cdiv(a1.N, p1.bn), m1 = avd_cdiv(a1.M, p1.bm);
   const int n2 = avd_cdiv(a2.N, p2.bn), m2 = avd_cdiv(a2.M, p2.bm);
-  const int blocks = n1 * m1 * p1.splits + n2 * m2 * p2.splits;
+  const int blocks = n1 * m1 * p1.splits + n2 * m2 * p2.splits + (d.db ? d.nrc * d.strips : 0);
 #define AVD_P(BM2_, BN2_)                                                                      \
   if (p2.bm == BM2_ && p2.bn == BN2_) {                                                        \
     gemm_pair_kernel<MODE, 128, 128, LAY_R, LAY_R, BM2_, BN2_, LAY_K, LAY_R>                   \
-        <<<blocks, 256, 0, st>>>(a1, n1, m1, a2, n2, m2);                                      \
+        <<<blocks, 256, 0, st>>>(a1, n1, m1, a2, n2, m2, d);                                   \
   }
   AVD_P(128, 128) else AVD_P(128, 64) else AVD_P(64, 64) else return false;
 #undef AVD_P
-  launch_splitk_reduce(p1, a1, st);
+  launch_splitk_reduce(p1, a1, st, &d);
   launch_splitk_reduce(p2, a2, st);
   return true;
+}
+
+__global__ __launch_bounds__(256) void db_partial_kernel(DbArgs d) { db_partial(d, (int)blockIdx.x); }
+
+// bias-gradient chunking: ~128 row chunks
+DbArgs db_args(const float* dout, long long ld, int rows, int O, float* part, float* db) {
+  DbArgs d{};
+  d.dout = dout; d.ld = ld; d.rows = rows; d.O = O;
+  d.chunk = std::max(1, avd_cdiv(rows, 128));
+  d.nrc = avd_cdiv(rows, d.chunk);
+  d.strips = avd_cdiv(O, 256);
+  d.part = part; d.db = db;
+  return d;
+}
+long long db_ws_elems(int rows, int O) {
+  const int chunk = std::max(1, avd_cdiv(rows, 128));
+  return (long long)avd_cdiv(rows, chunk) * O;
 }
 
 }  // namespace
@@ -510,12 +574,13 @@ bool launch_pair(const Plan& p1, const GemmArgs& a1, const Plan& p2, const GemmA
 extern "C" {
 
 long long avd_linear_bwd_ws_elems(int rows, int O, int In, int mode) {
-  return avd_gemm_ws_elems(O, In, rows, mode) + avd_gemm_ws_elems(rows, In, O, mode);
+  return avd_gemm_ws_elems(O, In, rows, mode) + avd_gemm_ws_elems(rows, In, O, mode) +
+         db_ws_elems(rows, O);
 }
 
 int avd_linear_bwd(int rows, int O, int In, const float* dout, long long dout_ld, const float* x,
-                   long long x_ld, const float* W, float* dW, float* dX, long long dx_ld, int mode,
-                   float* ws, long long ws_elems, void* stream) {
+                   long long x_ld, const float* W, float* dW, float* dX, long long dx_ld, float* db,
+                   int mode, float* ws, long long ws_elems, void* stream) {
   if (!dout || !x || !W || !dW || !dX) return AVD_ERR_ARG;
   if (rows <= 0 || O <= 0 || In <= 0 || dout_ld < O || x_ld < In || dx_ld < In) return AVD_ERR_SHAPE;
   if (mode != 1 && mode != 2) return AVD_ERR_ARG;
@@ -523,10 +588,13 @@ int avd_linear_bwd(int rows, int O, int In, const float* dout, long long dout_ld
   Plan p1 = plan_for(O, In, rows), p2 = plan_for(rows, In, O);
   const long long w1 = p1.splits > 1 ? (long long)p1.splits * O * In : 0;
   const long long w2 = p2.splits > 1 ? (long long)p2.splits * rows * In : 0;
+  const long long w3 = db_ws_elems(rows, O);
+  if (db && (!ws || ws_elems < w1 + w2 + w3)) return AVD_ERR_ARG;   // the bias partials need room
   if (!ws || ws_elems < w1 + w2) {   // no (or too small a) workspace: single passes over K
     if (p1.splits > 1) { p1.splits = 1; p1.kchunk = rows; }
     if (p2.splits > 1) { p2.splits = 1; p2.kchunk = O; }
   }
+  const DbArgs d = db_args(dout, dout_ld, rows, O, db ? ws + w1 + w2 : nullptr, db);
   // dW[o, i] = sum_r dout[r, o] x[r, i]; dX[r, i] = sum_o dout[r, o] W[o, i]
   const GemmArgs a1 = make_args(p1, O, In, rows, dout, 1, dout_ld, x, x_ld, 1, dW, In, nullptr,
                                 1.f, 0.f, ws);
@@ -536,8 +604,12 @@ int avd_linear_bwd(int rows, int O, int In, const float* dout, long long dout_ld
                    lay_of(dout, dout_ld, 1) == LAY_K && lay_of(W, 1, In) == LAY_R;
   bool done = false;
   if (lay)
-    done = mode == 1 ? launch_pair<1>(p1, a1, p2, a2, st) : launch_pair<2>(p1, a1, p2, a2, st);
+    done = mode == 1 ? launch_pair<1>(p1, a1, p2, a2, d, st) : launch_pair<2>(p1, a1, p2, a2, d, st);
   if (!done) {
+    if (db) {
+      db_partial_kernel<<<d.nrc * d.strips, 256, 0, st>>>(d);
+      db_final_kernel<<<avd_cdiv(O, 256), 256, 0, st>>>(d);
+    }
     const int l1a = lay_of(dout, 1, dout_ld), l1b = lay_of(x, 1, x_ld);
     const int l2a = lay_of(dout, dout_ld, 1), l2b = lay_of(W, 1, In);
     if (mode == 1) {
