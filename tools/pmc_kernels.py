@@ -9,7 +9,10 @@ from collections import defaultdict
 
 def main(root):
     acc = defaultdict(lambda: defaultdict(list))
-    for f in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True)):
+    files = sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True))
+    # one pass written straight into DIR (rocprofv3 -d DIR -o run)
+    files = files or sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True))
+    for f in files:
         per = defaultdict(float)
         with open(f) as fh:
             for row in csv.DictReader(fh):
