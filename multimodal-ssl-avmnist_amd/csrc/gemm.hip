@@ -456,7 +456,10 @@ Plan plan_for(int M, int N, int K) {
   if (N > 128 && N <= 256 && K >= 1024 && M >= 4096) {
     Plan p{128, 256, 1, K};
     const long long t = tiles(128, 256);
-    const int s = (int)std::max(1ll, std::min<long long>(avd_cdiv(224, t), K / 128));
+    // split target in blocks (AVDINO_GEMM_N256_BLOCKS, A/B runs)
+    static const int target256 =
+        getenv("AVDINO_GEMM_N256_BLOCKS") ? atoi(getenv("AVDINO_GEMM_N256_BLOCKS")) : 224;
+    const int s = (int)std::max(1ll, std::min<long long>(avd_cdiv(target256, t), K / 128));
     if (s > 1) {
       p.kchunk = avd_cdiv(avd_cdiv(K, s), 32) * 32;
       p.splits = avd_cdiv(K, p.kchunk);
