@@ -279,9 +279,12 @@ def main():
         raise SystemExit("--dtype fp8 is the multimodal DINO conv path (config 5); use --workload dino")
     eng, pool, B, workload, model = build_workload(args, device, act, world, rank, avdist)
 
+    last = [-1]
+
     def step(i):
         """Step i of the run over the batch pool (multimodal DINO: the next batch rides along
         for the pipelined teacher forward)."""
+        last[0] = i
         if getattr(eng, "pipeline", False):
             return eng.step(pool[i % len(pool)], next_batch=pool[(i + 1) % len(pool)])
         return eng.step(pool[i % len(pool)])
@@ -390,7 +393,7 @@ def main():
         around ``reps`` back-to-back replays: the kernel's own speed, free of the time-sharing
         with the other streams' kernels that the in-step duration includes."""
         ops.TIMER = ops.KernelTimer(only=[k])
-        step(args.warmup + args.steps + 3)
+        step(last[0] + 1)          # consecutive: a pipelined step expects the previous next_batch
         torch.cuda.synchronize()
         fn, ops.TIMER = ops.TIMER.replay, None
         if fn is None:
