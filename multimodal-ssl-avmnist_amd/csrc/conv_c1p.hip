@@ -1331,6 +1331,10 @@ __global__ __launch_bounds__(256) void c1p8_apply_kernel(
 //   M [8][25] | Gram [25][25] | S [25] | sum dz [8]
 constexpr int MOMC = COUT * 25 + 25 * 25 + 25 + COUT;
 
+#ifndef C1MC_DIAG
+#define C1MC_DIAG 0   // diagnostic builds only: 1 no input copies, 2 no dz map (wrong results)
+#endif
+
 __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ gz, const unsigned* __restrict__ codes,
     float* __restrict__ out, int B, int G, int R, int H, int W, int tps) {
@@ -1389,7 +1393,7 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int t = tid + 256 * s;
-      if (t >= nxt) continue;
+      if (t >= nxt || (C1MC_DIAG & 1)) continue;
       const int r = t / cpr, c = t - r * cpr;
       const unsigned wv[4] = {xv[s].x, xv[s].y, xv[s].z, xv[s].w};
       const unsigned e0 = (wv[0] & 0xffffu) | (wv[1] << 16), ee1 = (wv[2] & 0xffffu) | (wv[3] << 16);
@@ -1418,7 +1422,7 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int w = tid + 256 * s;
-      if (w >= nwin) continue;
+      if (w >= nwin || (C1MC_DIAG & 2)) continue;
       const int hp = w / Wp, wp = w - hp * Wp;
       const unsigned gw[4] = {gv[s].x, gv[s].y, gv[s].z, gv[s].w}, code = cv[s];
       unsigned ow[4][4];
