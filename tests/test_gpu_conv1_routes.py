@@ -1,0 +1,132 @@
+"""The first-layer training routes of the bf16 step against each other.
+
+* The image conv1's pixel-major passes (avd_cl_c1r5_stats / avd_cl_c1r5_apply_codes) and its
+  routed moments pass (avd_cl_c1r5_moments_codes) with AVDINO_GRID_CAP forcing a handful of
+  blocks, so every block walks many samples across BN-group boundaries: the pooled map and the
+  codes are bit-identical to the uncapped launch, the statistics and moments are fp32 sums in
+  another order (rel 1e-6).
+* The engine's routed conv1 backward (codes written by the forward pooling pass) against its
+  recomputing moments pass (AVDINO_C1_CODES=0) on the same state and batch: the forward is the
+  same launch sequence (bitwise equal loss), every gradient outside the two first layers is
+  bitwise equal, the first layers' weight / BN gradients agree to 1e-2 (the routed pass forms
+  sum dz * y at the exact conv output, the recomputing one at the bf16-rounded y; the bias,
+  analytically 0, is rounding noise under both).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+T = torch.bfloat16
+F64 = torch.float64
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from avdino import ops as _ops
+    return _ops
+
+
+def grel(a, b):
+    a, b = a.to(F64).reshape(-1), b.to(F64).reshape(-1)
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("cap", [3, 7])
+def test_image_conv1_passes_capped_grid(ops, monkeypatch, cap):
+    N, B, H, C = 96, 32, 28, 32
+    G, Hp = N // B, H // 2
+    g = torch.Generator(device="cuda").manual_seed(23)
+    x = (torch.randint(0, 256, (N, H, H, 1), generator=g, device="cuda").float() / 255).to(T)
+    w = ((torch.rand(C, 1, 5, 5, generator=g, device="cuda") - 0.5) / 2.5).to(T).float()
+    bias = (torch.rand(C, generator=g, device="cuda") - 0.5) / 5
+    wk = torch.empty(ops.cl_weight_elems(C, 1, 5, False), device="cuda", dtype=T)
+    ops.cl_weight_layout(w.contiguous(), wk, False)
+    gamma = 0.8 + 0.4 * torch.rand(C, generator=g, device="cuda")
+    beta = (torch.rand(C, generator=g, device="cuda") - 0.5) / 2.5
+    gz = ((torch.rand(N, Hp, Hp, C, generator=g, device="cuda") - 0.5) * 2).to(T)
+
+    def stats():
+        R = ops.c1r5_stats_rows(N, B, H, H)
+        sp = torch.empty(C * G * R * 2, device="cuda")
+        ops.c1r5_stats(x, wk, bias, sp, N, B, H, H)
+        bn = torch.empty(4, G * C, device="cuda")
+        ops.bn_finalize(sp, G, R, C, B * H * H, gamma, beta, bn[0], bn[1], bn[2], bn[3])
+        return bn
+
+    def apply(bn):
+        z = torch.full((N, Hp, Hp, C), float("nan"), device="cuda", dtype=T)
+        codes = torch.full((N * Hp * Hp * 8,), -1, device="cuda", dtype=torch.int16)
+        ops.c1r5_apply_codes(x, wk, bias, bn[2], bn[3], z, codes, N, B, H, H)
+        return z, codes
+
+    def moments(codes):
+        Rc, mc = ops.c1r5_codes_rows(N, B, H, H), ops.c1r5_codes_cols()
+        parts = torch.empty(Rc * G * mc, device="cuda")
+        ops.c1r5_moments_codes(x, gz, codes, parts, N, B, H, H)
+        mom = torch.empty(G * mc, device="cuda")
+        ops.sum_rows(parts, Rc, G * mc, mom)
+        return mom
+
+    bn0 = stats()
+    z0, c0 = apply(bn0)
+    m0 = moments(c0)
+    monkeypatch.setenv("AVDINO_GRID_CAP", str(cap))
+    bn1 = stats()
+    z1, c1 = apply(bn0)                   # the uncapped coefficients: a block-independent map
+    m1 = moments(c0)
+    monkeypatch.delenv("AVDINO_GRID_CAP")
+    assert grel(bn1, bn0) < 1e-6
+    assert torch.equal(z1, z0) and torch.equal(c1, c0)
+    assert grel(m1, m0) < 1e-6
+
+
+def test_engine_routed_conv1_backward_equals_recompute():
+    from avdino.engine import ConvBranch, Hyper, MultiCentralEngine
+    from avdino.params import ParamStore
+    from avdino.spec import multimodal_dino_sd
+    from oracle.params import make_state
+    from oracle import spec as OS
+    E = D = 64
+    P, B, G, L = 32, 64, 2, 4
+    state = make_state(OS.multimodal_dino_spec("mse", E, D, P), 411)
+    gen = torch.Generator(device="cuda").manual_seed(412)
+
+    def px(*s):
+        return torch.randint(0, 256, s, generator=gen, device="cuda", dtype=torch.int32).float() / 255
+
+    batch = dict(g_img=px(B, G, 1, 28, 28), g_aud=px(B, G, 1, 112, 112), l_img=px(B, L, 1, 28, 28),
+                 l_aud=px(B, L, 1, 112, 112), image=px(B, 1, 28, 28), audio=px(B, 1, 112, 112))
+    out = {}
+    for codes in (True, False):
+        old = ConvBranch.CODES
+        ConvBranch.CODES = codes
+        try:
+            store = ParamStore(multimodal_dino_sd("mse", E, D, P), "cuda")
+            store.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state.items()})
+            eng = MultiCentralEngine(store, "mse", E, D, P, Hyper(dropout=0.0, fusion_dropout=0.0),
+                                     act_dtype=torch.bfloat16)
+            loss = eng.forward(batch).item()
+            eng.backward()
+            torch.cuda.synchronize()
+            out[codes] = (loss, {k: store.grad_of(k).detach().clone() for k in store.live_keys})
+        finally:
+            ConvBranch.CODES = old
+    (l1, g1), (l0, g0) = out[True], out[False]
+    assert l1 == l0
+    first = ("student.audio_encoder.0.conv1.", "student.audio_encoder.0.bn1.",
+             "student.image_encoder.0.conv1.", "student.image_encoder.0.bn1.")
+    checked = 0
+    for k in g0:
+        if k.startswith(first):
+            if k.endswith("conv1.bias"):
+                # sum dy of a BN'd conv: analytically 0, both routes leave rounding noise
+                scale = g0[k.replace("conv1.bias", "bn1.bias")].norm().item()
+                assert g1[k].norm().item() < 1e-3 * scale and g0[k].norm().item() < 1e-3 * scale, k
+            else:
+                assert grel(g1[k], g0[k]) < 1e-2, (k, grel(g1[k], g0[k]))
+                checked += 1
+        else:
+            assert torch.equal(g1[k], g0[k]), k
+    assert checked == 6
