@@ -534,7 +534,8 @@ int avd_cl_c1_codes_combine(const float* moments, const void* wk, const float* b
  * group g) of avd_cl_c1r5_codes_rows rows, avd_cl_c1r5_codes_cols() floats: M[32][25] |
  * Gram[25][25] | S[25] | sum dz[32] at out[(r * G + g) * cols + ...] (reduce with avd_sum_rows);
  * the taps come from shifted copies of the image (no im2col gather).
- * avd_cl_c1r5_codes_combine: as avd_cl_c1_codes_combine for the 32 channels (G <= 8). */
+ * avd_cl_c1r5_codes_combine: as avd_cl_c1_codes_combine for the 32 channels (G <= 32; the rows
+ * functions return 0 beyond, and the engine then runs the recomputing moments pass). */
 /* avd_cl_c1r5_stats: BN partial sums (sum y, sum y^2 of the bf16 y) of the recomputed image conv1
  * output as parts [32][G][R][2], R = avd_cl_c1r5_stats_rows (avd_bn_finalize's layout); the
  * pixel-major MFMA of avd_cl_c1r5_apply_codes, whose codes argument may be NULL (no backward). */

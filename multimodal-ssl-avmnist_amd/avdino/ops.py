@@ -637,7 +637,7 @@ def c1r5_moments_codes(x, gz, codes, out, N, B, H, W):
 
 def c1r5_codes_combine(moments, wk, bias, gamma, mean, invstd, count, dw, dgamma, dbeta, dbias, coef, G):
     """bn1 backward + image conv1 bias / weight gradients from the row-summed moments."""
-    _need(moments.numel() >= G * c1r5_codes_cols() and dw.numel() >= 800 and G <= 8, "c1r5 codes combine")
+    _need(moments.numel() >= G * c1r5_codes_cols() and dw.numel() >= 800 and G <= 32, "c1r5 codes combine")
     call("avd_cl_c1r5_codes_combine", p(moments), p(wk), p(bias), p(gamma), p(mean), p(invstd),
          int(count), p(dw), p(dgamma), p(dbeta), p(dbias), p(coef), G, stream())
 

@@ -33,6 +33,7 @@ namespace {
 constexpr int C = 32, KK = 25, IH = 28, IW = 28, VW = 32;   // channels, taps, image, virtual width
 constexpr int HP = IH / 2, WP = IW / 2, NWIN = HP * WP;     // pooling windows per sample
 constexpr int MOMC5 = C * KK + KK * KK + KK + C;
+constexpr int C1R5_GMAX = 32;                              // BN groups served by the combine
 constexpr int NCOPY = 6, CROWS = IH + 4;                     // copies: tx = -2..2, ones; rows: pad 2
 constexpr int XS_R = IH + 4, XS_C = IW + 4 + 4;              // staged image, 2-pixel halo (+ pad)
 constexpr int LDS_X = XS_R * XS_C;                           // bf16 elements
@@ -459,12 +460,12 @@ __global__ __launch_bounds__(256) void c1r5_codes_combine_kernel(
     const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
     long long count, float* __restrict__ dw, float* __restrict__ dgamma, float* __restrict__ dbeta,
     float* __restrict__ dbias, float* __restrict__ coef, int G) {
-  __shared__ double sk[8 * C][3];
-  __shared__ double s12[8 * C][2];
+  __shared__ double sk[C1R5_GMAX * C][3];
+  __shared__ double s12[C1R5_GMAX * C][2];
   const int tid = threadIdx.x;
   const double n = (double)count;
-  if (tid < G * C) {
-    const int gq = tid / C, c = tid - gq * C;
+  for (int i = tid; i < G * C; i += 256) {
+    const int gq = i / C, c = i - gq * C;
     const float* mg = m + (size_t)gq * MOMC5;
     const double b = bias ? (double)bias[c] : 0.0;
     const double s1 = mg[C * KK + KK * KK + KK + c];
@@ -473,12 +474,12 @@ __global__ __launch_bounds__(256) void c1r5_codes_combine_kernel(
     const double mu = mean[gq * C + c], is = invstd[gq * C + c], ga = gamma[c];
     const double s2 = (sy - mu * s1) * is;                   // sum dz * xhat
     const double k1 = ga * is, kx = -ga * is * is * s2 / n, k0 = -ga * is * s1 / n + ga * is * is * mu * s2 / n;
-    sk[tid][0] = k1; sk[tid][1] = kx; sk[tid][2] = k0;
-    s12[tid][0] = s1; s12[tid][1] = s2;
+    sk[i][0] = k1; sk[i][1] = kx; sk[i][2] = k0;
+    s12[i][0] = s1; s12[i][1] = s2;
     if (coef) {
-      coef[tid * 3 + 0] = (float)k1;
-      coef[tid * 3 + 1] = (float)kx;
-      coef[tid * 3 + 2] = (float)k0;
+      coef[i * 3 + 0] = (float)k1;
+      coef[i * 3 + 1] = (float)kx;
+      coef[i * 3 + 2] = (float)k0;
     }
   }
   __syncthreads();
@@ -539,7 +540,7 @@ extern "C" {
 
 // shape served: Cin 1, Cout 32, 5x5 pad 2 on 28x28, bf16 (the CentralNet image conv1)
 int avd_cl_c1r5_codes_rows(int N, int B, int H, int W) {
-  if (N <= 0 || B <= 0 || N % B || H != IH || W != IW || N / B > 8) return 0;
+  if (N <= 0 || B <= 0 || N % B || H != IH || W != IW || N / B > C1R5_GMAX) return 0;
   return c1r5_rows(N, B);
 }
 
@@ -615,7 +616,7 @@ int avd_cl_c1r5_codes_combine(const float* moments, const void* wk, const float*
                               long long count, float* dw, float* dgamma, float* dbeta, float* dbias,
                               float* coef, int G, void* stream) {
   if (!moments || !wk || !gamma || !mean || !invstd || !dw) return AVD_ERR_ARG;
-  if (G <= 0 || G > 8 || count <= 1) return AVD_ERR_SHAPE;
+  if (G <= 0 || G > C1R5_GMAX || count <= 1) return AVD_ERR_SHAPE;
   c1r5_codes_combine_kernel<<<1, 256, 0, avd_stream(stream)>>>(moments, (const bf16*)wk, bias, gamma,
                                                                mean, invstd, count, dw, dgamma, dbeta,
                                                                dbias, coef, G);

@@ -212,8 +212,8 @@ int avd_cl_c1_recompute_combine(const float* moments, const float* coef, const v
 
 namespace {
 bool c1_codes_shape(int N, int B, int H, int W) {
-  return N > 0 && B > 0 && N % B == 0 && avd_c1p8_eligible(AVD_BF16, 1, 8, 5, H, W) && W <= 112 &&
-         H % 2 == 0 && W % 2 == 0;
+  return N > 0 && B > 0 && N % B == 0 && N / B <= 32 && avd_c1p8_eligible(AVD_BF16, 1, 8, 5, H, W) &&
+         W <= 112 && H % 2 == 0 && W % 2 == 0;   // <= 32 BN groups: the combine's table
 }
 }  // namespace
 

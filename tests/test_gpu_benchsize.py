@@ -514,9 +514,8 @@ def test_bf16_step_vs_fp32_step_config2(capsys, B, L):
     (the larger of its bf16-autocast and its fp16 '16-mixed' error, floor 1e-2: on an 8-value BN
     tensor either one alone can sit far below the other by chance -- B = 256 / L = 7 gave the
     audio bn1 weight 0.065 under bf16 and 0.448 under fp16, ours 0.335); the median within 1.25x
-    of the bf16-autocast median.  The B512_L7 case (9 student BN groups) takes the conv1
-    fallbacks: the routed moments passes serve at most 8 groups, so both first layers run the
-    recomputing moments pass."""
+    of the bf16-autocast median.  The B512_L7 case runs the student conv branches at 10 BN
+    groups (2 global + 7 local views + the originals)."""
     from avdino.engine import Hyper, MultiCentralEngine
     from avdino.params import ParamStore
     from avdino.spec import multimodal_dino_sd
@@ -774,7 +773,7 @@ def test_conv1_routed_backward_bench_size(ops):
     assert grel(dw, d4) < 3e-3 and grel(db, db4) < 1e-5
 
 
-@pytest.mark.parametrize("N,B", [(24, 8), (N_STUDENT, B_BENCH)])
+@pytest.mark.parametrize("N,B", [(24, 8), (320, 32), (N_STUDENT, B_BENCH)])
 def test_image_conv1_routed_backward(ops, N, B):
     """The IMAGE conv1 (1->32, 5x5 pad 2 on 28x28) training backward from the forward's routing
     codes (avd_cl_c1r5_apply_codes + avd_cl_c1r5_moments_codes + avd_cl_c1r5_codes_combine): the
