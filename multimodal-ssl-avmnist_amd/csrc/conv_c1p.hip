@@ -1362,13 +1362,15 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
 
   // global loads one tile ahead: <= 2 input-row vectors, and the pooled gradients + codes of
   // this thread's <= 2 windows
-  const int nxt = (TH + 4) * cpr, nwin = (TH / 2) * Wp;
+  // input rows: one row per 16-lane DPP row (lane c < cpr holds pixels 8c .. 8c+7), so the
+  // parity/shift copies take a neighbour's edge pair by DPP instead of sub-dword LDS stores
+  const int nwin = (TH / 2) * Wp;
   int xr[2], xoff[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const int t = tid + 256 * s;
-    const int r = t / cpr, c = t - r * cpr;
-    xr[s] = t < nxt ? r : -(1 << 20);
+    const int r = t >> 4, c = t & 15;
+    xr[s] = (r < TH + 4 && c < cpr) ? r : -(1 << 20);
     xoff[s] = (r - 2) * W + 8 * c;
   }
   u4 xv[2], gv[2];
@@ -1389,34 +1391,29 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
   if (t_begin < t_end) load(t_begin);
   for (int tile = t_begin; tile < t_end; ++tile) {
     __syncthreads();                     // the previous tile's MFMAs are done with LDS
-    // ---- parity/shift copies of the input rows (B operand)
+    // ---- parity/shift copies of the input rows (B operand): xc[b][a][r][P] = x[2(P+a-1)+b],
+    // three aligned 8-byte stores per parity; the pairs across a thread's edges come from its
+    // row neighbours by DPP (row_shr / row_shl 1; lanes past the row end hold zeros = the pads)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int t = tid + 256 * s;
-      if (t >= nxt || (C1MC_DIAG & 1)) continue;
-      const int r = t / cpr, c = t - r * cpr;
+      const int r = t >> 4, c = t & 15;
       const unsigned wv[4] = {xv[s].x, xv[s].y, xv[s].z, xv[s].w};
-      const unsigned e0 = (wv[0] & 0xffffu) | (wv[1] << 16), ee1 = (wv[2] & 0xffffu) | (wv[3] << 16);
-      const unsigned o0 = (wv[0] >> 16) | (wv[1] & 0xffff0000u), o1 = (wv[2] >> 16) | (wv[3] & 0xffff0000u);
-      const unsigned ev[2] = {e0, ee1}, od[2] = {o0, o1};
+      const unsigned ev[2] = {(wv[0] & 0xffffu) | (wv[1] << 16), (wv[2] & 0xffffu) | (wv[3] << 16)};
+      const unsigned od[2] = {(wv[0] >> 16) | (wv[1] & 0xffff0000u), (wv[2] >> 16) | (wv[3] & 0xffff0000u)};
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const unsigned lo = b ? od[0] : ev[0], hi = b ? od[1] : ev[1];
-        *reinterpret_cast<uint2*>(&xc[xbo(b, 1, r, 4 * c)]) = make_uint2(lo, hi);
-        bf16* d0 = &xc[xbo(b, 0, r, 4 * c + 1)];
-        st16(d0, (bf16)(lo & 0xffffu));
-        *reinterpret_cast<unsigned*>(d0 + 1) = (lo >> 16) | (hi << 16);
-        st16(d0 + 3, (bf16)(hi >> 16));
-        bf16* d2 = &xc[xbo(b, 2, r, 4 * c)];
-        if (c > 0) st16(d2 - 1, (bf16)(lo & 0xffffu));
-        *reinterpret_cast<unsigned*>(d2) = (lo >> 16) | (hi << 16);
-        st16(d2 + 2, (bf16)(hi >> 16));
+        const unsigned prev_hi = (unsigned)dpp_i<0x111>((int)hi);   // lane c-1 (0 at c = 0)
+        const unsigned next_lo = (unsigned)dpp_i<0x101>((int)lo);   // lane c+1
+        if (r < TH + 4 && c < cpr && !(C1MC_DIAG & 1)) {
+          *reinterpret_cast<uint2*>(&xc[xbo(b, 0, r, 4 * c)]) =
+              make_uint2((prev_hi >> 16) | (lo << 16), (lo >> 16) | (hi << 16));
+          *reinterpret_cast<uint2*>(&xc[xbo(b, 1, r, 4 * c)]) = make_uint2(lo, hi);
+          *reinterpret_cast<uint2*>(&xc[xbo(b, 2, r, 4 * c)]) =
+              make_uint2((lo >> 16) | (hi << 16), (hi >> 16) | (next_lo << 16));
+        }
       }
-    }
-    if (tid < (TH + 4) * 2) {
-      const int r = tid >> 1, b = tid & 1;
-      xc[xbo(b, 0, r, 0)] = bf16(0);
-      xc[xbo(b, 2, r, Wp - 1)] = bf16(0);
     }
     // ---- dz at the coded pixel of every window (4 pixels x 8 channels per window thread)
 #pragma unroll
