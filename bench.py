@@ -30,7 +30,7 @@ import torch  # noqa: E402
 METRIC = "AVMNIST audio-image pairs/sec (multimodal DINO step) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # dense, no sparsity; non-scaled fp8 MFMA (v_mfma_f32_16x16x32_fp8_fp8) runs at the bf16 rate
-MFMA_PEAK_TFS = {"bf16": 2500.0, "f32": 157.3, "fp8": 2500.0}
+MFMA_PEAK_TFS = {"bf16": 2500.0, "f32": 157.3, "fp8": 5000.0}   # fp8: the dense block-scaled peak
 # SURVEY 8(d) "BN-barrier" algorithmic HBM bytes per pair of a whole training step (inputs read
 # once, each train-mode-BN'd conv output written once and read once forward, saved output read
 # + its gradient written / read backward; weights amortised), bf16 storage; f32 doubles them
@@ -167,16 +167,20 @@ def build_workload(args, device, act, world, rank, avdist):
 
 def host_cpu():
     """The host CPU the baseline ran on (lscpu's model name and core counts, read from
-    /proc/cpuinfo: lscpu may be absent on the GPU box): model, physical cores, logical CPUs, and
-    the CPUs this process may run on (the box's CPU share)."""
-    model, phys = None, set()
+    /proc/cpuinfo: lscpu may be absent on the GPU box): model, physical cores, logical CPUs, the
+    CPUs this process may run on (affinity), the physical cores among them, and the cgroup CPU
+    quota (cpu.max) when one is set."""
+    model, phys, cpu2core = None, set(), {}
     cur = {}
     try:
         with open("/proc/cpuinfo") as f:
-            for line in f:
+            for line in list(f) + [""]:
                 if not line.strip():
                     if "physical id" in cur and "core id" in cur:
-                        phys.add((cur["physical id"], cur["core id"]))
+                        core = (cur["physical id"], cur["core id"])
+                        phys.add(core)
+                        if "processor" in cur:
+                            cpu2core[int(cur["processor"])] = core
                     cur = {}
                     continue
                 k, _, v = line.partition(":")
@@ -187,16 +191,56 @@ def host_cpu():
     except OSError:
         pass
     try:
-        aff = len(os.sched_getaffinity(0))
+        aff = sorted(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        aff = None
+        aff = list(range(os.cpu_count() or 1))
+    aff_cores = len({cpu2core[c] for c in aff if c in cpu2core}) or None
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = -(-int(q) // int(per))
+    except (OSError, ValueError):
+        pass
     return {"cpu_model": model, "physical_cores": len(phys) or None, "logical_cpus": os.cpu_count(),
-            "affinity_cpus": aff}
+            "affinity_cpus": len(aff), "affinity_physical_cores": aff_cores, "cgroup_cpu_quota": quota}
+
+
+def cpu_threads(host):
+    """Threads for the CPU baseline: one per physical core this process may use (BASELINE.md
+    section 2: torch.set_num_threads(cpu count)) -- the physical cores of its affinity set,
+    capped by a cgroup CPU quota when the box enforces one.  ``cores`` in the line is this
+    number: one thread per physical core."""
+    n = host.get("affinity_physical_cores") or host.get("affinity_cpus") or os.cpu_count() or 1
+    if host.get("cgroup_cpu_quota"):
+        n = min(n, host["cgroup_cpu_quota"])
+    return max(1, int(n))
+
+
+class _Threads:
+    """torch.set_num_threads(n) for a block, restored afterwards."""
+
+    def __init__(self, n):
+        self.n = n
+
+    def __enter__(self):
+        self.old = torch.get_num_threads()
+        torch.set_num_threads(self.n)
+
+    def __exit__(self, *exc):
+        torch.set_num_threads(self.old)
 
 
 def cpu_baseline_uni(batch, seconds):
     """Config 1's reference path on the host cores: training_structures.pretrain_dino's step
     (oracle/torch_port.py UniImageDINO + pretrain_step: AdamW, EMA after the step), fp32."""
+    host = host_cpu()
+    with _Threads(cpu_threads(host)):
+        return _cpu_baseline_uni(batch, seconds, host)
+
+
+def _cpu_baseline_uni(batch, seconds, host):
     from oracle import torch_port as TP
     torch.manual_seed(0)
     model = TP.UniImageDINO()
@@ -213,15 +257,22 @@ def cpu_baseline_uni(batch, seconds):
         if (n >= 2 and el >= seconds) or n >= 2000:
             break
     return {"value": round(batch * n / el, 2), "unit": "pairs/s", "cores": torch.get_num_threads(),
-            "kind": "port", "host": host_cpu(),
+            "kind": "port", "host": host,
             "sample": f"oracle/torch_port.py UniImageDINO training_structures.pretrain_dino step "
                       f"(dino_train.py:143-161), fp32, B={batch}, 2 global views, {n} timed steps "
-                      f"({el:.1f} s) after 1 warm-up, torch CPU {torch.get_num_threads()} threads"}
+                      f"({el:.1f} s) after 1 warm-up, torch CPU {torch.get_num_threads()} threads, one per "
+                      f"physical core"}
 
 
 def cpu_baseline(batch, seconds):
     """The reference algorithm on the host cores (oracle/torch_port.py, fp32, per-view loops,
     Python EMA, torch.optim.Adam) on a bounded sample: B pairs/step, >= 2 timed steps."""
+    host = host_cpu()
+    with _Threads(cpu_threads(host)):
+        return _cpu_baseline(batch, seconds, host)
+
+
+def _cpu_baseline(batch, seconds, host):
     from oracle import torch_port as TP
     torch.manual_seed(0)
     model = TP.DinoMSE()
@@ -247,11 +298,11 @@ def cpu_baseline(batch, seconds):
         if (n >= 2 and el >= seconds) or n >= 400:
             break
     return {"value": round(batch * n / el, 2), "unit": "pairs/s", "cores": torch.get_num_threads(),
-            "kind": "port", "host": host_cpu(),
+            "kind": "port", "host": host,
             "sample": f"oracle/torch_port.py multi_central mse step (the reference's Lightning "
                       f"training_step ops, dino.py:1214-1238), fp32, B={batch}, 2 global + 4 local "
                       f"views, {n} timed steps ({el:.1f} s) after a B=32 warm-up step, torch CPU "
-                      f"{torch.get_num_threads()} threads"}
+                      f"{torch.get_num_threads()} threads, one per physical core"}
 
 
 def main():

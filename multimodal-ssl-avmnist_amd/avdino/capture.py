@@ -62,11 +62,14 @@ class GraphedStep:
     A graph holds the device pointers of the scratch buffers it was captured over; when any of
     them is reallocated later (a larger key's eager warm-up grows a shared buffer, e.g. SimCLR's
     image/image mode captured before its audio/audio mode was first seen) the graph is stale:
-    each capture records the allocation epoch after it and is dropped and re-captured instead
-    of replayed once the epoch has moved."""
+    each capture records ``deps()`` after it -- the allocation epochs of exactly the buffers
+    the step uses (its engine's workspaces and the shared GEMM / row-sum scratch; default: the
+    shared scratch epoch alone) -- and is dropped and re-captured instead of replayed once
+    they have moved."""
 
-    def __init__(self, warmup=2):
+    def __init__(self, warmup=2, deps=None):
         self.warmup = warmup
+        self.deps = deps if deps is not None else ops.alloc_epoch
         self.graphs = {}     # key -> (segments, allocation epoch after the capture)
         self.seen = {}
         self.captures = 0
@@ -82,7 +85,7 @@ class GraphedStep:
         global _ACTIVE
         ent = self.graphs.get(key)
         if ent is not None:
-            if ent[1] == ops.alloc_epoch():
+            if ent[1] == self.deps():
                 for s in ent[0]:
                     if hasattr(s, "replay"):
                         s.replay()
@@ -125,5 +128,5 @@ class GraphedStep:
             finally:
                 _ACTIVE = None
         main.wait_stream(self.stream)
-        self.graphs[key] = (cap.seq, ops.alloc_epoch())
+        self.graphs[key] = (cap.seq, self.deps())
         self.captures += 1

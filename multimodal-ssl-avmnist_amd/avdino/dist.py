@@ -32,41 +32,61 @@ def rank(group=None):
 class GradAllReduce:
     """DDP's gradient averaging over the flat gradient arena, in buckets.
 
-    ``bucket(grad, ranges)`` all-reduces those ranges as soon as the step has produced them
-    (an engine calls it at a host point inside its captured step, avdino.capture): with RCCL
-    the collective runs on the process group's stream while the rest of the backward keeps
-    the compute stream busy.  ``hook(grad)`` -- after the step -- all-reduces whatever no
-    bucket covered (within ``ranges``, default the whole arena), waits for every bucket and
-    scales the reduced ranges by 1/world.  Every rank issues the same buckets in the same
-    order (same ranges, same step structure).  With no bucket it is one all-reduce over the
-    arena (the round-1/2 behaviour)."""
+    A step's exchange is ``begin()`` (eager, before the step), any number of
+    ``bucket(grad, ranges)`` calls as soon as the step has produced those ranges (an engine
+    calls it at a host point inside its captured step, avdino.capture: with RCCL the collective
+    runs on the process group's stream while the rest of the backward keeps the compute stream
+    busy), then ``finish(grad)`` -- all-reduce whatever no bucket covered (within ``ranges``,
+    default the whole arena) and make the caller's stream wait for every collective -- and
+    ``scale(grad)`` (x 1/world over the reduced ranges; plain device work, so a captured step
+    keeps it and the optimizer in its last graph segment).  ``hook(grad)`` = finish + scale.
+    Every rank issues the same buckets in the same order (same ranges, same step structure).
+    With no bucket it is one all-reduce over the arena.
 
-    def __init__(self, group=None):
+    ``overlap``: issue the bucket collectives asynchronously (default: on RCCL only -- gloo's
+    CUDA all-reduce stages through host memory on a worker thread, and left in flight under the
+    next replayed graph segment it stalled each step ~20x, 167-215 ms vs 9-11 ms per 2-rank
+    step); ``overlap=True`` under gloo runs the same pending / wait / scale order (tests)."""
+
+    def __init__(self, group=None, overlap=None):
         self.group = group
-        self.pending, self.covered = [], []
+        self.overlap = overlap
+        self.pending, self.covered, self.reduced = [], [], []
 
     def world(self):
         return dist.get_world_size(self.group)
 
+    def _async(self):
+        return self.overlap if self.overlap is not None else dist.get_backend(self.group) == "nccl"
+
+    def begin(self):
+        """Start a step's exchange.  Collectives still pending from an earlier step that never
+        reached finish() (an aborted step) are waited for and forgotten, so their ranges cannot
+        suppress this step's reduction of the same ranges (ranks would diverge silently)."""
+        for w in self.pending:
+            w.wait()
+        self.pending, self.covered, self.reduced = [], [], []
+
     def bucket(self, grad, ranges):
         if self.world() == 1:
             return
-        # RCCL: asynchronous on the process group's stream.  gloo (the 1-GPU rehearsal)
-        # completes it here: its CUDA all-reduce stages through host memory on a worker thread,
-        # and left in flight under the next replayed graph segment it stalled each step ~20x
-        # (measured 167-215 ms vs 9-11 ms per 2-rank step)
-        overlap = dist.get_backend(self.group) == "nccl"
+        overlap = self._async()
         for lo, hi in ranges:
             if hi > lo:
+                if any(lo < chi and clo < hi for clo, chi in self.covered):
+                    raise RuntimeError(f"gradient bucket [{lo}, {hi}) overlaps one already issued "
+                                       "this step (missing begin()?)")
                 w = dist.all_reduce(grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
                                     async_op=overlap)
                 if overlap:
                     self.pending.append(w)
                 self.covered.append((lo, hi))
 
-    def __call__(self, grad, ranges=None):
-        n = self.world()
-        if n > 1:
+    def finish(self, grad, ranges=None):
+        """All-reduce the rest of ``ranges`` and wait for every collective of this step;
+        records the reduced ranges for scale()."""
+        self.reduced = []
+        if self.world() > 1:
             want = [(0, grad.numel())] if ranges is None else list(ranges)
             rest = subtract_ranges(want, self.covered)
             for lo, hi in rest:
@@ -74,9 +94,18 @@ class GradAllReduce:
                                                     group=self.group, async_op=True))
             for w in self.pending:
                 w.wait()
-            for lo, hi in merge_ranges(self.covered + rest):
-                grad[lo:hi].mul_(1.0 / n)
+            self.reduced = merge_ranges(self.covered + rest)
         self.pending, self.covered = [], []
+
+    def scale(self, grad):
+        n = self.world()
+        for lo, hi in self.reduced:
+            grad[lo:hi].mul_(1.0 / n)
+
+    def __call__(self, grad, ranges=None):
+        self.finish(grad, ranges)
+        self.scale(grad)
+        self.reduced = []
 
 
 def merge_ranges(ranges):

@@ -35,19 +35,21 @@ BUCKETS = os.environ.get("AVDINO_GRAD_BUCKETS", "1") == "1"
 
 class Workspace:
     """Named device scratch buffers, grown on demand and reused across steps.  Every
-    (re)allocation bumps ops' allocation epoch, so graphs captured over the old buffers are
-    retired (GraphedStep)."""
+    (re)allocation bumps this workspace's own ``epoch``, so graphs captured over its old
+    buffers are retired (GraphedStep ``deps``) -- and only those: a probe's or a loss helper's
+    workspace growing does not retire an engine's graphs."""
 
     def __init__(self, device):
         self.device = device
         self.bufs = {}
+        self.epoch = 0
 
     def get(self, name, numel, dtype=F32):
         b = self.bufs.get(name)
         if b is None or b.numel() < numel or b.dtype != dtype:
             b = torch.empty(max(numel, 1), dtype=dtype, device=self.device)
             self.bufs[name] = b
-            ops.bump_alloc_epoch()
+            self.epoch += 1
         return b[:numel]
 
     def nbytes(self):
@@ -627,6 +629,28 @@ def ema_step(store, m):
     ops.ema(store.teacher, store.student[store.n_heads:], store.n_ema, m)
 
 
+def _exchange_in_step(hook):
+    """A bucket-capable gradient hook (dist.GradAllReduce) at world > 1: the step's final
+    exchange runs at a host point inside the step body (eager, or between captured segments),
+    followed by the 1/world scale and the optimizer in the same (last) graph segment."""
+    from . import dist as avdist
+    return (hasattr(hook, "finish") and BUCKETS
+            and avdist.world(getattr(hook, "group", None)) > 1)
+
+
+def _exchange_begin(hook):
+    """Start of a step's gradient exchange (eager, before any replayed segment)."""
+    if hasattr(hook, "begin"):
+        hook.begin()
+
+
+def _exchange_finish(hook, grad, ranges=None):
+    """Inside a step body, every forked stream joined: the rest of the all-reduce and the wait
+    at a host point, then x 1/world as device work of the current segment."""
+    host_point(lambda: hook.finish(grad, ranges))
+    hook.scale(grad)
+
+
 # ============================================================================ multimodal DINO
 class MultiCentralEngine:
     """Training step of MultiModalDINO{,WithMSE,WithINFONCE,SemiSupervised} over
@@ -681,7 +705,7 @@ class MultiCentralEngine:
         self.last = {}
         self.sstate = StepState(store.device, hp.lr, hp.betas)
         self.use_graph = False     # step(): capture the device work once, replay it (bench)
-        self.graph = GraphedStep()
+        self.graph = GraphedStep(deps=self._graph_deps)
         # pipeline=True: step(batch, next_batch) runs the teacher forward of next_batch on a
         # fourth stream under this step's backward (it only needs the EMA'd teacher and the next
         # batch's global views), so the next step's loss finds the teacher output ready.  Same
@@ -702,6 +726,11 @@ class MultiCentralEngine:
         self._t_ready = None       # (batch, B, G) of the teacher output waiting in t_proj
         self.tin_pending = None    # the next batch's teacher inputs while its forward is queued
         self._tseed = None
+
+    def _graph_deps(self):
+        """What a captured step's buffer addresses depend on: the shared GEMM / row-sum scratch
+        (ops.alloc_epoch) and this engine's own workspaces."""
+        return (ops.alloc_epoch(), self.ws.epoch, self.tws.epoch, self.iws.epoch)
 
     # student image branch on the side stream, concurrently with the audio branch: measured
     # slower (r1_39: 149.7k vs 152.4k pairs/s -- both branches' launches fill the chip, so
@@ -818,46 +847,70 @@ class MultiCentralEngine:
         self._pf = (batch, par, done, staged)
         return True
 
-    def stage(self, batch, with_orig):
+    def stage(self, batch, with_orig, training=True):
         """Device batch dict -> view-major staged image/audio inputs (act dtype) and the labels,
-        in fixed workspace buffers (what a captured step reads)."""
+        in fixed workspace buffers (what a captured step reads).
+
+        A pending prefetch (prefetch()) of THIS batch is consumed: wait for the data stream, use
+        its buffer set.  Any other staging first waits for that prefetch's data stream (it may
+        still be writing its buffer set) and stages into the set in use, so nothing races it;
+        an eval staging (``training=False``) leaves the prefetch pending for the step it was
+        made for, a training staging of another batch drops it (that batch is augmented again
+        when its own step comes)."""
         ws = self.ws
         main = torch.cuda.current_stream(self.store.device) if self.store.device.type == "cuda" else None
-        pf, self._pf = self._pf, None
+        pf = self._pf
         if pf is not None and pf[0] is batch:
             # prefetched under the previous step: wait for the data stream, use its buffers
+            self._pf = None
             main.wait_event(pf[2])
             self._par = pf[1]
             x_img, x_aud, B, G, L = pf[3]
-        elif "aug" in batch:
-            # real-data path: the device augmentation writes the views straight into the staged
-            # inputs ({"aug": MultiModalAugmentation, "idx": sample ids, "label": ...})
-            if pf is not None:         # a prefetched batch that was not the next one: drop it
-                main.wait_event(pf[2])
-            x_img, x_aud, B, G, L = self._aug_bufs(batch, with_orig, self._par)
-            batch["aug"].stage(batch["idx"], x_img, x_aud, with_orig)
         else:
-            g_img, l_img = batch["g_img"], batch["l_img"]
-            B, G = g_img.shape[:2]
-            L = l_img.shape[1]
-            nv = G + L + (1 if with_orig else 0)
-            x_img = ws.get("in.img", nv * B * 784, self.act)
-            x_aud = ws.get("in.aud", nv * B * 12544, self.act)
-            ops.stage_views(g_img.contiguous(), G, l_img.contiguous() if L else None, L,
-                            batch["image"].contiguous() if with_orig else None, B, 784, x_img)
-            ops.stage_views(batch["g_aud"].contiguous(), G, batch["l_aud"].contiguous() if L else None, L,
-                            batch["audio"].contiguous() if with_orig else None, B, 12544, x_aud)
-            self._par = 0
+            if pf is not None:
+                main.wait_event(pf[2])
+                if training:
+                    self._pf = None
+            # the set the prefetch does not own (every set is free once no prefetch is pending)
+            par = self._par if self._pf is not None else (self._par if "aug" in batch else 0)
+            if "aug" in batch:
+                # real-data path: the device augmentation writes the views straight into the
+                # staged inputs ({"aug": MultiModalAugmentation, "idx": sample ids, "label": ...})
+                x_img, x_aud, B, G, L = self._aug_bufs(batch, with_orig, par)
+                batch["aug"].stage(batch["idx"], x_img, x_aud, with_orig)
+            else:
+                g_img, l_img = batch["g_img"], batch["l_img"]
+                B, G = g_img.shape[:2]
+                L = l_img.shape[1]
+                nv = G + L + (1 if with_orig else 0)
+                sfx = "" if par == 0 else ".1"
+                x_img = ws.get("in.img" + sfx, nv * B * 784, self.act)
+                x_aud = ws.get("in.aud" + sfx, nv * B * 12544, self.act)
+                ops.stage_views(g_img.contiguous(), G, l_img.contiguous() if L else None, L,
+                                batch["image"].contiguous() if with_orig else None, B, 784, x_img)
+                ops.stage_views(batch["g_aud"].contiguous(), G, batch["l_aud"].contiguous() if L else None, L,
+                                batch["audio"].contiguous() if with_orig else None, B, 12544, x_aud)
+            self._par = par
         labels = None
         if self.mode == "semi_supervised":
             labels = ws.get("in.label" + ("" if self._par == 0 else ".1"), B, torch.int64)
             labels.copy_(batch["label"].reshape(-1))
-        if main is not None:
+        if main is not None and training:
             # everything queued on the main stream after this point reads THIS buffer set: the
             # other one is free for a prefetch once the main stream passes here
             self._ev_free = torch.cuda.Event()
             self._ev_free.record(main)
         return x_img, x_aud, B, G, L, labels
+
+    def reset_pipeline(self):
+        """Forget a pipelined teacher output and a pending prefetch (e.g. at an epoch boundary,
+        on resume, or before switching batches): the next step computes its own teacher forward
+        and stages its batch itself.  Waits for the prefetch's data stream, so its buffers are
+        free afterwards."""
+        if self._pf is not None and self.store.device.type == "cuda":
+            torch.cuda.current_stream(self.store.device).wait_event(self._pf[2])
+        self._pf = None
+        self._t_ready = None
 
     def stage_teacher(self, batch):
         """The global views of a (pre-augmented) batch into the teacher's own staged inputs
@@ -907,7 +960,7 @@ class MultiCentralEngine:
         # training=False skips the input-grad weight layouts (forward-only use of the API)
         """Forward of the whole step; fills self.last with everything backward needs.
         Returns the loss (a device scalar in the workspace)."""
-        return self._forward_staged(self.stage(batch, self.heads is not None), training)
+        return self._forward_staged(self.stage(batch, self.heads is not None, training), training)
 
     def _forward_staged(self, staged, training=True, teacher_ready=False):
         hp, ws, st = self.hp, self.ws, self.store
@@ -1111,24 +1164,41 @@ class MultiCentralEngine:
             g = self.store.grad
             host_point(lambda: self.grad_hook.bucket(g, self._early_ranges))
         fi, cimg, fa, caud = c["senc"]
+        iws = self.iws
+        dfi = iws.get("dfeat_img", N * fi.shape[1])
+        ilin, alin = "student." + self.img_lin, "student." + self.aud_lin
 
-        def image_branch():      # independent of the audio branch: side stream
-            ops.mark("img.bwd.begin")
-            iws = self.iws
-            dfi = iws.get("dfeat_img", N * fi.shape[1])
-            lin = "student." + self.img_lin
-            ops.linear_bwd(dcat, fi, st[lin + ".weight"], st.grad_of(lin + ".weight"),
-                           st.grad_of(lin + ".bias"), dfi, N, dout_ld=2 * E,
-                           mode=self.gm)
+        def image_linear():
+            ops.linear_bwd(dcat, fi, st[ilin + ".weight"], st.grad_of(ilin + ".weight"),
+                           st.grad_of(ilin + ".bias"), dfi, N, dout_ld=2 * E, mode=self.gm)
+
+        def image_convs():
             self.img.backward(iws, st, cimg, dfi)
             ops.mark("img.bwd.end")
 
-        _, i_done = self._on_side(image_branch)
+        def image_branch():      # independent of the audio branch: side stream
+            ops.mark("img.bwd.begin")
+            image_linear()
+            image_convs()
+
         dfa = ws.get("dfeat_aud", N * fa.shape[1])
-        lin = "student." + self.aud_lin
-        ops.linear_bwd(dcat, fa, st[lin + ".weight"], st.grad_of(lin + ".weight"),
-                       st.grad_of(lin + ".bias"), dfa, N, dout_ld=2 * E, dout_off=E,
-                       mode=self.gm)
+
+        def audio_linear():
+            ops.linear_bwd(dcat, fa, st[alin + ".weight"], st.grad_of(alin + ".weight"),
+                           st.grad_of(alin + ".bias"), dfa, N, dout_ld=2 * E, dout_off=E,
+                           mode=self.gm)
+
+        if self._bucketed():
+            # data parallel: both encoder Linears (1.2 M of the 2.1 M live gradients) first, on
+            # this stream, then their bucket goes out under the conv branches' backward
+            image_linear()
+            audio_linear()
+            g = self.store.grad
+            host_point(lambda: self.grad_hook.bucket(g, self._linear_ranges))
+            _, i_done = self._on_side(image_convs)
+        else:
+            _, i_done = self._on_side(image_branch)
+            audio_linear()
         self.aud.backward(ws, st, caud, dfa, wstream=self.wside)
         ops.mark("aud.bwd.end")
         self._join(i_done)
@@ -1156,6 +1226,22 @@ class MultiCentralEngine:
         return merge_ranges([(o, o + -(-n // ALIGN) * ALIGN) for k, (o, n) in st.s_offs.items()
                              if k in live and not k.startswith(br)])
 
+    @property
+    def _linear_ranges(self):
+        """Gradient-arena ranges of the two encoder Linears (the second bucket)."""
+        st = self.store
+        from .dist import merge_ranges
+        from .params import ALIGN
+        keys = [f"student.{lin}.{p}" for lin in (self.img_lin, self.aud_lin) for p in ("weight", "bias")]
+        return merge_ranges([(st.s_offs[k][0], st.s_offs[k][0] + -(-st.s_offs[k][1] // ALIGN) * ALIGN)
+                             for k in keys])
+
+    def _exchange_in_step(self):
+        """The final gradient exchange inside the step body (a host point after every stream is
+        joined), so the 1/world scale and Adam run in the step's last captured graph segment: a
+        GradAllReduce hook at world > 1.  Else the hook runs after the step."""
+        return _exchange_in_step(self.grad_hook)
+
     def step(self, batch, next_batch=None):
         """One full training step; returns the loss as a device tensor (no host sync).
         With ``use_graph`` everything after the input staging (and around the data-parallel
@@ -1173,11 +1259,15 @@ class MultiCentralEngine:
         # here cannot be served without drifting from the sequential run: refuse it.
         if self._t_ready is not None and not (self._t_ready[0] is batch and self._t_ready[1:] == (B, G)):
             raise ValueError("pipelined step: batch must be the previous step's next_batch (its "
-                             "teacher forward already ran); set pipeline=False to change batches")
+                             "teacher forward already ran); call reset_pipeline() (or set "
+                             "pipeline=False) to change batches")
         ready = self._t_ready is not None
         tin = None
         if self.pipeline and next_batch is not None and self.side is not None and "aug" not in next_batch:
             tin = self.stage_teacher(next_batch)
+
+        in_step = self._exchange_in_step()
+        _exchange_begin(self.grad_hook)
 
         def body():
             ops.mark_reset()
@@ -1187,9 +1277,12 @@ class MultiCentralEngine:
             ops.mark("ema")
             t_done = self._teacher_next(tin) if tin is not None else None
             self.backward()
+            self._join(t_done)
             if self.grad_hook is None:
                 adam_step_dev(self.store, self.hp, self.sstate)
-            self._join(t_done)
+            elif in_step:
+                _exchange_finish(self.grad_hook, self.store.grad)
+                adam_step_dev(self.store, self.hp, self.sstate)
             self.store.flush_nbt()
             ops.mark("end")
 
@@ -1202,7 +1295,7 @@ class MultiCentralEngine:
         self.tin_pending = None
         if next_batch is not None and "aug" in next_batch:
             self.prefetch(next_batch)
-        if self.grad_hook is not None:
+        if self.grad_hook is not None and not in_step:
             self.grad_hook(self.store.grad)
             adam_step_dev(self.store, self.hp, self.sstate)
         self.store.adam_step += 1
@@ -1314,7 +1407,7 @@ class UniModalEngine:
         self.last = {}
         self.sstate = StepState(store.device, hp.lr, hp.betas)
         self.use_graph = False
-        self.graph = GraphedStep()
+        self.graph = GraphedStep(deps=lambda: (ops.alloc_epoch(), self.ws.epoch))
 
     def stage(self, batch):
         key = "img" if self.modality == "image" else "aud"
@@ -1397,6 +1490,9 @@ class UniModalEngine:
             else:
                 adam_step_dev(self.store, self.hp, self.sstate)
 
+        in_step = _exchange_in_step(self.grad_hook)
+        _exchange_begin(self.grad_hook)
+
         def body():
             self._forward_staged(staged, training=True)
             self.update_center()
@@ -1405,12 +1501,15 @@ class UniModalEngine:
             self.backward()
             if self.grad_hook is None:
                 opt_and_ema()
+            elif in_step:
+                _exchange_finish(self.grad_hook, self.store.grad)
+                opt_and_ema()
 
         if self.use_graph:
             self.graph.run(staged[1:], body)
         else:
             body()
-        if self.grad_hook is not None:
+        if self.grad_hook is not None and not in_step:
             self.grad_hook(self.store.grad)
             opt_and_ema()
         self.store.adam_step += 1
@@ -1462,7 +1561,7 @@ class SimCLREngine:
         # one optimizer step count per tower (torch.optim.Adam keeps per-parameter steps)
         self.sstates = [StepState(store.device, hp.lr, hp.betas) for _ in range(2)]
         self.use_graph = False
-        self.graph = GraphedStep()
+        self.graph = GraphedStep(deps=lambda: (ops.alloc_epoch(), self.ws.epoch))
 
     def draw_mode(self):
         return int(torch.randint(0, 4, (1,), generator=self.gen).item())
@@ -1566,17 +1665,26 @@ class SimCLREngine:
         B = batch["img1"].shape[0]
         xs = self.stage(batch, mode)
 
+        in_step = _exchange_in_step(self.grad_hook)
+        _exchange_begin(self.grad_hook)
+
         def body():
             self._forward_staged(xs, mode, B)
             self.backward()
             if self.grad_hook is None:
+                self.adam()
+            elif in_step:
+                # only the used towers' ranges: every rank draws the same mode sequence (same
+                # generator seed, as the reference's seed_everything), so the sizes agree
+                _exchange_finish(self.grad_hook, self.store.grad,
+                                 [(o, o + n) for o, n in (self.ranges[t] for t in self.used_towers())])
                 self.adam()
 
         if self.use_graph:
             self.graph.run((mode, B), body)
         else:
             body()
-        if self.grad_hook is not None:
+        if self.grad_hook is not None and not in_step:
             if hasattr(self.grad_hook, "bucket"):
                 # only the used towers' ranges: every rank draws the same mode sequence (same
                 # generator seed, as the reference's seed_everything), so the sizes agree

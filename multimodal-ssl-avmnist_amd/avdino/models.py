@@ -219,6 +219,13 @@ def _finish_backward(eng):
     eng.step_idx = getattr(eng, "step_idx", 0) + 1
 
 
+def _begin_backward(eng):
+    """Before an engine backward: a new gradient exchange (its early buckets fire inside)."""
+    hook = getattr(eng, "grad_hook", None)
+    if hasattr(hook, "begin"):
+        hook.begin()
+
+
 def _begin_forward(eng):
     """Before an engine forward: the data-parallel buffer broadcast (DDP broadcast_buffers)."""
     if getattr(eng, "buffer_hook", None) is not None:
@@ -246,6 +253,7 @@ class _FusedStepFn(torch.autograd.Function):
     def backward(ctx, g):
         _check_token(ctx)
         eng = ctx.eng
+        _begin_backward(eng)
         eng.backward()
         _finish_backward(eng)
         return (None, None, None) + _arena_grads(eng, ctx.ranges, g)
@@ -296,6 +304,7 @@ class _MultiForwardFn(torch.autograd.Function):
         if dh:
             no = eng.heads[0].o
             dheads = (seed(dh[0], c["B"] * no, dev), seed(dh[1], c["B"] * no, dev))
+        _begin_backward(eng)
         eng.backward(ds=seed(ds, n, dev), dheads=dheads)
         _finish_backward(eng)
         return (None, None, None) + _arena_grads(eng, ctx.ranges, 1.0)
@@ -851,6 +860,7 @@ class _UniForwardFn(torch.autograd.Function):
         de = None if de is None else de.float().contiguous().view(-1)
         if de is None:
             de = torch.zeros(c["V"] * c["B"] * eng.D, device=dev)
+        _begin_backward(eng)
         eng.backward(ds=ds, demb=de)
         _finish_backward(eng)
         return (None, None, None) + _arena_grads(eng, ctx.ranges, 1.0)
@@ -1027,6 +1037,7 @@ class _SimCLRForwardFn(torch.autograd.Function):
         dev = eng.store.device
         z = torch.zeros(B, P, device=dev)
         dreps = torch.cat([z if d1 is None else d1.float(), z if d2 is None else d2.float()]).view(-1)
+        _begin_backward(eng)
         eng.backward(dreps=dreps)
         _finish_backward(eng)
         return (None, None, None, None) + _arena_grads(eng, ctx.ranges, 1.0)
@@ -1044,6 +1055,7 @@ class _SimCLRFusedFn(torch.autograd.Function):
     def backward(ctx, g):
         _check_token(ctx)
         eng = ctx.eng
+        _begin_backward(eng)
         eng.backward()
         _finish_backward(eng)
         return (None, None, None, None) + _arena_grads(eng, ctx.ranges, g)

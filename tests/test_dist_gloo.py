@@ -115,6 +115,54 @@ def test_bucketed_allreduce_equals_flat():
         np.testing.assert_array_equal(sub[~inside], grad[~inside])   # untouched outside
 
 
+def _async_buckets(r, world):
+    """The asynchronous bucket path (what RCCL runs: async_op=True, pending works waited in
+    finish, x 1/world in scale) under gloo, in the engines' order begin -> bucket* -> finish ->
+    scale, over two steps; the first step before it is ABORTED after a bucket (no finish), and
+    begin() must keep its stale ranges from suppressing the next step's reduction."""
+    from avdino import dist as D
+    g = torch.Generator().manual_seed(500 + r)
+    out = []
+    h = D.GradAllReduce(overlap=True)
+    aborted = torch.randn(1000, generator=g)
+    h.begin()
+    h.bucket(aborted, [(0, 400)])            # the step dies here: no finish()
+    for step in range(2):
+        grad = torch.randn(1000, generator=g)
+        raw = grad.clone()
+        flat = grad.clone()
+        D.GradAllReduce()(flat)
+        h.begin()
+        assert not h.pending and not h.covered
+        h.bucket(grad, [(0, 400)])          # early bucket (heads)
+        h.bucket(grad, [(400, 650)])        # second bucket (encoder Linears)
+        assert len(h.pending) == 2
+        h.finish(grad)                       # the rest (conv weights) + wait
+        assert h.reduced == [(0, 1000)] and not h.pending
+        h.scale(grad)
+        out.append((raw.numpy(), flat.numpy(), grad.numpy()))
+    spare = torch.zeros(100)
+    try:
+        h.begin()
+        h.bucket(spare, [(0, 10)])
+        h.bucket(spare, [(5, 20)])           # overlaps: a protocol error, not a silent skip
+        overlap_raised = False
+    except RuntimeError:
+        overlap_raised = True
+    h.begin()
+    return out, overlap_raised
+
+
+def test_async_buckets_equal_flat_and_survive_an_aborted_step():
+    res = _run(_async_buckets)
+    for _, (steps, raised) in res:
+        assert raised
+        for k, (raw, flat, got) in enumerate(steps):
+            mean = (res[0][1][0][k][0] + res[1][1][0][k][0]) / 2
+            np.testing.assert_array_equal(got, flat)
+            np.testing.assert_allclose(got, mean, rtol=1e-6, atol=1e-7)
+
+
 # ----------------------------------------------------------------- global negatives
 class _Gather(torch.autograd.Function):
     """gather_rows with its adjoint (scatter_rows_grad) as the backward."""

@@ -6,9 +6,11 @@ cuda:0 (the 1-GPU rehearsal of the 8-GPU RCCL run).
   ``use_graph`` no longer falls back to eager at world > 1.  Replayed steps == eager steps,
   bit for bit (losses, parameters, teacher, buffers).
 * The gradient all-reduce in buckets (avdino.dist.GradAllReduce: heads / fusion / projection
-  issued at a host point inside the backward, the conv branches after the step; SimCLR: the
-  first tower under the second's backward) == one flat all-reduce of the arena, bit for bit
-  (a 2-rank sum is order-free)."""
+  issued at a host point inside the backward, the two encoder Linears at a second one before
+  the conv branches, the rest -- the conv weights -- at the step's last host point, followed
+  by the 1/world scale and Adam in the last captured segment; SimCLR: the first tower under
+  the second's backward) == one flat all-reduce of the arena, bit for bit (a 2-rank sum is
+  order-free), and the buckets of every step cover the gradient arena exactly once."""
 import numpy as np
 import pytest
 
@@ -33,6 +35,42 @@ def _host(t):
     return t.detach().float().cpu().numpy()
 
 
+class _Logged:
+    """GradAllReduce that records the ranges each step's collectives reduce."""
+
+    def __new__(cls):
+        from avdino import dist as AD
+
+        class L(AD.GradAllReduce):
+            log = []
+
+            def begin(self):
+                super().begin()
+                L.log.append([])
+
+            def bucket(self, grad, ranges):
+                L.log[-1].extend((lo, hi) for lo, hi in ranges if hi > lo)
+                super().bucket(grad, ranges)
+
+            def finish(self, grad, ranges=None):
+                from avdino.dist import subtract_ranges
+                want = [(0, grad.numel())] if ranges is None else list(ranges)
+                L.log[-1].extend(subtract_ranges(want, self.covered))
+                super().finish(grad, ranges)
+        return L()
+
+
+def _partition(ranges, n):
+    """The ranges are disjoint and cover [0, n)."""
+    rs = sorted(ranges)
+    pos = 0
+    for lo, hi in rs:
+        if lo != pos:
+            return False
+        pos = hi
+    return pos == n
+
+
 def _multi(r, mode, graph, bucket, steps=5):
     from avdino import dist as AD
     from avdino.engine import Hyper, MultiCentralEngine
@@ -43,7 +81,7 @@ def _multi(r, mode, graph, bucket, steps=5):
     AD.broadcast_parameters(store)
     eng = MultiCentralEngine(store, mode, E, D, P, Hyper(dropout=0.3, fusion_dropout=0.3),
                              act_dtype=torch.bfloat16, seed=3,
-                             grad_hook=AD.GradAllReduce() if bucket else _flat_hook(),
+                             grad_hook=_Logged() if bucket else _flat_hook(),
                              buffer_hook=AD.broadcast_buffers, negatives="global")
     eng.use_graph = graph
     batches = []
@@ -53,8 +91,13 @@ def _multi(r, mode, graph, bucket, steps=5):
     losses = [eng.step(batches[i % 2]).item() for i in range(steps)]
     store.flush_nbt()
     segs = [eng.graph.segments(k) for k in eng.graph.graphs]
+    cover = None
+    if bucket:
+        log = type(eng.grad_hook).log
+        cover = (len(log), all(_partition(s, store.grad.numel()) for s in log),
+                 [len(s) for s in log])
     return dict(losses=losses, student=_host(store.student), teacher=_host(store.teacher),
-                buf=_host(store.buf_arena), m=_host(store.adam_m), segs=segs)
+                buf=_host(store.buf_arena), m=_host(store.adam_m), segs=segs, cover=cover)
 
 
 def _simclr(r, graph, bucket, modes=(0, 1, 3, 2, 2, 2, 2, 3, 3)):
@@ -109,8 +152,13 @@ def test_world2_graph_and_buckets_equal_eager_flat(world2, mode):
         _same(flat, buck, keys)        # bucketed all-reduce == one flat all-reduce
         _same(buck, graph, keys)       # captured + replayed == eager
         assert len(graph["segs"]) == 1
-        # segments: [gather, scatter,] early gradient bucket -> 4 (infonce) / 2 (mse)
-        assert graph["segs"][0] == (4 if mode == "infonce" else 2), graph["segs"]
+        # segments: [gather, scatter,] early bucket, encoder-Linear bucket, final exchange
+        # -> 6 (infonce) / 4 (mse)
+        assert graph["segs"][0] == (6 if mode == "infonce" else 4), graph["segs"]
+        for run in (buck, graph):   # every step's collectives partition the gradient arena
+            nsteps, exact, nranges = run["cover"]
+            assert nsteps == 5 and exact, run["cover"]
+            assert min(nranges) >= 3, run["cover"]
     # DDP keeps the replicas identical (BN running stats: each rank's own last batch)
     _same(world2[0][(mode, True, True)], world2[1][(mode, True, True)], ("student", "teacher"))
 
@@ -124,6 +172,6 @@ def test_world2_simclr_graph_and_buckets_equal_eager_flat(world2):
         _same(buck, graph, keys)
         # every mode's buffers sized first (0, 1, 3), then mode 2 (image/audio) 4 times:
         # captured on its third, replayed on its fourth; gather + scatter + the first
-        # tower's bucket -> 4 segments
-        assert graph["segs"].get((2, B)) == 4, graph["segs"]
+        # tower's bucket + the final exchange -> 5 segments
+        assert graph["segs"].get((2, B)) == 5, graph["segs"]
     _same(world2[0][("simclr", True, True)], world2[1][("simclr", True, True)], ("student",))

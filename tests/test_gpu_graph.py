@@ -169,3 +169,38 @@ def test_graph_recaptured_after_workspace_growth_simclr():
     g = res[1][2].graph
     # mode 0 was captured before mode 1 grew the buffers, then captured again
     assert g.captures > len(g.graphs), (g.captures, list(g.graphs))
+
+
+def test_only_graph_goes_stale_and_is_recaptured():
+    """The pool-reset branch of GraphedStep.run (capture.py): the ONLY captured graph goes stale
+    (one of the engine's workspaces grows after its capture), is dropped together with its
+    memory pool, and the step runs eagerly, captures again on a fresh pool and replays -- every
+    step equal to the eager run.  Another workspace growing (a probe's) retires nothing."""
+    from avdino.engine import Workspace
+    s0, l0, _ = _run_multi("mse", False, steps=8)
+    from avdino.engine import Hyper, MultiCentralEngine
+    from avdino.params import ParamStore
+    from avdino.spec import multimodal_dino_sd
+    E, D, P, B, G, L = 32, 32, 16, 8, 2, 4
+    store = ParamStore(multimodal_dino_sd("mse", E, D, P), "cuda")
+    store.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in
+                           make_state(OS.multimodal_dino_spec("mse", E, D, P), 401).items()})
+    eng = MultiCentralEngine(store, "mse", E, D, P, Hyper(dropout=0.3, fusion_dropout=0.3),
+                             act_dtype=torch.bfloat16, seed=3)
+    eng.use_graph = True
+    batches = [_dev(make_multimodal_batch(B, G, L, 4000 + i)) for i in range(2)]
+    losses = []
+    for i in range(4):                  # 2 eager, capture, replay
+        losses.append(eng.step(batches[i % 2]).item())
+    assert eng.graph.captures == 1 and eng.graph.pool is not None
+    Workspace("cuda").get("probe", 1 << 20)       # someone else's scratch: still replayed
+    losses.append(eng.step(batches[0]).item())
+    assert eng.graph.captures == 1 and len(eng.graph.graphs) == 1
+    eng.ws.get("grown.elsewhere", 1 << 20)        # the engine's own workspace moves
+    losses.append(eng.step(batches[1]).item())    # stale: dropped with its pool, eager
+    assert not eng.graph.graphs and eng.graph.pool is None
+    losses.append(eng.step(batches[0]).item())    # captured again on a new pool
+    assert eng.graph.captures == 2 and eng.graph.pool is not None
+    losses.append(eng.step(batches[1]).item())    # replayed
+    assert losses == l0, (losses, l0)
+    assert torch.equal(s0.student, store.student) and torch.equal(s0.teacher, store.teacher)

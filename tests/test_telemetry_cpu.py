@@ -96,17 +96,21 @@ def test_multi_simple_module_reference_keys():
 
 
 def test_graph_staleness_rule():
-    """GraphedStep replays a graph only while no scratch buffer moved since its capture."""
+    """GraphedStep replays a graph only while none of the buffers it depends on moved since its
+    capture: each Workspace keeps its own epoch, so another workspace growing (a probe's, a
+    loss helper's) does not retire the graph."""
     from avdino import ops
     from avdino.engine import GraphedStep, Workspace
     ws = Workspace(torch.device("cpu"))
-    e0 = ops.alloc_epoch()
+    other = Workspace(torch.device("cpu"))
+    e0, g0 = ws.epoch, ops.alloc_epoch()
     ws.get("a", 10)
-    assert ops.alloc_epoch() == e0 + 1
+    assert ws.epoch == e0 + 1
     ws.get("a", 5)                      # fits: no reallocation
-    assert ops.alloc_epoch() == e0 + 1
+    assert ws.epoch == e0 + 1
     ws.get("a", 20)
-    assert ops.alloc_epoch() == e0 + 2
+    assert ws.epoch == e0 + 2
+    assert ops.alloc_epoch() == g0      # the shared scratch epoch is not a workspace's
 
     class FakeGraph:
         replays = 0
@@ -114,16 +118,20 @@ def test_graph_staleness_rule():
         def replay(self):
             FakeGraph.replays += 1
 
-    g = GraphedStep(warmup=1)
-    g.graphs["k"] = ([FakeGraph()], ops.alloc_epoch())
+    g = GraphedStep(warmup=1, deps=lambda: (ops.alloc_epoch(), ws.epoch))
+    g.graphs["k"] = ([FakeGraph()], g.deps())
     g.seen["k"] = 1
     calls = []
     g.run("k", lambda: calls.append(1))
     assert FakeGraph.replays == 1 and not calls
-    ws.get("b", 4)                      # a buffer moved: the graph is stale
+    other.get("z", 1 << 10)             # someone else's workspace: still replayed
+    g.run("k", lambda: calls.append(1))
+    assert FakeGraph.replays == 2 and not calls
+    ws.get("b", 4)                      # one of ITS buffers moved: the graph is stale
     g.warmup = 2                        # (keep the re-run eager: no capture on CPU)
     g.run("k", lambda: calls.append(1))
-    assert "k" not in g.graphs and calls == [1] and FakeGraph.replays == 1
+    assert "k" not in g.graphs and calls == [1] and FakeGraph.replays == 2
+    assert g.pool is None               # the last graph went with its pool
 
 
 def test_segmented_replay_order():
