@@ -627,6 +627,36 @@ int avd_fp8_conv_fwd(const void* x, float xscale, const void* wq, const float* w
                      const float* bias, void* y, float* stats, int N, int B, int Cin, int H,
                      int W, int Cout, int K, int pad, void* stream);
 
+/* ------------------------------------------------------------------ MX (block-scaled) fp8 convs
+ * BASELINE config 5 ("fp8 MFMA conv path"): the mid-layer conv forward AND input gradient of
+ * CentralUnimodalImage/Audio (unimodal.py:127-221; the F.conv2d and its autograd dX under the
+ * reference's '16-mixed' precision, run_dino.py:360) on the block-scaled
+ * v_mfma_scale_f32_16x16x128_f8f6f4 (gfx950, 2x the bf16 MFMA rate): OCP e4m3 operands with
+ * E8M0 scales -- the weights one per (row, 32-k block), quantised per step by
+ * avd_mx_weight_layout; the bf16 NHWC input quantised while staged with one power-of-two scale
+ * per staged strip (its max maps into [128, 256): no saturation).  f32 accumulation; y / dX
+ * bf16 NHWC; the forward's BatchNorm partial rows as avd_cl_conv_fwd's
+ * ([Cout][N/B][avd_mx_stat_rows][2], optional pivot as avd_cl_conv_fwd_pv). */
+
+/* Bytes of the e4m3 weight rows (rows of 16/64, k padded to 128) and of their E8M0 scales. */
+long long avd_mx_weight_bytes(int Cout, int Cin, int K, int dgrad);
+long long avd_mx_scale_bytes(int Cout, int Cin, int K, int dgrad);
+/* W f32 [Cout][Cin][K][K] -> e4m3 rows + block scales; dgrad = 1: the input-gradient layout
+ * (rows = input channels, taps flipped), as avd_cl_weight_layout. */
+int avd_mx_weight_layout(const float* w, void* wq, void* wsc, int Cout, int Cin, int K, int dgrad,
+                         void* stream);
+/* 1 if the forward (dgrad 0) / input gradient (dgrad 1) of conv Cin -> Cout over H x W has an
+ * MX kernel. */
+int avd_mx_conv_serves(int Cin, int H, int W, int Cout, int K, int pad, int dgrad);
+/* BN partial rows per group written by avd_mx_conv_fwd (0: not served). */
+int avd_mx_stat_rows(int H, int W, int B, int K, int Cin, int Cout, int pad);
+int avd_mx_conv_fwd(const void* x, const void* wq, const void* wsc, const float* bias,
+                    const float* pivot, void* y, float* stats, int N, int B, int Cin, int H, int W,
+                    int Cout, int K, int pad, void* stream);
+/* dX [N][H][W][Cin] bf16 from dY [N][Ho][Wo][Cout] bf16 and the dgrad-layout MX weights. */
+int avd_mx_conv_dgrad(const void* dy, const void* wq_d, const void* wsc_d, void* dx, int N, int Cin,
+                      int H, int W, int Cout, int K, int pad, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

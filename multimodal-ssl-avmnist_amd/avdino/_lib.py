@@ -107,6 +107,13 @@ PROTOS = {
     "avd_fp8_conv_serves": [I, I, I],
     "avd_fp8_stat_rows": [I, I, I, I, I, I],
     "avd_fp8_conv_fwd": [P, F, P, P, P, P, P, I, I, I, I, I, I, I, I, P],
+    "avd_mx_weight_bytes": [I, I, I, I],
+    "avd_mx_scale_bytes": [I, I, I, I],
+    "avd_mx_weight_layout": [P, P, P, I, I, I, I, P],
+    "avd_mx_conv_serves": [I, I, I, I, I, I, I],
+    "avd_mx_stat_rows": [I, I, I, I, I, I, I],
+    "avd_mx_conv_fwd": [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, P],
+    "avd_mx_conv_dgrad": [P, P, P, P, I, I, I, I, I, I, I, P],
 }
 
 
@@ -126,6 +133,8 @@ def _load():
         fn.argtypes = args
         fn.restype = ctypes.c_int
     lib.avd_gemm_ws_elems.restype = ctypes.c_longlong
+    lib.avd_mx_weight_bytes.restype = ctypes.c_longlong
+    lib.avd_mx_scale_bytes.restype = ctypes.c_longlong
     lib.avd_last_error.argtypes = []
     lib.avd_last_error.restype = ctypes.c_char_p
     return lib

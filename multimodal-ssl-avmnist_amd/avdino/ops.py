@@ -283,6 +283,67 @@ def fp8_conv_fwd(x, xscale, wq, wscale, bias, y, stats, N, B, Cin, H, W, Cout, K
                         p(stats), N, B, Cin, H, W, Cout, K, pad, stream()))
 
 
+# ---- MX (block-scaled e4m3) conv forward + input gradient (config 5): include/avdino.h "MX"
+def mx_weight_bytes(Cout, Cin, K, dgrad):
+    return int(lib.avd_mx_weight_bytes(Cout, Cin, K, int(dgrad)))
+
+
+def mx_scale_bytes(Cout, Cin, K, dgrad):
+    return int(lib.avd_mx_scale_bytes(Cout, Cin, K, int(dgrad)))
+
+
+def mx_weight_layout(w, wq, wsc, dgrad):
+    """w f32 [Cout, Cin, K, K] -> e4m3 rows wq (uint8) + E8M0 block scales wsc (uint8)."""
+    Cout, Cin, K, _ = w.shape
+    _need(w.dtype == torch.float32 and w.is_contiguous(), "mx layout w")
+    _need(wq.dtype == torch.uint8 and wq.numel() >= mx_weight_bytes(Cout, Cin, K, dgrad), "mx layout wq")
+    _need(wsc.dtype == torch.uint8 and wsc.numel() >= mx_scale_bytes(Cout, Cin, K, dgrad), "mx layout wsc")
+    call("avd_mx_weight_layout", p(w), p(wq), p(wsc), Cout, Cin, K, int(dgrad), stream())
+
+
+def mx_conv_serves(Cin, H, Cout, K, pad, dgrad):
+    return bool(lib.avd_mx_conv_serves(Cin, H, H, Cout, K, pad, int(dgrad)))
+
+
+def mx_stat_rows(H, B, K, Cin, Cout, pad):
+    return lib.avd_mx_stat_rows(H, H, B, K, Cin, Cout, pad)
+
+
+def mx_conv_fwd(x, wq, wsc, bias, y, stats, N, B, Cin, H, W, Cout, K, pad, pivot=None):
+    """bf16 NHWC x -> bf16 NHWC y on the block-scaled e4m3 MFMA (+bias, + BN partial rows
+    [Cout][N/B][R][2], sums about ``pivot`` when given)."""
+    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
+    _need(H == W and mx_conv_serves(Cin, H, Cout, K, pad, 0), f"mx conv: no kernel for {Cin}->{Cout} @{H}")
+    _need(x.dtype == y.dtype == torch.bfloat16, "mx conv dtypes (bf16 maps)")
+    _need(x.numel() == N * H * W * Cin and y.numel() == N * Ho * Wo * Cout, "mx conv sizes")
+    _need(wq.numel() >= mx_weight_bytes(Cout, Cin, K, 0) and wsc.numel() >= mx_scale_bytes(Cout, Cin, K, 0),
+          "mx conv weights")
+    if stats is not None:
+        R = mx_stat_rows(H, B, K, Cin, Cout, pad)
+        _need(R > 0 and stats.numel() >= Cout * (N // B) * R * 2, "mx conv stats size")
+    _need(pivot is None or (stats is not None and pivot.numel() >= Cout and pivot.dtype == torch.float32),
+          "mx conv pivot")
+    nb = x.numel() * 2 + y.numel() * 2
+    fl = 2 * y.numel() * Cin * K * K
+    _timed(f"mx_conv_fwd[{N}x{H}x{W}x{Cin}->{Cout} k{K}p{pad}]", nb, fl,
+           lambda: call("avd_mx_conv_fwd", p(x), p(wq), p(wsc), p(bias), p(pivot), p(y), p(stats),
+                        N, B, Cin, H, W, Cout, K, pad, stream()))
+
+
+def mx_conv_dgrad(dy, wq_d, wsc_d, dx, N, Cin, H, W, Cout, K, pad):
+    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
+    _need(H == W and mx_conv_serves(Cin, H, Cout, K, pad, 1), f"mx dgrad: no kernel for {Cin}->{Cout} @{H}")
+    _need(dy.dtype == dx.dtype == torch.bfloat16, "mx dgrad dtypes (bf16 maps)")
+    _need(dy.numel() == N * Ho * Wo * Cout and dx.numel() == N * H * W * Cin, "mx dgrad sizes")
+    _need(wq_d.numel() >= mx_weight_bytes(Cout, Cin, K, 1) and wsc_d.numel() >= mx_scale_bytes(Cout, Cin, K, 1),
+          "mx dgrad weights")
+    nb = (dy.numel() + dx.numel()) * 2
+    fl = 2 * N * Cin * H * W * Cout * K * K
+    _timed(f"mx_conv_dgrad[{N}x{Ho}x{Wo}x{Cout}->{Cin} k{K}p{pad}]", nb, fl,
+           lambda: call("avd_mx_conv_dgrad", p(dy), p(wq_d), p(wsc_d), p(dx), N, Cin, H, W, Cout, K,
+                        pad, stream()))
+
+
 def cl_stat_pivot(Ho, Wo, B, K, Cin, Cout, dtype):
     return bool(lib.avd_cl_stat_pivot(Ho, Wo, B, K, Cin, Cout, _DT[dtype]))
 
