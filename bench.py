@@ -29,7 +29,8 @@ import torch  # noqa: E402
 
 METRIC = "AVMNIST audio-image pairs/sec (multimodal DINO step) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# dense, no sparsity; non-scaled fp8 MFMA (v_mfma_f32_16x16x32_fp8_fp8) runs at the bf16 rate
+# dense, no sparsity; fp8 = the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (2x bf16) the fp8
+# mode's conv kernels run on
 MFMA_PEAK_TFS = {"bf16": 2500.0, "f32": 157.3, "fp8": 5000.0}   # fp8: the dense block-scaled peak
 # SURVEY 8(d) "BN-barrier" algorithmic HBM bytes per pair of a whole training step (inputs read
 # once, each train-mode-BN'd conv output written once and read once forward, saved output read
@@ -157,7 +158,8 @@ def build_workload(args, device, act, world, rank, avdist):
                              negatives="global", conv_fp8=args.dtype == "fp8")
     eng.pipeline = args.pipeline
     pool = synthetic_pool(2, B, G, L, device, 1234 + rank)
-    prec = "e4m3 MFMA mid-layer conv forward, bf16 maps/backward" if args.dtype == "fp8" else args.dtype
+    prec = ("block-scaled e4m3 MFMA mid-layer conv forward + input gradient, bf16 maps / weight "
+            "gradients" if args.dtype == "fp8" else args.dtype)
     cfg = {"mse": "BASELINE config 2", "infonce": "BASELINE config 3 shape, all-gathered negatives",
            "semi_supervised": f"BASELINE config 5 shape, {prec}",
            "default": "default mode"}[args.mode]

@@ -68,35 +68,42 @@ class ConvBranch:
         self.stack = stack
         self.act = act_dtype
         self.dims = stack.layer_dims()
-        # fp8 (e4m3) MFMA forward for the layers after the first (config 5's "fp8 MFMA conv
-        # path"); maps stay bf16, the backward stays bf16 (avd_fp8_conv_fwd)
+        # fp8: the layers after the first run their forward and input gradient on the
+        # block-scaled e4m3 MFMA (config 5's "fp8 MFMA conv path", avd_mx_conv_*); maps,
+        # statistics and the weight gradient stay bf16 / f32
         self.fp8 = bool(fp8) and act_dtype == torch.bfloat16
 
-    def _fp8_ok(self, i):
-        ci, co, k, _p = self.stack.convs[i]
-        return self.fp8 and i > 0 and ops.fp8_conv_serves(ci, co, k)
+    def _mx_ok(self, i, dgrad=False):
+        ci, co, k, p = self.stack.convs[i]
+        return self.fp8 and i > 0 and ops.mx_conv_serves(ci, self.dims[i][0], co, k, p, dgrad)
+
+    # kept for callers of the round-2 name
+    _fp8_ok = _mx_ok
 
     def prepare(self, ws, store, tag, need_dgrad):
-        """MFMA weight layouts for this step (the weights change every step): (bf16 forward
-        rows, bf16 dgrad rows, (e4m3 rows, per-channel scales) for fp8 layers)."""
+        """MFMA weight layouts for this step (the weights change every step), per layer:
+        (bf16 forward rows, bf16 dgrad rows, MX forward (e4m3 rows, scales), MX dgrad)."""
         wts, batch = [], []
         for i, (ci, co, k, _p) in enumerate(self.stack.convs):
             w = store[self.stack.conv_keys[i] + ".weight"]
-            q = None
-            if self._fp8_ok(i):
-                q = (ws.get(f"{tag}.wq{i}", ops.fp8_weight_elems(co, ci, k), torch.uint8),
-                     ws.get(f"{tag}.wqs{i}", co))
-                ops.fp8_weight_quant(w, q[0], q[1])
-                wk = None
+            wk = wd = q = qd = None
+            if self._mx_ok(i):
+                q = (ws.get(f"{tag}.wq{i}", ops.mx_weight_bytes(co, ci, k, 0), torch.uint8),
+                     ws.get(f"{tag}.wqs{i}", ops.mx_scale_bytes(co, ci, k, 0), torch.uint8))
+                ops.mx_weight_layout(w, q[0], q[1], 0)
             else:
                 wk = ws.get(f"{tag}.wk{i}", ops.cl_weight_elems(co, ci, k, 0), self.act)
                 batch.append((w, wk, 0))
-            wd = None
             if need_dgrad and i > 0:
-                wd = ws.get(f"{tag}.wd{i}", ops.cl_weight_elems(co, ci, k, 1), self.act)
-                batch.append((w, wd, 1))
-            wts.append((wk, wd, q))
-        if batch:       # every layout of the stack in one launch
+                if self._mx_ok(i, dgrad=True):
+                    qd = (ws.get(f"{tag}.wqd{i}", ops.mx_weight_bytes(co, ci, k, 1), torch.uint8),
+                          ws.get(f"{tag}.wqds{i}", ops.mx_scale_bytes(co, ci, k, 1), torch.uint8))
+                    ops.mx_weight_layout(w, qd[0], qd[1], 1)
+                else:
+                    wd = ws.get(f"{tag}.wd{i}", ops.cl_weight_elems(co, ci, k, 1), self.act)
+                    batch.append((w, wd, 1))
+            wts.append((wk, wd, q, qd))
+        if batch:       # every bf16 layout of the stack in one launch
             ops.cl_weight_layout_batch(batch)
         return wts
 
@@ -104,27 +111,35 @@ class ConvBranch:
         ci, co, k, pad = self.stack.convs[i]
         H = self.dims[i][0]
         if wt[2] is not None:
-            ops.fp8_conv_fwd(h, 1.0, wt[2][0], wt[2][1], bias, y, parts, N, B, ci, H, H, co, k, pad)
+            ops.mx_conv_fwd(h, wt[2][0], wt[2][1], bias, y, parts, N, B, ci, H, H, co, k, pad, pivot=pivot)
         else:
             ops.cl_conv_fwd(h, wt[0], bias, y, parts, N, B, ci, H, H, co, k, pad, pivot=pivot)
+
+    def _conv_dgrad(self, i, dy, wt, dx, N):
+        ci, co, k, pad = self.stack.convs[i]
+        H = self.dims[i][0]
+        if wt[3] is not None:
+            ops.mx_conv_dgrad(dy, wt[3][0], wt[3][1], dx, N, ci, H, H, co, k, pad)
+        else:
+            ops.cl_conv_dgrad(dy, wt[1], dx, N, ci, H, H, co, k, pad)
 
     # A/B switch for the statistics pivot (AVDINO_NO_PIVOT=1: raw sums, as before round 3)
     NO_PIVOT = os.environ.get("AVDINO_NO_PIVOT", "0") == "1"
 
     def _stat_pivot(self, store, i, B):
         """The BN running mean as the statistics pivot where the producer takes one (the
-        persistent mid layers: avd_cl_stat_pivot) -- None elsewhere."""
+        persistent mid layers: avd_cl_stat_pivot, and the MX kernels) -- None elsewhere."""
         ci, co, k, _p = self.stack.convs[i]
         Ho = self.dims[i][1]
-        if self.NO_PIVOT or self._fp8_ok(i) or not ops.cl_stat_pivot(Ho, Ho, B, k, ci, co, self.act):
+        if self.NO_PIVOT or not (self._mx_ok(i) or ops.cl_stat_pivot(Ho, Ho, B, k, ci, co, self.act)):
             return None
         return store[self.stack.bn_keys[i] + ".running_mean"]
 
     def _stat_rows(self, i, B):
-        ci, co, k, _p = self.stack.convs[i]
-        Ho = self.dims[i][1]
-        if self._fp8_ok(i):
-            return ops.fp8_stat_rows(Ho, Ho, B, k, ci, co)
+        ci, co, k, p = self.stack.convs[i]
+        H, Ho = self.dims[i][0], self.dims[i][1]
+        if self._mx_ok(i):
+            return ops.mx_stat_rows(H, B, k, ci, co, p)
         return ops.cl_stat_rows(Ho, Ho, B, k, ci, co, self.act)
 
     def _tail_mode(self):
@@ -368,7 +383,8 @@ class ConvBranch:
 
     def _dgrad_reduce_rows(self, ctx, i, N, B):
         """Rows of the fused dgrad + previous-layer reduce at layer i (> 0), 0 = unfused."""
-        if not self.DGRAD_BNREDUCE or self.act != torch.bfloat16 or ctx["y"][i - 1] is None:
+        if (not self.DGRAD_BNREDUCE or self.act != torch.bfloat16 or ctx["y"][i - 1] is None
+                or ctx["wts"][i][1] is None):
             return 0
         ci, co, k, pad = self.stack.convs[i]
         H = self.dims[i][0]
@@ -429,7 +445,7 @@ class ConvBranch:
                 continue
             nch = ops.cl_wgrad_chunks(N, co, ci, k)
             wparts = ws.get("wgrad_parts", nch * co * ci * k * k)
-            if (self.BNAPPLY_FUSED and i > 0 and mode in (0, 2) and
+            if (self.BNAPPLY_FUSED and i > 0 and mode in (0, 2) and ctx["wts"][i][1] is not None and
                     ops.cl_bnapply_ok(self.act, N, B, ci, H, H, co, k, pad, mode)):
                 # dy = BN-backward apply is formed inside both consumers (no dy tensor)
                 ops.cl_conv_wgrad_bnapply(x, y, gout, mode, st[2], st[3], coef, wparts, N, B, ci, H, H,
@@ -441,7 +457,8 @@ class ConvBranch:
                 gout = dx
                 continue
             dy = ws.get(f"bwd_dy{i}" if wstream is not None else "bwd_dy", N * Ho * Ho * co, self.act)
-            if (self.DGRAD_APPLY and i > 0 and mode in (0, 2) and not self._dgrad_reduce_rows(ctx, i, N, B)
+            if (self.DGRAD_APPLY and i > 0 and mode in (0, 2) and ctx["wts"][i][1] is not None
+                    and not self._dgrad_reduce_rows(ctx, i, N, B)
                     and ops.cl_bnapply_ok(self.act, N, B, ci, H, H, co, k, pad, mode)):
                 # BN-backward apply formed in the input-gradient kernel's staging, which also
                 # stores dy for the weight gradient (no separate apply pass re-reading y)
@@ -489,7 +506,7 @@ class ConvBranch:
                                                fparts, N, B, ci, H, H, co, k, pad)
                     fused = (fparts, Rf)
                 else:
-                    ops.cl_conv_dgrad(dy, ctx["wts"][i][1], dx, N, ci, H, H, co, k, pad)
+                    self._conv_dgrad(i, dy, ctx["wts"][i], dx, N)
                 gout = dx
             ops.mark(f"b{i}")
         for ev in wdone:
@@ -669,7 +686,8 @@ class MultiCentralEngine:
         # exact-f32 MFMA in the fp32 (parity) mode
         self.gm = ops.GEMM_BF16_MFMA if act_dtype == torch.bfloat16 else ops.GEMM_F32_MFMA
         self.ws = Workspace(store.device)
-        # conv_fp8: e4m3 MFMA forward for the mid-layer convs (bf16 mode only; config 5)
+        # conv_fp8: block-scaled e4m3 MFMA forward + input gradient for the mid-layer convs
+        # (bf16 mode only; config 5)
         self.conv_fp8 = bool(conv_fp8) and act_dtype == torch.bfloat16
         self.encoder = encoder
         istack, self.img_lin, astack, self.aud_lin, _sd = MULTI_ENCODERS[encoder]
