@@ -12,12 +12,11 @@
 //     and the other consumers read it) and is quantised while staged, with one power-of-two
 //     scale per staged strip (its max |x| maps into [128, 256): no overflow, exact rescaling)
 //     passed as the B scale of every MFMA of the strip;
-//   * K = (tap, channel) runs 128 per MFMA: a lane holds 32 consecutive k of one output pixel
-//     (OCP layout: lane l -> row / column l & 15, k = 32 (l >> 4) .. +31, verified with exact
-//     data: tools/probe/mx_probe.hip), read from the staged fp8 strip as 4 x ds_read_b64
-//     (8 channels: 4 taps) or 2 x ds_read_b128 (16 channels: 2 taps; 32 / 64 channels: 32
-//     contiguous bytes of one tap); pixel stride and row pad of the strip from
-//     tools/lds_bank_sim8.py.
+//   * K = (tap, channel) runs 128 per MFMA: a lane holds two 16-k pieces of one output pixel
+//     (mx_k below: the instruction's operand layout, measured), read from the staged fp8 strip
+//     as 4 x ds_read_b64 (8 channels: 2 taps per piece) or 2 x ds_read_b128 (16 channels: one
+//     tap per piece; 32 / 64 channels: 16 channels of one tap); pixel stride and row pad of the
+//     strip from tools/lds_bank_sim8.py.
 // Accumulation is f32 in the MFMA; y = bf16(acc + bias) and the statistics epilogue are those of
 // conv_ws_kernel.
 #include <algorithm>
@@ -67,13 +66,21 @@ struct W8 {
   static_assert(LDS_BYTES + RED * 16 <= 96 * 1024, "LDS");
 };
 
-// byte offset, inside the staged strip, of read u of the fragment of k-step ks for lane group g
+// The MX operand layout of v_mfma_scale_f32_16x16x128_f8f6f4 (measured with exact data and
+// per-lane scales, tools/probe/mx_probe.hip): lane l of row / column r = l & 15 and group
+// g = l >> 4 holds k = 16 g .. 16 g + 15 in its bytes 0-15 and k = 64 + 16 g .. + 15 in bytes
+// 16-31; the scale register of lane r + 16 b is the scale of k-block b = [32 b, 32 b + 32).
+// k of byte piece p (0, 1) of lane group g in k-step ks:
+__device__ __forceinline__ int mx_k(int ks, int g, int p) { return 128 * ks + 64 * p + 16 * g; }
+
+// byte offset, inside the staged strip, of read u of the fragment of k-step ks for lane group
+// g: 8 channels -> four 8-byte reads (two taps per piece), else one 16-byte read per piece
 template <class L>
 __device__ __forceinline__ int koff8(int ks, int g, int u) {
-  const int k0 = 128 * ks + 32 * g + (L::CIN == 8 ? 8 * u : (L::CIN == 16 ? 16 * u : 0));
+  const int k0 = L::CIN == 8 ? mx_k(ks, g, u >> 1) + 8 * (u & 1) : mx_k(ks, g, u);
   int tap = k0 / L::CIN, c = k0 % L::CIN;
   if (tap >= L::KK) { tap = 0; c = 0; }                    // padded k: weights are zero there
-  return ((tap / L::K) * L::RS + tap % L::K) * L::PS + c + (L::CIN >= 32 ? 16 * u : 0);
+  return ((tap / L::K) * L::RS + tap % L::K) * L::PS + c;
 }
 
 __device__ __forceinline__ unsigned absmax_bf16x8(u4 v, unsigned m) {
@@ -151,8 +158,13 @@ __global__ __launch_bounds__(256, L::OCC) void conv_ws8_kernel(
 #pragma unroll
     for (int t = 0; t < L::NTW; ++t) {
       const int row = cob + 16 * t + r16;
-      a[j][t] = live ? *reinterpret_cast<const i8v*>(wq + (size_t)row * L::KPAD + 128 * ks + 32 * g)
-                     : i8v{0, 0, 0, 0, 0, 0, 0, 0};
+      if (live) {
+        const u4 lo = *reinterpret_cast<const u4*>(wq + (size_t)row * L::KPAD + mx_k(ks, g, 0));
+        const u4 hi = *reinterpret_cast<const u4*>(wq + (size_t)row * L::KPAD + mx_k(ks, g, 1));
+        a[j][t] = i8v{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      } else {
+        a[j][t] = i8v{0, 0, 0, 0, 0, 0, 0, 0};
+      }
       const int sc = live ? (int)wsc[(size_t)row * (L::KPAD / 32) + 4 * ks + g] : 127;
       sa[j / 4][t] = (sa[j / 4][t] & ~(0xff << (8 * (j % 4)))) | (sc << (8 * (j % 4)));
     }
@@ -379,12 +391,12 @@ __global__ __launch_bounds__(256, L::OCC) void conv_ws8_kernel(
 //        CIN COUT K PAD  H   W  TH NS NCW NKW GB OCC PS RP
 typedef W8<8, 16, 5, 2, 56, 56, 14, 1, 1, 1, 2, 2, 8, 7> F8A2;     // audio conv2 forward
 typedef W8<16, 32, 5, 2, 28, 28, 14, 1, 1, 1, 1, 2, 16, 12> F8A3;  // audio conv3
-typedef W8<32, 64, 5, 2, 14, 14, 14, 1, 2, 2, 1, 2, 48, 12> F8A4;  // audio conv4
-typedef W8<32, 64, 5, 0, 14, 14, 10, 2, 2, 2, 1, 2, 48, 12> F8I2;  // image conv2
-typedef W8<16, 8, 5, 2, 56, 56, 8, 1, 1, 1, 1, 3, 16, 7> D8A2;     // audio conv2 input gradient
-typedef W8<32, 16, 5, 2, 28, 28, 14, 1, 1, 1, 1, 2, 48, 12> D8A3;  // audio conv3
-typedef W8<64, 32, 5, 2, 14, 14, 14, 1, 2, 2, 2, 2, 80, 4> D8A4;   // audio conv4
-typedef W8<64, 32, 5, 4, 10, 10, 14, 1, 2, 2, 2, 2, 80, 4> D8I2;   // image conv2
+typedef W8<32, 64, 5, 2, 14, 14, 14, 1, 2, 2, 1, 2, 32, 4> F8A4;   // audio conv4
+typedef W8<32, 64, 5, 0, 14, 14, 10, 2, 2, 2, 1, 2, 32, 4> F8I2;   // image conv2
+typedef W8<16, 8, 5, 2, 56, 56, 8, 1, 1, 1, 1, 3, 16, 12> D8A2;    // audio conv2 input gradient
+typedef W8<32, 16, 5, 2, 28, 28, 14, 1, 1, 1, 1, 2, 32, 4> D8A3;   // audio conv3
+typedef W8<64, 32, 5, 2, 14, 14, 14, 1, 2, 2, 2, 2, 96, 4> D8A4;   // audio conv4
+typedef W8<64, 32, 5, 4, 10, 10, 14, 1, 2, 2, 2, 2, 96, 4> D8I2;   // image conv2
 
 int num_cus8() {
   static int cus = 0;

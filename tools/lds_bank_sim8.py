@@ -1,7 +1,7 @@
 """LDS bank-conflict model of the fp8 (block-scaled MFMA) weights-stationary conv's B-fragment
-reads (conv_ws.hip, conv_ws8_kernel): per lane 32 consecutive K = (tap, channel) of one output
-pixel, read as 4 x ds_read_b64 (8 channels: 4 taps) or 2 x ds_read_b128 (16 channels: 2 taps;
-32 / 64 channels: 32 contiguous bytes of one tap).
+reads (conv_ws8.hip): per lane two 16-k pieces (k = 128 ks + 64 p + 16 g, the MX operand
+layout) of K = (tap, channel) of one output pixel, read as 4 x ds_read_b64 (8 channels: 2 taps
+per piece) or 2 x ds_read_b128 (one 16-byte read per piece).
 
 gfx950 LDS (MI355X_MICROARCH.md LDS table): 64 banks x 4 B; ds_read_b128 is served in 4 passes of
 16 lanes ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32), ds_read_b64 in 2 passes of 32 lanes; a
@@ -46,11 +46,14 @@ def cost(CIN, K, PAD, H, TH, NS, PS, RS):
                 addrs = []
                 for lane in range(64):
                     g, r16 = lane >> 4, lane & 15
-                    k0 = 128 * ks + 32 * g + (8 * u if CIN == 8 else (16 * u if CIN <= 16 else 0))
+                    if CIN == 8:
+                        k0 = 128 * ks + 64 * (u >> 1) + 16 * g + 8 * (u & 1)
+                    else:
+                        k0 = 128 * ks + 64 * u + 16 * g
                     tap, c = divmod(k0, CIN)
                     if tap >= KK:
                         tap, c = 0, 0
-                    off = ((tap // K) * RS + tap % K) * PS + c + (16 * u if CIN >= 32 else 0)
+                    off = ((tap // K) * RS + tap % K) * PS + c
                     addrs.append(base[r16] + off)
                 groups = B64 if width == 8 else B128
                 nwin = 256 // width
