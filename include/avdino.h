@@ -656,6 +656,12 @@ int avd_mx_conv_fwd(const void* x, const void* wq, const void* wsc, const float*
 /* dX [N][H][W][Cin] bf16 from dY [N][Ho][Wo][Cout] bf16 and the dgrad-layout MX weights. */
 int avd_mx_conv_dgrad(const void* dy, const void* wq_d, const void* wsc_d, void* dx, int N, int Cin,
                       int H, int W, int Cout, int K, int pad, void* stream);
+/* The conv's weight gradient (the autograd dW of nn.Conv2d) on the MX MFMA: x and dY bf16 NHWC
+ * quantised while staged (one power-of-two scale per staged strip and operand), K = output
+ * pixels; per-slab partials parts [avd_mx_wgrad_chunks][Cout][Cin][K][K] (sum: avd_sum_rows). */
+int avd_mx_wgrad_chunks(int N, int Cin, int H, int Cout, int K, int pad);
+int avd_mx_conv_wgrad(const void* x, const void* dy, float* parts, int N, int Cin, int H, int W,
+                      int Cout, int K, int pad, void* stream);
 
 #ifdef __cplusplus
 }

@@ -114,6 +114,8 @@ PROTOS = {
     "avd_mx_stat_rows": [I, I, I, I, I, I, I],
     "avd_mx_conv_fwd": [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, P],
     "avd_mx_conv_dgrad": [P, P, P, P, I, I, I, I, I, I, I, P],
+    "avd_mx_wgrad_chunks": [I, I, I, I, I, I],
+    "avd_mx_conv_wgrad": [P, P, P, I, I, I, I, I, I, I, P],
 }
 
 

@@ -344,6 +344,24 @@ def mx_conv_dgrad(dy, wq_d, wsc_d, dx, N, Cin, H, W, Cout, K, pad):
                         pad, stream()))
 
 
+def mx_wgrad_chunks(N, Cin, H, Cout, K, pad):
+    return lib.avd_mx_wgrad_chunks(N, Cin, H, Cout, K, pad)
+
+
+def mx_conv_wgrad(x, dy, parts, N, Cin, H, W, Cout, K, pad):
+    """Per-slab weight-gradient partials [chunks][Cout][Cin][K][K] on the MX MFMA (sum: sum_rows)."""
+    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
+    nch = mx_wgrad_chunks(N, Cin, H, Cout, K, pad)
+    _need(H == W and nch > 0, f"mx wgrad: no kernel for {Cin}->{Cout} @{H}")
+    _need(x.dtype == dy.dtype == torch.bfloat16, "mx wgrad dtypes (bf16 maps)")
+    _need(x.numel() == N * H * W * Cin and dy.numel() == N * Ho * Wo * Cout, "mx wgrad sizes")
+    _need(parts.dtype == torch.float32 and parts.numel() >= nch * Cout * Cin * K * K, "mx wgrad parts")
+    nb = (x.numel() + dy.numel()) * 2 + nch * Cout * Cin * K * K * 4
+    fl = 2 * N * Ho * Wo * Cout * Cin * K * K
+    _timed(f"mx_conv_wgrad[{N}x{H}x{W}x{Cin}->{Cout} k{K}p{pad}]", nb, fl,
+           lambda: call("avd_mx_conv_wgrad", p(x), p(dy), p(parts), N, Cin, H, W, Cout, K, pad, stream()))
+
+
 def cl_stat_pivot(Ho, Wo, B, K, Cin, Cout, dtype):
     return bool(lib.avd_cl_stat_pivot(Ho, Wo, B, K, Cin, Cout, _DT[dtype]))
 

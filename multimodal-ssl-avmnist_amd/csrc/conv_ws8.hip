@@ -487,9 +487,309 @@ __global__ void mx_weight_layout_kernel(const float* __restrict__ w, unsigned ch
 int mx_rows(int O) { return O > 32 ? (O + 63) / 64 * 64 : (O + 15) / 16 * 16; }
 int mx_kpad(int C, int K) { return (K * K * C + 127) / 128 * 128; }
 
+// ============================================================================ weight gradient
+// dW[co][ci][kh][kw] = sum_{n, oy, ox} dY[n][oy][ox][co] X[n][oy+kh-p][ox+kw-p][ci] on the MX
+// MFMA: M = output channels (A = dY^T), N = columns (tap, 16 input channels; for 8 input
+// channels a PAIR of taps x 8 channels), K = output pixels, 128 per MFMA.  One persistent block
+// per slab walks a contiguous range of strips (TR output rows of NSS samples) as wgrad_ws_kernel
+// does; the strip's dY and X (+ halo) are staged as e4m3 with one power-of-two scale each (their
+// max |.| into [128, 256)), pixel-major; both operands need 16-pixel runs of ONE channel per
+// lane piece, which ds_read_b64_tr_b8 delivers (per 16-lane group: lane 2q+p addresses row q,
+// bytes 8p..8p+7; lane i receives byte i of rows 0..7 -- measured, tools/probe/tr8_probe.hip):
+// each piece is two transposed reads of 8 pixels.
+template <int CIN_, int COUT_, int K_, int PAD_, int H_, int W_, int TR_, int NCW_, int OCC_,
+          int NSS_, int DYS_, int XS_, int NTHR_ = 256, int NMW_ = 1, int PF_ = 2>
+struct G8 {
+  static constexpr int CIN = CIN_, COUT = COUT_, K = K_, PAD = PAD_, H = H_, W = W_;
+  static constexpr int OCC = OCC_, PF = PF_, NTHR = NTHR_, WAVES = NTHR / 64;
+  static constexpr int HO = H + 2 * PAD - K + 1, WO = W + 2 * PAD - K + 1;
+  static constexpr int TR = TR_, SPS = HO / TR, NSS = NSS_;
+  static constexpr int XR = TR + K - 1, XW = WO + K - 1;
+  static constexpr int MT = COUT / 16, TAPS = K * K;
+  static constexpr bool PAIR = CIN == 8;
+  static constexpr int NCT = PAIR ? cdv(TAPS, 2) : TAPS * (CIN / 16);
+  static constexpr int NMW = NMW_, MTW = MT / NMW, NCW = NCW_, NPW = WAVES / (NMW * NCW);
+  static constexpr int NW = cdv(NCT, NCW);
+  static constexpr int DYS = DYS_, XS = XS_;                 // LDS bytes per pixel
+  static constexpr int SPIX = TR * WO, NPIX = NSS * SPIX, KST = cdv(NPIX, 128), DYP = KST * 128;
+  static constexpr int DY_T = NSS * TR * WO * (COUT / 8), X_T = NSS * XR * XW * (CIN / 8);
+  static constexpr int SLOTS = cdv(DY_T + X_T, NTHR);
+  static constexpr int DY_BYTES = DYP * DYS, X_BYTES = NSS * XR * XW * XS;
+  static constexpr int RED = NPW > 1 ? (NPW - 1) * NCW * NMW * MTW * NW * 64 : 0;   // f4
+  static constexpr int PER_CO = CIN * TAPS;
+  static constexpr int SMEM0 = DY_BYTES + X_BYTES;
+  static constexpr int SMEM1 = RED * 16 > 16 * PER_CO * 4 ? RED * 16 : 16 * PER_CO * 4;
+  static constexpr int SMEM = SMEM0 > SMEM1 ? SMEM0 : SMEM1;
+  static_assert(HO % TR == 0 && (NSS == 1 || SPS == 1), "strips tile the map");
+  static_assert(COUT % 16 == 0 && (CIN == 8 || CIN % 16 == 0), "channel tiles");
+  static_assert(DYS % 8 == 0 && XS % 8 == 0 && DYS >= COUT && XS >= CIN, "strides");
+  static_assert(WAVES % (NMW * NCW) == 0 && MT % NMW == 0, "wave split");
+  static_assert(SMEM <= 160 * 1024, "LDS");
+};
+
+typedef __attribute__((ext_vector_type(2))) int i2v;
+__device__ __forceinline__ i2v tr8(const unsigned char* p) {
+  return __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+      (__attribute__((address_space(3))) i2v*)(reinterpret_cast<uintptr_t>(p)));
+}
+
+template <class L>
+__global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws8_kernel(const bf16* __restrict__ x,
+                                                                const bf16* __restrict__ dy,
+                                                                float* __restrict__ parts, int N,
+                                                                int chunks) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[L::SMEM];
+  __shared__ unsigned amx[2][L::WAVES];
+  unsigned char* dys = smem;                   // [DYP][DYS]: strip pixel (s * TR + r) * WO + ox
+  unsigned char* xs = smem + L::DY_BYTES;      // [NSS][XR][XW][XS]: X[y0 - PAD + r][c - PAD]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int g = lane >> 4, r16 = lane & 15, qr = r16 >> 1, p2 = r16 & 1;
+  const int wm = wave % L::NMW, wc = (wave / L::NMW) % L::NCW, wp = wave / (L::NMW * L::NCW);
+
+  const int ngrp = N / L::NSS;
+  const int g0 = (int)(((long long)blockIdx.x * ngrp) / chunks);
+  const int g1 = (int)(((long long)(blockIdx.x + 1) * ngrp) / chunks);
+  const int st0 = g0 * L::SPS, st1 = g1 * L::SPS;
+
+  // this lane's address part for column tile j: (tap of its 8-byte half, channel offset)
+  int xo[L::NW];
+  bool cv[L::NW];
+#pragma unroll
+  for (int j = 0; j < L::NW; ++j) {
+    const int ct = wc * L::NW + j;
+    int tap, ch;
+    if constexpr (L::PAIR) { tap = 2 * ct + p2; ch = 0; }
+    else { tap = ct / (L::CIN / 16); ch = 16 * (ct % (L::CIN / 16)) + 8 * p2; }
+    cv[j] = ct < L::NCT;
+    if (!cv[j] || tap >= L::TAPS) tap = 0;
+    xo[j] = ((tap / L::K) * L::XW + tap % L::K) * L::XS + ch;
+  }
+
+  f4 acc[L::MTW][L::NW];
+#pragma unroll
+  for (int m = 0; m < L::MTW; ++m)
+#pragma unroll
+    for (int j = 0; j < L::NW; ++j) acc[m][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // the k-step tail of the dY image (pixels >= NPIX) stays zero for the whole launch
+  for (int i = tid; i < (L::DYP - L::NPIX) * L::DYS / 8; i += L::NTHR)
+    *reinterpret_cast<uint2*>(dys + (size_t)L::NPIX * L::DYS + 8 * i) = make_uint2(0u, 0u);
+
+  struct Slot { int goff, loff, xrow; };   // xrow < 0: a dY task
+  auto slot = [&](int i) -> Slot {
+    const int task = tid + L::NTHR * i;
+    if (task < L::DY_T) {
+      constexpr int V = L::COUT / 8;
+      const int q = task % V, pix = task / V;
+      const int rs = pix / L::WO, ox = pix - rs * L::WO;
+      const int sm = rs / L::TR, r = rs - sm * L::TR;
+      return Slot{((sm * L::HO + r) * L::WO + ox) * L::COUT + 8 * q, pix * L::DYS + 8 * q, -1};
+    }
+    constexpr int V = L::CIN / 8;
+    const int t = task - L::DY_T;
+    const int q = t % V, pix = t / V;
+    const int rs = pix / L::XW, c = pix - rs * L::XW;
+    const int sm = rs / L::XR, r = rs - sm * L::XR;
+    const int ix = c - L::PAD;
+    return Slot{(task < L::DY_T + L::X_T && ix >= 0 && ix < L::W) ? ((sm * L::H + r) * L::W + ix) * L::CIN + 8 * q : -1,
+                L::DY_BYTES + pix * L::XS + 8 * q, r};
+  };
+  u4 pre[L::SLOTS];
+  auto load_strip = [&](int st) {
+    const int sg = st / L::SPS, y0 = (st - sg * L::SPS) * L::TR;
+    const int n = sg * L::NSS;
+    const bf16* bdy = dy + ((size_t)n * L::HO + y0) * L::WO * L::COUT;
+    const bf16* bx = x + ((long long)n * L::H + y0 - L::PAD) * L::W * L::CIN;
+#pragma unroll
+    for (int i = 0; i < L::SLOTS; ++i) {
+      const Slot sl = slot(i);
+      const void* src = &kZero8;
+      if (tid + L::NTHR * i < L::DY_T) src = bdy + sl.goff;
+      else if (sl.goff >= 0 && (unsigned)(y0 - L::PAD + sl.xrow) < (unsigned)L::H) src = bx + sl.goff;
+      pre[i] = ldg16(src);
+    }
+  };
+
+  if (st0 < st1) load_strip(st0);
+  for (int st = st0; st < st1; ++st) {
+    // the strip's max |dY| and max |X|: per wave, then through LDS
+    unsigned md = 0u, mx = 0u;
+#pragma unroll
+    for (int i = 0; i < L::SLOTS; ++i) {
+      if (tid + L::NTHR * i < L::DY_T) md = absmax_bf16x8(pre[i], md);
+      else mx = absmax_bf16x8(pre[i], mx);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      md = max(md, (unsigned)__shfl_xor((int)md, o, 64));
+      mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
+    }
+    if (lane == 0) { amx[0][wave] = md; amx[1][wave] = mx; }
+    __syncthreads();   // every wave is done with the previous strip; amx complete
+    md = amx[0][0];
+    mx = amx[1][0];
+#pragma unroll
+    for (int w = 1; w < L::WAVES; ++w) { md = max(md, amx[0][w]); mx = max(mx, amx[1][w]); }
+    const int shd = mx_shift(__uint_as_float(md << 16)), shx = mx_shift(__uint_as_float(mx << 16));
+    const float muld = ldexpf(1.f, shd), mulx = ldexpf(1.f, shx);
+    const int sbd = 127 - shd, sbx = 127 - shx;
+#pragma unroll
+    for (int i = 0; i < L::SLOTS; ++i) {
+      const int task = tid + L::NTHR * i;
+      if (task < L::DY_T + L::X_T)
+        *reinterpret_cast<uint2*>(smem + slot(i).loff) = q8(pre[i], task < L::DY_T ? muld : mulx);
+    }
+    __syncthreads();
+    if (st + 1 < st1) load_strip(st + 1);
+
+    for (int ks = wp; ks < L::KST; ks += L::NPW) {
+      // this lane's 4 rows (pixels) of the k-step: piece pc, transposed read h, row q8
+      int xb[2][2];
+      i8v a[L::MTW];
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int P = 128 * ks + 64 * pc + 16 * g + 8 * h + qr;
+          const int Pc = min(P, L::NPIX - 1);                 // tail pixels: dY is 0 there
+          const int sm = Pc / L::SPIX, rem = Pc - sm * L::SPIX;
+          const int r = rem / L::WO, ox = rem - r * L::WO;
+          xb[pc][h] = ((sm * L::XR + r) * L::XW + ox) * L::XS;
+#pragma unroll
+          for (int m = 0; m < L::MTW; ++m) {
+            const i2v v = tr8(dys + P * L::DYS + 16 * (wm * L::MTW + m) + 8 * p2);
+            a[m][4 * pc + 2 * h] = v.x;
+            a[m][4 * pc + 2 * h + 1] = v.y;
+          }
+        }
+      constexpr int PF = L::PF;
+      i8v bq[PF + 1];
+      auto ldb = [&](i8v& d, int j) {
+#pragma unroll
+        for (int pc = 0; pc < 2; ++pc)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const i2v v = tr8(xs + xb[pc][h] + xo[j]);
+            d[4 * pc + 2 * h] = v.x;
+            d[4 * pc + 2 * h + 1] = v.y;
+          }
+      };
+#pragma unroll
+      for (int j = 0; j < PF && j < L::NW; ++j) ldb(bq[j], j);
+#pragma unroll
+      for (int j = 0; j < L::NW; ++j) {
+        if (j + PF < L::NW) ldb(bq[(j + PF) % (PF + 1)], j + PF);
+#pragma unroll
+        for (int m = 0; m < L::MTW; ++m)
+          acc[m][j] = mxmma_<0>(a[m], bq[j % (PF + 1)], acc[m][j], sbd, sbx);
+      }
+    }
+  }
+
+  // pixel-split partials -> wave wp = 0 (fixed order), then the slab write (as wgrad_ws_kernel)
+  if constexpr (L::NPW > 1) {
+    f4* red = reinterpret_cast<f4*>(smem);
+    const int slot = wm * L::NCW + wc;
+    __syncthreads();
+    if (wp > 0) {
+#pragma unroll
+      for (int m = 0; m < L::MTW; ++m)
+#pragma unroll
+        for (int j = 0; j < L::NW; ++j)
+          red[((((wp - 1) * L::NCW * L::NMW + slot) * L::MTW + m) * L::NW + j) * 64 + lane] = acc[m][j];
+    }
+    __syncthreads();
+    if (wp == 0) {
+#pragma unroll
+      for (int w = 1; w < L::NPW; ++w)
+#pragma unroll
+        for (int m = 0; m < L::MTW; ++m)
+#pragma unroll
+          for (int j = 0; j < L::NW; ++j)
+            acc[m][j] += red[((((w - 1) * L::NCW * L::NMW + slot) * L::MTW + m) * L::NW + j) * 64 + lane];
+    }
+  }
+  float* tb = reinterpret_cast<float*>(smem);
+  float* out = parts + (size_t)blockIdx.x * L::COUT * L::PER_CO;
+  for (int mt = 0; mt < L::MT; ++mt) {
+    __syncthreads();
+    if (wp == 0) {
+#pragma unroll
+      for (int m = 0; m < L::MTW; ++m) {
+        if (wm * L::MTW + m != mt) continue;
+#pragma unroll
+        for (int j = 0; j < L::NW; ++j) {
+          if (!cv[j]) continue;
+          const int ct = wc * L::NW + j;
+          int tap, ci;
+          if constexpr (L::PAIR) { tap = 2 * ct + (r16 >> 3); ci = r16 & 7; }
+          else { tap = ct / (L::CIN / 16); ci = 16 * (ct % (L::CIN / 16)) + r16; }
+          if (tap >= L::TAPS) continue;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) tb[(4 * g + i) * L::PER_CO + ci * L::TAPS + tap] = acc[m][j][i];
+        }
+      }
+    }
+    __syncthreads();
+    float4* o4 = reinterpret_cast<float4*>(out + (size_t)mt * 16 * L::PER_CO);
+    const float4* t4 = reinterpret_cast<const float4*>(tb);
+    for (int e = tid; e < 16 * L::PER_CO / 4; e += L::NTHR) o4[e] = t4[e];
+  }
+}
+
+//          CIN COUT K PAD  H   W  TR NCW OCC NSS DYS XS
+typedef G8<8, 16, 5, 2, 56, 56, 8, 1, 2, 1, 16, 8> G8A2;     // audio conv2
+typedef G8<16, 32, 5, 2, 28, 28, 14, 4, 2, 1, 32, 16> G8A3;  // audio conv3
+typedef G8<32, 64, 5, 2, 14, 14, 14, 4, 1, 1, 64, 32, 512, 2, 1> G8A4;  // audio conv4
+typedef G8<32, 64, 5, 0, 14, 14, 10, 4, 1, 1, 64, 32, 512, 2, 1> G8I2;  // image conv2
+
+template <class L>
+bool g8_is(int Cin, int H, int Cout, int K, int pad) {
+  return Cin == L::CIN && Cout == L::COUT && K == L::K && pad == L::PAD && H == L::H;
+}
+
+template <class L>
+int g8_chunks(int N) {
+  static int occ = 0;
+  if (!occ) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wgrad_ws8_kernel<L>, L::NTHR, 0) != hipSuccess || occ <= 0)
+      occ = 1;
+  }
+  return std::max(1, grid_cap(std::min(N / L::NSS, num_cus8() * occ)));
+}
+
 }  // namespace
 
 extern "C" {
+
+// slabs of avd_mx_conv_wgrad for the conv Cin -> Cout over H x H (0: not served)
+int avd_mx_wgrad_chunks(int N, int Cin, int H, int Cout, int K, int pad) {
+#define AVD_G8(LL) if (g8_is<LL>(Cin, H, Cout, K, pad)) return N % LL::NSS ? 0 : g8_chunks<LL>(N);
+  AVD_G8(G8A2) AVD_G8(G8A3) AVD_G8(G8A4) AVD_G8(G8I2)
+#undef AVD_G8
+  return 0;
+}
+
+// per-slab weight gradients parts [chunks][Cout][Cin][K][K] (sum them: avd_sum_rows)
+int avd_mx_conv_wgrad(const void* x, const void* dy, float* parts, int N, int Cin, int H, int W,
+                      int Cout, int K, int pad, void* stream) {
+  if (!x || !dy || !parts) return AVD_ERR_ARG;
+  if (H != W) return AVD_ERR_SHAPE;
+  hipStream_t st = avd_stream(stream);
+#define AVD_G8(LL)                                                                               \
+  if (g8_is<LL>(Cin, H, Cout, K, pad)) {                                                        \
+    if (N % LL::NSS) return AVD_ERR_SHAPE;                                                      \
+    const int chunks = g8_chunks<LL>(N);                                                        \
+    wgrad_ws8_kernel<LL><<<chunks, LL::NTHR, 0, st>>>((const bf16*)x, (const bf16*)dy, parts, N, chunks); \
+    AVD_CHECK_LAUNCH();                                                                         \
+    return AVD_OK;                                                                              \
+  }
+  AVD_G8(G8A2) AVD_G8(G8A3) AVD_G8(G8A4) AVD_G8(G8I2)
+#undef AVD_G8
+  return AVD_ERR_SHAPE;
+}
+
+
 
 long long avd_mx_weight_bytes(int Cout, int Cin, int K, int dgrad) {
   const int O = dgrad ? Cin : Cout, C = dgrad ? Cout : Cin;

@@ -8,6 +8,8 @@ avd_mx_conv_fwd / avd_mx_conv_dgrad) against float64 on the same inputs.
   per-block weight scales and the flipped input-gradient weights, at test size with a capped
   grid (every block walks several strips) and uncapped.  The forward's BatchNorm partial sums
   equal the float64 sums of the stored y.
+* The weight gradient (avd_mx_conv_wgrad, K = output pixels): exact data -> the slab sum equals
+  float64 dW bit for bit.
 * Random data: the error against float64 of the unquantised operands is the e4m3 rounding's
   (rel-L2 < 0.06; 3 mantissa bits give ~3.6 % rms per operand)."""
 import os
@@ -109,3 +111,44 @@ def test_mx_conv_random_data_error_is_e4m3_rounding(layer):
     dref = _ref_dgrad(dy.float(), w, pad)
     derr = ((dx.double() - dref).norm() / dref.norm()).item()
     assert 0.005 < derr < 0.06, derr
+
+
+def _ref_wgrad(x, dy, w_shape, pad):
+    return torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), w_shape,
+                                       dy.double().permute(0, 3, 1, 2), padding=pad)
+
+
+def _wgrad(x, dy, N, Cin, H, Cout, K, pad):
+    from avdino import ops
+    nch = ops.mx_wgrad_chunks(N, Cin, H, Cout, K, pad)
+    assert nch > 0
+    parts = torch.full((nch * Cout * Cin * K * K,), float("nan"), device="cuda")
+    ops.mx_conv_wgrad(x, dy, parts, N, Cin, H, H, Cout, K, pad)
+    return parts.view(nch, Cout, Cin, K, K).double().sum(0)
+
+
+@pytest.mark.parametrize("layer", LAYERS, ids=[f"{l[0]}to{l[1]}@{l[4]}p{l[3]}" for l in LAYERS])
+def test_mx_wgrad_exact_data(layer, capped):
+    Cin, Cout, K, pad, H = layer
+    Ho = H + 2 * pad - K + 1
+    N = 6
+    g = torch.Generator().manual_seed(Cout * 10 + H)
+    x = _bf(torch.randint(-8, 9, (N, H, H, Cin), generator=g).float()).cuda()
+    dy = _bf(torch.randint(-8, 9, (N, Ho, Ho, Cout), generator=g).float()).cuda()
+    dw = _wgrad(x, dy, N, Cin, H, Cout, K, pad)
+    ref = _ref_wgrad(x.float(), dy.float(), (Cout, Cin, K, K), pad)
+    assert torch.equal(dw, ref), (dw - ref).abs().max()
+
+
+@pytest.mark.parametrize("layer", LAYERS, ids=[f"{l[0]}to{l[1]}@{l[4]}p{l[3]}" for l in LAYERS])
+def test_mx_wgrad_random_data_error_is_e4m3_rounding(layer):
+    Cin, Cout, K, pad, H = layer
+    Ho = H + 2 * pad - K + 1
+    N = 8
+    g = torch.Generator().manual_seed(70 + Cin)
+    x = _bf(torch.randn(N, H, H, Cin, generator=g).abs()).cuda()        # post-ReLU/pool-like
+    dy = _bf(torch.randn(N, Ho, Ho, Cout, generator=g) * 1e-5).cuda()   # gradient-sized
+    dw = _wgrad(x, dy, N, Cin, H, Cout, K, pad)
+    ref = _ref_wgrad(x.float(), dy.float(), (Cout, Cin, K, K), pad)
+    err = ((dw - ref).norm() / ref.norm()).item()
+    assert 0.002 < err < 0.06, err

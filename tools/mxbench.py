@@ -59,8 +59,14 @@ def main():
         t8 = timeit(lambda: ops.mx_conv_fwd(x, wq, ws, b, y, st, N, B, Cin, H, H, Cout, K, pad), a.reps)
         db = timeit(lambda: ops.cl_conv_dgrad(dy, wkd, dx, N, Cin, H, H, Cout, K, pad), a.reps)
         d8 = timeit(lambda: ops.mx_conv_dgrad(dy, wqd, wsd, dx, N, Cin, H, H, Cout, K, pad), a.reps)
+        nch = ops.cl_wgrad_chunks(N, Cout, Cin, K)
+        nch8 = ops.mx_wgrad_chunks(N, Cin, H, Cout, K, pad)
+        parts = torch.empty(max(nch, nch8) * Cout * Cin * K * K, device="cuda")
+        wb = timeit(lambda: ops.cl_conv_wgrad(x, dy, parts, N, Cin, H, H, Cout, K, pad), a.reps)
+        w8 = timeit(lambda: ops.mx_conv_wgrad(x, dy, parts, N, Cin, H, H, Cout, K, pad), a.reps)
         print(f"{Cin:>2}->{Cout:<2} @{H} p{pad} N={N}: fwd bf16 {tb:7.1f} us  mx {t8:7.1f} us ({tb / t8:4.2f}x, "
-              f"{fl / t8 / 1e6:6.0f} TF/s)   dgrad bf16 {db:7.1f}  mx {d8:7.1f} ({db / d8:4.2f}x)", flush=True)
+              f"{fl / t8 / 1e6:6.0f} TF/s)   dgrad bf16 {db:7.1f}  mx {d8:7.1f} ({db / d8:4.2f}x)   "
+              f"wgrad bf16 {wb:7.1f}  mx {w8:7.1f} ({wb / w8:4.2f}x)", flush=True)
 
 
 if __name__ == "__main__":
