@@ -123,6 +123,24 @@ class ConvBranch:
         else:
             ops.cl_conv_dgrad(dy, wt[1], dx, N, ci, H, H, co, k, pad)
 
+    def _mx_wgrad(self, i, N):
+        ci, co, k, p = self.stack.convs[i]
+        return self.fp8 and i > 0 and ops.mx_wgrad_chunks(N, ci, self.dims[i][0], co, k, p) > 0
+
+    def _wgrad_chunks(self, i, N):
+        ci, co, k, p = self.stack.convs[i]
+        if self._mx_wgrad(i, N):
+            return ops.mx_wgrad_chunks(N, ci, self.dims[i][0], co, k, p)
+        return ops.cl_wgrad_chunks(N, co, ci, k)
+
+    def _conv_wgrad(self, i, x, dy, wparts, N):
+        ci, co, k, pad = self.stack.convs[i]
+        H = self.dims[i][0]
+        if self._mx_wgrad(i, N):
+            ops.mx_conv_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
+        else:
+            ops.cl_conv_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
+
     # A/B switch for the statistics pivot (AVDINO_NO_PIVOT=1: raw sums, as before round 3)
     NO_PIVOT = os.environ.get("AVDINO_NO_PIVOT", "0") == "1"
 
@@ -443,7 +461,7 @@ class ConvBranch:
                 ops.sum_rows(wparts, nsl, co * ci * k * k, store.grad_of(ck + ".weight"))
                 ops.mark(f"b{i}")
                 continue
-            nch = ops.cl_wgrad_chunks(N, co, ci, k)
+            nch = self._wgrad_chunks(i, N)
             wparts = ws.get("wgrad_parts", nch * co * ci * k * k)
             if (self.BNAPPLY_FUSED and i > 0 and mode in (0, 2) and ctx["wts"][i][1] is not None and
                     ops.cl_bnapply_ok(self.act, N, B, ci, H, H, co, k, pad, mode)):
@@ -469,13 +487,13 @@ class ConvBranch:
                     wparts = ws.get(f"wgrad_parts{i}", nch * co * ci * k * k)
                     wstream.wait_stream(main)
                     with torch.cuda.stream(wstream):
-                        ops.cl_conv_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
+                        self._conv_wgrad(i, x, dy, wparts, N)
                         ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
                         ev = torch.cuda.Event()
                         ev.record(wstream)
                     wdone.append(ev)
                 else:
-                    ops.cl_conv_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
+                    self._conv_wgrad(i, x, dy, wparts, N)
                     ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
                 gout = dx
                 continue
@@ -485,14 +503,14 @@ class ConvBranch:
                 wstream.wait_stream(main)
                 with torch.cuda.stream(wstream):
                     ops.mark(f"w{i}.begin")
-                    ops.cl_conv_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
+                    self._conv_wgrad(i, x, dy, wparts, N)
                     ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
                     ops.mark(f"w{i}.end")
                     ev = torch.cuda.Event()
                     ev.record(wstream)
                 wdone.append(ev)
             else:
-                ops.cl_conv_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
+                self._conv_wgrad(i, x, dy, wparts, N)
                 ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
             if i > 0:
                 dx = ws.get("bwd_dx", N * H * H * ci, self.act)
