@@ -645,6 +645,10 @@ long long avd_mx_scale_bytes(int Cout, int Cin, int K, int dgrad);
  * (rows = input channels, taps flipped), as avd_cl_weight_layout. */
 int avd_mx_weight_layout(const float* w, void* wq, void* wsc, int Cout, int Cin, int K, int dgrad,
                          void* stream);
+/* n <= 16 layouts in one launch (a conv stack's per-step MX weights). */
+int avd_mx_weight_layout_batch(int n, const float* const* w, void* const* wq, void* const* wsc,
+                               const int* cout, const int* cin, const int* k, const int* dgrad,
+                               void* stream);
 /* 1 if the forward (dgrad 0) / input gradient (dgrad 1) of conv Cin -> Cout over H x W has an
  * MX kernel. */
 int avd_mx_conv_serves(int Cin, int H, int W, int Cout, int K, int pad, int dgrad);

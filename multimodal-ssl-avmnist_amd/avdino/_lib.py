@@ -110,6 +110,7 @@ PROTOS = {
     "avd_mx_weight_bytes": [I, I, I, I],
     "avd_mx_scale_bytes": [I, I, I, I],
     "avd_mx_weight_layout": [P, P, P, I, I, I, I, P],
+    "avd_mx_weight_layout_batch": [I, P, P, P, P, P, P, P, P],
     "avd_mx_conv_serves": [I, I, I, I, I, I, I],
     "avd_mx_stat_rows": [I, I, I, I, I, I, I],
     "avd_mx_conv_fwd": [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, P],

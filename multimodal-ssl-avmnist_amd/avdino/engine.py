@@ -83,14 +83,14 @@ class ConvBranch:
     def prepare(self, ws, store, tag, need_dgrad):
         """MFMA weight layouts for this step (the weights change every step), per layer:
         (bf16 forward rows, bf16 dgrad rows, MX forward (e4m3 rows, scales), MX dgrad)."""
-        wts, batch = [], []
+        wts, batch, mxb = [], [], []
         for i, (ci, co, k, _p) in enumerate(self.stack.convs):
             w = store[self.stack.conv_keys[i] + ".weight"]
             wk = wd = q = qd = None
             if self._mx_ok(i):
                 q = (ws.get(f"{tag}.wq{i}", ops.mx_weight_bytes(co, ci, k, 0), torch.uint8),
                      ws.get(f"{tag}.wqs{i}", ops.mx_scale_bytes(co, ci, k, 0), torch.uint8))
-                ops.mx_weight_layout(w, q[0], q[1], 0)
+                mxb.append((w, q[0], q[1], 0))
             else:
                 wk = ws.get(f"{tag}.wk{i}", ops.cl_weight_elems(co, ci, k, 0), self.act)
                 batch.append((w, wk, 0))
@@ -98,13 +98,15 @@ class ConvBranch:
                 if self._mx_ok(i, dgrad=True):
                     qd = (ws.get(f"{tag}.wqd{i}", ops.mx_weight_bytes(co, ci, k, 1), torch.uint8),
                           ws.get(f"{tag}.wqds{i}", ops.mx_scale_bytes(co, ci, k, 1), torch.uint8))
-                    ops.mx_weight_layout(w, qd[0], qd[1], 1)
+                    mxb.append((w, qd[0], qd[1], 1))
                 else:
                     wd = ws.get(f"{tag}.wd{i}", ops.cl_weight_elems(co, ci, k, 1), self.act)
                     batch.append((w, wd, 1))
             wts.append((wk, wd, q, qd))
         if batch:       # every bf16 layout of the stack in one launch
             ops.cl_weight_layout_batch(batch)
+        if mxb:         # and every MX layout in another
+            ops.mx_weight_layout_batch(mxb)
         return wts
 
     def _conv_fwd(self, i, h, wt, bias, y, parts, N, B, pivot=None):

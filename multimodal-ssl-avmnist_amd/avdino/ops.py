@@ -301,6 +301,23 @@ def mx_weight_layout(w, wq, wsc, dgrad):
     call("avd_mx_weight_layout", p(w), p(wq), p(wsc), Cout, Cin, K, int(dgrad), stream())
 
 
+def mx_weight_layout_batch(entries):
+    """entries: [(w f32 [Cout,Cin,K,K], wq, wsc, dgrad)] (<= 16) -> one launch."""
+    import ctypes as _ct
+    n = len(entries)
+    _need(0 < n <= 16, "mx layout batch size")
+    for w, wq, wsc, dg in entries:
+        Co, Ci, K, _ = w.shape
+        _need(w.dtype == torch.float32 and w.is_contiguous(), "mx batch w")
+        _need(wq.dtype == torch.uint8 and wq.numel() >= mx_weight_bytes(Co, Ci, K, dg), "mx batch wq")
+        _need(wsc.dtype == torch.uint8 and wsc.numel() >= mx_scale_bytes(Co, Ci, K, dg), "mx batch wsc")
+    PA, IA = _ct.c_void_p * n, _ct.c_int * n
+    call("avd_mx_weight_layout_batch", n, PA(*[e[0].data_ptr() for e in entries]),
+         PA(*[e[1].data_ptr() for e in entries]), PA(*[e[2].data_ptr() for e in entries]),
+         IA(*[e[0].shape[0] for e in entries]), IA(*[e[0].shape[1] for e in entries]),
+         IA(*[e[0].shape[2] for e in entries]), IA(*[int(e[3]) for e in entries]), stream())
+
+
 def mx_conv_serves(Cin, H, Cout, K, pad, dgrad):
     return bool(lib.avd_mx_conv_serves(Cin, H, H, Cout, K, pad, int(dgrad)))
 

@@ -448,12 +448,10 @@ bool is8(int Cin, int H, int W, int Cout, int K, int pad) {
 // MX weight layout: rows o (forward: output channels; input gradient: input channels, with
 // the taps flipped), k = tap * C + c zero-padded to KPAD = 128 * ceil(K*K*C / 128); one e4m3
 // byte per k and one E8M0 byte per 32-k block (its max |w| into [128, 256))
-__global__ void mx_weight_layout_kernel(const float* __restrict__ w, unsigned char* __restrict__ wq,
-                                        unsigned char* __restrict__ wsc, int Cout, int Cin, int KK,
-                                        int dgrad, int rows, int kpad) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void mx_weight_block(const float* __restrict__ w, unsigned char* __restrict__ wq,
+                                                unsigned char* __restrict__ wsc, int Cout, int Cin,
+                                                int KK, int dgrad, int kpad, int i) {
   const int nb = kpad / 32;
-  if (i >= rows * nb) return;
   const int o = i / nb, kb = i - o * nb;
   const int O = dgrad ? Cin : Cout, C = dgrad ? Cout : Cin;
   float v[32];
@@ -482,6 +480,28 @@ __global__ void mx_weight_layout_kernel(const float* __restrict__ w, unsigned ch
 #pragma unroll
   for (int q = 0; q < 8; ++q) dst[q] = word[q];
   wsc[i] = (unsigned char)(127 - sh);
+}
+
+__global__ void mx_weight_layout_kernel(const float* __restrict__ w, unsigned char* __restrict__ wq,
+                                        unsigned char* __restrict__ wsc, int Cout, int Cin, int KK,
+                                        int dgrad, int rows, int kpad) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < rows * (kpad / 32)) mx_weight_block(w, wq, wsc, Cout, Cin, KK, dgrad, kpad, i);
+}
+
+// several layouts in one launch (blockIdx.y = entry): a conv stack's per-step MX weights
+constexpr int MXB_MAX = 16;
+struct MXBatch {
+  const float* w[MXB_MAX];
+  unsigned char* wq[MXB_MAX];
+  unsigned char* wsc[MXB_MAX];
+  int cout[MXB_MAX], cin[MXB_MAX], kk[MXB_MAX], dgrad[MXB_MAX], n[MXB_MAX], kpad[MXB_MAX];
+};
+
+__global__ void mx_weight_layout_batch_kernel(MXBatch b) {
+  const int e = blockIdx.y;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < b.n[e]; i += gridDim.x * blockDim.x)
+    mx_weight_block(b.w[e], b.wq[e], b.wsc[e], b.cout[e], b.cin[e], b.kk[e], b.dgrad[e], b.kpad[e], i);
 }
 
 int mx_rows(int O) { return O > 32 ? (O + 63) / 64 * 64 : (O + 15) / 16 * 16; }
@@ -741,6 +761,9 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws8_kernel(const bf16* 
 typedef G8<8, 16, 5, 2, 56, 56, 8, 1, 2, 1, 16, 8> G8A2;     // audio conv2
 typedef G8<16, 32, 5, 2, 28, 28, 14, 4, 2, 1, 32, 16> G8A3;  // audio conv3
 typedef G8<32, 64, 5, 2, 14, 14, 7, 4, 1, 1, 64, 32, 512, 2, 1> G8A4;   // audio conv4
+// (A/B candidates for audio conv4, AVDINO_G8A4=1 / 2)
+typedef G8<32, 64, 5, 2, 14, 14, 7, 8, 1, 1, 64, 32, 512, 1, 1> G8A4b;
+typedef G8<32, 64, 5, 2, 14, 14, 7, 1, 1, 1, 64, 32, 256, 4, 1> G8A4c;  // audio conv4
 typedef G8<32, 64, 5, 0, 14, 14, 10, 4, 1, 1, 64, 32, 512, 2, 1> G8I2;  // image conv2
 
 template <class L>
@@ -764,7 +787,10 @@ extern "C" {
 
 // slabs of avd_mx_conv_wgrad for the conv Cin -> Cout over H x H (0: not served)
 int avd_mx_wgrad_chunks(int N, int Cin, int H, int Cout, int K, int pad) {
+  static const int a4 = getenv("AVDINO_G8A4") ? atoi(getenv("AVDINO_G8A4")) : 0;
 #define AVD_G8(LL) if (g8_is<LL>(Cin, H, Cout, K, pad)) return N % LL::NSS ? 0 : g8_chunks<LL>(N);
+  if (a4 == 1) AVD_G8(G8A4b)
+  if (a4 == 2) AVD_G8(G8A4c)
   AVD_G8(G8A2) AVD_G8(G8A3) AVD_G8(G8A4) AVD_G8(G8I2)
 #undef AVD_G8
   return 0;
@@ -784,6 +810,9 @@ int avd_mx_conv_wgrad(const void* x, const void* dy, float* parts, int N, int Ci
     AVD_CHECK_LAUNCH();                                                                         \
     return AVD_OK;                                                                              \
   }
+  static const int a4 = getenv("AVDINO_G8A4") ? atoi(getenv("AVDINO_G8A4")) : 0;
+  if (a4 == 1) AVD_G8(G8A4b)
+  if (a4 == 2) AVD_G8(G8A4c)
   AVD_G8(G8A2) AVD_G8(G8A3) AVD_G8(G8A4) AVD_G8(G8I2)
 #undef AVD_G8
   return AVD_ERR_SHAPE;
@@ -809,6 +838,30 @@ int avd_mx_weight_layout(const float* w, void* wq, void* wsc, int Cout, int Cin,
   const int n = rows * (kpad / 32);
   mx_weight_layout_kernel<<<avd_cdiv(n, 128), 128, 0, avd_stream(stream)>>>(
       w, (unsigned char*)wq, (unsigned char*)wsc, Cout, Cin, K * K, dgrad ? 1 : 0, rows, kpad);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+// n layouts (<= 16) in one launch: the arguments of avd_mx_weight_layout as arrays
+int avd_mx_weight_layout_batch(int n, const float* const* w, void* const* wq, void* const* wsc,
+                               const int* cout, const int* cin, const int* k, const int* dgrad,
+                               void* stream) {
+  if (n <= 0 || n > MXB_MAX) return AVD_ERR_ARG;
+  MXBatch b{};
+  int most = 1;
+  for (int e = 0; e < n; ++e) {
+    if (!w[e] || !wq[e] || !wsc[e]) return AVD_ERR_ARG;
+    if (cout[e] <= 0 || cin[e] <= 0 || k[e] <= 0) return AVD_ERR_SHAPE;
+    const int O = dgrad[e] ? cin[e] : cout[e], C = dgrad[e] ? cout[e] : cin[e];
+    b.w[e] = w[e];
+    b.wq[e] = (unsigned char*)wq[e];
+    b.wsc[e] = (unsigned char*)wsc[e];
+    b.cout[e] = cout[e]; b.cin[e] = cin[e]; b.kk[e] = k[e] * k[e]; b.dgrad[e] = dgrad[e] ? 1 : 0;
+    b.kpad[e] = mx_kpad(C, k[e]);
+    b.n[e] = mx_rows(O) * (b.kpad[e] / 32);
+    most = std::max(most, b.n[e]);
+  }
+  mx_weight_layout_batch_kernel<<<dim3(avd_cdiv(most, 128), n), 128, 0, avd_stream(stream)>>>(b);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
