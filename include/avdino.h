@@ -627,6 +627,28 @@ int avd_fp8_conv_fwd(const void* x, float xscale, const void* wq, const float* w
                      const float* bias, void* y, float* stats, int N, int B, int Cin, int H,
                      int W, int Cout, int K, int pad, void* stream);
 
+/* ------------------------------------------------------------------ routed 3x3 first layer
+ * The SimCLR / unimodal encoders' conv1 (audio_encoder / image_encoder, dino.py:18-73:
+ * Conv2d(1, 32, 3, padding=1) -> BN2d -> ReLU -> MaxPool2d on 112x112 / 28x28, bf16) without a
+ * stored conv output, backward routed by the forward's codes (the 3x3 counterpart of the
+ * avd_cl_c1r5_* entry points): the BN -> ReLU -> pool pass also writes, per pooling window and
+ * channel, the nibble 1 + (first argmax of relu(bn(y)) when > 0, else 0) -- u16 codes
+ * [N][H/2][W/2][8]; the backward pass forms M = sum dz x9 (+ sum dz), Gram = sum x9 x9^T and
+ * S = sum x9 per BN group from x, the pooled gradient and the codes (no y, no BN
+ * coefficients), [avd_cl_c1r3_codes_rows][G][avd_cl_c1r3_codes_cols] partials (sum_rows), and
+ * the float64 combine gives dW, dgamma, dbeta, dbias and the BN-backward coefficients. */
+int avd_cl_c1r3_codes_rows(int N, int B, int H, int W, int Cout);
+int avd_cl_c1r3_codes_cols(int Cout);
+int avd_cl_c1r3_apply_codes(const void* x, const void* wk, const float* bias, const float* scale,
+                            const float* shift, void* z, unsigned short* codes, int N, int B, int H,
+                            int W, int Cout, void* stream);
+int avd_cl_c1r3_moments_codes(const void* x, const void* wk, const void* gz, const unsigned short* codes,
+                              float* out, int N, int B, int H, int W, int Cout, void* stream);
+int avd_cl_c1r3_codes_combine(const float* moments, const void* wk, const float* bias,
+                              const float* gamma, const float* mean, const float* invstd,
+                              long long count, float* dw, float* dgamma, float* dbeta, float* dbias,
+                              float* coef, int G, int Cout, void* stream);
+
 /* ------------------------------------------------------------------ MX (block-scaled) fp8 convs
  * BASELINE config 5 ("fp8 MFMA conv path"): the mid-layer conv forward AND input gradient of
  * CentralUnimodalImage/Audio (unimodal.py:127-221; the F.conv2d and its autograd dX under the

@@ -107,6 +107,11 @@ PROTOS = {
     "avd_fp8_conv_serves": [I, I, I],
     "avd_fp8_stat_rows": [I, I, I, I, I, I],
     "avd_fp8_conv_fwd": [P, F, P, P, P, P, P, I, I, I, I, I, I, I, I, P],
+    "avd_cl_c1r3_codes_rows": [I, I, I, I, I],
+    "avd_cl_c1r3_codes_cols": [I],
+    "avd_cl_c1r3_apply_codes": [P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "avd_cl_c1r3_moments_codes": [P, P, P, P, P, I, I, I, I, I, P],
+    "avd_cl_c1r3_codes_combine": [P, P, P, P, P, P, L, P, P, P, P, P, I, I, P],
     "avd_mx_weight_bytes": [I, I, I, I],
     "avd_mx_scale_bytes": [I, I, I, I],
     "avd_mx_weight_layout": [P, P, P, I, I, I, I, P],

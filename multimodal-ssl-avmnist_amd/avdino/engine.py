@@ -294,7 +294,13 @@ class ConvBranch:
             return "audio"
         if (ci, co, k, pad) == (1, 32, 5, 2) and ops.c1r5_codes_rows(N, B, H, H) > 0:
             return "image"
+        if (ci, co, k, pad) == (1, 32, 3, 1) and self.CODES3 and ops.c1r3_codes_rows(N, B, H, H) > 0:
+            return "c3"
         return None
+
+    # the 3x3 first layers (SimCLR / unimodal encoders) routed the same way (avd_cl_c1r3_*);
+    # AVDINO_C1R3_CODES=0 keeps the recomputing moments pass (c1r3 pass 4)
+    CODES3 = os.environ.get("AVDINO_C1R3_CODES", "1") == "1"
 
     def _first_layer_recompute_fwd(self, ws, store, tag, ctx, x, N, G, B, update_running,
                                    need_dgrad=True):
@@ -331,6 +337,10 @@ class ConvBranch:
             codes = ws.get(f"{tag}.c1codes", N * Hp * Hp * 8, torch.int16)
             ops.c1r5_apply_codes(x, wk, bias, st[2], st[3], out, codes, N, B, H, H)
             ctx["codes"] = (route, codes)
+        elif route == "c3":
+            codes = ws.get(f"{tag}.c1codes", N * Hp * Hp * co // 4, torch.int16)
+            ops.c1r3_apply_codes(x, wk, bias, st[2], st[3], out, codes, N, B, H, H, co)
+            ctx["codes"] = (route, codes)
         elif pm:
             ops.c1r5_apply_codes(x, wk, bias, st[2], st[3], out, None, N, B, H, H)
         else:
@@ -351,6 +361,16 @@ class ConvBranch:
             # one pass over x, the pooled gradient and the routing codes; a float64 combine forms
             # the BN backward and dW from the moments (avd_cl_c1_codes_combine / c1r5)
             route, codes = ctx["codes"]
+            if route == "c3":
+                Rc, mc = ops.c1r3_codes_rows(N, B, H, H, co), ops.c1r3_codes_cols(co)
+                parts = ws.get("c1_codes_parts", Rc * G * mc)
+                ops.c1r3_moments_codes(x, wk, gout, codes, parts, N, B, H, H, co)
+                mom = ws.get("c1_codes_mom", G * mc)
+                ops.sum_rows(parts, Rc, G * mc, mom)
+                ops.c1r3_codes_combine(mom, wk, bias, store[bk + ".weight"], st[0], st[1], B * Ho * Ho,
+                                       store.grad_of(ck + ".weight"), store.grad_of(bk + ".weight"),
+                                       store.grad_of(bk + ".bias"), store.grad_of(ck + ".bias"), None, G, co)
+                return
             img = route == "image"
             Rc = (ops.c1r5_codes_rows if img else ops.c1_codes_rows)(N, B, H, H)
             mc = ops.c1r5_codes_cols() if img else ops.c1_codes_cols()

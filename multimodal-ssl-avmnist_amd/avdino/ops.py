@@ -672,6 +672,53 @@ def c1_codes_combine(moments, wk, bias, gamma, mean, invstd, count, dw, dgamma, 
          p(dw), p(dgamma), p(dbeta), p(dbias), p(coef), G, stream())
 
 
+# ---- the routed 3x3 first layer (include/avdino.h avd_cl_c1r3_*: SimCLR / unimodal conv1)
+def c1r3_codes_rows(N, B, H, W, Cout=32):
+    """Rows per BN group of avd_cl_c1r3_moments_codes (0 = shape not served)."""
+    return lib.avd_cl_c1r3_codes_rows(N, B, H, W, Cout)
+
+
+def c1r3_codes_cols(Cout=32):
+    return lib.avd_cl_c1r3_codes_cols(Cout)
+
+
+def c1r3_apply_codes(x, wk, bias, scale, shift, z, codes, N, B, H, W, Cout=32):
+    """BN -> ReLU -> 2x2 max-pool of the recomputed 3x3 conv1 output (c1r3 pass 1, same pooled
+    map) plus the routing codes [N, H/2, W/2, Cout/4] (int16 storage of the u16 nibble words)."""
+    npool = N * (H // 2) * (W // 2)
+    _need(c1r3_codes_rows(N, B, H, W, Cout) > 0 and x.numel() == N * H * W and x.dtype == torch.bfloat16,
+          "c1r3 codes shape")
+    _need(z.numel() == npool * Cout and z.dtype == x.dtype, "c1r3 codes z")
+    _need(codes.numel() >= npool * Cout // 4 and codes.element_size() == 2, "c1r3 codes buffer")
+    _timed(f"c1r3_apply_codes[{N}x{H}x{W}x1->{Cout} k3]", x.numel() * 2 + npool * Cout * 2 + npool * Cout // 2,
+           2 * N * H * W * Cout * 9,
+           lambda: call("avd_cl_c1r3_apply_codes", p(x), p(wk), p(bias), p(scale), p(shift), p(z),
+                        p(codes), N, B, H, W, Cout, stream()))
+
+
+def c1r3_moments_codes(x, wk, gz, codes, out, N, B, H, W, Cout=32):
+    """One pass over x, the pooled gradient and the codes -> moment rows [R][G][cols]."""
+    R = c1r3_codes_rows(N, B, H, W, Cout)
+    npool = N * (H // 2) * (W // 2)
+    _need(R > 0 and x.numel() == N * H * W and x.dtype == torch.bfloat16, "c1r3 moments codes shape")
+    _need(gz.numel() == npool * Cout and gz.dtype == x.dtype and codes.numel() >= npool * Cout // 4,
+          "c1r3 moments gz/codes")
+    _need(out.numel() >= R * (N // B) * c1r3_codes_cols(Cout), "c1r3 moments rows")
+    fl = 2 * N * H * W * (Cout * 10 + 10 * 10)
+    _timed(f"c1r3_moments_codes[{N}x{H}x{W}x1->{Cout} k3]",
+           x.numel() * 2 + npool * Cout * 2 + npool * Cout // 2, fl,
+           lambda: call("avd_cl_c1r3_moments_codes", p(x), p(wk), p(gz), p(codes), p(out), N, B, H, W,
+                        Cout, stream()))
+
+
+def c1r3_codes_combine(moments, wk, bias, gamma, mean, invstd, count, dw, dgamma, dbeta, dbias, coef, G,
+                       Cout=32):
+    _need(moments.numel() >= G * c1r3_codes_cols(Cout) and dw.numel() >= Cout * 9 and G <= 32,
+          "c1r3 codes combine")
+    call("avd_cl_c1r3_codes_combine", p(moments), p(wk), p(bias), p(gamma), p(mean), p(invstd),
+         int(count), p(dw), p(dgamma), p(dbeta), p(dbias), p(coef), G, Cout, stream())
+
+
 # ---- the image conv1 backward routed by forward codes (include/avdino.h avd_cl_c1r5_*)
 def c1r5_codes_rows(N, B, H, W):
     """Rows per BN group of avd_cl_c1r5_moments_codes (0 = shape not served)."""

@@ -327,13 +327,15 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C, K)) void c1r3_kernel(
     const float* __restrict__ scale, const float* __restrict__ shift,
     const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ coef, const bf16* __restrict__ gz, bf16* __restrict__ z,
-    float* __restrict__ out, int N, int B, int H, int W) {
+    float* __restrict__ out, int N, int B, int H, int W, unsigned short* __restrict__ codes) {
   constexpr int NT = C / 16;
   constexpr int DYS = C == 16 ? 16 : C + 16;
   constexpr int KK = K * K, PADK = K / 2, NTAP = c1r3_ntap(K), XSK = 16 * NTAP;
   constexpr bool GZ = P >= 2;
   constexpr bool RED = P == 2 || P == 4;            // BN-backward partial sums
   constexpr bool WG = P >= 3;                       // im2col tile + weight-gradient MFMAs
+  constexpr bool MOM = P == 4 || P == 5;            // moments: the ones tap and the Gram tiles
+  constexpr bool ROUTED = P == 5;                   // dz from the forward's routing codes
   extern __shared__ __attribute__((aligned(16))) bf16 sm[];
   constexpr int NGZ = TR == TRW ? NT : 4;          // pooled-gradient vectors per thread
   const int WV = (W + 7) & ~7;                      // virtual width (groups of 8 columns)
@@ -343,9 +345,11 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C, K)) void c1r3_kernel(
   const int XB = (TR + K - 1) * XS;                 // one xr buffer
   const int Hp = H / 2, Wp = W / 2;
   const int GB = (TR / 2) * Wp * C;                 // one gz buffer (a tile's pooled gradient)
+  const int CB = ROUTED ? (TR / 2) * Wp * (C / 4) : 0;   // one codes buffer (u16 per 4 channels)
   bf16* xr = sm;                                    // [2][TR + K - 1][XS]
   bf16* gzs = xr + 2 * XB;                          // [2][GB]
-  bf16* xk = gzs + (GZ ? 2 * GB : 0);               // [TP][XSK] (passes 3, 4)
+  unsigned short* cds = reinterpret_cast<unsigned short*>(gzs + (GZ ? 2 * GB : 0));   // [2][CB]
+  bf16* xk = reinterpret_cast<bf16*>(cds + 2 * CB); // [TP][XSK] (passes 3-5)
   bf16* dys = xk + TP * XSK;                        // [TP][DYS] (passes 3, 4)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -381,6 +385,7 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C, K)) void c1r3_kernel(
   const int xrow = tid / cpr, xcol = tid - xrow * cpr;
   u4 xv = u4{0u, 0u, 0u, 0u};
   u4 gv4[NGZ];
+  u4 cv4 = u4{0u, 0u, 0u, 0u};                      // routed pass: one codes vector per thread
   auto load = [&](int tl) {
     const int n = tl / tps, y0 = (tl - n * tps) * TR;
     const int iy = y0 - PADK + xrow;
@@ -401,6 +406,9 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C, K)) void c1r3_kernel(
         if (8 * e < GB) gv4[j] = *reinterpret_cast<const u4*>(gb + 8 * e);
       }
     }
+    if constexpr (ROUTED) {
+      if (8 * tid < CB) cv4 = *reinterpret_cast<const u4*>(codes + ((size_t)n * Hp + y0 / 2) * Wp * (C / 4) + 8 * tid);
+    }
   };
   auto put = [&](int buf) {
     if (tid < nxv) {
@@ -414,6 +422,9 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C, K)) void c1r3_kernel(
         const int e = tid + 256 * j;
         if (8 * e < GB) *reinterpret_cast<u4*>(gzs + buf * GB + 8 * e) = gv4[j];
       }
+    }
+    if constexpr (ROUTED) {
+      if (8 * tid < CB) *reinterpret_cast<u4*>(cds + buf * CB + 8 * tid) = cv4;
     }
   };
 
@@ -435,7 +446,28 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C, K)) void c1r3_kernel(
   f4 acc3[NT][NTAP], gacc[NG];
   const int WSZ = C * KK + KK * (KK + 1);           // pass 4 moments per (row, group)
   float* wmo = out + (size_t)C * G * R * 2;         // pass 4: [R][G][WSZ] after the sums
+  constexpr int MOMR = C * KK + KK * KK + KK + C;   // routed pass: M | Gram | S | sum dz
   auto flush = [&](int gp) {
+    if constexpr (ROUTED) {
+      float* o = out + ((size_t)srow * G + gp) * MOMR;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = 16 * t + 4 * g + i;
+          if (r16 < KK) o[c * KK + r16] = acc3[t][0][i];
+          else if (r16 == KK) o[C * KK + KK * KK + KK + c] = acc3[t][0][i];   // ones tap: sum dz
+          acc3[t][0][i] = 0.f;
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int a = 4 * g + i, c = r16;
+        if (a < KK && c < KK) o[C * KK + a * KK + c] = gacc[0][i];
+        else if (a < KK && c == KK) o[C * KK + KK * KK + a] = gacc[0][i];          // S
+        gacc[0][i] = 0.f;
+      }
+      return;
+    }
     if constexpr (P == 4) {
       // this wave's moments of group gp: sum dz xk [C][KK], then the Gram rows of xk
       // [KK][KK + 1] (column KK is the ones tap: sum xk); the lower tile (1,0) by symmetry
@@ -501,7 +533,7 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C, K)) void c1r3_kernel(
 
   for (int ti = t0; ti < t1; ++ti) {
     const int n = ti / tps, y0 = (ti - n * tps) * TR, gb = n / B, buf = ti & 1;
-    if constexpr (P == 0 || RED) {
+    if constexpr (P == 0 || RED || ROUTED) {
       const int gi = ti / tilesPG;
       if (gi != cur_g) {
         if (cur_g >= 0) flush(cur_g);
@@ -509,7 +541,7 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C, K)) void c1r3_kernel(
         zero_run();
       }
     }
-    if constexpr (P != 0) {
+    if constexpr (P != 0 && !ROUTED) {
       if (gb != cg) {
         cg = gb;
 #pragma unroll
@@ -544,7 +576,7 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C, K)) void c1r3_kernel(
 #pragma unroll
           for (int k = 0; k < XSK / 2; ++k) w8[k] = 0u;
           if (c < W) {
-            if constexpr (P == 4) w8[KK >> 1] = (KK & 1) ? 0x3F800000u : 0x3F80u;   // bf16 1.0 at tap KK
+            if constexpr (MOM) w8[KK >> 1] = (KK & 1) ? 0x3F800000u : 0x3F80u;   // bf16 1.0 at tap KK
 #pragma unroll
             for (int t = 0; t < KK; ++t) {
               const uint32_t b = __builtin_bit_cast(uint16_t, xb[(r0 + r + t / K) * XS + RXO - PADK + c + t % K]);
@@ -571,6 +603,24 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C, K)) void c1r3_kernel(
         else btaps<K, 3>(bs, xp, XS);
         const bf16x8 bx = __builtin_bit_cast(bf16x8, bs);
         const int wg = wvld ? (gr * Wp + 4 * gc8) * C + wlane : 0;     // window (lane part in wlane)
+        if constexpr (ROUTED) {
+          // dz = the pooled gradient at the window position the forward's code names (nibble =
+          // 1 + first argmax of relu(bn(y)) when > 0, else 0), 0 at the window's other pixels
+          const int win = wvld ? gr * Wp + 4 * gc8 + wcol : 0;
+          const unsigned me = 2u * (unsigned)e8 + (unsigned)e1 + 1u;
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            const uint2 gw = *reinterpret_cast<const uint2*>(gzt + wg + 16 * t);
+            const unsigned cw = cds[buf * CB + win * (C / 4) + 4 * t + g];
+            const unsigned gb4[4] = {gw.x & 0xffffu, gw.x >> 16, gw.y & 0xffffu, gw.y >> 16};
+            unsigned d[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) d[i] = (vld && ((cw >> (4 * i)) & 0xFu) == me) ? gb4[i] : 0u;
+            *reinterpret_cast<uint2*>(dys + (2 * grl * WV + 8 * gc8 + plane) * DYS + 16 * t + 4 * g) =
+                make_uint2(d[0] | (d[1] << 16), d[2] | (d[3] << 16));
+          }
+          continue;
+        }
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[t], bx, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
@@ -605,6 +655,29 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C, K)) void c1r3_kernel(
             }
             if (mn == 0 && wvld)
               *reinterpret_cast<uint2*>(z + zt + wg + 16 * t) = make_uint2(m[0], m[1]);
+            if (codes) {
+              // routing codes for the backward: this lane's position (1 + k) where it is the
+              // window's first argmax of bn(y) and > 0 (the tie rule of passes 2-4 below), OR-ed
+              // over the window's four lanes
+              unsigned cw = 0u;
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                const f2 v = __builtin_elementwise_fma(y2[h], sc2[t][h], sf2[t][h]);
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                  const int vi = __float_as_int(v[e]);
+                  const int u1 = dppi<0xB1>(vi) + e1, u8 = dppi<0x128>(vi) + e8,
+                            u9 = dppi<0x128>(dppi<0xB1>(vi)) + e8;
+                  const int thr = max(max(u1, u8), max(u9, 1));
+                  cw |= (vi >= thr ? 2u * (unsigned)e8 + (unsigned)e1 + 1u : 0u) << (4 * (2 * h + e));
+                }
+              }
+              cw |= (unsigned)dppi<0xB1>((int)cw);
+              cw |= (unsigned)dppi<0x128>((int)cw);
+              if (mn == 0 && wvld)
+                codes[((size_t)n * Hp + y0 / 2 + gr) * Wp * (C / 4) + (4 * gc8 + wcol) * (C / 4) + 4 * t + g] =
+                    (unsigned short)cw;
+            }
           } else {
             // first argmax of the window (k order (0,0),(0,1),(1,0),(1,1); lane L^m holds
             // k = 2 (m >> 3) + (m & 1)) on bn(y) as signed ints: ordered like the floats wherever
@@ -667,7 +740,7 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C, K)) void c1r3_kernel(
               acc3[t][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bvv[nt], acc3[t][nt], 0, 0, 0);
           }
           // the same fragments are the A operands of the im2col Gram matrix (rows: taps, k: pixels)
-          if constexpr (P == 4) {
+          if constexpr (MOM) {
             gacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bvv[0], bvv[0], gacc[0], 0, 0, 0);
             if constexpr (NTAP == 2) {
               gacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bvv[0], bvv[NTAP - 1], gacc[1], 0, 0, 0);
@@ -679,7 +752,7 @@ __global__ __launch_bounds__(256, c1r3_bpc(P, C, K)) void c1r3_kernel(
     }
   }
 
-  if constexpr (P == 0 || RED) {
+  if constexpr (P == 0 || RED || ROUTED) {
     if (cur_g >= 0) flush(cur_g);
     const int first = t0 < t1 ? t0 / tilesPG : 0, last = t0 < t1 ? (t1 - 1) / tilesPG : -1;
     zero_run();
@@ -714,7 +787,7 @@ size_t c1r3_lds(int P, int C, int W, int K, int TR) {
   const int WV = (W + 7) & ~7;
   const size_t XB = (size_t)(TR + K - 1) * (WV + 2 * RXO);
   const size_t GB = P >= 2 ? (size_t)(TR / 2) * (W / 2) * C : 0;
-  size_t e = 2 * XB + 2 * GB;
+  size_t e = 2 * XB + 2 * GB + (P == 5 ? 2 * (size_t)(TR / 2) * (W / 2) * (C / 4) : 0);
   const int XSK = 16 * c1r3_ntap(K);
   if (P >= 3) {
     const int DYS = C == 16 ? 16 : C + 16;
@@ -752,9 +825,126 @@ __global__ void c1r3_combine_kernel(const float* __restrict__ m, const float* __
   dw[e] = (float)acc;
 }
 
+// BN backward + dW of a routed 3x3 first layer from the row-summed moments m [G][C*KK + KK*KK + KK
+// + C] (M | Gram | S | sum dz) of pass 5, in float64 -- the c1r5 combine (c1r5.hip) for KK taps:
+//   sum dz y = w . M + b sum dz;  sum dz xhat = (sum dz y - mean sum dz) invstd;
+//   coef (k1, kx, k0) as avd_bn_bwd_finalize;  dW[c][t] = sum_g k1 M + kx (w Gram + b S) + k0 S;
+//   dgamma / dbeta / dbias (= sum dy) summed over the groups.
+constexpr int C1R3_GMAX = 32;
+template <int C, int KK>
+__global__ __launch_bounds__(256) void c1r3_codes_combine_kernel(
+    const float* __restrict__ m, const bf16* __restrict__ wk, const float* __restrict__ bias,
+    const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
+    long long count, float* __restrict__ dw, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    float* __restrict__ dbias, float* __restrict__ coef, int G) {
+  constexpr int MOM = C * KK + KK * KK + KK + C;
+  __shared__ double sk[C1R3_GMAX * C][3];
+  __shared__ double s12[C1R3_GMAX * C][2];
+  const int tid = threadIdx.x;
+  const double n = (double)count;
+  for (int i = tid; i < G * C; i += 256) {
+    const int gq = i / C, c = i - gq * C;
+    const float* mg = m + (size_t)gq * MOM;
+    const double b = bias ? (double)bias[c] : 0.0;
+    const double s1 = mg[C * KK + KK * KK + KK + c];
+    double sy = b * s1;
+    for (int t = 0; t < KK; ++t) sy = fma((double)bf2f(wk[c * 32 + t]), (double)mg[c * KK + t], sy);
+    const double mu = mean[gq * C + c], is = invstd[gq * C + c], ga = gamma[c];
+    const double s2 = (sy - mu * s1) * is;
+    const double k1 = ga * is, kx = -ga * is * is * s2 / n, k0 = -ga * is * s1 / n + ga * is * is * mu * s2 / n;
+    sk[i][0] = k1; sk[i][1] = kx; sk[i][2] = k0;
+    s12[i][0] = s1; s12[i][1] = s2;
+    if (coef) {
+      coef[i * 3 + 0] = (float)k1;
+      coef[i * 3 + 1] = (float)kx;
+      coef[i * 3 + 2] = (float)k0;
+    }
+  }
+  __syncthreads();
+  if (tid < C) {
+    double dg = 0.0, db = 0.0, dbi = 0.0;
+    for (int gq = 0; gq < G; ++gq) {
+      const int i = gq * C + tid;
+      const double mu = mean[i];
+      dg += s12[i][1];
+      db += s12[i][0];
+      dbi += sk[i][0] * s12[i][0] + sk[i][1] * mu * n + sk[i][2] * n;
+    }
+    if (dgamma) dgamma[tid] = (float)dg;
+    if (dbeta) dbeta[tid] = (float)db;
+    if (dbias) dbias[tid] = (float)dbi;
+  }
+  for (int e = tid; e < C * KK; e += 256) {
+    const int c = e / KK, t = e - c * KK;
+    double wr[KK];
+#pragma unroll
+    for (int k = 0; k < KK; ++k) wr[k] = (double)bf2f(wk[c * 32 + k]);
+    const double b = bias ? (double)bias[c] : 0.0;
+    double acc = 0.0;
+    for (int gq = 0; gq < G; ++gq) {
+      const float* mg = m + (size_t)gq * MOM;
+      const float* gram = mg + C * KK;
+      const double sx = gram[KK * KK + t];
+      double sy = b * sx;
+#pragma unroll
+      for (int k = 0; k < KK; ++k) sy = fma(wr[k], (double)gram[k * KK + t], sy);
+      const int i = gq * C + c;
+      acc += sk[i][0] * mg[e] + sk[i][1] * sy + sk[i][2] * sx;
+    }
+    dw[e] = (float)acc;
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int avd_c1r3_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad);
+int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, const float* scale,
+                    const float* shift, const float* mean, const float* invstd, const float* coef,
+                    const void* gz, void* z, float* out, int N, int B, int H, int W, int Cout, int K,
+                    hipStream_t st, unsigned short* codes);
+
+// ---- the routed 3x3 first layer (1 -> 32, pad 1: the SimCLR / unimodal encoders' conv1,
+// dino.py:18-73): the forward's pass 1 writes routing codes (one nibble per pooling window and
+// channel, u16 per 4 channels: [N][H/2][W/2][C/4]), the backward is pass 5 (moments from x, the
+// pooled gradient and the codes; no y, no BN coefficients) + the float64 combine.
+int avd_cl_c1r3_codes_rows(int N, int B, int H, int W, int Cout) {
+  if (Cout != 32 || B <= 0 || N % B || N / B > C1R3_GMAX) return 0;
+  if (!avd_c1r3_rows(4, AVD_BF16, N, B, 1, H, W, Cout, 3, 1)) return 0;
+  return 4 * c1r3_grid(5, Cout, 3);
+}
+
+int avd_cl_c1r3_codes_cols(int Cout) { return Cout * 9 + 81 + 9 + Cout; }
+
+int avd_cl_c1r3_apply_codes(const void* x, const void* wk, const float* bias, const float* scale,
+                            const float* shift, void* z, unsigned short* codes, int N, int B, int H,
+                            int W, int Cout, void* stream) {
+  if (!x || !wk || !scale || !shift || !z || !codes) return AVD_ERR_ARG;
+  if (!avd_cl_c1r3_codes_rows(N, B, H, W, Cout)) return AVD_ERR_SHAPE;
+  return avd_c1r3_launch(1, x, wk, bias, scale, shift, nullptr, nullptr, nullptr, nullptr, z, nullptr,
+                         N, B, H, W, Cout, 3, avd_stream(stream), codes);
+}
+
+int avd_cl_c1r3_moments_codes(const void* x, const void* wk, const void* gz, const unsigned short* codes,
+                              float* out, int N, int B, int H, int W, int Cout, void* stream) {
+  if (!x || !wk || !gz || !codes || !out) return AVD_ERR_ARG;
+  if (!avd_cl_c1r3_codes_rows(N, B, H, W, Cout)) return AVD_ERR_SHAPE;
+  return avd_c1r3_launch(5, x, wk, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, gz, nullptr, out,
+                         N, B, H, W, Cout, 3, avd_stream(stream), const_cast<unsigned short*>(codes));
+}
+
+int avd_cl_c1r3_codes_combine(const float* moments, const void* wk, const float* bias,
+                              const float* gamma, const float* mean, const float* invstd,
+                              long long count, float* dw, float* dgamma, float* dbeta, float* dbias,
+                              float* coef, int G, int Cout, void* stream) {
+  if (!moments || !wk || !gamma || !mean || !invstd || !dw) return AVD_ERR_ARG;
+  if (G <= 0 || G > C1R3_GMAX || count <= 1 || Cout != 32) return AVD_ERR_SHAPE;
+  c1r3_codes_combine_kernel<32, 9><<<1, 256, 0, avd_stream(stream)>>>(
+      moments, (const bf16*)wk, bias, gamma, mean, invstd, count, dw, dgamma, dbeta, dbias, coef, G);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
 
 // rows / slabs of a recompute pass for a Cin-1 first layer, 3x3 pad 1 or 5x5 pad 2 (0: not served)
 int avd_c1r3_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad) {
@@ -781,7 +971,7 @@ int avd_c1r3_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cou
 int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, const float* scale,
                     const float* shift, const float* mean, const float* invstd, const float* coef,
                     const void* gz, void* z, float* out, int N, int B, int H, int W, int Cout, int K,
-                    hipStream_t st) {
+                    hipStream_t st, unsigned short* codes) {
   const int grid = c1r3_grid(pass, Cout, K);
   const int TR = c1r3_tr(H, W);
   const size_t lds = c1r3_lds(pass, Cout, W, K, TR);
@@ -789,11 +979,12 @@ int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, 
   if (pass == P_ && Cout == C_ && K == K_ && TR == TR_)                                        \
     c1r3_kernel<P_, C_, K_, TR_><<<grid, 256, lds, st>>>((const bf16*)x, (const bf16*)wk, bias,   \
                                                          scale, shift, mean, invstd, coef,      \
-                                                         (const bf16*)gz, (bf16*)z, out, N, B, H, W);
+                                                         (const bf16*)gz, (bf16*)z, out, N, B, H, W, codes);
 #define AVD_PC(C_, K_, TR_) AVD_P(0, C_, K_, TR_) else AVD_P(1, C_, K_, TR_) else AVD_P(2, C_, K_, TR_) \
   else AVD_P(3, C_, K_, TR_) else AVD_P(4, C_, K_, TR_)
   AVD_PC(16, 3, 4) else AVD_PC(32, 3, 4) else AVD_PC(64, 3, 4) else AVD_PC(32, 5, 4)
-  else AVD_PC(16, 3, 28) else AVD_PC(32, 3, 28) else AVD_PC(32, 5, 28) else return AVD_ERR_SHAPE;
+  else AVD_PC(16, 3, 28) else AVD_PC(32, 3, 28) else AVD_PC(32, 5, 28)
+  else AVD_P(5, 32, 3, 4) else AVD_P(5, 32, 3, 28) else return AVD_ERR_SHAPE;
 #undef AVD_PC
 #undef AVD_P
   AVD_CHECK_LAUNCH();

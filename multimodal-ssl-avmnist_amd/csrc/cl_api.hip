@@ -167,7 +167,7 @@ int avd_c1r3_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cou
 int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, const float* scale,
                     const float* shift, const float* mean, const float* invstd, const float* coef,
                     const void* gz, void* z, float* out, int N, int B, int H, int W, int Cout, int K,
-                    hipStream_t st);
+                    hipStream_t st, unsigned short* codes = nullptr);
 
 int avd_c1r3_combine(const float* m, const float* coef, const void* wk, const float* bias,
                      float* dw, int G, int Cout, int K, hipStream_t st);
