@@ -9,8 +9,10 @@ avd_cl_c1r3_codes_combine), at config 4's size (N = 2048 per tower call) and sma
   (first max of relu(bn(y)) of the stored bf16 y, only a positive max routes);
 * dW, dgamma, dbeta and the BN-backward coefficients within 1e-5 / 1e-6 of the float64 formulas,
   and dW within 3e-3 of the recomputing moments pass (c1r3 pass 4, whose BN sums are f32);
-* in the engine, a SimCLR audio/audio step with the routed backward equals the recomputing one
-  (loss bit for bit, every gradient outside the first layers bit for bit, first layers 1e-4)."""
+* in the engine, a SimCLR audio/audio step with the routed backward equals the recomputing one:
+  loss and every gradient outside the first layers bit for bit; the first layers' within 5e-3
+  (the recomputing pass forms its BN-backward sums in f32: 2-3e-3 from float64 above, the
+  routed one 1e-5)."""
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -142,6 +144,6 @@ def test_simclr_step_routed_first_layer_equals_recomputing(monkeypatch):
     for k in s0.live_keys:
         a, b = s0.grad_of(k), s1.grad_of(k)
         if k in first:
-            assert grel(b, a) < 1e-4 or a.abs().max() < 1e-6, (k, grel(b, a))
+            assert grel(b, a) < 5e-3 or a.abs().max() < 1e-6, (k, grel(b, a))
         else:
             assert torch.equal(a, b), k
