@@ -627,6 +627,30 @@ int avd_fp8_conv_fwd(const void* x, float xscale, const void* wq, const float* w
                      const float* bias, void* y, float* stats, int N, int B, int Cin, int H,
                      int W, int Cout, int K, int pad, void* stream);
 
+/* ------------------------------------------------------------------ audio conv1 from its patch Gram
+ * The audio conv1 (CentralUnimodalAudio conv1: Conv2d(1, 8, 5, padding=2) on 112x112, bf16) has
+ * Cin = 1, so y = w . x25 + b and its BatchNorm statistics follow exactly from the
+ * weight-independent patch sums S = sum x25 and Gram = sum x25 x25^T per BN group:
+ *   sum y = w . S + n b,   sum y^2 = w^T Gram w + 2 b w . S + n b^2.
+ * avd_cl_c1_gram forms [avd_cl_c1_codes_rows][G][avd_cl_c1_gram_cols] partials (Gram 25x25 | S
+ * 25; sum them with avd_sum_rows) in one MFMA pass over x -- no y, no per-element statistics;
+ * avd_cl_c1_gram_finalize turns the row sums into avd_bn_finalize's outputs in float64 (mean,
+ * invstd, BN scale / shift, running statistics in group order).  The routed backward then needs
+ * no Gram of its own: avd_cl_c1_moments_codes_ng forms M and sum dz only (MOMC layout, Gram / S
+ * slots zero) and avd_cl_c1_codes_combine_gram reads the forward's Gram. */
+int avd_cl_c1_gram_cols(void);
+int avd_cl_c1_gram(const void* x, float* out, int N, int B, int H, int W, void* stream);
+int avd_cl_c1_gram_finalize(const float* gram, const void* wk, const float* bias, const float* gamma,
+                            const float* beta, long long count, float eps, float momentum,
+                            float* mean, float* invstd, float* scale, float* shift,
+                            float* running_mean, float* running_var, int G, void* stream);
+int avd_cl_c1_moments_codes_ng(const void* x, const void* gz, const unsigned* codes, float* out,
+                               int N, int B, int H, int W, void* stream);
+int avd_cl_c1_codes_combine_gram(const float* moments, const float* gram, const void* wk,
+                                 const float* bias, const float* gamma, const float* mean,
+                                 const float* invstd, long long count, float* dw, float* dgamma,
+                                 float* dbeta, float* dbias, float* coef, int G, void* stream);
+
 /* ------------------------------------------------------------------ routed 3x3 first layer
  * The SimCLR / unimodal encoders' conv1 (audio_encoder / image_encoder, dino.py:18-73:
  * Conv2d(1, 32, 3, padding=1) -> BN2d -> ReLU -> MaxPool2d on 112x112 / 28x28, bf16) without a

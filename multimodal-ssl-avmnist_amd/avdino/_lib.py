@@ -107,6 +107,11 @@ PROTOS = {
     "avd_fp8_conv_serves": [I, I, I],
     "avd_fp8_stat_rows": [I, I, I, I, I, I],
     "avd_fp8_conv_fwd": [P, F, P, P, P, P, P, I, I, I, I, I, I, I, I, P],
+    "avd_cl_c1_gram_cols": [],
+    "avd_cl_c1_gram": [P, P, I, I, I, I, P],
+    "avd_cl_c1_gram_finalize": [P, P, P, P, P, L, F, F, P, P, P, P, P, P, I, P],
+    "avd_cl_c1_moments_codes_ng": [P, P, P, P, I, I, I, I, P],
+    "avd_cl_c1_codes_combine_gram": [P, P, P, P, P, P, P, L, P, P, P, P, P, I, P],
     "avd_cl_c1r3_codes_rows": [I, I, I, I, I],
     "avd_cl_c1r3_codes_cols": [I],
     "avd_cl_c1r3_apply_codes": [P, P, P, P, P, P, P, I, I, I, I, I, P],

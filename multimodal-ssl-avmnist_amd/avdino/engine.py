@@ -302,6 +302,16 @@ class ConvBranch:
     # AVDINO_C1R3_CODES=0 keeps the recomputing moments pass (c1r3 pass 4)
     CODES3 = os.environ.get("AVDINO_C1R3_CODES", "1") == "1"
 
+    # the audio conv1's BN statistics from its patch Gram matrix (avd_cl_c1_gram) instead of a
+    # recomputing statistics pass; AVDINO_C1_GRAM=0 restores the latter
+    GRAM = os.environ.get("AVDINO_C1_GRAM", "1") == "1"
+
+    def _gram_ok(self, N, B):
+        ci, co, k, pad = self.stack.convs[0]
+        H = self.dims[0][0]
+        return (self.GRAM and (ci, co, k, pad) == (1, 8, 5, 2) and self.act == torch.bfloat16
+                and ops.c1_codes_rows(N, B, H, H) > 0)
+
     def _first_layer_recompute_fwd(self, ws, store, tag, ctx, x, N, G, B, update_running,
                                    need_dgrad=True):
         ci, co, k, pad = self.stack.convs[0]
@@ -309,20 +319,32 @@ class ConvBranch:
         wk = ctx["wts"][0][0]
         bias = store[self.stack.conv_keys[0] + ".bias"]
         pm = self._pixel_major(N, B)
-        if pm:
-            R = ops.c1r5_stats_rows(N, B, H, H)
-            parts = ws.get("stat_parts", co * G * R * 2)
-            ops.c1r5_stats(x, wk, bias, parts, N, B, H, H)
-        else:
-            R = ops.cl_c1_recompute_rows(ops.C1_STATS, self.act, N, B, ci, H, H, co, k, pad)
-            parts = ws.get("stat_parts", co * G * R * 2)
-            ops.cl_c1_recompute(ops.C1_STATS, x, wk, bias, N, B, ci, H, H, co, k, pad, out=parts)
         st = ws.get(f"{tag}.bn0", 4 * G * co).view(4, G * co)
         bk = self.stack.bn_keys[0]
-        ops.bn_finalize(parts, G, R, co, B * Ho * Ho, store[bk + ".weight"], store[bk + ".bias"],
-                        st[0], st[1], st[2], st[3],
-                        store[bk + ".running_mean"] if update_running else None,
-                        store[bk + ".running_var"] if update_running else None)
+        rm = store[bk + ".running_mean"] if update_running else None
+        rv = store[bk + ".running_var"] if update_running else None
+        if self._gram_ok(N, B):
+            # statistics of y = w . x25 + b from the patch Gram (one MFMA pass over x, no y);
+            # the routed backward reuses the Gram
+            R, gc = ops.c1_codes_rows(N, B, H, H), ops.c1_gram_cols()
+            gparts = ws.get("c1_gram_parts", R * G * gc)
+            ops.c1_gram(x, gparts, N, B, H, H)
+            gram = ws.get(f"{tag}.c1gram", G * gc)
+            ops.sum_rows(gparts, R, G * gc, gram)
+            ops.c1_gram_finalize(gram, wk, bias, store[bk + ".weight"], store[bk + ".bias"], B * Ho * Ho,
+                                 st[0], st[1], st[2], st[3], rm, rv, G)
+            ctx["gram"] = gram
+        else:
+            if pm:
+                R = ops.c1r5_stats_rows(N, B, H, H)
+                parts = ws.get("stat_parts", co * G * R * 2)
+                ops.c1r5_stats(x, wk, bias, parts, N, B, H, H)
+            else:
+                R = ops.cl_c1_recompute_rows(ops.C1_STATS, self.act, N, B, ci, H, H, co, k, pad)
+                parts = ws.get("stat_parts", co * G * R * 2)
+                ops.cl_c1_recompute(ops.C1_STATS, x, wk, bias, N, B, ci, H, H, co, k, pad, out=parts)
+            ops.bn_finalize(parts, G, R, co, B * Ho * Ho, store[bk + ".weight"], store[bk + ".bias"],
+                            st[0], st[1], st[2], st[3], rm, rv)
         if update_running:
             store.bump_nbt(bk + ".num_batches_tracked", G)
         out = ws.get(f"{tag}.x1", N * Hp * Hp * co, self.act)
@@ -361,6 +383,18 @@ class ConvBranch:
             # one pass over x, the pooled gradient and the routing codes; a float64 combine forms
             # the BN backward and dW from the moments (avd_cl_c1_codes_combine / c1r5)
             route, codes = ctx["codes"]
+            if route == "audio" and ctx.get("gram") is not None:
+                # M and sum dz only; the Gram / S are the forward statistics pass's
+                Rc, mc = ops.c1_codes_rows(N, B, H, H), ops.c1_codes_cols()
+                parts = ws.get("c1_codes_parts", Rc * G * mc)
+                ops.c1_moments_codes_ng(x, gout, codes, parts, N, B, H, H)
+                mom = ws.get("c1_codes_mom", G * mc)
+                ops.sum_rows(parts, Rc, G * mc, mom)
+                ops.c1_codes_combine_gram(mom, ctx["gram"], wk, bias, store[bk + ".weight"], st[0], st[1],
+                                          B * Ho * Ho, store.grad_of(ck + ".weight"),
+                                          store.grad_of(bk + ".weight"), store.grad_of(bk + ".bias"),
+                                          store.grad_of(ck + ".bias"), None, G)
+                return
             if route == "c3":
                 Rc, mc = ops.c1r3_codes_rows(N, B, H, H, co), ops.c1r3_codes_cols(co)
                 parts = ws.get("c1_codes_parts", Rc * G * mc)

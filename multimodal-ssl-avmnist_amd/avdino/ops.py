@@ -672,6 +672,46 @@ def c1_codes_combine(moments, wk, bias, gamma, mean, invstd, count, dw, dgamma, 
          p(dw), p(dgamma), p(dbeta), p(dbias), p(coef), G, stream())
 
 
+# ---- the audio conv1's statistics from its patch Gram (include/avdino.h avd_cl_c1_gram*)
+def c1_gram_cols():
+    return lib.avd_cl_c1_gram_cols()
+
+
+def c1_gram(x, out, N, B, H, W):
+    """Patch Gram + sums rows [R][G][650] of the audio conv1 input (R = c1_codes_rows)."""
+    R = c1_codes_rows(N, B, H, W)
+    _need(R > 0 and x.numel() == N * H * W and x.dtype == torch.bfloat16, "c1 gram shape")
+    _need(out.numel() >= R * (N // B) * c1_gram_cols(), "c1 gram rows")
+    _timed(f"c1_gram[{N}x{H}x{W}x1 k5]", x.numel() * 2, 2 * N * H * W * 26 * 26,
+           lambda: call("avd_cl_c1_gram", p(x), p(out), N, B, H, W, stream()))
+
+
+def c1_gram_finalize(gram, wk, bias, gamma, beta, count, mean, invstd, scale, shift, rm=None, rv=None,
+                     G=1, eps=1e-5, momentum=0.1):
+    _need(gram.numel() >= G * c1_gram_cols(), "c1 gram finalize")
+    call("avd_cl_c1_gram_finalize", p(gram), p(wk), p(bias), p(gamma), p(beta), int(count), eps, momentum,
+         p(mean), p(invstd), p(scale), p(shift), p(rm), p(rv), G, stream())
+
+
+def c1_moments_codes_ng(x, gz, codes, out, N, B, H, W):
+    """The routed backward's M and sum dz only (MOMC rows, Gram / S slots zero)."""
+    R = c1_codes_rows(N, B, H, W)
+    npool = N * (H // 2) * (W // 2)
+    _need(R > 0 and x.numel() == N * H * W and x.dtype == torch.bfloat16, "c1 moments ng shape")
+    _need(gz.numel() == npool * 8 and gz.dtype == x.dtype and codes.numel() >= npool, "c1 moments ng gz/codes")
+    _need(out.numel() >= R * (N // B) * c1_codes_cols(), "c1 moments ng rows")
+    _timed(f"c1_moments_codes_ng[{N}x{H}x{W}x1->8 k5]", x.numel() * 2 + npool * 20, 2 * N * H * W * 8 * 26,
+           lambda: call("avd_cl_c1_moments_codes_ng", p(x), p(gz), p(codes), p(out), N, B, H, W, stream()))
+
+
+def c1_codes_combine_gram(moments, gram, wk, bias, gamma, mean, invstd, count, dw, dgamma, dbeta, dbias,
+                          coef, G):
+    _need(moments.numel() >= G * c1_codes_cols() and gram.numel() >= G * c1_gram_cols() and dw.numel() >= 200,
+          "c1 codes combine gram")
+    call("avd_cl_c1_codes_combine_gram", p(moments), p(gram), p(wk), p(bias), p(gamma), p(mean), p(invstd),
+         int(count), p(dw), p(dgamma), p(dbeta), p(dbias), p(coef), G, stream())
+
+
 # ---- the routed 3x3 first layer (include/avdino.h avd_cl_c1r3_*: SimCLR / unimodal conv1)
 def c1r3_codes_rows(N, B, H, W, Cout=32):
     """Rows per BN group of avd_cl_c1r3_moments_codes (0 = shape not served)."""

@@ -47,7 +47,16 @@ int avd_c1_moments_codes_launch(const void* x, const void* gz, const unsigned* c
 int avd_c1_codes_combine_launch(const float* m, const void* wk, const float* bias,
                                 const float* gamma, const float* mean, const float* invstd,
                                 long long count, float* dw, float* dgamma, float* dbeta,
-                                float* dbias, float* coef, int G, hipStream_t st);
+                                float* dbias, float* coef, int G, hipStream_t st,
+                                const float* gram = nullptr);
+int avd_c1_gram_launch(const void* x, float* out, int N, int B, int H, int W, hipStream_t st);
+int avd_c1_moments_nogram_launch(const void* x, const void* gz, const unsigned* codes, float* out,
+                                 int N, int B, int H, int W, hipStream_t st);
+int avd_c1_gram_cols();
+int avd_c1_gram_finalize_launch(const float* gram, const void* wk, const float* bias,
+                                const float* gamma, const float* beta, float eps, float momentum,
+                                long long count, float* mean, float* invstd, float* scale,
+                                float* shift, float* rm, float* rv, int G, hipStream_t st);
 
 int avd_c1r_rows(int pass, int N, int B, int H);
 int avd_c1p8_moment_cols();
@@ -247,6 +256,42 @@ int avd_cl_c1_codes_combine(const float* moments, const void* wk, const float* b
   if (G <= 0 || count <= 1) return AVD_ERR_SHAPE;
   return avd_c1_codes_combine_launch(moments, wk, bias, gamma, mean, invstd, count, dw, dgamma,
                                      dbeta, dbias, coef, G, avd_stream(stream));
+}
+
+// the audio conv1's statistics from its patch Gram matrix (include/avdino.h)
+int avd_cl_c1_gram_cols(void) { return avd_c1_gram_cols(); }
+
+int avd_cl_c1_gram(const void* x, float* out, int N, int B, int H, int W, void* stream) {
+  if (!x || !out) return AVD_ERR_ARG;
+  if (!c1_codes_shape(N, B, H, W)) return AVD_ERR_SHAPE;
+  return avd_c1_gram_launch(x, out, N, B, H, W, avd_stream(stream));
+}
+
+int avd_cl_c1_gram_finalize(const float* gram, const void* wk, const float* bias, const float* gamma,
+                            const float* beta, long long count, float eps, float momentum,
+                            float* mean, float* invstd, float* scale, float* shift,
+                            float* running_mean, float* running_var, int G, void* stream) {
+  if (!gram || !wk || !gamma || !beta || !mean || !invstd || !scale || !shift) return AVD_ERR_ARG;
+  if (G <= 0 || count <= 1) return AVD_ERR_SHAPE;
+  return avd_c1_gram_finalize_launch(gram, wk, bias, gamma, beta, eps, momentum, count, mean, invstd,
+                                     scale, shift, running_mean, running_var, G, avd_stream(stream));
+}
+
+int avd_cl_c1_moments_codes_ng(const void* x, const void* gz, const unsigned* codes, float* out,
+                               int N, int B, int H, int W, void* stream) {
+  if (!x || !gz || !codes || !out) return AVD_ERR_ARG;
+  if (!c1_codes_shape(N, B, H, W)) return AVD_ERR_SHAPE;
+  return avd_c1_moments_nogram_launch(x, gz, codes, out, N, B, H, W, avd_stream(stream));
+}
+
+int avd_cl_c1_codes_combine_gram(const float* moments, const float* gram, const void* wk,
+                                 const float* bias, const float* gamma, const float* mean,
+                                 const float* invstd, long long count, float* dw, float* dgamma,
+                                 float* dbeta, float* dbias, float* coef, int G, void* stream) {
+  if (!moments || !gram || !wk || !gamma || !mean || !invstd || !dw) return AVD_ERR_ARG;
+  if (G <= 0 || count <= 1) return AVD_ERR_SHAPE;
+  return avd_c1_codes_combine_launch(moments, wk, bias, gamma, mean, invstd, count, dw, dgamma,
+                                     dbeta, dbias, coef, G, avd_stream(stream), gram);
 }
 
 int avd_cl_c1_moment_cols(int Cout, int K) {

@@ -1335,6 +1335,14 @@ constexpr int MOMC = COUT * 25 + 25 * 25 + 25 + COUT;
 #define C1MC_DIAG 0   // diagnostic builds only: 1 no input copies, 2 no dz map (wrong results)
 #endif
 
+// MM (what the pass accumulates): 0 = M, sum dz, Gram and S (the routed backward, MOMC floats
+// per row); 1 = Gram and S only (no pooled gradient: the FORWARD statistics pass -- y = w . x25 +
+// b, so sum y = w . S + n b and sum y^2 = w^T Gram w + 2 b w . S + n b^2 follow from it exactly,
+// GRAMC floats per row); 2 = M and sum dz only (the backward when the forward's Gram is kept;
+// MOMC floats, the Gram / S slots zero).
+constexpr int GRAMC = 25 * 25 + 25;
+
+template <int MM>
 __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ gz, const unsigned* __restrict__ codes,
     float* __restrict__ out, int B, int G, int R, int H, int W, int tps) {
@@ -1383,9 +1391,11 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
     for (int s = 0; s < 2; ++s) {
       const bool ok = (unsigned)(ty0 - 2 + xr[s]) < (unsigned)H;
       xv[s] = ldg16(ok ? (const void*)(xb + xoff[s]) : &kZeroC1);
-      const int w = min(tid + 256 * s, nwin - 1);
-      gv[s] = ldg16(gz + (w0 + w) * COUT);
-      cv[s] = codes[w0 + w];
+      if constexpr (MM != 1) {
+        const int w = min(tid + 256 * s, nwin - 1);
+        gv[s] = ldg16(gz + (w0 + w) * COUT);
+        cv[s] = codes[w0 + w];
+      }
     }
   };
   if (t_begin < t_end) load(t_begin);
@@ -1419,7 +1429,7 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int w = tid + 256 * s;
-      if (w >= nwin || (C1MC_DIAG & 2)) continue;
+      if (MM == 1 || w >= nwin || (C1MC_DIAG & 2)) continue;
       const int hp = w / Wp, wp = w - hp * Wp;
       const unsigned gw[4] = {gv[s].x, gv[s].y, gv[s].z, gv[s].w}, code = cv[s];
       unsigned ow[4][4];
@@ -1456,8 +1466,13 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
       u4 w0, w1;
       auto ld = [&](s4& a0, s4& a1, u4& c0, u4& c1) {
         const int P0 = 8 * sg, ab = (r * WMAX + 2 * P0) * COUT, bs = r * XB_RS + P0;
-        a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)&dys[ab + aoff0]);
-        a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)&dys[ab + aoff1]);
+        if constexpr (MM != 1) {
+          a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)&dys[ab + aoff0]);
+          a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)&dys[ab + aoff1]);
+        } else {
+          a0 = s4{0, 0, 0, 0};
+          a1 = s4{0, 0, 0, 0};
+        }
         c0 = *reinterpret_cast<const u4*>(&xc[bs + boff0]);
         c1 = *reinterpret_cast<const u4*>(&xc[bs + boff1]);
       };
@@ -1482,11 +1497,15 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
         const bf16x8 A = __builtin_bit_cast(bf16x8, s8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]});
         const bf16x8 X0 = __builtin_bit_cast(bf16x8, w0);
         const bf16x8 X1 = __builtin_bit_cast(bf16x8, ones ? one4 : w1);
-        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, X0, acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, X1, acc[1], 0, 0, 0);
-        ga[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X0, X0, ga[0], 0, 0, 0);
-        ga[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X0, X1, ga[1], 0, 0, 0);
-        ga[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X1, X1, ga[2], 0, 0, 0);
+        if constexpr (MM != 1) {
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, X0, acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, X1, acc[1], 0, 0, 0);
+        }
+        if constexpr (MM != 2) {
+          ga[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X0, X0, ga[0], 0, 0, 0);
+          ga[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X0, X1, ga[1], 0, 0, 0);
+          ga[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X1, X1, ga[2], 0, 0, 0);
+        }
         if (!more) break;
         h0 = n0; h1 = n1; w0 = v0; w1 = v1;
         n0 = m0; n1 = m1; v0 = x0v; v1 = x1v;
@@ -1509,7 +1528,8 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
       g6[(wave * 32 + 16 * ti + 4 * gq + i) * 32 + 16 * tj + col] = ga[b][i];
   }
   __syncthreads();
-  float* o = out + ((size_t)rr * G + grp) * MOMC;
+  constexpr int OC = MM == 1 ? GRAMC : MOMC;
+  float* o = out + ((size_t)rr * G + grp) * OC;
   auto g6v = [&](int t1, int t2) {        // the lower block (1,0) is the transpose of (0,1)
     if (t1 >= 16 && t2 < 16) { const int tmp = t1; t1 = t2; t2 = tmp; }
     float v = 0.f;
@@ -1517,8 +1537,27 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
     for (int wv = 0; wv < 4; ++wv) v += g6[(wv * 32 + t1) * 32 + t2];
     return v;
   };
+  if constexpr (MM == 1) {
+    for (int e = tid; e < GRAMC; e += 256) {
+      float v;
+      if (e < 625) {
+        const int a = e / 25, b = e % 25;
+        const int pa = (a / 5) * 6 + a % 5, pb = (b / 5) * 6 + b % 5;
+        v = g6v(pa, pb) + g6v(pa + 1, pb + 1);
+      } else {
+        const int a = e - 625, pa = (a / 5) * 6 + a % 5;
+        v = g6v(pa, 30) + g6v(pa + 1, 30);
+      }
+      o[e] = v;
+    }
+    return;
+  }
   for (int e = tid; e < MOMC; e += 256) {
     float v = 0.f;
+    if (MM == 2 && e >= COUT * 25 && e < COUT * 25 + 650) {
+      o[e] = 0.f;                         // Gram / S: the forward's (MM 1) are used instead
+      continue;
+    }
     if (e < COUT * 25) {
       const int c = e / 25, t = e - c * 25, ky = t / 5, kx = t - ky * 5;
 #pragma unroll
@@ -1549,7 +1588,7 @@ __global__ __launch_bounds__(256) void c1p8_codes_combine_kernel(
     const float* __restrict__ m, const bf16* __restrict__ wk, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
     long long count, float* __restrict__ dw, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    float* __restrict__ dbias, float* __restrict__ coef, int G) {
+    float* __restrict__ dbias, float* __restrict__ coef, int G, const float* __restrict__ gram_ext) {
   __shared__ double sk[32 * COUT][3];
   __shared__ double s12[32 * COUT][2];
   const int tid = threadIdx.x;
@@ -1595,7 +1634,8 @@ __global__ __launch_bounds__(256) void c1p8_codes_combine_kernel(
     double acc = 0.0;
     for (int g = 0; g < G; ++g) {
       const float* mg = m + (size_t)g * MOMC;
-      const float* gram = mg + COUT * 25;
+      // Gram / S: the forward statistics pass's (gram_ext [G][GRAMC]) or this pass's own
+      const float* gram = gram_ext ? gram_ext + (size_t)g * GRAMC : mg + COUT * 25;
       const double sx = gram[625 + t];
       double sy = b * sx;
 #pragma unroll
@@ -1607,6 +1647,51 @@ __global__ __launch_bounds__(256) void c1p8_codes_combine_kernel(
   }
 }
 
+// BatchNorm statistics of the conv output from the Gram pass (MM 1), float64: per group and
+// channel sum y = w . S + n b and sum y^2 = w^T Gram w + 2 b w . S + n b^2 (the exact conv
+// output y = w . x25 + b with the bf16 weights), then avd_bn_finalize's outputs: mean, invstd,
+// BN scale / shift, and the running statistics in group (view) order.
+__global__ __launch_bounds__(64) void c1p8_gram_finalize_kernel(
+    const float* __restrict__ gram, const bf16* __restrict__ wk, const float* __restrict__ bias,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
+    long long count, float* __restrict__ mean_o, float* __restrict__ invstd_o,
+    float* __restrict__ scale_o, float* __restrict__ shift_o, float* __restrict__ rm,
+    float* __restrict__ rv, int G) {
+  const int c = threadIdx.x;
+  if (c >= COUT) return;
+  double w[25];
+#pragma unroll
+  for (int t = 0; t < 25; ++t) w[t] = (double)bf2f(wk[c * 32 + t]);
+  const double b = bias ? (double)bias[c] : 0.0, n = (double)count;
+  double rmean = rm ? (double)rm[c] : 0.0, rvar = rv ? (double)rv[c] : 0.0;
+  for (int g = 0; g < G; ++g) {
+    const float* gm = gram + (size_t)g * GRAMC;
+    double ws = 0.0, q = 0.0;
+    for (int a = 0; a < 25; ++a) {
+      ws = fma(w[a], (double)gm[625 + a], ws);
+      double r = 0.0;
+      for (int t = 0; t < 25; ++t) r = fma((double)gm[a * 25 + t], w[t], r);
+      q = fma(w[a], r, q);
+    }
+    const double mean = (ws + n * b) / n;
+    const double ey2 = (q + 2.0 * b * ws + n * b * b) / n;
+    double var = ey2 - mean * mean;
+    if (var < 0) var = 0;
+    const double invstd = 1.0 / sqrt(var + (double)eps);
+    const double sc = (double)gamma[c] * invstd;
+    mean_o[g * COUT + c] = (float)mean;
+    invstd_o[g * COUT + c] = (float)invstd;
+    scale_o[g * COUT + c] = (float)sc;
+    shift_o[g * COUT + c] = (float)((double)beta[c] - mean * sc);
+    rmean = (1.0 - momentum) * rmean + momentum * mean;
+    rvar = (1.0 - momentum) * rvar + momentum * var * n / (n - 1.0);
+  }
+  if (rm) {
+    rm[c] = (float)rmean;
+    rv[c] = (float)rvar;
+  }
+}
+
 int c1p8_codes_rows(int N, int B) {
   static int resident = 0;
   if (!resident) {
@@ -1615,7 +1700,7 @@ int c1p8_codes_rows(int N, int B) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         cus <= 0)
       cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, c1p8_moments_codes_kernel, 256, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, c1p8_moments_codes_kernel<0>, 256, 0) !=
             hipSuccess || per <= 0)
       per = 2;
     resident = cus * per;
@@ -1718,8 +1803,38 @@ int avd_c1_apply_codes_launch(const void* x, const void* wk, const float* bias, 
 int avd_c1_moments_codes_launch(const void* x, const void* gz, const unsigned* codes, float* out,
                                 int N, int B, int H, int W, hipStream_t st) {
   const int tps = H / TH, G = N / B, R = c1p8_codes_rows(N, B);
-  c1p8_moments_codes_kernel<<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)gz, codes, out, B, G,
-                                                   R, H, W, tps);
+  c1p8_moments_codes_kernel<0><<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)gz, codes, out, B,
+                                                      G, R, H, W, tps);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+// the Gram pass (forward statistics) and the backward's moments without the Gram (MM 1 / 2)
+int avd_c1_gram_launch(const void* x, float* out, int N, int B, int H, int W, hipStream_t st) {
+  const int tps = H / TH, G = N / B, R = c1p8_codes_rows(N, B);
+  c1p8_moments_codes_kernel<1><<<G * R, 256, 0, st>>>((const bf16*)x, nullptr, nullptr, out, B, G, R,
+                                                      H, W, tps);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_c1_moments_nogram_launch(const void* x, const void* gz, const unsigned* codes, float* out,
+                                 int N, int B, int H, int W, hipStream_t st) {
+  const int tps = H / TH, G = N / B, R = c1p8_codes_rows(N, B);
+  c1p8_moments_codes_kernel<2><<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)gz, codes, out, B,
+                                                      G, R, H, W, tps);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_c1_gram_cols() { return GRAMC; }
+
+int avd_c1_gram_finalize_launch(const float* gram, const void* wk, const float* bias,
+                                const float* gamma, const float* beta, float eps, float momentum,
+                                long long count, float* mean, float* invstd, float* scale,
+                                float* shift, float* rm, float* rv, int G, hipStream_t st) {
+  c1p8_gram_finalize_kernel<<<1, 64, 0, st>>>(gram, (const bf16*)wk, bias, gamma, beta, eps, momentum,
+                                              count, mean, invstd, scale, shift, rm, rv, G);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
@@ -1727,10 +1842,11 @@ int avd_c1_moments_codes_launch(const void* x, const void* gz, const unsigned* c
 int avd_c1_codes_combine_launch(const float* m, const void* wk, const float* bias,
                                 const float* gamma, const float* mean, const float* invstd,
                                 long long count, float* dw, float* dgamma, float* dbeta,
-                                float* dbias, float* coef, int G, hipStream_t st) {
+                                float* dbias, float* coef, int G, hipStream_t st,
+                                const float* gram) {
   if (G <= 0 || G > 32) return AVD_ERR_SHAPE;
   c1p8_codes_combine_kernel<<<1, 256, 0, st>>>(m, (const bf16*)wk, bias, gamma, mean, invstd, count,
-                                               dw, dgamma, dbeta, dbias, coef, G);
+                                               dw, dgamma, dbeta, dbias, coef, G, gram);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
