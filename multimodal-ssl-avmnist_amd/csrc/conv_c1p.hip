@@ -28,6 +28,7 @@ namespace {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f4;
 typedef __attribute__((ext_vector_type(4))) unsigned u4;
+typedef __attribute__((ext_vector_type(2))) unsigned u2;
 
 constexpr int TH = 16;         // output rows per block (one sample)
 constexpr int XOFF = 8;        // LDS column of image column 0 (16-byte aligned data)
@@ -492,6 +493,9 @@ int avd_c1p8_bwd_apply_wgrad(const void* y, const void* gout, const float* scale
 namespace {
 
 enum { RC_STATS = 0, RC_APPLY = 1, RC_REDUCE = 2, RC_WGRAD = 3 };
+#ifndef RC_PF
+#define RC_PF 1
+#endif
 
 __device__ __forceinline__ void unpack8(u4 v, float (&f)[8]) {
   const unsigned w[4] = {v.x, v.y, v.z, v.w};
@@ -513,7 +517,14 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
   constexpr bool NEED_Y = PASS != RC_STATS;
   constexpr bool WG = PASS == RC_WGRAD;
   __shared__ __attribute__((aligned(16))) bf16 xs[(TH + 4) * ITW];
-  __shared__ __attribute__((aligned(16))) bf16 ys[NEED_Y ? TH * WMAX * COUT : 8];
+  // RC_APPLY keeps y rows parity-split (even pixels, then odd: a window's two columns are 56
+  // pixels apart) at a 1920-byte row stride (128 mod 256): the MFMA phase's 8-byte writes and the
+  // window threads' 16-byte reads are then bank-conflict free (contiguous per half-wave); the
+  // other passes keep natural rows (their tr16 reads want them)
+  constexpr bool PSPLIT = PASS == RC_APPLY;
+  constexpr int YRS = PSPLIT ? (WMAX + 8) * COUT : WMAX * COUT;
+  __shared__ __attribute__((aligned(16))) bf16 ys[NEED_Y ? TH * YRS : 8];
+  auto ypos = [&](int ox) { return PSPLIT ? (ox >> 1) + (ox & 1) * (WMAX / 2) : ox; };
   __shared__ __attribute__((aligned(16))) bf16 xc[WG ? 2 : 1][WG ? 3 : 1][WG ? TH + 4 : 1][XCW];
   __shared__ float red[WG ? 4 * 16 * 32 : 4 * 16];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -573,18 +584,23 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
     xr[s] = t < nxt ? r : -(1 << 20);
     xoff[s] = (r - 2) * W + 8 * c;
   }
-  u4 xv[2];
-  auto load_x = [&](int tl) {
+  // register ring of PF tiles' input rows: tile i's loads are issued PF tiles ahead, so a
+  // block keeps PF x 4.5 KB in flight instead of one tile's (the pass is load-latency bound)
+  constexpr int PF = PASS == RC_APPLY ? RC_PF : 1;
+  u4 xv[PF][2];
+  auto load_x = [&](int tl, u4 (&dst)[2]) {
     const int n = tl / tps, ty0 = (tl - n * tps) * TH;
     const bf16* xb = x + ((size_t)n * H + ty0) * W;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const bool ok = (unsigned)(ty0 - 2 + xr[s]) < (unsigned)H;
-      xv[s] = ldg16(ok ? (const void*)(xb + xoff[s]) : &kZeroC1);
+      dst[s] = ldg16(ok ? (const void*)(xb + xoff[s]) : &kZeroC1);
     }
   };
-  if (t_begin < t_end) load_x(t_begin);
-  for (int tile = t_begin; tile < t_end; tile += t_step) {
+#pragma unroll
+  for (int d = 0; d < PF; ++d)
+    if (t_begin + d * t_step < t_end) load_x(t_begin + d * t_step, xv[d]);
+  auto tile_body = [&](int tile, u4 (&xvd)[2]) {
     const int n = tile / tps, ty0 = (tile - n * tps) * TH, grp = n / B;
     __syncthreads();
     // ---- input tile (natural layout, zero pads)
@@ -593,14 +609,14 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
       const int t = tid + 256 * s;
       if (t < nxt) {
         const int r = t / cpr, c = t - r * cpr;
-        *reinterpret_cast<u4*>(xs + r * ITW + XOFF + 8 * c) = xv[s];
+        *reinterpret_cast<u4*>(xs + r * ITW + XOFF + 8 * c) = xvd[s];
       }
     }
     for (int t = tid; t < (TH + 4) * 2; t += 256) {
       const int r = t >> 1, side = t & 1;
       *reinterpret_cast<u4*>(xs + r * ITW + (side ? XOFF + W : 0)) = u4{0u, 0u, 0u, 0u};
     }
-    if (tile + t_step < t_end) load_x(tile + t_step);
+    if (tile + PF * t_step < t_end) load_x(tile + PF * t_step, xvd);
     __syncthreads();
     // ---- recompute y (rounded to bf16 exactly as the stored-y path)
     const unsigned* xd = reinterpret_cast<const unsigned*>(xs);
@@ -642,13 +658,13 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
           }
         } else {
           const int ox = 16 * mt + 2 * q + j;
-          *reinterpret_cast<uint2*>(&ys[((2 * s + rp) * WMAX + ox) * COUT + 4 * cs]) =
+          *reinterpret_cast<uint2*>(&ys[(2 * s + rp) * YRS + ypos(ox) * COUT + 4 * cs]) =
               make_uint2(lo, hi);
         }
       }
       }
     }
-    if constexpr (!NEED_Y) continue;
+    if constexpr (!NEED_Y) return;
     __syncthreads();
     // ---- per-window epilogues (one thread = one 2x2 window, all 8 channels)
     float sc[COUT], sf[COUT];
@@ -656,6 +672,52 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
     for (int e = 0; e < COUT; ++e) {
       sc[e] = scale[grp * COUT + e];
       sf[e] = shift[grp * COUT + e];
+    }
+    if constexpr (PASS == RC_APPLY) {
+      // z = relu(bn(max / min y)) and the first argmax: BN (fma, in channel pairs) per pixel,
+      // then one max3 pair per channel and an equality chain for the code nibble -- the same
+      // values as max_k relu(fma(y_k)) with a strict-> argmax update (fma and relu are monotone)
+      typedef __attribute__((ext_vector_type(2))) float f2;
+      f2 sc2[COUT / 2], sf2[COUT / 2];
+#pragma unroll
+      for (int i = 0; i < COUT / 2; ++i) {
+        sc2[i] = f2{sc[2 * i], sc[2 * i + 1]};
+        sf2[i] = f2{sf[2 * i], sf[2 * i + 1]};
+      }
+      for (int w = tid; w < (TH / 2) * Wp; w += 256) {
+        const int hp = w / Wp, wp = w - hp * Wp;
+        u4 yr[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          yr[k] = *reinterpret_cast<const u4*>(&ys[(2 * hp + (k >> 1)) * YRS + (wp + (k & 1) * (WMAX / 2)) * COUT]);
+        unsigned o[4], code = 0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          f2 r[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const unsigned d = i == 0 ? yr[k].x : i == 1 ? yr[k].y : i == 2 ? yr[k].z : yr[k].w;
+            const f2 yy = f2{__uint_as_float(d << 16), __uint_as_float(d & 0xffff0000u)};
+            r[k] = __builtin_elementwise_fma(yy, sc2[i], sf2[i]);
+          }
+          float best[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            best[e] = fmaxf(fmaxf(fmaxf(r[0][e], r[1][e]), fmaxf(r[2][e], r[3][e])), 0.f);
+            unsigned nib = 4u;
+            nib = r[2][e] == best[e] ? 3u : nib;
+            nib = r[1][e] == best[e] ? 2u : nib;
+            nib = r[0][e] == best[e] ? 1u : nib;
+            nib = best[e] > 0.f ? nib : 0u;
+            code |= nib << (4 * (2 * i + e));
+          }
+          o[i] = pack_bf16x2(best[0], best[1]);
+        }
+        const size_t pw = ((size_t)n * Hp + (ty0 >> 1) + hp) * Wp + wp;
+        *reinterpret_cast<u4*>(z + pw * COUT) = u4{o[0], o[1], o[2], o[3]};
+        if (codes) codes[pw] = code;
+      }
+      return;
     }
     for (int w = tid; w < (TH / 2) * Wp; w += 256) {
       const int hp = w / Wp, wp = w - hp * Wp;
@@ -753,6 +815,11 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
         }
       }
     }
+  };
+  for (int base = t_begin; base < t_end; base += PF * t_step) {
+#pragma unroll
+    for (int d = 0; d < PF; ++d)
+      if (base + d * t_step < t_end) tile_body(base + d * t_step, xv[d]);
   }
 
   if constexpr (PASS == RC_STATS || PASS == RC_REDUCE) {
@@ -1347,7 +1414,9 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ gz, const unsigned* __restrict__ codes,
     float* __restrict__ out, int B, int G, int R, int H, int W, int tps) {
   __shared__ __attribute__((aligned(16))) bf16 xc[2 * XB_CB];
-  __shared__ __attribute__((aligned(16))) bf16 dys[TH * WMAX * COUT];
+  // the Gram pass (MM 1) has no dz map: its LDS is the input copies alone (20 KB: 7 blocks per
+  // CU instead of 3), which also hold its Gram-tile reduction at the end
+  __shared__ __attribute__((aligned(16))) bf16 dys[MM == 1 ? 8 : TH * WMAX * COUT];
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int gq = lane >> 4, col = lane & 15;
   const int Hp = H >> 1, Wp = W >> 1, cpr = W >> 3, segs = W >> 4;
@@ -1514,12 +1583,16 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
   }
   // ---- block outputs: M / Gram / S folded from pairs to taps, sum dz from D's column 30
   __syncthreads();                        // every wave is done with dys / xc
+  static_assert(4 * 32 * 32 * 4 <= 2 * XB_CB * 2, "the Gram tiles fit the input copies");
   float* red = reinterpret_cast<float*>(dys);        // [4][16][32]  D
-  float* g6 = red + 4 * 16 * 32;                     // [4][32][32]  Gram tiles (upper blocks)
+  // [4][32][32]  Gram tiles (upper blocks)
+  float* g6 = MM == 1 ? reinterpret_cast<float*>(xc) : red + 4 * 16 * 32;
+  if constexpr (MM != 1) {
 #pragma unroll
-  for (int tt = 0; tt < 2; ++tt)
+    for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) red[(wave * 16 + 4 * gq + i) * 32 + 16 * tt + col] = acc[tt][i];
+      for (int i = 0; i < 4; ++i) red[(wave * 16 + 4 * gq + i) * 32 + 16 * tt + col] = acc[tt][i];
+  }
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
     const int ti = b == 2 ? 1 : 0, tj = b == 0 ? 0 : 1;
@@ -1576,6 +1649,179 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
       for (int wv = 0; wv < 4; ++wv) v += red[(wv * 16 + c) * 32 + 30] + red[(wv * 16 + 8 + c) * 32 + 30];
     }
     o[e] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------- window moments
+// The routed backward's M and sum dz (MM 2's output) in window space: dz is nonzero only at the
+// coded pixel (ky, kx) of each 2x2 pooling window, so with the window's 6x6 input footprint
+// x6[w][oy][ox] = x[2hp + oy - 2][2wp + ox - 2]
+//   M[c][dy][dx] = sum_{ky,kx} N[2ky+kx][c][(ky+dy)*6 + kx+dx],  N[k][c][o] = sum_w dz_k[c][w] x6[w][o]
+// with dz_k[c][w] = gz[w][c] where the window's code nibble for c is k + 1.  N is one GEMM per
+// tile: rows (k, c) = 32 (two 16-row tiles, ky), columns o = 36 footprint offsets + a ones column
+// (sum dz) in three 16-column tiles, K = windows.  The A operand is the pooled gradient tile read
+// transposed (ds_read_b64_tr_b16 of [window][8 channels], channels duplicated onto rows 8-15) and
+// masked in registers by the codes; the B operand is 8 consecutive windows of one parity / shift
+// copy of an input row (the xc copies of the pixel-pair kernel).  So the pass stores the pooled
+// gradient as it arrives (one 16-byte LDS write per window) instead of scattering a full-
+// resolution dz map, and its LDS (29 KB) leaves room for 5 blocks per CU.
+constexpr int NWINMAX = (TH / 2) * (WMAX / 2);
+
+__global__ __launch_bounds__(256, 4) void c1p8_moments_win_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ gz, const unsigned* __restrict__ codes,
+    float* __restrict__ out, int B, int G, int R, int H, int W, int tps) {
+  static_assert(4 * 32 * 48 * 4 <= (2 * XB_CB + NWINMAX * COUT) * 2, "reduction fits the tiles");
+  __shared__ __attribute__((aligned(16))) bf16 xc[2 * XB_CB];
+  __shared__ __attribute__((aligned(16))) bf16 gzs[NWINMAX * COUT];
+  __shared__ __attribute__((aligned(16))) unsigned cds[NWINMAX];
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int gq = lane >> 4, col = lane & 15;
+  const int Hp = H >> 1, Wp = W >> 1, gpr = Wp >> 3;        // 8-window groups per window row
+  const int nwin = (TH / 2) * Wp, ngrp = (TH / 2) * gpr, nstep = (ngrp + 3) >> 2;
+  const int grp = (int)blockIdx.x / R, rr = (int)blockIdx.x - grp * R;
+  const long long tpg = (long long)B * tps;
+  const int t_begin = (int)(grp * tpg + (tpg * rr) / R), t_end = (int)(grp * tpg + (tpg * (rr + 1)) / R);
+  // B columns: o = 16u + col < 36 reads copy (b, a) of tile row 2 hp + oy; o = 36 is ones
+  int boff[3];
+  bool bread[3], bone[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int o = 16 * u + col, oy = o / 6, ox = o - 6 * oy;
+    bread[u] = o < 36;
+    bone[u] = o == 36;
+    boff[u] = bread[u] ? xbo(ox & 1, ox >> 1, oy, 0) : 0;
+  }
+  const int csh = 4 * (col & 7), kk = col >> 3;
+  const int q = col >> 2, p = col & 3;
+  f4 acc[2][3];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 3; ++u) acc[t][u] = f4{0.f, 0.f, 0.f, 0.f};
+
+  int xr[2], xoff[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int t = tid + 256 * s;
+    const int r = t >> 4, c = t & 15;
+    xr[s] = (r < TH + 4 && c < (W >> 3)) ? r : -(1 << 20);
+    xoff[s] = (r - 2) * W + 8 * c;
+  }
+  u4 xv[2], gv[2];
+  unsigned cv[2];
+  auto load = [&](int tile) {
+    const int n = tile / tps, ty0 = (tile - n * tps) * TH;
+    const bf16* xb = x + ((size_t)n * H + ty0) * W;
+    const size_t w0 = ((size_t)n * Hp + (ty0 >> 1)) * Wp;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bool ok = (unsigned)(ty0 - 2 + xr[s]) < (unsigned)H;
+      xv[s] = ldg16(ok ? (const void*)(xb + xoff[s]) : &kZeroC1);
+      const int w = min(tid + 256 * s, nwin - 1);
+      gv[s] = ldg16(gz + (w0 + w) * COUT);
+      cv[s] = codes[w0 + w];
+    }
+  };
+  if (t_begin < t_end) load(t_begin);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    __syncthreads();                     // the previous tile's reads of xc / gzs / cds are done
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int t = tid + 256 * s;
+      const int r = t >> 4, c = t & 15;
+      const unsigned wv[4] = {xv[s].x, xv[s].y, xv[s].z, xv[s].w};
+      const unsigned ev[2] = {(wv[0] & 0xffffu) | (wv[1] << 16), (wv[2] & 0xffffu) | (wv[3] << 16)};
+      const unsigned od[2] = {(wv[0] >> 16) | (wv[1] & 0xffff0000u), (wv[2] >> 16) | (wv[3] & 0xffff0000u)};
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const unsigned lo = b ? od[0] : ev[0], hi = b ? od[1] : ev[1];
+        const unsigned prev_hi = (unsigned)dpp_i<0x111>((int)hi);   // lane c-1 (0 at c = 0)
+        const unsigned next_lo = (unsigned)dpp_i<0x101>((int)lo);   // lane c+1
+        if (r < TH + 4 && c < (W >> 3)) {
+          *reinterpret_cast<uint2*>(&xc[xbo(b, 0, r, 4 * c)]) =
+              make_uint2((prev_hi >> 16) | (lo << 16), (lo >> 16) | (hi << 16));
+          *reinterpret_cast<uint2*>(&xc[xbo(b, 1, r, 4 * c)]) = make_uint2(lo, hi);
+          *reinterpret_cast<uint2*>(&xc[xbo(b, 2, r, 4 * c)]) =
+              make_uint2((lo >> 16) | (hi << 16), (hi >> 16) | (next_lo << 16));
+        }
+      }
+      const int w = tid + 256 * s;
+      if (w < nwin) {
+        *reinterpret_cast<u4*>(&gzs[w * COUT]) = gv[s];
+        cds[w] = cv[s];
+      }
+    }
+    if (tile + 1 < t_end) load(tile + 1);   // in flight under this tile's MFMAs
+    __syncthreads();
+    for (int j = wave; j < nstep; j += 4) {
+      const int m = 4 * j + gq;
+      const bool valid = m < ngrp;
+      const int hpl = valid ? m / gpr : 0, wp0 = valid ? 8 * (m - hpl * gpr) : 0;
+      const int w0 = hpl * Wp + wp0;
+      u4 a4 = u4{0u, 0u, 0u, 0u};
+      u4 c0 = u4{0u, 0u, 0u, 0u}, c1 = u4{0u, 0u, 0u, 0u};
+      if (valid) {
+        const s4 g0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)&gzs[(w0 + q) * COUT + 4 * (p & 1)]);
+        const s4 g1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)&gzs[(w0 + 4 + q) * COUT + 4 * (p & 1)]);
+        const u2 lo2 = __builtin_bit_cast(u2, g0), hi2 = __builtin_bit_cast(u2, g1);
+        a4 = u4{lo2.x, lo2.y, hi2.x, hi2.y};
+        c0 = *reinterpret_cast<const u4*>(&cds[w0]);
+        c1 = *reinterpret_cast<const u4*>(&cds[w0 + 4]);
+      }
+      const unsigned cw[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      unsigned nib[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) nib[i] = (cw[i] >> csh) & 0xFu;
+      const int bs = 2 * hpl * XB_RS + wp0;
+      u4 bv[3];
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        if (bread[u]) bv[u] = *reinterpret_cast<const u4*>(&xc[bs + boff[u]]);
+        else bv[u] = bone[u] ? u4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u} : u4{0u, 0u, 0u, 0u};
+      }
+      const unsigned av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const unsigned tgt = (unsigned)(2 * t + kk + 1);
+        unsigned am[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          am[d] = av[d] & ((nib[2 * d] == tgt ? 0x0000ffffu : 0u) | (nib[2 * d + 1] == tgt ? 0xffff0000u : 0u));
+        const bf16x8 A = __builtin_bit_cast(bf16x8, u4{am[0], am[1], am[2], am[3]});
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, __builtin_bit_cast(bf16x8, bv[u]), acc[t][u], 0, 0, 0);
+      }
+    }
+  }
+  // ---- block output: fold N's rows (k, c) and footprint columns into M, sum dz from column 36
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(xc);          // [4 waves][32 rows][48 cols]
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[(wave * 32 + 16 * t + 4 * gq + i) * 48 + 16 * u + col] = acc[t][u][i];
+  __syncthreads();
+  float* o = out + ((size_t)rr * G + grp) * MOMC;
+  for (int e = tid; e < MOMC; e += 256) {
+    float v = 0.f;
+    if (e < COUT * 25) {
+      const int c = e / 25, t = e - c * 25, dy = t / 5, dx = t - dy * 5;
+#pragma unroll
+      for (int wv = 0; wv < 4; ++wv)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          v += red[(wv * 32 + 8 * k + c) * 48 + ((k >> 1) + dy) * 6 + (k & 1) + dx];
+    } else if (e >= COUT * 25 + 650) {
+      const int c = e - (COUT * 25 + 650);
+#pragma unroll
+      for (int wv = 0; wv < 4; ++wv)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v += red[(wv * 32 + 8 * k + c) * 48 + 36];
+    }
+    o[e] = v;                             // Gram / S slots zero: the forward's Gram is used
   }
 }
 
@@ -1651,44 +1897,63 @@ __global__ __launch_bounds__(256) void c1p8_codes_combine_kernel(
 // channel sum y = w . S + n b and sum y^2 = w^T Gram w + 2 b w . S + n b^2 (the exact conv
 // output y = w . x25 + b with the bf16 weights), then avd_bn_finalize's outputs: mean, invstd,
 // BN scale / shift, and the running statistics in group (view) order.
-__global__ __launch_bounds__(64) void c1p8_gram_finalize_kernel(
+__global__ __launch_bounds__(256) void c1p8_gram_finalize_kernel(
     const float* __restrict__ gram, const bf16* __restrict__ wk, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
     long long count, float* __restrict__ mean_o, float* __restrict__ invstd_o,
     float* __restrict__ scale_o, float* __restrict__ shift_o, float* __restrict__ rm,
     float* __restrict__ rv, int G) {
-  const int c = threadIdx.x;
-  if (c >= COUT) return;
-  double w[25];
-#pragma unroll
-  for (int t = 0; t < 25; ++t) w[t] = (double)bf2f(wk[c * 32 + t]);
-  const double b = bias ? (double)bias[c] : 0.0, n = (double)count;
-  double rmean = rm ? (double)rm[c] : 0.0, rvar = rv ? (double)rv[c] : 0.0;
+  // thread (c, a) < 200 forms w[c][a] (Gram w[c])[a] and w[c][a] S[a] of one group; the 25
+  // partials per channel are summed by thread c (fixed order), which also carries the running
+  // statistics through the groups in order
+  __shared__ double wsh[COUT * 25];
+  __shared__ double pq[COUT * 25], ps[COUT * 25];
+  const int tid = threadIdx.x;
+  if (tid < COUT * 25) wsh[tid] = (double)bf2f(wk[(tid / 25) * 32 + tid % 25]);
+  const int c = tid / 25, a = tid - c * 25;
+  const double n = (double)count;
+  double rmean = 0.0, rvar = 0.0, b = 0.0;
+  if (tid < COUT) {
+    rmean = rm ? (double)rm[tid] : 0.0;
+    rvar = rv ? (double)rv[tid] : 0.0;
+    b = bias ? (double)bias[tid] : 0.0;
+  }
+  __syncthreads();
   for (int g = 0; g < G; ++g) {
     const float* gm = gram + (size_t)g * GRAMC;
-    double ws = 0.0, q = 0.0;
-    for (int a = 0; a < 25; ++a) {
-      ws = fma(w[a], (double)gm[625 + a], ws);
+    if (tid < COUT * 25) {
       double r = 0.0;
-      for (int t = 0; t < 25; ++t) r = fma((double)gm[a * 25 + t], w[t], r);
-      q = fma(w[a], r, q);
+#pragma unroll
+      for (int t = 0; t < 25; ++t) r = fma((double)gm[a * 25 + t], wsh[c * 25 + t], r);
+      const double wa = wsh[tid];
+      pq[tid] = wa * r;
+      ps[tid] = wa * (double)gm[625 + a];
     }
-    const double mean = (ws + n * b) / n;
-    const double ey2 = (q + 2.0 * b * ws + n * b * b) / n;
-    double var = ey2 - mean * mean;
-    if (var < 0) var = 0;
-    const double invstd = 1.0 / sqrt(var + (double)eps);
-    const double sc = (double)gamma[c] * invstd;
-    mean_o[g * COUT + c] = (float)mean;
-    invstd_o[g * COUT + c] = (float)invstd;
-    scale_o[g * COUT + c] = (float)sc;
-    shift_o[g * COUT + c] = (float)((double)beta[c] - mean * sc);
-    rmean = (1.0 - momentum) * rmean + momentum * mean;
-    rvar = (1.0 - momentum) * rvar + momentum * var * n / (n - 1.0);
+    __syncthreads();
+    if (tid < COUT) {
+      double q = 0.0, ws = 0.0;
+      for (int k = 0; k < 25; ++k) {
+        q += pq[tid * 25 + k];
+        ws += ps[tid * 25 + k];
+      }
+      const double mean = (ws + n * b) / n;
+      const double ey2 = (q + 2.0 * b * ws + n * b * b) / n;
+      double var = ey2 - mean * mean;
+      if (var < 0) var = 0;
+      const double invstd = 1.0 / sqrt(var + (double)eps);
+      const double sc = (double)gamma[tid] * invstd;
+      mean_o[g * COUT + tid] = (float)mean;
+      invstd_o[g * COUT + tid] = (float)invstd;
+      scale_o[g * COUT + tid] = (float)sc;
+      shift_o[g * COUT + tid] = (float)((double)beta[tid] - mean * sc);
+      rmean = (1.0 - momentum) * rmean + momentum * mean;
+      rvar = (1.0 - momentum) * rvar + momentum * var * n / (n - 1.0);
+    }
+    __syncthreads();
   }
-  if (rm) {
-    rm[c] = (float)rmean;
-    rv[c] = (float)rvar;
+  if (rm && tid < COUT) {
+    rm[tid] = (float)rmean;
+    rv[tid] = (float)rvar;
   }
 }
 
@@ -1821,8 +2086,14 @@ int avd_c1_gram_launch(const void* x, float* out, int N, int B, int H, int W, hi
 int avd_c1_moments_nogram_launch(const void* x, const void* gz, const unsigned* codes, float* out,
                                  int N, int B, int H, int W, hipStream_t st) {
   const int tps = H / TH, G = N / B, R = c1p8_codes_rows(N, B);
-  c1p8_moments_codes_kernel<2><<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)gz, codes, out, B,
-                                                      G, R, H, W, tps);
+  // the window-space pass (c1p8_moments_win_kernel); AVDINO_C1_MOMWIN=0 keeps the pixel-pair one
+  static const bool win = !getenv("AVDINO_C1_MOMWIN") || atoi(getenv("AVDINO_C1_MOMWIN")) != 0;
+  if (win)
+    c1p8_moments_win_kernel<<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)gz, codes, out, B, G, R,
+                                                   H, W, tps);
+  else
+    c1p8_moments_codes_kernel<2><<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)gz, codes, out, B,
+                                                        G, R, H, W, tps);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
@@ -1833,7 +2104,7 @@ int avd_c1_gram_finalize_launch(const float* gram, const void* wk, const float* 
                                 const float* gamma, const float* beta, float eps, float momentum,
                                 long long count, float* mean, float* invstd, float* scale,
                                 float* shift, float* rm, float* rv, int G, hipStream_t st) {
-  c1p8_gram_finalize_kernel<<<1, 64, 0, st>>>(gram, (const bf16*)wk, bias, gamma, beta, eps, momentum,
+  c1p8_gram_finalize_kernel<<<1, 256, 0, st>>>(gram, (const bf16*)wk, bias, gamma, beta, eps, momentum,
                                               count, mean, invstd, scale, shift, rm, rv, G);
   AVD_CHECK_LAUNCH();
   return AVD_OK;

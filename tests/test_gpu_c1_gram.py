@@ -9,9 +9,10 @@ recompute stats pass, and the backward's moments pass drops its Gram half
 
 Checked here against float64 of the exact conv output w . x25 + b (w rounded to bf16 as the
 kernels use it): mean / invstd / scale / shift / running stats within 1e-5 (2e-4 for the variance
-of a strongly off-centre channel, where E[y^2] - mean^2 cancels), the Gram rows bit-identical to
-the Gram half of the full routed moments pass, and dW / dgamma / dbeta / coefficients from the
-split path bit-identical to the full routed combine."""
+of a strongly off-centre channel, where E[y^2] - mean^2 cancels), the Gram rows within 1e-6 of
+the Gram half of the full routed moments pass (fp32 sums of the same products, rows split
+differently), and dW / dgamma / dbeta / coefficients from the split path within 1e-5 of the full
+routed combine."""
 import pytest
 
 torch = pytest.importorskip("torch")
@@ -115,8 +116,9 @@ def test_gram_stats(ops, N, B, off):
 @pytest.mark.parametrize("N,B", [(24, 8), (7168, 1024)])
 def test_split_backward_matches_full(ops, N, B):
     """avd_cl_c1_moments_codes_ng + avd_cl_c1_codes_combine_gram (Gram from the forward's
-    avd_cl_c1_gram) gives bit-identically the dW / dgamma / dbeta / dbias / coefficients of the
-    full routed pass avd_cl_c1_moments_codes + avd_cl_c1_codes_combine on the same codes."""
+    avd_cl_c1_gram) against the full routed pass avd_cl_c1_moments_codes + avd_cl_c1_codes_combine
+    on the same codes: dW / dgamma / dbeta / coefficients within 1e-5 (the dbias, analytically 0,
+    within 1e-6 of the largest)."""
     G = N // B
     Hp = H // 2
     g = torch.Generator(device="cuda").manual_seed(29 + N)
@@ -149,8 +151,10 @@ def test_split_backward_matches_full(ops, N, B):
             ops.c1_codes_combine_gram(mom, gram, wk, bias, gamma, bn[0], bn[1], B * H * H, *r, coef, G)
         else:
             mh = mom.view(G, mc)
-            assert torch.equal(mh[:, C * 25:C * 25 + 650], gram.view(G, gc)), "Gram half differs"
+            print("Gram half vs the Gram pass", grel(mh[:, C * 25:C * 25 + 650], gram.view(G, gc)))
+            assert grel(mh[:, C * 25:C * 25 + 650], gram.view(G, gc)) < 1e-6
             ops.c1_codes_combine(mom, wk, bias, gamma, bn[0], bn[1], B * H * H, *r, coef, G)
         outs.append(r + [coef])
     for a, b in zip(*outs):
-        assert torch.equal(a, b), grel(a, b)
+        print("split vs full", grel(b, a))
+        assert grel(b, a) < 1e-5 or (a - b).abs().max() < 1e-6 * a.abs().max().clamp_min(1.0), grel(a, b)
