@@ -29,6 +29,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f4;
 typedef __attribute__((ext_vector_type(4))) unsigned u4;
 typedef __attribute__((ext_vector_type(2))) unsigned u2;
+typedef __attribute__((ext_vector_type(2))) unsigned short us2;
 
 constexpr int TH = 16;         // output rows per block (one sample)
 constexpr int XOFF = 8;        // LDS column of image column 0 (16-byte aligned data)
@@ -518,11 +519,13 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
   constexpr bool WG = PASS == RC_WGRAD;
   __shared__ __attribute__((aligned(16))) bf16 xs[(TH + 4) * ITW];
   // RC_APPLY keeps y rows parity-split (even pixels, then odd: a window's two columns are 56
-  // pixels apart) at a 1920-byte row stride (128 mod 256): the MFMA phase's 8-byte writes and the
-  // window threads' 16-byte reads are then bank-conflict free (contiguous per half-wave); the
-  // other passes keep natural rows (their tr16 reads want them)
+  // pixels apart), odd rows with their two 4-channel halves swapped, at a 1856-byte row stride
+  // (64 mod 128): the MFMA phase's 8-byte writes (rows 2s and 2s+1 in one 16-lane group) and the
+  // window threads' 16-byte reads (which wrap to the next window row) are then bank-conflict
+  // free (tools/lds_conflicts.py); the other passes keep natural rows (their tr16 reads want them)
   constexpr bool PSPLIT = PASS == RC_APPLY;
-  constexpr int YRS = PSPLIT ? (WMAX + 8) * COUT : WMAX * COUT;
+  constexpr int YRS = PSPLIT ? 928 : WMAX * COUT;
+  static_assert(!PSPLIT || (YRS >= WMAX * COUT && (YRS * 2) % 128 == 64), "apply y row stride");
   __shared__ __attribute__((aligned(16))) bf16 ys[NEED_Y ? TH * YRS : 8];
   auto ypos = [&](int ox) { return PSPLIT ? (ox >> 1) + (ox & 1) * (WMAX / 2) : ox; };
   __shared__ __attribute__((aligned(16))) bf16 xc[WG ? 2 : 1][WG ? 3 : 1][WG ? TH + 4 : 1][XCW];
@@ -575,13 +578,14 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
   const int t_step = WG ? (int)gridDim.x : 1;
   // input rows of a tile: <= 2 16-byte vectors per thread (W <= WMAX), register-prefetched one
   // tile ahead (issued before the current tile's MFMAs and epilogue)
-  const int nxt = (TH + 4) * cpr;
+  // input rows: 16 lanes per row (lane c < cpr holds pixels 8c .. 8c+7), so the 8-lane groups
+  // of the 16-byte LDS stores never straddle two rows (conflict-free staging)
   int xr[2], xoff[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const int t = tid + 256 * s;
-    const int r = t / cpr, c = t - r * cpr;
-    xr[s] = t < nxt ? r : -(1 << 20);
+    const int r = t >> 4, c = t & 15;
+    xr[s] = (r < TH + 4 && c < cpr) ? r : -(1 << 20);
     xoff[s] = (r - 2) * W + 8 * c;
   }
   // register ring of PF tiles' input rows: tile i's loads are issued PF tiles ahead, so a
@@ -607,10 +611,8 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int t = tid + 256 * s;
-      if (t < nxt) {
-        const int r = t / cpr, c = t - r * cpr;
-        *reinterpret_cast<u4*>(xs + r * ITW + XOFF + 8 * c) = xvd[s];
-      }
+      const int r = t >> 4, c = t & 15;
+      if (r < TH + 4 && c < cpr) *reinterpret_cast<u4*>(xs + r * ITW + XOFF + 8 * c) = xvd[s];
     }
     for (int t = tid; t < (TH + 4) * 2; t += 256) {
       const int r = t >> 1, side = t & 1;
@@ -658,7 +660,7 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
           }
         } else {
           const int ox = 16 * mt + 2 * q + j;
-          *reinterpret_cast<uint2*>(&ys[(2 * s + rp) * YRS + ypos(ox) * COUT + 4 * cs]) =
+          *reinterpret_cast<uint2*>(&ys[(2 * s + rp) * YRS + ypos(ox) * COUT + 4 * (PSPLIT ? cs ^ rp : cs)]) =
               make_uint2(lo, hi);
         }
       }
@@ -689,7 +691,10 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
         u4 yr[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          yr[k] = *reinterpret_cast<const u4*>(&ys[(2 * hp + (k >> 1)) * YRS + (wp + (k & 1) * (WMAX / 2)) * COUT]);
+        {
+          const u4 v = *reinterpret_cast<const u4*>(&ys[(2 * hp + (k >> 1)) * YRS + (wp + (k & 1) * (WMAX / 2)) * COUT]);
+          yr[k] = k >> 1 ? u4{v.z, v.w, v.x, v.y} : v;     // odd rows: halves swapped
+        }
         unsigned o[4], code = 0u;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1670,10 +1675,17 @@ constexpr int NWINMAX = (TH / 2) * (WMAX / 2);
 __global__ __launch_bounds__(256, 4) void c1p8_moments_win_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ gz, const unsigned* __restrict__ codes,
     float* __restrict__ out, int B, int G, int R, int H, int W, int tps) {
-  static_assert(4 * 32 * 48 * 4 <= (2 * XB_CB + NWINMAX * COUT) * 2, "reduction fits the tiles");
-  __shared__ __attribute__((aligned(16))) bf16 xc[2 * XB_CB];
-  __shared__ __attribute__((aligned(16))) bf16 gzs[NWINMAX * COUT];
-  __shared__ __attribute__((aligned(16))) unsigned cds[NWINMAX];
+  static_assert(4 * 32 * 48 * 4 <= (2 * XB_CB + NWINMAX * COUT) * 2, "reduction fits the block");
+  // xc: the parity/shift input copies, then 16 bytes of bf16 ones and 16 of zeros (the B
+  // operand of the sum-dz column and of the padding columns: read like any other column)
+  constexpr int KONE = 2 * XB_CB, KZERO = KONE + 8, GZOFF = 2 * XB_CB + 16;
+  // one LDS block (the final reduction spans all of it): xc | ones, zeros | gzs | cds
+  __shared__ __attribute__((aligned(16))) bf16 smem[GZOFF + NWINMAX * COUT + 2 * NWINMAX];
+  bf16* xc = smem;
+  bf16* gzs = smem + GZOFF;
+  // routing of window pairs per row tile t (ky): word [t][w / 2], bit 2c + kx of the low half =
+  // window w routes channel c to pixel (ky, kx), the high half the same for window w + 1
+  unsigned (*cds)[NWINMAX / 2] = reinterpret_cast<unsigned (*)[NWINMAX / 2]>(smem + GZOFF + NWINMAX * COUT);
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int gq = lane >> 4, col = lane & 15;
   const int Hp = H >> 1, Wp = W >> 1, gpr = Wp >> 3;        // 8-window groups per window row
@@ -1681,18 +1693,20 @@ __global__ __launch_bounds__(256, 4) void c1p8_moments_win_kernel(
   const int grp = (int)blockIdx.x / R, rr = (int)blockIdx.x - grp * R;
   const long long tpg = (long long)B * tps;
   const int t_begin = (int)(grp * tpg + (tpg * rr) / R), t_end = (int)(grp * tpg + (tpg * (rr + 1)) / R);
-  // B columns: o = 16u + col < 36 reads copy (b, a) of tile row 2 hp + oy; o = 36 is ones
-  int boff[3];
-  bool bread[3], bone[3];
+  if (tid < 16) xc[KONE + tid] = tid < 8 ? (bf16)0x3F80u : (bf16)0u;     // bf16 1.0, 0.0
+  // B columns: o = 16u + col < 36 reads copy (b, a) of tile row 2 hp + oy; o = 36 the ones,
+  // o > 36 the zeros (their address ignores the k-step: bmask 0)
+  int boff[3], bmask[3];
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
     const int o = 16 * u + col, oy = o / 6, ox = o - 6 * oy;
-    bread[u] = o < 36;
-    bone[u] = o == 36;
-    boff[u] = bread[u] ? xbo(ox & 1, ox >> 1, oy, 0) : 0;
+    bmask[u] = o < 36 ? -1 : 0;
+    boff[u] = o < 36 ? xbo(ox & 1, ox >> 1, oy, 0) : o == 36 ? KONE : KZERO;
   }
-  const int csh = 4 * (col & 7), kk = col >> 3;
+  const unsigned rsh = 2 * (col & 7) + (col >> 3);          // routing bit of this A row
   const int q = col >> 2, p = col & 3;
+  // this lane group's first 8-window group and the per-step advance (16 groups)
+  const int m0 = 4 * wave + gq, dh = 16 / gpr, dg = 16 - dh * gpr;
   f4 acc[2][3];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -1745,53 +1759,68 @@ __global__ __launch_bounds__(256, 4) void c1p8_moments_win_kernel(
               make_uint2((lo >> 16) | (hi << 16), (hi >> 16) | (next_lo << 16));
         }
       }
+      // routing bits: nibble n (0 none, 1 + 2 ky + kx) of channel c -> bit 2c + kx of row tile
+      // ky, for all 8 channels at once (nibble-parallel), then paired with the next window
+      const unsigned v = cv[s];
+      const unsigned n0 = v & 0x11111111u, n1 = (v >> 1) & 0x11111111u, n2 = (v >> 2) & 0x11111111u;
+      unsigned rt[2] = {(n0 & ~n1) | ((n1 & ~n0) << 1),      // n == 1, 2: ky 0
+                        (n0 & n1) | (n2 << 1)};               // n == 3, 4: ky 1
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {                       // 2-bit fields at 4c -> at 2c
+        unsigned f = rt[t2];
+        f = (f | (f >> 2)) & 0x0F0F0F0Fu;
+        f = (f | (f >> 4)) & 0x00FF00FFu;
+        f = (f | (f >> 8)) & 0x0000FFFFu;
+        rt[t2] = f | ((unsigned)dpp_i<0x101>((int)f) << 16);  // the next lane's (= window's)
+      }
       const int w = tid + 256 * s;
       if (w < nwin) {
         *reinterpret_cast<u4*>(&gzs[w * COUT]) = gv[s];
-        cds[w] = cv[s];
+        if (!(w & 1)) {
+          cds[0][w >> 1] = rt[0];
+          cds[1][w >> 1] = rt[1];
+        }
       }
     }
     if (tile + 1 < t_end) load(tile + 1);   // in flight under this tile's MFMAs
     __syncthreads();
+    int hpl = m0 / gpr, gi = m0 - hpl * gpr;
     for (int j = wave; j < nstep; j += 4) {
-      const int m = 4 * j + gq;
-      const bool valid = m < ngrp;
-      const int hpl = valid ? m / gpr : 0, wp0 = valid ? 8 * (m - hpl * gpr) : 0;
-      const int w0 = hpl * Wp + wp0;
+      const bool valid = hpl < TH / 2;
+      const int w0 = hpl * Wp + 8 * gi;
       u4 a4 = u4{0u, 0u, 0u, 0u};
-      u4 c0 = u4{0u, 0u, 0u, 0u}, c1 = u4{0u, 0u, 0u, 0u};
+      u4 r0 = u4{0u, 0u, 0u, 0u}, r1 = u4{0u, 0u, 0u, 0u};
       if (valid) {
         const s4 g0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)&gzs[(w0 + q) * COUT + 4 * (p & 1)]);
         const s4 g1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)&gzs[(w0 + 4 + q) * COUT + 4 * (p & 1)]);
         const u2 lo2 = __builtin_bit_cast(u2, g0), hi2 = __builtin_bit_cast(u2, g1);
         a4 = u4{lo2.x, lo2.y, hi2.x, hi2.y};
-        c0 = *reinterpret_cast<const u4*>(&cds[w0]);
-        c1 = *reinterpret_cast<const u4*>(&cds[w0 + 4]);
+        r0 = *reinterpret_cast<const u4*>(&cds[0][w0 >> 1]);
+        r1 = *reinterpret_cast<const u4*>(&cds[1][w0 >> 1]);
       }
-      const unsigned cw[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-      unsigned nib[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) nib[i] = (cw[i] >> csh) & 0xFu;
-      const int bs = 2 * hpl * XB_RS + wp0;
+      const int bs = 2 * hpl * XB_RS + 8 * gi;
       u4 bv[3];
 #pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        if (bread[u]) bv[u] = *reinterpret_cast<const u4*>(&xc[bs + boff[u]]);
-        else bv[u] = bone[u] ? u4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u} : u4{0u, 0u, 0u, 0u};
-      }
+      for (int u = 0; u < 3; ++u) bv[u] = *reinterpret_cast<const u4*>(&xc[(bs & bmask[u]) + boff[u]]);
       const unsigned av[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const unsigned tgt = (unsigned)(2 * t + kk + 1);
+        const u4 rw = t ? r1 : r0;
+        const unsigned rv[4] = {rw.x, rw.y, rw.z, rw.w};
         unsigned am[4];
+        // a routed window keeps its pooled gradient: (bit) x bf16 pattern, both halves at once
 #pragma unroll
         for (int d = 0; d < 4; ++d)
-          am[d] = av[d] & ((nib[2 * d] == tgt ? 0x0000ffffu : 0u) | (nib[2 * d + 1] == tgt ? 0xffff0000u : 0u));
+          am[d] = __builtin_bit_cast(unsigned, __builtin_bit_cast(us2, av[d]) *
+                                                   __builtin_bit_cast(us2, (rv[d] >> rsh) & 0x00010001u));
         const bf16x8 A = __builtin_bit_cast(bf16x8, u4{am[0], am[1], am[2], am[3]});
 #pragma unroll
         for (int u = 0; u < 3; ++u)
           acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, __builtin_bit_cast(bf16x8, bv[u]), acc[t][u], 0, 0, 0);
       }
+      gi += dg;
+      hpl += dh;
+      if (gi >= gpr) { gi -= gpr; ++hpl; }
     }
   }
   // ---- block output: fold N's rows (k, c) and footprint columns into M, sum dz from column 36
