@@ -249,7 +249,8 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     int t = 16 * tt + col;
-    if (t >= 30) t = 0;                    // padded taps: any finite data (their D is unused)
+    if (t >= 30) t = 29;                   // padded taps: any finite data (their D is unused);
+                                           // tap 29 as column 13 reads: a broadcast, no bank conflict
     const int ky = t / 6, k2 = t % 6 - 2;  // kx' - 2 = 2a' + b
     bky[tt] = ky;
     bb[tt] = k2 & 1;
@@ -494,6 +495,13 @@ int avd_c1p8_bwd_apply_wgrad(const void* y, const void* gout, const float* scale
 namespace {
 
 enum { RC_STATS = 0, RC_APPLY = 1, RC_REDUCE = 2, RC_WGRAD = 3 };
+#ifndef C1A_MTU
+#define C1A_MTU 1    // apply pass: column tiles per MFMA-phase step (B reads, MFMAs, stores batched)
+#endif
+#ifndef C1A_DIAG
+#define C1A_DIAG 0   // diagnostic builds of the apply pass only (wrong results): 1 no z / code
+                     // stores, 2 no window epilogue, 4 no MFMA phase (tools/build_variants.sh)
+#endif
 #ifndef RC_PF
 #define RC_PF 1
 #endif
@@ -564,7 +572,7 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     int t = 16 * tt + p;
-    if (t >= 30) t = 0;
+    if (t >= 30) t = 29;   // padded taps (unused, or replaced by ones): column 13's address, a broadcast
     const int ky = t / 6, k2 = t % 6 - 2;
     bky[tt] = ky;
     bb[tt] = k2 & 1;
@@ -622,11 +630,11 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
     __syncthreads();
     // ---- recompute y (rounded to bf16 exactly as the stored-y path)
     const unsigned* xd = reinterpret_cast<const unsigned*>(xs);
-    for (int s = wave; s < TH / 2; s += 4) {
+    for (int s = wave; s < ((PASS == RC_APPLY && (C1A_DIAG & 4)) ? 0 : TH / 2); s += 4) {
       // statistics pass: every column tile's B fragments first (their LDS reads in flight
       // together), then the MFMAs, then the epilogues (213 vs 224 us); the other passes keep
       // one tile at a time (the unrolled registers cost the apply pass an occupancy step)
-      constexpr int MTU = PASS == RC_STATS ? MTMAX : 1;
+      constexpr int MTU = PASS == RC_STATS ? MTMAX : PASS == RC_APPLY ? C1A_MTU : 1;
       for (int mt0 = 0; mt0 < mts; mt0 += MTU) {
       u4 bws[MTU];
 #pragma unroll
@@ -686,7 +694,7 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
         sc2[i] = f2{sc[2 * i], sc[2 * i + 1]};
         sf2[i] = f2{sf[2 * i], sf[2 * i + 1]};
       }
-      for (int w = tid; w < (TH / 2) * Wp; w += 256) {
+      for (int w = tid; w < ((C1A_DIAG & 2) ? 0 : (TH / 2) * Wp); w += 256) {
         const int hp = w / Wp, wp = w - hp * Wp;
         u4 yr[4];
 #pragma unroll
@@ -719,6 +727,10 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
           o[i] = pack_bf16x2(best[0], best[1]);
         }
         const size_t pw = ((size_t)n * Hp + (ty0 >> 1) + hp) * Wp + wp;
+        if (C1A_DIAG & 1) {
+          if (o[0] == 0x12345678u && code == 0x9abcdefu) z[0] = 0;   // keep the values live
+          continue;
+        }
         *reinterpret_cast<u4*>(z + pw * COUT) = u4{o[0], o[1], o[2], o[3]};
         if (codes) codes[pw] = code;
       }
@@ -964,7 +976,7 @@ __global__ __launch_bounds__(256, 2) void c1p8_moments_kernel(
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     int t = 16 * tt + col;
-    if (t >= 30) t = 0;
+    if (t >= 30) t = 29;   // padded taps (unused, or replaced by ones): column 13's address, a broadcast
     const int ky = t / 6, k2 = t % 6 - 2;
     bky[tt] = ky;
     bb[tt] = k2 & 1;
@@ -1432,7 +1444,7 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     int t = 16 * tt + col;
-    if (t >= 30) t = 0;
+    if (t >= 30) t = 29;   // padded taps (unused, or replaced by ones): column 13's address, a broadcast
     const int ky = t / 6, k2 = t % 6 - 2;
     bky[tt] = ky;
     bb[tt] = k2 & 1;

@@ -123,3 +123,82 @@ def main():
 
 if __name__ == "__main__" and len(sys.argv) == 1:
     main()
+
+
+# ---------------------------------------------------------------- parity/shift input copies
+def xc_accesses(RS=80, CA=1648, CB=5056, W=112, TH=16, window=True, dummy=0):
+    """The xc copies (xbo(b, a, r, P) = b CB + a CA + r RS + P, bf16 elements) of the Gram pass
+    (c1p8_moments_codes_kernel<1>) and the window moments pass: staging (16 lanes per input row,
+    lane c writes pairs 4c..4c+3 of the three shifts of both parities: 6 ds_write_b64), then the
+    B-fragment ds_read_b128 of one MFMA step -- pixel-pair taps (Gram pass) or 6x6 window
+    footprint columns (window pass)."""
+    cpr, segs, Wp = W // 8, W // 16, W // 2
+    xbo = lambda b, a, r, P: b * CB + a * CA + r * RS + P
+    acc = []
+    for b in range(2):
+        for a in range(3):
+            addrs = []
+            for lane in range(64):
+                t = lane          # first wave: rows 0..3
+                r, c = t >> 4, t & 15
+                addrs.append(2 * xbo(b, a, r, 4 * c) if c < cpr else None)
+            acc.append((f"staging write b{b} a{a}", "write_b64", addrs, 2 * 5 / 4))
+    if not window:
+        for tt in range(2):
+            for ks in range(4):
+                addrs = []
+                for lane in range(64):
+                    gq, col = lane >> 4, lane & 15
+                    t = 16 * tt + col
+                    if t >= 30:       # unused columns (30 is replaced by ones): any address
+                        t = dummy
+                    ky, k2 = t // 6, t % 6 - 2
+                    bb, ba = k2 & 1, (k2 >> 1 if k2 >= 0 else -1) + 1
+                    kb = 4 * ks + gq
+                    r, P0 = kb // segs, 8 * (kb % segs)
+                    addrs.append(2 * xbo(bb, ba, r + ky, P0))
+                acc.append((f"pair-tap B read tile{tt} step{ks}", "read_b128", addrs, 7 / 4))
+    else:
+        gpr = Wp // 8
+        for u in range(3):
+            for j in range(4):
+                addrs = []
+                for lane in range(64):
+                    gq, col = lane >> 4, lane & 15
+                    o = 16 * u + col
+                    m = 4 * j + gq
+                    hpl, gi = divmod(m, gpr)
+                    if o < 36:
+                        oy, ox = divmod(o, 6)
+                        addrs.append(2 * xbo(ox & 1, ox >> 1, 2 * hpl + oy, 8 * gi))
+                    else:
+                        addrs.append(2 * (2 * CB + (0 if o == 36 else 8)))
+                acc.append((f"window B read col tile{u} step{j}", "read_b128", addrs, 3.5 / 4))
+    return acc
+
+
+def xc_search(window, dummy=0):
+    res = []
+    for rs in range(64, 64 + 8 * 16, 8):
+        for cap in range(0, 16):
+            CA = 20 * rs + 8 * cap
+            for cbp in range(0, 16):
+                CB = 3 * CA + 8 * cbp
+                acc = xc_accesses(rs, CA, CB, window=window, dummy=dummy)
+                tot = sum(extra_cycles(k, a) * w for _, k, a, w in acc) / sum(w for *_, w in acc)
+                res.append((round(tot, 3), 2 * CB * 2, rs, CA, CB))
+    res.sort()
+    return res[:5]
+
+
+def main2():
+    report("xc copies, pair-tap reads (Gram pass), current strides", xc_accesses(window=False))
+    report("xc copies, window reads (window moments), current strides", xc_accesses(window=True))
+    print("best strides for the pair-tap reads (extra/instr, LDS B, RS, CA, CB):", xc_search(False))
+    print("best strides for the window reads:", xc_search(True))
+    for dm in (29, 28, 24, 18):
+        print(f"pair-tap reads with the unused columns reading tap {dm}:", xc_search(False, dm)[:2])
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "xc":
+    main2()
