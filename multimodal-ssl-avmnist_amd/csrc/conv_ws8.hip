@@ -389,11 +389,17 @@ __global__ __launch_bounds__(256, L::OCC) void conv_ws8_kernel(
 
 // ----------------------------------------------------------------------------- layer table
 //        CIN COUT K PAD  H   W  TH NS NCW NKW GB OCC PS RP
-typedef W8<8, 16, 5, 2, 56, 56, 14, 1, 1, 1, 2, 2, 8, 7> F8A2;     // audio conv2 forward
+#ifndef F8A2_T
+#define F8A2_T 14, 1, 1, 1, 2, 3, 8, 7   // OCC 3: 958 vs 986 us at N = 28672 (tools/build_variants.sh)
+#endif
+#ifndef D8A2_T
+#define D8A2_T 8, 1, 1, 1, 1, 3, 16, 12
+#endif
+typedef W8<8, 16, 5, 2, 56, 56, F8A2_T> F8A2;     // audio conv2 forward
 typedef W8<16, 32, 5, 2, 28, 28, 14, 1, 1, 1, 1, 2, 16, 12> F8A3;  // audio conv3
 typedef W8<32, 64, 5, 2, 14, 14, 14, 1, 2, 2, 1, 2, 32, 4> F8A4;   // audio conv4
 typedef W8<32, 64, 5, 0, 14, 14, 10, 2, 2, 2, 1, 2, 32, 4> F8I2;   // image conv2
-typedef W8<16, 8, 5, 2, 56, 56, 8, 1, 1, 1, 1, 3, 16, 12> D8A2;    // audio conv2 input gradient
+typedef W8<16, 8, 5, 2, 56, 56, D8A2_T> D8A2;    // audio conv2 input gradient
 typedef W8<32, 16, 5, 2, 28, 28, 14, 1, 1, 1, 1, 2, 32, 4> D8A3;   // audio conv3
 typedef W8<64, 32, 5, 2, 14, 14, 14, 1, 2, 2, 2, 2, 96, 4> D8A4;   // audio conv4
 typedef W8<64, 32, 5, 4, 10, 10, 14, 1, 2, 2, 2, 2, 96, 4> D8I2;   // image conv2
