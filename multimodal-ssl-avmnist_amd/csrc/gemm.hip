@@ -387,8 +387,17 @@ __device__ __forceinline__ void db_partial(const DbArgs& d, int b) {
 __device__ __forceinline__ void db_final(const DbArgs& d, int b) {
   const int c = b * 256 + (int)threadIdx.x;
   if (c >= d.O) return;
+  // fixed chunk order; 4 loads in flight per step (the sum stays sequential)
   float s = 0.f;
-  for (int rc = 0; rc < d.nrc; ++rc) s += d.part[(size_t)rc * d.O + c];
+  int rc = 0;
+  for (; rc + 4 <= d.nrc; rc += 4) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = d.part[(size_t)(rc + u) * d.O + c];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s += v[u];
+  }
+  for (; rc < d.nrc; ++rc) s += d.part[(size_t)rc * d.O + c];
   d.db[c] = s;
 }
 
@@ -415,7 +424,18 @@ __global__ __launch_bounds__(256) void gemm_pair_kernel(GemmArgs p1, int n1, int
 }
 
 // C = alpha * sum_{z < S} ws[z] (+bias) (+beta C), fixed split order; blocks >= nmain (when
-// the launch carries a bias gradient) fold its chunk partials instead
+// the launch carries a bias gradient) fold its chunk partials instead.  A thread owns 4
+// consecutive outputs (16-byte partial loads when N % 4 == 0) and keeps 4 splits' loads in
+// flight; each output's sum still runs z = 0, 1, ... in order (bit-identical to one at a time).
+__device__ __forceinline__ void splitk_out(float* __restrict__ C, long long ldc,
+                                           const float* __restrict__ bias, float alpha,
+                                           float beta, int m, int n, float s) {
+  float* c = C + (size_t)m * ldc + n;
+  float v = alpha * s + (bias ? bias[n] : 0.f);
+  if (beta != 0.f) v += beta * *c;
+  *c = v;
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S,
                                                             int M, int N, float* __restrict__ C,
                                                             long long ldc,
@@ -427,14 +447,36 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     return;
   }
   const long long MN = (long long)M * N;
+  if ((N & 3) == 0 && (reinterpret_cast<uintptr_t>(ws) & 15) == 0) {
+    for (long long i = 4 * (blockIdx.x * 256ll + threadIdx.x); i < MN; i += 4ll * nmain * 256) {
+      f4 s = f4{0.f, 0.f, 0.f, 0.f};
+      int z = 0;
+      for (; z + 4 <= S; z += 4) {
+        f4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f4*>(ws + (size_t)(z + u) * MN + i);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s += v[u];
+      }
+      for (; z < S; ++z) s += *reinterpret_cast<const f4*>(ws + (size_t)z * MN + i);
+      const int m = (int)(i / N), n = (int)(i % N);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) splitk_out(C, ldc, bias, alpha, beta, m, n + e, s[e]);
+    }
+    return;
+  }
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < MN; i += (long long)nmain * 256) {
     float s = 0.f;
-    for (int z = 0; z < S; ++z) s += ws[(size_t)z * MN + i];
-    const int m = (int)(i / N), n = (int)(i % N);
-    float* c = C + (size_t)m * ldc + n;
-    float v = alpha * s + (bias ? bias[n] : 0.f);
-    if (beta != 0.f) v += beta * *c;
-    *c = v;
+    int z = 0;
+    for (; z + 4 <= S; z += 4) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = ws[(size_t)(z + u) * MN + i];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s += v[u];
+    }
+    for (; z < S; ++z) s += ws[(size_t)z * MN + i];
+    splitk_out(C, ldc, bias, alpha, beta, (int)(i / N), (int)(i % N), s);
   }
 }
 
@@ -501,7 +543,8 @@ void launch_splitk_reduce(const Plan& pl, const GemmArgs& a, hipStream_t st, con
   const int nd = (d && d->db) ? avd_cdiv(d->O, 256) : 0;
   if (pl.splits > 1) {
     const long long MN = (long long)a.M * a.N;
-    const int blocks = (int)std::min<long long>(avd_cdiv(MN, 256), 4096);
+    const int per = (a.N & 3) == 0 ? 4 : 1;     // outputs per thread (the kernel's vector path)
+    const int blocks = (int)std::min<long long>(avd_cdiv(avd_cdiv(MN, per), 256), 4096);
     splitk_reduce_kernel<<<blocks + nd, 256, 0, st>>>(a.ws, pl.splits, a.M, a.N, a.C, a.ldc, a.bias,
                                                       a.alpha, a.beta, blocks, d ? *d : DbArgs{});
   } else if (nd) {
