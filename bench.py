@@ -356,10 +356,35 @@ def main():
     t_idx = min(1, args.warmup - 1)
     if use_graph and t_idx >= eng.graph.warmup:
         t_idx = -1
+    dominant = hbm_dom = watch = None
+
+    def pick_watch():
+        """The dominant launch (largest summed time in the timed eager warm-up step) and the
+        largest HBM-bound one (roofline_hbm: when the dominant launch trades HBM bytes for
+        recompute it is not a streaming kernel)."""
+        summ = wtimer.summary() if wtimer is not None else {}
+        dom = max(summ, key=lambda k: summ[k]["ms"]) if summ else None
+        if args.dominant:
+            if args.dominant not in summ:
+                raise SystemExit(f"--dominant {args.dominant!r}: no such launch key")
+            dom = args.dominant
+        hk = [k for k in summ if k != dom and
+              summ[k]["bytes"] / (HBM_PEAK_GBS * 1e9) >= summ[k]["flops"] / (MFMA_PEAK_TFS[args.dtype] * 1e12)]
+        hd = max(hk, key=lambda k: summ[k]["ms"]) if hk else None
+        return summ, dom, hd, [k for k in (dom, hd) if k is not None] or None
+
+    summ = {}
     for i in range(args.warmup):
         ops.TIMER = ops.KernelTimer() if i == t_idx else None
         wtimer = ops.TIMER or wtimer
         step(i)
+        if i == t_idx:
+            ops.TIMER = None
+            summ, dominant, hbm_dom, watch = pick_watch()
+            if use_graph and watch and not args.probe_dominant:
+                # in-graph spans of the watched launch sites, captured with the step: their
+                # duration inside the replayed timed region (no host hook exists there)
+                ops.SPANS = ops.SpanTimer(device, watch)
     ops.TIMER = None
     if use_graph and args.workload == "simclr":
         # SimCLR draws a modality pair per step (one captured graph per pair): capture all four
@@ -367,18 +392,8 @@ def main():
         for m in range(4):
             while eng.graph.segments((m, B)) is None:
                 eng.step(pool[0], mode=m)
-    summ = wtimer.summary() if wtimer is not None else {}
-    dominant = max(summ, key=lambda k: summ[k]["ms"]) if summ else None
-    if args.dominant:
-        if args.dominant not in summ:
-            raise SystemExit(f"--dominant {args.dominant!r}: no such launch key")
-        dominant = args.dominant
-    # the largest HBM-bound launch as well (roofline_hbm): when the dominant launch trades HBM
-    # bytes for recompute (the audio conv1 moments pass) it is not a streaming kernel
-    hbm_keys = [k for k in summ if k != dominant and
-                summ[k]["bytes"] / (HBM_PEAK_GBS * 1e9) >= summ[k]["flops"] / (MFMA_PEAK_TFS[args.dtype] * 1e12)]
-    hbm_dom = max(hbm_keys, key=lambda k: summ[k]["ms"]) if hbm_keys else None
-    watch = [k for k in (dominant, hbm_dom) if k is not None] or None
+    if dominant is None and watch is None and wtimer is not None:
+        summ, dominant, hbm_dom, watch = pick_watch()
     ops.TIMER = None if use_graph else ops.KernelTimer(only=watch)
 
     if args.probe_dominant:
@@ -395,6 +410,9 @@ def main():
                   flush=True)
         return
 
+    spans = ops.SPANS
+    if spans is not None:
+        spans.reset()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -413,9 +431,11 @@ def main():
     lv = loss.item()
     if not math.isfinite(lv):
         raise SystemExit(f"non-finite loss {lv}")
+    in_graph = spans.read() if spans is not None else {}
+    ops.SPANS = None
     if use_graph:
-        # the dominant launch's duration, HIP events around it, from eager steps after the
-        # timed region (inside a replayed graph there is no per-launch host hook)
+        # HIP events around the watched launches in eager steps after the timed region as well
+        # (eager_avg_launch_us); the in-graph spans of the timed region are the primary figure
         eng.use_graph = False
         ops.TIMER = ops.KernelTimer(only=watch)
         for i in range(args.warmup + args.steps, args.warmup + args.steps + 3):
@@ -423,6 +443,12 @@ def main():
         torch.cuda.synchronize()
 
     timed = ops.TIMER.summary()
+    eager = dict(timed)
+    for k in list(timed):
+        sp = in_graph.get(k.replace(" @side", ""))
+        if sp:
+            n, us, nb, fl = sp
+            timed[k] = {"calls": n, "ms": us / 1e3, "bytes": nb * n, "flops": fl * n, "in_graph": True}
     if dominant is None and timed:
         dominant = max(timed, key=lambda k: timed[k]["ms"])
 
@@ -439,13 +465,19 @@ def main():
             ach, peak, unit = nb / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
         else:
             ach, peak, unit = fl / avg_s / 1e12, peak_tf, "TFLOP/s"
-        return {"bound": "hbm" if hbm_bound else "mfma", "kernel": k,
-                "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
-                "traffic": load_traffic(args.traffic, k),
-                "avg_launch_us": round(avg_s * 1e6, 2),
-                "algorithmic_bytes": int(nb), "algorithmic_flops": int(fl),
-                "kernel_share_of_step": round(d["ms"] / (3 if use_graph else args.steps) /
-                                              (elapsed * 1e3 / args.steps), 4)}
+        r = {"bound": "hbm" if hbm_bound else "mfma", "kernel": k,
+             "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
+             "traffic": load_traffic(args.traffic, k),
+             "avg_launch_us": round(avg_s * 1e6, 2),
+             "timing": ("in-graph span marks over the timed region" if d.get("in_graph") else
+                        "HIP events, eager steps" + (" after the timed region" if use_graph else "")),
+             "algorithmic_bytes": int(nb), "algorithmic_flops": int(fl),
+             "kernel_share_of_step": round(d["ms"] / (args.steps if d.get("in_graph") or not use_graph else 3) /
+                                           (elapsed * 1e3 / args.steps), 4)}
+        if d.get("in_graph") and k in eager:
+            e = eager[k]
+            r["eager_avg_launch_us"] = round(e["ms"] / e["calls"] * 1e3, 2)
+        return r
 
     def isolated(k, reps=10):
         """The launch replayed alone (same inputs, its own stream idle otherwise), HIP events

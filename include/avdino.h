@@ -557,6 +557,10 @@ int avd_cl_c1r5_codes_combine(const float* moments, const void* wk, const float*
 /* Timeline mark: marks[idx] = the device real-time counter (100 MHz ticks) when the stream
  * reaches this launch (tools: phase timing of a replayed step without a profiler). */
 int avd_mark(unsigned long long* marks, int idx, void* stream);
+/* Launch span marks around one launch site (bench.py's in-graph kernel duration): end = 0
+ * stores the counter in spans[3 slot]; end = 1 adds (counter - spans[3 slot]) to spans[3 slot + 1]
+ * and 1 to spans[3 slot + 2]. */
+int avd_mark_span(unsigned long long* spans, int slot, int end, void* stream);
 int avd_counters_add(long long* arena, const long long* idx, const long long* val, int n,
                      void* stream);
 

@@ -55,6 +55,7 @@ PROTOS = {
     "avd_cl_c1r5_codes_combine": [P, P, P, P, P, P, L, P, P, P, P, P, I, P],
     "avd_counters_add": [P, P, P, I, P],
     "avd_mark": [P, I, P],
+    "avd_mark_span": [P, I, I, P],
     "avd_cl_conv_dgrad_bnreduce": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "avd_cl_conv_dgrad_bnapply": [P, P, I, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "avd_cl_conv_wgrad_bnapply": [P, P, P, I, P, P, P, I, P, I, I, I, I, I, I, I, I, P],

@@ -81,9 +81,48 @@ TIMER = None
 
 
 def _timed(key, nbytes, flops, fn):
+    if SPANS is not None:
+        return SPANS.wrap(key, nbytes, flops, fn)
     if TIMER is None:
         return fn()
     return TIMER.wrap(key, nbytes, flops, fn)
+
+
+class SpanTimer:
+    """In-graph duration of selected launch sites (bench.py's live roofline of a replayed step):
+    span marks (avd_mark_span, the device real-time counter) on the launching stream before and
+    after each launch of a watched key, captured into the step's graph with it, so every
+    replay of the timed region adds its duration.  Keys are matched without KernelTimer's
+    " @side" suffix (inside a capture every launch is on a non-default stream)."""
+
+    def __init__(self, device, keys, cap=64):
+        self.keys = {k.replace(" @side", "") for k in keys}
+        self.slots = {}
+        self.info = {}
+        self.buf = torch.zeros(3 * cap, dtype=torch.int64, device=device)
+
+    def wrap(self, key, nbytes, flops, fn):
+        if key not in self.keys or len(self.slots) >= self.buf.numel() // 3 and key not in self.slots:
+            return fn()
+        slot = self.slots.setdefault(key, len(self.slots))
+        self.info[key] = (nbytes, flops)
+        st = torch.cuda.current_stream().cuda_stream
+        call("avd_mark_span", p(self.buf), slot, 0, st)
+        out = fn()
+        call("avd_mark_span", p(self.buf), slot, 1, st)
+        return out
+
+    def reset(self):
+        self.buf.zero_()
+
+    def read(self):
+        """{key: (launches, total us, bytes per launch, flops per launch)} since reset()."""
+        torch.cuda.synchronize()
+        b = self.buf.view(-1, 3).cpu().tolist()
+        return {k: (b[s][2], b[s][1] / 100.0) + self.info[k] for k, s in self.slots.items() if b[s][2]}
+
+
+SPANS = None
 
 
 # Scratch allocation epoch: bumped whenever a workspace / scratch buffer is (re)allocated.  A

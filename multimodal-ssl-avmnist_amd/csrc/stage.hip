@@ -60,7 +60,28 @@ namespace {
 __global__ void mark_kernel(unsigned long long* __restrict__ marks, int idx) {
   if (threadIdx.x == 0) marks[idx] = wall_clock64();
 }
+
+// Launch spans: spans[3 slot] = the counter at the begin mark, spans[3 slot + 1] += end - begin,
+// spans[3 slot + 2] += 1 -- the in-graph duration of one launch site summed over replays.
+__global__ void mark_span_kernel(unsigned long long* __restrict__ spans, int slot, int end) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t = wall_clock64();
+  unsigned long long* s = spans + 3 * (size_t)slot;
+  if (!end) {
+    s[0] = t;
+  } else {
+    s[1] += t - s[0];
+    s[2] += 1;
+  }
+}
 }  // namespace
+
+extern "C" int avd_mark_span(unsigned long long* spans, int slot, int end, void* stream) {
+  if (!spans || slot < 0) return AVD_ERR_ARG;
+  mark_span_kernel<<<1, 64, 0, avd_stream(stream)>>>(spans, slot, end);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
 
 extern "C" int avd_mark(unsigned long long* marks, int idx, void* stream) {
   if (!marks || idx < 0) return AVD_ERR_ARG;
