@@ -107,7 +107,13 @@ typedef __attribute__((ext_vector_type(4))) float f4;
 template <int MODE>
 struct GemmT { typedef float T; static constexpr int LDK = 33; };
 template <>
-struct GemmT<2> { typedef bf16 T; static constexpr int LDK = 40; };
+struct GemmT<2> { typedef bf16 T; static constexpr int LDK = 32; };
+
+// bf16 tiles: 64-byte rows, the 16-byte chunk c of row r stored at chunk c ^ ((r >> 1) & 3).  The
+// MFMA fragment reads (16 rows x one chunk per 16 lanes, ds_read_b128) and the staging writes
+// (ds_write_b64) are then bank-conflict free; the LAY_R staging also pairs rows of opposite
+// parity in each 16-lane write group (tools/lds_conflicts.py gemm).
+__device__ __forceinline__ int gsw(int r, int k) { return r * 32 + (((k >> 3) ^ ((r >> 1) & 3)) << 3) + (k & 7); }
 
 // Operand layouts of a (rows x 32) tile of X with element (r, k) at X[r*sr + k*sk]:
 // LAY_K: k contiguous & 16B aligned rows (float4 along k); LAY_R: rows contiguous (float4 along
@@ -196,7 +202,7 @@ __device__ __forceinline__ void store_tile(const TileRegs<ROWS>& t, long long sr
     for (int i = 0; i < ROWS / 32; ++i) {
       const int e4 = tid + 256 * i;
       const int r = e4 >> 3, k = (e4 & 7) * 4;
-      typename GemmT<MODE>::T* d = S + r * LDK + k;
+      typename GemmT<MODE>::T* d = S + (MODE == 2 ? gsw(r, k) : r * LDK + k);
       if constexpr (MODE == 2) {
         // 4 bf16 = one 8-byte LDS store
         const unsigned lo = pack_bf16x2(t.v[4 * i], t.v[4 * i + 1]);
@@ -213,13 +219,27 @@ __device__ __forceinline__ void store_tile(const TileRegs<ROWS>& t, long long sr
       const int b = tid + 256 * i;
       if (b >= 2 * ROWS) continue;
       const int kb = b & 7, r = (b >> 3) * 4;                   // as load_tile<LAY_R>
+      if constexpr (MODE == 2) {
+        // odd row blocks write their rows rotated by one (row r + (j + 1) % 4 at step j): the two
+        // row blocks of a 16-lane group then hit opposite 64-byte halves of the bank row
+        const bool odd = (b >> 3) & 1;
+        uint2 w[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        typename GemmT<MODE>::T* d = S + (r + j) * LDK + 4 * kb;
-        const float* v = &t.v[16 * i + 4 * j];
-        if constexpr (MODE == 2) {
-          *reinterpret_cast<uint2*>(d) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-        } else {
+        for (int j = 0; j < 4; ++j) {
+          const float* v = &t.v[16 * i + 4 * j];
+          w[j] = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int jr = odd ? (j + 1) & 3 : j;
+          const uint2 wj = odd ? w[(j + 1) & 3] : w[j];
+          *reinterpret_cast<uint2*>(S + gsw(r + jr, 4 * kb)) = wj;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          typename GemmT<MODE>::T* d = S + (r + j) * LDK + 4 * kb;
+          const float* v = &t.v[16 * i + 4 * j];
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) d[kk] = v[kk];
         }
@@ -232,7 +252,7 @@ __device__ __forceinline__ void store_tile(const TileRegs<ROWS>& t, long long sr
       const int e = tid + 256 * i;
       int r, k;
       if (kfast) { r = e >> 5; k = e & 31; } else { k = e / ROWS; r = e % ROWS; }
-      lds_put<MODE>(S + r * LDK + k, t.v[i]);
+      lds_put<MODE>(S + (MODE == 2 ? gsw(r, k) : r * LDK + k), t.v[i]);
     }
   }
 }
@@ -302,10 +322,11 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& p, int tn, int tm, int
     const T* bs = Bs[cur] + (BN / 2 * wn + r16) * LDK;
     if constexpr (MODE == 2) {
       bf16x8 a[TI], b[TJ];
+      const int gc = 8 * (g ^ ((r16 >> 1) & 3));     // the swizzled chunk (tile rows are r16 mod 16)
 #pragma unroll
-      for (int i = 0; i < TI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(as + 16 * i * LDK + 8 * g);
+      for (int i = 0; i < TI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(as + 16 * i * LDK + gc);
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(bs + 16 * j * LDK + 8 * g);
+      for (int j = 0; j < TJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(bs + 16 * j * LDK + gc);
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll

@@ -202,3 +202,34 @@ def main2():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "xc":
     main2()
+
+
+# ---------------------------------------------------------------- bf16 GEMM tiles (gemm.hip)
+def gemm_tiles(swizzle=True, ldk=32):
+    """gemm_tile<2> (Linear forward / backward, gemm_pair_kernel): the MFMA fragment reads (lane
+    r16 = l & 15 reads 16 bytes of row r16 + 16 i, chunk g = l >> 4) and the staging writes of
+    LAY_K (8 lanes per row, 8 bytes each) and LAY_R (row blocks of 4, rotated by one in odd
+    blocks) operands; 16-byte chunk c of row r at c ^ ((r >> 1) & 3) when swizzled."""
+    def at(r, k):
+        c = (k >> 3) ^ (((r >> 1) & 3) if swizzle else 0)
+        return 2 * (r * ldk + 8 * c + (k & 7))
+    acc = []
+    for i in range(4):
+        acc.append((f"fragment read tile {i}", "read_b128",
+                    [at(16 * i + (l & 15), 8 * (l >> 4)) for l in range(64)], 2))
+    for base in (0, 8):
+        acc.append((f"LAY_K write rows {base}..", "write_b64",
+                    [at(base + (l >> 3), 4 * (l & 7)) for l in range(64)], 0.5))
+    for j in range(4):
+        addrs = []
+        for l in range(64):
+            rb, kb = l >> 3, l & 7
+            jr = (j + 1) & 3 if (rb & 1 and swizzle) else j
+            addrs.append(at(4 * rb + jr, 4 * kb))
+        acc.append((f"LAY_R write step {j}", "write_b64", addrs, 0.5))
+    return acc
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "gemm":
+    report("bf16 GEMM tiles, LDK 40 unswizzled (round 3)", gemm_tiles(False, 40))
+    report("bf16 GEMM tiles, LDK 32 swizzled", gemm_tiles(True, 32))
