@@ -37,8 +37,16 @@ constexpr int C1R5_GMAX = 32;                              // BN groups served b
 constexpr int NCOPY = 6, CROWS = IH + 4;                     // copies: tx = -2..2, ones; rows: pad 2
 constexpr int XS_R = IH + 4, XS_C = IW + 4 + 4;              // staged image, 2-pixel halo (+ pad)
 constexpr int LDS_X = XS_R * XS_C;                           // bf16 elements
-constexpr int LDS_CP = NCOPY * CROWS * VW;
-constexpr int LDS_DZ = C * IH * VW;
+// shifted copies: 48-element rows (32 used) and 1544-element copies, so the 16 taps of a
+// B-fragment ds_read_b128 spread over the bank slots (2 extra cycles per read instead of 16,
+// tools/lds_conflicts.py c1r5)
+constexpr int CP_RS = 48, CP_CS = CROWS * CP_RS + 8;
+constexpr int LDS_CP = NCOPY * CP_CS;
+// dZ channel stride: 28 rows x 32 columns + 16 pad elements (1824 B = 32 mod 256): the 16
+// channels of an A-fragment ds_read_b128 fall on 16 distinct 16-byte bank slots (no pad: all on
+// one, 16-way), tools/lds_conflicts.py c1r5
+constexpr int CSTR = IH * VW + 16;
+constexpr int LDS_DZ = C * CSTR;
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f4;
@@ -80,7 +88,7 @@ __global__ __launch_bounds__(256, 2) void c1r5_moments_codes_kernel(
       const unsigned lo = (rv && c0 < IW) ? 0x3F80u : 0u, hi = (rv && c0 + 1 < IW) ? 0x3F80u : 0u;
       vw[k] = lo | (hi << 16);
     }
-    reinterpret_cast<u4*>(cp + 5 * CROWS * VW)[i] = v;
+    *reinterpret_cast<u4*>(cp + 5 * CP_CS + row * CP_RS + 8 * seg) = v;
   }
 
   // this lane's taps: tile 0 = taps 0..15, tile 1 = taps 16..31 (25 = ones, > 25 = zero)
@@ -92,9 +100,9 @@ __global__ __launch_bounds__(256, 2) void c1r5_moments_codes_kernel(
     tzero[tt] = t > KK;
     if (t < KK) {
       const int ty = t / 5 - 2, tx = t % 5 - 2;
-      toff[tt] = (tx + 2) * CROWS * VW + (ty + 2) * VW + 8 * g;
+      toff[tt] = (tx + 2) * CP_CS + (ty + 2) * CP_RS + 8 * g;
     } else {
-      toff[tt] = 5 * CROWS * VW + 2 * VW + 8 * g;   // ones copy, row offset 0 (rows start at 2)
+      toff[tt] = 5 * CP_CS + 2 * CP_RS + 8 * g;   // ones copy, row offset 0 (rows start at 2)
     }
   }
 
@@ -137,7 +145,7 @@ __global__ __launch_bounds__(256, 2) void c1r5_moments_codes_kernel(
     __syncthreads();                      // xs complete; the previous sample's k-loop is done
     // the sample's codes to LDS (a gz vector's window codes sit in another thread's vector):
     // 3136 B in the space of copies 3-4, which are rebuilt after the codes are consumed
-    unsigned short* cst = reinterpret_cast<unsigned short*>(cp + 3 * CROWS * VW);
+    unsigned short* cst = reinterpret_cast<unsigned short*>(cp + 3 * CP_CS);
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
       const int e = tid + 256 * j;
@@ -150,15 +158,22 @@ __global__ __launch_bounds__(256, 2) void c1r5_moments_codes_kernel(
     for (int j = 0; j < VPT; ++j) {
       const int e = tid + 256 * j;
       if (e >= NXV && e < NXV + NGV) {
-        const int q = e - NXV, w = q >> 2, c0 = 8 * (q & 3);
+        const int q = e - NXV, w = q >> 2, kq = q & 3, c0 = 8 * kq;
         const int hp = w / WP, wp = w - hp * WP;
-        const unsigned gw[4] = {vv[j].x, vv[j].y, vv[j].z, vv[j].w};
+        // the four lanes of a window (channel octets kq) walk their channels rotated by kq, so
+        // their dword stores at each step fall on four different banks
+        const unsigned g8[8] = {vv[j].x, vv[j].y, vv[j].z, vv[j].w, vv[j].x, vv[j].y, vv[j].z, vv[j].w};
         const unsigned short k0 = cst[w * 8 + (c0 >> 2)], k1 = cst[w * 8 + (c0 >> 2) + 1];
+        const unsigned kw = (unsigned)k0 | ((unsigned)k1 << 16);
 #pragma unroll
         for (int cc = 0; cc < 8; ++cc) {
-          const unsigned nib = ((cc < 4 ? k0 : k1) >> (4 * (cc & 3))) & 0xFu;
-          const unsigned gv = (gw[cc >> 1] >> (16 * (cc & 1))) & 0xffffu;
-          bf16* d = dz + ((c0 + cc) * IH + 2 * hp) * VW + 2 * wp;
+          const int ch = (cc + kq) & 7;                       // channel c0 + ch
+          const unsigned nib = (kw >> (4 * ch)) & 0xFu;
+          // bf16 of channel ch: dword ch >> 1 (a lane-dependent index: select among the four)
+          const int dsel = ch >> 1;
+          const unsigned gdw = dsel == 0 ? g8[0] : dsel == 1 ? g8[1] : dsel == 2 ? g8[2] : g8[3];
+          const unsigned gv = (gdw >> (16 * (ch & 1))) & 0xffffu;
+          bf16* d = dz + (c0 + ch) * CSTR + 2 * hp * VW + 2 * wp;
           // row 2hp: positions 1, 2 (k = 0, 1); row 2hp+1: positions 3, 4 (k = 2, 3)
           const unsigned r0 = (nib == 1u ? gv : 0u) | ((nib == 2u ? gv : 0u) << 16);
           const unsigned r1 = (nib == 3u ? gv : 0u) | ((nib == 4u ? gv : 0u) << 16);
@@ -183,15 +198,15 @@ __global__ __launch_bounds__(256, 2) void c1r5_moments_codes_kernel(
         const unsigned hi = c0 + 1 < IW ? (unsigned)srow[c0 + 1] : 0u;
         vw[k] = lo | (hi << 16);
       }
-      reinterpret_cast<u4*>(cp)[i] = v;
+      *reinterpret_cast<u4*>(cp + ci * CP_CS + row * CP_RS + 8 * seg) = v;
     }
     __syncthreads();
     // ---- k-loop: image rows, a wave every fourth one
     for (int r = wave; r < IH; r += 4) {
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(dz + (r16 * IH + r) * VW + 8 * g);
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(dz + ((16 + r16) * IH + r) * VW + 8 * g);
-      const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(cp + toff[0] + r * VW);
-      bf16x8 x1 = *reinterpret_cast<const bf16x8*>(cp + toff[1] + r * VW);
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(dz + r16 * CSTR + r * VW + 8 * g);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(dz + (16 + r16) * CSTR + r * VW + 8 * g);
+      const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(cp + toff[0] + r * CP_RS);
+      bf16x8 x1 = *reinterpret_cast<const bf16x8*>(cp + toff[1] + r * CP_RS);
       if (tzero[1]) x1 = bf16x8{};
       acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, x0, acc[0][0], 0, 0, 0);
       acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, x1, acc[0][1], 0, 0, 0);

@@ -233,3 +233,41 @@ def gemm_tiles(swizzle=True, ldk=32):
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "gemm":
     report("bf16 GEMM tiles, LDK 40 unswizzled (round 3)", gemm_tiles(False, 40))
     report("bf16 GEMM tiles, LDK 32 swizzled", gemm_tiles(True, 32))
+
+
+# ---------------------------------------------------------------- image conv1 routed moments
+def c1r5_accesses(cstr=28 * 32 + 16, rotate=True, cp_rs=48, cp_cs=32 * 48 + 8):
+    """c1r5_moments_codes_kernel (c1r5.hip): the dz scatter (ds_write_b32 per channel and row
+    pair; four lanes per window = four channel octets, walked rotated by octet), the
+    channel-major A-fragment reads of dz and the shifted-copy B-fragment reads (ds_read_b128)."""
+    IH, VW, WP, KK = 28, 32, 14, 25
+    acc = []
+    for cc in range(8):
+        addrs = []
+        for l in range(64):
+            q = l                     # first 64 gz vectors of a sample
+            w, k = q >> 2, q & 3
+            c = 8 * k + (((cc + k) & 7) if rotate else cc)
+            hp, wp = divmod(w, WP)
+            addrs.append((c * cstr + 2 * hp * VW + 2 * wp) * 2)
+        acc.append((f"dz scatter channel step {cc}", "write_b32", addrs, 2 * 196 / 64 / 8))
+    for a in range(2):
+        acc.append((f"dZ A fragment, channels {16 * a}..", "read_b128",
+                    [((16 * a + (l & 15)) * cstr + 8 * (l >> 4)) * 2 for l in range(64)], 7 / 4))
+    for tt in range(2):
+        addrs = []
+        for l in range(64):
+            g, r16 = l >> 4, l & 15
+            t = 16 * tt + r16
+            if t < KK:
+                off = (t % 5) * cp_cs + (t // 5) * cp_rs + 8 * g
+            else:
+                off = 5 * cp_cs + 2 * cp_rs + 8 * g
+            addrs.append(off * 2)
+        acc.append((f"copy B fragment, tap tile {tt}", "read_b128", addrs, 7 / 4))
+    return acc
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "c1r5":
+    report("c1r5 moments, round 3 layout", c1r5_accesses(28 * 32, False, 32, 32 * 32))
+    report("c1r5 moments, padded dz / copies, rotated scatter", c1r5_accesses())
