@@ -23,6 +23,7 @@
 // Blocks own contiguous sample ranges of one BN group (G x R blocks); each writes one row of
 // MOMC5 = M [32][25] | Gram [25][25] | S [25] | sum dz [32] floats, reduced with avd_sum_rows.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -35,7 +36,7 @@ constexpr int HP = IH / 2, WP = IW / 2, NWIN = HP * WP;     // pooling windows p
 constexpr int MOMC5 = C * KK + KK * KK + KK + C;
 constexpr int C1R5_GMAX = 32;                              // BN groups served by the combine
 constexpr int NCOPY = 6, CROWS = IH + 4;                     // copies: tx = -2..2, ones; rows: pad 2
-constexpr int XS_R = IH + 4, XS_C = IW + 4 + 4;              // staged image, 2-pixel halo (+ pad)
+constexpr int XS_R = IH + 4, XS_C = 40;                     // staged image, 2-pixel halo, 16-B rows
 constexpr int LDS_X = XS_R * XS_C;                           // bf16 elements
 // shifted copies: 48-element rows (32 used) and 1544-element copies, so the 16 taps of a
 // B-fragment ds_read_b128 spread over the bank slots (2 extra cycles per read instead of 16,
@@ -52,6 +53,9 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f4;
 typedef __attribute__((ext_vector_type(4))) unsigned u4;
 typedef __attribute__((ext_vector_type(8))) unsigned short us8;   // raw bf16 bits
+typedef __attribute__((ext_vector_type(2))) unsigned short us2;
+typedef __attribute__((ext_vector_type(2))) unsigned us2x;
+typedef __attribute__((ext_vector_type(4))) short s4;
 
 template <int CTRL>
 __device__ __forceinline__ int dppi(int v) {
@@ -185,20 +189,29 @@ __global__ __launch_bounds__(256, 2) void c1r5_moments_codes_kernel(
     __syncthreads();                      // codes consumed: copies 3-4 may be rebuilt
     if (n + 1 < s_end) load(n + 1);       // in flight under this sample's copies and MFMAs
     // ---- the five shifted copies: copy[tx][row][col] = col < 28 ? x[row - 2][col + tx] : 0
+    // (one 16-byte chunk per thread: two aligned row reads and a funnel shift by tx + 2 pixels;
+    // the copy index is uniform over a wave -- 128 chunks per copy)
     for (int i = tid; i < 5 * CROWS * (VW / 8); i += 256) {
-      const int ci = i / (CROWS * (VW / 8)), rem = i - ci * (CROWS * (VW / 8));
+      const int ci = __builtin_amdgcn_readfirstlane(i / (CROWS * (VW / 8)));
+      const int rem = i - ci * (CROWS * (VW / 8));
       const int row = rem / (VW / 8), seg = rem - row * (VW / 8);
-      const bf16* srow = xs + row * XS_C + ci;                    // xs col = col + tx + 2
-      u4 v;
-      unsigned* vw = reinterpret_cast<unsigned*>(&v);
+      const u4 lo = *reinterpret_cast<const u4*>(xs + row * XS_C + 8 * seg);
+      const u4 hi = *reinterpret_cast<const u4*>(xs + row * XS_C + 8 * seg + 8);
+      const unsigned src[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      unsigned o[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int c0 = 8 * seg + 2 * k;
-        const unsigned lo = c0 < IW ? (unsigned)srow[c0] : 0u;
-        const unsigned hi = c0 + 1 < IW ? (unsigned)srow[c0 + 1] : 0u;
-        vw[k] = lo | (hi << 16);
+      for (int d = 0; d < 4; ++d) {
+        // elements 2d + ci, 2d + ci + 1 of src (ci wave-uniform: a scalar branch)
+        switch (ci) {
+          case 0: o[d] = src[d]; break;
+          case 1: o[d] = __builtin_amdgcn_alignbit(src[d + 1], src[d], 16); break;
+          case 2: o[d] = src[d + 1]; break;
+          case 3: o[d] = __builtin_amdgcn_alignbit(src[d + 2], src[d + 1], 16); break;
+          default: o[d] = src[d + 2]; break;
+        }
       }
-      *reinterpret_cast<u4*>(cp + ci * CP_CS + row * CP_RS + 8 * seg) = v;
+      if (seg == VW / 8 - 1) { o[2] = 0u; o[3] = 0u; }          // columns 28..31
+      *reinterpret_cast<u4*>(cp + ci * CP_CS + row * CP_RS + 8 * seg) = u4{o[0], o[1], o[2], o[3]};
     }
     __syncthreads();
     // ---- k-loop: image rows, a wave every fourth one
@@ -259,6 +272,245 @@ __global__ __launch_bounds__(256, 2) void c1r5_moments_codes_kernel(
       const int c = e - (C * KK + KK * KK + KK);
 #pragma unroll
       for (int wv = 0; wv < 4; ++wv) v += red[(wv * C + c) * 32 + KK];
+    }
+    o[e] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------- window moments
+// The same moments in window space (as the audio conv1's c1p8_moments_win_kernel): dz is
+// nonzero only at the coded pixel (ky, kx) of each 2x2 pooling window, so with the window's 6x6
+// input footprint x6[w][oy][ox] = x[2hp + oy - 2][2wp + ox - 2]
+//   M[c][dy][dx] = sum_{ky,kx} N[2ky+kx][c][(ky+dy)*6 + kx+dx],  N[k][c][o] = sum_w dz_k[c][w] x6[w][o]
+// and the pixel Gram is the fold of the window-footprint Gram G6 = sum_w x6 x6^T over the four
+// window positions (S from G6's ones column).  Wave o owns channel octet o: its A operand is the
+// pooled gradient of 8 channels read transposed from the [window slot][32 ch] tile and masked by
+// routing bits in registers -- no dz map, no scatter (the round-3 kernel's 16-way / 4-way LDS
+// bank conflicts).  Windows sit in slots hp * 16 + wp (wp 14, 15: zero padding, and their input
+// copies are zeroed so G6 sees no phantom windows); a k-step is 4 groups of 8 slots.
+#ifndef C1R5W_OCC
+#define C1R5W_OCC 3
+#endif
+constexpr int WSLOT = 16, NSLOT = HP * WSLOT;                 // 224 window slots per sample
+constexpr int WX_R = 16, WX_A = 560, WX_B = 1728;            // input copies: row / shift / parity
+constexpr int W_XS = 0, W_XC = W_XS + LDS_X, W_K1 = W_XC + 2 * WX_B, W_GZ = W_K1 + 16;
+constexpr int W_CDS = W_GZ + NSLOT * C;                        // u32 routing words follow (bf16 units)
+constexpr int W_END = W_CDS + 2 * (4 * 2 * (NSLOT / 2));
+constexpr int W_RED = 4 * 2 * 16 * 48 + 48 * 48;               // epilogue floats
+constexpr int W_LDS = (W_END * 2 > W_RED * 4 ? W_END * 2 : W_RED * 4);
+
+__global__ __launch_bounds__(256, C1R5W_OCC) void c1r5_moments_win_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ gz, const unsigned short* __restrict__ codes,
+    float* __restrict__ out, int B, int G, int R) {
+  static_assert(W_XC % 8 == 0 && W_GZ % 8 == 0 && W_CDS % 8 == 0, "16-byte aligned regions");
+  __shared__ __attribute__((aligned(16))) char lds[W_LDS];
+  bf16* sm = reinterpret_cast<bf16*>(lds);
+  bf16* xs = sm + W_XS;
+  bf16* xc = sm + W_XC;
+  bf16* gzs = sm + W_GZ;
+  unsigned* cds = reinterpret_cast<unsigned*>(sm + W_CDS);     // [octet][ky][pair]
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int gq = lane >> 4, col = lane & 15, q = col >> 2, p = col & 3;
+  const int grp = (int)blockIdx.x / R, rr = (int)blockIdx.x - grp * R;
+  const int s_begin = grp * B + (int)(((long long)B * rr) / R);
+  const int s_end = grp * B + (int)(((long long)B * (rr + 1)) / R);
+
+  // constant parts: zero image halo, zero padding slots / routing, the ones / zeros B columns
+  for (int i = tid; i < (W_END - W_XS) / 8; i += 256) reinterpret_cast<u4*>(sm)[i] = u4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  if (tid < 8) sm[W_K1 + tid] = (bf16)0x3F80u;                 // bf16 1.0 (W_K1 + 8.. stay 0)
+
+  // B columns: o = 16u + col < 36 reads copy (b, a) at row 2 hp + oy; 36 the ones, > 36 zeros
+  int boff[3], bmask[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int o = 16 * u + col, oy = o / 6, ox = o - 6 * oy;
+    bmask[u] = o < 36 ? -1 : 0;
+    boff[u] = o < 36 ? W_XC + (ox & 1) * WX_B + (ox >> 1) * WX_A + oy * WX_R
+                     : W_K1 + (o == 36 ? 0 : 8);
+  }
+  const unsigned rsh = 2 * (col & 7) + (col >> 3);            // routing bit of this A row
+  // G6 tiles (tu <= tv) of this wave: tiles wave and wave + 4 of (00 01 02 11 12 22)
+  const int gt0 = wave, gt1 = wave + 4;
+  auto tu_of = [](int t) { return t < 3 ? 0 : t < 5 ? 1 : 2; };
+  auto tv_of = [](int t) { return t < 3 ? t : t < 5 ? t - 2 : 2; };
+  f4 acc[2][3], ga[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    ga[t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 3; ++u) acc[t][u] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  u4 vv[VPT];
+  auto load = [&](int n) {
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int e = tid + 256 * j;
+      if (e < NXV) vv[j] = ldg16(x + (size_t)n * IH * IW + 8 * e);
+      else if (e < NXV + NGV) vv[j] = ldg16(gz + (size_t)n * NWIN * C + 8 * (e - NXV));
+      else if (e < NVEC) vv[j] = ldg16(codes + (size_t)n * NWIN * 8 + 8 * (e - NXV - NGV));
+    }
+  };
+  if (s_begin < s_end) load(s_begin);
+  for (int n = s_begin; n < s_end; ++n) {
+    __syncthreads();                      // the previous sample's k-loop is done with the tiles
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int e = tid + 256 * j;
+      if (e < NXV) {
+        const unsigned w4[4] = {vv[j].x, vv[j].y, vv[j].z, vv[j].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int pix = 8 * e + 2 * k, r = pix / IW, c = pix - r * IW;
+          *reinterpret_cast<unsigned*>(xs + (r + 2) * XS_C + c + 2) = w4[k];
+        }
+      } else if (e < NXV + NGV) {
+        const int qv = e - NXV, w = qv >> 2, hp = w / WP, wp = w - hp * WP;
+        *reinterpret_cast<u4*>(gzs + (hp * WSLOT + wp) * C + 8 * (qv & 3)) = vv[j];
+      }
+      // routing bits of one window (codes vectors: one per window, lanes = consecutive windows):
+      // per channel octet o and row tile ky a 16-bit word (bit 2c + kx), paired with the next
+      // window's in the high half (computed by every lane: the DPP reads the neighbour)
+      if (256 * j + 255 < NXV + NGV || 256 * j >= NVEC) continue;   // no codes vector in slot j
+      const int w = e - NXV - NGV;
+      const unsigned cw[4] = {vv[j].x, vv[j].y, vv[j].z, vv[j].w};
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        const unsigned v = cw[o];
+        const unsigned n0 = v & 0x11111111u, n1 = (v >> 1) & 0x11111111u, n2 = (v >> 2) & 0x11111111u;
+        unsigned rt[2] = {(n0 & ~n1) | ((n1 & ~n0) << 1), (n0 & n1) | (n2 << 1)};
+#pragma unroll
+        for (int ky = 0; ky < 2; ++ky) {
+          unsigned f = rt[ky];
+          f = (f | (f >> 2)) & 0x0F0F0F0Fu;
+          f = (f | (f >> 4)) & 0x00FF00FFu;
+          f = (f | (f >> 8)) & 0x0000FFFFu;
+          f |= (unsigned)dppi<0x101>((int)f) << 16;
+          if (e >= NXV + NGV && e < NVEC) {
+            const int hp = w / WP, wp = w - hp * WP;
+            if (!(wp & 1)) cds[(o * 2 + ky) * (NSLOT / 2) + ((hp * WSLOT + wp) >> 1)] = f;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (n + 1 < s_end) load(n + 1);       // in flight under this sample's copies and MFMAs
+    // parity / shift copies: xc[b][a][r][P] = x[r - 2][2(P + a - 1) + b] = xs[r][2P + 2a + b]
+    // (P 14, 15: zero); chunk (b, a, r, P0): one wave per (b, a), two aligned row reads
+    for (int i = tid; i < 6 * 32 * 2; i += 256) {
+      const int ba = __builtin_amdgcn_readfirstlane(i >> 6), b = ba / 3, a = ba - 3 * b;
+      const int r = (i >> 1) & 31, P0 = 8 * (i & 1);
+      const bf16* srow = xs + r * XS_C + 2 * P0;
+      const u4 l0 = *reinterpret_cast<const u4*>(srow), l1 = *reinterpret_cast<const u4*>(srow + 8);
+      const u4 l2 = *reinterpret_cast<const u4*>(srow + 16);
+      const unsigned d[12] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w, l2.x, l2.y, l2.z, l2.w};
+      unsigned o4[4];
+      // element 2(P + a) + b of the row: low (b = 0) / high (b = 1) half of dword P + a
+#pragma unroll
+      for (int dd = 0; dd < 4; ++dd) {
+        unsigned lo, hi;
+        switch (a) {
+          case 0: lo = d[2 * dd]; hi = d[2 * dd + 1]; break;
+          case 1: lo = d[2 * dd + 1]; hi = d[2 * dd + 2]; break;
+          default: lo = d[2 * dd + 2]; hi = d[2 * dd + 3]; break;
+        }
+        o4[dd] = b ? __builtin_amdgcn_perm(hi, lo, 0x07060302u) : __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+      }
+      if (P0) o4[3] = 0u;                                      // P = 14, 15: padding windows
+      *reinterpret_cast<u4*>(xc + b * WX_B + a * WX_A + r * WX_R + P0) = u4{o4[0], o4[1], o4[2], o4[3]};
+    }
+    __syncthreads();
+    // k-loop: 7 steps of 4 slot groups; wave = channel octet
+    for (int j = 0; j < 7; ++j) {
+      const int m = 4 * j + gq, hp = m >> 1, wp0 = 8 * (m & 1), s0 = hp * WSLOT + wp0;
+      const s4 g0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s4*)(gzs + (s0 + q) * C + 8 * wave + 4 * (p & 1)));
+      const s4 g1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s4*)(gzs + (s0 + 4 + q) * C + 8 * wave + 4 * (p & 1)));
+      const u4 rw0 = *reinterpret_cast<const u4*>(cds + (wave * 2 + 0) * (NSLOT / 2) + (s0 >> 1));
+      const u4 rw1 = *reinterpret_cast<const u4*>(cds + (wave * 2 + 1) * (NSLOT / 2) + (s0 >> 1));
+      const int bs = 2 * hp * WX_R + wp0;
+      u4 bv[3];
+#pragma unroll
+      for (int u = 0; u < 3; ++u) bv[u] = *reinterpret_cast<const u4*>(sm + (bs & bmask[u]) + boff[u]);
+      const us2x lo2 = __builtin_bit_cast(us2x, g0), hi2 = __builtin_bit_cast(us2x, g1);
+      const unsigned av[4] = {lo2.x, lo2.y, hi2.x, hi2.y};
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const u4 rw = t ? rw1 : rw0;
+        const unsigned rv[4] = {rw.x, rw.y, rw.z, rw.w};
+        unsigned am[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          am[d] = __builtin_bit_cast(unsigned, __builtin_bit_cast(us2, av[d]) *
+                                                   __builtin_bit_cast(us2, (rv[d] >> rsh) & 0x00010001u));
+        const bf16x8 A = __builtin_bit_cast(bf16x8, u4{am[0], am[1], am[2], am[3]});
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, __builtin_bit_cast(bf16x8, bv[u]), acc[t][u], 0, 0, 0);
+      }
+      // this wave's window-footprint Gram tiles (the B fragments are their own transposes)
+#pragma unroll
+      for (int gi = 0; gi < 2; ++gi) {
+        const int gt = gi ? gt1 : gt0;
+        if (gt < 6) {
+          const int tu = tu_of(gt), tv = tv_of(gt);
+          const u4 bu = tu == 0 ? bv[0] : tu == 1 ? bv[1] : bv[2];
+          const u4 bw = tv == 0 ? bv[0] : tv == 1 ? bv[1] : bv[2];
+          ga[gi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bu),
+                                                           __builtin_bit_cast(bf16x8, bw), ga[gi], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // ---- block row: N per wave (its octet), G6 tiles, folded to M / Gram / S / sum dz
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(lds);          // [4 waves][2 ky][16 rows][48 cols]
+  float* g6 = red + 4 * 2 * 16 * 48;                   // [48][48] (tiles tu <= tv)
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        red[((wave * 2 + t) * 16 + 4 * gq + i) * 48 + 16 * u + col] = acc[t][u][i];
+#pragma unroll
+  for (int gi = 0; gi < 2; ++gi) {
+    const int gt = gi ? gt1 : gt0;
+    if (gt < 6) {
+      const int tu = tu_of(gt), tv = tv_of(gt);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) g6[(16 * tu + 4 * gq + i) * 48 + 16 * tv + col] = ga[gi][i];
+    }
+  }
+  __syncthreads();
+  auto G6 = [&](int i, int jj) {           // symmetric: the lower tiles from the upper
+    return (i >> 4) <= (jj >> 4) ? g6[i * 48 + jj] : g6[jj * 48 + i];
+  };
+  float* o = out + ((size_t)rr * G + grp) * MOMC5;
+  for (int e = tid; e < MOMC5; e += 256) {
+    float v = 0.f;
+    if (e < C * KK) {
+      const int c = e / KK, t = e - c * KK, dy = t / 5, dx = t - 5 * dy;
+      const int ow = c >> 3, c8 = c & 7;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        v += red[((ow * 2 + (k >> 1)) * 16 + 8 * (k & 1) + c8) * 48 + ((k >> 1) + dy) * 6 + (k & 1) + dx];
+    } else if (e < C * KK + KK * KK) {
+      const int qq = e - C * KK, t1 = qq / KK, t2 = qq - KK * t1;
+      const int y1 = t1 / 5, x1 = t1 - 5 * y1, y2 = t2 / 5, x2 = t2 - 5 * y2;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        v += G6(((k >> 1) + y1) * 6 + (k & 1) + x1, ((k >> 1) + y2) * 6 + (k & 1) + x2);
+    } else if (e < C * KK + KK * KK + KK) {
+      const int t = e - C * KK - KK * KK, dy = t / 5, dx = t - 5 * dy;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v += G6(((k >> 1) + dy) * 6 + (k & 1) + dx, 36);
+    } else {
+      const int c = e - (C * KK + KK * KK + KK), ow = c >> 3, c8 = c & 7;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v += red[((ow * 2 + (k >> 1)) * 16 + 8 * (k & 1) + c8) * 48 + 36];
     }
     o[e] = v;
   }
@@ -539,7 +791,7 @@ int c1r5_rows(int N, int B) {
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, c1r5_moments_codes_kernel, 256, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, c1r5_moments_win_kernel, 256, 0) !=
             hipSuccess || per <= 0)
       per = 2;
     resident = cus * per;
@@ -620,8 +872,14 @@ int avd_cl_c1r5_moments_codes(const void* x, const void* gz, const unsigned shor
   const int R = avd_cl_c1r5_codes_rows(N, B, H, W);
   if (!R) return AVD_ERR_SHAPE;
   const int G = N / B;
-  c1r5_moments_codes_kernel<<<G * R, 256, 0, avd_stream(stream)>>>(
-      (const bf16*)x, (const bf16*)gz, codes, out, B, G, R);
+  // the window-space pass (c1r5_moments_win_kernel); AVDINO_C1R5_WIN=0 keeps the dz-map one
+  static const bool win = !getenv("AVDINO_C1R5_WIN") || atoi(getenv("AVDINO_C1R5_WIN")) != 0;
+  if (win)
+    c1r5_moments_win_kernel<<<G * R, 256, 0, avd_stream(stream)>>>(
+        (const bf16*)x, (const bf16*)gz, codes, out, B, G, R);
+  else
+    c1r5_moments_codes_kernel<<<G * R, 256, 0, avd_stream(stream)>>>(
+        (const bf16*)x, (const bf16*)gz, codes, out, B, G, R);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
