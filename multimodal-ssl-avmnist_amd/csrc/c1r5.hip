@@ -292,9 +292,13 @@ __global__ __launch_bounds__(256, 2) void c1r5_moments_codes_kernel(
 #define C1R5W_OCC 3
 #endif
 constexpr int WSLOT = 16, NSLOT = HP * WSLOT;                 // 224 window slots per sample
-constexpr int WX_R = 16, WX_A = 560, WX_B = 1728;            // input copies: row / shift / parity
+// input copies [parity][shift][P half][row][8 P]: B reads 0.67 extra cycles, copy writes 0
+// (tools/lds_conflicts.py)
+constexpr int WX_R = 8, WX_H = 256, WX_A = 536, WX_B = 1728;
 constexpr int W_XS = 0, W_XC = W_XS + LDS_X, W_K1 = W_XC + 2 * WX_B, W_GZ = W_K1 + 16;
-constexpr int W_CDS = W_GZ + NSLOT * C;                        // u32 routing words follow (bf16 units)
+constexpr int GZS = C + 8;                                     // window slot stride: 80 B (tr16 reads of the
+                                                               // four slot groups on distinct banks)
+constexpr int W_CDS = W_GZ + NSLOT * GZS;                      // u32 routing words follow (bf16 units)
 constexpr int W_END = W_CDS + 2 * (4 * 2 * (NSLOT / 2));
 constexpr int W_RED = 4 * 2 * 16 * 48 + 48 * 48;               // epilogue floats
 constexpr int W_LDS = (W_END * 2 > W_RED * 4 ? W_END * 2 : W_RED * 4);
@@ -367,7 +371,7 @@ __global__ __launch_bounds__(256, C1R5W_OCC) void c1r5_moments_win_kernel(
         }
       } else if (e < NXV + NGV) {
         const int qv = e - NXV, w = qv >> 2, hp = w / WP, wp = w - hp * WP;
-        *reinterpret_cast<u4*>(gzs + (hp * WSLOT + wp) * C + 8 * (qv & 3)) = vv[j];
+        *reinterpret_cast<u4*>(gzs + (hp * WSLOT + wp) * GZS + 8 * (qv & 3)) = vv[j];
       }
       // routing bits of one window (codes vectors: one per window, lanes = consecutive windows):
       // per channel octet o and row tile ky a 16-bit word (bit 2c + kx), paired with the next
@@ -400,7 +404,7 @@ __global__ __launch_bounds__(256, C1R5W_OCC) void c1r5_moments_win_kernel(
     // (P 14, 15: zero); chunk (b, a, r, P0): one wave per (b, a), two aligned row reads
     for (int i = tid; i < 6 * 32 * 2; i += 256) {
       const int ba = __builtin_amdgcn_readfirstlane(i >> 6), b = ba / 3, a = ba - 3 * b;
-      const int r = (i >> 1) & 31, P0 = 8 * (i & 1);
+      const int r = i & 31, P0 = 8 * ((i >> 5) & 1);          // 16 lanes = 16 rows: distinct slots
       const bf16* srow = xs + r * XS_C + 2 * P0;
       const u4 l0 = *reinterpret_cast<const u4*>(srow), l1 = *reinterpret_cast<const u4*>(srow + 8);
       const u4 l2 = *reinterpret_cast<const u4*>(srow + 16);
@@ -418,19 +422,19 @@ __global__ __launch_bounds__(256, C1R5W_OCC) void c1r5_moments_win_kernel(
         o4[dd] = b ? __builtin_amdgcn_perm(hi, lo, 0x07060302u) : __builtin_amdgcn_perm(hi, lo, 0x05040100u);
       }
       if (P0) o4[3] = 0u;                                      // P = 14, 15: padding windows
-      *reinterpret_cast<u4*>(xc + b * WX_B + a * WX_A + r * WX_R + P0) = u4{o4[0], o4[1], o4[2], o4[3]};
+      *reinterpret_cast<u4*>(xc + b * WX_B + a * WX_A + (P0 ? WX_H : 0) + r * WX_R) = u4{o4[0], o4[1], o4[2], o4[3]};
     }
     __syncthreads();
     // k-loop: 7 steps of 4 slot groups; wave = channel octet
     for (int j = 0; j < 7; ++j) {
       const int m = 4 * j + gq, hp = m >> 1, wp0 = 8 * (m & 1), s0 = hp * WSLOT + wp0;
       const s4 g0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) s4*)(gzs + (s0 + q) * C + 8 * wave + 4 * (p & 1)));
+          (__attribute__((address_space(3))) s4*)(gzs + (s0 + q) * GZS + 8 * wave + 4 * (p & 1)));
       const s4 g1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) s4*)(gzs + (s0 + 4 + q) * C + 8 * wave + 4 * (p & 1)));
+          (__attribute__((address_space(3))) s4*)(gzs + (s0 + 4 + q) * GZS + 8 * wave + 4 * (p & 1)));
       const u4 rw0 = *reinterpret_cast<const u4*>(cds + (wave * 2 + 0) * (NSLOT / 2) + (s0 >> 1));
       const u4 rw1 = *reinterpret_cast<const u4*>(cds + (wave * 2 + 1) * (NSLOT / 2) + (s0 >> 1));
-      const int bs = 2 * hp * WX_R + wp0;
+      const int bs = 2 * hp * WX_R + (wp0 ? WX_H : 0);
       u4 bv[3];
 #pragma unroll
       for (int u = 0; u < 3; ++u) bv[u] = *reinterpret_cast<const u4*>(sm + (bs & bmask[u]) + boff[u]);
