@@ -764,7 +764,10 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws8_kernel(const bf16* 
 }
 
 //          CIN COUT K PAD  H   W  TR NCW OCC NSS DYS XS
-typedef G8<8, 16, 5, 2, 56, 56, 8, 1, 2, 1, 16, 8> G8A2;     // audio conv2
+#ifndef G8A2_T
+#define G8A2_T 8, 1, 2, 1, 16, 8
+#endif
+typedef G8<8, 16, 5, 2, 56, 56, G8A2_T> G8A2;     // audio conv2
 typedef G8<16, 32, 5, 2, 28, 28, 14, 4, 2, 1, 32, 16> G8A3;  // audio conv3
 typedef G8<32, 64, 5, 2, 14, 14, 7, 4, 1, 1, 64, 32, 512, 2, 1> G8A4;   // audio conv4
 // (A/B candidates for audio conv4, AVDINO_G8A4=1 / 2)
