@@ -1,5 +1,7 @@
-"""fp8 (OCP e4m3fn) MFMA conv forward -- BASELINE config 5's "fp8 MFMA conv path"
-(avd_fp8_conv_fwd, csrc/conv8.hip).
+"""fp8 (OCP e4m3fn) MFMA convs -- BASELINE config 5's "fp8 MFMA conv path".  The engine's fp8
+mode runs the block-scaled MX kernels (avd_mx_conv_*, csrc/conv_ws8.hip; exact-data and
+rounding-bound tests in tests/test_gpu_mx.py); this file holds the non-scaled kernel's tests
+(avd_fp8_conv_fwd, csrc/conv8.hip, served where MX does not) and the step-level bands:
 
   * the weight quantiser against torch's own e4m3fn cast: per-output-channel scale
     max|W[o]| / 448 and the tap-major byte rows bit-exact;
@@ -12,7 +14,9 @@
     engine from identical state, beside the bf16 step: statistical parity (SURVEY 8(c):
     bf16/fp8 are compared by loss band and gradient agreement) -- loss within 2 %, flat
     gradient rel-L2 within 4x the bf16 step's own (e4m3 keeps 3 mantissa bits to bf16's 7;
-    measured 0.44 vs 0.13), flat gradient cosine >= 0.85.
+    measured 0.44 vs 0.13), flat gradient cosine >= 0.85;
+  * five full fp8 training steps against five bf16 ones from the same state: every loss within
+    3 % (the loss-curve band).
 """
 import numpy as np
 import pytest
@@ -140,6 +144,30 @@ def test_fp8_step_statistical_parity_with_bf16():
     assert dl["fp8"] <= 0.02 * abs(l32), (dl, l32)
     assert dg["fp8"] <= max(4.0 * dg["bf16"], 0.05), dg
     assert cs["fp8"] >= 0.85 and cs["bf16"] >= 0.95, cs
+
+
+def test_fp8_five_step_loss_curve_band():
+    """Five full training steps (forward, backward, Adam, teacher EMA, centre) of the
+    semi-supervised step in fp8 mode (MX forward / input gradient / weight gradient of the mid
+    layers) and in bf16 from the same state over the same batches: every step's loss within 3 %
+    of the bf16 step's (VERDICT r3 item 1's loss-curve band), and the fp8 curve as a whole
+    within 1.5 % in mean absolute deviation."""
+    from oracle import spec as OS
+    from oracle.params import make_multimodal_batch, make_state
+    state = {k: torch.from_numpy(np.array(v)) for k, v in
+             make_state(OS.multimodal_dino_spec("semi_supervised", 64, 64, 32), 93).items()}
+    batches = [{k: torch.from_numpy(v).cuda() for k, v in make_multimodal_batch(64, 2, 2, 94 + i).items()}
+               for i in range(5)]
+    curves = {}
+    for name, fp8 in (("bf16", False), ("fp8", True)):
+        store, eng = _engine(T, fp8, state)
+        if fp8:
+            assert any(eng.aud._mx_ok(i) for i in range(1, 4)), "MX kernels not selected"
+        curves[name] = [eng.step(b).item() for b in batches]
+    lb, lf = np.array(curves["bf16"]), np.array(curves["fp8"])
+    print("bf16", lb, "fp8", lf)
+    assert np.all(np.abs(lf - lb) <= 0.03 * np.abs(lb)), (lb, lf)
+    assert np.mean(np.abs(lf - lb) / np.abs(lb)) <= 0.015, (lb, lf)
 
 
 @pytest.mark.parametrize("cap", [1, 3])
