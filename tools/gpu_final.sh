@@ -12,7 +12,7 @@ tail -1 gpurun_out/smoke_$TAG.log
 timeout -k 10 600 python bench.py > gpurun_out/bench_final_$TAG.json 2> gpurun_out/bench_final_$TAG.err || { tail -5 gpurun_out/bench_final_$TAG.err; exit 1; }
 cut -c1-300 gpurun_out/bench_final_$TAG.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_final_$TAG -o run -- \
-    python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bprof_final_$TAG.json 2> gpurun_out/bprof_final_$TAG.err || exit $?
+    python bench.py --no-cpu-baseline > gpurun_out/bprof_final_$TAG.json 2> gpurun_out/bprof_final_$TAG.err || exit $?
 python tools/kstats.py gpurun_out/prof_final_$TAG/run_kernel_stats.csv 40 > gpurun_out/ks_final_$TAG.txt
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_eager_$TAG -o run -- \
     python bench.py --steps 10 --warmup 3 --no-graph --no-cpu-baseline > gpurun_out/bprof_eager_$TAG.json 2> gpurun_out/bprof_eager_$TAG.err || exit $?
