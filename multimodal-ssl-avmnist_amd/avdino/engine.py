@@ -470,6 +470,8 @@ class ConvBranch:
     DGRAD_APPLY = os.environ.get("AVDINO_DGRAD_APPLY", "0") == "1"
     # layers whose weight gradient stays on the main stream (A/B: AVDINO_WGRAD_MAIN=3,2)
     WGRAD_MAIN = {int(v) for v in os.environ.get("AVDINO_WGRAD_MAIN", "").split(",") if v.strip()}
+    # A/B: the side-stream weight gradients issued after the whole input-gradient chain
+    WGRAD_DEFER = os.environ.get("AVDINO_WGRAD_DEFER", "0") == "1"
 
     def backward(self, ws, store, ctx, dfeat, wstream=None):
         """dfeat: f32 [N, F] gradient of the features; writes conv/BN parameter grads.
@@ -480,7 +482,7 @@ class ConvBranch:
         gout = dfeat
         nl = len(self.stack.convs)
         main = torch.cuda.current_stream(dfeat.device) if wstream is not None else None
-        wdone = []
+        wdone, deferred = [], []
         fused = None       # (parts, R) this layer's reduce already formed by the dgrad above it
         for i in reversed(range(nl)):
             ci, co, k, pad = self.stack.convs[i]
@@ -556,15 +558,21 @@ class ConvBranch:
             ops.cl_bn_bwd_apply(y, gout, mode, st[2], st[3], coef, dy, N, B, co, Ho, Ho)
             if wstream is not None and i > 0 and i not in self.WGRAD_MAIN:
                 wparts = ws.get(f"wgrad_parts{i}", nch * co * ci * k * k)
-                wstream.wait_stream(main)
-                with torch.cuda.stream(wstream):
-                    ops.mark(f"w{i}.begin")
-                    self._conv_wgrad(i, x, dy, wparts, N)
-                    ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
-                    ops.mark(f"w{i}.end")
-                    ev = torch.cuda.Event()
-                    ev.record(wstream)
-                wdone.append(ev)
+
+                def wg(i=i, x=x, dy=dy, wparts=wparts, nch=nch, co=co, ci=ci, k=k, ck=ck):
+                    with torch.cuda.stream(wstream):
+                        ops.mark(f"w{i}.begin")
+                        self._conv_wgrad(i, x, dy, wparts, N)
+                        ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
+                        ops.mark(f"w{i}.end")
+                        ev = torch.cuda.Event()
+                        ev.record(wstream)
+                    wdone.append(ev)
+                if self.WGRAD_DEFER:
+                    deferred.append(wg)
+                else:
+                    wstream.wait_stream(main)
+                    wg()
             else:
                 self._conv_wgrad(i, x, dy, wparts, N)
                 ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
@@ -583,6 +591,11 @@ class ConvBranch:
                     self._conv_dgrad(i, dy, ctx["wts"][i], dx, N)
                 gout = dx
             ops.mark(f"b{i}")
+        if deferred:
+            # the weight gradients after the whole input-gradient chain (it runs alone)
+            wstream.wait_stream(main)
+            for wg in deferred:
+                wg()
         for ev in wdone:
             main.wait_event(ev)
 
