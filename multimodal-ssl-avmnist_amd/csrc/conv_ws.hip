@@ -73,6 +73,11 @@ struct Ws {
 
 template <int V> using IC = std::integral_constant<int, V>;
 
+// 1: two tiles' input loads in flight (two register sets) instead of one (AP = 0 launches)
+#ifndef WS_PF2
+#define WS_PF2 0
+#endif
+
 __device__ __forceinline__ f4 mma(bf16x8 a, bf16x8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -180,7 +185,7 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
                   ? ((s * L::H + r) * L::W + ix) * L::CIN + 8 * q : -1;
   }
   u4 pre[AP ? 1 : L::SLOTS];
-  auto load_tile = [&](int ti) {
+  auto load_into = [&](u4 (&dst)[AP ? 1 : L::SLOTS], int ti) {
     const int sg = ti / L::TPS, tt = ti - sg * L::TPS;
     const int n0 = sg * L::NS, ty0 = tt * L::TH;
     // row ty0 - PAD of sample n0 (only dereferenced for in-range rows)
@@ -192,8 +197,14 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
       // nothing waits for these loads before the next tile's LDS write
       const bool ok = goff[i] >= 0 && (unsigned)(ty0 - L::PAD + srow[i]) < (unsigned)L::H;
       const u4* src = ok ? reinterpret_cast<const u4*>(bx + goff[i]) : &kZero16;
-      pre[i] = ldg16(src);
+      dst[i] = ldg16(src);
     }
+  };
+  auto load_tile = [&](int ti) { load_into(pre, ti); };
+  auto store_pre = [&](const u4 (&src)[AP ? 1 : L::SLOTS]) {
+#pragma unroll
+    for (int i = 0; i < L::SLOTS; ++i)
+      if (tid + 256 * i < L::TASKS) *reinterpret_cast<u4*>(xs + loff[i]) = src[i];
   };
 
   // staging slots (AP != 0): one task = one 2x2 pooling window x 8 channels of y (windows
@@ -315,21 +326,7 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
   };
   zero_run();
 
-  if (t0 < t1) { if constexpr (AP) load_win_tile(t0); else load_tile(t0); }
-  for (int ti = t0; ti < t1; ++ti) {
-    __syncthreads();   // every wave is done reading the previous tile (and ctab is written)
-    if constexpr (AP) {
-      store_win_tile(ti);
-    } else {
-#pragma unroll
-      for (int i = 0; i < L::SLOTS; ++i)
-        if (tid + 256 * i < L::TASKS) *reinterpret_cast<u4*>(xs + loff[i]) = pre[i];
-    }
-    __syncthreads();
-    if (ti + 1 < t1) {   // in flight under this tile's MFMAs
-      if constexpr (AP) load_win_tile(ti + 1); else load_tile(ti + 1);
-    }
-
+  auto tile_body = [&](int ti) {
     const int sg = ti / L::TPS, tt = ti - sg * L::TPS;
     const int n0 = sg * L::NS, ty0 = tt * L::TH;
     // statistics: a new BN group starts a new running sum (lane-local over the block's tiles
@@ -465,6 +462,40 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
         }
       }
     }
+  };
+
+  if constexpr (!AP && WS_PF2 != 0) {
+    // two tiles' loads in flight: tile ti+2 is issued into the register set tile ti just
+    // left, so each load has two tiles of MFMAs to land (the loop is unrolled by two so the
+    // register sets stay static)
+    u4 preb[L::SLOTS];
+    if (t0 < t1) load_into(pre, t0);
+    if (t0 + 1 < t1) load_into(preb, t0 + 1);
+    for (int ti = t0; ti < t1; ti += 2) {
+      __syncthreads();
+      store_pre(pre);
+      __syncthreads();
+      if (ti + 2 < t1) load_into(pre, ti + 2);
+      tile_body(ti);
+      if (ti + 1 < t1) {
+        __syncthreads();
+        store_pre(preb);
+        __syncthreads();
+        if (ti + 3 < t1) load_into(preb, ti + 3);
+        tile_body(ti + 1);
+      }
+    }
+  } else {
+    if (t0 < t1) { if constexpr (AP) load_win_tile(t0); else load_tile(t0); }
+    for (int ti = t0; ti < t1; ++ti) {
+      __syncthreads();   // every wave is done reading the previous tile (and ctab is written)
+      if constexpr (AP) store_win_tile(ti); else store_pre(pre);
+      __syncthreads();
+      if (ti + 1 < t1) {   // in flight under this tile's MFMAs
+        if constexpr (AP) load_win_tile(ti + 1); else load_tile(ti + 1);
+      }
+      tile_body(ti);
+    }
   }
   if constexpr (STATS) {
     if (stats) {
@@ -485,7 +516,7 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
 #endif
 #if WS_VARIANT == 0   // per-layer best of the measured variants (opbench, B=1024 step shapes)
 typedef Ws<8, 16, 5, 2, 56, 56, 14, 1, 1, 1, 2, 2, 4> FwdA2;  // audio conv2        273 us
-typedef Ws<16, 32, 5, 2, 28, 28, 14, 1, 1, 1, 1, 2, 4> FwdA3; // audio conv3        231 us
+typedef Ws<16, 32, 5, 2, 28, 28, 14, 1, 2, 1, 1, 2, 4> FwdA3; // audio conv3 194 us (NCW 1: 236 us, spilled)
 typedef Ws<32, 64, 5, 2, 14, 14, 14, 1, 4, 1, 2, 2> FwdA4;    // audio conv4        168 us
 typedef Ws<32, 64, 5, 0, 14, 14, 10, 2, 4, 1, 2, 2> FwdI2;    // image conv2         87 us
 typedef Ws<16, 8, 5, 2, 56, 56, 8, 1, 1, 1, 1, 3> DgrA2;      // audio conv2 dgrad  275 us
@@ -519,6 +550,31 @@ typedef Ws<16, 8, 5, 2, 56, 56, 8, 1, 1, 1, 2, 3, 4> DgrA2;
 typedef Ws<32, 16, 5, 2, 28, 28, 14, 1, 1, 1, 2, 2, 4> DgrA3;
 typedef Ws<64, 32, 5, 2, 14, 14, 14, 1, 2, 2, 1, 2, 4> DgrA4;
 typedef Ws<64, 32, 5, 4, 10, 10, 14, 1, 2, 2, 1, 2, 4> DgrI2;
+#endif
+// per-layer overrides for variant builds: -DWS_FWDA3=16,32,5,2,28,28,14,1,2,1,1,2,4 etc.
+#ifdef WS_FWDA2
+typedef Ws<WS_FWDA2> FwdA2_;
+#define FwdA2 FwdA2_
+#endif
+#ifdef WS_FWDA3
+typedef Ws<WS_FWDA3> FwdA3_;
+#define FwdA3 FwdA3_
+#endif
+#ifdef WS_FWDA4
+typedef Ws<WS_FWDA4> FwdA4_;
+#define FwdA4 FwdA4_
+#endif
+#ifdef WS_DGRA2
+typedef Ws<WS_DGRA2> DgrA2_;
+#define DgrA2 DgrA2_
+#endif
+#ifdef WS_DGRA3
+typedef Ws<WS_DGRA3> DgrA3_;
+#define DgrA3 DgrA3_
+#endif
+#ifdef WS_DGRA4
+typedef Ws<WS_DGRA4> DgrA4_;
+#define DgrA4 DgrA4_
 #endif
 
 bool ws_disabled() {

@@ -51,6 +51,11 @@
 #define WG_VARIANT 0
 #endif
 
+// 1: two strips' input loads in flight (two register sets) instead of one (AP = 0 launches)
+#ifndef WG_PF2
+#define WG_PF2 0
+#endif
+
 using namespace avd;
 
 namespace {
@@ -187,7 +192,7 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* _
     }
   }
   u4 pre[L::SLOTS];
-  auto load_strip = [&](int st) {
+  auto load_into = [&](u4 (&dst)[L::SLOTS], int st) {
     if constexpr (AP) return;
     const int sg = st / L::SPS, y0 = (st - sg * L::SPS) * L::TR;
     const int n = sg * L::NSS;
@@ -201,14 +206,16 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* _
       } else if (goff[i] >= 0 && (unsigned)(y0 - L::PAD + xrow[i]) < (unsigned)L::H) {
         src = reinterpret_cast<const u4*>(bx + goff[i]);
       }
-      pre[i] = ldg16(src);
+      dst[i] = ldg16(src);
     }
   };
-  auto store_strip = [&]() {
+  auto load_strip = [&](int st) { load_into(pre, st); };
+  auto store_from = [&](const u4 (&src)[L::SLOTS]) {
 #pragma unroll
     for (int i = 0; i < L::SLOTS; ++i)
-      if (tid + L::NTHR * i < L::DY_T + L::X_T) *reinterpret_cast<u4*>(smem + loff[i]) = pre[i];
+      if (tid + L::NTHR * i < L::DY_T + L::X_T) *reinterpret_cast<u4*>(smem + loff[i]) = src[i];
   };
+  auto store_strip = [&]() { store_from(pre); };
 
   // AP: dY comes from windows of y (2x2 x 8 channels + the pooled gradient -> 4 dY vectors);
   // X keeps its 16-byte tasks in their own slots
@@ -298,19 +305,7 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* _
       if (tid + L::NTHR * i < L::X_T) *reinterpret_cast<u4*>(smem + xlo[i]) = xpre[i];
   };
 
-  if (st0 < st1) { if constexpr (AP) load_strip_ap(st0); else load_strip(st0); }
-  for (int st = st0; st < st1; ++st) {
-#ifndef WG_NOSTAGE
-    __syncthreads();
-    if constexpr (AP) store_strip_ap(st); else store_strip();
-    __syncthreads();
-#endif
-#ifndef WG_NOSTAGE
-    if (st + 1 < st1) { if constexpr (AP) load_strip_ap(st + 1); else load_strip(st + 1); }
-#endif
-#ifdef WG_NOMFMA
-    continue;
-#endif
+  auto strip_body = [&]() {
     for (int ks = wp; ks < L::KST; ks += L::NPW) {
       const int P0 = 32 * ks;
       int xb[2];
@@ -368,6 +363,40 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* _
         __builtin_amdgcn_sched_group_barrier(0x008, L::MTW, 0);
         if (j + PF < L::NW) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       }
+#endif
+    }
+  };
+
+  if constexpr (!AP && WG_PF2 != 0) {
+    // two strips' loads in flight (two register sets, the loop unrolled by two)
+    u4 preb[L::SLOTS];
+    if (st0 < st1) load_into(pre, st0);
+    if (st0 + 1 < st1) load_into(preb, st0 + 1);
+    for (int st = st0; st < st1; st += 2) {
+      __syncthreads();
+      store_from(pre);
+      __syncthreads();
+      if (st + 2 < st1) load_into(pre, st + 2);
+      strip_body();
+      if (st + 1 < st1) {
+        __syncthreads();
+        store_from(preb);
+        __syncthreads();
+        if (st + 3 < st1) load_into(preb, st + 3);
+        strip_body();
+      }
+    }
+  } else {
+    if (st0 < st1) { if constexpr (AP) load_strip_ap(st0); else load_strip(st0); }
+    for (int st = st0; st < st1; ++st) {
+#ifndef WG_NOSTAGE
+      __syncthreads();
+      if constexpr (AP) store_strip_ap(st); else store_strip();
+      __syncthreads();
+      if (st + 1 < st1) { if constexpr (AP) load_strip_ap(st + 1); else load_strip(st + 1); }
+#endif
+#ifndef WG_NOMFMA
+      strip_body();
 #endif
     }
   }
