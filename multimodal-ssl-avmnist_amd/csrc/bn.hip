@@ -395,11 +395,11 @@ int avd_bn_finalize(float* parts, int G, int R, int C, long long count, const fl
   if (G <= 0 || R <= 0 || C <= 0 || count <= 1) return AVD_ERR_SHAPE;
   if ((running_mean == nullptr) != (running_var == nullptr)) return AVD_ERR_ARG;
   hipStream_t st = avd_stream(stream);
-  // single pass (one block per channel reads all G*R rows of its channel) only on request
-  // (AVDINO_FIN1_ROWS = max G*R): A/B on the config-2 step, 2048 vs 0 (two-pass always) was
-  // within noise with two-pass ahead (6.42-6.46 vs 6.46-6.48 ms), so two-pass is the default
+  // single pass (one block per channel reads all G*R rows of its channel: one launch instead of
+  // two) up to AVDINO_FIN1_ROWS = max G*R rows; 0 = two passes always.  Round-4 A/B on the
+  // config-2 step (3 interleaved rounds): 5.483 vs 5.516 ms, so single pass is the default
   static const long long fin1_rows =
-      getenv("AVDINO_FIN1_ROWS") ? atoll(getenv("AVDINO_FIN1_ROWS")) : 0;
+      getenv("AVDINO_FIN1_ROWS") ? atoll(getenv("AVDINO_FIN1_ROWS")) : (1ll << 30);
   if (G <= 256 && R <= FIN1_MAXROWS && (long long)G * R <= fin1_rows) {
     bn_finalize1_kernel<<<C, 256, 0, st>>>(parts, G, R, C, count, gamma, beta, eps, momentum, mean,
                                            invstd, scale, shift, running_mean, running_var, pivot,

@@ -73,6 +73,13 @@ struct Ws {
 
 template <int V> using IC = std::integral_constant<int, V>;
 
+// 1: incremental pixel indices and packed-fp32 bias / statistics in the tile loop
+// (fewer VALU instructions per MFMA; same arithmetic, bit-identical maps and partials)
+#ifndef WS_LEAN
+#define WS_LEAN 1
+#endif
+typedef __attribute__((ext_vector_type(2))) float f2;
+
 // 1: two tiles' input loads in flight (two register sets) instead of one (AP = 0 launches)
 #ifndef WS_PF2
 #define WS_PF2 0
@@ -152,15 +159,15 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
   // bias, and the statistics pivot: forward partials are shifted sums of (y - K[c]) and
   // (y - K[c])^2 about a per-channel K near the batch mean (the layer's running mean), so the
   // variance E[(y-K)^2] - E[y-K]^2 does not cancel when |mean| >> std (avd_bn_finalize pivot)
-  float bv[L::NTW][4], pv[L::NTW][4];
+  f2 bv[L::NTW][2], pv[L::NTW][2];   // channel pairs
 #pragma unroll
   for (int t = 0; t < L::NTW; ++t)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int co = cob + 16 * t + 4 * g + i;
-      bv[t][i] = (FWD && bias && co < L::COUT) ? bias[co] : 0.f;
+      bv[t][i >> 1][i & 1] = (FWD && bias && co < L::COUT) ? bias[co] : 0.f;
       const float k = (FWD && pivot && co < L::COUT) ? pivot[co] : 0.f;
-      pv[t][i] = isfinite(k) ? k : 0.f;
+      pv[t][i >> 1][i & 1] = isfinite(k) ? k : 0.f;
     }
   constexpr bool STATS = FWD || RD;
 
@@ -288,14 +295,14 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
 
   // BN partial sums (forward): per-block running sums over the block's tiles of one
   // BatchNorm group, one row per (block, pixel wave set) and group: [COUT][G][R = grid*NPW][2]
-  float run_s[L::NTW][4], run_q[L::NTW][4];
+  f2 run_s[L::NTW][2], run_q[L::NTW][2];   // channel pairs (packed fp32 updates)
   int cur_g = -1;
   const int tilesPG = ntiles / ngroups, R = (int)gridDim.x * L::NPW;
   auto zero_run = [&]() {
 #pragma unroll
     for (int t = 0; t < L::NTW; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { run_s[t][i] = 0.f; run_q[t][i] = 0.f; }
+      for (int i = 0; i < 2; ++i) { run_s[t][i] = f2{0.f, 0.f}; run_q[t][i] = f2{0.f, 0.f}; }
   };
   auto flush = [&](int gp) {   // wave-uniform call: the row sums are DPP across the 16 lanes
     if (kw != 0) return;
@@ -303,8 +310,8 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
     for (int t = 0; t < L::NTW; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        run_s[t][i] = row16_sum(run_s[t][i]);
-        run_q[t][i] = row16_sum(run_q[t][i]);
+        run_s[t][i >> 1][i & 1] = row16_sum(run_s[t][i >> 1][i & 1]);
+        run_q[t][i >> 1][i & 1] = row16_sum(run_q[t][i >> 1][i & 1]);
       }
     if (r16 != 0) return;
 #pragma unroll
@@ -313,14 +320,14 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
       for (int i = 0; i < 4; ++i) {
         const int co = cob + 16 * t + 4 * g + i;
         if (co < L::COUT) {
-          float q = run_q[t][i];
+          float q = run_q[t][i >> 1][i & 1];
           if constexpr (RD) {
             // sum dz * xhat = (sum dz * p - beta * sum dz) / gamma; 0 for the fix-up channels
             const float ga = aa.scale[co], bb = aa.shift[co];
-            q = (ga == 0.f || fabsf(bb) > 8.f * fabsf(ga)) ? 0.f : (q - bb * run_s[t][i]) / ga;
+            q = (ga == 0.f || fabsf(bb) > 8.f * fabsf(ga)) ? 0.f : (q - bb * run_s[t][i >> 1][i & 1]) / ga;
           }
           *reinterpret_cast<float2*>(stats + (((size_t)co * ngroups + gp) * R + blockIdx.x * L::NPW + wp) * 2) =
-              make_float2(run_s[t][i], q);
+              make_float2(run_s[t][i >> 1][i & 1], q);
         }
       }
   };
@@ -344,15 +351,42 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
     auto& ss = run_s;
     auto& sq = run_q;
 
+#if WS_LEAN
+    // per-lane pixel (sample, row, column) of each of the GB groups: divided out once per tile,
+    // then advanced by DP pixels per step (one carry each way), not re-divided per group
+    constexpr int DP = L::NPW * L::GB * 16, DRY = DP / L::TW, DRX = DP % L::TW;
+    static_assert(DRY + 1 <= L::TH, "one row carry per step");
+    int lp[L::GB], ls[L::GB], lry[L::GB], lrx[L::GB];
+#pragma unroll
+    for (int b = 0; b < L::GB; ++b) {
+      lp[b] = (wp + L::NPW * b) * 16 + r16;
+      ls[b] = lp[b] / (L::TH * L::TW);
+      const int rem = lp[b] - ls[b] * (L::TH * L::TW);
+      lry[b] = rem / L::TW;
+      lrx[b] = rem - lry[b] * L::TW;
+    }
+#endif
+#pragma unroll 1
     for (int i0 = 0; i0 < L::GW; i0 += L::GB) {
       int base[L::GB], opix[L::GB];
       bool gv[L::GB];
 #pragma unroll
       for (int b = 0; b < L::GB; ++b) {
+#if WS_LEAN
+        const int p = lp[b], s = ls[b], ry = lry[b], rx = lrx[b];
+        lp[b] += DP;
+        lrx[b] += DRX;
+        lry[b] += DRY;
+        if (lrx[b] >= L::TW) { lrx[b] -= L::TW; ++lry[b]; }
+        if constexpr (L::NS > 1) {
+          if (lry[b] >= L::TH) { lry[b] -= L::TH; ++ls[b]; }
+        }
+#else
         const int p = (wp + L::NPW * (i0 + b)) * 16 + r16;
-        gv[b] = i0 + b < L::GW && p < L::PIX;
         const int s = p / (L::TH * L::TW), rem = p - s * (L::TH * L::TW);
         const int ry = rem / L::TW, rx = rem - ry * L::TW;
+#endif
+        gv[b] = i0 + b < L::GW && p < L::PIX;
         base[b] = gv[b] ? ((s * L::ITH + ry) * L::RS + rx) * L::PS : 0;
         opix[b] = ((n0 + s) * L::HO + ty0 + ry) * L::WO + rx;
       }
@@ -432,16 +466,30 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
           if (co >= L::COUT) continue;
           uint32_t lo, hi;
           if constexpr (FWD) {
-            lo = pack_bf16x2(acc[b][t][0] + bv[t][0], acc[b][t][1] + bv[t][1]);
-            hi = pack_bf16x2(acc[b][t][2] + bv[t][2], acc[b][t][3] + bv[t][3]);
+#if WS_LEAN
+            // pairs through the packed fp32 ALU (v_pk_add / v_pk_fma: the same IEEE ops)
+            const f2 y01 = f2{acc[b][t][0], acc[b][t][1]} + bv[t][0];
+            const f2 y23 = f2{acc[b][t][2], acc[b][t][3]} + bv[t][1];
+            lo = pack_bf16x2(y01.x, y01.y);
+            hi = pack_bf16x2(y23.x, y23.y);
+            const f2 d01 = f2{__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u)} - pv[t][0];
+            const f2 d23 = f2{__uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)} - pv[t][1];
+            ss[t][0] += d01;
+            ss[t][1] += d23;
+            sq[t][0] = __builtin_elementwise_fma(d01, d01, sq[t][0]);
+            sq[t][1] = __builtin_elementwise_fma(d23, d23, sq[t][1]);
+#else
+            lo = pack_bf16x2(acc[b][t][0] + bv[t][0][0], acc[b][t][1] + bv[t][0][1]);
+            hi = pack_bf16x2(acc[b][t][2] + bv[t][1][0], acc[b][t][3] + bv[t][1][1]);
             const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
                                 __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const float d = v[i] - pv[t][i];
-              ss[t][i] += d;
-              sq[t][i] = fmaf(d, d, sq[t][i]);
+              const float d = v[i] - pv[t][i >> 1][i & 1];
+              ss[t][i >> 1][i & 1] += d;
+              sq[t][i >> 1][i & 1] = fmaf(d, d, sq[t][i >> 1][i & 1]);
             }
+#endif
           } else {
             lo = pack_bf16x2(acc[b][t][0], acc[b][t][1]);
             hi = pack_bf16x2(acc[b][t][2], acc[b][t][3]);
@@ -453,8 +501,8 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
 #pragma unroll
               for (int i = 0; i < 4; ++i) {   // sum dz and sum dz * p (xhat applied at the flush)
                 const float dz = pv[i] > 0.f ? v[i] : 0.f;
-                ss[t][i] += dz;
-                sq[t][i] = fmaf(dz, pv[i], sq[t][i]);
+                ss[t][i >> 1][i & 1] += dz;
+                sq[t][i >> 1][i & 1] = fmaf(dz, pv[i], sq[t][i >> 1][i & 1]);
               }
             }
           }
