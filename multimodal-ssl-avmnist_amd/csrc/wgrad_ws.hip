@@ -51,6 +51,11 @@
 #define WG_VARIANT 0
 #endif
 
+// 1: incremental X-image pixel indices in the k-step loop (fewer VALU per MFMA; same reads)
+#ifndef WG_LEAN
+#define WG_LEAN 0   // measured slower (14x14: 168 vs 158 us, 56x56: 281 vs 275 us)
+#endif
+
 // 1: two strips' input loads in flight (two register sets) instead of one (AP = 0 launches)
 #ifndef WG_PF2
 #define WG_PF2 0
@@ -305,7 +310,30 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* _
       if (tid + L::NTHR * i < L::X_T) *reinterpret_cast<u4*>(smem + xlo[i]) = xpre[i];
   };
 
+#if WG_LEAN
+  // X-image pixel (sample, row, column) of this lane's two k-runs at k-step wp: divided out once
+  // per launch (the same for every strip), advanced by 32 NPW pixels per k-step with one carry
+  // each way; pixels past the strip (the k-step tail) read the last pixel, as the clamp did
+  constexpr int DPX = 32 * L::NPW, DR = DPX / L::WO8, DO = DPX % L::WO8;
+  static_assert(DR + 1 <= L::TR, "one row carry per k-step");
+  constexpr int PL = L::NPIX - 1, SML = PL / L::SPIX, RL = (PL - SML * L::SPIX) / L::WO8,
+                OXL = PL - SML * L::SPIX - RL * L::WO8;
+  constexpr int XBL = ((SML * L::XR + RL) * L::XW + OXL) * L::XS;
+  int xp0[2], xs0[2], xr0[2], xo0[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    xp0[h] = 32 * wp + kpix(g, h, q4);
+    xs0[h] = xp0[h] / L::SPIX;
+    const int rem = xp0[h] - xs0[h] * L::SPIX;
+    xr0[h] = rem / L::WO8;
+    xo0[h] = rem - xr0[h] * L::WO8;
+  }
+#endif
   auto strip_body = [&]() {
+#if WG_LEAN
+    int xpp[2] = {xp0[0], xp0[1]}, xss[2] = {xs0[0], xs0[1]}, xrr[2] = {xr0[0], xr0[1]},
+        xoo[2] = {xo0[0], xo0[1]};
+#endif
     for (int ks = wp; ks < L::KST; ks += L::NPW) {
       const int P0 = 32 * ks;
       int xb[2];
@@ -319,10 +347,21 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* _
       }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
+#if WG_LEAN
+        xb[h] = xpp[h] <= PL ? ((xss[h] * L::XR + xrr[h]) * L::XW + xoo[h]) * L::XS : XBL;
+        xpp[h] += DPX;
+        xoo[h] += DO;
+        xrr[h] += DR;
+        if (xoo[h] >= L::WO8) { xoo[h] -= L::WO8; ++xrr[h]; }
+        if constexpr (L::NSS > 1) {
+          if (xrr[h] >= L::TR) { xrr[h] -= L::TR; ++xss[h]; }
+        }
+#else
         const int P = min(P0 + kpix(g, h, q4), L::NPIX - 1);   // tail pixels: dY is 0 there
         const int sm = P / L::SPIX, rem = P - sm * L::SPIX;
         const int r = rem / L::WO8, ox = rem - r * L::WO8;
         xb[h] = ((sm * L::XR + r) * L::XW + ox) * L::XS;
+#endif
       }
       // B fragments PF columns ahead of their MFMAs
       constexpr int PF = L::PF;
