@@ -12,6 +12,7 @@
 // Partial-statistic layout everywhere: channel-major parts [C][G][R][2] so the finaliser
 // reads contiguous rows.  All reductions are fixed-order (f64 in the finalisers).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -534,7 +535,10 @@ int avd_sum_rows_chunks(int rows, int cols) {
   if (rows <= 0 || cols <= 0 || (long long)rows * cols < (1ll << 20)) return 1;
   const int cw = cols <= 2048 ? 16 : 64, ph = 1024 / cw;
   const int cb = avd_cdiv(cols, cw);
-  const int want = avd_cdiv(1024, cb), most = rows / (4 * ph);
+  // target blocks (AVDINO_SUMROWS_BLOCKS, A/B runs; a process-wide constant, so the order of
+  // every reduction is still fixed)
+  static const int target = getenv("AVDINO_SUMROWS_BLOCKS") ? std::max(1, atoi(getenv("AVDINO_SUMROWS_BLOCKS"))) : 1024;
+  const int want = avd_cdiv(target, cb), most = rows / (4 * ph);
   const int c = want < most ? want : most;
   return c > 1 ? c : 1;
 }
