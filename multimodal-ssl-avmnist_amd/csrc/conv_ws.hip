@@ -43,7 +43,18 @@ template <int CIN_, int COUT_, int K_, int PAD_, int H_, int W_, int TH_, int NS
           int NKW_, int GB_, int OCC_, int PF_ = 2>
 struct Ws {
   static constexpr int OCC = OCC_;                         // target waves per SIMD
+#ifndef WS_PF_ALL
+// B-read depth of every layer (with WS_SCHED pinning it): step A/B, 3 interleaved rounds, 6 vs
+// the per-layer table's 2 / 4: 5.35 vs 5.44 ms (5: 5.43, 8: 5.41).  The 56^2 / 28^2 forwards
+// drop to 2 resident blocks per CU (174 / 170 VGPRs) and are a little slower alone, but the step
+// (their grids beside the other stream's kernels) is faster.  -1 = the per-layer PF below.
+#define WS_PF_ALL 6
+#endif
+#if WS_PF_ALL > 0
+  static constexpr int PF = WS_PF_ALL;
+#else
   static constexpr int PF = PF_;                           // k-steps of B reads in flight
+#endif
   static constexpr int CIN = CIN_, COUT = COUT_, K = K_, PAD = PAD_, H = H_, W = W_;
   static constexpr int HO = H + 2 * PAD - K + 1, WO = W + 2 * PAD - K + 1;
   static constexpr int TH = TH_, TW = WO, NS = NS_;
@@ -79,6 +90,11 @@ template <int V> using IC = std::integral_constant<int, V>;
 #define WS_LEAN 1
 #endif
 typedef __attribute__((ext_vector_type(2))) float f2;
+
+// 1: B-fragment reads issued PF k-steps ahead of their MFMAs by sched_group_barrier
+#ifndef WS_SCHED
+#define WS_SCHED 1   // 188.9 k -> 191.7 k pairs/s; the 28^2 / 14^2 input gradients 8-10 % faster
+#endif
 
 // 1: two tiles' input loads in flight (two register sets) instead of one (AP = 0 launches)
 #ifndef WS_PF2
@@ -433,6 +449,17 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
             for (int t = 0; t < L::NTW; ++t)
               acc[b][t] = mma(a[j][t], bq[j % (PF + 1)][b], acc[b][t]);
         }
+#if WS_SCHED
+        // pin the interleave (hipcc otherwise pulls each B read down to one MFMA before its use
+        // and waits lgkmcnt right there): PF k-steps of reads, then per k-step its MFMAs and the
+        // reads of k-step j + PF
+        __builtin_amdgcn_sched_group_barrier(0x100, L::GB * (PF < L::KSH ? PF : L::KSH), 0);
+#pragma unroll
+        for (int j = 0; j < L::KSH; ++j) {
+          __builtin_amdgcn_sched_group_barrier(0x008, L::GB * L::NTW, 0);
+          if (j + PF < L::KSH) __builtin_amdgcn_sched_group_barrier(0x100, L::GB, 0);
+        }
+#endif
       };
       if constexpr (L::NKW == 1) {
         kloop(IC<0>{});
