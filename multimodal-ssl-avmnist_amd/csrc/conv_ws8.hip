@@ -27,6 +27,11 @@
 
 using namespace avd;
 
+// 1: LDS reads pinned PF k-steps / columns ahead of their MFMAs by sched_group_barrier
+#ifndef WS8_SCHED
+#define WS8_SCHED 0
+#endif
+
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) int i8v;     // 32 fp8 bytes: one MX operand
@@ -330,6 +335,19 @@ __global__ __launch_bounds__(256, L::OCC) void conv_ws8_kernel(
                 acc[b][t] = mxmma(j % 4, a[j][t], bq[j % (PF + 1)][b], acc[b][t], sa[j / 4][t], sb);
           }
         }
+#if WS8_SCHED
+        // pin the B reads PF k-steps ahead of their MFMAs (as conv_ws.hip); only where every
+        // k-step's MFMAs are unconditional (one scheduling region)
+        if constexpr (L::NKW == 1) {
+          constexpr int RPB = L::CIN == 8 ? 4 : 2;   // LDS reads per group and k-step
+          __builtin_amdgcn_sched_group_barrier(0x100, RPB * L::GB * (PF < L::KSH ? PF : L::KSH), 0);
+#pragma unroll
+          for (int j = 0; j < L::KSH; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, L::GB * L::NTW, 0);
+            if (j + PF < L::KSH) __builtin_amdgcn_sched_group_barrier(0x100, RPB * L::GB, 0);
+          }
+        }
+#endif
       }
       if constexpr (L::NKW > 1) {
         f4* r = red + (((i0 / L::GB) & 1) * L::NCW + wc) * L::GB * L::NTW * 64;
@@ -709,6 +727,15 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws8_kernel(const bf16* 
         for (int m = 0; m < L::MTW; ++m)
           acc[m][j] = mxmma_<0>(a[m], bq[j % (PF + 1)], acc[m][j], sbd, sbx);
       }
+#if WS8_SCHED
+      // A reads + PF columns of B reads, then per column its MFMAs and the reads of column j + PF
+      __builtin_amdgcn_sched_group_barrier(0x100, 4 * L::MTW + 4 * (PF < L::NW ? PF : L::NW), 0);
+#pragma unroll
+      for (int j = 0; j < L::NW; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x008, L::MTW, 0);
+        if (j + PF < L::NW) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+      }
+#endif
     }
   }
 
