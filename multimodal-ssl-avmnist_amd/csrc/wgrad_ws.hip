@@ -81,7 +81,11 @@ template <int CIN_, int COUT_, int K_, int PAD_, int H_, int W_, int TR_, int NC
           int PF_ = 3, int NTHR_ = 256, int NMW_ = 1, int NSS_ = 1>
 struct Wg {
   static constexpr int CIN = CIN_, COUT = COUT_, K = K_, PAD = PAD_, H = H_, W = W_;
+#ifdef WG_PF_ALL
+  static constexpr int OCC = OCC_, PF = WG_PF_ALL, NTHR = NTHR_, WAVES = NTHR / 64;   // variant builds
+#else
   static constexpr int OCC = OCC_, PF = PF_, NTHR = NTHR_, WAVES = NTHR / 64;
+#endif
   static constexpr int HO = H + 2 * PAD - K + 1, WO = W + 2 * PAD - K + 1;
   static constexpr int WO8 = (WO + 7) & ~7;                 // 8-pixel runs never cross a row
   static constexpr int TR = TR_, SPS = HO / TR, NSS = NSS_; // strip rows / strips per sample
