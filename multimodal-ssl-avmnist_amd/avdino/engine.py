@@ -73,9 +73,18 @@ class ConvBranch:
         # statistics and the weight gradient stay bf16 / f32
         self.fp8 = bool(fp8) and act_dtype == torch.bfloat16
 
+    # layers kept on the bf16 kernels in fp8 mode, as "<f|d|w><Cin>x<H>" entries (forward, input
+    # gradient, weight gradient of the layer with Cin input channels at H x H), e.g. "d16x56"
+    MX_OFF = {v.strip() for v in os.environ.get("AVDINO_MX_OFF", "").split(",") if v.strip()}
+
+    def _mx_off(self, kind, i):
+        ci = self.stack.convs[i][0]
+        return f"{kind}{ci}x{self.dims[i][0]}" in self.MX_OFF
+
     def _mx_ok(self, i, dgrad=False):
         ci, co, k, p = self.stack.convs[i]
-        return self.fp8 and i > 0 and ops.mx_conv_serves(ci, self.dims[i][0], co, k, p, dgrad)
+        return (self.fp8 and i > 0 and not self._mx_off("d" if dgrad else "f", i)
+                and ops.mx_conv_serves(ci, self.dims[i][0], co, k, p, dgrad))
 
     # kept for callers of the round-2 name
     _fp8_ok = _mx_ok
@@ -127,7 +136,8 @@ class ConvBranch:
 
     def _mx_wgrad(self, i, N):
         ci, co, k, p = self.stack.convs[i]
-        return self.fp8 and i > 0 and ops.mx_wgrad_chunks(N, ci, self.dims[i][0], co, k, p) > 0
+        return (self.fp8 and i > 0 and not self._mx_off("w", i)
+                and ops.mx_wgrad_chunks(N, ci, self.dims[i][0], co, k, p) > 0)
 
     def _wgrad_chunks(self, i, N):
         ci, co, k, p = self.stack.convs[i]
