@@ -47,8 +47,9 @@ struct Ws {
 // B-read depth of every layer (with WS_SCHED pinning it): step A/B, 3 interleaved rounds, 6 vs
 // the per-layer table's 2 / 4: 5.35 vs 5.44 ms (5: 5.43, 8: 5.41).  The 56^2 / 28^2 forwards
 // drop to 2 resident blocks per CU (174 / 170 VGPRs) and are a little slower alone, but the step
-// (their grids beside the other stream's kernels) is faster.  -1 = the per-layer PF below.
-#define WS_PF_ALL 6
+// (their grids beside the other stream's kernels) is faster.  The table below sets 6 per layer;
+// WS_PF_ALL > 0 overrides every layer (variant builds).
+#define WS_PF_ALL -1
 #endif
 #if WS_PF_ALL > 0
   static constexpr int PF = WS_PF_ALL;
@@ -590,14 +591,16 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
 #define WS_VARIANT 0
 #endif
 #if WS_VARIANT == 0   // per-layer best of the measured variants (opbench, B=1024 step shapes)
-typedef Ws<8, 16, 5, 2, 56, 56, 14, 1, 1, 1, 2, 2, 4> FwdA2;  // audio conv2        273 us
-typedef Ws<16, 32, 5, 2, 28, 28, 14, 1, 2, 1, 1, 2, 4> FwdA3; // audio conv3 194 us (NCW 1: 236 us, spilled)
-typedef Ws<32, 64, 5, 2, 14, 14, 14, 1, 4, 1, 2, 2> FwdA4;    // audio conv4        168 us
-typedef Ws<32, 64, 5, 0, 14, 14, 10, 2, 4, 1, 2, 2> FwdI2;    // image conv2         87 us
-typedef Ws<16, 8, 5, 2, 56, 56, 8, 1, 1, 1, 1, 3> DgrA2;      // audio conv2 dgrad  275 us
-typedef Ws<32, 16, 5, 2, 28, 28, 14, 1, 1, 1, 2, 2> DgrA3;    // audio conv3 dgrad  145 us
-typedef Ws<64, 32, 5, 2, 14, 14, 14, 1, 2, 2, 2, 2> DgrA4;    // audio conv4 dgrad  158 us
-typedef Ws<64, 32, 5, 4, 10, 10, 14, 1, 2, 2, 2, 2> DgrI2;    // image conv2 dgrad  154 us
+// (PF 6 everywhere: the step A/B above; the times are the round-3/4 per-layer picks at their
+// earlier PF)
+typedef Ws<8, 16, 5, 2, 56, 56, 14, 1, 1, 1, 2, 2, 6> FwdA2;  // audio conv2        273 us
+typedef Ws<16, 32, 5, 2, 28, 28, 14, 1, 2, 1, 1, 2, 6> FwdA3; // audio conv3 194 us (NCW 1: 236 us, spilled)
+typedef Ws<32, 64, 5, 2, 14, 14, 14, 1, 4, 1, 2, 2, 6> FwdA4; // audio conv4        168 us
+typedef Ws<32, 64, 5, 0, 14, 14, 10, 2, 4, 1, 2, 2, 6> FwdI2; // image conv2         87 us
+typedef Ws<16, 8, 5, 2, 56, 56, 8, 1, 1, 1, 1, 3, 6> DgrA2;   // audio conv2 dgrad  275 us
+typedef Ws<32, 16, 5, 2, 28, 28, 14, 1, 1, 1, 2, 2, 6> DgrA3; // audio conv3 dgrad  145 us
+typedef Ws<64, 32, 5, 2, 14, 14, 14, 1, 2, 2, 2, 2, 6> DgrA4; // audio conv4 dgrad  158 us
+typedef Ws<64, 32, 5, 4, 10, 10, 14, 1, 2, 2, 2, 2, 6> DgrI2; // image conv2 dgrad  154 us
 #elif WS_VARIANT == 1
 typedef Ws<8, 16, 5, 2, 56, 56, 14, 1, 1, 1, 4, 2> FwdA2;
 typedef Ws<16, 32, 5, 2, 28, 28, 14, 1, 1, 1, 2, 2> FwdA3;
