@@ -47,7 +47,11 @@ constexpr int cdv(int a, int b) { return (a + b - 1) / b; }
 template <int CIN_, int COUT_, int K_, int PAD_, int H_, int W_, int TH_, int NS_, int NCW_,
           int NKW_, int GB_, int OCC_, int PS_, int RP_, int PF_ = 2>
 struct W8 {
+#ifdef W8_PF_ALL
+  static constexpr int OCC = OCC_, PF = W8_PF_ALL;   // variant builds: one depth for all
+#else
   static constexpr int OCC = OCC_, PF = PF_;
+#endif
   static constexpr int CIN = CIN_, COUT = COUT_, K = K_, PAD = PAD_, H = H_, W = W_;
   static constexpr int HO = H + 2 * PAD - K + 1, WO = W + 2 * PAD - K + 1;
   static constexpr int TH = TH_, TW = WO, NS = NS_;
@@ -814,7 +818,10 @@ int g8_chunks(int N) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wgrad_ws8_kernel<L>, L::NTHR, 0) != hipSuccess || occ <= 0)
       occ = 1;
   }
-  return std::max(1, grid_cap(std::min(N / L::NSS, num_cus8() * occ)));
+  // AVDINO_G8_SLABS: at most this many slabs (every slab is a [Cout][Cin][K][K] f32 partial the
+  // fixed-order reduce reads back; one resident wave of blocks per slab by default)
+  static const int cap = getenv("AVDINO_G8_SLABS") ? std::max(1, atoi(getenv("AVDINO_G8_SLABS"))) : (1 << 30);
+  return std::max(1, grid_cap(std::min(std::min(N / L::NSS, num_cus8() * occ), cap)));
 }
 
 }  // namespace
