@@ -1684,6 +1684,11 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
 // resolution dz map, and its LDS (29 KB) leaves room for 5 blocks per CU.
 constexpr int NWINMAX = (TH / 2) * (WMAX / 2);
 
+// 1: the window moments loop reads step j + 4's LDS operands before step j's MFMAs
+#ifndef C1W_PIPE
+#define C1W_PIPE 0
+#endif
+
 __global__ __launch_bounds__(256, 4) void c1p8_moments_win_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ gz, const unsigned* __restrict__ codes,
     float* __restrict__ out, int B, int G, int R, int H, int W, int tps) {
@@ -1797,11 +1802,13 @@ __global__ __launch_bounds__(256, 4) void c1p8_moments_win_kernel(
     if (tile + 1 < t_end) load(tile + 1);   // in flight under this tile's MFMAs
     __syncthreads();
     int hpl = m0 / gpr, gi = m0 - hpl * gpr;
-    for (int j = wave; j < nstep; j += 4) {
-      const bool valid = hpl < TH / 2;
-      const int w0 = hpl * Wp + 8 * gi;
-      u4 a4 = u4{0u, 0u, 0u, 0u};
-      u4 r0 = u4{0u, 0u, 0u, 0u}, r1 = u4{0u, 0u, 0u, 0u};
+    // a step's LDS operands: pooled-gradient fragment, routing words, three input fragments
+    auto fetch = [&](int hp, int gq2, u4& a4, u4& r0, u4& r1, u4 (&bv)[3]) {
+      const bool valid = hp < TH / 2;
+      const int w0 = hp * Wp + 8 * gq2;
+      a4 = u4{0u, 0u, 0u, 0u};
+      r0 = u4{0u, 0u, 0u, 0u};
+      r1 = u4{0u, 0u, 0u, 0u};
       if (valid) {
         const s4 g0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)&gzs[(w0 + q) * COUT + 4 * (p & 1)]);
         const s4 g1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)&gzs[(w0 + 4 + q) * COUT + 4 * (p & 1)]);
@@ -1810,10 +1817,29 @@ __global__ __launch_bounds__(256, 4) void c1p8_moments_win_kernel(
         r0 = *reinterpret_cast<const u4*>(&cds[0][w0 >> 1]);
         r1 = *reinterpret_cast<const u4*>(&cds[1][w0 >> 1]);
       }
-      const int bs = 2 * hpl * XB_RS + 8 * gi;
-      u4 bv[3];
+      const int bs = 2 * hp * XB_RS + 8 * gq2;
 #pragma unroll
       for (int u = 0; u < 3; ++u) bv[u] = *reinterpret_cast<const u4*>(&xc[(bs & bmask[u]) + boff[u]]);
+    };
+#if C1W_PIPE
+    // software pipeline: step j + 4's operands are read before step j's masks and MFMAs
+    u4 na4, nr0, nr1, nbv[3];
+    if (wave < nstep) fetch(hpl, gi, na4, nr0, nr1, nbv);
+#endif
+    for (int j = wave; j < nstep; j += 4) {
+      u4 a4, r0, r1, bv[3];
+#if C1W_PIPE
+      a4 = na4; r0 = nr0; r1 = nr1;
+#pragma unroll
+      for (int u = 0; u < 3; ++u) bv[u] = nbv[u];
+      {
+        int h2 = hpl + dh, g2 = gi + dg;
+        if (g2 >= gpr) { g2 -= gpr; ++h2; }
+        if (j + 4 < nstep) fetch(h2, g2, na4, nr0, nr1, nbv);
+      }
+#else
+      fetch(hpl, gi, a4, r0, r1, bv);
+#endif
       const unsigned av[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
