@@ -535,9 +535,10 @@ int avd_sum_rows_chunks(int rows, int cols) {
   if (rows <= 0 || cols <= 0 || (long long)rows * cols < (1ll << 20)) return 1;
   const int cw = cols <= 2048 ? 16 : 64, ph = 1024 / cw;
   const int cb = avd_cdiv(cols, cw);
-  // target blocks (AVDINO_SUMROWS_BLOCKS, A/B runs; a process-wide constant, so the order of
-  // every reduction is still fixed)
-  static const int target = getenv("AVDINO_SUMROWS_BLOCKS") ? std::max(1, atoi(getenv("AVDINO_SUMROWS_BLOCKS"))) : 1024;
+  // target blocks (AVDINO_SUMROWS_BLOCKS; a process-wide constant, so the order of every
+  // reduction is still fixed).  512 vs 1024: config 5 fp8 18.01 vs 18.10 ms, config 5 bf16 and
+  // config 2 unchanged (profiles/r4g_sumrows_ab.txt)
+  static const int target = getenv("AVDINO_SUMROWS_BLOCKS") ? std::max(1, atoi(getenv("AVDINO_SUMROWS_BLOCKS"))) : 512;
   const int want = avd_cdiv(target, cb), most = rows / (4 * ph);
   const int c = want < most ? want : most;
   return c > 1 ? c : 1;
