@@ -539,6 +539,10 @@ typedef Wg<32, 64, 5, 0, 14, 14, 10, 4, 1, 3, 256, 1, 2> WgI2;
 typedef Wg<WG_A4> WgA4_;
 #define WgA4 WgA4_
 #endif
+#ifdef WG_I2
+typedef Wg<WG_I2> WgI2_;
+#define WgI2 WgI2_
+#endif
 
 bool wg_disabled() {
   const char* e = getenv("AVDINO_CONV_LEGACY");
