@@ -55,8 +55,8 @@ def parse():
                          "ImageEncoder 2 global views B=64 (config 1); simclr = multimodal SimCLR "
                          "with all-gathered NT-Xent negatives, B=2048/GPU (config 4)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32", "fp8"],
-                    help="fp8: e4m3 MFMA forward for the mid-layer convs (config 5), bf16 maps "
-                         "and backward")
+                    help="fp8: the mid-layer convs' forward, input gradient and weight gradient "
+                         "on the block-scaled e4m3 MFMA (config 5); maps stored bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every kernel from Python each step instead of replaying the "
@@ -158,8 +158,8 @@ def build_workload(args, device, act, world, rank, avdist):
                              negatives="global", conv_fp8=args.dtype == "fp8")
     eng.pipeline = args.pipeline
     pool = synthetic_pool(2, B, G, L, device, 1234 + rank)
-    prec = ("block-scaled e4m3 MFMA mid-layer conv forward + input gradient, bf16 maps / weight "
-            "gradients" if args.dtype == "fp8" else args.dtype)
+    prec = ("block-scaled e4m3 MFMA mid-layer conv forward, input gradient and weight gradient, "
+            "bf16 maps" if args.dtype == "fp8" else args.dtype)
     cfg = {"mse": "BASELINE config 2", "infonce": "BASELINE config 3 shape, all-gathered negatives",
            "semi_supervised": f"BASELINE config 5 shape, {prec}",
            "default": "default mode"}[args.mode]

@@ -15,7 +15,7 @@
  *   - host-side state: per-process caches filled on first use and read-only afterwards -- the
  *     CU count and the occupancy of each persistent kernel (hipOccupancy queries that size the
  *     persistent grids, e.g. conv_ws.hip ws_occ, conv_c1p.hip, wgrad_ws.hip, conv3.hip, c1w3.hip,
- *     conv8.hip) and the AVDINO_* environment switches, read once; no state depends on the
+ *     conv_ws8.hip) and the AVDINO_* environment switches, read once; no state depends on the
  *     data, so calls are reentrant for distinct streams (the first calls race benignly: every
  *     thread computes the same value);
  *   - `stream` is a hipStream_t (NULL = default stream); launches are asynchronous;
@@ -607,30 +607,6 @@ int avd_knn_select(const float* S, long long ldS, const float* xnorm, int M, int
  * compute_classification_metrics, dino_train.py:76). */
 int avd_argmax_rows(const float* logits, long long ld, int R, int C, int64_t* idx, void* stream);
 
-/* ------------------------------------------------------------------ fp8 conv path (config 5)
- * BASELINE config 5 ("fp8 MFMA conv path"), SURVEY 7 step 9: the mid-layer conv FORWARD on
- * v_mfma_f32_16x16x32_fp8_fp8 with OCP e4m3fn operands (gfx950); replaces the bf16
- * F.conv2d of CentralUnimodalImage/Audio.forward (unimodal.py:127-221) under the reference's
- * '16-mixed' Trainer precision (run_dino.py:360).  The input stays a bf16 NHWC map and is
- * quantised while staged (per-tensor scale xscale, RNE, saturating at +-448); the weights are
- * quantised per output channel by avd_fp8_weight_quant; y is bf16 NHWC plus BatchNorm partial
- * rows (layout of avd_cl_conv_fwd, avd_fp8_stat_rows rows per group).  The backward stays
- * bf16 (avd_cl_conv_dgrad / avd_cl_conv_wgrad on the stored maps). */
-
-/* Bytes of the e4m3 weight rows [Cout][32*ceil(K*K*Cin/32)] (k = tap*Cin + c). */
-int avd_fp8_weight_elems(int Cout, int Cin, int K);
-/* W f32 [Cout][Cin][K][K] -> wq e4m3 rows and wscale[Cout] = max|W[o]| / 448. */
-int avd_fp8_weight_quant(const float* w, int Cout, int Cin, int K, void* wq, float* wscale,
-                         void* stream);
-/* 1 if (Cin, Cout, K) has an fp8 kernel. */
-int avd_fp8_conv_serves(int Cin, int Cout, int K);
-/* BN partial rows per group written by avd_fp8_conv_fwd (0: not served). */
-int avd_fp8_stat_rows(int Ho, int Wo, int B, int K, int Cin, int Cout);
-/* y = bf16(conv(q(x / xscale), wq) * xscale * wscale[o] + bias[o]); stats as avd_cl_conv_fwd. */
-int avd_fp8_conv_fwd(const void* x, float xscale, const void* wq, const float* wscale,
-                     const float* bias, void* y, float* stats, int N, int B, int Cin, int H,
-                     int W, int Cout, int K, int pad, void* stream);
-
 /* ------------------------------------------------------------------ audio conv1 from its patch Gram
  * The audio conv1 (CentralUnimodalAudio conv1: Conv2d(1, 8, 5, padding=2) on 112x112, bf16) has
  * Cin = 1, so y = w . x25 + b and its BatchNorm statistics follow exactly from the
@@ -678,8 +654,9 @@ int avd_cl_c1r3_codes_combine(const float* moments, const void* wk, const float*
                               float* coef, int G, int Cout, void* stream);
 
 /* ------------------------------------------------------------------ MX (block-scaled) fp8 convs
- * BASELINE config 5 ("fp8 MFMA conv path"): the mid-layer conv forward AND input gradient of
- * CentralUnimodalImage/Audio (unimodal.py:127-221; the F.conv2d and its autograd dX under the
+ * BASELINE config 5 ("fp8 MFMA conv path"): the mid-layer conv forward, input gradient AND
+ * weight gradient of CentralUnimodalImage/Audio (unimodal.py:127-221; the F.conv2d and its
+ * autograd dX / dW under the
  * reference's '16-mixed' precision, run_dino.py:360) on the block-scaled
  * v_mfma_scale_f32_16x16x128_f8f6f4 (gfx950, 2x the bf16 MFMA rate): OCP e4m3 operands with
  * E8M0 scales -- the weights one per (row, 32-k block), quantised per step by
@@ -702,6 +679,10 @@ int avd_mx_weight_layout_batch(int n, const float* const* w, void* const* wq, vo
 /* 1 if the forward (dgrad 0) / input gradient (dgrad 1) of conv Cin -> Cout over H x W has an
  * MX kernel. */
 int avd_mx_conv_serves(int Cin, int H, int W, int Cout, int K, int pad, int dgrad);
+/* Samples per staged strip of that kernel (0: not served): it needs N % NS == 0, and a forward
+ * writing BN partials B % NS == 0 (callers fall back to the bf16 kernels otherwise, e.g. the
+ * last partial batch of the reference's DataLoader, get_data.py:464-467). */
+int avd_mx_conv_ns(int Cin, int H, int W, int Cout, int K, int pad, int dgrad);
 /* BN partial rows per group written by avd_mx_conv_fwd (0: not served). */
 int avd_mx_stat_rows(int H, int W, int B, int K, int Cin, int Cout, int pad);
 int avd_mx_conv_fwd(const void* x, const void* wq, const void* wsc, const float* bias,

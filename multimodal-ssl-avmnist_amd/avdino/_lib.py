@@ -103,11 +103,6 @@ PROTOS = {
     "avd_row_sqnorm": [P, I, I, P, P],
     "avd_knn_select": [P, L, P, I, I, I, P, P, I, P, I, P, P, P],
     "avd_argmax_rows": [P, L, I, I, P, P],
-    "avd_fp8_weight_elems": [I, I, I],
-    "avd_fp8_weight_quant": [P, I, I, I, P, P, P],
-    "avd_fp8_conv_serves": [I, I, I],
-    "avd_fp8_stat_rows": [I, I, I, I, I, I],
-    "avd_fp8_conv_fwd": [P, F, P, P, P, P, P, I, I, I, I, I, I, I, I, P],
     "avd_cl_c1_gram_cols": [],
     "avd_cl_c1_gram": [P, P, I, I, I, I, P],
     "avd_cl_c1_gram_finalize": [P, P, P, P, P, L, F, F, P, P, P, P, P, P, I, P],
@@ -123,6 +118,7 @@ PROTOS = {
     "avd_mx_weight_layout": [P, P, P, I, I, I, I, P],
     "avd_mx_weight_layout_batch": [I, P, P, P, P, P, P, P, P],
     "avd_mx_conv_serves": [I, I, I, I, I, I, I],
+    "avd_mx_conv_ns": [I, I, I, I, I, I, I],
     "avd_mx_stat_rows": [I, I, I, I, I, I, I],
     "avd_mx_conv_fwd": [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, P],
     "avd_mx_conv_dgrad": [P, P, P, P, I, I, I, I, I, I, I, P],

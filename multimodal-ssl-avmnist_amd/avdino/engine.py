@@ -68,9 +68,11 @@ class ConvBranch:
         self.stack = stack
         self.act = act_dtype
         self.dims = stack.layer_dims()
-        # fp8: the layers after the first run their forward and input gradient on the
-        # block-scaled e4m3 MFMA (config 5's "fp8 MFMA conv path", avd_mx_conv_*); maps,
-        # statistics and the weight gradient stay bf16 / f32
+        # fp8: the layers after the first run their forward, input gradient AND weight gradient
+        # on the block-scaled e4m3 MFMA (config 5's "fp8 MFMA conv path", avd_mx_conv_*: both
+        # operands quantised to e4m3 while staged, one E8M0 scale per strip / 32-k block); the
+        # stored maps stay bf16, statistics and accumulators f32.  A layer whose strip size does
+        # not divide the batch (an odd last batch) runs on the bf16 kernels.
         self.fp8 = bool(fp8) and act_dtype == torch.bfloat16
 
     # layers kept on the bf16 kernels in fp8 mode, as "<f|d|w><Cin>x<H>" entries (forward, input
@@ -81,22 +83,22 @@ class ConvBranch:
         ci = self.stack.convs[i][0]
         return f"{kind}{ci}x{self.dims[i][0]}" in self.MX_OFF
 
-    def _mx_ok(self, i, dgrad=False):
+    def _mx_ok(self, i, N, B=None, dgrad=False):
+        """MX kernel for layer i's forward (B: the BN group size when it writes partials) or
+        input gradient over N samples."""
         ci, co, k, p = self.stack.convs[i]
         return (self.fp8 and i > 0 and not self._mx_off("d" if dgrad else "f", i)
-                and ops.mx_conv_serves(ci, self.dims[i][0], co, k, p, dgrad))
+                and ops.mx_conv_serves(ci, self.dims[i][0], co, k, p, dgrad, N, None if dgrad else B))
 
-    # kept for callers of the round-2 name
-    _fp8_ok = _mx_ok
-
-    def prepare(self, ws, store, tag, need_dgrad):
+    def prepare(self, ws, store, tag, need_dgrad, N, B=None):
         """MFMA weight layouts for this step (the weights change every step), per layer:
-        (bf16 forward rows, bf16 dgrad rows, MX forward (e4m3 rows, scales), MX dgrad)."""
+        (bf16 forward rows, bf16 dgrad rows, MX forward (e4m3 rows, scales), MX dgrad).
+        B: BN group size of a training forward (None: eval, no partials)."""
         wts, batch, mxb = [], [], []
         for i, (ci, co, k, _p) in enumerate(self.stack.convs):
             w = store[self.stack.conv_keys[i] + ".weight"]
             wk = wd = q = qd = None
-            if self._mx_ok(i):
+            if self._mx_ok(i, N, B):
                 q = (ws.get(f"{tag}.wq{i}", ops.mx_weight_bytes(co, ci, k, 0), torch.uint8),
                      ws.get(f"{tag}.wqs{i}", ops.mx_scale_bytes(co, ci, k, 0), torch.uint8))
                 mxb.append((w, q[0], q[1], 0))
@@ -104,7 +106,7 @@ class ConvBranch:
                 wk = ws.get(f"{tag}.wk{i}", ops.cl_weight_elems(co, ci, k, 0), self.act)
                 batch.append((w, wk, 0))
             if need_dgrad and i > 0:
-                if self._mx_ok(i, dgrad=True):
+                if self._mx_ok(i, N, dgrad=True):
                     qd = (ws.get(f"{tag}.wqd{i}", ops.mx_weight_bytes(co, ci, k, 1), torch.uint8),
                           ws.get(f"{tag}.wqds{i}", ops.mx_scale_bytes(co, ci, k, 1), torch.uint8))
                     mxb.append((w, qd[0], qd[1], 1))
@@ -156,19 +158,19 @@ class ConvBranch:
     # A/B switch for the statistics pivot (AVDINO_NO_PIVOT=1: raw sums, as before round 3)
     NO_PIVOT = os.environ.get("AVDINO_NO_PIVOT", "0") == "1"
 
-    def _stat_pivot(self, store, i, B):
+    def _stat_pivot(self, store, i, N, B):
         """The BN running mean as the statistics pivot where the producer takes one (the
         persistent mid layers: avd_cl_stat_pivot, and the MX kernels) -- None elsewhere."""
         ci, co, k, _p = self.stack.convs[i]
         Ho = self.dims[i][1]
-        if self.NO_PIVOT or not (self._mx_ok(i) or ops.cl_stat_pivot(Ho, Ho, B, k, ci, co, self.act)):
+        if self.NO_PIVOT or not (self._mx_ok(i, N, B) or ops.cl_stat_pivot(Ho, Ho, B, k, ci, co, self.act)):
             return None
         return store[self.stack.bn_keys[i] + ".running_mean"]
 
-    def _stat_rows(self, i, B):
+    def _stat_rows(self, i, N, B):
         ci, co, k, p = self.stack.convs[i]
         H, Ho = self.dims[i][0], self.dims[i][1]
-        if self._mx_ok(i):
+        if self._mx_ok(i, N, B):
             return ops.mx_stat_rows(H, B, k, ci, co, p)
         return ops.cl_stat_rows(Ho, Ho, B, k, ci, co, self.act)
 
@@ -178,7 +180,7 @@ class ConvBranch:
     def forward(self, ws, store, tag, x, N, G, update_running=True, need_dgrad=False):
         """x: staged input [N,H,W,1] (act dtype).  Returns (features f32 [N, F], ctx)."""
         B = N // G
-        wts = self.prepare(ws, store, tag, need_dgrad)
+        wts = self.prepare(ws, store, tag, need_dgrad, N, B)
         ctx = {"x": [x], "y": [], "stats": [], "wts": wts, "N": N, "G": G}
         h = x
         nl = len(self.stack.convs)
@@ -189,10 +191,10 @@ class ConvBranch:
                                                     need_dgrad)
                 ops.mark(f"{tag}.f{i}")
                 continue
-            R = self._stat_rows(i, B)
+            R = self._stat_rows(i, N, B)
             y = ws.get(f"{tag}.y{i}", N * Ho * Ho * co, self.act)
             parts = ws.get("stat_parts", co * G * R * 2)
-            pv = self._stat_pivot(store, i, B)
+            pv = self._stat_pivot(store, i, N, B)
             self._conv_fwd(i, h, wts[i], store[self.stack.conv_keys[i] + ".bias"], y, parts, N, B, pv)
             st = ws.get(f"{tag}.bn{i}", 4 * G * co).view(4, G * co)
             bk = self.stack.bn_keys[i]
@@ -229,7 +231,7 @@ class ConvBranch:
     def forward_eval(self, ws, store, tag, x, N):
         """Eval-mode forward (nn.Module.eval(): BatchNorm from the running statistics, no
         statistics pass, nothing saved) -> features f32 [N, F]."""
-        wts = self.prepare(ws, store, tag, False)
+        wts = self.prepare(ws, store, tag, False, N)
         h = x
         nl = len(self.stack.convs)
         for i, (ci, co, k, pad) in enumerate(self.stack.convs):

@@ -102,11 +102,16 @@ class SpanTimer:
         self.buf = torch.zeros(3 * cap, dtype=torch.int64, device=device)
 
     def wrap(self, key, nbytes, flops, fn):
-        if key not in self.keys or len(self.slots) >= self.buf.numel() // 3 and key not in self.slots:
+        if key not in self.keys:
             return fn()
-        slot = self.slots.setdefault(key, len(self.slots))
-        self.info[key] = (nbytes, flops)
         st = torch.cuda.current_stream().cuda_stream
+        # one begin/end slot per (key, stream): the same launch key queued on two streams of
+        # one captured step would otherwise overwrite the other's begin mark
+        sk = (key, st)
+        if sk not in self.slots and len(self.slots) >= self.buf.numel() // 3:
+            return fn()
+        slot = self.slots.setdefault(sk, len(self.slots))
+        self.info[key] = (nbytes, flops)
         call("avd_mark_span", p(self.buf), slot, 0, st)
         out = fn()
         call("avd_mark_span", p(self.buf), slot, 1, st)
@@ -116,10 +121,16 @@ class SpanTimer:
         self.buf.zero_()
 
     def read(self):
-        """{key: (launches, total us, bytes per launch, flops per launch)} since reset()."""
+        """{key: (launches, total us, bytes per launch, flops per launch)} since reset(), summed
+        over the streams the key ran on."""
         torch.cuda.synchronize()
         b = self.buf.view(-1, 3).cpu().tolist()
-        return {k: (b[s][2], b[s][1] / 100.0) + self.info[k] for k, s in self.slots.items() if b[s][2]}
+        out = {}
+        for (k, _st), s in self.slots.items():
+            if b[s][2]:
+                n, us = out.get(k, (0, 0.0))[:2]
+                out[k] = (n + b[s][2], us + b[s][1] / 100.0) + self.info[k]
+        return out
 
 
 SPANS = None
@@ -283,45 +294,6 @@ def cl_stat_rows(Ho, Wo, B, K, Cin, Cout, dtype):
     return lib.avd_cl_stat_rows(Ho, Wo, B, K, Cin, Cout, _DT[dtype])
 
 
-# ---- fp8 (e4m3) conv forward (config 5): include/avdino.h "fp8 conv path"
-def fp8_conv_serves(Cin, Cout, K):
-    return bool(lib.avd_fp8_conv_serves(Cin, Cout, K))
-
-
-def fp8_weight_elems(Cout, Cin, K):
-    return lib.avd_fp8_weight_elems(Cout, Cin, K)
-
-
-def fp8_stat_rows(Ho, Wo, B, K, Cin, Cout):
-    return lib.avd_fp8_stat_rows(Ho, Wo, B, K, Cin, Cout)
-
-
-def fp8_weight_quant(w, wq, wscale):
-    """w f32 [Cout, Cin, K, K] -> wq uint8 e4m3 rows + wscale f32 [Cout] (per-channel max/448)."""
-    Cout, Cin, K, _ = w.shape
-    _need(w.dtype == torch.float32 and w.is_contiguous(), "fp8 quant w")
-    _need(wq.dtype == torch.uint8 and wq.numel() >= fp8_weight_elems(Cout, Cin, K), "fp8 quant wq")
-    _need(wscale.dtype == torch.float32 and wscale.numel() >= Cout, "fp8 quant scale")
-    call("avd_fp8_weight_quant", p(w), Cout, Cin, K, p(wq), p(wscale), stream())
-
-
-def fp8_conv_fwd(x, xscale, wq, wscale, bias, y, stats, N, B, Cin, H, W, Cout, K, pad):
-    """bf16 NHWC x -> bf16 NHWC y on the e4m3 MFMA (+bias, + BN partial rows [Cout][N/B][R][2])."""
-    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
-    _need(fp8_conv_serves(Cin, Cout, K), f"fp8 conv: no kernel for {Cin}->{Cout} k{K}")
-    _need(x.dtype == y.dtype == torch.bfloat16, "fp8 conv dtypes (bf16 maps)")
-    _need(x.numel() == N * H * W * Cin and y.numel() == N * Ho * Wo * Cout, "fp8 conv sizes")
-    _need(wq.numel() >= fp8_weight_elems(Cout, Cin, K) and wscale.numel() >= Cout, "fp8 conv weights")
-    if stats is not None:
-        R = fp8_stat_rows(Ho, Wo, B, K, Cin, Cout)
-        _need(R > 0 and stats.numel() >= Cout * (N // B) * R * 2, "fp8 conv stats size")
-    nb = x.numel() * 2 + y.numel() * 2
-    fl = 2 * y.numel() * Cin * K * K
-    _timed(f"fp8_conv_fwd[{N}x{H}x{W}x{Cin}->{Cout} k{K}p{pad}]", nb, fl,
-           lambda: call("avd_fp8_conv_fwd", p(x), float(xscale), p(wq), p(wscale), p(bias), p(y),
-                        p(stats), N, B, Cin, H, W, Cout, K, pad, stream()))
-
-
 # ---- MX (block-scaled e4m3) conv forward + input gradient (config 5): include/avdino.h "MX"
 def mx_weight_bytes(Cout, Cin, K, dgrad):
     return int(lib.avd_mx_weight_bytes(Cout, Cin, K, int(dgrad)))
@@ -357,8 +329,13 @@ def mx_weight_layout_batch(entries):
          IA(*[e[0].shape[2] for e in entries]), IA(*[int(e[3]) for e in entries]), stream())
 
 
-def mx_conv_serves(Cin, H, Cout, K, pad, dgrad):
-    return bool(lib.avd_mx_conv_serves(Cin, H, H, Cout, K, pad, int(dgrad)))
+def mx_conv_serves(Cin, H, Cout, K, pad, dgrad, N=None, B=None):
+    """An MX kernel for this layer shape; with N (and B for a forward with BN partials) also
+    that the strip size divides them (else the caller runs the bf16 kernels)."""
+    ns = lib.avd_mx_conv_ns(Cin, H, H, Cout, K, pad, int(dgrad))
+    if ns <= 0:
+        return False
+    return (N is None or N % ns == 0) and (B is None or B % ns == 0)
 
 
 def mx_stat_rows(H, B, K, Cin, Cout, pad):

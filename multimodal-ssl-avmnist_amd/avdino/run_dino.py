@@ -13,7 +13,10 @@ reference's; the loop is Lightning's automatic optimisation (avdino.trainer.Trai
 training_step -> zero_grad -> backward -> Adam per batch, on_train_epoch_end's linear probe,
 ModelCheckpoint on ``--metric``, CosineAnnealingLR per epoch), then ``load_from_checkpoint``
 of the best epoch and the downstream kNN (k=5) + 10-epoch MLP evaluation
-(``compute_accuracies``, run_dino.py:481-501) when labelled data is available.
+(``compute_accuracies``, run_dino.py:481-501) with ``--downstream``.  As experiment()
+(run_dino.py:346-402) this runs once per seed (1, 2, 3 by default, ``--seeds``), every seed
+from the same initial weights, and reports the mean and standard deviation of the seeds' kNN /
+MLP accuracies in ``final_results_*.csv`` / ``performance_summary.txt``.
 
 Data: with the AVMNIST files under ``data.data_dir`` (get_data.py's layout) the batches come
 from the HBM-resident loader and the device augmentation (avdino.data / avdino.augment, the
@@ -55,6 +58,9 @@ def parse_args(argv=None):
     p.add_argument("--out", default=None, help="checkpoint directory (default: a temp dir)")
     p.add_argument("--downstream", action="store_true",
                    help="after fit: load the best checkpoint, kNN + MLP downstream accuracies")
+    p.add_argument("--seeds", default="1,2,3",
+                   help="comma-separated seeds; one full fit (+ downstream) per seed from the same "
+                        "initial weights (run_dino.py:346: seeds = [1, 2, 3])")
     a = p.parse_args(argv)
     if a.unimodal_model and a.training_mode != "default":
         raise SystemExit(f"--training_mode '{a.training_mode}' is only compatible with --model "
@@ -69,8 +75,9 @@ def load_config(path):
         return yaml.safe_load(f)
 
 
-def build_model(args, config, device="cuda", group=None):
-    """run_dino.py:629-664: the Lightning-shaped module from the config's hyperparameters."""
+def build_model(args, config, device="cuda", group=None, seed=None):
+    """run_dino.py:629-664: the Lightning-shaped module from the config's hyperparameters
+    (``seed``: the module's initialisation / dropout seed, default the config's)."""
     from .models import MODEL_MAP, MULTIMODAL_WRAPPERS, UNIMODAL_MODEL_MAP, UniModalDINOLightning
     h = config["hyperparameters"]
     common = dict(data_dir=config["data"]["data_dir"], projection_dim=h["projection_dim"],
@@ -79,7 +86,8 @@ def build_model(args, config, device="cuda", group=None):
                   learning_rate=h["learning_rate"], num_epochs=h["num_epochs"],
                   weight_decay=h["weight_decay"], dropout=h["dropout"],
                   data_augmentation=h.get("data_augmentation", "burst_noise"),
-                  device=device, precision=args.precision, seed=config["experiment"]["seed"])
+                  device=device, precision=args.precision,
+                  seed=config["experiment"]["seed"] if seed is None else seed)
     if args.model:
         cls = MULTIMODAL_WRAPPERS[args.training_mode]
         return cls(encoder_class=MODEL_MAP[args.model], encoder_output_dim=h["encoder_output_dim"],
@@ -217,9 +225,19 @@ def model_stats(model, G, L):
 def write_run_summary(model, args, config, out, G, L, stats_cb, trainer, training_time,
                       knn=None, mlp=None):
     """run_dino.py:409-464: ``final_results_{model}.csv`` (one row, the reference's columns) and
-    ``performance_summary.txt`` (key: value lines + the augmentation summary)."""
+    ``performance_summary.txt`` (key: value lines + the augmentation summary).  ``knn`` / ``mlp``:
+    the per-seed accuracies (lists; their mean and population std, np.mean / np.std as
+    run_dino.py:395-398), or None without the downstream evaluation; the rest describes the last
+    seed's run, as the reference's summary does."""
     import csv
     from datetime import datetime
+
+    import numpy as np
+    knn_m = knn_s = mlp_m = mlp_s = None
+    if knn:
+        knn_m, knn_s = float(np.mean(knn)), float(np.std(knn))
+    if mlp:
+        mlp_m, mlp_s = float(np.mean(mlp)), float(np.std(mlp))
     h = config["hyperparameters"]
     gflops, params = model_stats(model, G, L)
     name = config.get("model", {}).get("name") or (args.model or args.unimodal_model)
@@ -247,11 +265,10 @@ def write_run_summary(model, args, config, out, G, L, stats_cb, trainer, trainin
         "avg_epoch_time_minutes": f"{epoch_time / 60:.2f}" if epoch_time else "N/A",
         "best_train_loss": f"{float(cm.get('train_loss', 0) or 0):.4f}",
         f"best_{metric}": f"{float(cm.get(metric, 0) or 0):.4f}",
-        "downstream_mlp_acc": f"{mlp:.4f}" if mlp is not None else "N/A",
-        "downstream_knn_accuracy": f"{knn:.4f}" if knn is not None else "N/A",
-        # one seed here (the reference averages 3 seeds): std over one run
-        "downstream_mlp_acc_std": f"{0.0:.4f}" if mlp is not None else "N/A",
-        "downstream_knn_accuracy_std": f"{0.0:.4f}" if knn is not None else "N/A",
+        "downstream_mlp_acc": f"{mlp_m:.4f}" if mlp_m is not None else "N/A",
+        "downstream_knn_accuracy": f"{knn_m:.4f}" if knn_m is not None else "N/A",
+        "downstream_mlp_acc_std": f"{mlp_s:.4f}" if mlp_s is not None else "N/A",
+        "downstream_knn_accuracy_std": f"{knn_s:.4f}" if knn_s is not None else "N/A",
         # gate_image / gate_audio exist only on the gated encoders (not on the MI355X path)
         "final_audio_gate": "N/A", "final_image_gate": "N/A",
     }
@@ -264,12 +281,23 @@ def write_run_summary(model, args, config, out, G, L, stats_cb, trainer, trainin
     return results, perf
 
 
+def _set_seed(seed):
+    """set_seed (run_dino.py's helper): Python, numpy and torch RNGs."""
+    import random
+
+    import numpy as np
+    import torch
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+
+
 def main(argv=None):
+    import copy
     import tempfile
+    import time
 
     import torch
-
-    import time
 
     from .trainer import CSVLogger, ModelCheckpoint, ModelStatsCallback, Trainer
     args = parse_args(argv)
@@ -280,58 +308,77 @@ def main(argv=None):
     rank, world = _init_distributed()
     ddp = config["hardware"].get("num_gpus", 1) > 1 and world > 1
     dev = torch.device("cuda", torch.cuda.current_device())
-    model = build_model(args, config, device=dev)
+    seeds = [int(v) for v in str(args.seeds).split(",") if v.strip()]
+    if not seeds:
+        raise SystemExit("--seeds: at least one seed")
+    # run_dino.py:300: the initial weights every seed starts from
+    initial = copy.deepcopy(build_model(args, config, device=dev).state_dict())
     epochs = args.epochs or h["num_epochs"]
     B = args.batch_size or h["batch_size"]
     G, L = h.get("n_global_views", 2), h.get("n_local_views", 4)
-    seed = config["experiment"]["seed"] + 7919 * rank
     mode = args.training_mode if args.model else None
     real = not args.synthetic and _have_data(config, h)
-    if real:
-        from .augment import MultiModalAugmentation, process_augment_config
-        from .data import AVMNISTDinoLoader, AVMNISTLabelledLoader
-        aug = MultiModalAugmentation(G, L, augment_values=process_augment_config(config))
-        loader = AVMNISTDinoLoader(config["data"]["data_dir"], B, G, L,
-                                   h.get("data_augmentation", "burst_noise"), aug, dev,
-                                   seed=config["experiment"]["seed"], multimodal_mode=mode,
-                                   rank=rank, world=world,
-                                   staged=hasattr(model, "prefetch") and mode is not None)
-        lab = dict(data_dir=config["data"]["data_dir"], batch_size=128, device=dev,
-                   type=h.get("data_augmentation", "burst_noise"), seed=config["experiment"]["seed"])
-        traindata = AVMNISTLabelledLoader(split="train", **lab)
-        validdata = AVMNISTLabelledLoader(split="val", **lab)
-        testdata = AVMNISTLabelledLoader(split="test", **lab)
-    else:
-        loader = SyntheticDinoLoader(B, G, L, args.steps_per_epoch or 20, dev, seed, mode)
-        traindata = synthetic_labelled(B, args.probe_batches, dev, seed + 1)
-        validdata = testdata = traindata[:1]
-    if args.probe_batches or real:
-        model.traindata, model.validdata = traindata, validdata
     out = args.out or tempfile.mkdtemp(prefix="avdino_run_")
+    # run_dino.py:333: ONE ModelCheckpoint for all seeds -- its best score carries over, so a
+    # later seed's best_model_path is that seed's best epoch only if it beats the earlier seeds'
     ckpt = ModelCheckpoint(dirpath=out, monitor=args.metric, save_top_k=1,
                            mode="max" if args.metric == "mlp_acc" else "min")
     stats_cb = ModelStatsCallback()
-    # run_dino.py:355-365: CSVLogger per seed, log_every_n_steps=10, [checkpoint, stats]
-    logger = CSVLogger(out, name=f"logs_seed{config['experiment']['seed']}") if rank == 0 else None
-    trainer = Trainer(max_epochs=epochs, strategy="ddp" if ddp else "auto", precision="16-mixed",
-                      callbacks=[ckpt, stats_cb, _EpochPrinter()], log_every_n_steps=10,
-                      logger=logger, deterministic=True,
-                      limit_train_batches=args.steps_per_epoch if real else None)
-    t0 = time.time()
-    trainer.fit(model, loader)
-    training_time = time.time() - t0
-    knn = mlp = None
-    if args.downstream and trainer.is_global_zero and ckpt.best_model_path:
-        from .downstream import compute_accuracies
-        best = type(model).load_from_checkpoint(ckpt.best_model_path, device=dev,
-                                                precision=args.precision)
-        knn, mlp, _ = compute_accuracies(best.model, traindata, validdata, testdata, out, "model",
-                                         num_epochs=2 if not real else 10)
-        print(json.dumps({"knn_acc": knn, "mlp_acc": mlp}), flush=True)
+    name = config.get("model", {}).get("name") or (args.model or args.unimodal_model)
+    knns, mlps = [], []
+    for s in seeds:
+        _set_seed(s)
+        seed = s + 7919 * rank
+        model = build_model(args, config, device=dev, seed=seed)
+        model.load_state_dict(initial)
+        if real:
+            from .augment import MultiModalAugmentation, process_augment_config
+            from .data import AVMNISTDinoLoader, AVMNISTLabelledLoader
+            aug = MultiModalAugmentation(G, L, augment_values=process_augment_config(config))
+            loader = AVMNISTDinoLoader(config["data"]["data_dir"], B, G, L,
+                                       h.get("data_augmentation", "burst_noise"), aug, dev,
+                                       seed=s, multimodal_mode=mode, rank=rank, world=world,
+                                       staged=hasattr(model, "prefetch") and mode is not None)
+            lab = dict(data_dir=config["data"]["data_dir"], batch_size=128, device=dev,
+                       type=h.get("data_augmentation", "burst_noise"), seed=config["experiment"]["seed"])
+            traindata = AVMNISTLabelledLoader(split="train", **lab)
+            validdata = AVMNISTLabelledLoader(split="val", **lab)
+            testdata = AVMNISTLabelledLoader(split="test", **lab)
+        else:
+            loader = SyntheticDinoLoader(B, G, L, args.steps_per_epoch or 20, dev, seed, mode)
+            traindata = synthetic_labelled(B, args.probe_batches, dev, seed + 1)
+            validdata = testdata = traindata[:1]
+        if args.probe_batches or real:
+            model.traindata, model.validdata = traindata, validdata
+        # run_dino.py:355-365: CSVLogger per seed, log_every_n_steps=10, [checkpoint, stats]
+        logger = CSVLogger(out, name=f"logs_seed{s}") if rank == 0 else None
+        trainer = Trainer(max_epochs=epochs, strategy="ddp" if ddp else "auto", precision="16-mixed",
+                          callbacks=[ckpt, stats_cb, _EpochPrinter()], log_every_n_steps=10,
+                          logger=logger, deterministic=True,
+                          limit_train_batches=args.steps_per_epoch if real else None)
+        t0 = time.time()
+        trainer.fit(model, loader)
+        training_time = time.time() - t0
+        if trainer.is_global_zero:
+            trainer.save_checkpoint(os.path.join(out, f"{name}.ckpt"))       # run_dino.py:379
+        if args.downstream and trainer.is_global_zero and ckpt.best_model_path:
+            from .downstream import compute_accuracies
+            best = type(model).load_from_checkpoint(ckpt.best_model_path, device=dev,
+                                                    precision=args.precision)
+            knn, mlp, _ = compute_accuracies(best.model, traindata, validdata, testdata, out, "model",
+                                             num_epochs=2 if not real else 10)
+            knns.append(knn)
+            mlps.append(mlp)
+            print(json.dumps({"seed": s, "knn_acc": knn, "mlp_acc": mlp}), flush=True)
     if trainer.is_global_zero:
-        write_run_summary(model, args, config, out, G, L, stats_cb, trainer, training_time, knn, mlp)
+        write_run_summary(model, args, config, out, G, L, stats_cb, trainer, training_time,
+                          knns or None, mlps or None)
+        if knns:
+            print(json.dumps({"knn_acc_mean": sum(knns) / len(knns), "mlp_acc_mean": sum(mlps) / len(mlps),
+                              "seeds": seeds}), flush=True)
     model.trainer_ = trainer
     model.out_dir_ = out
+    model.seed_accuracies_ = {"knn": knns, "mlp": mlps}
     return model
 
 

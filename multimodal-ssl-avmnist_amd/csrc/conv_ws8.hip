@@ -920,6 +920,25 @@ int avd_mx_conv_serves(int Cin, int H, int W, int Cout, int K, int pad, int dgra
          is8<D8A4>(Cout, Ho, Wo, Cin, K, dp) || is8<D8I2>(Cout, Ho, Wo, Cin, K, dp);
 }
 
+// samples per strip (NS) of the MX kernel serving the forward (dgrad = 0) or input gradient
+// (dgrad = 1) of the conv Cin -> Cout over H x W (0: not served); the launch needs N % NS == 0,
+// and a forward that writes BN partials also B % NS == 0
+int avd_mx_conv_ns(int Cin, int H, int W, int Cout, int K, int pad, int dgrad) {
+  if (!dgrad) {
+    if (is8<F8A2>(Cin, H, W, Cout, K, pad)) return F8A2::NS;
+    if (is8<F8A3>(Cin, H, W, Cout, K, pad)) return F8A3::NS;
+    if (is8<F8A4>(Cin, H, W, Cout, K, pad)) return F8A4::NS;
+    if (is8<F8I2>(Cin, H, W, Cout, K, pad)) return F8I2::NS;
+    return 0;
+  }
+  const int Ho = H + 2 * pad - K + 1, Wo = W + 2 * pad - K + 1, dp = K - 1 - pad;
+  if (is8<D8A2>(Cout, Ho, Wo, Cin, K, dp)) return D8A2::NS;
+  if (is8<D8A3>(Cout, Ho, Wo, Cin, K, dp)) return D8A3::NS;
+  if (is8<D8A4>(Cout, Ho, Wo, Cin, K, dp)) return D8A4::NS;
+  if (is8<D8I2>(Cout, Ho, Wo, Cin, K, dp)) return D8I2::NS;
+  return 0;
+}
+
 // BN partial rows per group written by avd_mx_conv_fwd (0: not served)
 int avd_mx_stat_rows(int H, int W, int B, int K, int Cin, int Cout, int pad) {
   auto rows = [&](auto l) -> int {

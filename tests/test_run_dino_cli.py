@@ -39,7 +39,7 @@ def test_run_dino_two_epochs_on_device(argv, capsys):
     import json
     from avdino import run_dino as R
     m = R.main(argv + ["--config", CFG, "--epochs", "2", "--steps-per-epoch", "3",
-                       "--batch-size", "8", "--probe-batches", "2", "--synthetic"])
+                       "--batch-size", "8", "--probe-batches", "2", "--synthetic", "--seeds", "1"])
     recs = [json.loads(line) for line in capsys.readouterr().out.splitlines() if line.startswith("{")]
     assert len(recs) == 2 and all(r["train_loss"] == r["train_loss"] for r in recs)
     assert 0 <= recs[-1]["mlp_acc"] <= 100
@@ -47,6 +47,39 @@ def test_run_dino_two_epochs_on_device(argv, capsys):
     assert recs[1]["lr"] < recs[0]["lr"] == pytest.approx(1e-4)
     assert m.model.engine.step_idx == 6
     assert m.trainer_.global_step == 6
+
+
+@pytest.mark.gpu
+def test_run_dino_three_seeds_downstream(tmp_path, capsys):
+    """experiment() (run_dino.py:346-402): seeds 1-3 from the same initial weights, each a full
+    fit + best-checkpoint reload + kNN / MLP downstream; the summary holds the seeds' mean and
+    population std (np.mean / np.std), one CSVLogger directory per seed."""
+    import json
+
+    import numpy as np
+    from avdino import run_dino as R
+    m = R.main(["--model", "multi_central", "--training_mode", "mse", "--config", CFG, "--epochs", "1",
+                "--steps-per-epoch", "2", "--batch-size", "8", "--probe-batches", "2", "--synthetic",
+                "--downstream", "--out", str(tmp_path)])
+    recs = [json.loads(line) for line in capsys.readouterr().out.splitlines() if line.startswith("{")]
+    per = [r for r in recs if "seed" in r]
+    assert [r["seed"] for r in per] == [1, 2, 3]
+    knn = [r["knn_acc"] for r in per]
+    mlp = [r["mlp_acc"] for r in per]
+    assert m.seed_accuracies_ == {"knn": knn, "mlp": mlp}
+    summ = dict(line.split(": ", 1) for line in open(tmp_path / "performance_summary.txt").read().splitlines()
+                if ": " in line)
+    assert float(summ["downstream_knn_accuracy"]) == pytest.approx(np.mean(knn), abs=1e-4)
+    assert float(summ["downstream_mlp_acc_std"]) == pytest.approx(np.std(mlp), abs=1e-4)
+    for s in (1, 2, 3):
+        assert (tmp_path / f"logs_seed{s}").is_dir()
+    assert (tmp_path / "multi_central.ckpt").exists() or any(tmp_path.glob("*.ckpt"))
+
+
+def test_seeds_argument():
+    from avdino import run_dino as R
+    a = R.parse_args(["--model", "multi_central", "--config", CFG])
+    assert a.seeds == "1,2,3"                     # run_dino.py:346
 
 
 def test_submit_models_surface(tmp_path):
