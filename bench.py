@@ -77,6 +77,11 @@ def parse():
     ap.add_argument("--dominant", default=None, metavar="KEY",
                     help="use this launch key as the roofline kernel instead of the warm-up's "
                          "most expensive one (tools/gpu_pmc.sh passes the bench line's key)")
+    ap.add_argument("--probe", action="store_true",
+                    help="--mode semi_supervised (config 5): after the timed region, time one "
+                         "epoch-end linear-probe epoch (on_train_epoch_end, dino.py:878-951: 55000 "
+                         "train + 5000 validation samples in batches of 128, dino.py:795-802) and "
+                         "report it separately under \"probe\" (SURVEY 8(d)); not part of value")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"),
                     help="PMC traffic table written by tools/pmc_traffic.py")
     return ap.parse_args()
@@ -165,6 +170,39 @@ def build_workload(args, device, act, world, rank, avdist):
            "default": "default mode"}[args.mode]
     return (eng, pool, B, f"multi_central {args.mode} training step, B={B}/GPU, {G} global + {L} "
                           f"local views, E=D={E}, P={P} ({cfg})", "multi_central")
+
+
+def time_probe(eng, args, device, act, rank):
+    """One epoch-end linear-probe epoch over the trained student (avdino.probe.LinearProbe =
+    DownstreamClassifier + AdamW over the reference's AVMNISTDataModule loaders, batch 128):
+    synthetic labelled samples resident in HBM, one warm-up pass over a few batches (workspace
+    sizing), then the full epoch timed with a device sync on both sides."""
+    from avdino.probe import LinearProbe
+    n_train, n_val, pb = 55000, 5000, 128
+    gen = torch.Generator(device=device).manual_seed(4321 + rank)
+
+    def split(n):
+        img = torch.randint(0, 256, (n, 1, 28, 28), generator=gen, device=device, dtype=torch.int32).float() / 255.0
+        aud = torch.randint(0, 256, (n, 1, 112, 112), generator=gen, device=device, dtype=torch.int32).float() / 255.0
+        lab = torch.randint(0, 10, (n,), generator=gen, device=device)
+        return [(img[i:i + pb], aud[i:i + pb], lab[i:i + pb]) for i in range(0, n, pb)]
+
+    train, valid = split(n_train), split(n_val)
+    probe = LinearProbe(eng.store, "multi_central", eng.D, eng.E, lr=eng.hp.lr, act_dtype=act,
+                        fusion_dropout=eng.hp.fusion_dropout)
+    probe.run_epoch(train[:3], valid[:2])             # warm-up: workspaces, first launches
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = probe.run_epoch(train, valid)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"epoch_ms": round(el * 1e3, 2), "samples_per_s": round((n_train + n_val) / el, 1),
+            "train_batches": len(train), "valid_batches": len(valid), "batch": pb,
+            "train_samples": n_train, "valid_samples": n_val, "dtype": args.dtype if args.dtype != "fp8" else "bf16",
+            "mlp_acc": round(out["mlp_acc"], 3), "val_loss": round(out["val_loss"], 5),
+            "what": "on_train_epoch_end linear probe (dino.py:878-951): frozen train-mode student copy, "
+                    "Linear(D,128)-ReLU-Linear(128,10) with AdamW per batch over the train split, then "
+                    "eval-mode evaluate() over the validation split; synthetic AVMNIST-shaped data in HBM"}
 
 
 def host_cpu():
@@ -546,6 +584,10 @@ def main():
         "teacher_pipelined": bool(getattr(eng, "pipeline", False)),
         "final_loss": round(lv, 6),
     }
+    if args.probe:
+        if args.workload != "dino" or args.mode != "semi_supervised":
+            raise SystemExit("--probe: the epoch-end probe is timed for --mode semi_supervised (config 5)")
+        out["probe"] = time_probe(eng, args, device, act, rank)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "dino" \
             and args.mode == "mse":
         out["cpu_baseline"] = cpu_baseline(args.cpu_batch, args.cpu_seconds)

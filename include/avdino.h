@@ -58,6 +58,26 @@ int avd_version(void);
 /* Human-readable name of the last HIP error seen by this thread (or "ok"). */
 const char* avd_last_error(void);
 
+/* Launch options.  The library reads no environment variables: every kernel route is the
+ * measured default unless a caller sets one of these test hooks explicitly (process-wide, set
+ * between launches, not while kernels are being queued from another thread):
+ *   grid_cap      > 0: the persistent kernels (conv_ws, wgrad_ws, conv_ws8, the conv1 passes)
+ *                 launch at most this many blocks, so at test sizes every block walks several
+ *                 tiles as at bench size; 0 = no cap;
+ *   generic_conv  1: every bf16 mid-layer conv / input gradient / weight gradient on the generic
+ *                 conv_cl / wgrad_cl kernels instead of the weights-stationary ones;
+ *   generic_m2    1: the BN-backward reduce of a (c,h,w)-flatten tail on the generic pooled
+ *                 reduce instead of its dedicated kernel. */
+typedef struct {
+  int grid_cap;
+  int generic_conv;
+  int generic_m2;
+} avd_options;
+/* Copy *opts into the library (NULL: the defaults, all zero). */
+int avd_set_options(const avd_options* opts);
+/* The current options. */
+int avd_get_options(avd_options* opts);
+
 /* ------------------------------------------------------------------ conv blocks
  * One CentralNet / CNN block is conv(KxK, stride 1) -> BatchNorm2d(train) -> ReLU -> maxpool2
  * (models/unimodal.py:127-153 and 185-211; models/dino.py:18-73).
@@ -211,47 +231,6 @@ int avd_cl_bn_bwd_reduce_pooled(const void* y, int dt, const void* pooled, const
                                 int mode, const float* gamma, const float* beta, const float* mean,
                                 const float* invstd, float* parts, int N, int B, int C, int H,
                                 int W, void* stream);
-
-/* avd_cl_conv_dgrad fused with the NEXT backward step's avd_cl_bn_bwd_reduce_pooled (bf16, the
- * 5x5 mid-layer convs of CentralUnimodalAudio conv2-4 / CentralUnimodalImage conv2): dx is the
- * gradient of this conv's input `pooled` [N,H,W,Cin] = maxpool2(relu(bn(yprev))) with yprev
- * [N,2H,2W,Cin] the previous layer's conv output, so the dgrad epilogue forms that layer's
- * BatchNorm-backward partial sums from dx while it is in registers -- dx is not read back.
- * parts [Cin][N/B][R][2], R = avd_cl_dgrad_bnreduce_rows() (0 = shape not served: use the two
- * unfused calls); gamma/beta/mean/invstd are the previous layer's.  A channel whose xhat needs y
- * (gamma == 0 or |beta| > 8|gamma|) triggers a second pass inside this call that rewrites the
- * rows from yprev.  Same sums as the unfused pair up to fp32 summation order; dx bit-identical
- * to avd_cl_conv_dgrad.  Replaces the tail of nn.BatchNorm2d's backward behind
- * unimodal.py:160-221 (autograd of the reference). */
-int avd_cl_dgrad_bnreduce_rows(int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
-                               int pad);
-int avd_cl_conv_dgrad_bnreduce(const void* dy, const void* wk_d, void* dx, const void* pooled,
-                               const void* yprev, const float* gamma, const float* beta,
-                               const float* mean, const float* invstd, float* parts, int dt, int N,
-                               int B, int Cin, int H, int W, int Cout, int K, int pad,
-                               void* stream);
-
-/* BatchNorm-backward apply fused into BOTH consumers of dy, for the mid-layer convs (bf16):
- * the input- and weight-gradient kernels read the conv output y [N,Ho,Wo,Cout] and the pooled
- * gradient gout (layout gmode: 0 = pooled NHWC in dt, 2 = f32 [N][Cout*Ho/2*Wo/2] in (c,h,w)
- * flatten order) and form dy = avd_cl_bn_bwd_apply(y, gout, gmode, scale, shift, coef) tile by
- * tile on chip, so dy is never written or read (replaces avd_cl_bn_bwd_apply +
- * avd_cl_conv_wgrad + avd_cl_conv_dgrad for CentralUnimodalAudio conv2-4 / bn2-4 and
- * CentralUnimodalImage conv2 / bn2, unimodal.py:127-221).  B = samples per BN group (N/B <= 8).
- * avd_cl_bnapply_ok() = 1 when both kernels serve the shape, else use the three unfused calls
- * (AVD_ERR_SHAPE from either entry point otherwise).  Bit-identical to the unfused calls.
- * avd_cl_conv_dgrad_bnapply's dy (nullable, NHWC like y, not aliasing y or dx) also receives the
- * dy it forms, so a plain avd_cl_conv_wgrad can follow without a separate apply pass. */
-int avd_cl_bnapply_ok(int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
-                      int gmode);
-int avd_cl_conv_dgrad_bnapply(const void* y, const void* gout, int gmode, const float* scale,
-                              const float* shift, const float* coef, const void* wk_d, void* dx,
-                              void* dy, int dt, int N, int B, int Cin, int H, int W, int Cout,
-                              int K, int pad, void* stream);
-int avd_cl_conv_wgrad_bnapply(const void* x, const void* y, const void* gout, int gmode,
-                              const float* scale, const float* shift, const float* coef, int dt,
-                              float* dw_parts, int N, int B, int Cin, int H, int W, int Cout,
-                              int K, int pad, void* stream);
 
 /* The same first layer WITHOUT storing its conv output: every pass recomputes y = conv(x) + b
  * (bf16-rounded, bit-identical across passes) into an on-chip tile from the 8x smaller input.

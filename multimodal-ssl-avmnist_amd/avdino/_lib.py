@@ -21,6 +21,8 @@ D = ctypes.c_double
 # name -> argtypes (restype is always c_int except where noted)
 PROTOS = {
     "avd_version": [],
+    "avd_set_options": [P],
+    "avd_get_options": [P],
     "avd_bn_finalize": [P, I, I, I, L, P, P, F, F, P, P, P, P, P, P, P, I, P],
     "avd_bn_bwd_finalize": [P, I, I, I, L, P, P, P, P, P, P, P, I, P],
     "avd_gemm": [I, I, I, P, L, L, P, L, L, P, L, P, F, F, I, P, L, P],
@@ -37,9 +39,7 @@ PROTOS = {
     "avd_cl_conv_dgrad": [P, P, P, I, I, I, I, I, I, I, I, P],
     "avd_cl_wgrad_chunks": [I, I, I, I],
     "avd_cl_conv_wgrad": [P, P, I, P, I, I, I, I, I, I, I, P],
-    "avd_cl_bnapply_ok": [I, I, I, I, I, I, I, I, I, I],
     "avd_cl_bn_bwd_reduce_pooled": [P, I, P, P, I, P, P, P, P, P, I, I, I, I, I, P],
-    "avd_cl_dgrad_bnreduce_rows": [I, I, I, I, I, I, I, I, I],
     "avd_cl_c1_moment_cols": [I, I],
     "avd_cl_c1_codes_rows": [I, I, I, I],
     "avd_cl_c1_codes_cols": [],
@@ -56,9 +56,6 @@ PROTOS = {
     "avd_counters_add": [P, P, P, I, P],
     "avd_mark": [P, I, P],
     "avd_mark_span": [P, I, I, P],
-    "avd_cl_conv_dgrad_bnreduce": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
-    "avd_cl_conv_dgrad_bnapply": [P, P, I, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
-    "avd_cl_conv_wgrad_bnapply": [P, P, P, I, P, P, P, I, P, I, I, I, I, I, I, I, I, P],
     "avd_cl_bn_relu_pool": [P, I, P, P, P, I, I, I, I, I, I, P],
     "avd_cl_bn_bwd_rows": [I, I, I, I, I],
     "avd_cl_bn_bwd_reduce": [P, I, P, I, P, P, P, P, P, I, I, I, I, I, P],

@@ -19,7 +19,6 @@ MI355X-native restructuring (results identical up to fp32 rounding):
   * cat() of image/audio features is a strided GEMM write; slices are pointer offsets;
   * EMA / Adam / grad all-reduce run on flat arenas (params.py).
 """
-import os
 
 import torch
 
@@ -28,9 +27,8 @@ from .capture import GraphedStep, host_point  # noqa: F401  (GraphedStep re-expo
 from .spec import HEAD_NAMES, MULTI_ENCODERS, PROJ_HIDDEN, UNI_ALIASES, UNI_ENCODERS
 
 F32 = torch.float32
-# early gradient buckets at a host point inside the step (AVDINO_GRAD_BUCKETS=0: one all-reduce
-# after the step)
-BUCKETS = os.environ.get("AVDINO_GRAD_BUCKETS", "1") == "1"
+# early gradient buckets at a host point inside the step (False: one all-reduce after the step)
+BUCKETS = True
 
 
 class Workspace:
@@ -75,19 +73,11 @@ class ConvBranch:
         # not divide the batch (an odd last batch) runs on the bf16 kernels.
         self.fp8 = bool(fp8) and act_dtype == torch.bfloat16
 
-    # layers kept on the bf16 kernels in fp8 mode, as "<f|d|w><Cin>x<H>" entries (forward, input
-    # gradient, weight gradient of the layer with Cin input channels at H x H), e.g. "d16x56"
-    MX_OFF = {v.strip() for v in os.environ.get("AVDINO_MX_OFF", "").split(",") if v.strip()}
-
-    def _mx_off(self, kind, i):
-        ci = self.stack.convs[i][0]
-        return f"{kind}{ci}x{self.dims[i][0]}" in self.MX_OFF
-
     def _mx_ok(self, i, N, B=None, dgrad=False):
         """MX kernel for layer i's forward (B: the BN group size when it writes partials) or
         input gradient over N samples."""
         ci, co, k, p = self.stack.convs[i]
-        return (self.fp8 and i > 0 and not self._mx_off("d" if dgrad else "f", i)
+        return (self.fp8 and i > 0
                 and ops.mx_conv_serves(ci, self.dims[i][0], co, k, p, dgrad, N, None if dgrad else B))
 
     def prepare(self, ws, store, tag, need_dgrad, N, B=None):
@@ -138,7 +128,7 @@ class ConvBranch:
 
     def _mx_wgrad(self, i, N):
         ci, co, k, p = self.stack.convs[i]
-        return (self.fp8 and i > 0 and not self._mx_off("w", i)
+        return (self.fp8 and i > 0
                 and ops.mx_wgrad_chunks(N, ci, self.dims[i][0], co, k, p) > 0)
 
     def _wgrad_chunks(self, i, N):
@@ -155,15 +145,12 @@ class ConvBranch:
         else:
             ops.cl_conv_wgrad(x, dy, wparts, N, ci, H, H, co, k, pad)
 
-    # A/B switch for the statistics pivot (AVDINO_NO_PIVOT=1: raw sums, as before round 3)
-    NO_PIVOT = os.environ.get("AVDINO_NO_PIVOT", "0") == "1"
-
     def _stat_pivot(self, store, i, N, B):
         """The BN running mean as the statistics pivot where the producer takes one (the
         persistent mid layers: avd_cl_stat_pivot, and the MX kernels) -- None elsewhere."""
         ci, co, k, _p = self.stack.convs[i]
         Ho = self.dims[i][1]
-        if self.NO_PIVOT or not (self._mx_ok(i, N, B) or ops.cl_stat_pivot(Ho, Ho, B, k, ci, co, self.act)):
+        if not (self._mx_ok(i, N, B) or ops.cl_stat_pivot(Ho, Ho, B, k, ci, co, self.act)):
             return None
         return store[self.stack.bn_keys[i] + ".running_mean"]
 
@@ -252,28 +239,27 @@ class ConvBranch:
             h = out
         return h.view(N, -1)
 
-    # ---- first layer without a stored conv output (avd_cl_c1_recompute): the audio conv1
-    # For a training forward, off by default: measured slower than storing y (the recomputing
-    # backward passes are VALU-bound); AVDINO_L1_RECOMPUTE=1 turns it on for experiments.
-    RECOMPUTE = os.environ.get("AVDINO_L1_RECOMPUTE", "0") == "1"
+    # ---- first layer without a stored conv output (avd_cl_c1_recompute).  The route switches
+    # below are plain class attributes (tests flip them to compare routes; nothing reads the
+    # environment).
     # forwards without a backward (the teacher): y is never needed, so never stored -- stats
     # and apply passes recompute it from the 8x smaller input (r1_34: +1.5 % step rate)
-    RC_NOGRAD = os.environ.get("AVDINO_L1_RC_NOGRAD", "1") == "1"
+    RC_NOGRAD = True
     # stored-y forward whose BN -> ReLU -> pool recomputes y from x instead of reading the
     # 1.44 GB it just wrote (bit-identical y; r1_34: +0.5 %)
-    RC_APPLY = os.environ.get("AVDINO_L1_RC_APPLY", "1") == "1"
+    RC_APPLY = True
     # 3x3 first layers (the SimCLR / unimodal encoders): recompute passes c1r3_kernel, whose y
     # is one MFMA per 16 channels x 16 pixels from the staged input tile
-    RECOMPUTE3 = os.environ.get("AVDINO_L1_RECOMPUTE3", "1") == "1"
+    RECOMPUTE3 = True
     # their backward as one pass (avd_cl_c1_recompute pass 4) + a tiny combine: dW is linear in
     # dy = k1 dz + kx y + k0, so the pass accumulates sum dz x9 and the Gram matrix of x9
-    RC_MOMENTS = os.environ.get("AVDINO_L1_RC_MOMENTS", "1") == "1"
+    RC_MOMENTS = True
     # the 5x5 audio conv1 in training: no stored y either -- its backward is the one moments
     # pass (x and the pooled gradient in, BN-backward sums + dW moments out) and a combine
-    MOMENTS5 = os.environ.get("AVDINO_L1_MOMENTS5", "1") == "1"
+    MOMENTS5 = True
 
     def _recompute_ok(self, N, B, ci, H, co, k, pad, need_dgrad=True):
-        rc = self.RECOMPUTE or (self.RECOMPUTE3 and k == 3) or (self.RC_NOGRAD and not need_dgrad)
+        rc = (self.RECOMPUTE3 and k == 3) or (self.RC_NOGRAD and not need_dgrad)
         if not rc and self.MOMENTS5 and self.RC_MOMENTS and k == 5 and self.act == torch.bfloat16:
             rc = ops.cl_c1_recompute_rows(ops.C1_REDUCE_MOMENTS, self.act, N, B, ci, H, H, co, k, pad) > 0
         return (rc and self.act == torch.bfloat16 and
@@ -281,13 +267,13 @@ class ConvBranch:
 
     # the 5x5 conv1 backwards from the forward's routing codes: the audio conv1 (1->8 at 112^2,
     # avd_cl_c1_moments_codes) and the image conv1 (1->32 at 28^2, avd_cl_c1r5_moments_codes);
-    # AVDINO_C1_CODES=0 keeps the recomputing moments pass (pass 4) for both
-    CODES = os.environ.get("AVDINO_C1_CODES", "1") == "1"
+    # False keeps the recomputing moments pass (pass 4) for both
+    CODES = True
 
     # the image conv1's forward passes (statistics; BN -> ReLU -> pool [+ codes]) on the
-    # pixel-major MFMA kernels of c1r5.hip (one pooling window per lane); AVDINO_C1R5_PM=0 runs
-    # them on c1r3 passes 0 / 1 instead (same pooled map; statistics summed in another order)
-    PIXEL_MAJOR = os.environ.get("AVDINO_C1R5_PM", "1") == "1"
+    # pixel-major MFMA kernels of c1r5.hip (one pooling window per lane); False runs them on
+    # c1r3 passes 0 / 1 instead (same pooled map; statistics summed in another order)
+    PIXEL_MAJOR = True
 
     def _pixel_major(self, N, B):
         ci, co, k, pad = self.stack.convs[0]
@@ -311,12 +297,12 @@ class ConvBranch:
         return None
 
     # the 3x3 first layers (SimCLR / unimodal encoders) routed the same way (avd_cl_c1r3_*);
-    # AVDINO_C1R3_CODES=0 keeps the recomputing moments pass (c1r3 pass 4)
-    CODES3 = os.environ.get("AVDINO_C1R3_CODES", "1") == "1"
+    # False keeps the recomputing moments pass (c1r3 pass 4)
+    CODES3 = True
 
     # the audio conv1's BN statistics from its patch Gram matrix (avd_cl_c1_gram) instead of a
-    # recomputing statistics pass; AVDINO_C1_GRAM=0 restores the latter
-    GRAM = os.environ.get("AVDINO_C1_GRAM", "1") == "1"
+    # recomputing statistics pass; False restores the latter
+    GRAM = True
 
     def _gram_ok(self, N, B):
         ci, co, k, pad = self.stack.convs[0]
@@ -458,32 +444,11 @@ class ConvBranch:
                             shift=st[3], coef=coef, gz=gout, out=wparts)
         ops.sum_rows(wparts, nsl, co * ci * k * k, store.grad_of(ck + ".weight"))
 
-    # BN-backward apply fused into the dgrad/wgrad staging (avd_cl_conv_*_bnapply, bit-identical
-    # to the unfused chain).  Off by default: measured slower (r1_27: 2.62 ms fused vs 2.17 ms
-    # apply + dgrad + wgrad for the four mid layers) -- the window math in the staging phase costs
-    # registers (occupancy 2 -> 1) and is not hidden behind the MFMAs.  AVDINO_BNAPPLY_FUSED=1.
-    BNAPPLY_FUSED = os.environ.get("AVDINO_BNAPPLY_FUSED", "0") == "1"
-    # the previous layer's BN-backward partial sums formed in the dgrad epilogue
-    # (avd_cl_conv_dgrad_bnreduce): the pooled gradient is not read back by a reduce pass
-    DGRAD_BNREDUCE = os.environ.get("AVDINO_DGRAD_BNREDUCE", "0") == "1"
-
-    def _dgrad_reduce_rows(self, ctx, i, N, B):
-        """Rows of the fused dgrad + previous-layer reduce at layer i (> 0), 0 = unfused."""
-        if (not self.DGRAD_BNREDUCE or self.act != torch.bfloat16 or ctx["y"][i - 1] is None
-                or ctx["wts"][i][1] is None):
-            return 0
-        ci, co, k, pad = self.stack.convs[i]
-        H = self.dims[i][0]
-        if self.dims[i - 1][1] != 2 * H:
-            return 0
-        return ops.cl_dgrad_bnreduce_rows(self.act, N, B, ci, H, H, co, k, pad)
-
-    # input-gradient kernel forms the BN-backward apply and stores dy (AVDINO_DGRAD_APPLY=1)
-    DGRAD_APPLY = os.environ.get("AVDINO_DGRAD_APPLY", "0") == "1"
-    # layers whose weight gradient stays on the main stream (A/B: AVDINO_WGRAD_MAIN=3,2)
-    WGRAD_MAIN = {int(v) for v in os.environ.get("AVDINO_WGRAD_MAIN", "").split(",") if v.strip()}
-    # A/B: the side-stream weight gradients issued after the whole input-gradient chain
-    WGRAD_DEFER = os.environ.get("AVDINO_WGRAD_DEFER", "0") == "1"
+    # Measured and removed (round 5 pruning): the BN-backward apply fused into
+    # the dgrad / wgrad staging (2.62 vs 2.17 ms for the four mid layers), the previous layer's
+    # BN-backward reduce in the dgrad epilogue (146k vs 159k pairs/s), the dgrad storing dy
+    # (160.2k vs 166.7k), weight gradients on the main stream or deferred after the input-gradient
+    # chain (within noise).
 
     def backward(self, ws, store, ctx, dfeat, wstream=None):
         """dfeat: f32 [N, F] gradient of the features; writes conv/BN parameter grads.
@@ -494,8 +459,7 @@ class ConvBranch:
         gout = dfeat
         nl = len(self.stack.convs)
         main = torch.cuda.current_stream(dfeat.device) if wstream is not None else None
-        wdone, deferred = [], []
-        fused = None       # (parts, R) this layer's reduce already formed by the dgrad above it
+        wdone = []
         for i in reversed(range(nl)):
             ci, co, k, pad = self.stack.convs[i]
             H, Ho, Hp = self.dims[i]
@@ -509,10 +473,7 @@ class ConvBranch:
             R = ops.cl_bn_bwd_rows(B, co, Ho, Ho, self.act)
             parts = ws.get("bwd_parts", co * G * R * 2)
             pooled = ctx["x"][i + 1] if i < nl - 1 else ctx.get("feat")
-            if fused is not None:
-                parts, R = fused
-                fused = None
-            elif mode in (0, 2) and pooled is not None and Ho % 2 == 0:
+            if mode in (0, 2) and pooled is not None and Ho % 2 == 0:
                 # from the pooled output (2/4 of y's bytes): xhat = (p - beta)/gamma at the argmax
                 ops.cl_bn_bwd_reduce_pooled(y, pooled, gout, mode, store[bk + ".weight"],
                                             store[bk + ".bias"], st[0], st[1], parts, N, B, co, Ho, Ho)
@@ -532,82 +493,28 @@ class ConvBranch:
                 ops.mark(f"b{i}")
                 continue
             nch = self._wgrad_chunks(i, N)
-            wparts = ws.get("wgrad_parts", nch * co * ci * k * k)
-            if (self.BNAPPLY_FUSED and i > 0 and mode in (0, 2) and ctx["wts"][i][1] is not None and
-                    ops.cl_bnapply_ok(self.act, N, B, ci, H, H, co, k, pad, mode)):
-                # dy = BN-backward apply is formed inside both consumers (no dy tensor)
-                ops.cl_conv_wgrad_bnapply(x, y, gout, mode, st[2], st[3], coef, wparts, N, B, ci, H, H,
-                                          co, k, pad)
-                ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
-                dx = ws.get("bwd_dx", N * H * H * ci, self.act)
-                ops.cl_conv_dgrad_bnapply(y, gout, mode, st[2], st[3], coef, ctx["wts"][i][1], dx, N, B,
-                                          ci, H, H, co, k, pad)
-                gout = dx
-                continue
             dy = ws.get(f"bwd_dy{i}" if wstream is not None else "bwd_dy", N * Ho * Ho * co, self.act)
-            if (self.DGRAD_APPLY and i > 0 and mode in (0, 2) and ctx["wts"][i][1] is not None
-                    and not self._dgrad_reduce_rows(ctx, i, N, B)
-                    and ops.cl_bnapply_ok(self.act, N, B, ci, H, H, co, k, pad, mode)):
-                # BN-backward apply formed in the input-gradient kernel's staging, which also
-                # stores dy for the weight gradient (no separate apply pass re-reading y)
-                dx = ws.get(f"bwd_dx{i % 2}", N * H * H * ci, self.act)   # != gout (bwd_dx{(i+1) % 2})
-                ops.cl_conv_dgrad_bnapply(y, gout, mode, st[2], st[3], coef, ctx["wts"][i][1], dx, N, B,
-                                          ci, H, H, co, k, pad, dy=dy)
-                if wstream is not None:
-                    wparts = ws.get(f"wgrad_parts{i}", nch * co * ci * k * k)
-                    wstream.wait_stream(main)
-                    with torch.cuda.stream(wstream):
-                        self._conv_wgrad(i, x, dy, wparts, N)
-                        ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
-                        ev = torch.cuda.Event()
-                        ev.record(wstream)
-                    wdone.append(ev)
-                else:
+            ops.cl_bn_bwd_apply(y, gout, mode, st[2], st[3], coef, dy, N, B, co, Ho, Ho)
+            if wstream is not None and i > 0:
+                wparts = ws.get(f"wgrad_parts{i}", nch * co * ci * k * k)
+                wstream.wait_stream(main)
+                with torch.cuda.stream(wstream):
+                    ops.mark(f"w{i}.begin")
                     self._conv_wgrad(i, x, dy, wparts, N)
                     ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
-                gout = dx
-                continue
-            ops.cl_bn_bwd_apply(y, gout, mode, st[2], st[3], coef, dy, N, B, co, Ho, Ho)
-            if wstream is not None and i > 0 and i not in self.WGRAD_MAIN:
-                wparts = ws.get(f"wgrad_parts{i}", nch * co * ci * k * k)
-
-                def wg(i=i, x=x, dy=dy, wparts=wparts, nch=nch, co=co, ci=ci, k=k, ck=ck):
-                    with torch.cuda.stream(wstream):
-                        ops.mark(f"w{i}.begin")
-                        self._conv_wgrad(i, x, dy, wparts, N)
-                        ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
-                        ops.mark(f"w{i}.end")
-                        ev = torch.cuda.Event()
-                        ev.record(wstream)
-                    wdone.append(ev)
-                if self.WGRAD_DEFER:
-                    deferred.append(wg)
-                else:
-                    wstream.wait_stream(main)
-                    wg()
+                    ops.mark(f"w{i}.end")
+                    ev = torch.cuda.Event()
+                    ev.record(wstream)
+                wdone.append(ev)
             else:
+                wparts = ws.get("wgrad_parts", nch * co * ci * k * k)
                 self._conv_wgrad(i, x, dy, wparts, N)
                 ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
             if i > 0:
                 dx = ws.get("bwd_dx", N * H * H * ci, self.act)
-                Rf = self._dgrad_reduce_rows(ctx, i, N, B)
-                if Rf:
-                    pk = self.stack.bn_keys[i - 1]
-                    pst = ctx["stats"][i - 1]
-                    fparts = ws.get("bwd_parts_rd", ci * G * Rf * 2)
-                    ops.cl_conv_dgrad_bnreduce(dy, ctx["wts"][i][1], dx, ctx["x"][i], ctx["y"][i - 1],
-                                               store[pk + ".weight"], store[pk + ".bias"], pst[0], pst[1],
-                                               fparts, N, B, ci, H, H, co, k, pad)
-                    fused = (fparts, Rf)
-                else:
-                    self._conv_dgrad(i, dy, ctx["wts"][i], dx, N)
+                self._conv_dgrad(i, dy, ctx["wts"][i], dx, N)
                 gout = dx
             ops.mark(f"b{i}")
-        if deferred:
-            # the weight gradients after the whole input-gradient chain (it runs alone)
-            wstream.wait_stream(main)
-            for wg in deferred:
-                wg()
         for ev in wdone:
             main.wait_event(ev)
 
@@ -804,11 +711,10 @@ class MultiCentralEngine:
         # teacher forward and the image-branch backward run on a side stream with their own
         # scratch (Workspace, split-K GEMM buffer), joined by events; concurrent=False keeps
         # everything on the caller's stream
-        concurrent = concurrent and os.environ.get("AVDINO_SINGLE_STREAM", "0") != "1"
+        # (one stream: 146.7k vs 162.6k pairs/s in round 2)
         self.side = torch.cuda.Stream(store.device) if (concurrent and store.device.type == "cuda") else None
-        # the audio branch's mid-layer weight gradients on a third stream (AVDINO_WGRAD_SIDE=0: off)
-        self.wside = (torch.cuda.Stream(store.device) if (self.side is not None and
-                      os.environ.get("AVDINO_WGRAD_SIDE", "1") == "1") else None)
+        # the audio branch's mid-layer weight gradients on a third stream
+        self.wside = torch.cuda.Stream(store.device) if self.side is not None else None
         self.tws = Workspace(store.device) if self.side is not None else self.ws
         self.iws = Workspace(store.device) if self.side is not None else self.ws
         self.grad_hook = grad_hook      # e.g. DDP all-reduce of store.grad (avdino.dist)
@@ -849,13 +755,10 @@ class MultiCentralEngine:
         (ops.alloc_epoch) and this engine's own workspaces."""
         return (ops.alloc_epoch(), self.ws.epoch, self.tws.epoch, self.iws.epoch)
 
-    # student image branch on the side stream, concurrently with the audio branch: measured
-    # slower (r1_39: 149.7k vs 152.4k pairs/s -- both branches' launches fill the chip, so
-    # they only contend), kept for experiments
-    IMAGE_SIDE = os.environ.get("AVDINO_IMAGE_SIDE", "0") == "1"
-    # the heads' backward queued interleaved with the main chain's (else after it)
-    INTERLEAVE = os.environ.get("AVDINO_INTERLEAVE", "1") == "1"
-    FHEADS_LATE = os.environ.get("AVDINO_FHEADS_LATE", "1") == "1"
+    # the heads' backward queued interleaved with the main chain's (else after it); the
+    # originals' heads forward queued after the fusion / projection (else before)
+    INTERLEAVE = True
+    FHEADS_LATE = True
 
     # -------------------------------------------------------------- streams
     def _on_side(self, fn, after=None):
@@ -886,25 +789,15 @@ class MultiCentralEngine:
         ws, st, E = ws or self.ws, self.store, self.E
         cat = ws.get(tag + ".cat", N * 2 * E)
 
-        def image():
-            iws = self.iws if side_image else ws
-            fi, ci = ib.forward(iws, st, tag + ".img", x_img, N, G, update_running, need_dgrad)
-            lin = f"{prefix}.{self.img_lin}"
-            ops.linear_fwd(fi, st[lin + ".weight"], st[lin + ".bias"], cat, N, out_ld=2 * E, out_off=0,
-                           mode=self.gm)
-            return fi, ci
-
-        # the student's image branch (cat columns [0, E)) on the side stream, concurrently with
-        # its audio branch (columns [E, 2E)); the teacher runs there already, so never for it
-        side_image = self.IMAGE_SIDE and prefix == "student" and self.side is not None
-        if side_image:
-            (fi, ci), i_done = self._on_side(image)
-        else:
-            (fi, ci), i_done = image(), None
+        # (the student's image branch on the side stream beside its audio branch measured slower:
+        # 149.7k vs 152.4k pairs/s, r1_39 -- both fill the chip)
+        fi, ci = ib.forward(ws, st, tag + ".img", x_img, N, G, update_running, need_dgrad)
+        lin = f"{prefix}.{self.img_lin}"
+        ops.linear_fwd(fi, st[lin + ".weight"], st[lin + ".bias"], cat, N, out_ld=2 * E, out_off=0,
+                       mode=self.gm)
         fa, ca = ab.forward(ws, st, tag + ".aud", x_aud, N, G, update_running, need_dgrad)
         lin = f"{prefix}.{self.aud_lin}"
         ops.linear_fwd(fa, st[lin + ".weight"], st[lin + ".bias"], cat, N, out_ld=2 * E, out_off=E, mode=self.gm)
-        self._join(i_done)
         return cat, (fi, ci, fa, ca)
 
     def _fusion_fwd(self, prefix, cat, rows, tag, seed, ws=None, seed_off=None):
@@ -922,8 +815,8 @@ class MultiCentralEngine:
         return out, (h, r)
 
     # the next real-data batch's device augmentation queued on a data stream under the current
-    # step (prefetch); AVDINO_AUG_PREFETCH=0 stages every batch synchronously
-    PREFETCH = os.environ.get("AVDINO_AUG_PREFETCH", "1") == "1"
+    # step (prefetch); False stages every batch synchronously
+    PREFETCH = True
 
     def _aug_bufs(self, batch, with_orig, par):
         """Staged-input buffers of set ``par`` (0/1) for a {"aug", "idx"} batch:

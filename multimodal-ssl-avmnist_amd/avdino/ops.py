@@ -4,7 +4,8 @@ Every function takes torch tensors that live on the HIP device, checks shapes/dt
 host, and launches on torch's current stream.  PyTorch is used here only for device memory
 and streams; all arithmetic happens in libavdino.so.
 """
-import os
+import contextlib
+import ctypes
 
 import torch
 
@@ -31,6 +32,35 @@ def p(t):
 
 def stream():
     return torch.cuda.current_stream().cuda_stream
+
+
+class _Options(ctypes.Structure):
+    """avd_options (include/avdino.h)."""
+    _fields_ = [("grid_cap", ctypes.c_int), ("generic_conv", ctypes.c_int), ("generic_m2", ctypes.c_int)]
+
+
+def get_options():
+    o = _Options()
+    call("avd_get_options", ctypes.byref(o))
+    return {k: getattr(o, k) for k, _ in _Options._fields_}
+
+
+@contextlib.contextmanager
+def options(**kw):
+    """The library's launch options (avd_set_options: grid_cap, generic_conv, generic_m2 -- test
+    hooks; the library reads no environment variables) set for the duration of the block."""
+    old = _Options()
+    call("avd_get_options", ctypes.byref(old))
+    new = _Options(old.grid_cap, old.generic_conv, old.generic_m2)
+    for k, v in kw.items():
+        if k not in dict(_Options._fields_):
+            raise KeyError(f"avd_options has no field {k!r}")
+        setattr(new, k, int(v))
+    call("avd_set_options", ctypes.byref(new))
+    try:
+        yield
+    finally:
+        call("avd_set_options", ctypes.byref(old))
 
 
 class KernelTimer:
@@ -220,8 +250,8 @@ def linear_fwd(x, w, b, out, rows, x_ld=None, x_off=0, out_ld=None, out_off=0, m
          mode=mode)
 
 
-# Linear backward's dW and dX GEMMs in one launch (avd_linear_bwd); AVDINO_PAIR_BWD=0: two launches
-PAIR_BWD = os.environ.get("AVDINO_PAIR_BWD", "1") == "1"
+# Linear backward's dW and dX GEMMs in one launch (avd_linear_bwd); False: two GEMM launches
+PAIR_BWD = True
 
 
 def linear_bwd(dout, x, w, dw, db, dx, rows, dout_ld=None, dout_off=0, x_ld=None, x_off=0,
@@ -448,50 +478,6 @@ def cl_conv_wgrad(x, dy, parts, N, Cin, H, W, Cout, K, pad):
                         K, pad, stream()))
 
 
-def cl_bnapply_ok(dtype, N, B, Cin, H, W, Cout, K, pad, gmode):
-    """True when the input- and weight-gradient kernels can apply the layer's BatchNorm backward
-    themselves (avd_cl_bnapply_ok): then no dy tensor is needed."""
-    return bool(lib.avd_cl_bnapply_ok(_DT[dtype], N, B, Cin, H, W, Cout, K, pad, gmode))
-
-
-def _gout_check(gout, gmode, y, N, Ho, Wo, Cout):
-    want = N * (Ho // 2) * (Wo // 2) * Cout
-    _need(gout.numel() == want and (gout.dtype == y.dtype if gmode == 0 else gout.dtype == torch.float32),
-          "bnapply gout")
-
-
-def cl_conv_dgrad_bnapply(y, gout, gmode, scale, shift, coef, wk_d, dx, N, B, Cin, H, W, Cout, K, pad,
-                          dy=None):
-    """dx = input gradient of the conv for dy = bn_bwd_apply(y, gout, ...) formed on chip;
-    ``dy`` (optional, like y) also receives that dy (for the weight gradient)."""
-    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
-    _need(y.numel() == N * Ho * Wo * Cout and dx.numel() == N * H * W * Cin, "bnapply dgrad sizes")
-    _need(y.dtype == dx.dtype == wk_d.dtype, "bnapply dgrad dtypes")
-    _need(dy is None or (dy.numel() == y.numel() and dy.dtype == y.dtype), "bnapply dgrad dy")
-    _gout_check(gout, gmode, y, N, Ho, Wo, Cout)
-    nb = ((y.numel() + dx.numel() + (0 if dy is None else dy.numel())) * y.element_size()
-          + gout.numel() * gout.element_size())
-    fl = 2 * N * Cin * H * W * Cout * K * K
-    _timed(f"cl_conv_dgrad_bnapply{'' if dy is None else '+dy'}[{N}x{Ho}x{Wo}x{Cout}->{Cin} k{K}p{pad} "
-           f"g{gmode} {y.dtype}]", nb, fl,
-           lambda: call("avd_cl_conv_dgrad_bnapply", p(y), p(gout), gmode, p(scale), p(shift), p(coef),
-                        p(wk_d), p(dx), p(dy), dtcode(y), N, B, Cin, H, W, Cout, K, pad, stream()))
-
-
-def cl_conv_wgrad_bnapply(x, y, gout, gmode, scale, shift, coef, parts, N, B, Cin, H, W, Cout, K, pad):
-    """Weight-gradient slabs (as cl_conv_wgrad) for dy = bn_bwd_apply(y, gout, ...) formed on chip."""
-    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
-    _need(x.numel() == N * H * W * Cin and y.numel() == N * Ho * Wo * Cout, "bnapply wgrad sizes")
-    _need(x.dtype == y.dtype, "bnapply wgrad dtypes")
-    _gout_check(gout, gmode, y, N, Ho, Wo, Cout)
-    _need(parts.numel() >= cl_wgrad_chunks(N, Cout, Cin, K) * Cout * Cin * K * K, "bnapply wgrad parts")
-    nb = (x.numel() + y.numel()) * x.element_size() + gout.numel() * gout.element_size()
-    fl = 2 * y.numel() * Cin * K * K
-    _timed(f"cl_conv_wgrad_bnapply[{N}x{H}x{W}x{Cin}->{Cout} k{K}p{pad} g{gmode} {x.dtype}]", nb, fl,
-           lambda: call("avd_cl_conv_wgrad_bnapply", p(x), p(y), p(gout), gmode, p(scale), p(shift),
-                        p(coef), dtcode(x), p(parts), N, B, Cin, H, W, Cout, K, pad, stream()))
-
-
 def cl_bn_relu_pool(y, scale, shift, out, mode, N, B, C, H, W):
     """mode 0: NHWC pooled (y dtype); 1: GAP f32 [N,C]; 2: f32 (c,h,w)-flattened pooled map."""
     _need(y.numel() == N * H * W * C, "cl pool y")
@@ -535,31 +521,6 @@ def counters_add(arena, idx, val):
     _need(arena.dtype == idx.dtype == val.dtype == torch.int64 and idx.numel() == val.numel(),
           "counters_add operands")
     call("avd_counters_add", p(arena), p(idx), p(val), idx.numel(), stream())
-
-
-def cl_dgrad_bnreduce_rows(dtype, N, B, Cin, H, W, Cout, K, pad):
-    """Rows per group of avd_cl_conv_dgrad_bnreduce's partial sums; 0 = shape not served."""
-    return lib.avd_cl_dgrad_bnreduce_rows(_DT[dtype], N, B, Cin, H, W, Cout, K, pad)
-
-
-def cl_conv_dgrad_bnreduce(dy, wk_d, dx, pooled, yprev, gamma, beta, mean, invstd, parts, N, B,
-                           Cin, H, W, Cout, K, pad):
-    """cl_conv_dgrad + the previous layer's cl_bn_bwd_reduce_pooled (gout = dx, pooled = this
-    conv's input) in one pass: the sums are formed in the dgrad epilogue."""
-    Ho, Wo = H + 2 * pad - K + 1, W + 2 * pad - K + 1
-    R = cl_dgrad_bnreduce_rows(dy.dtype, N, B, Cin, H, W, Cout, K, pad)
-    _need(R > 0, "dgrad_bnreduce: shape not served")
-    _need(dy.numel() == N * Ho * Wo * Cout and dx.numel() == N * H * W * Cin, "dgrad_bnreduce sizes")
-    _need(pooled.numel() == dx.numel() and yprev.numel() == 4 * dx.numel(), "dgrad_bnreduce maps")
-    _need(dy.dtype == dx.dtype == wk_d.dtype == pooled.dtype == yprev.dtype, "dgrad_bnreduce dtypes")
-    _need(parts.numel() >= Cin * (N // B) * R * 2, "dgrad_bnreduce parts")
-    nb = (dy.numel() + dx.numel() + pooled.numel()) * dy.element_size()
-    fl = 2 * N * Cin * H * W * Cout * K * K
-    _timed(f"cl_conv_dgrad_bnreduce[{N}x{Ho}x{Wo}x{Cout}->{Cin} k{K}p{pad} {dy.dtype}]", nb, fl,
-           lambda: call("avd_cl_conv_dgrad_bnreduce", p(dy), p(wk_d), p(dx), p(pooled), p(yprev),
-                        p(gamma), p(beta), p(mean), p(invstd), p(parts), dtcode(dy), N, B, Cin, H, W,
-                        Cout, K, pad, stream()))
-    return R
 
 
 def cl_bn_bwd_apply(y, gout, mode, scale, shift, coef, dy, N, B, C, H, W):
@@ -842,7 +803,7 @@ def c1r5_codes_combine(moments, wk, bias, gamma, mean, invstd, count, dw, dgamma
 
 
 _SUM_WS = {}
-_SUM_SPLIT = os.environ.get("AVDINO_SUMROWS_SPLIT", "1") == "1"   # 0: single pass (A/B runs)
+_SUM_SPLIT = True      # row chunks in parallel (False: one pass)
 
 
 def sum_rows(x, rows, cols, out, accumulate=0, ld=None, off=0):

@@ -348,6 +348,56 @@ __global__ __launch_bounds__(1024) void sum_rows_kernel(const float* __restrict_
   }
 }
 
+// The 16-byte path of sum_rows_kernel (cols and ld multiples of 4, 16-byte aligned in / out):
+// each lane owns 4 consecutive columns (one global_load_dwordx4 per row), CQ lanes per row phase
+// and 1024 / CQ phases per block; a phase sums its rows in double, row order, 4 rows' loads in
+// flight, then thread (0, lane) folds the phases in phase order.  Fixed order, deterministic.
+template <int CQ>
+__global__ __launch_bounds__(1024) void sum_rows4_kernel(const float* __restrict__ in, int rows,
+                                                         int cols, long long ld,
+                                                         float* __restrict__ out, int accumulate,
+                                                         int rows_per_chunk) {
+  constexpr int PH = 1024 / CQ;
+  __shared__ double sh[PH][CQ][4];
+  const int lq = threadIdx.x % CQ, ph = threadIdx.x / CQ;
+  const int c = 4 * (blockIdx.x * CQ + lq);
+  const int r0 = blockIdx.y * rows_per_chunk;
+  const int r1 = min(rows, r0 + rows_per_chunk);
+  out += (size_t)blockIdx.y * cols;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (c < cols) {
+    const float* base = in + c;
+    int r = r0 + ph;
+    for (; r + 3 * PH < r1; r += 4 * PH) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(base + (size_t)(r + u * PH) * ld);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s0 += (double)v[u].x; s1 += (double)v[u].y; s2 += (double)v[u].z; s3 += (double)v[u].w;
+      }
+    }
+    for (; r < r1; r += PH) {
+      const float4 v = *reinterpret_cast<const float4*>(base + (size_t)r * ld);
+      s0 += (double)v.x; s1 += (double)v.y; s2 += (double)v.z; s3 += (double)v.w;
+    }
+  }
+  sh[ph][lq][0] = s0; sh[ph][lq][1] = s1; sh[ph][lq][2] = s2; sh[ph][lq][3] = s3;
+  __syncthreads();
+  if (ph == 0 && c < cols) {
+    double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
+    for (int k = 0; k < PH; ++k) {
+      t0 += sh[k][lq][0]; t1 += sh[k][lq][1]; t2 += sh[k][lq][2]; t3 += sh[k][lq][3];
+    }
+    float4* o = reinterpret_cast<float4*>(out + c);
+    if (accumulate) {
+      const float4 a = *o;
+      t0 += a.x; t1 += a.y; t2 += a.z; t3 += a.w;
+    }
+    *o = make_float4((float)t0, (float)t1, (float)t2, (float)t3);
+  }
+}
+
 __global__ __launch_bounds__(1024) void sum_kernel(const float* __restrict__ in, int n, float scale,
                                                    float* out) {
   __shared__ double sh[16];
@@ -397,11 +447,9 @@ int avd_bn_finalize(float* parts, int G, int R, int C, long long count, const fl
   if ((running_mean == nullptr) != (running_var == nullptr)) return AVD_ERR_ARG;
   hipStream_t st = avd_stream(stream);
   // single pass (one block per channel reads all G*R rows of its channel: one launch instead of
-  // two) up to AVDINO_FIN1_ROWS = max G*R rows; 0 = two passes always.  Round-4 A/B on the
-  // config-2 step (3 interleaved rounds): 5.483 vs 5.516 ms, so single pass is the default
-  static const long long fin1_rows =
-      getenv("AVDINO_FIN1_ROWS") ? atoll(getenv("AVDINO_FIN1_ROWS")) : (1ll << 30);
-  if (G <= 256 && R <= FIN1_MAXROWS && (long long)G * R <= fin1_rows) {
+  // two) where it fits.  Round-4 A/B on the config-2 step (3 interleaved rounds): 5.483 vs
+  // 5.516 ms for the two-pass form, which stays for larger G / R
+  if (G <= 256 && R <= FIN1_MAXROWS) {
     bn_finalize1_kernel<<<C, 256, 0, st>>>(parts, G, R, C, count, gamma, beta, eps, momentum, mean,
                                            invstd, scale, shift, running_mean, running_var, pivot,
                                            pivot_gs);
@@ -507,10 +555,25 @@ int avd_bn1d_bwd_apply(const float* x, const float* dz, const float* coef, float
   return AVD_OK;
 }
 
+// columns per block of the launch sum_rows takes for this shape (the 16-byte path when cols % 4
+// == 0; the chunk count, and with it the summation order, depends on the shape only)
+static int sum_rows_cw(int cols) {
+  if (cols % 4 == 0) return cols <= 2048 ? 64 : 256;
+  return cols <= 2048 ? 16 : 64;
+}
+
 static void launch_sum_rows(const float* in, int rows, int cols, long long ld, float* out,
                             int accumulate, int chunks, hipStream_t st) {
   const int rpc = avd_cdiv(rows, chunks);
-  if (cols <= 2048)
+  const bool v4 = cols % 4 == 0 && ld % 4 == 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  if (v4 && cols <= 2048)
+    sum_rows4_kernel<16><<<dim3(avd_cdiv(cols, 64), chunks), 1024, 0, st>>>(in, rows, cols, ld, out,
+                                                                           accumulate, rpc);
+  else if (v4)
+    sum_rows4_kernel<64><<<dim3(avd_cdiv(cols, 256), chunks), 1024, 0, st>>>(in, rows, cols, ld, out,
+                                                                            accumulate, rpc);
+  else if (cols <= 2048)
     sum_rows_kernel<16><<<dim3(avd_cdiv(cols, 16), chunks), 1024, 0, st>>>(in, rows, cols, ld, out,
                                                                           accumulate, rpc);
   else
@@ -533,12 +596,11 @@ int avd_sum_rows(const float* in, int rows, int cols, long long ld, float* out, 
 int avd_sum_rows_chunks(int rows, int cols) {
   // small inputs: one launch (a second one costs more than the single pass takes)
   if (rows <= 0 || cols <= 0 || (long long)rows * cols < (1ll << 20)) return 1;
-  const int cw = cols <= 2048 ? 16 : 64, ph = 1024 / cw;
+  const int cw = sum_rows_cw(cols), ph = 1024 / (cols % 4 == 0 ? cw / 4 : cw);
   const int cb = avd_cdiv(cols, cw);
-  // target blocks (AVDINO_SUMROWS_BLOCKS; a process-wide constant, so the order of every
-  // reduction is still fixed).  512 vs 1024: config 5 fp8 18.01 vs 18.10 ms, config 5 bf16 and
-  // config 2 unchanged (profiles/r4g_sumrows_ab.txt)
-  static const int target = getenv("AVDINO_SUMROWS_BLOCKS") ? std::max(1, atoi(getenv("AVDINO_SUMROWS_BLOCKS"))) : 512;
+  // >= ~128 blocks per launch: a wide slab stack (51200 columns: 200 blocks of 1024 threads, 16
+  // rows of 16-byte loads per thread) is one pass, narrow ones split their rows
+  const int target = 128;
   const int want = avd_cdiv(target, cb), most = rows / (4 * ph);
   const int c = want < most ? want : most;
   return c > 1 ? c : 1;

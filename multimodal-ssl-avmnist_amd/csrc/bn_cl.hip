@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) void bwd_reduce_pooled_cl_kernel(
     const T* __restrict__ y, const void* __restrict__ pooled, const void* __restrict__ gout,
     int mode, const float* __restrict__ gamma, const float* __restrict__ beta,
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ parts,
-    int G, int B, int C, int H, int W, int R, long long per, int fixup) {
+    int G, int B, int C, int H, int W, int R, long long per) {
   constexpr int V = Vec<T>::V;
   __shared__ float sh[256][2 * V + 1];
   const int Hp = H / 2, Wp = W / 2, CV = C / V;
@@ -262,16 +262,6 @@ __global__ __launch_bounds__(256) void bwd_reduce_pooled_cl_kernel(
   const int c0 = cv * V;
   const long long nwin = (long long)B * Hp * Wp;
   const long long w0 = r * per, w1 = std::min(nwin, w0 + per);
-  if (fixup) {
-    // fix-up pass after a dgrad that formed these sums in its epilogue (conv_ws.hip, RD): only
-    // when some channel needs xhat from y are the rows rewritten (all of them, by this kernel)
-    bool need = false;
-    for (int c = 0; c < C; ++c) {
-      const float ga = gamma[c], bb = beta[c];
-      need |= ga == 0.f || fabsf(bb) > (sizeof(T) == 2 ? 8.f : 4096.f) * fabsf(ga);
-    }
-    if (!need) return;
-  }
   float ig[V], be[V], mu[V], is[V], s1[V], s2[V], gs[V];
   bool any0 = false;
 #pragma unroll
@@ -552,8 +542,8 @@ int avd_cl_bn_bwd_rows_impl(int B, int C, int H, int W, int dt) {
   const long long nwin = (long long)B * (H / 2) * (W / 2);
   const int slots = 256 / std::max(1, C / V);
   // windows per slot (thread) of a partial row: long enough that the block's fixed reduction is
-  // amortised over several rounds of 4 in-flight windows (AVDINO_BWD_WPS overrides)
-  static const int wps = getenv("AVDINO_BWD_WPS") ? std::max(1, atoi(getenv("AVDINO_BWD_WPS"))) : 16;
+  // amortised over several rounds of 4 in-flight windows
+  constexpr int wps = 16;
   const long long r = (nwin + (long long)slots * wps - 1) / ((long long)slots * wps);
   return (int)std::max(1ll, std::min(r, 4096ll));
 }
@@ -614,7 +604,7 @@ int avd_cl_bn_bwd_reduce_pooled_impl(const void* y, int dt, const void* pooled, 
   const long long nwin = (long long)B * (H / 2) * (W / 2);
   const long long per = (nwin + R - 1) / R;
   dim3 grid(R, G);
-  if (mode == 2 && R <= B && !getenv("AVDINO_REDUCE_M2_GENERIC")) {
+  if (mode == 2 && R <= B && !g_opts.generic_m2) {
     const dim3 g2(R, G, (C + 3) / 4);
     if (dt == AVD_BF16)
       bwd_reduce_pooled_m2_kernel<bf16><<<g2, 256, 0, st>>>((const bf16*)y, (const float*)pooled,
@@ -630,29 +620,12 @@ int avd_cl_bn_bwd_reduce_pooled_impl(const void* y, int dt, const void* pooled, 
   if (dt == AVD_BF16)
     bwd_reduce_pooled_cl_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)y, pooled, gout, mode, gamma,
                                                             beta, mean, invstd, parts, G, B, C, H, W,
-                                                            R, per, 0);
+                                                            R, per);
   else
     bwd_reduce_pooled_cl_kernel<float><<<grid, 256, 0, st>>>((const float*)y, pooled, gout, mode, gamma,
                                                              beta, mean, invstd, parts, G, B, C, H, W,
-                                                             R, per, 0);
+                                                             R, per);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
 
-// Fix-up pass of avd_cl_conv_dgrad_bnreduce (bf16, NHWC pooled maps): R rows as the dgrad
-// wrote them; every block returns at once unless a channel needs xhat from y.
-int avd_cl_bn_bwd_reduce_pooled_fixup_impl(const void* y, const void* pooled, const void* gout,
-                                           const float* gamma, const float* beta,
-                                           const float* mean, const float* invstd, float* parts,
-                                           int R, int N, int B, int C, int H, int W,
-                                           hipStream_t st) {
-  if (C % 8 || C / 8 > 256 || N % B || (H & 1) || (W & 1) || R <= 0) return AVD_ERR_SHAPE;
-  const int G = N / B;
-  const long long nwin = (long long)B * (H / 2) * (W / 2);
-  const long long per = (nwin + R - 1) / R;
-  bwd_reduce_pooled_cl_kernel<bf16><<<dim3(R, G), 256, 0, st>>>((const bf16*)y, pooled, gout, 0, gamma,
-                                                                beta, mean, invstd, parts, G, B, C, H,
-                                                                W, R, per, 1);
-  AVD_CHECK_LAUNCH();
-  return AVD_OK;
-}

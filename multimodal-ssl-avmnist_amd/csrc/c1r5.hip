@@ -31,23 +31,12 @@ using namespace avd;
 
 namespace {
 
-constexpr int C = 32, KK = 25, IH = 28, IW = 28, VW = 32;   // channels, taps, image, virtual width
+constexpr int C = 32, KK = 25, IH = 28, IW = 28;            // channels, taps, image
 constexpr int HP = IH / 2, WP = IW / 2, NWIN = HP * WP;     // pooling windows per sample
 constexpr int MOMC5 = C * KK + KK * KK + KK + C;
 constexpr int C1R5_GMAX = 32;                              // BN groups served by the combine
-constexpr int NCOPY = 6, CROWS = IH + 4;                     // copies: tx = -2..2, ones; rows: pad 2
 constexpr int XS_R = IH + 4, XS_C = 40;                     // staged image, 2-pixel halo, 16-B rows
 constexpr int LDS_X = XS_R * XS_C;                           // bf16 elements
-// shifted copies: 48-element rows (32 used) and 1544-element copies, so the 16 taps of a
-// B-fragment ds_read_b128 spread over the bank slots (2 extra cycles per read instead of 16,
-// tools/lds_conflicts.py c1r5)
-constexpr int CP_RS = 48, CP_CS = CROWS * CP_RS + 8;
-constexpr int LDS_CP = NCOPY * CP_CS;
-// dZ channel stride: 28 rows x 32 columns + 16 pad elements (1824 B = 32 mod 256): the 16
-// channels of an A-fragment ds_read_b128 fall on 16 distinct 16-byte bank slots (no pad: all on
-// one, 16-way), tools/lds_conflicts.py c1r5
-constexpr int CSTR = IH * VW + 16;
-constexpr int LDS_DZ = C * CSTR;
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f4;
@@ -65,217 +54,6 @@ __device__ __forceinline__ int dppi(int v) {
 // per-thread global vectors of one sample: x 98, gz 784, codes 196 (16-byte vectors)
 constexpr int NXV = IH * IW / 8, NGV = NWIN * C / 8, NCV = NWIN * 8 / 8;
 constexpr int NVEC = NXV + NGV + NCV, VPT = (NVEC + 255) / 256;
-
-__global__ __launch_bounds__(256, 2) void c1r5_moments_codes_kernel(
-    const bf16* __restrict__ x, const bf16* __restrict__ gz, const unsigned short* __restrict__ codes,
-    float* __restrict__ out, int B, int G, int R) {
-  __shared__ __attribute__((aligned(16))) bf16 xs[LDS_X];
-  __shared__ __attribute__((aligned(16))) bf16 cp[LDS_CP];
-  __shared__ __attribute__((aligned(16))) bf16 dz[LDS_DZ];
-  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int g = lane >> 4, r16 = lane & 15;
-  const int grp = (int)blockIdx.x / R, rr = (int)blockIdx.x - grp * R;
-  const int s_begin = grp * B + (int)(((long long)B * rr) / R);
-  const int s_end = grp * B + (int)(((long long)B * (rr + 1)) / R);
-
-  // constant parts: zero halo of the staged image, zero virtual columns of dZ, the ones copy
-  for (int i = tid; i < LDS_X / 8; i += 256) reinterpret_cast<u4*>(xs)[i] = u4{0u, 0u, 0u, 0u};
-  for (int i = tid; i < LDS_DZ / 8; i += 256) reinterpret_cast<u4*>(dz)[i] = u4{0u, 0u, 0u, 0u};
-  for (int i = tid; i < CROWS * VW / 8; i += 256) {
-    const int row = i / (VW / 8), seg = i - row * (VW / 8);
-    const bool rv = row >= 2 && row < IH + 2;
-    u4 v;
-    unsigned* vw = reinterpret_cast<unsigned*>(&v);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int c0 = 8 * seg + 2 * k;
-      const unsigned lo = (rv && c0 < IW) ? 0x3F80u : 0u, hi = (rv && c0 + 1 < IW) ? 0x3F80u : 0u;
-      vw[k] = lo | (hi << 16);
-    }
-    *reinterpret_cast<u4*>(cp + 5 * CP_CS + row * CP_RS + 8 * seg) = v;
-  }
-
-  // this lane's taps: tile 0 = taps 0..15, tile 1 = taps 16..31 (25 = ones, > 25 = zero)
-  int toff[2];
-  bool tzero[2];
-#pragma unroll
-  for (int tt = 0; tt < 2; ++tt) {
-    const int t = 16 * tt + r16;
-    tzero[tt] = t > KK;
-    if (t < KK) {
-      const int ty = t / 5 - 2, tx = t % 5 - 2;
-      toff[tt] = (tx + 2) * CP_CS + (ty + 2) * CP_RS + 8 * g;
-    } else {
-      toff[tt] = 5 * CP_CS + 2 * CP_RS + 8 * g;   // ones copy, row offset 0 (rows start at 2)
-    }
-  }
-
-  f4 acc[2][2], ga[3];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int b = 0; b < 3; ++b) ga[b] = f4{0.f, 0.f, 0.f, 0.f};
-
-  u4 vv[VPT];
-  auto load = [&](int n) {
-#pragma unroll
-    for (int j = 0; j < VPT; ++j) {
-      const int e = tid + 256 * j;
-      if (e < NXV) vv[j] = ldg16(x + (size_t)n * IH * IW + 8 * e);
-      else if (e < NXV + NGV) vv[j] = ldg16(gz + (size_t)n * NWIN * C + 8 * (e - NXV));
-      else if (e < NVEC) vv[j] = ldg16(codes + (size_t)n * NWIN * 8 + 8 * (e - NXV - NGV));
-    }
-  };
-  if (s_begin < s_end) load(s_begin);
-  __syncthreads();
-  for (int n = s_begin; n < s_end; ++n) {
-    // ---- the sample's image into the halo'd staging buffer; gz / codes stay in registers
-#pragma unroll
-    for (int j = 0; j < VPT; ++j) {
-      const int e = tid + 256 * j;
-      if (e < NXV) {
-        // 8 pixels may straddle a row (28 = 3.5 vectors), a pixel pair never does (28 even):
-        // one dword store per pair, 4-byte aligned (XS_C and the column are even)
-        const unsigned w4[4] = {vv[j].x, vv[j].y, vv[j].z, vv[j].w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int pix = 8 * e + 2 * k, r = pix / IW, c = pix - r * IW;
-          *reinterpret_cast<unsigned*>(xs + (r + 2) * XS_C + c + 2) = w4[k];
-        }
-      }
-    }
-    __syncthreads();                      // xs complete; the previous sample's k-loop is done
-    // the sample's codes to LDS (a gz vector's window codes sit in another thread's vector):
-    // 3136 B in the space of copies 3-4, which are rebuilt after the codes are consumed
-    unsigned short* cst = reinterpret_cast<unsigned short*>(cp + 3 * CP_CS);
-#pragma unroll
-    for (int j = 0; j < VPT; ++j) {
-      const int e = tid + 256 * j;
-      if (e >= NXV + NGV && e < NVEC) reinterpret_cast<u4*>(cst)[e - NXV - NGV] = vv[j];
-    }
-    __syncthreads();
-    // dZ: the routed pooled gradient at the coded pixel of every (window, channel), 0 at the
-    // window's other three pixels (each gz vector = one window x 8 channels)
-#pragma unroll
-    for (int j = 0; j < VPT; ++j) {
-      const int e = tid + 256 * j;
-      if (e >= NXV && e < NXV + NGV) {
-        const int q = e - NXV, w = q >> 2, kq = q & 3, c0 = 8 * kq;
-        const int hp = w / WP, wp = w - hp * WP;
-        // the four lanes of a window (channel octets kq) walk their channels rotated by kq, so
-        // their dword stores at each step fall on four different banks
-        const unsigned g8[8] = {vv[j].x, vv[j].y, vv[j].z, vv[j].w, vv[j].x, vv[j].y, vv[j].z, vv[j].w};
-        const unsigned short k0 = cst[w * 8 + (c0 >> 2)], k1 = cst[w * 8 + (c0 >> 2) + 1];
-        const unsigned kw = (unsigned)k0 | ((unsigned)k1 << 16);
-#pragma unroll
-        for (int cc = 0; cc < 8; ++cc) {
-          const int ch = (cc + kq) & 7;                       // channel c0 + ch
-          const unsigned nib = (kw >> (4 * ch)) & 0xFu;
-          // bf16 of channel ch: dword ch >> 1 (a lane-dependent index: select among the four)
-          const int dsel = ch >> 1;
-          const unsigned gdw = dsel == 0 ? g8[0] : dsel == 1 ? g8[1] : dsel == 2 ? g8[2] : g8[3];
-          const unsigned gv = (gdw >> (16 * (ch & 1))) & 0xffffu;
-          bf16* d = dz + (c0 + ch) * CSTR + 2 * hp * VW + 2 * wp;
-          // row 2hp: positions 1, 2 (k = 0, 1); row 2hp+1: positions 3, 4 (k = 2, 3)
-          const unsigned r0 = (nib == 1u ? gv : 0u) | ((nib == 2u ? gv : 0u) << 16);
-          const unsigned r1 = (nib == 3u ? gv : 0u) | ((nib == 4u ? gv : 0u) << 16);
-          *reinterpret_cast<unsigned*>(d) = r0;
-          *reinterpret_cast<unsigned*>(d + VW) = r1;
-        }
-      }
-    }
-    __syncthreads();                      // codes consumed: copies 3-4 may be rebuilt
-    if (n + 1 < s_end) load(n + 1);       // in flight under this sample's copies and MFMAs
-    // ---- the five shifted copies: copy[tx][row][col] = col < 28 ? x[row - 2][col + tx] : 0
-    // (one 16-byte chunk per thread: two aligned row reads and a funnel shift by tx + 2 pixels;
-    // the copy index is uniform over a wave -- 128 chunks per copy)
-    for (int i = tid; i < 5 * CROWS * (VW / 8); i += 256) {
-      const int ci = __builtin_amdgcn_readfirstlane(i / (CROWS * (VW / 8)));
-      const int rem = i - ci * (CROWS * (VW / 8));
-      const int row = rem / (VW / 8), seg = rem - row * (VW / 8);
-      const u4 lo = *reinterpret_cast<const u4*>(xs + row * XS_C + 8 * seg);
-      const u4 hi = *reinterpret_cast<const u4*>(xs + row * XS_C + 8 * seg + 8);
-      const unsigned src[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      unsigned o[4];
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        // elements 2d + ci, 2d + ci + 1 of src (ci wave-uniform: a scalar branch)
-        switch (ci) {
-          case 0: o[d] = src[d]; break;
-          case 1: o[d] = __builtin_amdgcn_alignbit(src[d + 1], src[d], 16); break;
-          case 2: o[d] = src[d + 1]; break;
-          case 3: o[d] = __builtin_amdgcn_alignbit(src[d + 2], src[d + 1], 16); break;
-          default: o[d] = src[d + 2]; break;
-        }
-      }
-      if (seg == VW / 8 - 1) { o[2] = 0u; o[3] = 0u; }          // columns 28..31
-      *reinterpret_cast<u4*>(cp + ci * CP_CS + row * CP_RS + 8 * seg) = u4{o[0], o[1], o[2], o[3]};
-    }
-    __syncthreads();
-    // ---- k-loop: image rows, a wave every fourth one
-    for (int r = wave; r < IH; r += 4) {
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(dz + r16 * CSTR + r * VW + 8 * g);
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(dz + (16 + r16) * CSTR + r * VW + 8 * g);
-      const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(cp + toff[0] + r * CP_RS);
-      bf16x8 x1 = *reinterpret_cast<const bf16x8*>(cp + toff[1] + r * CP_RS);
-      if (tzero[1]) x1 = bf16x8{};
-      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, x0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, x1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, x0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, x1, acc[1][1], 0, 0, 0);
-      ga[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, x0, ga[0], 0, 0, 0);
-      ga[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, x1, ga[1], 0, 0, 0);
-      ga[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, x1, ga[2], 0, 0, 0);
-    }
-    __syncthreads();                      // the k-loop is done with cp / dz before the next sample
-  }
-
-  // ---- block row: reduce the four waves' accumulators through LDS (dz is free now)
-  float* red = reinterpret_cast<float*>(dz);          // [4][32 ch][32 taps]  D
-  float* gr = red + 4 * C * 32;                       // [4][32][32]          Gram tiles
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        red[(wave * C + 16 * a + 4 * g + i) * 32 + 16 * b + r16] = acc[a][b][i];
-#pragma unroll
-  for (int b = 0; b < 3; ++b) {
-    const int ti = b == 2 ? 1 : 0, tj = b == 0 ? 0 : 1;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) gr[(wave * 32 + 16 * ti + 4 * g + i) * 32 + 16 * tj + r16] = ga[b][i];
-  }
-  __syncthreads();
-  auto gv = [&](int t1, int t2) {          // the lower block (1,0) is the transpose of (0,1)
-    if (t1 >= 16 && t2 < 16) { const int tmp = t1; t1 = t2; t2 = tmp; }
-    float v = 0.f;
-#pragma unroll
-    for (int wv = 0; wv < 4; ++wv) v += gr[(wv * 32 + t1) * 32 + t2];
-    return v;
-  };
-  float* o = out + ((size_t)rr * G + grp) * MOMC5;
-  for (int e = tid; e < MOMC5; e += 256) {
-    float v = 0.f;
-    if (e < C * KK) {
-      const int c = e / KK, t = e - c * KK;
-#pragma unroll
-      for (int wv = 0; wv < 4; ++wv) v += red[(wv * C + c) * 32 + t];
-    } else if (e < C * KK + KK * KK) {
-      const int q = e - C * KK, a = q / KK, b = q - a * KK;
-      v = gv(a, b);
-    } else if (e < C * KK + KK * KK + KK) {
-      v = gv(e - C * KK - KK * KK, KK);
-    } else {
-      const int c = e - (C * KK + KK * KK + KK);
-#pragma unroll
-      for (int wv = 0; wv < 4; ++wv) v += red[(wv * C + c) * 32 + KK];
-    }
-    o[e] = v;
-  }
-}
 
 // ---------------------------------------------------------------------------- window moments
 // The same moments in window space (as the audio conv1's c1p8_moments_win_kernel): dz is
@@ -876,14 +654,9 @@ int avd_cl_c1r5_moments_codes(const void* x, const void* gz, const unsigned shor
   const int R = avd_cl_c1r5_codes_rows(N, B, H, W);
   if (!R) return AVD_ERR_SHAPE;
   const int G = N / B;
-  // the window-space pass (c1r5_moments_win_kernel); AVDINO_C1R5_WIN=0 keeps the dz-map one
-  static const bool win = !getenv("AVDINO_C1R5_WIN") || atoi(getenv("AVDINO_C1R5_WIN")) != 0;
-  if (win)
-    c1r5_moments_win_kernel<<<G * R, 256, 0, avd_stream(stream)>>>(
-        (const bf16*)x, (const bf16*)gz, codes, out, B, G, R);
-  else
-    c1r5_moments_codes_kernel<<<G * R, 256, 0, avd_stream(stream)>>>(
-        (const bf16*)x, (const bf16*)gz, codes, out, B, G, R);
+  // the window-space pass (round 4; the dz-map pass it replaced: 90 vs 55 us at N = 7168)
+  c1r5_moments_win_kernel<<<G * R, 256, 0, avd_stream(stream)>>>(
+      (const bf16*)x, (const bf16*)gz, codes, out, B, G, R);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

@@ -242,7 +242,6 @@ extern "C" {
 
 // slabs of avd_c1w3_apply_wgrad (0: shape not served)
 int avd_c1w3_slabs(int dt, int N, int Cin, int H, int W, int Cout, int K, int pad) {
-  if (getenv("AVDINO_C1W3_OFF")) return 0;
   if (dt != AVD_BF16 || Cin != 1 || K != 3 || pad != 1) return 0;
   if (Cout != 16 && Cout != 32 && Cout != 64) return 0;
   if (H % TRW || W % 2 || W > 128 || (TRW / 2) * (W / 2) * (Cout / 8) > 512 || (TRW + 2) * (W + 2) > 768)
@@ -948,15 +947,11 @@ int avd_cl_c1r3_codes_combine(const float* moments, const void* wk, const float*
 
 // rows / slabs of a recompute pass for a Cin-1 first layer, 3x3 pad 1 or 5x5 pad 2 (0: not served)
 int avd_c1r3_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad) {
-  if (getenv("AVDINO_C1R3_OFF")) return 0;
   if (dt != AVD_BF16 || Cin != 1 || !((K == 3 && pad == 1) || (K == 5 && pad == 2)) || B <= 0 || N % B) return 0;
   // the 5x5 image conv1 (1->32 at 28^2): standalone its passes measure about what the stored-y
   // chain takes (tools/c1bench.py: 98 + 112 + 332 us vs 542 us for conv + pool + reduce + apply +
   // wgrad), but in the step they win: no 360 MB y written and re-read beside the concurrent
   // streams (round 3 same-box A/B: 175.7k vs 173.5k pairs/s, profiles/r3_ab_c1r5.txt).
-  // AVDINO_C1R5=0 keeps the stored-y chain.
-  const char* c1r5 = getenv("AVDINO_C1R5");
-  if (K == 5 && c1r5 && atoi(c1r5) == 0) return 0;
   if (Cout != 16 && Cout != 32 && Cout != 64) return 0;
   if (K == 5 && Cout != 32) return 0;                   // instantiated: the CentralNet image conv1
   if (H % TRW || W % 4 || W > 128 || pass < 0 || pass > 4) return 0;

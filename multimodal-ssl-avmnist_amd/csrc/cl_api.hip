@@ -71,59 +71,14 @@ namespace {
 bool dt_ok(int dt) { return dt == AVD_F32 || dt == AVD_BF16; }
 }  // namespace
 
-int avd_ws_dgrad_bnapply_serves(int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
-                                int pad, int gmode);
-int avd_ws_conv_dgrad_bnapply(const void* y, const void* gout, int gmode, const float* scale,
-                              const float* shift, const float* coef, const void* wk_d, void* dx,
-                              void* dy, int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
-                              int pad, hipStream_t st);
-int avd_wg_bnapply_serves(int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
-                          int gmode);
-int avd_wg_conv_wgrad_ex(const void* x, const void* dy, int dt, float* parts, int N, int Cin,
-                         int H, int W, int Cout, int K, int pad, int gmode, const void* gout,
-                         const float* scale, const float* shift, const float* coef, int B,
-                         hipStream_t st);
 
 int avd_cl_bn_bwd_reduce_pooled_impl(const void* y, int dt, const void* pooled, const void* gout,
                                      int mode, const float* gamma, const float* beta,
                                      const float* mean, const float* invstd, float* parts, int N,
                                      int B, int C, int H, int W, hipStream_t st);
 
-int avd_ws_dgrad_bnreduce_rows(int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad);
-int avd_ws_conv_dgrad_bnreduce(const void* dy, const void* wk_d, void* dx, const void* pooled,
-                               const float* gamma, const float* beta, float* parts, int dt, int N,
-                               int B, int Cin, int H, int W, int Cout, int K, int pad,
-                               hipStream_t st);
-int avd_cl_bn_bwd_reduce_pooled_fixup_impl(const void* y, const void* pooled, const void* gout,
-                                           const float* gamma, const float* beta,
-                                           const float* mean, const float* invstd, float* parts,
-                                           int R, int N, int B, int C, int H, int W,
-                                           hipStream_t st);
 
 extern "C" {
-
-int avd_cl_dgrad_bnreduce_rows(int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
-                               int pad) {
-  return avd_ws_dgrad_bnreduce_rows(dt, N, B, Cin, H, W, Cout, K, pad);
-}
-
-int avd_cl_conv_dgrad_bnreduce(const void* dy, const void* wk_d, void* dx, const void* pooled,
-                               const void* yprev, const float* gamma, const float* beta,
-                               const float* mean, const float* invstd, float* parts, int dt, int N,
-                               int B, int Cin, int H, int W, int Cout, int K, int pad,
-                               void* stream) {
-  if (!dy || !wk_d || !dx || !pooled || !yprev || !gamma || !beta || !mean || !invstd || !parts)
-    return AVD_ERR_ARG;
-  const int R = avd_ws_dgrad_bnreduce_rows(dt, N, B, Cin, H, W, Cout, K, pad);
-  if (R <= 0) return AVD_ERR_SHAPE;
-  const hipStream_t st = avd_stream(stream);
-  const int r = avd_ws_conv_dgrad_bnreduce(dy, wk_d, dx, pooled, gamma, beta, parts, dt, N, B, Cin,
-                                           H, W, Cout, K, pad, st);
-  if (r <= 0) return r == 0 ? AVD_ERR_SHAPE : r;
-  // the previous layer's conv output yprev is N x 2H x 2W x Cin
-  return avd_cl_bn_bwd_reduce_pooled_fixup_impl(yprev, pooled, dx, gamma, beta, mean, invstd, parts,
-                                                R, N, B, Cin, 2 * H, 2 * W, st);
-}
 
 int avd_cl_weight_elems(int Cout, int Cin, int K, int dgrad) {
   const int O = dgrad ? Cin : Cout, C = dgrad ? Cout : Cin;
@@ -187,7 +142,6 @@ int avd_cl_c1_recompute_rows(int pass, int dt, int N, int B, int Cin, int H, int
   // the 3x3 encoders' first layer (c1w3.hip); pass 4 (reduce + weight-gradient moments) only there
   if (const int r = avd_c1r3_rows(pass, dt, N, B, Cin, H, W, Cout, K, pad)) return r;
   if (!avd_c1p8_eligible(dt, Cin, Cout, K, H, W) || pad != 2 || W > 112) return 0;
-  if (pass == 4 && getenv("AVDINO_C1P8_MOMENTS_OFF")) return 0;
   return avd_c1r_rows(pass, N, B, H);
 }
 
@@ -340,34 +294,6 @@ int avd_cl_bn_bwd_reduce_pooled(const void* y, int dt, const void* pooled, const
   if (N <= 0 || B <= 0 || H < 2 || W < 2) return AVD_ERR_SHAPE;
   return avd_cl_bn_bwd_reduce_pooled_impl(y, dt, pooled, gout, mode, gamma, beta, mean, invstd,
                                           parts, N, B, C, H, W, avd_stream(stream));
-}
-
-int avd_cl_bnapply_ok(int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
-                      int gmode) {
-  return avd_ws_dgrad_bnapply_serves(dt, N, B, Cin, H, W, Cout, K, pad, gmode) &&
-         avd_wg_bnapply_serves(dt, N, B, Cin, H, W, Cout, K, pad, gmode);
-}
-
-int avd_cl_conv_dgrad_bnapply(const void* y, const void* gout, int gmode, const float* scale,
-                              const float* shift, const float* coef, const void* wk_d, void* dx,
-                              void* dy, int dt, int N, int B, int Cin, int H, int W, int Cout,
-                              int K, int pad, void* stream) {
-  if (!y || !gout || !scale || !shift || !coef || !wk_d || !dx || !dt_ok(dt)) return AVD_ERR_ARG;
-  if (dy && (dy == y || dy == dx)) return AVD_ERR_ARG;
-  const int r = avd_ws_conv_dgrad_bnapply(y, gout, gmode, scale, shift, coef, wk_d, dx, dy, dt, N,
-                                          B, Cin, H, W, Cout, K, pad, avd_stream(stream));
-  return r > 0 ? AVD_OK : (r == 0 ? AVD_ERR_SHAPE : r);
-}
-
-int avd_cl_conv_wgrad_bnapply(const void* x, const void* y, const void* gout, int gmode,
-                              const float* scale, const float* shift, const float* coef, int dt,
-                              float* dw_parts, int N, int B, int Cin, int H, int W, int Cout,
-                              int K, int pad, void* stream) {
-  if (!x || !y || !gout || !scale || !shift || !coef || !dw_parts || !dt_ok(dt)) return AVD_ERR_ARG;
-  if (gmode < 0) return AVD_ERR_ARG;
-  const int r = avd_wg_conv_wgrad_ex(x, y, dt, dw_parts, N, Cin, H, W, Cout, K, pad, gmode, gout,
-                                     scale, shift, coef, B, avd_stream(stream));
-  return r > 0 ? AVD_OK : (r == 0 ? AVD_ERR_SHAPE : r);
 }
 
 int avd_cl_wgrad_chunks(int N, int Cout, int Cin, int K) {

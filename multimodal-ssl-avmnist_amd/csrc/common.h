@@ -8,17 +8,17 @@
 
 namespace avd {
 
-// Test hook for the persistent kernels (conv_ws, wgrad_ws, c1p8 wgrad / recompute-wgrad):
-// AVDINO_GRID_CAP=n caps their grid at n blocks, so at test sizes every block walks several
-// tiles -- the cross-tile loop, the LDS reuse barrier and the next-tile prefetch run exactly
-// as at bench size.  Unset (the default) it changes nothing.
+// The library's launch options (avd_set_options, include/avdino.h): test hooks set explicitly
+// through the C ABI; no environment variable is read anywhere in the library.
+extern avd_options g_opts;
+
+// avd_options.grid_cap: caps the persistent kernels' grids (conv_ws, wgrad_ws, conv_ws8, the
+// conv1 passes) at n blocks, so at test sizes every block walks several tiles -- the cross-tile
+// loop, the LDS reuse barrier and the next-tile prefetch run exactly as at bench size.  0 (the
+// default) changes nothing.
 inline int grid_cap(int grid) {
-  const char* e = getenv("AVDINO_GRID_CAP");
-  if (e) {
-    const int c = atoi(e);
-    if (c > 0 && c < grid) return c;
-  }
-  return grid;
+  const int c = g_opts.grid_cap;
+  return (c > 0 && c < grid) ? c : grid;
 }
 
 typedef uint16_t bf16;

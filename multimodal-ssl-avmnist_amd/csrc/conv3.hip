@@ -76,7 +76,7 @@ template <int BO, int GPW, int IW8>
 __global__ __launch_bounds__(512, 1) void conv3p_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ wk, const float* __restrict__ bias,
     bf16* __restrict__ y, float* __restrict__ stats, int N, int H, int W, int C, int O, int TR,
-    int NS, int tilesPS, int xrows, int nitems, int G, int diag) {
+    int NS, int tilesPS, int xrows, int nitems, int G) {
   constexpr int NTW = BO / 32;                 // 16-channel tiles per wave
   constexpr int WROWS = 9 * BO;                // weight rows per unit
   extern __shared__ __attribute__((aligned(16))) bf16 smem[];
@@ -208,8 +208,8 @@ __global__ __launch_bounds__(512, 1) void conv3p_kernel(
       }
     }
     __syncthreads();
-    if (u + 2 < nunits && !(diag & 1)) stage(it0 + (u + 2) / nch, (u + 2) % nch, u & 1);
-    if (c == nch - 1 && !(diag & 2)) {
+    if (u + 2 < nunits) stage(it0 + (u + 2) / nch, (u + 2) % nch, u & 1);
+    if (c == nch - 1) {
       // ---- epilogue: bias, bf16 rounding, NHWC store, BN sums of the stored values
       const int og = item / tiles, ti = item - og * tiles;
       const int sg = ti / tilesPS, tt = ti - sg * tilesPS;
@@ -245,18 +245,12 @@ __global__ __launch_bounds__(512, 1) void conv3p_kernel(
           pk[t][0] = lo;
           pk[t][1] = hi;
         }
-        if (!(diag & 4)) {
-          if constexpr (NTW == 2) {
-            const u4 v = u4{pk[0][0], pk[0][1], pk[1][0], pk[1][1]};
-            if (diag & 16)
-              __builtin_nontemporal_store(v, reinterpret_cast<u4*>(yp));
-            else
-              *reinterpret_cast<u4*>(yp) = v;
-          } else
-            *reinterpret_cast<uint2*>(yp) = make_uint2(pk[0][0], pk[0][1]);
-        }
+        if constexpr (NTW == 2)
+          *reinterpret_cast<u4*>(yp) = u4{pk[0][0], pk[0][1], pk[1][0], pk[1][1]};
+        else
+          *reinterpret_cast<uint2*>(yp) = make_uint2(pk[0][0], pk[0][1]);
       }
-      if (stats && !(diag & 8)) {
+      if (stats) {
         // per-block running sums over the tiles of one (og, BatchNorm group): written once per
         // such run (and zeros for the pairs the block never reaches) into row blockIdx*4 + wp
         const int pair = og * G + ti / tilesPG;
@@ -282,7 +276,7 @@ __global__ __launch_bounds__(512, 1) void conv3p_kernel(
         for (int t = 0; t < NTW; ++t) acc[j][t] = f4{0.f, 0.f, 0.f, 0.f};
     }
   }
-  if (stats && !(diag & 8)) {
+  if (stats) {
     if (cur_pair >= 0) flush(cur_pair);
     // the (og, group) pairs this block never reached: zero rows.  The reached pairs are the
     // contiguous interval [first, last] of the og-major order.
@@ -311,9 +305,7 @@ Plan3 plan3(int H, int W, int B) {
   Plan3 best{0, 0, 0, 0, 0, 0};
   double bu = -1;
   const int IW8 = iw8_of(W);
-  const char* fg = getenv("AVDINO_C3_GPW");      // A/B experiments: force the pixel groups
   for (int gpw : {4, 7}) {
-    if (fg && atoi(fg) != gpw) continue;
     const int cap = gpw * 64;
     auto consider = [&](int TR, int NS) {
       if (TR <= 0 || NS <= 0 || TR * W * NS > cap || TR > 255) return;
@@ -345,14 +337,6 @@ int num_cus() {
   return n;
 }
 
-// diagnostics (wrong results): AVDINO_C3_DIAG bit 0 = no staging after the first two units,
-// bit 1 = no epilogue, bit 2 = no y stores, bit 3 = no statistics; bit 4 (correct results):
-// non-temporal y stores
-int diag3() {
-  static const int d = getenv("AVDINO_C3_DIAG") ? atoi(getenv("AVDINO_C3_DIAG")) : 0;
-  return d;
-}
-
 template <int BO, int GPW, int IW8>
 int launch3(const Plan3& p, const void* x, const void* wk, const float* bias, void* y, float* stats,
             int N, int B, int H, int W, int C, int O, hipStream_t st) {
@@ -363,7 +347,7 @@ int launch3(const Plan3& p, const void* x, const void* wk, const float* bias, vo
   const int grid = stats ? num_cus() : std::min(nitems, num_cus());
   conv3p_kernel<BO, GPW, IW8><<<grid, 512, lds, st>>>(
       (const bf16*)x, (const bf16*)wk, bias, (bf16*)y, stats, N, H, W, C, O, p.TR, p.NS,
-      p.tilesPS, p.xrows, nitems, N / B, diag3());
+      p.tilesPS, p.xrows, nitems, N / B);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
@@ -373,7 +357,6 @@ int launch3(const Plan3& p, const void* x, const void* wk, const float* bias, vo
 // Served: bf16, 3x3, pad 1, C (input channels of the executed conv) % 32 == 0, O % 32 == 0,
 // O <= 256, maps up to 62 pixels wide.
 bool avd_c3_serves(int dt, int C, int O, int K, int pad) {
-  if (getenv("AVDINO_C3_OFF")) return false;
   return dt == AVD_BF16 && K == 3 && pad == 1 && C % CH == 0 && C >= CH && O % 32 == 0 && O <= 256;
 }
 
@@ -553,12 +536,8 @@ size_t wg3_lds(int TR, int W, int BO) {
 }
 
 // strip rows for a map of H x W: the largest divisor of H whose strip fits 72 KB of LDS
-// (two blocks per CU) within 256 pixels (AVDINO_C3_TR overrides)
+// (two blocks per CU) within 256 pixels
 int tr3(int H, int W, int BO) {
-  if (const char* e = getenv("AVDINO_C3_TR")) {
-    const int t = atoi(e);
-    if (t > 0 && H % t == 0) return t;
-  }
   const int wo8 = (W + 7) & ~7;
   int best = 1;
   for (int tr = 1; tr <= H; ++tr)
@@ -572,9 +551,9 @@ int wg3_bo(int Cout) { return Cout % 128 == 0 ? 128 : 64; }
 
 // Slabs of avd_c3_wgrad for (N, Cout, Cin), or 0 if not served.
 int avd_c3_wgrad_chunks(int N, int Cout, int Cin, int K) {
-  if (getenv("AVDINO_C3_OFF") || K != 3 || Cin % CH || Cout % 64) return 0;
+  if (K != 3 || Cin % CH || Cout % 64) return 0;
   const int groups = (Cout / wg3_bo(Cout)) * (Cin / CH);
-  static const int target = getenv("AVDINO_C3_WBLK") ? atoi(getenv("AVDINO_C3_WBLK")) : 512;
+  constexpr int target = 512;
   int nchunk = std::max(1, target / groups);
   nchunk = std::min(nchunk, N);
   // the grid (nchunk * groups) must be a multiple of 8 for the XCD remap

@@ -1282,125 +1282,6 @@ __global__ void c1p8_combine_kernel(const float* __restrict__ m, const float* __
   dw[e] = (float)acc;
 }
 
-// The forward BN -> ReLU -> 2x2 max-pool pass (RC_APPLY) with the pooling done in registers:
-// y by the pixel-pair MFMA, relu(y * scale + shift) and the window max across the 4 lanes that
-// hold the window's pixels (v_permlane32_swap + DPP row_ror:8, as the moments pass), bf16
-// rounding of the max (= the max of the rounded values: rounding is monotone), one 8-byte store
-// per window and channel half -- no y tile in LDS, no per-window thread phase.  One block per
-// sample; bit-identical z to c1p8_recompute_kernel<RC_APPLY>.
-__global__ __launch_bounds__(256) void c1p8_apply_kernel(
-    const bf16* __restrict__ x, const bf16* __restrict__ wk, const float* __restrict__ bias,
-    const float* __restrict__ scale, const float* __restrict__ shift, bf16* __restrict__ z,
-    int B, int H, int W, int tps) {
-  __shared__ __attribute__((aligned(16))) bf16 xs[(TH + 4) * ITW];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int gq = lane >> 4, col = lane & 15;
-  const int n = blockIdx.x, grp = n / B;
-  const int Hp = H >> 1, Wp = W >> 1, cpr = W >> 3, mts = W >> 4;
-  bf16x8 aw;
-  {
-    const int m = lane & 15, jj = m >> 3, c = m & 7;
-    __bf16 e[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int k = 8 * gq + q, ky = k / 6, kx = k % 6 - jj;
-      const bool ok = k < 30 && kx >= 0 && kx < 5;
-      const float v = bf2f(wk[c * 32 + (ok ? ky * 5 + kx : 0)]);
-      e[q] = (__bf16)(ok ? v : 0.f);
-    }
-    aw = bf16x8{e[0], e[1], e[2], e[3], e[4], e[5], e[6], e[7]};
-  }
-  const int cs = gq & 1, jy = lane >> 5, qy = col & 7, rp = col >> 3;
-  float bv[4], sc[4], sf[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    bv[i] = bias ? bias[4 * cs + i] : 0.f;
-    sc[i] = scale[grp * COUT + 4 * cs + i];
-    sf[i] = shift[grp * COUT + 4 * cs + i];
-  }
-  int yo[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) yo[d] = boff(gq, d) + rp * ITWD + qy + 3;
-  const bool writer = jy == 0 && rp == 0;        // window pixel (0, 0) stores the max
-  const int nxt = (TH + 4) * cpr;
-  int xr[2], xoff[2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int t = tid + 256 * s;
-    const int r = t / cpr, c = t - r * cpr;
-    xr[s] = t < nxt ? r : -(1 << 20);
-    xoff[s] = (r - 2) * W + 8 * c;
-  }
-  u4 xv[2];
-  auto load_x = [&](int ty0) {
-    const bf16* xb = x + ((size_t)n * H + ty0) * W;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bool ok = (unsigned)(ty0 - 2 + xr[s]) < (unsigned)H;
-      xv[s] = ldg16(ok ? (const void*)(xb + xoff[s]) : &kZeroC1);
-    }
-  };
-  load_x(0);
-  for (int tile = 0; tile < tps; ++tile) {
-    const int ty0 = tile * TH;
-    if (tile) __syncthreads();
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int t = tid + 256 * s;
-      if (t < nxt) {
-        const int r = t / cpr, c = t - r * cpr;
-        *reinterpret_cast<u4*>(xs + r * ITW + XOFF + 8 * c) = xv[s];
-      }
-    }
-    if (tid < (TH + 4) * 2) {
-      const int r = tid >> 1, side = tid & 1;
-      *reinterpret_cast<u4*>(xs + r * ITW + (side ? XOFF + W : 0)) = u4{0u, 0u, 0u, 0u};
-    }
-    if (tile + 1 < tps) load_x(ty0 + TH);
-    __syncthreads();
-    const unsigned* xd = reinterpret_cast<const unsigned*>(xs);
-    for (int s = wave; s < TH / 2; s += 4) {
-      u4 bw[MTMAX];
-#pragma unroll
-      for (int mt = 0; mt < MTMAX; ++mt) {
-        if (mt >= mts) break;
-        const int base = 2 * s * ITWD + 8 * mt;
-        bw[mt] = u4{xd[base + yo[0]], xd[base + yo[1]], xd[base + yo[2]], xd[base + yo[3]]};
-      }
-      f4 r4[MTMAX];
-#pragma unroll
-      for (int mt = 0; mt < MTMAX; ++mt) {
-        if (mt >= mts) break;
-        r4[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, __builtin_bit_cast(bf16x8, bw[mt]),
-                                                         f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      }
-      bf16* zrow = z + ((size_t)n * Hp + (ty0 >> 1) + s) * Wp * COUT + 4 * cs;
-#pragma unroll
-      for (int mt = 0; mt < MTMAX; ++mt) {
-        if (mt >= mts) break;
-        float m[4];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const uint32_t yb = pack_bf16x2(r4[mt][2 * h] + bv[2 * h], r4[mt][2 * h + 1] + bv[2 * h + 1]);
-          const float yy[2] = {__uint_as_float(yb << 16), __uint_as_float(yb & 0xffff0000u)};
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const int i = 2 * h + e;
-            const float v = fmaxf(fmaf(yy[e], sc[i], sf[i]), 0.f);
-            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-            const float p1 = __uint_as_float(jy ? sw[0] : sw[1]);
-            const float m2 = fmaxf(v, p1);
-            m[i] = fmaxf(m2, __int_as_float(dpp_i<0x128>(__float_as_int(m2))));
-          }
-        }
-        if (writer)
-          *reinterpret_cast<uint2*>(zrow + (size_t)(8 * mt + qy) * COUT) =
-              make_uint2(pack_bf16x2(m[0], m[1]), pack_bf16x2(m[2], m[3]));
-      }
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------- routed backward
 // The training backward of the layer from the forward's routing codes instead of a recomputed y.
 // The forward apply pass (RC_APPLY with codes) already decides, per pooling window and channel,
@@ -2037,7 +1918,7 @@ int c1p8_codes_rows(int N, int B) {
       per = 2;
     resident = cus * per;
   }
-  static const int waves = getenv("AVDINO_C1M_WAVES") ? std::max(1, atoi(getenv("AVDINO_C1M_WAVES"))) : 8;
+  constexpr int waves = 8;
   const int G = N / B;
   return std::max(1, std::min(grid_cap(resident * waves) / G, B));
 }
@@ -2056,8 +1937,8 @@ int c1p8_moment_rows(int N, int B) {
     resident = cus * per;
   }
   // several waves of blocks: beside the concurrent streams' persistent kernels a block may start
-  // late, and shorter blocks bound that tail (AVDINO_C1M_WAVES, default 8)
-  static const int waves = getenv("AVDINO_C1M_WAVES") ? std::max(1, atoi(getenv("AVDINO_C1M_WAVES"))) : 8;
+  // late, and shorter blocks bound that tail
+  constexpr int waves = 8;
   const int G = N / B;
   return std::max(1, std::min(grid_cap(resident * waves) / G, B));
 }
@@ -2089,14 +1970,6 @@ int avd_c1r_launch(int pass, const void* x, const void* wk, const float* bias, c
     const int G = N / B, R = c1p8_moment_rows(N, B);
     c1p8_moments_kernel<<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, scale, shift,
                                                mean, invstd, (const bf16*)gz, out, B, G, R, H, W, tps);
-    AVD_CHECK_LAUNCH();
-    return AVD_OK;
-  }
-  // the in-register pooling variant measured slower (361 vs 268 us at N = 7168: ~5 VALU per
-  // element for the cross-lane max against 0.75 in the per-window threads): opt-in only
-  if (pass == RC_APPLY && getenv("AVDINO_C1_APPLY_REG")) {
-    c1p8_apply_kernel<<<N, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, scale, shift,
-                                          (bf16*)z, B, H, W, tps);
     AVD_CHECK_LAUNCH();
     return AVD_OK;
   }
@@ -2153,14 +2026,9 @@ int avd_c1_gram_launch(const void* x, float* out, int N, int B, int H, int W, hi
 int avd_c1_moments_nogram_launch(const void* x, const void* gz, const unsigned* codes, float* out,
                                  int N, int B, int H, int W, hipStream_t st) {
   const int tps = H / TH, G = N / B, R = c1p8_codes_rows(N, B);
-  // the window-space pass (c1p8_moments_win_kernel); AVDINO_C1_MOMWIN=0 keeps the pixel-pair one
-  static const bool win = !getenv("AVDINO_C1_MOMWIN") || atoi(getenv("AVDINO_C1_MOMWIN")) != 0;
-  if (win)
-    c1p8_moments_win_kernel<<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)gz, codes, out, B, G, R,
-                                                   H, W, tps);
-  else
-    c1p8_moments_codes_kernel<2><<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)gz, codes, out, B,
-                                                        G, R, H, W, tps);
+  // the window-space pass (round 4; the pixel-pair pass it replaced: 226 vs 159 us at N = 7168)
+  c1p8_moments_win_kernel<<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)gz, codes, out, B, G, R,
+                                                 H, W, tps);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

@@ -655,10 +655,8 @@ typedef Ws<WS_DGRA4> DgrA4_;
 #define DgrA4 DgrA4_
 #endif
 
-bool ws_disabled() {
-  const char* e = getenv("AVDINO_CONV_LEGACY");
-  return e && e[0] == '1';
-}
+// avd_options.generic_conv: every bf16 mid layer on the generic conv_cl kernels (parity tests)
+bool ws_disabled() { return g_opts.generic_conv != 0; }
 
 int num_cus() {
   static int cus = 0;
@@ -765,69 +763,3 @@ int avd_ws_conv_dgrad(const void* dy, const void* wk_d, void* dx, int dt, int N,
   return r == AVD_OK ? 1 : (r == AVD_ERR_SHAPE ? 0 : r);
 }
 
-// Input gradient of a forward conv (Cin -> Cout over H x W) whose output y went through
-// BatchNorm -> ReLU -> 2x2 max-pool: dY = BN-backward-apply(y, pooled gradient gout, coef) is
-// formed while staging (bnapply.h), so no dY tensor is read or written.  gmode: layout of gout
-// (0 = pooled NHWC bf16, 2 = f32 (c,h,w) flatten).  1 = launched, 0 = not served, < 0 = error.
-int avd_ws_conv_dgrad_bnapply(const void* y, const void* gout, int gmode, const float* scale,
-                              const float* shift, const float* coef, const void* wk_d, void* dx,
-                              void* dy, int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
-                              int pad, hipStream_t st) {
-  if (dt != AVD_BF16 || ws_disabled() || (gmode != 0 && gmode != 2) || B <= 0 || N % B) return 0;
-  const int Ho = H + 2 * pad - K + 1, Wo = W + 2 * pad - K + 1, dp = K - 1 - pad;
-  const ApplyArgs aa{gout, scale, shift, coef, B, N / B, dy};
-  int r = 0;
-#define AVD_DA(LL)                                                                               \
-  if (is<LL>(Cout, Ho, Wo, Cin, K, dp)) {                                                       \
-    r = gmode == 0 ? launch_ws<LL, false, 1>(y, wk_d, nullptr, dx, nullptr, N, N, st, aa)       \
-                   : launch_ws<LL, false, 2>(y, wk_d, nullptr, dx, nullptr, N, N, st, aa);      \
-    return r == AVD_OK ? 1 : (r == AVD_ERR_SHAPE ? 0 : r);                                      \
-  }
-  AVD_DA(DgrA2) AVD_DA(DgrA3) AVD_DA(DgrA4) AVD_DA(DgrI2)
-#undef AVD_DA
-  return 0;
-}
-
-// Input gradient + the previous layer's BatchNorm-backward partial sums (RD above).  The
-// previous layer: BN over Cin channels, ReLU, 2x2 max-pool whose output `pooled` (N x H x W x Cin,
-// NHWC bf16) is this conv's input.  parts [Cin][N/B][R][2], R = avd_ws_dgrad_bnreduce_rows.
-// 1 = launched, 0 = not served, < 0 = error.  (The fix-up pass is the caller's: cl_api.hip.)
-int avd_ws_dgrad_bnreduce_rows(int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad) {
-  if (dt != AVD_BF16 || ws_disabled() || B <= 0 || N % B) return 0;
-  const int Ho = H + 2 * pad - K + 1, Wo = W + 2 * pad - K + 1, dp = K - 1 - pad;
-#define AVD_RR(LL) \
-  if (is<LL>(Cout, Ho, Wo, Cin, K, dp)) return B % LL::NS ? 0 : ws_stat_grid<LL, false, true>() * LL::NPW;
-  AVD_RR(DgrA2) AVD_RR(DgrA3) AVD_RR(DgrA4) AVD_RR(DgrI2)
-#undef AVD_RR
-  return 0;
-}
-
-int avd_ws_conv_dgrad_bnreduce(const void* dy, const void* wk_d, void* dx, const void* pooled,
-                               const float* gamma, const float* beta, float* parts, int dt, int N,
-                               int B, int Cin, int H, int W, int Cout, int K, int pad,
-                               hipStream_t st) {
-  if (!avd_ws_dgrad_bnreduce_rows(dt, N, B, Cin, H, W, Cout, K, pad)) return 0;
-  const int Ho = H + 2 * pad - K + 1, Wo = W + 2 * pad - K + 1, dp = K - 1 - pad;
-  const ApplyArgs aa{pooled, gamma, beta, nullptr, B, N / B};
-  int r = 0;
-#define AVD_RD(LL)                                                                              \
-  if (is<LL>(Cout, Ho, Wo, Cin, K, dp)) {                                                      \
-    r = launch_ws<LL, false, 0, true>(dy, wk_d, nullptr, dx, parts, N, B, st, aa);             \
-    return r == AVD_OK ? 1 : (r == AVD_ERR_SHAPE ? 0 : r);                                     \
-  }
-  AVD_RD(DgrA2) AVD_RD(DgrA3) AVD_RD(DgrA4) AVD_RD(DgrI2)
-#undef AVD_RD
-  return 0;
-}
-
-int avd_ws_dgrad_bnapply_serves(int dt, int N, int B, int Cin, int H, int W, int Cout, int K,
-                                int pad, int gmode) {
-  if (dt != AVD_BF16 || ws_disabled() || (gmode != 0 && gmode != 2) || B <= 0 || N % B ||
-      N / B > APPLY_GMAX)
-    return 0;
-  const int Ho = H + 2 * pad - K + 1, Wo = W + 2 * pad - K + 1, dp = K - 1 - pad;
-#define AVD_DS(LL) if (is<LL>(Cout, Ho, Wo, Cin, K, dp)) return B % LL::NS == 0 && N % LL::NS == 0;
-  AVD_DS(DgrA2) AVD_DS(DgrA3) AVD_DS(DgrA4) AVD_DS(DgrI2)
-#undef AVD_DS
-  return 0;
-}

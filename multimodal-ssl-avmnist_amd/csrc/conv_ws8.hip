@@ -801,9 +801,6 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws8_kernel(const bf16* 
 typedef G8<8, 16, 5, 2, 56, 56, G8A2_T> G8A2;     // audio conv2
 typedef G8<16, 32, 5, 2, 28, 28, 14, 4, 2, 1, 32, 16> G8A3;  // audio conv3
 typedef G8<32, 64, 5, 2, 14, 14, 7, 4, 1, 1, 64, 32, 512, 2, 1> G8A4;   // audio conv4
-// (A/B candidates for audio conv4, AVDINO_G8A4=1 / 2)
-typedef G8<32, 64, 5, 2, 14, 14, 7, 8, 1, 1, 64, 32, 512, 1, 1> G8A4b;
-typedef G8<32, 64, 5, 2, 14, 14, 7, 1, 1, 1, 64, 32, 256, 4, 1> G8A4c;  // audio conv4
 typedef G8<32, 64, 5, 0, 14, 14, 10, 4, 1, 1, 64, 32, 512, 2, 1> G8I2;  // image conv2
 
 template <class L>
@@ -818,10 +815,9 @@ int g8_chunks(int N) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wgrad_ws8_kernel<L>, L::NTHR, 0) != hipSuccess || occ <= 0)
       occ = 1;
   }
-  // AVDINO_G8_SLABS: at most this many slabs (every slab is a [Cout][Cin][K][K] f32 partial the
-  // fixed-order reduce reads back; one resident wave of blocks per slab by default)
-  static const int cap = getenv("AVDINO_G8_SLABS") ? std::max(1, atoi(getenv("AVDINO_G8_SLABS"))) : (1 << 30);
-  return std::max(1, grid_cap(std::min(std::min(N / L::NSS, num_cus8() * occ), cap)));
+  // one resident wave of blocks, one slab each (every slab is a [Cout][Cin][K][K] f32 partial the
+  // fixed-order reduce reads back)
+  return std::max(1, grid_cap(std::min(N / L::NSS, num_cus8() * occ)));
 }
 
 }  // namespace
@@ -830,10 +826,7 @@ extern "C" {
 
 // slabs of avd_mx_conv_wgrad for the conv Cin -> Cout over H x H (0: not served)
 int avd_mx_wgrad_chunks(int N, int Cin, int H, int Cout, int K, int pad) {
-  static const int a4 = getenv("AVDINO_G8A4") ? atoi(getenv("AVDINO_G8A4")) : 0;
 #define AVD_G8(LL) if (g8_is<LL>(Cin, H, Cout, K, pad)) return N % LL::NSS ? 0 : g8_chunks<LL>(N);
-  if (a4 == 1) AVD_G8(G8A4b)
-  if (a4 == 2) AVD_G8(G8A4c)
   AVD_G8(G8A2) AVD_G8(G8A3) AVD_G8(G8A4) AVD_G8(G8I2)
 #undef AVD_G8
   return 0;
@@ -853,9 +846,6 @@ int avd_mx_conv_wgrad(const void* x, const void* dy, float* parts, int N, int Ci
     AVD_CHECK_LAUNCH();                                                                         \
     return AVD_OK;                                                                              \
   }
-  static const int a4 = getenv("AVDINO_G8A4") ? atoi(getenv("AVDINO_G8A4")) : 0;
-  if (a4 == 1) AVD_G8(G8A4b)
-  if (a4 == 2) AVD_G8(G8A4c)
   AVD_G8(G8A2) AVD_G8(G8A3) AVD_G8(G8A4) AVD_G8(G8I2)
 #undef AVD_G8
   return AVD_ERR_SHAPE;

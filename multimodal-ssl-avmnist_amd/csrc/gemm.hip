@@ -519,9 +519,8 @@ Plan plan_for(int M, int N, int K) {
   if (N > 128 && N <= 256 && K >= 1024 && M >= 4096) {
     Plan p{128, 256, 1, K};
     const long long t = tiles(128, 256);
-    // split target in blocks (AVDINO_GEMM_N256_BLOCKS, A/B runs)
-    static const int target256 =
-        getenv("AVDINO_GEMM_N256_BLOCKS") ? atoi(getenv("AVDINO_GEMM_N256_BLOCKS")) : 224;
+    // split target in blocks (112 / 448 / 896 measured slower, profiles/r3_gemm_ab_n256.txt)
+    constexpr int target256 = 224;
     const int s = (int)std::max(1ll, std::min<long long>(avd_cdiv(target256, t), K / 128));
     if (s > 1) {
       p.kchunk = avd_cdiv(avd_cdiv(K, s), 32) * 32;
@@ -535,9 +534,9 @@ Plan plan_for(int M, int N, int K) {
   else if (K >= 1024)   // deep K: the split below restores the block count
     p = (M >= 128 && N >= 128) ? Plan{128, 128, 1, K} : (M >= 128 ? Plan{128, 64, 1, K} : p);
   const long long t = tiles(p.bm, p.bn);
-  // split target (blocks) and minimum K rows per split: AVDINO_GEMM_SPLIT / AVDINO_GEMM_KMIN
-  static const int target = getenv("AVDINO_GEMM_SPLIT") ? atoi(getenv("AVDINO_GEMM_SPLIT")) : 512;
-  static const int kmin = getenv("AVDINO_GEMM_KMIN") ? atoi(getenv("AVDINO_GEMM_KMIN")) : 256;
+  // split target (blocks) and minimum K rows per split (512 / 256: the best of 128-2048 /
+  // 64-256, profiles/r3_gemm_ab.txt)
+  constexpr int target = 512, kmin = 256;
   if (t < 224 && K >= 512) {
     int s = (int)std::min<long long>(avd_cdiv(target, t), K / kmin);
     s = std::max(1, std::min(s, 128));

@@ -127,6 +127,10 @@ __global__ void counters_add_kernel(long long* __restrict__ arena, const long lo
 
 }  // namespace
 
+namespace avd {
+avd_options g_opts{};
+}  // namespace avd
+
 extern "C" {
 
 int avd_counters_add(long long* arena, const long long* idx, const long long* val, int n,
@@ -139,7 +143,20 @@ int avd_counters_add(long long* arena, const long long* idx, const long long* va
   return AVD_OK;
 }
 
-int avd_version(void) { return (0 << 16) | 1; }
+int avd_version(void) { return (0 << 16) | 2; }
+
+int avd_set_options(const avd_options* opts) {
+  if (opts && (opts->grid_cap < 0 || (opts->generic_conv & ~1) || (opts->generic_m2 & ~1)))
+    return AVD_ERR_ARG;
+  avd::g_opts = opts ? *opts : avd_options{};
+  return AVD_OK;
+}
+
+int avd_get_options(avd_options* opts) {
+  if (!opts) return AVD_ERR_ARG;
+  *opts = avd::g_opts;
+  return AVD_OK;
+}
 
 const char* avd_last_error(void) { return g_err; }
 

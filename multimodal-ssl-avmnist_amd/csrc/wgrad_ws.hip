@@ -544,10 +544,8 @@ typedef Wg<WG_I2> WgI2_;
 #define WgI2 WgI2_
 #endif
 
-bool wg_disabled() {
-  const char* e = getenv("AVDINO_CONV_LEGACY");
-  return e && e[0] == '1';
-}
+// avd_options.generic_conv: every bf16 weight gradient on the generic wgrad_cl kernel
+bool wg_disabled() { return g_opts.generic_conv != 0; }
 
 int wg_cus() {
   static int cus = 0;
@@ -577,54 +575,26 @@ int avd_wg_chunks(int N, int Cout, int Cin, int K) {
   else if (Cin == 16 && Cout == 32 && K == 5) occ = WgA3::OCC;
   else if (Cin == 32 && Cout == 64 && K == 5) occ = WgA4::OCC;
   else return 0;
-  // AVDINO_WG_CU_PCT: percent of the CUs the persistent grid occupies (it runs on a side stream
-  // beside the input-gradient chain; fewer slabs leave CUs to that chain's kernels)
-  static const int pct = getenv("AVDINO_WG_CU_PCT") ? std::min(100, std::max(1, atoi(getenv("AVDINO_WG_CU_PCT")))) : 100;
-  return std::max(1, grid_cap(std::min(N, std::max(1, wg_cus() * pct / 100) * occ)));
+  // (a grid on a fraction of the CUs, leaving CUs to the input-gradient chain beside it, measured
+  // within noise in round 4)
+  return std::max(1, grid_cap(std::min(N, wg_cus() * occ)));
 }
 
 // 1 = launched, 0 = not served, < 0 = error.  parts must hold avd_wg_chunks(...) slabs.
-// With gmode >= 0, dy is the conv output y and dY = BN-backward-apply(y, gout, coef) is formed
-// while staging (bnapply.h; gmode = layout of gout, B = samples per BN group).
-int avd_wg_conv_wgrad_ex(const void* x, const void* dy, int dt, float* parts, int N, int Cin,
-                         int H, int W, int Cout, int K, int pad, int gmode, const void* gout,
-                         const float* scale, const float* shift, const float* coef, int B,
-                         hipStream_t st) {
+int avd_wg_conv_wgrad(const void* x, const void* dy, int dt, float* parts, int N, int Cin, int H,
+                      int W, int Cout, int K, int pad, hipStream_t st) {
   if (dt != AVD_BF16 || wg_disabled()) return 0;
-  if (gmode >= 0 && (gmode == 1 || gmode > 2 || B <= 0 || N % B || N / B > APPLY_GMAX)) return 0;
   const int chunks = avd_wg_chunks(N, Cout, Cin, K);
   if (!chunks) return 0;
-  const ApplyArgs aa{gout, scale, shift, coef, B, B > 0 ? N / B : 0};
+  const ApplyArgs aa{};
 #define AVD_WG(LL)                                                                              \
   if (wg_is<LL>(Cin, H, W, Cout, K, pad)) {                                                    \
-    if (N % LL::NSS || (gmode >= 0 && B % LL::NSS)) return 0;                                  \
-    if (gmode < 0)                                                                             \
-      wgrad_ws_kernel<LL, 0><<<chunks, LL::NTHR, 0, st>>>((const bf16*)x, (const bf16*)dy, parts, N, chunks, aa); \
-    else if (gmode == 0)                                                                       \
-      wgrad_ws_kernel<LL, 1><<<chunks, LL::NTHR, 0, st>>>((const bf16*)x, (const bf16*)dy, parts, N, chunks, aa); \
-    else                                                                                       \
-      wgrad_ws_kernel<LL, 2><<<chunks, LL::NTHR, 0, st>>>((const bf16*)x, (const bf16*)dy, parts, N, chunks, aa); \
+    if (N % LL::NSS) return 0;                                                                 \
+    wgrad_ws_kernel<LL, 0><<<chunks, LL::NTHR, 0, st>>>((const bf16*)x, (const bf16*)dy, parts, N, chunks, aa); \
     AVD_CHECK_LAUNCH();                                                                         \
     return 1;                                                                                   \
   }
   AVD_WG(WgA2) AVD_WG(WgA3) AVD_WG(WgA4) AVD_WG(WgI2)
 #undef AVD_WG
-  return 0;
-}
-
-int avd_wg_conv_wgrad(const void* x, const void* dy, int dt, float* parts, int N, int Cin, int H,
-                      int W, int Cout, int K, int pad, hipStream_t st) {
-  return avd_wg_conv_wgrad_ex(x, dy, dt, parts, N, Cin, H, W, Cout, K, pad, -1, nullptr, nullptr,
-                              nullptr, nullptr, 0, st);
-}
-
-int avd_wg_bnapply_serves(int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
-                          int gmode) {
-  if (dt != AVD_BF16 || wg_disabled() || (gmode != 0 && gmode != 2) || B <= 0 || N % B ||
-      N / B > APPLY_GMAX || !avd_wg_chunks(N, Cout, Cin, K))
-    return 0;
-#define AVD_WS(LL) if (wg_is<LL>(Cin, H, W, Cout, K, pad)) return N % LL::NSS == 0 && B % LL::NSS == 0;
-  AVD_WS(WgA2) AVD_WS(WgA3) AVD_WS(WgA4) AVD_WS(WgI2)
-#undef AVD_WS
   return 0;
 }

@@ -27,3 +27,19 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture
+def avd_opts():
+    """Set libavdino's launch options (avd_set_options: grid_cap, generic_conv, generic_m2)
+    inside a test: avd_opts(grid_cap=3); every setting is undone when the test ends."""
+    import contextlib
+
+    from avdino import ops
+    stack = contextlib.ExitStack()
+
+    def set_(**kw):
+        stack.enter_context(ops.options(**kw))
+
+    yield set_
+    stack.close()

@@ -9,7 +9,7 @@ small-N tests (one tile per block) never reach.  Here they run:
 
   * at bench size, against a float64 reference computed on the GPU with torch (a tap loop of
     f64 matmuls -- no MIOpen, no libavdino) from the SAME bf16 operands;
-  * at small N with AVDINO_GRID_CAP forcing a few blocks (many tiles each), against the
+  * at small N with avd_options.grid_cap forcing a few blocks (many tiles each), against the
     uncapped launch: forward / dgrad tiles are independent of the block that computes them
     (bit-identical), weight gradients are fp32 sums in another order (rel 1e-6).
 
@@ -309,7 +309,7 @@ def test_ws_kernels_bench_size(ops, shape):
 
 
 @pytest.mark.parametrize("HC", [(14, 64), (10, 64)])
-def test_bn_bwd_reduce_pooled_mode2_bench_size(ops, HC, monkeypatch):
+def test_bn_bwd_reduce_pooled_mode2_bench_size(ops, HC, avd_opts):
     """The encoder tails' BN-backward sums from the (c, h, w)-flattened pooled map and gradient
     (bwd_reduce_pooled_m2_kernel: a wave per channel, coalesced planes) at N = 7168 against the
     generic pooled kernel and float64 of sum dz, sum dz * xhat."""
@@ -330,7 +330,7 @@ def test_bn_bwd_reduce_pooled_mode2_bench_size(ops, HC, monkeypatch):
     R = ops.cl_bn_bwd_rows(B, C, H, H, T)
     p1 = torch.full((C * G * R * 2,), float("nan"), device="cuda")
     ops.cl_bn_bwd_reduce_pooled(y, pooled, gout, 2, gamma, beta, mean, invstd, p1, N, B, C, H, H)
-    monkeypatch.setenv("AVDINO_REDUCE_M2_GENERIC", "1")
+    avd_opts(generic_m2=1)
     p0 = torch.full((C * G * R * 2,), float("nan"), device="cuda")
     ops.cl_bn_bwd_reduce_pooled(y, pooled, gout, 2, gamma, beta, mean, invstd, p0, N, B, C, H, H)
     s1 = p1.view(C, G, R, 2).to(F64).sum(2)
@@ -343,88 +343,20 @@ def test_bn_bwd_reduce_pooled_mode2_bench_size(ops, HC, monkeypatch):
     assert grel(s1[..., 1], (dz * xh).sum((1, 3)).T) < 1e-5
 
 
-# ------------------------------------------------------- dgrad + previous layer's BN-backward sums
-def _prev_layer(ops, g, N, B, Ci, H, small_gamma=False):
-    """The previous layer's BN -> ReLU -> pool over a random conv output yprev [N,2H,2H,Ci]:
-    (yprev, pooled, gamma, beta, mean, invstd) with per-(group, channel) statistics."""
-    G = N // B
-    yprev = (torch.randn(N, 2 * H, 2 * H, Ci, generator=g, device="cuda") * 0.7 + 0.2).to(T)
-    yv = yprev.to(F64).view(G, -1, Ci)
-    mean = yv.mean(1)
-    invstd = 1.0 / torch.sqrt(yv.var(1, unbiased=False) + 1e-5)
-    gamma = rnd(g, (Ci,), 0.5, 1.5)
-    beta = rnd(g, (Ci,), -0.3, 0.3)
-    if small_gamma:            # |beta| >> |gamma|: xhat must come from y (the fix-up pass)
-        gamma[1], beta[1] = 1e-2, 1.0
-        gamma[Ci - 1] = 0.0
-    scale = (gamma.to(F64) * invstd)
-    shift = beta.to(F64) - mean * scale
-    pooled = torch.empty(N, H, H, Ci, device="cuda", dtype=T)
-    ops.cl_bn_relu_pool(yprev, scale.float().reshape(-1).contiguous(), shift.float().reshape(-1).contiguous(),
-                        pooled, 0, N, B, Ci, 2 * H, 2 * H)
-    return yprev, pooled, gamma, beta, mean.float().reshape(-1).contiguous(), invstd.float().reshape(-1).contiguous()
-
-
-# (Cin, H, Cout, K, pad, N): the four conv_ws dgrad layers, N with many tiles per block
-RD_BENCH = [(8, 56, 16, 5, 2, 2048), (16, 28, 32, 5, 2, 2048), (32, 14, 64, 5, 2, 4096),
-            (32, 14, 64, 5, 0, 4096)]
-
-
-@pytest.mark.parametrize("small_gamma", [False, True])
-@pytest.mark.parametrize("shape", RD_BENCH)
-def test_dgrad_bnreduce_bench_size(ops, shape, small_gamma):
-    """avd_cl_conv_dgrad_bnreduce: dx bit-identical to avd_cl_conv_dgrad, and the previous
-    layer's BN-backward partial sums equal avd_cl_bn_bwd_reduce_pooled's (fp32 sum order, 1e-5)
-    and float64 of sum dz, sum dz * xhat.  small_gamma: channels whose xhat needs y go through
-    the fix-up pass (gamma = 1e-2 with beta = 1, and gamma = 0)."""
-    Ci, H, Co, K, pad, N = shape
-    B = 1024
-    G = N // B
-    Ho = H + 2 * pad - K + 1
-    g = torch.Generator(device="cuda").manual_seed(90 + H + pad + small_gamma)
-    w = (rnd(g, (Co, Ci, K, K)) / (Ci * K * K) ** 0.5).to(T).float()
-    wd = layout(ops, w, 1)
-    dy = rnd(g, (N, Ho, Ho, Co), dtype=T)
-    yprev, pooled, gamma, beta, mean, invstd = _prev_layer(ops, g, N, B, Ci, H, small_gamma)
-    Rf = ops.cl_dgrad_bnreduce_rows(T, N, B, Ci, H, H, Co, K, pad)
-    assert Rf > 0
-    dx1 = torch.full((N, H, H, Ci), float("nan"), device="cuda", dtype=T)
-    pf = torch.full((Ci * G * Rf * 2,), float("nan"), device="cuda")
-    ops.cl_conv_dgrad_bnreduce(dy, wd, dx1, pooled, yprev, gamma, beta, mean, invstd, pf, N, B,
-                               Ci, H, H, Co, K, pad)
-    dx0 = torch.empty_like(dx1)
-    ops.cl_conv_dgrad(dy, wd, dx0, N, Ci, H, H, Co, K, pad)
-    assert torch.equal(dx0, dx1)
-    R0 = ops.cl_bn_bwd_rows(B, Ci, 2 * H, 2 * H, T)
-    p0 = torch.empty(Ci * G * R0 * 2, device="cuda")
-    ops.cl_bn_bwd_reduce_pooled(yprev, pooled, dx0, 0, gamma, beta, mean, invstd, p0, N, B, Ci,
-                                2 * H, 2 * H)
-    s1 = pf.view(Ci, G, Rf, 2).to(F64).sum(2)
-    s0 = p0.view(Ci, G, R0, 2).to(F64).sum(2)
-    assert grel(s1[..., 0], s0[..., 0]) < 1e-5
-    assert grel(s1[..., 1], s0[..., 1]) < 1e-5
-    if not small_gamma:        # float64 from the pooled map: xhat = (p - beta) / gamma
-        pv, dv = pooled.to(F64).view(G, -1, Ci), dx0.to(F64).view(G, -1, Ci)
-        dz = torch.where(pv > 0, dv, torch.zeros_like(dv))
-        xh = (pv - beta.to(F64)) / gamma.to(F64)
-        assert grel(s1[..., 0], dz.sum(1).T) < 1e-5
-        assert grel(s1[..., 1], (dz * xh).sum(1).T) < 1e-5
-
-
 # ---------------------------------------------------------------------------- forced small grids
-def _capped(monkeypatch, cap, fn):
-    monkeypatch.delenv("AVDINO_GRID_CAP", raising=False)
+def _capped(avd_opts, cap, fn):
+    avd_opts(grid_cap=0)
     a = fn()
-    monkeypatch.setenv("AVDINO_GRID_CAP", str(cap))
+    avd_opts(grid_cap=cap)
     b = fn()
-    monkeypatch.delenv("AVDINO_GRID_CAP")
+    avd_opts(grid_cap=0)
     return a, b
 
 
 @pytest.mark.parametrize("shape", [(8, 56, 16, 5, 2, 48), (16, 28, 32, 5, 2, 48),
                                    (32, 14, 64, 5, 2, 96), (32, 14, 64, 5, 0, 96)])
 @pytest.mark.parametrize("cap", [1, 3, 7])
-def test_ws_kernels_many_tiles_per_block(ops, shape, cap, monkeypatch):
+def test_ws_kernels_many_tiles_per_block(ops, shape, cap, avd_opts):
     Ci, H, Co, K, pad, N = shape
     B = N // 2
     G = 2
@@ -452,7 +384,7 @@ def test_ws_kernels_many_tiles_per_block(ops, shape, cap, monkeypatch):
         torch.cuda.synchronize()
         return y, st.view(Co, G, R, 2).to(F64).sum(2), dx, dw
 
-    (y0, s0, dx0, dw0), (y1, s1, dx1, dw1) = _capped(monkeypatch, cap, run)
+    (y0, s0, dx0, dw0), (y1, s1, dx1, dw1) = _capped(avd_opts, cap, run)
     assert torch.equal(y0, y1) and torch.equal(dx0, dx1)
     # fp32 sum order: statistics are lane-local running sums over a block's tiles, so a cap of
     # one block sums ~10^4 values per lane (sum of signed values: 2.2e-6 measured at cap 1)
@@ -461,7 +393,7 @@ def test_ws_kernels_many_tiles_per_block(ops, shape, cap, monkeypatch):
 
 
 @pytest.mark.parametrize("cap", [1, 5])
-def test_conv1_wgrad_many_tiles_per_block(ops, cap, monkeypatch):
+def test_conv1_wgrad_many_tiles_per_block(ops, cap, avd_opts):
     N, B, H, C, K, pad = 12, 6, 112, 8, 5, 2
     G = N // B
     g = torch.Generator(device="cuda").manual_seed(60 + cap)
@@ -479,7 +411,7 @@ def test_conv1_wgrad_many_tiles_per_block(ops, cap, monkeypatch):
         torch.cuda.synchronize()
         return ns, dw
 
-    (n0, dw0), (n1, dw1) = _capped(monkeypatch, cap, run)
+    (n0, dw0), (n1, dw1) = _capped(avd_opts, cap, run)
     assert n1 == cap < n0
     assert grel(dw1, dw0) < 1e-6
 
@@ -606,7 +538,7 @@ def _offc_stats(ops, st, G, R, Co, n, rm=None, rv=None, pivot=None):
 
 @pytest.mark.parametrize("cap", [None, 8])
 @pytest.mark.parametrize("case", OFFC)
-def test_bn_stats_off_centre_bench_size(ops, case, cap, monkeypatch):
+def test_bn_stats_off_centre_bench_size(ops, case, cap, avd_opts):
     """BatchNorm forward statistics where |mean| >> std: x in [0, 1], positive
     weights, bias +20, so every channel's |mean|/std is >= 10 (the regime where var = E[y^2] -
     mean^2 amplifies the error of the fp32 running sums by mean^2 / var).  avd_bn_finalize's mean
@@ -623,10 +555,7 @@ def test_bn_stats_off_centre_bench_size(ops, case, cap, monkeypatch):
     stay within 3e-4 capped (1.4e-4 measured: what remains is the fp32 rounding of ~6000-term
     lane sums)."""
     kind, Ci, H, Co, K, pad, N = case
-    if cap is None:
-        monkeypatch.delenv("AVDINO_GRID_CAP", raising=False)
-    else:
-        monkeypatch.setenv("AVDINO_GRID_CAP", str(cap))
+    avd_opts(grid_cap=cap or 0)
     B = B_BENCH
     G = N // B
     Ho = H + 2 * pad - K + 1

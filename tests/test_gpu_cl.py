@@ -252,13 +252,11 @@ def test_cl_bn_bwd_apply_wgrad_fused_first_layer(ops, HN):
                                 # conv1 (1->32 at 28^2, unimodal.py:127-141)
                                 (28, 6, 32, 3, 1), (28, 6, 32, 5, 2), (20, 6, 32, 5, 2),
                                 (48, 4, 32, 5, 2)])
-def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN, monkeypatch):
+def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN, avd_opts):
     """avd_cl_c1_recompute (the audio conv1 without a stored conv output) against the stored-y
     kernels on the same bf16 operands: identical pooled output (bit-exact: same rounded y), and
     the statistics / BN-backward partials / weight gradient to fp32 summation order."""
     H, N, C, K, pad = HN
-    if K == 5 and C != 8:
-        monkeypatch.setenv("AVDINO_C1R5", "1")     # the 5x5 image conv1 passes (opt-in path)
     B, Cin = N // 2, 1
     G = N // B
     T = torch.bfloat16
@@ -375,7 +373,7 @@ def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN, monkeypatch):
 
 
 # The bench's mid-layer convs are served by the weights-stationary kernel (conv_ws.hip) in bf16;
-# AVDINO_CONV_LEGACY=1 routes them to conv_cl_kernel.  The 56x56 and 28x28 layers keep the
+# avd_options.generic_conv = 1 routes them to conv_cl_kernel.  The 56x56 and 28x28 layers keep the
 # legacy K order and accumulation order: bit-identical maps.  The 14x14 layers split K over two
 # waves (summed in fixed order), so there the two differ by bf16 rounding only; both paths are
 # also checked against float64.
@@ -384,17 +382,17 @@ WS_SHAPES = [  # N, B, Cin, H, Cout, K, pad
     (48, 24, 32, 14, 64, 5, 0)]
 
 
-def _both_paths(monkeypatch, fn):
-    monkeypatch.setenv("AVDINO_CONV_LEGACY", "0")
+def _both_paths(avd_opts, fn):
+    avd_opts(generic_conv=0)
     a = fn()
-    monkeypatch.setenv("AVDINO_CONV_LEGACY", "1")
+    avd_opts(generic_conv=1)
     b = fn()
-    monkeypatch.delenv("AVDINO_CONV_LEGACY")
+    avd_opts(generic_conv=0)
     return a, b
 
 
 @pytest.mark.parametrize("shape", WS_SHAPES)
-def test_ws_conv_fwd_matches_legacy(ops, shape, monkeypatch):
+def test_ws_conv_fwd_matches_legacy(ops, shape, avd_opts):
     N, B, Cin, H, Cout, K, pad = shape
     G = N // B
     x, w, b = _inputs((N, Cin, H, Cout, K, pad), "bf16", 11)
@@ -412,7 +410,7 @@ def test_ws_conv_fwd_matches_legacy(ops, shape, monkeypatch):
         torch.cuda.synchronize()
         return host(y), host(st).reshape(Cout, G, R, 2).sum(2)
 
-    (y1, s1), (y0, s0) = _both_paths(monkeypatch, run)
+    (y1, s1), (y0, s0) = _both_paths(avd_opts, run)
     if H > 14:
         assert np.array_equal(y1, y0)
         assert rel(s1, s0) < 1e-6
@@ -424,7 +422,7 @@ def test_ws_conv_fwd_matches_legacy(ops, shape, monkeypatch):
 
 
 @pytest.mark.parametrize("shape", WS_SHAPES)
-def test_ws_conv_dgrad_matches_legacy(ops, shape, monkeypatch):
+def test_ws_conv_dgrad_matches_legacy(ops, shape, avd_opts):
     N, _, Cin, H, Cout, K, pad = shape
     x, w, _ = _inputs((N, Cin, H, Cout, K, pad), "bf16", 12)
     y_ref, win = O.conv2d_fwd(x.astype(np.float64), w.astype(np.float64), np.zeros(Cout), pad)
@@ -440,7 +438,7 @@ def test_ws_conv_dgrad_matches_legacy(ops, shape, monkeypatch):
         torch.cuda.synchronize()
         return host(dx)
 
-    d1, d0 = _both_paths(monkeypatch, run)
+    d1, d0 = _both_paths(avd_opts, run)
     if H > 14:
         assert np.array_equal(d1, d0)
     else:
@@ -450,7 +448,7 @@ def test_ws_conv_dgrad_matches_legacy(ops, shape, monkeypatch):
 
 
 @pytest.mark.parametrize("shape", WS_SHAPES)
-def test_ws_conv_wgrad_matches_legacy(ops, shape, monkeypatch):
+def test_ws_conv_wgrad_matches_legacy(ops, shape, avd_opts):
     """wgrad_ws.hip (one block = all weight columns of its sample chunk) vs the legacy kernel
     and float64: exact bf16 products, fp32 sums in another order."""
     N, _, Cin, H, Cout, K, pad = shape
@@ -469,73 +467,12 @@ def test_ws_conv_wgrad_matches_legacy(ops, shape, monkeypatch):
         torch.cuda.synchronize()
         return host(dw)
 
-    w1, w0 = _both_paths(monkeypatch, run)
+    w1, w0 = _both_paths(avd_opts, run)
     wz = np.zeros((Cout, Cin, K, K))
     _, win = O.conv2d_fwd(x.astype(np.float64), wz, np.zeros(Cout), pad)
     _, dw_ref, _ = O.conv2d_bwd(dy.astype(np.float64), win, wz, x.shape, pad)
     assert rel(w1, dw_ref) < 1e-5
     assert rel(w0, dw_ref) < 1e-5
-
-
-# BatchNorm-backward apply fused into the dgrad / wgrad staging (bnapply.h): must equal the
-# unfused avd_cl_bn_bwd_apply -> avd_cl_conv_wgrad / avd_cl_conv_dgrad chain bit for bit.
-BNAPPLY_SHAPES = [  # N, B, Cin, H, Cout, K, pad, gmode (0: pooled NHWC bf16, 2: f32 flatten)
-    (48, 24, 8, 56, 16, 5, 2, 0), (48, 24, 16, 28, 32, 5, 2, 0), (48, 24, 32, 14, 64, 5, 2, 2),
-    (48, 24, 32, 14, 64, 5, 0, 2), (48, 16, 32, 14, 64, 5, 2, 0)]
-
-
-@pytest.mark.parametrize("shape", BNAPPLY_SHAPES)
-def test_bnapply_fused_dgrad_wgrad_match_unfused(ops, shape):
-    N, B, Cin, H, Cout, K, pad, gmode = shape
-    G = N // B
-    T = torch.bfloat16
-    Ho = H + 2 * pad - K + 1
-    assert ops.cl_bnapply_ok(T, N, B, Cin, H, H, Cout, K, pad, gmode)
-    g = torch.Generator(device="cuda").manual_seed(21)
-
-    def rnd(*shape, dtype=torch.float32, lo=-1.0, hi=1.0):
-        return (torch.rand(*shape, generator=g, device="cuda") * (hi - lo) + lo).to(dtype)
-
-    x = rnd(N, H, H, Cin, dtype=T)
-    y = rnd(N, Ho, Ho, Cout, dtype=T)
-    gout = rnd(N, Ho // 2, Ho // 2, Cout, dtype=T) if gmode == 0 else rnd(N * Cout * (Ho // 2) ** 2)
-    scale, shift = rnd(G * Cout, lo=0.5, hi=1.5), rnd(G * Cout, lo=-0.2, hi=0.2)
-    coef = rnd(G * Cout * 3, lo=-0.5, hi=0.5)
-    w = rnd(Cout, Cin, K, K) / (Cin * K * K) ** 0.5
-    wd = torch.empty(ops.cl_weight_elems(Cout, Cin, K, 1), device="cuda", dtype=T)
-    ops.cl_weight_layout(w, wd, 1)
-    nch = ops.cl_wgrad_chunks(N, Cout, Cin, K)
-
-    def wsum(parts):
-        dw = torch.empty(Cout * Cin * K * K, device="cuda")
-        ops.sum_rows(parts, nch, Cout * Cin * K * K, dw)
-        return dw
-
-    # unfused chain
-    dy = torch.empty_like(y)
-    ops.cl_bn_bwd_apply(y, gout, gmode, scale, shift, coef, dy, N, B, Cout, Ho, Ho)
-    p0 = torch.full((nch * Cout * Cin * K * K,), float("nan"), device="cuda")
-    ops.cl_conv_wgrad(x, dy, p0, N, Cin, H, H, Cout, K, pad)
-    dx0 = torch.empty(N, H, H, Cin, device="cuda", dtype=T)
-    ops.cl_conv_dgrad(dy, wd, dx0, N, Cin, H, H, Cout, K, pad)
-    # fused
-    p1 = torch.full_like(p0, float("nan"))
-    ops.cl_conv_wgrad_bnapply(x, y, gout, gmode, scale, shift, coef, p1, N, B, Cin, H, H, Cout, K, pad)
-    dx1 = torch.full_like(dx0, float("nan"))
-    ops.cl_conv_dgrad_bnapply(y, gout, gmode, scale, shift, coef, wd, dx1, N, B, Cin, H, H, Cout, K, pad)
-    # dgrad that also stores the dy it forms (AVDINO_DGRAD_APPLY), then the plain weight gradient
-    dx2 = torch.full_like(dx0, float("nan"))
-    dy2 = torch.full_like(dy, float("nan"))
-    ops.cl_conv_dgrad_bnapply(y, gout, gmode, scale, shift, coef, wd, dx2, N, B, Cin, H, H, Cout, K,
-                              pad, dy=dy2)
-    p2 = torch.full_like(p0, float("nan"))
-    ops.cl_conv_wgrad(x, dy2, p2, N, Cin, H, H, Cout, K, pad)
-    torch.cuda.synchronize()
-    assert torch.equal(wsum(p1), wsum(p0))
-    assert torch.equal(dx1, dx0)
-    assert torch.equal(dy2, dy)
-    assert torch.equal(dx2, dx0)
-    assert torch.equal(wsum(p2), wsum(p0))
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])

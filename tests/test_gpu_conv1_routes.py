@@ -35,7 +35,7 @@ def grel(a, b):
 
 
 @pytest.mark.parametrize("cap", [3, 7])
-def test_image_conv1_passes_capped_grid(ops, monkeypatch, cap):
+def test_image_conv1_passes_capped_grid(ops, avd_opts, cap):
     N, B, H, C = 96, 32, 28, 32
     G, Hp = N // B, H // 2
     g = torch.Generator(device="cuda").manual_seed(23)
@@ -73,11 +73,11 @@ def test_image_conv1_passes_capped_grid(ops, monkeypatch, cap):
     bn0 = stats()
     z0, c0 = apply(bn0)
     m0 = moments(c0)
-    monkeypatch.setenv("AVDINO_GRID_CAP", str(cap))
+    avd_opts(grid_cap=cap)
     bn1 = stats()
     z1, c1 = apply(bn0)                   # the uncapped coefficients: a block-independent map
     m1 = moments(c0)
-    monkeypatch.delenv("AVDINO_GRID_CAP")
+    avd_opts(grid_cap=0)
     assert grel(bn1, bn0) < 1e-6
     assert torch.equal(z1, z0) and torch.equal(c1, c0)
     assert grel(m1, m0) < 1e-6

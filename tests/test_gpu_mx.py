@@ -50,9 +50,9 @@ def _weights(w, dgrad):
 
 
 @pytest.fixture(params=[None, "5"], ids=["grid", "capped"])
-def capped(request, monkeypatch):
+def capped(request, avd_opts):
     if request.param:
-        monkeypatch.setenv("AVDINO_GRID_CAP", request.param)
+        avd_opts(grid_cap=int(request.param))
     return request.param
 
 

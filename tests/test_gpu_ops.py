@@ -407,3 +407,25 @@ def test_linear_bwd_pair_launch_equals_two_gemms(ops, monkeypatch, mode, rows, O
     assert c2[:, :In].abs().max().item() == 0
     ref = host(dout).astype(np.float64).T @ host(x).astype(np.float64)
     assert rel(host(a2), ref) < (1e-6 if mode == 1 else 1e-2)
+
+
+@pytest.mark.parametrize("rows,cols,off,acc", [(256, 51200, 0, 0), (256, 3200, 0, 1), (7168, 256, 0, 0),
+                                               (37, 1001, 0, 0), (96, 600, 3, 1), (1, 4, 0, 0)])
+def test_sum_rows_vs_float64(ops, rows, cols, off, acc):
+    """avd_sum_rows_split, the weight-gradient slab / bias-gradient reduction: the 16-byte path
+    (cols % 4 == 0, aligned), the scalar path (odd columns, an unaligned offset), one-pass and
+    row-chunked shapes, accumulate; float64 accumulation inside, so within 1 ulp of the float64
+    column sums; bitwise repeatable."""
+    g = torch.Generator(device="cuda").manual_seed(rows + cols)
+    x = torch.randn(off + rows * cols, generator=g, device="cuda")
+    base = torch.randn(cols, generator=g, device="cuda")
+    ref = x[off:].view(rows, cols).double().sum(0) + (base.double() if acc else 0.0)
+    outs = []
+    for _ in range(2):
+        out = base.clone()
+        ops.sum_rows(x, rows, cols, out, accumulate=acc, off=off)
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    err = (outs[0].double() - ref).abs().max().item()
+    assert err <= 2e-7 * max(ref.abs().max().item(), 1.0), err
