@@ -139,6 +139,31 @@ int avd_linear_bwd(int rows, int O, int In, const float* dout, long long dout_ld
                    long long x_ld, const float* W, float* dW, float* dX, long long dx_ld, float* db,
                    int mode, float* ws, long long ws_elems, void* stream);
 
+/* The encoder Linear of CentralUnimodalImage / Audio (unimodal.py:153 fc: Linear(1600 / 3136, E)
+ * over x.view(N, -1) of the last conv block's pooled map, dino.py:459-468) in the bf16 step, over
+ * the pooled map as it lies in HBM: feat [rows][HW*C] bf16 NHWC, i.e. features in (h, w, c)
+ * order, while W [O][C*HW] f32 keeps the reference's (c, h, w) flatten order (state_dict, Adam,
+ * EMA, all-reduce unchanged).  bf16 MFMA, f32 accumulate -- the same products as avd_gemm mode 2
+ * over the f32 (c, h, w) features, whose bf16 rounding the tail pass now does when it stores them.
+ *   avd_linear_weight_hwc: n <= 4 weights per launch, Wp[e] [O][HW*C] bf16 = W[e] with its
+ *     columns in (h, w, c) order (per step, after Adam / EMA changed W);
+ *   avd_linear_fwd_hwc: out[r*out_ld + o] = sum_i feat[r][i] Wp[o][i] + bias[o] (f32);
+ *   avd_linear_bwd_hwc: dW[o][(c,h,w)] = sum_r dout[r][o] feat[r][(h,w,c)] (f32, the reference's
+ *     order), db[o] = sum_r dout[r][o] (nullable), dX[r][(h,w,c)] = sum_o dout[r][o] Wp[o][...]
+ *     stored bf16 -- the last conv block's pooled gradient in NHWC (avd_cl_bn_bwd_* mode 0);
+ *     one paired launch + its split-K reduces, as avd_linear_bwd.
+ * ws: avd_linear_hwc_ws_elems floats (required by the backward).  C*HW % 8 == 0, O % 4 == 0,
+ * feat / Wp / dout 16-byte aligned. */
+long long avd_linear_hwc_ws_elems(int rows, int O, int In);
+int avd_linear_weight_hwc(int n, const float* const* W, void* const* Wp, const int* O, const int* C,
+                          const int* HW, void* stream);
+int avd_linear_fwd_hwc(int rows, int O, int C, int HW, const void* feat, const void* Wp,
+                       const float* bias, float* out, long long out_ld, float* ws,
+                       long long ws_elems, void* stream);
+int avd_linear_bwd_hwc(int rows, int O, int C, int HW, const float* dout, long long dout_ld,
+                       const void* feat, const void* Wp, float* dW, float* db, void* dX,
+                       float* ws, long long ws_elems, void* stream);
+
 /* ------------------------------------------------------------------ channels-last conv blocks
  * The training path's conv blocks on NHWC maps ([N][H][W][C]; Cin = 1 maps are the plain
  * images), on MFMA for both storage types: dt = AVD_BF16 (v_mfma_f32_16x16x32_bf16) or AVD_F32

@@ -29,6 +29,10 @@ PROTOS = {
     "avd_gemm_ws_elems": [I, I, I, I],
     "avd_linear_bwd": [I, I, I, P, L, P, L, P, P, P, L, P, I, P, L, P],
     "avd_linear_bwd_ws_elems": [I, I, I, I],
+    "avd_linear_hwc_ws_elems": [I, I, I],
+    "avd_linear_weight_hwc": [I, P, P, P, P, P, P],
+    "avd_linear_fwd_hwc": [I, I, I, I, P, P, P, P, L, P, L, P],
+    "avd_linear_bwd_hwc": [I, I, I, I, P, L, P, P, P, P, P, P, L, P],
     "avd_cl_weight_elems": [I, I, I, I],
     "avd_cl_weight_layout": [P, P, I, I, I, I, I, P],
     "avd_cl_weight_layout_batch": [I, P, P, P, P, P, P, I, P],
@@ -140,6 +144,7 @@ def _load():
         fn.argtypes = args
         fn.restype = ctypes.c_int
     lib.avd_gemm_ws_elems.restype = ctypes.c_longlong
+    lib.avd_linear_hwc_ws_elems.restype = ctypes.c_longlong
     lib.avd_mx_weight_bytes.restype = ctypes.c_longlong
     lib.avd_mx_scale_bytes.restype = ctypes.c_longlong
     lib.avd_last_error.argtypes = []

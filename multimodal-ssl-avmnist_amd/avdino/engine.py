@@ -59,13 +59,15 @@ class ConvBranch:
     """[conv -> BN(train, per group) -> ReLU -> maxpool2] x L (+ (c,h,w) flatten or GAP) over
     channels-last maps, forward and backward (CentralUnimodalImage/Audio.forward,
     unimodal.py:127-221; the 3x3 CNNs, dino.py:18-73).  Same kernels for f32 (parity, f32
-    MFMA) and bf16 (bench) storage; only the final features are f32 [N, F] in the reference's
-    flatten order."""
+    MFMA) and bf16 (bench) storage; the final features are f32 [N, F] in the reference's
+    flatten order, or -- ``hwc`` (bf16, flatten tails) -- the last pooled map itself, bf16 NHWC,
+    for the encoder Linear's (h, w, c)-ordered kernels (avd_linear_*_hwc)."""
 
-    def __init__(self, stack, act_dtype, fp8=False):
+    def __init__(self, stack, act_dtype, fp8=False, hwc=False):
         self.stack = stack
         self.act = act_dtype
         self.dims = stack.layer_dims()
+        self.hwc = bool(hwc) and act_dtype == torch.bfloat16 and not stack.gap
         # fp8: the layers after the first run their forward, input gradient AND weight gradient
         # on the block-scaled e4m3 MFMA (config 5's "fp8 MFMA conv path", avd_mx_conv_*: both
         # operands quantised to e4m3 while staged, one E8M0 scale per strip / 32-k block); the
@@ -162,10 +164,17 @@ class ConvBranch:
         return ops.cl_stat_rows(Ho, Ho, B, k, ci, co, self.act)
 
     def _tail_mode(self):
-        return 1 if self.stack.gap else 2
+        """Layout of the last block's pooled output: 1 = GAP f32, 2 = (c,h,w) flatten f32,
+        0 = NHWC in the activation dtype (hwc)."""
+        return 1 if self.stack.gap else (0 if self.hwc else 2)
+
+    def feat_shape(self):
+        """(channels, pooled pixels) of the last block: the hwc Linear's C and HW."""
+        return self.stack.convs[-1][1], self.dims[-1][2] ** 2
 
     def forward(self, ws, store, tag, x, N, G, update_running=True, need_dgrad=False):
-        """x: staged input [N,H,W,1] (act dtype).  Returns (features f32 [N, F], ctx)."""
+        """x: staged input [N,H,W,1] (act dtype).  Returns (features [N, F], ctx): f32 in the
+        reference's flatten order, or the NHWC pooled map (hwc)."""
         B = N // G
         wts = self.prepare(ws, store, tag, need_dgrad, N, B)
         ctx = {"x": [x], "y": [], "stats": [], "wts": wts, "N": N, "G": G}
@@ -196,7 +205,7 @@ class ConvBranch:
             ctx["stats"].append(st)
             if i == nl - 1:
                 mode = self._tail_mode()
-                out = ws.get(f"{tag}.feat", N * co * (1 if mode == 1 else Hp * Hp), F32)
+                out = ws.get(f"{tag}.feat", N * co * (1 if mode == 1 else Hp * Hp), F32 if mode else self.act)
             else:
                 mode = 0
                 out = ws.get(f"{tag}.x{i + 1}", N * Hp * Hp * co, self.act)
@@ -231,7 +240,7 @@ class ConvBranch:
                              store[bk + ".running_var"], coef[0], coef[1])
             if i == nl - 1:
                 mode = self._tail_mode()
-                out = ws.get(f"{tag}.feat", N * co * (1 if mode == 1 else Hp * Hp), F32)
+                out = ws.get(f"{tag}.feat", N * co * (1 if mode == 1 else Hp * Hp), F32 if mode else self.act)
             else:
                 mode = 0
                 out = ws.get(f"{tag}.x{i + 1}", N * Hp * Hp * co, self.act)
@@ -451,7 +460,8 @@ class ConvBranch:
     # chain (within noise).
 
     def backward(self, ws, store, ctx, dfeat, wstream=None):
-        """dfeat: f32 [N, F] gradient of the features; writes conv/BN parameter grads.
+        """dfeat: gradient of the features (f32 [N, F]; hwc: NHWC act dtype); writes conv/BN
+        parameter grads.
         wstream: a second stream for the mid layers' weight gradients (they only read dy and
         the layer input, so they overlap the input-gradient chain); joined before returning."""
         N, G = ctx["N"], ctx["G"]
@@ -697,10 +707,13 @@ class MultiCentralEngine:
         self.conv_fp8 = bool(conv_fp8) and act_dtype == torch.bfloat16
         self.encoder = encoder
         istack, self.img_lin, astack, self.aud_lin, _sd = MULTI_ENCODERS[encoder]
-        self.img = ConvBranch(istack("student"), act_dtype, conv_fp8)
-        self.aud = ConvBranch(astack("student"), act_dtype, conv_fp8)
-        self.t_img = ConvBranch(istack("teacher"), act_dtype, conv_fp8)
-        self.t_aud = ConvBranch(astack("teacher"), act_dtype, conv_fp8)
+        # bf16: the flatten tails stay NHWC bf16 and the encoder Linears run on the (h, w, c)
+        # ordered kernels (avd_linear_*_hwc) with a per-step bf16 copy of their weights
+        hwc = self.HWC and act_dtype == torch.bfloat16
+        self.img = ConvBranch(istack("student"), act_dtype, conv_fp8, hwc)
+        self.aud = ConvBranch(astack("student"), act_dtype, conv_fp8, hwc)
+        self.t_img = ConvBranch(istack("teacher"), act_dtype, conv_fp8, hwc)
+        self.t_aud = ConvBranch(astack("teacher"), act_dtype, conv_fp8, hwc)
         self.sproj = ProjHead("student_projection", D, P, gemm_mode=self.gm)
         self.tproj = ProjHead("teacher_projection", D, P, gemm_mode=self.gm)
         self.heads = None
@@ -755,6 +768,41 @@ class MultiCentralEngine:
         (ops.alloc_epoch) and this engine's own workspaces."""
         return (ops.alloc_epoch(), self.ws.epoch, self.tws.epoch, self.iws.epoch)
 
+    # encoder Linears over the NHWC bf16 pooled maps in the bf16 step (False: f32 (c,h,w)
+    # features through avd_gemm / avd_linear_bwd, as in the fp32 parity mode)
+    HWC = True
+
+    def _wp(self, prefix, branch):
+        """The per-step bf16 (h, w, c)-column copy of ``prefix``'s image / audio encoder Linear."""
+        lin = self.img_lin if branch == "img" else self.aud_lin
+        w = self.store[f"{prefix}.{lin}.weight"]
+        return self.ws.get(f"wp.{prefix}.{branch}", w.numel(), torch.bfloat16)
+
+    def _prepare_hwc(self, prefixes):
+        """Refresh the bf16 (h, w, c) weight copies of these prefixes' encoder Linears (one
+        launch), after Adam / EMA changed the weights."""
+        ent = []
+        for prefix in prefixes:
+            for branch, cb in (("img", self.img), ("aud", self.aud)):
+                if not cb.hwc:
+                    continue
+                lin = self.img_lin if branch == "img" else self.aud_lin
+                C, HW = cb.feat_shape()
+                ent.append((self.store[f"{prefix}.{lin}.weight"], self._wp(prefix, branch), C, HW))
+        if ent:
+            ops.linear_weight_hwc(ent)
+
+    def _linear_fwd(self, prefix, branch, cb, feat, cat, N, off):
+        E = self.E
+        lin = f"{prefix}.{self.img_lin if branch == 'img' else self.aud_lin}"
+        if cb.hwc:
+            C, HW = cb.feat_shape()
+            ops.linear_fwd_hwc(feat, self._wp(prefix, branch), self.store[lin + ".bias"], cat, N, E, C, HW,
+                               out_ld=2 * E, out_off=off)
+        else:
+            ops.linear_fwd(feat, self.store[lin + ".weight"], self.store[lin + ".bias"], cat, N,
+                           out_ld=2 * E, out_off=off, mode=self.gm)
+
     # the heads' backward queued interleaved with the main chain's (else after it); the
     # originals' heads forward queued after the fusion / projection (else before)
     INTERLEAVE = True
@@ -792,12 +840,9 @@ class MultiCentralEngine:
         # (the student's image branch on the side stream beside its audio branch measured slower:
         # 149.7k vs 152.4k pairs/s, r1_39 -- both fill the chip)
         fi, ci = ib.forward(ws, st, tag + ".img", x_img, N, G, update_running, need_dgrad)
-        lin = f"{prefix}.{self.img_lin}"
-        ops.linear_fwd(fi, st[lin + ".weight"], st[lin + ".bias"], cat, N, out_ld=2 * E, out_off=0,
-                       mode=self.gm)
+        self._linear_fwd(prefix, "img", ib, fi, cat, N, 0)
         fa, ca = ab.forward(ws, st, tag + ".aud", x_aud, N, G, update_running, need_dgrad)
-        lin = f"{prefix}.{self.aud_lin}"
-        ops.linear_fwd(fa, st[lin + ".weight"], st[lin + ".bias"], cat, N, out_ld=2 * E, out_off=E, mode=self.gm)
+        self._linear_fwd(prefix, "aud", ab, fa, cat, N, E)
         return cat, (fi, ci, fa, ca)
 
     def _fusion_fwd(self, prefix, cat, rows, tag, seed, ws=None, seed_off=None):
@@ -960,6 +1005,7 @@ class MultiCentralEngine:
         with torch.cuda.stream(self.tside):
             torch.add(self.sstate.seed_off, StepState.SEED_STRIDE, out=self._tseed)
             x_img, x_aud, B, G = tin
+            self._prepare_hwc(("teacher",))           # the EMA'd teacher's Linear copies
             self._teacher_fwd(x_img, x_aud, B, G, seed_off=self._tseed)
             done = torch.cuda.Event()
             done.record(self.tside)
@@ -984,6 +1030,9 @@ class MultiCentralEngine:
             self.sstate.begin()        # dropout offset of this step, optimizer step count
         ops.mark("fwd.begin")
         base = (self.seed * 1000003) & SEED_MASK
+        # this step's bf16 (h, w, c) copies of the encoder Linears (student; teacher unless its
+        # forward already ran under the previous step)
+        self._prepare_hwc(("student",) if teacher_ready else ("student", "teacher"))
 
         # teacher: global views (prefix of the staged buffers), train-mode BN, no grad -- on a
         # side stream, concurrently with the student (independent until the loss); pipelined
@@ -1175,10 +1224,15 @@ class MultiCentralEngine:
             host_point(lambda: self.grad_hook.bucket(g, self._early_ranges))
         fi, cimg, fa, caud = c["senc"]
         iws = self.iws
-        dfi = iws.get("dfeat_img", N * fi.shape[1])
+        dfi = iws.get("dfeat_img", fi.numel(), fi.dtype)
         ilin, alin = "student." + self.img_lin, "student." + self.aud_lin
 
         def image_linear():
+            if self.img.hwc:
+                C, HW = self.img.feat_shape()
+                ops.linear_bwd_hwc(dcat, fi, self._wp("student", "img"), st.grad_of(ilin + ".weight"),
+                                   st.grad_of(ilin + ".bias"), dfi, N, E, C, HW, dout_ld=2 * E)
+                return
             ops.linear_bwd(dcat, fi, st[ilin + ".weight"], st.grad_of(ilin + ".weight"),
                            st.grad_of(ilin + ".bias"), dfi, N, dout_ld=2 * E, mode=self.gm)
 
@@ -1191,9 +1245,14 @@ class MultiCentralEngine:
             image_linear()
             image_convs()
 
-        dfa = ws.get("dfeat_aud", N * fa.shape[1])
+        dfa = ws.get("dfeat_aud", fa.numel(), fa.dtype)
 
         def audio_linear():
+            if self.aud.hwc:
+                C, HW = self.aud.feat_shape()
+                ops.linear_bwd_hwc(dcat, fa, self._wp("student", "aud"), st.grad_of(alin + ".weight"),
+                                   st.grad_of(alin + ".bias"), dfa, N, E, C, HW, dout_ld=2 * E, dout_off=E)
+                return
             ops.linear_bwd(dcat, fa, st[alin + ".weight"], st.grad_of(alin + ".weight"),
                            st.grad_of(alin + ".bias"), dfa, N, dout_ld=2 * E, dout_off=E,
                            mode=self.gm)

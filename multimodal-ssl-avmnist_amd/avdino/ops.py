@@ -287,6 +287,59 @@ def linear_bwd(dout, x, w, dw, db, dx, rows, dout_ld=None, dout_off=0, x_ld=None
              mode=mode)
 
 
+# ---- the encoder Linear over NHWC bf16 features (include/avdino.h "encoder Linear ... NHWC")
+def linear_weight_hwc(entries):
+    """entries: [(W f32 [O, C*HW] in (c,h,w) column order, Wp bf16 [O*HW*C], C, HW)] (<= 4) ->
+    Wp = W with its columns in (h, w, c) order, one launch."""
+    import ctypes as _ct
+    n = len(entries)
+    _need(0 < n <= 4, "linear_weight_hwc batch size")
+    for W, Wp, C, HW in entries:
+        _need(W.dtype == torch.float32 and W.is_contiguous() and W.shape[1] == C * HW, "hwc W")
+        _need(Wp.dtype == torch.bfloat16 and Wp.numel() >= W.numel(), "hwc Wp")
+    ws = (_ct.c_void_p * n)(*[e[0].data_ptr() for e in entries])
+    wps = (_ct.c_void_p * n)(*[e[1].data_ptr() for e in entries])
+    Os = (_ct.c_int * n)(*[e[0].shape[0] for e in entries])
+    Cs = (_ct.c_int * n)(*[e[2] for e in entries])
+    HWs = (_ct.c_int * n)(*[e[3] for e in entries])
+    call("avd_linear_weight_hwc", n, ws, wps, Os, Cs, HWs, stream())
+
+
+def linear_fwd_hwc(feat, wp, b, out, rows, O, C, HW, out_ld=None, out_off=0):
+    """out[rows, O] (+out_ld/off) = feat_hwc[rows, HW*C] Wp^T + b on the bf16 MFMA (the encoder
+    Linear over the last conv block's NHWC pooled map)."""
+    In = C * HW
+    out_ld = O if out_ld is None else out_ld
+    _need(feat.dtype == torch.bfloat16 and feat.numel() >= rows * In, "hwc fwd feat")
+    _need(wp.dtype == torch.bfloat16 and wp.numel() >= O * In, "hwc fwd Wp")
+    _need(out.dtype == torch.float32 and out_off + (rows - 1) * out_ld + O <= out.numel(), "hwc fwd out")
+    nws = lib.avd_linear_hwc_ws_elems(rows, O, In)
+    ws = _gemm_workspace(out.device, nws)
+    _timed(f"linear_fwd_hwc[{rows}x{O}x{In}]", 2 * rows * In + 2 * O * In + 4 * rows * O,
+           2 * rows * O * In,
+           lambda: call("avd_linear_fwd_hwc", rows, O, C, HW, p(feat), p(wp), p(b),
+                        out.data_ptr() + 4 * out_off, out_ld, p(ws), nws, stream()))
+
+
+def linear_bwd_hwc(dout, feat, wp, dw, db, dx, rows, O, C, HW, dout_ld=None, dout_off=0):
+    """dW (reference (c,h,w) columns) = dout^T feat_hwc; db = sum_rows dout; dx (bf16 NHWC) =
+    dout Wp -- one paired launch + split-K reduces (avd_linear_bwd_hwc)."""
+    In = C * HW
+    dout_ld = O if dout_ld is None else dout_ld
+    _need(dout.dtype == torch.float32 and dout_off + (rows - 1) * dout_ld + O <= dout.numel(), "hwc bwd dout")
+    _need(feat.dtype == torch.bfloat16 and feat.numel() >= rows * In, "hwc bwd feat")
+    _need(wp.dtype == torch.bfloat16 and wp.numel() >= O * In, "hwc bwd Wp")
+    _need(dw.dtype == torch.float32 and dw.numel() >= O * In, "hwc bwd dW")
+    _need(dx.dtype == torch.bfloat16 and dx.numel() >= rows * In, "hwc bwd dX")
+    _need(db is None or db.numel() >= O, "hwc bwd db")
+    nws = lib.avd_linear_hwc_ws_elems(rows, O, In)
+    ws = _gemm_workspace(dout.device, nws)
+    _timed(f"linear_bwd_hwc[{rows}x{O}x{In}]",
+           4 * 2 * rows * O + 2 * 2 * rows * In + 2 * O * In + 4 * O * In, 4 * rows * O * In,
+           lambda: call("avd_linear_bwd_hwc", rows, O, C, HW, dout.data_ptr() + 4 * dout_off, dout_ld,
+                        p(feat), p(wp), p(dw), p(db), p(dx), p(ws), nws, stream()))
+
+
 # ---------------------------------------------------------------- channels-last conv blocks
 def cl_weight_elems(Cout, Cin, K, dgrad):
     return lib.avd_cl_weight_elems(Cout, Cin, K, int(dgrad))

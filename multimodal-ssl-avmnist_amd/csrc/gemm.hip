@@ -6,6 +6,7 @@
 // v1: LDS-tiled 64x64x16 tiles, 256 threads, 4x4 outputs per thread, fp32 FMA (bitwise
 // deterministic: no split-K).
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 
@@ -123,8 +124,12 @@ enum { LAY_K = 0, LAY_R = 1, LAY_S = 2 };
 template <int ROWS>
 struct TileRegs { float v[ROWS / 8 > 16 ? ROWS / 8 : 16]; };   // ROWS*32 elements over 256 threads
 
-template <int ROWS, int LAY>
-__device__ __forceinline__ void load_tile(const float* __restrict__ X, long long sr, long long sk,
+// f32 operand loads (bf16 operands go through the raw Stage specialisations below)
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+
+template <int ROWS, int LAY, typename S = float>
+__device__ __forceinline__ void load_tile(const S* __restrict__ X, long long sr, long long sk,
                                           int r0, int k0, int rows, int kend, TileRegs<ROWS>& t) {
   const int tid = threadIdx.x;
   if constexpr (LAY == LAY_K) {
@@ -135,12 +140,12 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ X, long long
       const int gr = r0 + r, gk = k0 + k;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (gr < rows) {
-        const float* p = X + (size_t)gr * sr + gk;
-        if (gk + 3 < kend) v = *reinterpret_cast<const float4*>(p);
+        const S* p = X + (size_t)gr * sr + gk;
+        if (gk + 3 < kend) v = ld4(p);
         else {
-          if (gk < kend) v.x = p[0];
-          if (gk + 1 < kend) v.y = p[1];
-          if (gk + 2 < kend) v.z = p[2];
+          if (gk < kend) v.x = ld1(p);
+          if (gk + 1 < kend) v.y = ld1(p + 1);
+          if (gk + 2 < kend) v.z = ld1(p + 2);
         }
       }
       t.v[4 * i] = v.x; t.v[4 * i + 1] = v.y; t.v[4 * i + 2] = v.z; t.v[4 * i + 3] = v.w;
@@ -162,12 +167,12 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ X, long long
         const int gk = k0 + 4 * kb + kk;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (b < 2 * ROWS && gk < kend) {
-          const float* p = X + (size_t)gk * sk + gr;
-          if (gr + 3 < rows) v = *reinterpret_cast<const float4*>(p);
+          const S* p = X + (size_t)gk * sk + gr;
+          if (gr + 3 < rows) v = ld4(p);
           else {
-            if (gr < rows) v.x = p[0];
-            if (gr + 1 < rows) v.y = p[1];
-            if (gr + 2 < rows) v.z = p[2];
+            if (gr < rows) v.x = ld1(p);
+            if (gr + 1 < rows) v.y = ld1(p + 1);
+            if (gr + 2 < rows) v.z = ld1(p + 2);
           }
         }
         t.v[16 * i + kk] = v.x; t.v[16 * i + 4 + kk] = v.y;
@@ -182,7 +187,7 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ X, long long
       int r, k;
       if (kfast) { r = e >> 5; k = e & 31; } else { k = e / ROWS; r = e % ROWS; }
       const int gr = r0 + r, gk = k0 + k;
-      t.v[i] = (gr < rows && gk < kend) ? X[(size_t)gr * sr + (size_t)gk * sk] : 0.f;
+      t.v[i] = (gr < rows && gk < kend) ? ld1(X + (size_t)gr * sr + (size_t)gk * sk) : 0.f;
     }
   }
 }
@@ -257,19 +262,137 @@ __device__ __forceinline__ void store_tile(const TileRegs<ROWS>& t, long long sr
   }
 }
 
+// Staging of one operand tile (ROWS x 32 k) from HBM through registers into the LDS ring.  f32
+// sources (and bf16 ones in the f32 MFMA mode) go through TileRegs as floats; bf16 sources in the
+// bf16 mode are copied raw, 16 bytes per load (8-byte accesses run at 0.54-0.70x the 16-byte rate,
+// MI355X_MICROARCH.md): k-contiguous rows as 16-byte chunks straight into their swizzled LDS
+// chunk, row-contiguous (LAY_R) ones as 8 rows x 4 k per thread transposed in registers.
+template <int MODE, int ROWS, int LAY, typename S,
+          bool RAW = (MODE == 2 && std::is_same<S, bf16>::value && LAY != LAY_S)>
+struct Stage {
+  TileRegs<ROWS> t;
+  __device__ __forceinline__ void load(const S* __restrict__ X, long long sr, long long sk, int r0,
+                                       int k0, int rows, int kend) {
+    load_tile<ROWS, LAY, S>(X, sr, sk, r0, k0, rows, kend, t);
+  }
+  __device__ __forceinline__ void store(long long sr, long long sk, typename GemmT<MODE>::T* dst) {
+    store_tile<MODE, ROWS, LAY>(t, sr, sk, dst);
+  }
+};
+
+__device__ __forceinline__ unsigned hw16(const uint4& v, int j) {
+  const unsigned w = j < 2 ? v.x : j < 4 ? v.y : j < 6 ? v.z : v.w;
+  return (j & 1) ? (w >> 16) : (w & 0xffffu);
+}
+
+template <int MODE, int ROWS, typename S>
+struct Stage<MODE, ROWS, LAY_K, S, true> {
+  static constexpr int NV = ROWS / 64 > 0 ? ROWS / 64 : 1;   // 16-byte chunks per thread
+  uint4 v[NV];
+  __device__ __forceinline__ void load(const S* __restrict__ X, long long sr, long long, int r0,
+                                       int k0, int rows, int kend) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = (int)threadIdx.x + 256 * i;
+      const int r = e >> 2, kc = e & 3;
+      const int gr = r0 + r, gk = k0 + 8 * kc;
+      uint4 u = make_uint4(0u, 0u, 0u, 0u);
+      if (r < ROWS && gr < rows) {
+        const bf16* p = reinterpret_cast<const bf16*>(X) + (size_t)gr * sr + gk;
+        if (gk + 7 < kend) {
+          u = *reinterpret_cast<const uint4*>(p);
+        } else {
+          unsigned h[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) h[j] = gk + j < kend ? p[j] : 0u;
+          u = make_uint4(h[0] | h[1] << 16, h[2] | h[3] << 16, h[4] | h[5] << 16, h[6] | h[7] << 16);
+        }
+      }
+      v[i] = u;
+    }
+  }
+  __device__ __forceinline__ void store(long long, long long, typename GemmT<MODE>::T* dst) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = (int)threadIdx.x + 256 * i;
+      const int r = e >> 2, kc = e & 3;
+      if (r < ROWS) *reinterpret_cast<uint4*>(dst + gsw(r, 8 * kc)) = v[i];
+    }
+  }
+};
+
+template <int MODE, int ROWS, typename S>
+struct Stage<MODE, ROWS, LAY_R, S, true> {
+  static_assert(ROWS <= 256 && ROWS % 8 == 0, "LAY_R raw tile");
+  static constexpr int RG = ROWS / 8;                         // 8-row groups; thread = (kq, rg)
+  uint4 v[4];
+  __device__ __forceinline__ void load(const S* __restrict__ X, long long, long long sk, int r0,
+                                       int k0, int rows, int kend) {
+    const int b = threadIdx.x;
+    const int rg = b % RG, kq = b / RG;
+    const int gr = r0 + 8 * rg;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int gk = k0 + 4 * kq + kk;
+      uint4 u = make_uint4(0u, 0u, 0u, 0u);
+      if (b < 8 * RG && gk < kend) {
+        const bf16* p = reinterpret_cast<const bf16*>(X) + (size_t)gk * sk + gr;
+        if (gr + 7 < rows) {
+          u = *reinterpret_cast<const uint4*>(p);
+        } else {
+          unsigned h[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) h[j] = gr + j < rows ? p[j] : 0u;
+          u = make_uint4(h[0] | h[1] << 16, h[2] | h[3] << 16, h[4] | h[5] << 16, h[6] | h[7] << 16);
+        }
+      }
+      v[kk] = u;
+    }
+  }
+  __device__ __forceinline__ void store(long long, long long, typename GemmT<MODE>::T* dst) {
+    const int b = threadIdx.x;
+    if (b >= 8 * RG) return;
+    const int rg = b % RG, kq = b / RG;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int j = (jj + rg) & 7;            // rotated per row group: the 16-lane write groups
+      const unsigned lo = hw16(v[0], j) | hw16(v[1], j) << 16;   // spread over the bank rows
+      const unsigned hi = hw16(v[2], j) | hw16(v[3], j) << 16;
+      *reinterpret_cast<uint2*>(dst + gsw(8 * rg + j, 4 * kq)) = make_uint2(lo, hi);
+    }
+  }
+};
+
 // One GEMM problem of a launch (the paired launch carries two).
 struct GemmArgs {
   int M, N, K, kchunk;
-  const float* A;
+  const void* A;      // f32 or bf16 (the kernel's SA / SB template types)
   long long sam, sak;
-  const float* B;
+  const void* B;
   long long sbk, sbn;
-  float* C;
+  void* C;            // f32, or bf16 when c_bf16
   long long ldc;
   const float* bias;
   float alpha, beta;
   float* ws;      // split-K partial tiles (nullptr: one pass over K)
+  int c_bf16;     // C stored as bf16 (beta must be 0)
+  int map_c;      // > 0: output column n lands at (n % map_c) * map_hw + n / map_c (an NHWC
+  int map_hw;     //      (h, w, c) feature index -> the reference's (c, h, w) flatten index)
 };
+
+// the output element (m, n) of a problem: bias, alpha / beta, bf16 or f32, optional column map
+__device__ __forceinline__ void gemm_out(const GemmArgs& p, int m, int n, float acc) {
+  const float bv = p.bias ? p.bias[n] : 0.f;
+  const int cn = p.map_c > 0 ? (n % p.map_c) * p.map_hw + n / p.map_c : n;
+  if (p.c_bf16) {
+    reinterpret_cast<bf16*>(p.C)[(size_t)m * p.ldc + cn] = f2bf(p.alpha * acc + bv);
+  } else {
+    float* c = reinterpret_cast<float*>(p.C) + (size_t)m * p.ldc + cn;
+    float v = p.alpha * acc + bv;
+    if (p.beta != 0.f) v += p.beta * *c;
+    *c = v;
+  }
+}
 
 // LDS bytes of one tile body: double-buffered A and B k-tiles
 template <int MODE, int BM, int BN>
@@ -279,7 +402,7 @@ struct GemmLds {
 
 // One BM x BN output tile (tile column tn, tile row tm) over the k-chunk tz of problem p, staged
 // through the LDS block `smem` (GemmLds bytes).
-template <int MODE, int BM, int BN, int LA, int LB>
+template <int MODE, int BM, int BN, int LA, int LB, typename SA = float, typename SB = float>
 __device__ __forceinline__ void gemm_tile(const GemmArgs& p, int tn, int tm, int tz, char* smem) {
   typedef typename GemmT<MODE>::T T;
   constexpr int LDK = GemmT<MODE>::LDK;
@@ -287,8 +410,8 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& p, int tn, int tm, int
   T (*As)[BM * LDK] = reinterpret_cast<T (*)[BM * LDK]>(smem);
   T (*Bs)[BN * LDK] = reinterpret_cast<T (*)[BN * LDK]>(smem + 2 * BM * LDK * sizeof(T));
   const int M = p.M, N = p.N, K = p.K;
-  const float* __restrict__ A = p.A;
-  const float* __restrict__ B = p.B;
+  const SA* __restrict__ A = static_cast<const SA*>(p.A);
+  const SB* __restrict__ B = static_cast<const SB*>(p.B);
   const long long sam = p.sam, sak = p.sak, sbk = p.sbk, sbn = p.sbn;
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
@@ -303,20 +426,20 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& p, int tn, int tm, int
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  TileRegs<BM> ta;
-  TileRegs<BN> tb;
+  Stage<MODE, BM, LA, SA> ta;
+  Stage<MODE, BN, LB, SB> tb;
   const int nk = (kend - kbeg + 31) / 32;
-  load_tile<BM, LA>(A, sam, sak, m0, kbeg, M, kend, ta);
-  load_tile<BN, LB>(B, sbn, sbk, n0, kbeg, N, kend, tb);   // B^T tile: rows = n
-  store_tile<MODE, BM, LA>(ta, sam, sak, As[0]);
-  store_tile<MODE, BN, LB>(tb, sbn, sbk, Bs[0]);
+  ta.load(A, sam, sak, m0, kbeg, M, kend);
+  tb.load(B, sbn, sbk, n0, kbeg, N, kend);   // B^T tile: rows = n
+  ta.store(sam, sak, As[0]);
+  tb.store(sbn, sbk, Bs[0]);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) {
-      load_tile<BM, LA>(A, sam, sak, m0, kbeg + 32 * (kt + 1), M, kend, ta);
-      load_tile<BN, LB>(B, sbn, sbk, n0, kbeg + 32 * (kt + 1), N, kend, tb);
+      ta.load(A, sam, sak, m0, kbeg + 32 * (kt + 1), M, kend);
+      tb.load(B, sbn, sbk, n0, kbeg + 32 * (kt + 1), N, kend);
     }
     const T* as = As[cur] + (BM / 2 * wm + r16) * LDK;
     const T* bs = Bs[cur] + (BN / 2 * wn + r16) * LDK;
@@ -348,8 +471,8 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& p, int tn, int tm, int
       }
     }
     if (more) {
-      store_tile<MODE, BM, LA>(ta, sam, sak, As[cur ^ 1]);
-      store_tile<MODE, BN, LB>(tb, sbn, sbk, Bs[cur ^ 1]);
+      ta.store(sam, sak, As[cur ^ 1]);
+      tb.store(sbn, sbk, Bs[cur ^ 1]);
     }
     __syncthreads();
   }
@@ -360,27 +483,22 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& p, int tn, int tm, int
     for (int j = 0; j < TJ; ++j) {
       const int n = n0 + BN / 2 * wn + 16 * j + r16;
       if (n >= N) continue;
-      const float bv = (!part && p.bias) ? p.bias[n] : 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int m = m0 + BM / 2 * wm + 16 * i + 4 * g + e;
         if (m >= M) continue;
-        if (part) {
+        if (part)
           part[(size_t)m * N + n] = acc[i][j][e];
-        } else {
-          float* c = p.C + (size_t)m * p.ldc + n;
-          float v = p.alpha * acc[i][j][e] + bv;
-          if (p.beta != 0.f) v += p.beta * *c;
-          *c = v;
-        }
+        else
+          gemm_out(p, m, n, acc[i][j][e]);
       }
     }
 }
 
-template <int MODE, int BM, int BN, int LA, int LB>
+template <int MODE, int BM, int BN, int LA, int LB, typename SA = float, typename SB = float>
 __global__ __launch_bounds__(256) void gemm_mfma_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[GemmLds<MODE, BM, BN>::BYTES];
-  gemm_tile<MODE, BM, BN, LA, LB>(p, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+  gemm_tile<MODE, BM, BN, LA, LB, SA, SB>(p, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
 // The bias gradient db[o] = sum_r dout[r, o] of a Linear backward, riding on the launches the
@@ -426,7 +544,8 @@ __device__ __forceinline__ void db_final(const DbArgs& d, int b) {
 // both read dout): blocks [0, nb1) run problem 1 on its (n1 x m1 x z1) tile grid, the next nb2
 // problem 2, and the last (when d.db) the bias gradient's chunk partials.  One launch boundary
 // instead of three, and the small grids fill the chip together.
-template <int MODE, int BM1, int BN1, int LA1, int LB1, int BM2, int BN2, int LA2, int LB2>
+template <int MODE, int BM1, int BN1, int LA1, int LB1, int BM2, int BN2, int LA2, int LB2,
+          typename SB = float>
 __global__ __launch_bounds__(256) void gemm_pair_kernel(GemmArgs p1, int n1, int m1, GemmArgs p2,
                                                         int n2, int m2, DbArgs d) {
   constexpr int L1 = GemmLds<MODE, BM1, BN1>::BYTES, L2 = GemmLds<MODE, BM2, BN2>::BYTES;
@@ -435,10 +554,10 @@ __global__ __launch_bounds__(256) void gemm_pair_kernel(GemmArgs p1, int n1, int
   const int nb1 = n1 * m1 * (p1.ws ? avd_cdiv_d(p1.K, p1.kchunk) : 1);
   const int nb2 = n2 * m2 * (p2.ws ? avd_cdiv_d(p2.K, p2.kchunk) : 1);
   if (b < nb1) {
-    gemm_tile<MODE, BM1, BN1, LA1, LB1>(p1, b % n1, (b / n1) % m1, b / (n1 * m1), smem);
+    gemm_tile<MODE, BM1, BN1, LA1, LB1, float, SB>(p1, b % n1, (b / n1) % m1, b / (n1 * m1), smem);
   } else if (b < nb1 + nb2) {
     b -= nb1;
-    gemm_tile<MODE, BM2, BN2, LA2, LB2>(p2, b % n2, (b / n2) % m2, b / (n2 * m2), smem);
+    gemm_tile<MODE, BM2, BN2, LA2, LB2, float, SB>(p2, b % n2, (b / n2) % m2, b / (n2 * m2), smem);
   } else {
     db_partial(d, b - nb1 - nb2);
   }
@@ -448,25 +567,13 @@ __global__ __launch_bounds__(256) void gemm_pair_kernel(GemmArgs p1, int n1, int
 // the launch carries a bias gradient) fold its chunk partials instead.  A thread owns 4
 // consecutive outputs (16-byte partial loads when N % 4 == 0) and keeps 4 splits' loads in
 // flight; each output's sum still runs z = 0, 1, ... in order (bit-identical to one at a time).
-__device__ __forceinline__ void splitk_out(float* __restrict__ C, long long ldc,
-                                           const float* __restrict__ bias, float alpha,
-                                           float beta, int m, int n, float s) {
-  float* c = C + (size_t)m * ldc + n;
-  float v = alpha * s + (bias ? bias[n] : 0.f);
-  if (beta != 0.f) v += beta * *c;
-  *c = v;
-}
-
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S,
-                                                            int M, int N, float* __restrict__ C,
-                                                            long long ldc,
-                                                            const float* __restrict__ bias,
-                                                            float alpha, float beta, int nmain,
-                                                            DbArgs d) {
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, int S, int nmain, DbArgs d) {
   if ((int)blockIdx.x >= nmain) {
     db_final(d, (int)blockIdx.x - nmain);
     return;
   }
+  const float* __restrict__ ws = a.ws;
+  const int M = a.M, N = a.N;
   const long long MN = (long long)M * N;
   if ((N & 3) == 0 && (reinterpret_cast<uintptr_t>(ws) & 15) == 0) {
     for (long long i = 4 * (blockIdx.x * 256ll + threadIdx.x); i < MN; i += 4ll * nmain * 256) {
@@ -482,7 +589,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       for (; z < S; ++z) s += *reinterpret_cast<const f4*>(ws + (size_t)z * MN + i);
       const int m = (int)(i / N), n = (int)(i % N);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) splitk_out(C, ldc, bias, alpha, beta, m, n + e, s[e]);
+      for (int e = 0; e < 4; ++e) gemm_out(a, m, n + e, s[e]);
     }
     return;
   }
@@ -497,7 +604,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       for (int u = 0; u < 4; ++u) s += v[u];
     }
     for (; z < S; ++z) s += ws[(size_t)z * MN + i];
-    splitk_out(C, ldc, bias, alpha, beta, (int)(i / N), (int)(i % N), s);
+    gemm_out(a, (int)(i / N), (int)(i % N), s);
   }
 }
 
@@ -548,11 +655,12 @@ Plan plan_for(int M, int N, int K) {
   return p;
 }
 
-GemmArgs make_args(const Plan& pl, int M, int N, int K, const float* A, long long sam,
-                   long long sak, const float* B, long long sbk, long long sbn, float* C,
-                   long long ldc, const float* bias, float alpha, float beta, float* ws) {
+GemmArgs make_args(const Plan& pl, int M, int N, int K, const void* A, long long sam,
+                   long long sak, const void* B, long long sbk, long long sbn, void* C,
+                   long long ldc, const float* bias, float alpha, float beta, float* ws,
+                   int c_bf16 = 0, int map_c = 0, int map_hw = 0) {
   return GemmArgs{M, N, K, pl.kchunk, A, sam, sak, B, sbk, sbn, C, ldc, bias, alpha, beta,
-                  pl.splits > 1 ? ws : nullptr};
+                  pl.splits > 1 ? ws : nullptr, c_bf16, map_c, map_hw};
 }
 
 __global__ __launch_bounds__(256) void db_final_kernel(DbArgs d) { db_final(d, (int)blockIdx.x); }
@@ -565,18 +673,17 @@ void launch_splitk_reduce(const Plan& pl, const GemmArgs& a, hipStream_t st, con
     const long long MN = (long long)a.M * a.N;
     const int per = (a.N & 3) == 0 ? 4 : 1;     // outputs per thread (the kernel's vector path)
     const int blocks = (int)std::min<long long>(avd_cdiv(avd_cdiv(MN, per), 256), 4096);
-    splitk_reduce_kernel<<<blocks + nd, 256, 0, st>>>(a.ws, pl.splits, a.M, a.N, a.C, a.ldc, a.bias,
-                                                      a.alpha, a.beta, blocks, d ? *d : DbArgs{});
+    splitk_reduce_kernel<<<blocks + nd, 256, 0, st>>>(a, pl.splits, blocks, d ? *d : DbArgs{});
   } else if (nd) {
     db_final_kernel<<<nd, 256, 0, st>>>(*d);
   }
 }
 
-template <int MODE, int LA, int LB>
+template <int MODE, int LA, int LB, typename SA = float, typename SB = float>
 void launch_gemm(const Plan& pl, const GemmArgs& a, hipStream_t st) {
   dim3 grid(avd_cdiv(a.N, pl.bn), avd_cdiv(a.M, pl.bm), pl.splits);
 #define AVD_G(BM_, BN_)                                                                        \
-  if (pl.bm == BM_ && pl.bn == BN_) gemm_mfma_kernel<MODE, BM_, BN_, LA, LB><<<grid, 256, 0, st>>>(a);
+  if (pl.bm == BM_ && pl.bn == BN_) gemm_mfma_kernel<MODE, BM_, BN_, LA, LB, SA, SB><<<grid, 256, 0, st>>>(a);
   AVD_G(128, 256) else AVD_G(128, 128) else AVD_G(128, 64) else AVD_G(64, 64)
 #undef AVD_G
   launch_splitk_reduce(pl, a, st);
@@ -599,7 +706,7 @@ void dispatch_gemm(const Plan& pl, int lA, int lB, const GemmArgs& a, hipStream_
 // rows contiguous), problem 2 = dX [rows, In] = dout W (A k-contiguous, B rows contiguous).
 // Tile plans served: dW 128x128 (every weight-gradient plan of the step), dX any of 128x128,
 // 128x64, 64x64; anything else returns false and the caller launches the two GEMMs separately.
-template <int MODE>
+template <int MODE, typename SB = float>
 bool launch_pair(const Plan& p1, const GemmArgs& a1, const Plan& p2, const GemmArgs& a2,
                  const DbArgs& d, hipStream_t st) {
   if (p1.bm != 128 || p1.bn != 128) return false;
@@ -608,7 +715,7 @@ bool launch_pair(const Plan& p1, const GemmArgs& a1, const Plan& p2, const GemmA
   const int blocks = n1 * m1 * p1.splits + n2 * m2 * p2.splits + (d.db ? d.nrc * d.strips : 0);
 #define AVD_P(BM2_, BN2_)                                                                      \
   if (p2.bm == BM2_ && p2.bn == BN2_) {                                                        \
-    gemm_pair_kernel<MODE, 128, 128, LAY_R, LAY_R, BM2_, BN2_, LAY_K, LAY_R>                   \
+    gemm_pair_kernel<MODE, 128, 128, LAY_R, LAY_R, BM2_, BN2_, LAY_K, LAY_R, SB>               \
         <<<blocks, 256, 0, st>>>(a1, n1, m1, a2, n2, m2, d);                                   \
   }
   AVD_P(128, 128) else AVD_P(128, 64) else AVD_P(64, 64) else return false;
@@ -633,6 +740,25 @@ DbArgs db_args(const float* dout, long long ld, int rows, int O, float* part, fl
 long long db_ws_elems(int rows, int O) {
   const int chunk = std::max(1, avd_cdiv(rows, 128));
   return (long long)avd_cdiv(rows, chunk) * O;
+}
+
+// The encoder Linear's weight with its columns in the NHWC (h, w, c) order of the bf16 features:
+// Wp[o][hw * C + c] = bf16(W[o][c * HW + hw]); up to HWCB_MAX weights per launch (blockIdx.y).
+constexpr int HWCB_MAX = 4;
+struct HwcBatch {
+  const float* w[HWCB_MAX];
+  bf16* wp[HWCB_MAX];
+  int O[HWCB_MAX], C[HWCB_MAX], HW[HWCB_MAX];
+};
+
+__global__ __launch_bounds__(256) void weight_hwc_kernel(HwcBatch b) {
+  const int e = blockIdx.y;
+  const int C = b.C[e], HW = b.HW[e], In = C * HW;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)b.O[e] * In) return;
+  const int o = (int)(i / In), j = (int)(i - (long long)o * In);    // j = hw * C + c
+  const int hw = j / C, c = j - hw * C;
+  b.wp[e][i] = f2bf(b.w[e][(size_t)o * In + (size_t)c * HW + hw]);
 }
 
 }  // namespace
@@ -685,6 +811,84 @@ int avd_linear_bwd(int rows, int O, int In, const float* dout, long long dout_ld
       dispatch_gemm<2>(p1, l1a, l1b, a1, st);
       dispatch_gemm<2>(p2, l2a, l2b, a2, st);
     }
+  }
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+// ---- encoder Linear over NHWC bf16 features (include/avdino.h "encoder Linear, NHWC features")
+long long avd_linear_hwc_ws_elems(int rows, int O, int In) {
+  if (rows <= 0 || O <= 0 || In <= 0) return 0;
+  const Plan pf = plan_for(rows, O, In), p1 = plan_for(O, In, rows), p2 = plan_for(rows, In, O);
+  const long long wf = pf.splits > 1 ? (long long)pf.splits * rows * O : 0;
+  const long long wb = (p1.splits > 1 ? (long long)p1.splits * O * In : 0) +
+                       (p2.splits > 1 ? (long long)p2.splits * rows * In : 0) + db_ws_elems(rows, O);
+  return std::max(wf, wb);
+}
+
+int avd_linear_weight_hwc(int n, const float* const* W, void* const* Wp, const int* O, const int* C,
+                          const int* HW, void* stream) {
+  if (n <= 0 || n > HWCB_MAX || !W || !Wp || !O || !C || !HW) return AVD_ERR_ARG;
+  HwcBatch b{};
+  int most = 1;
+  for (int e = 0; e < n; ++e) {
+    if (!W[e] || !Wp[e]) return AVD_ERR_ARG;
+    if (O[e] <= 0 || C[e] <= 0 || HW[e] <= 0) return AVD_ERR_SHAPE;
+    b.w[e] = W[e]; b.wp[e] = (bf16*)Wp[e]; b.O[e] = O[e]; b.C[e] = C[e]; b.HW[e] = HW[e];
+    most = std::max(most, O[e] * C[e] * HW[e]);
+  }
+  weight_hwc_kernel<<<dim3(avd_cdiv(most, 256), n), 256, 0, avd_stream(stream)>>>(b);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_linear_fwd_hwc(int rows, int O, int C, int HW, const void* feat, const void* Wp,
+                       const float* bias, float* out, long long out_ld, float* ws,
+                       long long ws_elems, void* stream) {
+  if (!feat || !Wp || !out) return AVD_ERR_ARG;
+  const int In = C * HW;
+  if (rows <= 0 || O <= 0 || C <= 0 || HW <= 0 || out_ld < O || In % 8) return AVD_ERR_SHAPE;
+  if ((reinterpret_cast<uintptr_t>(feat) & 15) || (reinterpret_cast<uintptr_t>(Wp) & 15)) return AVD_ERR_ARG;
+  Plan pl = plan_for(rows, O, In);
+  if (pl.splits > 1 && (!ws || ws_elems < (long long)pl.splits * rows * O)) { pl.splits = 1; pl.kchunk = In; }
+  // out[r, o] = sum_i feat[r, i] Wp[o, i]: A = feat (k contiguous), B^T rows = Wp rows
+  const GemmArgs a = make_args(pl, rows, O, In, feat, In, 1, Wp, 1, In, out, out_ld, bias, 1.f, 0.f, ws);
+  launch_gemm<2, LAY_K, LAY_K, bf16, bf16>(pl, a, avd_stream(stream));
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_linear_bwd_hwc(int rows, int O, int C, int HW, const float* dout, long long dout_ld,
+                       const void* feat, const void* Wp, float* dW, float* db, void* dX,
+                       float* ws, long long ws_elems, void* stream) {
+  if (!dout || !feat || !Wp || !dW || !dX) return AVD_ERR_ARG;
+  const int In = C * HW;
+  if (rows <= 0 || O <= 0 || C <= 0 || HW <= 0 || dout_ld < O || In % 8 || O % 4 || dout_ld % 4)
+    return AVD_ERR_SHAPE;
+  if ((reinterpret_cast<uintptr_t>(dout) & 15) || (reinterpret_cast<uintptr_t>(feat) & 15) ||
+      (reinterpret_cast<uintptr_t>(Wp) & 15))
+    return AVD_ERR_ARG;
+  hipStream_t st = avd_stream(stream);
+  Plan p1 = plan_for(O, In, rows), p2 = plan_for(rows, In, O);
+  const long long w1 = p1.splits > 1 ? (long long)p1.splits * O * In : 0;
+  const long long w2 = p2.splits > 1 ? (long long)p2.splits * rows * In : 0;
+  const long long w3 = db_ws_elems(rows, O);
+  if (!ws || ws_elems < w1 + w2 + w3) return AVD_ERR_ARG;
+  const DbArgs d = db_args(dout, dout_ld, rows, O, db ? ws + w1 + w2 : nullptr, db);
+  // dW[o, (c,h,w)] = sum_r dout[r, o] feat[r, (h,w,c)]: the column map scatters the hwc index
+  const GemmArgs a1 = make_args(p1, O, In, rows, dout, 1, dout_ld, feat, In, 1, dW, In, nullptr,
+                                1.f, 0.f, ws, 0, C, HW);
+  // dX[r, (h,w,c)] = sum_o dout[r, o] Wp[o, (h,w,c)], stored bf16 NHWC
+  const GemmArgs a2 = make_args(p2, rows, In, O, dout, dout_ld, 1, Wp, In, 1, dX, In, nullptr,
+                                1.f, 0.f, p1.splits > 1 ? ws + w1 : ws, 1);
+  if (!launch_pair<2, bf16>(p1, a1, p2, a2, d, st)) {
+    // shapes the paired launch does not serve (few rows: no 128x128 weight-gradient plan)
+    if (db) {
+      db_partial_kernel<<<d.nrc * d.strips, 256, 0, st>>>(d);
+      db_final_kernel<<<avd_cdiv(O, 256), 256, 0, st>>>(d);
+    }
+    launch_gemm<2, LAY_R, LAY_R, float, bf16>(p1, a1, st);
+    launch_gemm<2, LAY_K, LAY_R, float, bf16>(p2, a2, st);
   }
   AVD_CHECK_LAUNCH();
   return AVD_OK;

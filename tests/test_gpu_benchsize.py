@@ -434,20 +434,25 @@ def _ref_grads(state, batch, E, D, P, autocast_dtype):
                          if p.grad is not None}
 
 
-@pytest.mark.parametrize("B,L", [(1024, 4), (512, 7)], ids=["config2", "B512_L7"])
+@pytest.mark.parametrize("B,L", [(1024, 4), (512, 7), (256, 7)], ids=["config2", "B512_L7", "B256_L7"])
 def test_bf16_step_vs_fp32_step_config2(capsys, B, L):
     """The benchmarked bf16 step at config-2 size (B = 1024, 2 global + 4 local views, mse,
-    E = D = 256, P = 128) against the fp32 engine from identical parameters and inputs, with
-    per-tensor bounds taken from the REFERENCE's own mixed precision: the same step in the
-    reference's ops (torch_port) under bf16 autocast vs fp32, on the GPU.  At initialisation
-    the conv-weight / BN gradients are small sums of large cancelling terms, so one bf16
-    rounding of the stored maps moves them by ~10 % -- in the reference's recipe as in ours.
-    Bounds: loss 1e-3 relative; every tensor within 2x the reference's own mixed-precision error
-    (the larger of its bf16-autocast and its fp16 '16-mixed' error, floor 1e-2: on an 8-value BN
-    tensor either one alone can sit far below the other by chance -- B = 256 / L = 7 gave the
-    audio bn1 weight 0.065 under bf16 and 0.448 under fp16, ours 0.335); the median within 1.25x
-    of the bf16-autocast median.  The B512_L7 case runs the student conv branches at 10 BN
-    groups (2 global + 7 local views + the originals)."""
+    E = D = 256, P = 128: conv_ws / wgrad_ws mid layers, the Gram / routed / window-space conv1
+    passes) against the ORACLE: the reference's step restated in torch ops (oracle/torch_port.py,
+    pinned to the reference's own fixtures by tests/test_torch_port.py) in fp32 on the GPU, from
+    identical parameters and inputs -- no HIP-vs-HIP link.  Per-tensor bounds come
+    from the REFERENCE's own mixed precision: the same port under bf16 / fp16 autocast vs fp32.
+    At initialisation the conv-weight / BN gradients are small sums of large cancelling terms,
+    so one bf16 rounding of the stored maps moves them by ~10 % -- in the reference's recipe as
+    in ours.  Bounds: loss 1e-3 relative; every tensor within 2x the reference's own
+    mixed-precision error (the larger of its bf16-autocast and its fp16 '16-mixed' error, floor
+    1e-2: on an 8-value BN tensor either one alone can sit far below the other by chance); the
+    median within 1.25x of the bf16-autocast median.  The fp32 engine is checked against the same
+    oracle (loss 1e-4; every tensor within half the reference's own autocast error, floor 5e-3
+    rel-L2: bias gradients are sums over 6144-7168 rows that cancel, so fp32 summation order alone
+    moves them by up to 4e-3 -- measured).  B512_L7 / B256_L7 run the student conv
+    branches at 10 BN groups (2 global + 7 local views + the originals); B256_L7 is the case that
+    failed the bf16-only bound in round 3 (audio bn1 weight)."""
     from avdino.engine import Hyper, MultiCentralEngine
     from avdino.params import ParamStore
     from avdino.spec import multimodal_dino_sd
@@ -475,9 +480,11 @@ def test_bf16_step_vs_fp32_step_config2(capsys, B, L):
     ref = {n: _ref_grads(state, batch, E, D, P, a) for n, a in
            (("f32", None), ("bf16", torch.bfloat16), ("f16", torch.float16))}
     (l32, g32), (l16, g16) = out["f32"], out["bf16"]
-    big = max(v.norm().item() for v in g32.values())
-    keys = [k for k in g32 if g32[k].norm().item() > 1e-6 * big]
-    ours = {k: grel(g16[k], g32[k]) for k in keys}
+    r32 = ref["f32"][1]
+    big = max(v.norm().item() for v in r32.values())
+    keys = [k for k in g32 if r32[k].norm().item() > 1e-6 * big]
+    ours = {k: grel(g16[k], r32[k]) for k in keys}          # bf16 engine vs the fp32 oracle
+    e32 = {k: grel(g32[k], r32[k]) for k in keys}           # fp32 engine vs the fp32 oracle
     rbf = {k: grel(ref["bf16"][1][k], ref["f32"][1][k]) for k in keys}
     rfp = {k: grel(ref["f16"][1][k], ref["f32"][1][k]) for k in keys}
     ratio = sorted(((ours[k] / max(rbf[k], rfp[k], 1e-2), k) for k in keys), reverse=True)
@@ -491,10 +498,73 @@ def test_bf16_step_vs_fp32_step_config2(capsys, B, L):
               f"reference fp16-autocast {med[2]:.3e}")
         for r, k in ratio[:8]:
             print(f"  {k}: ours {ours[k]:.3e} ref-bf16 {rbf[k]:.3e} ref-fp16 {rfp[k]:.3e}")
+        print(f"fp32 engine vs fp32 oracle: worst rel-L2 {max(e32.values()):.2e}")
     assert abs(l32 - ref["f32"][0]) < 1e-4
-    assert abs(l16 - l32) / abs(l32) < 1e-3
+    bad32 = [(k, e32[k]) for k in keys if e32[k] > max(0.5 * max(rbf[k], rfp[k]), 5e-3)]
+    assert not bad32, bad32
+    assert abs(l16 - ref["f32"][0]) / abs(ref["f32"][0]) < 1e-3
     assert ratio[0][0] < 2.0, ratio[:4]
     assert med[0] < 1.25 * med[1], med
+
+
+def _ref_curve(state, batches, E, D, P, autocast_dtype):
+    """Losses of len(batches) full reference training steps (torch_port.train_step: forward,
+    loss, update_teacher, backward, Adam -- dino.py:1214-1238 with Lightning's automatic
+    optimisation), fp32 or under autocast, on the GPU."""
+    from oracle import torch_port as TP
+    torch.manual_seed(0)
+    m = TP.DinoMSE(E, D, P, dropout=0.0, fusion_dropout=0.0).cuda()
+    m.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state.items()}, strict=True)
+    opt = TP.make_optimizer(m)
+    out = []
+    for b in batches:
+        with torch.autocast("cuda", dtype=autocast_dtype or torch.float32, enabled=autocast_dtype is not None):
+            fi, fa, s_, t_ = m(b["image"], b["audio"], b["g_img"], b["g_aud"], b["l_img"], b["l_aud"])
+            loss = TP.dino_loss(s_.float(), t_.float()) + TP.mse_loss(fi.float(), fa.float())
+        m.update_teacher()
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        out.append(loss.item())
+    return np.array(out)
+
+
+def test_bf16_three_step_loss_curve_config2(capsys):
+    """Three full bf16 training steps of the benchmarked engine at config-2 size (B = 1024,
+    2 + 4 views, mse, E = D = 256, P = 128; Adam, teacher EMA, centre update between steps)
+    against the reference's own steps restated in torch ops (torch_port, the pinned oracle) in
+    fp32 and under bf16 / fp16 autocast, from the same state over the same batches.  Band: every
+    step's loss within max(2x the reference's own autocast deviation from fp32, 2e-4 relative)
+    of the fp32 reference."""
+    from avdino.engine import Hyper, MultiCentralEngine
+    from avdino.params import ParamStore
+    from avdino.spec import multimodal_dino_sd
+    from oracle.params import make_state
+    from oracle import spec as OS
+    E = D = 256
+    P, G, L, B = 128, 2, 4, 1024
+    state = make_state(OS.multimodal_dino_spec("mse", E, D, P), 311)
+    g = torch.Generator(device="cuda").manual_seed(312)
+
+    def px(*s):
+        return torch.randint(0, 256, s, generator=g, device="cuda", dtype=torch.int32).float() / 255
+
+    batches = [dict(g_img=px(B, G, 1, 28, 28), g_aud=px(B, G, 1, 112, 112), l_img=px(B, L, 1, 28, 28),
+                    l_aud=px(B, L, 1, 112, 112), image=px(B, 1, 28, 28), audio=px(B, 1, 112, 112))
+               for _ in range(3)]
+    store = ParamStore(multimodal_dino_sd("mse", E, D, P), "cuda")
+    store.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state.items()})
+    eng = MultiCentralEngine(store, "mse", E, D, P, Hyper(dropout=0.0, fusion_dropout=0.0),
+                             act_dtype=torch.bfloat16)
+    ours = np.array([eng.step(b).item() for b in batches])
+    r32 = _ref_curve(state, batches, E, D, P, None)
+    rbf = _ref_curve(state, batches, E, D, P, torch.bfloat16)
+    rfp = _ref_curve(state, batches, E, D, P, torch.float16)
+    band = np.maximum(2 * np.maximum(np.abs(rbf - r32), np.abs(rfp - r32)), 2e-4 * np.abs(r32))
+    with capsys.disabled():
+        print(f"\nconfig-2 bf16 3-step curve: ours {ours}, reference fp32 {r32}, bf16-autocast {rbf}, "
+              f"fp16-autocast {rfp}; |ours - fp32| {np.abs(ours - r32)} band {band}")
+    assert np.all(np.abs(ours - r32) <= band), (ours, r32, band)
 
 
 def test_simclr_conv1_bwd_apply_wgrad_bench_size(ops):

@@ -429,3 +429,42 @@ def test_sum_rows_vs_float64(ops, rows, cols, off, acc):
     assert torch.equal(outs[0], outs[1])
     err = (outs[0].double() - ref).abs().max().item()
     assert err <= 2e-7 * max(ref.abs().max().item(), 1.0), err
+
+
+@pytest.mark.parametrize("rows,O,C,HW", [(7168, 256, 64, 49), (7168, 256, 64, 25), (300, 256, 64, 49)])
+def test_linear_hwc_kernels_vs_float64(ops, rows, O, C, HW):
+    """The encoder Linear over NHWC bf16 features (avd_linear_*_hwc, the bf16 step's image /
+    audio Linear at config-2 size and a ragged row count): the weight copy equals torch's
+    permute + bf16 cast bit for bit; forward, dW (scattered back to the reference's (c, h, w)
+    columns), db and dX (bf16, NHWC) against float64 of the same bf16-rounded operands -- the
+    forward / dW / db differ only by fp32 accumulation order (rel-L2 1e-5), dX by its bf16
+    storage (4e-3)."""
+    g = torch.Generator(device="cuda").manual_seed(rows + HW)
+    In = C * HW
+    W = torch.randn(O, In, generator=g, device="cuda") / In ** 0.5
+    b = torch.randn(O, generator=g, device="cuda")
+    feat = torch.rand(rows, HW, C, generator=g, device="cuda").to(torch.bfloat16)     # NHWC
+    wp = torch.empty(O * In, device="cuda", dtype=torch.bfloat16)
+    ops.linear_weight_hwc([(W, wp, C, HW)])
+    ref_wp = W.view(O, C, HW).permute(0, 2, 1).reshape(O, In).to(torch.bfloat16)
+    torch.cuda.synchronize()
+    assert torch.equal(wp.view(O, In), ref_wp)
+    # the (c, h, w)-ordered features the reference's x.view(N, -1) sees
+    f_chw = feat.double().permute(0, 2, 1).reshape(rows, In)
+    Wd = W.to(torch.bfloat16).double()
+    out = torch.zeros(rows, 2 * O, device="cuda")
+    ops.linear_fwd_hwc(feat, wp, b, out, rows, O, C, HW, out_ld=2 * O, out_off=O)
+    ref = f_chw @ Wd.T + b.double()
+    assert out[:, :O].abs().max().item() == 0.0
+    assert rel(host(out[:, O:]), ref.cpu().numpy()) < 1e-5
+    dout_full = torch.randn(rows, 2 * O, generator=g, device="cuda")
+    dout = dout_full[:, O:]
+    dw = torch.empty(O, In, device="cuda")
+    db = torch.empty(O, device="cuda")
+    dx = torch.empty(rows, HW, C, device="cuda", dtype=torch.bfloat16)
+    ops.linear_bwd_hwc(dout_full, feat, wp, dw, db, dx, rows, O, C, HW, dout_ld=2 * O, dout_off=O)
+    dd = dout.to(torch.bfloat16).double()
+    assert rel(host(dw), (dd.T @ f_chw).cpu().numpy()) < 1e-5
+    assert rel(host(db), dout.double().sum(0).cpu().numpy()) < 1e-6
+    dx_ref = (dd @ Wd).view(rows, C, HW).permute(0, 2, 1)
+    assert rel(host(dx), dx_ref.cpu().numpy()) < 4e-3
