@@ -133,11 +133,13 @@ int avd_gemm(int M, int N, int K, const float* A, long long sam, long long sak,
  * split-K scratch (NULL: single passes over K).  db (nullable) = the bias gradient
  * sum_r dout[r, :], formed by extra blocks of the same launches (row-chunk partials in ws, then
  * a fixed-order fold in the split-K reduce launch): deterministic, no separate reduction
- * launches; needs ws (AVD_ERR_ARG without it). */
+ * launches; needs ws (AVD_ERR_ARG without it).  which: 3 = both gradients; 1 = dW (+ db) only,
+ * 2 = dX only (x / dW or W / dX may then be NULL) -- the step runs dX on its critical stream and
+ * dW beside it on another one (same results as which = 3). */
 long long avd_linear_bwd_ws_elems(int rows, int O, int In, int mode);
 int avd_linear_bwd(int rows, int O, int In, const float* dout, long long dout_ld, const float* x,
                    long long x_ld, const float* W, float* dW, float* dX, long long dx_ld, float* db,
-                   int mode, float* ws, long long ws_elems, void* stream);
+                   int mode, int which, float* ws, long long ws_elems, void* stream);
 
 /* The encoder Linear of CentralUnimodalImage / Audio (unimodal.py:153 fc: Linear(1600 / 3136, E)
  * over x.view(N, -1) of the last conv block's pooled map, dino.py:459-468) in the bf16 step, over
@@ -151,7 +153,7 @@ int avd_linear_bwd(int rows, int O, int In, const float* dout, long long dout_ld
  *   avd_linear_bwd_hwc: dW[o][(c,h,w)] = sum_r dout[r][o] feat[r][(h,w,c)] (f32, the reference's
  *     order), db[o] = sum_r dout[r][o] (nullable), dX[r][(h,w,c)] = sum_o dout[r][o] Wp[o][...]
  *     stored bf16 -- the last conv block's pooled gradient in NHWC (avd_cl_bn_bwd_* mode 0);
- *     one paired launch + its split-K reduces, as avd_linear_bwd.
+ *     one paired launch + its split-K reduces, as avd_linear_bwd (which: as there).
  * ws: avd_linear_hwc_ws_elems floats (required by the backward).  C*HW % 8 == 0, O % 4 == 0,
  * feat / Wp / dout 16-byte aligned. */
 long long avd_linear_hwc_ws_elems(int rows, int O, int In);
@@ -161,7 +163,7 @@ int avd_linear_fwd_hwc(int rows, int O, int C, int HW, const void* feat, const v
                        const float* bias, float* out, long long out_ld, float* ws,
                        long long ws_elems, void* stream);
 int avd_linear_bwd_hwc(int rows, int O, int C, int HW, const float* dout, long long dout_ld,
-                       const void* feat, const void* Wp, float* dW, float* db, void* dX,
+                       const void* feat, const void* Wp, float* dW, float* db, void* dX, int which,
                        float* ws, long long ws_elems, void* stream);
 
 /* ------------------------------------------------------------------ channels-last conv blocks

@@ -27,12 +27,12 @@ PROTOS = {
     "avd_bn_bwd_finalize": [P, I, I, I, L, P, P, P, P, P, P, P, I, P],
     "avd_gemm": [I, I, I, P, L, L, P, L, L, P, L, P, F, F, I, P, L, P],
     "avd_gemm_ws_elems": [I, I, I, I],
-    "avd_linear_bwd": [I, I, I, P, L, P, L, P, P, P, L, P, I, P, L, P],
+    "avd_linear_bwd": [I, I, I, P, L, P, L, P, P, P, L, P, I, I, P, L, P],
     "avd_linear_bwd_ws_elems": [I, I, I, I],
     "avd_linear_hwc_ws_elems": [I, I, I],
     "avd_linear_weight_hwc": [I, P, P, P, P, P, P],
     "avd_linear_fwd_hwc": [I, I, I, I, P, P, P, P, L, P, L, P],
-    "avd_linear_bwd_hwc": [I, I, I, I, P, L, P, P, P, P, P, P, L, P],
+    "avd_linear_bwd_hwc": [I, I, I, I, P, L, P, P, P, P, P, I, P, L, P],
     "avd_cl_weight_elems": [I, I, I, I],
     "avd_cl_weight_layout": [P, P, I, I, I, I, I, P],
     "avd_cl_weight_layout_batch": [I, P, P, P, P, P, P, I, P],

@@ -830,6 +830,7 @@ class MultiCentralEngine:
         if done is not None:
             torch.cuda.current_stream(self.store.device).wait_event(done)
 
+
     # -------------------------------------------------------------- pieces
     def _encoder_fwd(self, prefix, ib, ab, x_img, x_aud, N, G, tag, need_dgrad, update_running=True,
                      ws=None):
@@ -1173,6 +1174,9 @@ class MultiCentralEngine:
             yield from hi.backward_steps(hws, st, ci, dzi, dcat, dx_ld=2 * E, dx_off=off)
             yield from ha.backward_steps(hws, st, ca, dza, dcat, dx_ld=2 * E, dx_off=off + E)
 
+        # (the main chain's Linear weight gradients beside it on the weight-gradient stream, the
+        # chain running the input gradients only: measured no faster, round 5 -- bwd.main_heads
+        # 246.9 vs 245.2 us, and the conv weight gradients queued behind them start later)
         def main_steps():
             dfout = ws.get("dfout", V * B * D)
             yield from self.sproj.backward_steps(ws, st, c["spc"], c["ds"], dfout)

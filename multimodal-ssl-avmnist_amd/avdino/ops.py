@@ -256,11 +256,15 @@ PAIR_BWD = True
 
 def linear_bwd(dout, x, w, dw, db, dx, rows, dout_ld=None, dout_off=0, x_ld=None, x_off=0,
                dx_ld=None, dx_off=0, mode=GEMM_F32_MFMA):
-    """dW = dout^T x ; db = sum_rows dout ; dx = dout W  (dx optional)."""
+    """dW = dout^T x ; db = sum_rows dout ; dx = dout W  (dx or dw optional)."""
     O, In = w.shape
     dout_ld = O if dout_ld is None else dout_ld
     x_ld = In if x_ld is None else x_ld
     dx_ld = In if dx_ld is None else dx_ld
+    if dw is None:                  # the input gradient alone
+        _need(dx is not None, "linear_bwd: nothing to compute")
+        gemm(rows, In, O, dout, dout_ld, 1, w, In, 1, dx, dx_ld, a_off=dout_off, c_off=dx_off, mode=mode)
+        return
     if dx is not None and mode in (GEMM_F32_MFMA, GEMM_BF16_MFMA) and PAIR_BWD:
         # dW, dX and the bias gradient on the same launches (avd_linear_bwd)
         for t in (dout, x, w, dw, dx):
@@ -276,7 +280,22 @@ def linear_bwd(dout, x, w, dw, db, dx, rows, dout_ld=None, dout_off=0, x_ld=None
                4 * (2 * rows * O + rows * In + O * In + O * In + rows * In), 4 * rows * O * In,
                lambda: call("avd_linear_bwd", rows, O, In, dout.data_ptr() + 4 * dout_off, dout_ld,
                             x.data_ptr() + 4 * x_off, x_ld, p(w), p(dw),
-                            dx.data_ptr() + 4 * dx_off, dx_ld, p(db), mode, p(ws), nws, stream()))
+                            dx.data_ptr() + 4 * dx_off, dx_ld, p(db), mode, 3, p(ws), nws, stream()))
+        return
+    if dx is None and mode in (GEMM_F32_MFMA, GEMM_BF16_MFMA) and PAIR_BWD:
+        # the weight gradient alone (+ db) on the paired launch's dW grid and its reduce
+        for t in (dout, x, dw):
+            _need(t.dtype == torch.float32 and t.is_contiguous(), "linear_bwd operands are contiguous f32")
+        _need(dout_off + (rows - 1) * dout_ld + O <= dout.numel(), "linear_bwd dout bounds")
+        _need(x_off + (rows - 1) * x_ld + In <= x.numel(), "linear_bwd x bounds")
+        _need(dw.numel() >= O * In and (db is None or db.numel() >= O), "linear_bwd dw / db size")
+        nws = lib.avd_linear_bwd_ws_elems(rows, O, In, mode)
+        ws = _gemm_workspace(dout.device, nws)
+        _timed(f"linear_bwd_dw[{rows}x{O}x{In} m{mode}]", 4 * (rows * O + rows * In + O * In),
+               2 * rows * O * In,
+               lambda: call("avd_linear_bwd", rows, O, In, dout.data_ptr() + 4 * dout_off, dout_ld,
+                            x.data_ptr() + 4 * x_off, x_ld, None, p(dw), None, In, p(db), mode, 1,
+                            p(ws), nws, stream()))
         return
     # dW[o, i] = sum_r dout[r, o] x[r, i]: A = dout^T (M=O, K=rows), B = x (K=rows, N=In)
     gemm(O, In, rows, dout, 1, dout_ld, x, x_ld, 1, dw, In, a_off=dout_off, b_off=x_off, mode=mode)
@@ -321,9 +340,10 @@ def linear_fwd_hwc(feat, wp, b, out, rows, O, C, HW, out_ld=None, out_off=0):
                         out.data_ptr() + 4 * out_off, out_ld, p(ws), nws, stream()))
 
 
-def linear_bwd_hwc(dout, feat, wp, dw, db, dx, rows, O, C, HW, dout_ld=None, dout_off=0):
+def linear_bwd_hwc(dout, feat, wp, dw, db, dx, rows, O, C, HW, dout_ld=None, dout_off=0, which=3):
     """dW (reference (c,h,w) columns) = dout^T feat_hwc; db = sum_rows dout; dx (bf16 NHWC) =
-    dout Wp -- one paired launch + split-K reduces (avd_linear_bwd_hwc)."""
+    dout Wp -- one paired launch + split-K reduces (avd_linear_bwd_hwc; which 1 / 2: dW + db /
+    dX alone)."""
     In = C * HW
     dout_ld = O if dout_ld is None else dout_ld
     _need(dout.dtype == torch.float32 and dout_off + (rows - 1) * dout_ld + O <= dout.numel(), "hwc bwd dout")
@@ -334,10 +354,12 @@ def linear_bwd_hwc(dout, feat, wp, dw, db, dx, rows, O, C, HW, dout_ld=None, dou
     _need(db is None or db.numel() >= O, "hwc bwd db")
     nws = lib.avd_linear_hwc_ws_elems(rows, O, In)
     ws = _gemm_workspace(dout.device, nws)
-    _timed(f"linear_bwd_hwc[{rows}x{O}x{In}]",
-           4 * 2 * rows * O + 2 * 2 * rows * In + 2 * O * In + 4 * O * In, 4 * rows * O * In,
+    part = {3: "", 2: "_dx", 1: "_dw"}[which]
+    nb = {3: 4 * 2 * rows * O + 2 * 2 * rows * In + 2 * O * In + 4 * O * In,
+          2: 4 * rows * O + 2 * rows * In + 2 * O * In, 1: 4 * rows * O + 2 * rows * In + 4 * O * In}[which]
+    _timed(f"linear_bwd_hwc{part}[{rows}x{O}x{In}]", nb, (4 if which == 3 else 2) * rows * O * In,
            lambda: call("avd_linear_bwd_hwc", rows, O, C, HW, dout.data_ptr() + 4 * dout_off, dout_ld,
-                        p(feat), p(wp), p(dw), p(db), p(dx), p(ws), nws, stream()))
+                        p(feat), p(wp), p(dw), p(db), p(dx), which, p(ws), nws, stream()))
 
 
 # ---------------------------------------------------------------- channels-last conv blocks

@@ -66,9 +66,7 @@ constexpr int NVEC = NXV + NGV + NCV, VPT = (NVEC + 255) / 256;
 // routing bits in registers -- no dz map, no scatter (the round-3 kernel's 16-way / 4-way LDS
 // bank conflicts).  Windows sit in slots hp * 16 + wp (wp 14, 15: zero padding, and their input
 // copies are zeroed so G6 sees no phantom windows); a k-step is 4 groups of 8 slots.
-#ifndef C1R5W_OCC
-#define C1R5W_OCC 3
-#endif
+constexpr int C1R5W_OCC = 3;                                  // blocks per CU
 constexpr int WSLOT = 16, NSLOT = HP * WSLOT;                 // 224 window slots per sample
 // input copies [parity][shift][P half][row][8 P]: B reads 0.67 extra cycles, copy writes 0
 // (tools/lds_conflicts.py)

@@ -39,15 +39,8 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
 // __device__ zero vector is otherwise a generic pointer, i.e. a flat_load, which also counts in
 // lgkmcnt: every later LDS wait would then wait for the (prefetch) loads to land as well.
 typedef __attribute__((ext_vector_type(4))) unsigned u4v;
-#ifndef AVD_LDG_FLAT
-#define AVD_LDG_FLAT 0   // 1: generic (flat) loads, for A/B builds (tools/build_ws_variants.sh)
-#endif
 __device__ __forceinline__ u4v ldg16(const void* p) {
-#if AVD_LDG_FLAT
-  return *(const u4v*)p;
-#else
   return *(const __attribute__((address_space(1))) u4v*)p;
-#endif
 }
 
 template <typename T> struct io;

@@ -217,9 +217,6 @@ __device__ const u4 kZeroC1 = {0u, 0u, 0u, 0u};
 // copy strides of 80 / 1648 / 5056 elements (160 / 3296 / 10112 B) spread the 16 taps of a
 // B-fragment read over distinct 16-byte bank windows: 13.1 instead of 52 LDS cycles per
 // pair of ds_read_b128 (tools/lds_bank_sim.py); 20.2 KB instead of 15.4 KB
-#ifndef C1B_DIAG
-#define C1B_DIAG 0   // diagnostic builds only (tools/build_ws_variants.sh SRC=conv_c1p MACRO=C1B_DIAG)
-#endif
 constexpr int XB_RS = 80, XB_CA = 1648, XB_CB = 5056;
 __device__ __forceinline__ int xbo(int b, int a, int r, int P) {
   return b * XB_CB + a * XB_CA + r * XB_RS + P;
@@ -340,11 +337,6 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
       const int w = tid + 256 * s;
       if (w >= nwin) continue;
       const int hp = w / Wp, wp = w - hp * Wp;
-#if C1B_DIAG & 1   // diagnostic: no window math (y copied as dy)
-      for (int k = 0; k < 4; ++k)
-        *reinterpret_cast<u4*>(&dys[((2 * hp + (k >> 1)) * WMAX + dys_px(2 * hp + (k >> 1), 2 * wp + (k & 1), segs)) * COUT]) = yv4[s][k] ^ gv[s];
-      continue;
-#endif
       float yv[4][COUT];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -394,7 +386,7 @@ __global__ __launch_bounds__(256) void c1p8_bwd_wgrad_kernel(
     // takes kb = 4 ks + gq for ks = w, w + 4, ... (kb advances by 16: its parity, i.e. the
     // dys half swap, is fixed per lane).  The next k-block's operands are read before the
     // current MFMAs issue.
-    const int nkb = (C1B_DIAG & 2) ? 0 : TH * segs;   // diagnostic 2: no MFMA
+    const int nkb = TH * segs;
     if (4 * wave < nkb) {
       typedef __attribute__((ext_vector_type(8))) short s8;
       const int q = col >> 2, pp = col & 3;
@@ -495,16 +487,6 @@ int avd_c1p8_bwd_apply_wgrad(const void* y, const void* gout, const float* scale
 namespace {
 
 enum { RC_STATS = 0, RC_APPLY = 1, RC_REDUCE = 2, RC_WGRAD = 3 };
-#ifndef C1A_MTU
-#define C1A_MTU 1    // apply pass: column tiles per MFMA-phase step (B reads, MFMAs, stores batched)
-#endif
-#ifndef C1A_DIAG
-#define C1A_DIAG 0   // diagnostic builds of the apply pass only (wrong results): 1 no z / code
-                     // stores, 2 no window epilogue, 4 no MFMA phase (tools/build_variants.sh)
-#endif
-#ifndef RC_PF
-#define RC_PF 1
-#endif
 
 __device__ __forceinline__ void unpack8(u4 v, float (&f)[8]) {
   const unsigned w[4] = {v.x, v.y, v.z, v.w};
@@ -598,7 +580,7 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
   }
   // register ring of PF tiles' input rows: tile i's loads are issued PF tiles ahead, so a
   // block keeps PF x 4.5 KB in flight instead of one tile's (the pass is load-latency bound)
-  constexpr int PF = PASS == RC_APPLY ? RC_PF : 1;
+  constexpr int PF = 1;
   u4 xv[PF][2];
   auto load_x = [&](int tl, u4 (&dst)[2]) {
     const int n = tl / tps, ty0 = (tl - n * tps) * TH;
@@ -630,11 +612,11 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
     __syncthreads();
     // ---- recompute y (rounded to bf16 exactly as the stored-y path)
     const unsigned* xd = reinterpret_cast<const unsigned*>(xs);
-    for (int s = wave; s < ((PASS == RC_APPLY && (C1A_DIAG & 4)) ? 0 : TH / 2); s += 4) {
+    for (int s = wave; s < TH / 2; s += 4) {
       // statistics pass: every column tile's B fragments first (their LDS reads in flight
       // together), then the MFMAs, then the epilogues (213 vs 224 us); the other passes keep
       // one tile at a time (the unrolled registers cost the apply pass an occupancy step)
-      constexpr int MTU = PASS == RC_STATS ? MTMAX : PASS == RC_APPLY ? C1A_MTU : 1;
+      constexpr int MTU = PASS == RC_STATS ? MTMAX : 1;
       for (int mt0 = 0; mt0 < mts; mt0 += MTU) {
       u4 bws[MTU];
 #pragma unroll
@@ -694,7 +676,7 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
         sc2[i] = f2{sc[2 * i], sc[2 * i + 1]};
         sf2[i] = f2{sf[2 * i], sf[2 * i + 1]};
       }
-      for (int w = tid; w < ((C1A_DIAG & 2) ? 0 : (TH / 2) * Wp); w += 256) {
+      for (int w = tid; w < (TH / 2) * Wp; w += 256) {
         const int hp = w / Wp, wp = w - hp * Wp;
         u4 yr[4];
 #pragma unroll
@@ -727,10 +709,6 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
           o[i] = pack_bf16x2(best[0], best[1]);
         }
         const size_t pw = ((size_t)n * Hp + (ty0 >> 1) + hp) * Wp + wp;
-        if (C1A_DIAG & 1) {
-          if (o[0] == 0x12345678u && code == 0x9abcdefu) z[0] = 0;   // keep the values live
-          continue;
-        }
         *reinterpret_cast<u4*>(z + pw * COUT) = u4{o[0], o[1], o[2], o[3]};
         if (codes) codes[pw] = code;
       }
@@ -911,9 +889,6 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
 //   out[((c * G + g) * R + r) * 2 + {0, 1}]                 BN sums of channel c
 //   out[C * G * R * 2 + (r * G + g) * MOM5 + ...]             M [8][25] | G [25][25] | S [25]
 constexpr int MOM5 = COUT * 25 + 25 * 25 + 25;
-#ifndef C1M_DIAG
-#define C1M_DIAG 0   // diagnostic builds only: 1 no window math, 2 no Gram MFMAs, 4 no y MFMA, 8 no k-loop
-#endif
 
 typedef __attribute__((ext_vector_type(2))) float f2;
 
@@ -1050,7 +1025,7 @@ __global__ __launch_bounds__(256, 2) void c1p8_moments_kernel(
     __syncthreads();
     // ---- y (bf16, as every other pass rounds it) into dys at the wgrad A-operand positions:
     // per 2-row strip every column tile's operands first, then the MFMAs, then the stores
-    if (!(C1M_DIAG & 4)) {
+    {
       const unsigned* xd = reinterpret_cast<const unsigned*>(xs);
       for (int s = wave; s < TH / 2; s += 4) {
         const int ry = 2 * s + rp;
@@ -1077,7 +1052,7 @@ __global__ __launch_bounds__(256, 2) void c1p8_moments_kernel(
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int w = tid + 256 * s;
-      if (w >= nwin || (C1M_DIAG & 1)) continue;
+      if (w >= nwin) continue;
       const int hp = w / Wp, wp = w - hp * Wp;
       int po[4];
       float yv[4][COUT];
@@ -1140,7 +1115,7 @@ __global__ __launch_bounds__(256, 2) void c1p8_moments_kernel(
     }
     __syncthreads();
     // ---- k-blocks of pixel pairs: D += dZ X (tap tiles 0, 1) and the Gram tiles (0,0) (0,1) (1,1)
-    const int nkb = (C1M_DIAG & 8) ? 0 : TH * segs;
+    const int nkb = TH * segs;
     if (4 * wave < nkb) {
       typedef __attribute__((ext_vector_type(8))) short s8;
       const int q = col >> 2, pp = col & 3;
@@ -1185,7 +1160,7 @@ __global__ __launch_bounds__(256, 2) void c1p8_moments_kernel(
         const bf16x8 X1 = __builtin_bit_cast(bf16x8, ones ? one4 : w1);
         acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, X0, acc[0], 0, 0, 0);
         acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, X1, acc[1], 0, 0, 0);
-        if (!(C1M_DIAG & 2)) {
+        {
           ga[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X0, X0, ga[0], 0, 0, 0);
           ga[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X0, X1, ga[1], 0, 0, 0);
           ga[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X1, X1, ga[2], 0, 0, 0);
@@ -1296,9 +1271,6 @@ __global__ void c1p8_combine_kernel(const float* __restrict__ m, const float* __
 //   M [8][25] | Gram [25][25] | S [25] | sum dz [8]
 constexpr int MOMC = COUT * 25 + 25 * 25 + 25 + COUT;
 
-#ifndef C1MC_DIAG
-#define C1MC_DIAG 0   // diagnostic builds only: 1 no input copies, 2 no dz map (wrong results)
-#endif
 
 // MM (what the pass accumulates): 0 = M, sum dz, Gram and S (the routed backward, MOMC floats
 // per row); 1 = Gram and S only (no pooled gradient: the FORWARD statistics pass -- y = w . x25 +
@@ -1383,7 +1355,7 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
         const unsigned lo = b ? od[0] : ev[0], hi = b ? od[1] : ev[1];
         const unsigned prev_hi = (unsigned)dpp_i<0x111>((int)hi);   // lane c-1 (0 at c = 0)
         const unsigned next_lo = (unsigned)dpp_i<0x101>((int)lo);   // lane c+1
-        if (r < TH + 4 && c < cpr && !(C1MC_DIAG & 1)) {
+        if (r < TH + 4 && c < cpr) {
           *reinterpret_cast<uint2*>(&xc[xbo(b, 0, r, 4 * c)]) =
               make_uint2((prev_hi >> 16) | (lo << 16), (lo >> 16) | (hi << 16));
           *reinterpret_cast<uint2*>(&xc[xbo(b, 1, r, 4 * c)]) = make_uint2(lo, hi);
@@ -1396,7 +1368,7 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int w = tid + 256 * s;
-      if (MM == 1 || w >= nwin || (C1MC_DIAG & 2)) continue;
+      if (MM == 1 || w >= nwin) continue;
       const int hp = w / Wp, wp = w - hp * Wp;
       const unsigned gw[4] = {gv[s].x, gv[s].y, gv[s].z, gv[s].w}, code = cv[s];
       unsigned ow[4][4];
@@ -1565,10 +1537,6 @@ __global__ __launch_bounds__(256, 3) void c1p8_moments_codes_kernel(
 // resolution dz map, and its LDS (29 KB) leaves room for 5 blocks per CU.
 constexpr int NWINMAX = (TH / 2) * (WMAX / 2);
 
-// 1: the window moments loop reads step j + 4's LDS operands before step j's MFMAs
-#ifndef C1W_PIPE
-#define C1W_PIPE 0
-#endif
 
 __global__ __launch_bounds__(256, 4) void c1p8_moments_win_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ gz, const unsigned* __restrict__ codes,
@@ -1702,25 +1670,9 @@ __global__ __launch_bounds__(256, 4) void c1p8_moments_win_kernel(
 #pragma unroll
       for (int u = 0; u < 3; ++u) bv[u] = *reinterpret_cast<const u4*>(&xc[(bs & bmask[u]) + boff[u]]);
     };
-#if C1W_PIPE
-    // software pipeline: step j + 4's operands are read before step j's masks and MFMAs
-    u4 na4, nr0, nr1, nbv[3];
-    if (wave < nstep) fetch(hpl, gi, na4, nr0, nr1, nbv);
-#endif
     for (int j = wave; j < nstep; j += 4) {
       u4 a4, r0, r1, bv[3];
-#if C1W_PIPE
-      a4 = na4; r0 = nr0; r1 = nr1;
-#pragma unroll
-      for (int u = 0; u < 3; ++u) bv[u] = nbv[u];
-      {
-        int h2 = hpl + dh, g2 = gi + dg;
-        if (g2 >= gpr) { g2 -= gpr; ++h2; }
-        if (j + 4 < nstep) fetch(h2, g2, na4, nr0, nr1, nbv);
-      }
-#else
       fetch(hpl, gi, a4, r0, r1, bv);
-#endif
       const unsigned av[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
       for (int t = 0; t < 2; ++t) {

@@ -406,9 +406,7 @@ __global__ void weight_layout_batch_kernel(WLBatch b) {
 // ----------------------------------------------------------------------------- host plan
 struct Plan { int TH, TW, NS, GPW, NB, tilesX, tiles; };
 // widest output-channel block that may use 7 pixel groups per wave (AGPR budget / occupancy)
-#ifndef GPW7_MAX_COUT
-#define GPW7_MAX_COUT 32
-#endif
+constexpr int GPW7_MAX_COUT = 32;
 
 // Tiling of an Ho x Wo output map into blocks of 64*GPW*NB pixels (GPW in {4, 7}; NB batches,
 // only when all input channels fit one LDS chunk).  Whole small maps are packed NS per block

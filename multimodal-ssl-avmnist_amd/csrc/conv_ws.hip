@@ -43,19 +43,7 @@ template <int CIN_, int COUT_, int K_, int PAD_, int H_, int W_, int TH_, int NS
           int NKW_, int GB_, int OCC_, int PF_ = 2>
 struct Ws {
   static constexpr int OCC = OCC_;                         // target waves per SIMD
-#ifndef WS_PF_ALL
-// B-read depth of every layer (with WS_SCHED pinning it): step A/B, 3 interleaved rounds, 6 vs
-// the per-layer table's 2 / 4: 5.35 vs 5.44 ms (5: 5.43, 8: 5.41).  The 56^2 / 28^2 forwards
-// drop to 2 resident blocks per CU (174 / 170 VGPRs) and are a little slower alone, but the step
-// (their grids beside the other stream's kernels) is faster.  The table below sets 6 per layer;
-// WS_PF_ALL > 0 overrides every layer (variant builds).
-#define WS_PF_ALL -1
-#endif
-#if WS_PF_ALL > 0
-  static constexpr int PF = WS_PF_ALL;
-#else
   static constexpr int PF = PF_;                           // k-steps of B reads in flight
-#endif
   static constexpr int CIN = CIN_, COUT = COUT_, K = K_, PAD = PAD_, H = H_, W = W_;
   static constexpr int HO = H + 2 * PAD - K + 1, WO = W + 2 * PAD - K + 1;
   static constexpr int TH = TH_, TW = WO, NS = NS_;
@@ -85,22 +73,11 @@ struct Ws {
 
 template <int V> using IC = std::integral_constant<int, V>;
 
-// 1: incremental pixel indices and packed-fp32 bias / statistics in the tile loop
-// (fewer VALU instructions per MFMA; same arithmetic, bit-identical maps and partials)
-#ifndef WS_LEAN
-#define WS_LEAN 1
-#endif
+// The tile loop advances pixel indices incrementally and forms bias / statistics on the packed
+// fp32 ALU (round 4: fewer VALU per MFMA, bit-identical); B-fragment reads are pinned PF k-steps
+// ahead of their MFMAs by sched_group_barrier (round 4: 188.9 k -> 191.7 k pairs/s).  Measured
+// and removed: two tiles' input loads in flight (two register sets; 172-173 k vs 190-191 k).
 typedef __attribute__((ext_vector_type(2))) float f2;
-
-// 1: B-fragment reads issued PF k-steps ahead of their MFMAs by sched_group_barrier
-#ifndef WS_SCHED
-#define WS_SCHED 1   // 188.9 k -> 191.7 k pairs/s; the 28^2 / 14^2 input gradients 8-10 % faster
-#endif
-
-// 1: two tiles' input loads in flight (two register sets) instead of one (AP = 0 launches)
-#ifndef WS_PF2
-#define WS_PF2 0
-#endif
 
 __device__ __forceinline__ f4 mma(bf16x8 a, bf16x8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -368,7 +345,6 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
     auto& ss = run_s;
     auto& sq = run_q;
 
-#if WS_LEAN
     // per-lane pixel (sample, row, column) of each of the GB groups: divided out once per tile,
     // then advanced by DP pixels per step (one carry each way), not re-divided per group
     constexpr int DP = L::NPW * L::GB * 16, DRY = DP / L::TW, DRX = DP % L::TW;
@@ -382,14 +358,12 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
       lry[b] = rem / L::TW;
       lrx[b] = rem - lry[b] * L::TW;
     }
-#endif
 #pragma unroll 1
     for (int i0 = 0; i0 < L::GW; i0 += L::GB) {
       int base[L::GB], opix[L::GB];
       bool gv[L::GB];
 #pragma unroll
       for (int b = 0; b < L::GB; ++b) {
-#if WS_LEAN
         const int p = lp[b], s = ls[b], ry = lry[b], rx = lrx[b];
         lp[b] += DP;
         lrx[b] += DRX;
@@ -398,11 +372,6 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
         if constexpr (L::NS > 1) {
           if (lry[b] >= L::TH) { lry[b] -= L::TH; ++ls[b]; }
         }
-#else
-        const int p = (wp + L::NPW * (i0 + b)) * 16 + r16;
-        const int s = p / (L::TH * L::TW), rem = p - s * (L::TH * L::TW);
-        const int ry = rem / L::TW, rx = rem - ry * L::TW;
-#endif
         gv[b] = i0 + b < L::GW && p < L::PIX;
         base[b] = gv[b] ? ((s * L::ITH + ry) * L::RS + rx) * L::PS : 0;
         opix[b] = ((n0 + s) * L::HO + ty0 + ry) * L::WO + rx;
@@ -450,7 +419,6 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
             for (int t = 0; t < L::NTW; ++t)
               acc[b][t] = mma(a[j][t], bq[j % (PF + 1)][b], acc[b][t]);
         }
-#if WS_SCHED
         // pin the interleave (hipcc otherwise pulls each B read down to one MFMA before its use
         // and waits lgkmcnt right there): PF k-steps of reads, then per k-step its MFMAs and the
         // reads of k-step j + PF
@@ -460,7 +428,6 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
           __builtin_amdgcn_sched_group_barrier(0x008, L::GB * L::NTW, 0);
           if (j + PF < L::KSH) __builtin_amdgcn_sched_group_barrier(0x100, L::GB, 0);
         }
-#endif
       };
       if constexpr (L::NKW == 1) {
         kloop(IC<0>{});
@@ -494,7 +461,6 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
           if (co >= L::COUT) continue;
           uint32_t lo, hi;
           if constexpr (FWD) {
-#if WS_LEAN
             // pairs through the packed fp32 ALU (v_pk_add / v_pk_fma: the same IEEE ops)
             const f2 y01 = f2{acc[b][t][0], acc[b][t][1]} + bv[t][0];
             const f2 y23 = f2{acc[b][t][2], acc[b][t][3]} + bv[t][1];
@@ -506,18 +472,6 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
             ss[t][1] += d23;
             sq[t][0] = __builtin_elementwise_fma(d01, d01, sq[t][0]);
             sq[t][1] = __builtin_elementwise_fma(d23, d23, sq[t][1]);
-#else
-            lo = pack_bf16x2(acc[b][t][0] + bv[t][0][0], acc[b][t][1] + bv[t][0][1]);
-            hi = pack_bf16x2(acc[b][t][2] + bv[t][1][0], acc[b][t][3] + bv[t][1][1]);
-            const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
-                                __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float d = v[i] - pv[t][i >> 1][i & 1];
-              ss[t][i >> 1][i & 1] += d;
-              sq[t][i >> 1][i & 1] = fmaf(d, d, sq[t][i >> 1][i & 1]);
-            }
-#endif
           } else {
             lo = pack_bf16x2(acc[b][t][0], acc[b][t][1]);
             hi = pack_bf16x2(acc[b][t][2], acc[b][t][3]);
@@ -540,38 +494,15 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
     }
   };
 
-  if constexpr (!AP && WS_PF2 != 0) {
-    // two tiles' loads in flight: tile ti+2 is issued into the register set tile ti just
-    // left, so each load has two tiles of MFMAs to land (the loop is unrolled by two so the
-    // register sets stay static)
-    u4 preb[L::SLOTS];
-    if (t0 < t1) load_into(pre, t0);
-    if (t0 + 1 < t1) load_into(preb, t0 + 1);
-    for (int ti = t0; ti < t1; ti += 2) {
-      __syncthreads();
-      store_pre(pre);
-      __syncthreads();
-      if (ti + 2 < t1) load_into(pre, ti + 2);
-      tile_body(ti);
-      if (ti + 1 < t1) {
-        __syncthreads();
-        store_pre(preb);
-        __syncthreads();
-        if (ti + 3 < t1) load_into(preb, ti + 3);
-        tile_body(ti + 1);
-      }
+  if (t0 < t1) { if constexpr (AP) load_win_tile(t0); else load_tile(t0); }
+  for (int ti = t0; ti < t1; ++ti) {
+    __syncthreads();   // every wave is done reading the previous tile (and ctab is written)
+    if constexpr (AP) store_win_tile(ti); else store_pre(pre);
+    __syncthreads();
+    if (ti + 1 < t1) {   // in flight under this tile's MFMAs
+      if constexpr (AP) load_win_tile(ti + 1); else load_tile(ti + 1);
     }
-  } else {
-    if (t0 < t1) { if constexpr (AP) load_win_tile(t0); else load_tile(t0); }
-    for (int ti = t0; ti < t1; ++ti) {
-      __syncthreads();   // every wave is done reading the previous tile (and ctab is written)
-      if constexpr (AP) store_win_tile(ti); else store_pre(pre);
-      __syncthreads();
-      if (ti + 1 < t1) {   // in flight under this tile's MFMAs
-        if constexpr (AP) load_win_tile(ti + 1); else load_tile(ti + 1);
-      }
-      tile_body(ti);
-    }
+    tile_body(ti);
   }
   if constexpr (STATS) {
     if (stats) {
@@ -587,10 +518,6 @@ __global__ __launch_bounds__(256, (AP || (RD && L::OCC > 2)) ? (L::OCC > 1 ? L::
 
 // ----------------------------------------------------------------------------- layer table
 //        CIN COUT K PAD  H   W  TH NS NCW NKW GB OCC
-#ifndef WS_VARIANT
-#define WS_VARIANT 0
-#endif
-#if WS_VARIANT == 0   // per-layer best of the measured variants (opbench, B=1024 step shapes)
 // (PF 6 everywhere: the step A/B above; the times are the round-3/4 per-layer picks at their
 // earlier PF)
 typedef Ws<8, 16, 5, 2, 56, 56, 14, 1, 1, 1, 2, 2, 6> FwdA2;  // audio conv2        273 us
@@ -601,59 +528,6 @@ typedef Ws<16, 8, 5, 2, 56, 56, 8, 1, 1, 1, 1, 3, 6> DgrA2;   // audio conv2 dgr
 typedef Ws<32, 16, 5, 2, 28, 28, 14, 1, 1, 1, 2, 2, 6> DgrA3; // audio conv3 dgrad  145 us
 typedef Ws<64, 32, 5, 2, 14, 14, 14, 1, 2, 2, 2, 2, 6> DgrA4; // audio conv4 dgrad  158 us
 typedef Ws<64, 32, 5, 4, 10, 10, 14, 1, 2, 2, 2, 2, 6> DgrI2; // image conv2 dgrad  154 us
-#elif WS_VARIANT == 1
-typedef Ws<8, 16, 5, 2, 56, 56, 14, 1, 1, 1, 4, 2> FwdA2;
-typedef Ws<16, 32, 5, 2, 28, 28, 14, 1, 1, 1, 2, 2> FwdA3;
-typedef Ws<32, 64, 5, 2, 14, 14, 14, 1, 2, 2, 2, 2> FwdA4;
-typedef Ws<32, 64, 5, 0, 14, 14, 10, 2, 2, 2, 2, 2> FwdI2;
-typedef Ws<16, 8, 5, 2, 56, 56, 14, 1, 1, 1, 2, 2> DgrA2;
-typedef Ws<32, 16, 5, 2, 28, 28, 14, 1, 1, 1, 4, 2> DgrA3;
-typedef Ws<64, 32, 5, 2, 14, 14, 14, 1, 2, 2, 2, 2> DgrA4;
-typedef Ws<64, 32, 5, 4, 10, 10, 14, 1, 2, 2, 2, 2> DgrI2;
-#elif WS_VARIANT == 2
-typedef Ws<8, 16, 5, 2, 56, 56, 8, 1, 1, 1, 1, 3> FwdA2;
-typedef Ws<16, 32, 5, 2, 28, 28, 7, 1, 1, 1, 1, 3> FwdA3;
-typedef Ws<32, 64, 5, 2, 14, 14, 14, 1, 4, 1, 2, 2> FwdA4;
-typedef Ws<32, 64, 5, 0, 14, 14, 10, 2, 4, 1, 2, 2> FwdI2;
-typedef Ws<16, 8, 5, 2, 56, 56, 8, 1, 1, 1, 1, 3> DgrA2;
-typedef Ws<32, 16, 5, 2, 28, 28, 7, 1, 1, 1, 1, 3> DgrA3;
-typedef Ws<64, 32, 5, 2, 14, 14, 14, 1, 2, 2, 1, 3> DgrA4;
-typedef Ws<64, 32, 5, 4, 10, 10, 14, 1, 2, 2, 1, 3> DgrI2;
-#else
-typedef Ws<8, 16, 5, 2, 56, 56, 14, 1, 1, 1, 2, 2, 4> FwdA2;
-typedef Ws<16, 32, 5, 2, 28, 28, 14, 1, 1, 1, 1, 2, 4> FwdA3;
-typedef Ws<32, 64, 5, 2, 14, 14, 14, 1, 2, 2, 1, 2, 4> FwdA4;
-typedef Ws<32, 64, 5, 0, 14, 14, 10, 2, 2, 2, 1, 2, 4> FwdI2;
-typedef Ws<16, 8, 5, 2, 56, 56, 8, 1, 1, 1, 2, 3, 4> DgrA2;
-typedef Ws<32, 16, 5, 2, 28, 28, 14, 1, 1, 1, 2, 2, 4> DgrA3;
-typedef Ws<64, 32, 5, 2, 14, 14, 14, 1, 2, 2, 1, 2, 4> DgrA4;
-typedef Ws<64, 32, 5, 4, 10, 10, 14, 1, 2, 2, 1, 2, 4> DgrI2;
-#endif
-// per-layer overrides for variant builds: -DWS_FWDA3=16,32,5,2,28,28,14,1,2,1,1,2,4 etc.
-#ifdef WS_FWDA2
-typedef Ws<WS_FWDA2> FwdA2_;
-#define FwdA2 FwdA2_
-#endif
-#ifdef WS_FWDA3
-typedef Ws<WS_FWDA3> FwdA3_;
-#define FwdA3 FwdA3_
-#endif
-#ifdef WS_FWDA4
-typedef Ws<WS_FWDA4> FwdA4_;
-#define FwdA4 FwdA4_
-#endif
-#ifdef WS_DGRA2
-typedef Ws<WS_DGRA2> DgrA2_;
-#define DgrA2 DgrA2_
-#endif
-#ifdef WS_DGRA3
-typedef Ws<WS_DGRA3> DgrA3_;
-#define DgrA3 DgrA3_
-#endif
-#ifdef WS_DGRA4
-typedef Ws<WS_DGRA4> DgrA4_;
-#define DgrA4 DgrA4_
-#endif
 
 // avd_options.generic_conv: every bf16 mid layer on the generic conv_cl kernels (parity tests)
 bool ws_disabled() { return g_opts.generic_conv != 0; }

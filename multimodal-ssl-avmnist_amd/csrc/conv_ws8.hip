@@ -28,9 +28,6 @@
 using namespace avd;
 
 // 1: LDS reads pinned PF k-steps / columns ahead of their MFMAs by sched_group_barrier
-#ifndef WS8_SCHED
-#define WS8_SCHED 0
-#endif
 
 namespace {
 
@@ -47,11 +44,7 @@ constexpr int cdv(int a, int b) { return (a + b - 1) / b; }
 template <int CIN_, int COUT_, int K_, int PAD_, int H_, int W_, int TH_, int NS_, int NCW_,
           int NKW_, int GB_, int OCC_, int PS_, int RP_, int PF_ = 2>
 struct W8 {
-#ifdef W8_PF_ALL
-  static constexpr int OCC = OCC_, PF = W8_PF_ALL;   // variant builds: one depth for all
-#else
   static constexpr int OCC = OCC_, PF = PF_;
-#endif
   static constexpr int CIN = CIN_, COUT = COUT_, K = K_, PAD = PAD_, H = H_, W = W_;
   static constexpr int HO = H + 2 * PAD - K + 1, WO = W + 2 * PAD - K + 1;
   static constexpr int TH = TH_, TW = WO, NS = NS_;
@@ -339,19 +332,6 @@ __global__ __launch_bounds__(256, L::OCC) void conv_ws8_kernel(
                 acc[b][t] = mxmma(j % 4, a[j][t], bq[j % (PF + 1)][b], acc[b][t], sa[j / 4][t], sb);
           }
         }
-#if WS8_SCHED
-        // pin the B reads PF k-steps ahead of their MFMAs (as conv_ws.hip); only where every
-        // k-step's MFMAs are unconditional (one scheduling region)
-        if constexpr (L::NKW == 1) {
-          constexpr int RPB = L::CIN == 8 ? 4 : 2;   // LDS reads per group and k-step
-          __builtin_amdgcn_sched_group_barrier(0x100, RPB * L::GB * (PF < L::KSH ? PF : L::KSH), 0);
-#pragma unroll
-          for (int j = 0; j < L::KSH; ++j) {
-            __builtin_amdgcn_sched_group_barrier(0x008, L::GB * L::NTW, 0);
-            if (j + PF < L::KSH) __builtin_amdgcn_sched_group_barrier(0x100, RPB * L::GB, 0);
-          }
-        }
-#endif
       }
       if constexpr (L::NKW > 1) {
         f4* r = red + (((i0 / L::GB) & 1) * L::NCW + wc) * L::GB * L::NTW * 64;
@@ -411,17 +391,11 @@ __global__ __launch_bounds__(256, L::OCC) void conv_ws8_kernel(
 
 // ----------------------------------------------------------------------------- layer table
 //        CIN COUT K PAD  H   W  TH NS NCW NKW GB OCC PS RP
-#ifndef F8A2_T
-#define F8A2_T 14, 1, 1, 1, 2, 3, 8, 7   // OCC 3: 958 vs 986 us at N = 28672 (tools/build_variants.sh)
-#endif
-#ifndef D8A2_T
-#define D8A2_T 8, 1, 1, 1, 1, 3, 16, 12
-#endif
-typedef W8<8, 16, 5, 2, 56, 56, F8A2_T> F8A2;     // audio conv2 forward
+typedef W8<8, 16, 5, 2, 56, 56, 14, 1, 1, 1, 2, 3, 8, 7> F8A2;     // audio conv2 forward
 typedef W8<16, 32, 5, 2, 28, 28, 14, 1, 1, 1, 1, 2, 16, 12> F8A3;  // audio conv3
 typedef W8<32, 64, 5, 2, 14, 14, 14, 1, 2, 2, 1, 2, 32, 4> F8A4;   // audio conv4
 typedef W8<32, 64, 5, 0, 14, 14, 10, 2, 2, 2, 1, 2, 32, 4> F8I2;   // image conv2
-typedef W8<16, 8, 5, 2, 56, 56, D8A2_T> D8A2;    // audio conv2 input gradient
+typedef W8<16, 8, 5, 2, 56, 56, 8, 1, 1, 1, 1, 3, 16, 12> D8A2;    // audio conv2 input gradient
 typedef W8<32, 16, 5, 2, 28, 28, 14, 1, 1, 1, 1, 2, 32, 4> D8A3;   // audio conv3
 typedef W8<64, 32, 5, 2, 14, 14, 14, 1, 2, 2, 2, 2, 96, 4> D8A4;   // audio conv4
 typedef W8<64, 32, 5, 4, 10, 10, 14, 1, 2, 2, 2, 2, 96, 4> D8I2;   // image conv2
@@ -731,15 +705,6 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws8_kernel(const bf16* 
         for (int m = 0; m < L::MTW; ++m)
           acc[m][j] = mxmma_<0>(a[m], bq[j % (PF + 1)], acc[m][j], sbd, sbx);
       }
-#if WS8_SCHED
-      // A reads + PF columns of B reads, then per column its MFMAs and the reads of column j + PF
-      __builtin_amdgcn_sched_group_barrier(0x100, 4 * L::MTW + 4 * (PF < L::NW ? PF : L::NW), 0);
-#pragma unroll
-      for (int j = 0; j < L::NW; ++j) {
-        __builtin_amdgcn_sched_group_barrier(0x008, L::MTW, 0);
-        if (j + PF < L::NW) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-      }
-#endif
     }
   }
 
@@ -795,10 +760,7 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws8_kernel(const bf16* 
 }
 
 //          CIN COUT K PAD  H   W  TR NCW OCC NSS DYS XS
-#ifndef G8A2_T
-#define G8A2_T 8, 1, 2, 1, 16, 8
-#endif
-typedef G8<8, 16, 5, 2, 56, 56, G8A2_T> G8A2;     // audio conv2
+typedef G8<8, 16, 5, 2, 56, 56, 8, 1, 2, 1, 16, 8> G8A2;     // audio conv2
 typedef G8<16, 32, 5, 2, 28, 28, 14, 4, 2, 1, 32, 16> G8A3;  // audio conv3
 typedef G8<32, 64, 5, 2, 14, 14, 7, 4, 1, 1, 64, 32, 512, 2, 1> G8A4;   // audio conv4
 typedef G8<32, 64, 5, 0, 14, 14, 10, 4, 1, 1, 64, 32, 512, 2, 1> G8I2;  // image conv2

@@ -477,6 +477,42 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& p, int tn, int tm, int
     __syncthreads();
   }
   float* part = p.ws ? p.ws + (size_t)tz * M * N : nullptr;
+  if constexpr (MODE == 2 && BM * BN * 2 <= GemmLds<MODE, BM, BN>::BYTES) {
+    if (!part && p.c_bf16 && p.map_c == 0) {
+      // bf16 output tile: staged in the (now idle) operand LDS as [BM][BN] with 16-byte chunks
+      // XOR-swizzled by row, then written as 16-byte row segments (the MFMA layout would store
+      // 2 bytes per lane, 32-byte segments per row)
+      bf16* ts = reinterpret_cast<bf16*>(smem);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int nl = BN / 2 * wn + 16 * j + r16;
+          const float bv = p.bias && n0 + nl < N ? p.bias[n0 + nl] : 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int ml = BM / 2 * wm + 16 * i + 4 * g + e;
+            ts[ml * BN + ((((nl >> 3) ^ (ml & 7)) << 3) | (nl & 7))] = f2bf(p.alpha * acc[i][j][e] + bv);
+          }
+        }
+      __syncthreads();
+      bf16* C = reinterpret_cast<bf16*>(p.C);
+      for (int c = tid; c < BM * BN / 8; c += 256) {
+        const int ml = c / (BN / 8), ch = c % (BN / 8);
+        const int m = m0 + ml, n = n0 + 8 * ch;
+        if (m >= M || n >= N) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>(ts + ml * BN + ((ch ^ (ml & 7)) << 3));
+        bf16* dst = C + (size_t)m * p.ldc + n;
+        if (n + 7 < N && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0)) {
+          *reinterpret_cast<uint4*>(dst) = v;
+        } else {
+          const unsigned w[4] = {v.x, v.y, v.z, v.w};
+          for (int k = 0; k < 8 && n + k < N; ++k) dst[k] = (bf16)((w[k >> 1] >> (16 * (k & 1))) & 0xffffu);
+        }
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -706,12 +742,14 @@ void dispatch_gemm(const Plan& pl, int lA, int lB, const GemmArgs& a, hipStream_
 // rows contiguous), problem 2 = dX [rows, In] = dout W (A k-contiguous, B rows contiguous).
 // Tile plans served: dW 128x128 (every weight-gradient plan of the step), dX any of 128x128,
 // 128x64, 64x64; anything else returns false and the caller launches the two GEMMs separately.
+// which: 3 = both problems; 1 = the weight gradient (+ bias gradient) only, the input-gradient
+// grid empty (the caller runs dX on the critical stream and dW beside it, on another stream).
 template <int MODE, typename SB = float>
 bool launch_pair(const Plan& p1, const GemmArgs& a1, const Plan& p2, const GemmArgs& a2,
-                 const DbArgs& d, hipStream_t st) {
+                 const DbArgs& d, hipStream_t st, int which = 3) {
   if (p1.bm != 128 || p1.bn != 128) return false;
   const int n1 = avd_cdiv(a1.N, p1.bn), m1 = avd_cdiv(a1.M, p1.bm);
-  const int n2 = avd_cdiv(a2.N, p2.bn), m2 = avd_cdiv(a2.M, p2.bm);
+  const int n2 = which & 2 ? avd_cdiv(a2.N, p2.bn) : 0, m2 = which & 2 ? avd_cdiv(a2.M, p2.bm) : 0;
   const int blocks = n1 * m1 * p1.splits + n2 * m2 * p2.splits + (d.db ? d.nrc * d.strips : 0);
 #define AVD_P(BM2_, BN2_)                                                                      \
   if (p2.bm == BM2_ && p2.bn == BN2_) {                                                        \
@@ -721,7 +759,7 @@ bool launch_pair(const Plan& p1, const GemmArgs& a1, const Plan& p2, const GemmA
   AVD_P(128, 128) else AVD_P(128, 64) else AVD_P(64, 64) else return false;
 #undef AVD_P
   launch_splitk_reduce(p1, a1, st, &d);
-  launch_splitk_reduce(p2, a2, st);
+  if (which & 2) launch_splitk_reduce(p2, a2, st);
   return true;
 }
 
@@ -772,8 +810,9 @@ long long avd_linear_bwd_ws_elems(int rows, int O, int In, int mode) {
 
 int avd_linear_bwd(int rows, int O, int In, const float* dout, long long dout_ld, const float* x,
                    long long x_ld, const float* W, float* dW, float* dX, long long dx_ld, float* db,
-                   int mode, float* ws, long long ws_elems, void* stream) {
-  if (!dout || !x || !W || !dW || !dX) return AVD_ERR_ARG;
+                   int mode, int which, float* ws, long long ws_elems, void* stream) {
+  if (which < 1 || which > 3) return AVD_ERR_ARG;
+  if (!dout || ((which & 1) && (!x || !dW)) || ((which & 2) && (!W || !dX))) return AVD_ERR_ARG;
   if (rows <= 0 || O <= 0 || In <= 0 || dout_ld < O || x_ld < In || dx_ld < In) return AVD_ERR_SHAPE;
   if (mode != 1 && mode != 2) return AVD_ERR_ARG;
   hipStream_t st = avd_stream(stream);
@@ -792,24 +831,26 @@ int avd_linear_bwd(int rows, int O, int In, const float* dout, long long dout_ld
                                 1.f, 0.f, ws);
   const GemmArgs a2 = make_args(p2, rows, In, O, dout, dout_ld, 1, W, In, 1, dX, dx_ld, nullptr,
                                 1.f, 0.f, p1.splits > 1 ? ws + w1 : ws);
-  const bool lay = lay_of(dout, 1, dout_ld) == LAY_R && lay_of(x, 1, x_ld) == LAY_R &&
-                   lay_of(dout, dout_ld, 1) == LAY_K && lay_of(W, 1, In) == LAY_R;
+  const bool lay = (which & 1) && lay_of(dout, 1, dout_ld) == LAY_R && lay_of(x, 1, x_ld) == LAY_R &&
+                   (!(which & 2) || (lay_of(dout, dout_ld, 1) == LAY_K && lay_of(W, 1, In) == LAY_R));
   bool done = false;
   if (lay)
-    done = mode == 1 ? launch_pair<1>(p1, a1, p2, a2, d, st) : launch_pair<2>(p1, a1, p2, a2, d, st);
+    done = mode == 1 ? launch_pair<1>(p1, a1, p2, a2, d, st, which)
+                     : launch_pair<2>(p1, a1, p2, a2, d, st, which);
   if (!done) {
-    if (db) {
+    if (db && (which & 1)) {
       db_partial_kernel<<<d.nrc * d.strips, 256, 0, st>>>(d);
       db_final_kernel<<<avd_cdiv(O, 256), 256, 0, st>>>(d);
     }
-    const int l1a = lay_of(dout, 1, dout_ld), l1b = lay_of(x, 1, x_ld);
-    const int l2a = lay_of(dout, dout_ld, 1), l2b = lay_of(W, 1, In);
-    if (mode == 1) {
-      dispatch_gemm<1>(p1, l1a, l1b, a1, st);
-      dispatch_gemm<1>(p2, l2a, l2b, a2, st);
-    } else {
-      dispatch_gemm<2>(p1, l1a, l1b, a1, st);
-      dispatch_gemm<2>(p2, l2a, l2b, a2, st);
+    if (which & 1) {
+      const int l1a = lay_of(dout, 1, dout_ld), l1b = lay_of(x, 1, x_ld);
+      if (mode == 1) dispatch_gemm<1>(p1, l1a, l1b, a1, st);
+      else dispatch_gemm<2>(p1, l1a, l1b, a1, st);
+    }
+    if (which & 2) {
+      const int l2a = lay_of(dout, dout_ld, 1), l2b = lay_of(W, 1, In);
+      if (mode == 1) dispatch_gemm<1>(p2, l2a, l2b, a2, st);
+      else dispatch_gemm<2>(p2, l2a, l2b, a2, st);
     }
   }
   AVD_CHECK_LAUNCH();
@@ -859,15 +900,16 @@ int avd_linear_fwd_hwc(int rows, int O, int C, int HW, const void* feat, const v
 }
 
 int avd_linear_bwd_hwc(int rows, int O, int C, int HW, const float* dout, long long dout_ld,
-                       const void* feat, const void* Wp, float* dW, float* db, void* dX,
+                       const void* feat, const void* Wp, float* dW, float* db, void* dX, int which,
                        float* ws, long long ws_elems, void* stream) {
-  if (!dout || !feat || !Wp || !dW || !dX) return AVD_ERR_ARG;
+  if (which < 1 || which > 3) return AVD_ERR_ARG;
+  if (!dout || ((which & 1) && (!feat || !dW)) || ((which & 2) && (!Wp || !dX))) return AVD_ERR_ARG;
   const int In = C * HW;
   if (rows <= 0 || O <= 0 || C <= 0 || HW <= 0 || dout_ld < O || In % 8 || O % 4 || dout_ld % 4)
     return AVD_ERR_SHAPE;
   if ((reinterpret_cast<uintptr_t>(dout) & 15) || (reinterpret_cast<uintptr_t>(feat) & 15) ||
       (reinterpret_cast<uintptr_t>(Wp) & 15))
-    return AVD_ERR_ARG;
+    return AVD_ERR_ARG;       // (NULL, for a part not computed, passes)
   hipStream_t st = avd_stream(stream);
   Plan p1 = plan_for(O, In, rows), p2 = plan_for(rows, In, O);
   const long long w1 = p1.splits > 1 ? (long long)p1.splits * O * In : 0;
@@ -881,14 +923,14 @@ int avd_linear_bwd_hwc(int rows, int O, int C, int HW, const float* dout, long l
   // dX[r, (h,w,c)] = sum_o dout[r, o] Wp[o, (h,w,c)], stored bf16 NHWC
   const GemmArgs a2 = make_args(p2, rows, In, O, dout, dout_ld, 1, Wp, In, 1, dX, In, nullptr,
                                 1.f, 0.f, p1.splits > 1 ? ws + w1 : ws, 1);
-  if (!launch_pair<2, bf16>(p1, a1, p2, a2, d, st)) {
-    // shapes the paired launch does not serve (few rows: no 128x128 weight-gradient plan)
-    if (db) {
+  if (!(which & 1) || !launch_pair<2, bf16>(p1, a1, p2, a2, d, st, which)) {
+    // dX alone, or shapes the paired launch does not serve (few rows: no 128x128 dW plan)
+    if ((which & 1) && db) {
       db_partial_kernel<<<d.nrc * d.strips, 256, 0, st>>>(d);
       db_final_kernel<<<avd_cdiv(O, 256), 256, 0, st>>>(d);
     }
-    launch_gemm<2, LAY_R, LAY_R, float, bf16>(p1, a1, st);
-    launch_gemm<2, LAY_K, LAY_R, float, bf16>(p2, a2, st);
+    if (which & 1) launch_gemm<2, LAY_R, LAY_R, float, bf16>(p1, a1, st);
+    if (which & 2) launch_gemm<2, LAY_K, LAY_R, float, bf16>(p2, a2, st);
   }
   AVD_CHECK_LAUNCH();
   return AVD_OK;

@@ -26,40 +26,8 @@
 #include "common.h"
 #include "bnapply.h"
 
-// diagnostics builds (wrong results): WG_VARIANT 10 = no staging, 11 = no MFMA loop,
-// 12 = no staging + B fragments read once per k-step only for column 0, 13 = no staging + no MFMA
-// (LDS reads only, folded into a register)
-#if defined(WG_VARIANT) && WG_VARIANT >= 10
-#if WG_VARIANT == 10
-#define WG_NOSTAGE
-#elif WG_VARIANT == 11
-#define WG_NOMFMA
-#elif WG_VARIANT == 12
-#define WG_NOSTAGE
-#define WG_NOBREAD
-#elif WG_VARIANT == 14
-#define WG_NOSLAB
-#elif WG_VARIANT == 15
-#define WG_NOSTAGE
-#define WG_NOMMA
-#define WG_NOSLAB
-#else
-#define WG_NOSTAGE
-#define WG_NOMMA
-#endif
-#undef WG_VARIANT
-#define WG_VARIANT 0
-#endif
-
-// 1: incremental X-image pixel indices in the k-step loop (fewer VALU per MFMA; same reads)
-#ifndef WG_LEAN
-#define WG_LEAN 0   // measured slower (14x14: 168 vs 158 us, 56x56: 281 vs 275 us)
-#endif
-
-// 1: two strips' input loads in flight (two register sets) instead of one (AP = 0 launches)
-#ifndef WG_PF2
-#define WG_PF2 0
-#endif
+// Measured and removed (round 4): incremental X-image pixel indices in the k-step loop (14^2:
+// 168 vs 158 us), two strips' input loads in flight (two register sets: slower).
 
 using namespace avd;
 
@@ -81,11 +49,7 @@ template <int CIN_, int COUT_, int K_, int PAD_, int H_, int W_, int TR_, int NC
           int PF_ = 3, int NTHR_ = 256, int NMW_ = 1, int NSS_ = 1>
 struct Wg {
   static constexpr int CIN = CIN_, COUT = COUT_, K = K_, PAD = PAD_, H = H_, W = W_;
-#ifdef WG_PF_ALL
-  static constexpr int OCC = OCC_, PF = WG_PF_ALL, NTHR = NTHR_, WAVES = NTHR / 64;   // variant builds
-#else
   static constexpr int OCC = OCC_, PF = PF_, NTHR = NTHR_, WAVES = NTHR / 64;
-#endif
   static constexpr int HO = H + 2 * PAD - K + 1, WO = W + 2 * PAD - K + 1;
   static constexpr int WO8 = (WO + 7) & ~7;                 // 8-pixel runs never cross a row
   static constexpr int TR = TR_, SPS = HO / TR, NSS = NSS_; // strip rows / strips per sample
@@ -314,30 +278,7 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* _
       if (tid + L::NTHR * i < L::X_T) *reinterpret_cast<u4*>(smem + xlo[i]) = xpre[i];
   };
 
-#if WG_LEAN
-  // X-image pixel (sample, row, column) of this lane's two k-runs at k-step wp: divided out once
-  // per launch (the same for every strip), advanced by 32 NPW pixels per k-step with one carry
-  // each way; pixels past the strip (the k-step tail) read the last pixel, as the clamp did
-  constexpr int DPX = 32 * L::NPW, DR = DPX / L::WO8, DO = DPX % L::WO8;
-  static_assert(DR + 1 <= L::TR, "one row carry per k-step");
-  constexpr int PL = L::NPIX - 1, SML = PL / L::SPIX, RL = (PL - SML * L::SPIX) / L::WO8,
-                OXL = PL - SML * L::SPIX - RL * L::WO8;
-  constexpr int XBL = ((SML * L::XR + RL) * L::XW + OXL) * L::XS;
-  int xp0[2], xs0[2], xr0[2], xo0[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    xp0[h] = 32 * wp + kpix(g, h, q4);
-    xs0[h] = xp0[h] / L::SPIX;
-    const int rem = xp0[h] - xs0[h] * L::SPIX;
-    xr0[h] = rem / L::WO8;
-    xo0[h] = rem - xr0[h] * L::WO8;
-  }
-#endif
   auto strip_body = [&]() {
-#if WG_LEAN
-    int xpp[2] = {xp0[0], xp0[1]}, xss[2] = {xs0[0], xs0[1]}, xrr[2] = {xr0[0], xr0[1]},
-        xoo[2] = {xo0[0], xo0[1]};
-#endif
     for (int ks = wp; ks < L::KST; ks += L::NPW) {
       const int P0 = 32 * ks;
       int xb[2];
@@ -351,21 +292,10 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* _
       }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-#if WG_LEAN
-        xb[h] = xpp[h] <= PL ? ((xss[h] * L::XR + xrr[h]) * L::XW + xoo[h]) * L::XS : XBL;
-        xpp[h] += DPX;
-        xoo[h] += DO;
-        xrr[h] += DR;
-        if (xoo[h] >= L::WO8) { xoo[h] -= L::WO8; ++xrr[h]; }
-        if constexpr (L::NSS > 1) {
-          if (xrr[h] >= L::TR) { xrr[h] -= L::TR; ++xss[h]; }
-        }
-#else
         const int P = min(P0 + kpix(g, h, q4), L::NPIX - 1);   // tail pixels: dY is 0 there
         const int sm = P / L::SPIX, rem = P - sm * L::SPIX;
         const int r = rem / L::WO8, ox = rem - r * L::WO8;
         xb[h] = ((sm * L::XR + r) * L::XW + ox) * L::XS;
-#endif
       }
       // B fragments PF columns ahead of their MFMAs
       constexpr int PF = L::PF;
@@ -377,71 +307,33 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* _
       }
 #pragma unroll
       for (int j = 0; j < L::NW; ++j) {
-#ifndef WG_NOBREAD
         if (j + PF < L::NW) {
           bq[(j + PF) % (PF + 1)][0] = tr4(xs + xb[0] + xo[j + PF]);
           bq[(j + PF) % (PF + 1)][1] = tr4(xs + xb[1] + xo[j + PF]);
         }
         const bf16x8 b = frag8(bq[j % (PF + 1)][0], bq[j % (PF + 1)][1]);
-#else
-        const bf16x8 b = frag8(bq[0][0], bq[0][1]);
-#endif
-#ifndef WG_NOMMA
 #pragma unroll
         for (int m = 0; m < L::MTW; ++m) acc[m][j] = mma(a[m], b, acc[m][j]);
-#else
-        {
-          const u4 bb = __builtin_bit_cast(u4, b);
-          acc[0][j][0] += __uint_as_float(bb.x ^ bb.y ^ bb.z ^ bb.w);
-        }
-#endif
       }
       // pin the interleave (hipcc otherwise pulls each fragment's reads down to its MFMAs and
       // waits lgkmcnt(0) every few MFMAs): A + PF columns of reads, then MTW MFMAs per column
       // with the reads of column j + PF between them
-#if !defined(WG_NOMMA) && !defined(WG_NOBREAD)
       __builtin_amdgcn_sched_group_barrier(0x100, 2 * L::MTW + 2 * (PF < L::NW ? PF : L::NW), 0);
 #pragma unroll
       for (int j = 0; j < L::NW; ++j) {
         __builtin_amdgcn_sched_group_barrier(0x008, L::MTW, 0);
         if (j + PF < L::NW) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       }
-#endif
     }
   };
 
-  if constexpr (!AP && WG_PF2 != 0) {
-    // two strips' loads in flight (two register sets, the loop unrolled by two)
-    u4 preb[L::SLOTS];
-    if (st0 < st1) load_into(pre, st0);
-    if (st0 + 1 < st1) load_into(preb, st0 + 1);
-    for (int st = st0; st < st1; st += 2) {
-      __syncthreads();
-      store_from(pre);
-      __syncthreads();
-      if (st + 2 < st1) load_into(pre, st + 2);
-      strip_body();
-      if (st + 1 < st1) {
-        __syncthreads();
-        store_from(preb);
-        __syncthreads();
-        if (st + 3 < st1) load_into(preb, st + 3);
-        strip_body();
-      }
-    }
-  } else {
-    if (st0 < st1) { if constexpr (AP) load_strip_ap(st0); else load_strip(st0); }
-    for (int st = st0; st < st1; ++st) {
-#ifndef WG_NOSTAGE
-      __syncthreads();
-      if constexpr (AP) store_strip_ap(st); else store_strip();
-      __syncthreads();
-      if (st + 1 < st1) { if constexpr (AP) load_strip_ap(st + 1); else load_strip(st + 1); }
-#endif
-#ifndef WG_NOMFMA
-      strip_body();
-#endif
-    }
+  if (st0 < st1) { if constexpr (AP) load_strip_ap(st0); else load_strip(st0); }
+  for (int st = st0; st < st1; ++st) {
+    __syncthreads();
+    if constexpr (AP) store_strip_ap(st); else store_strip();
+    __syncthreads();
+    if (st + 1 < st1) { if constexpr (AP) load_strip_ap(st + 1); else load_strip(st + 1); }
+    strip_body();
   }
 
   // pixel-split partials -> wave wp = 0 (fixed order), then the slab write
@@ -467,9 +359,6 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* _
             acc[m][j] += red[((((w - 1) * L::NCW * L::NMW + slot) * L::MTW + m) * L::NW + j) * 64 + lane];
     }
   }
-#ifdef WG_NOSLAB
-  if (N >= 0) return;
-#endif
   // slab write [co][ci][tap], staged through LDS RC output-channel tiles at a time so the HBM
   // stores are contiguous float4s (written straight from the MFMA layout they were 4-byte
   // scatters at a 25-float stride: ~110 us of a 270 us launch on the 14x14 shapes)
@@ -509,40 +398,11 @@ __global__ __launch_bounds__(L::NTHR, L::OCC) void wgrad_ws_kernel(const bf16* _
 }
 
 //        CIN COUT K PAD  H   W  TR NCW OCC PF NTHR NMW NSS
-#ifndef WG_VARIANT
-#define WG_VARIANT 0
-#endif
-#if WG_VARIANT == 0
 typedef Wg<8, 16, 5, 2, 56, 56, 8, 1, 2> WgA2;      // audio conv2
 typedef Wg<16, 32, 5, 2, 28, 28, 14, 4, 2> WgA3;    // audio conv3
 typedef Wg<32, 64, 5, 2, 14, 14, 14, 2, 1, 3, 256, 2> WgA4;   // audio conv4: 2x2 waves over (M, columns); 170 vs 161 us alone, step 5.279 vs 5.317 ms
 typedef Wg<32, 64, 5, 0, 14, 14, 10, 4, 1> WgI2;    // image conv2
-#elif WG_VARIANT == 1
-typedef Wg<8, 16, 5, 2, 56, 56, 8, 1, 2, 1> WgA2;
-typedef Wg<16, 32, 5, 2, 28, 28, 14, 4, 2, 1> WgA3;
-typedef Wg<32, 64, 5, 2, 14, 14, 14, 4, 1, 1> WgA4;
-typedef Wg<32, 64, 5, 0, 14, 14, 10, 4, 1, 1> WgI2;
-#elif WG_VARIANT == 2
-typedef Wg<8, 16, 5, 2, 56, 56, 8, 1, 1, 3, 512> WgA2;
-typedef Wg<16, 32, 5, 2, 28, 28, 14, 4, 1, 3, 512> WgA3;
-typedef Wg<32, 64, 5, 2, 14, 14, 14, 4, 1, 3, 512, 2> WgA4;
-typedef Wg<32, 64, 5, 0, 14, 14, 10, 4, 1, 3, 512, 2> WgI2;
-#else
-typedef Wg<8, 16, 5, 2, 56, 56, 14, 1, 2> WgA2;
-typedef Wg<16, 32, 5, 2, 28, 28, 28, 4, 2> WgA3;
-typedef Wg<32, 64, 5, 2, 14, 14, 14, 4, 1, 3, 256, 1, 2> WgA4;
-typedef Wg<32, 64, 5, 0, 14, 14, 10, 4, 1, 3, 256, 1, 2> WgI2;
-#endif
 
-// per-layer override for variant builds: -DWG_A4=32,64,5,2,14,14,14,4,1,3,256,1,2 etc.
-#ifdef WG_A4
-typedef Wg<WG_A4> WgA4_;
-#define WgA4 WgA4_
-#endif
-#ifdef WG_I2
-typedef Wg<WG_I2> WgI2_;
-#define WgI2 WgI2_
-#endif
 
 // avd_options.generic_conv: every bf16 weight gradient on the generic wgrad_cl kernel
 bool wg_disabled() { return g_opts.generic_conv != 0; }
