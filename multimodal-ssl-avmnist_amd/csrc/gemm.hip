@@ -126,6 +126,12 @@ struct TileRegs { float v[ROWS / 8 > 16 ? ROWS / 8 : 16]; };   // ROWS*32 elemen
 
 // f32 operand loads (bf16 operands go through the raw Stage specialisations below)
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+// 16 zero bytes the out-of-range lanes of a k-tile load read instead of their operand: the
+// loads then need neither a per-lane branch nor a select on the loaded value (either makes the
+// compiler wait for the load right where it is issued)
+__device__ uint4 g_zero16 = {0u, 0u, 0u, 0u};   // (global, not constant, address space: loads stay global_load)
+template <typename S>
+__device__ __forceinline__ const S* zero16() { return reinterpret_cast<const S*>(&g_zero16); }
 __device__ __forceinline__ float ld1(const float* p) { return *p; }
 
 template <int ROWS, int LAY, typename S = float>
@@ -138,16 +144,11 @@ __device__ __forceinline__ void load_tile(const S* __restrict__ X, long long sr,
       const int e4 = tid + 256 * i;
       const int r = e4 >> 3, k = (e4 & 7) * 4;
       const int gr = r0 + r, gk = k0 + k;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (gr < rows) {
-        const S* p = X + (size_t)gr * sr + gk;
-        if (gk + 3 < kend) v = ld4(p);
-        else {
-          if (gk < kend) v.x = ld1(p);
-          if (gk + 1 < kend) v.y = ld1(p + 1);
-          if (gk + 2 < kend) v.z = ld1(p + 2);
-        }
-      }
+      // whole-vector bounds (the host serves LAY_K only for k extents % 4 == 0): an
+      // out-of-range lane reads g_zero16 -- no per-lane branch, so the compiler can count the
+      // k-tile's loads exactly (s_waitcnt vmcnt(n), not vmcnt(0))
+      const bool ok = gr < rows && gk < kend;
+      const float4 v = ld4(ok ? X + (size_t)gr * sr + gk : zero16<S>());
       t.v[4 * i] = v.x; t.v[4 * i + 1] = v.y; t.v[4 * i + 2] = v.z; t.v[4 * i + 3] = v.w;
     }
   } else if constexpr (LAY == LAY_R) {
@@ -165,16 +166,9 @@ __device__ __forceinline__ void load_tile(const S* __restrict__ X, long long sr,
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         const int gk = k0 + 4 * kb + kk;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (b < 2 * ROWS && gk < kend) {
-          const S* p = X + (size_t)gk * sk + gr;
-          if (gr + 3 < rows) v = ld4(p);
-          else {
-            if (gr < rows) v.x = ld1(p);
-            if (gr + 1 < rows) v.y = ld1(p + 1);
-            if (gr + 2 < rows) v.z = ld1(p + 2);
-          }
-        }
+        // whole-vector bounds (LAY_R only for row extents % 4 == 0), branch-free as LAY_K
+        const bool ok = b < 2 * ROWS && gk < kend && gr < rows;
+        const float4 v = ld4(ok ? X + (size_t)gk * sk + gr : zero16<S>());
         t.v[16 * i + kk] = v.x; t.v[16 * i + 4 + kk] = v.y;
         t.v[16 * i + 8 + kk] = v.z; t.v[16 * i + 12 + kk] = v.w;
       }
@@ -222,7 +216,8 @@ __device__ __forceinline__ void store_tile(const TileRegs<ROWS>& t, long long sr
 #pragma unroll
     for (int i = 0; i < (ROWS + 127) / 128; ++i) {
       const int b = tid + 256 * i;
-      if (b >= 2 * ROWS) continue;
+      // (wave-uniform: a scalar branch keeps the k-tile's load counting exact)
+      if ((2 * ROWS) % 256 != 0 && __builtin_amdgcn_readfirstlane(b) >= 2 * ROWS) continue;
       const int kb = b & 7, r = (b >> 3) * 4;                   // as load_tile<LAY_R>
       if constexpr (MODE == 2) {
         // odd row blocks write their rows rotated by one (row r + (j + 1) % 4 at step j): the two
@@ -280,7 +275,11 @@ struct Stage {
   }
 };
 
-__device__ __forceinline__ unsigned hw16(const uint4& v, int j) {
+// raw bf16 staging registers: a native vector (HIP's uint4 class copies through memory when
+// loaded from a selected pointer)
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned hw16(const u32x4& v, int j) {
   const unsigned w = j < 2 ? v.x : j < 4 ? v.y : j < 6 ? v.z : v.w;
   return (j & 1) ? (w >> 16) : (w & 0xffffu);
 }
@@ -288,7 +287,7 @@ __device__ __forceinline__ unsigned hw16(const uint4& v, int j) {
 template <int MODE, int ROWS, typename S>
 struct Stage<MODE, ROWS, LAY_K, S, true> {
   static constexpr int NV = ROWS / 64 > 0 ? ROWS / 64 : 1;   // 16-byte chunks per thread
-  uint4 v[NV];
+  u32x4 v[NV];
   __device__ __forceinline__ void load(const S* __restrict__ X, long long sr, long long, int r0,
                                        int k0, int rows, int kend) {
 #pragma unroll
@@ -296,19 +295,10 @@ struct Stage<MODE, ROWS, LAY_K, S, true> {
       const int e = (int)threadIdx.x + 256 * i;
       const int r = e >> 2, kc = e & 3;
       const int gr = r0 + r, gk = k0 + 8 * kc;
-      uint4 u = make_uint4(0u, 0u, 0u, 0u);
-      if (r < ROWS && gr < rows) {
-        const bf16* p = reinterpret_cast<const bf16*>(X) + (size_t)gr * sr + gk;
-        if (gk + 7 < kend) {
-          u = *reinterpret_cast<const uint4*>(p);
-        } else {
-          unsigned h[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) h[j] = gk + j < kend ? p[j] : 0u;
-          u = make_uint4(h[0] | h[1] << 16, h[2] | h[3] << 16, h[4] | h[5] << 16, h[6] | h[7] << 16);
-        }
-      }
-      v[i] = u;
+      // whole 16-byte chunks (bf16 operands need k extents % 8 == 0), branch-free
+      const bool ok = r < ROWS && gr < rows && gk < kend;
+      const bf16* p = ok ? reinterpret_cast<const bf16*>(X) + (size_t)gr * sr + gk : zero16<bf16>();
+      v[i] = *reinterpret_cast<const u32x4*>(p);
     }
   }
   __device__ __forceinline__ void store(long long, long long, typename GemmT<MODE>::T* dst) {
@@ -316,7 +306,7 @@ struct Stage<MODE, ROWS, LAY_K, S, true> {
     for (int i = 0; i < NV; ++i) {
       const int e = (int)threadIdx.x + 256 * i;
       const int r = e >> 2, kc = e & 3;
-      if (r < ROWS) *reinterpret_cast<uint4*>(dst + gsw(r, 8 * kc)) = v[i];
+      if (ROWS >= 64 || r < ROWS) *reinterpret_cast<u32x4*>(dst + gsw(r, 8 * kc)) = v[i];
     }
   }
 };
@@ -325,7 +315,7 @@ template <int MODE, int ROWS, typename S>
 struct Stage<MODE, ROWS, LAY_R, S, true> {
   static_assert(ROWS <= 256 && ROWS % 8 == 0, "LAY_R raw tile");
   static constexpr int RG = ROWS / 8;                         // 8-row groups; thread = (kq, rg)
-  uint4 v[4];
+  u32x4 v[4];
   __device__ __forceinline__ void load(const S* __restrict__ X, long long, long long sk, int r0,
                                        int k0, int rows, int kend) {
     const int b = threadIdx.x;
@@ -334,24 +324,15 @@ struct Stage<MODE, ROWS, LAY_R, S, true> {
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int gk = k0 + 4 * kq + kk;
-      uint4 u = make_uint4(0u, 0u, 0u, 0u);
-      if (b < 8 * RG && gk < kend) {
-        const bf16* p = reinterpret_cast<const bf16*>(X) + (size_t)gk * sk + gr;
-        if (gr + 7 < rows) {
-          u = *reinterpret_cast<const uint4*>(p);
-        } else {
-          unsigned h[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) h[j] = gr + j < rows ? p[j] : 0u;
-          u = make_uint4(h[0] | h[1] << 16, h[2] | h[3] << 16, h[4] | h[5] << 16, h[6] | h[7] << 16);
-        }
-      }
-      v[kk] = u;
+      // whole 16-byte chunks (row extents % 8 == 0), branch-free
+      const bool ok = b < 8 * RG && gk < kend && gr < rows;
+      const bf16* p = ok ? reinterpret_cast<const bf16*>(X) + (size_t)gk * sk + gr : zero16<bf16>();
+      v[kk] = *reinterpret_cast<const u32x4*>(p);
     }
   }
   __device__ __forceinline__ void store(long long, long long, typename GemmT<MODE>::T* dst) {
     const int b = threadIdx.x;
-    if (b >= 8 * RG) return;
+    if (__builtin_amdgcn_readfirstlane(b) >= 8 * RG) return;   // whole waves (ROWS % 64 == 0)
     const int rg = b % RG, kq = b / RG;
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
@@ -644,10 +625,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a, int S, i
   }
 }
 
-int lay_of(const float* p, long long s_rows, long long s_k) {
+// (the vector layouts also need the bounded extent to be whole vectors: the loads test bounds
+// per float4, not per element -- n_k for LAY_K, n_rows for LAY_R)
+int lay_of(const float* p, long long s_rows, long long s_k, long long n_rows, long long n_k) {
   const bool al = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
-  if (s_k == 1 && s_rows % 4 == 0 && al) return LAY_K;
-  if (s_rows == 1 && s_k % 4 == 0 && al) return LAY_R;
+  if (s_k == 1 && s_rows % 4 == 0 && n_k % 4 == 0 && al) return LAY_K;
+  if (s_rows == 1 && s_k % 4 == 0 && n_rows % 4 == 0 && al) return LAY_R;
   return LAY_S;
 }
 
@@ -831,8 +814,10 @@ int avd_linear_bwd(int rows, int O, int In, const float* dout, long long dout_ld
                                 1.f, 0.f, ws);
   const GemmArgs a2 = make_args(p2, rows, In, O, dout, dout_ld, 1, W, In, 1, dX, dx_ld, nullptr,
                                 1.f, 0.f, p1.splits > 1 ? ws + w1 : ws);
-  const bool lay = (which & 1) && lay_of(dout, 1, dout_ld) == LAY_R && lay_of(x, 1, x_ld) == LAY_R &&
-                   (!(which & 2) || (lay_of(dout, dout_ld, 1) == LAY_K && lay_of(W, 1, In) == LAY_R));
+  const bool lay = (which & 1) && lay_of(dout, 1, dout_ld, O, rows) == LAY_R &&
+                   lay_of(x, 1, x_ld, In, rows) == LAY_R &&
+                   (!(which & 2) || (lay_of(dout, dout_ld, 1, rows, O) == LAY_K &&
+                                     lay_of(W, 1, In, In, O) == LAY_R));
   bool done = false;
   if (lay)
     done = mode == 1 ? launch_pair<1>(p1, a1, p2, a2, d, st, which)
@@ -843,12 +828,12 @@ int avd_linear_bwd(int rows, int O, int In, const float* dout, long long dout_ld
       db_final_kernel<<<avd_cdiv(O, 256), 256, 0, st>>>(d);
     }
     if (which & 1) {
-      const int l1a = lay_of(dout, 1, dout_ld), l1b = lay_of(x, 1, x_ld);
+      const int l1a = lay_of(dout, 1, dout_ld, O, rows), l1b = lay_of(x, 1, x_ld, In, rows);
       if (mode == 1) dispatch_gemm<1>(p1, l1a, l1b, a1, st);
       else dispatch_gemm<2>(p1, l1a, l1b, a1, st);
     }
     if (which & 2) {
-      const int l2a = lay_of(dout, dout_ld, 1), l2b = lay_of(W, 1, In);
+      const int l2a = lay_of(dout, dout_ld, 1, rows, O), l2b = lay_of(W, 1, In, In, O);
       if (mode == 1) dispatch_gemm<1>(p2, l2a, l2b, a2, st);
       else dispatch_gemm<2>(p2, l2a, l2b, a2, st);
     }
@@ -959,8 +944,8 @@ int avd_gemm(int M, int N, int K, const float* A, long long sam, long long sak, 
       pl.splits = 1;   // no (or too small a) workspace: single pass over K
       pl.kchunk = K;
     }
-    const int lA = lay_of(A, sam, sak);
-    const int lB = lay_of(B, sbn, sbk);
+    const int lA = lay_of(A, sam, sak, M, K);
+    const int lB = lay_of(B, sbn, sbk, N, K);
     const GemmArgs a = make_args(pl, M, N, K, A, sam, sak, B, sbk, sbn, C, ldc, bias, alpha, beta, ws);
     if (mode == 1)
       dispatch_gemm<1>(pl, lA, lB, a, st);
