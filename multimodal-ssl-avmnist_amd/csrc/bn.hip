@@ -350,14 +350,17 @@ __global__ __launch_bounds__(1024) void sum_rows_kernel(const float* __restrict_
 
 // The 16-byte path of sum_rows_kernel (cols and ld multiples of 4, 16-byte aligned in / out):
 // each lane owns 4 consecutive columns (one global_load_dwordx4 per row), CQ lanes per row phase
-// and 1024 / CQ phases per block; a phase sums its rows in double, row order, 4 rows' loads in
+// and 256 / CQ phases per block; a phase sums its rows in double, row order, 4 rows' loads in
 // flight, then thread (0, lane) folds the phases in phase order.  Fixed order, deterministic.
+// 256-thread blocks: the slab reductions run beside the other streams' kernels, and a
+// 1024-thread block waits for a CU with 16 free wave slots (the round-4 form took 50-60 us in
+// the step for 6.5-52 MB)
 template <int CQ>
-__global__ __launch_bounds__(1024) void sum_rows4_kernel(const float* __restrict__ in, int rows,
-                                                         int cols, long long ld,
-                                                         float* __restrict__ out, int accumulate,
-                                                         int rows_per_chunk) {
-  constexpr int PH = 1024 / CQ;
+__global__ __launch_bounds__(256) void sum_rows4_kernel(const float* __restrict__ in, int rows,
+                                                        int cols, long long ld,
+                                                        float* __restrict__ out, int accumulate,
+                                                        int rows_per_chunk) {
+  constexpr int PH = 256 / CQ;
   __shared__ double sh[PH][CQ][4];
   const int lq = threadIdx.x % CQ, ph = threadIdx.x / CQ;
   const int c = 4 * (blockIdx.x * CQ + lq);
@@ -558,21 +561,19 @@ int avd_bn1d_bwd_apply(const float* x, const float* dz, const float* coef, float
 // columns per block of the launch sum_rows takes for this shape (the 16-byte path when cols % 4
 // == 0; the chunk count, and with it the summation order, depends on the shape only)
 static int sum_rows_cw(int cols) {
-  if (cols % 4 == 0) return cols <= 2048 ? 64 : 256;
+  if (cols % 4 == 0) return 64;            // sum_rows4_kernel<16>: 16 phases of 256 threads
   return cols <= 2048 ? 16 : 64;
 }
+static int sum_rows_phases(int cols) { return cols % 4 == 0 ? 16 : 1024 / sum_rows_cw(cols); }
 
 static void launch_sum_rows(const float* in, int rows, int cols, long long ld, float* out,
                             int accumulate, int chunks, hipStream_t st) {
   const int rpc = avd_cdiv(rows, chunks);
   const bool v4 = cols % 4 == 0 && ld % 4 == 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 &&
                   (reinterpret_cast<uintptr_t>(out) & 15) == 0;
-  if (v4 && cols <= 2048)
-    sum_rows4_kernel<16><<<dim3(avd_cdiv(cols, 64), chunks), 1024, 0, st>>>(in, rows, cols, ld, out,
-                                                                           accumulate, rpc);
-  else if (v4)
-    sum_rows4_kernel<64><<<dim3(avd_cdiv(cols, 256), chunks), 1024, 0, st>>>(in, rows, cols, ld, out,
-                                                                            accumulate, rpc);
+  if (v4)
+    sum_rows4_kernel<16><<<dim3(avd_cdiv(cols, 64), chunks), 256, 0, st>>>(in, rows, cols, ld, out,
+                                                                          accumulate, rpc);
   else if (cols <= 2048)
     sum_rows_kernel<16><<<dim3(avd_cdiv(cols, 16), chunks), 1024, 0, st>>>(in, rows, cols, ld, out,
                                                                           accumulate, rpc);
@@ -596,11 +597,11 @@ int avd_sum_rows(const float* in, int rows, int cols, long long ld, float* out, 
 int avd_sum_rows_chunks(int rows, int cols) {
   // small inputs: one launch (a second one costs more than the single pass takes)
   if (rows <= 0 || cols <= 0 || (long long)rows * cols < (1ll << 20)) return 1;
-  const int cw = sum_rows_cw(cols), ph = 1024 / (cols % 4 == 0 ? cw / 4 : cw);
+  const int cw = sum_rows_cw(cols), ph = sum_rows_phases(cols);
   const int cb = avd_cdiv(cols, cw);
-  // >= ~128 blocks per launch: a wide slab stack (51200 columns: 200 blocks of 1024 threads, 16
+  // >= ~512 blocks per launch: a wide slab stack (51200 columns: 800 blocks of 256 threads, 16
   // rows of 16-byte loads per thread) is one pass, narrow ones split their rows
-  const int target = 128;
+  const int target = 512;
   const int want = avd_cdiv(target, cb), most = rows / (4 * ph);
   const int c = want < most ? want : most;
   return c > 1 ? c : 1;

@@ -95,7 +95,7 @@ __global__ __launch_bounds__(256) void sgemm_kernel(int M, int N, int K, const f
 // parity mode); MODE 2: v_mfma_f32_16x16x32_bf16 (operands rounded to bf16 while staging,
 // fp32 accumulate: the bf16 training mode, like the reference's fp16 autocast Linear).
 //
-// Block tile BM x BN (128x128, 128x64 or 64x64), BK 32, 4 waves in a 2x2 grid, each wave
+// Block tile BM x BN (128x128, 128x64 or 64x64), BK 32 (f32) / 64 (bf16), 4 waves in a 2x2 grid, each wave
 // (BM/2)x(BN/2) = TI x TJ MFMA 16x16 tiles.  Operands live in LDS k-contiguous ([m][k] for A,
 // [n][k] for B) so every fragment is one LDS read.  Software pipeline: the next k-tile is
 // loaded into registers (float4 whenever a stride is 1) while the current one feeds the
@@ -106,23 +106,27 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f4;
 
 template <int MODE>
-struct GemmT { typedef float T; static constexpr int LDK = 33; };
+struct GemmT { typedef float T; static constexpr int LDK = 33, BK = 32; };
 template <>
-struct GemmT<2> { typedef bf16 T; static constexpr int LDK = 32; };
+struct GemmT<2> { typedef bf16 T; static constexpr int LDK = 64, BK = 64; };
 
-// bf16 tiles: 64-byte rows, the 16-byte chunk c of row r stored at chunk c ^ ((r >> 1) & 3).  The
-// MFMA fragment reads (16 rows x one chunk per 16 lanes, ds_read_b128) and the staging writes
-// (ds_write_b64) are then bank-conflict free; the LAY_R staging also pairs rows of opposite
-// parity in each 16-lane write group (tools/lds_conflicts.py gemm).
-__device__ __forceinline__ int gsw(int r, int k) { return r * 32 + (((k >> 3) ^ ((r >> 1) & 3)) << 3) + (k & 7); }
+// bf16 tiles (BK 64): 128-byte rows, the 16-byte chunk c of row r stored at chunk c ^ ((r >> 1) & 7).
+// The MFMA fragment reads (16 rows x one chunk per 16 lanes, ds_read_b128) and the staging
+// writes are then bank-conflict free (tools/lds_conflicts.py gemm).
+__device__ __forceinline__ int gsw(int r, int k) { return r * 64 + (((k >> 3) ^ ((r >> 1) & 7)) << 3) + (k & 7); }
 
-// Operand layouts of a (rows x 32) tile of X with element (r, k) at X[r*sr + k*sk]:
+// Operand layouts of a (rows x BK) tile of X with element (r, k) at X[r*sr + k*sk]:
 // LAY_K: k contiguous & 16B aligned rows (float4 along k); LAY_R: rows contiguous (float4 along
 // r); LAY_S: anything else (scalar).
 enum { LAY_K = 0, LAY_R = 1, LAY_S = 2 };
 
-template <int ROWS>
-struct TileRegs { float v[ROWS / 8 > 16 ? ROWS / 8 : 16]; };   // ROWS*32 elements over 256 threads
+// f32 staging registers of a ROWS x BK tile over 256 threads (LAY_R: 4x4 blocks, 16 per pass)
+template <int ROWS, int BK>
+struct TileRegs {
+  static constexpr int NK = ROWS * BK / 256;
+  static constexpr int NR = 16 * ((ROWS * BK / 16 + 255) / 256);
+  float v[NK > NR ? NK : NR];
+};
 
 // f32 operand loads (bf16 operands go through the raw Stage specialisations below)
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -134,15 +138,20 @@ template <typename S>
 __device__ __forceinline__ const S* zero16() { return reinterpret_cast<const S*>(&g_zero16); }
 __device__ __forceinline__ float ld1(const float* p) { return *p; }
 
-template <int ROWS, int LAY, typename S = float>
+// LAY_R row-block order: bits 0 and 1 swapped (row blocks 2m, 2m + 1 of the lane order sit
+// 8 rows apart)
+__device__ __forceinline__ int lrb(int q) { return (q & ~3) | ((q & 1) << 1) | ((q >> 1) & 1); }
+
+template <int ROWS, int BK, int LAY, typename S = float>
 __device__ __forceinline__ void load_tile(const S* __restrict__ X, long long sr, long long sk,
-                                          int r0, int k0, int rows, int kend, TileRegs<ROWS>& t) {
+                                          int r0, int k0, int rows, int kend, TileRegs<ROWS, BK>& t) {
   const int tid = threadIdx.x;
   if constexpr (LAY == LAY_K) {
+    constexpr int KV = BK / 4;                        // float4 per tile row
 #pragma unroll
-    for (int i = 0; i < ROWS / 32; ++i) {
+    for (int i = 0; i < ROWS * KV / 256; ++i) {
       const int e4 = tid + 256 * i;
-      const int r = e4 >> 3, k = (e4 & 7) * 4;
+      const int r = e4 / KV, k = (e4 % KV) * 4;
       const int gr = r0 + r, gk = k0 + k;
       // whole-vector bounds (the host serves LAY_K only for k extents % 4 == 0): an
       // out-of-range lane reads g_zero16 -- no per-lane branch, so the compiler can count the
@@ -153,21 +162,23 @@ __device__ __forceinline__ void load_tile(const S* __restrict__ X, long long sr,
     }
   } else if constexpr (LAY == LAY_R) {
     // a 4 (k) x 4 (rows) block per thread: four float4 loads along the rows, transposed in
-    // registers so store_tile writes 4 consecutive k of a row at once
+    // registers so store_tile writes 4 consecutive k of a row at once.  Block b: k-block
+    // b & 7 of the 32-k half b / (8 * ROWS / 4), row block lrb((b >> 3) % (ROWS / 4)): 8 lanes
+    // cover one row's 32 k and the next 8 lanes rows 8 further on (lrb swaps bits 0 and 1), so a
+    // 16-lane group of 8-byte LDS writes covers both 64-byte halves of the 128-byte bank row
+    // (tools/lds_conflicts.py gemm); a wave still reads whole 128-byte row segments
+    constexpr int NB = ROWS * BK / 16;
 #pragma unroll
-    for (int i = 0; i < (ROWS + 127) / 128; ++i) {
+    for (int i = 0; i < (NB + 255) / 256; ++i) {
       const int b = tid + 256 * i;
-      // k-block fastest: 8 lanes cover one row's 32 k (64 LDS bytes) and the next 8 lanes the
-      // next 4 rows, so a 16-lane group of store_tile's 8-byte LDS writes is bank-conflict free
-      // (rows fastest put lanes 4 apart on one bank: 4-way); the global reads stay whole
-      // 128-byte row segments (8 lanes x 16 bytes per k row)
-      const int kb = b & 7, r = (b >> 3) * 4;
+      const int kb = b & 7, rest = b >> 3;
+      const int r = lrb(rest % (ROWS / 4)) * 4, kh = rest / (ROWS / 4);
       const int gr = r0 + r;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
-        const int gk = k0 + 4 * kb + kk;
+        const int gk = k0 + 32 * kh + 4 * kb + kk;
         // whole-vector bounds (LAY_R only for row extents % 4 == 0), branch-free as LAY_K
-        const bool ok = b < 2 * ROWS && gk < kend && gr < rows;
+        const bool ok = b < NB && gk < kend && gr < rows;
         const float4 v = ld4(ok ? X + (size_t)gk * sk + gr : zero16<S>());
         t.v[16 * i + kk] = v.x; t.v[16 * i + 4 + kk] = v.y;
         t.v[16 * i + 8 + kk] = v.z; t.v[16 * i + 12 + kk] = v.w;
@@ -176,10 +187,10 @@ __device__ __forceinline__ void load_tile(const S* __restrict__ X, long long sr,
   } else {
     const bool kfast = sk <= sr;
 #pragma unroll
-    for (int i = 0; i < ROWS / 8; ++i) {
+    for (int i = 0; i < ROWS * BK / 256; ++i) {
       const int e = tid + 256 * i;
       int r, k;
-      if (kfast) { r = e >> 5; k = e & 31; } else { k = e / ROWS; r = e % ROWS; }
+      if (kfast) { r = e / BK; k = e % BK; } else { k = e / ROWS; r = e % ROWS; }
       const int gr = r0 + r, gk = k0 + k;
       t.v[i] = (gr < rows && gk < kend) ? ld1(X + (size_t)gr * sr + (size_t)gk * sk) : 0.f;
     }
@@ -192,15 +203,16 @@ __device__ __forceinline__ void lds_put(typename GemmT<MODE>::T* p, float v) {
 }
 
 template <int MODE, int ROWS, int LAY>
-__device__ __forceinline__ void store_tile(const TileRegs<ROWS>& t, long long sr, long long sk,
-                                           typename GemmT<MODE>::T* S) {
-  constexpr int LDK = GemmT<MODE>::LDK;
+__device__ __forceinline__ void store_tile(const TileRegs<ROWS, GemmT<MODE>::BK>& t, long long sr,
+                                           long long sk, typename GemmT<MODE>::T* S) {
+  constexpr int LDK = GemmT<MODE>::LDK, BK = GemmT<MODE>::BK;
   const int tid = threadIdx.x;
   if constexpr (LAY == LAY_K) {
+    constexpr int KV = BK / 4;
 #pragma unroll
-    for (int i = 0; i < ROWS / 32; ++i) {
+    for (int i = 0; i < ROWS * KV / 256; ++i) {
       const int e4 = tid + 256 * i;
-      const int r = e4 >> 3, k = (e4 & 7) * 4;
+      const int r = e4 / KV, k = (e4 % KV) * 4;
       typename GemmT<MODE>::T* d = S + (MODE == 2 ? gsw(r, k) : r * LDK + k);
       if constexpr (MODE == 2) {
         // 4 bf16 = one 8-byte LDS store
@@ -213,32 +225,25 @@ __device__ __forceinline__ void store_tile(const TileRegs<ROWS>& t, long long sr
       }
     }
   } else if constexpr (LAY == LAY_R) {
+    constexpr int NB = ROWS * BK / 16;
 #pragma unroll
-    for (int i = 0; i < (ROWS + 127) / 128; ++i) {
+    for (int i = 0; i < (NB + 255) / 256; ++i) {
       const int b = tid + 256 * i;
       // (wave-uniform: a scalar branch keeps the k-tile's load counting exact)
-      if ((2 * ROWS) % 256 != 0 && __builtin_amdgcn_readfirstlane(b) >= 2 * ROWS) continue;
-      const int kb = b & 7, r = (b >> 3) * 4;                   // as load_tile<LAY_R>
+      if (NB % 256 != 0 && __builtin_amdgcn_readfirstlane(b) >= NB) continue;
+      const int kb = b & 7, rest = b >> 3;                      // as load_tile<LAY_R>
+      const int r = lrb(rest % (ROWS / 4)) * 4, k = 32 * (rest / (ROWS / 4)) + 4 * kb;
       if constexpr (MODE == 2) {
-        // odd row blocks write their rows rotated by one (row r + (j + 1) % 4 at step j): the two
-        // row blocks of a 16-lane group then hit opposite 64-byte halves of the bank row
-        const bool odd = (b >> 3) & 1;
-        uint2 w[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float* v = &t.v[16 * i + 4 * j];
-          w[j] = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int jr = odd ? (j + 1) & 3 : j;
-          const uint2 wj = odd ? w[(j + 1) & 3] : w[j];
-          *reinterpret_cast<uint2*>(S + gsw(r + jr, 4 * kb)) = wj;
+          *reinterpret_cast<uint2*>(S + gsw(r + j, k)) =
+              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
         }
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          typename GemmT<MODE>::T* d = S + (r + j) * LDK + 4 * kb;
+          typename GemmT<MODE>::T* d = S + (r + j) * LDK + k;
           const float* v = &t.v[16 * i + 4 * j];
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk) d[kk] = v[kk];
@@ -248,16 +253,16 @@ __device__ __forceinline__ void store_tile(const TileRegs<ROWS>& t, long long sr
   } else {
     const bool kfast = sk <= sr;
 #pragma unroll
-    for (int i = 0; i < ROWS / 8; ++i) {
+    for (int i = 0; i < ROWS * BK / 256; ++i) {
       const int e = tid + 256 * i;
       int r, k;
-      if (kfast) { r = e >> 5; k = e & 31; } else { k = e / ROWS; r = e % ROWS; }
+      if (kfast) { r = e / BK; k = e % BK; } else { k = e / ROWS; r = e % ROWS; }
       lds_put<MODE>(S + (MODE == 2 ? gsw(r, k) : r * LDK + k), t.v[i]);
     }
   }
 }
 
-// Staging of one operand tile (ROWS x 32 k) from HBM through registers into the LDS ring.  f32
+// Staging of one operand tile (ROWS x BK k) from HBM through registers into the LDS ring.  f32
 // sources (and bf16 ones in the f32 MFMA mode) go through TileRegs as floats; bf16 sources in the
 // bf16 mode are copied raw, 16 bytes per load (8-byte accesses run at 0.54-0.70x the 16-byte rate,
 // MI355X_MICROARCH.md): k-contiguous rows as 16-byte chunks straight into their swizzled LDS
@@ -265,10 +270,10 @@ __device__ __forceinline__ void store_tile(const TileRegs<ROWS>& t, long long sr
 template <int MODE, int ROWS, int LAY, typename S,
           bool RAW = (MODE == 2 && std::is_same<S, bf16>::value && LAY != LAY_S)>
 struct Stage {
-  TileRegs<ROWS> t;
+  TileRegs<ROWS, GemmT<MODE>::BK> t;
   __device__ __forceinline__ void load(const S* __restrict__ X, long long sr, long long sk, int r0,
                                        int k0, int rows, int kend) {
-    load_tile<ROWS, LAY, S>(X, sr, sk, r0, k0, rows, kend, t);
+    load_tile<ROWS, GemmT<MODE>::BK, LAY, S>(X, sr, sk, r0, k0, rows, kend, t);
   }
   __device__ __forceinline__ void store(long long sr, long long sk, typename GemmT<MODE>::T* dst) {
     store_tile<MODE, ROWS, LAY>(t, sr, sk, dst);
@@ -284,16 +289,17 @@ __device__ __forceinline__ unsigned hw16(const u32x4& v, int j) {
   return (j & 1) ? (w >> 16) : (w & 0xffffu);
 }
 
+// (raw stages exist in the bf16 mode only: BK 64, 8 chunks per tile row)
 template <int MODE, int ROWS, typename S>
 struct Stage<MODE, ROWS, LAY_K, S, true> {
-  static constexpr int NV = ROWS / 64 > 0 ? ROWS / 64 : 1;   // 16-byte chunks per thread
+  static constexpr int NV = ROWS * 8 / 256 > 0 ? ROWS * 8 / 256 : 1;   // 16-byte chunks per thread
   u32x4 v[NV];
   __device__ __forceinline__ void load(const S* __restrict__ X, long long sr, long long, int r0,
                                        int k0, int rows, int kend) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int e = (int)threadIdx.x + 256 * i;
-      const int r = e >> 2, kc = e & 3;
+      const int r = e >> 3, kc = e & 7;
       const int gr = r0 + r, gk = k0 + 8 * kc;
       // whole 16-byte chunks (bf16 operands need k extents % 8 == 0), branch-free
       const bool ok = r < ROWS && gr < rows && gk < kend;
@@ -305,41 +311,55 @@ struct Stage<MODE, ROWS, LAY_K, S, true> {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int e = (int)threadIdx.x + 256 * i;
-      const int r = e >> 2, kc = e & 3;
-      if (ROWS >= 64 || r < ROWS) *reinterpret_cast<u32x4*>(dst + gsw(r, 8 * kc)) = v[i];
+      const int r = e >> 3, kc = e & 7;
+      if (ROWS >= 32 || r < ROWS) *reinterpret_cast<u32x4*>(dst + gsw(r, 8 * kc)) = v[i];
     }
   }
 };
 
 template <int MODE, int ROWS, typename S>
 struct Stage<MODE, ROWS, LAY_R, S, true> {
-  static_assert(ROWS <= 256 && ROWS % 8 == 0, "LAY_R raw tile");
-  static constexpr int RG = ROWS / 8;                         // 8-row groups; thread = (kq, rg)
-  u32x4 v[4];
+  static_assert(ROWS <= 256 && ROWS % 64 == 0, "LAY_R raw tile");
+  static constexpr int RG = ROWS / 8;                 // 8-row groups; thread = (kq, rg), kq < 16
+  static constexpr int IT = (16 * RG + 255) / 256;    // passes over the 256 threads
+  static constexpr int LG = RG == 8 ? 0 : RG == 16 ? 1 : 2;
+  u32x4 v[4 * IT];
+  // thread b: row group (b & 7) | (b >> 4 & (RG / 8 - 1)) << 3, k-quad (b >> 3 & 1) | (b >> (4 + LG)) << 1:
+  // a 16-lane group writes 8 row groups x both 8-byte halves of one k chunk, which the rotated
+  // row order spreads over all 32 banks (tools/lds_conflicts.py gemm); a wave reads 16 row
+  // groups' 16 bytes = 256 contiguous bytes per k row
+  __device__ __forceinline__ static int rg_of(int b) { return (b & 7) | (((b >> 4) & (RG / 8 - 1)) << 3); }
+  __device__ __forceinline__ static int kq_of(int b) { return ((b >> 3) & 1) | ((b >> (4 + LG)) << 1); }
   __device__ __forceinline__ void load(const S* __restrict__ X, long long, long long sk, int r0,
                                        int k0, int rows, int kend) {
-    const int b = threadIdx.x;
-    const int rg = b % RG, kq = b / RG;
-    const int gr = r0 + 8 * rg;
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int gk = k0 + 4 * kq + kk;
-      // whole 16-byte chunks (row extents % 8 == 0), branch-free
-      const bool ok = b < 8 * RG && gk < kend && gr < rows;
-      const bf16* p = ok ? reinterpret_cast<const bf16*>(X) + (size_t)gk * sk + gr : zero16<bf16>();
-      v[kk] = *reinterpret_cast<const u32x4*>(p);
+    for (int it = 0; it < IT; ++it) {
+      const int b = (int)threadIdx.x + 256 * it;
+      const int rg = rg_of(b), kq = kq_of(b);
+      const int gr = r0 + 8 * rg;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int gk = k0 + 4 * kq + kk;
+        // whole 16-byte chunks (row extents % 8 == 0), branch-free
+        const bool ok = b < 16 * RG && gk < kend && gr < rows;
+        const bf16* p = ok ? reinterpret_cast<const bf16*>(X) + (size_t)gk * sk + gr : zero16<bf16>();
+        v[4 * it + kk] = *reinterpret_cast<const u32x4*>(p);
+      }
     }
   }
   __device__ __forceinline__ void store(long long, long long, typename GemmT<MODE>::T* dst) {
-    const int b = threadIdx.x;
-    if (__builtin_amdgcn_readfirstlane(b) >= 8 * RG) return;   // whole waves (ROWS % 64 == 0)
-    const int rg = b % RG, kq = b / RG;
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const int j = (jj + rg) & 7;            // rotated per row group: the 16-lane write groups
-      const unsigned lo = hw16(v[0], j) | hw16(v[1], j) << 16;   // spread over the bank rows
-      const unsigned hi = hw16(v[2], j) | hw16(v[3], j) << 16;
-      *reinterpret_cast<uint2*>(dst + gsw(8 * rg + j, 4 * kq)) = make_uint2(lo, hi);
+    for (int it = 0; it < IT; ++it) {
+      const int b = (int)threadIdx.x + 256 * it;
+      if ((16 * RG) % 256 != 0 && __builtin_amdgcn_readfirstlane(b) >= 16 * RG) continue;   // whole waves
+      const int rg = rg_of(b), kq = kq_of(b);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int j = (jj + rg) & 7;            // rotated per row group: the 16-lane write groups
+        const unsigned lo = hw16(v[4 * it], j) | hw16(v[4 * it + 1], j) << 16;   // spread over the banks
+        const unsigned hi = hw16(v[4 * it + 2], j) | hw16(v[4 * it + 3], j) << 16;
+        *reinterpret_cast<uint2*>(dst + gsw(8 * rg + j, 4 * kq)) = make_uint2(lo, hi);
+      }
     }
   }
 };
@@ -386,7 +406,7 @@ struct GemmLds {
 template <int MODE, int BM, int BN, int LA, int LB, typename SA = float, typename SB = float>
 __device__ __forceinline__ void gemm_tile(const GemmArgs& p, int tn, int tm, int tz, char* smem) {
   typedef typename GemmT<MODE>::T T;
-  constexpr int LDK = GemmT<MODE>::LDK;
+  constexpr int LDK = GemmT<MODE>::LDK, BK = GemmT<MODE>::BK;
   constexpr int TI = BM / 32, TJ = BN / 32;   // MFMA tiles per wave
   T (*As)[BM * LDK] = reinterpret_cast<T (*)[BM * LDK]>(smem);
   T (*Bs)[BN * LDK] = reinterpret_cast<T (*)[BN * LDK]>(smem + 2 * BM * LDK * sizeof(T));
@@ -409,7 +429,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& p, int tn, int tm, int
 
   Stage<MODE, BM, LA, SA> ta;
   Stage<MODE, BN, LB, SB> tb;
-  const int nk = (kend - kbeg + 31) / 32;
+  const int nk = (kend - kbeg + BK - 1) / BK;
   ta.load(A, sam, sak, m0, kbeg, M, kend);
   tb.load(B, sbn, sbk, n0, kbeg, N, kend);   // B^T tile: rows = n
   ta.store(sam, sak, As[0]);
@@ -419,23 +439,27 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& p, int tn, int tm, int
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) {
-      ta.load(A, sam, sak, m0, kbeg + 32 * (kt + 1), M, kend);
-      tb.load(B, sbn, sbk, n0, kbeg + 32 * (kt + 1), N, kend);
+      ta.load(A, sam, sak, m0, kbeg + BK * (kt + 1), M, kend);
+      tb.load(B, sbn, sbk, n0, kbeg + BK * (kt + 1), N, kend);
     }
     const T* as = As[cur] + (BM / 2 * wm + r16) * LDK;
     const T* bs = Bs[cur] + (BN / 2 * wn + r16) * LDK;
     if constexpr (MODE == 2) {
-      bf16x8 a[TI], b[TJ];
-      const int gc = 8 * (g ^ ((r16 >> 1) & 3));     // the swizzled chunk (tile rows are r16 mod 16)
 #pragma unroll
-      for (int i = 0; i < TI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(as + 16 * i * LDK + gc);
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        bf16x8 a[TI], b[TJ];
+        // the swizzled chunk of k-chunk 4 ks + g (tile rows are r16 mod 16)
+        const int gc = 8 * ((4 * ks + g) ^ ((r16 >> 1) & 7));
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(bs + 16 * j * LDK + gc);
+        for (int i = 0; i < TI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(as + 16 * i * LDK + gc);
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
+        for (int j = 0; j < TJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(bs + 16 * j * LDK + gc);
 #pragma unroll
-        for (int j = 0; j < TJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
     } else {
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
@@ -649,7 +673,7 @@ Plan plan_for(int M, int N, int K) {
     constexpr int target256 = 224;
     const int s = (int)std::max(1ll, std::min<long long>(avd_cdiv(target256, t), K / 128));
     if (s > 1) {
-      p.kchunk = avd_cdiv(avd_cdiv(K, s), 32) * 32;
+      p.kchunk = avd_cdiv(avd_cdiv(K, s), 64) * 64;   // whole k-tiles of either mode
       p.splits = avd_cdiv(K, p.kchunk);
     }
     return p;
@@ -667,7 +691,7 @@ Plan plan_for(int M, int N, int K) {
     int s = (int)std::min<long long>(avd_cdiv(target, t), K / kmin);
     s = std::max(1, std::min(s, 128));
     if (s > 1) {
-      p.kchunk = avd_cdiv(avd_cdiv(K, s), 32) * 32;
+      p.kchunk = avd_cdiv(avd_cdiv(K, s), 64) * 64;   // whole k-tiles of either mode
       p.splits = avd_cdiv(K, p.kchunk);
     }
   }
