@@ -230,9 +230,44 @@ def gemm_tiles(swizzle=True, ldk=32):
     return acc
 
 
+def gemm_tiles64():
+    """gemm_tile<2> with 64-wide k-tiles (round 5): 128-byte rows, chunk c of row r at
+    c ^ ((r >> 1) & 7); fragment reads of k-chunks 4 ks + g; staging writes of raw LAY_K (16-byte
+    chunks, 8 lanes per row), f32 LAY_K (8 bytes, 16 lanes per row), f32 LAY_R (row blocks of 4,
+    lane-order blocks 2m / 2m + 1 eight rows apart: gemm.hip lrb) and raw LAY_R (8 row groups x
+    both halves of a k chunk per 16 lanes, rows rotated by row group)."""
+    def at(r, k):
+        return 2 * (r * 64 + 8 * ((k >> 3) ^ ((r >> 1) & 7)) + (k & 7))
+    lrb = lambda q: (q & ~3) | ((q & 1) << 1) | ((q >> 1) & 1)  # noqa: E731
+    acc = []
+    for ks in range(2):
+        for i in range(4):
+            acc.append((f"fragment read ks {ks} tile {i}", "read_b128",
+                        [at(16 * i + (l & 15), 8 * (4 * ks + (l >> 4))) for l in range(64)], 1))
+    for w in range(4):
+        acc.append((f"raw LAY_K write wave {w}", "write_b128",
+                    [at((64 * w + l) >> 3, 8 * ((64 * w + l) & 7)) for l in range(64)], 0.25))
+        acc.append((f"f32 LAY_K write wave {w}", "write_b64",
+                    [at((64 * w + l) // 16, 4 * ((64 * w + l) % 16)) for l in range(64)], 0.25))
+    for j in range(4):
+        addrs = []
+        for l in range(64):
+            rest = l >> 3
+            addrs.append(at(4 * lrb(rest % 32) + j, 32 * (rest // 32) + 4 * (l & 7)))
+        acc.append((f"f32 LAY_R write step {j}", "write_b64", addrs, 0.25))
+    for jj in range(8):
+        addrs = []
+        for l in range(64):       # ROWS 128: row group (b & 7) | (b >> 4 & 1) << 3, k-quad (b >> 3 & 1) | (b >> 5) << 1
+            rg, kq = (l & 7) | (((l >> 4) & 1) << 3), ((l >> 3) & 1) | ((l >> 5) << 1)
+            addrs.append(at(8 * rg + ((jj + rg) & 7), 4 * kq))
+        acc.append((f"raw LAY_R write step {jj}", "write_b64", addrs, 0.125))
+    return acc
+
+
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "gemm":
     report("bf16 GEMM tiles, LDK 40 unswizzled (round 3)", gemm_tiles(False, 40))
-    report("bf16 GEMM tiles, LDK 32 swizzled", gemm_tiles(True, 32))
+    report("bf16 GEMM tiles, LDK 32 swizzled (round 4)", gemm_tiles(True, 32))
+    report("bf16 GEMM tiles, 64-wide k-tiles (round 5)", gemm_tiles64())
 
 
 # ---------------------------------------------------------------- image conv1 routed moments
