@@ -343,6 +343,15 @@ int avd_act_bwd_dev(const float* x, const float* dout, float* dx, int act, const
 int avd_bn1d_bwd_reduce(const float* x, const float* dz, const float* mean, const float* invstd,
                         int rows, int G, int C, float* parts, void* stream);
 
+/* avd_act_bwd_dev (act 1: GELU over the BatchNorm1d affine, then dropout) and
+ * avd_bn1d_bwd_reduce in one launch: dz = dropout(dout) * gelu'(scale*x + shift) is written to
+ * dz and its partials (sum dz, sum dz*xhat) to parts [C, G, R, 2] -- bit-identical to the two
+ * launches (same operations, same row order).  ProjectionHead backward, dino.py:1240-1254. */
+int avd_bn1d_act_bwd_reduce(const float* x, const float* dout, float* dz, const float* scale,
+                            const float* shift, const float* mean, const float* invstd, int rows,
+                            int G, int C, float p, unsigned long long seed,
+                            const unsigned long long* seed_off, float* parts, void* stream);
+
 /* dx = k1*dz + kx*x + k0 per (group, column), coef [G,C,3] from avd_bn_bwd_finalize. */
 int avd_bn1d_bwd_apply(const float* x, const float* dz, const float* coef, float* dx,
                        int rows, int G, int C, void* stream);

@@ -82,6 +82,7 @@ PROTOS = {
     "avd_adam_dev": [P, P, P, P, L, P, F, F, F, F, P],
     "avd_adamw_dev": [P, P, P, P, L, P, F, F, F, F, P],
     "avd_bn1d_bwd_reduce": [P, P, P, P, I, I, I, P, P],
+    "avd_bn1d_act_bwd_reduce": [P, P, P, P, P, P, P, I, I, I, F, U64, P, P, P],
     "avd_bn1d_bwd_apply": [P, P, P, P, I, I, I, P],
     "avd_dino_loss": [P, P, P, I, I, I, I, F, F, F, I, P, P, P, P, P],
     "avd_mse_loss": [P, P, I, I, P, P, P, P],

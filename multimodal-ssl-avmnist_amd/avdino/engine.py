@@ -580,12 +580,12 @@ class ProjHead:
         yield
         st = ctx["st"]
         dz = ws.get("head_dz", rows * Hd)
-        ops.act_bwd(ctx["h"], da, dz, 1, st[2], st[3], rows, G, Hd, ctx["drop_p"], ctx["seed"],
-                    ctx.get("seed_off"))
-        yield
         R = ops.colstats_parts(rpg)
         parts = ws.get("bwd_parts", Hd * G * R * 2)
-        ops.bn1d_bwd_reduce(ctx["h"], dz, st[0], st[1], rows, G, Hd, parts)
+        # GELU / dropout backward and the BatchNorm1d partials in one launch
+        ops.bn1d_act_bwd_reduce(ctx["h"], da, dz, st[2], st[3], st[0], st[1], rows, G, Hd,
+                                ctx["drop_p"], ctx["seed"], parts, ctx.get("seed_off"))
+        yield
         coef = ws.get("bwd_coef", G * Hd * 3)
         ops.bn_bwd_finalize(parts, G, R, Hd, rpg, store[p + ".mlp.1.weight"], st[0], st[1], coef,
                             store.grad_of(p + ".mlp.1.weight"), store.grad_of(p + ".mlp.1.bias"), None)

@@ -925,6 +925,13 @@ def act_bwd(x, dout, dx, act, scale, shift, rows, G, C, drop_p, seed, seed_off=N
          stream())
 
 
+def bn1d_act_bwd_reduce(x, dout, dz, scale, shift, mean, invstd, rows, G, C, drop_p, seed, parts,
+                        seed_off=None):
+    """act_bwd(act=1) + bn1d_bwd_reduce in one launch (avd_bn1d_act_bwd_reduce; bit-identical)."""
+    call("avd_bn1d_act_bwd_reduce", p(x), p(dout), p(dz), p(scale), p(shift), p(mean), p(invstd),
+         rows, G, C, drop_p, seed, p(seed_off) if seed_off is not None else None, p(parts), stream())
+
+
 def bn1d_bwd_reduce(x, dz, mean, invstd, rows, G, C, parts):
     call("avd_bn1d_bwd_reduce", p(x), p(dz), p(mean), p(invstd), rows, G, C, p(parts), stream())
 

@@ -259,6 +259,43 @@ __global__ __launch_bounds__(256) void bn1d_bwd_reduce_kernel(
   p[1] = s2;
 }
 
+__device__ __forceinline__ float gelu_f(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_d(float z) {
+  return 0.5f * (1.f + erff(z * 0.70710678118654752f)) + z * 0.39894228040143268f * expf(-0.5f * z * z);
+}
+
+// act_bwd_kernel (act 1) + bn1d_bwd_reduce_kernel in one pass over the same grid as the reduce:
+// a thread owns column c of a CS_ROWS row chunk, forms dz exactly as act_bwd_kernel does (same
+// dropout hash of the flat index, same GELU derivative), stores it and folds it into the
+// chunk's partials in row order as bn1d_bwd_reduce_kernel does.
+__global__ __launch_bounds__(256) void bn1d_act_bwd_reduce_kernel(
+    const float* __restrict__ x, const float* __restrict__ dout, float* __restrict__ dz,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ mean, const float* __restrict__ invstd, int rpg, int G, int C, int R,
+    float p, unsigned long long seed, const unsigned long long* __restrict__ seed_off,
+    float* __restrict__ parts) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int r = blockIdx.y, g = blockIdx.z;
+  if (c >= C) return;
+  if (seed_off) seed += seed_off[0];
+  const float sc = scale[g * C + c], sf = shift[g * C + c];
+  const float mu = mean[g * C + c], is = invstd[g * C + c];
+  const int r0 = r * CS_ROWS, r1 = min(rpg, r0 + CS_ROWS);
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll 4
+  for (int row = r0; row < r1; ++row) {
+    const size_t o = ((size_t)g * rpg + row) * C + c;
+    const float v = x[o];
+    const float d = dout[o] * dropout_scale(seed, (unsigned long long)o, p) * gelu_d(fmaf(v, sc, sf));
+    dz[o] = d;
+    s1 += d;
+    s2 += d * (v - mu) * is;
+  }
+  float* q = parts + (((size_t)c * G + g) * R + r) * 2;
+  q[0] = s1;
+  q[1] = s2;
+}
+
 __global__ __launch_bounds__(256) void bn1d_bwd_apply_kernel(
     const float* __restrict__ x, const float* __restrict__ dz, const float* __restrict__ coef,
     float* __restrict__ dx, long long total, int rpg, int C) {
@@ -270,10 +307,6 @@ __global__ __launch_bounds__(256) void bn1d_bwd_apply_kernel(
   }
 }
 
-__device__ __forceinline__ float gelu_f(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_d(float z) {
-  return 0.5f * (1.f + erff(z * 0.70710678118654752f)) + z * 0.39894228040143268f * expf(-0.5f * z * z);
-}
 
 __global__ __launch_bounds__(256) void act_fwd_kernel(
     const float* __restrict__ x, float* __restrict__ out, int act, const float* __restrict__ scale,
@@ -543,6 +576,20 @@ int avd_bn1d_bwd_reduce(const float* x, const float* dz, const float* mean, cons
   dim3 grid(avd_cdiv(C, 256), R, G);
   bn1d_bwd_reduce_kernel<<<grid, 256, 0, avd_stream(stream)>>>(x, dz, mean, invstd, rpg, G, C, R,
                                                                parts);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+int avd_bn1d_act_bwd_reduce(const float* x, const float* dout, float* dz, const float* scale,
+                            const float* shift, const float* mean, const float* invstd, int rows,
+                            int G, int C, float p, unsigned long long seed,
+                            const unsigned long long* seed_off, float* parts, void* stream) {
+  if (!x || !dout || !dz || !scale || !shift || !mean || !invstd || !parts) return AVD_ERR_ARG;
+  if (rows <= 0 || G <= 0 || rows % G || C <= 0 || p < 0.f || p >= 1.f) return AVD_ERR_SHAPE;
+  const int rpg = rows / G, R = avd_colstats_parts(rpg);
+  dim3 grid(avd_cdiv(C, 256), R, G);
+  bn1d_act_bwd_reduce_kernel<<<grid, 256, 0, avd_stream(stream)>>>(
+      x, dout, dz, scale, shift, mean, invstd, rpg, G, C, R, p, seed, seed_off, parts);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

@@ -468,3 +468,28 @@ def test_linear_hwc_kernels_vs_float64(ops, rows, O, C, HW):
     assert rel(host(db), dout.double().sum(0).cpu().numpy()) < 1e-6
     dx_ref = (dd @ Wd).view(rows, C, HW).permute(0, 2, 1)
     assert rel(host(dx), dx_ref.cpu().numpy()) < 4e-3
+
+
+@pytest.mark.parametrize("rows,G,C,drop,dev_seed", [(6144, 1, 512, 0.3, False), (6144, 6, 256, 0.3, True),
+                                                   (1000, 2, 128, 0.0, False)])
+def test_bn1d_act_bwd_reduce_equals_two_launches(ops, rows, G, C, drop, dev_seed):
+    """The fused GELU/dropout backward + BatchNorm1d partials (ProjectionHead backward,
+    dino.py:1240-1254) is bit-identical to avd_act_bwd + avd_bn1d_bwd_reduce."""
+    g = torch.Generator(device="cuda").manual_seed(7)
+    h = torch.randn(rows, C, device="cuda", generator=g)
+    da = torch.randn(rows, C, device="cuda", generator=g)
+    mean = torch.randn(G * C, device="cuda", generator=g) * 0.1
+    invstd = torch.rand(G * C, device="cuda", generator=g) + 0.5
+    scale = torch.rand(G * C, device="cuda", generator=g) + 0.5
+    shift = torch.randn(G * C, device="cuda", generator=g) * 0.2
+    seed_off = torch.tensor([12345], dtype=torch.int64, device="cuda") if dev_seed else None
+    R = ops.colstats_parts(rows // G)
+    dz1, dz2 = torch.empty_like(h), torch.empty_like(h)
+    p1 = torch.empty(C * G * R * 2, device="cuda")
+    p2 = torch.empty_like(p1)
+    ops.act_bwd(h, da, dz1, 1, scale, shift, rows, G, C, drop, 99, seed_off)
+    ops.bn1d_bwd_reduce(h, dz1, mean, invstd, rows, G, C, p1)
+    ops.bn1d_act_bwd_reduce(h, da, dz2, scale, shift, mean, invstd, rows, G, C, drop, 99, p2, seed_off)
+    torch.cuda.synchronize()
+    assert torch.equal(dz1, dz2)
+    assert torch.equal(p1, p2)
