@@ -55,6 +55,14 @@ class Workspace:
 
 
 # ============================================================================ conv stacks
+def launch_layouts(batch, mxb):
+    """Every bf16 conv weight layout in one launch (16 per launch) and every MX one in another."""
+    for j in range(0, len(batch), 16):
+        ops.cl_weight_layout_batch(batch[j:j + 16])
+    for j in range(0, len(mxb), 16):
+        ops.mx_weight_layout_batch(mxb[j:j + 16])
+
+
 class ConvBranch:
     """[conv -> BN(train, per group) -> ReLU -> maxpool2] x L (+ (c,h,w) flatten or GAP) over
     channels-last maps, forward and backward (CentralUnimodalImage/Audio.forward,
@@ -82,10 +90,12 @@ class ConvBranch:
         return (self.fp8 and i > 0
                 and ops.mx_conv_serves(ci, self.dims[i][0], co, k, p, dgrad, N, None if dgrad else B))
 
-    def prepare(self, ws, store, tag, need_dgrad, N, B=None):
+    def prepare(self, ws, store, tag, need_dgrad, N, B=None, launch=True):
         """MFMA weight layouts for this step (the weights change every step), per layer:
         (bf16 forward rows, bf16 dgrad rows, MX forward (e4m3 rows, scales), MX dgrad).
-        B: BN group size of a training forward (None: eval, no partials)."""
+        B: BN group size of a training forward (None: eval, no partials).  launch=False: returns
+        (layouts, bf16 batch entries, MX batch entries) for the caller to launch together with
+        other branches' (``launch_layouts``)."""
         wts, batch, mxb = [], [], []
         for i, (ci, co, k, _p) in enumerate(self.stack.convs):
             w = store[self.stack.conv_keys[i] + ".weight"]
@@ -106,10 +116,9 @@ class ConvBranch:
                     wd = ws.get(f"{tag}.wd{i}", ops.cl_weight_elems(co, ci, k, 1), self.act)
                     batch.append((w, wd, 1))
             wts.append((wk, wd, q, qd))
-        if batch:       # every bf16 layout of the stack in one launch
-            ops.cl_weight_layout_batch(batch)
-        if mxb:         # and every MX layout in another
-            ops.mx_weight_layout_batch(mxb)
+        if not launch:
+            return wts, batch, mxb
+        launch_layouts(batch, mxb)
         return wts
 
     def _conv_fwd(self, i, h, wt, bias, y, parts, N, B, pivot=None):
@@ -172,11 +181,13 @@ class ConvBranch:
         """(channels, pooled pixels) of the last block: the hwc Linear's C and HW."""
         return self.stack.convs[-1][1], self.dims[-1][2] ** 2
 
-    def forward(self, ws, store, tag, x, N, G, update_running=True, need_dgrad=False):
+    def forward(self, ws, store, tag, x, N, G, update_running=True, need_dgrad=False, wts=None):
         """x: staged input [N,H,W,1] (act dtype).  Returns (features [N, F], ctx): f32 in the
-        reference's flatten order, or the NHWC pooled map (hwc)."""
+        reference's flatten order, or the NHWC pooled map (hwc).  wts: this call's layouts
+        from prepare(..., launch=False), already launched."""
         B = N // G
-        wts = self.prepare(ws, store, tag, need_dgrad, N, B)
+        if wts is None:
+            wts = self.prepare(ws, store, tag, need_dgrad, N, B)
         ctx = {"x": [x], "y": [], "stats": [], "wts": wts, "N": N, "G": G}
         h = x
         nl = len(self.stack.convs)
@@ -792,6 +803,18 @@ class MultiCentralEngine:
         if ent:
             ops.linear_weight_hwc(ent)
 
+    def _layouts(self, jobs):
+        """The conv weight layouts of several branch passes in one launch (per kind): jobs =
+        [(branch, ws, tag, need_dgrad, N, B)] -> each pass's layouts for ``forward(wts=...)``."""
+        out, batch, mxb = [], [], []
+        for cb, ws, tag, need_dgrad, N, B in jobs:
+            w, b, m = cb.prepare(ws, self.store, tag, need_dgrad, N, B, launch=False)
+            out.append(w)
+            batch += b
+            mxb += m
+        launch_layouts(batch, mxb)
+        return out
+
     def _linear_fwd(self, prefix, branch, cb, feat, cat, N, off):
         E = self.E
         lin = f"{prefix}.{self.img_lin if branch == 'img' else self.aud_lin}"
@@ -833,16 +856,17 @@ class MultiCentralEngine:
 
     # -------------------------------------------------------------- pieces
     def _encoder_fwd(self, prefix, ib, ab, x_img, x_aud, N, G, tag, need_dgrad, update_running=True,
-                     ws=None):
-        """Image + audio conv stacks and their Linear(., E) into one [N, 2E] buffer (= the cat)."""
+                     ws=None, wts=(None, None)):
+        """Image + audio conv stacks and their Linear(., E) into one [N, 2E] buffer (= the cat).
+        wts: the two branches' conv layouts when already launched (``_layouts``)."""
         ws, st, E = ws or self.ws, self.store, self.E
         cat = ws.get(tag + ".cat", N * 2 * E)
 
         # (the student's image branch on the side stream beside its audio branch measured slower:
         # 149.7k vs 152.4k pairs/s, r1_39 -- both fill the chip)
-        fi, ci = ib.forward(ws, st, tag + ".img", x_img, N, G, update_running, need_dgrad)
+        fi, ci = ib.forward(ws, st, tag + ".img", x_img, N, G, update_running, need_dgrad, wts=wts[0])
         self._linear_fwd(prefix, "img", ib, fi, cat, N, 0)
-        fa, ca = ab.forward(ws, st, tag + ".aud", x_aud, N, G, update_running, need_dgrad)
+        fa, ca = ab.forward(ws, st, tag + ".aud", x_aud, N, G, update_running, need_dgrad, wts=wts[1])
         self._linear_fwd(prefix, "aud", ab, fa, cat, N, E)
         return cat, (fi, ci, fa, ca)
 
@@ -981,13 +1005,14 @@ class MultiCentralEngine:
         ops.stage_views(g_aud.contiguous(), G, None, 0, None, B, 12544, x_aud)
         return x_img, x_aud, B, G
 
-    def _teacher_fwd(self, x_img, x_aud, B, G, seed_off=None):
+    def _teacher_fwd(self, x_img, x_aud, B, G, seed_off=None, wts=(None, None)):
         """Teacher: global views, train-mode BN, no grad, into t_proj [G*B, P] (its workspace)."""
         tws, st = self.tws, self.store
         base = (self.seed * 1000003) & SEED_MASK
         ops.mark("t.begin")
         tcat, _ = self._encoder_fwd("teacher", self.t_img, self.t_aud, x_img[:G * B * 784],
-                                    x_aud[:G * B * 12544], G * B, G, "t", need_dgrad=False, ws=tws)
+                                    x_aud[:G * B * 12544], G * B, G, "t", need_dgrad=False, ws=tws,
+                                    wts=wts)
         tout, _ = self._fusion_fwd("teacher", tcat, G * B, "t", base + 2, ws=tws, seed_off=seed_off)
         t_proj = tws.get("t_proj", G * B * self.P)
         self.tproj.forward(tws, st, "tp", tout, G * B, t_proj, 0.0, 0)
@@ -1034,6 +1059,12 @@ class MultiCentralEngine:
         # this step's bf16 (h, w, c) copies of the encoder Linears (student; teacher unless its
         # forward already ran under the previous step)
         self._prepare_hwc(("student",) if teacher_ready else ("student", "teacher"))
+        # and the student's (and teacher's) conv weight layouts, all in one launch
+        jobs = [(self.img, ws, "s.img", training, N, B), (self.aud, ws, "s.aud", training, N, B)]
+        if not teacher_ready:
+            jobs += [(self.t_img, self.tws, "t.img", False, G * B, B),
+                     (self.t_aud, self.tws, "t.aud", False, G * B, B)]
+        lw = self._layouts(jobs)
 
         # teacher: global views (prefix of the staged buffers), train-mode BN, no grad -- on a
         # side stream, concurrently with the student (independent until the loss); pipelined
@@ -1041,10 +1072,11 @@ class MultiCentralEngine:
         if teacher_ready:
             t_proj, t_done = self.tws.get("t_proj", G * B * P), None
         else:
-            t_proj, t_done = self._on_side(lambda: self._teacher_fwd(x_img, x_aud, B, G))
+            t_proj, t_done = self._on_side(lambda: self._teacher_fwd(x_img, x_aud, B, G,
+                                                                     wts=(lw[2], lw[3])))
         # student: all views (+ originals) in one pass per conv layer
         cat, senc = self._encoder_fwd("student", self.img, self.aud, x_img, x_aud, N, NG, "s",
-                                      need_dgrad=training)
+                                      need_dgrad=training, wts=(lw[0], lw[1]))
         loss_parts = ws.get("loss_parts", V * B + B)
         head_out = None
         hctx = None
