@@ -670,10 +670,7 @@ Plan plan_for(int M, int N, int K) {
     Plan p{128, 256, 1, K};
     const long long t = tiles(128, 256);
     // split target in blocks (112 / 448 / 896 measured slower, profiles/r3_gemm_ab_n256.txt)
-#ifndef GEMM_T256
-#define GEMM_T256 224
-#endif
-    constexpr int target256 = GEMM_T256;
+    constexpr int target256 = 224;
     const int s = (int)std::max(1ll, std::min<long long>(avd_cdiv(target256, t), K / 128));
     if (s > 1) {
       p.kchunk = avd_cdiv(avd_cdiv(K, s), 64) * 64;   // whole k-tiles of either mode
@@ -688,14 +685,9 @@ Plan plan_for(int M, int N, int K) {
     p = (M >= 128 && N >= 128) ? Plan{128, 128, 1, K} : (M >= 128 ? Plan{128, 64, 1, K} : p);
   const long long t = tiles(p.bm, p.bn);
   // split target (blocks) and minimum K rows per split (512 / 256: the best of 128-2048 /
-  // 64-256, profiles/r3_gemm_ab.txt)
-#ifndef GEMM_TGT
-#define GEMM_TGT 512
-#endif
-#ifndef GEMM_KMIN
-#define GEMM_KMIN 256
-#endif
-  constexpr int target = GEMM_TGT, kmin = GEMM_KMIN;
+  // 64-256, profiles/r3_gemm_ab.txt; re-measured with 64-wide k-tiles against kmin 128 / 512
+  // and target 1024, profiles/r5j_gemm_plan_ab.txt)
+  constexpr int target = 512, kmin = 256;
   if (t < 224 && K >= 512) {
     int s = (int)std::min<long long>(avd_cdiv(target, t), K / kmin);
     s = std::max(1, std::min(s, 128));
