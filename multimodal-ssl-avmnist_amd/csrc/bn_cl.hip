@@ -182,6 +182,42 @@ __device__ __forceinline__ void load_gout(const void* __restrict__ gout, int mod
 }
 
 // ------------------------------------------------------------------------------ backward
+// Fixed-order fold of the block's per-thread partials sh[slot * CV + cv][2e + k] over its slots
+// into parts[c][g][r][2].  When the C*2 outputs divide the block, every thread sums one
+// contiguous segment of one output's slots and one thread per output adds the segments in
+// order (a 32-output block used to leave 224 threads idle while 32 walked 128 slots each);
+// otherwise one thread per output walks all slots.
+template <int V>
+__device__ __forceinline__ void fold_slots(float (*sh)[2 * V + 1], int C, int slots, float* parts,
+                                           int G, int g, int R, int r) {
+  const int CV = C / V, no = 2 * C;
+  if (no <= 256 && 256 % no == 0) {
+    __shared__ float red[256];
+    const int tpo = 256 / no;
+    const int o = threadIdx.x % no, q = threadIdx.x / no;
+    const int c = o >> 1, k = o & 1, ocv = c / V, e = c % V;
+    const int seg = (slots + tpo - 1) / tpo;
+    const int s0 = q * seg, s1 = min(slots, s0 + seg);
+    float t = 0.f;
+    for (int s = s0; s < s1; ++s) t += sh[s * CV + ocv][2 * e + k];
+    red[q * no + o] = t;
+    __syncthreads();
+    if ((int)threadIdx.x < no) {
+      float u = 0.f;
+      for (int j = 0; j < tpo; ++j) u += red[j * no + o];
+      parts[(((size_t)c * G + g) * R + r) * 2 + k] = u;
+    }
+    return;
+  }
+  for (int o = threadIdx.x; o < no; o += 256) {
+    const int c = o >> 1, k = o & 1;
+    const int ocv = c / V, e = c % V;
+    float t = 0.f;
+    for (int s = 0; s < slots; ++s) t += sh[s * CV + ocv][2 * e + k];
+    parts[(((size_t)c * G + g) * R + r) * 2 + k] = t;
+  }
+}
+
 // Partial sums over (samples of the group, windows) per channel: parts[c][g][r][2] =
 // (sum dz, sum dz * xhat) with dz the ReLU/pool-routed gradient at the window's argmax.
 // Block (r, g) covers windows [r*per, (r+1)*per) of group g; thread = (window slot, vector).
@@ -231,14 +267,7 @@ __global__ __launch_bounds__(256) void bwd_reduce_cl_kernel(
     sh[threadIdx.x][2 * e + 1] = s2[e];
   }
   __syncthreads();
-  // fixed-order fold over the slots: thread (cv, e, k) for C*2 outputs
-  for (int o = threadIdx.x; o < C * 2; o += 256) {
-    const int c = o >> 1, k = o & 1;
-    const int ocv = c / V, e = c % V;
-    float t = 0.f;
-    for (int s = 0; s < slots; ++s) t += sh[s * CV + ocv][2 * e + k];
-    parts[(((size_t)c * G + g) * R + r) * 2 + k] = t;
-  }
+  fold_slots<V>(sh, C, slots, parts, G, g, R, r);
 }
 
 // The same partial sums from the POOLED output p = max_k relu(y_k*scale + shift) (the next
@@ -350,13 +379,7 @@ __global__ __launch_bounds__(256) void bwd_reduce_pooled_cl_kernel(
     sh[threadIdx.x][2 * e + 1] = s2[e];
   }
   __syncthreads();
-  for (int o = threadIdx.x; o < C * 2; o += 256) {
-    const int c = o >> 1, k = o & 1;
-    const int ocv = c / V, e = c % V;
-    float t = 0.f;
-    for (int s = 0; s < slots; ++s) t += sh[s * CV + ocv][2 * e + k];
-    parts[(((size_t)c * G + g) * R + r) * 2 + k] = t;
-  }
+  fold_slots<V>(sh, C, slots, parts, G, g, R, r);
 }
 
 __device__ __forceinline__ float to_f(bf16 v) { return bf2f(v); }
