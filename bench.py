@@ -95,7 +95,9 @@ def load_traffic(path, key):
             tab = json.load(f)
     except (OSError, ValueError):
         return None
-    e = tab.get(key)
+    # (the bytes of a launch do not depend on the stream it was issued on)
+    base = key.replace(" @side", "")
+    e = tab.get(key) or tab.get(base) or tab.get(base + " @side")
     return None if e is None else e.get("traffic_bytes")
 
 

@@ -470,6 +470,10 @@ class ConvBranch:
     # (160.2k vs 166.7k), weight gradients on the main stream or deferred after the input-gradient
     # chain (within noise).
 
+    # layers whose weight gradient runs on the input-gradient (main) stream even when a
+    # weight-gradient stream is given
+    WGRAD_MAIN = frozenset()
+
     def backward(self, ws, store, ctx, dfeat, wstream=None):
         """dfeat: gradient of the features (f32 [N, F]; hwc: NHWC act dtype); writes conv/BN
         parameter grads.
@@ -516,7 +520,7 @@ class ConvBranch:
             nch = self._wgrad_chunks(i, N)
             dy = ws.get(f"bwd_dy{i}" if wstream is not None else "bwd_dy", N * Ho * Ho * co, self.act)
             ops.cl_bn_bwd_apply(y, gout, mode, st[2], st[3], coef, dy, N, B, co, Ho, Ho)
-            if wstream is not None and i > 0:
+            if wstream is not None and i > 0 and i not in self.WGRAD_MAIN:
                 wparts = ws.get(f"wgrad_parts{i}", nch * co * ci * k * k)
                 wstream.wait_stream(main)
                 with torch.cuda.stream(wstream):
@@ -529,8 +533,10 @@ class ConvBranch:
                 wdone.append(ev)
             else:
                 wparts = ws.get("wgrad_parts", nch * co * ci * k * k)
+                ops.mark(f"w{i}.begin")
                 self._conv_wgrad(i, x, dy, wparts, N)
                 ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
+                ops.mark(f"w{i}.end")
             if i > 0:
                 dx = ws.get("bwd_dx", N * H * H * ci, self.act)
                 self._conv_dgrad(i, dy, ctx["wts"][i], dx, N)
