@@ -471,8 +471,11 @@ class ConvBranch:
     # chain (within noise).
 
     # layers whose weight gradient runs on the input-gradient (main) stream even when a
-    # weight-gradient stream is given
-    WGRAD_MAIN = frozenset()
+    # weight-gradient stream is given: the audio 28^2 / 14^2 layers.  Same step time as all on
+    # the third stream (3 interleaved rounds: 5.018-5.051 vs 5.012-5.026 ms,
+    # profiles/r5n_wgrad_main_ab.txt), but their launches no longer share the CUs with two other
+    # streams' kernels (the 14^2 one ran 640-650 us in the graph beside them, 153 us alone)
+    WGRAD_MAIN = frozenset({2, 3})
 
     def backward(self, ws, store, ctx, dfeat, wstream=None):
         """dfeat: gradient of the features (f32 [N, F]; hwc: NHWC act dtype); writes conv/BN
