@@ -30,6 +30,8 @@ pixel output is "parity unpinned"; the kernel's pixel maths is pinned by oracle/
 """
 import math
 
+import collections
+
 import numpy as np
 import torch
 
@@ -294,6 +296,7 @@ class ViewAugmenter:
         # parameters drawn by avd_augment_records (default) or by numpy on the host
         self.device_params = device_params
         self._stage_cache = {}
+        self._pinned = collections.deque(maxlen=64)    # host ids of in-flight transfers
 
     def records_dev(self, chain, B, n_views, group=4):
         """(rec [B*n_views, REC], gm [B*n_views, words] or None) drawn on the device."""
@@ -350,10 +353,16 @@ class ViewAugmenter:
         shape = (B, n_views, 1, self.H, self.W) if order == 0 else (n_views, B, 1, self.H, self.W)
         if out is None:
             out = torch.empty(shape, dtype=torch.float32, device=dev)
-        # pinned + non-blocking: a data-stream prefetch must not block the host on that stream
+        # pinned + non-blocking: a data-stream prefetch must not block the host on that stream.
+        # The pinned copy of the ids is also held here for a while: a prefetch's transfer runs
+        # only once its data stream's wait is over, possibly after this call has returned
         idx_t = torch.from_numpy(idx)
-        idx_d = (idx_t.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda"
-                 else idx_t.to(dev))
+        if dev.type == "cuda":
+            pin = idx_t.pin_memory()
+            self._pinned.append(pin)
+            idx_d = pin.to(dev, non_blocking=True)
+        else:
+            idx_d = idx_t.to(dev)
         if on_dev:
             rec_d, gm_d = rec, gm
         else:

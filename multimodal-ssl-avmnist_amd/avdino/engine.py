@@ -774,11 +774,10 @@ class MultiCentralEngine:
         self.pipeline = False
         self.tside = None
         # real-data input prefetch (prefetch()): data stream, the staging buffer set in use (0/1),
-        # the pending prefetch (batch, set, done event, staged) and the "other set is free" event
+        # the pending prefetch (batch, set, done event, staged)
         self.dstream = None
         self._par = 0
         self._pf = None
-        self._ev_free = None
         self._t_ready = None       # (batch, B, G) of the teacher output waiting in t_proj
         self.tin_pending = None    # the next batch's teacher inputs while its forward is queued
         self._tseed = None
@@ -920,13 +919,15 @@ class MultiCentralEngine:
         par = 1 - self._par
         if self.dstream is None:
             self.dstream = torch.cuda.Stream(self.store.device)
-        # the other buffers were last read by the step before the current one: free once the
-        # main stream is past the event stage() recorded in front of the current step
-        free = self._ev_free
-        if free is not None:
-            self.dstream.wait_event(free)
-        else:
-            self.dstream.wait_stream(torch.cuda.current_stream(self.store.device))
+        # The other buffers were last read by the step before the current one, so the data
+        # stream could start once the main stream is past the event stage() recorded in front
+        # of the current step and overlap the current step.  That overlap made the
+        # prefetched steps differ from the serial ones in about 1 of 3 graph-replayed runs
+        # (tests/test_gpu_augment.py; root cause not found: no kernel of the step writes outside
+        # its buffers into the staging set, tools/dbg_oob.py), so the data stream waits for the
+        # whole step queued so far: the host-side work of the next batch stays hidden, its GPU
+        # work runs after the step.
+        self.dstream.wait_stream(torch.cuda.current_stream(self.store.device))
         with_orig = self.heads is not None
         staged = self._aug_bufs(batch, with_orig, par)      # allocated outside the data stream
         with torch.cuda.stream(self.dstream):
@@ -984,11 +985,6 @@ class MultiCentralEngine:
         if self.mode == "semi_supervised":
             labels = ws.get("in.label" + ("" if self._par == 0 else ".1"), B, torch.int64)
             labels.copy_(batch["label"].reshape(-1))
-        if main is not None and training:
-            # everything queued on the main stream after this point reads THIS buffer set: the
-            # other one is free for a prefetch once the main stream passes here
-            self._ev_free = torch.cuda.Event()
-            self._ev_free.record(main)
         return x_img, x_aud, B, G, L, labels
 
     def reset_pipeline(self):

@@ -1,0 +1,75 @@
+"""Debug helper: tests/test_gpu_augment.py::test_prefetched_augmentation_steps_equal_serial_steps
+(graph=True) under engine attribute overrides; prints both loss curves."""
+import os
+import sys
+import tempfile
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "multimodal-ssl-avmnist_amd"))
+import torch  # noqa: E402
+
+from tests.test_gpu_augment import _fake_avmnist  # noqa: E402
+from avdino import engine as EN  # noqa: E402
+from avdino.data import AVMNISTDinoLoader  # noqa: E402
+from avdino.params import ParamStore  # noqa: E402
+from avdino.spec import multimodal_dino_sd  # noqa: E402
+
+
+def run(graph, attrs):
+    for k, v in attrs.items():
+        cls, a = k.split(".")
+        setattr(getattr(EN, cls), a, v)
+    root = _fake_avmnist(__import__("pathlib").Path(tempfile.mkdtemp()), n=40)
+    E, D, P = 32, 32, 16
+    res = []
+    for pre in (False, True):
+        ld = AVMNISTDinoLoader(root, batch_size=8, train_size=36, val_size=4, seed=3,
+                               multimodal_mode="semi_supervised", device="cuda", staged=True)
+        batches = list(ld)[:4] * 2
+        store = ParamStore(multimodal_dino_sd("semi_supervised", E, D, P), "cuda:0", seed=1)
+        eng = EN.MultiCentralEngine(store, "semi_supervised", E, D, P,
+                                    EN.Hyper(dropout=0.0, fusion_dropout=0.0), act_dtype=torch.bfloat16)
+        eng.use_graph = graph
+        eng.graph.warmup = 1
+        losses, ins = [], []
+        for i, b in enumerate(batches):
+            nxt = batches[i + 1] if (pre and i + 1 < len(batches)) else None
+            losses.append(eng.step(b, next_batch=nxt).item())
+            torch.cuda.synchronize()
+            sfx = "" if eng._par == 0 else ".1"
+            ins.append((eng.ws.bufs["in.img" + sfx].float().clone(), eng.ws.bufs["in.aud" + sfx].float().clone(),
+                        eng.ws.bufs["in.label" + sfx].clone(), store.student.clone()))
+        res.append((losses, ins))
+    (l0, i0), (l1, i1) = res
+    first = next((k for k in range(len(l0)) if l0[k] != l1[k]), None)
+    inp = [k for k in range(len(l0)) if not (torch.equal(i0[k][0], i1[k][0]) and torch.equal(i0[k][1], i1[k][1]))]
+    lab = [k for k in range(len(l0)) if not torch.equal(i0[k][2], i1[k][2])]
+    par = [k for k in range(len(l0)) if not torch.equal(i0[k][3], i1[k][3])]
+    nv = 2 + 4 + 1  # the test's loader: 2 global + 4 local views + the originals
+    det = {}
+    for k in inp:
+        for m, j in (("img", 0), ("aud", 1)):
+            a, b = i0[k][j].view(nv, -1), i1[k][j].view(nv, -1)
+            det[(k, m)] = [v for v in range(a.shape[0]) if not torch.equal(a[v], b[v])]
+    print("  view diffs", det, flush=True)
+    print(attrs, graph, "equal" if l0 == l1 else "DIFF", "first loss diff", first, "input diffs", inp,
+          "label diffs", lab, "param diffs after step", par, flush=True)
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "nolayouts":
+        # the round-4 placement: every branch pass launches its own layouts
+        EN.MultiCentralEngine._layouts = lambda self, jobs: [None] * len(jobs)
+    graph = not (len(sys.argv) > 1 and sys.argv[1] == "eager")
+    if "waitmain" in sys.argv:
+        orig = EN.MultiCentralEngine.prefetch
+
+        def pf(self, batch):
+            self._ev_free = None      # -> the data stream waits for everything queued on main
+            return orig(self, batch)
+        EN.MultiCentralEngine.prefetch = pf
+    if "nopin" in sys.argv:
+        torch.Tensor.pin_memory = lambda self, *a, **k: self
+    for _ in range(4):
+        run(graph, {})
