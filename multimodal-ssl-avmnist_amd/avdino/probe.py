@@ -20,7 +20,8 @@ activation dtype.  Per-batch losses stay on the device (no host sync inside the 
 import torch
 
 from . import ops
-from .engine import F32, ConvBranch, UniEncoder, Workspace
+from .capture import GraphedStep
+from .engine import F32, ConvBranch, StepState, UniEncoder, Workspace
 from .params import ParamStore
 from .spec import MULTI_ENCODERS, UNI_ALIASES, UNI_ENCODERS
 
@@ -48,7 +49,7 @@ class _MultiEncoder:
         self.aud = ConvBranch(astack("student"), act)
         self.ilin, self.alin = "student." + ilin, "student." + alin
 
-    def __call__(self, ws, st, x_img, x_aud, N, train, seed):
+    def __call__(self, ws, st, x_img, x_aud, N, train, seed, seed_off=None):
         E = self.E
         if train:
             fi, _ = self.img.forward(ws, st, "pi", x_img, N, 1, True, False)
@@ -66,7 +67,7 @@ class _MultiEncoder:
         ops.linear_fwd(cat, st["student.fusion.0.weight"], st["student.fusion.0.bias"], h, N,
                        x_ld=2 * E, mode=self.gm)
         r = ws.get("p.fr", N * E)
-        ops.act_fwd(h, r, 0, None, None, N, 1, E, self.p if train else 0.0, seed)
+        ops.act_fwd(h, r, 0, None, None, N, 1, E, self.p if train else 0.0, seed, seed_off)
         out = ws.get("p.feat", N * self.D)
         ops.linear_fwd(r, st["student.fusion.3.weight"], st["student.fusion.3.bias"], out, N,
                        mode=self.gm)
@@ -94,7 +95,7 @@ class LinearProbe:
     """
 
     def __init__(self, source, kind, D, E=None, lr=1e-4, weight_decay=0.01, act_dtype=F32,
-                 fusion_dropout=0.3, seed=0, classifier_state=None):
+                 fusion_dropout=0.3, seed=0, classifier_state=None, use_graph=True):
         dev = source.device
         self.store = ParamStore(source.spec, dev, has_teacher=source.teacher is not None)
         self.store.student.copy_(source.student)          # copy.deepcopy(model.student)
@@ -118,14 +119,23 @@ class LinearProbe:
         self.lr, self.wd = lr, weight_decay
         self.t = 0
         self.seed = seed
+        # step count, AdamW bias corrections and the dropout counter offset on the device, so a
+        # training batch is one replayable hipGraph (a 128-sample batch is launch-bound: ~50
+        # launches, 0.65 ms issued eagerly); the ragged last batch of an epoch runs eagerly
+        self.sstate = StepState(dev, lr, (0.9, 0.999)) if dev.type == "cuda" else None
+        self.use_graph = use_graph and dev.type == "cuda"
+        self.graph = (GraphedStep(warmup=2, deps=lambda: (ops.alloc_epoch(), self.ws.epoch))
+                      if self.use_graph else None)
 
-    def _features(self, images, audios, train):
-        ws, N = self.ws, images.shape[0]
+    def _features(self, images, audios, train, seed_off=None):
+        ws, N = self.ws, (images if images is not None else audios).shape[0]
         if self.multimodal:
             xi = ws.get("p.in.img", N * 784, self.act)
             xa = ws.get("p.in.aud", N * 12544, self.act)
             ops.stage_views(images.contiguous(), 1, None, 0, None, N, 784, xi)
             ops.stage_views(audios.contiguous(), 1, None, 0, None, N, 12544, xa)
+            if seed_off is not None:      # device counter: seed + t * StepState.SEED_STRIDE
+                return self.enc(ws, self.store, xi, xa, N, train, self.seed * 7919, seed_off)
             return self.enc(ws, self.store, xi, xa, N, train, self.seed * 7919 + self.t)
         src, HW = (images, 784) if self.modality == "image" else (audios, 12544)
         x = ws.get("p.in.x", N * HW, self.act)
@@ -143,10 +153,36 @@ class LinearProbe:
         return h, r, logits
 
     def train_batch(self, images, audios, labels, loss_out):
-        """One classifier step; loss_out: 1-element device slot for this batch's mean CE."""
+        """One classifier step; loss_out: 1-element device slot for this batch's mean CE.
+        With ``use_graph`` the batch is copied into fixed buffers and the step replayed as a
+        hipGraph per batch size (after two eager batches of that size)."""
+        if self.sstate is not None:
+            self.sstate.set_lr(self.lr)   # (a host-side schedule change; eager)
+        if not self.use_graph:
+            self._train_step(images, audios, labels, loss_out)
+            return
+        ws = self.ws
+
+        def fixed(name, t):
+            if t is None:
+                return None
+            b = ws.get(name, t.numel(), t.dtype).view_as(t)
+            b.copy_(t)
+            return b
+        bi, ba, bl = fixed("p.src.img", images), fixed("p.src.aud", audios), fixed("p.src.lab", labels)
+        slot = ws.get("p.loss", 1)
+        key = tuple(None if t is None else (tuple(t.shape), t.dtype) for t in (images, audios, labels))
+        self.graph.run(key, lambda: self._train_step(bi, ba, bl, slot))
+        loss_out.copy_(slot)
+
+    def _train_step(self, images, audios, labels, loss_out):
         ws, c = self.ws, self.cls
-        N = images.shape[0]
-        feat = self._features(images, audios, True)
+        N = (images if images is not None else audios).shape[0]
+        dev_state = self.sstate is not None
+        if dev_state:
+            self.sstate.begin()           # t += 1, bias corrections, dropout offset
+        feat = self._features(images, audios, True,
+                              self.sstate.seed_off if dev_state and self.multimodal else None)
         h, r, logits = self._logits(feat, N)
         parts, dl = ws.get("p.parts", N), ws.get("p.dl", N * 10)
         ops.softmax_xent(logits, 10, N, 10, labels, 0, False, False, 1.0 / N, parts, dl, 10, False)
@@ -158,10 +194,14 @@ class LinearProbe:
         ops.act_bwd(h, dr, dh, 0, None, None, N, 1, 128, 0.0, 0)
         ops.linear_bwd(dh, feat, c["classifier.0.weight"], c.grad_of("classifier.0.weight"),
                        c.grad_of("classifier.0.bias"), None, N)
-        self.t += 1
+        self.t += 1                       # (host count; not read by a captured step)
         b1, b2 = 0.9, 0.999
-        ops.adamw(c.student, c.grad, c.adam_m, c.adam_v, c.n_live, self.lr, b1, b2, 1e-8, self.wd,
-                  1 - b1 ** self.t, 1 - b2 ** self.t)
+        if dev_state:
+            ops.adam_dev(c.student, c.grad, c.adam_m, c.adam_v, c.n_live, self.sstate.hyp, b1, b2,
+                         1e-8, self.wd, decoupled=True)
+        else:
+            ops.adamw(c.student, c.grad, c.adam_m, c.adam_v, c.n_live, self.lr, b1, b2, 1e-8,
+                      self.wd, 1 - b1 ** self.t, 1 - b2 ** self.t)
 
     def evaluate(self, batches):
         """evaluate() (dino.py:913-947): eval-mode copy; returns (mean loss, accuracy %, logits)."""

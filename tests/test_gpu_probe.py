@@ -76,3 +76,35 @@ def test_linear_probe_matches_oracle(case):
                         "student.projection.0.weight"]),
                state["student.fusion.0.weight" if kind == "multi_central" else
                      "student.projection.0.weight"]) == 0
+
+
+def test_probe_graph_replay_equals_eager():
+    """The probe's training batches replayed as hipGraphs (fixed input buffers, device step
+    count / bias corrections / dropout offset) equal the eager batches bit for bit, with the
+    fusion dropout on and a ragged last batch (run eagerly)."""
+    from avdino.params import ParamStore
+    from avdino.probe import LinearProbe
+    from avdino.spec import multimodal_dino_sd
+    kind, E, D, P = "multi_central", 32, 32, 16
+    state = make_state(OS.multimodal_dino_spec("default", E, D, P), 211)
+    cls = make_state(OS.classifier_spec(D), 212)
+    batches = [make_multimodal_batch(8 if i < 6 else 5, 1, 0, 2100 + i) for i in range(7)]
+
+    def dev(b):
+        return (torch.from_numpy(b["image"]).cuda(), torch.from_numpy(b["audio"]).cuda(),
+                torch.from_numpy(b["label"]).cuda())
+
+    outs = []
+    for use_graph in (False, True):
+        src = ParamStore(multimodal_dino_sd("default", E, D, P), "cuda")
+        src.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state.items()})
+        probe = LinearProbe(src, kind, D, E, lr=LR, fusion_dropout=0.3, use_graph=use_graph,
+                            classifier_state={k: torch.from_numpy(v) for k, v in cls.items()})
+        out = probe.run_epoch([dev(b) for b in batches], [dev(b) for b in batches[:2]])
+        outs.append((out, probe.cls.student.clone(), probe.store.buf_arena.clone()))
+        if use_graph:
+            assert probe.graph.captures >= 1
+    (o0, c0, b0), (o1, c1, b1) = outs
+    assert torch.equal(o0["train_losses"], o1["train_losses"])
+    assert o0["eval_loss"] == o1["eval_loss"] and o0["mlp_acc"] == o1["mlp_acc"]
+    assert torch.equal(c0, c1) and torch.equal(b0, b1)
