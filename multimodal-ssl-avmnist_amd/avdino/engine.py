@@ -778,6 +778,7 @@ class MultiCentralEngine:
         self.dstream = None
         self._par = 0
         self._pf = None
+        self._ev_free = None
         self._t_ready = None       # (batch, B, G) of the teacher output waiting in t_proj
         self.tin_pending = None    # the next batch's teacher inputs while its forward is queued
         self._tseed = None
@@ -895,6 +896,9 @@ class MultiCentralEngine:
     # the next real-data batch's device augmentation queued on a data stream under the current
     # step (prefetch); False stages every batch synchronously
     PREFETCH = True
+    # the prefetch's data stream starts once the previous step's reads are done (overlapping the
+    # current step) instead of after the current step: off, see prefetch()
+    PREFETCH_OVERLAP = False
 
     def _aug_bufs(self, batch, with_orig, par):
         """Staged-input buffers of set ``par`` (0/1) for a {"aug", "idx"} batch:
@@ -921,13 +925,17 @@ class MultiCentralEngine:
             self.dstream = torch.cuda.Stream(self.store.device)
         # The other buffers were last read by the step before the current one, so the data
         # stream could start once the main stream is past the event stage() recorded in front
-        # of the current step and overlap the current step.  That overlap made the
-        # prefetched steps differ from the serial ones in about 1 of 3 graph-replayed runs
-        # (tests/test_gpu_augment.py; root cause not found: no kernel of the step writes outside
-        # its buffers into the staging set, tools/dbg_oob.py), so the data stream waits for the
-        # whole step queued so far: the host-side work of the next batch stays hidden, its GPU
-        # work runs after the step.
-        self.dstream.wait_stream(torch.cuda.current_stream(self.store.device))
+        # of the current step and overlap the current step (PREFETCH_OVERLAP).  That overlap made
+        # graph-replayed prefetched steps differ from the serial ones in about 1 of 3 runs
+        # (tests/test_gpu_augment.py, tools/dbg_prefetch.py: one audio global view of the
+        # prefetched batch differs; no kernel of the step writes into the staging set,
+        # tools/dbg_oob.py; blocking id copies made it rarer, not gone).  Off: the data stream
+        # waits for the whole step queued so far -- the next batch's host work stays hidden,
+        # its GPU work runs after the step.
+        if self.PREFETCH_OVERLAP and self._ev_free is not None:
+            self.dstream.wait_event(self._ev_free)
+        else:
+            self.dstream.wait_stream(torch.cuda.current_stream(self.store.device))
         with_orig = self.heads is not None
         staged = self._aug_bufs(batch, with_orig, par)      # allocated outside the data stream
         with torch.cuda.stream(self.dstream):
@@ -985,6 +993,9 @@ class MultiCentralEngine:
         if self.mode == "semi_supervised":
             labels = ws.get("in.label" + ("" if self._par == 0 else ".1"), B, torch.int64)
             labels.copy_(batch["label"].reshape(-1))
+        if main is not None and training and self.PREFETCH_OVERLAP:
+            self._ev_free = torch.cuda.Event()
+            self._ev_free.record(main)
         return x_img, x_aud, B, G, L, labels
 
     def reset_pipeline(self):
