@@ -896,6 +896,20 @@ __global__ __launch_bounds__(256) void c1r3_codes_combine_kernel(
 
 }  // namespace
 
+namespace avd {
+// the pixel-major forward passes of the 3x3 1 -> 32 layer (c1s3.hip)
+bool c1s3_serves(int N, int B, int H, int W, int Cout);
+int c1s3_stats_rows(int N, int B, int W);
+int c1s3_stats(const void* x, const void* wk, const float* bias, float* out, int N, int B, int W,
+               hipStream_t st);
+int c1s3_apply_codes(const void* x, const void* wk, const float* bias, const float* scale,
+                     const float* shift, void* z, unsigned short* codes, int N, int B, int W,
+                     hipStream_t st);
+int c1s3_moments_rows(int N, int B, int H, int W, int Cout);
+int c1s3_moments(const void* x, const void* gz, const unsigned short* codes, float* out, int N, int B,
+                 int W, hipStream_t st);
+}  // namespace avd
+
 extern "C" {
 
 int avd_c1r3_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad);
@@ -911,6 +925,7 @@ int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, 
 int avd_cl_c1r3_codes_rows(int N, int B, int H, int W, int Cout) {
   if (Cout != 32 || B <= 0 || N % B || N / B > C1R3_GMAX) return 0;
   if (!avd_c1r3_rows(4, AVD_BF16, N, B, 1, H, W, Cout, 3, 1)) return 0;
+  if (const int r = c1s3_moments_rows(N, B, H, W, Cout)) return r;     // 28^2 / 112^2: c1s3.hip
   return 4 * c1r3_grid(5, Cout, 3);
 }
 
@@ -929,6 +944,7 @@ int avd_cl_c1r3_moments_codes(const void* x, const void* wk, const void* gz, con
                               float* out, int N, int B, int H, int W, int Cout, void* stream) {
   if (!x || !wk || !gz || !codes || !out) return AVD_ERR_ARG;
   if (!avd_cl_c1r3_codes_rows(N, B, H, W, Cout)) return AVD_ERR_SHAPE;
+  if (c1s3_moments_rows(N, B, H, W, Cout)) return c1s3_moments(x, gz, codes, out, N, B, W, avd_stream(stream));
   return avd_c1r3_launch(5, x, wk, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, gz, nullptr, out,
                          N, B, H, W, Cout, 3, avd_stream(stream), const_cast<unsigned short*>(codes));
 }
@@ -959,6 +975,8 @@ int avd_c1r3_rows(int pass, int dt, int N, int B, int Cin, int H, int W, int Cou
   if (TR != TRW && ((W > 32) || Cout > 32)) return 0;   // whole-sample tiles: gz staging bound
   if ((TR + K - 1) * (W % 8 ? W / 4 : W / 8) > 256) return 0;                // one x vector per thread
   if (c1r3_lds(3, Cout, W, K, TR) > 80 * 1024 || c1r3_lds(4, Cout, W, K, TR) > 80 * 1024) return 0;   // every pass, or none
+  // 3x3 1 -> 32 at 28^2 / 112^2: statistics on the pixel-major pass (c1s3.hip)
+  if (K == 3 && pass == 0 && c1s3_serves(N, B, H, W, Cout)) return c1s3_stats_rows(N, B, W);
   const int grid = c1r3_grid(pass, Cout, K);
   return pass == 1 ? 1 : pass == 3 ? grid : 4 * grid;   // pass 4: rows R of both its outputs
 }
@@ -967,6 +985,11 @@ int avd_c1r3_launch(int pass, const void* x, const void* wk, const float* bias, 
                     const float* shift, const float* mean, const float* invstd, const float* coef,
                     const void* gz, void* z, float* out, int N, int B, int H, int W, int Cout, int K,
                     hipStream_t st, unsigned short* codes) {
+  if (K == 3 && (pass == 0 || pass == 1) && c1s3_serves(N, B, H, W, Cout)) {
+    // the pixel-major passes (c1s3.hip): one pooling window per lane
+    if (pass == 0) return c1s3_stats(x, wk, bias, out, N, B, W, st);
+    return c1s3_apply_codes(x, wk, bias, scale, shift, z, codes, N, B, W, st);
+  }
   const int grid = c1r3_grid(pass, Cout, K);
   const int TR = c1r3_tr(H, W);
   const size_t lds = c1r3_lds(pass, Cout, W, K, TR);

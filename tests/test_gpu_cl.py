@@ -250,7 +250,7 @@ def test_cl_bn_bwd_apply_wgrad_fused_first_layer(ops, HN):
                                 (48, 6, 32, 3, 1), (8, 4, 16, 3, 1),
                                 # widths 4 mod 8 (virtual columns) and the 5x5 CentralNet image
                                 # conv1 (1->32 at 28^2, unimodal.py:127-141)
-                                (28, 6, 32, 3, 1), (28, 6, 32, 5, 2), (20, 6, 32, 5, 2),
+                                (28, 6, 32, 3, 1), (28, 8, 32, 3, 1), (28, 6, 32, 5, 2), (20, 6, 32, 5, 2),
                                 (48, 4, 32, 5, 2)])
 def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN, avd_opts):
     """avd_cl_c1_recompute (the audio conv1 without a stored conv output) against the stored-y
