@@ -317,15 +317,16 @@ struct MGeo {
 };
 constexpr int GZS = 40;                                         // window slot stride of the gz tile (80 B)
 constexpr int MOMR = C * 9 + 81 + 9 + C;
-constexpr int M_RED = 4 * 3 * 64 * 4;                           // epilogue floats [wave][tile][lane][4]
+constexpr int M_RED = 4 * 3 * 64 * 4 + 100;                     // epilogue floats [wave][tile][lane][4] + [10][10]
 
-template <int W>
+template <int W, bool GRAM>
 __global__ __launch_bounds__(256) void c1s3_moments_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ gz, const unsigned short* __restrict__ codes,
-    float* __restrict__ out, int B, int G, int R) {
+    const bf16* __restrict__ wk, const float* __restrict__ bias, float* __restrict__ out, int B, int G, int R) {
   using Mg = MGeo<W>;
   constexpr int XS = Mg::XS, WP = Mg::WP;
-  constexpr int LDSB = Mg::L_END * 2 > M_RED * 4 ? Mg::L_END * 2 : M_RED * 4;
+  constexpr int LEND = GRAM ? Mg::L_GZ : Mg::L_END;            // the statistics pass stages x only
+  constexpr int LDSB = LEND * 2 > M_RED * 4 ? LEND * 2 : M_RED * 4;
   __shared__ __attribute__((aligned(16))) char lds[LDSB];
   bf16* sm = reinterpret_cast<bf16*>(lds);
   const unsigned short* gzs = reinterpret_cast<const unsigned short*>(sm + Mg::L_GZ);
@@ -347,7 +348,7 @@ __global__ __launch_bounds__(256) void c1s3_moments_kernel(
   f4 macc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}}, gacc = f4{0.f, 0.f, 0.f, 0.f};
 
   // halos, and (28^2) the padding window slots of the gz / codes tiles: zero once
-  for (int i = tid; i < Mg::L_END / 2; i += 256) reinterpret_cast<unsigned*>(sm)[i] = 0u;
+  for (int i = tid; i < LEND / 2; i += 256) reinterpret_cast<unsigned*>(sm)[i] = 0u;
 
   u4 xv = u4{0u, 0u, 0u, 0u}, cv = u4{0u, 0u, 0u, 0u}, gv[4];
   bool xok = false;
@@ -364,10 +365,12 @@ __global__ __launch_bounds__(256) void c1s3_moments_kernel(
       xok = true;
       xv = ldg16(x + (size_t)n * W * W + 8 * e);
     }
-    const size_t w0 = (size_t)n * WP * WP + (size_t)(y0 / 2) * WP;      // the tile's first window
+    if constexpr (!GRAM) {
+      const size_t w0 = (size_t)n * WP * WP + (size_t)(y0 / 2) * WP;    // the tile's first window
 #pragma unroll
-    for (int j = 0; j < 4; ++j) gv[j] = ldg16(gz + w0 * C + 8 * min(tid + 256 * j, Mg::NG - 1));
-    cv = ldg16(codes + (w0 + min(tid, Mg::NWIN - 1)) * 8);
+      for (int j = 0; j < 4; ++j) gv[j] = ldg16(gz + w0 * C + 8 * min(tid + 256 * j, Mg::NG - 1));
+      cv = ldg16(codes + (w0 + min(tid, Mg::NWIN - 1)) * 8);
+    }
   };
   auto slot = [&](int w) { return W % 8 == 0 ? w : (w / WP) * Mg::WSL + (w - (w / WP) * WP); };
   auto put = [&]() {
@@ -395,12 +398,14 @@ __global__ __launch_bounds__(256) void c1s3_moments_kernel(
         }
       }
     }
+    if constexpr (!GRAM) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int e = tid + 256 * j;
-      if (e < Mg::NG) *reinterpret_cast<u4*>(sm + Mg::L_GZ + slot(e >> 2) * GZS + 8 * (e & 3)) = gv[j];
+      for (int j = 0; j < 4; ++j) {
+        const int e = tid + 256 * j;
+        if (e < Mg::NG) *reinterpret_cast<u4*>(sm + Mg::L_GZ + slot(e >> 2) * GZS + 8 * (e & 3)) = gv[j];
+      }
+      if (tid < Mg::NWIN) *reinterpret_cast<u4*>(sm + Mg::L_CD + 8 * slot(tid)) = cv;
     }
-    if (tid < Mg::NWIN) *reinterpret_cast<u4*>(sm + Mg::L_CD + 8 * slot(tid)) = cv;
   };
 
   if (t0 < t1) load(t0);
@@ -422,7 +427,7 @@ __global__ __launch_bounds__(256) void c1s3_moments_kernel(
       const bf16x8 bx = __builtin_bit_cast(bf16x8, bv);
       const int w = hr * Mg::WSL + wc0 + 2 * g;                 // the lane's first window slot
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
+      for (int ct = 0; ct < (GRAM ? 0 : 2); ++ct) {
         const int c = 16 * ct + r16;
         unsigned av[4];
 #pragma unroll
@@ -457,6 +462,31 @@ __global__ __launch_bounds__(256) void c1s3_moments_kernel(
     for (int wv = 0; wv < 4; ++wv) v += red[((wv * 3 + tile) * 64 + l) * 4 + i];
     return v;
   };
+  if constexpr (GRAM) {
+    // BN partial sums of the exact conv output y = w . x9 + b from the block's patch Gram, in
+    // float64: sum y = w . S + n b, sum y^2 = w' Gram w + 2 b w . S + n b^2 (n = the ones' count);
+    // rows [C][G][R][2] (avd_bn_finalize's layout, c1r3 pass 0's contract)
+    float* g10 = red + 4 * 3 * 64 * 4;                          // [10][10] after the wave tiles
+    if (tid < 100) g10[tid] = at(2, tid / 10, tid % 10);
+    __syncthreads();
+    if (tid < C) {
+      double ws = 0.0, wgw = 0.0;
+#pragma unroll 1
+      for (int t = 0; t < 9; ++t) {
+        const double wt = (double)bf2f(wk[tid * 32 + t]);
+        ws += wt * (double)g10[t * 10 + 9];
+        double r = 0.0;
+#pragma unroll 1
+        for (int u = 0; u < 9; ++u) r += (double)bf2f(wk[tid * 32 + u]) * (double)g10[t * 10 + u];
+        wgw += wt * r;
+      }
+      const double n = (double)g10[99], b = bias ? (double)bias[tid] : 0.0;
+      float* o = out + (((size_t)tid * G + grp) * R + rr) * 2;
+      o[0] = (float)(ws + n * b);
+      o[1] = (float)(wgw + 2.0 * b * ws + n * b * b);
+    }
+    return;
+  }
   float* o = out + ((size_t)rr * G + grp) * MOMR;
   for (int e = tid; e < MOMR; e += 256) {
     float v;
@@ -497,25 +527,24 @@ bool c1s3_serves(int N, int B, int H, int W, int Cout) {
   return W == 112;
 }
 
-// rows per BN group of the statistics pass (c1r3 pass 0's contract)
+// rows per BN group of the statistics pass (c1r3 pass 0's contract): the patch-Gram pass
 int c1s3_stats_rows(int N, int B, int W) {
   static int res28 = 0, res112 = 0;
   int& res = W == 28 ? res28 : res112;
-  if (!res) res = W == 28 ? resident_blocks(c1s3_kernel<28, false>) : resident_blocks(c1s3_kernel<112, false>);
-  const int G = N / B;
-  const int tg = W == 28 ? B / 2 : B * Geo<112>::TPS;        // tiles per group
-  return std::max(1, std::min(grid_cap(res) / G, std::max(1, tg / 2)));
+  if (!res) res = W == 28 ? resident_blocks(c1s3_moments_kernel<28, true>) : resident_blocks(c1s3_moments_kernel<112, true>);
+  const int G = N / B, tg = B * (W == 28 ? MGeo<28>::TPS : MGeo<112>::TPS);
+  return std::max(1, std::min(grid_cap(res) / G, std::max(1, tg / 4)));
 }
 
 int c1s3_stats(const void* x, const void* wk, const float* bias, float* out, int N, int B, int W,
                hipStream_t st) {
   const int R = c1s3_stats_rows(N, B, W), G = N / B;
   if (W == 28)
-    c1s3_kernel<28, false><<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, nullptr, nullptr,
-                                                  nullptr, nullptr, out, N, B, G, R);
+    c1s3_moments_kernel<28, true><<<G * R, 256, 0, st>>>((const bf16*)x, nullptr, nullptr, (const bf16*)wk, bias,
+                                                         out, B, G, R);
   else
-    c1s3_kernel<112, false><<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, nullptr, nullptr,
-                                                   nullptr, nullptr, out, N, B, G, R);
+    c1s3_moments_kernel<112, true><<<G * R, 256, 0, st>>>((const bf16*)x, nullptr, nullptr, (const bf16*)wk,
+                                                          bias, out, B, G, R);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
@@ -525,7 +554,8 @@ int c1s3_moments_rows(int N, int B, int H, int W, int Cout) {
   if (Cout != C || H != W || (W != 28 && W != 112) || N <= 0 || B <= 0 || N % B) return 0;
   static int res28 = 0, res112 = 0;
   int& res = W == 28 ? res28 : res112;
-  if (!res) res = W == 28 ? resident_blocks(c1s3_moments_kernel<28>) : resident_blocks(c1s3_moments_kernel<112>);
+  if (!res)
+    res = W == 28 ? resident_blocks(c1s3_moments_kernel<28, false>) : resident_blocks(c1s3_moments_kernel<112, false>);
   const int G = N / B, tg = B * (W == 28 ? MGeo<28>::TPS : MGeo<112>::TPS);
   return std::max(1, std::min(grid_cap(res) / G, std::max(1, tg / 4)));
 }
@@ -534,9 +564,11 @@ int c1s3_moments(const void* x, const void* gz, const unsigned short* codes, flo
                  int W, hipStream_t st) {
   const int R = c1s3_moments_rows(N, B, W, W, C), G = N / B;
   if (W == 28)
-    c1s3_moments_kernel<28><<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)gz, codes, out, B, G, R);
+    c1s3_moments_kernel<28, false><<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)gz, codes, nullptr, nullptr,
+                                                          out, B, G, R);
   else
-    c1s3_moments_kernel<112><<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)gz, codes, out, B, G, R);
+    c1s3_moments_kernel<112, false><<<G * R, 256, 0, st>>>((const bf16*)x, (const bf16*)gz, codes, nullptr,
+                                                           nullptr, out, B, G, R);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

@@ -278,7 +278,17 @@ def test_cl_c1_recompute_passes_match_stored_y_path(ops, HN, avd_opts):
     ops.cl_c1_recompute(ops.C1_STATS, tx, wk, tb, N, B, 1, H, H, C, K, pad, out=st1)
     s0 = host(st0).reshape(C, G, R0, 2).sum(2)
     s1 = host(st1).reshape(C, G, R1, 2).sum(2)
-    assert rel(s1, s0) < 1e-6
+    if K == 3 and C == 32 and (H == 112 or (H == 28 and B % 2 == 0)):
+        # the 3x3 1 -> 32 statistics pass (c1s3.hip) sums the EXACT conv output from the block's
+        # patch Gram (as the audio conv1's, avd_cl_c1_gram): float64 of the exact conv
+        y64 = torch.nn.functional.conv2d(torch.from_numpy(x).double().permute(0, 3, 1, 2),
+                                         torch.from_numpy(w).double(), torch.from_numpy(b).double(),
+                                         padding=pad).view(G, B, C, H * H)
+        ref = torch.stack([y64.sum((1, 3)), (y64 ** 2).sum((1, 3))], -1).transpose(0, 1).numpy()
+        assert rel(s1, ref) < 1e-6, rel(s1, ref)
+        assert rel(s1, s0) < 1e-4              # the stored-y sums are of the bf16-rounded y
+    else:
+        assert rel(s1, s0) < 1e-6
     gamma = (1 + g.uniform(-.2, .2, C)).astype(np.float32)
     beta = g.uniform(-.2, .2, C).astype(np.float32)
     bn = torch.empty(4, G * C, device="cuda")
