@@ -1,25 +1,15 @@
-// The 3x3 first layer's forward passes on PIXEL-major MFMAs: Conv2d(1, 32, 3, padding=1) -> BN2d
-// -> ReLU -> MaxPool2d(2) of the SimCLR / unimodal encoders' image_encoder (28x28) and
-// audio_encoder (112x112) (dino.py:18-73), bf16, as c1r5.hip does for the CentralNet 5x5 conv1:
-//   * c1s3_kernel<W, APPLY>: BN -> ReLU -> 2x2 max-pool of the recomputed conv output plus the
-//     routing codes the routed backward reads (avd_cl_c1r3_apply_codes), or the BN partial sums
-//     of y (c1r3 pass 0's contract, avd_c1r3_rows / avd_c1r3_launch pass 0);
-//   * A = the im2col fragment of 16 pixels ordered window by window (pixel p = 4 w + k, k = (0,0)
-//     (0,1) (1,0) (1,1)), B = the weights of 16 channels, so D lane l holds ONE whole pooling
-//     window of one channel: max, first argmax and the > 0 test are in-lane integer compares of
-//     the f32 bn(y) bits, and y is the same bf16(acc + b) as the stored-y conv's;
-//   * k = tap (0..8, the stored-y conv's order: lane group 0 holds taps 0..7, group 1 tap 8, and
-//     the k slots >= 9 meet zero weights).  A layout with filter row ty in lane group ty gave a
-//     pooled map that differs from the stored-y chain's at N = 2048 (tests/test_gpu_c1r3_codes.py):
-//     the MFMA's sum of the nine products depends on their k slots;
-//   * the staged rows are kept twice, the second copy shifted right by one pixel, so a lane's 3x3
-//     patch row (columns c - 1 .. c + 1) starts on a dword in one of them: 3 dword-pair reads per
-//     lane and group instead of 8 two-byte gathers;
-//   * tiles: TR staged rows (+ 2 halo rows) of SPT samples, register-prefetched one tile ahead,
-//     one barrier per tile; pooled map stores are 4 bytes per lane (lane pairs trade channel
-//     halves), codes 2 bytes per lane (one quad of channels).
-// The recomputing channel-major passes (c1w3.hip c1r3_kernel, 16 lanes per window, DPP
-// exchanges) took 549 us (apply + codes) at config 4's N = 2048 x 112^2.
+// The 3x3 first layer of the SimCLR / unimodal encoders without a stored conv output:
+// Conv2d(1, 32, 3, padding=1) -> BN2d -> ReLU -> MaxPool2d(2) of image_encoder (28x28) and
+// audio_encoder (112x112) (dino.py:18-73), bf16, in three passes over the input:
+//   * statistics: the per-block patch Gram (9 taps + ones) on MFMAs, turned into the BN partial
+//     sums of the EXACT conv output in float64 (c1r3 pass 0's row contract; as the audio
+//     conv1's avd_cl_c1_gram) -- c1s3_moments_kernel<W, true>;
+//   * BN -> ReLU -> 2x2 max-pool plus the routing codes the backward reads
+//     (avd_cl_c1r3_apply_codes) -- c1s3_apply_kernel<W>, PIXEL-major like c1r5.hip's;
+//   * the routed backward moments M = sum dz x9, Gram, S, sum dz (avd_cl_c1r3_moments_codes) --
+//     c1s3_moments_kernel<W, false>, a GEMM over window-ordered pixels with dz built in registers.
+// The recomputing channel-major passes they replace (c1w3.hip c1r3_kernel) took 168 / 549 /
+// 540 us at config 4's N = 2048 x 112^2 (profiles/r5w_*).
 #include <algorithm>
 
 #include "common.h"
@@ -34,6 +24,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f4;
 typedef __attribute__((ext_vector_type(4))) unsigned u4;
 typedef __attribute__((ext_vector_type(8))) unsigned short us8;
+typedef __attribute__((ext_vector_type(2))) float f2;
 
 template <int CTRL>
 __device__ __forceinline__ int dppi(int v) {
@@ -70,37 +61,43 @@ struct Geo {
   // else SPT whole samples (the halo rows stay zero)
   static constexpr int NV = W % 8 == 0 ? (TR + 2) * (W / 8) : SPT * (H * W / 8);
   static_assert(NV <= 256, "one staging vector per thread");
+  static_assert(NGC >= 4, "one carry per group step");
   static_assert(W % 8 == 0 ? TR * TPS == H : TR == H, "tiles cover the sample");
 };
 
-template <int W, bool APPLY>
-__global__ __launch_bounds__(256) void c1s3_kernel(
+// BN -> ReLU -> 2x2 max-pool of the recomputed conv output plus the routing codes:
+//   * A = the im2col fragment of 16 pixels ordered window by window (pixel p = 4 w + k, k = (0,0)
+//     (0,1) (1,0) (1,1)), B = the weights of 16 channels, so D lane l holds ONE whole pooling
+//     window of one channel: max, first argmax and the > 0 test are in-lane integer compares of
+//     the f32 bn(y) bits, and y is the same bf16(acc + b) as the stored-y conv's (bit-identical
+//     pooled map, tests/test_gpu_c1r3_codes.py);
+//   * k = tap (0..8, the stored-y conv's order: lane group 0 holds taps 0..7, group 1 tap 8, and
+//     the k slots >= 9 meet zero weights).  A layout with filter row ty in lane group ty gave a
+//     pooled map that differs from the stored-y chain's at N = 2048: the MFMA's sum of the nine
+//     products depends on their k slots;
+//   * the staged rows are kept twice, the second copy shifted right by one pixel, so a lane's 3x3
+//     patch row (columns c - 1 .. c + 1) starts on a dword in one of them: 3 dword-pair reads per
+//     lane and group instead of 8 two-byte gathers;
+//   * tiles: TR staged rows (+ 2 halo rows) of SPT samples, register-prefetched one tile ahead,
+//     one barrier per tile; pooled map stores are 4 bytes per lane (lane pairs trade channel
+//     halves), codes 2 bytes per lane (one quad of channels).
+template <int W>
+__global__ __launch_bounds__(256) void c1s3_apply_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ wk, const float* __restrict__ bias,
     const float* __restrict__ scale, const float* __restrict__ shift, bf16* __restrict__ z,
-    unsigned short* __restrict__ codes, float* __restrict__ out, int N, int B, int G, int R) {
+    unsigned short* __restrict__ codes, int N, int B) {
   using Gm = Geo<W>;
   constexpr int XS = Gm::XS, TR = Gm::TR, SPT = Gm::SPT, WP = Gm::WP, NGC = Gm::NGC;
   __shared__ __attribute__((aligned(16))) bf16 xs[2 * Gm::BUF];
-  __shared__ float red[APPLY ? 1 : 4 * 4 * 2 * 16 * 2];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
-  // tiles: SPT samples x TR rows; apply: a contiguous share of all tiles, statistics: block
-  // (group, rr) a contiguous share of one BN group's tiles (B % SPT == 0, checked by the host)
+  // tiles: SPT samples x TR rows; a block takes a contiguous share of them
   const int tps = SPT == 1 ? Gm::TPS : 1;
-  int t0, t1, grp = 0, rr = 0;
-  if constexpr (APPLY) {
-    const int nt = (N + SPT - 1) / SPT * tps;
-    const int per = nt / (int)gridDim.x, extra = nt % (int)gridDim.x;
-    t0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
-    t1 = t0 + per + ((int)blockIdx.x < extra ? 1 : 0);
-  } else {
-    grp = (int)blockIdx.x / R;
-    rr = (int)blockIdx.x - grp * R;
-    const int tg = B / SPT * tps;                   // tiles per group
-    t0 = grp * tg + (int)(((long long)tg * rr) / R);
-    t1 = grp * tg + (int)(((long long)tg * (rr + 1)) / R);
-  }
+  const int nt = (N + SPT - 1) / SPT * tps;
+  const int per = nt / (int)gridDim.x, extra = nt % (int)gridDim.x;
+  const int t0 = (int)blockIdx.x * per + min((int)blockIdx.x, extra);
+  const int t1 = t0 + per + ((int)blockIdx.x < extra ? 1 : 0);
 
   // B operand: lane (channel 16 t + r16, k = 8 g + j) = w[c][8 g + j] (taps >= 9 are zero in wk)
   bf16x8 aw[2];
@@ -109,7 +106,7 @@ __global__ __launch_bounds__(256) void c1s3_kernel(
   for (int t = 0; t < 2; ++t) {
     const u4 wv = *reinterpret_cast<const u4*>(wk + (16 * t + r16) * 32 + 8 * g);
     aw[t] = __builtin_bit_cast(bf16x8, u4{vkeep(wv.x), vkeep(wv.y), vkeep(wv.z), vkeep(wv.w)});
-    bv[t] = __uint_as_float(vkeep(__float_as_uint(bias ? bias[16 * t + r16] : 0.f)));
+    bv[t] = vkeepf(bias ? bias[16 * t + r16] : 0.f);
   }
   // A operand: lane (pixel r16 of a group = window r16 / 4, position r16 % 4; taps 8 g + j):
   // patch rows read from the copy where column pcol - 1 sits on a dword (odd pcol: the copy,
@@ -170,7 +167,6 @@ __global__ __launch_bounds__(256) void c1s3_kernel(
   __syncthreads();                                  // zeroed
   if (t0 < t1) put(xs);
 
-  float sm[2] = {0.f, 0.f}, sq[2] = {0.f, 0.f};
   float sc[SPT][2] = {}, sf[SPT][2] = {};
   int cgs[SPT];
 #pragma unroll
@@ -181,28 +177,29 @@ __global__ __launch_bounds__(256) void c1s3_kernel(
     const int n0 = ti / tps * SPT, y0 = (ti - ti / tps * tps) * TR;
     // BN coefficients of the tile's samples, re-read only when the BN group changes and waited
     // for right there (vkeepf): no load but the prefetch is outstanding in the group loop
-    if constexpr (APPLY) {
 #pragma unroll
-      for (int s = 0; s < SPT; ++s) {
-        const int cg = min(n0 + s, N - 1) / B;
-        if (cg != cgs[s]) {
-          cgs[s] = cg;
+    for (int s = 0; s < SPT; ++s) {
+      const int cg = min(n0 + s, N - 1) / B;
+      if (cg != cgs[s]) {
+        cgs[s] = cg;
 #pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            sc[s][t] = vkeepf(scale[cg * C + 16 * t + r16]);
-            sf[s][t] = vkeepf(shift[cg * C + 16 * t + r16]);
-          }
+        for (int t = 0; t < 2; ++t) {
+          sc[s][t] = vkeepf(scale[cg * C + 16 * t + r16]);
+          sf[s][t] = vkeepf(shift[cg * C + 16 * t + r16]);
         }
       }
     }
     // in flight under this tile's MFMAs; issued on the last tile too (its own tile again), so
     // every path has the same loads outstanding and the coefficients' wait leaves it in flight
     load(min(ti + 1, t1 - 1));
+    // the tile's first window; group (s, rp, cq) advanced by 4 with one carry per step
+    bf16* zt = z + ((size_t)n0 * (W / 2) + y0 / 2) * WP * C;
+    unsigned short* ct = codes ? codes + ((size_t)n0 * (W / 2) + y0 / 2) * WP * 8 : nullptr;
+    int cq = wave, rp = 0, s = 0;                   // NGC >= 4: at most one carry per step
     for (int q = wave; q < Gm::GPT; q += 4) {
-      const int s = q / ((TR / 2) * NGC), rem = q - s * ((TR / 2) * NGC);
-      const int rp = rem / NGC, cq = rem - rp * NGC;          // row pair, 8-column group
       // patch rows 0..2: (c - 1, c), (c + 1, c + 2) of each
-      const unsigned* pr = reinterpret_cast<const unsigned*>(xb + s * Gm::SR + 2 * rp * XS + 8 * cq + aoff);
+      const int sm = SPT == 1 ? 0 : s;                        // the tile's sample (SPT 1: always 0)
+      const unsigned* pr = reinterpret_cast<const unsigned*>(xb + sm * Gm::SR + 2 * rp * XS + 8 * cq + aoff);
       const unsigned d00 = pr[0], d01 = pr[1], d10 = pr[XS / 2], d11 = pr[XS / 2 + 1];
       const unsigned d20 = pr[XS], d21 = pr[XS + 1];
       // k 0..7 = taps (0,0) (0,1) | (0,2) (1,0) | (1,1) (1,2) | (2,0) (2,1); lane groups >= 1:
@@ -211,75 +208,45 @@ __global__ __launch_bounds__(256) void c1s3_kernel(
                        __builtin_amdgcn_alignbit(d11, d10, 16), d20};
       const bf16x8 px = __builtin_bit_cast(bf16x8, av);
       const int wcol = 4 * cq + g;                            // the lane's window column
-      const int n = n0 + s;
-      const bool live = wcol < WP && n < N;
-      if constexpr (APPLY) {
-        unsigned zw = 0u, cw = 0u;
+      const bool live = wcol < WP && n0 + sm < N;
+      const int win = (sm * (W / 2) + rp) * WP + wcol;        // from the tile's first window
+      unsigned zw = 0u, cw = 0u;
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(px, aw[t], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          const uint32_t y01 = pack_bf16x2(acc[0] + bv[t], acc[1] + bv[t]);
-          const uint32_t y23 = pack_bf16x2(acc[2] + bv[t], acc[3] + bv[t]);
-          const float y[4] = {__uint_as_float(y01 << 16), __uint_as_float(y01 & 0xffff0000u),
-                              __uint_as_float(y23 << 16), __uint_as_float(y23 & 0xffff0000u)};
-          int v[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = __float_as_int(fmaf(y[i], sc[s][t], sf[s][t]));
-          // signed-int order = float order where either side is > 0; max with 0 = the ReLU
-          const int mx = max(max(v[0], v[1]), max(v[2], max(v[3], 0)));
-          const int a = v[0] == mx ? 1 : v[1] == mx ? 2 : v[2] == mx ? 3 : 4;   // first argmax + 1
-          const unsigned nib = mx > 0 ? (unsigned)a : 0u;
-          zw |= (pack_bf16x2(__int_as_float(mx), 0.f) & 0xffffu) << (16 * t);
-          cw |= nib << (4 * pk + 16 * t);
-        }
-        // pooled map: lane pairs trade halves so each stores 2 adjacent channels (4 bytes):
-        // even r16 -> channels (r16, r16 + 1), odd r16 -> (15 + r16, 16 + r16)
-        const unsigned zo = (unsigned)dppi<0xB1>((int)zw);
-        const bool ev = (r16 & 1) == 0;
-        const unsigned word = ev ? (zw & 0xffffu) | (zo << 16) : (zo >> 16) | (zw & 0xffff0000u);
-        // codes: the 4 channels of a u16 sit in one lane quad
-        cw |= (unsigned)dppi<0xB1>((int)cw);
-        cw |= (unsigned)dppi<0x4E>((int)cw);
-        if (live) {
-          const size_t win = ((size_t)n * (W / 2) + (y0 / 2 + rp)) * WP + wcol;
-          *reinterpret_cast<unsigned*>(z + win * C + (ev ? r16 : 15 + r16)) = word;
-          if (codes && pk < 2) codes[win * 8 + 4 * pk + (r16 >> 2)] = (unsigned short)(cw >> (16 * pk));
-        }
-      } else {
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(px, aw[t], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          const uint32_t y01 = pack_bf16x2(acc[0] + bv[t], acc[1] + bv[t]);
-          const uint32_t y23 = pack_bf16x2(acc[2] + bv[t], acc[3] + bv[t]);
-          const float y0f = __uint_as_float(y01 << 16), y1f = __uint_as_float(y01 & 0xffff0000u);
-          const float y2f = __uint_as_float(y23 << 16), y3f = __uint_as_float(y23 & 0xffff0000u);
-          if (live) {   // after the MFMA: the whole wave issues it
-            sm[t] += (y0f + y1f) + (y2f + y3f);
-            sq[t] += fmaf(y0f, y0f, y1f * y1f) + fmaf(y2f, y2f, y3f * y3f);
-          }
-        }
+      for (int t = 0; t < 2; ++t) {
+        const f4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(px, aw[t], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        // y = bf16(acc + b) and bn(y) on packed pairs (the same IEEE operations per element)
+        const f2 b2 = f2{bv[t], bv[t]}, sc2 = f2{sc[sm][t], sc[sm][t]}, sf2 = f2{sf[sm][t], sf[sm][t]};
+        const f2 a01 = f2{acc[0], acc[1]} + b2, a23 = f2{acc[2], acc[3]} + b2;
+        const uint32_t y01 = pack_bf16x2(a01.x, a01.y), y23 = pack_bf16x2(a23.x, a23.y);
+        const f2 v01 = __builtin_elementwise_fma(f2{__uint_as_float(y01 << 16), __uint_as_float(y01 & 0xffff0000u)}, sc2, sf2);
+        const f2 v23 = __builtin_elementwise_fma(f2{__uint_as_float(y23 << 16), __uint_as_float(y23 & 0xffff0000u)}, sc2, sf2);
+        const int v[4] = {__float_as_int(v01.x), __float_as_int(v01.y), __float_as_int(v23.x), __float_as_int(v23.y)};
+        // signed-int order = float order where either side is > 0; max with 0 = the ReLU
+        const int mx = max(max(v[0], v[1]), max(v[2], max(v[3], 0)));
+        const int a = v[0] == mx ? 1 : v[1] == mx ? 2 : v[2] == mx ? 3 : 4;   // first argmax + 1
+        const unsigned nib = mx > 0 ? (unsigned)a : 0u;
+        zw |= (pack_bf16x2(__int_as_float(mx), 0.f) & 0xffffu) << (16 * t);
+        cw |= nib << (4 * pk + 16 * t);
+      }
+      // pooled map: lane pairs trade halves so each stores 2 adjacent channels (4 bytes):
+      // even r16 -> channels (r16, r16 + 1), odd r16 -> (15 + r16, 16 + r16)
+      const unsigned zo = (unsigned)dppi<0xB1>((int)zw);
+      const bool ev = (r16 & 1) == 0;
+      const unsigned word = ev ? (zw & 0xffffu) | (zo << 16) : (zo >> 16) | (zw & 0xffff0000u);
+      // codes: the 4 channels of a u16 sit in one lane quad
+      cw |= (unsigned)dppi<0xB1>((int)cw);
+      cw |= (unsigned)dppi<0x4E>((int)cw);
+      if (live) {
+        *reinterpret_cast<unsigned*>(zt + win * C + (ev ? r16 : 15 + r16)) = word;
+        if (ct && pk < 2) ct[win * 8 + 4 * pk + (r16 >> 2)] = (unsigned short)(cw >> (16 * pk));
+      }
+      cq += 4;
+      if (cq >= NGC) {
+        cq -= NGC;
+        if (++rp == TR / 2) { rp = 0; ++s; }
       }
     }
     if (ti + 1 < t1) put(xs + ((ti + 1 - t0) & 1) * Gm::BUF);
-  }
-  if constexpr (!APPLY) {
-    // rows [C][G][R][2] (avd_bn_finalize's layout): the block's 16 lane partials per channel
-    // summed in fixed order
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      red[(((wave * 4 + g) * 2 + t) * 16 + r16) * 2 + 0] = sm[t];
-      red[(((wave * 4 + g) * 2 + t) * 16 + r16) * 2 + 1] = sq[t];
-    }
-    __syncthreads();
-    if (tid < 2 * C) {
-      const int c = tid >> 1, k = tid & 1, t = c >> 4, ch = c & 15;
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < 4; ++w)
-#pragma unroll
-        for (int gg = 0; gg < 4; ++gg) v += red[(((w * 4 + gg) * 2 + t) * 16 + ch) * 2 + k];
-      out[(((size_t)c * G + grp) * R + rr) * 2 + k] = v;
-    }
   }
 }
 
@@ -578,15 +545,15 @@ int c1s3_apply_codes(const void* x, const void* wk, const float* bias, const flo
                      hipStream_t st) {
   static int res28 = 0, res112 = 0;
   int& res = W == 28 ? res28 : res112;
-  if (!res) res = W == 28 ? resident_blocks(c1s3_kernel<28, true>) : resident_blocks(c1s3_kernel<112, true>);
+  if (!res) res = W == 28 ? resident_blocks(c1s3_apply_kernel<28>) : resident_blocks(c1s3_apply_kernel<112>);
   const int tiles = W == 28 ? (N + 1) / 2 : N * Geo<112>::TPS;
   const int grid = grid_cap(std::min(tiles, res));
   if (W == 28)
-    c1s3_kernel<28, true><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, scale, shift,
-                                                (bf16*)z, codes, nullptr, N, B, 1, 1);
+    c1s3_apply_kernel<28><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, scale, shift,
+                                                (bf16*)z, codes, N, B);
   else
-    c1s3_kernel<112, true><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, scale, shift,
-                                                 (bf16*)z, codes, nullptr, N, B, 1, 1);
+    c1s3_apply_kernel<112><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, scale, shift,
+                                                 (bf16*)z, codes, N, B);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
