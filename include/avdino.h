@@ -263,7 +263,7 @@ int avd_cl_bn_bwd_reduce_pooled(const void* y, int dt, const void* pooled, const
  * (bf16-rounded, bit-identical across passes) into an on-chip tile from the 8x smaller input.
  *   pass 0 (stats):  out = BN partial rows [Cout][G][R][2] of the rounded y
  *                    (R = avd_cl_c1_recompute_rows(0, ...); feed avd_bn_finalize); for the
- *                    3x3 1 -> 32 layer at 28^2 (B even) / 112^2 the rows are of the EXACT conv
+ *                    3x3 1 -> 32 layer at 28^2 / 112^2 the rows are of the EXACT conv
  *                    output, formed from per-block patch Gram matrices (c1s3.hip);
  *   pass 1 (apply):  z = maxpool2(relu(y*scale + shift)) NHWC [N][H/2][W/2][Cout] (bf16);
  *   pass 2 (reduce): out = BN-backward partial rows (sum dz, sum dz*xhat) as
@@ -649,7 +649,7 @@ int avd_cl_c1_codes_combine_gram(const float* moments, const float* gram, const 
                                  float* dbeta, float* dbias, float* coef, int G, void* stream);
 
 /* ------------------------------------------------------------------ routed 3x3 first layer
- * (28^2 with B even and 112^2 run on the pixel-major / window-ordered kernels of c1s3.hip;
+ * (28^2 and 112^2 run on the pixel-major / window-ordered kernels of c1s3.hip;
  * other shapes on c1w3.hip's recompute passes -- same contracts.)
  * The SimCLR / unimodal encoders' conv1 (audio_encoder / image_encoder, dino.py:18-73:
  * Conv2d(1, 32, 3, padding=1) -> BN2d -> ReLU -> MaxPool2d on 112x112 / 28x28, bf16) without a

@@ -47,7 +47,7 @@ struct Geo {
   static constexpr int WP = W / 2;                  // pooling windows per row
   static constexpr int NGC = (WP + 3) / 4;          // 4-window (16-pixel) groups per row pair
   static constexpr int TR = W <= 32 ? W : 16;       // staged rows per sample of a tile
-  static constexpr int SPT = W <= 32 ? 2 : 1;       // samples per tile
+  static constexpr int SPT = 1;                     // samples per tile
   static constexpr int TPS = H / TR;                // tiles per sample (SPT == 1)
   static constexpr int XO = 8;                      // staged column of pixel 0 (left halo at 7)
   // row stride: the widest read is column 8 NGC (+ XO); 112: 272-B rows (4 banks of skew)
@@ -487,11 +487,10 @@ int resident_blocks(Kern k) {
 
 namespace avd {
 
-// shapes served: Cin 1, Cout 32, 3x3 pad 1, square 28^2 (B, N even) or 112^2 maps, bf16
+// shapes served: Cin 1, Cout 32, 3x3 pad 1, square 28^2 or 112^2 maps, bf16
 bool c1s3_serves(int N, int B, int H, int W, int Cout) {
   if (Cout != C || H != W || N <= 0 || B <= 0 || N % B) return false;
-  if (W == 28) return B % 2 == 0;
-  return W == 112;
+  return W == 28 || W == 112;
 }
 
 // rows per BN group of the statistics pass (c1r3 pass 0's contract): the patch-Gram pass
@@ -546,7 +545,7 @@ int c1s3_apply_codes(const void* x, const void* wk, const float* bias, const flo
   static int res28 = 0, res112 = 0;
   int& res = W == 28 ? res28 : res112;
   if (!res) res = W == 28 ? resident_blocks(c1s3_apply_kernel<28>) : resident_blocks(c1s3_apply_kernel<112>);
-  const int tiles = W == 28 ? (N + 1) / 2 : N * Geo<112>::TPS;
+  const int tiles = N * (W == 28 ? Geo<28>::TPS : Geo<112>::TPS);
   const int grid = grid_cap(std::min(tiles, res));
   if (W == 28)
     c1s3_apply_kernel<28><<<grid, 256, 0, st>>>((const bf16*)x, (const bf16*)wk, bias, scale, shift,
