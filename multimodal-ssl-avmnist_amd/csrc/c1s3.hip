@@ -208,8 +208,9 @@ __global__ __launch_bounds__(256) void c1s3_apply_kernel(
                        __builtin_amdgcn_alignbit(d11, d10, 16), d20};
       const bf16x8 px = __builtin_bit_cast(bf16x8, av);
       const int wcol = 4 * cq + g;                            // the lane's window column
-      const bool live = wcol < WP && n0 + sm < N;
-      const int win = (sm * (W / 2) + rp) * WP + wcol;        // from the tile's first window
+      // every window is real at 112^2 (4 NGC == WP) and every tile sample is < N with SPT 1
+      const bool live = (4 * NGC == WP || wcol < WP) && (SPT == 1 || n0 + sm < N);
+      const unsigned win = (unsigned)((sm * (W / 2) + rp) * WP + wcol);   // from the tile's first window
       unsigned zw = 0u, cw = 0u;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -237,8 +238,9 @@ __global__ __launch_bounds__(256) void c1s3_apply_kernel(
       cw |= (unsigned)dppi<0xB1>((int)cw);
       cw |= (unsigned)dppi<0x4E>((int)cw);
       if (live) {
-        *reinterpret_cast<unsigned*>(zt + win * C + (ev ? r16 : 15 + r16)) = word;
-        if (ct && pk < 2) ct[win * 8 + 4 * pk + (r16 >> 2)] = (unsigned short)(cw >> (16 * pk));
+        // 32-bit element offsets from the tile's (uniform) base pointers
+        *reinterpret_cast<unsigned*>(zt + (win * C + (unsigned)(ev ? r16 : 15 + r16))) = word;
+        if (ct && pk < 2) ct[win * 8u + (unsigned)(4 * pk + (r16 >> 2))] = (unsigned short)(cw >> (16 * pk));
       }
       cq += 4;
       if (cq >= NGC) {
