@@ -15,9 +15,12 @@
  *   - host-side state: per-process caches filled on first use and read-only afterwards -- the
  *     CU count and the occupancy of each persistent kernel (hipOccupancy queries that size the
  *     persistent grids, e.g. conv_ws.hip ws_occ, conv_c1p.hip, wgrad_ws.hip, conv3.hip, c1w3.hip,
- *     conv_ws8.hip) and the AVDINO_* environment switches, read once; no state depends on the
- *     data, so calls are reentrant for distinct streams (the first calls race benignly: every
- *     thread computes the same value);
+ *     conv_ws8.hip); no environment variable is read; no state depends on the data, so calls
+ *     are reentrant for distinct streams (the first calls race benignly: every thread computes
+ *     the same value).  The one mutable setting is the avd_options test hook (avd_set_options):
+ *     it must not change while launches are being issued, nor between a *_rows / *_parts /
+ *     *_chunks sizing query and the launch whose buffer it sized (the row counts of the
+ *     persistent kernels follow options.grid_cap);
  *   - `stream` is a hipStream_t (NULL = default stream); launches are asynchronous;
  *   - return AVD_OK (0) or a negative avd_status; shapes are validated before any launch;
  *   - layouts: conv feature maps are channels-last NHWC ([N, H, W, C], bf16 or f32), N = G*B

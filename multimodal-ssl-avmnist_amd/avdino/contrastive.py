@@ -33,20 +33,22 @@ class _Norm:
 
 
 def _world(local, group):
-    if local:
-        return 1, 0
-    return dist.world(group), dist.rank(group)
+    """(world, rank, exchange?) of the negatives: exchange = the gathered path (world > 1, or
+    the world-1 collectives forced by dist.forced())."""
+    if local or not dist.distributed(group):
+        return 1, 0, False
+    return dist.world(group), dist.rank(group), True
 
 
 def infonce(ws, zi, za, B, P, dzi, dza, loss_parts, temperature=0.07, gm=ops.GEMM_F32_MFMA,
             group=None, local=False):
     """zi, za [B, P] (this rank's rows) -> loss_parts [2B] per-row CE (this rank's loss =
     sum(loss_parts) * 0.5 / B), dzi, dza [B, P] (d of that loss).  Returns the scale."""
-    W, r = _world(local, group)
+    W, r, xg = _world(local, group)
     inv_t = 1.0 / temperature
     ni, na = _Norm(ws, "nce.i", zi, B, P), _Norm(ws, "nce.a", za, B, P)
     C = W * B
-    if W == 1:
+    if not xg:
         ni_all, na_all = ni.y, na.y
     else:   # host point: the all-gathers write fixed buffers the next graph segment reads
         ni_all, na_all = ws.get("nce.ni_all", C * P), ws.get("nce.na_all", C * P)
@@ -67,7 +69,7 @@ def infonce(ws, zi, za, B, P, dzi, dza, loss_parts, temperature=0.07, gm=ops.GEM
     cA, cI = ws.get("nce.colA", C * P), ws.get("nce.colI", C * P)
     ops.gemm(C, P, B, dS1, 1, C, ni.y, P, 1, cA, P, alpha=inv_t, mode=gm)
     ops.gemm(C, P, B, dS2, 1, C, na.y, P, 1, cI, P, alpha=inv_t, mode=gm)
-    if W == 1:
+    if not xg:
         ops.axpy(dna, cA)
         ops.axpy(dni, cI)
     else:
@@ -85,11 +87,11 @@ def nt_xent(ws, reps, B, P, dreps, loss_parts, temperature=0.07, gm=ops.GEMM_F32
             local=False):
     """reps [2B, P] = [z1; z2] of this rank -> loss_parts [2B] per-row CE (this rank's loss =
     sum(loss_parts) / 2B), dreps [2B, P].  Returns the scale."""
-    W, r = _world(local, group)
+    W, r, xg = _world(local, group)
     inv_t = 1.0 / temperature
     n = _Norm(ws, "ntx", reps, 2 * B, P)
     nv = n.y.view(2 * B, P)
-    if W == 1:
+    if not xg:
         n_all = n.y
     else:   # global layout [z1 of every rank; z2 of every rank]; host point as in infonce
         n_all = ws.get("ntx.all", 2 * W * B * P)
@@ -110,7 +112,7 @@ def nt_xent(ws, reps, B, P, dreps, loss_parts, temperature=0.07, gm=ops.GEMM_F32
     ops.gemm(2 * B, P, C, dS, C, 1, n_all, P, 1, dn, P, alpha=inv_t, mode=gm)   # row side
     col = ws.get("ntx.col", C * P)
     ops.gemm(C, P, 2 * B, dS, 1, C, n.y, P, 1, col, P, alpha=inv_t, mode=gm)   # column side
-    if W == 1:
+    if not xg:
         ops.axpy(dn, col)
     else:
         cv = col.view(2, W * B, P)

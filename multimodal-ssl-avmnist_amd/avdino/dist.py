@@ -25,6 +25,31 @@ def world(group=None):
     return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
 
 
+# Test hook: issue every collective of the data-parallel path even at world 1 (an all-reduce,
+# all-gather or reduce-scatter over one rank is the identity), so the RCCL branches -- the
+# asynchronous buckets, all_gather_into_tensor, reduce_scatter_tensor -- and the graph-segmented
+# step around them execute on a one-GPU box (tests/test_gpu_rccl.py).  Set through forced().
+_FORCE = [False]
+
+
+class forced:
+    """``with dist.forced(): ...`` -- the data-parallel path at any initialised world size."""
+
+    def __enter__(self):
+        self.prev, _FORCE[0] = _FORCE[0], True
+        return self
+
+    def __exit__(self, *exc):
+        _FORCE[0] = self.prev
+
+
+def distributed(group=None):
+    """Does the step exchange data with other ranks (world > 1, or forced at world 1)?"""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return _FORCE[0] or dist.get_world_size(group) > 1
+
+
 def rank(group=None):
     return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
 
@@ -68,7 +93,7 @@ class GradAllReduce:
         self.pending, self.covered, self.reduced = [], [], []
 
     def bucket(self, grad, ranges):
-        if self.world() == 1:
+        if not distributed(self.group):
             return
         overlap = self._async()
         for lo, hi in ranges:
@@ -86,7 +111,7 @@ class GradAllReduce:
         """All-reduce the rest of ``ranges`` and wait for every collective of this step;
         records the reduced ranges for scale()."""
         self.reduced = []
-        if self.world() > 1:
+        if distributed(self.group):
             want = [(0, grad.numel())] if ranges is None else list(ranges)
             rest = subtract_ranges(want, self.covered)
             for lo, hi in rest:
@@ -145,7 +170,7 @@ def grad_allreduce_hook(group=None):
 def broadcast_buffers(store, src=0, group=None):
     """Rank ``src``'s buffers to every rank: the f32 arena (centre, BN running stats) and the
     int64 num_batches_tracked counters (pending increments applied first)."""
-    if dist.get_world_size(group) > 1:
+    if distributed(group):
         dist.broadcast(store.buf_arena, src=src, group=group)
         store.flush_nbt()
         dist.broadcast(store.nbt_arena, src=src, group=group)
@@ -153,7 +178,7 @@ def broadcast_buffers(store, src=0, group=None):
 
 def broadcast_parameters(store, src=0, group=None):
     """Initial replication (DDP does this once at wrap time): student + teacher arenas."""
-    if dist.get_world_size(group) > 1:
+    if distributed(group):
         dist.broadcast(store.student, src=src, group=group)
         if store.teacher is not None:
             dist.broadcast(store.teacher, src=src, group=group)
@@ -164,7 +189,7 @@ def gather_rows(x, group=None, out=None):
     r*B:(r+1)*B).  Every rank must pass the same B.  ``out``: a fixed destination (what a
     captured step's next segment reads, avdino.capture)."""
     n = dist.get_world_size(group)
-    if n == 1:
+    if not distributed(group):
         if out is not None:
             out.copy_(x)
             return out
@@ -186,7 +211,7 @@ def scatter_rows_grad(dx_all, group=None, out=None):
     """d loss / d(global rows) [world*B, F] from this rank -> SUM over ranks of each rank's
     contribution to MY rows [B, F] (the adjoint of :func:`gather_rows`); ``out`` as there."""
     n = dist.get_world_size(group)
-    if n == 1:
+    if not distributed(group):
         if out is not None:
             out.copy_(dx_all)
             return out

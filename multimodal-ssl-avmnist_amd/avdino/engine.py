@@ -35,7 +35,17 @@ class Workspace:
     """Named device scratch buffers, grown on demand and reused across steps.  Every
     (re)allocation bumps this workspace's own ``epoch``, so graphs captured over its old
     buffers are retired (GraphedStep ``deps``) -- and only those: a probe's or a loss helper's
-    workspace growing does not retire an engine's graphs."""
+    workspace growing does not retire an engine's graphs.
+
+    Cross-stream safety.  A workspace buffer is used by several streams (main,
+    side, weight-gradient, data), but the caching allocator hands out memory in the order of
+    the ALLOCATING stream only: a new buffer may be a block that stream freed while kernels
+    still queued on it use the block, and the buffer a regrowth drops may still be read by
+    another stream.  So every (re)allocation outside a graph capture synchronises the device
+    once the new buffer exists and before the old one is dropped; allocations happen only in
+    warm-up steps and at shape changes, never in a steady-state step.  (Without this, the
+    real-data prefetch's second staging set -- allocated on the main stream under step 0 and
+    written on the data stream -- could land on a block step 0 was still using.)"""
 
     def __init__(self, device):
         self.device = device
@@ -45,8 +55,10 @@ class Workspace:
     def get(self, name, numel, dtype=F32):
         b = self.bufs.get(name)
         if b is None or b.numel() < numel or b.dtype != dtype:
-            b = torch.empty(max(numel, 1), dtype=dtype, device=self.device)
-            self.bufs[name] = b
+            nb = torch.empty(max(numel, 1), dtype=dtype, device=self.device)
+            if nb.is_cuda and not torch.cuda.is_current_stream_capturing():
+                torch.cuda.synchronize(self.device)
+            self.bufs[name] = b = nb
             self.epoch += 1
         return b[:numel]
 
@@ -688,7 +700,7 @@ def _exchange_in_step(hook):
     followed by the 1/world scale and the optimizer in the same (last) graph segment."""
     from . import dist as avdist
     return (hasattr(hook, "finish") and BUCKETS
-            and avdist.world(getattr(hook, "group", None)) > 1)
+            and avdist.distributed(getattr(hook, "group", None)))
 
 
 def _exchange_begin(hook):
@@ -896,9 +908,6 @@ class MultiCentralEngine:
     # the next real-data batch's device augmentation queued on a data stream under the current
     # step (prefetch); False stages every batch synchronously
     PREFETCH = True
-    # the prefetch's data stream starts once the previous step's reads are done (overlapping the
-    # current step) instead of after the current step: off, see prefetch()
-    PREFETCH_OVERLAP = False
 
     def _aug_bufs(self, batch, with_orig, par):
         """Staged-input buffers of set ``par`` (0/1) for a {"aug", "idx"} batch:
@@ -923,21 +932,21 @@ class MultiCentralEngine:
         par = 1 - self._par
         if self.dstream is None:
             self.dstream = torch.cuda.Stream(self.store.device)
-        # The other buffers were last read by the step before the current one, so the data
-        # stream could start once the main stream is past the event stage() recorded in front
-        # of the current step and overlap the current step (PREFETCH_OVERLAP).  That overlap made
-        # graph-replayed prefetched steps differ from the serial ones in about 1 of 3 runs
-        # (tests/test_gpu_augment.py, tools/dbg_prefetch.py: one audio global view of the
-        # prefetched batch differs; no kernel of the step writes into the staging set,
-        # tools/dbg_oob.py; blocking id copies made it rarer, not gone).  Off: the data stream
-        # waits for the whole step queued so far -- the next batch's host work stays hidden,
-        # its GPU work runs after the step.
-        if self.PREFETCH_OVERLAP and self._ev_free is not None:
+        # The other set was last read by the step before the current one, so the data stream
+        # starts once the main stream is past the event stage() recorded in front of the current
+        # step, and the augmentation overlaps the current step.  The set's buffers are taken
+        # from the workspace here, on the main stream: a first allocation (or a regrowth for a
+        # larger batch) synchronises the device inside Workspace.get, so the block cannot be
+        # one that kernels of the current step still use (that was the round-5
+        # race -- set 1 is first allocated under step 0, and the main stream's caching
+        # allocator could hand it a block step 0 had freed but was still writing).
+        main = torch.cuda.current_stream(self.store.device)
+        if self._ev_free is not None:
             self.dstream.wait_event(self._ev_free)
         else:
-            self.dstream.wait_stream(torch.cuda.current_stream(self.store.device))
+            self.dstream.wait_stream(main)
         with_orig = self.heads is not None
-        staged = self._aug_bufs(batch, with_orig, par)      # allocated outside the data stream
+        staged = self._aug_bufs(batch, with_orig, par)
         with torch.cuda.stream(self.dstream):
             batch["aug"].stage(batch["idx"], staged[0], staged[1], with_orig)
             done = torch.cuda.Event()
@@ -993,7 +1002,8 @@ class MultiCentralEngine:
         if self.mode == "semi_supervised":
             labels = ws.get("in.label" + ("" if self._par == 0 else ".1"), B, torch.int64)
             labels.copy_(batch["label"].reshape(-1))
-        if main is not None and training and self.PREFETCH_OVERLAP:
+        if main is not None and training:
+            # everything queued before this step (the last readers of the other set)
             self._ev_free = torch.cuda.Event()
             self._ev_free.record(main)
         return x_img, x_aud, B, G, L, labels
@@ -1326,14 +1336,14 @@ class MultiCentralEngine:
 
     def _global_negatives(self):
         from . import dist as avdist
-        return self.negatives != "local" and avdist.world(self.group) > 1
+        return self.negatives != "local" and avdist.distributed(self.group)
 
     def _bucketed(self):
         """Early gradient bucket: a bucket-capable hook, world > 1, and no pipelined teacher
         forward in flight on its own stream at the bucket's host point."""
         from . import dist as avdist
         return (hasattr(self.grad_hook, "bucket") and self.tin_pending is None and BUCKETS
-                and avdist.world(getattr(self.grad_hook, "group", None)) > 1)
+                and avdist.distributed(getattr(self.grad_hook, "group", None)))
 
     @property
     def _early_ranges(self):
@@ -1777,7 +1787,7 @@ class SimCLREngine:
     def _bucketed(self):
         from . import dist as avdist
         return (hasattr(self.grad_hook, "bucket") and BUCKETS
-                and avdist.world(getattr(self.grad_hook, "group", None)) > 1)
+                and avdist.distributed(getattr(self.grad_hook, "group", None)))
 
     def step(self, batch, mode=None):
         mode = self.draw_mode() if mode is None else int(mode)

@@ -158,6 +158,9 @@ class LinearProbe:
         hipGraph per batch size (after two eager batches of that size)."""
         if self.sstate is not None:
             self.sstate.set_lr(self.lr)   # (a host-side schedule change; eager)
+        # host step count (AdamW bias corrections of the host-state path, snapshot()): counted
+        # here, outside the captured body, so graph-replayed batches advance it too
+        self.t += 1
         if not self.use_graph:
             self._train_step(images, audios, labels, loss_out)
             return
@@ -194,7 +197,6 @@ class LinearProbe:
         ops.act_bwd(h, dr, dh, 0, None, None, N, 1, 128, 0.0, 0)
         ops.linear_bwd(dh, feat, c["classifier.0.weight"], c.grad_of("classifier.0.weight"),
                        c.grad_of("classifier.0.bias"), None, N)
-        self.t += 1                       # (host count; not read by a captured step)
         b1, b2 = 0.9, 0.999
         if dev_state:
             ops.adam_dev(c.student, c.grad, c.adam_m, c.adam_v, c.n_live, self.sstate.hyp, b1, b2,

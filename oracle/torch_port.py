@@ -9,8 +9,10 @@ reference (per-view encoder calls, Python EMA loop, torch.optim.Adam), fp32:
   CentralMultiModalEncoder     models/dino.py:454-468 (+ SimpleMultiModalEncoder 214-234)
   ProjectionHead               models/dino.py:1240-1254
   MultiModalDINO(+WithMSE)     models/dino.py:588-727, 1156-1171
+  MultiModalDINOSemiSupervised models/dino.py:964-980 (mode="semi_supervised")
   dino_loss / mse_loss         models/dino.py:822-854, 1193-1211
-  step order                   dino.py:1214-1238 + Lightning automatic optimisation
+  supervised_loss              models/dino.py:1001-1025
+  step order                   dino.py:1214-1238 (1027-1051) + Lightning automatic optimisation
 Checked against the numpy oracle in tests/test_torch_port.py.
 """
 import torch
@@ -58,9 +60,13 @@ def head(i, o, p=0.0):
 
 
 class DinoMSE(nn.Module):
-    """MultiModalDINOWithMSE(CentralMultiModalEncoder); state-dict keys as the reference."""
+    """MultiModalDINOWithMSE(CentralMultiModalEncoder); state-dict keys as the reference.
+    mode="semi_supervised": MultiModalDINOSemiSupervised (dino.py:964-980) -- the two heads are
+    ``image_classifier`` / ``audio_classifier`` = ProjectionHead(E, num_classes) and forward
+    returns their logits in place of the MSE features."""
 
-    def __init__(self, E=256, D=256, P=128, dropout=0.3, fusion_dropout=0.3):
+    def __init__(self, E=256, D=256, P=128, dropout=0.3, fusion_dropout=0.3, mode="mse",
+                 num_classes=10):
         super().__init__()
         self.student = CentralMM(E, D, fusion_dropout)
         self.teacher = CentralMM(E, D, fusion_dropout)
@@ -73,8 +79,13 @@ class DinoMSE(nn.Module):
         for p in self.teacher_projection.parameters():
             p.requires_grad = False
         self.register_buffer("center", torch.zeros(1, P))
-        self.image_projection_head = head(E, P)
-        self.audio_projection_head = head(E, P)
+        self.mode = mode
+        if mode == "semi_supervised":
+            self.image_classifier = head(E, num_classes)
+            self.audio_classifier = head(E, num_classes)
+        else:
+            self.image_projection_head = head(E, P)
+            self.audio_projection_head = head(E, P)
 
     @torch.no_grad()
     def update_teacher(self, m=0.996):
@@ -96,8 +107,10 @@ class DinoMSE(nn.Module):
             tc = tp - self.center
             self.center = self.center * cm + tp.mean(0, keepdim=True) * (1 - cm)
         B = g_img.shape[0]
-        fi = self.image_projection_head.mlp(self.student.image_encoder(image))
-        fa = self.audio_projection_head.mlp(self.student.audio_encoder(audio))
+        hi, ha = ((self.image_classifier, self.audio_classifier) if self.mode == "semi_supervised"
+                  else (self.image_projection_head, self.audio_projection_head))
+        fi = hi.mlp(self.student.image_encoder(image))
+        fa = ha.mlp(self.student.audio_encoder(audio))
         return fi, fa, sp.view(G + L, B, -1), tc.view(G, B, -1)
 
 
@@ -117,6 +130,11 @@ def mse_loss(a, b):
     return F.mse_loss(F.normalize(a, p=2, dim=1), F.normalize(b, p=2, dim=1))
 
 
+def supervised_loss(il, al, labels):
+    """CE(image logits) + CE(audio logits), mean over the batch (dino.py:1001-1025)."""
+    return F.cross_entropy(il, labels) + F.cross_entropy(al, labels)
+
+
 def make_optimizer(model, lr=1e-4, wd=1e-6):
     return torch.optim.Adam(model.parameters(), lr=lr, weight_decay=wd)
 
@@ -125,7 +143,10 @@ def train_step(model, opt, batch):
     """fwd -> loss -> update_teacher -> zero_grad -> backward -> Adam (dino.py:1214-1238)."""
     fi, fa, s, t = model(batch["image"], batch["audio"], batch["g_img"], batch["g_aud"],
                          batch["l_img"], batch["l_aud"])
-    loss = dino_loss(s, t) + mse_loss(fi, fa)
+    if model.mode == "semi_supervised":
+        loss = dino_loss(s, t) + supervised_loss(fi, fa, batch["label"])
+    else:
+        loss = dino_loss(s, t) + mse_loss(fi, fa)
     model.update_teacher()
     opt.zero_grad()
     loss.backward()

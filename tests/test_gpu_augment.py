@@ -317,11 +317,33 @@ def test_grouped_masking_kernel_equals_the_references_output():
     np.testing.assert_array_equal(out.cpu().numpy()[:, 0], np.stack(refs))
 
 
+def test_workspace_allocation_leaves_no_queued_work():
+    """The round-5 prefetch race: a workspace buffer allocated on the main stream
+    while that stream still had queued kernels could be a block those kernels were using, and the
+    data stream then wrote into it.  Workspace.get now synchronises after every (re)allocation,
+    so a new buffer is safe for any stream: nothing is pending on the allocating stream after
+    it, and a regrowth drops its old buffer only then."""
+    from avdino.engine import Workspace
+    ws = Workspace(torch.device("cuda"))
+    a = torch.randn(2048, 2048, device="cuda")
+    for _ in range(20):                      # a few ms of queued work on the current stream
+        a = a @ a
+        a /= a.norm()
+    b = ws.get("x", 1 << 20)
+    assert torch.cuda.current_stream().query(), "allocation returned with work still queued"
+    for _ in range(20):
+        a = a @ a
+    ws.get("x", 1 << 21)                    # regrowth
+    assert torch.cuda.current_stream().query()
+    assert ws.get("x", 1 << 20).data_ptr() == ws.bufs["x"].data_ptr() != b.data_ptr()
+
+
 @pytest.mark.parametrize("graph", [False, True])
 def test_prefetched_augmentation_steps_equal_serial_steps(tmp_path, graph):
     """Real-data steps whose next batch is augmented on the data stream under the current step
-    (engine.prefetch, double-buffered staged inputs) give the same losses and parameters, bit
-    for bit, as steps that augment each batch in front of it -- eager and graph-replayed."""
+    (engine.prefetch, double-buffered staged inputs; the data stream waits only for the steps
+    before the current one) give the same losses and parameters, bit for bit, as steps that
+    augment each batch in front of it -- eager and graph-replayed."""
     from avdino.data import AVMNISTDinoLoader
     from avdino.engine import Hyper, MultiCentralEngine
     from avdino.params import ParamStore

@@ -116,3 +116,138 @@ def test_fp8_odd_batch_falls_back_per_layer():
         losses[name] = eng.step(batch).item()
         assert np.isfinite(store.grad.double().norm().item())
     assert abs(losses["fp8"] - losses["bf16"]) <= 0.02 * abs(losses["bf16"]), losses
+
+
+# --------------------------------------------------------------- config 5 at size vs the oracle
+def _q_e4m3(t):
+    """Fake e4m3 quantisation with one power-of-two scale per tensor (the MX kernels' rule per
+    staged strip / 32-k block: amax -> [128, 256)), float32 in and out."""
+    a = t.detach().abs().max().item()
+    if a == 0.0:
+        return t
+    k = 7 - int(np.floor(np.log2(a)))
+    s = 2.0 ** k
+    return (t * s).to(torch.float8_e4m3fn).to(t.dtype) / s
+
+
+class _FP8Conv(torch.autograd.Function):
+    """conv2d whose forward, input gradient and weight gradient all see e4m3-rounded operands --
+    the operand treatment of avd_mx_conv_fwd / _dgrad / _wgrad, restated in torch ops."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, pad):
+        xq, wq = _q_e4m3(x), _q_e4m3(w)
+        ctx.save_for_backward(xq, wq)
+        ctx.pad = pad
+        return torch.nn.functional.conv2d(xq, wq, b, padding=pad)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xq, wq = ctx.saved_tensors
+        dq = _q_e4m3(dy)
+        dx = torch.nn.grad.conv2d_input(xq.shape, wq, dq, padding=ctx.pad)
+        dw = torch.nn.grad.conv2d_weight(xq, wq.shape, dq, padding=ctx.pad)
+        return dx, dw, dy.sum((0, 2, 3)), None
+
+
+def _fp8_emulate(model):
+    """Route every conv after the first of each branch (the layers the engine's fp8 mode runs
+    on the MX kernels) through _FP8Conv."""
+    import types
+    for enc in (model.student.image_encoder[0], model.student.audio_encoder[0]):
+        for i in range(2, enc.n + 1):
+            conv = getattr(enc, f"conv{i}")
+
+            def fwd(self, x):
+                return _FP8Conv.apply(x, self.weight, self.bias, self.padding[0])
+            conv.forward = types.MethodType(fwd, conv)
+
+
+def _port_semi(state, batch, E, D, P, autocast_dtype=None, fp8=False):
+    from oracle import torch_port as TP
+    torch.manual_seed(0)
+    m = TP.DinoMSE(E, D, P, dropout=0.0, fusion_dropout=0.0, mode="semi_supervised").cuda()
+    m.load_state_dict(state, strict=True)
+    if fp8:
+        _fp8_emulate(m)
+    b = batch
+    with torch.autocast("cuda", dtype=autocast_dtype or torch.float32, enabled=autocast_dtype is not None):
+        il, al, s_, t_ = m(b["image"], b["audio"], b["g_img"], b["g_aud"], b["l_img"], b["l_aud"])
+        loss = TP.dino_loss(s_.float(), t_.float()) + TP.supervised_loss(il.float(), al.float(), b["label"])
+    loss.backward()
+    out = loss.item(), {k: p.grad.detach().double().clone() for k, p in m.named_parameters()
+                        if p.grad is not None}
+    del m
+    torch.cuda.empty_cache()
+    return out
+
+
+def test_fp8_step_vs_fp32_oracle_config5(capsys):
+    """Config 5's fp8 step at its size -- semi-supervised, B = 4096, 2 global + 4 local views +
+    the originals (N = 28672 samples per conv launch), E = D = 256, P = 128 -- against the ORACLE:
+    the reference's semi-supervised step restated in torch ops (oracle/torch_port.py, pinned to
+    the reference's mm_semi_small fixtures by tests/test_torch_port.py) in fp32, from identical
+    parameters and inputs (no HIP-vs-HIP link).  Bands are derived the way
+    test_bf16_step_vs_fp32_step_config2 derives them: the reference has no fp8 recipe, so its
+    nearest is the same port with the mid-layer convs' forward / input-gradient / weight-gradient
+    operands rounded to e4m3 (_FP8Conv: one power-of-two scale per tensor -- coarser than the
+    kernels' per-strip / per-32-k-block scales) next to its bf16 / fp16 autocast runs.  Every
+    tensor within 2x the larger of those errors (floor 1e-2), the median within 1.25x the
+    emulation's median, the loss within 2x the emulation's loss error (floor 1e-3 relative)."""
+    from avdino.engine import Hyper, MultiCentralEngine
+    from avdino.params import ParamStore
+    from avdino.spec import multimodal_dino_sd
+    from oracle import spec as OS
+    from oracle.params import make_state
+    E = D = 256
+    P, G, L, B = 128, 2, 4, 4096
+    state = {k: torch.from_numpy(np.array(v)) for k, v in
+             make_state(OS.multimodal_dino_spec("semi_supervised", E, D, P), 501).items()}
+    g = torch.Generator(device="cuda").manual_seed(502)
+
+    def px(*s):
+        return torch.randint(0, 256, s, generator=g, device="cuda", dtype=torch.int32).float() / 255
+
+    batch = dict(g_img=px(B, G, 1, 28, 28), g_aud=px(B, G, 1, 112, 112), l_img=px(B, L, 1, 28, 28),
+                 l_aud=px(B, L, 1, 112, 112), image=px(B, 1, 28, 28), audio=px(B, 1, 112, 112),
+                 label=torch.randint(0, 10, (B,), generator=g, device="cuda"))
+    store = ParamStore(multimodal_dino_sd("semi_supervised", E, D, P), "cuda")
+    store.load_state_dict(state)
+    eng = MultiCentralEngine(store, "semi_supervised", E, D, P, Hyper(dropout=0.0, fusion_dropout=0.0),
+                             act_dtype=T, conv_fp8=True)
+    N = (G + L + 1) * B
+    sel = [eng.aud._mx_ok(i, N, B) for i in (1, 2, 3)] + [eng.img._mx_ok(1, N, B)]
+    assert all(sel), ("config 5: every mid-layer forward on the MX kernels", sel)
+    l8 = eng.forward(batch).item()
+    eng.backward()
+    g8 = {k: store.grad_of(k).detach().double().clone() for k in store.live_keys}
+    del eng, store
+    torch.cuda.empty_cache()
+    ref = {n: _port_semi(state, batch, E, D, P, a, f) for n, a, f in
+           (("f32", None, False), ("bf16", torch.bfloat16, False), ("f16", torch.float16, False),
+            ("e4m3", None, True))}
+    l32, r32 = ref["f32"]
+    big = max(v.norm().item() for v in r32.values())
+    keys = [k for k in g8 if r32[k].norm().item() > 1e-6 * big]
+
+    def grel(a, b):
+        return ((a - b).norm() / b.norm()).item()
+    ours = {k: grel(g8[k], r32[k]) for k in keys}
+    ref_err = {n: {k: grel(ref[n][1][k], r32[k]) for k in keys} for n in ("bf16", "f16", "e4m3")}
+    bound = {k: max(ref_err["bf16"][k], ref_err["f16"][k], ref_err["e4m3"][k], 1e-2) for k in keys}
+    ratio = sorted(((ours[k] / bound[k], k) for k in keys), reverse=True)
+    med = float(np.median(list(ours.values())))
+    med_e = float(np.median(list(ref_err["e4m3"].values())))
+    le = abs(ref["e4m3"][0] - l32)
+    with capsys.disabled():
+        print(f"\nconfig-5 fp8 step vs fp32 oracle (B={B}): loss {l8:.6f} vs {l32:.6f} (|d| "
+              f"{abs(l8 - l32):.2e}; e4m3-emulated port {le:.2e}, bf16-autocast "
+              f"{abs(ref['bf16'][0] - l32):.2e})")
+        print(f"grad rel-L2 median: ours fp8 {med:.3e}, port e4m3 {med_e:.3e}, port bf16 "
+              f"{np.median(list(ref_err['bf16'].values())):.3e}")
+        for r, k in ratio[:8]:
+            print(f"  {k}: ours {ours[k]:.3e} port-e4m3 {ref_err['e4m3'][k]:.3e} "
+                  f"port-bf16 {ref_err['bf16'][k]:.3e} (x{r:.2f} of bound)")
+    assert abs(l8 - l32) <= max(2 * le, 1e-3 * abs(l32)), (l8, l32, le)
+    assert ratio[0][0] < 2.0, ratio[:4]
+    assert med < 1.25 * med_e, (med, med_e)

@@ -1,6 +1,7 @@
 """The CPU baseline (oracle/torch_port.py) computes the same step as the float64 oracle:
 same state-dict keys as the reference, same loss on the same inputs (fp32 tolerance)."""
 import numpy as np
+import pytest
 import torch
 
 from oracle import numpy_oracle as O
@@ -47,33 +48,35 @@ def test_config1_pretrain_port_matches_reference_fixture():
     np.testing.assert_allclose(ls, fx["step_losses"], atol=1e-6, rtol=0)
 
 
-def _port_step_grads(dtype, fx):
+def _port_step_grads(dtype, fx, mode="mse"):
     E, D, P, B, G, L, pseed, bseed = [int(x) for x in fx["meta_dims"]]
-    model = TP.DinoMSE(E, D, P, dropout=0.0, fusion_dropout=0.0)
-    state = make_state(S.multimodal_dino_spec("mse", E, D, P), pseed)
+    model = TP.DinoMSE(E, D, P, dropout=0.0, fusion_dropout=0.0, mode=mode)
+    state = make_state(S.multimodal_dino_spec(mode, E, D, P), pseed)
     model.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state.items()})
     model = model.to(dtype)
     model.train()
     b = {k: torch.from_numpy(v) for k, v in make_multimodal_batch(B, G, L, bseed).items()}
     b = {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in b.items()}
     fi, fa, s, t = model(b["image"], b["audio"], b["g_img"], b["g_aud"], b["l_img"], b["l_aud"])
-    loss = TP.dino_loss(s, t) + TP.mse_loss(fi, fa)
+    aux = TP.supervised_loss(fi, fa, b["label"]) if mode == "semi_supervised" else TP.mse_loss(fi, fa)
+    loss = TP.dino_loss(s, t) + aux
     model.update_teacher()
     model.zero_grad()
     loss.backward()
     return loss.item(), {k: p.grad.double().numpy() for k, p in model.named_parameters() if p.grad is not None}
 
 
-def test_torch_port_gradients_match_reference_fixture():
+@pytest.mark.parametrize("mode,name", [("mse", "mm_mse_small"), ("semi_supervised", "mm_semi_small")])
+def test_torch_port_gradients_match_reference_fixture(mode, name):
     """the CPU baseline's gradients, not only its loss, against the reference's
     own step (fixture mm_mse_small): run in float64 it matches the reference's float64 run to
     1e-8 (same algorithm); in fp32 (how bench.py times it) it stays within the reference's own
     fp32-vs-float64 spread (2e-2 on the audio conv tensors, 1e-3 elsewhere)."""
     from tests import golden_util as gu
-    f64, f32 = gu.load("mm_mse_small_f64"), gu.load("mm_mse_small")
+    f64, f32 = gu.load(name + "_f64"), gu.load(name)
     zero = gu.zero_grad_keys(f64)
     for dtype, fx, tol, lt in ((torch.float64, f64, 1e-8, 1e-9), (torch.float32, f32, None, 2e-5)):
-        loss, grads = _port_step_grads(dtype, fx)
+        loss, grads = _port_step_grads(dtype, fx, mode)
         assert abs(loss - float(fx["loss"])) < lt, (loss, float(fx["loss"]))
         live = [str(k) for k in fx["live_keys"]]
         assert sorted(live) == sorted(grads)

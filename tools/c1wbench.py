@@ -1,7 +1,6 @@
 """HIP-event times of the audio conv1 (1->8, 5x5 pad 2, 112x112) training passes at config 2's
 student size (N = 7168, B = 1024): the Gram statistics pass + its float64 finalize, the
-codes-writing BN -> ReLU -> pool pass, the routed moments pass (window / pixel-pair variants by
-AVDINO_C1_MOMWIN) and the combine.  AVDINO_LIB selects a library variant
+codes-writing BN -> ReLU -> pool pass, the routed window-moments pass and the combine.  AVDINO_LIB selects a library variant
 (tools/build_variants.sh).  One line: us per pass and their sum."""
 import os
 import sys
@@ -59,7 +58,7 @@ def main():
                                                            dw, *d3, None, G))
     three = t["gram"] + t["apply"] + t["moments"]
     lib = os.path.basename(os.environ.get("AVDINO_LIB", "libavdino.so"))
-    print(f"{lib} MOMWIN={os.environ.get('AVDINO_C1_MOMWIN', '1')}: " +
+    print(f"{lib}: " +
           "  ".join(f"{k} {v:.1f}" for k, v in t.items()) + f"  | three passes {three:.1f} us")
 
 

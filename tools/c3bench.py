@@ -1,5 +1,5 @@
 """Time the 3x3 conv kernels (fwd / dgrad / wgrad) of config 4 per shape with HIP events.
-    AVDINO_C3_NT=2 AVDINO_C3_GPW=4 python tools/c3bench.py"""
+    python tools/c3bench.py   (AVDINO_LIB=... selects a library build)"""
 import os
 import sys
 
@@ -27,7 +27,7 @@ def timeit(fn, n=10):
 
 def main():
     N, B = 2048, 1024
-    tag = f"NT={os.environ.get('AVDINO_C3_NT', '-')} GPW={os.environ.get('AVDINO_C3_GPW', '-')}"
+    tag = os.path.basename(os.environ.get("AVDINO_LIB", "libavdino.so"))
     only = os.environ.get("C3B_ONLY")            # profiling: one op ("fwd"/"dgrad"/"wgrad")
     pick = os.environ.get("C3B_SHAPE")           # profiling: one shape index
     for si, (Ci, H, Co) in enumerate(SHAPES):

@@ -69,8 +69,6 @@ if __name__ == "__main__":
             self._ev_free = None      # -> the data stream waits for everything queued on main
             return orig(self, batch)
         EN.MultiCentralEngine.prefetch = pf
-    if "nooverlap" in sys.argv:
-        EN.MultiCentralEngine.PREFETCH_OVERLAP = False
     if "nopin" in sys.argv:
         torch.Tensor.pin_memory = lambda self, *a, **k: self
     for _ in range(4):

@@ -1,7 +1,6 @@
 #!/bin/bash
 # Bench lines of every BASELINE config (no CPU baseline): config 5 bf16 and fp8 (B=4096), config 4
-# SimCLR (all 4 modality graphs captured before timing) with the routed 3x3 first layer on and
-# off, config 3 InfoNCE, config 1 UniModal, then the default config 2 line.
+# SimCLR (all 4 modality graphs captured before timing), config 3 InfoNCE, config 1 UniModal, then the default config 2 line.
 #   usage: bash tools/gpu_lines.sh TAG
 TAG=$1
 export TMPDIR=/tmp
@@ -16,7 +15,6 @@ run() {   # label, env, args
 run c5_bf16 "" --mode semi_supervised --dtype bf16
 run c5_fp8 "" --mode semi_supervised --dtype fp8
 run c4_simclr "" --workload simclr
-run c4_simclr_c3off "AVDINO_C1R3_CODES=0" --workload simclr
 run c3_infonce "" --mode infonce
 run c1_uni "" --workload uni
 run c2_mse "" --mode mse
