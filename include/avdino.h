@@ -251,6 +251,24 @@ int avd_cl_bn_bwd_apply_wgrad(const void* y, const void* gout, const float* scal
                               int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
                               void* stream);
 
+/* The whole backward of the audio conv2 layer in one launch (lbwd.hip; CentralUnimodalAudio
+ * conv2 -> bn2 -> ReLU -> MaxPool2d, unimodal.py:185-221: 56x56, Cin 8 -> Cout 16, 5x5 pad 2,
+ * bf16): from y [N][56][56][16] and the pooled gradient gout [N][28][28][16] (layout 0) with
+ * avd_bn_finalize's scale / shift and avd_bn_bwd_finalize's coef -- or, with y == NULL, from a
+ * given dy -- it forms dy exactly as avd_cl_bn_bwd_apply (never stored), and from each staged dy
+ * tile both
+ *   dx [N][56][56][8]   = the input gradient, bit-identical to avd_cl_conv_dgrad (wk_d: the
+ *                         avd_cl_weight_layout(..., dgrad = 1) rows), and
+ *   parts[s][16*8*25]   = per-slab partial dW (sum with avd_sum_rows over `slabs` rows).
+ * Replaces avd_cl_bn_bwd_apply + avd_cl_conv_dgrad + avd_cl_conv_wgrad for that layer.  `slabs`
+ * is the grid: pass the avd_cl_layer_bwd_slabs() value the parts buffer was sized with (0: the
+ * shape is not served).  N / B <= 8 BN groups when y is given. */
+int avd_cl_layer_bwd_slabs(int dt, int N, int Cin, int H, int W, int Cout, int K, int pad);
+int avd_cl_layer_bwd(const void* y, const void* gout, const float* scale, const float* shift,
+                     const float* coef, const void* dy, const void* x, const void* wk_d, void* dx,
+                     float* parts, int slabs, int dt, int N, int B, int Cin, int H, int W, int Cout,
+                     int K, int pad, void* stream);
+
 /* The partial sums of avd_cl_bn_bwd_reduce (same rows and layout, for avd_bn_bwd_finalize)
  * from the POOLED output p = maxpool2(relu(y*scale + shift)) instead of y: at the window's
  * argmax z = gamma*xhat + beta = p, so xhat = (p - beta)/gamma wherever the gradient is routed

@@ -69,6 +69,8 @@ PROTOS = {
     "avd_cl_c1_recompute": [I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "avd_cl_c1_recompute_combine": [P, P, P, P, P, I, I, I, P],
     "avd_cl_bn_bwd_apply_wgrad": [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "avd_cl_layer_bwd_slabs": [I, I, I, I, I, I, I, I],
+    "avd_cl_layer_bwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
     "avd_sum_rows": [P, I, I, L, P, I, P],
     "avd_sum_rows_chunks": [I, I],
     "avd_sum_rows_split": [P, I, I, L, P, I, P, L, P],

@@ -489,6 +489,10 @@ class ConvBranch:
     # streams' kernels (the 14^2 one ran 640-650 us in the graph beside them, 153 us alone)
     WGRAD_MAIN = frozenset({2, 3})
 
+    # the audio conv2 (56^2) backward as ONE launch (avd_cl_layer_bwd: BN-backward apply, input
+    # and weight gradient from the same staged tiles, no dY in HBM); False: apply + dgrad + wgrad
+    LAYER_BWD = True
+
     def backward(self, ws, store, ctx, dfeat, wstream=None):
         """dfeat: gradient of the features (f32 [N, F]; hwc: NHWC act dtype); writes conv/BN
         parameter grads.
@@ -524,6 +528,24 @@ class ConvBranch:
                                 coef, store.grad_of(bk + ".weight"), store.grad_of(bk + ".bias"),
                                 store.grad_of(ck + ".bias"))
             x = ctx["x"][i]
+            wt = ctx["wts"][i]
+            lbs = (ops.cl_layer_bwd_slabs(self.act, N, ci, H, H, co, k, pad)
+                   if (self.LAYER_BWD and i > 0 and mode == 0 and wt[1] is not None and wt[3] is None
+                       and not self._mx_wgrad(i, N)) else 0)
+            if lbs:
+                # the whole layer backward in one launch: dY formed in LDS from y and the pooled
+                # gradient, dX and the dW slabs from the same tiles (lbwd.hip); its own dX
+                # buffer, since gout is the previous dgrad's "bwd_dx"
+                wparts = ws.get(f"lb_parts{i}", lbs * co * ci * k * k)
+                dx = ws.get("bwd_dx_lb", N * H * H * ci, self.act)
+                ops.mark(f"w{i}.begin")
+                ops.cl_layer_bwd(y, gout, st[2], st[3], coef, None, x, wt[1], dx, wparts, lbs, N, B, ci,
+                                 H, H, co, k, pad)
+                ops.sum_rows(wparts, lbs, co * ci * k * k, store.grad_of(ck + ".weight"))
+                ops.mark(f"w{i}.end")
+                gout = dx
+                ops.mark(f"b{i}")
+                continue
             nsl = ops.cl_apply_wgrad_slabs(self.act, N, ci, H, H, co, k, pad) if (i == 0 and mode == 0) else 0
             if nsl:   # first layer: BN-backward apply fused with the weight gradient (no dy)
                 wparts = ws.get("wgrad_parts", nsl * co * ci * k * k)

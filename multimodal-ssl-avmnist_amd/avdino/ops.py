@@ -623,6 +623,38 @@ def cl_bn_bwd_apply_wgrad(y, gout, scale, shift, coef, x, parts, N, B, Cin, H, W
                         p(parts), dtcode(y), N, B, Cin, H, W, Cout, K, pad, stream()))
 
 
+def cl_layer_bwd_slabs(dtype, N, Cin, H, W, Cout, K, pad):
+    """Slabs (= grid) of the fused layer backward (avd_cl_layer_bwd), 0 if the shape is not
+    served (the audio conv2: 56^2, 8 -> 16, 5x5 pad 2, bf16)."""
+    return lib.avd_cl_layer_bwd_slabs(_DT[dtype], N, Cin, H, W, Cout, K, pad)
+
+
+def cl_layer_bwd(y, gout, scale, shift, coef, dy, x, wk_d, dx, parts, slabs, N, B, Cin, H, W, Cout,
+                 K, pad):
+    """The whole backward of one conv layer in one launch (lbwd.hip): dY formed from y and the
+    pooled gradient (or taken from ``dy`` when y is None) in LDS only, dX (bit-identical to
+    cl_conv_dgrad) and the weight-gradient slabs parts[slabs][Cout*Cin*K*K] (sum_rows)."""
+    Ho = H + 2 * pad - K + 1
+    _need(slabs > 0 and parts.dtype == torch.float32 and parts.numel() >= slabs * Cout * Cin * K * K,
+          "layer bwd slabs / parts")
+    _need(x.dtype == dx.dtype == torch.bfloat16 and x.numel() == N * H * W * Cin and dx.numel() == x.numel(),
+          "layer bwd x / dx")
+    _need(wk_d.numel() >= cl_weight_elems(Cout, Cin, K, 1), "layer bwd dgrad weights")
+    if y is not None:
+        _need(y.dtype == torch.bfloat16 and y.numel() == N * Ho * Ho * Cout, "layer bwd y")
+        _need(gout.dtype == torch.bfloat16 and gout.numel() == N * (Ho // 2) * (Ho // 2) * Cout, "layer bwd gout")
+        _need(N % B == 0 and N // B <= 8, "layer bwd groups")
+        nb = (y.numel() + gout.numel() + x.numel() + dx.numel()) * 2
+    else:
+        _need(dy is not None and dy.dtype == torch.bfloat16 and dy.numel() == N * Ho * Ho * Cout, "layer bwd dy")
+        nb = (dy.numel() + x.numel() + dx.numel()) * 2
+    nb += slabs * Cout * Cin * K * K * 4
+    fl = 2 * 2 * N * Ho * Ho * Cout * Cin * K * K
+    _timed(f"cl_layer_bwd[{N}x{H}x{W}x{Cin}->{Cout} k{K} {'apply' if y is not None else 'dy'}]", nb, fl,
+           lambda: call("avd_cl_layer_bwd", p(y), p(gout), p(scale), p(shift), p(coef), p(dy), p(x),
+                        p(wk_d), p(dx), p(parts), int(slabs), 1, N, B, Cin, H, W, Cout, K, pad, stream()))
+
+
 C1_STATS, C1_APPLY, C1_REDUCE, C1_WGRAD, C1_REDUCE_MOMENTS = 0, 1, 2, 3, 4
 
 

@@ -514,7 +514,11 @@ def test_fp32_step_vs_float64_port_config2(capsys):
     reference's step restated in torch ops in fp32 (torch_port) both differ from the float64
     port by their own fp32 rounding and summation order; the engine must not be worse than the
     reference's own fp32 recipe: per tensor, rel-L2(engine, f64) <= max(1.5 x rel-L2(port fp32,
-    f64), 1e-4), where 1e-4 is SURVEY 8(c)'s per-tensor bound.  Loss within 1e-5 of float64.
+    f64), 1e-4), where 1e-4 is SURVEY 8(c)'s per-tensor bound, and the median over tensors within
+    1.1x the port's median.  Loss within 1e-5 of float64.  Measured (round 6): engine median 2.41e-5
+    vs port 2.50e-5, worst 2.11e-3 (audio bn3 bias, 1.50x the port's 1.41e-3) vs the port's worst
+    2.43e-3 -- the 2.9e-3 between the fp32 engine and the fp32 port is the two fp32 recipes'
+    own rounding, not an engine error.
     Tensors whose float64 gradient is below 1e-6 of the largest (the conv / Linear biases that
     feed a BatchNorm: mathematically zero, rounding noise only) are excluded, as in SURVEY 8(c)."""
     from avdino.engine import Hyper, MultiCentralEngine
@@ -560,6 +564,7 @@ def test_fp32_step_vs_float64_port_config2(capsys):
         print(f"  worst engine tensor {worst}: {ours[worst]:.3e} (port {port[worst]:.3e})")
     assert abs(l32 - l64) < 1e-5, (l32, l64)
     assert not bad, bad
+    assert np.median(list(ours.values())) <= 1.1 * np.median(list(port.values()))
 
 
 def _ref_curve(state, batches, E, D, P, autocast_dtype):

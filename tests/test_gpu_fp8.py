@@ -132,22 +132,25 @@ def _q_e4m3(t):
 
 class _FP8Conv(torch.autograd.Function):
     """conv2d whose forward, input gradient and weight gradient all see e4m3-rounded operands --
-    the operand treatment of avd_mx_conv_fwd / _dgrad / _wgrad, restated in torch ops."""
+    the operand treatment of avd_mx_conv_fwd / _dgrad / _wgrad, restated in torch ops.  Under
+    bf16 autocast the conv runs on the (bf16-exact) e4m3 values and its output and input
+    gradient are bf16, like the engine's stored maps."""
 
     @staticmethod
     def forward(ctx, x, w, b, pad):
-        xq, wq = _q_e4m3(x), _q_e4m3(w)
+        xq, wq = _q_e4m3(x.float()), _q_e4m3(w.float())
         ctx.save_for_backward(xq, wq)
-        ctx.pad = pad
-        return torch.nn.functional.conv2d(xq, wq, b, padding=pad)
+        ctx.pad, ctx.xdt = pad, x.dtype
+        cdt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else torch.float32
+        return torch.nn.functional.conv2d(xq.to(cdt), wq.to(cdt), b.to(cdt), padding=pad)
 
     @staticmethod
     def backward(ctx, dy):
         xq, wq = ctx.saved_tensors
-        dq = _q_e4m3(dy)
+        dq = _q_e4m3(dy.float())
         dx = torch.nn.grad.conv2d_input(xq.shape, wq, dq, padding=ctx.pad)
         dw = torch.nn.grad.conv2d_weight(xq, wq.shape, dq, padding=ctx.pad)
-        return dx, dw, dy.sum((0, 2, 3)), None
+        return dx.to(ctx.xdt), dw, dy.float().sum((0, 2, 3)), None
 
 
 def _fp8_emulate(model):
@@ -183,24 +186,27 @@ def _port_semi(state, batch, E, D, P, autocast_dtype=None, fp8=False):
 
 
 def test_fp8_step_vs_fp32_oracle_config5(capsys):
-    """Config 5's fp8 step at its size -- semi-supervised, B = 4096, 2 global + 4 local views +
-    the originals (N = 28672 samples per conv launch), E = D = 256, P = 128 -- against the ORACLE:
+    """Config 5's fp8 step at scale -- semi-supervised, B = 1024, 2 global + 4 local views + the
+    originals (N = 7168 samples per conv launch; the MX kernels themselves are checked at config
+    5's N = 28672 in test_gpu_mx.py), E = D = 256, P = 128 -- against the ORACLE:
     the reference's semi-supervised step restated in torch ops (oracle/torch_port.py, pinned to
     the reference's mm_semi_small fixtures by tests/test_torch_port.py) in fp32, from identical
     parameters and inputs (no HIP-vs-HIP link).  Bands are derived the way
     test_bf16_step_vs_fp32_step_config2 derives them: the reference has no fp8 recipe, so its
     nearest is the same port with the mid-layer convs' forward / input-gradient / weight-gradient
     operands rounded to e4m3 (_FP8Conv: one power-of-two scale per tensor -- coarser than the
-    kernels' per-strip / per-32-k-block scales) next to its bf16 / fp16 autocast runs.  Every
-    tensor within 2x the larger of those errors (floor 1e-2), the median within 1.25x the
-    emulation's median, the loss within 2x the emulation's loss error (floor 1e-3 relative)."""
+    kernels' per-strip / per-32-k-block scales), in fp32 and under bf16 autocast (the
+    reference's mixed-precision recipe with fp8 convs: bf16 maps like ours), next to its bf16 /
+    fp16 autocast runs.  Every tensor within 2x the largest of those errors (floor 1e-2), the
+    median within 1.25x the emulations' median, the loss within 2x the emulations' loss error
+    (floor 1e-3 relative)."""
     from avdino.engine import Hyper, MultiCentralEngine
     from avdino.params import ParamStore
     from avdino.spec import multimodal_dino_sd
     from oracle import spec as OS
     from oracle.params import make_state
     E = D = 256
-    P, G, L, B = 128, 2, 4, 4096
+    P, G, L, B = 128, 2, 4, 1024
     state = {k: torch.from_numpy(np.array(v)) for k, v in
              make_state(OS.multimodal_dino_spec("semi_supervised", E, D, P), 501).items()}
     g = torch.Generator(device="cuda").manual_seed(502)
@@ -220,12 +226,17 @@ def test_fp8_step_vs_fp32_oracle_config5(capsys):
     assert all(sel), ("config 5: every mid-layer forward on the MX kernels", sel)
     l8 = eng.forward(batch).item()
     eng.backward()
+    with capsys.disabled():
+        print(f"\n  fp8 engine: loss {l8:.6f}", flush=True)
     g8 = {k: store.grad_of(k).detach().double().clone() for k in store.live_keys}
     del eng, store
     torch.cuda.empty_cache()
-    ref = {n: _port_semi(state, batch, E, D, P, a, f) for n, a, f in
-           (("f32", None, False), ("bf16", torch.bfloat16, False), ("f16", torch.float16, False),
-            ("e4m3", None, True))}
+    ref = {}
+    for n, a, f in (("f32", None, False), ("bf16", torch.bfloat16, False), ("f16", torch.float16, False),
+                    ("e4m3", None, True), ("e4m3_bf16", torch.bfloat16, True)):
+        ref[n] = _port_semi(state, batch, E, D, P, a, f)
+        with capsys.disabled():
+            print(f"  port {n}: loss {ref[n][0]:.6f}", flush=True)
     l32, r32 = ref["f32"]
     big = max(v.norm().item() for v in r32.values())
     keys = [k for k in g8 if r32[k].norm().item() > 1e-6 * big]
@@ -233,12 +244,13 @@ def test_fp8_step_vs_fp32_oracle_config5(capsys):
     def grel(a, b):
         return ((a - b).norm() / b.norm()).item()
     ours = {k: grel(g8[k], r32[k]) for k in keys}
-    ref_err = {n: {k: grel(ref[n][1][k], r32[k]) for k in keys} for n in ("bf16", "f16", "e4m3")}
-    bound = {k: max(ref_err["bf16"][k], ref_err["f16"][k], ref_err["e4m3"][k], 1e-2) for k in keys}
+    em = ("bf16", "f16", "e4m3", "e4m3_bf16")
+    ref_err = {n: {k: grel(ref[n][1][k], r32[k]) for k in keys} for n in em}
+    bound = {k: max([ref_err[n][k] for n in em] + [1e-2]) for k in keys}
     ratio = sorted(((ours[k] / bound[k], k) for k in keys), reverse=True)
     med = float(np.median(list(ours.values())))
-    med_e = float(np.median(list(ref_err["e4m3"].values())))
-    le = abs(ref["e4m3"][0] - l32)
+    med_e = float(np.median([max(ref_err["e4m3"][k], ref_err["e4m3_bf16"][k]) for k in keys]))
+    le = max(abs(ref["e4m3"][0] - l32), abs(ref["e4m3_bf16"][0] - l32))
     with capsys.disabled():
         print(f"\nconfig-5 fp8 step vs fp32 oracle (B={B}): loss {l8:.6f} vs {l32:.6f} (|d| "
               f"{abs(l8 - l32):.2e}; e4m3-emulated port {le:.2e}, bf16-autocast "
@@ -246,8 +258,8 @@ def test_fp8_step_vs_fp32_oracle_config5(capsys):
         print(f"grad rel-L2 median: ours fp8 {med:.3e}, port e4m3 {med_e:.3e}, port bf16 "
               f"{np.median(list(ref_err['bf16'].values())):.3e}")
         for r, k in ratio[:8]:
-            print(f"  {k}: ours {ours[k]:.3e} port-e4m3 {ref_err['e4m3'][k]:.3e} "
-                  f"port-bf16 {ref_err['bf16'][k]:.3e} (x{r:.2f} of bound)")
+            print(f"  {k}: ours {ours[k]:.3e} port-e4m3 {ref_err['e4m3'][k]:.3e} port-e4m3-bf16 "
+                  f"{ref_err['e4m3_bf16'][k]:.3e} port-bf16 {ref_err['bf16'][k]:.3e} (x{r:.2f} of bound)")
     assert abs(l8 - l32) <= max(2 * le, 1e-3 * abs(l32)), (l8, l32, le)
     assert ratio[0][0] < 2.0, ratio[:4]
     assert med < 1.25 * med_e, (med, med_e)
