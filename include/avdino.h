@@ -251,6 +251,20 @@ int avd_cl_bn_bwd_apply_wgrad(const void* y, const void* gout, const float* scal
                               int dt, int N, int B, int Cin, int H, int W, int Cout, int K, int pad,
                               void* stream);
 
+/* Fused softmax cross-entropy over S = inv_t Q K^T without storing S (xent.hip): the InfoNCE
+ * (dino.py:1091-1128) and NT-Xent (multimodal_simclr.py:74-89) losses with both gradients, for
+ * this rank's rows q [R][P] (L2-normalised, f32) against the gathered columns k [C][P], on the
+ * bf16 MFMA (flash-style: online row softmax, column pass from the row lse).  Row i is in half
+ * h = i / Bh (R <= 2 Bh) with i' = i - h Bh; its target column is tgt_h + i', its masked column
+ * msk_h + i' (msk_h < 0: none).  Writes loss[R] = lse_i - S[i][t(i)] (the unscaled per-row CE,
+ * as avd_softmax_xent's loss_parts), dq[R][P] = gscale inv_t (sum_j p_ij k_j - k_t(i)) and
+ * dk[C][P] = gscale inv_t (sum_i p_ij q_i - sum_{t(i) = j} q_i).  P = 128 or 256; ws holds
+ * avd_xent_fused_ws(R, C, P) floats.  Deterministic (fixed-order partial sums, no atomics). */
+int avd_xent_fused_ws(int R, int C, int P);
+int avd_xent_fused(const float* q, const float* k, int R, int C, int P, int Bh, int tgt0, int tgt1,
+                   int msk0, int msk1, float inv_t, float gscale, float* loss, float* dq, float* dk,
+                   float* ws, long long ws_elems, void* stream);
+
 /* The whole backward of the audio conv2 layer in one launch (lbwd.hip; CentralUnimodalAudio
  * conv2 -> bn2 -> ReLU -> MaxPool2d, unimodal.py:185-221: 56x56, Cin 8 -> Cout 16, 5x5 pad 2,
  * bf16): from y [N][56][56][16] and the pooled gradient gout [N][28][28][16] (layout 0) with

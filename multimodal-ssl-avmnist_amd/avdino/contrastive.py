@@ -15,7 +15,10 @@ reference's single-device loss exactly.  The collectives are host points (avdino
 fixed workspace buffers, so a global-negative step is still a captured graph -- three
 segments around the gather and the scatter.
 
-Compute is libavdino: l2norm, MFMA GEMMs, softmax-CE with offset targets / masks, axpy.
+Compute is libavdino: l2norm, then -- with bf16 MFMA operands (the bench precision) and P = 128
+or 256 -- the fused softmax-CE avd_xent_fused (xent.hip: S never stored; rows then columns,
+flash-style), else (the fp32 parity mode) MFMA GEMMs into f32 S / dS and avd_softmax_xent with
+offset targets / masks; axpy.
 """
 from . import dist, ops
 from .capture import host_point
@@ -40,6 +43,14 @@ def _world(local, group):
     return dist.world(group), dist.rank(group), True
 
 
+# the bf16 step's contrastive losses on the fused kernel (False: GEMMs + softmax-CE over S)
+FUSED = True
+
+
+def _fused(gm, P):
+    return FUSED and gm == ops.GEMM_BF16_MFMA and P in (128, 256)
+
+
 def infonce(ws, zi, za, B, P, dzi, dza, loss_parts, temperature=0.07, gm=ops.GEMM_F32_MFMA,
             group=None, local=False):
     """zi, za [B, P] (this rank's rows) -> loss_parts [2B] per-row CE (this rank's loss =
@@ -54,6 +65,16 @@ def infonce(ws, zi, za, B, P, dzi, dza, loss_parts, temperature=0.07, gm=ops.GEM
         ni_all, na_all = ws.get("nce.ni_all", C * P), ws.get("nce.na_all", C * P)
         host_point(lambda: (dist.gather_rows(ni.y.view(B, P), group, out=ni_all.view(C, P)),
                             dist.gather_rows(na.y.view(B, P), group, out=na_all.view(C, P))))
+    if _fused(gm, P):
+        # rows of S1 = n(i) n(a_all)^T / tau and S2 = n(a) n(i_all)^T / tau, targets r*B + i
+        xw = ws.get("nce.xws", ops.xent_fused_ws(B, C, P))
+        dni, dna = ws.get("nce.dni", B * P), ws.get("nce.dna", B * P)
+        cA, cI = ws.get("nce.colA", C * P), ws.get("nce.colI", C * P)
+        ops.xent_fused(ni.y, na_all, B, C, P, B, (r * B, 0), (-1, -1), inv_t, 0.5 / B, loss_parts[:B],
+                       dni, cA, xw)
+        ops.xent_fused(na.y, ni_all, B, C, P, B, (r * B, 0), (-1, -1), inv_t, 0.5 / B,
+                       loss_parts[B:2 * B], dna, cI, xw)
+        return _infonce_tail(ws, ni, na, dni, dna, cA, cI, dzi, dza, B, P, C, xg, group)
     S1, S2 = ws.get("nce.S1", B * C), ws.get("nce.S2", B * C)
     ops.gemm(B, C, P, ni.y, P, 1, na_all, 1, P, S1, C, alpha=inv_t, mode=gm)   # image rows
     ops.gemm(B, C, P, na.y, P, 1, ni_all, 1, P, S2, C, alpha=inv_t, mode=gm)   # audio rows
@@ -69,6 +90,12 @@ def infonce(ws, zi, za, B, P, dzi, dza, loss_parts, temperature=0.07, gm=ops.GEM
     cA, cI = ws.get("nce.colA", C * P), ws.get("nce.colI", C * P)
     ops.gemm(C, P, B, dS1, 1, C, ni.y, P, 1, cA, P, alpha=inv_t, mode=gm)
     ops.gemm(C, P, B, dS2, 1, C, na.y, P, 1, cI, P, alpha=inv_t, mode=gm)
+    return _infonce_tail(ws, ni, na, dni, dna, cA, cI, dzi, dza, B, P, C, xg, group)
+
+
+def _infonce_tail(ws, ni, na, dni, dna, cA, cI, dzi, dza, B, P, C, xg, group):
+    """Column gradients home (added, or reduce-scattered to their owners), then the l2norm
+    backward."""
     if not xg:
         ops.axpy(dna, cA)
         ops.axpy(dni, cI)
@@ -99,19 +126,29 @@ def nt_xent(ws, reps, B, P, dreps, loss_parts, temperature=0.07, gm=ops.GEMM_F32
         host_point(lambda: (dist.gather_rows(nv[:B], group, out=av[0]),
                             dist.gather_rows(nv[B:], group, out=av[1])))
     C = 2 * W * B
+    g = 1.0 / (2 * B)
+    dn = ws.get("ntx.dn", 2 * B * P)
+    col = ws.get("ntx.col", C * P)
+    if _fused(gm, P):
+        # z1 rows: target W*B + r*B + i, own column r*B + i masked; z2 rows the other way round
+        xw = ws.get("ntx.xws", ops.xent_fused_ws(2 * B, C, P))
+        ops.xent_fused(n.y, n_all, 2 * B, C, P, B, (W * B + r * B, r * B), (r * B, W * B + r * B), inv_t, g,
+                       loss_parts, dn, col, xw)
+        return _ntxent_tail(ws, n, dn, col, dreps, B, P, W, xg, group, g)
     S = ws.get("ntx.S", 2 * B * C)
     ops.gemm(2 * B, C, P, n.y, P, 1, n_all, 1, P, S, C, alpha=inv_t, mode=gm)
     dS = ws.get("ntx.dS", 2 * B * C)
-    g = 1.0 / (2 * B)
     # z1 rows: global row r*B + i, positive W*B + r*B + i; z2 rows: W*B + r*B + i -> r*B + i
     ops.softmax_xent(S, C, B, C, None, 1, False, True, g, loss_parts[:B], dS, C, False,
                      tgt_off=W * B + r * B, mask_off=r * B)
     ops.softmax_xent(S[B * C:], C, B, C, None, 1, False, True, g, loss_parts[B:2 * B], dS[B * C:],
                      C, False, tgt_off=r * B, mask_off=W * B + r * B)
-    dn = ws.get("ntx.dn", 2 * B * P)
     ops.gemm(2 * B, P, C, dS, C, 1, n_all, P, 1, dn, P, alpha=inv_t, mode=gm)   # row side
-    col = ws.get("ntx.col", C * P)
     ops.gemm(C, P, 2 * B, dS, 1, C, n.y, P, 1, col, P, alpha=inv_t, mode=gm)   # column side
+    return _ntxent_tail(ws, n, dn, col, dreps, B, P, W, xg, group, g)
+
+
+def _ntxent_tail(ws, n, dn, col, dreps, B, P, W, xg, group, g):
     if not xg:
         ops.axpy(dn, col)
     else:

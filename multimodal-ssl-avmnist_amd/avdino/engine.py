@@ -946,8 +946,8 @@ class MultiCentralEngine:
         data stream, into the staging buffers the current step does not read, so it runs under
         the step just queued instead of in front of the next one.  The next stage() of that same
         batch object waits for it and takes those buffers.  Returns False when not applicable
-        (synthetic views, no side streams, prefetch off)."""
-        if not self.PREFETCH or "aug" not in batch or self.side is None:
+        (synthetic views, no GPU, prefetch off)."""
+        if not self.PREFETCH or "aug" not in batch or self.store.device.type != "cuda":
             return False
         if self._pf is not None:
             raise RuntimeError("prefetch: the previously prefetched batch was never consumed")

@@ -1002,6 +1002,24 @@ def softmax_xent(logits, ld, R, C, targets, target_mode, col_major, mask_diag, g
          stream())
 
 
+def xent_fused_ws(R, C, P):
+    n = lib.avd_xent_fused_ws(R, C, P)
+    _need(n > 0, f"fused softmax-CE: P must be 128 or 256 (got {P})")
+    return n
+
+
+def xent_fused(q, k, R, C, P, Bh, tgt, msk, inv_t, gscale, loss, dq, dk, ws):
+    """Softmax cross-entropy over S = inv_t q k^T with per-half targets / masks, loss rows and
+    both gradients, without materialising S (avd_xent_fused, xent.hip; bf16 MFMA)."""
+    for t, n in ((q, R * P), (k, C * P), (dq, R * P), (dk, C * P), (loss, R)):
+        _need(t.dtype == torch.float32 and t.is_contiguous() and t.numel() >= n, "xent operand")
+    _need(ws.dtype == torch.float32 and ws.numel() >= xent_fused_ws(R, C, P), "xent workspace")
+    fl = 4 * 2 * R * C * P
+    _timed(f"xent_fused[{R}x{C}x{P}]", 4 * (2 * R * P + 2 * C * P + R), fl,
+           lambda: call("avd_xent_fused", p(q), p(k), R, C, P, Bh, int(tgt[0]), int(tgt[1]), int(msk[0]),
+                        int(msk[1]), inv_t, gscale, p(loss), p(dq), p(dk), p(ws), ws.numel(), stream()))
+
+
 def cosine_consistency(emb, V, B, D, alpha, loss_parts, demb):
     _need(emb.numel() >= V * B * D and (demb is None or demb.numel() >= V * B * D)
           and (loss_parts is None or loss_parts.numel() >= B), "cosine consistency shapes")

@@ -13,8 +13,9 @@ reduce-scatter records the full column gradient d(gathered rows) and hands back 
 slice (the other ranks' contributions to it are theirs to send).  Against float64 autograd of
 the same per-rank loss (the reference's formula over the global batch, restricted to this
 rank's rows): per-row CE terms, d loss / d(local rows) (row side + this rank's column side) and
-the column gradient of every other rank's rows.  fp32 operands (the parity mode): loss 1e-6
-relative, gradients 1e-4 rel-L2; bf16 MFMA operands (the bench mode): within 2x the torch
+the column gradient of every other rank's rows.  fp32 operands (the parity mode: GEMMs and
+softmax-CE over a stored S): loss 1e-6 relative, gradients 1e-4 rel-L2; bf16 MFMA operands (the
+bench mode: the fused kernel avd_xent_fused, S never stored): within 2x the torch
 fp16-autocast error of the same loss (the reference's '16-mixed'), floor 1e-3 / 1e-2."""
 import numpy as np
 import pytest
@@ -180,3 +181,63 @@ def test_ntxent_config4_gathered_size(monkeypatch, mode, capsys):
     with capsys.disabled():
         print(f"\nNT-Xent [{2 * B} x {C}] {mode}: " + ", ".join(f"{k} {v:.2e} (tol {tol[k]:.1e})" for k, v in err.items()))
     assert all(err[k] <= tol[k] for k in err), (err, tol)
+
+
+def _xent_ref(q, k, Bh, tgt, msk, inv_t, g, cast=None):
+    """float64 autograd of the per-row CE over S = inv_t q k^T with per-half targets / masks."""
+    q = q.detach().to(F64).requires_grad_()
+    k = k.detach().to(F64).requires_grad_()
+    R, C = q.shape[0], k.shape[0]
+    a, b = (q, k) if cast is None else (q.to(cast), k.to(cast))
+    S = (a @ b.T).to(F64) * inv_t
+    i = torch.arange(R, device="cuda")
+    h = (i >= Bh).long()
+    ii = i - h * Bh
+    t = torch.tensor(tgt, device="cuda")[h] + ii
+    m = torch.tensor(msk, device="cuda")[h]
+    mask = torch.zeros(R, C, dtype=torch.bool, device="cuda")
+    has = m >= 0
+    mask[i[has], (m + ii)[has]] = True
+    S = S.masked_fill(mask, float("-inf"))
+    ce = torch.nn.functional.cross_entropy(S, t, reduction="none")
+    (ce.sum() * g).backward()
+    return ce.detach(), q.grad, k.grad
+
+
+XCASES = [  # R, C, P, Bh, tgt, msk  (NT-Xent: R = 2 Bh, C = 2 W Bh; InfoNCE: R = Bh, C = W Bh)
+    (10, 10, 128, 5, (5, 0), (0, 5)),                 # NT-Xent, world 1, tails everywhere
+    (6, 24, 256, 3, (15, 3), (3, 15)),                # NT-Xent, a rank of world 4
+    (7, 21, 256, 7, (7, 0), (-1, -1)),                # InfoNCE, rank 1 of world 3
+    (200, 200, 128, 100, (100, 0), (0, 100)),         # several row / column blocks
+    (96, 768, 128, 96, (288, 0), (-1, -1)),           # InfoNCE rank 3 of 8, column splits
+]
+
+
+@pytest.mark.parametrize("case", XCASES, ids=[f"R{c[0]}C{c[1]}P{c[2]}" for c in XCASES])
+def test_xent_fused_against_float64(case, capsys):
+    """avd_xent_fused (xent.hip) on edge shapes -- rows / columns not multiples of the 64-row
+    block or the 32-column step, one or two halves, with and without a masked own column --
+    against float64 autograd of the same loss; bands as above (2x the fp16-operand error of the
+    same float64 computation, floors 1e-3 / 1e-2)."""
+    from avdino import ops
+    R, C, P, Bh, tgt, msk = case
+    g_ = torch.Generator(device="cuda").manual_seed(R * 1000 + C)
+    q, k = _unit(g_, R, P), _unit(g_, C, P)
+    inv_t, gs = 1.0 / 0.07, 1.0 / R
+    loss = torch.empty(R, device="cuda")
+    dq, dk = torch.empty(R, P, device="cuda"), torch.empty(C, P, device="cuda")
+    ws = torch.empty(ops.xent_fused_ws(R, C, P), device="cuda")
+    ops.xent_fused(q, k, R, C, P, Bh, tgt, msk, inv_t, gs, loss, dq, dk, ws)
+    torch.cuda.synchronize()
+    ce, gq, gk = _xent_ref(q, k, Bh, tgt, msk, inv_t, gs)
+    c16, q16, k16 = _xent_ref(q, k, Bh, tgt, msk, inv_t, gs, cast=torch.float16)
+    err = dict(loss=_rel(loss, ce), dq=_rel(dq, gq), dk=_rel(dk, gk))
+    band = dict(loss=_rel(c16, ce), dq=_rel(q16, gq), dk=_rel(k16, gk))
+    tol = {n: max(2 * band[n], 1e-3 if n == "loss" else 1e-2) for n in err}
+    with capsys.disabled():
+        print(f"\nxent R={R} C={C} P={P}: " + ", ".join(f"{n} {err[n]:.2e} (tol {tol[n]:.1e})" for n in err))
+    assert all(err[n] <= tol[n] for n in err), (err, tol)
+    # deterministic: a second launch is bit-identical
+    loss2, dq2, dk2 = torch.empty_like(loss), torch.empty_like(dq), torch.empty_like(dk)
+    ops.xent_fused(q, k, R, C, P, Bh, tgt, msk, inv_t, gs, loss2, dq2, dk2, ws)
+    assert torch.equal(loss, loss2) and torch.equal(dq, dq2) and torch.equal(dk, dk2)

@@ -154,10 +154,11 @@ class _FP8Conv(torch.autograd.Function):
 
 
 def _fp8_emulate(model):
-    """Route every conv after the first of each branch (the layers the engine's fp8 mode runs
-    on the MX kernels) through _FP8Conv."""
+    """Route every conv after the first of each branch, student AND teacher (the layers the
+    engine's fp8 mode runs on the MX kernels), through _FP8Conv."""
     import types
-    for enc in (model.student.image_encoder[0], model.student.audio_encoder[0]):
+    for enc in (model.student.image_encoder[0], model.student.audio_encoder[0],
+                model.teacher.image_encoder[0], model.teacher.audio_encoder[0]):
         for i in range(2, enc.n + 1):
             conv = getattr(enc, f"conv{i}")
 

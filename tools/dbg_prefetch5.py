@@ -1,0 +1,106 @@
+"""Debug: which ingredient does the prefetch mismatch need?  REPS runs per variant, graph-replayed,
+no synchronisation between steps (the test's setting), compared with the serial run:
+  A  prefetch as shipped (data stream overlaps the current step; two staging sets)
+  F  the data stream waits for the whole queued step (no overlap)
+  G  overlap, but the data stream writes a private scratch set that the main stream copies into
+     the staging set after the step (no graph-referenced memory written concurrently)
+  I  overlap, one stream per step (concurrent=False: no side streams inside the graphs)
+    python tools/dbg_prefetch5.py REPS A F G I"""
+import os
+import sys
+import tempfile
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "multimodal-ssl-avmnist_amd")]
+import torch  # noqa: E402
+
+from tests.test_gpu_augment import _fake_avmnist  # noqa: E402
+from avdino import engine as EN  # noqa: E402
+from avdino.data import AVMNISTDinoLoader  # noqa: E402
+from avdino.params import ParamStore  # noqa: E402
+from avdino.spec import multimodal_dino_sd  # noqa: E402
+
+_orig_pf = EN.MultiCentralEngine.prefetch
+_orig_bufs = EN.MultiCentralEngine._aug_bufs
+_orig_stage = EN.MultiCentralEngine.stage
+
+
+def pf_wait_all(self, batch):
+    self._ev_free = None
+    return _orig_pf(self, batch)
+
+
+def bufs_scratch(self, batch, with_orig, par):
+    # prefetch() asks for set `par`: hand it a scratch set; stage() copies it over on main
+    if getattr(self, "_in_pf", False):
+        x_img, x_aud, B, G, L = _orig_bufs(self, batch, with_orig, par)
+        si = self.ws.get("scr.img", x_img.numel(), x_img.dtype)
+        sa = self.ws.get("scr.aud", x_aud.numel(), x_aud.dtype)
+        self._scr = (si, sa, x_img, x_aud)
+        return si, sa, B, G, L
+    return _orig_bufs(self, batch, with_orig, par)
+
+
+def pf_scratch(self, batch):
+    self._in_pf = True
+    try:
+        return _orig_pf(self, batch)
+    finally:
+        self._in_pf = False
+
+
+def stage_scratch(self, batch, with_orig, training=True):
+    pf = self._pf
+    out = _orig_stage(self, batch, with_orig, training)
+    if pf is not None and pf[0] is batch:
+        si, sa, x_img, x_aud = self._scr
+        x_img.copy_(si)
+        x_aud.copy_(sa)
+        out = (x_img, x_aud) + tuple(out[2:])
+    return out
+
+
+def run(pre, root, variant):
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
+    EN.MultiCentralEngine.prefetch = {"F": pf_wait_all, "G": pf_scratch}.get(variant, _orig_pf)
+    EN.MultiCentralEngine._aug_bufs = bufs_scratch if variant == "G" else _orig_bufs
+    EN.MultiCentralEngine.stage = stage_scratch if variant == "G" else _orig_stage
+    ld = AVMNISTDinoLoader(root, batch_size=8, train_size=36, val_size=4, seed=3,
+                           multimodal_mode="semi_supervised", device="cuda", staged=True)
+    batches = list(ld)[:4] * 2
+    store = ParamStore(multimodal_dino_sd("semi_supervised", 32, 32, 16), "cuda:0", seed=1)
+    eng = EN.MultiCentralEngine(store, "semi_supervised", 32, 32, 16,
+                                EN.Hyper(dropout=0.0, fusion_dropout=0.0), act_dtype=torch.bfloat16,
+                                concurrent=variant != "I")
+    eng.use_graph = True
+    eng.graph.warmup = 1
+    losses = []
+    for i, b in enumerate(batches):
+        n = batches[i + 1] if (pre and i + 1 < len(batches)) else None
+        losses.append(eng.step(b, next_batch=n).item())
+    torch.cuda.synchronize()
+    return losses, store.student.clone()
+
+
+def main():
+    reps = int(sys.argv[1])
+    root = _fake_avmnist(__import__("pathlib").Path(tempfile.mkdtemp()), n=40)
+    for variant in sys.argv[2:]:
+        l0, s0 = run(False, root, variant)
+        bad = []
+        for r in range(reps):
+            l1, s1 = run(True, root, variant)
+            if l1 != l0 or not torch.equal(s0, s1):
+                ks = [k for k in range(len(l0)) if l0[k] != l1[k]]
+                bad.append(ks)
+                if ks:
+                    k = ks[0]
+                    print(f"   {variant} rep {r}: step {k} loss {l1[k]!r} vs serial {l0[k]!r} "
+                          f"(d {l1[k] - l0[k]:.3e}); finite params {bool(torch.isfinite(s1).all())}", flush=True)
+        print(f"{variant}: {len(bad)} of {reps} runs differ; first differing steps {bad[:5]}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
