@@ -265,6 +265,10 @@ int avd_xent_fused(const float* q, const float* k, int R, int C, int P, int Bh, 
                    int msk0, int msk1, float inv_t, float gscale, float* loss, float* dq, float* dk,
                    float* ws, long long ws_elems, void* stream);
 
+/* Test hook: fill the LDS of every CU with NaN bit patterns (0x7fc07fc0), so a kernel that reads
+ * LDS it never wrote sees NaN instead of a benign leftover (tools/lds_poison.py). */
+int avd_lds_poison(void* stream);
+
 /* The whole backward of the audio conv2 layer in one launch (lbwd.hip; CentralUnimodalAudio
  * conv2 -> bn2 -> ReLU -> MaxPool2d, unimodal.py:185-221: 56x56, Cin 8 -> Cout 16, 5x5 pad 2,
  * bf16): from y [N][56][56][16] and the pooled gradient gout [N][28][28][16] (layout 0) with

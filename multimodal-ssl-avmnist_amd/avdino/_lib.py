@@ -69,6 +69,7 @@ PROTOS = {
     "avd_cl_c1_recompute": [I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "avd_cl_c1_recompute_combine": [P, P, P, P, P, I, I, I, P],
     "avd_cl_bn_bwd_apply_wgrad": [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "avd_lds_poison": [P],
     "avd_xent_fused_ws": [I, I, I],
     "avd_xent_fused": [P, P, I, I, I, I, I, I, I, I, F, F, P, P, P, P, L, P],
     "avd_cl_layer_bwd_slabs": [I, I, I, I, I, I, I, I],

@@ -19,6 +19,7 @@ from . import ops
 _ACTIVE = None     # the _Capture in progress (host_point's target), else None
 
 
+
 class _Capture:
     def __init__(self, pool):
         self.pool, self.seq, self.g = pool, [], None

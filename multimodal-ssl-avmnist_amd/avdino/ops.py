@@ -1002,6 +1002,13 @@ def softmax_xent(logits, ld, R, C, targets, target_mode, col_major, mask_diag, g
          stream())
 
 
+def lds_poison():
+    """Test hook (avd_lds_poison): fill the LDS of every CU with NaN bit patterns, so a kernel
+    launched after it that reads LDS it never wrote sees NaN instead of a benign leftover
+    (tools/lds_poison.py)."""
+    call("avd_lds_poison", stream())
+
+
 def xent_fused_ws(R, C, P):
     n = lib.avd_xent_fused_ws(R, C, P)
     _need(n > 0, f"fused softmax-CE: P must be 128 or 256 (got {P})")

@@ -89,3 +89,24 @@ extern "C" int avd_mark(unsigned long long* marks, int idx, void* stream) {
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }
+
+// Test hook: every block fills its 64 KB of LDS with NaN bit patterns and exits; 8 blocks per CU
+// slot cover every CU's LDS several times over.  A later kernel that reads LDS it never wrote
+// then reads NaN (tools/lds_poison.py finds such reads by comparing results with and without).
+__global__ __launch_bounds__(1024) void lds_poison_kernel() {
+  extern __shared__ __attribute__((aligned(16))) unsigned lds_all[];
+  constexpr int WORDS = 64 * 1024 / 4;
+  for (int i = threadIdx.x; i < WORDS; i += blockDim.x) lds_all[i] = 0x7fc07fc0u;
+  __syncthreads();
+  // keep the stores: a value read back decides nothing, but the compiler cannot drop the loop
+  if (lds_all[(threadIdx.x * 37) % WORDS] == 1u) lds_all[0] = 0u;
+}
+
+extern "C" int avd_lds_poison(void* stream) {
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  lds_poison_kernel<<<cus * 8, 1024, 64 * 1024, avd_stream(stream)>>>();
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}

@@ -5,7 +5,12 @@ no synchronisation between steps (the test's setting), compared with the serial 
   G  overlap, but the data stream writes a private scratch set that the main stream copies into
      the staging set after the step (no graph-referenced memory written concurrently)
   I  overlap, one stream per step (concurrent=False: no side streams inside the graphs)
-    python tools/dbg_prefetch5.py REPS A F G I"""
+  X_keepev  variant X with every torch.cuda.Event kept alive for the whole run (no event is
+            destroyed while a stream may still wait on it)
+  C  variant A, and after each prefetch the device is synchronised and the prefetched views are
+     compared with the same augmentation redone on the main stream (are the INPUTS wrong, or
+     the step computed from right inputs?)
+    python tools/dbg_prefetch5.py REPS A F G I C"""
 import os
 import sys
 import tempfile
@@ -60,20 +65,52 @@ def stage_scratch(self, batch, with_orig, training=True):
     return out
 
 
+CHK = []
+
+
+def pf_check(self, batch):
+    aug = batch["aug"]
+    c0 = (aug.image.calls, aug.audio.calls)
+    ok = _orig_pf(self, batch)
+    torch.cuda.synchronize()
+    c1 = (aug.image.calls, aug.audio.calls)
+    x_img, x_aud = self._pf[3][0], self._pf[3][1]
+    si, sa = torch.empty_like(x_img), torch.empty_like(x_aud)
+    aug.image.calls, aug.audio.calls = c0
+    aug.stage(batch["idx"], si, sa, self.heads is not None)
+    torch.cuda.synchronize()
+    aug.image.calls, aug.audio.calls = c1
+    CHK.append(torch.equal(si, x_img) and torch.equal(sa, x_aud))
+    return ok
+
+
+_KEEP = []
+_OrigEvent = torch.cuda.Event
+
+
+class _KeptEvent(_OrigEvent):
+    def __new__(cls, *a, **k):
+        e = _OrigEvent.__new__(cls, *a, **k)
+        _KEEP.append(e)
+        return e
+
+
 def run(pre, root, variant):
+    keep = variant.endswith("keepev")
+    torch.cuda.Event = torch.cuda.streams.Event = _KeptEvent if keep else _OrigEvent
     import gc
     gc.collect()
     torch.cuda.synchronize()
-    EN.MultiCentralEngine.prefetch = {"F": pf_wait_all, "G": pf_scratch}.get(variant, _orig_pf)
-    EN.MultiCentralEngine._aug_bufs = bufs_scratch if variant == "G" else _orig_bufs
-    EN.MultiCentralEngine.stage = stage_scratch if variant == "G" else _orig_stage
+    EN.MultiCentralEngine.prefetch = {"F": pf_wait_all, "G": pf_scratch, "C": pf_check}.get(variant[:1], _orig_pf)
+    EN.MultiCentralEngine._aug_bufs = bufs_scratch if variant[:1] == "G" else _orig_bufs
+    EN.MultiCentralEngine.stage = stage_scratch if variant[:1] == "G" else _orig_stage
     ld = AVMNISTDinoLoader(root, batch_size=8, train_size=36, val_size=4, seed=3,
                            multimodal_mode="semi_supervised", device="cuda", staged=True)
     batches = list(ld)[:4] * 2
     store = ParamStore(multimodal_dino_sd("semi_supervised", 32, 32, 16), "cuda:0", seed=1)
     eng = EN.MultiCentralEngine(store, "semi_supervised", 32, 32, 16,
                                 EN.Hyper(dropout=0.0, fusion_dropout=0.0), act_dtype=torch.bfloat16,
-                                concurrent=variant != "I")
+                                concurrent=variant[:1] != "I")
     eng.use_graph = True
     eng.graph.warmup = 1
     losses = []
@@ -81,7 +118,9 @@ def run(pre, root, variant):
         n = batches[i + 1] if (pre and i + 1 < len(batches)) else None
         losses.append(eng.step(b, next_batch=n).item())
     torch.cuda.synchronize()
-    return losses, store.student.clone()
+    out = losses, store.student.clone()
+    torch.cuda.Event = torch.cuda.streams.Event = _OrigEvent
+    return out
 
 
 def main():
@@ -91,7 +130,10 @@ def main():
         l0, s0 = run(False, root, variant)
         bad = []
         for r in range(reps):
+            CHK.clear()
             l1, s1 = run(True, root, variant)
+            if CHK:
+                print(f"   {variant} rep {r}: prefetched inputs equal to redone: {CHK}", flush=True)
             if l1 != l0 or not torch.equal(s0, s1):
                 ks = [k for k in range(len(l0)) if l0[k] != l1[k]]
                 bad.append(ks)
