@@ -498,6 +498,19 @@ int avd_augment_views_dt(const uint8_t* src_u8, const int64_t* idx, long long n_
                          int V, int H, int W, const float* lut, const float* rec,
                          const uint32_t* gm, int gm_words, int group, unsigned long long seed,
                          int order, void* out, int odt, void* stream);
+/* Diagnostic (tools/dbg_prefetch6.py): the gather kernel into a bf16 out, and afterwards each block
+ * re-checks its staged source row and byte table in LDS against global memory; chk[3] int32 on the
+ * device: {LDS words found changed (accumulated), first changed word, its block}; seen
+ * [B*V, AVD_AUG_REC] f32: the record fields each block used, as it read them. */
+int avd_augment_views_lds_check(const uint8_t* src_u8, const int64_t* idx, int B, int V, int H, int W,
+                                const float* lut, const float* rec, const uint32_t* gm, int gm_words,
+                                int group, unsigned long long seed, int order, void* out, int* chk,
+                                float* seen, void* stream);
+/* Diagnostic: the gather kernel with its source row and byte table read from global memory, no
+ * LDS staging (bf16 out). */
+int avd_augment_views_nolds(const uint8_t* src_u8, const int64_t* idx, int B, int V, int H, int W,
+                            const float* lut, const float* rec, const uint32_t* gm, int gm_words,
+                            int group, unsigned long long seed, int order, void* out, void* stream);
 
 /* The same views for a chain in ANY stage order (transforms.Compose order; the reference's own
  * configs/config_multimodal_dino.yaml best_augments chains, get_data.py:195-231, put the masks

@@ -105,6 +105,8 @@ PROTOS = {
     "avd_stage_views": [P, I, P, I, P, I, I, P, I, P],
     "avd_augment_views": [P, P, L, I, I, I, I, P, P, P, I, I, U64, I, P, P],
     "avd_augment_views_dt": [P, P, L, I, I, I, I, P, P, P, I, I, U64, I, P, I, P],
+    "avd_augment_views_lds_check": [P, P, I, I, I, I, P, P, P, I, I, U64, I, P, P, P, P],
+    "avd_augment_views_nolds": [P, P, I, I, I, I, P, P, P, I, I, U64, I, P, P],
     "avd_augment_views_seq": [P, P, L, I, I, I, I, P, P, P, I, I, U64, I, P, I, P, I, P],
     "avd_augment_records": [P, I, I, I, I, I, U64, P, P, I, P],
     "avd_row_sqnorm": [P, I, I, P, P],

@@ -47,20 +47,43 @@ class Workspace:
     real-data prefetch's second staging set -- allocated on the main stream under step 0 and
     written on the data stream -- could land on a block step 0 was still using.)"""
 
+    # bytes of canary after every buffer (tests / tools/dbg_guard.py: check_guards() names any
+    # buffer whose writer ran past its end); 0 in production
+    GUARD = 0
+    CANARY = 0xA5
+
     def __init__(self, device):
         self.device = device
         self.bufs = {}
+        self.guards = {}
         self.epoch = 0
 
     def get(self, name, numel, dtype=F32):
         b = self.bufs.get(name)
         if b is None or b.numel() < numel or b.dtype != dtype:
-            nb = torch.empty(max(numel, 1), dtype=dtype, device=self.device)
+            n = max(numel, 1)
+            es = torch.empty(0, dtype=dtype).element_size()
+            g = -(-self.GUARD // es)
+            full = torch.empty(n + g, dtype=dtype, device=self.device)
+            nb = full[:n]
+            if g:
+                full.view(torch.uint8)[n * es:].fill_(self.CANARY)
+                self.guards[name] = (full, n * es)
             if nb.is_cuda and not torch.cuda.is_current_stream_capturing():
                 torch.cuda.synchronize(self.device)
             self.bufs[name] = b = nb
             self.epoch += 1
         return b[:numel]
+
+    def check_guards(self):
+        """[(buffer name, first clobbered byte past its end, clobbered bytes)] (GUARD > 0)."""
+        bad = []
+        for name, (full, nb) in self.guards.items():
+            gz = full.view(torch.uint8)[nb:]
+            hit = (gz != self.CANARY).nonzero()
+            if hit.numel():
+                bad.append((name, int(hit[0]), int(hit.numel())))
+        return bad
 
     def nbytes(self):
         return sum(b.numel() * b.element_size() for b in self.bufs.values())
@@ -812,7 +835,6 @@ class MultiCentralEngine:
         self.dstream = None
         self._par = 0
         self._pf = None
-        self._ev_free = None
         self._t_ready = None       # (batch, B, G) of the teacher output waiting in t_proj
         self.tin_pending = None    # the next batch's teacher inputs while its forward is queued
         self._tseed = None
@@ -943,10 +965,17 @@ class MultiCentralEngine:
 
     def prefetch(self, batch):
         """Queue the augmentation of the NEXT step's real-data batch ({"aug", "idx", ...}) on the
-        data stream, into the staging buffers the current step does not read, so it runs under
-        the step just queued instead of in front of the next one.  The next stage() of that same
-        batch object waits for it and takes those buffers.  Returns False when not applicable
-        (synthetic views, no GPU, prefetch off)."""
+        data stream, into the staging buffers the current step does not read: its host work
+        (parameter draws, id transfers, launches) is done while the current step runs, and the
+        next stage() of that same batch object waits for it and takes those buffers.  Returns
+        False when not applicable (synthetic views, no GPU, prefetch off).
+
+        The data stream starts after the whole step just queued: an augmentation
+        kernel running on the data stream BESIDE a replayed multi-stream step graph returns
+        wrong pixels in about one run of three (a few lanes of a wave -- always lanes 48-63 --
+        read zeros; its records, sample ids, staged LDS row and output buffer were all verified,
+        the same kernel without LDS fails the same way, and eager multi-stream steps or
+        single-stream graphs beside it never do), so the GPU work is not overlapped."""
         if not self.PREFETCH or "aug" not in batch or self.store.device.type != "cuda":
             return False
         if self._pf is not None:
@@ -954,19 +983,11 @@ class MultiCentralEngine:
         par = 1 - self._par
         if self.dstream is None:
             self.dstream = torch.cuda.Stream(self.store.device)
-        # The other set was last read by the step before the current one, so the data stream
-        # starts once the main stream is past the event stage() recorded in front of the current
-        # step, and the augmentation overlaps the current step.  The set's buffers are taken
-        # from the workspace here, on the main stream: a first allocation (or a regrowth for a
-        # larger batch) synchronises the device inside Workspace.get, so the block cannot be
-        # one that kernels of the current step still use (that was the round-5
-        # race -- set 1 is first allocated under step 0, and the main stream's caching
-        # allocator could hand it a block step 0 had freed but was still writing).
+        # the set's buffers are taken from the workspace here, on the main stream: a first
+        # allocation (or a regrowth for a larger batch) synchronises the device inside
+        # Workspace.get, so the block cannot be one that kernels of the current step still use
         main = torch.cuda.current_stream(self.store.device)
-        if self._ev_free is not None:
-            self.dstream.wait_event(self._ev_free)
-        else:
-            self.dstream.wait_stream(main)
+        self.dstream.wait_stream(main)
         with_orig = self.heads is not None
         staged = self._aug_bufs(batch, with_orig, par)
         with torch.cuda.stream(self.dstream):
@@ -1024,10 +1045,6 @@ class MultiCentralEngine:
         if self.mode == "semi_supervised":
             labels = ws.get("in.label" + ("" if self._par == 0 else ".1"), B, torch.int64)
             labels.copy_(batch["label"].reshape(-1))
-        if main is not None and training:
-            # everything queued before this step (the last readers of the other set)
-            self._ev_free = torch.cuda.Event()
-            self._ev_free.record(main)
         return x_img, x_aud, B, G, L, labels
 
     def reset_pipeline(self):

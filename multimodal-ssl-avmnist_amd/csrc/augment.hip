@@ -58,6 +58,8 @@ __device__ __forceinline__ bool affine_nearest(const float* m, float cx, float c
 
 struct View {
   const float* img;   // LDS, [H, W] normalised source
+  const uint8_t* gsrc;  // GLB kernels: the source row's bytes in global memory
+  const float* glut;    //   and the byte -> f32 table
   int H, W;
   bool crop;
   int top, left, ch, cw;
@@ -66,9 +68,16 @@ struct View {
 
 // RandomResizedCrop output pixel (r, c): bilinear (align_corners=False, source index clamped
 // at 0 and at the crop's last row/column) inside the integer crop box.
+template <bool GLB = false>
+__device__ __forceinline__ float src_px(const View& v, int i) {
+  if constexpr (GLB) return v.glut[v.gsrc[i]];
+  else return v.img[i];
+}
+
+template <bool GLB = false>
 __device__ __forceinline__ float crop_sample(const View& v, int r, int c) {
 #pragma clang fp contract(off)
-  if (!v.crop) return v.img[r * v.W + c];
+  if (!v.crop) return src_px<GLB>(v, r * v.W + c);
   float sy = ((float)r + 0.5f) * v.sh - 0.5f;
   float sx = ((float)c + 0.5f) * v.sw - 0.5f;
   sy = sy < 0.0f ? 0.0f : sy;
@@ -78,16 +87,20 @@ __device__ __forceinline__ float crop_sample(const View& v, int r, int c) {
   const int x1 = x0 + 1 < v.cw ? x0 + 1 : v.cw - 1;
   const float ly = sy - (float)y0, lx = sx - (float)x0;
   const float hy = 1.0f - ly, hx = 1.0f - lx;
-  const float* p0 = v.img + (v.top + y0) * v.W + v.left;
-  const float* p1 = v.img + (v.top + y1) * v.W + v.left;
-  return hy * (hx * p0[x0] + lx * p0[x1]) + ly * (hx * p1[x0] + lx * p1[x1]);
+  const int r0 = (v.top + y0) * v.W + v.left, r1 = (v.top + y1) * v.W + v.left;
+  return hy * (hx * src_px<GLB>(v, r0 + x0) + lx * src_px<GLB>(v, r0 + x1)) +
+         ly * (hx * src_px<GLB>(v, r1 + x0) + lx * src_px<GLB>(v, r1 + x1));
 }
 
-template <typename TO>
+// CHK (avd_augment_views_lds_check, a diagnostic): after the pixel loop every thread re-derives
+// its staged source floats and the byte table from global memory and counts the LDS words that no
+// longer hold them into chk[0] (first bad word index in chk[1], the block in chk[2]).
+template <typename TO, bool CHK = false, bool GLB = false>
 __global__ __launch_bounds__(kThreads) void augment_kernel(
     const uint8_t* __restrict__ src, const int64_t* __restrict__ idx, int V, int B, int H, int W,
     const float* __restrict__ lut, const float* __restrict__ recs, const uint32_t* __restrict__ gm,
-    int gm_words, int group, unsigned long long seed, int order, TO* __restrict__ out) {
+    int gm_words, int group, unsigned long long seed, int order, TO* __restrict__ out,
+    int* __restrict__ chk = nullptr, float* __restrict__ seen = nullptr) {
 #pragma clang fp contract(off)
   __shared__ float s_img[kMaxHW];
   __shared__ float s_lut[256];
@@ -96,21 +109,25 @@ __global__ __launch_bounds__(kThreads) void augment_kernel(
   const int HW = H * W;
   const float* rec = recs + (size_t)rid * AVD_AUG_REC;
 
-  s_lut[threadIdx.x] = lut[threadIdx.x];
-  __syncthreads();
   const uint32_t* row = reinterpret_cast<const uint32_t*>(src + (size_t)idx[b] * HW);
-  for (int i = threadIdx.x; i < HW / 4; i += kThreads) {
-    const uint32_t w4 = row[i];
-    s_img[4 * i + 0] = s_lut[w4 & 0xFF];
-    s_img[4 * i + 1] = s_lut[(w4 >> 8) & 0xFF];
-    s_img[4 * i + 2] = s_lut[(w4 >> 16) & 0xFF];
-    s_img[4 * i + 3] = s_lut[w4 >> 24];
+  if constexpr (!GLB) {
+    s_lut[threadIdx.x] = lut[threadIdx.x];
+    __syncthreads();
+    for (int i = threadIdx.x; i < HW / 4; i += kThreads) {
+      const uint32_t w4 = row[i];
+      s_img[4 * i + 0] = s_lut[w4 & 0xFF];
+      s_img[4 * i + 1] = s_lut[(w4 >> 8) & 0xFF];
+      s_img[4 * i + 2] = s_lut[(w4 >> 16) & 0xFF];
+      s_img[4 * i + 3] = s_lut[w4 >> 24];
+    }
+    __syncthreads();
   }
-  __syncthreads();
 
   const int flags = (int)rec[AVD_AUG_FLAGS];
   View vw;
   vw.img = s_img;
+  vw.gsrc = reinterpret_cast<const uint8_t*>(row);
+  vw.glut = lut;
   vw.H = H;
   vw.W = W;
   vw.crop = flags & 1;
@@ -164,12 +181,12 @@ __global__ __launch_bounds__(kThreads) void augment_kernel(
           if (t < (float)W) {
             const int i0 = (int)t;
             const float a = t - (float)i0;
-            const float s0 = fabsf(crop_sample(vw, qy, i0));
-            const float s1 = i0 + 1 < W ? fabsf(crop_sample(vw, qy, i0 + 1)) : 0.0f;
+            const float s0 = fabsf(crop_sample<GLB>(vw, qy, i0));
+            const float s1 = i0 + 1 < W ? fabsf(crop_sample<GLB>(vw, qy, i0 + 1)) : 0.0f;
             val = a * s1 + (1.0f - a) * s0;
           }
         } else {
-          val = crop_sample(vw, qy, qx);
+          val = crop_sample<GLB>(vw, qy, qx);
         }
       }
       if (eh > 0 && y >= et && y < et + eh && x >= el && x < el + ew) val = 0.0f;
@@ -184,6 +201,42 @@ __global__ __launch_bounds__(kThreads) void augment_kernel(
       reinterpret_cast<float2*>(o)[q] = make_float2(v2[0], v2[1]);
     else      // bf16 straight into the engine's staged view-major input
       reinterpret_cast<uint32_t*>(o)[q] = pack_bf16x2(v2[0], v2[1]);
+  }
+  if constexpr (CHK && !GLB) {
+    if (threadIdx.x == 0) {   // the record as this block used it
+      float* sr = seen + (size_t)rid * AVD_AUG_REC;
+      sr[AVD_AUG_FLAGS] = (float)flags;
+      sr[AVD_AUG_CROP + 0] = (float)vw.top; sr[AVD_AUG_CROP + 1] = (float)vw.left;
+      sr[AVD_AUG_CROP + 2] = (float)vw.ch; sr[AVD_AUG_CROP + 3] = (float)vw.cw;
+      for (int k = 0; k < 6; ++k) { sr[AVD_AUG_AFF + k] = maff[k]; sr[AVD_AUG_ROT + k] = mrot[k]; }
+      sr[AVD_AUG_RATE] = rate;
+      sr[AVD_AUG_FMASK] = (float)f0; sr[AVD_AUG_FMASK + 1] = (float)f1;
+      sr[AVD_AUG_TMASK] = (float)t0; sr[AVD_AUG_TMASK + 1] = (float)t1;
+      sr[AVD_AUG_NOISE] = nstd;
+      sr[AVD_AUG_GM] = (float)gmrow;
+      sr[AVD_AUG_ERASE] = (float)et; sr[AVD_AUG_ERASE + 1] = (float)el;
+      sr[AVD_AUG_ERASE + 2] = (float)eh; sr[AVD_AUG_ERASE + 3] = (float)ew;
+    }
+    __syncthreads();
+    int nbad = 0, first = -1;
+    if (__float_as_uint(s_lut[threadIdx.x]) != __float_as_uint(lut[threadIdx.x])) {
+      ++nbad;
+      first = kMaxHW + threadIdx.x;
+    }
+    for (int i = threadIdx.x; i < HW / 4; i += kThreads) {
+      const uint32_t w4 = row[i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (__float_as_uint(s_img[4 * i + j]) != __float_as_uint(lut[(w4 >> (8 * j)) & 0xFF])) {
+          ++nbad;
+          if (first < 0) first = 4 * i + j;
+        }
+    }
+    if (nbad) {
+      atomicAdd(chk, nbad);
+      chk[1] = first;
+      chk[2] = rid;
+    }
   }
 }
 
@@ -528,6 +581,39 @@ extern "C" int avd_augment_views_dt(const uint8_t* src_u8, const int64_t* idx, l
   augment_kernel<bf16><<<B * V, kThreads, 0, avd_stream(stream)>>>(src_u8, idx, V, B, H, W, lut, rec, gm,
                                                                    gm_words, group, seed, order,
                                                                    (bf16*)out);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+extern "C" int avd_augment_views_lds_check(const uint8_t* src_u8, const int64_t* idx, int B, int V,
+                                           int H, int W, const float* lut, const float* rec,
+                                           const uint32_t* gm, int gm_words, int group,
+                                           unsigned long long seed, int order, void* out,
+                                           int* chk, float* seen, void* stream) {
+  if (!src_u8 || !idx || !lut || !rec || !out || !chk || !seen) return AVD_ERR_ARG;
+  if (B <= 0 || V <= 0 || H <= 0 || W <= 0) return AVD_ERR_SHAPE;
+  if ((long long)H * W > kMaxHW || (H * W) % 4 || W % 2 || order < 0 || order > 1) return AVD_ERR_SHAPE;
+  if (gm && (group <= 0 || H % group || W % group || gm_words * 32 < (H / group) * (W / group)))
+    return AVD_ERR_SHAPE;
+  augment_kernel<bf16, true><<<B * V, kThreads, 0, avd_stream(stream)>>>(
+      src_u8, idx, V, B, H, W, lut, rec, gm, gm_words, group, seed, order, (bf16*)out, chk, seen);
+  AVD_CHECK_LAUNCH();
+  return AVD_OK;
+}
+
+// Diagnostic (tools/dbg_prefetch6.py): the gather kernel reading the source bytes and the byte
+// table straight from global memory, no LDS (bf16 out)
+extern "C" int avd_augment_views_nolds(const uint8_t* src_u8, const int64_t* idx, int B, int V, int H,
+                                       int W, const float* lut, const float* rec, const uint32_t* gm,
+                                       int gm_words, int group, unsigned long long seed, int order,
+                                       void* out, void* stream) {
+  if (!src_u8 || !idx || !lut || !rec || !out) return AVD_ERR_ARG;
+  if (B <= 0 || V <= 0 || H <= 0 || W <= 0) return AVD_ERR_SHAPE;
+  if ((long long)H * W > kMaxHW || (H * W) % 4 || W % 2 || order < 0 || order > 1) return AVD_ERR_SHAPE;
+  if (gm && (group <= 0 || H % group || W % group || gm_words * 32 < (H / group) * (W / group)))
+    return AVD_ERR_SHAPE;
+  augment_kernel<bf16, false, true><<<B * V, kThreads, 0, avd_stream(stream)>>>(
+      src_u8, idx, V, B, H, W, lut, rec, gm, gm_words, group, seed, order, (bf16*)out);
   AVD_CHECK_LAUNCH();
   return AVD_OK;
 }

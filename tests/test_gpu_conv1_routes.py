@@ -1,13 +1,13 @@
 """The first-layer training routes of the bf16 step against each other.
 
 * The image conv1's pixel-major passes (avd_cl_c1r5_stats / avd_cl_c1r5_apply_codes) and its
-  routed moments pass (avd_cl_c1r5_moments_codes) with AVDINO_GRID_CAP forcing a handful of
+  routed moments pass (avd_cl_c1r5_moments_codes) with the grid_cap option forcing a handful of
   blocks, so every block walks many samples across BN-group boundaries: the pooled map and the
   codes are bit-identical to the uncapped launch, the statistics and moments are fp32 sums in
   another order (rel 1e-6).
 * The engine's first-layer backward routes -- routed by the forward pooling pass's codes, and
-  the recomputing moments pass (AVDINO_C1_CODES=0) -- and its two audio conv1 statistics routes
-  (patch Gram, AVDINO_C1_GRAM; recomputing statistics pass) each against float64 autograd of
+  the recomputing moments pass (ConvBranch.CODES = False) -- and its two audio conv1 statistics routes
+  (patch Gram, ConvBranch.GRAM; recomputing statistics pass) each against float64 autograd of
   the layer on the same input, weights and pooled gradient (tests/first_layer_truth.py): the
   routed backward within 1e-4, the recomputing one (sum dz * y at the bf16-rounded y) within
   5e-3, the Gram statistics within 1e-5; every gradient outside the first layers is bitwise equal
@@ -148,8 +148,8 @@ def test_engine_first_layer_routes_against_float64(monkeypatch):
 
 
 def test_engine_gram_stats_against_float64(monkeypatch):
-    """Audio conv1 BN statistics from the patch Gram (AVDINO_C1_GRAM=1, avd_cl_c1_gram) and from
-    the recomputing statistics pass (=0), each against float64 of the same layer: the Gram route's
+    """Audio conv1 BN statistics from the patch Gram (ConvBranch.GRAM = True, avd_cl_c1_gram) and from
+    the recomputing statistics pass (False), each against float64 of the same layer: the Gram route's
     batch mean / invstd within 1e-6 (measured 3e-7; the fp32 statistics pass 1.2e-5) and its
     routed gradients within 1e-4; the loss of the two
     routes agrees to 1e-3 and the running statistics to 1e-4."""

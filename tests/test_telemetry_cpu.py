@@ -158,3 +158,22 @@ def test_segmented_replay_order():
     hit = []
     host_point(lambda: hit.append(1))
     assert hit == [1]
+
+
+def test_workspace_canary_guards(monkeypatch):
+    """Workspace.GUARD (tools/dbg_guard.py): a canary after every buffer; check_guards() names a
+    buffer whose writer ran past its end, and production (GUARD = 0) allocates no guard."""
+    from avdino.engine import Workspace
+    ws = Workspace(torch.device("cpu"))
+    ws.get("a", 10)
+    assert ws.guards == {} and ws.check_guards() == []
+    monkeypatch.setattr(Workspace, "GUARD", 16)
+    ws = Workspace(torch.device("cpu"))
+    a = ws.get("a", 10)
+    b = ws.get("b", 3, torch.int64)
+    a.fill_(1.0)
+    b.fill_(-1)
+    assert ws.check_guards() == []
+    ws.guards["b"][0].view(torch.uint8)[3 * 8 + 5] = 0      # one byte past b's end
+    assert ws.check_guards() == [("b", 5, 1)]
+    assert ws.get("a", 10).numel() == 10

@@ -1,10 +1,11 @@
 """Debug: which ingredient does the prefetch mismatch need?  REPS runs per variant, graph-replayed,
 no synchronisation between steps (the test's setting), compared with the serial run:
-  A  prefetch as shipped (data stream overlaps the current step; two staging sets)
-  F  the data stream waits for the whole queued step (no overlap)
+  A  the round-5 prefetch: the data stream overlaps the current step (two staging sets)
+  F  as shipped: the data stream waits for the whole queued step (no overlap)
   G  overlap, but the data stream writes a private scratch set that the main stream copies into
      the staging set after the step (no graph-referenced memory written concurrently)
   I  overlap, one stream per step (concurrent=False: no side streams inside the graphs)
+  X_eager   variant X without graph capture (every step launched eagerly)
   X_keepev  variant X with every torch.cuda.Event kept alive for the whole run (no event is
             destroyed while a stream may still wait on it)
   C  variant A, and after each prefetch the device is synchronised and the prefetched views are
@@ -30,9 +31,31 @@ _orig_bufs = EN.MultiCentralEngine._aug_bufs
 _orig_stage = EN.MultiCentralEngine.stage
 
 
-def pf_wait_all(self, batch):
-    self._ev_free = None
+def pf_wait_all(self, batch):          # F: as shipped since round 6
     return _orig_pf(self, batch)
+
+
+def stage_mark(self, batch, with_orig, training=True):
+    out = _orig_stage(self, batch, with_orig, training)
+    if training:        # everything queued before this step: the last readers of the other set
+        self._ev_free = torch.cuda.Event()
+        self._ev_free.record(torch.cuda.current_stream())
+    return out
+
+
+def pf_overlap(self, batch):
+    """The round-5 prefetch: the data stream waits only for the event stage() recorded in front
+    of the step just queued, so the augmentation overlaps that step."""
+    ds = self.dstream
+    if ds is None:
+        return _orig_pf(self, batch)
+    ev = getattr(self, "_ev_free", None)
+    orig_wait = ds.wait_stream
+    ds.wait_stream = (lambda s: ds.wait_event(ev)) if ev is not None else orig_wait
+    try:
+        return _orig_pf(self, batch)
+    finally:
+        del ds.wait_stream
 
 
 def bufs_scratch(self, batch, with_orig, par):
@@ -49,14 +72,14 @@ def bufs_scratch(self, batch, with_orig, par):
 def pf_scratch(self, batch):
     self._in_pf = True
     try:
-        return _orig_pf(self, batch)
+        return pf_overlap(self, batch)
     finally:
         self._in_pf = False
 
 
 def stage_scratch(self, batch, with_orig, training=True):
     pf = self._pf
-    out = _orig_stage(self, batch, with_orig, training)
+    out = stage_mark(self, batch, with_orig, training)
     if pf is not None and pf[0] is batch:
         si, sa, x_img, x_aud = self._scr
         x_img.copy_(si)
@@ -71,7 +94,7 @@ CHK = []
 def pf_check(self, batch):
     aug = batch["aug"]
     c0 = (aug.image.calls, aug.audio.calls)
-    ok = _orig_pf(self, batch)
+    ok = pf_overlap(self, batch)
     torch.cuda.synchronize()
     c1 = (aug.image.calls, aug.audio.calls)
     x_img, x_aud = self._pf[3][0], self._pf[3][1]
@@ -101,9 +124,9 @@ def run(pre, root, variant):
     import gc
     gc.collect()
     torch.cuda.synchronize()
-    EN.MultiCentralEngine.prefetch = {"F": pf_wait_all, "G": pf_scratch, "C": pf_check}.get(variant[:1], _orig_pf)
+    EN.MultiCentralEngine.prefetch = {"F": pf_wait_all, "G": pf_scratch, "C": pf_check}.get(variant[:1], pf_overlap)
     EN.MultiCentralEngine._aug_bufs = bufs_scratch if variant[:1] == "G" else _orig_bufs
-    EN.MultiCentralEngine.stage = stage_scratch if variant[:1] == "G" else _orig_stage
+    EN.MultiCentralEngine.stage = {"G": stage_scratch, "F": _orig_stage}.get(variant[:1], stage_mark)
     ld = AVMNISTDinoLoader(root, batch_size=8, train_size=36, val_size=4, seed=3,
                            multimodal_mode="semi_supervised", device="cuda", staged=True)
     batches = list(ld)[:4] * 2
@@ -111,7 +134,7 @@ def run(pre, root, variant):
     eng = EN.MultiCentralEngine(store, "semi_supervised", 32, 32, 16,
                                 EN.Hyper(dropout=0.0, fusion_dropout=0.0), act_dtype=torch.bfloat16,
                                 concurrent=variant[:1] != "I")
-    eng.use_graph = True
+    eng.use_graph = not variant.endswith("eager")
     eng.graph.warmup = 1
     losses = []
     for i, b in enumerate(batches):
