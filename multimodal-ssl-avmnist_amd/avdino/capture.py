@@ -77,6 +77,15 @@ class GraphedStep:
         self.pool = None
         self.stream = None
 
+    def recapture(self):
+        """Drop every captured graph; each key captures again at its next call (no eager
+        warm-up: its workspaces are sized already) -- e.g. after changing what is captured
+        with the step (bench.py's span marks)."""
+        for key in self.graphs:
+            self.seen[key] = self.warmup
+        self.graphs = {}
+        self.pool = None
+
     def segments(self, key):
         """Number of graph segments of the capture for ``key`` (None: not captured)."""
         ent = self.graphs.get(key)

@@ -552,9 +552,11 @@ class ConvBranch:
                                 store.grad_of(ck + ".bias"))
             x = ctx["x"][i]
             wt = ctx["wts"][i]
+            # (the fused layer's BN-backward apply holds at most ops.APPLY_GMAX groups' coefficients,
+            # e.g. not 2 + 7 views)
             lbs = (ops.cl_layer_bwd_slabs(self.act, N, ci, H, H, co, k, pad)
                    if (self.LAYER_BWD and i > 0 and mode == 0 and wt[1] is not None and wt[3] is None
-                       and not self._mx_wgrad(i, N)) else 0)
+                       and N // B <= ops.APPLY_GMAX and not self._mx_wgrad(i, N)) else 0)
             if lbs:
                 # the whole layer backward in one launch: dY formed in LDS from y and the pooled
                 # gradient, dX and the dW slabs from the same tiles (lbwd.hip); its own dX

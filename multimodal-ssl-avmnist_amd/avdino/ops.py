@@ -623,6 +623,9 @@ def cl_bn_bwd_apply_wgrad(y, gout, scale, shift, coef, x, parts, N, B, Cin, H, W
                         p(parts), dtcode(y), N, B, Cin, H, W, Cout, K, pad, stream()))
 
 
+APPLY_GMAX = 8          # BN groups a fused BN-backward apply serves (csrc/bnapply.h)
+
+
 def cl_layer_bwd_slabs(dtype, N, Cin, H, W, Cout, K, pad):
     """Slabs (= grid) of the fused layer backward (avd_cl_layer_bwd), 0 if the shape is not
     served (the audio conv2: 56^2, 8 -> 16, 5x5 pad 2, bf16)."""
@@ -643,7 +646,7 @@ def cl_layer_bwd(y, gout, scale, shift, coef, dy, x, wk_d, dx, parts, slabs, N, 
     if y is not None:
         _need(y.dtype == torch.bfloat16 and y.numel() == N * Ho * Ho * Cout, "layer bwd y")
         _need(gout.dtype == torch.bfloat16 and gout.numel() == N * (Ho // 2) * (Ho // 2) * Cout, "layer bwd gout")
-        _need(N % B == 0 and N // B <= 8, "layer bwd groups")
+        _need(N % B == 0 and N // B <= APPLY_GMAX, "layer bwd groups")
         nb = (y.numel() + gout.numel() + x.numel() + dx.numel()) * 2
     else:
         _need(dy is not None and dy.dtype == torch.bfloat16 and dy.numel() == N * Ho * Ho * Cout, "layer bwd dy")
