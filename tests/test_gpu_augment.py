@@ -390,3 +390,37 @@ def test_trainer_prefetches_staged_batches(tmp_path):
         tr.fit(m, ld)
         out.append(m.model.store.student.clone())
     assert torch.equal(out[0], out[1])
+
+
+@pytest.mark.parametrize("view,mod", [("local", "image"), ("global", "audio")])
+def test_augment_diagnostic_kernels_equal_the_gather_kernel(view, mod):
+    """DESIGN 3.6's diagnostic builds of the gather kernel (tools/dbg_prefetch6.py): the LDS
+    self-check build and the LDS-free build give the shipped kernel's bf16 views bit for bit on
+    device-drawn records; the self-check finds its staged row intact and reports the record
+    fields it used."""
+    H = W = 28 if mod == "image" else 112
+    rng = np.random.default_rng(6)
+    src = torch.from_numpy(rng.integers(0, 256, (9, H * W), dtype=np.uint8)).cuda()
+    lut = torch.from_numpy(OA.normalise_lut(mod)).cuda()
+    aug = A.ViewAugmenter(src, lut, H, W, seed=3)
+    B, V = 6, 4
+    rec, gm = aug.records_dev(A.default_chains()[view][mod], B, V)
+    idx = torch.from_numpy(rng.integers(0, 9, B)).cuda()
+    seed, words = 0x5EED, gm.shape[1] if gm is not None else 0
+    ref = torch.empty(V * B * H * W, dtype=torch.bfloat16, device="cuda")
+    ops.augment_views(src, idx, lut, rec, gm, 4, seed, V, H, W, ref, 1)
+    a = torch.empty_like(ref)
+    b = torch.empty_like(ref)
+    chk = torch.zeros(3, dtype=torch.int32, device="cuda")
+    seen = torch.full_like(rec, -7.0)
+    ops.call("avd_augment_views_lds_check", ops.p(src), ops.p(idx), B, V, H, W, ops.p(lut), ops.p(rec),
+             ops.p(gm), words, 4, seed, 1, ops.p(a), ops.p(chk), ops.p(seen), ops.stream())
+    ops.call("avd_augment_views_nolds", ops.p(src), ops.p(idx), B, V, H, W, ops.p(lut), ops.p(rec),
+             ops.p(gm), words, 4, seed, 1, ops.p(b), ops.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(a, ref) and torch.equal(b, ref)
+    assert chk.tolist()[0] == 0
+    ints = [0, 1, 2, 3, 17, 18, 19, 20, 22, 23, 24, 25, 26, 27]
+    want = rec.clone()
+    want[:, ints] = want[:, ints].trunc()
+    assert torch.equal(seen, want)
