@@ -50,10 +50,10 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-template <int TH_, int OCC_, int PFD_ = 6, int PFW_ = 3, int GB_ = 1, int NCW_ = 1, int RP_ = 0>
+template <int TH_, int OCC_, int PFD_ = 6, int GB_ = 1, int NCW_ = 1, int RP_ = 0>
 struct Lb {
   static constexpr int CIN = 8, COUT = 16, K = 5, PAD = 2, H = 56, W = 56;   // the forward conv
-  static constexpr int TH = TH_, TPS = H / TH, OCC = OCC_, PFD = PFD_, PFW = PFW_, GB = GB_;
+  static constexpr int TH = TH_, TPS = H / TH, OCC = OCC_, PFD = PFD_, GB = GB_;
   static constexpr int ITH = TH + K - 1, ITW = W + K - 1;        // staged rows / columns (halo)
   // dY tile [ITH][RS][PS]: DgrA2's conflict-free image (pixel stride 16 channels, rows padded
   // by 4 pixels); X tile [ITH][XW][XS]: WgA2's
@@ -77,9 +77,12 @@ struct Lb {
   static constexpr int DT = ITH * ITW * (COUT / 8);               // AP = 0: 16-byte dY tasks
   static constexpr int XT = ITH * ITW * (CIN / 8);                // 16-byte X tasks
   static constexpr int RED = (NPW - 1) * NCW * NW * 64;           // f4 slots: pixel partials
-  static constexpr int SMEM = (DY_ELEMS + X_ELEMS) > RED * 8 ? DY_ELEMS + X_ELEMS : RED * 8;
+  // two tile images (double buffer): tile i + 1 is staged while tile i's MFMAs run, one barrier
+  // per tile (the apply's VALU work beside the MFMAs instead of between two barriers)
+  static constexpr int BUF = DY_ELEMS + X_ELEMS;
+  static constexpr int SMEM = 2 * BUF > RED * 8 ? 2 * BUF : RED * 8;
   static_assert(H % TH == 0 && TH % 2 == 0 && PIX % 32 == 0 && PIX % 16 == 0, "tiles");
-  static_assert(SMEM * 2 <= 64 * 1024, "LDS");
+  static_assert(SMEM * 2 <= 76 * 1024, "LDS (two blocks per CU: 160 KB)");
   static_assert(4 % NCW == 0, "wave split");
   static_assert(!RP || (KTAPS * COUT) % 32 == 0, "row-pair k-steps");
 };
@@ -156,8 +159,13 @@ __global__ __launch_bounds__(256, L::OCC) void lbwd_kernel(const bf16* __restric
                                                           ApplyArgs aa) {
   __shared__ __attribute__((aligned(16))) bf16 smem[L::SMEM];
   __shared__ __attribute__((aligned(16))) float ctab[AP ? APPLY_GMAX * 5 * L::COUT : 4];
-  bf16* dys = smem;                      // dY tile: row ty0 - PAD + r, column c - PAD
-  bf16* xs = smem + L::DY_ELEMS;         // X tile, same origin
+  // dY tile (row ty0 - PAD + r, column c - PAD) then the X tile (same origin), per buffer
+  bf16* dys = smem;
+  bf16* xs = smem + L::DY_ELEMS;
+  auto set_buf = [&](int b) {
+    dys = smem + b * L::BUF;
+    xs = dys + L::DY_ELEMS;
+  };
   const int tid = threadIdx.x, wp = tid >> 6, lane = tid & 63;
   const int g = lane >> 4, r16 = lane & 15, q4 = r16 >> 2, p4 = r16 & 3;
   const int wc = wp / L::NPW, wq = wp % L::NPW;     // weight gradient: column group, pixel part
@@ -325,18 +333,17 @@ __global__ __launch_bounds__(256, L::OCC) void lbwd_kernel(const bf16* __restric
           dst[b] = *reinterpret_cast<const bf16x8*>(dys + base[b] + ln + tapoff<L>(t0));
       };
       static_for<0, (PF < L::KS ? PF : L::KS)>([&](auto jc) { ld(bq[decltype(jc)::value], jc); });
+      // the fragment of k-step j + PF is read before the MFMA of k-step j, and scheduling
+      // barriers keep it there: without them (round-6 ISA) the scheduler sank every read to its
+      // MFMA, the ring collapsed to one register and each k-step waited out a whole LDS latency
       static_for<0, L::KS>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         if constexpr (j + PF < L::KS) ld(bq[(j + PF) % (PF + 1)], IC<j + PF>{});
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int b = 0; b < L::GB; ++b) acc[b] = mma(a[j], bq[j % (PF + 1)][b], acc[b]);
+        __builtin_amdgcn_sched_barrier(0);
       });
-      __builtin_amdgcn_sched_group_barrier(0x100, L::GB * (PF < L::KS ? PF : L::KS), 0);
-#pragma unroll
-      for (int j = 0; j < L::KS; ++j) {
-        __builtin_amdgcn_sched_group_barrier(0x008, L::GB, 0);
-        if (j + PF < L::KS) __builtin_amdgcn_sched_group_barrier(0x100, L::GB, 0);
-      }
       // rows 4g..4g+3 of the D tile: dX channels 4 (g & 1).. of row y (g < 2) or, with RP, of
       // row y + 1 (g >= 2); without RP rows 8-15 are padding
       if (L::RP || g < 2) {
@@ -350,52 +357,66 @@ __global__ __launch_bounds__(256, L::OCC) void lbwd_kernel(const bf16* __restric
     }
   };
 
-  // ---- weight-gradient contribution of one tile (wgrad_ws_kernel<WgA2>'s strip body); the
-  // tile's interior pixel P (row P / W, column P % W) sits at dY tile row + PAD, column + PAD
+  // ---- weight gradient of one tile (wgrad_ws_kernel<WgA2>'s strip body), software-pipelined over k-steps: k-step ks + NPW's fragments (address
+  // math included) are read before k-step ks's MFMAs, pinned by scheduling barriers
+  auto wg_load = [&](int ks, u2 (&af)[2], u2 (&bb)[L::NW][2]) {
+    int pa[2], xb[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int P = 32 * ks + kpix(g, h, q4);
+      const int r = P / L::W, ox = P - r * L::W;
+      pa[h] = ((r + L::PAD) * L::RS + ox + L::PAD) * L::PS + 4 * p4;
+      xb[h] = (r * L::XW + ox) * L::XS;
+    }
+    af[0] = tr4(dys + pa[0]);
+    af[1] = tr4(dys + pa[1]);
+#pragma unroll
+    for (int j = 0; j < L::NW; ++j) {
+      bb[j][0] = tr4(xs + xb[0] + xo[j]);
+      bb[j][1] = tr4(xs + xb[1] + xo[j]);
+    }
+  };
+  // the tile's interior pixel P (row P / W, column P % W) sits at dY tile row + PAD, column + PAD
   auto wgrad_tile = [&]() {
-    for (int ks = wq; ks < L::WKS; ks += L::NPW) {
-      const int P0 = 32 * ks;
-      int pa[2], xb[2];
+    int ks = wq;
+    if (ks >= L::WKS) return;
+    u2 af[2][2], bb[2][L::NW][2];
+    wg_load(ks, af[0], bb[0]);
+#pragma unroll 2
+    for (int it = 0; ks < L::WKS; ks += L::NPW, ++it) {
+      const int c = it & 1;
+      if (ks + L::NPW < L::WKS) wg_load(ks + L::NPW, af[c ^ 1], bb[c ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x8 a8 = frag8(af[c][0], af[c][1]);
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int P = P0 + kpix(g, h, q4);
-        const int r = P / L::W, ox = P - r * L::W;
-        pa[h] = ((r + L::PAD) * L::RS + ox + L::PAD) * L::PS + 4 * p4;
-        xb[h] = (r * L::XW + ox) * L::XS;
-      }
-      const bf16x8 af = frag8(tr4(dys + pa[0]), tr4(dys + pa[1]));
-      constexpr int PF = L::PFW;
-      u2 bq[PF + 1][2];
-#pragma unroll
-      for (int j = 0; j < PF && j < L::NW; ++j) {
-        bq[j][0] = tr4(xs + xb[0] + xo[j]);
-        bq[j][1] = tr4(xs + xb[1] + xo[j]);
-      }
-#pragma unroll
-      for (int j = 0; j < L::NW; ++j) {
-        if (j + PF < L::NW) {
-          bq[(j + PF) % (PF + 1)][0] = tr4(xs + xb[0] + xo[j + PF]);
-          bq[(j + PF) % (PF + 1)][1] = tr4(xs + xb[1] + xo[j + PF]);
-        }
-        wacc[j] = mma(af, frag8(bq[j % (PF + 1)][0], bq[j % (PF + 1)][1]), wacc[j]);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x100, 2 + 2 * (PF < L::NW ? PF : L::NW), 0);
-#pragma unroll
-      for (int j = 0; j < L::NW; ++j) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if (j + PF < L::NW) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      }
+      for (int j = 0; j < L::NW; ++j) wacc[j] = mma(a8, frag8(bb[c][j][0], bb[c][j][1]), wacc[j]);
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
-  if (t0 < t1) load_tile(t0);
-  for (int ti = t0; ti < t1; ++ti) {
-    __syncthreads();   // every wave is done with the previous tile (and ctab is written)
-    store_tile(ti);
-    __syncthreads();
-    if (ti + 1 < t1) load_tile(ti + 1);   // in flight under this tile's MFMAs
-    dgrad_tile(ti);
-    wgrad_tile();
+  {
+    // tile ti in buffer (ti - t0) & 1: its MFMAs, then tile ti + 1 staged into the other buffer
+    // (its loads were issued one tile earlier), then the loads of tile ti + 2; one barrier
+    if (t0 < t1) {
+      load_tile(t0);
+      __syncthreads();   // ctab is written
+      set_buf(0);
+      store_tile(t0);
+      if (t0 + 1 < t1) load_tile(t0 + 1);
+      __syncthreads();
+    }
+    for (int ti = t0; ti < t1; ++ti) {
+      const int b = (ti - t0) & 1;
+      set_buf(b);
+      dgrad_tile(ti);
+      wgrad_tile();
+      if (ti + 1 < t1) {
+        set_buf(b ^ 1);   // last read by tile ti - 1, before the previous barrier
+        store_tile(ti + 1);
+        if (ti + 2 < t1) load_tile(ti + 2);
+      }
+      __syncthreads();
+    }
   }
 
   // ---- pixel-split dW partials -> wave 0 (fixed order), slab [co][ci][tap] through LDS
@@ -431,17 +452,8 @@ __global__ __launch_bounds__(256, L::OCC) void lbwd_kernel(const bf16* __restric
   for (int e = tid; e < L::COUT * PER_CO / 4; e += 256) o4[e] = t4[e];
 }
 
-//          TH OCC PFD PFW GB NCW
-#ifndef LBWD_RP
-#define LBWD_RP 1
-#endif
-#ifndef LBWD_PFD
-#define LBWD_PFD 2
-#endif
-#ifndef LBWD_NCW
-#define LBWD_NCW 4
-#endif
-typedef Lb<8, 2, LBWD_PFD, 3, 1, LBWD_NCW, LBWD_RP> LbA2;
+//          TH OCC PFD GB NCW RP
+typedef Lb<8, 2, 3, 1, 4, 1> LbA2;
 
 int lb_occ_ap() {
   static int occ = 0;
