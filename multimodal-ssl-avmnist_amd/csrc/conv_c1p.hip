@@ -612,45 +612,10 @@ __global__ __launch_bounds__(256) void c1p8_recompute_kernel(
     __syncthreads();
     // ---- recompute y (rounded to bf16 exactly as the stored-y path)
     const unsigned* xd = reinterpret_cast<const unsigned*>(xs);
-    if constexpr (PASS != RC_STATS) {
-      // the other passes: one column tile at a time, software-pipelined -- tile mt + 1's four
-      // fragment reads go out before tile mt's MFMA, and tile mt's epilogue (bias, bf16 pack,
-      // LDS store) runs after tile mt + 1's MFMA is issued, pinned by scheduling barriers
-      // (compiled as written, each tile waited out an LDS read and then its MFMA's result)
-      auto rd = [&](int base) {
-        return u4{xd[base + off[0]], xd[base + off[1]], xd[base + off[2]], xd[base + off[3]]};
-      };
-      auto store_y = [&](int s, int mt, const f4& r4) {
-        const uint32_t lo = pack_bf16x2(r4[0] + bv[0], r4[1] + bv[1]);
-        const uint32_t hi = pack_bf16x2(r4[2] + bv[2], r4[3] + bv[3]);
-        const int ox = 16 * mt + 2 * q + j;
-        *reinterpret_cast<uint2*>(&ys[(2 * s + rp) * YRS + ypos(ox) * COUT + 4 * (PSPLIT ? cs ^ rp : cs)]) =
-            make_uint2(lo, hi);
-      };
-      for (int s = wave; s < TH / 2; s += 4) {
-        const int b0 = 2 * s * ITWD;
-        f4 rp4 = f4{0.f, 0.f, 0.f, 0.f};
-        // two fragment registers, alternating (the last tile re-reads itself: no branch)
-        auto step = [&](int mt, const u4& cur, u4& nxt) {
-          nxt = rd(b0 + 8 * min(mt + 1, mts - 1));
-          __builtin_amdgcn_sched_barrier(0);
-          const f4 r4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8, cur),
-                                                                f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-          if (mt > 0) store_y(s, mt - 1, rp4);
-          rp4 = r4;
-        };
-        u4 f0 = rd(b0), f1;
-        for (int mt = 0; mt < mts; mt += 2) {
-          step(mt, f0, f1);
-          if (mt + 1 < mts) step(mt + 1, f1, f0);
-        }
-        store_y(s, mts - 1, rp4);
-      }
-    } else
     for (int s = wave; s < TH / 2; s += 4) {
       // statistics pass: every column tile's B fragments first (their LDS reads in flight
-      // together), then the MFMAs, then the epilogues (213 vs 224 us)
+      // together), then the MFMAs, then the epilogues (213 vs 224 us); the other passes keep
+      // one tile at a time (the unrolled registers cost the apply pass an occupancy step)
       constexpr int MTU = PASS == RC_STATS ? MTMAX : 1;
       for (int mt0 = 0; mt0 < mts; mt0 += MTU) {
       u4 bws[MTU];
