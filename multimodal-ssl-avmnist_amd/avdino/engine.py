@@ -118,11 +118,22 @@ class ConvBranch:
         # not divide the batch (an odd last batch) runs on the bf16 kernels.
         self.fp8 = bool(fp8) and act_dtype == torch.bfloat16
 
+    # fp8 (config 5): a layer the fused bf16 layer backward serves (the audio conv2, 56^2) keeps
+    # its input and weight gradient in bf16 through that one launch; its forward stays MX
+    # (16.7-17.0 vs 17.4-17.8 ms per B = 4096 step, profiles/r6_ab_fp8_fused_bwd.txt)
+    FP8_FUSED_BWD = True
+
+    def _fused_bwd(self, i, N):
+        ci, co, k, p = self.stack.convs[i]
+        H = self.dims[i][0]
+        return (self.FP8_FUSED_BWD and self.LAYER_BWD and i > 0
+                and ops.cl_layer_bwd_slabs(self.act, N, ci, H, H, co, k, p) > 0)
+
     def _mx_ok(self, i, N, B=None, dgrad=False):
         """MX kernel for layer i's forward (B: the BN group size when it writes partials) or
         input gradient over N samples."""
         ci, co, k, p = self.stack.convs[i]
-        return (self.fp8 and i > 0
+        return (self.fp8 and i > 0 and not (dgrad and self._fused_bwd(i, N))
                 and ops.mx_conv_serves(ci, self.dims[i][0], co, k, p, dgrad, N, None if dgrad else B))
 
     def prepare(self, ws, store, tag, need_dgrad, N, B=None, launch=True):
@@ -174,7 +185,7 @@ class ConvBranch:
 
     def _mx_wgrad(self, i, N):
         ci, co, k, p = self.stack.convs[i]
-        return (self.fp8 and i > 0
+        return (self.fp8 and i > 0 and not self._fused_bwd(i, N)
                 and ops.mx_wgrad_chunks(N, ci, self.dims[i][0], co, k, p) > 0)
 
     def _wgrad_chunks(self, i, N):
