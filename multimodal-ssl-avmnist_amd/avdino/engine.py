@@ -517,11 +517,11 @@ class ConvBranch:
     # chain (within noise).
 
     # layers whose weight gradient runs on the input-gradient (main) stream even when a
-    # weight-gradient stream is given: the audio 28^2 / 14^2 layers.  Same step time as all on
-    # the third stream (3 interleaved rounds: 5.018-5.051 vs 5.012-5.026 ms,
-    # profiles/r5n_wgrad_main_ab.txt), but their launches no longer share the CUs with two other
-    # streams' kernels (the 14^2 one ran 640-650 us in the graph beside them, 153 us alone)
-    WGRAD_MAIN = frozenset({2, 3})
+    # weight-gradient stream is given: the audio 14^2 layer (its launch ran 640-650 us in the
+    # graph beside two other streams' kernels, 153 us alone).  Round 6, with the fused 56^2 layer
+    # backward, three interleaved rounds (profiles/r6_ab_wgrad_main.txt): {3} 4.913-4.936 ms,
+    # none 4.911-4.957, {2} 4.973-5.004, {2, 3} (round 5's choice) 4.991-5.031
+    WGRAD_MAIN = frozenset({3})
 
     # the audio conv2 (56^2) backward as ONE launch (avd_cl_layer_bwd: BN-backward apply, input
     # and weight gradient from the same staged tiles, no dY in HBM); False: apply + dgrad + wgrad
