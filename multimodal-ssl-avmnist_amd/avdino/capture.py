@@ -12,12 +12,43 @@ collective in the same order on every rank.  Work forked to side streams must be
 before a host point (a segment, like any captured graph, ends with every forked stream
 rejoined); callers join exactly there and nowhere else.
 """
+import collections
+
 import torch
 
 from . import ops
 
 _ACTIVE = None     # the _Capture in progress (host_point's target), else None
 
+
+
+# Event lifetimes.  On this stack a HIP event destroyed while the device may still reach it
+# (a fork / join event of a step queued ahead of the GPU, or one recorded into a capture) can
+# corrupt the runtime: replays then segfaulted on the host in hipGraphLaunch
+# (tests/test_gpu_step.py followed by tests/test_gpu_graph.py in one process, 4 of 4 runs; 0 of
+# 2 with events kept alive, tools/pytest_keep_events.py).  So every event the engine creates
+# (new_event) and every temporary of Stream.wait_stream / record_event (torch.cuda.streams.Event
+# is this class from import on) stays referenced for the next 4096 event creations, and events
+# created during a capture for as long as the graph exists.
+_RING = collections.deque(maxlen=4096)
+_HOLD = None
+
+
+class _HeldEvent(torch.cuda.Event):
+    def __new__(cls, *args, **kwargs):
+        ev = super().__new__(cls, *args, **kwargs)
+        _RING.append(ev)
+        if _HOLD is not None:
+            _HOLD.append(ev)
+        return ev
+
+
+torch.cuda.streams.Event = _HeldEvent
+
+
+def new_event(**kwargs):
+    """A torch.cuda.Event held alive past the work that waits on it (see above)."""
+    return _HeldEvent(**kwargs)
 
 
 class _Capture:
@@ -71,7 +102,7 @@ class GraphedStep:
     def __init__(self, warmup=2, deps=None):
         self.warmup = warmup
         self.deps = deps if deps is not None else ops.alloc_epoch
-        self.graphs = {}     # key -> (segments, allocation epoch after the capture)
+        self.graphs = {}     # key -> (segments, allocation epoch after the capture, held events)
         self.seen = {}
         self.captures = 0
         self.pool = None
@@ -122,8 +153,11 @@ class GraphedStep:
         main = torch.cuda.current_stream()
         self.stream.wait_stream(main)
         cap = _Capture(self.pool)
+        global _HOLD
+        held = []
         with torch.cuda.stream(self.stream):
             _ACTIVE = cap
+            _HOLD = held
             try:
                 cap.begin()
                 body()
@@ -137,6 +171,7 @@ class GraphedStep:
                 raise
             finally:
                 _ACTIVE = None
+                _HOLD = None
         main.wait_stream(self.stream)
-        self.graphs[key] = (cap.seq, self.deps())
+        self.graphs[key] = (cap.seq, self.deps(), held)
         self.captures += 1

@@ -23,7 +23,7 @@ MI355X-native restructuring (results identical up to fp32 rounding):
 import torch
 
 from . import contrastive, ops
-from .capture import GraphedStep, host_point  # noqa: F401  (GraphedStep re-exported)
+from .capture import GraphedStep, host_point, new_event  # noqa: F401  (GraphedStep re-exported)
 from .spec import HEAD_NAMES, MULTI_ENCODERS, PROJ_HIDDEN, UNI_ALIASES, UNI_ENCODERS
 
 F32 = torch.float32
@@ -601,7 +601,7 @@ class ConvBranch:
                     self._conv_wgrad(i, x, dy, wparts, N)
                     ops.sum_rows(wparts, nch, co * ci * k * k, store.grad_of(ck + ".weight"))
                     ops.mark(f"w{i}.end")
-                    ev = torch.cuda.Event()
+                    ev = new_event()
                     ev.record(wstream)
                 wdone.append(ev)
             else:
@@ -923,7 +923,7 @@ class MultiCentralEngine:
             self.side.wait_stream(main)
         with torch.cuda.stream(self.side):
             out = fn()
-            done = torch.cuda.Event()
+            done = new_event()
             done.record(self.side)
         return out, done
 
@@ -1005,7 +1005,7 @@ class MultiCentralEngine:
         staged = self._aug_bufs(batch, with_orig, par)
         with torch.cuda.stream(self.dstream):
             batch["aug"].stage(batch["idx"], staged[0], staged[1], with_orig)
-            done = torch.cuda.Event()
+            done = new_event()
             done.record(self.dstream)
         self._pf = (batch, par, done, staged)
         return True
@@ -1111,7 +1111,7 @@ class MultiCentralEngine:
             x_img, x_aud, B, G = tin
             self._prepare_hwc(("teacher",))           # the EMA'd teacher's Linear copies
             self._teacher_fwd(x_img, x_aud, B, G, seed_off=self._tseed)
-            done = torch.cuda.Event()
+            done = new_event()
             done.record(self.tside)
         return done
 
@@ -1200,7 +1200,7 @@ class MultiCentralEngine:
             elif self.FHEADS_LATE and self.side is not None:
                 # queued (captured) after the fusion / projection below, depending only on
                 # what is queued so far (the cat)
-                f_after = torch.cuda.Event()
+                f_after = new_event()
                 f_after.record(torch.cuda.current_stream(st.device))
             else:
                 (head_out, hctx), h_done = self._on_side(heads)
@@ -1321,10 +1321,10 @@ class MultiCentralEngine:
                     with torch.cuda.stream(g[1]):
                         if next(g[0], StopIteration) is StopIteration:
                             gens.remove(g)
-            h_done = torch.cuda.Event()
+            h_done = new_event()
             h_done.record(self.side)
         else:
-            h_after = torch.cuda.Event()
+            h_after = new_event()
             h_after.record(torch.cuda.current_stream(self.store.device))
             drain(main_steps())
             _, h_done = self._on_side(lambda: drain(heads_steps()), after=h_after)
