@@ -177,3 +177,12 @@ def test_workspace_canary_guards(monkeypatch):
     ws.guards["b"][0].view(torch.uint8)[3 * 8 + 5] = 0      # one byte past b's end
     assert ws.check_guards() == [("b", 5, 1)]
     assert ws.get("a", 10).numel() == 10
+
+
+def test_event_ring_is_installed():
+    """avdino.capture holds events past the work that waits on them: importing it
+    makes Stream.wait_stream's temporaries the holding subclass, bounded to the last 4096."""
+    from avdino import capture
+    assert torch.cuda.streams.Event is capture._HeldEvent
+    assert issubclass(capture._HeldEvent, torch.cuda.Event) and torch.cuda.Event is not capture._HeldEvent
+    assert capture._RING.maxlen == 4096
