@@ -250,14 +250,19 @@ __global__ __launch_bounds__(256, L::OCC) void lbwd_kernel(const bf16* __restric
   WinIn wpre[AP ? YSL : 1];
   u4 ypre[AP ? 1 : YSL];
   u4 xpre[XSL];
-  auto load_tile = [&](int ti) {
+  // cont: the block's previous tile is the rows just above this one in the same sample, so the
+  // first 2 * PAD staged rows (dY and X) are copied from that tile's last rows instead of loaded
+  // and recomputed (a third of the BN-backward apply and of the y / x loads)
+  constexpr int RR = 2 * L::PAD;
+  auto load_tile = [&](int ti, bool cont) {
     const int n = ti / L::TPS, ty0 = (ti - n * L::TPS) * L::TH;
     const long long row0 = (long long)n * L::H + ty0 - L::PAD;     // first staged row
     const bf16* by = ysrc + row0 * L::W * L::COUT;
     const bf16* bx = x + row0 * L::W * L::CIN;
 #pragma unroll
     for (int i = 0; i < YSL; ++i) {
-      const bool ok = ygo[i] >= 0 && (unsigned)(ty0 - L::PAD + yrow[i]) < (unsigned)L::H;
+      const bool ok = ygo[i] >= 0 && (unsigned)(ty0 - L::PAD + yrow[i]) < (unsigned)L::H &&
+                      !(cont && yrow[i] < RR);
       const bf16* p = by + (ok ? ygo[i] : 0);
       if constexpr (AP) {
         wpre[i].y[0] = ldg16(ok ? (const void*)(p) : &kZeroL);
@@ -272,16 +277,27 @@ __global__ __launch_bounds__(256, L::OCC) void lbwd_kernel(const bf16* __restric
     }
 #pragma unroll
     for (int i = 0; i < XSL; ++i) {
-      const bool ok = xgo[i] >= 0 && (unsigned)(ty0 - L::PAD + xrow[i]) < (unsigned)L::H;
+      const bool ok = xgo[i] >= 0 && (unsigned)(ty0 - L::PAD + xrow[i]) < (unsigned)L::H &&
+                      !(cont && xrow[i] < RR);
       xpre[i] = ldg16(ok ? (const void*)(bx + xgo[i]) : &kZeroL);
     }
   };
-  auto store_tile = [&](int ti) {
+  auto store_tile = [&](int ti, bool cont, const bf16* pdys, const bf16* pxs) {
     const int n = ti / L::TPS, ty0 = (ti - n * L::TPS) * L::TH;
+    if (cont) {
+      // rows 0 .. RR-1 of this tile = rows TH .. TH+RR-1 of the previous one (other buffer)
+      constexpr int DQ = RR * L::RS * L::PS / 8, XQ = RR * L::XW * L::XS / 8;   // 16-byte chunks
+      const u4* sd = reinterpret_cast<const u4*>(pdys + L::TH * L::RS * L::PS);
+      u4* dd = reinterpret_cast<u4*>(dys);
+      for (int c = tid; c < DQ; c += 256) dd[c] = sd[c];
+      const u4* sx = reinterpret_cast<const u4*>(pxs + L::TH * L::XW * L::XS);
+      u4* dxs = reinterpret_cast<u4*>(xs);
+      for (int c = tid; c < XQ; c += 256) dxs[c] = sx[c];
+    }
 #pragma unroll
     for (int i = 0; i < YSL; ++i) {
       const int task = tid + 256 * i;
-      if (task >= YT) continue;
+      if (task >= YT || (cont && yrow[i] < RR)) continue;
       if constexpr (AP) {
         u4 o[4] = {u4{0u, 0u, 0u, 0u}, u4{0u, 0u, 0u, 0u}, u4{0u, 0u, 0u, 0u}, u4{0u, 0u, 0u, 0u}};
         if (ygo[i] >= 0 && (unsigned)(ty0 - L::PAD + yrow[i]) < (unsigned)L::H)
@@ -296,7 +312,8 @@ __global__ __launch_bounds__(256, L::OCC) void lbwd_kernel(const bf16* __restric
     }
 #pragma unroll
     for (int i = 0; i < XSL; ++i)
-      if (tid + 256 * i < L::XT) *reinterpret_cast<u4*>(xs + xlo[i]) = xpre[i];
+      if (tid + 256 * i < L::XT && !(cont && xrow[i] < RR))
+        *reinterpret_cast<u4*>(xs + xlo[i]) = xpre[i];
   };
 
   // ---- input gradient of one tile (conv_ws_kernel<DgrA2, false>'s tile body)
@@ -398,11 +415,11 @@ __global__ __launch_bounds__(256, L::OCC) void lbwd_kernel(const bf16* __restric
     // tile ti in buffer (ti - t0) & 1: its MFMAs, then tile ti + 1 staged into the other buffer
     // (its loads were issued one tile earlier), then the loads of tile ti + 2; one barrier
     if (t0 < t1) {
-      load_tile(t0);
+      load_tile(t0, false);
       __syncthreads();   // ctab is written
       set_buf(0);
-      store_tile(t0);
-      if (t0 + 1 < t1) load_tile(t0 + 1);
+      store_tile(t0, false, nullptr, nullptr);
+      if (t0 + 1 < t1) load_tile(t0 + 1, (t0 + 1) % L::TPS != 0);
       __syncthreads();
     }
     for (int ti = t0; ti < t1; ++ti) {
@@ -411,9 +428,11 @@ __global__ __launch_bounds__(256, L::OCC) void lbwd_kernel(const bf16* __restric
       dgrad_tile(ti);
       wgrad_tile();
       if (ti + 1 < t1) {
+        const bf16* pd = dys;     // tile ti's images: its last rows may seed tile ti + 1
+        const bf16* px = xs;
         set_buf(b ^ 1);   // last read by tile ti - 1, before the previous barrier
-        store_tile(ti + 1);
-        if (ti + 2 < t1) load_tile(ti + 2);
+        store_tile(ti + 1, (ti + 1) % L::TPS != 0, pd, px);
+        if (ti + 2 < t1) load_tile(ti + 2, (ti + 2) % L::TPS != 0);
       }
       __syncthreads();
     }
