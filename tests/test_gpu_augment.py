@@ -340,10 +340,10 @@ def test_workspace_allocation_leaves_no_queued_work():
 
 @pytest.mark.parametrize("graph", [False, True])
 def test_prefetched_augmentation_steps_equal_serial_steps(tmp_path, graph):
-    """Real-data steps whose next batch is augmented on the data stream under the current step
-    (engine.prefetch, double-buffered staged inputs; the data stream waits only for the steps
-    before the current one) give the same losses and parameters, bit for bit, as steps that
-    augment each batch in front of it -- eager and graph-replayed."""
+    """Real-data steps whose next batch is prefetched on the data stream (engine.prefetch,
+    double-buffered staged inputs; the data stream starts after the step just queued, DESIGN
+    3.6) give the same losses and parameters, bit for bit, as steps that augment each batch in
+    front of it -- eager and graph-replayed."""
     from avdino.data import AVMNISTDinoLoader
     from avdino.engine import Hyper, MultiCentralEngine
     from avdino.params import ParamStore
